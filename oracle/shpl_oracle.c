@@ -1,0 +1,299 @@
+/*
+ * shpl_oracle.c -- CPU restatement of the reference SHPL path.
+ *
+ * TEST INFRASTRUCTURE ONLY. This file is the parity checker and the
+ * bench's `cpu_baseline` ("port"); it is never linked into, loaded by or
+ * called from the product library (sparse_pooling_amd/libshpl.so).
+ *
+ * What it restates (file:line relative to the reference checkout):
+ *   index builder  avod/avod/utils/transform.py:3-40          (projectToImage, clip3DwithinImage)
+ *                  avod/avod/utils/sparse_pool_utils.py:6-20   (gen_sparse_pooling_input_avod)
+ *                  avod/avod/utils/sparse_pool_utils.py:22-58  (produce_sparse_pooling_input)
+ *   pooling ops    avod/avod/utils/sparse_pool_utils.py:96-117 (_sparse_pool_op, _sparse_pool_trans_op)
+ *                  whose arithmetic lives in TensorFlow 1.8.0 (avod/README.md:31,
+ *                  MV3D_TF_release/README.md:11), a dependency absent from the
+ *                  reference tree. Restated from TF 1.8's CPU kernels:
+ *                    GatherNd                  copy params[idx[k]] -> P[k]; OOB is InvalidArgument
+ *                    SparseTensorDenseMatMul   out = 0; for i in nnz order: out[m] += a_i * B[k]
+ *                                              (adjoint_a swaps m/k; separate mul and add, the
+ *                                              pip TF 1.8 binaries are built without FMA)
+ *                    SparseTranspose           permute index columns, then SparseReorder:
+ *                                              lexicographic (col,row) order; equal keys keep
+ *                                              input order here (TF's std::sort leaves them unspecified)
+ *                    ScatterNd                 out = 0; for k in update order: out[idx[k]] += U[k]
+ *                  and TF 1.8's registered gradients: GatherNd' = ScatterNd,
+ *                  SparseTensorDenseMatMul'(B) = matmul(A, dY, adjoint_a=True),
+ *                  ScatterNd'(updates) = GatherNd.
+ *
+ * Parity status: the index builder is PINNED by tests/golden/index_*.npz,
+ * produced by running the reference's own numpy builders in the survey
+ * container (tests/golden/make_golden.py). The pooling ops are pinned to the
+ * reference's call sites only: TensorFlow cannot be run here and the
+ * reference holds no SHPL fixtures -- their numerics
+ * are "parity unpinned" beyond TF's documented kernel order.
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define SHPLO_OK 0
+#define SHPLO_ERR_INDEX 2
+#define SHPLO_ERR_SHAPE 1
+
+/* ---- a1: projectToImage (avod/avod/utils/transform.py:3-26) -----------------
+ * numpy evaluates np.dot(P, [x;y;z;1]) through OpenBLAS dgemm, which
+ * accumulates the K=4 products as one fused-multiply-add chain in k order.
+ * That chain was checked bit-exact against np.dot on 2M random points
+ * (every column count >= 2; a single column goes through dgemv instead). */
+static void project(const double *P, double x, double y, double z, double *u, double *v)
+{
+    const double a[4] = {x, y, z, 1.0};
+    double r[3];
+    for (int i = 0; i < 3; ++i) {
+        double s = P[4 * i] * a[0];
+        for (int k = 1; k < 4; ++k)
+            s = fma(P[4 * i + k], a[k], s);
+        r[i] = s;
+    }
+    *u = r[0] / r[2];
+    *v = r[1] / r[2];
+}
+
+/* a2: clip3DwithinImage (transform.py:28-40) -- strict upper bounds, image_size=[W,H]. */
+static int inside_image(double u, double v, double w_img, double h_img)
+{
+    return (u < w_img - 1.0) && (u >= 0.0) && (v >= 0.0) && (v < h_img - 1.0);
+}
+
+/* a3: gen_sparse_pooling_input_avod (sparse_pool_utils.py:6-20).
+ * pts: n x 3 (camera frame), vox: n x 2, P: 3 x 4 (row-major).
+ * Outputs (capacity n): bv_index nv x 2, img_index 3 rows of stride `ld`
+ * ([u; v; 0], rounded half-to-even like np.round). Returns nv. */
+int64_t shplo_gen_index(int64_t n, const double *pts, const int64_t *vox, const double *P,
+                        double im_w, double im_h, int64_t *bv_index, double *img_index, int64_t ld)
+{
+    int64_t nv = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        double u, v;
+        project(P, pts[3 * i], pts[3 * i + 1], pts[3 * i + 2], &u, &v);
+        if (!inside_image(u, v, im_w, im_h))
+            continue;
+        bv_index[2 * nv] = vox[2 * i];
+        bv_index[2 * nv + 1] = vox[2 * i + 1];
+        img_index[nv] = (double)(int64_t)nearbyint(u);
+        img_index[ld + nv] = (double)(int64_t)nearbyint(v);
+        img_index[2 * ld + nv] = 0.0;
+        ++nv;
+    }
+    return nv;
+}
+
+/* a4: produce_sparse_pooling_input (sparse_pool_utils.py:22-58).
+ * stride[0] (s_img) applies to the image, stride[1] (s_bv) to BEV.
+ * img_index (3 rows, stride ld) is MUTATED in place exactly as the reference
+ * mutates the caller's dict. bv_size is (H, W), im_size is (W, H).
+ * Outputs: mij nk x 2 = [r, k], flip nk x 3 = [0, v, u], msize = [Hb'*Wb', nk].
+ * Returns nk. */
+int64_t shplo_produce(int64_t nv, const int64_t *bv_index, double *img_index, int64_t ld,
+                      double im_w, double im_h, double bv_h, double bv_w,
+                      double s_img, double s_bv, int64_t *mij, int64_t *flip, int64_t *msize)
+{
+    const double wq = floor(im_w / s_img), hq = floor(im_h / s_img);
+    const double bhq = floor(bv_h / s_bv), bwq = floor(bv_w / s_bv);
+    const int64_t n_cells = (int64_t)(bhq * bwq);
+    int64_t nk = 0;
+    for (int64_t j = 0; j < nv; ++j) {
+        double u = floor(img_index[j] / s_img);
+        double v = floor(img_index[ld + j] / s_img);
+        if (u >= wq) u = wq - 1.0;
+        if (v >= hq) v = hq - 1.0;
+        img_index[j] = u;
+        img_index[ld + j] = v;
+        const double bx = floor((double)bv_index[2 * j] / s_bv);
+        const double bz = floor((double)bv_index[2 * j + 1] / s_bv);
+        const int64_t r = (int64_t)(bz * bwq + bx);
+        if (!(r < n_cells))
+            continue;
+        mij[2 * nk] = r;
+        mij[2 * nk + 1] = nk;
+        flip[3 * nk] = (int64_t)floor(img_index[2 * ld + j]);
+        flip[3 * nk + 1] = (int64_t)v;
+        flip[3 * nk + 2] = (int64_t)u;
+        ++nk;
+    }
+    msize[0] = (int64_t)(bhq * bwq);
+    msize[1] = nk;
+    return nk;
+}
+
+/* ---- TF op restatements ---------------------------------------------------- */
+
+/* GatherNd index check for a [B,H,W,C] params tensor; returns flat pixel or -1. */
+static int64_t pixel_of(const int64_t *idx, int64_t k, int64_t B, int64_t H, int64_t W)
+{
+    const int64_t b = idx[3 * k], y = idx[3 * k + 1], x = idx[3 * k + 2];
+    if (b < 0 || b >= B || y < 0 || y >= H || x < 0 || x >= W)
+        return -1;
+    return (b * H + y) * W + x;
+}
+
+static int check_m(const int64_t *mij, int64_t nnz, int64_t R, int64_t ncols)
+{
+    for (int64_t i = 0; i < nnz; ++i)
+        if (mij[2 * i] < 0 || mij[2 * i] >= R || mij[2 * i + 1] < 0 || mij[2 * i + 1] >= ncols)
+            return SHPLO_ERR_INDEX;
+    return SHPLO_OK;
+}
+
+/* a8: _sparse_pool_op = reshape(sparse_tensor_dense_matmul(M, gather_nd(img, idx))).
+ * img [B,H,W,C] f32; idx n_idx x 3; M (mij nnz x 2, mval nnz, shape R x ncols).
+ * out R x C. */
+int shplo_pool(const float *img, int64_t B, int64_t H, int64_t W, int64_t C,
+               const int64_t *idx, int64_t n_idx, const int64_t *mij, const float *mval,
+               int64_t nnz, int64_t R, int64_t ncols, float *out)
+{
+    if (ncols != n_idx)
+        return SHPLO_ERR_SHAPE;
+    for (int64_t k = 0; k < n_idx; ++k)
+        if (pixel_of(idx, k, B, H, W) < 0)
+            return SHPLO_ERR_INDEX;
+    if (check_m(mij, nnz, R, ncols))
+        return SHPLO_ERR_INDEX;
+    memset(out, 0, sizeof(float) * (size_t)(R * C));
+    for (int64_t i = 0; i < nnz; ++i) {
+        const int64_t m = mij[2 * i], k = mij[2 * i + 1];
+        const float a = mval[i];
+        const float *b = img + pixel_of(idx, k, B, H, W) * C;
+        float *o = out + m * C;
+        for (int64_t c = 0; c < C; ++c) {
+            const float prod = a * b[c];
+            o[c] = o[c] + prod;
+        }
+    }
+    return SHPLO_OK;
+}
+
+/* SparseReorder order of M^T: entries sorted by (col, row), ties by input order. */
+static const int64_t *g_mij;
+static int cmp_col_row(const void *pa, const void *pb)
+{
+    const int64_t a = *(const int64_t *)pa, b = *(const int64_t *)pb;
+    const int64_t ca = g_mij[2 * a + 1], cb = g_mij[2 * b + 1];
+    if (ca != cb) return ca < cb ? -1 : 1;
+    const int64_t ra = g_mij[2 * a], rb = g_mij[2 * b];
+    if (ra != rb) return ra < rb ? -1 : 1;
+    return a < b ? -1 : (a > b);
+}
+
+static int64_t *transpose_order(const int64_t *mij, int64_t nnz)
+{
+    int64_t *ord = (int64_t *)malloc(sizeof(int64_t) * (size_t)(nnz > 0 ? nnz : 1));
+    for (int64_t i = 0; i < nnz; ++i)
+        ord[i] = i;
+    g_mij = mij;
+    qsort(ord, (size_t)nnz, sizeof(int64_t), cmp_col_row);
+    return ord;
+}
+
+/* a9: _sparse_pool_trans_op = scatter_nd(idx, sparse_tensor_dense_matmul(
+ *     sparse_transpose(M), reshape(bev, [-1, C])), [B,H,W,C]).
+ * bev R x C; out B*H*W x C. */
+int shplo_pool_trans(const float *bev, int64_t R, int64_t C, const int64_t *mij,
+                     const float *mval, int64_t nnz, int64_t ncols, const int64_t *idx,
+                     int64_t n_idx, int64_t B, int64_t H, int64_t W, float *out)
+{
+    if (ncols != n_idx)
+        return SHPLO_ERR_SHAPE;
+    if (check_m(mij, nnz, R, ncols))
+        return SHPLO_ERR_INDEX;
+    for (int64_t k = 0; k < n_idx; ++k)
+        if (pixel_of(idx, k, B, H, W) < 0)
+            return SHPLO_ERR_INDEX;
+    float *q = (float *)calloc((size_t)(ncols * C > 0 ? ncols * C : 1), sizeof(float));
+    int64_t *ord = transpose_order(mij, nnz);
+    for (int64_t t = 0; t < nnz; ++t) {
+        const int64_t i = ord[t];
+        const int64_t m = mij[2 * i + 1], k = mij[2 * i]; /* transposed: row=col(M), col=row(M) */
+        const float a = mval[i];
+        for (int64_t c = 0; c < C; ++c) {
+            const float prod = a * bev[k * C + c];
+            q[m * C + c] = q[m * C + c] + prod;
+        }
+    }
+    memset(out, 0, sizeof(float) * (size_t)(B * H * W * C));
+    for (int64_t k = 0; k < n_idx; ++k) {
+        float *o = out + pixel_of(idx, k, B, H, W) * C;
+        for (int64_t c = 0; c < C; ++c)
+            o[c] = o[c] + q[k * C + c];
+    }
+    free(ord);
+    free(q);
+    return SHPLO_OK;
+}
+
+/* a11 (part): gradient of a8 w.r.t. img.
+ * grad_P = sparse_tensor_dense_matmul(M, dY, adjoint_a=True) (nnz order);
+ * d_img = scatter_nd(idx, grad_P, img.shape).  dY is R x C. */
+int shplo_pool_grad_img(const float *dY, int64_t R, int64_t C, const int64_t *mij,
+                        const float *mval, int64_t nnz, int64_t ncols, const int64_t *idx,
+                        int64_t n_idx, int64_t B, int64_t H, int64_t W, float *d_img)
+{
+    if (ncols != n_idx)
+        return SHPLO_ERR_SHAPE;
+    if (check_m(mij, nnz, R, ncols))
+        return SHPLO_ERR_INDEX;
+    for (int64_t k = 0; k < n_idx; ++k)
+        if (pixel_of(idx, k, B, H, W) < 0)
+            return SHPLO_ERR_INDEX;
+    float *g = (float *)calloc((size_t)(ncols * C > 0 ? ncols * C : 1), sizeof(float));
+    for (int64_t i = 0; i < nnz; ++i) {
+        const int64_t m = mij[2 * i + 1], k = mij[2 * i];
+        const float a = mval[i];
+        for (int64_t c = 0; c < C; ++c) {
+            const float prod = a * dY[k * C + c];
+            g[m * C + c] = g[m * C + c] + prod;
+        }
+    }
+    memset(d_img, 0, sizeof(float) * (size_t)(B * H * W * C));
+    for (int64_t k = 0; k < n_idx; ++k) {
+        float *o = d_img + pixel_of(idx, k, B, H, W) * C;
+        for (int64_t c = 0; c < C; ++c)
+            o[c] = o[c] + g[k * C + c];
+    }
+    free(g);
+    return SHPLO_OK;
+}
+
+/* a11 (part): gradient of a9 w.r.t. bev.
+ * dQ = gather_nd(dZ, idx); d_bev = sparse_tensor_dense_matmul(M^T, dQ, adjoint_a=True)
+ * iterating M^T's reordered (col,row) entries. dZ is [B,H,W,C]; d_bev R x C. */
+int shplo_pool_trans_grad_bev(const float *dZ, int64_t B, int64_t H, int64_t W, int64_t C,
+                              const int64_t *idx, int64_t n_idx, const int64_t *mij,
+                              const float *mval, int64_t nnz, int64_t R, int64_t ncols,
+                              float *d_bev)
+{
+    if (ncols != n_idx)
+        return SHPLO_ERR_SHAPE;
+    for (int64_t k = 0; k < n_idx; ++k)
+        if (pixel_of(idx, k, B, H, W) < 0)
+            return SHPLO_ERR_INDEX;
+    if (check_m(mij, nnz, R, ncols))
+        return SHPLO_ERR_INDEX;
+    int64_t *ord = transpose_order(mij, nnz);
+    memset(d_bev, 0, sizeof(float) * (size_t)(R * C));
+    for (int64_t t = 0; t < nnz; ++t) {
+        const int64_t i = ord[t];
+        const int64_t r = mij[2 * i], k = mij[2 * i + 1];
+        const float a = mval[i];
+        const float *b = dZ + pixel_of(idx, k, B, H, W) * C;
+        for (int64_t c = 0; c < C; ++c) {
+            const float prod = a * b[c];
+            d_bev[r * C + c] = d_bev[r * C + c] + prod;
+        }
+    }
+    free(ord);
+    return SHPLO_OK;
+}

@@ -1,0 +1,194 @@
+"""ctypes front-end of the C oracle (oracle/shpl_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg -- as the checker, never as the product path.
+See the header of shpl_oracle.c for what is restated from where and for the
+parity status (index builder pinned by the reference-generated goldens;
+pooling ops restated from TensorFlow 1.8's kernel order, "parity unpinned"
+beyond that).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libshpl_oracle.so")
+_lib = None
+
+
+class OracleError(ValueError):
+    """Mirror of TF's InvalidArgumentError for the oracle."""
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+        i64, p = ctypes.c_int64, ctypes.c_void_p
+        d = ctypes.c_double
+        _lib.shplo_gen_index.restype = i64
+        _lib.shplo_gen_index.argtypes = [i64, p, p, p, d, d, p, p, i64]
+        _lib.shplo_produce.restype = i64
+        _lib.shplo_produce.argtypes = [i64, p, p, i64, d, d, d, d, d, d, p, p, p]
+        _lib.shplo_pool.restype = ctypes.c_int
+        _lib.shplo_pool.argtypes = [p, i64, i64, i64, i64, p, i64, p, p, i64, i64, i64, p]
+        _lib.shplo_pool_trans.restype = ctypes.c_int
+        _lib.shplo_pool_trans.argtypes = [p, i64, i64, p, p, i64, i64, p, i64, i64, i64, i64, p]
+        _lib.shplo_pool_grad_img.restype = ctypes.c_int
+        _lib.shplo_pool_grad_img.argtypes = [p, i64, i64, p, p, i64, i64, p, i64, i64, i64, i64, p]
+        _lib.shplo_pool_trans_grad_bev.restype = ctypes.c_int
+        _lib.shplo_pool_trans_grad_bev.argtypes = [p, i64, i64, i64, i64, p, i64, p, p, i64, i64,
+                                                    i64, p]
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+# ---- index builder -------------------------------------------------------
+
+def gen_sparse_pooling_input_avod(points, voxel_indices, p2, im_size, bv_size):
+    """Restates avod/avod/utils/sparse_pool_utils.py:6-20. ``p2`` is the 3x4 P."""
+    pts = _c(points, np.float64).reshape(-1, 3)
+    vox = _c(np.asarray(voxel_indices)[:, :2], np.int64)
+    n = pts.shape[0]
+    bv = np.zeros((max(n, 1), 2), np.int64)
+    img = np.zeros((3, max(n, 1)), np.float64)
+    nv = lib().shplo_gen_index(n, _p(pts), _p(vox), _p(_c(p2, np.float64)),
+                               float(im_size[0]), float(im_size[1]), _p(bv), _p(img), img.shape[1])
+    return {"bv_index": bv[:nv].copy(), "img_index": np.ascontiguousarray(img[:, :nv]),
+            "bv_size": np.array([bv_size[0], bv_size[1]]), "img_size": np.array(im_size)}
+
+
+def produce_sparse_pooling_input(input_dict, M_val=None, stride=(1, 1)):
+    """Restates avod/avod/utils/sparse_pool_utils.py:22-58, including the
+    in-place update of ``input_dict['img_index']``."""
+    img = input_dict["img_index"]
+    assert img.shape[0] == 3, "wrong img_index shape, should be 3xN instead " + str(img.shape)
+    work = _c(img, np.float64)
+    bv = _c(input_dict["bv_index"], np.int64).reshape(-1, 2)
+    nv = work.shape[1]
+    mij = np.zeros((max(nv, 1), 2), np.int64)
+    flip = np.zeros((max(nv, 1), 3), np.int64)
+    msize = np.zeros(2, np.int64)
+    im = input_dict["img_size"]
+    bs = input_dict["bv_size"]
+    nk = lib().shplo_produce(nv, _p(bv), _p(work), work.shape[1], float(im[0]), float(im[1]),
+                             float(bs[0]), float(bs[1]), float(stride[0]), float(stride[1]),
+                             _p(mij), _p(flip), _p(msize))
+    img[...] = work  # the reference mutates the caller's array
+    if M_val is None:
+        M_val = np.ones(nk)
+    return {"Mij_pool": mij[:nk].copy(), "M_val": M_val, "M_size": msize,
+            "img_index_flip_pool": flip[:nk].copy(), "bev_index_flip_pool": np.zeros((0, 3))}
+
+
+# ---- TF op restatements ----------------------------------------------------
+
+def _check(rc):
+    if rc == 1:
+        raise OracleError("shape mismatch")
+    if rc == 2:
+        raise OracleError("index out of bounds")
+
+
+def sparse_pool_op(mij, mval, m_size, img, idx):
+    """_sparse_pool_op (sparse_pool_utils.py:96-103) before the reshape: R x C."""
+    img = _c(img, np.float32)
+    B, H, W, C = img.shape
+    mij = _c(mij, np.int64).reshape(-1, 2)
+    mval = _c(mval, np.float32).reshape(-1)
+    idx = _c(idx, np.int64).reshape(-1, 3)
+    if mval.shape[0] != mij.shape[0]:
+        raise OracleError("values/indices length mismatch")
+    R, ncols = int(m_size[0]), int(m_size[1])
+    out = np.empty((R, C), np.float32)
+    _check(lib().shplo_pool(_p(img), B, H, W, C, _p(idx), idx.shape[0], _p(mij), _p(mval),
+                            mij.shape[0], R, ncols, _p(out)))
+    return out
+
+
+def sparse_pool_trans_op(mij, mval, m_size, bev_flat, idx, img_shape):
+    """_sparse_pool_trans_op (sparse_pool_utils.py:105-117): returns [B,H,W,C]."""
+    bev = _c(bev_flat, np.float32)
+    R, C = bev.shape
+    mij = _c(mij, np.int64).reshape(-1, 2)
+    mval = _c(mval, np.float32).reshape(-1)
+    idx = _c(idx, np.int64).reshape(-1, 3)
+    if mval.shape[0] != mij.shape[0]:
+        raise OracleError("values/indices length mismatch")
+    if int(m_size[0]) != R:
+        raise OracleError("matmul inner dimension mismatch")
+    B, H, W = img_shape[:3]
+    out = np.empty((B, H, W, C), np.float32)
+    _check(lib().shplo_pool_trans(_p(bev), R, C, _p(mij), _p(mval), mij.shape[0], int(m_size[1]),
+                                  _p(idx), idx.shape[0], B, H, W, _p(out)))
+    return out
+
+
+def sparse_pool_grad_img(mij, mval, m_size, dY, idx, img_shape):
+    dY = _c(dY, np.float32)
+    R, C = dY.shape
+    mij = _c(mij, np.int64).reshape(-1, 2)
+    mval = _c(mval, np.float32).reshape(-1)
+    idx = _c(idx, np.int64).reshape(-1, 3)
+    B, H, W = img_shape[:3]
+    out = np.empty((B, H, W, C), np.float32)
+    _check(lib().shplo_pool_grad_img(_p(dY), R, C, _p(mij), _p(mval), mij.shape[0],
+                                     int(m_size[1]), _p(idx), idx.shape[0], B, H, W, _p(out)))
+    return out
+
+
+def sparse_pool_trans_grad_bev(mij, mval, m_size, dZ, idx):
+    dZ = _c(dZ, np.float32)
+    B, H, W, C = dZ.shape
+    mij = _c(mij, np.int64).reshape(-1, 2)
+    mval = _c(mval, np.float32).reshape(-1)
+    idx = _c(idx, np.int64).reshape(-1, 3)
+    R = int(m_size[0])
+    out = np.empty((R, C), np.float32)
+    _check(lib().shplo_pool_trans_grad_bev(_p(dZ), B, H, W, C, _p(idx), idx.shape[0], _p(mij),
+                                           _p(mval), mij.shape[0], R, int(m_size[1]), _p(out)))
+    return out
+
+
+def sparse_pool_layer(bev, img, mij, mval, m_size, idx, dual=False):
+    """sparse_pool_layer (sparse_pool_utils.py:61-92), use_bn=False:
+    returns (bv_fused, img_fused) as [1,H,W,C] arrays."""
+    bev = _c(bev, np.float32)
+    img = _c(img, np.float32)
+    _, Hb, Wb, Cb = bev.shape
+    pooled = sparse_pool_op(mij, mval, m_size, img, idx).reshape(1, Hb, Wb, img.shape[3])
+    bv_fused = np.concatenate([bev, pooled], axis=3)
+    if dual:
+        tp = sparse_pool_trans_op(mij, mval, m_size, bev.reshape(-1, Cb), idx, img.shape)
+        img_fused = np.concatenate([img, tp], axis=3)
+    else:
+        img_fused = img
+    return bv_fused, img_fused
+
+
+def to_bf16_bits(x):
+    """f32 -> bf16 round-to-nearest-even (as uint16 bits)."""
+    u = np.ascontiguousarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    nan = np.isnan(np.asarray(x, np.float32))
+    r[nan] = 0x7FC0
+    return r
+
+
+def from_bf16_bits(b):
+    return (np.asarray(b, np.uint16).astype(np.uint32) << 16).view(np.float32)

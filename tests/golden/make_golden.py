@@ -1,0 +1,202 @@
+"""Generate the committed golden fixtures by RUNNING the reference's own numpy
+index builders in this container.
+
+This script is the only place the reference is executed. It needs
+``/root/reference`` (absent on the GPU box) and trivial stubs for
+``tensorflow`` / ``cv2`` / ``easydict`` (TensorFlow 1.8 is not installable
+here; the builders below use only numpy -- the stubs merely satisfy
+module-level imports). Fixtures are data only: inputs and the reference's
+outputs, written as ``.npz`` next to this file.
+
+Reference functions executed (file:line, relative to /root/reference):
+
+* ``gen_sparse_pooling_input_avod``   avod/avod/utils/sparse_pool_utils.py:6-20
+* ``produce_sparse_pooling_input``    avod/avod/utils/sparse_pool_utils.py:22-58
+* MV3D ``produce_sparse_pooling_input`` MV3D_TF_release/lib/utils/sparse_pool_utils.py:22-55
+* ``BevSlices.generate_bev(output_indices=True)``
+                                      avod/avod/core/bev_generators/bev_slices.py:33-156
+* MV3D ``point_cloud_2_top_sparse``   MV3D_TF_release/lib/utils/construct_voxel.py:37-162
+
+Run:  python tests/golden/make_golden.py
+"""
+import os
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+
+from sparse_pooling_amd import synth  # noqa: E402
+
+
+def _install_stubs():
+    tf = types.ModuleType("tensorflow")
+    tf.contrib = types.SimpleNamespace(slim=types.SimpleNamespace())
+    sys.modules.setdefault("tensorflow", tf)
+    sys.modules.setdefault("cv2", types.ModuleType("cv2"))
+    ed = types.ModuleType("easydict")
+
+    class EasyDict(dict):
+        def __getattr__(self, k):
+            try:
+                return self[k]
+            except KeyError as e:
+                raise AttributeError(k) from e
+
+        def __setattr__(self, k, v):
+            self[k] = v
+
+    ed.EasyDict = EasyDict
+    sys.modules.setdefault("easydict", ed)
+    for p in (os.path.join(REF, "avod"), os.path.join(REF, "avod", "wavedata"),
+              os.path.join(REF, "MV3D_TF_release", "lib")):
+        if p not in sys.path:
+            sys.path.append(p)
+
+
+def _ref_avod():
+    import importlib
+    return importlib.import_module("avod.utils.sparse_pool_utils")
+
+
+def _index_case(name, frame, im_size, bv_size, stride, M_val=None, mv3d=False):
+    spu = _ref_avod()
+    calib = synth.StereoCalib(frame.P)
+    g = spu.gen_sparse_pooling_input_avod(frame.points.copy(), frame.voxel_indices.copy(),
+                                          calib, list(im_size), tuple(bv_size))
+    gen = {k: np.array(v, copy=True) for k, v in g.items()}
+    if mv3d:
+        import importlib
+        mv = importlib.import_module("utils.sparse_pool_utils")
+        out = mv.produce_sparse_pooling_input(g, M_val=M_val, stride=list(stride))
+    else:
+        out = spu.produce_sparse_pooling_input(g, M_val=M_val, stride=list(stride))
+    rec = dict(points=frame.points, voxel_indices=frame.voxel_indices, P=frame.P,
+               im_size=np.array(im_size), bv_size=np.array(bv_size),
+               stride=np.array(stride, dtype=np.float64),
+               gen_bv_index=gen["bv_index"], gen_img_index=gen["img_index"],
+               gen_bv_size=gen["bv_size"], gen_img_size=gen["img_size"],
+               mutated_img_index=np.asarray(g["img_index"]),
+               Mij_pool=np.asarray(out["Mij_pool"]), M_val=np.asarray(out["M_val"]),
+               M_size=np.asarray(out["M_size"]),
+               img_index_flip_pool=np.asarray(out["img_index_flip_pool"]),
+               bev_index_flip_pool=np.asarray(out["bev_index_flip_pool"]))
+    if M_val is not None:
+        rec["M_val_in"] = np.asarray(M_val)
+    np.savez_compressed(os.path.join(HERE, f"index_{name}.npz"), **rec)
+    print(f"index_{name}: N={frame.points.shape[0]} nnz={rec['Mij_pool'].shape[0]} M_size={rec['M_size']}")
+
+
+def _kat_frame():
+    """Known-answer points: with P = [[1,0,0,0],[0,1,0,0],[0,0,0,1]] the
+    projection is u=x, v=y exactly, so round-half-even ties, the strict
+    ``< W-1`` / ``>= 0`` clip bounds and the ``>= W'`` clamp are hit exactly."""
+    P = np.array([[1.0, 0, 0, 0], [0, 1.0, 0, 0], [0, 0, 0, 1.0]])
+    W, H = 1201, 363
+    xs = [0.0, -0.0, -1e-300, 0.5, 1.5, 2.5, 3.49999999, W - 1.0, W - 1.0 - 1e-9,
+          W - 1.5, W - 1.49, 1196.0, 1199.5, 598.5, 7.5, -0.5, 10.0, 11.0]
+    ys = [0.0, 0.5, 1.5, H - 1.0, H - 1 - 1e-9, H - 1.5, -1e-12, 2.5, 100.5, 361.6]
+    pts = []
+    for i, x in enumerate(xs):
+        for j, y in enumerate(ys):
+            pts.append((x, y, 1.0 + 0.25 * ((i + j) % 5)))
+    pts = np.array(pts, dtype=np.float64)
+    n = pts.shape[0]
+    hb, wb = 707, 803
+    rng = np.random.default_rng(7)
+    vox = np.stack([rng.integers(0, wb, n), rng.integers(0, hb + 2, n)], axis=1).astype(np.int64)
+    vox[:6] = [[0, 0], [wb - 1, hb - 1], [wb - 1, hb], [0, hb], [wb, hb - 1], [wb + 3, hb - 1]]
+    fr = synth.Frame(pts, vox, P, synth.FrameSpec(n, (W, H), (hb, wb)))
+    return fr, (W, H), (hb, wb)
+
+
+def _bev_slices_case():
+    """BevSlices.generate_bev(output_indices=True): voxel indices + one point per
+    BEV cell per slice (the input of the index builder)."""
+    from avod.core.bev_generators.bev_slices import BevSlices
+    from wavedata.tools.obj_detection import obj_utils
+
+    class _Utils:
+        # KittiUtils.create_slice_filter (avod/avod/datasets/kitti/kitti_utils.py:79-107)
+        # = xor of two obj_utils.get_point_filter masks.
+        @staticmethod
+        def create_slice_filter(pc, ext, gp, lo, hi):
+            a = obj_utils.get_point_filter(pc, ext, gp, hi)
+            b = obj_utils.get_point_filter(pc, ext, gp, lo)
+            return np.logical_xor(a, b)
+
+    cfg = types.SimpleNamespace(height_lo=-0.2, height_hi=2.3, num_slices=5)
+    bev = BevSlices(cfg, _Utils())
+    rng = np.random.default_rng(11)
+    n = 20000
+    pts = np.stack([rng.uniform(-39.9, 39.9, n), rng.uniform(-0.5, 2.2, n),
+                    rng.uniform(0.05, 69.9, n)], axis=0)
+    area = np.array([[-40, 40], [-5, 3], [0, 70]], dtype=np.float64)
+    gp = np.array([0.0, -1.0, 0.0, 1.65])
+    maps, vox, upts = bev.generate_bev("lidar", pts, gp, area, 0.1, output_indices=True)
+    np.savez_compressed(os.path.join(HERE, "bev_slices.npz"), point_cloud=pts, ground_plane=gp,
+                        area_extents=area, voxel_size=np.array(0.1), height_lo=np.array(-0.2),
+                        height_hi=np.array(2.3), num_slices=np.array(5),
+                        voxel_indices=vox, pts_in_voxel=upts,
+                        height_maps=np.stack(maps["height_maps"]), density_map=maps["density_map"])
+    print(f"bev_slices: N={n} voxel_indices={vox.shape} maps={np.stack(maps['height_maps']).shape}")
+
+
+def _mv3d_voxel_case():
+    """MV3D point_cloud_2_top_sparse: img_index, bv_index and M_val = 1/count."""
+    import importlib
+    cv = importlib.import_module("utils.construct_voxel")
+    rng = np.random.default_rng(13)
+    n = 6000
+    # camera frame: x side, y height (down), z forward
+    pts = np.stack([rng.uniform(-19, 19, n), rng.uniform(-0.9, 2.9, n), rng.uniform(0.5, 47, n),
+                    rng.uniform(0, 1, n)], axis=1)
+    P = synth.KITTI_P2
+    uvw = P @ np.vstack((pts[:, :3].T, np.ones(n)))
+    img_index2 = np.round(uvw[:2] / uvw[2]).astype(int)
+    calib = np.zeros((4, 12))
+    calib[0] = P.reshape(-1)
+    vd, full, img_index, bv_index, M_val = cv.point_cloud_2_top_sparse(
+        pts.copy(), points_in_cam=True, calib=calib, img_index2=img_index2.copy())
+    np.savez_compressed(os.path.join(HERE, "mv3d_voxel.npz"), points=pts, img_index2=img_index2,
+                        voxel_full_size=np.asarray(full), img_index=img_index, bv_index=bv_index,
+                        M_val=M_val, coordinate_buffer=vd["coordinate_buffer"],
+                        number_buffer=vd["number_buffer"])
+    print(f"mv3d_voxel: N={n} kept={bv_index.shape[0]} voxels={vd['number_buffer'].shape[0]}")
+
+
+def main():
+    _install_stubs()
+    c1 = synth.CONFIG1
+    f1 = synth.make_frame(c1, seed=0, n_outside=64)
+    _index_case("config1", f1, c1.im_size, c1.bv_size, c1.stride)
+    s2 = synth.FrameSpec(4000, (1200, 360), (704, 800), (1, 1))
+    _index_case("stride1", synth.make_frame(s2, seed=1, n_outside=32), s2.im_size, s2.bv_size, (1, 1))
+    s3 = synth.FrameSpec(3000, (1242, 375), (700, 800), (8, 2))
+    f3 = synth.make_frame(s3, seed=2)
+    # MV3D convention: stride[0] applies to the image, stride[1] to BEV; M_val given.
+    # All voxel rows kept in range so that len(M_val) == nnz (MV3D never drops).
+    f3.voxel_indices[:, 1] = np.minimum(f3.voxel_indices[:, 1], s3.bv_size[0] - 1)
+    mval = 1.0 / np.random.default_rng(3).integers(1, 9, f3.points.shape[0])
+    _index_case("mv3d", f3, s3.im_size, s3.bv_size, s3.stride, M_val=mval, mv3d=True)
+    s4 = synth.FrameSpec(2500, (1200, 360), (704, 800), (3, 5))
+    _index_case("oddstride", synth.make_frame(s4, seed=4, n_outside=16), s4.im_size, s4.bv_size, s4.stride)
+    fk, imk, bvk = _kat_frame()
+    _index_case("kat", fk, imk, bvk, (4, 4))
+    _index_case("kat_s1", _kat_frame()[0], imk, bvk, (1, 1))
+    s0 = synth.FrameSpec(0, (1200, 360), (704, 800), (4, 4))
+    e = synth.Frame(np.zeros((0, 3)), np.zeros((0, 2), dtype=np.int64), synth.KITTI_P2, s0)
+    try:
+        _index_case("empty", e, s0.im_size, s0.bv_size, s0.stride)
+    except Exception as ex:  # record what the reference does with no points
+        print("empty frame: reference raised", type(ex).__name__, ex)
+    _bev_slices_case()
+    _mv3d_voxel_case()
+
+
+if __name__ == "__main__":
+    main()
