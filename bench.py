@@ -1,0 +1,217 @@
+"""SHPL bench: fused frames/s + achieved HBM GB/s of the SHPL gather/scatter.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--config 2]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+Workload (BASELINE.json configs[1], "config 2"): synthetic KITTI-shaped
+frames of 20k camera-frame points, BEV 704x800x32, image 360x1200x32, fp32,
+img->BEV fused SHPL forward. One step processes F frames per GPU (default 64,
+the config-4 batch) through the whole hot path, inputs resident in HBM:
+device index build (projection, clip, strides, flatten, compaction) ->
+BEV-keyed CSR of M -> fused pooled gather + concat write of bv_fused.
+
+Frames are independent: each rank draws its own frames and runs
+them with no data-path collective ("scaling": "weak"); the only collectives
+are the barriers around the timed loop and a MAX all-reduce of the elapsed
+time. `value` = all frames of all ranks / max elapsed.
+
+roofline: the dominant kernel is the fused layer pull; its algorithmic bytes
+per launch (SURVEY §8d `layer_fwd` per frame x F) over its mean duration,
+timed with events on the launch stream. cpu_baseline: the C restatement of
+the reference path (oracle/, index build + TF-order pooling + concat), one
+core, on a bounded sample of the same frames (rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=64, help="frames per GPU per step")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 5])
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def layer_bytes(spec, nnz, u_src, frames, esz=4):
+    """SURVEY §8d layer_fwd: read bev + write bv_fused + gather unique source
+    rows + 12 B per entry (int32 dst, int32 src, f32 val)."""
+    Hb, Wb = spec.bev_feat_hw
+    cells = frames * Hb * Wb
+    return (cells * spec.c_bev * esz + cells * (spec.c_bev + spec.c_img) * esz
+            + u_src * spec.c_img * esz + 12 * nnz)
+
+
+def cpu_baseline(spec, frames_np, budget_s):
+    """Oracle (C port of the reference path) on one core, bounded sample."""
+    from oracle import shpl_oracle as orc
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    rng = np.random.default_rng(0)
+    bev = rng.standard_normal((1, Hb, Wb, spec.c_bev), dtype=np.float32)
+    img = rng.standard_normal((1, Hi, Wi, spec.c_img), dtype=np.float32)
+    t_index = t_pool = 0.0
+    done = 0
+    t0 = time.perf_counter()
+    while done < 3 or (time.perf_counter() - t0 < budget_s and done < len(frames_np)):
+        fr = frames_np[done % len(frames_np)]
+        a = time.perf_counter()
+        g = orc.gen_sparse_pooling_input_avod(fr.points, fr.voxel_indices, fr.P, list(spec.im_size),
+                                              tuple(spec.bv_size))
+        ref = orc.produce_sparse_pooling_input(g, stride=spec.stride)
+        b = time.perf_counter()
+        orc.sparse_pool_layer(bev, img, ref["Mij_pool"], ref["M_val"], ref["M_size"],
+                              ref["img_index_flip_pool"])
+        c = time.perf_counter()
+        t_index += b - a
+        t_pool += c - b
+        done += 1
+    total = t_index + t_pool
+    return {"value": round(done / total, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": (f"{done} config-{spec.n_points}pt frames through oracle/shpl_oracle.c "
+                       f"(index build {1e3 * t_index / done:.2f} ms/frame + TF-order pooling and "
+                       f"concat {1e3 * t_pool / done:.2f} ms/frame), single thread, "
+                       f"{os.cpu_count()} host cpus visible")}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from sparse_pooling_amd import pipeline, synth
+
+    spec = synth.CONFIGS[args.config]
+    dual = args.config == 5
+    F = args.frames
+    frames = [synth.make_frame(spec, seed=100000 * rank + f, n_outside=200) for f in range(F)]
+    pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, dev)
+    pl = pipeline.FusedPipeline(F, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev,
+                                spec.c_img, dual=dual, device=dev)
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    bev = torch.randn((F, Hb, Wb, spec.c_bev), device=dev, generator=g)
+    img = torch.randn((F, Hi, Wi, spec.c_img), device=dev, generator=g)
+
+    def step(ev=None):
+        pl.build_index(pts, vox, off, P)
+        pl.build_csr()
+        if ev is not None:
+            ev[0].record()
+        pl.layer(bev, img)
+        if ev is not None:
+            ev[1].record()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    nnz = int(pl.frame_off[F].item())
+    u_src = int(torch.unique(pl.pix[:nnz]).numel())
+    err = int(pl.err.item())
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    layer_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+
+    bytes_per_launch = layer_bytes(spec, nnz, u_src, F)
+    if dual:  # + the BEV->img direction: read img, write img_fused, gather BEV rows
+        bytes_per_launch += (F * Hi * Wi * spec.c_img * 4 + F * Hi * Wi * (spec.c_img + spec.c_bev) * 4
+                             + nnz * spec.c_bev * 4 + 12 * nnz)
+    achieved = bytes_per_launch / (layer_ms * 1e-3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(spec, frames[: min(F, 64)], args.cpu_seconds)
+
+    if rank == 0:
+        total_frames = F * world * args.steps
+        traffic = None
+        tpath = os.path.join(HERE, "profiles", "traffic.json")
+        if os.path.exists(tpath):
+            with open(tpath) as fh:
+                tj = json.load(fh)
+            key = f"config{args.config}_F{F}"
+            if key in tj:
+                traffic = tj[key]["hbm_bytes_per_launch"]
+        out = {
+            "metric": "SHPL fused frames/sec + achieved HBM GB/s (% of MI355X peak), 1/2/4/8 GPU",
+            "value": round(total_frames / elapsed, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded KITTI-shaped frames; no dataset on the box)",
+            "config": {
+                "workload": (f"config{args.config}: {spec.n_points} pts/frame, BEV {Hb}x{Wb}x{spec.c_bev}, "
+                             f"img {Hi}x{Wi}x{spec.c_img}, fp32, "
+                             + ("bidirectional SHPL" if dual else "img->BEV SHPL fwd")
+                             + "; step = device index build + CSR + fused layer"),
+                "frames_per_gpu_per_step": F,
+                "nnz_per_step_rank0": nnz,
+                "unique_src_pixels_rank0": u_src,
+                "parallelism": f"frame-sharded x{world}",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_pull (fused pooled gather + concat write)",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "kernel_ms": round(layer_ms, 4),
+            },
+            "cpu_baseline": cpu,
+            "index_errors": err,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,200 @@
+/*
+ * shpl.h -- C ABI of libshpl.so, the MI355X (gfx950) Sparse Non-homogeneous
+ * Pooling Layer (SHPL).
+ *
+ * The reference (YeungLy/Sparse_Pooling) has no native SHPL code: its path is
+ * numpy on the host plus four stock TensorFlow 1.8 ops. Each entry point
+ * below replaces one piece of that path; the reference interface it stands in
+ * for is cited as file:line relative to the reference checkout.
+ *
+ * Conventions
+ *   - Every pointer named d_* is DEVICE memory (HBM), owned by the caller.
+ *     The library never allocates: work buffers come from a caller-provided
+ *     workspace whose size is returned by the *_workspace_bytes queries.
+ *   - Feature maps are NHWC, contiguous per pixel row. A "row" is one BEV
+ *     cell (b*Hb*Wb + y*Wb + x) or one image pixel (b*Hi*Wi + v*Wi + u);
+ *     several frames of one batch are addressed by these global row ids.
+ *   - All calls are stream-ordered on `stream` (a hipStream_t), reentrant,
+ *     keep no global mutable state, and never synchronise the host.
+ *   - Index errors are reported through a caller-provided device word
+ *     (d_err, bit mask SHPL_EBIT_*), mirroring TF-CPU's InvalidArgumentError
+ *     without a device->host sync on the hot path; kernels skip offending
+ *     entries and never touch memory out of bounds.
+ *   - Return value: shpl_status (launch/argument errors only).
+ */
+#ifndef SHPL_H
+#define SHPL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    SHPL_OK = 0,
+    SHPL_ERR_BAD_SHAPE = 1,  /* inconsistent sizes / strides / alignment */
+    SHPL_ERR_INDEX_OOB = 2,  /* host-detectable out-of-range index */
+    SHPL_ERR_HIP = 3,        /* a HIP runtime call failed */
+    SHPL_ERR_WORKSPACE = 4,  /* workspace too small */
+    SHPL_ERR_ARG = 5         /* null pointer / bad enum */
+} shpl_status;
+
+/* bits of the device error word */
+#define SHPL_EBIT_ROW 1u     /* M row (BEV cell) outside [0, M_size[0]) */
+#define SHPL_EBIT_COL 2u     /* M column outside [0, M_size[1]) */
+#define SHPL_EBIT_PIXEL 4u   /* source index (b,v,u) outside the image */
+#define SHPL_EBIT_VALUES 8u  /* len(M_val) != nnz */
+
+typedef enum { SHPL_F32 = 0, SHPL_BF16 = 1, SHPL_F64 = 2 } shpl_dtype;
+typedef enum { SHPL_I32 = 0, SHPL_I64 = 1 } shpl_itype;
+
+/* CSR direction: which side of M the destination rows live on. */
+typedef enum {
+    SHPL_BY_CELL = 0,   /* destination = BEV cell (M row): img->BEV pooling, d_bev of trans */
+    SHPL_BY_PIXEL = 1   /* destination = image pixel of column k: BEV->img, d_img of pooling */
+} shpl_direction;
+
+/* Order of the entries that share one destination (TF-CPU accumulation order). */
+typedef enum {
+    SHPL_ORDER_ENTRY = 0,    /* nnz order: SparseTensorDenseMatMul(M, .)            */
+    SHPL_ORDER_COL_ROW = 1,  /* (col,row) order: matmul(sparse_transpose(M), .)     */
+    SHPL_ORDER_COL_ENTRY = 2 /* (col, nnz) order: matmul(M, ., adjoint_a=True) and   */
+                             /* the gradient of the transposed product              */
+} shpl_order;
+
+/* Output composition of a pull. */
+typedef enum {
+    SHPL_OUT_POOL = 0,    /* out = pooled                                  */
+    SHPL_OUT_CONCAT = 1,  /* out = [pass || pooled]   (tf.concat axis=3)    */
+    SHPL_OUT_ADD = 2      /* out = pass + pooled      (gradient add_n)      */
+} shpl_out_mode;
+
+const char *shpl_version(void);
+const char *shpl_status_string(int status);
+
+/* ---------------------------------------------------------------------------
+ * Index builder
+ * ------------------------------------------------------------------------- */
+
+/* Fused, batched: points -> projection (f64, FMA chain as numpy/OpenBLAS) ->
+ * image clip (strict bounds) -> round half-even -> strides -> BEV flatten ->
+ * in-grid filter -> stable compaction, for n_frames frames in one pass.
+ * Replaces gen_sparse_pooling_input_avod + produce_sparse_pooling_input
+ * (avod/avod/utils/sparse_pool_utils.py:6-58; projection/clip
+ * avod/avod/utils/transform.py:3-40) as called per frame by
+ * KittiDataset.load_samples (avod/avod/datasets/kitti/kitti_dataset.py:374-379).
+ *
+ *   d_point_offsets [n_frames+1] i64 : frame f owns points [off[f], off[f+1])
+ *   d_points        [N,3] f64 or f32 (camera frame)
+ *   d_voxels        [N, vox_stride] i32/i64, columns 0,1 = (x, z) BEV voxel index
+ *   d_P             [n_frames, 3, 4] f64 camera matrices (stereo_calib.p2)
+ *   im_w, im_h      image size the projection is clipped to ([W,H])
+ *   bv_h, bv_w      full-resolution BEV size ((H,W))
+ *   s_img, s_bv     strides (stride[0], stride[1] of the reference)
+ *   d_mval          optional [N] f32 weight per INPUT point (MV3D 1/count); NULL = 1.0
+ * Outputs (capacity N entries, in frame-major, point order; global ids):
+ *   d_cell [N] i32  = f*Hb'*Wb' + r           (M row)
+ *   d_pix  [N] i32  = f*Hi'*Wi' + v'*Wi' + u' (image pixel of column k)
+ *   d_val  [N] f32
+ *   d_mij  optional [N,2] i64 = reference Mij_pool rows [r, k_local]
+ *   d_flip optional [N,3] i64 = reference img_index_flip_pool rows [0, v', u']
+ *   d_frame_nnz     [n_frames] i64 (reference M_size[1] per frame)
+ *   d_frame_out_off [n_frames+1] i64 (first entry of each frame; last = total nnz)
+ * The column of entry e is e itself (M's columns are arange per frame).
+ * A kept entry whose flattened row is negative (the reference keeps it and TF
+ * then rejects it) or whose pixel is negative gets cell/pix = -1 and sets
+ * SHPL_EBIT_ROW / SHPL_EBIT_PIXEL in *d_err (nullable).
+ */
+int shpl_build_index_workspace_bytes(int n_frames, int64_t max_points_per_frame, size_t *bytes);
+int shpl_build_index(int n_frames, const int64_t *d_point_offsets, int64_t max_points_per_frame,
+                     const void *d_points, int points_dtype, const void *d_voxels, int voxels_itype,
+                     int64_t vox_stride, const double *d_P, double im_w, double im_h, double bv_h,
+                     double bv_w, double s_img, double s_bv, const float *d_mval,
+                     int32_t *d_cell, int32_t *d_pix, float *d_val, int64_t *d_mij,
+                     int64_t *d_flip, int64_t *d_frame_nnz, int64_t *d_frame_out_off,
+                     uint32_t *d_err, void *d_ws, size_t ws_bytes, void *stream);
+
+/* gen_sparse_pooling_input_avod alone (sparse_pool_utils.py:6-20), one frame:
+ * outputs bv_index [nv,2] i64 and img_index 3 rows of stride ld f64 ([u;v;0]),
+ * *d_nv = nv. Capacity n. */
+int shpl_gen_index(int64_t n, const void *d_points, int points_dtype, const void *d_voxels,
+                   int voxels_itype, int64_t vox_stride, const double *d_P, double im_w,
+                   double im_h, int64_t *d_bv_index, double *d_img_index, int64_t ld,
+                   int64_t *d_nv, void *d_ws, size_t ws_bytes, void *stream);
+
+/* produce_sparse_pooling_input alone (sparse_pool_utils.py:22-58), one frame.
+ * d_img_index (3 rows, stride ld, f64) is UPDATED IN PLACE like the
+ * reference mutates its input dict. Outputs mij/flip (reference layout) and the
+ * device map (cell, pix; val = 1). *d_nk = nk. Capacity nv. */
+int shpl_produce_index(int64_t nv, const void *d_bv_index, int bv_itype, int64_t bv_stride,
+                       double *d_img_index, int64_t ld, double im_w, double im_h, double bv_h,
+                       double bv_w, double s_img, double s_bv, int64_t *d_mij, int64_t *d_flip,
+                       int32_t *d_cell, int32_t *d_pix, int64_t *d_nk, uint32_t *d_err,
+                       void *d_ws, size_t ws_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Correspondence matrix M: validation + device map (SURVEY a8-a10 inputs)
+ * ------------------------------------------------------------------------- */
+
+/* Pack a reference-format M = tf.SparseTensor(indices=Mij [nnz,2] i64,
+ * values [n_values] f32, dense_shape=[R, ncols]) and the gather/scatter index
+ * img_index_flip [ncols,3] (b,v,u) into the device map used by the pulls,
+ * checking every index like TF-CPU's GatherNd / SparseTensorDenseMatMul /
+ * ScatterNd kernels (rpn_model.py:328-336, retinanet_model.py:330-340,
+ * network.py:243-246 build that SparseTensor from the placeholders).
+ * Global ids: cell = row_base + r, col = col_base + k, pix = pix_base +
+ * (b*img_h + v)*img_w + u. Invalid entries get -1 and set bits in *d_err. */
+int shpl_pack_map(int64_t nnz, const int64_t *d_mij, const float *d_values, int64_t n_values,
+                  int64_t n_rows, int64_t n_cols, const void *d_idx, int idx_itype,
+                  int64_t img_b, int64_t img_h, int64_t img_w, int64_t row_base, int64_t col_base,
+                  int64_t pix_base, int32_t *d_cell, int32_t *d_col, float *d_val,
+                  int32_t *d_pix, uint32_t *d_err, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * CSR keyed by destination (stable, TF accumulation order)
+ * ------------------------------------------------------------------------- */
+
+/* Sort the nnz entries by destination (cell for SHPL_BY_CELL, pix[col] for
+ * SHPL_BY_PIXEL) keeping `order` among equal destinations, and gather the
+ * per-entry source ids so the pull kernels read one contiguous list:
+ *   BY_CELL : ent_src = pix[col[e]] (image pixel), ent_col unused
+ *   BY_PIXEL: ent_src = cell[e] (BEV row),         ent_col = col[e]
+ * d_col NULL means col[e] = e. d_nnz (device, nullable) bounds the live
+ * entries (<= nnz_cap). n_keys = number of destination rows. */
+int shpl_csr_workspace_bytes(int64_t n_keys, int64_t nnz_cap, size_t *bytes);
+int shpl_build_csr(int direction, int order, int64_t nnz_cap, const int64_t *d_nnz,
+                   const int32_t *d_cell, const int32_t *d_col, const float *d_val,
+                   const int32_t *d_pix, int64_t n_keys, int32_t *d_rowptr, int32_t *d_ent_src,
+                   float *d_ent_val, int32_t *d_ent_col, void *d_ws, size_t ws_bytes,
+                   void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Pull kernels: the sparse gather / scatter-add of SHPL
+ * ------------------------------------------------------------------------- */
+
+/* For every destination row d in [0, n_dst):
+ *   pooled[d] = sum over its CSR entries e (in CSR order) of
+ *               ent_val[e] * src[ent_src[e]*src_stride + src_off + c],  c < c_pool
+ *   with d_ent_col != NULL the entries of one column k are first summed into
+ *   a partial (TF's Q[k]) which is then added to pooled (ScatterNd order);
+ *   every output element is written exactly once (zeros where d is empty).
+ *   mode SHPL_OUT_POOL  : out[d, 0:c_pool] = pooled
+ *   mode SHPL_OUT_CONCAT: out[d, 0:c_pass] = pass[d]; out[d, c_pass:] = pooled
+ *   mode SHPL_OUT_ADD   : out[d, 0:c_pool] = pass[d] + pooled
+ * f32 arithmetic without FMA contraction (matches TF-CPU bit for bit);
+ * SHPL_BF16 stores bf16 and accumulates in f32.
+ * Replaces: _sparse_pool_op + concat  (sparse_pool_utils.py:96-103, :72)  -> BY_CELL, CONCAT
+ *           _sparse_pool_trans_op + concat (sparse_pool_utils.py:105-117, :87) -> BY_PIXEL, CONCAT
+ *           their TF autodiff gradients                       -> the other direction */
+int shpl_pull(int direction, int dtype, int64_t n_dst, const int32_t *d_rowptr,
+              const int32_t *d_ent_src, const float *d_ent_val, const int32_t *d_ent_col,
+              const void *d_src, int64_t src_stride, int64_t src_off, int64_t c_pool,
+              const void *d_pass, int64_t pass_stride, int64_t pass_off, int64_t c_pass,
+              int mode, void *d_out, int64_t out_stride, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHPL_H */

@@ -1,0 +1,116 @@
+"""ctypes binding of libshpl.so (include/shpl.h).
+
+The product path has no fallback: if the HIP library is missing or cannot be
+loaded, every SHPL op raises ``ShplLibraryError``. Tensors cross the C ABI as
+raw device pointers plus the current HIP stream of the calling thread.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libshpl.so")
+
+# enums of include/shpl.h
+OK, ERR_BAD_SHAPE, ERR_INDEX_OOB, ERR_HIP, ERR_WORKSPACE, ERR_ARG = range(6)
+EBIT_ROW, EBIT_COL, EBIT_PIXEL, EBIT_VALUES = 1, 2, 4, 8
+F32, BF16, F64 = 0, 1, 2
+I32, I64 = 0, 1
+BY_CELL, BY_PIXEL = 0, 1
+ORDER_ENTRY, ORDER_COL_ROW, ORDER_COL_ENTRY = 0, 1, 2
+OUT_POOL, OUT_CONCAT, OUT_ADD = 0, 1, 2
+
+_lib = None
+
+
+class ShplLibraryError(RuntimeError):
+    pass
+
+
+def _declare(lib):
+    p, i32, i64, d, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double, ctypes.c_size_t
+    psz = ctypes.POINTER(ctypes.c_size_t)
+    sig = {
+        "shpl_version": (ctypes.c_char_p, []),
+        "shpl_status_string": (ctypes.c_char_p, [i32]),
+        "shpl_build_index_workspace_bytes": (i32, [i32, i64, psz]),
+        "shpl_build_index": (i32, [i32, p, i64, p, i32, p, i32, i64, p, d, d, d, d, d, d, p,
+                                   p, p, p, p, p, p, p, p, p, sz, p]),
+        "shpl_gen_index": (i32, [i64, p, i32, p, i32, i64, p, d, d, p, p, i64, p, p, sz, p]),
+        "shpl_produce_index": (i32, [i64, p, i32, i64, p, i64, d, d, d, d, d, d, p, p, p, p, p,
+                                     p, p, sz, p]),
+        "shpl_pack_map": (i32, [i64, p, p, i64, i64, i64, p, i32, i64, i64, i64, i64, i64, i64,
+                                p, p, p, p, p, p]),
+        "shpl_csr_workspace_bytes": (i32, [i64, i64, psz]),
+        "shpl_build_csr": (i32, [i32, i32, i64, p, p, p, p, p, i64, p, p, p, p, p, sz, p]),
+        "shpl_pull": (i32, [i32, i32, i64, p, p, p, p, p, i64, i64, i64, p, i64, i64, i64, i32,
+                            p, i64, p]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return sig
+
+
+EXPORTED = None
+
+
+def lib():
+    """Load libshpl.so once; raise loudly if it is absent (no CPU fallback)."""
+    global _lib, EXPORTED
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ShplLibraryError(
+                f"{LIB_PATH} not found: build it with `python -m sparse_pooling_amd.build` "
+                "(the SHPL path has no CPU fallback)")
+        try:
+            _lib = ctypes.CDLL(LIB_PATH)
+        except OSError as e:
+            raise ShplLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+        EXPORTED = sorted(_declare(_lib))
+    return _lib
+
+
+def check(rc, what):
+    if rc != OK:
+        msg = lib().shpl_status_string(rc).decode()
+        raise ShplLibraryError(f"{what} failed: {msg} (status {rc})")
+
+
+def ptr(t):
+    """Device pointer of a tensor (NULL for None)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def workspace(nbytes, device):
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+
+
+def index_ws_bytes(n_frames, max_points):
+    out = ctypes.c_size_t()
+    check(lib().shpl_build_index_workspace_bytes(int(n_frames), int(max_points), ctypes.byref(out)),
+          "shpl_build_index_workspace_bytes")
+    return out.value
+
+
+def csr_ws_bytes(n_keys, nnz_cap):
+    out = ctypes.c_size_t()
+    check(lib().shpl_csr_workspace_bytes(int(n_keys), int(nnz_cap), ctypes.byref(out)),
+          "shpl_csr_workspace_bytes")
+    return out.value
+
+
+def dtype_code(t):
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise TypeError(f"SHPL features must be float32 or bfloat16, got {t.dtype}")

@@ -1,0 +1,76 @@
+// shpl_common.h -- device helpers shared by the SHPL HIP kernels (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/shpl.h"
+
+#define SHPL_WAVE 64
+#define SHPL_BLOCK 256
+
+#define SHPL_HIP_CHECK(expr)                         \
+    do {                                             \
+        if ((expr) != hipSuccess) return SHPL_ERR_HIP; \
+    } while (0)
+
+#define SHPL_LAUNCH_CHECK()                                   \
+    do {                                                      \
+        if (hipGetLastError() != hipSuccess) return SHPL_ERR_HIP; \
+    } while (0)
+
+namespace shpl {
+
+// Number of set bits of `mask` in lanes below this lane (wave64).
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// Exclusive scan of one int per thread across a 256-thread block.
+// `lds` needs SHPL_BLOCK/64 + 1 ints. Returns the exclusive prefix; *total gets the block sum.
+__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t *lds, int64_t *total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds[wid] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t s = 0;
+        for (int w = 0; w < SHPL_BLOCK / 64; ++w) {
+            const int64_t t = lds[w];
+            lds[w] = s;
+            s += t;
+        }
+        lds[SHPL_BLOCK / 64] = s;
+    }
+    __syncthreads();
+    const int64_t r = x - v + lds[wid];
+    *total = lds[SHPL_BLOCK / 64];
+    __syncthreads();
+    return r;
+}
+
+// f32 -> bf16 round-to-nearest-even; NaN stays NaN (quiet).
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+    const uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+    return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+inline int grid_for(int64_t work, int64_t per_block, int cap) {
+    int64_t g = (work + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace shpl

@@ -1,0 +1,468 @@
+// shpl_index.hip -- device index builder of SHPL.
+//
+// Reference (host numpy, once per frame inside the data loader):
+//   projectToImage / clip3DwithinImage      avod/avod/utils/transform.py:3-40
+//   gen_sparse_pooling_input_avod           avod/avod/utils/sparse_pool_utils.py:6-20
+//   produce_sparse_pooling_input            avod/avod/utils/sparse_pool_utils.py:22-58
+//
+// Here every point is one thread. A frame's points are split into 256-point
+// blocks; three launches give a stable (point-order) compaction over all
+// frames of a batch at once:
+//   1. count  : evaluate each point, one kept-count per block
+//   2. scan   : one workgroup scans the block counts (frame-major) and derives
+//               the per-frame entry offsets and counts
+//   3. write  : re-evaluate, rank kept points inside the block with a wave
+//               ballot, emit at block offset + rank
+// Projection runs in f64 with the exact operation order numpy uses (an FMA
+// chain over k for np.dot, IEEE division, rint = round-half-even), so the
+// integer outputs are bit-identical to the reference (tests/golden/index_*).
+#include "shpl_common.h"
+
+namespace shpl {
+namespace {
+
+struct Frames {
+    const int64_t *pt_off;  // [n_frames+1] (device)
+    int n_frames;
+    int bpf;                // blocks per frame
+};
+
+template <typename PT>
+__device__ __forceinline__ void load_point(const void *pts, int64_t i, double &x, double &y, double &z) {
+    const PT *p = reinterpret_cast<const PT *>(pts) + 3 * i;
+    x = (double)p[0];
+    y = (double)p[1];
+    z = (double)p[2];
+}
+
+template <typename IT>
+__device__ __forceinline__ int64_t load_idx(const void *a, int64_t i) {
+    return (int64_t)reinterpret_cast<const IT *>(a)[i];
+}
+
+// projectToImage (transform.py:3-26): [u;v;w] = P [x;y;z;1]; u/=w; v/=w.
+// np.dot -> OpenBLAS dgemm: s = P0*a0, then s = fma(Pk, ak, s) for k = 1..3.
+__device__ __forceinline__ void project(const double *P, double x, double y, double z, double &u,
+                                        double &v) {
+    double r[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        double s = __dmul_rn(P[4 * i + 0], x);
+        s = __fma_rn(P[4 * i + 1], y, s);
+        s = __fma_rn(P[4 * i + 2], z, s);
+        s = __fma_rn(P[4 * i + 3], 1.0, s);
+        r[i] = s;
+    }
+    u = __ddiv_rn(r[0], r[2]);
+    v = __ddiv_rn(r[1], r[2]);
+}
+
+// clip3DwithinImage (transform.py:28-40): 0 <= u < W-1, 0 <= v < H-1.
+__device__ __forceinline__ bool in_image(double u, double v, double w, double h) {
+    return (u < w - 1.0) && (u >= 0.0) && (v >= 0.0) && (v < h - 1.0);
+}
+
+struct Geometry {
+    double im_w, im_h, s_img, s_bv;
+    double wq, hq, bhq, bwq;  // floor(size / stride)
+    int64_t n_cells;          // int(bhq*bwq)
+    int64_t n_pix;            // hq*wq
+};
+
+Geometry make_geometry(double im_w, double im_h, double bv_h, double bv_w, double s_img, double s_bv) {
+    Geometry g;
+    g.im_w = im_w;
+    g.im_h = im_h;
+    g.s_img = s_img;
+    g.s_bv = s_bv;
+    g.wq = floor(im_w / s_img);
+    g.hq = floor(im_h / s_img);
+    g.bhq = floor(bv_h / s_bv);
+    g.bwq = floor(bv_w / s_bv);
+    g.n_cells = (int64_t)(g.bhq * g.bwq);
+    g.n_pix = (int64_t)g.hq * (int64_t)g.wq;
+    return g;
+}
+
+// produce_sparse_pooling_input (sparse_pool_utils.py:22-58) on one rounded
+// image index (ur, vr) and one voxel index (vx, vz).
+struct Produced {
+    double u, v;   // strided + clamped image index (what the reference writes back)
+    int64_t r;     // flattened BEV row
+    bool inside;   // r < n_cells
+};
+
+__device__ __forceinline__ Produced produce(const Geometry &g, double ur, double vr, int64_t vx,
+                                            int64_t vz) {
+    Produced o;
+    double u = floor(__ddiv_rn(ur, g.s_img));
+    double v = floor(__ddiv_rn(vr, g.s_img));
+    if (u >= g.wq) u = g.wq - 1.0;
+    if (v >= g.hq) v = g.hq - 1.0;
+    o.u = u;
+    o.v = v;
+    const double bx = floor(__ddiv_rn((double)vx, g.s_bv));
+    const double bz = floor(__ddiv_rn((double)vz, g.s_bv));
+    o.r = (int64_t)__dadd_rn(__dmul_rn(bz, g.bwq), bx);
+    o.inside = o.r < g.n_cells;
+    return o;
+}
+
+// ------------------------------------------------------------------ stages
+// Each stage: eval() decides whether point i (of frame f) is kept; emit()
+// writes kept point i at global position pos (frame starts at fstart);
+// touch() runs for every point in the write pass (in-place side effects).
+
+template <typename PT, typename VT>
+struct FusedStage {
+    const void *pts;
+    const void *vox;
+    int64_t vstride;
+    const double *P;
+    Geometry g;
+    const float *mval;
+    int32_t *cell, *pix;
+    float *val;
+    int64_t *mij, *flip;
+    uint32_t *err;
+
+    struct Payload {
+        Produced pr;
+    };
+
+    __device__ bool eval(int f, int64_t i, Payload &pl) const {
+        double x, y, z, u, v;
+        load_point<PT>(pts, i, x, y, z);
+        project(P + 12 * f, x, y, z, u, v);
+        if (!in_image(u, v, g.im_w, g.im_h)) return false;
+        const double ur = (double)(int64_t)rint(u);
+        const double vr = (double)(int64_t)rint(v);
+        pl.pr = produce(g, ur, vr, load_idx<VT>(vox, i * vstride), load_idx<VT>(vox, i * vstride + 1));
+        return pl.pr.inside;
+    }
+    __device__ void touch(int, int64_t, const Payload &, bool) const {}
+    __device__ void emit(int f, int64_t i, int64_t pos, int64_t fstart, const Payload &pl) const {
+        const int64_t r = pl.pr.r;
+        const int64_t vi = (int64_t)pl.pr.v, ui = (int64_t)pl.pr.u;
+        const bool rok = r >= 0;
+        const bool pok = vi >= 0 && ui >= 0;
+        if ((!rok || !pok) && err) atomicOr(err, (rok ? 0u : SHPL_EBIT_ROW) | (pok ? 0u : SHPL_EBIT_PIXEL));
+        cell[pos] = rok ? (int32_t)(f * g.n_cells + r) : -1;
+        pix[pos] = pok ? (int32_t)(f * g.n_pix + vi * (int64_t)g.wq + ui) : -1;
+        val[pos] = mval ? mval[i] : 1.0f;
+        if (mij) {
+            mij[2 * pos] = r;
+            mij[2 * pos + 1] = pos - fstart;
+        }
+        if (flip) {
+            flip[3 * pos] = 0;
+            flip[3 * pos + 1] = vi;
+            flip[3 * pos + 2] = ui;
+        }
+    }
+};
+
+template <typename PT, typename VT>
+struct GenStage {  // gen_sparse_pooling_input_avod
+    const void *pts;
+    const void *vox;
+    int64_t vstride;
+    const double *P;
+    double im_w, im_h;
+    int64_t *bv_index;
+    double *img_index;
+    int64_t ld;
+
+    struct Payload {
+        double u, v;
+    };
+
+    __device__ bool eval(int f, int64_t i, Payload &pl) const {
+        double x, y, z;
+        load_point<PT>(pts, i, x, y, z);
+        project(P + 12 * f, x, y, z, pl.u, pl.v);
+        return in_image(pl.u, pl.v, im_w, im_h);
+    }
+    __device__ void touch(int, int64_t, const Payload &, bool) const {}
+    __device__ void emit(int, int64_t i, int64_t pos, int64_t, const Payload &pl) const {
+        bv_index[2 * pos] = load_idx<VT>(vox, i * vstride);
+        bv_index[2 * pos + 1] = load_idx<VT>(vox, i * vstride + 1);
+        img_index[pos] = (double)(int64_t)rint(pl.u);
+        img_index[ld + pos] = (double)(int64_t)rint(pl.v);
+        img_index[2 * ld + pos] = 0.0;
+    }
+};
+
+template <typename VT>
+struct ProduceStage {  // produce_sparse_pooling_input (in-place img_index update)
+    const void *bv;
+    int64_t bstride;
+    double *img;  // 3 rows, stride ld
+    int64_t ld;
+    Geometry g;
+    int64_t *mij, *flip;
+    int32_t *cell, *pix;
+    uint32_t *err;
+
+    struct Payload {
+        Produced pr;
+        double w;  // third row
+    };
+
+    __device__ bool eval(int, int64_t i, Payload &pl) const {
+        pl.pr = produce(g, img[i], img[ld + i], load_idx<VT>(bv, i * bstride),
+                        load_idx<VT>(bv, i * bstride + 1));
+        pl.w = img[2 * ld + i];
+        return pl.pr.inside;
+    }
+    // img_index[0:2] = floor(img_index/stride), clamped -- for EVERY point
+    // (sparse_pool_utils.py:30-34), after this thread has read its own value.
+    __device__ void touch(int, int64_t i, const Payload &pl, bool) const {
+        img[i] = pl.pr.u;
+        img[ld + i] = pl.pr.v;
+    }
+    __device__ void emit(int, int64_t, int64_t pos, int64_t, const Payload &pl) const {
+        const int64_t r = pl.pr.r;
+        const int64_t vi = (int64_t)pl.pr.v, ui = (int64_t)pl.pr.u;
+        const bool rok = r >= 0, pok = vi >= 0 && ui >= 0;
+        if ((!rok || !pok) && err) atomicOr(err, (rok ? 0u : SHPL_EBIT_ROW) | (pok ? 0u : SHPL_EBIT_PIXEL));
+        mij[2 * pos] = r;
+        mij[2 * pos + 1] = pos;
+        flip[3 * pos] = (int64_t)floor(pl.w);
+        flip[3 * pos + 1] = vi;
+        flip[3 * pos + 2] = ui;
+        if (cell) cell[pos] = rok ? (int32_t)r : -1;
+        if (pix) pix[pos] = pok ? (int32_t)(vi * (int64_t)g.wq + ui) : -1;
+    }
+};
+
+// ----------------------------------------------------------- 3-pass compaction
+
+template <typename Stage>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_count(Stage st, Frames fr, int32_t *blk_cnt) {
+    const int f = blockIdx.y;
+    const int64_t beg = fr.pt_off[f], end = fr.pt_off[f + 1];
+    const int64_t i = beg + (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x;
+    bool keep = false;
+    if (i < end) {
+        typename Stage::Payload pl;
+        keep = st.eval(f, i, pl);
+    }
+    const uint64_t m = __ballot(keep);
+    __shared__ int32_t wsum[SHPL_BLOCK / 64];
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = (int32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t s = 0;
+        for (int w = 0; w < SHPL_BLOCK / 64; ++w) s += wsum[w];
+        blk_cnt[(int64_t)f * fr.bpf + blockIdx.x] = s;
+    }
+}
+
+// One workgroup: exclusive scan of all block counts (frame-major), then the
+// per-frame offsets / counts.
+__global__ __launch_bounds__(SHPL_BLOCK) void k_scan_blocks(const int32_t *blk_cnt, int64_t *blk_off,
+                                                            Frames fr, int64_t *frame_nnz,
+                                                            int64_t *frame_out_off) {
+    __shared__ int64_t lds[SHPL_BLOCK / 64 + 1];
+    const int64_t n = (int64_t)fr.n_frames * fr.bpf;
+    int64_t carry = 0;
+    for (int64_t base = 0; base < n; base += SHPL_BLOCK) {
+        const int64_t j = base + threadIdx.x;
+        const int64_t v = j < n ? blk_cnt[j] : 0;
+        int64_t tot;
+        const int64_t ex = block_excl_scan(v, lds, &tot);
+        if (j < n) blk_off[j] = carry + ex;
+        carry += tot;
+    }
+    __syncthreads();
+    for (int f = threadIdx.x; f < fr.n_frames; f += SHPL_BLOCK) {
+        const int64_t s = blk_off[(int64_t)f * fr.bpf];
+        const int64_t e = (f + 1 < fr.n_frames) ? blk_off[(int64_t)(f + 1) * fr.bpf] : carry;
+        if (frame_out_off) frame_out_off[f] = s;
+        if (frame_nnz) frame_nnz[f] = e - s;
+    }
+    if (threadIdx.x == 0 && frame_out_off) frame_out_off[fr.n_frames] = carry;
+}
+
+template <typename Stage>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_write(Stage st, Frames fr, const int64_t *blk_off) {
+    const int f = blockIdx.y;
+    const int64_t beg = fr.pt_off[f], end = fr.pt_off[f + 1];
+    const int64_t i = beg + (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x;
+    bool keep = false;
+    typename Stage::Payload pl;
+    if (i < end) {
+        keep = st.eval(f, i, pl);
+        st.touch(f, i, pl, keep);
+    }
+    const uint64_t m = __ballot(keep);
+    __shared__ int32_t wsum[SHPL_BLOCK / 64];
+    const int wid = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) wsum[wid] = (int32_t)__popcll(m);
+    __syncthreads();
+    int32_t before = 0;
+    for (int w = 0; w < wid; ++w) before += wsum[w];
+    if (keep) {
+        const int64_t pos = blk_off[(int64_t)f * fr.bpf + blockIdx.x] + before + lane_rank(m);
+        st.emit(f, i, pos, blk_off[(int64_t)f * fr.bpf], pl);
+    }
+}
+
+struct IndexWs {
+    int32_t *blk_cnt;
+    int64_t *blk_off;
+    int64_t *frame_nnz;
+    int64_t *frame_off;
+    size_t bytes;
+};
+
+IndexWs carve(int n_frames, int64_t max_points, void *base) {
+    const int64_t bpf = (max_points + SHPL_BLOCK - 1) / SHPL_BLOCK > 0 ? (max_points + SHPL_BLOCK - 1) / SHPL_BLOCK : 1;
+    const int64_t nb = (int64_t)n_frames * bpf;
+    IndexWs w;
+    size_t o = 0;
+    char *b = (char *)base;
+    w.blk_cnt = (int32_t *)(b + o);
+    o = align_up(o + sizeof(int32_t) * nb, 256);
+    w.blk_off = (int64_t *)(b + o);
+    o = align_up(o + sizeof(int64_t) * nb, 256);
+    w.frame_nnz = (int64_t *)(b + o);
+    o = align_up(o + sizeof(int64_t) * (n_frames + 1), 256);
+    w.frame_off = (int64_t *)(b + o);
+    o = align_up(o + sizeof(int64_t) * (n_frames + 2), 256);
+    w.bytes = o;
+    return w;
+}
+
+template <typename Stage>
+int run_compaction(const Stage &st, int n_frames, const int64_t *pt_off, int64_t max_points,
+                   int64_t *frame_nnz, int64_t *frame_out_off, void *ws, size_t ws_bytes,
+                   hipStream_t stream) {
+    IndexWs w = carve(n_frames, max_points, ws);
+    if (w.bytes > ws_bytes) return SHPL_ERR_WORKSPACE;
+    Frames fr;
+    fr.pt_off = pt_off;
+    fr.n_frames = n_frames;
+    fr.bpf = (int)((max_points + SHPL_BLOCK - 1) / SHPL_BLOCK);
+    if (fr.bpf < 1) fr.bpf = 1;
+    const dim3 grid(fr.bpf, n_frames);
+    hipLaunchKernelGGL(k_count<Stage>, grid, dim3(SHPL_BLOCK), 0, stream, st, fr, w.blk_cnt);
+    SHPL_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(SHPL_BLOCK), 0, stream, w.blk_cnt, w.blk_off, fr,
+                       frame_nnz ? frame_nnz : w.frame_nnz, frame_out_off ? frame_out_off : w.frame_off);
+    SHPL_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_write<Stage>, grid, dim3(SHPL_BLOCK), 0, stream, st, fr, w.blk_off);
+    SHPL_LAUNCH_CHECK();
+    return SHPL_OK;
+}
+
+__global__ void k_set_pair(int64_t *o, int64_t a, int64_t b) {
+    o[0] = a;
+    o[1] = b;
+}
+
+}  // namespace
+}  // namespace shpl
+
+using namespace shpl;
+
+extern "C" int shpl_build_index_workspace_bytes(int n_frames, int64_t max_points_per_frame, size_t *bytes) {
+    if (!bytes || n_frames < 1 || max_points_per_frame < 0) return SHPL_ERR_ARG;
+    // + room for a single-frame [0, n] offset pair
+    *bytes = carve(n_frames, max_points_per_frame, nullptr).bytes + 256;
+    return SHPL_OK;
+}
+
+extern "C" int shpl_build_index(int n_frames, const int64_t *d_point_offsets, int64_t max_points_per_frame,
+                                const void *d_points, int points_dtype, const void *d_voxels,
+                                int voxels_itype, int64_t vox_stride, const double *d_P, double im_w,
+                                double im_h, double bv_h, double bv_w, double s_img, double s_bv,
+                                const float *d_mval, int32_t *d_cell, int32_t *d_pix, float *d_val,
+                                int64_t *d_mij, int64_t *d_flip, int64_t *d_frame_nnz,
+                                int64_t *d_frame_out_off, uint32_t *d_err, void *d_ws, size_t ws_bytes,
+                                void *stream) {
+    if (n_frames < 1 || !d_point_offsets || !d_points || !d_voxels || !d_P || !d_cell || !d_pix ||
+        !d_val || !d_ws)
+        return SHPL_ERR_ARG;
+    if (vox_stride < 2 || !(s_img > 0) || !(s_bv > 0)) return SHPL_ERR_BAD_SHAPE;
+    const Geometry g = make_geometry(im_w, im_h, bv_h, bv_w, s_img, s_bv);
+    if ((double)n_frames * (double)(g.n_cells > 0 ? g.n_cells : 0) >= 2147483647.0 ||
+        (double)n_frames * (double)(g.n_pix > 0 ? g.n_pix : 0) >= 2147483647.0)
+        return SHPL_ERR_BAD_SHAPE;
+    hipStream_t s = (hipStream_t)stream;
+#define SHPL_FUSED(PT, VT)                                                                       \
+    {                                                                                            \
+        FusedStage<PT, VT> st{d_points, d_voxels, vox_stride, d_P, g, d_mval, d_cell, d_pix,     \
+                              d_val, d_mij, d_flip, d_err};                                      \
+        return run_compaction(st, n_frames, d_point_offsets, max_points_per_frame, d_frame_nnz,  \
+                              d_frame_out_off, d_ws, ws_bytes, s);                               \
+    }
+    if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I64) SHPL_FUSED(double, int64_t)
+    if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I32) SHPL_FUSED(double, int32_t)
+    if (points_dtype == SHPL_F32 && voxels_itype == SHPL_I64) SHPL_FUSED(float, int64_t)
+    if (points_dtype == SHPL_F32 && voxels_itype == SHPL_I32) SHPL_FUSED(float, int32_t)
+#undef SHPL_FUSED
+    return SHPL_ERR_ARG;
+}
+
+// Writes the device [0, n] offsets of a single frame into the workspace tail.
+static int single_frame_offsets(int64_t n, void *ws, size_t ws_bytes, hipStream_t s, int64_t **off) {
+    const size_t need = carve(1, n, nullptr).bytes;
+    if (need + 256 > ws_bytes) return SHPL_ERR_WORKSPACE;
+    // A single frame needs device-side [0, n] offsets; they live in the workspace tail.
+    int64_t *o = (int64_t *)((char *)ws + need);
+    hipLaunchKernelGGL(k_set_pair, dim3(1), dim3(1), 0, s, o, (int64_t)0, n);
+    SHPL_LAUNCH_CHECK();
+    *off = o;
+    return SHPL_OK;
+}
+
+extern "C" int shpl_gen_index(int64_t n, const void *d_points, int points_dtype, const void *d_voxels,
+                              int voxels_itype, int64_t vox_stride, const double *d_P, double im_w,
+                              double im_h, int64_t *d_bv_index, double *d_img_index, int64_t ld,
+                              int64_t *d_nv, void *d_ws, size_t ws_bytes, void *stream) {
+    if (n < 0 || !d_P || !d_bv_index || !d_img_index || !d_nv || !d_ws) return SHPL_ERR_ARG;
+    if (n > 0 && (!d_points || !d_voxels)) return SHPL_ERR_ARG;
+    if (vox_stride < 2 || ld < n) return SHPL_ERR_BAD_SHAPE;
+    hipStream_t s = (hipStream_t)stream;
+    int64_t *off;
+    int rc = single_frame_offsets(n, d_ws, ws_bytes, s, &off);
+    if (rc) return rc;
+#define SHPL_GEN(PT, VT)                                                                          \
+    {                                                                                             \
+        GenStage<PT, VT> st{d_points, d_voxels, vox_stride, d_P, im_w, im_h, d_bv_index,          \
+                            d_img_index, ld};                                                     \
+        return run_compaction(st, 1, off, n, d_nv, nullptr, d_ws, ws_bytes, s);                   \
+    }
+    if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I64) SHPL_GEN(double, int64_t)
+    if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I32) SHPL_GEN(double, int32_t)
+    if (points_dtype == SHPL_F32 && voxels_itype == SHPL_I64) SHPL_GEN(float, int64_t)
+    if (points_dtype == SHPL_F32 && voxels_itype == SHPL_I32) SHPL_GEN(float, int32_t)
+#undef SHPL_GEN
+    return SHPL_ERR_ARG;
+}
+
+extern "C" int shpl_produce_index(int64_t nv, const void *d_bv_index, int bv_itype, int64_t bv_stride,
+                                  double *d_img_index, int64_t ld, double im_w, double im_h, double bv_h,
+                                  double bv_w, double s_img, double s_bv, int64_t *d_mij, int64_t *d_flip,
+                                  int32_t *d_cell, int32_t *d_pix, int64_t *d_nk, uint32_t *d_err,
+                                  void *d_ws, size_t ws_bytes, void *stream) {
+    if (nv < 0 || !d_mij || !d_flip || !d_nk || !d_ws) return SHPL_ERR_ARG;
+    if (nv > 0 && (!d_bv_index || !d_img_index)) return SHPL_ERR_ARG;
+    if (bv_stride < 2 || ld < nv || !(s_img > 0) || !(s_bv > 0)) return SHPL_ERR_BAD_SHAPE;
+    const Geometry g = make_geometry(im_w, im_h, bv_h, bv_w, s_img, s_bv);
+    hipStream_t s = (hipStream_t)stream;
+    int64_t *off;
+    int rc = single_frame_offsets(nv, d_ws, ws_bytes, s, &off);
+    if (rc) return rc;
+    if (bv_itype == SHPL_I64) {
+        ProduceStage<int64_t> st{d_bv_index, bv_stride, d_img_index, ld, g, d_mij, d_flip, d_cell, d_pix, d_err};
+        return run_compaction(st, 1, off, nv, d_nk, nullptr, d_ws, ws_bytes, s);
+    }
+    if (bv_itype == SHPL_I32) {
+        ProduceStage<int32_t> st{d_bv_index, bv_stride, d_img_index, ld, g, d_mij, d_flip, d_cell, d_pix, d_err};
+        return run_compaction(st, 1, off, nv, d_nk, nullptr, d_ws, ws_bytes, s);
+    }
+    return SHPL_ERR_ARG;
+}

@@ -1,0 +1,126 @@
+"""Preallocated batched SHPL pipeline: the per-step hot path of the bench.
+
+One step over a batch of B frames (all inputs already in HBM):
+
+1. ``shpl_build_index`` -- points + voxel indices + P of every frame ->
+   M (cell, pix, val) and per-frame entry counts (a1-a4, one pass);
+2. ``shpl_build_csr``   -- BEV-cell-keyed CSR of M, TF nnz order;
+3. ``shpl_pull``        -- bv_fused = [bev || pool(img)] for all frames
+   (a8 + the concat of a10), the dominant, HBM-bound kernel.
+
+Buffers are sized once for the largest frame; nothing allocates or
+synchronises inside ``step``.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .shpl_map import ShplMap
+
+
+class FusedPipeline:
+    def __init__(self, n_frames, max_points_per_frame, total_points, im_size, bv_size, stride,
+                 c_bev, c_img, dtype=torch.float32, device="cuda", dual=False):
+        dev = torch.device(device)
+        self.dev, self.dtype, self.dual = dev, dtype, dual
+        self.B = int(n_frames)
+        self.max_points = int(max_points_per_frame)
+        self.N = int(total_points)
+        self.im_size, self.bv_size = tuple(im_size), tuple(bv_size)
+        self.stride = (float(stride[0]), float(stride[1]))
+        self.Cb, self.Ci = int(c_bev), int(c_img)
+        self.Hb = int(np.floor(bv_size[0] / self.stride[1]))
+        self.Wb = int(np.floor(bv_size[1] / self.stride[1]))
+        self.Hi = int(np.floor(im_size[1] / self.stride[0]))
+        self.Wi = int(np.floor(im_size[0] / self.stride[0]))
+        self.n_cells = self.B * self.Hb * self.Wb
+        self.n_pix = self.B * self.Hi * self.Wi
+        N = max(self.N, 1)
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.cell = torch.empty(N, **i32)
+        self.pix = torch.empty(N, **i32)
+        self.val = torch.empty(N, dtype=torch.float32, device=dev)
+        self.frame_nnz = torch.empty(self.B, dtype=torch.int64, device=dev)
+        self.frame_off = torch.empty(self.B + 1, dtype=torch.int64, device=dev)
+        self.err = torch.zeros(1, **i32)
+        self.index_ws = L.workspace(L.index_ws_bytes(self.B, self.max_points), dev)
+        # BEV-cell CSR (img -> BEV)
+        self.rowptr = torch.empty(self.n_cells + 1, **i32)
+        self.ent_src = torch.empty(N, **i32)
+        self.ent_val = torch.empty(N, dtype=torch.float32, device=dev)
+        self.csr_ws = L.workspace(L.csr_ws_bytes(self.n_cells, self.N), dev)
+        self.bv_fused = torch.empty((self.B, self.Hb, self.Wb, self.Cb + self.Ci), dtype=dtype, device=dev)
+        if dual:
+            self.prowptr = torch.empty(self.n_pix + 1, **i32)
+            self.pent_src = torch.empty(N, **i32)
+            self.pent_val = torch.empty(N, dtype=torch.float32, device=dev)
+            self.pent_col = torch.empty(N, **i32)
+            self.pcsr_ws = L.workspace(L.csr_ws_bytes(self.n_pix, self.N), dev)
+            self.img_fused = torch.empty((self.B, self.Hi, self.Wi, self.Ci + self.Cb), dtype=dtype,
+                                         device=dev)
+        self._lib = L.lib()
+
+    # ------------------------------------------------------------------ steps
+    def build_index(self, points, voxels, point_offsets, P, mval=None):
+        st = L.stream_of(self.dev)
+        L.check(self._lib.shpl_build_index(
+            self.B, L.ptr(point_offsets), self.max_points, L.ptr(points),
+            L.F64 if points.dtype == torch.float64 else L.F32, L.ptr(voxels),
+            L.I64 if voxels.dtype == torch.int64 else L.I32, int(voxels.stride(0)), L.ptr(P),
+            float(self.im_size[0]), float(self.im_size[1]), float(self.bv_size[0]),
+            float(self.bv_size[1]), self.stride[0], self.stride[1], L.ptr(mval), L.ptr(self.cell),
+            L.ptr(self.pix), L.ptr(self.val), None, None, L.ptr(self.frame_nnz), L.ptr(self.frame_off),
+            L.ptr(self.err), L.ptr(self.index_ws), self.index_ws.numel(), st), "shpl_build_index")
+
+    def build_csr(self):
+        st = L.stream_of(self.dev)
+        nnz = self.frame_off[self.B:]
+        L.check(self._lib.shpl_build_csr(
+            L.BY_CELL, L.ORDER_ENTRY, self.N, L.ptr(nnz), L.ptr(self.cell), None, L.ptr(self.val),
+            L.ptr(self.pix), self.n_cells, L.ptr(self.rowptr), L.ptr(self.ent_src), L.ptr(self.ent_val),
+            None, L.ptr(self.csr_ws), self.csr_ws.numel(), st), "shpl_build_csr")
+        if self.dual:
+            L.check(self._lib.shpl_build_csr(
+                L.BY_PIXEL, L.ORDER_COL_ROW, self.N, L.ptr(nnz), L.ptr(self.cell), None,
+                L.ptr(self.val), L.ptr(self.pix), self.n_pix, L.ptr(self.prowptr),
+                L.ptr(self.pent_src), L.ptr(self.pent_val), L.ptr(self.pent_col),
+                L.ptr(self.pcsr_ws), self.pcsr_ws.numel(), st), "shpl_build_csr")
+
+    def layer(self, bev, img):
+        """bv_fused = [bev || pool(img)] (+ img_fused = [img || trans(bev)] if dual)."""
+        st = L.stream_of(self.dev)
+        dt = L.dtype_code(self.bv_fused)
+        L.check(self._lib.shpl_pull(
+            L.BY_CELL, dt, self.n_cells, L.ptr(self.rowptr), L.ptr(self.ent_src), L.ptr(self.ent_val),
+            None, L.ptr(img), self.Ci, 0, self.Ci, L.ptr(bev), self.Cb, 0, self.Cb, L.OUT_CONCAT,
+            L.ptr(self.bv_fused), self.Cb + self.Ci, st), "shpl_pull")
+        if self.dual:
+            L.check(self._lib.shpl_pull(
+                L.BY_PIXEL, dt, self.n_pix, L.ptr(self.prowptr), L.ptr(self.pent_src),
+                L.ptr(self.pent_val), L.ptr(self.pent_col), L.ptr(bev), self.Cb, 0, self.Cb, L.ptr(img),
+                self.Ci, 0, self.Ci, L.OUT_CONCAT, L.ptr(self.img_fused), self.Ci + self.Cb, st),
+                "shpl_pull")
+
+    def step(self, points, voxels, point_offsets, P, bev, img, mval=None):
+        self.build_index(points, voxels, point_offsets, P, mval)
+        self.build_csr()
+        self.layer(bev, img)
+
+    def map(self):
+        """The current M as a ShplMap (for tests)."""
+        return ShplMap(self.cell, None, self.val, self.pix, self.N, self.n_cells, self.n_pix, self.N,
+                       self.dev, nnz_dev=self.frame_off[self.B:], err=self.err)
+
+
+def stack_frames(frames, device):
+    """Upload a list of synth.Frame to the device as one batch."""
+    pts = np.concatenate([f.points for f in frames], axis=0)
+    vox = np.concatenate([f.voxel_indices for f in frames], axis=0)
+    off = np.zeros(len(frames) + 1, dtype=np.int64)
+    off[1:] = np.cumsum([f.points.shape[0] for f in frames])
+    P = np.stack([f.P.reshape(12) for f in frames])
+    t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt).to(device)  # noqa: E731
+    return (t(pts, torch.float64), t(vox, torch.int64), t(off, torch.int64), t(P, torch.float64),
+            int(max(f.points.shape[0] for f in frames)), int(pts.shape[0]))

@@ -1,0 +1,321 @@
+"""Device-side correspondence matrix M and the SHPL pulls (torch plumbing over
+the libshpl C ABI).
+
+``ShplMap`` is M resident in HBM as four flat arrays over global ids (so one
+map can hold a whole batch of frames):
+
+* ``cell[e]``  BEV row of entry e (M row, frame offset included)
+* ``col[e]``   column k of entry e (None = identity, as the index builder emits)
+* ``val[e]``   M value (f32, what TF's float32 placeholder holds)
+* ``pix[k]``   image pixel of column k (img_index_flip row, frame offset included)
+
+plus the destination-keyed CSRs built from it on demand. The pulls that use
+them implement the reference ops (avod/avod/utils/sparse_pool_utils.py:61-117)
+and their TF gradients.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .errors import InvalidArgumentError
+
+
+def _i32(n, device):
+    return torch.empty(max(int(n), 1), dtype=torch.int32, device=device)
+
+
+class ShplMap:
+    def __init__(self, cell, col, val, pix, nnz_cap, n_cells, n_pix, n_cols, device,
+                 nnz_dev=None, err=None):
+        self.cell, self.col, self.val, self.pix = cell, col, val, pix
+        self.nnz_cap = int(nnz_cap)
+        self.n_cells = int(n_cells)
+        self.n_pix = int(n_pix)
+        self.n_cols = int(n_cols)
+        self.device = device
+        self.nnz_dev = nnz_dev
+        self.err = err if err is not None else torch.zeros(1, dtype=torch.int32, device=device)
+        self._csr = {}
+
+    # ---------------------------------------------------------------- checks
+    def error_bits(self):
+        return int(self.err.item()) & 0xFFFFFFFF
+
+    def check(self):
+        """Raise like TF-CPU's InvalidArgumentError if any index was invalid
+        (one device->host read of the error word)."""
+        bits = self.error_bits()
+        if bits:
+            what = []
+            if bits & L.EBIT_ROW:
+                what.append("M row index outside [0, M_size[0])")
+            if bits & L.EBIT_COL:
+                what.append("M column index outside [0, M_size[1])")
+            if bits & L.EBIT_PIXEL:
+                what.append("source index (b, v, u) outside the feature map")
+            if bits & L.EBIT_VALUES:
+                what.append("number of M values does not match number of indices")
+            raise InvalidArgumentError("; ".join(what))
+
+    # ------------------------------------------------------------------ CSR
+    def csr(self, direction, order):
+        key = (direction, order)
+        if key in self._csr:
+            return self._csr[key]
+        n_keys = self.n_cells if direction == L.BY_CELL else self.n_pix
+        dev = self.device
+        rowptr = torch.empty(n_keys + 1, dtype=torch.int32, device=dev)
+        ent_src = _i32(self.nnz_cap, dev)
+        ent_val = torch.empty(max(self.nnz_cap, 1), dtype=torch.float32, device=dev)
+        ent_col = _i32(self.nnz_cap, dev) if direction == L.BY_PIXEL else None
+        ws = L.workspace(L.csr_ws_bytes(n_keys, self.nnz_cap), dev)
+        L.check(L.lib().shpl_build_csr(direction, order, self.nnz_cap, L.ptr(self.nnz_dev),
+                                       L.ptr(self.cell), L.ptr(self.col), L.ptr(self.val),
+                                       L.ptr(self.pix), n_keys, L.ptr(rowptr), L.ptr(ent_src),
+                                       L.ptr(ent_val), L.ptr(ent_col), L.ptr(ws), ws.numel(),
+                                       L.stream_of(dev)), "shpl_build_csr")
+        out = (rowptr, ent_src, ent_val, ent_col, ws)
+        self._csr[key] = out
+        return out
+
+
+def pack_map(mij, values, m_size, idx, img_shape, validate=True):
+    """Reference-format M (Mij [nnz,2] i64, M_val [nnz], M_size [2]) and the
+    gather index img_index_flip [ncols,3] -> ShplMap (single frame, as the
+    reference's batch-1 graphs)."""
+    dev = idx.device
+    mij = mij.to(device=dev, dtype=torch.int64).reshape(-1, 2).contiguous()
+    values = values.to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
+    if idx.dtype not in (torch.int32, torch.int64):
+        idx = idx.to(torch.int64)
+    idx = idx.reshape(-1, 3).contiguous()
+    R, ncols = int(m_size[0]), int(m_size[1])
+    if ncols != idx.shape[0]:
+        raise InvalidArgumentError(
+            f"Cannot multiply A and B because inner dimension does not match: {ncols} vs. {idx.shape[0]}")
+    nnz = mij.shape[0]
+    B, H, W = (int(s) for s in img_shape[:3])
+    cell, col = _i32(nnz, dev), _i32(nnz, dev)
+    val = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+    pix = _i32(ncols, dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    L.check(L.lib().shpl_pack_map(nnz, L.ptr(mij), L.ptr(values), values.numel(), R, ncols,
+                                  L.ptr(idx), L.I64 if idx.dtype == torch.int64 else L.I32,
+                                  B, H, W, 0, 0, 0, L.ptr(cell), L.ptr(col), L.ptr(val), L.ptr(pix),
+                                  L.ptr(err), L.stream_of(dev)), "shpl_pack_map")
+    m = ShplMap(cell, col, val, pix, nnz, R, B * H * W, ncols, dev, err=err)
+    if validate:
+        m.check()
+    return m
+
+
+# -------------------------------------------------------------------- pulls
+
+def pull(smap, direction, order, src, src_stride, src_off, c_pool, out, out_stride,
+         pass_=None, pass_stride=0, pass_off=0, c_pass=0, mode=L.OUT_POOL, n_dst=None):
+    rowptr, ent_src, ent_val, ent_col, _ = smap.csr(direction, order)
+    if n_dst is None:
+        n_dst = smap.n_cells if direction == L.BY_CELL else smap.n_pix
+    L.check(L.lib().shpl_pull(direction, L.dtype_code(out), n_dst, L.ptr(rowptr), L.ptr(ent_src),
+                              L.ptr(ent_val), L.ptr(ent_col), L.ptr(src), src_stride, src_off,
+                              c_pool, L.ptr(pass_), pass_stride, pass_off, c_pass, mode,
+                              L.ptr(out), out_stride, L.stream_of(out.device)), "shpl_pull")
+    return out
+
+
+def pool_img_to_bev(smap, img, bev_shape, bev=None):
+    """img [.., Ci] -> [B,Hb,Wb,Ci] (or [bev || pooled] when ``bev`` is given)."""
+    Ci = img.shape[-1]
+    if bev is None:
+        out = torch.empty(tuple(bev_shape[:3]) + (Ci,), dtype=img.dtype, device=img.device)
+        return pull(smap, L.BY_CELL, L.ORDER_ENTRY, img, Ci, 0, Ci, out, Ci)
+    Cb = bev.shape[-1]
+    out = torch.empty(tuple(bev.shape[:3]) + (Cb + Ci,), dtype=img.dtype, device=img.device)
+    return pull(smap, L.BY_CELL, L.ORDER_ENTRY, img, Ci, 0, Ci, out, Cb + Ci,
+                pass_=bev, pass_stride=Cb, c_pass=Cb, mode=L.OUT_CONCAT)
+
+
+def pool_bev_to_img(smap, bev, img_shape, img=None):
+    """bev [.., Cb] -> [B,Hi,Wi,Cb] (or [img || pooled] when ``img`` is given)."""
+    Cb = bev.shape[-1]
+    if img is None:
+        out = torch.empty(tuple(img_shape[:3]) + (Cb,), dtype=bev.dtype, device=bev.device)
+        return pull(smap, L.BY_PIXEL, L.ORDER_COL_ROW, bev, Cb, 0, Cb, out, Cb)
+    Ci = img.shape[-1]
+    out = torch.empty(tuple(img.shape[:3]) + (Ci + Cb,), dtype=bev.dtype, device=bev.device)
+    return pull(smap, L.BY_PIXEL, L.ORDER_COL_ROW, bev, Cb, 0, Cb, out, Ci + Cb,
+                pass_=img, pass_stride=Ci, c_pass=Ci, mode=L.OUT_CONCAT)
+
+
+# ------------------------------------------------------------------ autograd
+
+def _c(t):
+    return t if t.is_contiguous() else t.contiguous()
+
+
+class _PoolFn(torch.autograd.Function):
+    """_sparse_pool_op: gather_nd + sparse_tensor_dense_matmul + reshape."""
+
+    @staticmethod
+    def forward(ctx, img, smap, bev_shape):
+        ctx.smap = smap
+        ctx.img_shape = img.shape
+        return pool_img_to_bev(smap, _c(img), bev_shape)
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _c(g)
+        C = g.shape[-1]
+        d = torch.empty(ctx.img_shape, dtype=g.dtype, device=g.device)
+        # TF: scatter_nd(idx, matmul(M, dY, adjoint_a=True))
+        pull(ctx.smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, g, C, 0, C, d, C)
+        return d, None, None
+
+
+class _TransFn(torch.autograd.Function):
+    """_sparse_pool_trans_op: sparse_transpose + matmul + scatter_nd."""
+
+    @staticmethod
+    def forward(ctx, bev, smap, img_shape):
+        ctx.smap = smap
+        ctx.bev_shape = bev.shape
+        return pool_bev_to_img(smap, _c(bev), img_shape)
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _c(g)
+        C = g.shape[-1]
+        d = torch.empty(ctx.bev_shape, dtype=g.dtype, device=g.device)
+        # TF: matmul(sparse_transpose(M), gather_nd(dZ, idx), adjoint_a=True)
+        pull(ctx.smap, L.BY_CELL, L.ORDER_COL_ENTRY, g, C, 0, C, d, C)
+        return d, None, None
+
+
+class _PoolConcatFn(torch.autograd.Function):
+    """bv_fused = tf.concat([bev, _sparse_pool_op(M, img, idx, .)], axis=3)
+    (sparse_pool_utils.py:65-72), the concat fused into the pull."""
+
+    @staticmethod
+    def forward(ctx, bev, img, smap):
+        bev, img = _c(bev), _c(img)
+        ctx.smap, ctx.Cb, ctx.img_shape = smap, bev.shape[-1], img.shape
+        return pool_img_to_bev(smap, img, bev.shape, bev=bev)
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _c(g)
+        Cb, Ci = ctx.Cb, ctx.img_shape[-1]
+        d_img = torch.empty(ctx.img_shape, dtype=g.dtype, device=g.device)
+        pull(ctx.smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, g, Cb + Ci, Cb, Ci, d_img, Ci)
+        return g[..., :Cb].contiguous(), d_img, None
+
+
+class _DualFn(torch.autograd.Function):
+    """Dual SHPL (sparse_pool_layer with bv_index set, sparse_pool_utils.py:61-92):
+
+    forward : bv_fused  = [bev || pool(img)],  img_fused = [img || trans(bev)]
+    backward: TF's gradient with the concat split and the add_n of the two
+              paths into each input fused into one pull per input (OUT_ADD).
+    """
+
+    @staticmethod
+    def forward(ctx, bev, img, smap):
+        bev, img = _c(bev), _c(img)
+        ctx.smap, ctx.Cb, ctx.Ci = smap, bev.shape[-1], img.shape[-1]
+        ctx.bev_shape, ctx.img_shape = bev.shape, img.shape
+        return (pool_img_to_bev(smap, img, bev.shape, bev=bev),
+                pool_bev_to_img(smap, bev, img.shape, img=img))
+
+    @staticmethod
+    def backward(ctx, g_bv, g_img):
+        smap, Cb, Ci = ctx.smap, ctx.Cb, ctx.Ci
+        ref = g_bv if g_bv is not None else g_img
+        dev, dt = ref.device, ref.dtype
+        w = Cb + Ci
+        d_bev = torch.empty(ctx.bev_shape, dtype=dt, device=dev)
+        d_img = torch.empty(ctx.img_shape, dtype=dt, device=dev)
+        if g_bv is not None:
+            g_bv = _c(g_bv)
+        if g_img is not None:
+            g_img = _c(g_img)
+        # d_bev = g_bv[..., :Cb] + matmul(sparse_transpose(M), gather_nd(g_img[..., Ci:]), adjoint_a)
+        if g_img is None:
+            d_bev.copy_(g_bv[..., :Cb])
+        elif g_bv is None:
+            pull(smap, L.BY_CELL, L.ORDER_COL_ENTRY, g_img, w, Ci, Cb, d_bev, Cb)
+        else:
+            pull(smap, L.BY_CELL, L.ORDER_COL_ENTRY, g_img, w, Ci, Cb, d_bev, Cb,
+                 pass_=g_bv, pass_stride=w, c_pass=Cb, mode=L.OUT_ADD)
+        # d_img = g_img[..., :Ci] + scatter_nd(idx, matmul(M, g_bv[..., Cb:], adjoint_a))
+        if g_bv is None:
+            d_img.copy_(g_img[..., :Ci])
+        elif g_img is None:
+            pull(smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, g_bv, w, Cb, Ci, d_img, Ci)
+        else:
+            pull(smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, g_bv, w, Cb, Ci, d_img, Ci,
+                 pass_=g_img, pass_stride=w, c_pass=Ci, mode=L.OUT_ADD)
+        return d_bev, d_img, None
+
+
+def layer(bev, img, smap, dual=False):
+    """(bv_fused, img_fused) of sparse_pool_layer for a packed map."""
+    if dual:
+        return _DualFn.apply(bev, img, smap)
+    return _PoolConcatFn.apply(bev, img, smap), img
+
+
+def pool_op(img, smap, bev_shape):
+    return _PoolFn.apply(img, smap, tuple(bev_shape))
+
+
+def trans_op(bev, smap, img_shape):
+    return _TransFn.apply(bev, smap, tuple(img_shape))
+
+
+# --------------------------------------------------------------- index build
+
+class IndexBatch:
+    """Result of the fused device index builder over a batch of frames."""
+
+    def __init__(self, smap, mij, flip, frame_nnz, frame_off, n_frames, bev_hw, img_hw):
+        self.map = smap
+        self.mij, self.flip = mij, flip
+        self.frame_nnz, self.frame_off = frame_nnz, frame_off
+        self.n_frames = n_frames
+        self.bev_hw, self.img_hw = bev_hw, img_hw
+
+
+def build_index_batch(points, voxels, point_offsets, P, im_size, bv_size, stride, max_points,
+                      mval=None, ref_outputs=False, ws=None):
+    """Fused gen_sparse_pooling_input_avod + produce_sparse_pooling_input for a
+    batch of frames in one pass (shpl_build_index). All inputs are device
+    tensors; nothing synchronises the host."""
+    dev = points.device
+    n_frames = int(point_offsets.numel()) - 1
+    N = int(points.shape[0])
+    s_img, s_bv = float(stride[0]), float(stride[1])
+    wq, hq = int(np.floor(im_size[0] / s_img)), int(np.floor(im_size[1] / s_img))
+    bhq, bwq = int(np.floor(bv_size[0] / s_bv)), int(np.floor(bv_size[1] / s_bv))
+    cell, pix = _i32(N, dev), _i32(N, dev)
+    val = torch.empty(max(N, 1), dtype=torch.float32, device=dev)
+    mij = torch.empty((max(N, 1), 2), dtype=torch.int64, device=dev) if ref_outputs else None
+    flip = torch.empty((max(N, 1), 3), dtype=torch.int64, device=dev) if ref_outputs else None
+    frame_nnz = torch.empty(n_frames, dtype=torch.int64, device=dev)
+    frame_off = torch.empty(n_frames + 1, dtype=torch.int64, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    if ws is None:
+        ws = L.workspace(L.index_ws_bytes(n_frames, max_points), dev)
+    pdt = L.F64 if points.dtype == torch.float64 else L.F32
+    vit = L.I64 if voxels.dtype == torch.int64 else L.I32
+    L.check(L.lib().shpl_build_index(n_frames, L.ptr(point_offsets), int(max_points), L.ptr(points),
+                                     pdt, L.ptr(voxels), vit, int(voxels.stride(0)), L.ptr(P),
+                                     float(im_size[0]), float(im_size[1]), float(bv_size[0]),
+                                     float(bv_size[1]), s_img, s_bv, L.ptr(mval), L.ptr(cell),
+                                     L.ptr(pix), L.ptr(val), L.ptr(mij), L.ptr(flip),
+                                     L.ptr(frame_nnz), L.ptr(frame_off), L.ptr(err), L.ptr(ws),
+                                     ws.numel(), L.stream_of(dev)), "shpl_build_index")
+    smap = ShplMap(cell, None, val, pix, N, n_frames * bhq * bwq, n_frames * hq * wq, N, dev,
+                   nnz_dev=frame_off[n_frames:], err=err)
+    return IndexBatch(smap, mij, flip, frame_nnz, frame_off, n_frames, (bhq, bwq), (hq, wq))

@@ -1,0 +1,329 @@
+"""HIP path vs the CPU oracle (and the reference-generated goldens) on MI355X.
+
+Integer / index outputs must be bit-exact. Floating-point outputs carry the
+north_star contract ``max |gpu - ref| <= 1e-5`` (TOL below) and, since the
+kernels keep TF-CPU's operation order with no FMA contraction, are also
+asserted bit-identical where the oracle computes in the same precision.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import shpl_oracle as orc
+from sparse_pooling_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5  # north_star: "within 1e-5 fp32" of the TF CPU reference
+DEV = "cuda"
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _np(t):
+    return t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t)
+
+
+def _close_and_exact(a, b):
+    a, b = _np(a).astype(np.float32), _np(b).astype(np.float32)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    if a.size:
+        assert np.nanmax(np.abs(a - b)) <= TOL
+    np.testing.assert_array_equal(a, b)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from sparse_pooling_amd import _lib as L
+    L.lib()
+    assert torch.cuda.is_available()
+
+
+# ---------------------------------------------------------------- index builder
+
+INDEX = sorted(glob.glob(os.path.join(GOLD, "index_*.npz")))
+
+
+@pytest.mark.parametrize("path", INDEX, ids=[os.path.basename(p) for p in INDEX])
+def test_index_builder_vs_reference_goldens(path):
+    from sparse_pooling_amd import sparse_pool_utils as spu
+    g = np.load(path)
+    calib = synth.StereoCalib(g["P"])
+    gen = spu.gen_sparse_pooling_input_avod(g["points"], g["voxel_indices"], calib, list(g["im_size"]),
+                                            tuple(g["bv_size"]))
+    np.testing.assert_array_equal(_np(gen["bv_index"]), g["gen_bv_index"].reshape(-1, 2))
+    np.testing.assert_array_equal(_np(gen["img_index"]), g["gen_img_index"].reshape(3, -1))
+    mval = g["M_val_in"] if "M_val_in" in g.files else None
+    out = spu.produce_sparse_pooling_input(gen, M_val=mval, stride=list(g["stride"]))
+    np.testing.assert_array_equal(_np(out["Mij_pool"]), g["Mij_pool"].reshape(-1, 2))
+    np.testing.assert_array_equal(_np(out["img_index_flip_pool"]), g["img_index_flip_pool"].reshape(-1, 3))
+    np.testing.assert_array_equal(out["M_size"], g["M_size"])
+    np.testing.assert_array_equal(_np(out["M_val"]), g["M_val"])
+    np.testing.assert_array_equal(_np(gen["img_index"]), g["mutated_img_index"].reshape(3, -1))
+    # the fused single-pass builder gives the same M
+    fused = spu.build_sparse_pooling_input(g["points"], g["voxel_indices"], calib, list(g["im_size"]),
+                                           tuple(g["bv_size"]), stride=tuple(g["stride"]))
+    np.testing.assert_array_equal(_np(fused["Mij_pool"]), g["Mij_pool"].reshape(-1, 2))
+    np.testing.assert_array_equal(_np(fused["img_index_flip_pool"]), g["img_index_flip_pool"].reshape(-1, 3))
+    np.testing.assert_array_equal(fused["M_size"], g["M_size"])
+
+
+def test_produce_mutates_numpy_input_like_reference():
+    from sparse_pooling_amd import sparse_pool_utils as spu
+    g = np.load(os.path.join(GOLD, "index_config1.npz"))
+    d = {"bv_index": g["gen_bv_index"], "img_index": g["gen_img_index"].copy(),
+         "bv_size": g["gen_bv_size"], "img_size": g["gen_img_size"]}
+    spu.produce_sparse_pooling_input(d, stride=list(g["stride"]))
+    np.testing.assert_array_equal(d["img_index"], g["mutated_img_index"])
+
+
+def _oracle_frame(fr, stride):
+    gen = orc.gen_sparse_pooling_input_avod(fr.points, fr.voxel_indices, fr.P, list(fr.spec.im_size),
+                                            tuple(fr.spec.bv_size))
+    return orc.produce_sparse_pooling_input(gen, stride=stride)
+
+
+@pytest.mark.parametrize("cfg", [1, 2, 3])
+def test_batched_index_builder_matches_oracle_per_frame(cfg):
+    from sparse_pooling_amd import pipeline, shpl_map as sm
+    spec = synth.CONFIGS[cfg]
+    frames = [synth.make_frame(spec, seed=100 + f, n_outside=37 * f) for f in range(4)]
+    pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
+    ib = sm.build_index_batch(pts, vox, off, P, spec.im_size, spec.bv_size, spec.stride, maxp,
+                              ref_outputs=True)
+    fo = _np(ib.frame_off)
+    for f, fr in enumerate(frames):
+        ref = _oracle_frame(fr, spec.stride)
+        a, b = fo[f], fo[f + 1]
+        np.testing.assert_array_equal(_np(ib.mij[a:b]), ref["Mij_pool"])
+        np.testing.assert_array_equal(_np(ib.flip[a:b]), ref["img_index_flip_pool"])
+        R = int(ref["M_size"][0])
+        np.testing.assert_array_equal(_np(ib.map.cell[a:b]), ref["Mij_pool"][:, 0] + f * R)
+    assert ib.map.error_bits() == 0
+
+
+# ---------------------------------------------------------------- pooling ops
+
+def _frame_case(cfg, seed=0, dtype=np.float32):
+    spec = synth.CONFIGS[cfg]
+    fr = synth.make_frame(spec, seed=seed, n_outside=50)
+    ref = _oracle_frame(fr, spec.stride)
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    bev = synth.make_features((1, Hb, Wb, spec.c_bev), seed + 1)
+    img = synth.make_features((1, Hi, Wi, spec.c_img), seed + 2)
+    return spec, ref, bev, img
+
+
+def _M(ref):
+    from sparse_pooling_amd.sparse_pool_utils import SparseTensor
+    return SparseTensor(ref["Mij_pool"], ref["M_val"], ref["M_size"])
+
+
+@pytest.mark.parametrize("cfg", [1, 2])
+def test_sparse_pool_layer_forward(cfg):
+    from sparse_pooling_amd import sparse_pool_utils as spu
+    spec, ref, bev, img = _frame_case(cfg)
+    tb, ti = torch.from_numpy(bev).to(DEV), torch.from_numpy(img).to(DEV)
+    bv_f, img_f = spu.sparse_pool_layer([tb, ti], [spec.c_img, spec.c_bev], _M(ref),
+                                        img_index_flip=ref["img_index_flip_pool"].astype(np.int32))
+    eb, ei = orc.sparse_pool_layer(bev, img, ref["Mij_pool"], ref["M_val"], ref["M_size"],
+                                   ref["img_index_flip_pool"])
+    _close_and_exact(bv_f, eb)
+    assert img_f is ti
+
+
+@pytest.mark.parametrize("cfg", [1, 2])
+def test_dual_layer_forward_backward(cfg):
+    from sparse_pooling_amd import sparse_pool_utils as spu
+    spec, ref, bev, img = _frame_case(cfg, seed=3)
+    tb = torch.from_numpy(bev).to(DEV).requires_grad_(True)
+    ti = torch.from_numpy(img).to(DEV).requires_grad_(True)
+    bv_f, img_f = spu.sparse_pool_layer([tb, ti], [spec.c_img, spec.c_bev], _M(ref),
+                                        img_index_flip=ref["img_index_flip_pool"], bv_index=np.zeros((1, 3)))
+    eb, ei = orc.sparse_pool_layer(bev, img, ref["Mij_pool"], ref["M_val"], ref["M_size"],
+                                   ref["img_index_flip_pool"], dual=True)
+    _close_and_exact(bv_f, eb)
+    _close_and_exact(img_f, ei)
+    gb = synth.make_features(tuple(bv_f.shape), 11)
+    gi = synth.make_features(tuple(img_f.shape), 12)
+    torch.autograd.backward([bv_f, img_f], [torch.from_numpy(gb).to(DEV), torch.from_numpy(gi).to(DEV)])
+    Cb, Ci = spec.c_bev, spec.c_img
+    mij, mval, msize, idx = ref["Mij_pool"], ref["M_val"], ref["M_size"], ref["img_index_flip_pool"]
+    # TF gradient: d_img = g_img[..., :Ci] + scatter_nd(idx, M^T g_bv[..., Cb:])
+    d_img = orc.sparse_pool_grad_img(mij, mval, msize, gb[0, ..., Cb:].reshape(-1, Ci), idx, img.shape)
+    d_img = (gi[..., :Ci] + d_img).astype(np.float32)
+    # d_bev = g_bv[..., :Cb] + (M^T)^T gather_nd(g_img[..., Ci:], idx)
+    d_bev = orc.sparse_pool_trans_grad_bev(mij, mval, msize, np.ascontiguousarray(gi[..., Ci:]), idx)
+    d_bev = (gb[..., :Cb] + d_bev.reshape(bev.shape)).astype(np.float32)
+    _close_and_exact(ti.grad, d_img)
+    _close_and_exact(tb.grad, d_bev)
+
+
+def test_single_direction_ops_and_grads():
+    from sparse_pooling_amd import sparse_pool_utils as spu
+    spec, ref, bev, img = _frame_case(1, seed=5)
+    M = _M(ref)
+    idx = ref["img_index_flip_pool"]
+    ti = torch.from_numpy(img).to(DEV).requires_grad_(True)
+    Hb, Wb = spec.bev_feat_hw
+    y = spu._sparse_pool_op(M, ti, idx, [1, Hb, Wb, spec.c_img])
+    ey = orc.sparse_pool_op(ref["Mij_pool"], ref["M_val"], ref["M_size"], img, idx)
+    _close_and_exact(y, ey.reshape(1, Hb, Wb, -1))
+    g = synth.make_features(tuple(y.shape), 9)
+    y.backward(torch.from_numpy(g).to(DEV))
+    _close_and_exact(ti.grad, orc.sparse_pool_grad_img(ref["Mij_pool"], ref["M_val"], ref["M_size"],
+                                                       g.reshape(-1, spec.c_img), idx, img.shape))
+    tb = torch.from_numpy(bev).to(DEV).requires_grad_(True)
+    z = spu._sparse_pool_trans_op(M, tb, idx, [1, img.shape[1], img.shape[2], spec.c_bev])
+    ez = orc.sparse_pool_trans_op(ref["Mij_pool"], ref["M_val"], ref["M_size"], bev.reshape(-1, spec.c_bev),
+                                  idx, img.shape)
+    _close_and_exact(z, ez)
+    gz = synth.make_features(tuple(z.shape), 10)
+    z.backward(torch.from_numpy(gz).to(DEV))
+    _close_and_exact(tb.grad, orc.sparse_pool_trans_grad_bev(ref["Mij_pool"], ref["M_val"], ref["M_size"], gz,
+                                                             idx).reshape(bev.shape))
+
+
+def test_noncanonical_M_weights_and_collisions():
+    """Shuffled nnz order, several entries per column, non-unit weights,
+    heavy pixel / cell collisions, odd channel count (scalar path)."""
+    from sparse_pooling_amd import sparse_pool_utils as spu
+    rng = np.random.default_rng(21)
+    n, R, hb, wb, h, w, c = 500, 600, 20, 30, 15, 17, 3
+    idx = np.stack([np.zeros(n, np.int64), rng.integers(0, h, n), rng.integers(0, w, n)], 1)
+    idx[: n // 4, 1:] = idx[0, 1:]
+    rows = rng.integers(0, R, n)
+    rows[100:180] = rows[100]
+    extra = np.stack([rng.integers(0, R, 300), rng.integers(0, n, 300)], 1)
+    mij = np.concatenate([np.stack([rows, np.arange(n)], 1), extra]).astype(np.int64)
+    mij = mij[rng.permutation(len(mij))]
+    mval = rng.uniform(-2, 2, len(mij)).astype(np.float32)
+    img = rng.standard_normal((1, h, w, c)).astype(np.float32)
+    bev = rng.standard_normal((1, hb, wb, c)).astype(np.float32)
+    M = spu.SparseTensor(mij, mval, np.array([R, n]))
+    y = spu._sparse_pool_op(M, torch.from_numpy(img).to(DEV), idx, [1, hb, wb, c])
+    _close_and_exact(y, orc.sparse_pool_op(mij, mval, [R, n], img, idx).reshape(1, hb, wb, c))
+    z = spu._sparse_pool_trans_op(M, torch.from_numpy(bev).to(DEV), idx, [1, h, w, c])
+    _close_and_exact(z, orc.sparse_pool_trans_op(mij, mval, [R, n], bev.reshape(-1, c), idx, img.shape))
+    tb = torch.from_numpy(bev).to(DEV).requires_grad_(True)
+    ti = torch.from_numpy(img).to(DEV).requires_grad_(True)
+    bv_f, img_f = spu.sparse_pool_layer([tb, ti], [c, c], M, img_index_flip=idx, bv_index=1)
+    gb = rng.standard_normal(tuple(bv_f.shape)).astype(np.float32)
+    gi = rng.standard_normal(tuple(img_f.shape)).astype(np.float32)
+    torch.autograd.backward([bv_f, img_f], [torch.from_numpy(gb).to(DEV), torch.from_numpy(gi).to(DEV)])
+    d_img = gi[..., :c] + orc.sparse_pool_grad_img(mij, mval, [R, n], gb[0, ..., c:].reshape(-1, c), idx,
+                                                   img.shape)
+    d_bev = gb[..., :c] + orc.sparse_pool_trans_grad_bev(mij, mval, [R, n], np.ascontiguousarray(gi[..., c:]),
+                                                         idx).reshape(bev.shape)
+    _close_and_exact(ti.grad, d_img)
+    _close_and_exact(tb.grad, d_bev)
+
+
+def test_invalid_indices_raise():
+    from sparse_pooling_amd import sparse_pool_utils as spu
+    from sparse_pooling_amd.errors import InvalidArgumentError
+    spec, ref, bev, img = _frame_case(1, seed=7)
+    ti = torch.from_numpy(img).to(DEV)
+    tb = torch.from_numpy(bev).to(DEV)
+    idx = ref["img_index_flip_pool"].copy()
+    idx[5, 2] = img.shape[2]
+    with pytest.raises(InvalidArgumentError):
+        spu.sparse_pool_layer([tb, ti], [spec.c_img, spec.c_bev], _M(ref), img_index_flip=idx)
+    mij = ref["Mij_pool"].copy()
+    mij[3, 0] = ref["M_size"][0]
+    from sparse_pooling_amd.sparse_pool_utils import SparseTensor
+    with pytest.raises(InvalidArgumentError):
+        spu.sparse_pool_layer([tb, ti], [spec.c_img, spec.c_bev], SparseTensor(mij, ref["M_val"], ref["M_size"]),
+                              img_index_flip=ref["img_index_flip_pool"])
+    with pytest.raises(InvalidArgumentError):  # len(M_val) != nnz
+        spu.sparse_pool_layer([tb, ti], [spec.c_img, spec.c_bev],
+                              SparseTensor(ref["Mij_pool"], ref["M_val"][:-1], ref["M_size"]),
+                              img_index_flip=ref["img_index_flip_pool"])
+    with pytest.raises(TypeError):  # concat_bn_op is broken in the reference
+        spu.sparse_pool_layer([tb, ti], [spec.c_img, spec.c_bev], _M(ref),
+                              img_index_flip=ref["img_index_flip_pool"], use_bn=True)
+
+
+def test_empty_M():
+    from sparse_pooling_amd import sparse_pool_utils as spu
+    img = synth.make_features((1, 9, 11, 4), 1)
+    bev = synth.make_features((1, 6, 7, 4), 2)
+    M = spu.SparseTensor(np.zeros((0, 2), np.int64), np.zeros(0), np.array([42, 0]))
+    bv_f, _ = spu.sparse_pool_layer([torch.from_numpy(bev).to(DEV), torch.from_numpy(img).to(DEV)], [4, 4], M,
+                                    img_index_flip=np.zeros((0, 3), np.int32))
+    out = _np(bv_f)
+    np.testing.assert_array_equal(out[..., :4], bev)
+    assert not out[..., 4:].any()
+
+
+def test_bf16_storage_fp32_accumulate():
+    """Config 3 storage: bf16 in/out, f32 accumulation, rounded once (RNE)."""
+    from sparse_pooling_amd import sparse_pool_utils as spu
+    spec, ref, bev, img = _frame_case(3, seed=8)
+    bev16, img16 = orc.to_bf16_bits(bev), orc.to_bf16_bits(img)
+    tb = torch.from_numpy(bev16.view(np.int16)).to(DEV).view(torch.bfloat16)
+    ti = torch.from_numpy(img16.view(np.int16)).to(DEV).view(torch.bfloat16)
+    bv_f, img_f = spu.sparse_pool_layer([tb, ti], [spec.c_img, spec.c_bev], _M(ref),
+                                        img_index_flip=ref["img_index_flip_pool"], bv_index=1)
+    eb, ei = orc.sparse_pool_layer(orc.from_bf16_bits(bev16), orc.from_bf16_bits(img16), ref["Mij_pool"],
+                                   ref["M_val"], ref["M_size"], ref["img_index_flip_pool"], dual=True)
+    np.testing.assert_array_equal(_np(bv_f.view(torch.int16)).view(np.uint16), orc.to_bf16_bits(eb))
+    np.testing.assert_array_equal(_np(img_f.view(torch.int16)).view(np.uint16), orc.to_bf16_bits(ei))
+
+
+# ------------------------------------------------------------ batched pipeline
+
+@pytest.mark.parametrize("cfg,dual", [(2, False), (5, True)])
+def test_pipeline_batch_matches_oracle(cfg, dual):
+    """The bench's exact hot path (index -> CSR -> fused layer) on 3 frames."""
+    from sparse_pooling_amd import pipeline
+    spec = synth.CONFIGS[cfg]
+    frames = [synth.make_frame(spec, seed=40 + f, n_outside=25) for f in range(3)]
+    pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
+    pl = pipeline.FusedPipeline(3, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev, spec.c_img,
+                                dual=dual)
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    bev = synth.make_features((3, Hb, Wb, spec.c_bev), 1)
+    img = synth.make_features((3, Hi, Wi, spec.c_img), 2)
+    pl.step(pts, vox, off, P, torch.from_numpy(bev).to(DEV), torch.from_numpy(img).to(DEV))
+    torch.cuda.synchronize()
+    assert int(pl.err.item()) == 0
+    out = _np(pl.bv_fused)
+    iout = _np(pl.img_fused) if dual else None
+    for f, fr in enumerate(frames):
+        ref = _oracle_frame(fr, spec.stride)
+        eb, ei = orc.sparse_pool_layer(bev[f:f + 1], img[f:f + 1], ref["Mij_pool"], ref["M_val"], ref["M_size"],
+                                       ref["img_index_flip_pool"], dual=dual)
+        _close_and_exact(out[f:f + 1], eb)
+        if dual:
+            _close_and_exact(iout[f:f + 1], ei)
+
+
+def test_full_size_properties_config5():
+    """Config 5 (40k points, 64 channels, both directions) at full size:
+    adjointness <pool(x), y> == <x, trans(y)> and the pass-through halves."""
+    from sparse_pooling_amd import pipeline
+    spec = synth.CONFIGS[5]
+    frames = [synth.make_frame(spec, seed=77)]
+    pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
+    pl = pipeline.FusedPipeline(1, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev, spec.c_img,
+                                dual=True)
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    x = torch.randn((1, Hi, Wi, spec.c_img), device=DEV)
+    y = torch.randn((1, Hb, Wb, spec.c_bev), device=DEV)
+    pl.step(pts, vox, off, P, y, x)
+    torch.cuda.synchronize()
+    pooled = pl.bv_fused[..., spec.c_bev:]
+    trans = pl.img_fused[..., spec.c_img:]
+    assert torch.equal(pl.bv_fused[..., :spec.c_bev], y)
+    assert torch.equal(pl.img_fused[..., :spec.c_img], x)
+    lhs = (pooled.double() * y.double()).sum().item()
+    rhs = (x.double() * trans.double()).sum().item()
+    assert abs(lhs - rhs) <= 1e-4 * max(1.0, abs(lhs))
+    assert int(pl.frame_nnz.item()) == frames[0].points.shape[0] - int(
+        (frames[0].voxel_indices[:, 1] >= spec.bv_size[0]).sum())
