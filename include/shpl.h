@@ -156,43 +156,56 @@ int shpl_pack_map(int64_t nnz, const int64_t *d_mij, const float *d_values, int6
  * CSR keyed by destination (stable, TF accumulation order)
  * ------------------------------------------------------------------------- */
 
+/* Destination-keyed CSR of M (all device arrays, caller-owned). */
+typedef struct {
+    int32_t *rowptr;   /* [n_keys+1] entry range of each destination; rowptr[n_keys] = live nnz */
+    int32_t *ent_dst;  /* [nnz_cap] destination of each sorted entry                          */
+    int32_t *ent_src;  /* [nnz_cap] source row of each sorted entry                           */
+    float *ent_val;    /* [nnz_cap] M value of each sorted entry                              */
+    int32_t *ent_col;  /* [nnz_cap] column k of each sorted entry (SHPL_BY_PIXEL; else NULL)  */
+    uint32_t *occ;     /* [(n_keys+31)/32] occupancy bitmap: bit d set iff d has entries      */
+    int64_t n_keys;    /* destination rows                                                     */
+    int64_t nnz_cap;   /* capacity of the entry arrays                                         */
+} shpl_csr;
+
 /* Sort the nnz entries by destination (cell for SHPL_BY_CELL, pix[col] for
  * SHPL_BY_PIXEL) keeping `order` among equal destinations, and gather the
- * per-entry source ids so the pull kernels read one contiguous list:
+ * per-entry source ids so the pulls read one contiguous list:
  *   BY_CELL : ent_src = pix[col[e]] (image pixel), ent_col unused
  *   BY_PIXEL: ent_src = cell[e] (BEV row),         ent_col = col[e]
  * d_col NULL means col[e] = e. d_nnz (device, nullable) bounds the live
- * entries (<= nnz_cap). n_keys = number of destination rows. */
+ * entries (<= csr->nnz_cap). Entries whose row, column or pixel is invalid
+ * (-1 from the pack / index builder) are left out. */
 int shpl_csr_workspace_bytes(int64_t n_keys, int64_t nnz_cap, size_t *bytes);
-int shpl_build_csr(int direction, int order, int64_t nnz_cap, const int64_t *d_nnz,
-                   const int32_t *d_cell, const int32_t *d_col, const float *d_val,
-                   const int32_t *d_pix, int64_t n_keys, int32_t *d_rowptr, int32_t *d_ent_src,
-                   float *d_ent_val, int32_t *d_ent_col, void *d_ws, size_t ws_bytes,
-                   void *stream);
+int shpl_build_csr(int direction, int order, const int64_t *d_nnz, const int32_t *d_cell,
+                   const int32_t *d_col, const float *d_val, const int32_t *d_pix,
+                   const shpl_csr *csr, void *d_ws, size_t ws_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Pull kernels: the sparse gather / scatter-add of SHPL
  * ------------------------------------------------------------------------- */
 
-/* For every destination row d in [0, n_dst):
+/* For every destination row d in [0, csr->n_keys):
  *   pooled[d] = sum over its CSR entries e (in CSR order) of
  *               ent_val[e] * src[ent_src[e]*src_stride + src_off + c],  c < c_pool
- *   with d_ent_col != NULL the entries of one column k are first summed into
- *   a partial (TF's Q[k]) which is then added to pooled (ScatterNd order);
- *   every output element is written exactly once (zeros where d is empty).
- *   mode SHPL_OUT_POOL  : out[d, 0:c_pool] = pooled
+ *   with csr->ent_col set (SHPL_BY_PIXEL) the entries of one column k are
+ *   first summed into a partial (TF's Q[k]) which is then added to pooled
+ *   (ScatterNd order); every output element is written exactly once.
+ *   mode SHPL_OUT_POOL  : out[d, 0:c_pool] = pooled          (0 where d is empty)
  *   mode SHPL_OUT_CONCAT: out[d, 0:c_pass] = pass[d]; out[d, c_pass:] = pooled
  *   mode SHPL_OUT_ADD   : out[d, 0:c_pool] = pass[d] + pooled
  * f32 arithmetic without FMA contraction (matches TF-CPU bit for bit);
  * SHPL_BF16 stores bf16 and accumulates in f32.
+ * Two passes in one launch: a streaming pass writes every row that has no
+ * entries (and the pass-through half of CONCAT), a sparse pass walks the
+ * sorted entries and writes the occupied rows' pooled part.
  * Replaces: _sparse_pool_op + concat  (sparse_pool_utils.py:96-103, :72)  -> BY_CELL, CONCAT
  *           _sparse_pool_trans_op + concat (sparse_pool_utils.py:105-117, :87) -> BY_PIXEL, CONCAT
  *           their TF autodiff gradients                       -> the other direction */
-int shpl_pull(int direction, int dtype, int64_t n_dst, const int32_t *d_rowptr,
-              const int32_t *d_ent_src, const float *d_ent_val, const int32_t *d_ent_col,
-              const void *d_src, int64_t src_stride, int64_t src_off, int64_t c_pool,
-              const void *d_pass, int64_t pass_stride, int64_t pass_off, int64_t c_pass,
-              int mode, void *d_out, int64_t out_stride, void *stream);
+int shpl_pull(int direction, int dtype, const shpl_csr *csr, const void *d_src, int64_t src_stride,
+              int64_t src_off, int64_t c_pool, const void *d_pass, int64_t pass_stride,
+              int64_t pass_off, int64_t c_pass, int mode, void *d_out, int64_t out_stride,
+              void *stream);
 
 #ifdef __cplusplus
 }

@@ -135,14 +135,22 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_scan_tile_sums(int64_t *tile_sum
     if (threadIdx.x == 0) rowptr[n] = (int32_t)carry;
 }
 
+// Also writes the occupancy bitmap: thread pairs own one 32-bit word.
 __global__ __launch_bounds__(SHPL_BLOCK) void k_scan_apply(const int32_t *cnt, int64_t n, const int64_t *tile_off,
-                                                           int32_t *rowptr) {
+                                                           int32_t *rowptr, uint32_t *occ) {
+    static_assert(SCAN_ITEMS == 16, "two threads per bitmap word");
     int32_t v[SCAN_ITEMS];
     const int64_t first = (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
     load_items(cnt, n, first, v);
     int64_t s = 0;
+    uint32_t bits = 0;
 #pragma unroll
-    for (int j = 0; j < SCAN_ITEMS; ++j) s += v[j];
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+        s += v[j];
+        bits |= (v[j] > 0 ? 1u : 0u) << j;
+    }
+    const uint32_t hi = __shfl_down(bits, 1, 64);
+    if ((threadIdx.x & 1) == 0 && first < n) occ[first >> 5] = bits | (hi << 16);
     __shared__ int64_t lds[SHPL_BLOCK / 64 + 1];
     int64_t tot;
     int64_t run = block_excl_scan(s, lds, &tot) + tile_off[blockIdx.x];
@@ -189,7 +197,8 @@ __device__ __forceinline__ uint64_t order_key(const CsrIn &c, int32_t e) {
 }
 
 __global__ __launch_bounds__(SHPL_BLOCK) void k_fix(CsrIn c, const int32_t *rowptr, int64_t n_keys, const int32_t *tmp,
-                                                    int32_t *ent_src, float *ent_val, int32_t *ent_col) {
+                                                    int32_t *ent_dst, int32_t *ent_src, float *ent_val,
+                                                    int32_t *ent_col) {
     const int64_t n = rowptr[n_keys];
     for (int64_t s = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x; s < n; s += (int64_t)gridDim.x * SHPL_BLOCK) {
         const int32_t e = tmp[s];
@@ -206,6 +215,7 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_fix(CsrIn c, const int32_t *rowp
         }
         const int32_t d = a + rank;
         const int32_t k = col_of(c, e);
+        ent_dst[d] = key;
         ent_src[d] = c.direction == SHPL_BY_CELL ? c.pix[k] : c.cell[e];
         ent_val[d] = c.val[e];
         if (ent_col) ent_col[d] = k;
@@ -274,16 +284,19 @@ extern "C" int shpl_csr_workspace_bytes(int64_t n_keys, int64_t nnz_cap, size_t 
     return SHPL_OK;
 }
 
-extern "C" int shpl_build_csr(int direction, int order, int64_t nnz_cap, const int64_t *d_nnz, const int32_t *d_cell,
-                              const int32_t *d_col, const float *d_val, const int32_t *d_pix, int64_t n_keys,
-                              int32_t *d_rowptr, int32_t *d_ent_src, float *d_ent_val, int32_t *d_ent_col,
+extern "C" int shpl_build_csr(int direction, int order, const int64_t *d_nnz, const int32_t *d_cell,
+                              const int32_t *d_col, const float *d_val, const int32_t *d_pix, const shpl_csr *csr,
                               void *d_ws, size_t ws_bytes, void *stream) {
+    if (!csr) return SHPL_ERR_ARG;
     if (direction != SHPL_BY_CELL && direction != SHPL_BY_PIXEL) return SHPL_ERR_ARG;
     if (order < SHPL_ORDER_ENTRY || order > SHPL_ORDER_COL_ENTRY) return SHPL_ERR_ARG;
+    const int64_t n_keys = csr->n_keys, nnz_cap = csr->nnz_cap;
     if (n_keys < 0 || nnz_cap < 0 || n_keys >= 2147483647LL || nnz_cap >= 2147483647LL) return SHPL_ERR_BAD_SHAPE;
-    if (((uintptr_t)d_rowptr & 15u) != 0) return SHPL_ERR_BAD_SHAPE;  // int4 stores in the scan
-    if (!d_rowptr || !d_ws || (nnz_cap > 0 && (!d_cell || !d_val || !d_pix || !d_ent_src || !d_ent_val)))
+    if (!csr->rowptr || !csr->occ || !d_ws) return SHPL_ERR_ARG;
+    if (nnz_cap > 0 && (!d_cell || !d_val || !d_pix || !csr->ent_dst || !csr->ent_src || !csr->ent_val))
         return SHPL_ERR_ARG;
+    if (direction == SHPL_BY_PIXEL && nnz_cap > 0 && !csr->ent_col) return SHPL_ERR_ARG;
+    if (((uintptr_t)csr->rowptr & 15u) != 0) return SHPL_ERR_BAD_SHAPE;  // int4 stores in the scan
     CsrWs w = carve_csr(n_keys, nnz_cap, d_ws);
     if (w.bytes > ws_bytes) return SHPL_ERR_WORKSPACE;
     hipStream_t s = (hipStream_t)stream;
@@ -299,18 +312,18 @@ extern "C" int shpl_build_csr(int direction, int order, int64_t nnz_cap, const i
         hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)n_tiles), dim3(SHPL_BLOCK), 0, s, w.cnt, n_keys, w.tile);
         SHPL_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(k_scan_tile_sums, dim3(1), dim3(SHPL_BLOCK), 0, s, w.tile, n_tiles, d_rowptr, n_keys);
+    hipLaunchKernelGGL(k_scan_tile_sums, dim3(1), dim3(SHPL_BLOCK), 0, s, w.tile, n_tiles, csr->rowptr, n_keys);
     SHPL_LAUNCH_CHECK();
     if (n_tiles > 0) {
         hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)n_tiles), dim3(SHPL_BLOCK), 0, s, w.cnt, n_keys, w.tile,
-                           d_rowptr);
+                           csr->rowptr, csr->occ);
         SHPL_LAUNCH_CHECK();
     }
     if (nnz_cap > 0) {
-        hipLaunchKernelGGL(k_place, dim3(ge), dim3(SHPL_BLOCK), 0, s, c, d_rowptr, w.cnt, w.tmp);
+        hipLaunchKernelGGL(k_place, dim3(ge), dim3(SHPL_BLOCK), 0, s, c, csr->rowptr, w.cnt, w.tmp);
         SHPL_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_fix, dim3(ge), dim3(SHPL_BLOCK), 0, s, c, d_rowptr, n_keys, w.tmp, d_ent_src,
-                           d_ent_val, d_ent_col);
+        hipLaunchKernelGGL(k_fix, dim3(ge), dim3(SHPL_BLOCK), 0, s, c, csr->rowptr, n_keys, w.tmp, csr->ent_dst,
+                           csr->ent_src, csr->ent_val, csr->ent_col);
         SHPL_LAUNCH_CHECK();
     }
     return SHPL_OK;

@@ -382,9 +382,8 @@ extern "C" int shpl_build_index(int n_frames, const int64_t *d_point_offsets, in
                                 int64_t *d_mij, int64_t *d_flip, int64_t *d_frame_nnz,
                                 int64_t *d_frame_out_off, uint32_t *d_err, void *d_ws, size_t ws_bytes,
                                 void *stream) {
-    if (n_frames < 1 || !d_point_offsets || !d_points || !d_voxels || !d_P || !d_cell || !d_pix ||
-        !d_val || !d_ws)
-        return SHPL_ERR_ARG;
+    if (n_frames < 1 || !d_point_offsets || !d_P || !d_ws) return SHPL_ERR_ARG;
+    if (max_points_per_frame > 0 && (!d_points || !d_voxels || !d_cell || !d_pix || !d_val)) return SHPL_ERR_ARG;
     if (vox_stride < 2 || !(s_img > 0) || !(s_bv > 0)) return SHPL_ERR_BAD_SHAPE;
     const Geometry g = make_geometry(im_w, im_h, bv_h, bv_w, s_img, s_bv);
     if ((double)n_frames * (double)(g.n_cells > 0 ? g.n_cells : 0) >= 2147483647.0 ||

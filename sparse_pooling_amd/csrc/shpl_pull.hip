@@ -78,17 +78,24 @@ struct Chunk {
 };
 
 struct PullParams {
-    const int32_t *rowptr;
-    const int32_t *ent_src;
+    // CSR (sparse role)
+    const int32_t *nnz_live;  // &rowptr[n_keys]
+    const int32_t *ent_dst, *ent_src, *ent_col;
     const float *ent_val;
-    const int32_t *ent_col;
+    const uint32_t *occ;
+    // features
     const void *src;
     int64_t src_stride, src_off;
     const void *pass;
     int64_t pass_stride, pass_off;
     void *out;
     int64_t out_stride;
-    uint32_t n_rows, cpr, cpass;
+    // geometry (chunks of VEC elements)
+    uint32_t row0, n_rows;  // dense rows of this launch
+    uint32_t cpr;           // chunks per output row
+    uint32_t cpass;         // chunks of the pass-through half (CONCAT)
+    uint32_t cpool;         // chunks of the pooled part
+    uint32_t sparse_blocks; // blocks [0, sparse_blocks) run the sparse role
     int mode;
 };
 
@@ -98,130 +105,166 @@ __device__ __forceinline__ void fma_free_accumulate(float (&acc)[VEC], float w, 
     for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(acc[j], __fmul_rn(w, x[j]));
 }
 
-template <typename T, int VEC, bool GROUP, int U>
-__global__ __launch_bounds__(SHPL_BLOCK) void k_pull(const PullParams p) {
+__device__ __forceinline__ bool occupied(const uint32_t *occ, uint32_t row) {
+    return (occ[row >> 5] >> (row & 31u)) & 1u;
+}
+
+// Sparse role: one thread per (sorted entry s, pooled chunk c); the thread at
+// the first entry of a destination walks that destination's entries in CSR
+// (= TF) order and writes its pooled chunk once.
+template <typename T, int VEC, bool GROUP>
+__device__ __forceinline__ void sparse_role(const PullParams &p) {
     typedef Chunk<T, VEC> C;
-    typedef typename C::raw_t raw_t;
-    const uint32_t total = p.n_rows * p.cpr;
-    const uint32_t step = gridDim.x * SHPL_BLOCK;
+    const int64_t nnz = *p.nnz_live;
+    const int64_t total = nnz * (int64_t)p.cpool;
     const T *src = reinterpret_cast<const T *>(p.src) + p.src_off;
     const T *pass = reinterpret_cast<const T *>(p.pass) + p.pass_off;
     T *out = reinterpret_cast<T *>(p.out);
     const bool concat = p.mode == SHPL_OUT_CONCAT;
-    const bool add = p.mode == SHPL_OUT_ADD;
-
-    for (uint32_t g0 = blockIdx.x * SHPL_BLOCK + threadIdx.x; g0 < total; g0 += U * step) {
-        uint32_t row[U], ch[U];
-        bool live[U], copy[U];
-        raw_t r[U];
-        int32_t beg[U], end[U];
-        // phase 1: independent loads of all U chunks
+    for (int64_t t = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x; t < total;
+         t += (int64_t)p.sparse_blocks * SHPL_BLOCK) {
+        const int64_t s = t / p.cpool;
+        const uint32_t c = (uint32_t)(t - s * p.cpool);
+        const int32_t key = p.ent_dst[s];
+        if (s > 0 && p.ent_dst[s - 1] == key) continue;
+        const T *sc = src + (int64_t)c * VEC;
+        float acc[VEC];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t g = g0 + u * step;
-            live[u] = g < total && g >= g0;  // second test guards u32 wrap
-            row[u] = live[u] ? g / p.cpr : 0;
-            ch[u] = live[u] ? g - row[u] * p.cpr : 0;
-            copy[u] = live[u] && concat && ch[u] < p.cpass;
-            beg[u] = end[u] = 0;
-            if (copy[u]) {
-                r[u] = C::load_nt(pass + (int64_t)row[u] * p.pass_stride + (int64_t)ch[u] * VEC);
-            } else if (live[u]) {
-                beg[u] = p.rowptr[row[u]];
-                end[u] = p.rowptr[row[u] + 1];
-                if (add) r[u] = C::load_nt(pass + (int64_t)row[u] * p.pass_stride + (int64_t)ch[u] * VEC);
-            }
-        }
-        // phase 2: the sparse sums
+        for (int j = 0; j < VEC; ++j) acc[j] = 0.0f;
+        if (GROUP) {
+            // TF: Q[k] = sum of k's entries; out = 0 + Q[k1] + Q[k2] ... (ScatterNd order)
+            float q[VEC];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (!live[u] || copy[u]) continue;
-            const uint32_t pc = concat ? ch[u] - p.cpass : ch[u];
-            const T *s = src + (int64_t)pc * VEC;
-            float acc[VEC];
+            for (int j = 0; j < VEC; ++j) q[j] = 0.0f;
+            int32_t kprev = p.ent_col[s];
+            for (int64_t e = s; e < nnz && p.ent_dst[e] == key; ++e) {
+                const int32_t k = p.ent_col[e];
+                if (k != kprev) {
 #pragma unroll
-            for (int j = 0; j < VEC; ++j) acc[j] = 0.0f;
-            if (GROUP) {
-                // TF: Q[k] = sum over k's entries; out = 0 + Q[k1] + Q[k2] ... (ScatterNd order)
-                float q[VEC];
-#pragma unroll
-                for (int j = 0; j < VEC; ++j) q[j] = 0.0f;
-                int32_t kprev = beg[u] < end[u] ? p.ent_col[beg[u]] : 0;
-                for (int32_t e = beg[u]; e < end[u]; ++e) {
-                    const int32_t k = p.ent_col[e];
-                    if (k != kprev) {
-#pragma unroll
-                        for (int j = 0; j < VEC; ++j) {
-                            acc[j] = __fadd_rn(acc[j], q[j]);
-                            q[j] = 0.0f;
-                        }
-                        kprev = k;
+                    for (int j = 0; j < VEC; ++j) {
+                        acc[j] = __fadd_rn(acc[j], q[j]);
+                        q[j] = 0.0f;
                     }
-                    float x[VEC];
-                    C::to_f32(C::load(s + (int64_t)p.ent_src[e] * p.src_stride), x);
-                    fma_free_accumulate<VEC>(q, p.ent_val[e], x);
+                    kprev = k;
                 }
-                if (beg[u] < end[u]) {
-#pragma unroll
-                    for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(acc[j], q[j]);
-                }
-            } else {
-                for (int32_t e = beg[u]; e < end[u]; ++e) {
-                    float x[VEC];
-                    C::to_f32(C::load(s + (int64_t)p.ent_src[e] * p.src_stride), x);
-                    fma_free_accumulate<VEC>(acc, p.ent_val[e], x);
-                }
+                float x[VEC];
+                C::to_f32(C::load(sc + (int64_t)p.ent_src[e] * p.src_stride), x);
+                fma_free_accumulate<VEC>(q, p.ent_val[e], x);
             }
-            if (add) {
-                float a[VEC];
-                C::to_f32(r[u], a);
 #pragma unroll
-                for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(a[j], acc[j]);
+            for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(acc[j], q[j]);
+        } else {
+            for (int64_t e = s; e < nnz && p.ent_dst[e] == key; ++e) {
+                float x[VEC];
+                C::to_f32(C::load(sc + (int64_t)p.ent_src[e] * p.src_stride), x);
+                fma_free_accumulate<VEC>(acc, p.ent_val[e], x);
             }
-            r[u] = C::from_f32(acc);
         }
-        // phase 3: one coalesced streaming store per chunk
+        if (p.mode == SHPL_OUT_ADD) {
+            float a[VEC];
+            C::to_f32(C::load(pass + (int64_t)key * p.pass_stride + (int64_t)c * VEC), a);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (live[u]) C::store_nt(out + (int64_t)row[u] * p.out_stride + (int64_t)ch[u] * VEC, r[u]);
+            for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(a[j], acc[j]);
+        }
+        const uint32_t oc = (concat ? p.cpass : 0u) + c;
+        C::store_nt(out + (int64_t)key * p.out_stride + (int64_t)oc * VEC, C::from_f32(acc));
     }
 }
 
+// Dense role: every chunk of every row that the sparse role does not own --
+// the pass-through half of CONCAT, zeros of empty rows (POOL / CONCAT),
+// pass + 0 of empty rows (ADD). U chunks per thread, loads issued first.
+template <typename T, int VEC, int U>
+__device__ __forceinline__ void dense_role(const PullParams &p, uint32_t vblock, uint32_t vgrid) {
+    typedef Chunk<T, VEC> C;
+    typedef typename C::raw_t raw_t;
+    const uint32_t total = p.n_rows * p.cpr;
+    const uint32_t step = vgrid * SHPL_BLOCK;
+    const T *pass = reinterpret_cast<const T *>(p.pass) + p.pass_off;
+    T *out = reinterpret_cast<T *>(p.out);
+    const bool concat = p.mode == SHPL_OUT_CONCAT;
+    const bool add = p.mode == SHPL_OUT_ADD;
+    for (uint32_t g0 = vblock * SHPL_BLOCK + threadIdx.x; g0 < total; g0 += U * step) {
+        uint32_t row[U], ch[U];
+        bool store[U], load[U];
+        raw_t r[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t g = g0 + u * step;
+            const bool live = g < total && g >= g0;
+            row[u] = live ? p.row0 + g / p.cpr : 0u;
+            ch[u] = live ? g - (row[u] - p.row0) * p.cpr : 0u;
+            const bool copy = concat && ch[u] < p.cpass;
+            store[u] = live && (copy || !occupied(p.occ, row[u]));
+            load[u] = store[u] && (copy || add);
+            if (load[u]) r[u] = C::load_nt(pass + (int64_t)row[u] * p.pass_stride + (int64_t)ch[u] * VEC);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!store[u]) continue;
+            if (add) {  // pass + 0.0f (TF's add_n with an all-zero scatter turns -0 into +0)
+                float a[VEC];
+                C::to_f32(r[u], a);
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) a[j] = __fadd_rn(a[j], 0.0f);
+                r[u] = C::from_f32(a);
+            } else if (!load[u]) {
+                float z[VEC];
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) z[j] = 0.0f;
+                r[u] = C::from_f32(z);
+            }
+            C::store_nt(out + (int64_t)row[u] * p.out_stride + (int64_t)ch[u] * VEC, r[u]);
+        }
+    }
+}
+
+template <typename T, int VEC, bool GROUP, int U>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_pull(const PullParams p) {
+    if (blockIdx.x < p.sparse_blocks)
+        sparse_role<T, VEC, GROUP>(p);
+    else
+        dense_role<T, VEC, U>(p, blockIdx.x - p.sparse_blocks, gridDim.x - p.sparse_blocks);
+}
+
 constexpr int PULL_U = 4;
+constexpr int DENSE_BLOCKS_MAX = 256 * 8;
+constexpr int SPARSE_BLOCKS_MAX = 512;
 
 template <typename T, int VEC>
-int launch_pull(PullParams p, bool group, hipStream_t s) {
+int launch_pull(PullParams p, bool group, int64_t nnz_cap, hipStream_t s) {
     const uint64_t total = (uint64_t)p.n_rows * p.cpr;
-    // grid: enough 256-thread blocks to fill every CU several times, each thread U chunks per step
-    const int grid = grid_for((int64_t)((total + PULL_U - 1) / PULL_U), SHPL_BLOCK, 256 * 8);
+    const int dense = grid_for((int64_t)((total + PULL_U - 1) / PULL_U), SHPL_BLOCK, DENSE_BLOCKS_MAX);
+    const int grid = dense + (int)p.sparse_blocks;
     if (group)
         hipLaunchKernelGGL((k_pull<T, VEC, true, PULL_U>), dim3(grid), dim3(SHPL_BLOCK), 0, s, p);
     else
         hipLaunchKernelGGL((k_pull<T, VEC, false, PULL_U>), dim3(grid), dim3(SHPL_BLOCK), 0, s, p);
     SHPL_LAUNCH_CHECK();
+    (void)nnz_cap;
     return SHPL_OK;
 }
 
-bool aligned(const void *ptr, int64_t off_elems, int64_t elem, int64_t a) {
-    return ((uintptr_t)ptr + (uintptr_t)(off_elems * elem)) % (uintptr_t)a == 0;
-}
+bool aligned(const void *ptr, int64_t a) { return ((uintptr_t)ptr) % (uintptr_t)a == 0; }
 
 }  // namespace
 }  // namespace shpl
 
 using namespace shpl;
 
-extern "C" int shpl_pull(int direction, int dtype, int64_t n_dst, const int32_t *d_rowptr, const int32_t *d_ent_src,
-                         const float *d_ent_val, const int32_t *d_ent_col, const void *d_src, int64_t src_stride,
+extern "C" int shpl_pull(int direction, int dtype, const shpl_csr *csr, const void *d_src, int64_t src_stride,
                          int64_t src_off, int64_t c_pool, const void *d_pass, int64_t pass_stride, int64_t pass_off,
                          int64_t c_pass, int mode, void *d_out, int64_t out_stride, void *stream) {
+    if (!csr) return SHPL_ERR_ARG;
     if (direction != SHPL_BY_CELL && direction != SHPL_BY_PIXEL) return SHPL_ERR_ARG;
-    if (direction == SHPL_BY_CELL && d_ent_col) return SHPL_ERR_ARG;
+    if (direction == SHPL_BY_PIXEL && csr->nnz_cap > 0 && !csr->ent_col) return SHPL_ERR_ARG;
     if (dtype != SHPL_F32 && dtype != SHPL_BF16) return SHPL_ERR_ARG;
     if (mode < SHPL_OUT_POOL || mode > SHPL_OUT_ADD) return SHPL_ERR_ARG;
-    if (n_dst < 0 || c_pool < 0 || c_pass < 0) return SHPL_ERR_BAD_SHAPE;
+    const int64_t n_dst = csr->n_keys;
+    if (n_dst < 0 || n_dst >= 2147483647LL || c_pool < 0 || c_pass < 0) return SHPL_ERR_BAD_SHAPE;
     if (n_dst == 0) return SHPL_OK;
-    if (!d_rowptr || !d_out || (c_pool > 0 && !d_src)) return SHPL_ERR_ARG;
+    if (!csr->rowptr || !csr->occ || !d_out || (c_pool > 0 && !d_src)) return SHPL_ERR_ARG;
+    if (csr->nnz_cap > 0 && (!csr->ent_dst || !csr->ent_src || !csr->ent_val)) return SHPL_ERR_ARG;
     if (mode != SHPL_OUT_POOL && !d_pass) return SHPL_ERR_ARG;
     if (mode == SHPL_OUT_ADD && c_pass != c_pool) return SHPL_ERR_BAD_SHAPE;
     const int64_t width = mode == SHPL_OUT_CONCAT ? c_pass + c_pool : c_pool;
@@ -232,39 +275,49 @@ extern "C" int shpl_pull(int direction, int dtype, int64_t n_dst, const int32_t 
     const int64_t esz = dtype == SHPL_F32 ? 4 : 2;
     const int64_t vec = 16 / esz;
     // 16-byte chunks need every row start and every channel split on a 16-byte boundary
-    bool v16 = c_pool % vec == 0 && out_stride % vec == 0 && aligned(d_out, 0, esz, 16);
-    if (c_pool > 0) v16 = v16 && src_stride % vec == 0 && src_off % vec == 0 && aligned(d_src, 0, esz, 16);
+    bool v16 = c_pool % vec == 0 && out_stride % vec == 0 && aligned(d_out, 16);
+    if (c_pool > 0)
+        v16 = v16 && src_stride % vec == 0 && src_off % vec == 0 && aligned(d_src, 16);
     if (mode != SHPL_OUT_POOL)
-        v16 = v16 && c_pass % vec == 0 && pass_stride % vec == 0 && pass_off % vec == 0 && aligned(d_pass, 0, esz, 16);
+        v16 = v16 && c_pass % vec == 0 && pass_stride % vec == 0 && pass_off % vec == 0 && aligned(d_pass, 16);
     const int64_t v = v16 ? vec : 1;
     PullParams p;
-    p.ent_src = d_ent_src;
-    p.ent_val = d_ent_val;
-    p.ent_col = d_ent_col;
+    p.nnz_live = csr->rowptr + n_dst;
+    p.ent_dst = csr->ent_dst;
+    p.ent_src = csr->ent_src;
+    p.ent_col = csr->ent_col;
+    p.ent_val = csr->ent_val;
+    p.occ = csr->occ;
     p.src = d_src;
     p.src_stride = src_stride;
     p.src_off = src_off;
+    p.pass = d_pass;
     p.pass_stride = pass_stride;
     p.pass_off = pass_off;
+    p.out = d_out;
     p.out_stride = out_stride;
     p.mode = mode;
     p.cpr = (uint32_t)(width / v);
     p.cpass = mode == SHPL_OUT_CONCAT ? (uint32_t)(c_pass / v) : 0u;
+    p.cpool = (uint32_t)(c_pool / v);
     hipStream_t s = (hipStream_t)stream;
-    // keep n_rows*cpr inside u32 (a launch covers at most 2^31 chunks)
+    const bool group = direction == SHPL_BY_PIXEL;
+    // a launch covers at most 2^31 dense chunks (u32 index math); the sparse
+    // role rides on the first launch only
     const int64_t rows_per_launch = ((int64_t)1 << 31) / (int64_t)p.cpr;
     for (int64_t r0 = 0; r0 < n_dst; r0 += rows_per_launch) {
         const int64_t nr = (n_dst - r0) < rows_per_launch ? (n_dst - r0) : rows_per_launch;
-        p.rowptr = d_rowptr + r0;
-        p.pass = d_pass ? (const void *)((const char *)d_pass + r0 * pass_stride * esz) : nullptr;
-        p.out = (void *)((char *)d_out + r0 * out_stride * esz);
+        p.row0 = (uint32_t)r0;
         p.n_rows = (uint32_t)nr;
+        p.sparse_blocks = (r0 == 0 && c_pool > 0 && csr->nnz_cap > 0)
+                              ? (uint32_t)grid_for(csr->nnz_cap * (int64_t)p.cpool, SHPL_BLOCK, SPARSE_BLOCKS_MAX)
+                              : 0u;
         int rc;
-        const bool group = d_ent_col != nullptr;
         if (dtype == SHPL_F32)
-            rc = v16 ? launch_pull<float, 4>(p, group, s) : launch_pull<float, 1>(p, group, s);
+            rc = v16 ? launch_pull<float, 4>(p, group, csr->nnz_cap, s) : launch_pull<float, 1>(p, group, csr->nnz_cap, s);
         else
-            rc = v16 ? launch_pull<uint16_t, 8>(p, group, s) : launch_pull<uint16_t, 1>(p, group, s);
+            rc = v16 ? launch_pull<uint16_t, 8>(p, group, csr->nnz_cap, s)
+                     : launch_pull<uint16_t, 1>(p, group, csr->nnz_cap, s);
         if (rc) return rc;
     }
     return SHPL_OK;

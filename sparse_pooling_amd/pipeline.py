@@ -46,18 +46,10 @@ class FusedPipeline:
         self.frame_off = torch.empty(self.B + 1, dtype=torch.int64, device=dev)
         self.err = torch.zeros(1, **i32)
         self.index_ws = L.workspace(L.index_ws_bytes(self.B, self.max_points), dev)
-        # BEV-cell CSR (img -> BEV)
-        self.rowptr = torch.empty(self.n_cells + 1, **i32)
-        self.ent_src = torch.empty(N, **i32)
-        self.ent_val = torch.empty(N, dtype=torch.float32, device=dev)
-        self.csr_ws = L.workspace(L.csr_ws_bytes(self.n_cells, self.N), dev)
+        self.csr = L.Csr(self.n_cells, self.N, dev, with_col=False)  # BEV-cell CSR (img -> BEV)
         self.bv_fused = torch.empty((self.B, self.Hb, self.Wb, self.Cb + self.Ci), dtype=dtype, device=dev)
         if dual:
-            self.prowptr = torch.empty(self.n_pix + 1, **i32)
-            self.pent_src = torch.empty(N, **i32)
-            self.pent_val = torch.empty(N, dtype=torch.float32, device=dev)
-            self.pent_col = torch.empty(N, **i32)
-            self.pcsr_ws = L.workspace(L.csr_ws_bytes(self.n_pix, self.N), dev)
+            self.pcsr = L.Csr(self.n_pix, self.N, dev, with_col=True)  # pixel CSR (BEV -> img)
             self.img_fused = torch.empty((self.B, self.Hi, self.Wi, self.Ci + self.Cb), dtype=dtype,
                                          device=dev)
         self._lib = L.lib()
@@ -78,30 +70,25 @@ class FusedPipeline:
         st = L.stream_of(self.dev)
         nnz = self.frame_off[self.B:]
         L.check(self._lib.shpl_build_csr(
-            L.BY_CELL, L.ORDER_ENTRY, self.N, L.ptr(nnz), L.ptr(self.cell), None, L.ptr(self.val),
-            L.ptr(self.pix), self.n_cells, L.ptr(self.rowptr), L.ptr(self.ent_src), L.ptr(self.ent_val),
-            None, L.ptr(self.csr_ws), self.csr_ws.numel(), st), "shpl_build_csr")
+            L.BY_CELL, L.ORDER_ENTRY, L.ptr(nnz), L.ptr(self.cell), None, L.ptr(self.val), L.ptr(self.pix),
+            self.csr.ref(), L.ptr(self.csr.ws), self.csr.ws.numel(), st), "shpl_build_csr")
         if self.dual:
             L.check(self._lib.shpl_build_csr(
-                L.BY_PIXEL, L.ORDER_COL_ROW, self.N, L.ptr(nnz), L.ptr(self.cell), None,
-                L.ptr(self.val), L.ptr(self.pix), self.n_pix, L.ptr(self.prowptr),
-                L.ptr(self.pent_src), L.ptr(self.pent_val), L.ptr(self.pent_col),
-                L.ptr(self.pcsr_ws), self.pcsr_ws.numel(), st), "shpl_build_csr")
+                L.BY_PIXEL, L.ORDER_COL_ROW, L.ptr(nnz), L.ptr(self.cell), None, L.ptr(self.val),
+                L.ptr(self.pix), self.pcsr.ref(), L.ptr(self.pcsr.ws), self.pcsr.ws.numel(), st),
+                "shpl_build_csr")
 
     def layer(self, bev, img):
         """bv_fused = [bev || pool(img)] (+ img_fused = [img || trans(bev)] if dual)."""
         st = L.stream_of(self.dev)
         dt = L.dtype_code(self.bv_fused)
         L.check(self._lib.shpl_pull(
-            L.BY_CELL, dt, self.n_cells, L.ptr(self.rowptr), L.ptr(self.ent_src), L.ptr(self.ent_val),
-            None, L.ptr(img), self.Ci, 0, self.Ci, L.ptr(bev), self.Cb, 0, self.Cb, L.OUT_CONCAT,
-            L.ptr(self.bv_fused), self.Cb + self.Ci, st), "shpl_pull")
+            L.BY_CELL, dt, self.csr.ref(), L.ptr(img), self.Ci, 0, self.Ci, L.ptr(bev), self.Cb, 0, self.Cb,
+            L.OUT_CONCAT, L.ptr(self.bv_fused), self.Cb + self.Ci, st), "shpl_pull")
         if self.dual:
             L.check(self._lib.shpl_pull(
-                L.BY_PIXEL, dt, self.n_pix, L.ptr(self.prowptr), L.ptr(self.pent_src),
-                L.ptr(self.pent_val), L.ptr(self.pent_col), L.ptr(bev), self.Cb, 0, self.Cb, L.ptr(img),
-                self.Ci, 0, self.Ci, L.OUT_CONCAT, L.ptr(self.img_fused), self.Ci + self.Cb, st),
-                "shpl_pull")
+                L.BY_PIXEL, dt, self.pcsr.ref(), L.ptr(bev), self.Cb, 0, self.Cb, L.ptr(img), self.Ci, 0,
+                self.Ci, L.OUT_CONCAT, L.ptr(self.img_fused), self.Ci + self.Cb, st), "shpl_pull")
 
     def step(self, points, voxels, point_offsets, P, bev, img, mval=None):
         self.build_index(points, voxels, point_offsets, P, mval)

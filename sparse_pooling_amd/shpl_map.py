@@ -65,20 +65,13 @@ class ShplMap:
         if key in self._csr:
             return self._csr[key]
         n_keys = self.n_cells if direction == L.BY_CELL else self.n_pix
-        dev = self.device
-        rowptr = torch.empty(n_keys + 1, dtype=torch.int32, device=dev)
-        ent_src = _i32(self.nnz_cap, dev)
-        ent_val = torch.empty(max(self.nnz_cap, 1), dtype=torch.float32, device=dev)
-        ent_col = _i32(self.nnz_cap, dev) if direction == L.BY_PIXEL else None
-        ws = L.workspace(L.csr_ws_bytes(n_keys, self.nnz_cap), dev)
-        L.check(L.lib().shpl_build_csr(direction, order, self.nnz_cap, L.ptr(self.nnz_dev),
-                                       L.ptr(self.cell), L.ptr(self.col), L.ptr(self.val),
-                                       L.ptr(self.pix), n_keys, L.ptr(rowptr), L.ptr(ent_src),
-                                       L.ptr(ent_val), L.ptr(ent_col), L.ptr(ws), ws.numel(),
-                                       L.stream_of(dev)), "shpl_build_csr")
-        out = (rowptr, ent_src, ent_val, ent_col, ws)
-        self._csr[key] = out
-        return out
+        c = L.Csr(n_keys, self.nnz_cap, self.device, with_col=direction == L.BY_PIXEL)
+        L.check(L.lib().shpl_build_csr(direction, order, L.ptr(self.nnz_dev), L.ptr(self.cell),
+                                       L.ptr(self.col), L.ptr(self.val), L.ptr(self.pix), c.ref(),
+                                       L.ptr(c.ws), c.ws.numel(), L.stream_of(self.device)),
+                "shpl_build_csr")
+        self._csr[key] = c
+        return c
 
 
 def pack_map(mij, values, m_size, idx, img_shape, validate=True):
@@ -114,12 +107,9 @@ def pack_map(mij, values, m_size, idx, img_shape, validate=True):
 # -------------------------------------------------------------------- pulls
 
 def pull(smap, direction, order, src, src_stride, src_off, c_pool, out, out_stride,
-         pass_=None, pass_stride=0, pass_off=0, c_pass=0, mode=L.OUT_POOL, n_dst=None):
-    rowptr, ent_src, ent_val, ent_col, _ = smap.csr(direction, order)
-    if n_dst is None:
-        n_dst = smap.n_cells if direction == L.BY_CELL else smap.n_pix
-    L.check(L.lib().shpl_pull(direction, L.dtype_code(out), n_dst, L.ptr(rowptr), L.ptr(ent_src),
-                              L.ptr(ent_val), L.ptr(ent_col), L.ptr(src), src_stride, src_off,
+         pass_=None, pass_stride=0, pass_off=0, c_pass=0, mode=L.OUT_POOL):
+    c = smap.csr(direction, order)
+    L.check(L.lib().shpl_pull(direction, L.dtype_code(out), c.ref(), L.ptr(src), src_stride, src_off,
                               c_pool, L.ptr(pass_), pass_stride, pass_off, c_pass, mode,
                               L.ptr(out), out_stride, L.stream_of(out.device)), "shpl_pull")
     return out
