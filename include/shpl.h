@@ -156,28 +156,34 @@ int shpl_pack_map(int64_t nnz, const int64_t *d_mij, const float *d_values, int6
  * CSR keyed by destination (stable, TF accumulation order)
  * ------------------------------------------------------------------------- */
 
-/* Destination-keyed CSR of M (all device arrays, caller-owned). */
+/* M's entries sorted by destination (all device arrays, caller-owned): a CSR
+ * whose row segments are the runs of equal ent_dst. Layout follows the frames
+ * of the map: frame f's entries occupy [frame_off[f], frame_off[f] + nnz_f)
+ * sorted by (destination, TF order); its remaining capacity slots, and every
+ * slot past frame_off[n_frames], hold ent_dst = -1 and are skipped. */
 typedef struct {
-    int32_t *rowptr;   /* [n_keys+1] entry range of each destination; rowptr[n_keys] = live nnz */
-    int32_t *ent_dst;  /* [nnz_cap] destination of each sorted entry                          */
-    int32_t *ent_src;  /* [nnz_cap] source row of each sorted entry                           */
-    float *ent_val;    /* [nnz_cap] M value of each sorted entry                              */
-    int32_t *ent_col;  /* [nnz_cap] column k of each sorted entry (SHPL_BY_PIXEL; else NULL)  */
-    uint32_t *occ;     /* [(n_keys+31)/32] occupancy bitmap: bit d set iff d has entries      */
-    int64_t n_keys;    /* destination rows                                                     */
-    int64_t nnz_cap;   /* capacity of the entry arrays                                         */
+    int32_t *ent_dst;  /* [nnz_cap] destination row of each sorted entry (-1 = empty slot) */
+    int32_t *ent_src;  /* [nnz_cap] source row of each sorted entry                        */
+    float *ent_val;    /* [nnz_cap] M value of each sorted entry                           */
+    int32_t *ent_col;  /* [nnz_cap] column k of each sorted entry (SHPL_BY_PIXEL; else NULL) */
+    int64_t n_keys;    /* destination rows (all frames)                                      */
+    int64_t nnz_cap;   /* capacity of the entry arrays                                       */
 } shpl_csr;
 
-/* Sort the nnz entries by destination (cell for SHPL_BY_CELL, pix[col] for
- * SHPL_BY_PIXEL) keeping `order` among equal destinations, and gather the
- * per-entry source ids so the pulls read one contiguous list:
+/* Sort the entries of every frame by destination (cell for SHPL_BY_CELL,
+ * pix[col] for SHPL_BY_PIXEL) keeping `order` among equal destinations, and
+ * gather the per-entry source ids so the pulls read one contiguous list:
  *   BY_CELL : ent_src = pix[col[e]] (image pixel), ent_col unused
  *   BY_PIXEL: ent_src = cell[e] (BEV row),         ent_col = col[e]
- * d_col NULL means col[e] = e. d_nnz (device, nullable) bounds the live
- * entries (<= csr->nnz_cap). Entries whose row, column or pixel is invalid
- * (-1 from the pack / index builder) are left out. */
+ * Frame f owns entries [d_frame_off[f], d_frame_off[f] + d_frame_nnz[f])
+ * (d_frame_nnz NULL: the whole range) and destinations
+ * [f*keys_per_frame, (f+1)*keys_per_frame); one workgroup sorts one frame
+ * (LDS tile histogram + stable rank inside each tile). d_col NULL means
+ * col[e] = e. Entries whose row, column or pixel is -1 or whose destination
+ * lies outside the frame are left out. */
 int shpl_csr_workspace_bytes(int64_t n_keys, int64_t nnz_cap, size_t *bytes);
-int shpl_build_csr(int direction, int order, const int64_t *d_nnz, const int32_t *d_cell,
+int shpl_build_csr(int direction, int order, int n_frames, const int64_t *d_frame_off,
+                   const int64_t *d_frame_nnz, int64_t keys_per_frame, const int32_t *d_cell,
                    const int32_t *d_col, const float *d_val, const int32_t *d_pix,
                    const shpl_csr *csr, void *d_ws, size_t ws_bytes, void *stream);
 
@@ -196,9 +202,12 @@ int shpl_build_csr(int direction, int order, const int64_t *d_nnz, const int32_t
  *   mode SHPL_OUT_ADD   : out[d, 0:c_pool] = pass[d] + pooled
  * f32 arithmetic without FMA contraction (matches TF-CPU bit for bit);
  * SHPL_BF16 stores bf16 and accumulates in f32.
- * Two passes in one launch: a streaming pass writes every row that has no
- * entries (and the pass-through half of CONCAT), a sparse pass walks the
- * sorted entries and writes the occupied rows' pooled part.
+ * Two stream-ordered launches: k_dense writes every row (pass-through half
+ * copied, pooled part 0 -- or pass + 0 for ADD) reading no index at all,
+ * then k_sparse walks the sorted entries and overwrites the occupied rows'
+ * pooled part. shpl_pull = shpl_pull_dense + shpl_pull_sparse on one stream;
+ * the split entry points let a caller start the dense pass before M is built
+ * (the sparse pass must follow the dense pass of the same output).
  * Replaces: _sparse_pool_op + concat  (sparse_pool_utils.py:96-103, :72)  -> BY_CELL, CONCAT
  *           _sparse_pool_trans_op + concat (sparse_pool_utils.py:105-117, :87) -> BY_PIXEL, CONCAT
  *           their TF autodiff gradients                       -> the other direction */
@@ -206,6 +215,14 @@ int shpl_pull(int direction, int dtype, const shpl_csr *csr, const void *d_src, 
               int64_t src_off, int64_t c_pool, const void *d_pass, int64_t pass_stride,
               int64_t pass_off, int64_t c_pass, int mode, void *d_out, int64_t out_stride,
               void *stream);
+int shpl_pull_dense(int direction, int dtype, const shpl_csr *csr, const void *d_src,
+                    int64_t src_stride, int64_t src_off, int64_t c_pool, const void *d_pass,
+                    int64_t pass_stride, int64_t pass_off, int64_t c_pass, int mode, void *d_out,
+                    int64_t out_stride, void *stream);
+int shpl_pull_sparse(int direction, int dtype, const shpl_csr *csr, const void *d_src,
+                     int64_t src_stride, int64_t src_off, int64_t c_pool, const void *d_pass,
+                     int64_t pass_stride, int64_t pass_off, int64_t c_pass, int mode, void *d_out,
+                     int64_t out_stride, void *stream);
 
 #ifdef __cplusplus
 }

@@ -30,30 +30,25 @@ class ShplLibraryError(RuntimeError):
 
 class ShplCsr(ctypes.Structure):
     """struct shpl_csr of include/shpl.h (device pointers + sizes)."""
-    _fields_ = [("rowptr", ctypes.c_void_p), ("ent_dst", ctypes.c_void_p),
-                ("ent_src", ctypes.c_void_p), ("ent_val", ctypes.c_void_p),
-                ("ent_col", ctypes.c_void_p), ("occ", ctypes.c_void_p),
+    _fields_ = [("ent_dst", ctypes.c_void_p), ("ent_src", ctypes.c_void_p),
+                ("ent_val", ctypes.c_void_p), ("ent_col", ctypes.c_void_p),
                 ("n_keys", ctypes.c_int64), ("nnz_cap", ctypes.c_int64)]
 
 
 class Csr:
-    """Device buffers of one destination-keyed CSR (owned tensors + the ABI struct)."""
+    """Device buffers of one destination-sorted entry list (owned tensors + the ABI struct)."""
 
     def __init__(self, n_keys, nnz_cap, device, with_col):
         i32 = dict(dtype=torch.int32, device=device)
         cap = max(int(nnz_cap), 1)
         self.n_keys, self.nnz_cap = int(n_keys), int(nnz_cap)
-        self.rowptr = torch.empty(self.n_keys + 1, **i32)
         self.ent_dst = torch.empty(cap, **i32)
         self.ent_src = torch.empty(cap, **i32)
         self.ent_val = torch.empty(cap, dtype=torch.float32, device=device)
         self.ent_col = torch.empty(cap, **i32) if with_col else None
-        self.occ = torch.empty((self.n_keys + 31) // 32 + 1, **i32)
         self.ws = workspace(csr_ws_bytes(self.n_keys, self.nnz_cap), device)
-        self.struct = ShplCsr(self.rowptr.data_ptr(), self.ent_dst.data_ptr(), self.ent_src.data_ptr(),
-                              self.ent_val.data_ptr(),
-                              self.ent_col.data_ptr() if with_col else None, self.occ.data_ptr(),
-                              self.n_keys, self.nnz_cap)
+        self.struct = ShplCsr(self.ent_dst.data_ptr(), self.ent_src.data_ptr(), self.ent_val.data_ptr(),
+                              self.ent_col.data_ptr() if with_col else None, self.n_keys, self.nnz_cap)
 
     def ref(self):
         return ctypes.byref(self.struct)
@@ -62,6 +57,7 @@ class Csr:
 def _declare(lib):
     p, i32, i64, d, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double, ctypes.c_size_t
     psz = ctypes.POINTER(ctypes.c_size_t)
+    pull_args = [i32, i32, ctypes.POINTER(ShplCsr), p, i64, i64, i64, p, i64, i64, i64, i32, p, i64, p]
     sig = {
         "shpl_version": (ctypes.c_char_p, []),
         "shpl_status_string": (ctypes.c_char_p, [i32]),
@@ -74,9 +70,11 @@ def _declare(lib):
         "shpl_pack_map": (i32, [i64, p, p, i64, i64, i64, p, i32, i64, i64, i64, i64, i64, i64,
                                 p, p, p, p, p, p]),
         "shpl_csr_workspace_bytes": (i32, [i64, i64, psz]),
-        "shpl_build_csr": (i32, [i32, i32, p, p, p, p, p, ctypes.POINTER(ShplCsr), p, sz, p]),
-        "shpl_pull": (i32, [i32, i32, ctypes.POINTER(ShplCsr), p, i64, i64, i64, p, i64, i64, i64,
-                            i32, p, i64, p]),
+        "shpl_build_csr": (i32, [i32, i32, i32, p, p, i64, p, p, p, p, ctypes.POINTER(ShplCsr), p, sz,
+                                 p]),
+        "shpl_pull": (i32, pull_args),
+        "shpl_pull_dense": (i32, pull_args),
+        "shpl_pull_sparse": (i32, pull_args),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -8,13 +8,11 @@
 // and consumed by gather_nd / sparse_tensor_dense_matmul / sparse_transpose /
 // scatter_nd (avod/avod/utils/sparse_pool_utils.py:96-117).
 //
-// CSR build (all launches stream-ordered, no host sync):
-//   memset counts -> histogram (atomicAdd per entry) -> 3-phase exclusive scan
-//   -> placement (atomicSub slot, arbitrary order inside a destination)
-//   -> rank fix-up: each entry counts the entries of its destination that
-//      precede it in TF order and moves to that rank (deterministic, stable).
-// Destinations hold few entries (one to a few dozen), so the quadratic rank
-// is cheaper than a second sort pass.
+// CSR build: one workgroup per frame, one launch (k_csr_frame): an LDS
+// histogram over destination tiles, a scan, an LDS-atomic placement and a
+// rank fix-up that restores TF's order inside each tile. Nothing is sized by
+// the number of destinations (no per-cell counters in HBM), and tiles hold
+// a few entries each, so the quadratic rank costs less than a sort pass.
 #include "shpl_common.h"
 
 namespace shpl {
@@ -53,23 +51,22 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_pack(int64_t nnz, const int64_t 
 }
 
 // ------------------------------------------------------------------ CSR
+constexpr int CSR_BLOCK = 1024;           // one workgroup per frame
+constexpr int CSR_TILES = 16384;          // LDS tile counters (64 KiB)
+constexpr int CSR_PER_THREAD = CSR_TILES / CSR_BLOCK;
+
 struct CsrIn {
-    int direction, order;
-    int64_t nnz_cap;
-    const int64_t *d_nnz;
+    int direction, order, n_frames;
+    const int64_t *frame_off, *frame_nnz;
+    int64_t keys_per_frame;
+    int log_tile;  // destinations per tile = 1 << log_tile
     const int32_t *cell, *col, *pix;
     const float *val;
 };
 
-__device__ __forceinline__ int64_t live_nnz(const CsrIn &c) {
-    if (!c.d_nnz) return c.nnz_cap;
-    const int64_t n = *c.d_nnz;
-    return n < c.nnz_cap ? n : c.nnz_cap;
-}
-
 __device__ __forceinline__ int32_t col_of(const CsrIn &c, int64_t e) { return c.col ? c.col[e] : (int32_t)e; }
 
-// Destination key of entry e, or -1 if the entry is invalid (already flagged).
+// Destination of entry e, or -1 if the entry is invalid (flagged upstream).
 __device__ __forceinline__ int32_t key_of(const CsrIn &c, int64_t e) {
     const int32_t r = c.cell[e];
     const int32_t k = col_of(c, e);
@@ -77,111 +74,6 @@ __device__ __forceinline__ int32_t key_of(const CsrIn &c, int64_t e) {
     const int32_t p = c.pix[k];
     if (p < 0) return -1;
     return c.direction == SHPL_BY_CELL ? r : p;
-}
-
-__global__ __launch_bounds__(SHPL_BLOCK) void k_hist(CsrIn c, int32_t *cnt) {
-    const int64_t n = live_nnz(c);
-    for (int64_t e = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x; e < n; e += (int64_t)gridDim.x * SHPL_BLOCK) {
-        const int32_t key = key_of(c, e);
-        if (key >= 0) atomicAdd(&cnt[key], 1);
-    }
-}
-
-// ---- exclusive scan of cnt[0..n) into rowptr[0..n], rowptr[n] = total
-constexpr int SCAN_ITEMS = 16;
-constexpr int SCAN_TILE = SHPL_BLOCK * SCAN_ITEMS;
-
-__device__ __forceinline__ void load_items(const int32_t *a, int64_t n, int64_t first, int32_t (&v)[SCAN_ITEMS]) {
-    if (first + SCAN_ITEMS <= n) {
-        const int4 *p = reinterpret_cast<const int4 *>(a + first);
-#pragma unroll
-        for (int q = 0; q < SCAN_ITEMS / 4; ++q) {
-            const int4 t = p[q];
-            v[4 * q] = t.x;
-            v[4 * q + 1] = t.y;
-            v[4 * q + 2] = t.z;
-            v[4 * q + 3] = t.w;
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < SCAN_ITEMS; ++j) v[j] = (first + j < n) ? a[first + j] : 0;
-    }
-}
-
-__global__ __launch_bounds__(SHPL_BLOCK) void k_scan_tiles(const int32_t *cnt, int64_t n, int64_t *tile_sum) {
-    int32_t v[SCAN_ITEMS];
-    load_items(cnt, n, (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS, v);
-    int64_t s = 0;
-#pragma unroll
-    for (int j = 0; j < SCAN_ITEMS; ++j) s += v[j];
-    __shared__ int64_t lds[SHPL_BLOCK / 64 + 1];
-    int64_t tot;
-    block_excl_scan(s, lds, &tot);
-    if (threadIdx.x == 0) tile_sum[blockIdx.x] = tot;
-}
-
-__global__ __launch_bounds__(SHPL_BLOCK) void k_scan_tile_sums(int64_t *tile_sum, int64_t n_tiles, int32_t *rowptr,
-                                                               int64_t n) {
-    __shared__ int64_t lds[SHPL_BLOCK / 64 + 1];
-    int64_t carry = 0;
-    for (int64_t base = 0; base < n_tiles; base += SHPL_BLOCK) {
-        const int64_t j = base + threadIdx.x;
-        const int64_t v = j < n_tiles ? tile_sum[j] : 0;
-        int64_t tot;
-        const int64_t ex = block_excl_scan(v, lds, &tot);
-        if (j < n_tiles) tile_sum[j] = carry + ex;
-        carry += tot;
-    }
-    if (threadIdx.x == 0) rowptr[n] = (int32_t)carry;
-}
-
-// Also writes the occupancy bitmap: thread pairs own one 32-bit word.
-__global__ __launch_bounds__(SHPL_BLOCK) void k_scan_apply(const int32_t *cnt, int64_t n, const int64_t *tile_off,
-                                                           int32_t *rowptr, uint32_t *occ) {
-    static_assert(SCAN_ITEMS == 16, "two threads per bitmap word");
-    int32_t v[SCAN_ITEMS];
-    const int64_t first = (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
-    load_items(cnt, n, first, v);
-    int64_t s = 0;
-    uint32_t bits = 0;
-#pragma unroll
-    for (int j = 0; j < SCAN_ITEMS; ++j) {
-        s += v[j];
-        bits |= (v[j] > 0 ? 1u : 0u) << j;
-    }
-    const uint32_t hi = __shfl_down(bits, 1, 64);
-    if ((threadIdx.x & 1) == 0 && first < n) occ[first >> 5] = bits | (hi << 16);
-    __shared__ int64_t lds[SHPL_BLOCK / 64 + 1];
-    int64_t tot;
-    int64_t run = block_excl_scan(s, lds, &tot) + tile_off[blockIdx.x];
-    if (first + SCAN_ITEMS <= n) {
-        int32_t o[SCAN_ITEMS];
-#pragma unroll
-        for (int j = 0; j < SCAN_ITEMS; ++j) {
-            o[j] = (int32_t)run;
-            run += v[j];
-        }
-        int4 *p = reinterpret_cast<int4 *>(rowptr + first);
-#pragma unroll
-        for (int q = 0; q < SCAN_ITEMS / 4; ++q) p[q] = make_int4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-    } else {
-        for (int j = 0; j < SCAN_ITEMS; ++j) {
-            if (first + j < n) rowptr[first + j] = (int32_t)run;
-            run += v[j];
-        }
-    }
-}
-
-// Placement: slots of a destination are handed out downwards from its end;
-// cnt returns to zero.
-__global__ __launch_bounds__(SHPL_BLOCK) void k_place(CsrIn c, const int32_t *rowptr, int32_t *cnt, int32_t *tmp) {
-    const int64_t n = live_nnz(c);
-    for (int64_t e = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x; e < n; e += (int64_t)gridDim.x * SHPL_BLOCK) {
-        const int32_t key = key_of(c, e);
-        if (key < 0) continue;
-        const int32_t slot = rowptr[key] + atomicSub(&cnt[key], 1) - 1;
-        tmp[slot] = (int32_t)e;
-    }
 }
 
 // Sort key of entry e inside its destination, TF-CPU order (see shpl_order).
@@ -196,52 +88,103 @@ __device__ __forceinline__ uint64_t order_key(const CsrIn &c, int32_t e) {
     }
 }
 
-__global__ __launch_bounds__(SHPL_BLOCK) void k_fix(CsrIn c, const int32_t *rowptr, int64_t n_keys, const int32_t *tmp,
-                                                    int32_t *ent_dst, int32_t *ent_src, float *ent_val,
-                                                    int32_t *ent_col) {
-    const int64_t n = rowptr[n_keys];
-    for (int64_t s = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x; s < n; s += (int64_t)gridDim.x * SHPL_BLOCK) {
-        const int32_t e = tmp[s];
+// One frame per workgroup:
+//  1. LDS histogram of the frame's entries over destination tiles
+//  2. exclusive scan of the tile counts (in place)
+//  3. placement into tile segments (LDS atomics: arbitrary order inside a tile)
+//  4. rank fix-up: each entry counts the tile entries that precede it in
+//     (destination, TF order, entry) and moves to that rank -> stable, sorted.
+__global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, int32_t *tmp, int64_t nnz_cap, int32_t *ent_dst,
+                                                         int32_t *ent_src, float *ent_val, int32_t *ent_col) {
+    __shared__ int32_t cnt[CSR_TILES];
+    __shared__ int32_t wsum[CSR_BLOCK / 64];
+    const int f = blockIdx.x;
+    const int64_t e0 = c.frame_off[f];
+    const int64_t cap_end = c.frame_off[f + 1];
+    int64_t e1 = cap_end;
+    if (c.frame_nnz) {
+        const int64_t n = c.frame_nnz[f];
+        e1 = e0 + n < cap_end ? e0 + n : cap_end;
+    }
+    const int64_t kbase = (int64_t)f * c.keys_per_frame;
+    const int n_tiles = (int)(((c.keys_per_frame - 1) >> c.log_tile) + 1);
+    for (int t = threadIdx.x; t < CSR_TILES; t += CSR_BLOCK) cnt[t] = 0;
+    __syncthreads();
+    // 1. histogram
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += CSR_BLOCK) {
+        const int64_t k = (int64_t)key_of(c, e) - kbase;
+        if (k >= 0 && k < c.keys_per_frame) atomicAdd(&cnt[k >> c.log_tile], 1);
+    }
+    __syncthreads();
+    // 2. exclusive scan: thread j owns tiles [j*16, j*16+16)
+    {
+        int32_t v[CSR_PER_THREAD];
+        int32_t sum = 0;
+#pragma unroll
+        for (int q = 0; q < CSR_PER_THREAD; ++q) {
+            v[q] = cnt[threadIdx.x * CSR_PER_THREAD + q];
+            sum += v[q];
+        }
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        int32_t x = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[wid] = x;
+        __syncthreads();
+        int32_t run = x - sum;
+        for (int w = 0; w < wid; ++w) run += wsum[w];
+#pragma unroll
+        for (int q = 0; q < CSR_PER_THREAD; ++q) {
+            cnt[threadIdx.x * CSR_PER_THREAD + q] = run;
+            run += v[q];
+        }
+    }
+    __syncthreads();
+    // 3. placement: cnt[t] advances from start(t) to end(t) = start(t+1)
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += CSR_BLOCK) {
+        const int64_t k = (int64_t)key_of(c, e) - kbase;
+        if (k >= 0 && k < c.keys_per_frame) tmp[e0 + atomicAdd(&cnt[k >> c.log_tile], 1)] = (int32_t)e;
+    }
+    __syncthreads();
+    // tmp was written by other waves of this workgroup through the vector memory path
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __syncthreads();
+    const int32_t n_valid = cnt[n_tiles - 1];
+    // 4. rank fix-up
+    for (int32_t s = threadIdx.x; s < n_valid; s += CSR_BLOCK) {
+        const int32_t e = tmp[e0 + s];
         const int32_t key = key_of(c, e);
-        const int32_t a = rowptr[key], b = rowptr[key + 1];
+        const int t = (int)((key - kbase) >> c.log_tile);
+        const int32_t a = t ? cnt[t - 1] : 0, b = cnt[t];
         int32_t rank = 0;
         if (b - a > 1) {
             const uint64_t ke = order_key(c, e);
-            for (int32_t t = a; t < b; ++t) {
-                const int32_t o = tmp[t];
-                const uint64_t ko = order_key(c, o);
-                rank += (ko < ke || (ko == ke && o < e)) ? 1 : 0;
+            for (int32_t u = a; u < b; ++u) {
+                const int32_t o = tmp[e0 + u];
+                if (o == e) continue;
+                const int32_t ko = key_of(c, o);
+                bool before = ko < key;
+                if (ko == key) {
+                    const uint64_t oo = order_key(c, o);
+                    before = oo < ke || (oo == ke && o < e);
+                }
+                rank += before ? 1 : 0;
             }
         }
-        const int32_t d = a + rank;
+        const int64_t d = e0 + a + rank;
         const int32_t k = col_of(c, e);
         ent_dst[d] = key;
         ent_src[d] = c.direction == SHPL_BY_CELL ? c.pix[k] : c.cell[e];
         ent_val[d] = c.val[e];
         if (ent_col) ent_col[d] = k;
     }
-}
-
-struct CsrWs {
-    int32_t *cnt;
-    int64_t *tile;
-    int32_t *tmp;
-    size_t bytes;
-};
-
-CsrWs carve_csr(int64_t n_keys, int64_t nnz_cap, void *base) {
-    CsrWs w;
-    char *b = (char *)base;
-    size_t o = 0;
-    w.cnt = (int32_t *)(b + o);
-    o = align_up(o + sizeof(int32_t) * (size_t)(n_keys + 1), 256);
-    const int64_t n_tiles = (n_keys + SCAN_TILE - 1) / SCAN_TILE + 1;
-    w.tile = (int64_t *)(b + o);
-    o = align_up(o + sizeof(int64_t) * (size_t)n_tiles, 256);
-    w.tmp = (int32_t *)(b + o);
-    o = align_up(o + sizeof(int32_t) * (size_t)(nnz_cap > 0 ? nnz_cap : 1), 256);
-    w.bytes = o;
-    return w;
+    // empty slots of this frame's capacity, and past the last frame
+    int64_t hole_end = cap_end;
+    if (f == c.n_frames - 1) hole_end = nnz_cap;
+    for (int64_t d = e0 + n_valid + threadIdx.x; d < hole_end; d += CSR_BLOCK) ent_dst[d] = -1;
 }
 
 }  // namespace
@@ -280,51 +223,32 @@ extern "C" int shpl_pack_map(int64_t nnz, const int64_t *d_mij, const float *d_v
 
 extern "C" int shpl_csr_workspace_bytes(int64_t n_keys, int64_t nnz_cap, size_t *bytes) {
     if (!bytes || n_keys < 0 || nnz_cap < 0) return SHPL_ERR_ARG;
-    *bytes = carve_csr(n_keys, nnz_cap, nullptr).bytes;
+    *bytes = align_up(sizeof(int32_t) * (size_t)(nnz_cap > 0 ? nnz_cap : 1), 256);
     return SHPL_OK;
 }
 
-extern "C" int shpl_build_csr(int direction, int order, const int64_t *d_nnz, const int32_t *d_cell,
+extern "C" int shpl_build_csr(int direction, int order, int n_frames, const int64_t *d_frame_off,
+                              const int64_t *d_frame_nnz, int64_t keys_per_frame, const int32_t *d_cell,
                               const int32_t *d_col, const float *d_val, const int32_t *d_pix, const shpl_csr *csr,
                               void *d_ws, size_t ws_bytes, void *stream) {
-    if (!csr) return SHPL_ERR_ARG;
+    if (!csr || !d_frame_off || n_frames < 1) return SHPL_ERR_ARG;
     if (direction != SHPL_BY_CELL && direction != SHPL_BY_PIXEL) return SHPL_ERR_ARG;
     if (order < SHPL_ORDER_ENTRY || order > SHPL_ORDER_COL_ENTRY) return SHPL_ERR_ARG;
-    const int64_t n_keys = csr->n_keys, nnz_cap = csr->nnz_cap;
-    if (n_keys < 0 || nnz_cap < 0 || n_keys >= 2147483647LL || nnz_cap >= 2147483647LL) return SHPL_ERR_BAD_SHAPE;
-    if (!csr->rowptr || !csr->occ || !d_ws) return SHPL_ERR_ARG;
-    if (nnz_cap > 0 && (!d_cell || !d_val || !d_pix || !csr->ent_dst || !csr->ent_src || !csr->ent_val))
-        return SHPL_ERR_ARG;
-    if (direction == SHPL_BY_PIXEL && nnz_cap > 0 && !csr->ent_col) return SHPL_ERR_ARG;
-    if (((uintptr_t)csr->rowptr & 15u) != 0) return SHPL_ERR_BAD_SHAPE;  // int4 stores in the scan
-    CsrWs w = carve_csr(n_keys, nnz_cap, d_ws);
-    if (w.bytes > ws_bytes) return SHPL_ERR_WORKSPACE;
-    hipStream_t s = (hipStream_t)stream;
-    CsrIn c{direction, order, nnz_cap, d_nnz, d_cell, d_col, d_pix, d_val};
-    SHPL_HIP_CHECK(hipMemsetAsync(w.cnt, 0, sizeof(int32_t) * (size_t)(n_keys + 1), s));
-    const int ge = grid_for(nnz_cap > 0 ? nnz_cap : 1, SHPL_BLOCK, 8192);
-    if (nnz_cap > 0) {
-        hipLaunchKernelGGL(k_hist, dim3(ge), dim3(SHPL_BLOCK), 0, s, c, w.cnt);
-        SHPL_LAUNCH_CHECK();
-    }
-    const int64_t n_tiles = (n_keys + SCAN_TILE - 1) / SCAN_TILE;
-    if (n_tiles > 0) {
-        hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)n_tiles), dim3(SHPL_BLOCK), 0, s, w.cnt, n_keys, w.tile);
-        SHPL_LAUNCH_CHECK();
-    }
-    hipLaunchKernelGGL(k_scan_tile_sums, dim3(1), dim3(SHPL_BLOCK), 0, s, w.tile, n_tiles, csr->rowptr, n_keys);
+    const int64_t nnz_cap = csr->nnz_cap;
+    if (keys_per_frame < 1 || nnz_cap < 0 || csr->n_keys < (int64_t)n_frames * keys_per_frame ||
+        csr->n_keys >= 2147483647LL || nnz_cap >= 2147483647LL)
+        return SHPL_ERR_BAD_SHAPE;
+    if (nnz_cap == 0) return SHPL_OK;
+    if (!d_cell || !d_val || !d_pix || !csr->ent_dst || !csr->ent_src || !csr->ent_val || !d_ws) return SHPL_ERR_ARG;
+    if (direction == SHPL_BY_PIXEL && !csr->ent_col) return SHPL_ERR_ARG;
+    size_t need;
+    shpl_csr_workspace_bytes(csr->n_keys, nnz_cap, &need);
+    if (need > ws_bytes) return SHPL_ERR_WORKSPACE;
+    int log_tile = 0;
+    while (((keys_per_frame - 1) >> log_tile) + 1 > CSR_TILES) ++log_tile;
+    CsrIn c{direction, order, n_frames, d_frame_off, d_frame_nnz, keys_per_frame, log_tile, d_cell, d_col, d_pix, d_val};
+    hipLaunchKernelGGL(k_csr_frame, dim3(n_frames), dim3(CSR_BLOCK), 0, (hipStream_t)stream, c, (int32_t *)d_ws,
+                       nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_val, csr->ent_col);
     SHPL_LAUNCH_CHECK();
-    if (n_tiles > 0) {
-        hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)n_tiles), dim3(SHPL_BLOCK), 0, s, w.cnt, n_keys, w.tile,
-                           csr->rowptr, csr->occ);
-        SHPL_LAUNCH_CHECK();
-    }
-    if (nnz_cap > 0) {
-        hipLaunchKernelGGL(k_place, dim3(ge), dim3(SHPL_BLOCK), 0, s, c, csr->rowptr, w.cnt, w.tmp);
-        SHPL_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_fix, dim3(ge), dim3(SHPL_BLOCK), 0, s, c, csr->rowptr, n_keys, w.tmp, csr->ent_dst,
-                           csr->ent_src, csr->ent_val, csr->ent_col);
-        SHPL_LAUNCH_CHECK();
-    }
     return SHPL_OK;
 }

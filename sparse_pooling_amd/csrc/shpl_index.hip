@@ -5,14 +5,13 @@
 //   gen_sparse_pooling_input_avod           avod/avod/utils/sparse_pool_utils.py:6-20
 //   produce_sparse_pooling_input            avod/avod/utils/sparse_pool_utils.py:22-58
 //
-// Here every point is one thread. A frame's points are split into 256-point
-// blocks; three launches give a stable (point-order) compaction over all
-// frames of a batch at once:
-//   1. count  : evaluate each point, one kept-count per block
-//   2. scan   : one workgroup scans the block counts (frame-major) and derives
-//               the per-frame entry offsets and counts
-//   3. write  : re-evaluate, rank kept points inside the block with a wave
-//               ballot, emit at block offset + rank
+// One workgroup per frame (1024 threads) does the whole frame in one launch:
+// it walks the frame's points in 1024-point chunks, evaluates each point
+// (one thread per point), ranks the kept points with a wave ballot + LDS
+// prefix, and writes them in point order (a stable compaction). A frame's
+// entries start at its first input point ("capacity layout"); the tail up to
+// the next frame is filled with -1 sentinels that every consumer skips, so no
+// cross-frame scan or second launch is needed.
 // Projection runs in f64 with the exact operation order numpy uses (an FMA
 // chain over k for np.dot, IEEE division, rint = round-half-even), so the
 // integer outputs are bit-identical to the reference (tests/golden/index_*).
@@ -21,11 +20,7 @@
 namespace shpl {
 namespace {
 
-struct Frames {
-    const int64_t *pt_off;  // [n_frames+1] (device)
-    int n_frames;
-    int bpf;                // blocks per frame
-};
+constexpr int IDX_BLOCK = 1024;  // one workgroup per frame
 
 template <typename PT>
 __device__ __forceinline__ void load_point(const void *pts, int64_t i, double &x, double &y, double &z) {
@@ -160,6 +155,11 @@ struct FusedStage {
             flip[3 * pos + 2] = ui;
         }
     }
+    __device__ void hole(int64_t pos) const {  // capacity slot past the frame's last entry
+        cell[pos] = -1;
+        pix[pos] = -1;
+        val[pos] = 0.0f;
+    }
 };
 
 template <typename PT, typename VT>
@@ -191,6 +191,7 @@ struct GenStage {  // gen_sparse_pooling_input_avod
         img_index[ld + pos] = (double)(int64_t)rint(pl.v);
         img_index[2 * ld + pos] = 0.0;
     }
+    __device__ void hole(int64_t) const {}
 };
 
 template <typename VT>
@@ -234,125 +235,58 @@ struct ProduceStage {  // produce_sparse_pooling_input (in-place img_index updat
         if (cell) cell[pos] = rok ? (int32_t)r : -1;
         if (pix) pix[pos] = pok ? (int32_t)(vi * (int64_t)g.wq + ui) : -1;
     }
+    __device__ void hole(int64_t pos) const {
+        if (cell) cell[pos] = -1;
+        if (pix) pix[pos] = -1;
+    }
 };
 
-// ----------------------------------------------------------- 3-pass compaction
+// ------------------------------------------------- per-frame stable compaction
 
 template <typename Stage>
-__global__ __launch_bounds__(SHPL_BLOCK) void k_count(Stage st, Frames fr, int32_t *blk_cnt) {
-    const int f = blockIdx.y;
-    const int64_t beg = fr.pt_off[f], end = fr.pt_off[f + 1];
-    const int64_t i = beg + (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x;
-    bool keep = false;
-    if (i < end) {
-        typename Stage::Payload pl;
-        keep = st.eval(f, i, pl);
-    }
-    const uint64_t m = __ballot(keep);
-    __shared__ int32_t wsum[SHPL_BLOCK / 64];
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = (int32_t)__popcll(m);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int32_t s = 0;
-        for (int w = 0; w < SHPL_BLOCK / 64; ++w) s += wsum[w];
-        blk_cnt[(int64_t)f * fr.bpf + blockIdx.x] = s;
-    }
-}
-
-// One workgroup: exclusive scan of all block counts (frame-major), then the
-// per-frame offsets / counts.
-__global__ __launch_bounds__(SHPL_BLOCK) void k_scan_blocks(const int32_t *blk_cnt, int64_t *blk_off,
-                                                            Frames fr, int64_t *frame_nnz,
-                                                            int64_t *frame_out_off) {
-    __shared__ int64_t lds[SHPL_BLOCK / 64 + 1];
-    const int64_t n = (int64_t)fr.n_frames * fr.bpf;
-    int64_t carry = 0;
-    for (int64_t base = 0; base < n; base += SHPL_BLOCK) {
-        const int64_t j = base + threadIdx.x;
-        const int64_t v = j < n ? blk_cnt[j] : 0;
-        int64_t tot;
-        const int64_t ex = block_excl_scan(v, lds, &tot);
-        if (j < n) blk_off[j] = carry + ex;
-        carry += tot;
-    }
-    __syncthreads();
-    for (int f = threadIdx.x; f < fr.n_frames; f += SHPL_BLOCK) {
-        const int64_t s = blk_off[(int64_t)f * fr.bpf];
-        const int64_t e = (f + 1 < fr.n_frames) ? blk_off[(int64_t)(f + 1) * fr.bpf] : carry;
-        if (frame_out_off) frame_out_off[f] = s;
-        if (frame_nnz) frame_nnz[f] = e - s;
-    }
-    if (threadIdx.x == 0 && frame_out_off) frame_out_off[fr.n_frames] = carry;
-}
-
-template <typename Stage>
-__global__ __launch_bounds__(SHPL_BLOCK) void k_write(Stage st, Frames fr, const int64_t *blk_off) {
-    const int f = blockIdx.y;
-    const int64_t beg = fr.pt_off[f], end = fr.pt_off[f + 1];
-    const int64_t i = beg + (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x;
-    bool keep = false;
-    typename Stage::Payload pl;
-    if (i < end) {
-        keep = st.eval(f, i, pl);
-        st.touch(f, i, pl, keep);
-    }
-    const uint64_t m = __ballot(keep);
-    __shared__ int32_t wsum[SHPL_BLOCK / 64];
+__global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, const int64_t *pt_off, int64_t *frame_nnz,
+                                                       int64_t *frame_out_off, int n_frames) {
+    __shared__ int32_t wsum[IDX_BLOCK / 64];
+    const int f = blockIdx.x;
+    const int64_t p0 = pt_off[f], p1 = pt_off[f + 1];
     const int wid = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) wsum[wid] = (int32_t)__popcll(m);
-    __syncthreads();
-    int32_t before = 0;
-    for (int w = 0; w < wid; ++w) before += wsum[w];
-    if (keep) {
-        const int64_t pos = blk_off[(int64_t)f * fr.bpf + blockIdx.x] + before + lane_rank(m);
-        st.emit(f, i, pos, blk_off[(int64_t)f * fr.bpf], pl);
+    int64_t kept = 0;
+    for (int64_t base = p0; base < p1; base += IDX_BLOCK) {
+        const int64_t i = base + threadIdx.x;
+        bool keep = false;
+        typename Stage::Payload pl;
+        if (i < p1) {
+            keep = st.eval(f, i, pl);
+            st.touch(f, i, pl, keep);
+        }
+        const uint64_t m = __ballot(keep);
+        if ((threadIdx.x & 63) == 0) wsum[wid] = (int32_t)__popcll(m);
+        __syncthreads();
+        int32_t before = 0, tot = 0;
+        for (int w = 0; w < IDX_BLOCK / 64; ++w) {
+            const int32_t c = wsum[w];
+            before += w < wid ? c : 0;
+            tot += c;
+        }
+        if (keep) st.emit(f, i, p0 + kept + before + lane_rank(m), p0, pl);
+        kept += tot;
+        __syncthreads();  // wsum is rewritten by the next chunk
+    }
+    for (int64_t pos = p0 + kept + threadIdx.x; pos < p1; pos += IDX_BLOCK) st.hole(pos);
+    if (threadIdx.x == 0) {
+        if (frame_nnz) frame_nnz[f] = kept;
+        if (frame_out_off) {
+            frame_out_off[f] = p0;
+            if (f == n_frames - 1) frame_out_off[n_frames] = p1;
+        }
     }
 }
 
-struct IndexWs {
-    int32_t *blk_cnt;
-    int64_t *blk_off;
-    int64_t *frame_nnz;
-    int64_t *frame_off;
-    size_t bytes;
-};
-
-IndexWs carve(int n_frames, int64_t max_points, void *base) {
-    const int64_t bpf = (max_points + SHPL_BLOCK - 1) / SHPL_BLOCK > 0 ? (max_points + SHPL_BLOCK - 1) / SHPL_BLOCK : 1;
-    const int64_t nb = (int64_t)n_frames * bpf;
-    IndexWs w;
-    size_t o = 0;
-    char *b = (char *)base;
-    w.blk_cnt = (int32_t *)(b + o);
-    o = align_up(o + sizeof(int32_t) * nb, 256);
-    w.blk_off = (int64_t *)(b + o);
-    o = align_up(o + sizeof(int64_t) * nb, 256);
-    w.frame_nnz = (int64_t *)(b + o);
-    o = align_up(o + sizeof(int64_t) * (n_frames + 1), 256);
-    w.frame_off = (int64_t *)(b + o);
-    o = align_up(o + sizeof(int64_t) * (n_frames + 2), 256);
-    w.bytes = o;
-    return w;
-}
-
 template <typename Stage>
-int run_compaction(const Stage &st, int n_frames, const int64_t *pt_off, int64_t max_points,
-                   int64_t *frame_nnz, int64_t *frame_out_off, void *ws, size_t ws_bytes,
-                   hipStream_t stream) {
-    IndexWs w = carve(n_frames, max_points, ws);
-    if (w.bytes > ws_bytes) return SHPL_ERR_WORKSPACE;
-    Frames fr;
-    fr.pt_off = pt_off;
-    fr.n_frames = n_frames;
-    fr.bpf = (int)((max_points + SHPL_BLOCK - 1) / SHPL_BLOCK);
-    if (fr.bpf < 1) fr.bpf = 1;
-    const dim3 grid(fr.bpf, n_frames);
-    hipLaunchKernelGGL(k_count<Stage>, grid, dim3(SHPL_BLOCK), 0, stream, st, fr, w.blk_cnt);
-    SHPL_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(SHPL_BLOCK), 0, stream, w.blk_cnt, w.blk_off, fr,
-                       frame_nnz ? frame_nnz : w.frame_nnz, frame_out_off ? frame_out_off : w.frame_off);
-    SHPL_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_write<Stage>, grid, dim3(SHPL_BLOCK), 0, stream, st, fr, w.blk_off);
+int run_compaction(const Stage &st, int n_frames, const int64_t *pt_off, int64_t *frame_nnz,
+                   int64_t *frame_out_off, hipStream_t stream) {
+    hipLaunchKernelGGL(k_compact<Stage>, dim3(n_frames), dim3(IDX_BLOCK), 0, stream, st, pt_off, frame_nnz,
+                       frame_out_off, n_frames);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
 }
@@ -369,8 +303,7 @@ using namespace shpl;
 
 extern "C" int shpl_build_index_workspace_bytes(int n_frames, int64_t max_points_per_frame, size_t *bytes) {
     if (!bytes || n_frames < 1 || max_points_per_frame < 0) return SHPL_ERR_ARG;
-    // + room for a single-frame [0, n] offset pair
-    *bytes = carve(n_frames, max_points_per_frame, nullptr).bytes + 256;
+    *bytes = 256;  // the single-frame calls keep a device [0, n] offset pair here
     return SHPL_OK;
 }
 
@@ -394,8 +327,7 @@ extern "C" int shpl_build_index(int n_frames, const int64_t *d_point_offsets, in
     {                                                                                            \
         FusedStage<PT, VT> st{d_points, d_voxels, vox_stride, d_P, g, d_mval, d_cell, d_pix,     \
                               d_val, d_mij, d_flip, d_err};                                      \
-        return run_compaction(st, n_frames, d_point_offsets, max_points_per_frame, d_frame_nnz,  \
-                              d_frame_out_off, d_ws, ws_bytes, s);                               \
+        return run_compaction(st, n_frames, d_point_offsets, d_frame_nnz, d_frame_out_off, s);   \
     }
     if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I64) SHPL_FUSED(double, int64_t)
     if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I32) SHPL_FUSED(double, int32_t)
@@ -407,10 +339,9 @@ extern "C" int shpl_build_index(int n_frames, const int64_t *d_point_offsets, in
 
 // Writes the device [0, n] offsets of a single frame into the workspace tail.
 static int single_frame_offsets(int64_t n, void *ws, size_t ws_bytes, hipStream_t s, int64_t **off) {
-    const size_t need = carve(1, n, nullptr).bytes;
-    if (need + 256 > ws_bytes) return SHPL_ERR_WORKSPACE;
-    // A single frame needs device-side [0, n] offsets; they live in the workspace tail.
-    int64_t *o = (int64_t *)((char *)ws + need);
+    if (ws_bytes < 2 * sizeof(int64_t)) return SHPL_ERR_WORKSPACE;
+    // A single frame needs device-side [0, n] offsets; they live in the workspace.
+    int64_t *o = (int64_t *)ws;
     hipLaunchKernelGGL(k_set_pair, dim3(1), dim3(1), 0, s, o, (int64_t)0, n);
     SHPL_LAUNCH_CHECK();
     *off = o;
@@ -432,7 +363,7 @@ extern "C" int shpl_gen_index(int64_t n, const void *d_points, int points_dtype,
     {                                                                                             \
         GenStage<PT, VT> st{d_points, d_voxels, vox_stride, d_P, im_w, im_h, d_bv_index,          \
                             d_img_index, ld};                                                     \
-        return run_compaction(st, 1, off, n, d_nv, nullptr, d_ws, ws_bytes, s);                   \
+        return run_compaction(st, 1, off, d_nv, nullptr, s);                                     \
     }
     if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I64) SHPL_GEN(double, int64_t)
     if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I32) SHPL_GEN(double, int32_t)
@@ -457,11 +388,11 @@ extern "C" int shpl_produce_index(int64_t nv, const void *d_bv_index, int bv_ity
     if (rc) return rc;
     if (bv_itype == SHPL_I64) {
         ProduceStage<int64_t> st{d_bv_index, bv_stride, d_img_index, ld, g, d_mij, d_flip, d_cell, d_pix, d_err};
-        return run_compaction(st, 1, off, nv, d_nk, nullptr, d_ws, ws_bytes, s);
+        return run_compaction(st, 1, off, d_nk, nullptr, s);
     }
     if (bv_itype == SHPL_I32) {
         ProduceStage<int32_t> st{d_bv_index, bv_stride, d_img_index, ld, g, d_mij, d_flip, d_cell, d_pix, d_err};
-        return run_compaction(st, 1, off, nv, d_nk, nullptr, d_ws, ws_bytes, s);
+        return run_compaction(st, 1, off, d_nk, nullptr, s);
     }
     return SHPL_ERR_ARG;
 }

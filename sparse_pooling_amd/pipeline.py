@@ -68,37 +68,72 @@ class FusedPipeline:
 
     def build_csr(self):
         st = L.stream_of(self.dev)
-        nnz = self.frame_off[self.B:]
+        args = (self.B, L.ptr(self.frame_off), L.ptr(self.frame_nnz))
         L.check(self._lib.shpl_build_csr(
-            L.BY_CELL, L.ORDER_ENTRY, L.ptr(nnz), L.ptr(self.cell), None, L.ptr(self.val), L.ptr(self.pix),
-            self.csr.ref(), L.ptr(self.csr.ws), self.csr.ws.numel(), st), "shpl_build_csr")
+            L.BY_CELL, L.ORDER_ENTRY, *args, self.Hb * self.Wb, L.ptr(self.cell), None, L.ptr(self.val),
+            L.ptr(self.pix), self.csr.ref(), L.ptr(self.csr.ws), self.csr.ws.numel(), st), "shpl_build_csr")
         if self.dual:
             L.check(self._lib.shpl_build_csr(
-                L.BY_PIXEL, L.ORDER_COL_ROW, L.ptr(nnz), L.ptr(self.cell), None, L.ptr(self.val),
+                L.BY_PIXEL, L.ORDER_COL_ROW, *args, self.Hi * self.Wi, L.ptr(self.cell), None, L.ptr(self.val),
                 L.ptr(self.pix), self.pcsr.ref(), L.ptr(self.pcsr.ws), self.pcsr.ws.numel(), st),
                 "shpl_build_csr")
 
+    def _pull(self, fn, csr, direction, src, cs, pass_, cp, out, st):
+        L.check(fn(direction, L.dtype_code(out), csr.ref(), L.ptr(src), cs, 0, cs, L.ptr(pass_), cp, 0, cp,
+                   L.OUT_CONCAT, L.ptr(out), cs + cp, st), "shpl_pull")
+
+    def layer_dense(self, bev, img):
+        """Streaming half of the layer (needs no M): pass-through copy + zeros."""
+        st = L.stream_of(self.dev)
+        self._pull(self._lib.shpl_pull_dense, self.csr, L.BY_CELL, img, self.Ci, bev, self.Cb, self.bv_fused, st)
+        if self.dual:
+            self._pull(self._lib.shpl_pull_dense, self.pcsr, L.BY_PIXEL, bev, self.Cb, img, self.Ci,
+                       self.img_fused, st)
+
+    def layer_sparse(self, bev, img):
+        """Pooled rows, after layer_dense and build_csr."""
+        st = L.stream_of(self.dev)
+        self._pull(self._lib.shpl_pull_sparse, self.csr, L.BY_CELL, img, self.Ci, bev, self.Cb, self.bv_fused, st)
+        if self.dual:
+            self._pull(self._lib.shpl_pull_sparse, self.pcsr, L.BY_PIXEL, bev, self.Cb, img, self.Ci,
+                       self.img_fused, st)
+
     def layer(self, bev, img):
         """bv_fused = [bev || pool(img)] (+ img_fused = [img || trans(bev)] if dual)."""
-        st = L.stream_of(self.dev)
-        dt = L.dtype_code(self.bv_fused)
-        L.check(self._lib.shpl_pull(
-            L.BY_CELL, dt, self.csr.ref(), L.ptr(img), self.Ci, 0, self.Ci, L.ptr(bev), self.Cb, 0, self.Cb,
-            L.OUT_CONCAT, L.ptr(self.bv_fused), self.Cb + self.Ci, st), "shpl_pull")
-        if self.dual:
-            L.check(self._lib.shpl_pull(
-                L.BY_PIXEL, dt, self.pcsr.ref(), L.ptr(bev), self.Cb, 0, self.Cb, L.ptr(img), self.Ci, 0,
-                self.Ci, L.OUT_CONCAT, L.ptr(self.img_fused), self.Ci + self.Cb, st), "shpl_pull")
+        self.layer_dense(bev, img)
+        self.layer_sparse(bev, img)
 
     def step(self, points, voxels, point_offsets, P, bev, img, mval=None):
         self.build_index(points, voxels, point_offsets, P, mval)
         self.build_csr()
         self.layer(bev, img)
 
+    def step_overlapped(self, points, voxels, point_offsets, P, bev, img, side, mval=None, events=None):
+        """Same result as step(): the streaming half runs on `side` while the
+        current stream builds M and its CSR; the sparse half then waits for it.
+        `events` (4 timing events) bracket the dense and the sparse launches."""
+        main = torch.cuda.current_stream(self.dev)
+        side.wait_stream(main)            # inputs / previous step done
+        with torch.cuda.stream(side):
+            if events:
+                events[0].record(side)
+            self.layer_dense(bev, img)
+            if events:
+                events[1].record(side)
+        self.build_index(points, voxels, point_offsets, P, mval)
+        self.build_csr()
+        main.wait_stream(side)            # sparse overwrites rows the dense pass wrote
+        if events:
+            events[2].record(main)
+        self.layer_sparse(bev, img)
+        if events:
+            events[3].record(main)
+
     def map(self):
         """The current M as a ShplMap (for tests)."""
         return ShplMap(self.cell, None, self.val, self.pix, self.N, self.n_cells, self.n_pix, self.N,
-                       self.dev, nnz_dev=self.frame_off[self.B:], err=self.err)
+                       self.dev, frame_off=self.frame_off, frame_nnz=self.frame_nnz, n_frames=self.B,
+                       err=self.err)
 
 
 def stack_frames(frames, device):

@@ -27,15 +27,23 @@ def _i32(n, device):
 
 
 class ShplMap:
+    """M on the device. Entries are grouped by frame: frame f owns entry slots
+    [frame_off[f], frame_off[f+1]) of which the first frame_nnz[f] are live
+    (frame_nnz None: all), BEV rows [f*n_cells/F, (f+1)*n_cells/F) and image
+    pixels [f*n_pix/F, (f+1)*n_pix/F)."""
+
     def __init__(self, cell, col, val, pix, nnz_cap, n_cells, n_pix, n_cols, device,
-                 nnz_dev=None, err=None):
+                 frame_off=None, frame_nnz=None, n_frames=1, err=None):
         self.cell, self.col, self.val, self.pix = cell, col, val, pix
         self.nnz_cap = int(nnz_cap)
         self.n_cells = int(n_cells)
         self.n_pix = int(n_pix)
         self.n_cols = int(n_cols)
         self.device = device
-        self.nnz_dev = nnz_dev
+        self.n_frames = int(n_frames)
+        if frame_off is None:
+            frame_off = torch.tensor([0, self.nnz_cap], dtype=torch.int64, device=device)
+        self.frame_off, self.frame_nnz = frame_off, frame_nnz
         self.err = err if err is not None else torch.zeros(1, dtype=torch.int32, device=device)
         self._csr = {}
 
@@ -66,10 +74,11 @@ class ShplMap:
             return self._csr[key]
         n_keys = self.n_cells if direction == L.BY_CELL else self.n_pix
         c = L.Csr(n_keys, self.nnz_cap, self.device, with_col=direction == L.BY_PIXEL)
-        L.check(L.lib().shpl_build_csr(direction, order, L.ptr(self.nnz_dev), L.ptr(self.cell),
-                                       L.ptr(self.col), L.ptr(self.val), L.ptr(self.pix), c.ref(),
-                                       L.ptr(c.ws), c.ws.numel(), L.stream_of(self.device)),
-                "shpl_build_csr")
+        L.check(L.lib().shpl_build_csr(direction, order, self.n_frames, L.ptr(self.frame_off),
+                                       L.ptr(self.frame_nnz), n_keys // self.n_frames,
+                                       L.ptr(self.cell), L.ptr(self.col), L.ptr(self.val),
+                                       L.ptr(self.pix), c.ref(), L.ptr(c.ws), c.ws.numel(),
+                                       L.stream_of(self.device)), "shpl_build_csr")
         self._csr[key] = c
         return c
 
@@ -307,5 +316,5 @@ def build_index_batch(points, voxels, point_offsets, P, im_size, bv_size, stride
                                      L.ptr(frame_nnz), L.ptr(frame_off), L.ptr(err), L.ptr(ws),
                                      ws.numel(), L.stream_of(dev)), "shpl_build_index")
     smap = ShplMap(cell, None, val, pix, N, n_frames * bhq * bwq, n_frames * hq * wq, N, dev,
-                   nnz_dev=frame_off[n_frames:], err=err)
+                   frame_off=frame_off, frame_nnz=frame_nnz, n_frames=n_frames, err=err)
     return IndexBatch(smap, mij, flip, frame_nnz, frame_off, n_frames, (bhq, bwq), (hq, wq))

@@ -93,10 +93,11 @@ def test_batched_index_builder_matches_oracle_per_frame(cfg):
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
     ib = sm.build_index_batch(pts, vox, off, P, spec.im_size, spec.bv_size, spec.stride, maxp,
                               ref_outputs=True)
-    fo = _np(ib.frame_off)
+    fo, fn = _np(ib.frame_off), _np(ib.frame_nnz)
     for f, fr in enumerate(frames):
         ref = _oracle_frame(fr, spec.stride)
-        a, b = fo[f], fo[f + 1]
+        a, b = fo[f], fo[f] + fn[f]
+        assert (_np(ib.map.cell[b:fo[f + 1]]) == -1).all()  # capacity tail of the frame
         np.testing.assert_array_equal(_np(ib.mij[a:b]), ref["Mij_pool"])
         np.testing.assert_array_equal(_np(ib.flip[a:b]), ref["img_index_flip_pool"])
         R = int(ref["M_size"][0])
