@@ -94,7 +94,7 @@ __device__ __forceinline__ uint64_t order_key(const CsrIn &c, int32_t e) {
 //  3. placement into tile segments (LDS atomics: arbitrary order inside a tile)
 //  4. rank fix-up: each entry counts the tile entries that precede it in
 //     (destination, TF order, entry) and moves to that rank -> stable, sorted.
-__global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, int32_t *tmp, int64_t nnz_cap, int32_t *ent_dst,
+__global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, uint64_t *tmp, int64_t nnz_cap, int32_t *ent_dst,
                                                          int32_t *ent_src, float *ent_val, int32_t *ent_col) {
     __shared__ int32_t cnt[CSR_TILES];
     __shared__ int32_t wsum[CSR_BLOCK / 64];
@@ -143,35 +143,44 @@ __global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, int32_t *tmp, 
         }
     }
     __syncthreads();
-    // 3. placement: cnt[t] advances from start(t) to end(t) = start(t+1)
+    // 3. placement of (destination << 32 | entry): cnt[t] advances from start(t) to end(t) = start(t+1)
     for (int64_t e = e0 + threadIdx.x; e < e1; e += CSR_BLOCK) {
-        const int64_t k = (int64_t)key_of(c, e) - kbase;
-        if (k >= 0 && k < c.keys_per_frame) tmp[e0 + atomicAdd(&cnt[k >> c.log_tile], 1)] = (int32_t)e;
+        const int32_t key = key_of(c, e);
+        const int64_t k = (int64_t)key - kbase;
+        if (k >= 0 && k < c.keys_per_frame)
+            tmp[e0 + atomicAdd(&cnt[k >> c.log_tile], 1)] = ((uint64_t)(uint32_t)key << 32) | (uint32_t)e;
     }
     __syncthreads();
     // tmp was written by other waves of this workgroup through the vector memory path
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     __syncthreads();
     const int32_t n_valid = cnt[n_tiles - 1];
+    // With identity columns every TF order collapses to entry order, so the
+    // packed (destination, entry) word alone sorts the tile.
+    const bool entry_order = c.order == SHPL_ORDER_ENTRY || !c.col;
     // 4. rank fix-up
     for (int32_t s = threadIdx.x; s < n_valid; s += CSR_BLOCK) {
-        const int32_t e = tmp[e0 + s];
-        const int32_t key = key_of(c, e);
+        const uint64_t me = tmp[e0 + s];
+        const int32_t key = (int32_t)(me >> 32);
+        const int32_t e = (int32_t)(uint32_t)me;
         const int t = (int)((key - kbase) >> c.log_tile);
         const int32_t a = t ? cnt[t - 1] : 0, b = cnt[t];
         int32_t rank = 0;
         if (b - a > 1) {
-            const uint64_t ke = order_key(c, e);
-            for (int32_t u = a; u < b; ++u) {
-                const int32_t o = tmp[e0 + u];
-                if (o == e) continue;
-                const int32_t ko = key_of(c, o);
-                bool before = ko < key;
-                if (ko == key) {
-                    const uint64_t oo = order_key(c, o);
-                    before = oo < ke || (oo == ke && o < e);
+            if (entry_order) {
+                for (int32_t u = a; u < b; ++u) rank += tmp[e0 + u] < me ? 1 : 0;
+            } else {
+                const uint64_t ke = order_key(c, e);
+                for (int32_t u = a; u < b; ++u) {
+                    const uint64_t ot = tmp[e0 + u];
+                    const int32_t ko = (int32_t)(ot >> 32), o = (int32_t)(uint32_t)ot;
+                    bool before = ko < key;
+                    if (ko == key && o != e) {
+                        const uint64_t oo = order_key(c, o);
+                        before = oo < ke || (oo == ke && o < e);
+                    }
+                    rank += before ? 1 : 0;
                 }
-                rank += before ? 1 : 0;
             }
         }
         const int64_t d = e0 + a + rank;
@@ -223,7 +232,7 @@ extern "C" int shpl_pack_map(int64_t nnz, const int64_t *d_mij, const float *d_v
 
 extern "C" int shpl_csr_workspace_bytes(int64_t n_keys, int64_t nnz_cap, size_t *bytes) {
     if (!bytes || n_keys < 0 || nnz_cap < 0) return SHPL_ERR_ARG;
-    *bytes = align_up(sizeof(int32_t) * (size_t)(nnz_cap > 0 ? nnz_cap : 1), 256);
+    *bytes = align_up(sizeof(uint64_t) * (size_t)(nnz_cap > 0 ? nnz_cap : 1), 256);
     return SHPL_OK;
 }
 
@@ -247,7 +256,7 @@ extern "C" int shpl_build_csr(int direction, int order, int n_frames, const int6
     int log_tile = 0;
     while (((keys_per_frame - 1) >> log_tile) + 1 > CSR_TILES) ++log_tile;
     CsrIn c{direction, order, n_frames, d_frame_off, d_frame_nnz, keys_per_frame, log_tile, d_cell, d_col, d_pix, d_val};
-    hipLaunchKernelGGL(k_csr_frame, dim3(n_frames), dim3(CSR_BLOCK), 0, (hipStream_t)stream, c, (int32_t *)d_ws,
+    hipLaunchKernelGGL(k_csr_frame, dim3(n_frames), dim3(CSR_BLOCK), 0, (hipStream_t)stream, c, (uint64_t *)d_ws,
                        nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_val, csr->ent_col);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_workspace_queries_are_host_only():
     from sparse_pooling_amd import _lib as L
-    assert L.csr_ws_bytes(563200 * 64, 20000 * 64) > 4 * 563200 * 64
+    assert L.csr_ws_bytes(563200 * 64, 20000 * 64) >= 4 * 20000 * 64
     assert L.index_ws_bytes(64, 20000) > 0
 
 
