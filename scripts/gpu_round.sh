@@ -22,5 +22,14 @@ for s in $STEPS; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
         python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
       rc=$?; echo "prof rc=$rc"; tail -2 gpurun_out/prof.log; ok $rc || exit $rc ;;
+    pmc)
+      # HBM traffic of the SHPL kernels: FETCH_SIZE and WRITE_SIZE in separate passes
+      # (they do not fit one TCC pass), kernel filter on the shpl kernels only.
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -k 10 600 rocprofv3 --pmc $c --kernel-include-regex 'k_dense|k_sparse|k_csr_frame|k_compact' \
+          -d gpurun_out/pmc_$c -o run --output-format csv -- \
+          python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/pmc_$c.log 2>&1
+        rc=$?; echo "pmc $c rc=$rc"; tail -1 gpurun_out/pmc_$c.log | cut -c1-200; ok $rc || exit $rc
+      done ;;
   esac
 done
