@@ -1,26 +1,33 @@
 """SHPL bench: fused frames/s + achieved HBM GB/s of the SHPL gather/scatter.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--config 2]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--config 2|3|5]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
-Workload (BASELINE.json configs[1], "config 2"): synthetic KITTI-shaped
-frames of 20k camera-frame points, BEV 704x800x32, image 360x1200x32, fp32,
-img->BEV fused SHPL forward. One step processes F frames per GPU (default 64,
-the config-4 batch) through the whole hot path, inputs resident in HBM:
-device index build (projection, clip, strides, flatten, compaction) ->
-BEV-keyed CSR of M -> fused pooled gather + concat write of bv_fused.
+Default workload (BASELINE.json configs[1], "config 2"): synthetic
+KITTI-shaped frames of 20k camera-frame points, BEV 704x800x32, image
+360x1200x32, fp32, img->BEV fused SHPL forward. One step processes F frames
+per GPU (default 64, the config-4 batch) through the whole hot path with the
+inputs resident in HBM: device index build (projection, clip, strides,
+flatten, compaction) -> destination-sorted M -> fused pooled gather + concat
+write of bv_fused. The streaming half of the layer needs no index and runs
+on a side stream beside the index build (--no-overlap: strictly sequential).
+Other configs: 3 = bf16 dual SHPL forward + backward at the fusion_vgg
+conv4 level (88x100x256 / 45x150x256, 4 frames); 5 = fp32 dual forward,
+40k points, 64 channels.
 
 Frames are independent: each rank draws its own frames and runs
 them with no data-path collective ("scaling": "weak"); the only collectives
-are the barriers around the timed loop and a MAX all-reduce of the elapsed
-time. `value` = all frames of all ranks / max elapsed.
+are the barriers around the timed loop, a MAX all-reduce of the elapsed time
+and an all-gather of per-rank checksums. `value` = frames of all ranks / max
+elapsed.
 
-roofline: the dominant kernel is the fused layer pull; its algorithmic bytes
-per launch (SURVEY §8d `layer_fwd` per frame x F) over its mean duration,
-timed with events on the launch stream. cpu_baseline: the C restatement of
-the reference path (oracle/, index build + TF-order pooling + concat), one
-core, on a bounded sample of the same frames (rank 0, N=1 only).
+roofline: the SHPL layer kernels (k_dense + k_sparse of every pull in the
+step); algorithmic bytes per step (SURVEY §8d per frame x F) over their
+summed mean durations, timed with events on their launch streams.
+cpu_baseline: the C restatement of the reference path (oracle/: index build +
+TF-order pooling + concat), one core, on a bounded sample of the same
+frames (rank 0, N=1 only).
 """
 import argparse
 import json
@@ -35,6 +42,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+DEFAULT_FRAMES = {2: 64, 3: 4, 5: 64}
 
 
 def parse():
@@ -42,25 +50,42 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=64, help="frames per GPU per step")
-    ap.add_argument("--config", type=int, default=2, choices=[2, 5])
+    ap.add_argument("--frames", type=int, default=None, help="frames per GPU per step")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true",
-                    help="run the layer's streaming pass after the index/CSR build instead of beside it")
+                    help="run the layer's streaming pass after the index build instead of beside it")
     return ap.parse_args()
 
 
-def layer_bytes(spec, nnz, u_src, frames, esz=4):
-    """SURVEY §8d layer_fwd: read bev + write bv_fused + gather unique source
-    rows + 12 B per entry (int32 dst, int32 src, f32 val)."""
+def pull_bytes(rows, c_pass, c_pool, u_src, nnz, esz, write_width):
+    """read the pass-through rows, write the output rows, gather
+    the unique source rows, 12 B per entry (int32 dst, int32 src, f32 val)."""
+    return rows * c_pass * esz + rows * write_width * esz + u_src * c_pool * esz + 12 * nnz
+
+
+def layer_bytes(spec, nnz, u_pix, frames, esz=4):
+    """img->BEV layer_fwd of config 2 (kept for scripts/pull_sweep.py)."""
     Hb, Wb = spec.bev_feat_hw
-    cells = frames * Hb * Wb
-    return (cells * spec.c_bev * esz + cells * (spec.c_bev + spec.c_img) * esz
-            + u_src * spec.c_img * esz + 12 * nnz)
+    return pull_bytes(frames * Hb * Wb, spec.c_bev, spec.c_img, u_pix, nnz, esz, spec.c_bev + spec.c_img)
 
 
-def cpu_baseline(spec, frames_np, budget_s):
+def step_bytes(cfg, spec, nnz, u_pix, u_cell, F, esz):
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    cb, ci = spec.c_bev, spec.c_img
+    nb, ni = F * Hb * Wb, F * Hi * Wi
+    b = pull_bytes(nb, cb, ci, u_pix, nnz, esz, cb + ci)                  # bv_fused = [bev || pool(img)]
+    if cfg in (3, 5):
+        b += pull_bytes(ni, ci, cb, u_cell, nnz, esz, ci + cb)            # img_fused = [img || trans(bev)]
+    if cfg == 3:
+        b += pull_bytes(nb, cb, cb, u_pix, nnz, esz, cb)                  # d_bev = g[:, :Cb] + M^T g_img
+        b += pull_bytes(ni, ci, ci, u_cell, nnz, esz, ci)                 # d_img = g[:, :Ci] + M g_bv
+    return b
+
+
+def cpu_baseline(spec, frames_np, budget_s, dual):
     """Oracle (C port of the reference path) on one core, bounded sample."""
     from oracle import shpl_oracle as orc
     Hb, Wb = spec.bev_feat_hw
@@ -79,17 +104,18 @@ def cpu_baseline(spec, frames_np, budget_s):
         ref = orc.produce_sparse_pooling_input(g, stride=spec.stride)
         b = time.perf_counter()
         orc.sparse_pool_layer(bev, img, ref["Mij_pool"], ref["M_val"], ref["M_size"],
-                              ref["img_index_flip_pool"])
+                              ref["img_index_flip_pool"], dual=dual)
         c = time.perf_counter()
         t_index += b - a
         t_pool += c - b
         done += 1
     total = t_index + t_pool
     return {"value": round(done / total, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": (f"{done} config-{spec.n_points}pt frames through oracle/shpl_oracle.c "
-                       f"(index build {1e3 * t_index / done:.2f} ms/frame + TF-order pooling and "
-                       f"concat {1e3 * t_pool / done:.2f} ms/frame), single thread, "
-                       f"{os.cpu_count()} host cpus visible")}
+            "sample": (f"{done} frames of this workload ({spec.n_points} pts) through oracle/shpl_oracle.c: "
+                       f"index build {1e3 * t_index / done:.2f} ms/frame + TF-order pooling and concat "
+                       f"{1e3 * t_pool / done:.2f} ms/frame"
+                       + (" (both directions, forward only)" if dual else "")
+                       + f", single thread, {os.cpu_count()} host cpus visible")}
 
 
 def main():
@@ -105,23 +131,31 @@ def main():
 
     from sparse_pooling_amd import dist as sd, pipeline, synth
 
-    spec = synth.CONFIGS[args.config]
-    dual = args.config == 5
-    F = args.frames
+    cfg = args.config
+    spec = synth.CONFIGS[cfg]
+    dual = cfg in (3, 5)
+    backward = cfg == 3
+    dtype = torch.bfloat16 if cfg == 3 else torch.float32
+    esz = 2 if dtype == torch.bfloat16 else 4
+    F = args.frames or DEFAULT_FRAMES[cfg]
     frames = [synth.make_frame(spec, seed=s, n_outside=200) for s in sd.frame_seeds(rank, F)]
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, dev)
     pl = pipeline.FusedPipeline(F, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev,
-                                spec.c_img, dual=dual, device=dev)
+                                spec.c_img, dtype=dtype, dual=dual, device=dev)
     Hb, Wb = spec.bev_feat_hw
     Hi, Wi = spec.img_feat_hw
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
-    bev = torch.randn((F, Hb, Wb, spec.c_bev), device=dev, generator=g)
-    img = torch.randn((F, Hi, Wi, spec.c_img), device=dev, generator=g)
-
+    bev = torch.randn((F, Hb, Wb, spec.c_bev), device=dev, generator=g).to(dtype)
+    img = torch.randn((F, Hi, Wi, spec.c_img), device=dev, generator=g).to(dtype)
+    if backward:
+        g_bv = torch.randn(tuple(pl.bv_fused.shape), device=dev, generator=g).to(dtype)
+        g_img = torch.randn(tuple(pl.img_fused.shape), device=dev, generator=g).to(dtype)
+        d_bev, d_img = torch.empty_like(bev), torch.empty_like(img)
     side = torch.cuda.Stream(device=dev)
 
     def step(ev=None):
+        # ev: [dense start, dense end, sparse start, sparse end, bwd start, bwd end]
         if args.no_overlap:
             pl.build_index(pts, vox, off, P)
             pl.build_csr()
@@ -135,31 +169,36 @@ def main():
             if ev is not None:
                 ev[3].record()
         else:
-            pl.step_overlapped(pts, vox, off, P, bev, img, side, events=ev)
+            pl.step_overlapped(pts, vox, off, P, bev, img, side, events=ev[:4] if ev else None)
+        if backward:
+            if ev is not None:
+                ev[4].record()
+            pl.backward(g_bv, g_img, d_bev, d_img)
+            if ev is not None:
+                ev[5].record()
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     nnz = int(pl.frame_nnz.sum().item())
-    u_src = int(torch.unique(pl.pix[pl.pix >= 0]).numel())
+    u_pix = int(torch.unique(pl.pix[pl.pix >= 0]).numel())
+    u_cell = int(torch.unique(pl.cell[pl.cell >= 0]).numel())
     err = int(pl.err.item())
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(args.steps)]
     elapsed = sd.timed(lambda k: step(evs[k]), args.steps, device=dev)
     checksums = sd.gather_checksums(pl.bv_fused[..., spec.c_bev:].double().sum().item(), device=dev)
     dense_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     sparse_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
-    layer_ms = dense_ms + sparse_ms
+    bwd_ms = sum(e[4].elapsed_time(e[5]) for e in evs) / args.steps if backward else 0.0
+    layer_ms = dense_ms + sparse_ms + bwd_ms
 
-    bytes_per_launch = layer_bytes(spec, nnz, u_src, F)
-    if dual:  # + the BEV->img direction: read img, write img_fused, gather BEV rows
-        bytes_per_launch += (F * Hi * Wi * spec.c_img * 4 + F * Hi * Wi * (spec.c_img + spec.c_bev) * 4
-                             + nnz * spec.c_bev * 4 + 12 * nnz)
-    achieved = bytes_per_launch / (layer_ms * 1e-3) / 1e9
+    nbytes = step_bytes(cfg, spec, nnz, u_pix, u_cell, F, esz)
+    achieved = nbytes / (layer_ms * 1e-3) / 1e9
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(spec, frames[: min(F, 64)], args.cpu_seconds)
+        cpu = cpu_baseline(spec, frames[: min(F, 64)], args.cpu_seconds, dual)
 
     if rank == 0:
         total_frames = F * world * args.steps
@@ -168,9 +207,11 @@ def main():
         if os.path.exists(tpath):
             with open(tpath) as fh:
                 tj = json.load(fh)
-            key = f"config{args.config}_F{F}"
+            key = f"config{cfg}_F{F}"
             if key in tj:
                 traffic = tj[key]["hbm_bytes_per_launch"]
+        what = {2: "img->BEV SHPL fwd", 3: "dual SHPL fwd + bwd (bf16 storage, f32 accumulate)",
+                5: "dual SHPL fwd (img->BEV and BEV->img)"}[cfg]
         out = {
             "metric": "SHPL fused frames/sec + achieved HBM GB/s (% of MI355X peak), 1/2/4/8 GPU",
             "value": round(total_frames / elapsed, 2),
@@ -182,30 +223,33 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "bf16" if esz == 2 else "f32",
             "data": "synthetic (seeded KITTI-shaped frames; no dataset on the box)",
             "config": {
-                "workload": (f"config{args.config}: {spec.n_points} pts/frame, BEV {Hb}x{Wb}x{spec.c_bev}, "
-                             f"img {Hi}x{Wi}x{spec.c_img}, fp32, "
-                             + ("bidirectional SHPL" if dual else "img->BEV SHPL fwd")
-                             + "; step = device index build + CSR + fused layer"),
+                "workload": (f"config{cfg}: {spec.n_points} pts/frame, BEV {Hb}x{Wb}x{spec.c_bev}, "
+                             f"img {Hi}x{Wi}x{spec.c_img}, {what}; step = device index build + sorted M "
+                             "+ fused layer" + (" + gradient" if backward else "")),
                 "frames_per_gpu_per_step": F,
                 "nnz_per_step_rank0": nnz,
-                "unique_src_pixels_rank0": u_src,
+                "unique_src_pixels_rank0": u_pix,
+                "unique_cells_rank0": u_cell,
+                "overlap_index_build": not args.no_overlap,
                 "parallelism": f"frame-sharded x{world}",
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "SHPL layer = k_dense (concat stream) + k_sparse (pooled gather); achieved over their summed durations",
+                "kernel": "SHPL layer pulls: k_dense (concat stream) + k_sparse (pooled gather); "
+                          "achieved over their summed durations",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "algorithmic_bytes_per_launch": nbytes,
                 "kernel_ms": round(layer_ms, 4),
                 "k_dense_ms": round(dense_ms, 4),
                 "k_sparse_ms": round(sparse_ms, 4),
+                "backward_ms": round(bwd_ms, 4),
             },
             "cpu_baseline": cpu,
             "index_errors": err,

@@ -86,7 +86,9 @@ const char *shpl_status_string(int status);
  * avod/avod/utils/transform.py:3-40) as called per frame by
  * KittiDataset.load_samples (avod/avod/datasets/kitti/kitti_dataset.py:374-379).
  *
- *   d_point_offsets [n_frames+1] i64 : frame f owns points [off[f], off[f+1])
+ *   d_point_offsets [n_frames+1] i64 : frame f owns point slots [off[f], off[f+1])
+ *   d_point_counts  optional [n_frames] i64: only the first count[f] slots are live
+ *                   (the capacity layout shpl_bev_slices emits)
  *   d_points        [N,3] f64 or f32 (camera frame)
  *   d_voxels        [N, vox_stride] i32/i64, columns 0,1 = (x, z) BEV voxel index
  *   d_P             [n_frames, 3, 4] f64 camera matrices (stereo_calib.p2)
@@ -94,21 +96,23 @@ const char *shpl_status_string(int status);
  *   bv_h, bv_w      full-resolution BEV size ((H,W))
  *   s_img, s_bv     strides (stride[0], stride[1] of the reference)
  *   d_mval          optional [N] f32 weight per INPUT point (MV3D 1/count); NULL = 1.0
- * Outputs (capacity N entries, in frame-major, point order; global ids):
+ * Outputs (capacity layout: frame f's entries at [off[f], off[f] + nnz_f) in
+ * point order, -1 sentinels up to off[f+1]; global ids):
  *   d_cell [N] i32  = f*Hb'*Wb' + r           (M row)
  *   d_pix  [N] i32  = f*Hi'*Wi' + v'*Wi' + u' (image pixel of column k)
  *   d_val  [N] f32
  *   d_mij  optional [N,2] i64 = reference Mij_pool rows [r, k_local]
  *   d_flip optional [N,3] i64 = reference img_index_flip_pool rows [0, v', u']
  *   d_frame_nnz     [n_frames] i64 (reference M_size[1] per frame)
- *   d_frame_out_off [n_frames+1] i64 (first entry of each frame; last = total nnz)
+ *   d_frame_out_off [n_frames+1] i64 (= d_point_offsets: entry slots of each frame)
  * The column of entry e is e itself (M's columns are arange per frame).
  * A kept entry whose flattened row is negative (the reference keeps it and TF
  * then rejects it) or whose pixel is negative gets cell/pix = -1 and sets
  * SHPL_EBIT_ROW / SHPL_EBIT_PIXEL in *d_err (nullable).
  */
 int shpl_build_index_workspace_bytes(int n_frames, int64_t max_points_per_frame, size_t *bytes);
-int shpl_build_index(int n_frames, const int64_t *d_point_offsets, int64_t max_points_per_frame,
+int shpl_build_index(int n_frames, const int64_t *d_point_offsets, const int64_t *d_point_counts,
+                     int64_t max_points_per_frame,
                      const void *d_points, int points_dtype, const void *d_voxels, int voxels_itype,
                      int64_t vox_stride, const double *d_P, double im_w, double im_h, double bv_h,
                      double bv_w, double s_img, double s_bv, const float *d_mval,
@@ -133,6 +137,37 @@ int shpl_produce_index(int64_t nv, const void *d_bv_index, int bv_itype, int64_t
                        double bv_w, double s_img, double s_bv, int64_t *d_mij, int64_t *d_flip,
                        int32_t *d_cell, int32_t *d_pix, int64_t *d_nk, uint32_t *d_err,
                        void *d_ws, size_t ws_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * BEV slice voxelizer: the index builder's input
+ * ------------------------------------------------------------------------- */
+
+/* BevSlices.generate_bev(output_indices=True) (avod/avod/core/bev_generators/
+ * bev_slices.py:33-156) with VoxelGrid2D.voxelize_2d (avod/wavedata/wavedata/
+ * tools/core/voxel_grid_2d.py:43-162), for n_frames frames in one launch.
+ *   d_points       [N,3] f64 camera-frame points; frame f owns [off[f], off[f+1])
+ *   d_planes       [n_frames,4] f64 ground planes (a, b, c, d)
+ *   area_extents   host [3][2] f64 ([[xmin,xmax],[ymin,ymax],[zmin,zmax]])
+ *   slice_lo/hi    host [num_slices] plane offsets of each height slice, computed
+ *                  as the reference does (height_lo + s*hpd, + hpd)
+ *   density_lo/hi  offsets of the density map's slice (height_lo, height_hi)
+ *   density_table  host [16]: min(1, log(n+1)/norm_value), n >= 15 saturates
+ * Outputs (capacity N, frame f at [off[f], off[f] + d_frame_nvox[f]), -1 after):
+ *   d_voxel_indices [N,2] i32 = reference voxel_indices_rot rows (x, nz - z)
+ *   d_pts_in_voxel  [N,3] f64 = the first point of each cell (unique_pts)
+ *   d_height_maps   optional [n_frames, num_slices, nz, nx] f64 (rotated like the reference)
+ *   d_density_map   optional [n_frames, nz, nx] f64
+ * Slices are emitted in order and cells in (x, z) order, matching
+ * np.vstack(voxel_indices_stack). Workspace: shpl_bev_workspace_bytes. */
+int shpl_bev_workspace_bytes(int64_t total_points, int num_slices, size_t *bytes);
+int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, int64_t total_points,
+                    const void *d_points, int points_dtype, const double *d_planes,
+                    const double *area_extents, double voxel_size, int num_slices,
+                    const double *slice_lo, const double *slice_hi, double density_lo,
+                    double density_hi, double height_per_division, const double *density_table,
+                    int32_t *d_voxel_indices, double *d_pts_in_voxel, int64_t *d_frame_nvox,
+                    double *d_height_maps, double *d_density_map, uint32_t *d_err, void *d_ws,
+                    size_t ws_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Correspondence matrix M: validation + device map (SURVEY a8-a10 inputs)

@@ -297,3 +297,89 @@ int shplo_pool_trans_grad_bev(const float *dZ, int64_t B, int64_t H, int64_t W, 
     free(ord);
     return SHPLO_OK;
 }
+
+/* ---- a5/a6: BevSlices.generate_bev(output_indices=True) ------------------
+ * avod/avod/core/bev_generators/bev_slices.py:58-154 and
+ * avod/wavedata/wavedata/tools/core/voxel_grid_2d.py:64-152, restated per
+ * slice: slice filter (kitti_utils.py:79-107 -> obj_utils.py:444-491),
+ * floor(p / vs), stable lexsort by (x, z, y), first point of every (x, z)
+ * cell, cells in (x, z) order. The plane test np.dot(plane', [p;1]) goes
+ * through OpenBLAS dgemv whose accumulation order is not reproduced here
+ * (an FMA chain is used): results can differ only for points within one ulp
+ * of a slice plane. Slices with <= 1 point are voxelized too (the reference
+ * reuses the previous slice's grid there, bev_slices.py:79-93, a bug). */
+typedef struct { int32_t x, y, z; int64_t i; } shplo_vox;
+
+static int cmp_vox(const void *pa, const void *pb)
+{
+    const shplo_vox *a = (const shplo_vox *)pa, *b = (const shplo_vox *)pb;
+    if (a->x != b->x) return a->x < b->x ? -1 : 1;
+    if (a->z != b->z) return a->z < b->z ? -1 : 1;
+    if (a->y != b->y) return a->y < b->y ? -1 : 1;
+    return a->i < b->i ? -1 : (a->i > b->i);
+}
+
+static int plane_below(const double *pl, double off, double x, double y, double z)
+{
+    double s = pl[0] * x;
+    s = fma(pl[1], y, s);
+    s = fma(pl[2], z, s);
+    s = fma(pl[3] - off, 1.0, s);
+    return s < 0.0;
+}
+
+/* pts n x 3; ext [3][2]; outputs: vox (cap x 2: x, nz - z), upts (cap x 3),
+ * hmaps [num_slices][nz][nx] (zero-filled here), dmap [nz][nx]; returns the
+ * number of voxel rows (all slices) or -1 if cap is too small. */
+int64_t shplo_bev_slices(int64_t n, const double *pts, const double *plane, const double *ext, double vs,
+                         int num_slices, const double *lo, const double *hi, double dlo, double dhi,
+                         double hpd, const double *dens_table, int64_t cap, int64_t *vox, double *upts,
+                         double *hmaps, double *dmap)
+{
+    const int min_x = (int)floor(ext[0] / vs), min_z = (int)floor(ext[4] / vs);
+    const int nx = (int)(ceil(ext[1] / vs - 1) - min_x + 1), nz = (int)(ceil(ext[5] / vs - 1) - min_z + 1);
+    const double norm = sqrt(plane[0] * plane[0] + plane[1] * plane[1] + plane[2] * plane[2]);
+    memset(hmaps, 0, sizeof(double) * (size_t)num_slices * nx * nz);
+    memset(dmap, 0, sizeof(double) * (size_t)nx * nz);
+    shplo_vox *buf = (shplo_vox *)malloc(sizeof(shplo_vox) * (size_t)(n > 0 ? n : 1));
+    int64_t out = 0;
+    for (int s = 0; s <= num_slices; ++s) {
+        const double l = s < num_slices ? lo[s] : dlo, h = s < num_slices ? hi[s] : dhi;
+        int64_t m = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            const double x = pts[3 * i], y = pts[3 * i + 1], z = pts[3 * i + 2];
+            if (!(x > ext[0] && x < ext[1] && y > ext[2] && y < ext[3] && z > ext[4] && z < ext[5])) continue;
+            if (plane_below(plane, h, x, y, z) == plane_below(plane, l, x, y, z)) continue;
+            buf[m].x = (int32_t)floor(x / vs);
+            buf[m].y = (int32_t)floor(y / vs);
+            buf[m].z = (int32_t)floor(z / vs);
+            buf[m].i = i;
+            ++m;
+        }
+        qsort(buf, (size_t)m, sizeof(shplo_vox), cmp_vox);
+        for (int64_t j = 0; j < m;) {
+            int64_t k = j + 1;
+            while (k < m && buf[k].x == buf[j].x && buf[k].z == buf[j].z) ++k;
+            const int xi = buf[j].x - min_x, zi = buf[j].z - min_z;
+            const int64_t pix = (int64_t)(nz - 1 - zi) * nx + xi;
+            const double *p = pts + 3 * buf[j].i;
+            if (s < num_slices) {
+                if (out >= cap) { free(buf); return -1; }
+                vox[2 * out] = xi;
+                vox[2 * out + 1] = nz - zi;
+                upts[3 * out] = p[0];
+                upts[3 * out + 1] = p[1];
+                upts[3 * out + 2] = p[2];
+                ++out;
+                const double dist = (plane[0] * p[0] + plane[1] * p[1] + plane[2] * p[2] + plane[3]) / norm;
+                hmaps[(int64_t)s * nx * nz + pix] = (dist - l) / hpd;
+            } else {
+                const int64_t c = k - j;
+                dmap[pix] = c < 16 ? dens_table[c] : 1.0;
+            }
+            j = k;
+        }
+    }
+    free(buf);
+    return out;
+}

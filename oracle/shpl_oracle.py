@@ -47,6 +47,9 @@ def lib():
         _lib.shplo_pool_trans_grad_bev.restype = ctypes.c_int
         _lib.shplo_pool_trans_grad_bev.argtypes = [p, i64, i64, i64, i64, p, i64, p, p, i64, i64,
                                                     i64, p]
+        _lib.shplo_bev_slices.restype = i64
+        _lib.shplo_bev_slices.argtypes = [i64, p, p, p, d, ctypes.c_int, p, p, d, d, d, p, i64, p, p,
+                                          p, p]
     return _lib
 
 
@@ -94,6 +97,42 @@ def produce_sparse_pooling_input(input_dict, M_val=None, stride=(1, 1)):
         M_val = np.ones(nk)
     return {"Mij_pool": mij[:nk].copy(), "M_val": M_val, "M_size": msize,
             "img_index_flip_pool": flip[:nk].copy(), "bev_index_flip_pool": np.zeros((0, 3))}
+
+
+# ---- BEV slices (a5/a6) ------------------------------------------------------
+
+def slice_bounds(height_lo, height_hi, num_slices):
+    """BevSlices' per-slice plane offsets, computed exactly as bev_slices.py:30-31, :66-67."""
+    hpd = (height_hi - height_lo) / num_slices
+    lo = [height_lo + s * hpd for s in range(num_slices)]
+    return hpd, np.array(lo), np.array([v + hpd for v in lo])
+
+
+def density_table(norm_value=np.log(16)):
+    """min(1, log(n + 1) / norm) for n = 0..15 (bev_generator.py:33-34)."""
+    return np.minimum(1.0, np.log(np.arange(16) + 1) / norm_value)
+
+
+def bev_slices(point_cloud, ground_plane, area_extents, voxel_size, height_lo, height_hi, num_slices):
+    """Restates BevSlices.generate_bev(output_indices=True): returns
+    (height_maps [S,nz,nx], density_map [nz,nx], voxel_indices [M,2], pts_in_voxel [M,3])."""
+    pts = _c(np.asarray(point_cloud).T, np.float64)
+    ext = _c(area_extents, np.float64).reshape(3, 2)
+    n = pts.shape[0]
+    hpd, lo, hi = slice_bounds(height_lo, height_hi, num_slices)
+    min_x, min_z = np.floor(ext[0, 0] / voxel_size), np.floor(ext[2, 0] / voxel_size)
+    nx = int(np.ceil(ext[0, 1] / voxel_size - 1) - min_x + 1)
+    nz = int(np.ceil(ext[2, 1] / voxel_size - 1) - min_z + 1)
+    cap = max(n * num_slices, 1)
+    vox = np.zeros((cap, 2), np.int64)
+    upts = np.zeros((cap, 3), np.float64)
+    hm = np.zeros((num_slices, nz, nx), np.float64)
+    dm = np.zeros((nz, nx), np.float64)
+    m = lib().shplo_bev_slices(n, _p(pts), _p(_c(ground_plane, np.float64)), _p(ext), float(voxel_size),
+                               num_slices, _p(_c(lo, np.float64)), _p(_c(hi, np.float64)), float(height_lo),
+                               float(height_hi), float(hpd), _p(_c(density_table(), np.float64)), cap,
+                               _p(vox), _p(upts), _p(hm), _p(dm))
+    return hm, dm, vox[:m].copy(), upts[:m].copy()
 
 
 # ---- TF op restatements ----------------------------------------------------

@@ -62,8 +62,11 @@ def _declare(lib):
         "shpl_version": (ctypes.c_char_p, []),
         "shpl_status_string": (ctypes.c_char_p, [i32]),
         "shpl_build_index_workspace_bytes": (i32, [i32, i64, psz]),
-        "shpl_build_index": (i32, [i32, p, i64, p, i32, p, i32, i64, p, d, d, d, d, d, d, p,
+        "shpl_build_index": (i32, [i32, p, p, i64, p, i32, p, i32, i64, p, d, d, d, d, d, d, p,
                                    p, p, p, p, p, p, p, p, p, sz, p]),
+        "shpl_bev_workspace_bytes": (i32, [i64, i32, psz]),
+        "shpl_bev_slices": (i32, [i32, p, i64, p, i32, p, p, d, i32, p, p, d, d, d, p, p, p, p, p, p, p,
+                                  p, sz, p]),
         "shpl_gen_index": (i32, [i64, p, i32, p, i32, i64, p, d, d, p, p, i64, p, p, sz, p]),
         "shpl_produce_index": (i32, [i64, p, i32, i64, p, i64, d, d, d, d, d, d, p, p, p, p, p,
                                      p, p, sz, p]),

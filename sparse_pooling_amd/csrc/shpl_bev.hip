@@ -1,0 +1,301 @@
+// shpl_bev.hip -- device BEV slice voxelizer: the input side of the SHPL
+// index builder.
+//
+// Reference (host numpy, once per frame in the data loader, ~32 ms/frame):
+//   BevSlices.generate_bev(output_indices=True)  avod/avod/core/bev_generators/bev_slices.py:33-156
+//   VoxelGrid2D.voxelize_2d                      avod/wavedata/wavedata/tools/core/voxel_grid_2d.py:43-162
+//   create_slice_filter / get_point_filter       avod/avod/datasets/kitti/kitti_utils.py:79-107,
+//                                                avod/wavedata/wavedata/tools/obj_detection/obj_utils.py:444-491
+//   dist_to_plane                                avod/wavedata/wavedata/tools/core/geometry_utils.py:26-40
+//   _create_density_map                          avod/avod/core/bev_generators/bev_generator.py:23-41
+//
+// What the reference computes, per height slice s (and once more over the
+// whole height range for the density map): keep the points inside the area
+// extents whose plane offset lies in [lo_s, hi_s); discretise by
+// floor(p / voxel_size); lexsort by (x, z, y) (stable); keep the first point
+// of every (x, z) cell -- the smallest discrete y, ties by point order; emit
+// the cells in (x, z) order with that point, its height above the ground
+// plane and the cell's point count.
+//
+// Here one 1024-thread workgroup voxelizes one frame, all slices at once:
+// every (point, slice) membership is an entry keyed
+//   v * n_cells + x_idx * nz + z_idx   (v = slice, or num_slices = density)
+// and packed with (discrete y, point index) into one 64-bit word whose
+// numeric order IS the reference's lexsort order. An LDS tile histogram +
+// scan + LDS-atomic placement + in-tile rank (the k_csr_frame scheme) sorts
+// the words; the first word of each key run is the cell's point and the run
+// length its count. Outputs keep the reference's order: slice-major, then
+// (x, z) ascending, exactly np.vstack(voxel_indices_stack).
+#include "shpl_common.h"
+
+namespace shpl {
+namespace {
+
+constexpr int BEV_BLOCK = 1024;
+constexpr int BEV_TILES = 16384;
+constexpr int BEV_MAX_SLICES = 8;
+constexpr int KEY_SHIFT = 42;  // [63:42] key, [41:32] discrete y - y0, [31:0] point index in frame
+
+struct BevGeom {
+    double ext[3][2];     // area extents (strict bounds)
+    double vs;            // voxel size
+    double lo[BEV_MAX_SLICES + 1], hi[BEV_MAX_SLICES + 1];  // plane offsets; [num_slices] = density range
+    double hpd;           // height per division
+    double dens[16];      // min(1, log(n + 1) / norm_value) for n = 0..15 (n >= 15 -> 1.0)
+    int num_slices;
+    int min_x, min_y, min_z;  // floor(ext_min / vs)
+    int nx, nz;           // divisions
+    int log_tile;
+};
+
+__device__ __forceinline__ bool below(const double *pl, double off, double x, double y, double z) {
+    // obj_utils.get_point_filter: np.dot(plane + [0,0,0,-off], [x;y;z;1]) < 0
+    double s = __dmul_rn(pl[0], x);
+    s = __fma_rn(pl[1], y, s);
+    s = __fma_rn(pl[2], z, s);
+    s = __fma_rn(__dsub_rn(pl[3], off), 1.0, s);
+    return s < 0.0;
+}
+
+template <typename PT>
+struct Pt {
+    static __device__ __forceinline__ void load(const void *p, int64_t i, double &x, double &y, double &z) {
+        const PT *q = reinterpret_cast<const PT *>(p) + 3 * i;
+        x = (double)q[0];
+        y = (double)q[1];
+        z = (double)q[2];
+    }
+};
+
+// Entries of one point: calls emit(word) for each slice it is in and for the density range.
+template <typename PT, typename F>
+__device__ __forceinline__ void point_entries(const BevGeom &g, const double *plane, const void *pts, int64_t i,
+                                              uint32_t li, int64_t n_cells, F &&emit) {
+    double x, y, z;
+    Pt<PT>::load(pts, i, x, y, z);
+    const bool inside = x > g.ext[0][0] && x < g.ext[0][1] && y > g.ext[1][0] && y < g.ext[1][1] &&
+                        z > g.ext[2][0] && z < g.ext[2][1];
+    if (!inside) return;
+    // voxelize_2d: floor(pts / voxel_size).astype(int32)
+    const int xd = (int)floor(__ddiv_rn(x, g.vs));
+    const int yd = (int)floor(__ddiv_rn(y, g.vs));
+    const int zd = (int)floor(__ddiv_rn(z, g.vs));
+    const int64_t cell = (int64_t)(xd - g.min_x) * g.nz + (zd - g.min_z);
+    const uint64_t low = ((uint64_t)(uint32_t)(yd - g.min_y) << 32) | li;
+    for (int s = 0; s <= g.num_slices; ++s) {
+        // create_slice_filter: xor(filter(hi), filter(lo)), both inside the extents
+        if (below(plane, g.hi[s], x, y, z) != below(plane, g.lo[s], x, y, z))
+            emit(((uint64_t)(s * n_cells + cell) << KEY_SHIFT) | low);
+    }
+}
+
+template <typename PT>
+__global__ __launch_bounds__(BEV_BLOCK) void k_bev_frame(BevGeom g, const int64_t *pt_off, const void *pts,
+                                                         const double *planes, uint64_t *tmp, uint64_t *srt,
+                                                         int64_t ent_per_point, int32_t *vox_out, double *pts_out,
+                                                         int64_t *frame_nvox, double *hmaps, double *dmap,
+                                                         uint32_t *err) {
+    __shared__ int32_t cnt[BEV_TILES];
+    __shared__ int32_t wsum[BEV_BLOCK / 64];
+    const int f = blockIdx.x;
+    const int64_t p0 = pt_off[f], p1 = pt_off[f + 1];
+    const int64_t t0 = p0 * ent_per_point;  // this frame's entry slots
+    const double *plane = planes + 4 * f;
+    const int64_t n_cells = (int64_t)g.nx * g.nz;
+    const int64_t n_keys = n_cells * (g.num_slices + 1);
+    const int n_tiles = (int)(((n_keys - 1) >> g.log_tile) + 1);
+    for (int t = threadIdx.x; t < BEV_TILES; t += BEV_BLOCK) cnt[t] = 0;
+    __syncthreads();
+    // 1. tile histogram of all (point, slice) entries
+    for (int64_t i = p0 + threadIdx.x; i < p1; i += BEV_BLOCK)
+        point_entries<PT>(g, plane, pts, i, (uint32_t)(i - p0), n_cells,
+                          [&](uint64_t w) { atomicAdd(&cnt[(int)((w >> KEY_SHIFT) >> g.log_tile)], 1); });
+    __syncthreads();
+    // 2. exclusive scan of the tile counts
+    {
+        constexpr int PER = BEV_TILES / BEV_BLOCK;
+        int32_t v[PER];
+        int32_t sum = 0;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            v[q] = cnt[threadIdx.x * PER + q];
+            sum += v[q];
+        }
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        int32_t x = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[wid] = x;
+        __syncthreads();
+        int32_t run = x - sum;
+        for (int w = 0; w < wid; ++w) run += wsum[w];
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            cnt[threadIdx.x * PER + q] = run;
+            run += v[q];
+        }
+    }
+    __syncthreads();
+    // 3. placement
+    for (int64_t i = p0 + threadIdx.x; i < p1; i += BEV_BLOCK)
+        point_entries<PT>(g, plane, pts, i, (uint32_t)(i - p0), n_cells, [&](uint64_t w) {
+            tmp[t0 + atomicAdd(&cnt[(int)((w >> KEY_SHIFT) >> g.log_tile)], 1)] = w;
+        });
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __syncthreads();
+    const int32_t n_ent = cnt[n_tiles - 1];
+    // 4. in-tile rank: the packed word's numeric order is (key, discrete y, point index)
+    for (int32_t s = threadIdx.x; s < n_ent; s += BEV_BLOCK) {
+        const uint64_t me = tmp[t0 + s];
+        const int t = (int)((me >> KEY_SHIFT) >> g.log_tile);
+        const int32_t a = t ? cnt[t - 1] : 0, b = cnt[t];
+        int32_t rank = 0;
+        for (int32_t u = a; u < b; ++u) rank += tmp[t0 + u] < me ? 1 : 0;
+        srt[t0 + a + rank] = me;
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __syncthreads();
+    // 5. one output per key run, slice cells compacted in sorted order
+    const double a = plane[0], b = plane[1], c = plane[2], d = plane[3];
+    const double norm = sqrt(__dadd_rn(__dadd_rn(__dmul_rn(a, a), __dmul_rn(b, b)), __dmul_rn(c, c)));
+    const int64_t cap = p1 - p0;
+    int64_t kept = 0;
+    const int wid = threadIdx.x >> 6;
+    for (int32_t base = 0; base < n_ent; base += BEV_BLOCK) {
+        const int32_t s = base + threadIdx.x;
+        bool first = false, slice_cell = false;
+        uint64_t me = 0, key = 0;
+        if (s < n_ent) {
+            me = srt[t0 + s];
+            key = me >> KEY_SHIFT;
+            first = s == 0 || (srt[t0 + s - 1] >> KEY_SHIFT) != key;
+            slice_cell = first && (int64_t)key < (int64_t)g.num_slices * n_cells;
+        }
+        const uint64_t m = __ballot(slice_cell);
+        if ((threadIdx.x & 63) == 0) wsum[wid] = (int32_t)__popcll(m);
+        __syncthreads();
+        int32_t before = 0, tot = 0;
+        for (int w = 0; w < BEV_BLOCK / 64; ++w) {
+            before += w < wid ? wsum[w] : 0;
+            tot += wsum[w];
+        }
+        if (first) {
+            const int v = (int)((int64_t)key / n_cells);
+            const int64_t cell = (int64_t)key - (int64_t)v * n_cells;
+            const int xi = (int)(cell / g.nz), zi = (int)(cell - (int64_t)xi * g.nz);
+            const int64_t pix = (int64_t)(g.nz - 1 - zi) * g.nx + xi;  // np.flip(map.T, axis=0)
+            if (v < g.num_slices) {
+                const int64_t pos = kept + before + lane_rank(m);
+                const int64_t li = (int64_t)(uint32_t)me;
+                double x, y, z;
+                Pt<PT>::load(pts, p0 + li, x, y, z);
+                if (pos < cap) {
+                    vox_out[2 * (p0 + pos)] = xi;
+                    vox_out[2 * (p0 + pos) + 1] = g.nz - zi;  // bev_slices.py:108 (num_div_z - z)
+                    pts_out[3 * (p0 + pos)] = x;
+                    pts_out[3 * (p0 + pos) + 1] = y;
+                    pts_out[3 * (p0 + pos) + 2] = z;
+                } else if (err) {
+                    atomicOr(err, SHPL_EBIT_ROW);
+                }
+                if (hmaps) {
+                    // dist_to_plane: (a*x + b*y + c*z + d) / sqrt(a^2 + b^2 + c^2)
+                    const double dist =
+                        __ddiv_rn(__dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(a, x), __dmul_rn(b, y)), __dmul_rn(c, z)), d),
+                                  norm);
+                    hmaps[((int64_t)f * g.num_slices + v) * n_cells + pix] = __ddiv_rn(__dsub_rn(dist, g.lo[v]), g.hpd);
+                }
+            } else if (dmap) {
+                int32_t n = 1;
+                while (s + n < n_ent && (srt[t0 + s + n] >> KEY_SHIFT) == key) ++n;
+                dmap[(int64_t)f * n_cells + pix] = n < 16 ? g.dens[n] : 1.0;
+            }
+        }
+        kept += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) frame_nvox[f] = kept < cap ? kept : cap;
+    for (int64_t pos = kept + threadIdx.x; pos < cap; pos += BEV_BLOCK) {
+        vox_out[2 * (p0 + pos)] = -1;
+        vox_out[2 * (p0 + pos) + 1] = -1;
+    }
+}
+
+}  // namespace
+}  // namespace shpl
+
+using namespace shpl;
+
+extern "C" int shpl_bev_workspace_bytes(int64_t total_points, int num_slices, size_t *bytes) {
+    if (!bytes || total_points < 0 || num_slices < 1 || num_slices > BEV_MAX_SLICES) return SHPL_ERR_ARG;
+    const size_t n = (size_t)(total_points > 0 ? total_points : 1) * (size_t)(num_slices + 1);
+    *bytes = 2 * align_up(n * sizeof(uint64_t), 256);
+    return SHPL_OK;
+}
+
+extern "C" int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, int64_t total_points,
+                               const void *d_points, int points_dtype, const double *d_planes,
+                               const double *area_extents, double voxel_size, int num_slices,
+                               const double *slice_lo, const double *slice_hi, double density_lo,
+                               double density_hi, double height_per_division, const double *density_table,
+                               int32_t *d_voxel_indices, double *d_pts_in_voxel, int64_t *d_frame_nvox,
+                               double *d_height_maps, double *d_density_map, uint32_t *d_err, void *d_ws,
+                               size_t ws_bytes, void *stream) {
+    if (n_frames < 1 || !d_point_offsets || !d_planes || !area_extents || !slice_lo || !slice_hi ||
+        !density_table || !d_frame_nvox || !d_ws)
+        return SHPL_ERR_ARG;
+    if (num_slices < 1 || num_slices > BEV_MAX_SLICES || !(voxel_size > 0)) return SHPL_ERR_BAD_SHAPE;
+    if (total_points > 0 && (!d_points || !d_voxel_indices || !d_pts_in_voxel)) return SHPL_ERR_ARG;
+    if (total_points >= ((int64_t)1 << 31)) return SHPL_ERR_BAD_SHAPE;
+    size_t need;
+    shpl_bev_workspace_bytes(total_points, num_slices, &need);
+    if (need > ws_bytes) return SHPL_ERR_WORKSPACE;
+    BevGeom g{};
+    for (int i = 0; i < 3; ++i) {
+        g.ext[i][0] = area_extents[2 * i];
+        g.ext[i][1] = area_extents[2 * i + 1];
+    }
+    g.vs = voxel_size;
+    g.num_slices = num_slices;
+    for (int s = 0; s < num_slices; ++s) {
+        g.lo[s] = slice_lo[s];
+        g.hi[s] = slice_hi[s];
+    }
+    g.lo[num_slices] = density_lo;
+    g.hi[num_slices] = density_hi;
+    g.hpd = height_per_division;
+    for (int n = 0; n < 16; ++n) g.dens[n] = density_table[n];
+    // voxel_grid_2d.py:127-149: min = floor(ext_min / vs), max = ceil(ext_max / vs - 1), y collapsed
+    g.min_x = (int)floor(g.ext[0][0] / voxel_size);
+    g.min_y = (int)floor(g.ext[1][0] / voxel_size);
+    g.min_z = (int)floor(g.ext[2][0] / voxel_size);
+    g.nx = (int)(ceil(g.ext[0][1] / voxel_size - 1) - g.min_x + 1);
+    g.nz = (int)(ceil(g.ext[2][1] / voxel_size - 1) - g.min_z + 1);
+    const int ny = (int)(floor(g.ext[1][1] / voxel_size) - g.min_y + 1);
+    if (g.nx < 1 || g.nz < 1 || ny < 1 || ny >= 1024) return SHPL_ERR_BAD_SHAPE;
+    const int64_t n_keys = (int64_t)g.nx * g.nz * (num_slices + 1);
+    if (n_keys >= ((int64_t)1 << 22)) return SHPL_ERR_BAD_SHAPE;  // key field of the packed word
+    g.log_tile = 0;
+    while (((n_keys - 1) >> g.log_tile) + 1 > BEV_TILES) ++g.log_tile;
+    const size_t half = need / 2;
+    uint64_t *tmp = (uint64_t *)d_ws;
+    uint64_t *srt = (uint64_t *)((char *)d_ws + half);
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t per_map = (int64_t)g.nx * g.nz;
+    if (d_height_maps)
+        SHPL_HIP_CHECK(hipMemsetAsync(d_height_maps, 0, sizeof(double) * (size_t)(per_map * num_slices * n_frames), s));
+    if (d_density_map) SHPL_HIP_CHECK(hipMemsetAsync(d_density_map, 0, sizeof(double) * (size_t)(per_map * n_frames), s));
+    if (points_dtype == SHPL_F64)
+        hipLaunchKernelGGL(k_bev_frame<double>, dim3(n_frames), dim3(BEV_BLOCK), 0, s, g, d_point_offsets, d_points,
+                           d_planes, tmp, srt, (int64_t)(num_slices + 1), d_voxel_indices, d_pts_in_voxel,
+                           d_frame_nvox, d_height_maps, d_density_map, d_err);
+    else
+        return SHPL_ERR_ARG;
+    SHPL_LAUNCH_CHECK();
+    return SHPL_OK;
+}

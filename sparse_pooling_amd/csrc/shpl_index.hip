@@ -244,11 +244,13 @@ struct ProduceStage {  // produce_sparse_pooling_input (in-place img_index updat
 // ------------------------------------------------- per-frame stable compaction
 
 template <typename Stage>
-__global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, const int64_t *pt_off, int64_t *frame_nnz,
-                                                       int64_t *frame_out_off, int n_frames) {
+__global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, const int64_t *pt_off, const int64_t *pt_count,
+                                                       int64_t *frame_nnz, int64_t *frame_out_off, int n_frames) {
     __shared__ int32_t wsum[IDX_BLOCK / 64];
     const int f = blockIdx.x;
-    const int64_t p0 = pt_off[f], p1 = pt_off[f + 1];
+    const int64_t p0 = pt_off[f], cap_end = pt_off[f + 1];
+    // live points of the frame: [p0, p0 + count) when counts are given (capacity layout input)
+    const int64_t p1 = pt_count ? (p0 + pt_count[f] < cap_end ? p0 + pt_count[f] : cap_end) : cap_end;
     const int wid = threadIdx.x >> 6;
     int64_t kept = 0;
     for (int64_t base = p0; base < p1; base += IDX_BLOCK) {
@@ -272,20 +274,20 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, const int64_t *
         kept += tot;
         __syncthreads();  // wsum is rewritten by the next chunk
     }
-    for (int64_t pos = p0 + kept + threadIdx.x; pos < p1; pos += IDX_BLOCK) st.hole(pos);
+    for (int64_t pos = p0 + kept + threadIdx.x; pos < cap_end; pos += IDX_BLOCK) st.hole(pos);
     if (threadIdx.x == 0) {
         if (frame_nnz) frame_nnz[f] = kept;
         if (frame_out_off) {
             frame_out_off[f] = p0;
-            if (f == n_frames - 1) frame_out_off[n_frames] = p1;
+            if (f == n_frames - 1) frame_out_off[n_frames] = cap_end;
         }
     }
 }
 
 template <typename Stage>
-int run_compaction(const Stage &st, int n_frames, const int64_t *pt_off, int64_t *frame_nnz,
-                   int64_t *frame_out_off, hipStream_t stream) {
-    hipLaunchKernelGGL(k_compact<Stage>, dim3(n_frames), dim3(IDX_BLOCK), 0, stream, st, pt_off, frame_nnz,
+int run_compaction(const Stage &st, int n_frames, const int64_t *pt_off, const int64_t *pt_count,
+                   int64_t *frame_nnz, int64_t *frame_out_off, hipStream_t stream) {
+    hipLaunchKernelGGL(k_compact<Stage>, dim3(n_frames), dim3(IDX_BLOCK), 0, stream, st, pt_off, pt_count, frame_nnz,
                        frame_out_off, n_frames);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
@@ -307,7 +309,8 @@ extern "C" int shpl_build_index_workspace_bytes(int n_frames, int64_t max_points
     return SHPL_OK;
 }
 
-extern "C" int shpl_build_index(int n_frames, const int64_t *d_point_offsets, int64_t max_points_per_frame,
+extern "C" int shpl_build_index(int n_frames, const int64_t *d_point_offsets, const int64_t *d_point_counts,
+                                int64_t max_points_per_frame,
                                 const void *d_points, int points_dtype, const void *d_voxels,
                                 int voxels_itype, int64_t vox_stride, const double *d_P, double im_w,
                                 double im_h, double bv_h, double bv_w, double s_img, double s_bv,
@@ -327,7 +330,7 @@ extern "C" int shpl_build_index(int n_frames, const int64_t *d_point_offsets, in
     {                                                                                            \
         FusedStage<PT, VT> st{d_points, d_voxels, vox_stride, d_P, g, d_mval, d_cell, d_pix,     \
                               d_val, d_mij, d_flip, d_err};                                      \
-        return run_compaction(st, n_frames, d_point_offsets, d_frame_nnz, d_frame_out_off, s);   \
+        return run_compaction(st, n_frames, d_point_offsets, d_point_counts, d_frame_nnz, d_frame_out_off, s); \
     }
     if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I64) SHPL_FUSED(double, int64_t)
     if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I32) SHPL_FUSED(double, int32_t)
@@ -363,7 +366,7 @@ extern "C" int shpl_gen_index(int64_t n, const void *d_points, int points_dtype,
     {                                                                                             \
         GenStage<PT, VT> st{d_points, d_voxels, vox_stride, d_P, im_w, im_h, d_bv_index,          \
                             d_img_index, ld};                                                     \
-        return run_compaction(st, 1, off, d_nv, nullptr, s);                                     \
+        return run_compaction(st, 1, off, nullptr, d_nv, nullptr, s);                            \
     }
     if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I64) SHPL_GEN(double, int64_t)
     if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I32) SHPL_GEN(double, int32_t)
@@ -388,11 +391,11 @@ extern "C" int shpl_produce_index(int64_t nv, const void *d_bv_index, int bv_ity
     if (rc) return rc;
     if (bv_itype == SHPL_I64) {
         ProduceStage<int64_t> st{d_bv_index, bv_stride, d_img_index, ld, g, d_mij, d_flip, d_cell, d_pix, d_err};
-        return run_compaction(st, 1, off, d_nk, nullptr, s);
+        return run_compaction(st, 1, off, nullptr, d_nk, nullptr, s);
     }
     if (bv_itype == SHPL_I32) {
         ProduceStage<int32_t> st{d_bv_index, bv_stride, d_img_index, ld, g, d_mij, d_flip, d_cell, d_pix, d_err};
-        return run_compaction(st, 1, off, d_nk, nullptr, s);
+        return run_compaction(st, 1, off, nullptr, d_nk, nullptr, s);
     }
     return SHPL_ERR_ARG;
 }

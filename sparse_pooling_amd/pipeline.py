@@ -55,10 +55,10 @@ class FusedPipeline:
         self._lib = L.lib()
 
     # ------------------------------------------------------------------ steps
-    def build_index(self, points, voxels, point_offsets, P, mval=None):
+    def build_index(self, points, voxels, point_offsets, P, mval=None, point_counts=None):
         st = L.stream_of(self.dev)
         L.check(self._lib.shpl_build_index(
-            self.B, L.ptr(point_offsets), self.max_points, L.ptr(points),
+            self.B, L.ptr(point_offsets), L.ptr(point_counts), self.max_points, L.ptr(points),
             L.F64 if points.dtype == torch.float64 else L.F32, L.ptr(voxels),
             L.I64 if voxels.dtype == torch.int64 else L.I32, int(voxels.stride(0)), L.ptr(P),
             float(self.im_size[0]), float(self.im_size[1]), float(self.bv_size[0]),
@@ -129,6 +129,21 @@ class FusedPipeline:
         if events:
             events[3].record(main)
 
+    def backward(self, g_bv, g_img, d_bev, d_img):
+        """TF gradient of the dual layer with the concat split and add_n fused:
+        d_bev = g_bv[..., :Cb] + M^T-pull of g_img[..., Ci:]
+        d_img = g_img[..., :Ci] + scatter of M-pulled g_bv[..., Cb:].
+        With the builder's identity columns the forward entry lists already are
+        in the gradients' TF order (ORDER_COL_ENTRY == ORDER_ENTRY / COL_ROW)."""
+        assert self.dual
+        st = L.stream_of(self.dev)
+        w = self.Cb + self.Ci
+        dt = L.dtype_code(d_bev)
+        L.check(self._lib.shpl_pull(L.BY_CELL, dt, self.csr.ref(), L.ptr(g_img), w, self.Ci, self.Cb, L.ptr(g_bv),
+                                    w, 0, self.Cb, L.OUT_ADD, L.ptr(d_bev), self.Cb, st), "shpl_pull")
+        L.check(self._lib.shpl_pull(L.BY_PIXEL, dt, self.pcsr.ref(), L.ptr(g_bv), w, self.Cb, self.Ci,
+                                    L.ptr(g_img), w, 0, self.Ci, L.OUT_ADD, L.ptr(d_img), self.Ci, st), "shpl_pull")
+
     def map(self):
         """The current M as a ShplMap (for tests)."""
         return ShplMap(self.cell, None, self.val, self.pix, self.N, self.n_cells, self.n_pix, self.N,
@@ -146,3 +161,38 @@ def stack_frames(frames, device):
     t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt).to(device)  # noqa: E731
     return (t(pts, torch.float64), t(vox, torch.int64), t(off, torch.int64), t(P, torch.float64),
             int(max(f.points.shape[0] for f in frames)), int(pts.shape[0]))
+
+
+class FramePipeline(FusedPipeline):
+    """The whole per-frame SHPL path from raw camera-frame point clouds:
+    shpl_bev_slices (BevSlices.generate_bev(output_indices=True), bev_slices.py:33-156)
+    -> shpl_build_index on its voxel points (kitti_dataset.py:374-379)
+    -> destination-sorted M -> fused layer. bv_size is the BEV map size (nz, nx)."""
+
+    def __init__(self, n_frames, total_points, im_size, area_extents, voxel_size, height_lo, height_hi,
+                 num_slices, stride, c_bev, c_img, dtype=torch.float32, device="cuda", dual=False, maps=True):
+        from . import bev as _bev
+        nx, nz = _bev.grid_divisions(area_extents, voxel_size)
+        # a frame can hold up to total_points voxels in the capacity layout
+        super().__init__(n_frames, total_points, total_points, im_size, (nz, nx), stride, c_bev, c_img,
+                         dtype=dtype, device=device, dual=dual)
+        self.bev_args = (area_extents, voxel_size, height_lo, height_hi, num_slices)
+        self.maps = maps
+        import ctypes
+        nb = ctypes.c_size_t()
+        L.check(self._lib.shpl_bev_workspace_bytes(self.N, int(num_slices), ctypes.byref(nb)),
+                "shpl_bev_workspace_bytes")
+        self.bev_ws = L.workspace(nb.value, self.dev)
+        self.bev = None
+
+    def build_bev(self, points, point_offsets, planes):
+        from . import bev as _bev
+        self.bev = _bev.bev_slices_batch(points, point_offsets, planes, *self.bev_args, maps=self.maps,
+                                         ws=self.bev_ws)
+        return self.bev
+
+    def frame_step(self, points, point_offsets, planes, P, bev_feat, img_feat):
+        b = self.build_bev(points, point_offsets, planes)
+        self.build_index(b.pts_in_voxel, b.voxel_indices, point_offsets, P, point_counts=b.frame_nvox)
+        self.build_csr()
+        self.layer(bev_feat, img_feat)

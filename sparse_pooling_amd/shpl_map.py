@@ -287,7 +287,7 @@ class IndexBatch:
 
 
 def build_index_batch(points, voxels, point_offsets, P, im_size, bv_size, stride, max_points,
-                      mval=None, ref_outputs=False, ws=None):
+                      mval=None, ref_outputs=False, ws=None, point_counts=None):
     """Fused gen_sparse_pooling_input_avod + produce_sparse_pooling_input for a
     batch of frames in one pass (shpl_build_index). All inputs are device
     tensors; nothing synchronises the host."""
@@ -308,7 +308,8 @@ def build_index_batch(points, voxels, point_offsets, P, im_size, bv_size, stride
         ws = L.workspace(L.index_ws_bytes(n_frames, max_points), dev)
     pdt = L.F64 if points.dtype == torch.float64 else L.F32
     vit = L.I64 if voxels.dtype == torch.int64 else L.I32
-    L.check(L.lib().shpl_build_index(n_frames, L.ptr(point_offsets), int(max_points), L.ptr(points),
+    L.check(L.lib().shpl_build_index(n_frames, L.ptr(point_offsets), L.ptr(point_counts), int(max_points),
+                                     L.ptr(points),
                                      pdt, L.ptr(voxels), vit, int(voxels.stride(0)), L.ptr(P),
                                      float(im_size[0]), float(im_size[1]), float(bv_size[0]),
                                      float(bv_size[1]), s_img, s_bv, L.ptr(mval), L.ptr(cell),

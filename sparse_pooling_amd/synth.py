@@ -113,3 +113,22 @@ class StereoCalib:
 
     def __init__(self, p2):
         self.p2 = np.asarray(p2, dtype=np.float64)
+
+
+# Area / slicing of the reference's SHPL configs (e.g. configs/retinanet_car_SHPL.config:115-124)
+AREA_EXTENTS = np.array([[-40.0, 40.0], [-5.0, 3.0], [0.0, 70.0]])
+GROUND_PLANE = np.array([0.0, -1.0, 0.0, 1.65])
+VOXEL_SIZE, HEIGHT_LO, HEIGHT_HI, NUM_SLICES = 0.1, -0.2, 2.3, 5
+
+
+def make_cloud(n, seed, plane=GROUND_PLANE):
+    """A raw camera-frame LiDAR-like cloud (3, n): x across, y down, z forward,
+    heights spread over the BEV slices above the ground plane, some points
+    outside the area extents and the height range."""
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(-42, 42, n)
+    z = rng.uniform(-1, 72, n)
+    h = rng.uniform(-0.6, 2.8, n)                  # height above the ground plane
+    a, b, c, d = plane
+    y = (h * np.sqrt(a * a + b * b + c * c) - a * x - c * z - d) / b
+    return np.stack([x, y, z])

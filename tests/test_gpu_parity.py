@@ -328,3 +328,118 @@ def test_full_size_properties_config5():
     assert abs(lhs - rhs) <= 1e-4 * max(1.0, abs(lhs))
     assert int(pl.frame_nnz.item()) == frames[0].points.shape[0] - int(
         (frames[0].voxel_indices[:, 1] >= spec.bv_size[0]).sum())
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_pipeline_backward_matches_oracle(dtype):
+    """FusedPipeline.backward (the config-3 bench gradient) vs the oracle's TF gradients."""
+    from sparse_pooling_amd import pipeline
+    spec = synth.CONFIGS[1]
+    frames = [synth.make_frame(spec, seed=60 + f, n_outside=10) for f in range(2)]
+    pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
+    tdt = torch.float32 if dtype == "f32" else torch.bfloat16
+    pl = pipeline.FusedPipeline(2, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev, spec.c_img,
+                                dtype=tdt, dual=True)
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    Cb, Ci = spec.c_bev, spec.c_img
+
+    def mk(shape, seed):
+        x = synth.make_features(shape, seed)
+        if dtype == "bf16":
+            x = orc.from_bf16_bits(orc.to_bf16_bits(x)).reshape(shape)
+        return x, torch.from_numpy(x).to(DEV).to(tdt)
+    bev, tb = mk((2, Hb, Wb, Cb), 1)
+    img, ti = mk((2, Hi, Wi, Ci), 2)
+    gb, tgb = mk((2, Hb, Wb, Cb + Ci), 3)
+    gi, tgi = mk((2, Hi, Wi, Ci + Cb), 4)
+    pl.step(pts, vox, off, P, tb, ti)
+    d_bev, d_img = torch.empty_like(tb), torch.empty_like(ti)
+    pl.backward(tgb, tgi, d_bev, d_img)
+    torch.cuda.synchronize()
+    for f, fr in enumerate(frames):
+        ref = _oracle_frame(fr, spec.stride)
+        mij, mval, msize, idx = ref["Mij_pool"], ref["M_val"], ref["M_size"], ref["img_index_flip_pool"]
+        e_img = gi[f:f + 1, ..., :Ci] + orc.sparse_pool_grad_img(
+            mij, mval, msize, gb[f, ..., Cb:].reshape(-1, Ci), idx, (1, Hi, Wi, Ci))
+        e_bev = gb[f:f + 1, ..., :Cb] + orc.sparse_pool_trans_grad_bev(
+            mij, mval, msize, np.ascontiguousarray(gi[f:f + 1, ..., Ci:]), idx).reshape(1, Hb, Wb, Cb)
+        if dtype == "f32":
+            _close_and_exact(d_img[f:f + 1], e_img)
+            _close_and_exact(d_bev[f:f + 1], e_bev)
+        else:
+            got_i = _np(d_img[f:f + 1].view(torch.int16)).view(np.uint16)
+            got_b = _np(d_bev[f:f + 1].view(torch.int16)).view(np.uint16)
+            np.testing.assert_array_equal(got_i, orc.to_bf16_bits(e_img.astype(np.float32)))
+            np.testing.assert_array_equal(got_b, orc.to_bf16_bits(e_bev.astype(np.float32)))
+
+
+# ---------------------------------------------------------------- BEV voxelizer
+
+def test_bev_slices_vs_reference_golden():
+    from sparse_pooling_amd import bev
+    g = np.load(os.path.join(GOLD, "bev_slices.npz"))
+    import types
+    cfg = types.SimpleNamespace(height_lo=float(g["height_lo"]), height_hi=float(g["height_hi"]),
+                                num_slices=int(g["num_slices"]))
+    maps, vox, upts = bev.BevSlices(cfg).generate_bev("lidar", g["point_cloud"], g["ground_plane"],
+                                                      g["area_extents"], float(g["voxel_size"]),
+                                                      output_indices=True)
+    np.testing.assert_array_equal(_np(vox), g["voxel_indices"])
+    np.testing.assert_array_equal(_np(upts), g["pts_in_voxel"])
+    np.testing.assert_array_equal(np.stack([_np(m) for m in maps["height_maps"]]), g["height_maps"])
+    np.testing.assert_array_equal(_np(maps["density_map"]), g["density_map"])
+
+
+def test_bev_slices_batch_vs_oracle():
+    from sparse_pooling_amd import bev
+    clouds = [synth.make_cloud(15000 + 3000 * f, seed=200 + f) for f in range(3)]
+    planes = [synth.GROUND_PLANE + np.array([0.01 * f, 0, -0.005 * f, 0.02 * f]) for f in range(3)]
+    pts = torch.from_numpy(np.concatenate([c.T for c in clouds])).to(DEV)
+    off = torch.tensor(np.concatenate([[0], np.cumsum([c.shape[1] for c in clouds])]), device=DEV)
+    pl = torch.from_numpy(np.stack(planes)).to(DEV)
+    b = bev.bev_slices_batch(pts, off, pl, synth.AREA_EXTENTS, synth.VOXEL_SIZE, synth.HEIGHT_LO,
+                             synth.HEIGHT_HI, synth.NUM_SLICES)
+    torch.cuda.synchronize()
+    o, n = _np(off), _np(b.frame_nvox)
+    for f, c in enumerate(clouds):
+        hm, dm, vox, upts = orc.bev_slices(c, planes[f], synth.AREA_EXTENTS, synth.VOXEL_SIZE, synth.HEIGHT_LO,
+                                           synth.HEIGHT_HI, synth.NUM_SLICES)
+        a = o[f]
+        np.testing.assert_array_equal(_np(b.voxel_indices[a:a + n[f]]), vox)
+        np.testing.assert_array_equal(_np(b.pts_in_voxel[a:a + n[f]]), upts)
+        np.testing.assert_array_equal(_np(b.height_maps[f]), hm)
+        np.testing.assert_array_equal(_np(b.density_map[f]), dm)
+    assert int(b.err.item()) == 0
+
+
+def test_points_to_fused_layer_pipeline():
+    """Raw clouds -> device BEV voxelizer -> index builder -> sorted M -> fused
+    layer, against the oracle chain (bev_slices -> gen -> produce -> pool)."""
+    from sparse_pooling_amd import pipeline
+    F = 2
+    clouds = [synth.make_cloud(30000, seed=300 + f) for f in range(F)]
+    planes = np.stack([synth.GROUND_PLANE] * F)
+    Ps = [synth.KITTI_P2, synth.KITTI_P2 + np.array([[0.5, 0, 1.0, 0], [0, 0.5, -1.0, 0], [0, 0, 0, 0]])]
+    im_size, stride, C = (1242, 375), (4, 4), 8
+    pts = torch.from_numpy(np.concatenate([c.T for c in clouds])).to(DEV)
+    off = torch.tensor(np.concatenate([[0], np.cumsum([c.shape[1] for c in clouds])]), device=DEV)
+    pl = pipeline.FramePipeline(F, int(pts.shape[0]), im_size, synth.AREA_EXTENTS, synth.VOXEL_SIZE,
+                                synth.HEIGHT_LO, synth.HEIGHT_HI, synth.NUM_SLICES, stride, C, C, dual=True)
+    bev = synth.make_features((F, pl.Hb, pl.Wb, C), 1)
+    img = synth.make_features((F, pl.Hi, pl.Wi, C), 2)
+    pl.frame_step(pts, off, torch.from_numpy(planes).to(DEV), torch.from_numpy(np.stack([p.reshape(12) for p in Ps])).to(DEV),
+                  torch.from_numpy(bev).to(DEV), torch.from_numpy(img).to(DEV))
+    torch.cuda.synchronize()
+    assert int(pl.err.item()) == 0
+    out, iout = _np(pl.bv_fused), _np(pl.img_fused)
+    for f, c in enumerate(clouds):
+        hm, dm, vox, upts = orc.bev_slices(c, planes[f], synth.AREA_EXTENTS, synth.VOXEL_SIZE, synth.HEIGHT_LO,
+                                           synth.HEIGHT_HI, synth.NUM_SLICES)
+        g = orc.gen_sparse_pooling_input_avod(upts, vox, Ps[f], list(im_size), (hm.shape[1], hm.shape[2]))
+        ref = orc.produce_sparse_pooling_input(g, stride=stride)
+        assert int(_np(pl.frame_nnz)[f]) == ref["Mij_pool"].shape[0]
+        eb, ei = orc.sparse_pool_layer(bev[f:f + 1], img[f:f + 1], ref["Mij_pool"], ref["M_val"], ref["M_size"],
+                                       ref["img_index_flip_pool"], dual=True)
+        _close_and_exact(out[f:f + 1], eb)
+        _close_and_exact(iout[f:f + 1], ei)

@@ -140,3 +140,14 @@ def test_projection_fma_chain_matches_numpy():
     ok = (u >= 0) & (v >= 0)
     np.testing.assert_array_equal(g["img_index"][0], np.round(u[ok]))
     np.testing.assert_array_equal(g["img_index"][1], np.round(v[ok]))
+
+
+def test_bev_slices_oracle_matches_reference(golden_dir):
+    g = np.load(os.path.join(golden_dir, "bev_slices.npz"))
+    hm, dm, vox, upts = orc.bev_slices(g["point_cloud"], g["ground_plane"], g["area_extents"],
+                                       float(g["voxel_size"]), float(g["height_lo"]), float(g["height_hi"]),
+                                       int(g["num_slices"]))
+    np.testing.assert_array_equal(vox, g["voxel_indices"])
+    np.testing.assert_array_equal(upts, g["pts_in_voxel"])
+    np.testing.assert_array_equal(hm, g["height_maps"])
+    np.testing.assert_array_equal(dm, g["density_map"])
