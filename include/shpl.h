@@ -169,6 +169,26 @@ int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, int64_t total_
                     double *d_height_maps, double *d_density_map, uint32_t *d_err, void *d_ws,
                     size_t ws_bytes, void *stream);
 
+/* MV3D_TF's producer point_cloud_2_top_sparse
+ * (MV3D_TF_release/lib/utils/construct_voxel.py:37-162), n_frames at once:
+ *   d_points     [N, point_stride] f64 camera-frame points (x, y, z, ...)
+ *   d_img_index2 optional [2, N] i64 rounded projections (minibatch_mv3d_img.py:88-91);
+ *                NULL: computed on the device from d_P [n_frames,3,4] like the reference
+ *   ranges       host [6] f64: fwd (lo, hi), side (lo, hi), height (lo, hi), strict bounds
+ *   res, zres, voxel_point_count  cfg.VOXEL_X_SIZE, VOXEL_Z_SIZE, VOXEL_POINT_COUNT
+ * Outputs, capacity layout (frame f at [off[f], off[f] + d_frame_n[f])):
+ *   d_img_index [3, ld] f64 ([u; v; 0]), d_bv_index [N,2] i64 (fwd, side),
+ *   d_mval [N] f64 = 1 / points accepted by the point's voxel;
+ *   d_number_buffer optional [N] i32: accepted points per voxel in voxel order,
+ *   d_frame_nvox voxels per frame. */
+int shpl_mv3d_workspace_bytes(int64_t total_points, size_t *bytes);
+int shpl_mv3d_voxels(int n_frames, const int64_t *d_point_offsets, int64_t total_points,
+                     const double *d_points, int64_t point_stride, const int64_t *d_img_index2,
+                     const double *d_P, const double *ranges, double res, double zres,
+                     int voxel_point_count, double *d_img_index, int64_t ld, int64_t *d_bv_index,
+                     double *d_mval, int64_t *d_frame_n, int32_t *d_number_buffer,
+                     int64_t *d_frame_nvox, void *d_ws, size_t ws_bytes, void *stream);
+
 /* ---------------------------------------------------------------------------
  * Correspondence matrix M: validation + device map (SURVEY a8-a10 inputs)
  * ------------------------------------------------------------------------- */

@@ -383,3 +383,79 @@ int64_t shplo_bev_slices(int64_t n, const double *pts, const double *plane, cons
     free(buf);
     return out;
 }
+
+/* ---- a7: MV3D point_cloud_2_top_sparse (construct_voxel.py:37-162) --------
+ * pts n x stride camera frame (x, y, z, ...), img2 [2][n] rounded projections
+ * of every point (minibatch_mv3d_img.py:88-91); ranges fwd/side/height (lo, hi).
+ * The per-point loop of the reference (:134-140) is kept as is: a voxel
+ * accepts points in point order until it holds `cap`. Outputs img_index
+ * [3][ld] f64, bv_index n' x 2 (fwd, side), mval n' (1 / accepted count).
+ * Returns n'. */
+static int64_t *g_vkey;
+static int cmp_key_idx(const void *pa, const void *pb)
+{
+    const int64_t a = *(const int64_t *)pa, b = *(const int64_t *)pb;
+    if (g_vkey[a] != g_vkey[b]) return g_vkey[a] < g_vkey[b] ? -1 : 1;
+    return a < b ? -1 : (a > b);
+}
+
+int64_t shplo_mv3d_voxels(int64_t n, const double *pts, int64_t stride, const int64_t *img2, const double *ranges,
+                          double res, double zres, int cap, double *img_index, int64_t ld, int64_t *bv_index,
+                          double *mval, int32_t *number_buffer, int64_t *n_vox)
+{
+    const int n_fwd = (int)((ranges[1] - ranges[0]) / res) + 1;
+    const int n_h = (int)((ranges[5] - ranges[4]) / zres) + 1;
+    int64_t *key = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+    int64_t *ord = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+    int32_t *vid = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+    int32_t *fi = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+    int32_t *si = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+    int64_t m = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const double *q = pts + i * stride;
+        const double fwd = q[2], side = q[0], h = q[1];
+        key[i] = -1;
+        if (!(fwd > ranges[0] && fwd < ranges[1] && side > ranges[2] && side < ranges[3] && h > ranges[4] &&
+              h < ranges[5]))
+            continue;
+        si[i] = (int32_t)((side - ranges[2]) / res);
+        fi[i] = (int32_t)((fwd - ranges[0]) / res);
+        const int32_t hi = (int32_t)((h - ranges[4]) / zres);
+        key[i] = ((int64_t)si[i] * n_fwd + fi[i]) * n_h + hi;
+        ord[m++] = i;
+    }
+    /* np.unique(xyz_img, axis=0, return_inverse=True): voxel ids in lexicographic order */
+    g_vkey = key;
+    qsort(ord, (size_t)m, sizeof(int64_t), cmp_key_idx);
+    int32_t nv = 0;
+    for (int64_t j = 0; j < m; ++j) {
+        if (j > 0 && key[ord[j]] != key[ord[j - 1]]) ++nv;
+        vid[ord[j]] = nv;
+    }
+    const int32_t n_voxels = m > 0 ? nv + 1 : 0;
+    int32_t *count = (int32_t *)calloc((size_t)(n_voxels > 0 ? n_voxels : 1), sizeof(int32_t));
+    unsigned char *keep = (unsigned char *)calloc((size_t)(n > 0 ? n : 1), 1);
+    for (int64_t i = 0; i < n; ++i) { /* the reference's per-point loop, in point order */
+        if (key[i] < 0) continue;
+        if (count[vid[i]] < cap) {
+            ++count[vid[i]];
+            keep[i] = 1;
+        }
+    }
+    int64_t out = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (!keep[i]) continue;
+        img_index[out] = (double)img2[i];
+        img_index[ld + out] = (double)img2[n + i];
+        img_index[2 * ld + out] = 0.0;
+        bv_index[2 * out] = fi[i];
+        bv_index[2 * out + 1] = si[i];
+        mval[out] = 1.0 / (double)count[vid[i]];
+        ++out;
+    }
+    if (number_buffer)
+        for (int32_t v = 0; v < n_voxels; ++v) number_buffer[v] = count[v];
+    if (n_vox) *n_vox = n_voxels;
+    free(key); free(ord); free(vid); free(fi); free(si); free(count); free(keep);
+    return out;
+}

@@ -47,6 +47,8 @@ def lib():
         _lib.shplo_pool_trans_grad_bev.restype = ctypes.c_int
         _lib.shplo_pool_trans_grad_bev.argtypes = [p, i64, i64, i64, i64, p, i64, p, p, i64, i64,
                                                     i64, p]
+        _lib.shplo_mv3d_voxels.restype = i64
+        _lib.shplo_mv3d_voxels.argtypes = [i64, p, i64, p, p, d, d, ctypes.c_int, p, i64, p, p, p, p]
         _lib.shplo_bev_slices.restype = i64
         _lib.shplo_bev_slices.argtypes = [i64, p, p, p, d, ctypes.c_int, p, p, d, d, d, p, i64, p, p,
                                           p, p]
@@ -133,6 +135,30 @@ def bev_slices(point_cloud, ground_plane, area_extents, voxel_size, height_lo, h
                                float(height_hi), float(hpd), _p(_c(density_table(), np.float64)), cap,
                                _p(vox), _p(upts), _p(hm), _p(dm))
     return hm, dm, vox[:m].copy(), upts[:m].copy()
+
+
+# ---- MV3D producer (a7) ------------------------------------------------------
+
+# MV3D cfg (MV3D_TF_release/lib/utils/config_voxels.py:49-59, DETECT_OBJ != 'Car') and the
+# ranges construct_voxel.py:11-13 derives from it.
+MV3D_PED = dict(ranges=(0.0, 48 - 0.01, -20.0, 20 - 0.01, -1.0, 3 - 0.01), res=0.2, zres=0.4, cap=45)
+
+
+def mv3d_voxels(points, img_index2, ranges, res, zres, cap):
+    """Restates point_cloud_2_top_sparse's SHPL outputs: (img_index [3,n'] f64,
+    bv_index [n',2] (fwd, side), M_val [n'], number_buffer [V])."""
+    pts = _c(points, np.float64)
+    n, stride = pts.shape
+    img2 = _c(img_index2, np.int64).reshape(2, n)
+    img = np.zeros((3, max(n, 1)), np.float64)
+    bv = np.zeros((max(n, 1), 2), np.int64)
+    mv = np.zeros(max(n, 1), np.float64)
+    nb = np.zeros(max(n, 1), np.int32)
+    nvox = ctypes.c_int64()
+    k = lib().shplo_mv3d_voxels(n, _p(pts), stride, _p(img2), _p(_c(ranges, np.float64)), float(res),
+                                float(zres), int(cap), _p(img), img.shape[1], _p(bv), _p(mv), _p(nb),
+                                ctypes.byref(nvox))
+    return np.ascontiguousarray(img[:, :k]), bv[:k].copy(), mv[:k].copy(), nb[:nvox.value].copy()
 
 
 # ---- TF op restatements ----------------------------------------------------

@@ -26,13 +26,13 @@
 // the words; the first word of each key run is the cell's point and the run
 // length its count. Outputs keep the reference's order: slice-major, then
 // (x, z) ascending, exactly np.vstack(voxel_indices_stack).
-#include "shpl_common.h"
+#include "shpl_tilesort.h"
 
 namespace shpl {
 namespace {
 
-constexpr int BEV_BLOCK = 1024;
-constexpr int BEV_TILES = 16384;
+constexpr int BEV_BLOCK = TS_BLOCK;
+constexpr int BEV_TILES = TS_TILES;
 constexpr int BEV_MAX_SLICES = 8;
 constexpr int KEY_SHIFT = 42;  // [63:42] key, [41:32] discrete y - y0, [31:0] point index in frame
 
@@ -95,8 +95,7 @@ __global__ __launch_bounds__(BEV_BLOCK) void k_bev_frame(BevGeom g, const int64_
                                                          int64_t ent_per_point, int32_t *vox_out, double *pts_out,
                                                          int64_t *frame_nvox, double *hmaps, double *dmap,
                                                          uint32_t *err) {
-    __shared__ int32_t cnt[BEV_TILES];
-    __shared__ int32_t wsum[BEV_BLOCK / 64];
+    __shared__ TileSortLds lds;
     const int f = blockIdx.x;
     const int64_t p0 = pt_off[f], p1 = pt_off[f + 1];
     const int64_t t0 = p0 * ent_per_point;  // this frame's entry slots
@@ -104,62 +103,15 @@ __global__ __launch_bounds__(BEV_BLOCK) void k_bev_frame(BevGeom g, const int64_
     const int64_t n_cells = (int64_t)g.nx * g.nz;
     const int64_t n_keys = n_cells * (g.num_slices + 1);
     const int n_tiles = (int)(((n_keys - 1) >> g.log_tile) + 1);
-    for (int t = threadIdx.x; t < BEV_TILES; t += BEV_BLOCK) cnt[t] = 0;
-    __syncthreads();
-    // 1. tile histogram of all (point, slice) entries
-    for (int64_t i = p0 + threadIdx.x; i < p1; i += BEV_BLOCK)
-        point_entries<PT>(g, plane, pts, i, (uint32_t)(i - p0), n_cells,
-                          [&](uint64_t w) { atomicAdd(&cnt[(int)((w >> KEY_SHIFT) >> g.log_tile)], 1); });
-    __syncthreads();
-    // 2. exclusive scan of the tile counts
-    {
-        constexpr int PER = BEV_TILES / BEV_BLOCK;
-        int32_t v[PER];
-        int32_t sum = 0;
-#pragma unroll
-        for (int q = 0; q < PER; ++q) {
-            v[q] = cnt[threadIdx.x * PER + q];
-            sum += v[q];
-        }
-        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-        int32_t x = sum;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) wsum[wid] = x;
-        __syncthreads();
-        int32_t run = x - sum;
-        for (int w = 0; w < wid; ++w) run += wsum[w];
-#pragma unroll
-        for (int q = 0; q < PER; ++q) {
-            cnt[threadIdx.x * PER + q] = run;
-            run += v[q];
-        }
-    }
-    __syncthreads();
-    // 3. placement
-    for (int64_t i = p0 + threadIdx.x; i < p1; i += BEV_BLOCK)
-        point_entries<PT>(g, plane, pts, i, (uint32_t)(i - p0), n_cells, [&](uint64_t w) {
-            tmp[t0 + atomicAdd(&cnt[(int)((w >> KEY_SHIFT) >> g.log_tile)], 1)] = w;
-        });
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    __syncthreads();
-    const int32_t n_ent = cnt[n_tiles - 1];
-    // 4. in-tile rank: the packed word's numeric order is (key, discrete y, point index)
-    for (int32_t s = threadIdx.x; s < n_ent; s += BEV_BLOCK) {
-        const uint64_t me = tmp[t0 + s];
-        const int t = (int)((me >> KEY_SHIFT) >> g.log_tile);
-        const int32_t a = t ? cnt[t - 1] : 0, b = cnt[t];
-        int32_t rank = 0;
-        for (int32_t u = a; u < b; ++u) rank += tmp[t0 + u] < me ? 1 : 0;
-        srt[t0 + a + rank] = me;
-    }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    __syncthreads();
+    // 1-4. sort all (point, slice) words: numeric order = (key, discrete y, point index)
+    const int32_t n_ent = tile_sort(
+        lds, n_tiles, tmp + t0, srt + t0,
+        [&](auto &&emit) {
+            for (int64_t i = p0 + threadIdx.x; i < p1; i += BEV_BLOCK)
+                point_entries<PT>(g, plane, pts, i, (uint32_t)(i - p0), n_cells, emit);
+        },
+        [&](uint64_t w) { return (int)((w >> KEY_SHIFT) >> g.log_tile); });
+    int32_t *wsum = lds.wsum;
     // 5. one output per key run, slice cells compacted in sorted order
     const double a = plane[0], b = plane[1], c = plane[2], d = plane[3];
     const double norm = sqrt(__dadd_rn(__dadd_rn(__dmul_rn(a, a), __dmul_rn(b, b)), __dmul_rn(c, c)));

@@ -29,3 +29,61 @@ def produce_sparse_pooling_input(img_index, im_size, bv_index, bv_size, M_val=No
 def sparse_pool(input, pooled_size):  # noqa: A002 (reference signature)
     """0 is the sparse matrix M, 1 the source feature map, 2 the pooling index."""
     return spu._sparse_pool_op(input[0], input[1], input[2], pooled_size)
+
+
+# MV3D voxel config (MV3D_TF_release/lib/utils/config_voxels.py:49-59, DETECT_OBJ != 'Car')
+# and the ranges construct_voxel.py:11-13 derives from it.
+PED_RANGES = (0.0, 48 - 0.01, -20.0, 20 - 0.01, -1.0, 3 - 0.01)   # fwd, side, height
+CAR_RANGES = (0.0, 70.4 - 0.01, -40.0, 40 - 0.01, -1.0, 3 - 0.01)
+
+
+def mv3d_voxels_batch(points, point_offsets, img_index2=None, P=None, ranges=PED_RANGES, res=0.2, zres=0.4,
+                      voxel_point_count=45, number_buffer=False):
+    """The SHPL outputs of point_cloud_2_top_sparse (construct_voxel.py:37-162)
+    for a batch of frames on the device. points [N, >=3] f64 camera frame;
+    img_index2 [2, N] i64 (or P [F,3,4] f64 to project on the device).
+    Returns dict(img_index [3,N] f64, bv_index [N,2] i64, M_val [N] f64,
+    frame_n [F]; number_buffer [N] i32 + frame_nvox [F]), capacity layout."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    from . import _lib as L
+    dev = points.device
+    F = int(point_offsets.numel()) - 1
+    N = int(points.shape[0])
+    cap = max(N, 1)
+    img = torch.empty((3, cap), dtype=torch.float64, device=dev)
+    bv = torch.empty((cap, 2), dtype=torch.int64, device=dev)
+    mv = torch.empty(cap, dtype=torch.float64, device=dev)
+    fn = torch.empty(F, dtype=torch.int64, device=dev)
+    nb = torch.empty(cap, dtype=torch.int32, device=dev) if number_buffer else None
+    nvox = torch.empty(F, dtype=torch.int64, device=dev) if number_buffer else None
+    nbytes = ctypes.c_size_t()
+    L.check(L.lib().shpl_mv3d_workspace_bytes(N, ctypes.byref(nbytes)), "shpl_mv3d_workspace_bytes")
+    ws = L.workspace(nbytes.value, dev)
+    rng = np.ascontiguousarray(ranges, dtype=np.float64)
+    L.check(L.lib().shpl_mv3d_voxels(F, L.ptr(point_offsets), N, L.ptr(points), int(points.stride(0)),
+                                     L.ptr(img_index2), L.ptr(P), rng.ctypes.data_as(ctypes.c_void_p), float(res),
+                                     float(zres), int(voxel_point_count), L.ptr(img), cap, L.ptr(bv), L.ptr(mv),
+                                     L.ptr(fn), L.ptr(nb), L.ptr(nvox), L.ptr(ws), ws.numel(),
+                                     L.stream_of(dev)), "shpl_mv3d_voxels")
+    return {"img_index": img, "bv_index": bv, "M_val": mv, "frame_n": fn, "number_buffer": nb,
+            "frame_nvox": nvox}
+
+
+def mv3d_sparse_pooling_input(points, img_index2=None, P=None, ranges=PED_RANGES, res=0.2, zres=0.4,
+                              voxel_point_count=45):
+    """One frame: (img_index [3,n'], bv_index [n',2], M_val [n']) as
+    point_cloud_2_top_sparse returns them (construct_voxel.py:156-162)."""
+    import numpy as np
+    import torch
+    dev = torch.device("cuda", torch.cuda.current_device())
+    pts = torch.as_tensor(np.ascontiguousarray(points, dtype=np.float64)).to(dev)
+    off = torch.tensor([0, pts.shape[0]], dtype=torch.int64, device=dev)
+    i2 = None if img_index2 is None else torch.as_tensor(np.ascontiguousarray(img_index2, dtype=np.int64)).to(dev)
+    Pd = None if P is None else torch.as_tensor(np.asarray(P, dtype=np.float64).reshape(1, 12)).to(dev)
+    out = mv3d_voxels_batch(pts, off, i2, Pd, ranges, res, zres, voxel_point_count)
+    k = int(out["frame_n"][0].item())
+    return out["img_index"][:, :k], out["bv_index"][:k], out["M_val"][:k]

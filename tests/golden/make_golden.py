@@ -146,15 +146,20 @@ def _bev_slices_case():
     print(f"bev_slices: N={n} voxel_indices={vox.shape} maps={np.stack(maps['height_maps']).shape}")
 
 
-def _mv3d_voxel_case():
-    """MV3D point_cloud_2_top_sparse: img_index, bv_index and M_val = 1/count."""
+def _mv3d_voxel_case(dense=False):
+    """MV3D point_cloud_2_top_sparse: img_index, bv_index and M_val = 1/count.
+    dense: clustered points so that many voxels exceed VOXEL_POINT_COUNT (45)."""
     import importlib
     cv = importlib.import_module("utils.construct_voxel")
-    rng = np.random.default_rng(13)
+    rng = np.random.default_rng(13 + dense)
     n = 6000
-    # camera frame: x side, y height (down), z forward
-    pts = np.stack([rng.uniform(-19, 19, n), rng.uniform(-0.9, 2.9, n), rng.uniform(0.5, 47, n),
+    # camera frame: x side, y height (down), z forward; some points outside the ranges
+    pts = np.stack([rng.uniform(-21, 21, n), rng.uniform(-1.2, 3.2, n), rng.uniform(-0.5, 49, n),
                     rng.uniform(0, 1, n)], axis=1)
+    if dense:
+        centers = np.stack([rng.uniform(-15, 15, 40), rng.uniform(0, 2, 40), rng.uniform(5, 40, 40)], 1)
+        pick = rng.integers(0, 40, n)
+        pts[:, :3] = centers[pick] + rng.normal(0, 0.08, (n, 3))
     P = synth.KITTI_P2
     uvw = P @ np.vstack((pts[:, :3].T, np.ones(n)))
     img_index2 = np.round(uvw[:2] / uvw[2]).astype(int)
@@ -162,11 +167,13 @@ def _mv3d_voxel_case():
     calib[0] = P.reshape(-1)
     vd, full, img_index, bv_index, M_val = cv.point_cloud_2_top_sparse(
         pts.copy(), points_in_cam=True, calib=calib, img_index2=img_index2.copy())
-    np.savez_compressed(os.path.join(HERE, "mv3d_voxel.npz"), points=pts, img_index2=img_index2,
+    np.savez_compressed(os.path.join(HERE, "mv3d_voxel_dense.npz" if dense else "mv3d_voxel.npz"),
+                        points=pts, img_index2=img_index2,
                         voxel_full_size=np.asarray(full), img_index=img_index, bv_index=bv_index,
                         M_val=M_val, coordinate_buffer=vd["coordinate_buffer"],
                         number_buffer=vd["number_buffer"])
-    print(f"mv3d_voxel: N={n} kept={bv_index.shape[0]} voxels={vd['number_buffer'].shape[0]}")
+    print(f"mv3d_voxel(dense={dense}): N={n} kept={bv_index.shape[0]} voxels={vd['number_buffer'].shape[0]} "
+          f"capped={(vd['number_buffer'] >= 45).sum()}")
 
 
 def main():
@@ -196,6 +203,7 @@ def main():
         print("empty frame: reference raised", type(ex).__name__, ex)
     _bev_slices_case()
     _mv3d_voxel_case()
+    _mv3d_voxel_case(dense=True)
 
 
 if __name__ == "__main__":

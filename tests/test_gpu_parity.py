@@ -443,3 +443,51 @@ def test_points_to_fused_layer_pipeline():
                                        ref["img_index_flip_pool"], dual=True)
         _close_and_exact(out[f:f + 1], eb)
         _close_and_exact(iout[f:f + 1], ei)
+
+
+# ---------------------------------------------------------------- MV3D producer
+
+@pytest.mark.parametrize("name", ["mv3d_voxel.npz", "mv3d_voxel_dense.npz"])
+def test_mv3d_producer_vs_reference_golden(name):
+    from sparse_pooling_amd import mv3d
+    g = np.load(os.path.join(GOLD, name))
+    img, bv, mv = mv3d.mv3d_sparse_pooling_input(g["points"], img_index2=g["img_index2"])
+    np.testing.assert_array_equal(_np(img), g["img_index"])
+    np.testing.assert_array_equal(_np(bv), g["bv_index"])
+    np.testing.assert_array_equal(_np(mv), g["M_val"])
+    # projecting on the device gives the same img_index2
+    img_p, _, _ = mv3d.mv3d_sparse_pooling_input(g["points"], P=synth.KITTI_P2)
+    np.testing.assert_array_equal(_np(img_p), g["img_index"])
+
+
+def test_mv3d_chain_to_pooling():
+    """MV3D: device producer -> produce_sparse_pooling_input(stride [8,2]) with
+    M_val = 1/count -> sparse_pool (network.py:243-246) vs the oracle chain,
+    on image-visible points (MV3D's minibatches are FOV-filtered) with
+    clustered voxels over the 45-point cap."""
+    from sparse_pooling_amd import mv3d
+    from sparse_pooling_amd.sparse_pool_utils import SparseTensor
+    fr = synth.make_frame(synth.FrameSpec(8000, (1280, 384), (200, 240)), seed=9)
+    rng = np.random.default_rng(9)
+    pts = np.concatenate([fr.points, rng.uniform(0, 1, (len(fr.points), 1))], axis=1)
+    pts[:3000, :3] = pts[rng.integers(0, 40, 3000), :3] + rng.normal(0, 0.05, (3000, 3))
+    uvw = synth.KITTI_P2 @ np.vstack((pts[:, :3].T, np.ones(len(pts))))
+    img2 = np.round(uvw[:2] / uvw[2]).astype(np.int64)
+    img2 = np.clip(img2, 0, [[1279], [383]])
+    img, bv, mv = mv3d.mv3d_sparse_pooling_input(pts, img_index2=img2)
+    e_img, e_bv, e_mv, _ = orc.mv3d_voxels(pts, img2, **orc.MV3D_PED)
+    np.testing.assert_array_equal(_np(img), e_img)
+    np.testing.assert_array_equal(_np(mv), e_mv)
+    assert (e_mv < 1).any()
+    Mij, M_val, M_size, flip = mv3d.produce_sparse_pooling_input(img.clone(), np.array([1280, 384]), bv, [200, 240],
+                                                                 M_val=mv, stride=[8, 2])
+    ref = orc.produce_sparse_pooling_input({"img_index": e_img.copy(), "bv_index": e_bv,
+                                            "img_size": np.array([1280, 384]), "bv_size": np.array([200, 240])},
+                                           M_val=e_mv, stride=(8, 2))
+    np.testing.assert_array_equal(_np(Mij), ref["Mij_pool"])
+    np.testing.assert_array_equal(_np(flip), ref["img_index_flip_pool"])
+    feat = synth.make_features((1, 48, 160, 8), 5)
+    out = mv3d.sparse_pool([SparseTensor(Mij, M_val, M_size), torch.from_numpy(feat).to(DEV), flip],
+                           [1, 100, 120, 8])
+    e = orc.sparse_pool_op(ref["Mij_pool"], ref["M_val"], ref["M_size"], feat, ref["img_index_flip_pool"])
+    _close_and_exact(out, e.reshape(1, 100, 120, 8))

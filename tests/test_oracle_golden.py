@@ -151,3 +151,16 @@ def test_bev_slices_oracle_matches_reference(golden_dir):
     np.testing.assert_array_equal(upts, g["pts_in_voxel"])
     np.testing.assert_array_equal(hm, g["height_maps"])
     np.testing.assert_array_equal(dm, g["density_map"])
+
+
+@pytest.mark.parametrize("name", ["mv3d_voxel.npz", "mv3d_voxel_dense.npz"])
+def test_mv3d_oracle_matches_reference(golden_dir, name):
+    path = os.path.join(golden_dir, name)
+    if not os.path.exists(path):
+        pytest.skip("golden not generated")
+    g = np.load(path)
+    img, bv, mv, nb = orc.mv3d_voxels(g["points"], g["img_index2"], **orc.MV3D_PED)
+    np.testing.assert_array_equal(img, g["img_index"])
+    np.testing.assert_array_equal(bv, g["bv_index"])
+    np.testing.assert_array_equal(mv, g["M_val"])
+    np.testing.assert_array_equal(nb, g["number_buffer"])
