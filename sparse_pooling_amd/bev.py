@@ -59,6 +59,9 @@ def bev_slices_batch(points, point_offsets, planes, area_extents, voxel_size, he
     N = int(points.shape[0])
     if points.dtype != torch.float64:
         raise TypeError("BEV slicing runs on f64 camera-frame points, as the reference does")
+    points = points.contiguous()
+    point_offsets = point_offsets.to(torch.int64).contiguous()
+    planes = planes.to(torch.float64).contiguous()
     nx, nz = grid_divisions(area_extents, voxel_size)
     hpd, lo, hi = slice_bounds(float(height_lo), float(height_hi), int(num_slices))
     ext = np.ascontiguousarray(np.asarray(area_extents, dtype=np.float64).reshape(6))

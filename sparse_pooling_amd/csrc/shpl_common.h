@@ -64,6 +64,18 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 
+// Make this workgroup's global stores visible to its other waves: every wave
+// drains its vector-memory stores before the barrier (a workgroup-scope
+// __syncthreads does not wait for them on gfx950), then invalidates the
+// CU's L1 and waits for the invalidate before its next load
+// (MI355X_MICROARCH.md, inter-workgroup visibility: producer / consumer forms).
+__device__ __forceinline__ void block_publish() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 inline int grid_for(int64_t work, int64_t per_block, int cap) {
     int64_t g = (work + per_block - 1) / per_block;
     if (g < 1) g = 1;

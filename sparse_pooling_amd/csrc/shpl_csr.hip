@@ -150,10 +150,7 @@ __global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, uint64_t *tmp,
         if (k >= 0 && k < c.keys_per_frame)
             tmp[e0 + atomicAdd(&cnt[k >> c.log_tile], 1)] = ((uint64_t)(uint32_t)key << 32) | (uint32_t)e;
     }
-    __syncthreads();
-    // tmp was written by other waves of this workgroup through the vector memory path
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    __syncthreads();
+    block_publish();  // tmp was written by other waves of this workgroup through memory
     const int32_t n_valid = cnt[n_tiles - 1];
     // With identity columns every TF order collapses to entry order, so the
     // packed (destination, entry) word alone sorts the tile.

@@ -88,9 +88,7 @@ __global__ __launch_bounds__(TS_BLOCK) void k_mv3d_frame(Mv3dGeom g, const int64
         const int32_t a = run < g.cap ? run : g.cap;
         for (int32_t u = 0; u < a; ++u) acc[p0 + (uint32_t)srt[p0 + s + u]] = a;
     }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    __syncthreads();
+    block_publish();
     // optional VFE buffers: number_buffer per voxel in voxel order
     if (vox_count) {
         int64_t base = 0;

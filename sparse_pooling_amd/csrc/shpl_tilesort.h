@@ -53,15 +53,13 @@ __device__ __forceinline__ void ts_scan(TileSortLds &l) {
 template <typename Each, typename Tile>
 __device__ int32_t tile_sort(TileSortLds &l, int n_tiles, uint64_t *tmp, uint64_t *srt, Each &&each, Tile &&tile) {
     for (int t = threadIdx.x; t < TS_TILES; t += TS_BLOCK) l.cnt[t] = 0;
-    __syncthreads();
+    block_publish();  // the caller's earlier global stores (e.g. zeroed flags) land first
     each([&](uint64_t w) { atomicAdd(&l.cnt[tile(w)], 1); });
     __syncthreads();
     ts_scan(l);
     __syncthreads();
     each([&](uint64_t w) { tmp[atomicAdd(&l.cnt[tile(w)], 1)] = w; });
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // tmp came from other waves through memory
-    __syncthreads();
+    block_publish();  // tmp came from other waves through memory
     const int32_t n = l.cnt[n_tiles - 1];
     for (int32_t s = threadIdx.x; s < n; s += TS_BLOCK) {
         const uint64_t me = tmp[s];
@@ -71,9 +69,7 @@ __device__ int32_t tile_sort(TileSortLds &l, int n_tiles, uint64_t *tmp, uint64_
         for (int32_t u = a; u < b; ++u) rank += tmp[u] < me ? 1 : 0;
         srt[a + rank] = me;
     }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    __syncthreads();
+    block_publish();
     return n;
 }
 

@@ -51,6 +51,12 @@ def mv3d_voxels_batch(points, point_offsets, img_index2=None, P=None, ranges=PED
 
     from . import _lib as L
     dev = points.device
+    points = points.to(torch.float64).contiguous()
+    point_offsets = point_offsets.to(torch.int64).contiguous()
+    if img_index2 is not None:
+        img_index2 = img_index2.to(torch.int64).contiguous()
+    if P is not None:
+        P = P.to(torch.float64).contiguous()
     F = int(point_offsets.numel()) - 1
     N = int(points.shape[0])
     cap = max(N, 1)

@@ -56,6 +56,8 @@ class FusedPipeline:
 
     # ------------------------------------------------------------------ steps
     def build_index(self, points, voxels, point_offsets, P, mval=None, point_counts=None):
+        assert points.is_contiguous() and point_offsets.is_contiguous() and P.is_contiguous()
+        assert voxels.stride(1) == 1, "voxel rows must be contiguous"
         st = L.stream_of(self.dev)
         L.check(self._lib.shpl_build_index(
             self.B, L.ptr(point_offsets), L.ptr(point_counts), self.max_points, L.ptr(points),

@@ -292,6 +292,9 @@ def build_index_batch(points, voxels, point_offsets, P, im_size, bv_size, stride
     batch of frames in one pass (shpl_build_index). All inputs are device
     tensors; nothing synchronises the host."""
     dev = points.device
+    points, point_offsets, P = points.contiguous(), point_offsets.contiguous(), P.contiguous()
+    if voxels.stride(1) != 1:
+        voxels = voxels.contiguous()
     n_frames = int(point_offsets.numel()) - 1
     N = int(points.shape[0])
     s_img, s_bv = float(stride[0]), float(stride[1])
