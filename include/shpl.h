@@ -46,6 +46,7 @@ typedef enum {
 #define SHPL_EBIT_COL 2u     /* M column outside [0, M_size[1]) */
 #define SHPL_EBIT_PIXEL 4u   /* source index (b,v,u) outside the image */
 #define SHPL_EBIT_VALUES 8u  /* len(M_val) != nnz */
+#define SHPL_EBIT_CAPACITY 16u /* a frame holds more points than max_points_per_frame */
 
 typedef enum { SHPL_F32 = 0, SHPL_BF16 = 1, SHPL_F64 = 2 } shpl_dtype;
 typedef enum { SHPL_I32 = 0, SHPL_I64 = 1 } shpl_itype;
@@ -80,7 +81,10 @@ const char *shpl_status_string(int status);
 
 /* Fused, batched: points -> projection (f64, FMA chain as numpy/OpenBLAS) ->
  * image clip (strict bounds) -> round half-even -> strides -> BEV flatten ->
- * in-grid filter -> stable compaction, for n_frames frames in one pass.
+ * in-grid filter -> stable compaction, for n_frames frames in two launches
+ * (a per-chunk count, then the placement), each with one 1024-thread
+ * workgroup per 4096 points of every frame. max_points_per_frame bounds the
+ * capacity off[f+1]-off[f] of every frame (SHPL_EBIT_CAPACITY otherwise).
  * Replaces gen_sparse_pooling_input_avod + produce_sparse_pooling_input
  * (avod/avod/utils/sparse_pool_utils.py:6-58; projection/clip
  * avod/avod/utils/transform.py:3-40) as called per frame by

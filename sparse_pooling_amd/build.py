@@ -22,7 +22,7 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=o
 
 def _compile(src):
     obj = os.path.join(OBJ, os.path.basename(src).replace(".hip", ".o"))
-    deps = [src, os.path.join(CSRC, "shpl_common.h"),
+    deps = [src, *glob.glob(os.path.join(CSRC, "*.h")),
             os.path.join(os.path.dirname(HERE), "include", "shpl.h")]
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return obj

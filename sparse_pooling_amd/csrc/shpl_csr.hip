@@ -88,16 +88,43 @@ __device__ __forceinline__ uint64_t order_key(const CsrIn &c, int32_t e) {
     }
 }
 
+constexpr int CSR_BATCH = 8;     // entries per thread whose loads are in flight together
+constexpr int CSR_WIN = 10240;   // packed words staged in LDS for the rank fix-up (80 KiB)
+
+// Destinations of entries first + u*CSR_BLOCK (u < U), -1 for invalid or past e1.
+// All loads of the batch are issued before any is used.
+template <bool HAS_COL, int U>
+__device__ __forceinline__ void keys_batch(const CsrIn &c, int64_t first, int64_t e1, int32_t (&key)[U]) {
+    int32_t r[U], k[U], p[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t e = first + (int64_t)u * CSR_BLOCK;
+        const bool ok = e < e1;
+        r[u] = ok ? c.cell[e] : -1;
+        k[u] = ok ? (HAS_COL ? c.col[e] : (int32_t)e) : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) p[u] = k[u] >= 0 ? c.pix[k[u]] : -1;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        key[u] = (r[u] < 0 || k[u] < 0 || p[u] < 0) ? -1 : (c.direction == SHPL_BY_CELL ? r[u] : p[u]);
+}
+
 // One frame per workgroup:
 //  1. LDS histogram of the frame's entries over destination tiles
 //  2. exclusive scan of the tile counts (in place)
 //  3. placement into tile segments (LDS atomics: arbitrary order inside a tile)
 //  4. rank fix-up: each entry counts the tile entries that precede it in
 //     (destination, TF order, entry) and moves to that rank -> stable, sorted.
+//     With identity columns (or ORDER_ENTRY) the packed word alone orders a
+//     tile; the words are then staged in LDS windows so that the quadratic
+//     count reads LDS, not HBM.
+template <bool HAS_COL>
 __global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, uint64_t *tmp, int64_t nnz_cap, int32_t *ent_dst,
                                                          int32_t *ent_src, float *ent_val, int32_t *ent_col) {
     __shared__ int32_t cnt[CSR_TILES];
     __shared__ int32_t wsum[CSR_BLOCK / 64];
+    __shared__ uint64_t win[CSR_WIN];
     const int f = blockIdx.x;
     const int64_t e0 = c.frame_off[f];
     const int64_t cap_end = c.frame_off[f + 1];
@@ -111,9 +138,14 @@ __global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, uint64_t *tmp,
     for (int t = threadIdx.x; t < CSR_TILES; t += CSR_BLOCK) cnt[t] = 0;
     __syncthreads();
     // 1. histogram
-    for (int64_t e = e0 + threadIdx.x; e < e1; e += CSR_BLOCK) {
-        const int64_t k = (int64_t)key_of(c, e) - kbase;
-        if (k >= 0 && k < c.keys_per_frame) atomicAdd(&cnt[k >> c.log_tile], 1);
+    for (int64_t b = e0 + threadIdx.x; b < e1; b += (int64_t)CSR_BLOCK * CSR_BATCH) {
+        int32_t key[CSR_BATCH];
+        keys_batch<HAS_COL>(c, b, e1, key);
+#pragma unroll
+        for (int u = 0; u < CSR_BATCH; ++u) {
+            const int64_t k = (int64_t)key[u] - kbase;
+            if (key[u] >= 0 && k >= 0 && k < c.keys_per_frame) atomicAdd(&cnt[k >> c.log_tile], 1);
+        }
     }
     __syncthreads();
     // 2. exclusive scan: thread j owns tiles [j*16, j*16+16)
@@ -144,48 +176,98 @@ __global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, uint64_t *tmp,
     }
     __syncthreads();
     // 3. placement of (destination << 32 | entry): cnt[t] advances from start(t) to end(t) = start(t+1)
-    for (int64_t e = e0 + threadIdx.x; e < e1; e += CSR_BLOCK) {
-        const int32_t key = key_of(c, e);
-        const int64_t k = (int64_t)key - kbase;
-        if (k >= 0 && k < c.keys_per_frame)
-            tmp[e0 + atomicAdd(&cnt[k >> c.log_tile], 1)] = ((uint64_t)(uint32_t)key << 32) | (uint32_t)e;
+    for (int64_t b = e0 + threadIdx.x; b < e1; b += (int64_t)CSR_BLOCK * CSR_BATCH) {
+        int32_t key[CSR_BATCH];
+        keys_batch<HAS_COL>(c, b, e1, key);
+#pragma unroll
+        for (int u = 0; u < CSR_BATCH; ++u) {
+            const int64_t k = (int64_t)key[u] - kbase;
+            const int64_t e = b + (int64_t)u * CSR_BLOCK;
+            if (key[u] >= 0 && k >= 0 && k < c.keys_per_frame)
+                tmp[e0 + atomicAdd(&cnt[k >> c.log_tile], 1)] = ((uint64_t)(uint32_t)key[u] << 32) | (uint32_t)e;
+        }
     }
     block_publish();  // tmp was written by other waves of this workgroup through memory
     const int32_t n_valid = cnt[n_tiles - 1];
     // With identity columns every TF order collapses to entry order, so the
     // packed (destination, entry) word alone sorts the tile.
-    const bool entry_order = c.order == SHPL_ORDER_ENTRY || !c.col;
+    const bool entry_order = c.order == SHPL_ORDER_ENTRY || !HAS_COL;
     // 4. rank fix-up
-    for (int32_t s = threadIdx.x; s < n_valid; s += CSR_BLOCK) {
-        const uint64_t me = tmp[e0 + s];
-        const int32_t key = (int32_t)(me >> 32);
-        const int32_t e = (int32_t)(uint32_t)me;
-        const int t = (int)((key - kbase) >> c.log_tile);
-        const int32_t a = t ? cnt[t - 1] : 0, b = cnt[t];
-        int32_t rank = 0;
-        if (b - a > 1) {
-            if (entry_order) {
-                for (int32_t u = a; u < b; ++u) rank += tmp[e0 + u] < me ? 1 : 0;
-            } else {
-                const uint64_t ke = order_key(c, e);
-                for (int32_t u = a; u < b; ++u) {
-                    const uint64_t ot = tmp[e0 + u];
-                    const int32_t ko = (int32_t)(ot >> 32), o = (int32_t)(uint32_t)ot;
-                    bool before = ko < key;
-                    if (ko == key && o != e) {
-                        const uint64_t oo = order_key(c, o);
-                        before = oo < ke || (oo == ke && o < e);
+    if (entry_order) {
+        for (int32_t w0 = 0; w0 < n_valid; w0 += CSR_WIN) {
+            const int32_t w1 = w0 + CSR_WIN < n_valid ? w0 + CSR_WIN : n_valid;
+            for (int32_t s = w0 + threadIdx.x; s < w1; s += CSR_BLOCK) win[s - w0] = tmp[e0 + s];
+            __syncthreads();
+            for (int32_t s0 = w0 + threadIdx.x; s0 < w1; s0 += CSR_BLOCK * CSR_BATCH) {
+                int32_t d[CSR_BATCH], ee[CSR_BATCH], kk[CSR_BATCH], key[CSR_BATCH];
+#pragma unroll
+                for (int u = 0; u < CSR_BATCH; ++u) {
+                    const int32_t s = s0 + u * CSR_BLOCK;
+                    d[u] = -1;
+                    if (s >= w1) continue;
+                    const uint64_t me = win[s - w0];
+                    key[u] = (int32_t)(me >> 32);
+                    ee[u] = (int32_t)(uint32_t)me;
+                    const int t = (int)((key[u] - kbase) >> c.log_tile);
+                    const int32_t a = t ? cnt[t - 1] : 0, b = cnt[t];
+                    int32_t rank = 0;
+                    if (b - a > 1) {
+                        if (a >= w0 && b <= w1) {
+                            for (int32_t x = a; x < b; ++x) rank += win[x - w0] < me ? 1 : 0;
+                        } else {  // tile straddles the window edge
+                            for (int32_t x = a; x < b; ++x) rank += tmp[e0 + x] < me ? 1 : 0;
+                        }
                     }
-                    rank += before ? 1 : 0;
+                    d[u] = a + rank;
+                }
+#pragma unroll
+                for (int u = 0; u < CSR_BATCH; ++u) kk[u] = d[u] >= 0 ? (HAS_COL ? c.col[ee[u]] : ee[u]) : 0;
+                int32_t src[CSR_BATCH];
+                float val[CSR_BATCH];
+#pragma unroll
+                for (int u = 0; u < CSR_BATCH; ++u) {
+                    if (d[u] < 0) continue;
+                    src[u] = c.direction == SHPL_BY_CELL ? c.pix[kk[u]] : c.cell[ee[u]];
+                    val[u] = c.val[ee[u]];
+                }
+#pragma unroll
+                for (int u = 0; u < CSR_BATCH; ++u) {
+                    if (d[u] < 0) continue;
+                    const int64_t o = e0 + d[u];
+                    ent_dst[o] = key[u];
+                    ent_src[o] = src[u];
+                    ent_val[o] = val[u];
+                    if (ent_col) ent_col[o] = kk[u];
                 }
             }
+            __syncthreads();  // the next window overwrites win
         }
-        const int64_t d = e0 + a + rank;
-        const int32_t k = col_of(c, e);
-        ent_dst[d] = key;
-        ent_src[d] = c.direction == SHPL_BY_CELL ? c.pix[k] : c.cell[e];
-        ent_val[d] = c.val[e];
-        if (ent_col) ent_col[d] = k;
+    } else {
+        for (int32_t s = threadIdx.x; s < n_valid; s += CSR_BLOCK) {
+            const uint64_t me = tmp[e0 + s];
+            const int32_t key = (int32_t)(me >> 32);
+            const int32_t e = (int32_t)(uint32_t)me;
+            const int t = (int)((key - kbase) >> c.log_tile);
+            const int32_t a = t ? cnt[t - 1] : 0, b = cnt[t];
+            int32_t rank = 0;
+            const uint64_t ke = order_key(c, e);
+            for (int32_t u = a; u < b; ++u) {
+                const uint64_t ot = tmp[e0 + u];
+                const int32_t ko = (int32_t)(ot >> 32), o = (int32_t)(uint32_t)ot;
+                bool before = ko < key;
+                if (ko == key && o != e) {
+                    const uint64_t oo = order_key(c, o);
+                    before = oo < ke || (oo == ke && o < e);
+                }
+                rank += before ? 1 : 0;
+            }
+            const int64_t d = e0 + a + rank;
+            const int32_t k = col_of(c, e);
+            ent_dst[d] = key;
+            ent_src[d] = c.direction == SHPL_BY_CELL ? c.pix[k] : c.cell[e];
+            ent_val[d] = c.val[e];
+            if (ent_col) ent_col[d] = k;
+        }
     }
     // empty slots of this frame's capacity, and past the last frame
     int64_t hole_end = cap_end;
@@ -253,8 +335,12 @@ extern "C" int shpl_build_csr(int direction, int order, int n_frames, const int6
     int log_tile = 0;
     while (((keys_per_frame - 1) >> log_tile) + 1 > CSR_TILES) ++log_tile;
     CsrIn c{direction, order, n_frames, d_frame_off, d_frame_nnz, keys_per_frame, log_tile, d_cell, d_col, d_pix, d_val};
-    hipLaunchKernelGGL(k_csr_frame, dim3(n_frames), dim3(CSR_BLOCK), 0, (hipStream_t)stream, c, (uint64_t *)d_ws,
-                       nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_val, csr->ent_col);
+    if (d_col)
+        hipLaunchKernelGGL(k_csr_frame<true>, dim3(n_frames), dim3(CSR_BLOCK), 0, (hipStream_t)stream, c,
+                           (uint64_t *)d_ws, nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_val, csr->ent_col);
+    else
+        hipLaunchKernelGGL(k_csr_frame<false>, dim3(n_frames), dim3(CSR_BLOCK), 0, (hipStream_t)stream, c,
+                           (uint64_t *)d_ws, nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_val, csr->ent_col);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
 }

@@ -124,15 +124,23 @@ struct FusedStage {
     struct Payload {
         Produced pr;
     };
+    struct In {
+        double x, y, z;
+        int64_t vx, vz;
+    };
 
-    __device__ bool eval(int f, int64_t i, Payload &pl) const {
-        double x, y, z, u, v;
-        load_point<PT>(pts, i, x, y, z);
-        project(P + 12 * f, x, y, z, u, v);
+    __device__ void load(int64_t i, In &in) const {
+        load_point<PT>(pts, i, in.x, in.y, in.z);
+        in.vx = load_idx<VT>(vox, i * vstride);
+        in.vz = load_idx<VT>(vox, i * vstride + 1);
+    }
+    __device__ bool eval(int f, int64_t, const In &in, Payload &pl) const {
+        double u, v;
+        project(P + 12 * f, in.x, in.y, in.z, u, v);
         if (!in_image(u, v, g.im_w, g.im_h)) return false;
         const double ur = (double)(int64_t)rint(u);
         const double vr = (double)(int64_t)rint(v);
-        pl.pr = produce(g, ur, vr, load_idx<VT>(vox, i * vstride), load_idx<VT>(vox, i * vstride + 1));
+        pl.pr = produce(g, ur, vr, in.vx, in.vz);
         return pl.pr.inside;
     }
     __device__ void touch(int, int64_t, const Payload &, bool) const {}
@@ -176,11 +184,13 @@ struct GenStage {  // gen_sparse_pooling_input_avod
     struct Payload {
         double u, v;
     };
-
-    __device__ bool eval(int f, int64_t i, Payload &pl) const {
+    struct In {
         double x, y, z;
-        load_point<PT>(pts, i, x, y, z);
-        project(P + 12 * f, x, y, z, pl.u, pl.v);
+    };
+
+    __device__ void load(int64_t i, In &in) const { load_point<PT>(pts, i, in.x, in.y, in.z); }
+    __device__ bool eval(int f, int64_t, const In &in, Payload &pl) const {
+        project(P + 12 * f, in.x, in.y, in.z, pl.u, pl.v);
         return in_image(pl.u, pl.v, im_w, im_h);
     }
     __device__ void touch(int, int64_t, const Payload &, bool) const {}
@@ -209,11 +219,21 @@ struct ProduceStage {  // produce_sparse_pooling_input (in-place img_index updat
         Produced pr;
         double w;  // third row
     };
+    struct In {
+        double u, v, w;
+        int64_t vx, vz;
+    };
 
-    __device__ bool eval(int, int64_t i, Payload &pl) const {
-        pl.pr = produce(g, img[i], img[ld + i], load_idx<VT>(bv, i * bstride),
-                        load_idx<VT>(bv, i * bstride + 1));
-        pl.w = img[2 * ld + i];
+    __device__ void load(int64_t i, In &in) const {
+        in.u = img[i];
+        in.v = img[ld + i];
+        in.w = img[2 * ld + i];
+        in.vx = load_idx<VT>(bv, i * bstride);
+        in.vz = load_idx<VT>(bv, i * bstride + 1);
+    }
+    __device__ bool eval(int, int64_t, const In &in, Payload &pl) const {
+        pl.pr = produce(g, in.u, in.v, in.vx, in.vz);
+        pl.w = in.w;
         return pl.pr.inside;
     }
     // img_index[0:2] = floor(img_index/stride), clamped -- for EVERY point
@@ -243,52 +263,146 @@ struct ProduceStage {  // produce_sparse_pooling_input (in-place img_index updat
 
 // ------------------------------------------------- per-frame stable compaction
 
-template <typename Stage>
-__global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, const int64_t *pt_off, const int64_t *pt_count,
-                                                       int64_t *frame_nnz, int64_t *frame_out_off, int n_frames) {
-    __shared__ int32_t wsum[IDX_BLOCK / 64];
-    const int f = blockIdx.x;
-    const int64_t p0 = pt_off[f], cap_end = pt_off[f + 1];
+constexpr int IDX_BATCH = 4;                      // point rows per thread whose loads are in flight together
+constexpr int IDX_CHUNK = IDX_BLOCK * IDX_BATCH;  // points per workgroup: one round
+
+struct Frames {
+    const int64_t *pt_off, *pt_count;
+    int n_frames, n_chunks;  // chunks of IDX_CHUNK points per frame (grid.x)
+    int32_t *chunk_kept;     // [n_frames][n_chunks] workspace
+    int64_t *frame_nnz, *frame_out_off;
+    uint32_t *err;
+};
+
+__device__ __forceinline__ void frame_range(const Frames &fr, int f, int64_t &p0, int64_t &p1, int64_t &cap_end) {
+    p0 = fr.pt_off[f];
+    cap_end = fr.pt_off[f + 1];
     // live points of the frame: [p0, p0 + count) when counts are given (capacity layout input)
-    const int64_t p1 = pt_count ? (p0 + pt_count[f] < cap_end ? p0 + pt_count[f] : cap_end) : cap_end;
-    const int wid = threadIdx.x >> 6;
-    int64_t kept = 0;
-    for (int64_t base = p0; base < p1; base += IDX_BLOCK) {
-        const int64_t i = base + threadIdx.x;
-        bool keep = false;
+    p1 = fr.pt_count ? (p0 + fr.pt_count[f] < cap_end ? p0 + fr.pt_count[f] : cap_end) : cap_end;
+}
+
+// Pass 1 (grid n_chunks x n_frames): kept points per chunk.
+template <typename Stage>
+__global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr) {
+    __shared__ int32_t wsum[IDX_BLOCK / 64];
+    const int f = blockIdx.y, j = blockIdx.x;
+    int64_t p0, p1, cap_end;
+    frame_range(fr, f, p0, p1, cap_end);
+    const int64_t base = p0 + (int64_t)j * IDX_CHUNK;
+    if (j == fr.n_chunks - 1 && p1 > base + IDX_CHUNK && threadIdx.x == 0 && fr.err)
+        atomicOr(fr.err, SHPL_EBIT_CAPACITY);  // frame larger than max_points_per_frame
+    typename Stage::In in[IDX_BATCH];
+#pragma unroll
+    for (int u = 0; u < IDX_BATCH; ++u) {
+        const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
+        if (i < p1) st.load(i, in[u]);
+    }
+    int32_t n = 0;
+#pragma unroll
+    for (int u = 0; u < IDX_BATCH; ++u) {
+        const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
         typename Stage::Payload pl;
+        if (i < p1 && st.eval(f, i, in[u], pl)) ++n;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = n;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t t = 0;
+        for (int w = 0; w < IDX_BLOCK / 64; ++w) t += wsum[w];
+        fr.chunk_kept[(int64_t)f * fr.n_chunks + j] = t;
+    }
+}
+
+// Pass 2 (same grid): the chunk's kept points land after those of the
+// frame's earlier chunks, in point order (a stable compaction); rows of the
+// chunk are ranked in order by wave ballots + an LDS prefix. The frame's
+// last chunk also writes the sentinels of the unused capacity and the
+// frame's entry count.
+template <typename Stage>
+__global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr) {
+    __shared__ int32_t wsum[IDX_BATCH][IDX_BLOCK / 64];
+    __shared__ int32_t pre[IDX_BLOCK / 64];
+    const int f = blockIdx.y, j = blockIdx.x;
+    int64_t p0, p1, cap_end;
+    frame_range(fr, f, p0, p1, cap_end);
+    const int wid = threadIdx.x >> 6;
+    // kept points of the earlier chunks
+    int32_t mine = 0;
+    for (int q = threadIdx.x; q < j; q += IDX_BLOCK) mine += fr.chunk_kept[(int64_t)f * fr.n_chunks + q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+    if ((threadIdx.x & 63) == 0) pre[wid] = mine;
+    const int64_t base = p0 + (int64_t)j * IDX_CHUNK;
+    typename Stage::In in[IDX_BATCH];
+    typename Stage::Payload pl[IDX_BATCH];
+    bool keep[IDX_BATCH];
+#pragma unroll
+    for (int u = 0; u < IDX_BATCH; ++u) {
+        const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
+        if (i < p1) st.load(i, in[u]);
+    }
+    uint64_t m[IDX_BATCH];
+#pragma unroll
+    for (int u = 0; u < IDX_BATCH; ++u) {
+        const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
+        keep[u] = false;
         if (i < p1) {
-            keep = st.eval(f, i, pl);
-            st.touch(f, i, pl, keep);
+            keep[u] = st.eval(f, i, in[u], pl[u]);
+            st.touch(f, i, pl[u], keep[u]);
         }
-        const uint64_t m = __ballot(keep);
-        if ((threadIdx.x & 63) == 0) wsum[wid] = (int32_t)__popcll(m);
-        __syncthreads();
+        m[u] = __ballot(keep[u]);
+        if ((threadIdx.x & 63) == 0) wsum[u][wid] = (int32_t)__popcll(m[u]);
+    }
+    __syncthreads();
+    int64_t kept = 0;
+    for (int w = 0; w < IDX_BLOCK / 64; ++w) kept += pre[w];
+#pragma unroll
+    for (int u = 0; u < IDX_BATCH; ++u) {
         int32_t before = 0, tot = 0;
         for (int w = 0; w < IDX_BLOCK / 64; ++w) {
-            const int32_t c = wsum[w];
+            const int32_t c = wsum[u][w];
             before += w < wid ? c : 0;
             tot += c;
         }
-        if (keep) st.emit(f, i, p0 + kept + before + lane_rank(m), p0, pl);
+        const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
+        if (keep[u]) st.emit(f, i, p0 + kept + before + lane_rank(m[u]), p0, pl[u]);
         kept += tot;
-        __syncthreads();  // wsum is rewritten by the next chunk
     }
+    if (j != fr.n_chunks - 1) return;
     for (int64_t pos = p0 + kept + threadIdx.x; pos < cap_end; pos += IDX_BLOCK) st.hole(pos);
     if (threadIdx.x == 0) {
-        if (frame_nnz) frame_nnz[f] = kept;
-        if (frame_out_off) {
-            frame_out_off[f] = p0;
-            if (f == n_frames - 1) frame_out_off[n_frames] = cap_end;
+        if (fr.frame_nnz) fr.frame_nnz[f] = kept;
+        if (fr.frame_out_off) {
+            fr.frame_out_off[f] = p0;
+            if (f == fr.n_frames - 1) fr.frame_out_off[fr.n_frames] = cap_end;
         }
     }
 }
 
+int n_chunks_for(int64_t max_points) {
+    const int64_t c = (max_points + IDX_CHUNK - 1) / IDX_CHUNK;
+    return (int)(c < 1 ? 1 : c);
+}
+
+constexpr size_t IDX_WS_HEAD = 256;  // single-frame [0, n] offsets
+
+size_t index_ws_bytes(int n_frames, int64_t max_points) {
+    return IDX_WS_HEAD + align_up(sizeof(int32_t) * (size_t)n_frames * (size_t)n_chunks_for(max_points), 256);
+}
+
 template <typename Stage>
-int run_compaction(const Stage &st, int n_frames, const int64_t *pt_off, const int64_t *pt_count,
-                   int64_t *frame_nnz, int64_t *frame_out_off, hipStream_t stream) {
-    hipLaunchKernelGGL(k_compact<Stage>, dim3(n_frames), dim3(IDX_BLOCK), 0, stream, st, pt_off, pt_count, frame_nnz,
-                       frame_out_off, n_frames);
+int run_compaction(const Stage &st, int n_frames, int64_t max_points, const int64_t *pt_off,
+                   const int64_t *pt_count, int64_t *frame_nnz, int64_t *frame_out_off, uint32_t *err, void *ws,
+                   size_t ws_bytes, hipStream_t stream) {
+    if (ws_bytes < index_ws_bytes(n_frames, max_points)) return SHPL_ERR_WORKSPACE;
+    Frames fr{pt_off, pt_count, n_frames, n_chunks_for(max_points),
+              (int32_t *)((char *)ws + IDX_WS_HEAD), frame_nnz, frame_out_off, err};
+    const dim3 grid(fr.n_chunks, n_frames);
+    hipLaunchKernelGGL(k_count<Stage>, grid, dim3(IDX_BLOCK), 0, stream, st, fr);
+    SHPL_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_compact<Stage>, grid, dim3(IDX_BLOCK), 0, stream, st, fr);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
 }
@@ -305,7 +419,7 @@ using namespace shpl;
 
 extern "C" int shpl_build_index_workspace_bytes(int n_frames, int64_t max_points_per_frame, size_t *bytes) {
     if (!bytes || n_frames < 1 || max_points_per_frame < 0) return SHPL_ERR_ARG;
-    *bytes = 256;  // the single-frame calls keep a device [0, n] offset pair here
+    *bytes = index_ws_bytes(n_frames, max_points_per_frame);  // [0, n] pair of the single-frame calls + chunk counts
     return SHPL_OK;
 }
 
@@ -330,7 +444,8 @@ extern "C" int shpl_build_index(int n_frames, const int64_t *d_point_offsets, co
     {                                                                                            \
         FusedStage<PT, VT> st{d_points, d_voxels, vox_stride, d_P, g, d_mval, d_cell, d_pix,     \
                               d_val, d_mij, d_flip, d_err};                                      \
-        return run_compaction(st, n_frames, d_point_offsets, d_point_counts, d_frame_nnz, d_frame_out_off, s); \
+        return run_compaction(st, n_frames, max_points_per_frame, d_point_offsets, d_point_counts, d_frame_nnz, \
+                              d_frame_out_off, d_err, d_ws, ws_bytes, s);                        \
     }
     if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I64) SHPL_FUSED(double, int64_t)
     if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I32) SHPL_FUSED(double, int32_t)
@@ -366,7 +481,7 @@ extern "C" int shpl_gen_index(int64_t n, const void *d_points, int points_dtype,
     {                                                                                             \
         GenStage<PT, VT> st{d_points, d_voxels, vox_stride, d_P, im_w, im_h, d_bv_index,          \
                             d_img_index, ld};                                                     \
-        return run_compaction(st, 1, off, nullptr, d_nv, nullptr, s);                            \
+        return run_compaction(st, 1, n, off, nullptr, d_nv, nullptr, nullptr, d_ws, ws_bytes, s);   \
     }
     if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I64) SHPL_GEN(double, int64_t)
     if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I32) SHPL_GEN(double, int32_t)
@@ -391,11 +506,11 @@ extern "C" int shpl_produce_index(int64_t nv, const void *d_bv_index, int bv_ity
     if (rc) return rc;
     if (bv_itype == SHPL_I64) {
         ProduceStage<int64_t> st{d_bv_index, bv_stride, d_img_index, ld, g, d_mij, d_flip, d_cell, d_pix, d_err};
-        return run_compaction(st, 1, off, nullptr, d_nk, nullptr, s);
+        return run_compaction(st, 1, nv, off, nullptr, d_nk, nullptr, d_err, d_ws, ws_bytes, s);
     }
     if (bv_itype == SHPL_I32) {
         ProduceStage<int32_t> st{d_bv_index, bv_stride, d_img_index, ld, g, d_mij, d_flip, d_cell, d_pix, d_err};
-        return run_compaction(st, 1, off, nullptr, d_nk, nullptr, s);
+        return run_compaction(st, 1, nv, off, nullptr, d_nk, nullptr, d_err, d_ws, ws_bytes, s);
     }
     return SHPL_ERR_ARG;
 }

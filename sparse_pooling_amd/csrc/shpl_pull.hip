@@ -159,6 +159,14 @@ __device__ __forceinline__ void fma_free_accumulate(float (&acc)[VEC], float w, 
     for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(acc[j], __fmul_rn(w, x[j]));
 }
 
+#ifndef SHPL_WALK
+#define SHPL_WALK 2
+#endif
+#ifndef SHPL_WALK_PRED
+#define SHPL_WALK_PRED 0
+#endif
+constexpr int WALK = SHPL_WALK;
+
 template <typename T, int VEC, bool GROUP>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse(const Feat f, const Ents e) {
     typedef Chunk<T, VEC> C;
@@ -176,34 +184,72 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse(const Feat f, const Ents 
         float acc[VEC];
 #pragma unroll
         for (int j = 0; j < VEC; ++j) acc[j] = 0.0f;
-        if (GROUP) {
-            // TF: Q[k] = sum of column k's entries; out = 0 + Q[k1] + Q[k2] ... (ScatterNd order)
-            float q[VEC];
+        // Walk the destination's run WALK entries at a time: the index loads
+        // and the feature loads of a batch are all issued before the first
+        // add, then the adds run in TF order (a run of length L costs
+        // about 2*ceil(L/WALK) memory latencies instead of 3*L).
+        float q[VEC];  // GROUP: the current column's partial, TF's Q[k]
 #pragma unroll
-            for (int j = 0; j < VEC; ++j) q[j] = 0.0f;
-            int32_t kprev = e.col[s];
-            for (int64_t i = s; i < nnz && e.dst[i] == key; ++i) {
-                const int32_t k = e.col[i];
-                if (k != kprev) {
+        for (int j = 0; j < VEC; ++j) q[j] = 0.0f;
+        int32_t kprev = -1;  // no column yet: the first flush adds a zero partial (0 + 0 = +0)
+        for (int64_t i = s;; i += WALK) {
+            bool in[WALK];
+            int32_t d[WALK], sr[WALK], kc[WALK];
+            float w[WALK];
+#if SHPL_WALK_PRED
+            // src / val / col only for entries of the run (one more latency, fewer loads)
 #pragma unroll
-                    for (int j = 0; j < VEC; ++j) {
-                        acc[j] = __fadd_rn(acc[j], q[j]);
-                        q[j] = 0.0f;
-                    }
-                    kprev = k;
-                }
-                float x[VEC];
-                C::to_f32(C::load(sc + (int64_t)e.src[i] * f.src_stride), x);
-                fma_free_accumulate<VEC>(q, e.val[i], x);
+            for (int u = 0; u < WALK; ++u) d[u] = i + u < nnz ? e.dst[i + u] : -1;
+#pragma unroll
+            for (int u = 0; u < WALK; ++u) in[u] = d[u] == key && (u == 0 || in[u - 1]);
+#pragma unroll
+            for (int u = 0; u < WALK; ++u) {
+                sr[u] = in[u] ? e.src[i + u] : 0;
+                w[u] = in[u] ? e.val[i + u] : 0.0f;
+                kc[u] = (GROUP && in[u]) ? e.col[i + u] : 0;
             }
+#else
+            // index loads of the batch do not wait for each other (dst need not match yet)
+#pragma unroll
+            for (int u = 0; u < WALK; ++u) {
+                const bool ok = i + u < nnz;
+                d[u] = ok ? e.dst[i + u] : -1;
+                sr[u] = ok ? e.src[i + u] : 0;
+                w[u] = ok ? e.val[i + u] : 0.0f;
+                kc[u] = (GROUP && ok) ? e.col[i + u] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < WALK; ++u) in[u] = d[u] == key && (u == 0 || in[u - 1]);
+#endif
+            typename C::raw_t raw[WALK];
+#pragma unroll
+            for (int u = 0; u < WALK; ++u)
+                if (in[u]) raw[u] = C::load(sc + (int64_t)sr[u] * f.src_stride);
+#pragma unroll
+            for (int u = 0; u < WALK; ++u) {
+                if (!in[u]) break;
+                float x[VEC];
+                C::to_f32(raw[u], x);
+                if (GROUP) {
+                    // TF: Q[k] = sum of column k's entries; out = 0 + Q[k1] + Q[k2] ... (ScatterNd order)
+                    if (kc[u] != kprev) {
+#pragma unroll
+                        for (int j = 0; j < VEC; ++j) {
+                            acc[j] = __fadd_rn(acc[j], q[j]);
+                            q[j] = 0.0f;
+                        }
+                        kprev = kc[u];
+                    }
+                    fma_free_accumulate<VEC>(q, w[u], x);
+                } else {
+                    fma_free_accumulate<VEC>(acc, w[u], x);
+                }
+            }
+            if (!in[WALK - 1]) break;
+        }
+        if (GROUP) {
 #pragma unroll
             for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(acc[j], q[j]);
-        } else {
-            for (int64_t i = s; i < nnz && e.dst[i] == key; ++i) {
-                float x[VEC];
-                C::to_f32(C::load(sc + (int64_t)e.src[i] * f.src_stride), x);
-                fma_free_accumulate<VEC>(acc, e.val[i], x);
-            }
         }
         if (f.mode == SHPL_OUT_ADD) {
             float a[VEC];

@@ -172,11 +172,13 @@ class FramePipeline(FusedPipeline):
     -> destination-sorted M -> fused layer. bv_size is the BEV map size (nz, nx)."""
 
     def __init__(self, n_frames, total_points, im_size, area_extents, voxel_size, height_lo, height_hi,
-                 num_slices, stride, c_bev, c_img, dtype=torch.float32, device="cuda", dual=False, maps=True):
+                 num_slices, stride, c_bev, c_img, dtype=torch.float32, device="cuda", dual=False, maps=True,
+                 max_points_per_frame=None):
         from . import bev as _bev
         nx, nz = _bev.grid_divisions(area_extents, voxel_size)
-        # a frame can hold up to total_points voxels in the capacity layout
-        super().__init__(n_frames, total_points, total_points, im_size, (nz, nx), stride, c_bev, c_img,
+        # a frame holds at most as many voxels as points (capacity layout)
+        maxp = total_points if max_points_per_frame is None else max_points_per_frame
+        super().__init__(n_frames, maxp, total_points, im_size, (nz, nx), stride, c_bev, c_img,
                          dtype=dtype, device=device, dual=dual)
         self.bev_args = (area_extents, voxel_size, height_lo, height_hi, num_slices)
         self.maps = maps

@@ -65,6 +65,8 @@ class ShplMap:
                 what.append("source index (b, v, u) outside the feature map")
             if bits & L.EBIT_VALUES:
                 what.append("number of M values does not match number of indices")
+            if bits & L.EBIT_CAPACITY:
+                what.append("a frame holds more points than max_points_per_frame")
             raise InvalidArgumentError("; ".join(what))
 
     # ------------------------------------------------------------------ CSR

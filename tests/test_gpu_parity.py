@@ -105,6 +105,35 @@ def test_batched_index_builder_matches_oracle_per_frame(cfg):
     assert ib.map.error_bits() == 0
 
 
+def test_batched_index_builder_ragged_frames_across_chunks():
+    """Frames straddling the builder's 4096-point workgroup chunks, an empty
+    frame and a one-point frame, in one batch (SHPL_EBIT_CAPACITY when the
+    declared max_points_per_frame is too small)."""
+    from sparse_pooling_amd import pipeline, shpl_map as sm, _lib as L
+    base = synth.CONFIGS[2]
+    frames = []
+    for f, n in enumerate([4097, 0, 1, 4095, 4096, 9000, 12289]):
+        if n == 0:
+            frames.append(synth.Frame(np.zeros((0, 3)), np.zeros((0, 2), dtype=np.int64), synth.KITTI_P2,
+                                      synth.FrameSpec(0, base.im_size, base.bv_size, base.stride)))
+            continue
+        spec = synth.FrameSpec(n, base.im_size, base.bv_size, base.stride)
+        frames.append(synth.make_frame(spec, seed=300 + f, n_outside=min(n, 41 * f)))
+    pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
+    ib = sm.build_index_batch(pts, vox, off, P, base.im_size, base.bv_size, base.stride, maxp, ref_outputs=True)
+    fo, fn = _np(ib.frame_off), _np(ib.frame_nnz)
+    for f, fr in enumerate(frames):
+        a, b = fo[f], fo[f] + fn[f]
+        assert (_np(ib.map.cell[b:fo[f + 1]]) == -1).all()
+        ref = _oracle_frame(fr, base.stride)  # the oracle's FMA chain also for the 1-point frame
+        np.testing.assert_array_equal(_np(ib.mij[a:b]), ref["Mij_pool"])
+        np.testing.assert_array_equal(_np(ib.flip[a:b]), ref["img_index_flip_pool"])
+    assert ib.map.error_bits() == 0
+    small = sm.build_index_batch(pts, vox, off, P, base.im_size, base.bv_size, base.stride, 4096)
+    torch.cuda.synchronize()
+    assert small.map.error_bits() & L.EBIT_CAPACITY
+
+
 # ---------------------------------------------------------------- pooling ops
 
 def _frame_case(cfg, seed=0, dtype=np.float32):
