@@ -150,6 +150,7 @@ int shpl_produce_index(int64_t nv, const void *d_bv_index, int bv_itype, int64_t
  * bev_slices.py:33-156) with VoxelGrid2D.voxelize_2d (avod/wavedata/wavedata/
  * tools/core/voxel_grid_2d.py:43-162), for n_frames frames in one launch.
  *   d_points       [N,3] f64 camera-frame points; frame f owns [off[f], off[f+1])
+ *   d_point_counts optional [n_frames] i64: only the first count[f] points are live
  *   d_planes       [n_frames,4] f64 ground planes (a, b, c, d)
  *   area_extents   host [3][2] f64 ([[xmin,xmax],[ymin,ymax],[zmin,zmax]])
  *   slice_lo/hi    host [num_slices] plane offsets of each height slice, computed
@@ -164,7 +165,8 @@ int shpl_produce_index(int64_t nv, const void *d_bv_index, int bv_itype, int64_t
  * Slices are emitted in order and cells in (x, z) order, matching
  * np.vstack(voxel_indices_stack). Workspace: shpl_bev_workspace_bytes. */
 int shpl_bev_workspace_bytes(int64_t total_points, int num_slices, size_t *bytes);
-int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, int64_t total_points,
+int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, const int64_t *d_point_counts,
+                    int64_t total_points,
                     const void *d_points, int points_dtype, const double *d_planes,
                     const double *area_extents, double voxel_size, int num_slices,
                     const double *slice_lo, const double *slice_hi, double density_lo,
@@ -178,6 +180,8 @@ int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, int64_t total_
  *   d_points     [N, point_stride] f64 camera-frame points (x, y, z, ...)
  *   d_img_index2 optional [2, N] i64 rounded projections (minibatch_mv3d_img.py:88-91);
  *                NULL: computed on the device from d_P [n_frames,3,4] like the reference
+ *   d_fv_aug     optional [n_frames,3] f64 (expansion_ratio, sx, sy) of augment_fv
+ *                (minibatch_mv3d_img.py:191-209): u = int(u*ratio + sx), v = int(v*ratio + sy)
  *   ranges       host [6] f64: fwd (lo, hi), side (lo, hi), height (lo, hi), strict bounds
  *   res, zres, voxel_point_count  cfg.VOXEL_X_SIZE, VOXEL_Z_SIZE, VOXEL_POINT_COUNT
  * Outputs, capacity layout (frame f at [off[f], off[f] + d_frame_n[f])):
@@ -188,10 +192,35 @@ int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, int64_t total_
 int shpl_mv3d_workspace_bytes(int64_t total_points, size_t *bytes);
 int shpl_mv3d_voxels(int n_frames, const int64_t *d_point_offsets, int64_t total_points,
                      const double *d_points, int64_t point_stride, const int64_t *d_img_index2,
-                     const double *d_P, const double *ranges, double res, double zres,
-                     int voxel_point_count, double *d_img_index, int64_t ld, int64_t *d_bv_index,
+                     const double *d_P, const double *d_fv_aug, const double *ranges, double res,
+                     double zres, int voxel_point_count, double *d_img_index, int64_t ld, int64_t *d_bv_index,
                      double *d_mval, int64_t *d_frame_n, int32_t *d_number_buffer,
                      int64_t *d_frame_nvox, void *d_ws, size_t ws_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * KITTI velodyne loader: the BEV voxelizer's input
+ * ------------------------------------------------------------------------- */
+
+/* obj_utils.get_lidar_point_cloud (avod/wavedata/wavedata/tools/obj_detection/
+ * obj_utils.py:220-268) after read_lidar, for n_frames scans at once:
+ * calib_utils.lidar_to_cam_frame (calib_utils.py:371-410), then with an image
+ * size: z > 0, project with P2 (calib_utils.py:281-298), 0 < u < W, 0 < v < H;
+ * then optionally kitti_aug.flip_point_cloud (kitti_aug.py:24-29).
+ *   d_point_offsets [n_frames+1] i64: scan f is rows [off[f], off[f+1]) of d_xyzi
+ *   d_xyzi      [N,4] f32 velodyne points (x, y, z, intensity), 16-byte aligned
+ *   d_rect      [n_frames,3,4] f64 rows 0-2 of R0_rect4 . Tr_velo_to_cam4 (numpy's
+ *               4x4 product on the host, as calib_utils.py:404 forms it)
+ *   d_P, d_im_size  [n_frames,3,4] P2 and [n_frames,2] (w, h); both NULL = no filter
+ *   min_intensity   NaN = none (see DESIGN.md for the reference's mask bug)
+ *   d_flip      optional [n_frames] i32, nonzero = negate x of the kept points
+ * Outputs, capacity layout: d_points [N,3] f64 (frame f's kept points at
+ * [off[f], off[f] + d_counts[f]) in scan order, NaN rows after). The result
+ * feeds shpl_bev_slices (d_point_counts = d_counts) directly. */
+int shpl_velo_workspace_bytes(int n_frames, int64_t max_points_per_frame, size_t *bytes);
+int shpl_velo_to_cam(int n_frames, const int64_t *d_point_offsets, int64_t max_points_per_frame,
+                     const float *d_xyzi, const double *d_rect, const double *d_P, const double *d_im_size,
+                     double min_intensity, const int32_t *d_flip, double *d_points, int64_t *d_counts,
+                     uint32_t *d_err, void *d_ws, size_t ws_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Correspondence matrix M: validation + device map (SURVEY a8-a10 inputs)

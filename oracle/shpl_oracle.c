@@ -459,3 +459,50 @@ int64_t shplo_mv3d_voxels(int64_t n, const double *pts, int64_t stride, const in
     free(key); free(ord); free(vid); free(fi); free(si); free(count); free(keep);
     return out;
 }
+
+/* ---- §8f item 3: KITTI velodyne -> camera-frame point cloud ------------------
+ * obj_utils.get_lidar_point_cloud (avod/wavedata/wavedata/tools/obj_detection/obj_utils.py:220-268):
+ *   lidar_to_cam_frame (calib_utils.py:371-410): p_cam = (R0_rect4 . Tr_velo_to_cam4) . [x;y;z;1]
+ *     -- `rect` is that 4x4 product's rows 0-2, computed by numpy on the host; the
+ *     per-point np.dot is OpenBLAS dgemm, i.e. the same FMA chain as project()
+ *     (checked bit-exact against numpy for N = 2 .. 120000);
+ *   keep z > 0 (:250), project with P2 (calib_utils.project_to_image :281-298),
+ *   keep 0 < u < W and 0 < v < H (strict, :256-259), im_size = [W, H].
+ * has_filter = 0 mirrors im_size=None (every point, :244-246).
+ * min_intensity (NaN = none): the reference compares the intensities of ALL
+ * points against a mask of the z-filtered ones (:265-267), which raises as
+ * soon as one point has z <= 0; restated here with the evident intent
+ * (intensity of the same point), documented in DESIGN.md.
+ * flip != 0 applies kitti_aug.flip_point_cloud (x -> -x, kitti_aug.py:24-29)
+ * after the filter, as kitti_dataset.py:305-306 does.
+ * xyzi: n x 4 f32 (read_lidar, calib_utils.py:328-368). out: n x 3. Returns kept. */
+int64_t shplo_velo_to_cam(int64_t n, const float *xyzi, const double *rect, const double *P, int has_filter,
+                          double im_w, double im_h, double min_intensity, int flip, double *out)
+{
+    int64_t k = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const double a[4] = {(double)xyzi[4 * i], (double)xyzi[4 * i + 1], (double)xyzi[4 * i + 2], 1.0};
+        double c[3];
+        for (int r = 0; r < 3; ++r) {
+            double s = rect[4 * r] * a[0];
+            for (int q = 1; q < 4; ++q)
+                s = fma(rect[4 * r + q], a[q], s);
+            c[r] = s;
+        }
+        if (has_filter) {
+            if (!(c[2] > 0.0))
+                continue;
+            double u, v;
+            project(P, c[0], c[1], c[2], &u, &v);
+            if (!(u > 0.0 && u < im_w && v > 0.0 && v < im_h))
+                continue;
+            if (!isnan(min_intensity) && !((double)xyzi[4 * i + 3] > min_intensity))
+                continue;
+        }
+        out[3 * k] = flip ? -c[0] : c[0];
+        out[3 * k + 1] = c[1];
+        out[3 * k + 2] = c[2];
+        ++k;
+    }
+    return k;
+}

@@ -5,7 +5,8 @@ bench.py's cpu_baseline leg -- as the checker, never as the product path.
 See the header of shpl_oracle.c for what is restated from where and for the
 parity status (index builder pinned by the reference-generated goldens;
 pooling ops restated from TensorFlow 1.8's kernel order, "parity unpinned"
-beyond that).
+beyond that; BEV slices, MV3D producer and the KITTI velodyne loader pinned
+by reference-generated goldens).
 """
 import ctypes
 import os
@@ -49,6 +50,8 @@ def lib():
                                                     i64, p]
         _lib.shplo_mv3d_voxels.restype = i64
         _lib.shplo_mv3d_voxels.argtypes = [i64, p, i64, p, p, d, d, ctypes.c_int, p, i64, p, p, p, p]
+        _lib.shplo_velo_to_cam.restype = i64
+        _lib.shplo_velo_to_cam.argtypes = [i64, p, p, p, ctypes.c_int, d, d, d, ctypes.c_int, p]
         _lib.shplo_bev_slices.restype = i64
         _lib.shplo_bev_slices.argtypes = [i64, p, p, p, d, ctypes.c_int, p, p, d, d, d, p, i64, p, p,
                                           p, p]
@@ -159,6 +162,44 @@ def mv3d_voxels(points, img_index2, ranges, res, zres, cap):
                                 float(zres), int(cap), _p(img), img.shape[1], _p(bv), _p(mv), _p(nb),
                                 ctypes.byref(nvox))
     return np.ascontiguousarray(img[:, :k]), bv[:k].copy(), mv[:k].copy(), nb[:nvox.value].copy()
+
+
+def augment_fv_index(img_index, expansion_ratio, sx, sy):
+    """augment_fv's index transform (MV3D_TF_release/lib/roi_data_layer/minibatch_mv3d_img.py:205-206)
+    on an int img_index [3, n]: row = (row * ratio + shift).astype(int)."""
+    out = np.array(img_index, dtype=np.int64, copy=True)
+    r = np.array([expansion_ratio], dtype=np.float64)  # np.random.uniform(0.95, 1.05, 1)
+    out[0, :] = (out[0, :] * r + sx).astype(int)
+    out[1, :] = (out[1, :] * r + sy).astype(int)
+    return out
+
+
+# ---- KITTI velodyne -> camera frame (§8f item 3) ------------------------------
+
+def rect_matrix(r0_rect, tr_velodyne_to_cam):
+    """Rows 0-2 of np.dot(R0_rect padded 4x4, Tr_velo_to_cam padded 4x4), computed
+    exactly as calib_utils.lidar_to_cam_frame does (calib_utils.py:388-404)."""
+    r0 = np.pad(np.asarray(r0_rect, np.float64).reshape(3, 3), ((0, 1), (0, 1)), "constant", constant_values=0)
+    r0[3, 3] = 1
+    tf = np.pad(np.asarray(tr_velodyne_to_cam, np.float64).reshape(3, 4), ((0, 1), (0, 0)), "constant",
+                constant_values=0)
+    tf[3, 3] = 1
+    return np.ascontiguousarray(np.dot(r0, tf)[0:3])
+
+
+def velo_to_cam(xyzi, rect, p2=None, im_size=None, min_intensity=None, flip=False):
+    """get_lidar_point_cloud (obj_utils.py:220-268) on an [n,4] f32 velodyne scan:
+    returns the (3, n') camera-frame cloud (im_size=None: no filter)."""
+    x = _c(xyzi, np.float32).reshape(-1, 4)
+    n = x.shape[0]
+    out = np.zeros((max(n, 1), 3), np.float64)
+    has = im_size is not None
+    P = _c(p2 if p2 is not None else np.zeros((3, 4)), np.float64)
+    w, h = (float(im_size[0]), float(im_size[1])) if has else (0.0, 0.0)
+    k = lib().shplo_velo_to_cam(n, _p(x), _p(_c(rect, np.float64)), _p(P), int(has), w, h,
+                                float("nan") if min_intensity is None else float(min_intensity), int(bool(flip)),
+                                _p(out))
+    return np.ascontiguousarray(out[:k].T)
 
 
 # ---- TF op restatements ----------------------------------------------------

@@ -66,10 +66,12 @@ def _declare(lib):
                                    p, p, p, p, p, p, p, p, p, sz, p]),
         "shpl_bev_workspace_bytes": (i32, [i64, i32, psz]),
         "shpl_mv3d_workspace_bytes": (i32, [i64, psz]),
-        "shpl_mv3d_voxels": (i32, [i32, p, i64, p, i64, p, p, p, d, d, i32, p, i64, p, p, p, p, p, p, sz,
-                                   p]),
-        "shpl_bev_slices": (i32, [i32, p, i64, p, i32, p, p, d, i32, p, p, d, d, d, p, p, p, p, p, p, p,
-                                  p, sz, p]),
+        "shpl_mv3d_voxels": (i32, [i32, p, i64, p, i64, p, p, p, p, d, d, i32, p, i64, p, p, p, p, p, p,
+                                   sz, p]),
+        "shpl_bev_slices": (i32, [i32, p, p, i64, p, i32, p, p, d, i32, p, p, d, d, d, p, p, p, p, p, p,
+                                  p, p, sz, p]),
+        "shpl_velo_workspace_bytes": (i32, [i32, i64, psz]),
+        "shpl_velo_to_cam": (i32, [i32, p, i64, p, p, p, p, d, p, p, p, p, p, sz, p]),
         "shpl_gen_index": (i32, [i64, p, i32, p, i32, i64, p, d, d, p, p, i64, p, p, sz, p]),
         "shpl_produce_index": (i32, [i64, p, i32, i64, p, i64, d, d, d, d, d, d, p, p, p, p, p,
                                      p, p, sz, p]),

@@ -51,8 +51,9 @@ class BevBatch:
 
 
 def bev_slices_batch(points, point_offsets, planes, area_extents, voxel_size, height_lo, height_hi,
-                     num_slices, norm_value=np.log(16), maps=True, ws=None):
-    """points [N,3] f64 (camera frame), point_offsets [F+1] i64, planes [F,4] f64 -- all on the device.
+                     num_slices, norm_value=np.log(16), maps=True, ws=None, point_counts=None):
+    """points [N,3] f64 (camera frame), point_offsets [F+1] i64, planes [F,4] f64 -- all on the device;
+    point_counts [F] i64: only the first count[f] points of each frame are live (shpl_velo_to_cam output).
     Returns a BevBatch; frame f's voxels are rows [off[f], off[f] + frame_nvox[f])."""
     dev = points.device
     F = int(point_offsets.numel()) - 1
@@ -62,6 +63,8 @@ def bev_slices_batch(points, point_offsets, planes, area_extents, voxel_size, he
     points = points.contiguous()
     point_offsets = point_offsets.to(torch.int64).contiguous()
     planes = planes.to(torch.float64).contiguous()
+    if point_counts is not None:
+        point_counts = point_counts.to(torch.int64).contiguous()
     nx, nz = grid_divisions(area_extents, voxel_size)
     hpd, lo, hi = slice_bounds(float(height_lo), float(height_hi), int(num_slices))
     ext = np.ascontiguousarray(np.asarray(area_extents, dtype=np.float64).reshape(6))
@@ -79,7 +82,7 @@ def bev_slices_batch(points, point_offsets, planes, area_extents, voxel_size, he
         L.check(L.lib().shpl_bev_workspace_bytes(N, int(num_slices), ctypes.byref(nb)), "shpl_bev_workspace_bytes")
         ws = L.workspace(nb.value, dev)
     p = lambda a: a.ctypes.data_as(L.ctypes.c_void_p)  # noqa: E731
-    L.check(L.lib().shpl_bev_slices(F, L.ptr(point_offsets), N, L.ptr(points), L.F64, L.ptr(planes), p(ext),
+    L.check(L.lib().shpl_bev_slices(F, L.ptr(point_offsets), L.ptr(point_counts), N, L.ptr(points), L.F64, L.ptr(planes), p(ext),
                                     float(voxel_size), int(num_slices), p(lo_a), p(hi_a), float(height_lo),
                                     float(height_hi), float(hpd), p(table), L.ptr(vox), L.ptr(upts), L.ptr(nvox),
                                     L.ptr(hm), L.ptr(dm), L.ptr(err), L.ptr(ws), ws.numel(),

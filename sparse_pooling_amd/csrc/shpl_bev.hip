@@ -90,14 +90,17 @@ __device__ __forceinline__ void point_entries(const BevGeom &g, const double *pl
 }
 
 template <typename PT>
-__global__ __launch_bounds__(BEV_BLOCK) void k_bev_frame(BevGeom g, const int64_t *pt_off, const void *pts,
+__global__ __launch_bounds__(BEV_BLOCK) void k_bev_frame(BevGeom g, const int64_t *pt_off, const int64_t *pt_count,
+                                                         const void *pts,
                                                          const double *planes, uint64_t *tmp, uint64_t *srt,
                                                          int64_t ent_per_point, int32_t *vox_out, double *pts_out,
                                                          int64_t *frame_nvox, double *hmaps, double *dmap,
                                                          uint32_t *err) {
     __shared__ TileSortLds lds;
     const int f = blockIdx.x;
-    const int64_t p0 = pt_off[f], p1 = pt_off[f + 1];
+    const int64_t p0 = pt_off[f], cap_end = pt_off[f + 1];
+    // live points: [p0, p0 + count) when counts are given (capacity layout input, e.g. shpl_velo_to_cam)
+    const int64_t p1 = pt_count ? (p0 + pt_count[f] < cap_end ? p0 + pt_count[f] : cap_end) : cap_end;
     const int64_t t0 = p0 * ent_per_point;  // this frame's entry slots
     const double *plane = planes + 4 * f;
     const int64_t n_cells = (int64_t)g.nx * g.nz;
@@ -115,7 +118,7 @@ __global__ __launch_bounds__(BEV_BLOCK) void k_bev_frame(BevGeom g, const int64_
     // 5. one output per key run, slice cells compacted in sorted order
     const double a = plane[0], b = plane[1], c = plane[2], d = plane[3];
     const double norm = sqrt(__dadd_rn(__dadd_rn(__dmul_rn(a, a), __dmul_rn(b, b)), __dmul_rn(c, c)));
-    const int64_t cap = p1 - p0;
+    const int64_t cap = cap_end - p0;
     int64_t kept = 0;
     const int wid = threadIdx.x >> 6;
     for (int32_t base = 0; base < n_ent; base += BEV_BLOCK) {
@@ -190,7 +193,8 @@ extern "C" int shpl_bev_workspace_bytes(int64_t total_points, int num_slices, si
     return SHPL_OK;
 }
 
-extern "C" int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, int64_t total_points,
+extern "C" int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, const int64_t *d_point_counts,
+                               int64_t total_points,
                                const void *d_points, int points_dtype, const double *d_planes,
                                const double *area_extents, double voxel_size, int num_slices,
                                const double *slice_lo, const double *slice_hi, double density_lo,
@@ -243,7 +247,8 @@ extern "C" int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, int
         SHPL_HIP_CHECK(hipMemsetAsync(d_height_maps, 0, sizeof(double) * (size_t)(per_map * num_slices * n_frames), s));
     if (d_density_map) SHPL_HIP_CHECK(hipMemsetAsync(d_density_map, 0, sizeof(double) * (size_t)(per_map * n_frames), s));
     if (points_dtype == SHPL_F64)
-        hipLaunchKernelGGL(k_bev_frame<double>, dim3(n_frames), dim3(BEV_BLOCK), 0, s, g, d_point_offsets, d_points,
+        hipLaunchKernelGGL(k_bev_frame<double>, dim3(n_frames), dim3(BEV_BLOCK), 0, s, g, d_point_offsets,
+                           d_point_counts, d_points,
                            d_planes, tmp, srt, (int64_t)(num_slices + 1), d_voxel_indices, d_pts_in_voxel,
                            d_frame_nvox, d_height_maps, d_density_map, d_err);
     else

@@ -76,6 +76,25 @@ __device__ __forceinline__ void block_publish() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// One row of a 3x4 (or 4x4) matrix times [a0; a1; a2; 1] the way numpy's
+// np.dot evaluates it for N >= 2 columns (OpenBLAS dgemm): the first product
+// rounded, then a fused multiply-add per k in k order (checked bit-exact
+// against numpy; tests/golden/index_*, kitti_frames).
+__device__ __forceinline__ double dot4_chain(const double *row, double a0, double a1, double a2) {
+    double s = __dmul_rn(row[0], a0);
+    s = __fma_rn(row[1], a1, s);
+    s = __fma_rn(row[2], a2, s);
+    return __fma_rn(row[3], 1.0, s);
+}
+
+// projectToImage (avod/avod/utils/transform.py:3-26; calib_utils.project_to_image
+// :281-298): [u;v;w] = P [x;y;z;1]; u/=w; v/=w (IEEE division).
+__device__ __forceinline__ void project(const double *P, double x, double y, double z, double &u, double &v) {
+    const double r0 = dot4_chain(P, x, y, z), r1 = dot4_chain(P + 4, x, y, z), r2 = dot4_chain(P + 8, x, y, z);
+    u = __ddiv_rn(r0, r2);
+    v = __ddiv_rn(r1, r2);
+}
+
 inline int grid_for(int64_t work, int64_t per_block, int cap) {
     int64_t g = (work + per_block - 1) / per_block;
     if (g < 1) g = 1;

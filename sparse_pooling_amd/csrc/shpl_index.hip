@@ -5,22 +5,20 @@
 //   gen_sparse_pooling_input_avod           avod/avod/utils/sparse_pool_utils.py:6-20
 //   produce_sparse_pooling_input            avod/avod/utils/sparse_pool_utils.py:22-58
 //
-// One workgroup per frame (1024 threads) does the whole frame in one launch:
-// it walks the frame's points in 1024-point chunks, evaluates each point
-// (one thread per point), ranks the kept points with a wave ballot + LDS
-// prefix, and writes them in point order (a stable compaction). A frame's
+// Two launches over 4096-point chunks of every frame (shpl_compact.h): a
+// per-chunk count of the kept points, then the placement, where each thread
+// evaluates one point per row and the kept points are ranked by wave ballots
+// + an LDS prefix and written in point order (a stable compaction). A frame's
 // entries start at its first input point ("capacity layout"); the tail up to
 // the next frame is filled with -1 sentinels that every consumer skips, so no
-// cross-frame scan or second launch is needed.
+// cross-frame scan is needed.
 // Projection runs in f64 with the exact operation order numpy uses (an FMA
 // chain over k for np.dot, IEEE division, rint = round-half-even), so the
 // integer outputs are bit-identical to the reference (tests/golden/index_*).
-#include "shpl_common.h"
+#include "shpl_compact.h"
 
 namespace shpl {
 namespace {
-
-constexpr int IDX_BLOCK = 1024;  // one workgroup per frame
 
 template <typename PT>
 __device__ __forceinline__ void load_point(const void *pts, int64_t i, double &x, double &y, double &z) {
@@ -33,23 +31,6 @@ __device__ __forceinline__ void load_point(const void *pts, int64_t i, double &x
 template <typename IT>
 __device__ __forceinline__ int64_t load_idx(const void *a, int64_t i) {
     return (int64_t)reinterpret_cast<const IT *>(a)[i];
-}
-
-// projectToImage (transform.py:3-26): [u;v;w] = P [x;y;z;1]; u/=w; v/=w.
-// np.dot -> OpenBLAS dgemm: s = P0*a0, then s = fma(Pk, ak, s) for k = 1..3.
-__device__ __forceinline__ void project(const double *P, double x, double y, double z, double &u,
-                                        double &v) {
-    double r[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        double s = __dmul_rn(P[4 * i + 0], x);
-        s = __fma_rn(P[4 * i + 1], y, s);
-        s = __fma_rn(P[4 * i + 2], z, s);
-        s = __fma_rn(P[4 * i + 3], 1.0, s);
-        r[i] = s;
-    }
-    u = __ddiv_rn(r[0], r[2]);
-    v = __ddiv_rn(r[1], r[2]);
 }
 
 // clip3DwithinImage (transform.py:28-40): 0 <= u < W-1, 0 <= v < H-1.
@@ -262,150 +243,6 @@ struct ProduceStage {  // produce_sparse_pooling_input (in-place img_index updat
 };
 
 // ------------------------------------------------- per-frame stable compaction
-
-constexpr int IDX_BATCH = 4;                      // point rows per thread whose loads are in flight together
-constexpr int IDX_CHUNK = IDX_BLOCK * IDX_BATCH;  // points per workgroup: one round
-
-struct Frames {
-    const int64_t *pt_off, *pt_count;
-    int n_frames, n_chunks;  // chunks of IDX_CHUNK points per frame (grid.x)
-    int32_t *chunk_kept;     // [n_frames][n_chunks] workspace
-    int64_t *frame_nnz, *frame_out_off;
-    uint32_t *err;
-};
-
-__device__ __forceinline__ void frame_range(const Frames &fr, int f, int64_t &p0, int64_t &p1, int64_t &cap_end) {
-    p0 = fr.pt_off[f];
-    cap_end = fr.pt_off[f + 1];
-    // live points of the frame: [p0, p0 + count) when counts are given (capacity layout input)
-    p1 = fr.pt_count ? (p0 + fr.pt_count[f] < cap_end ? p0 + fr.pt_count[f] : cap_end) : cap_end;
-}
-
-// Pass 1 (grid n_chunks x n_frames): kept points per chunk.
-template <typename Stage>
-__global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr) {
-    __shared__ int32_t wsum[IDX_BLOCK / 64];
-    const int f = blockIdx.y, j = blockIdx.x;
-    int64_t p0, p1, cap_end;
-    frame_range(fr, f, p0, p1, cap_end);
-    const int64_t base = p0 + (int64_t)j * IDX_CHUNK;
-    if (j == fr.n_chunks - 1 && p1 > base + IDX_CHUNK && threadIdx.x == 0 && fr.err)
-        atomicOr(fr.err, SHPL_EBIT_CAPACITY);  // frame larger than max_points_per_frame
-    typename Stage::In in[IDX_BATCH];
-#pragma unroll
-    for (int u = 0; u < IDX_BATCH; ++u) {
-        const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
-        if (i < p1) st.load(i, in[u]);
-    }
-    int32_t n = 0;
-#pragma unroll
-    for (int u = 0; u < IDX_BATCH; ++u) {
-        const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
-        typename Stage::Payload pl;
-        if (i < p1 && st.eval(f, i, in[u], pl)) ++n;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = n;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int32_t t = 0;
-        for (int w = 0; w < IDX_BLOCK / 64; ++w) t += wsum[w];
-        fr.chunk_kept[(int64_t)f * fr.n_chunks + j] = t;
-    }
-}
-
-// Pass 2 (same grid): the chunk's kept points land after those of the
-// frame's earlier chunks, in point order (a stable compaction); rows of the
-// chunk are ranked in order by wave ballots + an LDS prefix. The frame's
-// last chunk also writes the sentinels of the unused capacity and the
-// frame's entry count.
-template <typename Stage>
-__global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr) {
-    __shared__ int32_t wsum[IDX_BATCH][IDX_BLOCK / 64];
-    __shared__ int32_t pre[IDX_BLOCK / 64];
-    const int f = blockIdx.y, j = blockIdx.x;
-    int64_t p0, p1, cap_end;
-    frame_range(fr, f, p0, p1, cap_end);
-    const int wid = threadIdx.x >> 6;
-    // kept points of the earlier chunks
-    int32_t mine = 0;
-    for (int q = threadIdx.x; q < j; q += IDX_BLOCK) mine += fr.chunk_kept[(int64_t)f * fr.n_chunks + q];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
-    if ((threadIdx.x & 63) == 0) pre[wid] = mine;
-    const int64_t base = p0 + (int64_t)j * IDX_CHUNK;
-    typename Stage::In in[IDX_BATCH];
-    typename Stage::Payload pl[IDX_BATCH];
-    bool keep[IDX_BATCH];
-#pragma unroll
-    for (int u = 0; u < IDX_BATCH; ++u) {
-        const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
-        if (i < p1) st.load(i, in[u]);
-    }
-    uint64_t m[IDX_BATCH];
-#pragma unroll
-    for (int u = 0; u < IDX_BATCH; ++u) {
-        const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
-        keep[u] = false;
-        if (i < p1) {
-            keep[u] = st.eval(f, i, in[u], pl[u]);
-            st.touch(f, i, pl[u], keep[u]);
-        }
-        m[u] = __ballot(keep[u]);
-        if ((threadIdx.x & 63) == 0) wsum[u][wid] = (int32_t)__popcll(m[u]);
-    }
-    __syncthreads();
-    int64_t kept = 0;
-    for (int w = 0; w < IDX_BLOCK / 64; ++w) kept += pre[w];
-#pragma unroll
-    for (int u = 0; u < IDX_BATCH; ++u) {
-        int32_t before = 0, tot = 0;
-        for (int w = 0; w < IDX_BLOCK / 64; ++w) {
-            const int32_t c = wsum[u][w];
-            before += w < wid ? c : 0;
-            tot += c;
-        }
-        const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
-        if (keep[u]) st.emit(f, i, p0 + kept + before + lane_rank(m[u]), p0, pl[u]);
-        kept += tot;
-    }
-    if (j != fr.n_chunks - 1) return;
-    for (int64_t pos = p0 + kept + threadIdx.x; pos < cap_end; pos += IDX_BLOCK) st.hole(pos);
-    if (threadIdx.x == 0) {
-        if (fr.frame_nnz) fr.frame_nnz[f] = kept;
-        if (fr.frame_out_off) {
-            fr.frame_out_off[f] = p0;
-            if (f == fr.n_frames - 1) fr.frame_out_off[fr.n_frames] = cap_end;
-        }
-    }
-}
-
-int n_chunks_for(int64_t max_points) {
-    const int64_t c = (max_points + IDX_CHUNK - 1) / IDX_CHUNK;
-    return (int)(c < 1 ? 1 : c);
-}
-
-constexpr size_t IDX_WS_HEAD = 256;  // single-frame [0, n] offsets
-
-size_t index_ws_bytes(int n_frames, int64_t max_points) {
-    return IDX_WS_HEAD + align_up(sizeof(int32_t) * (size_t)n_frames * (size_t)n_chunks_for(max_points), 256);
-}
-
-template <typename Stage>
-int run_compaction(const Stage &st, int n_frames, int64_t max_points, const int64_t *pt_off,
-                   const int64_t *pt_count, int64_t *frame_nnz, int64_t *frame_out_off, uint32_t *err, void *ws,
-                   size_t ws_bytes, hipStream_t stream) {
-    if (ws_bytes < index_ws_bytes(n_frames, max_points)) return SHPL_ERR_WORKSPACE;
-    Frames fr{pt_off, pt_count, n_frames, n_chunks_for(max_points),
-              (int32_t *)((char *)ws + IDX_WS_HEAD), frame_nnz, frame_out_off, err};
-    const dim3 grid(fr.n_chunks, n_frames);
-    hipLaunchKernelGGL(k_count<Stage>, grid, dim3(IDX_BLOCK), 0, stream, st, fr);
-    SHPL_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_compact<Stage>, grid, dim3(IDX_BLOCK), 0, stream, st, fr);
-    SHPL_LAUNCH_CHECK();
-    return SHPL_OK;
-}
 
 __global__ void k_set_pair(int64_t *o, int64_t a, int64_t b) {
     o[0] = a;

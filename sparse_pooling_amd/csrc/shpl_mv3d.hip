@@ -11,6 +11,8 @@
 //   points; the accepted points, in point order, give
 //     img_index = [img_index2; 0], bv_index = (fwd, side),
 //     M_val = 1 / (points accepted by the point's voxel)   (MV3D's mean pooling).
+// Optionally the front-view augmentation's index transform follows
+// (augment_fv, MV3D_TF_release/lib/roi_data_layer/minibatch_mv3d_img.py:191-209).
 // Here one workgroup per frame sorts the packed (voxel, point) words
 // (shpl_tilesort.h); the thread at the start of each voxel run marks the run's
 // first VOXEL_POINT_COUNT points accepted with weight 1/min(run, cap); a
@@ -29,19 +31,12 @@ struct Mv3dGeom {
     int has_proj;            // 1: img_index2 from P2 on the device
 };
 
-// projectToImage + np.round (dgemm FMA chain as in shpl_index.hip)
+// projectToImage + np.round (minibatch_mv3d_img.py:88-91)
 __device__ __forceinline__ void project_round(const double *P, double x, double y, double z, int64_t &u, int64_t &v) {
-    double r[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        double s = __dmul_rn(P[4 * i + 0], x);
-        s = __fma_rn(P[4 * i + 1], y, s);
-        s = __fma_rn(P[4 * i + 2], z, s);
-        s = __fma_rn(P[4 * i + 3], 1.0, s);
-        r[i] = s;
-    }
-    u = (int64_t)rint(__ddiv_rn(r[0], r[2]));
-    v = (int64_t)rint(__ddiv_rn(r[1], r[2]));
+    double uf, vf;
+    project(P, x, y, z, uf, vf);
+    u = (int64_t)rint(uf);
+    v = (int64_t)rint(vf);
 }
 
 // voxel key of camera-frame point (x, y, z) or -1 when outside the ranges
@@ -57,7 +52,8 @@ __device__ __forceinline__ int64_t voxel_key(const Mv3dGeom &g, double x, double
 
 __global__ __launch_bounds__(TS_BLOCK) void k_mv3d_frame(Mv3dGeom g, const int64_t *pt_off, const double *pts,
                                                          int64_t pt_stride, const int64_t *img2, int64_t img2_ld,
-                                                         const double *P, uint64_t *tmp, uint64_t *srt, int32_t *acc,
+                                                         const double *P, const double *fv_aug, uint64_t *tmp,
+                                                         uint64_t *srt, int32_t *acc,
                                                          double *img_index, int64_t ld, int64_t *bv_index,
                                                          double *mval, int64_t *frame_n, int32_t *vox_count,
                                                          int64_t *frame_nvox) {
@@ -144,6 +140,12 @@ __global__ __launch_bounds__(TS_BLOCK) void k_mv3d_frame(Mv3dGeom g, const int64
                 u = img2[i];
                 v = img2[img2_ld + i];
             }
+            if (fv_aug) {
+                // augment_fv (minibatch_mv3d_img.py:205-206): (img_index * ratio + shift).astype(int)
+                const double *a = fv_aug + 3 * f;
+                u = (int64_t)__dadd_rn(__dmul_rn((double)u, a[0]), a[1]);
+                v = (int64_t)__dadd_rn(__dmul_rn((double)v, a[0]), a[2]);
+            }
             img_index[pos] = (double)u;
             img_index[ld + pos] = (double)v;
             img_index[2 * ld + pos] = 0.0;
@@ -171,8 +173,8 @@ extern "C" int shpl_mv3d_workspace_bytes(int64_t total_points, size_t *bytes) {
 
 extern "C" int shpl_mv3d_voxels(int n_frames, const int64_t *d_point_offsets, int64_t total_points,
                                 const double *d_points, int64_t point_stride, const int64_t *d_img_index2,
-                                const double *d_P, const double *ranges, double res, double zres,
-                                int voxel_point_count, double *d_img_index, int64_t ld, int64_t *d_bv_index,
+                                const double *d_P, const double *d_fv_aug, const double *ranges, double res,
+                                double zres, int voxel_point_count, double *d_img_index, int64_t ld, int64_t *d_bv_index,
                                 double *d_mval, int64_t *d_frame_n, int32_t *d_number_buffer,
                                 int64_t *d_frame_nvox, void *d_ws, size_t ws_bytes, void *stream) {
     if (n_frames < 1 || !d_point_offsets || !ranges || !d_frame_n || !d_ws) return SHPL_ERR_ARG;
@@ -209,7 +211,7 @@ extern "C" int shpl_mv3d_voxels(int n_frames, const int64_t *d_point_offsets, in
     uint64_t *srt = (uint64_t *)((char *)d_ws + align_up(n * sizeof(uint64_t), 256));
     int32_t *acc = (int32_t *)((char *)d_ws + 2 * align_up(n * sizeof(uint64_t), 256));
     hipLaunchKernelGGL(k_mv3d_frame, dim3(n_frames), dim3(TS_BLOCK), 0, (hipStream_t)stream, g, d_point_offsets,
-                       d_points, point_stride, d_img_index2, total_points, d_P, tmp, srt, acc, d_img_index, ld,
+                       d_points, point_stride, d_img_index2, total_points, d_P, d_fv_aug, tmp, srt, acc, d_img_index, ld,
                        d_bv_index, d_mval,
                        d_frame_n, d_number_buffer, d_frame_nvox);
     SHPL_LAUNCH_CHECK();

@@ -38,10 +38,12 @@ CAR_RANGES = (0.0, 70.4 - 0.01, -40.0, 40 - 0.01, -1.0, 3 - 0.01)
 
 
 def mv3d_voxels_batch(points, point_offsets, img_index2=None, P=None, ranges=PED_RANGES, res=0.2, zres=0.4,
-                      voxel_point_count=45, number_buffer=False):
+                      voxel_point_count=45, number_buffer=False, fv_aug=None):
     """The SHPL outputs of point_cloud_2_top_sparse (construct_voxel.py:37-162)
     for a batch of frames on the device. points [N, >=3] f64 camera frame;
-    img_index2 [2, N] i64 (or P [F,3,4] f64 to project on the device).
+    img_index2 [2, N] i64 (or P [F,3,4] f64 to project on the device);
+    fv_aug [F,3] f64 (expansion_ratio, sx, sy): augment_fv's index transform
+    (minibatch_mv3d_img.py:191-209) applied to img_index.
     Returns dict(img_index [3,N] f64, bv_index [N,2] i64, M_val [N] f64,
     frame_n [F]; number_buffer [N] i32 + frame_nvox [F]), capacity layout."""
     import ctypes
@@ -57,6 +59,8 @@ def mv3d_voxels_batch(points, point_offsets, img_index2=None, P=None, ranges=PED
         img_index2 = img_index2.to(torch.int64).contiguous()
     if P is not None:
         P = P.to(torch.float64).contiguous()
+    if fv_aug is not None:
+        fv_aug = torch.as_tensor(fv_aug, dtype=torch.float64).to(dev).reshape(-1, 3).contiguous()
     F = int(point_offsets.numel()) - 1
     N = int(points.shape[0])
     cap = max(N, 1)
@@ -71,7 +75,8 @@ def mv3d_voxels_batch(points, point_offsets, img_index2=None, P=None, ranges=PED
     ws = L.workspace(nbytes.value, dev)
     rng = np.ascontiguousarray(ranges, dtype=np.float64)
     L.check(L.lib().shpl_mv3d_voxels(F, L.ptr(point_offsets), N, L.ptr(points), int(points.stride(0)),
-                                     L.ptr(img_index2), L.ptr(P), rng.ctypes.data_as(ctypes.c_void_p), float(res),
+                                     L.ptr(img_index2), L.ptr(P), L.ptr(fv_aug), rng.ctypes.data_as(ctypes.c_void_p),
+                                     float(res),
                                      float(zres), int(voxel_point_count), L.ptr(img), cap, L.ptr(bv), L.ptr(mv),
                                      L.ptr(fn), L.ptr(nb), L.ptr(nvox), L.ptr(ws), ws.numel(),
                                      L.stream_of(dev)), "shpl_mv3d_voxels")
@@ -80,7 +85,7 @@ def mv3d_voxels_batch(points, point_offsets, img_index2=None, P=None, ranges=PED
 
 
 def mv3d_sparse_pooling_input(points, img_index2=None, P=None, ranges=PED_RANGES, res=0.2, zres=0.4,
-                              voxel_point_count=45):
+                              voxel_point_count=45, fv_aug=None):
     """One frame: (img_index [3,n'], bv_index [n',2], M_val [n']) as
     point_cloud_2_top_sparse returns them (construct_voxel.py:156-162)."""
     import numpy as np
@@ -90,6 +95,7 @@ def mv3d_sparse_pooling_input(points, img_index2=None, P=None, ranges=PED_RANGES
     off = torch.tensor([0, pts.shape[0]], dtype=torch.int64, device=dev)
     i2 = None if img_index2 is None else torch.as_tensor(np.ascontiguousarray(img_index2, dtype=np.int64)).to(dev)
     Pd = None if P is None else torch.as_tensor(np.asarray(P, dtype=np.float64).reshape(1, 12)).to(dev)
-    out = mv3d_voxels_batch(pts, off, i2, Pd, ranges, res, zres, voxel_point_count)
+    out = mv3d_voxels_batch(pts, off, i2, Pd, ranges, res, zres, voxel_point_count,
+                            fv_aug=None if fv_aug is None else np.asarray(fv_aug, dtype=np.float64).reshape(1, 3))
     k = int(out["frame_n"][0].item())
     return out["img_index"][:, :k], out["bv_index"][:k], out["M_val"][:k]

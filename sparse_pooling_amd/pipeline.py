@@ -188,15 +188,30 @@ class FramePipeline(FusedPipeline):
                 "shpl_bev_workspace_bytes")
         self.bev_ws = L.workspace(nb.value, self.dev)
         self.bev = None
+        self._velo_ws = None
 
-    def build_bev(self, points, point_offsets, planes):
+    def build_bev(self, points, point_offsets, planes, point_counts=None):
         from . import bev as _bev
         self.bev = _bev.bev_slices_batch(points, point_offsets, planes, *self.bev_args, maps=self.maps,
-                                         ws=self.bev_ws)
+                                         ws=self.bev_ws, point_counts=point_counts)
         return self.bev
 
-    def frame_step(self, points, point_offsets, planes, P, bev_feat, img_feat):
-        b = self.build_bev(points, point_offsets, planes)
+    def frame_step(self, points, point_offsets, planes, P, bev_feat, img_feat, point_counts=None):
+        b = self.build_bev(points, point_offsets, planes, point_counts)
         self.build_index(b.pts_in_voxel, b.voxel_indices, point_offsets, P, point_counts=b.frame_nvox)
         self.build_csr()
         self.layer(bev_feat, img_feat)
+
+    def velo_step(self, frames, bev_feat, img_feat):
+        """Raw KITTI scans (kitti.KittiFrames) -> camera-frame clouds (shpl_velo_to_cam)
+        -> BEV slices -> M -> fused layer, all on the device (kitti_dataset.py:285-379)."""
+        if self._velo_ws is None:
+            import ctypes
+            nb = ctypes.c_size_t()
+            L.check(self._lib.shpl_velo_workspace_bytes(frames.n_frames, frames.max_points, ctypes.byref(nb)),
+                    "shpl_velo_workspace_bytes")
+            self._velo_ws = L.workspace(nb.value, self.dev)
+            self._velo_pts = torch.empty((max(self.N, 1), 3), dtype=torch.float64, device=self.dev)
+        self.velo = frames.point_clouds(ws=self._velo_ws, out=self._velo_pts)
+        self.frame_step(self.velo.points, frames.point_offsets, frames.planes, frames.P2, bev_feat, img_feat,
+                        point_counts=self.velo.counts)

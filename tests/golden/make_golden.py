@@ -16,8 +16,13 @@ Reference functions executed (file:line, relative to /root/reference):
 * ``BevSlices.generate_bev(output_indices=True)``
                                       avod/avod/core/bev_generators/bev_slices.py:33-156
 * MV3D ``point_cloud_2_top_sparse``   MV3D_TF_release/lib/utils/construct_voxel.py:37-162
+* ``obj_utils.get_lidar_point_cloud``  avod/wavedata/wavedata/tools/obj_detection/obj_utils.py:220-268
+  (``calib_utils.read_calibration`` / ``read_lidar`` / ``lidar_to_cam_frame``,
+  calib_utils.py:55-112, 328-410), ``obj_utils.get_road_plane`` :271-303 and
+  ``kitti_aug.flip_point_cloud`` / ``flip_stereo_calib_p2`` / ``flip_ground_plane``
+  (avod/avod/datasets/kitti/kitti_aug.py:24-29, 88-121) on synthetic KITTI files
 
-Run:  python tests/golden/make_golden.py
+Run:  python tests/golden/make_golden.py [case ...]   (e.g. ``kitti``; no argument: all)
 """
 import os
 import sys
@@ -176,6 +181,76 @@ def _mv3d_voxel_case(dense=False):
           f"capped={(vd['number_buffer'] >= 45).sum()}")
 
 
+KITTI_CALIB = {  # KITTI object-detection calib layout (values of a typical left-camera setup)
+    "P0": [7.215377e+02, 0, 6.095593e+02, 0, 0, 7.215377e+02, 1.728540e+02, 0, 0, 0, 1, 0],
+    "P1": [7.215377e+02, 0, 6.095593e+02, -3.875744e+02, 0, 7.215377e+02, 1.728540e+02, 0, 0, 0, 1, 0],
+    "P2": [7.215377e+02, 0, 6.095593e+02, 4.485728e+01, 0, 7.215377e+02, 1.728540e+02, 2.163791e-01,
+           0, 0, 1, 2.745884e-03],
+    "P3": [7.215377e+02, 0, 6.095593e+02, -3.395242e+02, 0, 7.215377e+02, 1.728540e+02, 2.199936e+00,
+           0, 0, 1, 2.729905e-03],
+    "R0_rect": [9.999239e-01, 9.837760e-03, -7.445048e-03, -9.869795e-03, 9.999421e-01, -4.278459e-03,
+                7.402527e-03, 4.351614e-03, 9.999631e-01],
+    "Tr_velo_to_cam": [7.533745e-03, -9.999714e-01, -6.166020e-04, -4.069766e-03, 1.480249e-02,
+                       7.280733e-04, -9.998902e-01, -7.631618e-02, 9.998621e-01, 7.523790e-03,
+                       1.480755e-02, -2.717806e-01],
+    "Tr_imu_to_velo": [9.999976e-01, 7.553071e-04, -2.035826e-03, -8.086759e-01, -7.854027e-04,
+                       9.998898e-01, -1.482298e-02, 3.195559e-01, 2.024406e-03, 1.482454e-02,
+                       9.998881e-01, -7.997231e-01],
+}
+
+
+def synthetic_scan(rng, n):
+    """A 64-beam-like velodyne sweep in the lidar frame (x fwd, y left, z up), f32 x 4."""
+    az = rng.uniform(-np.pi, np.pi, n)
+    el = np.deg2rad(rng.uniform(-24.8, 2.0, n))
+    rng_m = rng.uniform(2.0, 80.0, n)
+    xyz = np.stack([rng_m * np.cos(el) * np.cos(az), rng_m * np.cos(el) * np.sin(az), rng_m * np.sin(el)], 1)
+    xyz[:, 2] = np.maximum(xyz[:, 2], -1.73 + rng.normal(0, 0.02, n))  # ground
+    return np.concatenate([xyz, rng.uniform(0, 1, (n, 1))], 1).astype(np.float32)
+
+
+def _kitti_case():
+    """obj_utils.get_lidar_point_cloud / calib_utils.read_calibration /
+    get_road_plane + the kitti_aug flips on synthetic KITTI files."""
+    import tempfile
+    from wavedata.tools.core import calib_utils
+    from wavedata.tools.obj_detection import obj_utils
+    from avod.datasets.kitti import kitti_aug
+    rng = np.random.default_rng(21)
+    rec = {}
+    with tempfile.TemporaryDirectory() as d:
+        for sub in ("calib", "velodyne", "planes"):
+            os.makedirs(os.path.join(d, sub))
+        for idx, (n, plane_b_sign, shape) in {7: (5000, -1, (375, 1242)), 8: (4000, 1, (376, 1241))}.items():
+            calib = dict(KITTI_CALIB)
+            if idx == 8:  # a second camera geometry
+                calib["P2"] = list(np.array(calib["P2"]) * np.array([1, 1, 1.0003, 1, 1, 1, 0.999, 1, 1, 1, 1, 1]))
+            text = "".join(f"{k}: " + " ".join(f"{v:.12e}" for v in vals) + "\n" for k, vals in calib.items())
+            with open(os.path.join(d, "calib", "%06d.txt" % idx), "w") as fh:
+                fh.write(text)
+            scan = synthetic_scan(rng, n)
+            scan.tofile(os.path.join(d, "velodyne", "%06d.bin" % idx))
+            plane = np.array([-1.851372e-02, plane_b_sign * 9.998285e-01, -5.362401e-04, 1.678541e+00])
+            ptext = "# Plane\nWidth 4\nHeight 1\n" + " ".join(f"{v:e}" for v in plane) + "\n"
+            with open(os.path.join(d, "planes", "%06d.txt" % idx), "w") as fh:
+                fh.write(ptext)
+            fc = calib_utils.read_calibration(os.path.join(d, "calib"), idx)
+            im_size = [shape[1], shape[0]]  # kitti_utils.get_point_cloud: (w, h)
+            pc = obj_utils.get_lidar_point_cloud(idx, os.path.join(d, "calib"), os.path.join(d, "velodyne"),
+                                                 im_size=im_size)
+            pc_all = obj_utils.get_lidar_point_cloud(idx, os.path.join(d, "calib"), os.path.join(d, "velodyne"))
+            gp = obj_utils.get_road_plane(idx, os.path.join(d, "planes"))
+            rec.update({f"{idx}_calib_text": np.array(text), f"{idx}_plane_text": np.array(ptext),
+                        f"{idx}_velo": scan, f"{idx}_image_shape": np.array(shape),
+                        f"{idx}_p2": fc.p2, f"{idx}_r0_rect": fc.r0_rect, f"{idx}_tr": fc.tr_velodyne_to_cam,
+                        f"{idx}_point_cloud": pc, f"{idx}_point_cloud_all": pc_all, f"{idx}_ground_plane": gp,
+                        f"{idx}_flip_point_cloud": kitti_aug.flip_point_cloud(pc),
+                        f"{idx}_flip_p2": kitti_aug.flip_stereo_calib_p2(fc.p2, shape),
+                        f"{idx}_flip_ground_plane": kitti_aug.flip_ground_plane(gp)})
+            print(f"kitti {idx}: scan {n} -> FOV {pc.shape[1]} points; plane {gp}")
+    np.savez_compressed(os.path.join(HERE, "kitti_frames.npz"), **rec)
+
+
 def main():
     _install_stubs()
     c1 = synth.CONFIG1
@@ -204,7 +279,13 @@ def main():
     _bev_slices_case()
     _mv3d_voxel_case()
     _mv3d_voxel_case(dense=True)
+    _kitti_case()
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1:  # regenerate only the named cases, e.g. `kitti`
+        _install_stubs()
+        for name in sys.argv[1:]:
+            globals()[f"_{name}_case"]()
+    else:
+        main()

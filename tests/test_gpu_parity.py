@@ -520,3 +520,101 @@ def test_mv3d_chain_to_pooling():
                            [1, 100, 120, 8])
     e = orc.sparse_pool_op(ref["Mij_pool"], ref["M_val"], ref["M_size"], feat, ref["img_index_flip_pool"])
     _close_and_exact(out, e.reshape(1, 100, 120, 8))
+
+
+def test_mv3d_augment_fv_index_transform():
+    """augment_fv's img_index transform (minibatch_mv3d_img.py:205-206) fused into the producer."""
+    from sparse_pooling_amd import mv3d
+    g = np.load(os.path.join(GOLD, "mv3d_voxel.npz"))
+    for ratio, sx, sy in ((1.0312, 3.7, 8.25), (0.9514, 0.0, 9.99)):
+        img, _, _ = mv3d.mv3d_sparse_pooling_input(g["points"], img_index2=g["img_index2"], fv_aug=(ratio, sx, sy))
+        np.testing.assert_array_equal(_np(img), orc.augment_fv_index(g["img_index"], ratio, sx, sy))
+
+
+# ---------------------------------------------------------------- KITTI loader (§8f item 3)
+
+def test_kitti_loader_vs_reference_golden(kitti_dir):
+    """get_lidar_point_cloud from the KITTI files, transform + FOV filter on the device."""
+    from sparse_pooling_amd import kitti
+    d, g = kitti_dir
+    for idx in (7, 8):
+        h, w = g[f"{idx}_image_shape"]
+        pc = kitti.get_lidar_point_cloud(idx, os.path.join(d, "calib"), os.path.join(d, "velodyne"), im_size=[w, h])
+        np.testing.assert_array_equal(_np(pc), g[f"{idx}_point_cloud"])
+        pa = kitti.get_lidar_point_cloud(idx, os.path.join(d, "calib"), os.path.join(d, "velodyne"))
+        np.testing.assert_array_equal(_np(pa), g[f"{idx}_point_cloud_all"])
+    fr = kitti.KittiFrames(os.path.join(d, "calib"), os.path.join(d, "velodyne"), os.path.join(d, "planes"),
+                           [7, 8, 7], [tuple(g["7_image_shape"]), tuple(g["8_image_shape"]),
+                                       tuple(g["7_image_shape"])], flips=[False, True, True])
+    b = fr.point_clouds()
+    torch.cuda.synchronize()
+    off, n = _np(fr.point_offsets), _np(b.counts)
+    want = [g["7_point_cloud"], g["8_flip_point_cloud"], g["7_flip_point_cloud"]]
+    for f in range(3):
+        np.testing.assert_array_equal(_np(b.points[off[f]:off[f] + n[f]]).T, want[f])
+        assert np.isnan(_np(b.points[off[f] + n[f]:off[f + 1]])).all()
+    np.testing.assert_array_equal(_np(fr.planes[1]), g["8_flip_ground_plane"])
+    np.testing.assert_array_equal(_np(fr.P2[1]), g["8_flip_p2"])
+
+
+def test_kitti_loader_batch_vs_oracle():
+    """Scans of ragged sizes across the 4096-point chunks, the intensity filter, flips."""
+    from sparse_pooling_amd import kitti
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("mg", os.path.join(GOLD, "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    rng = np.random.default_rng(5)
+    sizes = [4097, 1, 0, 12000, 4096, 30000]
+    scans = [mg.synthetic_scan(rng, n) if n else np.zeros((0, 4), np.float32) for n in sizes]
+    fc = kitti.FrameCalibrationData()
+    fc.r0_rect = np.array(mg.KITTI_CALIB["R0_rect"]).reshape(3, 3)
+    fc.tr_velodyne_to_cam = np.array(mg.KITTI_CALIB["Tr_velo_to_cam"]).reshape(3, 4)
+    rect = kitti.rect_matrix(fc)
+    P = np.array(mg.KITTI_CALIB["P2"]).reshape(3, 4)
+    flips = [0, 1, 0, 1, 0, 0]
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    xyzi = torch.from_numpy(np.concatenate(scans)).to(DEV)
+    for mi in (None, 0.35):
+        b = kitti.velo_to_cam_batch(xyzi, torch.from_numpy(off).to(DEV), np.stack([rect] * 6), np.stack([P] * 6),
+                                    [[1242, 375]] * 6, min_intensity=mi, flip=flips)
+        torch.cuda.synchronize()
+        n = _np(b.counts)
+        for f in range(6):
+            e = orc.velo_to_cam(scans[f], rect, P, [1242, 375], min_intensity=mi, flip=flips[f])
+            np.testing.assert_array_equal(_np(b.points[off[f]:off[f] + n[f]]).T, e)
+        assert int(b.err.item()) == 0
+
+
+def test_velodyne_to_fused_layer_pipeline(kitti_dir):
+    """KITTI files -> device velodyne loader -> BEV slices -> index -> sorted M -> fused
+    layer (kitti_dataset.py:285-379), against the oracle chain."""
+    from sparse_pooling_amd import kitti, pipeline
+    d, g = kitti_dir
+    shapes = [tuple(g["7_image_shape"]), tuple(g["8_image_shape"])]
+    fr = kitti.KittiFrames(os.path.join(d, "calib"), os.path.join(d, "velodyne"), os.path.join(d, "planes"),
+                           [7, 8], shapes, flips=[False, True])
+    im_size, stride, C = (1242, 375), (4, 4), 8
+    pl = pipeline.FramePipeline(2, fr.total_points, im_size, synth.AREA_EXTENTS, synth.VOXEL_SIZE,
+                                synth.HEIGHT_LO, synth.HEIGHT_HI, synth.NUM_SLICES, stride, C, C, dual=True,
+                                max_points_per_frame=fr.max_points)
+    bev = synth.make_features((2, pl.Hb, pl.Wb, C), 3)
+    img = synth.make_features((2, pl.Hi, pl.Wi, C), 4)
+    pl.velo_step(fr, torch.from_numpy(bev).to(DEV), torch.from_numpy(img).to(DEV))
+    torch.cuda.synchronize()
+    assert int(pl.err.item()) == 0 and int(pl.bev.err.item()) == 0
+    out, iout = _np(pl.bv_fused), _np(pl.img_fused)
+    clouds = [g["7_point_cloud"], g["8_flip_point_cloud"]]
+    planes = [g["7_ground_plane"], g["8_flip_ground_plane"]]
+    Ps = [g["7_p2"], g["8_flip_p2"]]
+    for f in range(2):
+        hm, dm, vox, upts = orc.bev_slices(clouds[f], planes[f], synth.AREA_EXTENTS, synth.VOXEL_SIZE,
+                                           synth.HEIGHT_LO, synth.HEIGHT_HI, synth.NUM_SLICES)
+        np.testing.assert_array_equal(_np(pl.bev.height_maps[f]), hm)
+        gi = orc.gen_sparse_pooling_input_avod(upts, vox, Ps[f], list(im_size), (hm.shape[1], hm.shape[2]))
+        ref = orc.produce_sparse_pooling_input(gi, stride=stride)
+        assert int(_np(pl.frame_nnz)[f]) == ref["Mij_pool"].shape[0] > 0
+        eb, ei = orc.sparse_pool_layer(bev[f:f + 1], img[f:f + 1], ref["Mij_pool"], ref["M_val"], ref["M_size"],
+                                       ref["img_index_flip_pool"], dual=True)
+        _close_and_exact(out[f:f + 1], eb)
+        _close_and_exact(iout[f:f + 1], ei)

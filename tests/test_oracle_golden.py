@@ -164,3 +164,38 @@ def test_mv3d_oracle_matches_reference(golden_dir, name):
     np.testing.assert_array_equal(bv, g["bv_index"])
     np.testing.assert_array_equal(mv, g["M_val"])
     np.testing.assert_array_equal(nb, g["number_buffer"])
+
+
+# ---------------------------------------------------------------- KITTI loader (§8f item 3)
+
+def test_kitti_host_readers_vs_reference_golden(kitti_dir):
+    from sparse_pooling_amd import kitti
+    d, g = kitti_dir
+    for idx in (7, 8):
+        fc = kitti.read_calibration(os.path.join(d, "calib"), idx)
+        np.testing.assert_array_equal(fc.p2, g[f"{idx}_p2"])
+        np.testing.assert_array_equal(fc.r0_rect, g[f"{idx}_r0_rect"])
+        np.testing.assert_array_equal(fc.tr_velodyne_to_cam, g[f"{idx}_tr"])
+        gp = kitti.get_road_plane(idx, os.path.join(d, "planes"))
+        np.testing.assert_array_equal(gp, g[f"{idx}_ground_plane"])
+        np.testing.assert_array_equal(kitti.flip_ground_plane(gp), g[f"{idx}_flip_ground_plane"])
+        np.testing.assert_array_equal(kitti.flip_stereo_calib_p2(fc.p2, tuple(g[f"{idx}_image_shape"])),
+                                      g[f"{idx}_flip_p2"])
+        x, y, z, i = kitti.read_lidar(os.path.join(d, "velodyne"), idx)
+        np.testing.assert_array_equal(np.stack([x, y, z, i], 1), g[f"{idx}_velo"])
+        np.testing.assert_array_equal(kitti.rect_matrix(fc), orc.rect_matrix(fc.r0_rect, fc.tr_velodyne_to_cam))
+    assert kitti.read_lidar(os.path.join(d, "velodyne"), 99) == []
+
+
+def test_kitti_oracle_vs_reference_golden(kitti_dir):
+    """get_lidar_point_cloud with and without the image filter, and flip_point_cloud,
+    restated in C, against the reference run on the same files."""
+    _, g = kitti_dir
+    for idx in (7, 8):
+        rect = orc.rect_matrix(g[f"{idx}_r0_rect"], g[f"{idx}_tr"])
+        h, w = g[f"{idx}_image_shape"]
+        pc = orc.velo_to_cam(g[f"{idx}_velo"], rect, g[f"{idx}_p2"], [w, h])
+        np.testing.assert_array_equal(pc, g[f"{idx}_point_cloud"])
+        np.testing.assert_array_equal(orc.velo_to_cam(g[f"{idx}_velo"], rect), g[f"{idx}_point_cloud_all"])
+        np.testing.assert_array_equal(orc.velo_to_cam(g[f"{idx}_velo"], rect, g[f"{idx}_p2"], [w, h], flip=True),
+                                      g[f"{idx}_flip_point_cloud"])
