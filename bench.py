@@ -56,6 +56,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the layer's streaming pass after the index build instead of beside it")
+    ap.add_argument("--workload", default="layer", choices=["layer", "frames"],
+                    help="layer: BASELINE configs 2/3/5 from prepared points + voxel indices (default); "
+                         "frames: raw velodyne scans -> loader -> BEV slices -> index -> fused layer")
+    ap.add_argument("--scan-points", type=int, default=120000, help="points per velodyne scan (frames)")
     return ap.parse_args()
 
 
@@ -130,6 +134,12 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from sparse_pooling_amd import dist as sd, pipeline, synth
+
+    if args.workload == "frames":
+        run_frames(args, world, rank, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     cfg = args.config
     spec = synth.CONFIGS[cfg]
@@ -258,6 +268,108 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def cpu_baseline_frames(frames_np, calib, plane, im_size, c, budget_s):
+    """Oracle chain of the frames workload on one core: velodyne -> camera frame + FOV
+    filter -> BEV slices (maps + voxel indices) -> gen + produce -> pool + concat."""
+    from oracle import shpl_oracle as orc
+    from sparse_pooling_amd import synth
+    rect = orc.rect_matrix(calib.r0_rect, calib.tr_velodyne_to_cam)
+    nx, nz = 800, 700
+    rng = np.random.default_rng(0)
+    bev = rng.standard_normal((1, nz, nx, c), dtype=np.float32)
+    img = rng.standard_normal((1, im_size[1], im_size[0], c), dtype=np.float32)
+    t = {"load": 0.0, "bev": 0.0, "index": 0.0, "pool": 0.0}
+    done = 0
+    t0 = time.perf_counter()
+    while done < 2 or (time.perf_counter() - t0 < budget_s and done < len(frames_np)):
+        a = time.perf_counter()
+        pc = orc.velo_to_cam(frames_np[done % len(frames_np)], rect, calib.p2, im_size)
+        b = time.perf_counter()
+        hm, dm, vox, upts = orc.bev_slices(pc, plane, synth.AREA_EXTENTS, synth.VOXEL_SIZE, synth.HEIGHT_LO,
+                                           synth.HEIGHT_HI, synth.NUM_SLICES)
+        cc = time.perf_counter()
+        g = orc.gen_sparse_pooling_input_avod(upts, vox, calib.p2, list(im_size), (nz, nx))
+        ref = orc.produce_sparse_pooling_input(g, stride=(1, 1))
+        d = time.perf_counter()
+        orc.sparse_pool_layer(bev, img, ref["Mij_pool"], ref["M_val"], ref["M_size"], ref["img_index_flip_pool"])
+        e = time.perf_counter()
+        t["load"] += b - a
+        t["bev"] += cc - b
+        t["index"] += d - cc
+        t["pool"] += e - d
+        done += 1
+    total = sum(t.values())
+    return {"value": round(done / total, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": (f"{done} scans through oracle/shpl_oracle.c, single thread: velodyne->camera + FOV "
+                       f"{1e3 * t['load'] / done:.2f} ms, BEV slices {1e3 * t['bev'] / done:.2f} ms, index "
+                       f"{1e3 * t['index'] / done:.2f} ms, pooling + concat {1e3 * t['pool'] / done:.2f} ms per "
+                       f"frame; {os.cpu_count()} host cpus visible")}
+
+
+def run_frames(args, world, rank, dev):
+    """Raw-scan workload: the whole per-frame SHPL path of kitti_dataset.py:285-379 +
+    rpn_model.py's fused layer, from velodyne scans resident in HBM."""
+    from sparse_pooling_amd import dist as sd, kitti, pipeline, synth
+    F = args.frames or 64
+    C = 32
+    h, w = synth.KITTI_IMAGE_SHAPE
+    im_size = (w, h)
+    fr = kitti.synthetic_frames(F, args.scan_points, seed=1000 + rank, device=dev)
+    pl = pipeline.FramePipeline(F, fr.total_points, im_size, synth.AREA_EXTENTS, synth.VOXEL_SIZE,
+                                synth.HEIGHT_LO, synth.HEIGHT_HI, synth.NUM_SLICES, (1, 1), C, C, device=dev,
+                                max_points_per_frame=fr.max_points)
+    g = torch.Generator(device=dev)
+    g.manual_seed(4321 + rank)
+    bev = torch.randn((F, pl.Hb, pl.Wb, C), device=dev, generator=g)
+    img = torch.randn((F, pl.Hi, pl.Wi, C), device=dev, generator=g)
+    side = torch.cuda.Stream(device=dev)
+    for _ in range(args.warmup):
+        pl.velo_step(fr, bev, img, side=side)
+    torch.cuda.synchronize()
+    nnz = int(pl.frame_nnz.sum().item())
+    u_pix = int(torch.unique(pl.pix[pl.pix >= 0]).numel())
+    n_cam = int(pl.velo.counts.sum().item())
+    n_vox = int(pl.bev.frame_nvox.sum().item())
+    errs = int(pl.err.item()) | int(pl.bev.err.item()) | int(pl.velo.err.item())
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(9)] for _ in range(args.steps)]
+    elapsed = sd.timed(lambda k: pl.velo_step(fr, bev, img, side=side, events=evs[k]), args.steps, device=dev)
+    mean = lambda i, j: sum(e[i].elapsed_time(e[j]) for e in evs) / args.steps  # noqa: E731
+    dense_ms, sparse_ms = mean(0, 1), mean(7, 8)
+    stages = {"velo_to_cam_ms": mean(2, 3), "bev_slices_ms": mean(3, 4), "index_ms": mean(4, 5),
+              "csr_ms": mean(5, 6), "k_dense_ms": dense_ms, "k_sparse_ms": sparse_ms}
+    nbytes = pull_bytes(F * pl.Hb * pl.Wb, C, C, u_pix, nnz, 4, 2 * C)
+    achieved = nbytes / ((dense_ms + sparse_ms) * 1e-3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        scans = [fr.xyzi[int(fr.point_offsets[f]):int(fr.point_offsets[f + 1])].cpu().numpy() for f in range(min(F, 8))]
+        calib = kitti.FrameCalibrationData()
+        c = synth.KITTI_CALIB
+        calib.p2 = np.array(c["P2"]).reshape(3, 4)
+        calib.r0_rect = np.array(c["R0_rect"]).reshape(3, 3)
+        calib.tr_velodyne_to_cam = np.array(c["Tr_velo_to_cam"]).reshape(3, 4)
+        cpu = cpu_baseline_frames(scans, calib, fr.planes[0].cpu().numpy(), im_size, C, args.cpu_seconds)
+    if rank == 0:
+        out = {
+            "metric": "SHPL frames/sec from raw velodyne scans (loader + BEV slices + index + fused layer)",
+            "value": round(F * world * args.steps / elapsed, 2), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded 64-beam-like velodyne scans, KITTI calib; no dataset on the box)",
+            "config": {"workload": (f"frames: {args.scan_points} pts/scan -> {n_cam / F:.0f} FOV pts -> "
+                                    f"{n_vox / F:.0f} BEV voxel pts -> {nnz / F:.0f} M entries; BEV "
+                                    f"{pl.Hb}x{pl.Wb}x{C} (5 slices + density maps), img {pl.Hi}x{pl.Wi}x{C}, "
+                                    "img->BEV fused layer"),
+                       "frames_per_gpu_per_step": F, "parallelism": f"frame-sharded x{world}"},
+            "stages_ms": {k: round(v, 4) for k, v in stages.items()},
+            "roofline": {"bound": "hbm", "kernel": "k_dense + k_sparse (fused layer)", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None, "algorithmic_bytes_per_launch": nbytes},
+            "cpu_baseline": cpu,
+            "index_errors": errs,
+        }
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

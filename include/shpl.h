@@ -157,7 +157,8 @@ int shpl_produce_index(int64_t nv, const void *d_bv_index, int bv_itype, int64_t
  *                  as the reference does (height_lo + s*hpd, + hpd)
  *   density_lo/hi  offsets of the density map's slice (height_lo, height_hi)
  *   density_table  host [16]: min(1, log(n+1)/norm_value), n >= 15 saturates
- * Outputs (capacity N, frame f at [off[f], off[f] + d_frame_nvox[f]), -1 after):
+ * Outputs (capacity N, frame f at [off[f], off[f] + d_frame_nvox[f]); the rest
+ * of the frame's slots is left untouched):
  *   d_voxel_indices [N,2] i32 = reference voxel_indices_rot rows (x, nz - z)
  *   d_pts_in_voxel  [N,3] f64 = the first point of each cell (unique_pts)
  *   d_height_maps   optional [n_frames, num_slices, nz, nx] f64 (rotated like the reference)

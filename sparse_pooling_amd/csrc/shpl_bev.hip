@@ -175,10 +175,6 @@ __global__ __launch_bounds__(BEV_BLOCK) void k_bev_frame(BevGeom g, const int64_
         __syncthreads();
     }
     if (threadIdx.x == 0) frame_nvox[f] = kept < cap ? kept : cap;
-    for (int64_t pos = kept + threadIdx.x; pos < cap; pos += BEV_BLOCK) {
-        vox_out[2 * (p0 + pos)] = -1;
-        vox_out[2 * (p0 + pos) + 1] = -1;
-    }
 }
 
 }  // namespace

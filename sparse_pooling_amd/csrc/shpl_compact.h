@@ -3,8 +3,9 @@
 // into chunks of IDX_CHUNK points, one 1024-thread workgroup per chunk.
 //   k_count   -- kept points per chunk (Stage::load + Stage::eval)
 //   k_compact -- the chunk's kept points land after those of the frame's
-//                earlier chunks, in point order; the frame's last chunk writes
-//                the sentinels of the unused capacity and the frame's count.
+//                earlier chunks, in point order; each chunk also writes the
+//                sentinels of the unused capacity in its stretch of slots, and
+//                the frame's last chunk the frame's count.
 // A Stage provides: In/Payload types, load(i, in), eval(f, i, in, pl) -> keep,
 // touch(f, i, pl, keep) (every point, write pass), emit(f, i, pos, fstart, pl)
 // and hole(pos).
@@ -70,23 +71,33 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr) {
 
 // Pass 2 (same grid): the chunk's kept points land after those of the
 // frame's earlier chunks, in point order (a stable compaction); rows of the
-// chunk are ranked in order by wave ballots + an LDS prefix. The frame's
-// last chunk also writes the sentinels of the unused capacity and the
-// frame's entry count.
+// chunk are ranked in order by wave ballots + an LDS prefix. Each chunk also
+// writes the sentinels of the unused capacity that falls in its stretch of
+// slots, and the frame's last chunk the frame's entry count.
 template <typename Stage>
 __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr) {
     __shared__ int32_t wsum[IDX_BATCH][IDX_BLOCK / 64];
-    __shared__ int32_t pre[IDX_BLOCK / 64];
+    __shared__ int32_t pre[IDX_BLOCK / 64], all[IDX_BLOCK / 64];
     const int f = blockIdx.y, j = blockIdx.x;
     int64_t p0, p1, cap_end;
     frame_range(fr, f, p0, p1, cap_end);
     const int wid = threadIdx.x >> 6;
-    // kept points of the earlier chunks
-    int32_t mine = 0;
-    for (int q = threadIdx.x; q < j; q += IDX_BLOCK) mine += fr.chunk_kept[(int64_t)f * fr.n_chunks + q];
+    // kept points of the earlier chunks, and of the whole frame
+    int32_t mine = 0, every = 0;
+    for (int q = threadIdx.x; q < fr.n_chunks; q += IDX_BLOCK) {
+        const int32_t c = fr.chunk_kept[(int64_t)f * fr.n_chunks + q];
+        mine += q < j ? c : 0;
+        every += c;
+    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
-    if ((threadIdx.x & 63) == 0) pre[wid] = mine;
+    for (int o = 32; o > 0; o >>= 1) {
+        mine += __shfl_xor(mine, o, 64);
+        every += __shfl_xor(every, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        pre[wid] = mine;
+        all[wid] = every;
+    }
     const int64_t base = p0 + (int64_t)j * IDX_CHUNK;
     typename Stage::In in[IDX_BATCH];
     typename Stage::Payload pl[IDX_BATCH];
@@ -123,10 +134,15 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr) {
         if (keep[u]) st.emit(f, i, p0 + kept + before + lane_rank(m[u]), p0, pl[u]);
         kept += tot;
     }
+    // sentinels of the unused capacity [p0 + total, cap_end), each chunk its own stretch
+    int64_t total = 0;
+    for (int w = 0; w < IDX_BLOCK / 64; ++w) total += all[w];
+    const int64_t h0 = p0 + total > base ? p0 + total : base;
+    const int64_t h1 = j == fr.n_chunks - 1 ? cap_end : (base + IDX_CHUNK < cap_end ? base + IDX_CHUNK : cap_end);
+    for (int64_t pos = h0 + threadIdx.x; pos < h1; pos += IDX_BLOCK) st.hole(pos);
     if (j != fr.n_chunks - 1) return;
-    for (int64_t pos = p0 + kept + threadIdx.x; pos < cap_end; pos += IDX_BLOCK) st.hole(pos);
     if (threadIdx.x == 0) {
-        if (fr.frame_nnz) fr.frame_nnz[f] = kept;
+        if (fr.frame_nnz) fr.frame_nnz[f] = total;
         if (fr.frame_out_off) {
             fr.frame_out_off[f] = p0;
             if (f == fr.n_frames - 1) fr.frame_out_off[fr.n_frames] = cap_end;

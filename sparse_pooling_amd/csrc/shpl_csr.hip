@@ -119,12 +119,58 @@ __device__ __forceinline__ void keys_batch(const CsrIn &c, int64_t first, int64_
 //     With identity columns (or ORDER_ENTRY) the packed word alone orders a
 //     tile; the words are then staged in LDS windows so that the quadratic
 //     count reads LDS, not HBM.
+// Unused capacity of every frame, [off[f] + nnz[f], off[f+1]), and the slots
+// past the last frame: empty (dst = -1), skipped by the pulls. Done by extra
+// workgroups of the CSR launch (blockIdx.x >= n_frames), each clearing a span
+// of HOLE_SPAN slots beside the sorting workgroups; they need only the index
+// builder's frame counts, not the sort.
+constexpr int HOLE_SPAN = 16384;
+
+__device__ void clear_unused(const CsrIn &c, int64_t nnz_cap, int32_t *ent_dst, int span) {
+    __shared__ int f0s;
+    const int64_t b0 = (int64_t)span * HOLE_SPAN;
+    if (threadIdx.x == 0) {
+        int lo = 0, hi = c.n_frames;  // last f with frame_off[f] <= b0 (n_frames: past the last frame)
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) / 2;
+            if (c.frame_off[mid] <= b0)
+                lo = mid;
+            else
+                hi = mid - 1;
+        }
+        f0s = lo;
+    }
+    __syncthreads();
+    const int64_t b1 = b0 + HOLE_SPAN < nnz_cap ? b0 + HOLE_SPAN : nnz_cap;
+    int f = f0s;
+    int64_t fend = 0, live = 0;
+    auto bounds = [&]() {
+        if (f < c.n_frames) {
+            fend = c.frame_off[f + 1];
+            const int64_t l = c.frame_off[f] + c.frame_nnz[f];
+            live = l < fend ? l : fend;
+        }
+    };
+    bounds();
+    for (int64_t d = b0 + threadIdx.x; d < b1; d += CSR_BLOCK) {
+        while (f < c.n_frames && d >= fend) {
+            ++f;
+            bounds();
+        }
+        if (f >= c.n_frames || d >= live) ent_dst[d] = -1;
+    }
+}
+
 template <bool HAS_COL>
 __global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, uint64_t *tmp, int64_t nnz_cap, int32_t *ent_dst,
                                                          int32_t *ent_src, float *ent_val, int32_t *ent_col) {
     __shared__ int32_t cnt[CSR_TILES];
     __shared__ int32_t wsum[CSR_BLOCK / 64];
     __shared__ uint64_t win[CSR_WIN];
+    if ((int)blockIdx.x >= c.n_frames) {
+        clear_unused(c, nnz_cap, ent_dst, (int)blockIdx.x - c.n_frames);
+        return;
+    }
     const int f = blockIdx.x;
     const int64_t e0 = c.frame_off[f];
     const int64_t cap_end = c.frame_off[f + 1];
@@ -269,9 +315,11 @@ __global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, uint64_t *tmp,
             if (ent_col) ent_col[d] = k;
         }
     }
-    // empty slots of this frame's capacity, and past the last frame
-    int64_t hole_end = cap_end;
-    if (f == c.n_frames - 1) hole_end = nnz_cap;
+    // Slots of invalid entries (flagged upstream) become empty here; the unused
+    // capacity past the frame's live entries is cleared by the launch's extra
+    // workgroups (frame_nnz given), or here (no frame_nnz: the frame's capacity
+    // is all live, so only invalid entries leave slots).
+    const int64_t hole_end = c.frame_nnz ? e1 : (f == c.n_frames - 1 ? nnz_cap : cap_end);
     for (int64_t d = e0 + n_valid + threadIdx.x; d < hole_end; d += CSR_BLOCK) ent_dst[d] = -1;
 }
 
@@ -335,12 +383,15 @@ extern "C" int shpl_build_csr(int direction, int order, int n_frames, const int6
     int log_tile = 0;
     while (((keys_per_frame - 1) >> log_tile) + 1 > CSR_TILES) ++log_tile;
     CsrIn c{direction, order, n_frames, d_frame_off, d_frame_nnz, keys_per_frame, log_tile, d_cell, d_col, d_pix, d_val};
+    // n_frames sorting workgroups + the workgroups clearing the unused capacity
+    const int64_t spans = d_frame_nnz ? (nnz_cap + HOLE_SPAN - 1) / HOLE_SPAN : 0;
+    const dim3 grid((unsigned)(n_frames + spans));
     if (d_col)
-        hipLaunchKernelGGL(k_csr_frame<true>, dim3(n_frames), dim3(CSR_BLOCK), 0, (hipStream_t)stream, c,
-                           (uint64_t *)d_ws, nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_val, csr->ent_col);
+        hipLaunchKernelGGL(k_csr_frame<true>, grid, dim3(CSR_BLOCK), 0, (hipStream_t)stream, c, (uint64_t *)d_ws,
+                           nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_val, csr->ent_col);
     else
-        hipLaunchKernelGGL(k_csr_frame<false>, dim3(n_frames), dim3(CSR_BLOCK), 0, (hipStream_t)stream, c,
-                           (uint64_t *)d_ws, nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_val, csr->ent_col);
+        hipLaunchKernelGGL(k_csr_frame<false>, grid, dim3(CSR_BLOCK), 0, (hipStream_t)stream, c, (uint64_t *)d_ws,
+                           nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_val, csr->ent_col);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
 }

@@ -3,8 +3,8 @@
 // the reference's order (voxel cells, MV3D voxels): an LDS histogram over
 // key tiles, an exclusive scan, LDS-atomic placement into tile segments and
 // an in-tile rank (words are unique, so the rank is the count of smaller
-// words of the tile). Tiles hold a few words each, so the quadratic rank is
-// cheaper than a second sort pass.
+// words of the tile, read from an LDS window of the placed words). Tiles hold
+// a few words each, so the quadratic rank is cheaper than a second sort pass.
 #pragma once
 
 #include "shpl_common.h"
@@ -13,10 +13,12 @@ namespace shpl {
 
 constexpr int TS_BLOCK = 1024;
 constexpr int TS_TILES = 16384;
+constexpr int TS_WIN = 10240;  // placed words staged in LDS for the rank (80 KiB)
 
 struct TileSortLds {
     int32_t cnt[TS_TILES];
     int32_t wsum[TS_BLOCK / 64];
+    uint64_t win[TS_WIN];
 };
 
 // Block-wide exclusive scan of the TS_TILES counters in place.
@@ -61,13 +63,24 @@ __device__ int32_t tile_sort(TileSortLds &l, int n_tiles, uint64_t *tmp, uint64_
     each([&](uint64_t w) { tmp[atomicAdd(&l.cnt[tile(w)], 1)] = w; });
     block_publish();  // tmp came from other waves through memory
     const int32_t n = l.cnt[n_tiles - 1];
-    for (int32_t s = threadIdx.x; s < n; s += TS_BLOCK) {
-        const uint64_t me = tmp[s];
-        const int t = tile(me);
-        const int32_t a = t ? l.cnt[t - 1] : 0, b = l.cnt[t];
-        int32_t rank = 0;
-        for (int32_t u = a; u < b; ++u) rank += tmp[u] < me ? 1 : 0;
-        srt[a + rank] = me;
+    // rank of each word inside its tile, the tile's words read from an LDS window
+    for (int32_t w0 = 0; w0 < n; w0 += TS_WIN) {
+        const int32_t w1 = w0 + TS_WIN < n ? w0 + TS_WIN : n;
+        for (int32_t s = w0 + threadIdx.x; s < w1; s += TS_BLOCK) l.win[s - w0] = tmp[s];
+        __syncthreads();
+        for (int32_t s = w0 + threadIdx.x; s < w1; s += TS_BLOCK) {
+            const uint64_t me = l.win[s - w0];
+            const int t = tile(me);
+            const int32_t a = t ? l.cnt[t - 1] : 0, b = l.cnt[t];
+            int32_t rank = 0;
+            if (a >= w0 && b <= w1) {
+                for (int32_t u = a; u < b; ++u) rank += l.win[u - w0] < me ? 1 : 0;
+            } else {  // the tile straddles the window edge
+                for (int32_t u = a; u < b; ++u) rank += tmp[u] < me ? 1 : 0;
+            }
+            srt[a + rank] = me;
+        }
+        __syncthreads();  // the next window overwrites win
     }
     block_publish();
     return n;

@@ -178,31 +178,25 @@ def get_lidar_point_cloud(img_idx, calib_dir, velo_dir, im_size=None, min_intens
 
 
 class KittiFrames:
-    """A batch of KITTI samples read from a dataset directory and laid out for the
-    device: what KittiDataset.load_samples (kitti_dataset.py:285-311) gathers per
-    sample before the BEV maps and the SHPL inputs are built.
+    """A batch of KITTI samples laid out for the device: what KittiDataset.load_samples
+    (kitti_dataset.py:285-311) gathers per sample before the BEV maps and the SHPL
+    inputs are built -- the scans as one [N,4] f32 array with frame offsets, the
+    per-frame lidar->camera matrices, P2, image sizes, ground planes and flips.
 
     image_shapes: (h, w) per sample (the reference reads them from the PNGs).
     flips: per-sample AUG_FLIPPING. The flipped P2 is the one the index builder
     gets here (the reference hands it the unflipped calib, kitti_dataset.py:376:
     SURVEY §8a quirk 3, a bug not replicated)."""
 
-    def __init__(self, calib_dir, velo_dir, planes_dir, indices, image_shapes, flips=None, device="cuda"):
+    def __init__(self, scans, calibs, planes, image_shapes, flips=None, device="cuda"):
         dev = torch.device(device)
-        flips = list(flips) if flips is not None else [False] * len(indices)
-        scans, rects, p2s, p2_index, sizes, planes = [], [], [], [], [], []
-        for idx, shape, fl in zip(indices, image_shapes, flips):
-            fc = read_calibration(calib_dir, idx)
-            scans.append(read_lidar_xyzi(velo_dir, idx))
+        flips = list(flips) if flips is not None else [False] * len(scans)
+        rects, p2s, p2_index, sizes, gps = [], [], [], [], []
+        for fc, gp, shape, fl in zip(calibs, planes, image_shapes, flips):
             rects.append(rect_matrix(fc))
-            gp = get_road_plane(idx, planes_dir)
-            p2 = fc.p2
-            if fl:
-                gp = flip_ground_plane(gp)
-                p2 = flip_stereo_calib_p2(p2, shape)
             p2s.append(fc.p2)  # the FOV filter projects with the file's P2 (before the flip)
-            p2_index.append(p2)
-            planes.append(gp)
+            p2_index.append(flip_stereo_calib_p2(fc.p2, shape) if fl else fc.p2)
+            gps.append(flip_ground_plane(gp) if fl else gp)
             sizes.append([shape[1], shape[0]])
         off = np.zeros(len(scans) + 1, np.int64)
         off[1:] = np.cumsum([s.shape[0] for s in scans])
@@ -215,11 +209,34 @@ class KittiFrames:
         self.P2_filter = torch.as_tensor(np.stack(p2s)).to(dev)
         self.P2 = torch.as_tensor(np.stack(p2_index)).to(dev)
         self.im_size = torch.as_tensor(np.asarray(sizes, np.float64)).to(dev)
-        self.planes = torch.as_tensor(np.stack(planes)).to(dev)
+        self.planes = torch.as_tensor(np.stack(gps)).to(dev)
         self.flip = torch.as_tensor(np.asarray(flips, np.int32)).to(dev)
         self.image_shapes = [tuple(s) for s in image_shapes]
+
+    @classmethod
+    def from_dirs(cls, calib_dir, velo_dir, planes_dir, indices, image_shapes, flips=None, device="cuda"):
+        """Read the samples' calib / velodyne / planes files (KITTI layout)."""
+        scans = [read_lidar_xyzi(velo_dir, idx) for idx in indices]
+        calibs = [read_calibration(calib_dir, idx) for idx in indices]
+        planes = [get_road_plane(idx, planes_dir) for idx in indices]
+        return cls(scans, calibs, planes, image_shapes, flips, device)
 
     def point_clouds(self, ws=None, out=None):
         """All samples' camera-frame clouds (get_point_cloud + flip_point_cloud), capacity layout."""
         return velo_to_cam_batch(self.xyzi, self.point_offsets, self.rect, self.P2_filter, self.im_size,
                                  flip=self.flip, max_points_per_frame=self.max_points, ws=ws, out=out)
+
+
+def synthetic_frames(n_frames, points_per_scan, seed=0, device="cuda", flips=None):
+    """Seeded synthetic KITTI samples (synth.synthetic_scan, synth.KITTI_CALIB) for the bench."""
+    from . import synth
+    rng = np.random.default_rng(seed)
+    fc = FrameCalibrationData()
+    c = synth.KITTI_CALIB
+    fc.p0, fc.p1, fc.p2, fc.p3 = (np.array(c[k]).reshape(3, 4) for k in ("P0", "P1", "P2", "P3"))
+    fc.r0_rect = np.array(c["R0_rect"]).reshape(3, 3)
+    fc.tr_velodyne_to_cam = np.array(c["Tr_velo_to_cam"]).reshape(3, 4)
+    scans = [synth.synthetic_scan(rng, points_per_scan) for _ in range(n_frames)]
+    plane = synth.KITTI_PLANE / np.linalg.norm(synth.KITTI_PLANE[:3])
+    return KittiFrames(scans, [fc] * n_frames, [plane] * n_frames, [synth.KITTI_IMAGE_SHAPE] * n_frames,
+                       flips, device)

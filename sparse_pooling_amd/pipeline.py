@@ -202,9 +202,48 @@ class FramePipeline(FusedPipeline):
         self.build_csr()
         self.layer(bev_feat, img_feat)
 
-    def velo_step(self, frames, bev_feat, img_feat):
+    def velo_step(self, frames, bev_feat, img_feat, side=None, events=None):
         """Raw KITTI scans (kitti.KittiFrames) -> camera-frame clouds (shpl_velo_to_cam)
-        -> BEV slices -> M -> fused layer, all on the device (kitti_dataset.py:285-379)."""
+        -> BEV slices -> M -> fused layer, all on the device (kitti_dataset.py:285-379).
+        side: a stream for the layer's streaming half (it needs no index), run beside
+        the index chain. events: 9 timing events (dense start/end on `side`; then
+        velo, bev, index, csr boundaries, sparse start/end on the current stream)."""
+        if side is not None:
+            main = torch.cuda.current_stream(self.dev)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                if events:
+                    events[0].record(side)
+                self.layer_dense(bev_feat, img_feat)
+                if events:
+                    events[1].record(side)
+            if events:
+                events[2].record(main)
+            self._velo(frames)
+            if events:
+                events[3].record(main)
+            b = self.build_bev(self.velo.points, frames.point_offsets, frames.planes, self.velo.counts)
+            if events:
+                events[4].record(main)
+            self.build_index(b.pts_in_voxel, b.voxel_indices, frames.point_offsets, frames.P2,
+                             point_counts=b.frame_nvox)
+            if events:
+                events[5].record(main)
+            self.build_csr()
+            if events:
+                events[6].record(main)
+            main.wait_stream(side)
+            if events:
+                events[7].record(main)
+            self.layer_sparse(bev_feat, img_feat)
+            if events:
+                events[8].record(main)
+            return
+        self._velo(frames)
+        self.frame_step(self.velo.points, frames.point_offsets, frames.planes, frames.P2, bev_feat, img_feat,
+                        point_counts=self.velo.counts)
+
+    def _velo(self, frames):
         if self._velo_ws is None:
             import ctypes
             nb = ctypes.c_size_t()
@@ -213,5 +252,3 @@ class FramePipeline(FusedPipeline):
             self._velo_ws = L.workspace(nb.value, self.dev)
             self._velo_pts = torch.empty((max(self.N, 1), 3), dtype=torch.float64, device=self.dev)
         self.velo = frames.point_clouds(ws=self._velo_ws, out=self._velo_pts)
-        self.frame_step(self.velo.points, frames.point_offsets, frames.planes, frames.P2, bev_feat, img_feat,
-                        point_counts=self.velo.counts)

@@ -181,32 +181,8 @@ def _mv3d_voxel_case(dense=False):
           f"capped={(vd['number_buffer'] >= 45).sum()}")
 
 
-KITTI_CALIB = {  # KITTI object-detection calib layout (values of a typical left-camera setup)
-    "P0": [7.215377e+02, 0, 6.095593e+02, 0, 0, 7.215377e+02, 1.728540e+02, 0, 0, 0, 1, 0],
-    "P1": [7.215377e+02, 0, 6.095593e+02, -3.875744e+02, 0, 7.215377e+02, 1.728540e+02, 0, 0, 0, 1, 0],
-    "P2": [7.215377e+02, 0, 6.095593e+02, 4.485728e+01, 0, 7.215377e+02, 1.728540e+02, 2.163791e-01,
-           0, 0, 1, 2.745884e-03],
-    "P3": [7.215377e+02, 0, 6.095593e+02, -3.395242e+02, 0, 7.215377e+02, 1.728540e+02, 2.199936e+00,
-           0, 0, 1, 2.729905e-03],
-    "R0_rect": [9.999239e-01, 9.837760e-03, -7.445048e-03, -9.869795e-03, 9.999421e-01, -4.278459e-03,
-                7.402527e-03, 4.351614e-03, 9.999631e-01],
-    "Tr_velo_to_cam": [7.533745e-03, -9.999714e-01, -6.166020e-04, -4.069766e-03, 1.480249e-02,
-                       7.280733e-04, -9.998902e-01, -7.631618e-02, 9.998621e-01, 7.523790e-03,
-                       1.480755e-02, -2.717806e-01],
-    "Tr_imu_to_velo": [9.999976e-01, 7.553071e-04, -2.035826e-03, -8.086759e-01, -7.854027e-04,
-                       9.998898e-01, -1.482298e-02, 3.195559e-01, 2.024406e-03, 1.482454e-02,
-                       9.998881e-01, -7.997231e-01],
-}
-
-
-def synthetic_scan(rng, n):
-    """A 64-beam-like velodyne sweep in the lidar frame (x fwd, y left, z up), f32 x 4."""
-    az = rng.uniform(-np.pi, np.pi, n)
-    el = np.deg2rad(rng.uniform(-24.8, 2.0, n))
-    rng_m = rng.uniform(2.0, 80.0, n)
-    xyz = np.stack([rng_m * np.cos(el) * np.cos(az), rng_m * np.cos(el) * np.sin(az), rng_m * np.sin(el)], 1)
-    xyz[:, 2] = np.maximum(xyz[:, 2], -1.73 + rng.normal(0, 0.02, n))  # ground
-    return np.concatenate([xyz, rng.uniform(0, 1, (n, 1))], 1).astype(np.float32)
+KITTI_CALIB = synth.KITTI_CALIB
+synthetic_scan = synth.synthetic_scan
 
 
 def _kitti_case():

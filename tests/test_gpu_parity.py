@@ -543,7 +543,7 @@ def test_kitti_loader_vs_reference_golden(kitti_dir):
         np.testing.assert_array_equal(_np(pc), g[f"{idx}_point_cloud"])
         pa = kitti.get_lidar_point_cloud(idx, os.path.join(d, "calib"), os.path.join(d, "velodyne"))
         np.testing.assert_array_equal(_np(pa), g[f"{idx}_point_cloud_all"])
-    fr = kitti.KittiFrames(os.path.join(d, "calib"), os.path.join(d, "velodyne"), os.path.join(d, "planes"),
+    fr = kitti.KittiFrames.from_dirs(os.path.join(d, "calib"), os.path.join(d, "velodyne"), os.path.join(d, "planes"),
                            [7, 8, 7], [tuple(g["7_image_shape"]), tuple(g["8_image_shape"]),
                                        tuple(g["7_image_shape"])], flips=[False, True, True])
     b = fr.point_clouds()
@@ -560,10 +560,7 @@ def test_kitti_loader_vs_reference_golden(kitti_dir):
 def test_kitti_loader_batch_vs_oracle():
     """Scans of ragged sizes across the 4096-point chunks, the intensity filter, flips."""
     from sparse_pooling_amd import kitti
-    import importlib.util
-    spec = importlib.util.spec_from_file_location("mg", os.path.join(GOLD, "make_golden.py"))
-    mg = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(mg)
+    mg = synth
     rng = np.random.default_rng(5)
     sizes = [4097, 1, 0, 12000, 4096, 30000]
     scans = [mg.synthetic_scan(rng, n) if n else np.zeros((0, 4), np.float32) for n in sizes]
@@ -592,7 +589,7 @@ def test_velodyne_to_fused_layer_pipeline(kitti_dir):
     from sparse_pooling_amd import kitti, pipeline
     d, g = kitti_dir
     shapes = [tuple(g["7_image_shape"]), tuple(g["8_image_shape"])]
-    fr = kitti.KittiFrames(os.path.join(d, "calib"), os.path.join(d, "velodyne"), os.path.join(d, "planes"),
+    fr = kitti.KittiFrames.from_dirs(os.path.join(d, "calib"), os.path.join(d, "velodyne"), os.path.join(d, "planes"),
                            [7, 8], shapes, flips=[False, True])
     im_size, stride, C = (1242, 375), (4, 4), 8
     pl = pipeline.FramePipeline(2, fr.total_points, im_size, synth.AREA_EXTENTS, synth.VOXEL_SIZE,
