@@ -56,6 +56,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the layer's streaming pass after the index build instead of beside it")
+    ap.add_argument("--groups", type=int, default=1,
+                    help="config 2: frame groups of the layer; group g's pooled rows are gathered while "
+                         "group g+1 streams (1 = one dense + one sparse launch; measured fastest, "
+                         "profiles/r01_groups.log)")
     ap.add_argument("--workload", default="layer", choices=["layer", "frames"],
                     help="layer: BASELINE configs 2/3/5 from prepared points + voxel indices (default); "
                          "frames: raw velodyne scans -> loader -> BEV slices -> index -> fused layer")
@@ -163,8 +167,21 @@ def main():
         g_img = torch.randn(tuple(pl.img_fused.shape), device=dev, generator=g).to(dtype)
         d_bev, d_img = torch.empty_like(bev), torch.empty_like(img)
     side = torch.cuda.Stream(device=dev)
+    grouped = not dual and not args.no_overlap and args.groups > 1
+    if grouped:
+        host_off = np.concatenate([[0], np.cumsum([f.points.shape[0] for f in frames])])
+        G = len(pl.set_frame_layout(host_off, args.groups))
+        sstream = torch.cuda.Stream(device=dev)
+
+        def new_events():
+            e = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+            return {"span": [e(), e()], "dense": [[e(), e()] for _ in range(G)],
+                    "sparse": [[e(), e()] for _ in range(G)]}
 
     def step(ev=None):
+        if grouped:
+            pl.step_pipelined(pts, vox, off, P, bev, img, side, sstream, events=ev)
+            return
         # ev: [dense start, dense end, sparse start, sparse end, bwd start, bwd end]
         if args.no_overlap:
             pl.build_index(pts, vox, off, P)
@@ -195,15 +212,32 @@ def main():
     u_cell = int(torch.unique(pl.cell[pl.cell >= 0]).numel())
     err = int(pl.err.item())
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(args.steps)]
+    if grouped:
+        evs = [new_events() for _ in range(args.steps)]
+    else:
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(args.steps)]
     elapsed = sd.timed(lambda k: step(evs[k]), args.steps, device=dev)
     checksums = sd.gather_checksums(pl.bv_fused[..., spec.c_bev:].double().sum().item(), device=dev)
-    dense_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
-    sparse_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
-    bwd_ms = sum(e[4].elapsed_time(e[5]) for e in evs) / args.steps if backward else 0.0
-    layer_ms = dense_ms + sparse_ms + bwd_ms
-
     nbytes = step_bytes(cfg, spec, nnz, u_pix, u_cell, F, esz)
+    kernels = {}
+    if grouped:
+        # the layer's window: first k_dense start -> last k_sparse end (the two overlap)
+        layer_ms = sum(e["span"][0].elapsed_time(e["span"][1]) for e in evs) / args.steps
+        dense_ms = sum(sum(d[0].elapsed_time(d[1]) for d in e["dense"]) for e in evs) / args.steps
+        sparse_ms = sum(sum(d[0].elapsed_time(d[1]) for d in e["sparse"]) for e in evs) / args.steps
+        bwd_ms = 0.0
+        dense_bytes = F * Hb * Wb * (2 * spec.c_bev + spec.c_img) * esz  # read bev + write bv_fused
+        kernels = {"k_dense": {"launches_per_step": G, "ms_per_launch": round(dense_ms / G, 4),
+                               "algorithmic_bytes_per_launch": dense_bytes // G,
+                               "GBps": round(dense_bytes / (dense_ms * 1e-3) / 1e9, 1)},
+                   "k_sparse": {"launches_per_step": G, "ms_per_launch": round(sparse_ms / G, 4),
+                                "algorithmic_bytes_per_launch": (nbytes - dense_bytes) // G,
+                                "GBps": round((nbytes - dense_bytes) / (sparse_ms * 1e-3) / 1e9, 1)}}
+    else:
+        dense_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+        sparse_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
+        bwd_ms = sum(e[4].elapsed_time(e[5]) for e in evs) / args.steps if backward else 0.0
+        layer_ms = dense_ms + sparse_ms + bwd_ms
     achieved = nbytes / (layer_ms * 1e-3) / 1e9
 
     cpu = None
@@ -248,8 +282,11 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "SHPL layer pulls: k_dense (concat stream) + k_sparse (pooled gather); "
-                          "achieved over their summed durations",
+                "kernel": ("SHPL layer: k_dense (concat stream) + k_sparse (pooled gather) in "
+                           f"{G} frame groups, gathers of group g beside the stream of group g+1; achieved "
+                           "over the layer's window (first k_dense start to last k_sparse end)") if grouped else
+                          ("SHPL layer pulls: k_dense (concat stream) + k_sparse (pooled gather); "
+                           "achieved over their summed durations"),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -260,6 +297,7 @@ def main():
                 "k_dense_ms": round(dense_ms, 4),
                 "k_sparse_ms": round(sparse_ms, 4),
                 "backward_ms": round(bwd_ms, 4),
+                **({"kernels": kernels} if kernels else {}),
             },
             "cpu_baseline": cpu,
             "index_errors": err,

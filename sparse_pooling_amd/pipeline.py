@@ -13,6 +13,8 @@ synchronises inside ``step``.
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 import torch
 
@@ -130,6 +132,79 @@ class FusedPipeline:
         self.layer_sparse(bev, img)
         if events:
             events[3].record(main)
+
+    # ----------------------------------------------- frame-group pipelining
+    def set_frame_layout(self, host_point_offsets, groups=4):
+        """Host copy of the point offsets (the entry slots of each frame), for
+        step_pipelined: the batch is cut into `groups` frame groups whose
+        pooled rows are filled while the next group's rows stream."""
+        off = np.asarray(host_point_offsets, dtype=np.int64)
+        assert off.shape == (self.B + 1,)
+        G = max(1, min(int(groups), self.B))
+        bounds = [round(g * self.B / G) for g in range(G + 1)]
+        cells = self.Hb * self.Wb
+        self._groups = []
+        for g in range(G):
+            f0, f1 = bounds[g], bounds[g + 1]
+            e0, e1 = int(off[f0]), int(off[f1])
+            c = self.csr
+            sp = L.ShplCsr(c.ent_dst.data_ptr() + 4 * e0, c.ent_src.data_ptr() + 4 * e0,
+                           c.ent_val.data_ptr() + 4 * e0, None, c.n_keys, e1 - e0)
+            dn = L.ShplCsr(c.ent_dst.data_ptr(), c.ent_src.data_ptr(), c.ent_val.data_ptr(), None,
+                           (f1 - f0) * cells, max(e1 - e0, 1))
+            self._groups.append(dict(sparse=sp, dense=dn, rows=(f0 * cells, f1 * cells), frames=(f0, f1),
+                                     entries=(e0, e1)))
+        return self._groups
+
+    def step_pipelined(self, points, voxels, point_offsets, P, bev, img, dstream, sstream, mval=None,
+                       events=None):
+        """step() with the layer cut into frame groups (set_frame_layout): group g's
+        streaming rows (k_dense) run on `dstream` back to back, and its pooled rows
+        (k_sparse) on `sstream` as soon as group g streamed and M is sorted -- the
+        gathers of group g overlap the streaming of group g+1. The index build and
+        the CSR run on the current stream beside the first groups.
+        events: None or dict of lists 'dense' / 'sparse' ([start, end] per group)
+        and 'span' ([start on dstream, end on sstream])."""
+        assert not self.dual, "frame-group pipelining covers the img->BEV layer"
+        main = torch.cuda.current_stream(self.dev)
+        dstream.wait_stream(main)
+        sstream.wait_stream(main)
+        width = self.Cb + self.Ci
+        esz = self.bv_fused.element_size()
+        dt = L.dtype_code(self.bv_fused)
+        ds, ss = ctypes.c_void_p(dstream.cuda_stream), ctypes.c_void_p(sstream.cuda_stream)
+        done = []
+        if events:
+            events["span"][0].record(dstream)
+        for g, grp in enumerate(self._groups):
+            r0 = grp["rows"][0]
+            if events:
+                events["dense"][g][0].record(dstream)
+            L.check(self._lib.shpl_pull_dense(
+                L.BY_CELL, dt, ctypes.byref(grp["dense"]), L.ptr(img), self.Ci, 0, self.Ci,
+                ctypes.c_void_p(bev.data_ptr() + r0 * self.Cb * esz), self.Cb, 0, self.Cb, L.OUT_CONCAT,
+                ctypes.c_void_p(self.bv_fused.data_ptr() + r0 * width * esz), width, ds), "shpl_pull_dense")
+            ev = torch.cuda.Event()
+            ev.record(dstream)
+            done.append(ev)
+            if events:
+                events["dense"][g][1].record(dstream)
+        self.build_index(points, voxels, point_offsets, P, mval)
+        self.build_csr()
+        sstream.wait_stream(main)  # M sorted
+        for g, grp in enumerate(self._groups):
+            sstream.wait_event(done[g])
+            if events:
+                events["sparse"][g][0].record(sstream)
+            L.check(self._lib.shpl_pull_sparse(
+                L.BY_CELL, dt, ctypes.byref(grp["sparse"]), L.ptr(img), self.Ci, 0, self.Ci, L.ptr(bev), self.Cb, 0,
+                self.Cb, L.OUT_CONCAT, L.ptr(self.bv_fused), width, ss), "shpl_pull_sparse")
+            if events:
+                events["sparse"][g][1].record(sstream)
+        if events:
+            events["span"][1].record(sstream)
+        main.wait_stream(sstream)
+        main.wait_stream(dstream)
 
     def backward(self, g_bv, g_img, d_bev, d_img):
         """TF gradient of the dual layer with the concat split and add_n fused:

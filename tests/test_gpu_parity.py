@@ -333,6 +333,38 @@ def test_pipeline_batch_matches_oracle(cfg, dual):
             _close_and_exact(iout[f:f + 1], ei)
 
 
+@pytest.mark.parametrize("groups", [2, 3])
+def test_pipelined_frame_groups_match_oracle(groups):
+    """step_pipelined (the bench's config-2 step: layer cut into frame groups,
+    gathers on a second stream beside the next group's stream) == oracle, twice
+    in a row (buffers reused across steps)."""
+    from sparse_pooling_amd import pipeline
+    spec = synth.CONFIGS[2]
+    F = 5
+    frames = [synth.make_frame(spec, seed=60 + f, n_outside=31 * f) for f in range(F)]
+    pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
+    pl = pipeline.FusedPipeline(F, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev, spec.c_img)
+    host_off = np.concatenate([[0], np.cumsum([f.points.shape[0] for f in frames])])
+    pl.set_frame_layout(host_off, groups)
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    bev = torch.from_numpy(synth.make_features((F, Hb, Wb, spec.c_bev), 3)).to(DEV)
+    img = torch.from_numpy(synth.make_features((F, Hi, Wi, spec.c_img), 4)).to(DEV)
+    d, s_ = torch.cuda.Stream(), torch.cuda.Stream()
+    pl.step_pipelined(pts, vox, off, P, bev, img, d, s_)
+    first = pl.bv_fused.clone()
+    pl.bv_fused.fill_(float("nan"))
+    pl.step_pipelined(pts, vox, off, P, bev, img, d, s_)
+    torch.cuda.synchronize()
+    assert torch.equal(first, pl.bv_fused)
+    out = _np(pl.bv_fused)
+    for f in (0, F - 1):
+        ref = _oracle_frame(frames[f], spec.stride)
+        eb, _ = orc.sparse_pool_layer(_np(bev[f:f + 1]), _np(img[f:f + 1]), ref["Mij_pool"], ref["M_val"],
+                                      ref["M_size"], ref["img_index_flip_pool"])
+        _close_and_exact(out[f:f + 1], eb)
+
+
 def test_full_size_properties_config5():
     """Config 5 (40k points, 64 channels, both directions) at full size:
     adjointness <pool(x), y> == <x, trans(y)> and the pass-through halves."""
