@@ -60,6 +60,8 @@ def parse():
                     help="config 2: frame groups of the layer; group g's pooled rows are gathered while "
                          "group g+1 streams (1 = one dense + one sparse launch; measured fastest, "
                          "profiles/r01_groups.log)")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="launch every step eagerly instead of replaying one captured HIP graph of it")
     ap.add_argument("--workload", default="layer", choices=["layer", "frames"],
                     help="layer: BASELINE configs 2/3/5 from prepared points + voxel indices (default); "
                          "frames: raw velodyne scans -> loader -> BEV slices -> index -> fused layer")
@@ -212,19 +214,42 @@ def main():
     u_cell = int(torch.unique(pl.cell[pl.cell >= 0]).numel())
     err = int(pl.err.item())
 
+    # One step captured as a HIP graph (torch.cuda.graph over hipStreamBeginCapture):
+    # the timed loop replays it, so host launch gaps leave the step. Kernel
+    # durations for the roofline come from the same step run eagerly with events.
+    graph, graph_note = None, None
+    if not args.no_graph:
+        try:
+            gstream = torch.cuda.Stream(device=dev)
+            gstream.wait_stream(torch.cuda.current_stream(dev))
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=gstream):
+                step()
+            graph.replay()
+            torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001 -- report and run eagerly
+            graph, graph_note = None, f"graph capture failed, eager launches: {type(e).__name__}: {e}"[:200]
+    n_ev = min(args.steps, 10) if graph is not None else args.steps
     if grouped:
-        evs = [new_events() for _ in range(args.steps)]
+        evs = [new_events() for _ in range(n_ev)]
     else:
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(args.steps)]
-    elapsed = sd.timed(lambda k: step(evs[k]), args.steps, device=dev)
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(n_ev)]
+    if graph is not None:
+        elapsed = sd.timed(lambda k: graph.replay(), args.steps, device=dev)
+        for k in range(n_ev):
+            step(evs[k])
+        torch.cuda.synchronize()
+    else:
+        elapsed = sd.timed(lambda k: step(evs[k]), args.steps, device=dev)
+    args_steps_ev = n_ev
     checksums = sd.gather_checksums(pl.bv_fused[..., spec.c_bev:].double().sum().item(), device=dev)
     nbytes = step_bytes(cfg, spec, nnz, u_pix, u_cell, F, esz)
     kernels = {}
     if grouped:
         # the layer's window: first k_dense start -> last k_sparse end (the two overlap)
-        layer_ms = sum(e["span"][0].elapsed_time(e["span"][1]) for e in evs) / args.steps
-        dense_ms = sum(sum(d[0].elapsed_time(d[1]) for d in e["dense"]) for e in evs) / args.steps
-        sparse_ms = sum(sum(d[0].elapsed_time(d[1]) for d in e["sparse"]) for e in evs) / args.steps
+        layer_ms = sum(e["span"][0].elapsed_time(e["span"][1]) for e in evs) / args_steps_ev
+        dense_ms = sum(sum(d[0].elapsed_time(d[1]) for d in e["dense"]) for e in evs) / args_steps_ev
+        sparse_ms = sum(sum(d[0].elapsed_time(d[1]) for d in e["sparse"]) for e in evs) / args_steps_ev
         bwd_ms = 0.0
         dense_bytes = F * Hb * Wb * (2 * spec.c_bev + spec.c_img) * esz  # read bev + write bv_fused
         kernels = {"k_dense": {"launches_per_step": G, "ms_per_launch": round(dense_ms / G, 4),
@@ -234,9 +259,9 @@ def main():
                                 "algorithmic_bytes_per_launch": (nbytes - dense_bytes) // G,
                                 "GBps": round((nbytes - dense_bytes) / (sparse_ms * 1e-3) / 1e9, 1)}}
     else:
-        dense_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
-        sparse_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
-        bwd_ms = sum(e[4].elapsed_time(e[5]) for e in evs) / args.steps if backward else 0.0
+        dense_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args_steps_ev
+        sparse_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args_steps_ev
+        bwd_ms = sum(e[4].elapsed_time(e[5]) for e in evs) / args_steps_ev if backward else 0.0
         layer_ms = dense_ms + sparse_ms + bwd_ms
     achieved = nbytes / (layer_ms * 1e-3) / 1e9
 
@@ -278,6 +303,8 @@ def main():
                 "unique_src_pixels_rank0": u_pix,
                 "unique_cells_rank0": u_cell,
                 "overlap_index_build": not args.no_overlap,
+                "hip_graph": graph is not None,
+                **({"graph_note": graph_note} if graph_note else {}),
                 "parallelism": f"frame-sharded x{world}",
             },
             "roofline": {
