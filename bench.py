@@ -169,6 +169,7 @@ def main():
         g_img = torch.randn(tuple(pl.img_fused.shape), device=dev, generator=g).to(dtype)
         d_bev, d_img = torch.empty_like(bev), torch.empty_like(img)
     side = torch.cuda.Stream(device=dev)
+    side2 = torch.cuda.Stream(device=dev) if dual else None  # pixel-keyed CSR / pulls beside the cell-keyed
     grouped = not dual and not args.no_overlap and args.groups > 1
     if grouped:
         host_off = np.concatenate([[0], np.cumsum([f.points.shape[0] for f in frames])])
@@ -198,11 +199,11 @@ def main():
             if ev is not None:
                 ev[3].record()
         else:
-            pl.step_overlapped(pts, vox, off, P, bev, img, side, events=ev[:4] if ev else None)
+            pl.step_overlapped(pts, vox, off, P, bev, img, side, events=ev[:4] if ev else None, side2=side2)
         if backward:
             if ev is not None:
                 ev[4].record()
-            pl.backward(g_bv, g_img, d_bev, d_img)
+            pl.backward(g_bv, g_img, d_bev, d_img, side2=side2)
             if ev is not None:
                 ev[5].record()
 

@@ -70,13 +70,14 @@ class FusedPipeline:
             L.ptr(self.pix), L.ptr(self.val), None, None, L.ptr(self.frame_nnz), L.ptr(self.frame_off),
             L.ptr(self.err), L.ptr(self.index_ws), self.index_ws.numel(), st), "shpl_build_index")
 
-    def build_csr(self):
+    def build_csr(self, which=("cell", "pixel")):
         st = L.stream_of(self.dev)
         args = (self.B, L.ptr(self.frame_off), L.ptr(self.frame_nnz))
-        L.check(self._lib.shpl_build_csr(
-            L.BY_CELL, L.ORDER_ENTRY, *args, self.Hb * self.Wb, L.ptr(self.cell), None, L.ptr(self.val),
-            L.ptr(self.pix), self.csr.ref(), L.ptr(self.csr.ws), self.csr.ws.numel(), st), "shpl_build_csr")
-        if self.dual:
+        if "cell" in which:
+            L.check(self._lib.shpl_build_csr(
+                L.BY_CELL, L.ORDER_ENTRY, *args, self.Hb * self.Wb, L.ptr(self.cell), None, L.ptr(self.val),
+                L.ptr(self.pix), self.csr.ref(), L.ptr(self.csr.ws), self.csr.ws.numel(), st), "shpl_build_csr")
+        if self.dual and "pixel" in which:
             L.check(self._lib.shpl_build_csr(
                 L.BY_PIXEL, L.ORDER_COL_ROW, *args, self.Hi * self.Wi, L.ptr(self.cell), None, L.ptr(self.val),
                 L.ptr(self.pix), self.pcsr.ref(), L.ptr(self.pcsr.ws), self.pcsr.ws.numel(), st),
@@ -94,11 +95,13 @@ class FusedPipeline:
             self._pull(self._lib.shpl_pull_dense, self.pcsr, L.BY_PIXEL, bev, self.Cb, img, self.Ci,
                        self.img_fused, st)
 
-    def layer_sparse(self, bev, img):
+    def layer_sparse(self, bev, img, which=("cell", "pixel")):
         """Pooled rows, after layer_dense and build_csr."""
         st = L.stream_of(self.dev)
-        self._pull(self._lib.shpl_pull_sparse, self.csr, L.BY_CELL, img, self.Ci, bev, self.Cb, self.bv_fused, st)
-        if self.dual:
+        if "cell" in which:
+            self._pull(self._lib.shpl_pull_sparse, self.csr, L.BY_CELL, img, self.Ci, bev, self.Cb, self.bv_fused,
+                       st)
+        if self.dual and "pixel" in which:
             self._pull(self._lib.shpl_pull_sparse, self.pcsr, L.BY_PIXEL, bev, self.Cb, img, self.Ci,
                        self.img_fused, st)
 
@@ -112,9 +115,12 @@ class FusedPipeline:
         self.build_csr()
         self.layer(bev, img)
 
-    def step_overlapped(self, points, voxels, point_offsets, P, bev, img, side, mval=None, events=None):
+    def step_overlapped(self, points, voxels, point_offsets, P, bev, img, side, mval=None, events=None,
+                        side2=None):
         """Same result as step(): the streaming half runs on `side` while the
         current stream builds M and its CSR; the sparse half then waits for it.
+        Dual layers with `side2`: the pixel-keyed CSR and pull run on side2,
+        beside the cell-keyed ones (they share only M).
         `events` (4 timing events) bracket the dense and the sparse launches."""
         main = torch.cuda.current_stream(self.dev)
         side.wait_stream(main)            # inputs / previous step done
@@ -125,11 +131,20 @@ class FusedPipeline:
             if events:
                 events[1].record(side)
         self.build_index(points, voxels, point_offsets, P, mval)
-        self.build_csr()
+        split = self.dual and side2 is not None
+        if split:
+            side2.wait_stream(main)       # M built
+            with torch.cuda.stream(side2):
+                self.build_csr(("pixel",))
+                side2.wait_stream(side)
+                self.layer_sparse(bev, img, ("pixel",))
+        self.build_csr(("cell",) if split else ("cell", "pixel"))
         main.wait_stream(side)            # sparse overwrites rows the dense pass wrote
         if events:
             events[2].record(main)
-        self.layer_sparse(bev, img)
+        self.layer_sparse(bev, img, ("cell",) if split else ("cell", "pixel"))
+        if split:
+            main.wait_stream(side2)
         if events:
             events[3].record(main)
 
@@ -206,20 +221,29 @@ class FusedPipeline:
         main.wait_stream(sstream)
         main.wait_stream(dstream)
 
-    def backward(self, g_bv, g_img, d_bev, d_img):
+    def backward(self, g_bv, g_img, d_bev, d_img, side2=None):
         """TF gradient of the dual layer with the concat split and add_n fused:
         d_bev = g_bv[..., :Cb] + M^T-pull of g_img[..., Ci:]
         d_img = g_img[..., :Ci] + scatter of M-pulled g_bv[..., Cb:].
         With the builder's identity columns the forward entry lists already are
-        in the gradients' TF order (ORDER_COL_ENTRY == ORDER_ENTRY / COL_ROW)."""
+        in the gradients' TF order (ORDER_COL_ENTRY == ORDER_ENTRY / COL_ROW).
+        side2: the d_img pull runs there, beside the d_bev pull."""
         assert self.dual
-        st = L.stream_of(self.dev)
+        main = torch.cuda.current_stream(self.dev)
         w = self.Cb + self.Ci
         dt = L.dtype_code(d_bev)
+        if side2 is not None:
+            side2.wait_stream(main)       # forward done
+            st = ctypes.c_void_p(side2.cuda_stream)
+        else:
+            st = L.stream_of(self.dev)
         L.check(self._lib.shpl_pull(L.BY_CELL, dt, self.csr.ref(), L.ptr(g_img), w, self.Ci, self.Cb, L.ptr(g_bv),
-                                    w, 0, self.Cb, L.OUT_ADD, L.ptr(d_bev), self.Cb, st), "shpl_pull")
+                                    w, 0, self.Cb, L.OUT_ADD, L.ptr(d_bev), self.Cb, L.stream_of(self.dev)),
+                "shpl_pull")
         L.check(self._lib.shpl_pull(L.BY_PIXEL, dt, self.pcsr.ref(), L.ptr(g_bv), w, self.Cb, self.Ci,
                                     L.ptr(g_img), w, 0, self.Ci, L.OUT_ADD, L.ptr(d_img), self.Ci, st), "shpl_pull")
+        if side2 is not None:
+            main.wait_stream(side2)
 
     def map(self):
         """The current M as a ShplMap (for tests)."""

@@ -391,9 +391,12 @@ def test_full_size_properties_config5():
         (frames[0].voxel_indices[:, 1] >= spec.bv_size[0]).sum())
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_pipeline_backward_matches_oracle(dtype):
-    """FusedPipeline.backward (the config-3 bench gradient) vs the oracle's TF gradients."""
+@pytest.mark.parametrize("dtype,mode", [("f32", "eager"), ("bf16", "eager"), ("bf16", "streams"),
+                                        ("f32", "graph")])
+def test_pipeline_backward_matches_oracle(dtype, mode):
+    """FusedPipeline.backward (the config-3 bench gradient) vs the oracle's TF gradients;
+    mode streams/graph: the bench's step (side streams for the streaming half and the
+    pixel-keyed chain), launched eagerly or replayed from a captured HIP graph."""
     from sparse_pooling_amd import pipeline
     spec = synth.CONFIGS[1]
     frames = [synth.make_frame(spec, seed=60 + f, n_outside=10) for f in range(2)]
@@ -414,10 +417,37 @@ def test_pipeline_backward_matches_oracle(dtype):
     img, ti = mk((2, Hi, Wi, Ci), 2)
     gb, tgb = mk((2, Hb, Wb, Cb + Ci), 3)
     gi, tgi = mk((2, Hi, Wi, Ci + Cb), 4)
-    pl.step(pts, vox, off, P, tb, ti)
     d_bev, d_img = torch.empty_like(tb), torch.empty_like(ti)
-    pl.backward(tgb, tgi, d_bev, d_img)
+    if mode == "eager":
+        pl.step(pts, vox, off, P, tb, ti)
+        pl.backward(tgb, tgi, d_bev, d_img)
+    else:
+        side, side2 = torch.cuda.Stream(), torch.cuda.Stream()
+
+        def step():
+            pl.step_overlapped(pts, vox, off, P, tb, ti, side, side2=side2)
+            pl.backward(tgb, tgi, d_bev, d_img, side2=side2)
+        step()
+        if mode == "graph":
+            torch.cuda.synchronize()
+            for t in (pl.bv_fused, pl.img_fused, d_bev, d_img):
+                t.fill_(float("nan"))
+            g = torch.cuda.CUDAGraph()
+            gs = torch.cuda.Stream()
+            gs.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.graph(g, stream=gs):
+                step()
+            g.replay()
+            g.replay()
     torch.cuda.synchronize()
+    if mode != "eager":  # the forward outputs as well
+        for f, fr in enumerate(frames):
+            ref = _oracle_frame(fr, spec.stride)
+            eb, ei = orc.sparse_pool_layer(bev[f:f + 1], img[f:f + 1], ref["Mij_pool"], ref["M_val"],
+                                           ref["M_size"], ref["img_index_flip_pool"], dual=True)
+            if dtype == "f32":
+                _close_and_exact(pl.bv_fused[f:f + 1], eb)
+                _close_and_exact(pl.img_fused[f:f + 1], ei)
     for f, fr in enumerate(frames):
         ref = _oracle_frame(fr, spec.stride)
         mij, mval, msize, idx = ref["Mij_pool"], ref["M_val"], ref["M_size"], ref["img_index_flip_pool"]
