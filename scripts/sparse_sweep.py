@@ -17,6 +17,9 @@ sys.path.insert(0, ROOT)
 VDIR = os.path.join(ROOT, "sparse_pooling_amd", "variants")
 
 VARIANTS = {f"w{w}_p{p}": [f"-DSHPL_WALK={w}", f"-DSHPL_WALK_PRED={p}"] for w in (1, 2, 4, 8) for p in (0, 1)}
+# (profiles/r01_sparse_sweep.log also holds a timing-only experiment that cut the
+# run walk after 2/8/16 entries: c3_pix 9.6/19.0/27.4 us against 38.5 us in full --
+# the pixel-keyed pull is bound by the long runs of coarse-stride pixels.)
 
 
 def build():
@@ -80,6 +83,12 @@ def run(reps):
                 assert rc == 0
             ms = timeit(call)
             row[cname] = {"us": round(1e3 * ms, 1), "exact": bool(torch.equal(out, refs[cname]))}
+            # run-length profile of this map (first variant only)
+            if name == next(iter(VARIANTS)):
+                d = csr.ent_dst[csr.ent_dst >= 0]
+                _, counts = torch.unique_consecutive(d, return_counts=True)
+                row[cname]["runs"] = {"n": int(counts.numel()), "max": int(counts.max()),
+                                      "gt8": int((counts > 8).sum()), "gt16": int((counts > 16).sum())}
         res[name] = row
         print(name, row, flush=True)
     print(json.dumps(res))
