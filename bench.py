@@ -95,7 +95,7 @@ def step_bytes(cfg, spec, nnz, u_pix, u_cell, F, esz):
     return b
 
 
-def cpu_baseline(spec, frames_np, budget_s, dual):
+def cpu_baseline(spec, frames_np, budget_s, dual, backward=False):
     """Oracle (C port of the reference path) on one core, bounded sample."""
     from oracle import shpl_oracle as orc
     Hb, Wb = spec.bev_feat_hw
@@ -103,6 +103,9 @@ def cpu_baseline(spec, frames_np, budget_s, dual):
     rng = np.random.default_rng(0)
     bev = rng.standard_normal((1, Hb, Wb, spec.c_bev), dtype=np.float32)
     img = rng.standard_normal((1, Hi, Wi, spec.c_img), dtype=np.float32)
+    if backward:
+        g_bev_pool = rng.standard_normal((1, Hb, Wb, spec.c_img), dtype=np.float32)
+        g_img_pool = rng.standard_normal((1, Hi, Wi, spec.c_bev), dtype=np.float32)
     t_index = t_pool = 0.0
     done = 0
     t0 = time.perf_counter()
@@ -115,6 +118,12 @@ def cpu_baseline(spec, frames_np, budget_s, dual):
         b = time.perf_counter()
         orc.sparse_pool_layer(bev, img, ref["Mij_pool"], ref["M_val"], ref["M_size"],
                               ref["img_index_flip_pool"], dual=dual)
+        if backward:  # TF's gradients of both directions (the concat split is a view)
+            Cb, Ci = spec.c_bev, spec.c_img
+            orc.sparse_pool_grad_img(ref["Mij_pool"], ref["M_val"], ref["M_size"], g_bev_pool.reshape(-1, Ci),
+                                     ref["img_index_flip_pool"], (1, Hi, Wi, Ci))
+            orc.sparse_pool_trans_grad_bev(ref["Mij_pool"], ref["M_val"], ref["M_size"], g_img_pool,
+                                           ref["img_index_flip_pool"])
         c = time.perf_counter()
         t_index += b - a
         t_pool += c - b
@@ -124,7 +133,8 @@ def cpu_baseline(spec, frames_np, budget_s, dual):
             "sample": (f"{done} frames of this workload ({spec.n_points} pts) through oracle/shpl_oracle.c: "
                        f"index build {1e3 * t_index / done:.2f} ms/frame + TF-order pooling and concat "
                        f"{1e3 * t_pool / done:.2f} ms/frame"
-                       + (" (both directions, forward only)" if dual else "")
+                       + ((" (both directions, forward + gradients, f32)" if backward else
+                           " (both directions, forward only)") if dual else "")
                        + f", single thread, {os.cpu_count()} host cpus visible")}
 
 
@@ -268,7 +278,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(spec, frames[: min(F, 64)], args.cpu_seconds, dual)
+        cpu = cpu_baseline(spec, frames[: min(F, 64)], args.cpu_seconds, dual, backward)
 
     if rank == 0:
         total_frames = F * world * args.steps

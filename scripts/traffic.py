@@ -23,7 +23,7 @@ def per_kernel(counter):
             if r.get("Counter_Name") != counter:
                 continue
             name = r["Kernel_Name"]
-            short = next((k for k in ("k_dense", "k_sparse", "k_csr_frame", "k_compact") if k in name), name)
+            short = next((k for k in ("k_dense", "k_sparse", "k_csr_frame", "k_compact", "k_count") if k in name), name)
             acc[short].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
