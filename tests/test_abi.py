@@ -47,3 +47,58 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(L, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(L.ShplLibraryError):
         L.lib()
+
+
+def test_argument_validation_is_host_side():
+    """Bad arguments are rejected with a status code before anything reaches the GPU
+    (so this runs without one); fake non-null device pointers are never dereferenced."""
+    import math
+    from sparse_pooling_amd import _lib as L
+    lib = L.lib()
+    P = ctypes.c_void_p(256)  # a fake, aligned, non-null device pointer
+    N = None
+    # index builder: no frames / null offsets / voxel stride / workspace size
+    assert lib.shpl_build_index(0, P, N, 10, P, L.F64, P, L.I64, 2, P, 1200., 360., 704., 800., 1., 1., N, P, P, P,
+                                N, N, P, P, N, P, 1 << 20, N) == L.ERR_ARG
+    assert lib.shpl_build_index(1, N, N, 10, P, L.F64, P, L.I64, 2, P, 1200., 360., 704., 800., 1., 1., N, P, P, P,
+                                N, N, P, P, N, P, 1 << 20, N) == L.ERR_ARG
+    assert lib.shpl_build_index(1, P, N, 10, P, L.F64, P, L.I64, 1, P, 1200., 360., 704., 800., 1., 1., N, P, P, P,
+                                N, N, P, P, N, P, 1 << 20, N) == L.ERR_BAD_SHAPE
+    assert lib.shpl_build_index(1, P, N, 10, P, L.F64, P, L.I64, 2, P, 1200., 360., 704., 800., 0., 1., N, P, P, P,
+                                N, N, P, P, N, P, 1 << 20, N) == L.ERR_BAD_SHAPE
+    assert lib.shpl_build_index(64, P, N, 100000, P, L.F64, P, L.I64, 2, P, 1200., 360., 704., 800., 1., 1., N, P,
+                                P, P, N, N, P, P, N, P, 16, N) == L.ERR_WORKSPACE
+    # CSR: bad order / direction / keys
+    csr = L.ShplCsr(256, 256, 256, None, 100, 10)
+    assert lib.shpl_build_csr(L.BY_CELL, 7, 1, P, N, 100, P, N, P, P, ctypes.byref(csr), P, 1 << 20, N) == L.ERR_ARG
+    assert lib.shpl_build_csr(5, L.ORDER_ENTRY, 1, P, N, 100, P, N, P, P, ctypes.byref(csr), P, 1 << 20,
+                              N) == L.ERR_ARG
+    assert lib.shpl_build_csr(L.BY_PIXEL, L.ORDER_COL_ROW, 1, P, N, 100, P, N, P, P, ctypes.byref(csr), P, 1 << 20,
+                              N) == L.ERR_ARG  # pixel-keyed lists need ent_col
+    assert lib.shpl_build_csr(L.BY_CELL, L.ORDER_ENTRY, 2, P, N, 100, P, N, P, P, ctypes.byref(csr), P, 1 << 20,
+                              N) == L.ERR_BAD_SHAPE  # n_keys < n_frames * keys_per_frame
+    # pulls: bad enums, ADD with different widths, output narrower than the concat
+    for fn in (lib.shpl_pull, lib.shpl_pull_dense, lib.shpl_pull_sparse):
+        assert fn(9, L.F32, ctypes.byref(csr), P, 32, 0, 32, P, 32, 0, 32, L.OUT_CONCAT, P, 64, N) == L.ERR_ARG
+        assert fn(L.BY_CELL, 7, ctypes.byref(csr), P, 32, 0, 32, P, 32, 0, 32, L.OUT_CONCAT, P, 64, N) == L.ERR_ARG
+        assert fn(L.BY_CELL, L.F32, ctypes.byref(csr), P, 32, 0, 32, P, 16, 0, 16, L.OUT_ADD, P, 32,
+                  N) == L.ERR_BAD_SHAPE
+        assert fn(L.BY_CELL, L.F32, ctypes.byref(csr), P, 32, 0, 32, P, 32, 0, 32, L.OUT_CONCAT, P, 48,
+                  N) == L.ERR_BAD_SHAPE
+        assert fn(L.BY_CELL, L.F32, ctypes.byref(csr), P, 32, 0, 32, N, 32, 0, 32, L.OUT_CONCAT, P, 64,
+                  N) == L.ERR_ARG
+    # velodyne loader: P2 without image size, misaligned scan
+    assert lib.shpl_velo_to_cam(1, P, 10, P, P, P, N, math.nan, N, P, P, N, P, 1 << 20, N) == L.ERR_ARG
+    assert lib.shpl_velo_to_cam(1, P, 10, ctypes.c_void_p(260), P, N, N, math.nan, N, P, P, N, P, 1 << 20,
+                                N) == L.ERR_BAD_SHAPE
+    assert lib.shpl_velo_to_cam(1, P, -1, P, P, N, N, math.nan, N, P, P, N, P, 1 << 20, N) == L.ERR_BAD_SHAPE
+    # BEV slices: slice count outside [1, 8]; MV3D: neither img_index2 nor P
+    ext = (ctypes.c_double * 6)(-40, 40, -5, 3, 0, 70)
+    lo = (ctypes.c_double * 9)()
+    tab = (ctypes.c_double * 16)()
+    for ns in (0, 9):
+        assert lib.shpl_bev_slices(1, P, N, 10, P, L.F64, P, ext, 0.1, ns, lo, lo, 0., 1., 0.5, tab, P, P, P, N, N,
+                                   N, P, 1 << 20, N) in (L.ERR_BAD_SHAPE, L.ERR_ARG)
+    rng = (ctypes.c_double * 6)(0, 48, -20, 20, -1, 3)
+    assert lib.shpl_mv3d_voxels(1, P, 10, P, 4, N, N, N, rng, 0.2, 0.4, 45, P, 10, P, P, P, N, N, P, 1 << 20,
+                                N) == L.ERR_ARG
