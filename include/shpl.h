@@ -313,6 +313,61 @@ int shpl_pull_sparse(int direction, int dtype, const shpl_csr *csr, const void *
                      int64_t pass_stride, int64_t pass_off, int64_t c_pass, int mode, void *d_out,
                      int64_t out_stride, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * Post-fusion 3x3 convolution
+ * ------------------------------------------------------------------------- */
+
+typedef enum { SHPL_ACT_NONE = 0, SHPL_ACT_RELU = 1 } shpl_act;
+
+/* out[f,y,x,co] = act((sum_{ky,kx,ci} in[f, y+ky-1, x+kx-1, ci] * W[ky,kx,ci,co]
+ *                      - center[co]) * scale[co] + shift[co])
+ * SAME padding (zeros outside the map), stride 1, n_frames frames of h x w
+ * pixels, NHWC rows of global id (f*h + y)*w + x. Input channels
+ * [0, c_a) are row r of d_a (element r*a_stride + a_off + c), channels
+ * [c_a, c_a + c_b) come from d_b:
+ *   pool == NULL: row r of d_b (r*b_stride + b_off + c), a second dense map;
+ *   pool != NULL: the img->BEV pooled map, computed in the staging from the
+ *                 cell-keyed CSR (shpl_build_csr SHPL_BY_CELL, SHPL_ORDER_ENTRY,
+ *                 n_keys = n_frames*h*w, entry slots of frame f from
+ *                 d_frame_off[f] on) over the image map d_b, with the
+ *                 arithmetic of shpl_pull: the result is bitwise the conv of
+ *                 [a || shpl_pull(SHPL_BY_CELL, ...)] without writing it.
+ * d_weights: HWIO [3][3][c_a+c_b][c_out] in the feature dtype (slim.conv2d's
+ * variable). d_center / d_scale / d_shift: optional [c_out] f32 (NULL = 0 / 1
+ * / 0) -- BatchNorm inference: center = moving_mean, scale = gamma /
+ * sqrt(moving_var + eps), shift = beta; conv bias: shift = bias.
+ * d_stats (optional, [2][c_out] f64): per-channel sum and sum of squares of
+ * the pre-epilogue output, for BatchNorm in training mode (shpl_batch_norm).
+ * f32: v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulation);
+ * SHPL_BF16: bf16 storage, v_mfma_f32_32x32x16_bf16, f32 accumulation, one
+ * rounding at the store. Workspace: shpl_conv3x3_workspace_bytes.
+ * Replaces: bv_fused = sparse_pool_layer(...) (sparse_pool_utils.py:61-92)
+ *   followed by slim.conv2d(bv_fused, Ci, [3,3], normalizer_fn=slim.batch_norm)
+ *   (avod/avod/core/models/rpn_model.py:338-346, scope pyramid_fusion_pooled_bev;
+ *   the img side :347-354) and slim.conv2d(bev_fused, 256, [3,3])
+ *   (avod/avod/core/models/retinanet_model.py:343-348). */
+int shpl_conv3x3_workspace_bytes(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_t c_b,
+                                 int64_t c_out, int pooled, int stats, size_t *bytes);
+int shpl_conv3x3(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a, int64_t a_stride,
+                 int64_t a_off, int64_t c_a, const void *d_b, int64_t b_stride, int64_t b_off,
+                 int64_t c_b, const shpl_csr *pool, const int64_t *d_frame_off, const void *d_weights,
+                 int64_t c_out, const float *d_center, const float *d_scale, const float *d_shift,
+                 int act, void *d_out, int64_t out_stride, double *d_stats, void *d_ws,
+                 size_t ws_bytes, void *stream);
+
+/* BatchNorm in training mode over rows x c (in place), from d_stats of
+ * shpl_conv3x3 and count = rows: mean = sum/count, var = sumsq/count - mean^2,
+ * x = act((x - mean) * gamma / sqrt(var + eps) + beta); moving averages
+ * m -= (m - v) * (1 - decay) with the Bessel-corrected variance (TF
+ * FusedBatchNorm, slim.batch_norm defaults eps 1e-3, decay 0.999, gamma
+ * NULL = 1). d_batch_mean / d_batch_var (optional) receive the batch
+ * moments (variance Bessel-corrected, as FusedBatchNorm's outputs).
+ * d_ws: 2*c floats. */
+int shpl_batch_norm(int dtype, int64_t rows, void *d_x, int64_t stride, int64_t c, const double *d_stats,
+                    double count, float eps, const float *d_gamma, const float *d_beta, int act,
+                    float *d_moving_mean, float *d_moving_var, float decay, float *d_batch_mean,
+                    float *d_batch_var, float *d_ws, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -24,6 +24,12 @@
  *                  and TF 1.8's registered gradients: GatherNd' = ScatterNd,
  *                  SparseTensorDenseMatMul'(B) = matmul(A, dY, adjoint_a=True),
  *                  ScatterNd'(updates) = GatherNd.
+ *   post-fusion    avod/avod/core/models/rpn_model.py:338-355 (slim.conv2d 3x3 SAME, no bias,
+ *   conv + BN      slim.batch_norm: center, no scale, eps 1e-3, decay 0.999, ReLU) and
+ *                  avod/avod/core/models/retinanet_model.py:343-348 (conv2d + bias + ReLU).
+ *                  TF's Conv2D / FusedBatchNorm CPU kernels (Eigen contractions) fix no
+ *                  summation order, so the oracle sums in double: the tests compare
+ *                  within a stated tolerance, cross-checked against torch's CPU conv2d.
  *
  * Parity status: the index builder is PINNED by tests/golden/index_*.npz,
  * produced by running the reference's own numpy builders in the survey
@@ -505,4 +511,82 @@ int64_t shplo_velo_to_cam(int64_t n, const float *xyzi, const double *rect, cons
         ++k;
     }
     return k;
+}
+
+/* ---- f4: post-fusion 3x3 convolution + epilogue ----------------------------
+ * out[f,y,x,co] = act((sum in[f,y+ky-1,x+kx-1,ci] * w[ky][kx][ci][co]
+ *                      - center[co]) * scale[co] + shift[co]),
+ * SAME zero padding, stride 1, sums in double, one rounding to f32 at the
+ * end (NULL center / scale / shift = 0 / 1 / 0). `raw` (optional) receives
+ * the pre-epilogue sums in double (for the training BatchNorm statistics). */
+void shplo_conv3x3(const float *in, int64_t B, int64_t H, int64_t W, int64_t Cin, const float *w,
+                   int64_t Cout, const float *center, const float *scale, const float *shift, int relu,
+                   float *out, double *raw)
+{
+    double *acc = (double *)malloc(sizeof(double) * (size_t)(Cout > 0 ? Cout : 1));
+    for (int64_t f = 0; f < B; ++f)
+        for (int64_t y = 0; y < H; ++y)
+            for (int64_t x = 0; x < W; ++x) {
+                for (int64_t co = 0; co < Cout; ++co) acc[co] = 0.0;
+                for (int64_t ky = 0; ky < 3; ++ky) {
+                    const int64_t yy = y + ky - 1;
+                    if (yy < 0 || yy >= H) continue;
+                    for (int64_t kx = 0; kx < 3; ++kx) {
+                        const int64_t xx = x + kx - 1;
+                        if (xx < 0 || xx >= W) continue;
+                        const float *a = in + ((f * H + yy) * W + xx) * Cin;
+                        const float *wt = w + (ky * 3 + kx) * Cin * Cout;
+                        for (int64_t ci = 0; ci < Cin; ++ci) {
+                            const double av = a[ci];
+                            const float *wr = wt + ci * Cout;
+                            for (int64_t co = 0; co < Cout; ++co) acc[co] += av * (double)wr[co];
+                        }
+                    }
+                }
+                const int64_t row = (f * H + y) * W + x;
+                for (int64_t co = 0; co < Cout; ++co) {
+                    double v = acc[co];
+                    if (raw) raw[row * Cout + co] = v;
+                    if (center) v -= center[co];
+                    if (scale) v *= scale[co];
+                    if (shift) v += shift[co];
+                    if (relu && v < 0.0) v = 0.0;
+                    out[row * Cout + co] = (float)v;
+                }
+            }
+    free(acc);
+}
+
+/* BatchNorm in training mode (TF FusedBatchNorm, is_training=True) over the
+ * double pre-activation `raw` [rows][C]: batch mean and biased variance
+ * normalise, y = act((x - mean) * gamma / sqrt(var + eps) + beta); the
+ * moving averages take the Bessel-corrected variance:
+ * m -= (m - batch) * (1 - decay). */
+void shplo_bn_train(const double *raw, int64_t rows, int64_t C, double eps, const float *gamma,
+                    const float *beta, int relu, float *out, float *moving_mean, float *moving_var,
+                    double decay, double *batch_mean, double *batch_var)
+{
+    for (int64_t c = 0; c < C; ++c) {
+        double s = 0.0, s2 = 0.0;
+        for (int64_t r = 0; r < rows; ++r) s += raw[r * C + c];
+        const double mean = s / (double)rows;
+        for (int64_t r = 0; r < rows; ++r) {
+            const double d = raw[r * C + c] - mean;
+            s2 += d * d;
+        }
+        const double var = s2 / (double)rows;
+        const double g = gamma ? gamma[c] : 1.0;
+        const double k = g / sqrt(var + eps);
+        for (int64_t r = 0; r < rows; ++r) {
+            double v = (raw[r * C + c] - mean) * k;
+            if (beta) v += beta[c];
+            if (relu && v < 0.0) v = 0.0;
+            out[r * C + c] = (float)v;
+        }
+        const double vu = rows > 1 ? var * (double)rows / (double)(rows - 1) : var;
+        if (moving_mean) moving_mean[c] = (float)(moving_mean[c] - (moving_mean[c] - mean) * (1.0 - decay));
+        if (moving_var) moving_var[c] = (float)(moving_var[c] - (moving_var[c] - vu) * (1.0 - decay));
+        if (batch_mean) batch_mean[c] = mean;
+        if (batch_var) batch_var[c] = vu;
+    }
 }

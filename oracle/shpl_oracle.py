@@ -55,6 +55,10 @@ def lib():
         _lib.shplo_bev_slices.restype = i64
         _lib.shplo_bev_slices.argtypes = [i64, p, p, p, d, ctypes.c_int, p, p, d, d, d, p, i64, p, p,
                                           p, p]
+        _lib.shplo_conv3x3.restype = None
+        _lib.shplo_conv3x3.argtypes = [p, i64, i64, i64, i64, p, i64, p, p, p, ctypes.c_int, p, p]
+        _lib.shplo_bn_train.restype = None
+        _lib.shplo_bn_train.argtypes = [p, i64, i64, d, p, p, ctypes.c_int, p, p, p, d, p, p]
     return _lib
 
 
@@ -298,3 +302,45 @@ def to_bf16_bits(x):
 
 def from_bf16_bits(b):
     return (np.asarray(b, np.uint16).astype(np.uint32) << 16).view(np.float32)
+
+
+# ---- f4: post-fusion conv + BatchNorm (rpn_model.py:338-355, retinanet_model.py:343-348)
+
+def _opt(a):
+    return None if a is None else _p(_c(a, np.float32))
+
+
+def conv3x3(x, w, center=None, scale=None, shift=None, relu=False, raw=False):
+    """SAME 3x3 conv of NHWC ``x`` [B,H,W,Cin] with HWIO ``w`` [3,3,Cin,Cout],
+    summed in double, then act((acc - center) * scale + shift) rounded to f32.
+    raw=True also returns the double pre-epilogue sums."""
+    x = _c(x, np.float32)
+    w = _c(w, np.float32)
+    B, H, W, Cin = x.shape
+    Cout = w.shape[3]
+    assert w.shape == (3, 3, Cin, Cout)
+    out = np.empty((B, H, W, Cout), np.float32)
+    r = np.empty((B, H, W, Cout), np.float64) if raw else None
+    keep = [_c(a, np.float32) if a is not None else None for a in (center, scale, shift)]
+    lib().shplo_conv3x3(_p(x), B, H, W, Cin, _p(w), Cout, *[None if a is None else _p(a) for a in keep],
+                        int(bool(relu)), _p(out), None if r is None else _p(r))
+    return (out, r) if raw else out
+
+
+def batch_norm_train(raw, eps=1e-3, gamma=None, beta=None, relu=True, moving_mean=None, moving_var=None,
+                     decay=0.999):
+    """FusedBatchNorm (is_training) over the channels of ``raw`` (double, [..., C]).
+    Returns (y f32, batch_mean, batch_var (Bessel-corrected), moving_mean, moving_var)."""
+    raw = _c(raw, np.float64)
+    C = raw.shape[-1]
+    rows = raw.size // C
+    out = np.empty(raw.shape, np.float32)
+    mm = None if moving_mean is None else _c(moving_mean, np.float32).copy()
+    mv = None if moving_var is None else _c(moving_var, np.float32).copy()
+    bm, bv = np.empty(C, np.float64), np.empty(C, np.float64)
+    g = None if gamma is None else _c(gamma, np.float32)
+    b = None if beta is None else _c(beta, np.float32)
+    lib().shplo_bn_train(_p(raw), rows, C, float(eps), None if g is None else _p(g), None if b is None else _p(b),
+                         int(bool(relu)), _p(out), None if mm is None else _p(mm), None if mv is None else _p(mv),
+                         float(decay), _p(bm), _p(bv))
+    return out, bm, bv, mm, mv

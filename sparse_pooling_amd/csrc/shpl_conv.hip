@@ -1,0 +1,618 @@
+// shpl_conv.hip -- the post-fusion 3x3 convolution, with
+// the SHPL concat (and, optionally, the img->BEV pooling itself) fused into
+// its input staging.
+//
+// Reference (avod/avod/core/models/rpn_model.py:338-355, config switch
+// rpn_sparse_pooling_conv_after_fusion, model.proto:88):
+//     bv_fused = sparse_pool_layer([bev, img], ...)          # [1,Hb,Wb,Cb+Ci]
+//     bev_out  = slim.conv2d(bv_fused, Ci, [3,3], normalizer_fn=slim.batch_norm,
+//                            normalizer_params={'is_training': ...})
+// i.e. SAME padding, stride 1, no bias, BatchNorm (center, no scale,
+// eps 1e-3, decay 0.999), ReLU; and retinanet_model.py:343-348 (conv2d with
+// bias + ReLU, no BN). Both epilogues are  y = act((acc - center) * scale + shift).
+//
+// Implicit GEMM on MFMA: M = output pixels, N = output channels (32 per
+// workgroup), K = 9 taps x input channels. One workgroup owns an 8 x 32
+// output tile of one frame; wave w owns tile rows 2w and 2w+1 (two 32-pixel
+// M subtiles against all 32 channels: v_mfma_f32_32x32x2_f32 for f32,
+// v_mfma_f32_32x32x16_bf16 for bf16 storage, f32 accumulation in both).
+// The input channels are walked in chunks of 32 bytes per pixel (8 f32 / 16
+// bf16): a chunk of the 10 x 34 halo tile and the chunk's 9 x 32 weights are
+// staged in LDS (48-byte rows: conflict-free ds_read_b128), then 9 taps of
+// MFMAs consume them.
+//
+// Input channels [0, c_a) come from tensor A (the BEV map), [c_a, c_a+c_b)
+// from tensor B. B is either a dense tensor (the materialised pooled map, or
+// nothing) or -- POOLED -- the image feature map read through the img->BEV
+// CSR of shpl_build_csr: the chunk is zero-filled and the halo cells that own
+// entries get their pooled vector computed on the spot, with exactly the
+// arithmetic of k_sparse (shpl_pull.hip: TF order, separate multiply and
+// add), so the conv of the fused form is bitwise the conv of
+// [bev || shpl_pull(...)] and bv_fused never reaches HBM.
+#include "shpl_common.h"
+
+namespace shpl {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int TH = 8, TW = 32;              // output tile (rows x columns)
+constexpr int HH = TH + 2, HWD = TW + 2;    // halo tile
+constexpr int NCO = 32;                     // output channels per workgroup
+constexpr int CONV_BLOCK = 256;             // 4 waves, wave w: tile rows 2w, 2w+1
+constexpr int CHUNK_B = 32;                 // bytes of one pixel's chunk (8 f32 / 16 bf16)
+constexpr int PSTR = 48;                    // LDS row stride: 32 B + 16 B pad
+constexpr int IN_HALVES = HH * HWD * 2;     // 16-byte pieces of a staged input chunk
+constexpr int W_ROWS = 9 * NCO;             // weight rows of a chunk (tap, out channel)
+constexpr int W_HALVES = W_ROWS * 2;
+constexpr int IN_LDS = HH * HWD * PSTR;
+constexpr int W_LDS = W_ROWS * PSTR;
+
+template <typename T>
+struct Elem {
+    static constexpr int CK = CHUNK_B / sizeof(T);  // channels per chunk
+    static constexpr int HE = 16 / sizeof(T);       // channels per 16-byte piece
+    static __device__ __forceinline__ float f(T v) {
+        if constexpr (sizeof(T) == 4)
+            return v;
+        else
+            return bf16_to_f32(v);
+    }
+    static __device__ __forceinline__ T back(float v) {
+        if constexpr (sizeof(T) == 4)
+            return v;
+        else
+            return f32_to_bf16(v);
+    }
+};
+
+struct ConvArgs {
+    int n_frames, h, w;
+    int tiles_x, tiles_per_frame, n_tiles;
+    const void *a;
+    int64_t a_stride, a_off;
+    int c_a, qa;  // channels of A, chunks of A
+    const void *b;
+    int64_t b_stride, b_off;
+    int c_b, qb;
+    bool vec_a, vec_b;  // 16-byte aligned rows and offsets
+    // POOLED: B rows are image pixels read through the cell-keyed CSR
+    const int32_t *ent_dst, *ent_src, *row_ptr;
+    const float *ent_val;
+    const void *wp;  // packed weights [co_block][chunk][tap][32][CK]
+    const float *center, *scale, *shift;
+    int act;
+    void *out;
+    int64_t out_stride;
+    int c_out;
+    double *part;  // STATS: [(co_block*32 + co)*2 + stat][n_tiles]
+};
+
+// 16 bytes of channels [c, c + HE) of one row, channels >= c_src read as 0.
+template <typename T>
+__device__ __forceinline__ u32x4 load_piece(const T *row, int c, int c_src, bool vec) {
+    constexpr int HE = Elem<T>::HE;
+    if (vec && c + HE <= c_src) return *reinterpret_cast<const u32x4 *>(row + c);
+    T e[HE];
+#pragma unroll
+    for (int j = 0; j < HE; ++j) e[j] = c + j < c_src ? row[c + j] : T(0);
+    u32x4 r;
+    __builtin_memcpy(&r, e, 16);
+    return r;
+}
+
+// blockIdx -> tile, so that each XCD (blocks b, b+8, ...) gets one contiguous
+// run of tiles: neighbouring tiles share halo rows through that XCD's L2.
+__device__ __forceinline__ int xcd_tile(int bid, int n) {
+    const int q = n >> 3, r = n & 7, xcd = bid & 7, i = bid >> 3;
+    return xcd < r ? xcd * (q + 1) + i : r * (q + 1) + (xcd - r) * q + i;
+}
+
+__device__ __forceinline__ int32_t lower_bound(const int32_t *v, int32_t lo, int32_t hi, int32_t key) {
+    while (lo < hi) {
+        const int32_t mid = lo + ((hi - lo) >> 1);
+        if ((uint32_t)v[mid] < (uint32_t)key)  // empty slots (-1) sort last
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+template <typename T, bool POOLED, bool STATS>
+__global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3(const ConvArgs p) {
+    typedef Elem<T> E;
+    constexpr int CK = E::CK, HE = E::HE;
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[IN_LDS];
+    __shared__ __attribute__((aligned(16))) uint8_t s_w[W_LDS];
+    __shared__ int32_t s_lo[HH], s_pre[HH + 1];
+    __shared__ float s_red[4][2][NCO];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int pl = lane & 31, hf = lane >> 5;
+    const int tile = xcd_tile(blockIdx.x, p.n_tiles);
+    const int cob = blockIdx.y;
+    const int f = tile / p.tiles_per_frame;
+    const int t_in = tile - f * p.tiles_per_frame;
+    const int ty = t_in / p.tiles_x, tx = t_in - ty * p.tiles_x;
+    const int y0 = ty * TH, x0 = tx * TW;
+    const int H = p.h, W = p.w;
+    const int64_t frame_row0 = (int64_t)f * H * W;
+    const int Q = p.qa + p.qb;
+
+    if (POOLED) {
+        // entry range of each halo row: cells [x0-1, x0+TW+1) of row y, from
+        // the per-row entry pointers and a binary search inside the row
+        if (tid < HH) {
+            const int y = y0 - 1 + tid;
+            int32_t lo = 0, hi = 0;
+            if (y >= 0 && y < H) {
+                const int32_t ra = p.row_ptr[(int64_t)f * (H + 1) + y];
+                const int32_t rb = p.row_ptr[(int64_t)f * (H + 1) + y + 1];
+                const int32_t kl = (int32_t)(frame_row0 + (int64_t)y * W + (x0 > 0 ? x0 - 1 : 0));
+                const int32_t kh = (int32_t)(frame_row0 + (int64_t)y * W + (x0 + TW + 1 < W ? x0 + TW + 1 : W));
+                lo = lower_bound(p.ent_dst, ra, rb, kl);
+                hi = lower_bound(p.ent_dst, lo, rb, kh);
+            }
+            s_lo[tid] = lo;
+            s_pre[tid + 1] = hi - lo;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            s_pre[0] = 0;
+            for (int r = 0; r < HH; ++r) s_pre[r + 1] += s_pre[r];
+        }
+        __syncthreads();
+    }
+
+    f32x16 acc[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[m][i] = 0.0f;
+
+    const T *wq = reinterpret_cast<const T *>(p.wp) + (int64_t)cob * Q * W_ROWS * CK;
+    for (int q = 0; q < Q; ++q) {
+        // ---- weights of the chunk: 288 rows of 32 B, contiguous in the packed array
+        {
+            u32x4 v[3];
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+                const int j = tid + u * CONV_BLOCK;
+                if (j < W_HALVES) v[u] = *reinterpret_cast<const u32x4 *>(wq + (int64_t)q * W_ROWS * CK + j * HE);
+            }
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+                const int j = tid + u * CONV_BLOCK;
+                if (j < W_HALVES) *reinterpret_cast<u32x4 *>(s_w + (j >> 1) * PSTR + (j & 1) * 16) = v[u];
+            }
+        }
+        // ---- input chunk of the halo tile
+        const bool from_a = q < p.qa;
+        if (from_a || !POOLED) {
+            const T *src = reinterpret_cast<const T *>(from_a ? p.a : p.b) + (from_a ? p.a_off : p.b_off);
+            const int64_t stride = from_a ? p.a_stride : p.b_stride;
+            const int c_src = from_a ? p.c_a : p.c_b;
+            const int c0 = (from_a ? q : q - p.qa) * CK;
+            const bool vec = from_a ? p.vec_a : p.vec_b;
+            u32x4 v[3];
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+                const int j = tid + u * CONV_BLOCK;
+                v[u] = u32x4{0u, 0u, 0u, 0u};
+                if (j < IN_HALVES) {
+                    const int pix = j >> 1, hr = pix / HWD, hc = pix - hr * HWD;
+                    const int y = y0 - 1 + hr, x = x0 - 1 + hc;
+                    if (y >= 0 && y < H && x >= 0 && x < W)
+                        v[u] = load_piece<T>(src + (frame_row0 + (int64_t)y * W + x) * stride, c0 + (j & 1) * HE,
+                                             c_src, vec);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+                const int j = tid + u * CONV_BLOCK;
+                if (j < IN_HALVES) *reinterpret_cast<u32x4 *>(s_in + (j >> 1) * PSTR + (j & 1) * 16) = v[u];
+            }
+        } else {
+            // pooled chunk: zeros, then the occupied cells' sums (k_sparse arithmetic)
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+                const int j = tid + u * CONV_BLOCK;
+                if (j < IN_HALVES)
+                    *reinterpret_cast<u32x4 *>(s_in + (j >> 1) * PSTR + (j & 1) * 16) = u32x4{0u, 0u, 0u, 0u};
+            }
+            __syncthreads();
+            const T *img = reinterpret_cast<const T *>(p.b) + p.b_off;
+            const int c0 = (q - p.qa) * CK;
+            const int n_ent = s_pre[HH];
+            for (int j = tid; j < n_ent; j += CONV_BLOCK) {
+                int r = 0;
+                while (j >= s_pre[r + 1]) ++r;
+                const int32_t e = s_lo[r] + (j - s_pre[r]);
+                const int32_t e_end = s_lo[r] + (s_pre[r + 1] - s_pre[r]);
+                const int32_t d = p.ent_dst[e];
+                if (j > s_pre[r] && p.ent_dst[e - 1] == d) continue;  // not the first entry of its cell
+                float sum[CK];
+#pragma unroll
+                for (int c = 0; c < CK; ++c) sum[c] = 0.0f;
+                for (int32_t i = e; i < e_end && p.ent_dst[i] == d; ++i) {
+                    const float wv = p.ent_val[i];
+                    const T *row = img + (int64_t)p.ent_src[i] * p.b_stride;
+                    u32x4 raw[2];
+                    raw[0] = load_piece<T>(row, c0, p.c_b, p.vec_b);
+                    raw[1] = load_piece<T>(row, c0 + HE, p.c_b, p.vec_b);
+                    T x[CK];
+                    __builtin_memcpy(x, raw, sizeof(raw));
+#pragma unroll
+                    for (int c = 0; c < CK; ++c) sum[c] = __fadd_rn(sum[c], __fmul_rn(wv, E::f(x[c])));
+                }
+                T o[CK];
+#pragma unroll
+                for (int c = 0; c < CK; ++c) o[c] = E::back(sum[c]);
+                const int y = y0 - 1 + r;
+                const int hc = (int)((int64_t)d - frame_row0 - (int64_t)y * W) - (x0 - 1);
+                uint8_t *dstp = s_in + (r * HWD + hc) * PSTR;
+                __builtin_memcpy(dstp, o, 16);
+                __builtin_memcpy(dstp + 16, reinterpret_cast<uint8_t *>(o) + 16, 16);
+            }
+        }
+        __syncthreads();
+        // ---- 9 taps of MFMA over the chunk
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                const uint8_t *wrow = s_w + ((ky * 3 + kx) * NCO + pl) * PSTR + hf * 16;
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    const uint8_t *arow = s_in + ((2 * wave + m + ky) * HWD + pl + kx) * PSTR + hf * 16;
+                    if constexpr (sizeof(T) == 4) {
+                        // lane half h supplies channels 4h+s of the chunk to MFMA s (A and B alike)
+                        const f32x4 a4 = *reinterpret_cast<const f32x4 *>(arow);
+                        const f32x4 b4 = *reinterpret_cast<const f32x4 *>(wrow);
+#pragma unroll
+                        for (int s = 0; s < 4; ++s)
+                            acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[s], b4[s], acc[m], 0, 0, 0);
+                    } else {
+                        const bf16x8 a8 = *reinterpret_cast<const bf16x8 *>(arow);
+                        const bf16x8 b8 = *reinterpret_cast<const bf16x8 *>(wrow);
+                        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a8, b8, acc[m], 0, 0, 0);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- epilogue: acc element i of subtile m is pixel (y0+2w+m, x0+(i&3)+8(i>>2)+4h), channel pl
+    const int co = cob * NCO + pl;
+    const bool co_ok = co < p.c_out;
+    float cen = 0.0f, scl = 1.0f, sft = 0.0f;
+    if (co_ok) {
+        if (p.center) cen = p.center[co];
+        if (p.scale) scl = p.scale[co];
+        if (p.shift) sft = p.shift[co];
+    }
+    T *out = reinterpret_cast<T *>(p.out);
+    float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        const int y = y0 + 2 * wave + m;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int x = x0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+            if (!(co_ok && y < H && x < W)) continue;
+            float v = acc[m][i];
+            if (STATS) {
+                s1 = __fadd_rn(s1, v);
+                s2 = __fadd_rn(s2, __fmul_rn(v, v));
+            }
+            if (p.center) v = __fsub_rn(v, cen);
+            if (p.scale) v = __fmul_rn(v, scl);
+            if (p.shift) v = __fadd_rn(v, sft);
+            if (p.act == 1) v = v > 0.0f ? v : 0.0f;
+            out[(frame_row0 + (int64_t)y * W + x) * p.out_stride + co] = E::back(v);
+        }
+    }
+    if (STATS) {
+        s1 = __fadd_rn(s1, __shfl_xor(s1, 32, 64));
+        s2 = __fadd_rn(s2, __shfl_xor(s2, 32, 64));
+        if (hf == 0) {
+            s_red[wave][0][pl] = s1;
+            s_red[wave][1][pl] = s2;
+        }
+        __syncthreads();
+        if (tid < 2 * NCO) {
+            const int st = tid >> 5, c = tid & 31;
+            double s = 0.0;
+            for (int w = 0; w < 4; ++w) s += (double)s_red[w][st][c];
+            p.part[((int64_t)(cob * NCO + c) * 2 + st) * p.n_tiles + tile] = s;
+        }
+    }
+}
+
+// Packed weights: HWIO [3][3][c_a+c_b][c_out] -> [co_block][chunk][tap][32][CK],
+// chunks of A's channels first, then B's, zero padded.
+template <typename T>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_pack_w(const T *w, int c_a, int qa, int c_b, int qb, int c_out,
+                                                       int n_cob, T *wp) {
+    constexpr int CK = Elem<T>::CK;
+    const int Q = qa + qb;
+    const int64_t total = (int64_t)n_cob * Q * W_ROWS * CK;
+    const int cin = c_a + c_b;
+    for (int64_t t = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * SHPL_BLOCK) {
+        const int k = (int)(t % CK);
+        int64_t r = t / CK;
+        const int co_l = (int)(r % NCO);
+        r /= NCO;
+        const int tap = (int)(r % 9);
+        r /= 9;
+        const int q = (int)(r % Q);
+        const int cob = (int)(r / Q);
+        const int co = cob * NCO + co_l;
+        int ci;
+        bool ok;
+        if (q < qa) {
+            ci = q * CK + k;
+            ok = ci < c_a;
+        } else {
+            const int cb = (q - qa) * CK + k;
+            ci = c_a + cb;
+            ok = cb < c_b;
+        }
+        wp[t] = (ok && co < c_out) ? w[((int64_t)tap * cin + ci) * c_out + co] : T(0);
+    }
+}
+
+// Entry pointer of every BEV row of every frame over the destination-sorted
+// CSR: row_ptr[f*(H+1) + y] = first entry of frame f whose cell lies in row
+// >= y (empty slots, dst -1, count as row H).
+__global__ __launch_bounds__(SHPL_BLOCK) void k_row_ptr(const int32_t *dst, const int64_t *frame_off, int H, int W,
+                                                        int32_t *row_ptr) {
+    const int f = blockIdx.y;
+    const int64_t s = frame_off[f], e_end = frame_off[f + 1];
+    const int64_t base = (int64_t)f * H * W;
+    int32_t *rp = row_ptr + (int64_t)f * (H + 1);
+    for (int64_t e = s + (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x; e <= e_end;
+         e += (int64_t)gridDim.x * SHPL_BLOCK) {
+        const int32_t dc = e < e_end ? dst[e] : -1;
+        const int yc = dc < 0 ? H : (int)((dc - base) / W);
+        int yp = -1;
+        if (e > s) {
+            const int32_t dp = dst[e - 1];
+            yp = dp < 0 ? H : (int)((dp - base) / W);
+        }
+        for (int y = yp + 1; y <= yc; ++y) rp[y] = (int32_t)e;
+    }
+}
+
+// Per-channel sum / sum of squares of the pre-activation output, summed over
+// the per-tile partials in a fixed order (deterministic): one block per
+// (channel, statistic).
+__global__ __launch_bounds__(SHPL_BLOCK) void k_stats_reduce(const double *part, int n_tiles, int c_out,
+                                                             double *stats) {
+    __shared__ double red[SHPL_BLOCK];
+    const int ch = blockIdx.x >> 1, st = blockIdx.x & 1;
+    const double *v = part + ((int64_t)ch * 2 + st) * n_tiles;
+    double s = 0.0;
+    for (int i = threadIdx.x; i < n_tiles; i += SHPL_BLOCK) s += v[i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = SHPL_BLOCK / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && ch < c_out) stats[st * c_out + ch] = red[0];
+}
+
+// BatchNorm (training) from the batch statistics: mean, biased variance for
+// the normalisation, Bessel-corrected variance for the moving average (TF
+// FusedBatchNorm), then y = act((x - mean) * gamma / sqrt(var + eps) + beta)
+// in place.
+__global__ __launch_bounds__(SHPL_BLOCK) void k_bn_finalize(const double *stats, double count, int c, float eps,
+                                                            const float *gamma, float *mean_out, float *scale_out,
+                                                            float *moving_mean, float *moving_var, float decay,
+                                                            float *batch_mean, float *batch_var) {
+    for (int ch = threadIdx.x; ch < c; ch += SHPL_BLOCK) {
+        const double mean = stats[ch] / count;
+        double var = stats[c + ch] / count - mean * mean;
+        if (var < 0.0) var = 0.0;
+        const float mf = (float)mean, vf = (float)var;
+        const float g = gamma ? gamma[ch] : 1.0f;
+        mean_out[ch] = mf;
+        scale_out[ch] = __fmul_rn(g, __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(vf, eps))));
+        const float vu = count > 1.0 ? (float)(var * count / (count - 1.0)) : vf;
+        if (moving_mean) moving_mean[ch] = __fsub_rn(moving_mean[ch], __fmul_rn(__fsub_rn(moving_mean[ch], mf), 1.0f - decay));
+        if (moving_var) moving_var[ch] = __fsub_rn(moving_var[ch], __fmul_rn(__fsub_rn(moving_var[ch], vu), 1.0f - decay));
+        if (batch_mean) batch_mean[ch] = mf;
+        if (batch_var) batch_var[ch] = vu;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_bn_apply(T *x, int64_t rows, int64_t stride, int c,
+                                                         const float *mean, const float *scale, const float *beta,
+                                                         int act) {
+    const int64_t total = rows * c;
+    for (int64_t t = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * SHPL_BLOCK) {
+        const int64_t r = t / c;
+        const int ch = (int)(t - r * c);
+        T *px = x + r * stride + ch;
+        float v = __fmul_rn(__fsub_rn(Elem<T>::f(*px), mean[ch]), scale[ch]);
+        if (beta) v = __fadd_rn(v, beta[ch]);
+        if (act == 1) v = v > 0.0f ? v : 0.0f;
+        *px = Elem<T>::back(v);
+    }
+}
+
+struct ConvPlan {
+    int ck, qa, qb, n_cob, tiles_x, tiles_y, tiles_per_frame;
+    int64_t n_tiles;
+    size_t wp_bytes, rp_bytes, part_bytes, total;
+};
+
+int conv_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_t c_b, int64_t c_out, bool pooled,
+              bool stats, ConvPlan *pl) {
+    if (dtype != SHPL_F32 && dtype != SHPL_BF16) return SHPL_ERR_ARG;
+    if (n_frames < 0 || h < 0 || w < 0 || c_a < 0 || c_b < 0 || c_out < 1 || c_a + c_b < 1) return SHPL_ERR_BAD_SHAPE;
+    if (h > (1 << 20) || w > (1 << 20) || c_a + c_b > (1 << 16) || c_out > (1 << 16)) return SHPL_ERR_BAD_SHAPE;
+    const int esz = dtype == SHPL_F32 ? 4 : 2;
+    pl->ck = CHUNK_B / esz;
+    pl->qa = (int)((c_a + pl->ck - 1) / pl->ck);
+    pl->qb = (int)((c_b + pl->ck - 1) / pl->ck);
+    pl->n_cob = (int)((c_out + NCO - 1) / NCO);
+    pl->tiles_x = (int)((w + TW - 1) / TW);
+    pl->tiles_y = (int)((h + TH - 1) / TH);
+    pl->tiles_per_frame = pl->tiles_x * pl->tiles_y;
+    pl->n_tiles = (int64_t)n_frames * pl->tiles_per_frame;
+    if (pl->n_tiles >= (1LL << 31) || (int64_t)n_frames * h * w >= (1LL << 31)) return SHPL_ERR_BAD_SHAPE;
+    pl->wp_bytes = align_up((size_t)pl->n_cob * (pl->qa + pl->qb) * W_ROWS * CHUNK_B, 256);
+    pl->rp_bytes = pooled ? align_up((size_t)n_frames * (h + 1) * 4, 256) : 0;
+    pl->part_bytes = stats ? align_up((size_t)pl->n_cob * NCO * 2 * pl->n_tiles * 8, 256) : 0;
+    pl->total = pl->wp_bytes + pl->rp_bytes + pl->part_bytes;
+    return SHPL_OK;
+}
+
+bool aligned16(const void *ptr) { return ((uintptr_t)ptr & 15u) == 0; }
+
+template <typename T>
+int conv_launch(const ConvPlan &pl, ConvArgs &a, bool pooled, bool stats, const void *w, const int64_t *frame_off,
+                double *d_stats, hipStream_t s) {
+    T *wp = reinterpret_cast<T *>(const_cast<void *>(a.wp));
+    const int64_t wtot = (int64_t)pl.n_cob * (pl.qa + pl.qb) * W_ROWS * Elem<T>::CK;
+    hipLaunchKernelGGL(k_pack_w<T>, dim3(grid_for(wtot, SHPL_BLOCK, 4096)), dim3(SHPL_BLOCK), 0, s,
+                       reinterpret_cast<const T *>(w), a.c_a, pl.qa, a.c_b, pl.qb, a.c_out, pl.n_cob, wp);
+    SHPL_LAUNCH_CHECK();
+    if (pooled) {
+        hipLaunchKernelGGL(k_row_ptr, dim3(16, a.n_frames), dim3(SHPL_BLOCK), 0, s, a.ent_dst, frame_off, a.h, a.w,
+                           const_cast<int32_t *>(a.row_ptr));
+        SHPL_LAUNCH_CHECK();
+    }
+    const dim3 grid((unsigned)pl.n_tiles, (unsigned)pl.n_cob);
+    if (pooled) {
+        if (stats)
+            hipLaunchKernelGGL((k_conv3x3<T, true, true>), grid, dim3(CONV_BLOCK), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_conv3x3<T, true, false>), grid, dim3(CONV_BLOCK), 0, s, a);
+    } else {
+        if (stats)
+            hipLaunchKernelGGL((k_conv3x3<T, false, true>), grid, dim3(CONV_BLOCK), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_conv3x3<T, false, false>), grid, dim3(CONV_BLOCK), 0, s, a);
+    }
+    SHPL_LAUNCH_CHECK();
+    if (stats) {
+        hipLaunchKernelGGL(k_stats_reduce, dim3(pl.n_cob * NCO * 2), dim3(SHPL_BLOCK), 0, s, a.part, (int)pl.n_tiles,
+                           a.c_out, d_stats);
+        SHPL_LAUNCH_CHECK();
+    }
+    return SHPL_OK;
+}
+
+}  // namespace
+}  // namespace shpl
+
+using namespace shpl;
+
+extern "C" int shpl_conv3x3_workspace_bytes(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_t c_b,
+                                            int64_t c_out, int pooled, int stats, size_t *bytes) {
+    if (!bytes) return SHPL_ERR_ARG;
+    ConvPlan pl;
+    const int rc = conv_plan(dtype, n_frames, h, w, c_a, c_b, c_out, pooled != 0, stats != 0, &pl);
+    if (rc) return rc;
+    *bytes = pl.total;
+    return SHPL_OK;
+}
+
+extern "C" int shpl_conv3x3(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a, int64_t a_stride,
+                            int64_t a_off, int64_t c_a, const void *d_b, int64_t b_stride, int64_t b_off,
+                            int64_t c_b, const shpl_csr *pool, const int64_t *d_frame_off, const void *d_weights,
+                            int64_t c_out, const float *d_center, const float *d_scale, const float *d_shift,
+                            int act, void *d_out, int64_t out_stride, double *d_stats, void *d_ws, size_t ws_bytes,
+                            void *stream) {
+    const bool pooled = pool != nullptr, stats = d_stats != nullptr;
+    ConvPlan pl;
+    int rc = conv_plan(dtype, n_frames, h, w, c_a, c_b, c_out, pooled, stats, &pl);
+    if (rc) return rc;
+    if (act != 0 && act != 1) return SHPL_ERR_ARG;
+    if (!d_weights || (ws_bytes > 0 && !d_ws)) return SHPL_ERR_ARG;
+    if (ws_bytes < pl.total) return SHPL_ERR_WORKSPACE;
+    if (a_stride < a_off + c_a || out_stride < c_out || a_off < 0 || b_off < 0) return SHPL_ERR_BAD_SHAPE;
+    if (c_b > 0 && b_stride < b_off + c_b) return SHPL_ERR_BAD_SHAPE;
+    if (pooled) {
+        if (!d_frame_off || c_b < 1 || !d_b) return SHPL_ERR_ARG;
+        if (pool->n_keys != (int64_t)n_frames * h * w) return SHPL_ERR_BAD_SHAPE;
+        if (pool->nnz_cap > 0 && (!pool->ent_dst || !pool->ent_src || !pool->ent_val)) return SHPL_ERR_ARG;
+    } else if (c_b > 0 && !d_b) {
+        return SHPL_ERR_ARG;
+    }
+    if (pl.n_tiles == 0) return SHPL_OK;
+    if (!d_out || (c_a > 0 && !d_a)) return SHPL_ERR_ARG;
+    const int esz = dtype == SHPL_F32 ? 4 : 2, he = 16 / esz;
+    ConvArgs a;
+    a.n_frames = n_frames;
+    a.h = (int)h;
+    a.w = (int)w;
+    a.tiles_x = pl.tiles_x;
+    a.tiles_per_frame = pl.tiles_per_frame;
+    a.n_tiles = (int)pl.n_tiles;
+    a.a = d_a;
+    a.a_stride = a_stride;
+    a.a_off = a_off;
+    a.c_a = (int)c_a;
+    a.qa = pl.qa;
+    a.b = d_b;
+    a.b_stride = b_stride;
+    a.b_off = b_off;
+    a.c_b = (int)c_b;
+    a.qb = pl.qb;
+    a.vec_a = aligned16(d_a) && a_stride % he == 0 && a_off % he == 0;
+    a.vec_b = aligned16(d_b) && b_stride % he == 0 && b_off % he == 0;
+    a.ent_dst = pooled ? pool->ent_dst : nullptr;
+    a.ent_src = pooled ? pool->ent_src : nullptr;
+    a.ent_val = pooled ? pool->ent_val : nullptr;
+    uint8_t *ws = reinterpret_cast<uint8_t *>(d_ws);
+    a.wp = ws;
+    a.row_ptr = pooled ? reinterpret_cast<const int32_t *>(ws + pl.wp_bytes) : nullptr;
+    a.part = stats ? reinterpret_cast<double *>(ws + pl.wp_bytes + pl.rp_bytes) : nullptr;
+    a.center = d_center;
+    a.scale = d_scale;
+    a.shift = d_shift;
+    a.act = act;
+    a.out = d_out;
+    a.out_stride = out_stride;
+    a.c_out = (int)c_out;
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == SHPL_F32) return conv_launch<float>(pl, a, pooled, stats, d_weights, d_frame_off, d_stats, s);
+    return conv_launch<uint16_t>(pl, a, pooled, stats, d_weights, d_frame_off, d_stats, s);
+}
+
+extern "C" int shpl_batch_norm(int dtype, int64_t rows, void *d_x, int64_t stride, int64_t c, const double *d_stats,
+                               double count, float eps, const float *d_gamma, const float *d_beta, int act,
+                               float *d_moving_mean, float *d_moving_var, float decay, float *d_batch_mean,
+                               float *d_batch_var, float *d_ws, void *stream) {
+    if (dtype != SHPL_F32 && dtype != SHPL_BF16) return SHPL_ERR_ARG;
+    if (rows < 0 || c < 1 || stride < c || c > (1 << 16)) return SHPL_ERR_BAD_SHAPE;
+    if (act != 0 && act != 1) return SHPL_ERR_ARG;
+    if (!d_stats || !d_ws || (rows > 0 && !d_x) || !(count > 0.0)) return SHPL_ERR_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    float *mean = d_ws, *scale = d_ws + c;
+    hipLaunchKernelGGL(k_bn_finalize, dim3(1), dim3(SHPL_BLOCK), 0, s, d_stats, count, (int)c, eps, d_gamma, mean,
+                       scale, d_moving_mean, d_moving_var, decay, d_batch_mean, d_batch_var);
+    SHPL_LAUNCH_CHECK();
+    if (rows == 0) return SHPL_OK;
+    const int grid = grid_for(rows * c, SHPL_BLOCK, 1 << 16);
+    if (dtype == SHPL_F32)
+        hipLaunchKernelGGL(k_bn_apply<float>, dim3(grid), dim3(SHPL_BLOCK), 0, s, reinterpret_cast<float *>(d_x), rows,
+                           stride, (int)c, mean, scale, d_beta, act);
+    else
+        hipLaunchKernelGGL(k_bn_apply<uint16_t>, dim3(grid), dim3(SHPL_BLOCK), 0, s, reinterpret_cast<uint16_t *>(d_x),
+                           rows, stride, (int)c, mean, scale, d_beta, act);
+    SHPL_LAUNCH_CHECK();
+    return SHPL_OK;
+}

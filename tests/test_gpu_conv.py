@@ -1,0 +1,260 @@
+"""Post-fusion 3x3 conv (shpl_conv3x3 / shpl_batch_norm)
+vs the CPU oracle on MI355X.
+
+The reference's Conv2D / FusedBatchNorm run through Eigen contractions that
+fix no summation order, so the oracle sums in double and the HIP kernel in
+f32 (exact f32 MFMA products, f32 accumulation). The tolerance is the
+north_star's 1e-5 plus the f32 summation error of a K = 9*Cin term dot
+product, 2^-19 * sum_k |a_k * w_k| (about 16 ulp of the absolute sum; TF's
+own f32 Conv2D carries an error of the same order against the exact sum).
+The fused form (pooled channels computed from the CSR inside the conv's
+staging) must be BITWISE equal to the conv of the materialised bv_fused.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import shpl_oracle as orc
+from sparse_pooling_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+ACC = 2.0 ** -19  # f32 accumulation term, relative to sum |a*w|
+DEV = "cuda"
+
+
+def _bound(x, w, scale=None):
+    """Per-output tolerance: TOL + ACC * sum_k |x_k w_k| (times |scale|)."""
+    _, ab = orc.conv3x3(np.abs(x), np.abs(w), raw=True)
+    b = ACC * ab
+    if scale is not None:
+        b = b * np.abs(scale)
+    return TOL + b
+
+
+def _assert_within(got, ref, bound):
+    err = np.abs(_np(got).astype(np.float64) - ref)
+    assert (err <= bound).all(), (err.max(), (err / bound).max())
+
+
+def _np(t):
+    return t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t)
+
+
+def _weights(cin, cout, seed):
+    rng = np.random.default_rng(seed)
+    lim = np.sqrt(6.0 / (9 * cin + 9 * cout))
+    # 3x xavier: outputs of a few units on N(0,1) inputs
+    return (3.0 * rng.uniform(-lim, lim, (3, 3, cin, cout))).astype(np.float32)
+
+
+def _t(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def _bf16(a):
+    return torch.from_numpy(orc.to_bf16_bits(a).view(np.int16)).to(DEV).view(torch.bfloat16)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from sparse_pooling_amd import _lib as L
+    L.lib()
+    assert torch.cuda.is_available()
+
+
+SHAPES = [  # B, H, W, Cin, Cout: partial tiles, channel tails, several output blocks
+    (1, 9, 33, 10, 5),
+    (2, 16, 64, 64, 32),
+    (1, 5, 7, 3, 40),
+    (3, 17, 70, 24, 33),
+    (1, 1, 1, 8, 1),
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+@pytest.mark.parametrize("epi", ["none", "bias_relu", "bn_infer"])
+def test_conv_dense_vs_oracle(shape, epi):
+    from sparse_pooling_amd import fusion_conv as fc
+    B, H, W, Cin, Cout = shape
+    x = synth.make_features((B, H, W, Cin), 3)
+    w = _weights(Cin, Cout, 4)
+    rng = np.random.default_rng(5)
+    center = scale = shift = None
+    if epi == "bias_relu":
+        shift = rng.standard_normal(Cout).astype(np.float32)
+    elif epi == "bn_infer":
+        center = rng.standard_normal(Cout).astype(np.float32)
+        scale = rng.uniform(0.5, 2.0, Cout).astype(np.float32)
+        shift = rng.standard_normal(Cout).astype(np.float32)
+    relu = epi != "none"
+    y = fc.conv3x3(_t(x), _t(w), center=None if center is None else _t(center),
+                   scale=None if scale is None else _t(scale), shift=None if shift is None else _t(shift), relu=relu)
+    ref = orc.conv3x3(x, w, center, scale, shift, relu)
+    _assert_within(y, ref, _bound(x, w, scale))
+
+
+def test_conv_two_dense_sources_equal_concat():
+    """Channels split over two tensors == the conv of their concatenation,
+    bitwise when the split falls on a staging chunk (8 f32 channels)."""
+    from sparse_pooling_amd import fusion_conv as fc
+    a = synth.make_features((2, 12, 40, 16), 6)
+    b = synth.make_features((2, 12, 40, 24), 7)
+    w = _weights(40, 32, 8)
+    y2 = fc.conv3x3(_t(a), _t(w), b=_t(b), relu=False)
+    y1 = fc.conv3x3(_t(np.concatenate([a, b], -1)), _t(w), relu=False)
+    np.testing.assert_array_equal(_np(y2), _np(y1))
+    ab = np.concatenate([a, b], -1)
+    bound = _bound(ab, w)
+    _assert_within(y1, orc.conv3x3(ab, w), bound)
+    # a split off the chunk grid (12 + 28) still computes the same conv
+    y3 = fc.conv3x3(_t(np.ascontiguousarray(ab[..., :12])), _t(w), b=_t(np.ascontiguousarray(ab[..., 12:])),
+                    relu=False)
+    _assert_within(y3, orc.conv3x3(ab, w), bound)
+
+
+def _batch_map(cfg, n_frames, seed):
+    from sparse_pooling_amd import pipeline, shpl_map as sm
+    spec = synth.CONFIGS[cfg]
+    frames = [synth.make_frame(spec, seed=seed + f, n_outside=20 * f) for f in range(n_frames)]
+    pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
+    ib = sm.build_index_batch(pts, vox, off, P, spec.im_size, spec.bv_size, spec.stride, maxp)
+    return spec, frames, ib
+
+
+@pytest.mark.parametrize("cfg,n_frames", [(1, 3), (2, 2)])
+def test_fused_pool_conv_is_the_conv_of_bv_fused(cfg, n_frames):
+    """FusionConv.fused (pooling inside the conv's staging, bv_fused never
+    written) == FusionConv(bv_fused) bitwise, and == the oracle's conv of the
+    oracle's bv_fused within TOL (checked on a band of rows at config 2)."""
+    from sparse_pooling_amd import fusion_conv as fc, shpl_map as sm
+    spec, frames, ib = _batch_map(cfg, n_frames, 500)
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    Cb, Ci = spec.c_bev, spec.c_img
+    bev = synth.make_features((n_frames, Hb, Wb, Cb), 11)
+    img = synth.make_features((n_frames, Hi, Wi, Ci), 12)
+    tb, ti = _t(bev), _t(img)
+    conv = fc.FusionConv(Cb + Ci, Ci, device=DEV, seed=3)
+    conv.weights = _t(_weights(Cb + Ci, Ci, 13))
+    conv.moving_mean = _t(np.random.default_rng(1).standard_normal(Ci).astype(np.float32) * 0.1)
+    conv.beta = _t(np.random.default_rng(2).standard_normal(Ci).astype(np.float32) * 0.1)
+    bv_fused = sm.pool_img_to_bev(ib.map, ti, tb.shape, bev=tb)
+    y_unf = conv(bv_fused)
+    y_fus = conv.fused(tb, ti, ib.map)
+    torch.cuda.synchronize()
+    assert ib.map.error_bits() == 0
+    np.testing.assert_array_equal(_np(y_fus), _np(y_unf))
+    # oracle: bv_fused per frame (TF-order pooling), conv in double, on a band of rows
+    center, scale, shift = (_np(v) for v in conv._inference_epilogue())
+    y0, y1 = (0, Hb) if cfg == 1 else (300, 340)
+    fo, fn = _np(ib.frame_off), _np(ib.frame_nnz)
+    for f, fr in enumerate(frames):
+        gen = orc.gen_sparse_pooling_input_avod(fr.points, fr.voxel_indices, fr.P, list(spec.im_size),
+                                                tuple(spec.bv_size))
+        ref = orc.produce_sparse_pooling_input(gen, stride=spec.stride)
+        eb, _ = orc.sparse_pool_layer(bev[f:f + 1], img[f:f + 1], ref["Mij_pool"], ref["M_val"], ref["M_size"],
+                                      ref["img_index_flip_pool"])
+        np.testing.assert_array_equal(_np(bv_fused[f:f + 1]), eb)
+        lo, hi = max(y0 - 1, 0), min(y1 + 1, Hb)
+        band = orc.conv3x3(eb[:, lo:hi], _np(conv.weights), center, scale, shift, True)
+        bound = _bound(eb[:, lo:hi], _np(conv.weights), scale)
+        sl = slice(y0 - lo, y0 - lo + (y1 - y0))
+        _assert_within(y_fus[f:f + 1, y0:y1], band[:, sl], bound[:, sl])
+
+
+def test_fused_conv_noncanonical_map():
+    """Shuffled entries, cells with many entries (the run walk), negative
+    weights, an empty frame-less corner, odd channel counts (scalar staging)."""
+    from sparse_pooling_amd import fusion_conv as fc, shpl_map as sm
+    rng = np.random.default_rng(31)
+    n, hb, wb, h, w, cb, ci, cout = 700, 20, 45, 15, 17, 5, 3, 7
+    R = hb * wb
+    idx = np.stack([np.zeros(n, np.int64), rng.integers(0, h, n), rng.integers(0, w, n)], 1)
+    rows = rng.integers(0, R, n)
+    rows[100:260] = rows[100]               # one cell with 160 entries
+    rows[300:340] = rng.integers(0, wb, 40)  # a crowded first row
+    extra = np.stack([rng.integers(0, R, 300), rng.integers(0, n, 300)], 1)
+    mij = np.concatenate([np.stack([rows, np.arange(n)], 1), extra]).astype(np.int64)
+    mij = mij[rng.permutation(len(mij))]
+    mval = rng.uniform(-2, 2, len(mij)).astype(np.float32)
+    img = rng.standard_normal((1, h, w, ci)).astype(np.float32)
+    bev = rng.standard_normal((1, hb, wb, cb)).astype(np.float32)
+    smap = sm.pack_map(_t(mij), _t(mval), [R, n], _t(idx), img.shape)
+    wts = _weights(cb + ci, cout, 32)
+    fused = fc.conv3x3(_t(bev), _t(wts), b=_t(img), pool=smap.csr(0, 0), frame_off=smap.frame_off, relu=False)
+    bv = sm.pool_img_to_bev(smap, _t(img), (1, hb, wb, cb), bev=_t(bev))
+    unf = fc.conv3x3(_t(_np(bv)[..., :cb]), _t(wts), b=_t(_np(bv)[..., cb:]), relu=False)
+    np.testing.assert_array_equal(_np(fused), _np(unf))
+    pooled = orc.sparse_pool_op(mij, mval, [R, n], img, idx).reshape(1, hb, wb, ci)
+    x = np.concatenate([bev, pooled], -1)
+    _assert_within(fused, orc.conv3x3(x, wts), _bound(x, wts))
+
+
+def test_fused_conv_empty_map():
+    from sparse_pooling_amd import fusion_conv as fc, shpl_map as sm
+    bev = synth.make_features((1, 6, 7, 8), 2)
+    img = synth.make_features((1, 9, 11, 8), 1)
+    smap = sm.pack_map(torch.zeros((0, 2), dtype=torch.int64, device=DEV), torch.zeros(0, device=DEV), [42, 0],
+                       torch.zeros((0, 3), dtype=torch.int32, device=DEV), img.shape)
+    wts = _weights(16, 8, 3)
+    y = fc.conv3x3(_t(bev), _t(wts), b=_t(img), pool=smap.csr(0, 0), frame_off=smap.frame_off, relu=False)
+    x = np.concatenate([bev, np.zeros_like(bev)], -1)
+    _assert_within(y, orc.conv3x3(x, wts), _bound(x, wts))
+
+
+def test_batch_norm_training_vs_oracle():
+    """is_training: conv statistics -> batch moments -> normalise + ReLU in
+    place, moving averages with the Bessel-corrected variance."""
+    from sparse_pooling_amd import fusion_conv as fc
+    B, H, W, Cin, Cout = 2, 19, 37, 24, 40
+    x = synth.make_features((B, H, W, Cin), 9) + 0.5
+    w = _weights(Cin, Cout, 10)
+    conv = fc.FusionConv(Cin, Cout, device=DEV)
+    conv.weights = _t(w)
+    rng = np.random.default_rng(3)
+    beta = rng.standard_normal(Cout).astype(np.float32)
+    mm0 = rng.standard_normal(Cout).astype(np.float32)
+    mv0 = rng.uniform(0.5, 2, Cout).astype(np.float32)
+    conv.beta, conv.moving_mean, conv.moving_var = _t(beta), _t(mm0), _t(mv0)
+    y = conv(_t(x), is_training=True)
+    _, raw = orc.conv3x3(x, w, raw=True)
+    ey, bm, bv, emm, emv = orc.batch_norm_train(raw, 1e-3, None, beta, True, mm0, mv0, 0.999)
+    k = 1.0 / np.sqrt(bv * (B * H * W - 1) / (B * H * W) + 1e-3)
+    _assert_within(y, ey, _bound(x, w, k) + 1e-6 * np.abs(ey))
+    np.testing.assert_allclose(_np(conv.moving_mean), emm, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(_np(conv.moving_var), emv, rtol=1e-6, atol=1e-7)
+    # inference afterwards uses the moving statistics
+    yi = conv(_t(x), is_training=False)
+    k = 1.0 / np.sqrt(emv.astype(np.float64) + 1e-3)
+    _assert_within(yi, orc.conv3x3(x, w, emm, k, beta, True), _bound(x, w, k))
+
+
+def test_bf16_conv_and_fused():
+    """bf16 storage: bf16 MFMA products are exact, f32 accumulation, one
+    rounding at the store (|err| <= one bf16 ulp of the f32 result + TOL)."""
+    from sparse_pooling_amd import fusion_conv as fc, shpl_map as sm
+    spec, frames, ib = _batch_map(1, 2, 600)
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    bev = orc.from_bf16_bits(orc.to_bf16_bits(synth.make_features((2, Hb, Wb, 16), 21)))
+    img = orc.from_bf16_bits(orc.to_bf16_bits(synth.make_features((2, Hi, Wi, 16), 22)))
+    w = orc.from_bf16_bits(orc.to_bf16_bits(_weights(32, 16, 23)))
+    tb, ti, tw = _bf16(bev), _bf16(img), _bf16(w)
+    bv = sm.pool_img_to_bev(ib.map, ti, tb.shape, bev=tb)
+    y_unf = fc.conv3x3(bv, tw, relu=False)
+    y_fus = fc.conv3x3(tb, tw, b=ti, pool=ib.map.csr(0, 0), frame_off=ib.map.frame_off, relu=False)
+    np.testing.assert_array_equal(_np(y_fus.float()), _np(y_unf.float()))
+    x = _np(bv.float())
+    ref = orc.conv3x3(x, w)
+    _assert_within(y_unf.float(), ref, _bound(x, w) + np.abs(ref) * 2.0 ** -8)
+
+
+def test_conv_argument_errors():
+    from sparse_pooling_amd import fusion_conv as fc, _lib as L
+    x = _t(synth.make_features((1, 4, 4, 8), 1))
+    with pytest.raises(ValueError):
+        fc.conv3x3(x, _t(_weights(9, 4, 1)))
+    with pytest.raises(L.ShplLibraryError):
+        fc.conv3x3(x, _t(_weights(8, 4, 1)), ws=torch.empty(16, dtype=torch.uint8, device=DEV))
