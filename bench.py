@@ -42,6 +42,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+# dense MFMA peaks (MI355X_MICROARCH.md, Matrix cores): f32-input 157.3 TF, bf16 ~2.5 PF
+MFMA_PEAK_TFS = {"f32": 157.3, "bf16": 2500.0}
 DEFAULT_FRAMES = {2: 64, 3: 4, 5: 64}
 
 
@@ -62,9 +64,13 @@ def parse():
                          "profiles/r01_groups.log)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step eagerly instead of replaying one captured HIP graph of it")
-    ap.add_argument("--workload", default="layer", choices=["layer", "frames"],
+    ap.add_argument("--workload", default="layer", choices=["layer", "frames", "conv"],
                     help="layer: BASELINE configs 2/3/5 from prepared points + voxel indices (default); "
-                         "frames: raw velodyne scans -> loader -> BEV slices -> index -> fused layer")
+                         "frames: raw velodyne scans -> loader -> BEV slices -> index -> fused layer; "
+                         "conv: config 2 + the post-fusion 3x3 conv/BN/ReLU (rpn_model.py:338-346) with the "
+                         "pooling fused into the conv (SURVEY §8f row 4)")
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"], help="conv workload storage dtype")
+    ap.add_argument("--train-bn", action="store_true", help="conv workload: BatchNorm in training mode")
     ap.add_argument("--scan-points", type=int, default=120000, help="points per velodyne scan (frames)")
     return ap.parse_args()
 
@@ -151,8 +157,8 @@ def main():
 
     from sparse_pooling_amd import dist as sd, pipeline, synth
 
-    if args.workload == "frames":
-        run_frames(args, world, rank, dev)
+    if args.workload in ("frames", "conv"):
+        (run_frames if args.workload == "frames" else run_conv)(args, world, rank, dev)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -446,6 +452,151 @@ def run_frames(args, world, rank, dev):
             "index_errors": errs,
         }
         print(json.dumps(out), flush=True)
+
+
+def cpu_baseline_conv(spec, frames_np, budget_s):
+    """Oracle on one core: index build + TF-order pooling + concat of one frame,
+    and the conv/BN/ReLU over a band of rows of it, scaled to the frame."""
+    from oracle import shpl_oracle as orc
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    cb, ci = spec.c_bev, spec.c_img
+    rng = np.random.default_rng(0)
+    bev = rng.standard_normal((1, Hb, Wb, cb), dtype=np.float32)
+    img = rng.standard_normal((1, Hi, Wi, ci), dtype=np.float32)
+    w = (rng.standard_normal((3, 3, cb + ci, ci)) * 0.05).astype(np.float32)
+    sc = np.full(ci, 1.0 / np.sqrt(1.0 + 1e-3), np.float32)
+    fr = frames_np[0]
+    a = time.perf_counter()
+    g = orc.gen_sparse_pooling_input_avod(fr.points, fr.voxel_indices, fr.P, list(spec.im_size), tuple(spec.bv_size))
+    ref = orc.produce_sparse_pooling_input(g, stride=spec.stride)
+    b = time.perf_counter()
+    eb, _ = orc.sparse_pool_layer(bev, img, ref["Mij_pool"], ref["M_val"], ref["M_size"], ref["img_index_flip_pool"])
+    c = time.perf_counter()
+    rows, t_conv = 0, 0.0
+    band = 8
+    while rows < band or (t_conv < budget_s and rows + band <= Hb):
+        d = time.perf_counter()
+        orc.conv3x3(eb[:, max(rows - 1, 0):min(rows + band + 1, Hb)], w, None, sc, None, True)
+        t_conv += time.perf_counter() - d
+        rows += band
+    conv_frame = t_conv * Hb / rows
+    total = (b - a) + (c - b) + conv_frame
+    return {"value": round(1.0 / total, 4), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": (f"1 frame ({spec.n_points} pts) through oracle/shpl_oracle.c, single thread: index "
+                       f"{1e3 * (b - a):.1f} ms + TF-order pooling and concat {1e3 * (c - b):.1f} ms + 3x3 conv/BN/"
+                       f"ReLU (double accumulation) timed on {rows} of {Hb} rows, scaled: {1e3 * conv_frame:.0f} ms; "
+                       f"{os.cpu_count()} host cpus visible")}
+
+
+def run_conv(args, world, rank, dev):
+    """Config 2 + the post-fusion conv: index build -> cell CSR ->
+    conv3x3(BN, ReLU) of [bev || pool(img)] with the pooling inside the conv's staging
+    (bv_fused never written). The unfused form (fused layer -> bv_fused -> conv) is
+    timed beside it."""
+    from sparse_pooling_amd import dist as sd, fusion_conv as fc, pipeline, synth
+    spec = synth.CONFIG2
+    F = args.frames or 64
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    frames = [synth.make_frame(spec, seed=s, n_outside=200) for s in sd.frame_seeds(rank, F)]
+    pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, dev)
+    pl = pipeline.FusedPipeline(F, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev, spec.c_img,
+                                dtype=dtype, device=dev)
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    cb, ci = spec.c_bev, spec.c_img
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    bev = torch.randn((F, Hb, Wb, cb), device=dev, generator=g).to(dtype)
+    img = torch.randn((F, Hi, Wi, ci), device=dev, generator=g).to(dtype)
+    conv = fc.FusionConv(cb + ci, ci, dtype=dtype, device=dev, seed=rank)
+    out = torch.empty((F, Hb, Wb, ci), dtype=dtype, device=dev)
+    out_unf = torch.empty_like(out)
+    train = args.train_bn
+
+    def step(ev=None):
+        pl.build_index(pts, vox, off, P)
+        pl.build_csr(("cell",))
+        if ev is not None:
+            ev[0].record()
+        conv.fused_csr(bev, img, pl.csr, pl.frame_off, is_training=train, out=out)
+        if ev is not None:
+            ev[1].record()
+
+    def unfused(ev):
+        ev[0].record()
+        pl.layer_dense(bev, img)
+        pl.layer_sparse(bev, img)
+        ev[1].record()
+        conv(pl.bv_fused, is_training=train, out=out_unf)
+        ev[2].record()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    err = int(pl.err.item())
+    graph = None
+    if not args.no_graph and not train:
+        gstream = torch.cuda.Stream(device=dev)
+        gstream.wait_stream(torch.cuda.current_stream(dev))
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=gstream):
+            step()
+        graph.replay()
+        torch.cuda.synchronize()
+    n_ev = min(args.steps, 10)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(n_ev)]
+    if graph is not None:
+        elapsed = sd.timed(lambda k: graph.replay(), args.steps, device=dev)
+    else:
+        elapsed = sd.timed(lambda k: step(), args.steps, device=dev)
+    for k in range(n_ev):
+        step(evs[k])
+    uev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(n_ev)]
+    for k in range(n_ev):
+        unfused(uev[k])
+    torch.cuda.synchronize()
+    same = bool(torch.equal(out, out_unf))
+    conv_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / n_ev
+    pull_ms = sum(e[0].elapsed_time(e[1]) for e in uev) / n_ev
+    uconv_ms = sum(e[1].elapsed_time(e[2]) for e in uev) / n_ev
+    esz = 2 if dtype == torch.bfloat16 else 4
+    flops = 2.0 * F * Hb * Wb * 9 * (cb + ci) * ci
+    nnz = int(pl.frame_nnz.sum().item())
+    u_pix = int(torch.unique(pl.pix[pl.pix >= 0]).numel())
+    hbm_bytes = F * Hb * Wb * (cb + ci) * esz + u_pix * ci * esz + 12 * nnz  # read bev, write out, gather
+    tflops = flops / (conv_ms * 1e-3) / 1e12
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_conv(spec, frames[:1], args.cpu_seconds)
+    if rank == 0:
+        dname = "bf16" if esz == 2 else "f32"
+        out_j = {
+            "metric": "SHPL + post-fusion conv frames/sec (MFMA roofline), 1/2/4/8 GPU",
+            "value": round(F * world * args.steps / elapsed, 2), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dname,
+            "data": "synthetic (seeded KITTI-shaped frames, xavier-initialised conv weights; no dataset on the box)",
+            "config": {"workload": (f"conv: config2 ({spec.n_points} pts/frame, BEV {Hb}x{Wb}x{cb}, img {Hi}x{Wi}x{ci})"
+                                    f" -> index -> cell CSR -> conv3x3 {cb + ci}->{ci} + BatchNorm "
+                                    f"({'training' if train else 'inference'}) + ReLU of [bev || pool(img)], pooling "
+                                    "fused into the conv's staging (rpn_model.py:338-346)"),
+                       "frames_per_gpu_per_step": F, "hip_graph": graph is not None,
+                       "parallelism": f"frame-sharded x{world}"},
+            "roofline": {"bound": "mfma", "kernel": "k_conv3x3 (fused pooling), MFMA "
+                         + ("v_mfma_f32_32x32x16_bf16" if esz == 2 else "v_mfma_f32_32x32x2_f32"),
+                         "achieved": round(tflops, 2), "peak": MFMA_PEAK_TFS[dname], "unit": "TFLOP/s",
+                         "frac": round(tflops / MFMA_PEAK_TFS[dname], 4), "traffic": None,
+                         "algorithmic_flops_per_launch": flops, "kernel_ms": round(conv_ms, 4),
+                         "hbm_algorithmic_bytes_per_launch": hbm_bytes,
+                         "hbm_GBps": round(hbm_bytes / (conv_ms * 1e-3) / 1e9, 1)},
+            "unfused": {"pull_ms": round(pull_ms, 4), "conv_ms": round(uconv_ms, 4),
+                        "total_ms": round(pull_ms + uconv_ms, 4), "fused_conv_ms": round(conv_ms, 4),
+                        "bitwise_equal": same},
+            "cpu_baseline": cpu,
+            "index_errors": err,
+        }
+        print(json.dumps(out_j), flush=True)
 
 
 if __name__ == "__main__":

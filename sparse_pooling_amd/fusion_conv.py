@@ -152,5 +152,9 @@ class FusionConv:
     def fused(self, bev, img, smap, is_training=False, out=None):
         """The conv of [bev || _sparse_pool_op(M, img)] without writing the
         concat: ``smap`` is the ShplMap of the frames of ``bev``."""
-        csr = smap.csr(L.BY_CELL, L.ORDER_ENTRY)
-        return self._run(bev, img, csr, smap.frame_off, is_training, out)
+        return self.fused_csr(bev, img, smap.csr(L.BY_CELL, L.ORDER_ENTRY), smap.frame_off, is_training, out)
+
+    def fused_csr(self, bev, img, csr, frame_off, is_training=False, out=None):
+        """fused() over an already built cell-keyed CSR (``_lib.Csr``) and the
+        per-frame entry slots ``frame_off`` (FusedPipeline.csr / .frame_off)."""
+        return self._run(bev, img, csr, frame_off, is_training, out)
