@@ -330,8 +330,10 @@ typedef enum { SHPL_ACT_NONE = 0, SHPL_ACT_RELU = 1 } shpl_act;
  *                 cell-keyed CSR (shpl_build_csr SHPL_BY_CELL, SHPL_ORDER_ENTRY,
  *                 n_keys = n_frames*h*w, entry slots of frame f from
  *                 d_frame_off[f] on) over the image map d_b, with the
- *                 arithmetic of shpl_pull: the result is bitwise the conv of
- *                 [a || shpl_pull(SHPL_BY_CELL, ...)] without writing it.
+ *                 arithmetic of shpl_pull: the result is the conv of
+ *                 [a || shpl_pull(SHPL_BY_CELL, ...)] without writing it --
+ *                 bitwise, when c_a is a multiple of the staging chunk (8 f32
+ *                 / 16 bf16 channels; otherwise the K order differs).
  * d_weights: HWIO [3][3][c_a+c_b][c_out] in the feature dtype (slim.conv2d's
  * variable). d_center / d_scale / d_shift: optional [c_out] f32 (NULL = 0 / 1
  * / 0) -- BatchNorm inference: center = moving_mean, scale = gamma /

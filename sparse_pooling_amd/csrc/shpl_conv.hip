@@ -16,16 +16,18 @@
 // output tile of one frame; wave w owns tile rows 2w and 2w+1 (two 32-pixel
 // M subtiles against all 32 channels: v_mfma_f32_32x32x2_f32 for f32,
 // v_mfma_f32_32x32x16_bf16 for bf16 storage, f32 accumulation in both).
-// The input channels are walked in chunks of 32 bytes per pixel (8 f32 / 16
-// bf16): a chunk of the 10 x 34 halo tile and the chunk's 9 x 32 weights are
-// staged in LDS (48-byte rows: conflict-free ds_read_b128), then 9 taps of
-// MFMAs consume them.
+// The input channels are walked in chunks (8 f32 / 16 bf16 channels): a
+// chunk of the 10 x 34 halo tile and the chunk's 9 x 32 weights are staged
+// in LDS (rows padded by 16 B: conflict-free ds_read_b128), then 9 taps of
+// MFMAs consume them. Staging is synchronous; 4-5 workgroups per CU keep
+// the MFMAs busy across each other's staging.
 //
 // Input channels [0, c_a) come from tensor A (the BEV map), [c_a, c_a+c_b)
 // from tensor B. B is either a dense tensor (the materialised pooled map, or
 // nothing) or -- POOLED -- the image feature map read through the img->BEV
-// CSR of shpl_build_csr: the chunk is zero-filled and the halo cells that own
-// entries get their pooled vector computed on the spot, with exactly the
+// CSR of shpl_build_csr: the tile's runs of entries (one per occupied halo
+// cell) are listed once in LDS; each pooled chunk is zero where no entry
+// lands and the run's pooled vector elsewhere, computed on the spot with the
 // arithmetic of k_sparse (shpl_pull.hip: TF order, separate multiply and
 // add), so the conv of the fused form is bitwise the conv of
 // [bev || shpl_pull(...)] and bv_fused never reaches HBM.
@@ -43,18 +45,20 @@ constexpr int TH = 8, TW = 32;              // output tile (rows x columns)
 constexpr int HH = TH + 2, HWD = TW + 2;    // halo tile
 constexpr int NCO = 32;                     // output channels per workgroup
 constexpr int CONV_BLOCK = 256;             // 4 waves, wave w: tile rows 2w, 2w+1
-constexpr int CHUNK_B = 32;                 // bytes of one pixel's chunk (8 f32 / 16 bf16)
-constexpr int PSTR = 48;                    // LDS row stride: 32 B + 16 B pad
-constexpr int IN_HALVES = HH * HWD * 2;     // 16-byte pieces of a staged input chunk
 constexpr int W_ROWS = 9 * NCO;             // weight rows of a chunk (tap, out channel)
-constexpr int W_HALVES = W_ROWS * 2;
-constexpr int IN_LDS = HH * HWD * PSTR;
-constexpr int W_LDS = W_ROWS * PSTR;
 
+// One chunk = the input channels staged per LDS round, 32 B per pixel: 8
+// f32 channels (4 f32 MFMAs of K=2 per tap) or 16 bf16 channels (one bf16
+// MFMA of K=16 per tap). 64 B bf16 chunks measured slower (fewer workgroups
+// per CU). LDS rows are padded by 16 B: ds_read_b128 of 16 consecutive
+// pixels then hits 16 distinct bank quads.
 template <typename T>
 struct Elem {
-    static constexpr int CK = CHUNK_B / sizeof(T);  // channels per chunk
-    static constexpr int HE = 16 / sizeof(T);       // channels per 16-byte piece
+    static constexpr int CB = 32;                        // chunk bytes per pixel
+    static constexpr int CK = CB / sizeof(T);            // channels per chunk
+    static constexpr int HE = 16 / sizeof(T);            // channels per 16-byte piece
+    static constexpr int NP = CB / 16;                   // pieces per pixel
+    static constexpr int PSTR = CB + 16;                 // LDS row stride
     static __device__ __forceinline__ float f(T v) {
         if constexpr (sizeof(T) == 4)
             return v;
@@ -122,13 +126,52 @@ __device__ __forceinline__ int32_t lower_bound(const int32_t *v, int32_t lo, int
     return lo;
 }
 
+// Pooled vector of one occupied cell for the channels [c0, c0 + CK) of the
+// chunk: sum over the cell's run of CSR entries [e0, e1) of val * img[src],
+// in entry order with separate multiply and add from 0 -- the arithmetic of
+// k_sparse (shpl_pull.hip) -- written to the cell's LDS row.
+template <typename T>
+__device__ __forceinline__ void pool_run(const ConvArgs &p, const T *img, int c0, int32_t e0, int32_t e1,
+                                         int32_t src0, float val0, uint8_t *dst) {
+    typedef Elem<T> E;
+    constexpr int HE = E::HE;
+    for (int g = 0; g < E::NP; ++g) {  // one 16-byte piece (4 f32 / 8 bf16 channels) at a time
+        float sum[HE];
+#pragma unroll
+        for (int c = 0; c < HE; ++c) sum[c] = 0.0f;
+        for (int32_t i = e0; i < e1; ++i) {
+            const T *row = img + (int64_t)(i == e0 ? src0 : p.ent_src[i]) * p.b_stride;
+            const float wv = i == e0 ? val0 : p.ent_val[i];
+            const u32x4 raw = load_piece<T>(row, c0 + g * HE, p.c_b, p.vec_b);
+            T x[HE];
+            __builtin_memcpy(x, &raw, sizeof(raw));
+#pragma unroll
+            for (int c = 0; c < HE; ++c) sum[c] = __fadd_rn(sum[c], __fmul_rn(wv, E::f(x[c])));
+        }
+        T o[HE];
+#pragma unroll
+        for (int c = 0; c < HE; ++c) o[c] = E::back(sum[c]);
+        __builtin_memcpy(dst + g * 16, o, 16);
+    }
+}
+
 template <typename T, bool POOLED, bool STATS>
 __global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3(const ConvArgs p) {
     typedef Elem<T> E;
-    constexpr int CK = E::CK, HE = E::HE;
-    __shared__ __attribute__((aligned(16))) uint8_t s_in[IN_LDS];
-    __shared__ __attribute__((aligned(16))) uint8_t s_w[W_LDS];
+    constexpr int CK = E::CK, HE = E::HE, NP = E::NP, PSTR = E::PSTR;
+    constexpr int NPIX = HH * HWD;  // halo cells; at most one run of entries per cell
+    constexpr int IN_PIECES = NPIX * NP, W_PIECES = W_ROWS * NP;
+    constexpr int IN_IT = (IN_PIECES + CONV_BLOCK - 1) / CONV_BLOCK;
+    constexpr int W_IT = (W_PIECES + CONV_BLOCK - 1) / CONV_BLOCK;
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[NPIX * PSTR];
+    __shared__ __attribute__((aligned(16))) uint8_t s_w[W_ROWS * PSTR];
+    // POOLED: the halo tile's runs of CSR entries (one run = one occupied cell)
     __shared__ int32_t s_lo[HH], s_pre[HH + 1];
+    __shared__ int32_t s_run_pix[POOLED ? NPIX : 1], s_run_e[POOLED ? NPIX : 1], s_run_end[POOLED ? NPIX : 1];
+    __shared__ int32_t s_run_src[POOLED ? NPIX : 1];
+    __shared__ float s_run_val[POOLED ? NPIX : 1];
+    __shared__ uint8_t s_occ[POOLED ? NPIX : 1];
+    __shared__ int64_t s_scan[SHPL_BLOCK / 64 + 1];
     __shared__ float s_red[4][2][NCO];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -143,9 +186,11 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3(const ConvArgs p) {
     const int64_t frame_row0 = (int64_t)f * H * W;
     const int Q = p.qa + p.qb;
 
+    int n_run = 0;
     if (POOLED) {
-        // entry range of each halo row: cells [x0-1, x0+TW+1) of row y, from
-        // the per-row entry pointers and a binary search inside the row
+        // 1. entry range of each halo row: cells [x0-1, x0+TW+1) of row y, from
+        //    the per-row entry pointers and a binary search inside the row
+        for (int j = tid; j < NPIX; j += CONV_BLOCK) s_occ[j] = 0;
         if (tid < HH) {
             const int y = y0 - 1 + tid;
             int32_t lo = 0, hi = 0;
@@ -166,6 +211,41 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3(const ConvArgs p) {
             for (int r = 0; r < HH; ++r) s_pre[r + 1] += s_pre[r];
         }
         __syncthreads();
+        // 2. runs (first / one-past-last entry of each occupied cell) in entry
+        //    order, with the source row and weight of their first entry
+        const int n_ent = s_pre[HH];
+        int n_tail = 0;
+        for (int base = 0; base < n_ent; base += CONV_BLOCK) {
+            const int j = base + tid;
+            int64_t flags = 0;
+            int32_t e = 0, pix = 0;
+            if (j < n_ent) {
+                int r = 0;
+                while (j >= s_pre[r + 1]) ++r;
+                e = s_lo[r] + (j - s_pre[r]);
+                const int32_t last = s_lo[r] + (s_pre[r + 1] - s_pre[r]) - 1;
+                const int32_t d = p.ent_dst[e];
+                const bool head = j == s_pre[r] || p.ent_dst[e - 1] != d;
+                const bool tail = e == last || p.ent_dst[e + 1] != d;
+                flags = (head ? 1 : 0) | (tail ? (int64_t)1 << 32 : 0);
+                const int y = y0 - 1 + r;
+                pix = r * HWD + (int)((int64_t)d - frame_row0 - (int64_t)y * W) - (x0 - 1);
+            }
+            int64_t tot;
+            const int64_t ex = block_excl_scan(flags, s_scan, &tot);
+            if (flags & 1) {
+                const int k = n_run + (int)(ex & 0xffffffff);
+                s_run_e[k] = e;
+                s_run_pix[k] = pix;
+                s_occ[pix] = 1;
+                s_run_src[k] = p.ent_src[e];
+                s_run_val[k] = p.ent_val[e];
+            }
+            if (flags >> 32) s_run_end[n_tail + (int)(ex >> 32)] = e + 1;
+            n_run += (int)(tot & 0xffffffff);
+            n_tail += (int)(tot >> 32);  // a run may open in one round and close in the next
+        }
+        __syncthreads();
     }
 
     f32x16 acc[2];
@@ -175,22 +255,24 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3(const ConvArgs p) {
         for (int i = 0; i < 16; ++i) acc[m][i] = 0.0f;
 
     const T *wq = reinterpret_cast<const T *>(p.wp) + (int64_t)cob * Q * W_ROWS * CK;
+    const T *img = reinterpret_cast<const T *>(p.b) + p.b_off;
     for (int q = 0; q < Q; ++q) {
-        // ---- weights of the chunk: 288 rows of 32 B, contiguous in the packed array
+        // ---- stage chunk q in LDS, synchronously: the other workgroups on the
+        // CU keep the MFMAs busy meanwhile (a register-staged prefetch of chunk
+        // q+1 cost more occupancy than it hid latency)
         {
-            u32x4 v[3];
+            u32x4 v[W_IT];  // weights: 288 rows, contiguous in the packed array
 #pragma unroll
-            for (int u = 0; u < 3; ++u) {
+            for (int u = 0; u < W_IT; ++u) {
                 const int j = tid + u * CONV_BLOCK;
-                if (j < W_HALVES) v[u] = *reinterpret_cast<const u32x4 *>(wq + (int64_t)q * W_ROWS * CK + j * HE);
+                if (j < W_PIECES) v[u] = *reinterpret_cast<const u32x4 *>(wq + ((int64_t)q * W_ROWS * NP + j) * HE);
             }
 #pragma unroll
-            for (int u = 0; u < 3; ++u) {
+            for (int u = 0; u < W_IT; ++u) {
                 const int j = tid + u * CONV_BLOCK;
-                if (j < W_HALVES) *reinterpret_cast<u32x4 *>(s_w + (j >> 1) * PSTR + (j & 1) * 16) = v[u];
+                if (j < W_PIECES) *reinterpret_cast<u32x4 *>(s_w + (j / NP) * PSTR + (j % NP) * 16) = v[u];
             }
         }
-        // ---- input chunk of the halo tile
         const bool from_a = q < p.qa;
         if (from_a || !POOLED) {
             const T *src = reinterpret_cast<const T *>(from_a ? p.a : p.b) + (from_a ? p.a_off : p.b_off);
@@ -198,66 +280,36 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3(const ConvArgs p) {
             const int c_src = from_a ? p.c_a : p.c_b;
             const int c0 = (from_a ? q : q - p.qa) * CK;
             const bool vec = from_a ? p.vec_a : p.vec_b;
-            u32x4 v[3];
+            u32x4 v[IN_IT];
 #pragma unroll
-            for (int u = 0; u < 3; ++u) {
+            for (int u = 0; u < IN_IT; ++u) {
                 const int j = tid + u * CONV_BLOCK;
                 v[u] = u32x4{0u, 0u, 0u, 0u};
-                if (j < IN_HALVES) {
-                    const int pix = j >> 1, hr = pix / HWD, hc = pix - hr * HWD;
+                if (j < IN_PIECES) {
+                    const int pix = j / NP, hr = pix / HWD, hc = pix - hr * HWD;
                     const int y = y0 - 1 + hr, x = x0 - 1 + hc;
                     if (y >= 0 && y < H && x >= 0 && x < W)
-                        v[u] = load_piece<T>(src + (frame_row0 + (int64_t)y * W + x) * stride, c0 + (j & 1) * HE,
+                        v[u] = load_piece<T>(src + (frame_row0 + (int64_t)y * W + x) * stride, c0 + (j % NP) * HE,
                                              c_src, vec);
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 3; ++u) {
+            for (int u = 0; u < IN_IT; ++u) {
                 const int j = tid + u * CONV_BLOCK;
-                if (j < IN_HALVES) *reinterpret_cast<u32x4 *>(s_in + (j >> 1) * PSTR + (j & 1) * 16) = v[u];
+                if (j < IN_PIECES) *reinterpret_cast<u32x4 *>(s_in + (j / NP) * PSTR + (j % NP) * 16) = v[u];
             }
         } else {
-            // pooled chunk: zeros, then the occupied cells' sums (k_sparse arithmetic)
+            // pooled chunk: zeros where no entry lands, each run's sum elsewhere
+            // (disjoint cells: no barrier between the two)
 #pragma unroll
-            for (int u = 0; u < 3; ++u) {
+            for (int u = 0; u < IN_IT; ++u) {
                 const int j = tid + u * CONV_BLOCK;
-                if (j < IN_HALVES)
-                    *reinterpret_cast<u32x4 *>(s_in + (j >> 1) * PSTR + (j & 1) * 16) = u32x4{0u, 0u, 0u, 0u};
+                if (j < IN_PIECES && !s_occ[j / NP])
+                    *reinterpret_cast<u32x4 *>(s_in + (j / NP) * PSTR + (j % NP) * 16) = u32x4{0u, 0u, 0u, 0u};
             }
-            __syncthreads();
-            const T *img = reinterpret_cast<const T *>(p.b) + p.b_off;
-            const int c0 = (q - p.qa) * CK;
-            const int n_ent = s_pre[HH];
-            for (int j = tid; j < n_ent; j += CONV_BLOCK) {
-                int r = 0;
-                while (j >= s_pre[r + 1]) ++r;
-                const int32_t e = s_lo[r] + (j - s_pre[r]);
-                const int32_t e_end = s_lo[r] + (s_pre[r + 1] - s_pre[r]);
-                const int32_t d = p.ent_dst[e];
-                if (j > s_pre[r] && p.ent_dst[e - 1] == d) continue;  // not the first entry of its cell
-                float sum[CK];
-#pragma unroll
-                for (int c = 0; c < CK; ++c) sum[c] = 0.0f;
-                for (int32_t i = e; i < e_end && p.ent_dst[i] == d; ++i) {
-                    const float wv = p.ent_val[i];
-                    const T *row = img + (int64_t)p.ent_src[i] * p.b_stride;
-                    u32x4 raw[2];
-                    raw[0] = load_piece<T>(row, c0, p.c_b, p.vec_b);
-                    raw[1] = load_piece<T>(row, c0 + HE, p.c_b, p.vec_b);
-                    T x[CK];
-                    __builtin_memcpy(x, raw, sizeof(raw));
-#pragma unroll
-                    for (int c = 0; c < CK; ++c) sum[c] = __fadd_rn(sum[c], __fmul_rn(wv, E::f(x[c])));
-                }
-                T o[CK];
-#pragma unroll
-                for (int c = 0; c < CK; ++c) o[c] = E::back(sum[c]);
-                const int y = y0 - 1 + r;
-                const int hc = (int)((int64_t)d - frame_row0 - (int64_t)y * W) - (x0 - 1);
-                uint8_t *dstp = s_in + (r * HWD + hc) * PSTR;
-                __builtin_memcpy(dstp, o, 16);
-                __builtin_memcpy(dstp + 16, reinterpret_cast<uint8_t *>(o) + 16, 16);
-            }
+            for (int k = tid; k < n_run; k += CONV_BLOCK)
+                pool_run<T>(p, img, (q - p.qa) * CK, s_run_e[k], s_run_end[k], s_run_src[k], s_run_val[k],
+                            s_in + s_run_pix[k] * PSTR);
         }
         __syncthreads();
         // ---- 9 taps of MFMA over the chunk
@@ -277,9 +329,13 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3(const ConvArgs p) {
                         for (int s = 0; s < 4; ++s)
                             acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[s], b4[s], acc[m], 0, 0, 0);
                     } else {
-                        const bf16x8 a8 = *reinterpret_cast<const bf16x8 *>(arow);
-                        const bf16x8 b8 = *reinterpret_cast<const bf16x8 *>(wrow);
-                        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a8, b8, acc[m], 0, 0, 0);
+                        // k-step s covers channels 16s .. 16s+15; lane half h holds 16s+8h .. +7
+#pragma unroll
+                        for (int s = 0; s < NP / 2; ++s) {
+                            const bf16x8 a8 = *reinterpret_cast<const bf16x8 *>(arow + 32 * s);
+                            const bf16x8 b8 = *reinterpret_cast<const bf16x8 *>(wrow + 32 * s);
+                            acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a8, b8, acc[m], 0, 0, 0);
+                        }
                     }
                 }
             }
@@ -462,7 +518,8 @@ int conv_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_
     if (n_frames < 0 || h < 0 || w < 0 || c_a < 0 || c_b < 0 || c_out < 1 || c_a + c_b < 1) return SHPL_ERR_BAD_SHAPE;
     if (h > (1 << 20) || w > (1 << 20) || c_a + c_b > (1 << 16) || c_out > (1 << 16)) return SHPL_ERR_BAD_SHAPE;
     const int esz = dtype == SHPL_F32 ? 4 : 2;
-    pl->ck = CHUNK_B / esz;
+    const int chunk_b = 32;  // Elem<T>::CB
+    pl->ck = chunk_b / esz;
     pl->qa = (int)((c_a + pl->ck - 1) / pl->ck);
     pl->qb = (int)((c_b + pl->ck - 1) / pl->ck);
     pl->n_cob = (int)((c_out + NCO - 1) / NCO);
@@ -471,7 +528,7 @@ int conv_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_
     pl->tiles_per_frame = pl->tiles_x * pl->tiles_y;
     pl->n_tiles = (int64_t)n_frames * pl->tiles_per_frame;
     if (pl->n_tiles >= (1LL << 31) || (int64_t)n_frames * h * w >= (1LL << 31)) return SHPL_ERR_BAD_SHAPE;
-    pl->wp_bytes = align_up((size_t)pl->n_cob * (pl->qa + pl->qb) * W_ROWS * CHUNK_B, 256);
+    pl->wp_bytes = align_up((size_t)pl->n_cob * (pl->qa + pl->qb) * W_ROWS * chunk_b, 256);
     pl->rp_bytes = pooled ? align_up((size_t)n_frames * (h + 1) * 4, 256) : 0;
     pl->part_bytes = stats ? align_up((size_t)pl->n_cob * NCO * 2 * pl->n_tiles * 8, 256) : 0;
     pl->total = pl->wp_bytes + pl->rp_bytes + pl->part_bytes;

@@ -233,22 +233,28 @@ def test_batch_norm_training_vs_oracle():
 
 def test_bf16_conv_and_fused():
     """bf16 storage: bf16 MFMA products are exact, f32 accumulation, one
-    rounding at the store (|err| <= one bf16 ulp of the f32 result + TOL)."""
+    rounding at the store (|err| <= one bf16 ulp of the f32 result + TOL).
+    Fused == unfused bitwise needs the BEV channels to end on a staging chunk
+    (16 bf16 channels); a 24-channel BEV still agrees within the bound."""
     from sparse_pooling_amd import fusion_conv as fc, shpl_map as sm
     spec, frames, ib = _batch_map(1, 2, 600)
     Hb, Wb = spec.bev_feat_hw
     Hi, Wi = spec.img_feat_hw
-    bev = orc.from_bf16_bits(orc.to_bf16_bits(synth.make_features((2, Hb, Wb, 16), 21)))
-    img = orc.from_bf16_bits(orc.to_bf16_bits(synth.make_features((2, Hi, Wi, 16), 22)))
-    w = orc.from_bf16_bits(orc.to_bf16_bits(_weights(32, 16, 23)))
-    tb, ti, tw = _bf16(bev), _bf16(img), _bf16(w)
-    bv = sm.pool_img_to_bev(ib.map, ti, tb.shape, bev=tb)
-    y_unf = fc.conv3x3(bv, tw, relu=False)
-    y_fus = fc.conv3x3(tb, tw, b=ti, pool=ib.map.csr(0, 0), frame_off=ib.map.frame_off, relu=False)
-    np.testing.assert_array_equal(_np(y_fus.float()), _np(y_unf.float()))
-    x = _np(bv.float())
-    ref = orc.conv3x3(x, w)
-    _assert_within(y_unf.float(), ref, _bound(x, w) + np.abs(ref) * 2.0 ** -8)
+    for cb, ci in ((16, 16), (24, 8)):
+        bev = orc.from_bf16_bits(orc.to_bf16_bits(synth.make_features((2, Hb, Wb, cb), 21)))
+        img = orc.from_bf16_bits(orc.to_bf16_bits(synth.make_features((2, Hi, Wi, ci), 22)))
+        w = orc.from_bf16_bits(orc.to_bf16_bits(_weights(cb + ci, 16, 23)))
+        tb, ti, tw = _bf16(bev), _bf16(img), _bf16(w)
+        bv = sm.pool_img_to_bev(ib.map, ti, tb.shape, bev=tb)
+        y_unf = fc.conv3x3(bv, tw, relu=False)
+        y_fus = fc.conv3x3(tb, tw, b=ti, pool=ib.map.csr(0, 0), frame_off=ib.map.frame_off, relu=False)
+        x = _np(bv.float())
+        ref = orc.conv3x3(x, w)
+        bound = _bound(x, w) + np.abs(ref) * 2.0 ** -8
+        _assert_within(y_unf.float(), ref, bound)
+        _assert_within(y_fus.float(), ref, bound)
+        if cb % 16 == 0:
+            np.testing.assert_array_equal(_np(y_fus.float()), _np(y_unf.float()))
 
 
 def test_conv_argument_errors():
