@@ -566,6 +566,14 @@ def run_conv(args, world, rank, dev):
     u_pix = int(torch.unique(pl.pix[pl.pix >= 0]).numel())
     hbm_bytes = F * Hb * Wb * (cb + ci) * esz + u_pix * ci * esz + 12 * nnz  # read bev, write out, gather
     tflops = flops / (conv_ms * 1e-3) / 1e12
+    traffic, mfma_busy = None, None
+    tpath = os.path.join(HERE, "profiles", "traffic.json")
+    if os.path.exists(tpath):
+        with open(tpath) as fh:
+            tj = json.load(fh).get(f"conv_{args.dtype}_F{F}")
+        if tj:
+            traffic = tj["hbm_bytes_per_launch"]
+            mfma_busy = tj["kernels"].get(f"k_conv3x3_pooled_{args.dtype}", {}).get("mfma_busy_share")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_conv(spec, frames[:1], args.cpu_seconds)
@@ -586,7 +594,8 @@ def run_conv(args, world, rank, dev):
             "roofline": {"bound": "mfma", "kernel": "k_conv3x3 (fused pooling), MFMA "
                          + ("v_mfma_f32_32x32x16_bf16" if esz == 2 else "v_mfma_f32_32x32x2_f32"),
                          "achieved": round(tflops, 2), "peak": MFMA_PEAK_TFS[dname], "unit": "TFLOP/s",
-                         "frac": round(tflops / MFMA_PEAK_TFS[dname], 4), "traffic": None,
+                         "frac": round(tflops / MFMA_PEAK_TFS[dname], 4), "traffic": traffic,
+                         "mfma_busy_share_pmc": mfma_busy,
                          "algorithmic_flops_per_launch": flops, "kernel_ms": round(conv_ms, 4),
                          "hbm_algorithmic_bytes_per_launch": hbm_bytes,
                          "hbm_GBps": round(hbm_bytes / (conv_ms * 1e-3) / 1e9, 1)},

@@ -14,18 +14,51 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def per_kernel(counter):
-    files = glob.glob(os.path.join(ROOT, "gpurun_out", f"pmc_{counter}", "**", "*counter_collection.csv"),
-                      recursive=True)
+SHORT = (("k_conv3x3<float, true", "k_conv3x3_pooled_f32"), ("k_conv3x3<float, false", "k_conv3x3_dense_f32"),
+         ("k_conv3x3<unsigned short, true", "k_conv3x3_pooled_bf16"),
+         ("k_conv3x3<unsigned short, false", "k_conv3x3_dense_bf16"),
+         ("k_dense", "k_dense"), ("k_sparse", "k_sparse"), ("k_csr_frame", "k_csr_frame"), ("k_compact", "k_compact"),
+         ("k_count", "k_count"))
+
+
+def per_kernel(counter, pattern=None):
+    pattern = pattern or f"pmc_{counter}"
+    files = glob.glob(os.path.join(ROOT, "gpurun_out", pattern, "**", "*counter_collection.csv"), recursive=True)
     acc = defaultdict(list)
     for f in files:
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") != counter:
                 continue
             name = r["Kernel_Name"]
-            short = next((k for k in ("k_dense", "k_sparse", "k_csr_frame", "k_compact", "k_count") if k in name), name)
+            short = next((s for k, s in SHORT if k in name), name)
             acc[short].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def conv(key, dt):
+    """scripts/gpu_conv_prof.sh passes: pmc_conv_<dt>_1 FETCH_SIZE, _2 WRITE_SIZE,
+    _3 SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE (MFMA busy share, clock)."""
+    fetch = per_kernel("FETCH_SIZE", f"pmc_conv_{dt}_1")
+    write = per_kernel("WRITE_SIZE", f"pmc_conv_{dt}_2")
+    mfma = per_kernel("SQ_VALU_MFMA_BUSY_CYCLES", f"pmc_conv_{dt}_3")
+    grbm = per_kernel("GRBM_GUI_ACTIVE", f"pmc_conv_{dt}_3")
+    out = {}
+    for k in sorted(set(fetch) | set(write)):
+        f_b, w_b = 2 * fetch.get(k, 0.0) * 1024, write.get(k, 0.0) * 1024
+        cyc = grbm.get(k, 0.0) / 8.0  # GRBM_GUI_ACTIVE sums the 8 XCDs
+        out[k] = {"fetch_bytes": f_b, "write_bytes": w_b, "raw_FETCH_SIZE_KiB": fetch.get(k),
+                  "raw_WRITE_SIZE_KiB": write.get(k), "SQ_VALU_MFMA_BUSY_CYCLES": mfma.get(k),
+                  "GRBM_GUI_ACTIVE": grbm.get(k),
+                  "mfma_busy_share": mfma.get(k, 0.0) / (1024 * cyc) if cyc else None}
+    main_k = f"k_conv3x3_pooled_{dt}"
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    tj = json.load(open(path)) if os.path.exists(path) else {}
+    tj[key] = {"hbm_bytes_per_launch": out[main_k]["fetch_bytes"] + out[main_k]["write_bytes"], "kernels": out,
+               "note": (f"{main_k} = the fused conv; FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes; "
+                        "WRITE_SIZE of 4 B/lane stores is uncalibrated (MI355X_MICROARCH.md HBM); mfma_busy_share "
+                        "= MFMA busy cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)")}
+    json.dump(tj, open(path, "w"), indent=1)
+    print(json.dumps(tj[key], indent=1))
 
 
 def main(key):
@@ -47,4 +80,8 @@ def main(key):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "config2_F64")
+    key = sys.argv[1] if len(sys.argv) > 1 else "config2_F64"
+    if key.startswith("conv_"):
+        conv(key, key.split("_")[1])
+    else:
+        main(key)
