@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHORT = (("k_conv3x3<float, true", "k_conv3x3_pooled_f32"), ("k_conv3x3<float, false", "k_conv3x3_dense_f32"),
          ("k_conv3x3<unsigned short, true", "k_conv3x3_pooled_bf16"),
          ("k_conv3x3<unsigned short, false", "k_conv3x3_dense_bf16"),
-         ("k_dense", "k_dense"), ("k_sparse", "k_sparse"), ("k_csr_frame", "k_csr_frame"), ("k_compact", "k_compact"),
+         ("k_dense", "k_dense"), ("k_sparse_long", "k_sparse_long"), ("k_sparse", "k_sparse"), ("k_csr_frame", "k_csr_frame"), ("k_compact", "k_compact"),
          ("k_count", "k_count"))
 
 
@@ -70,11 +70,12 @@ def main(key):
         w_b = write.get(k, 0.0) * 1024
         out[k] = {"fetch_bytes": f_b, "write_bytes": w_b, "raw_FETCH_SIZE_KiB": fetch.get(k),
                   "raw_WRITE_SIZE_KiB": write.get(k)}
-    layer = sum(out[k]["fetch_bytes"] + out[k]["write_bytes"] for k in ("k_dense", "k_sparse") if k in out)
+    layer = sum(out[k]["fetch_bytes"] + out[k]["write_bytes"] for k in ("k_dense", "k_sparse", "k_sparse_long")
+                if k in out)
     path = os.path.join(ROOT, "profiles", "traffic.json")
     tj = json.load(open(path)) if os.path.exists(path) else {}
     tj[key] = {"hbm_bytes_per_launch": layer, "kernels": out,
-               "note": "layer = k_dense + k_sparse; FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes"}
+               "note": "layer = k_dense + k_sparse (+ k_sparse_long); FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes"}
     json.dump(tj, open(path, "w"), indent=1)
     print(json.dumps(tj[key], indent=1))
 

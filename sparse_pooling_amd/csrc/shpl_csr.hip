@@ -15,6 +15,8 @@
 // a few entries each, so the quadratic rank costs less than a sort pass.
 #include "shpl_common.h"
 
+#include <stdlib.h>
+
 namespace shpl {
 namespace {
 
@@ -161,88 +163,54 @@ __device__ void clear_unused(const CsrIn &c, int64_t nnz_cap, int32_t *ent_dst, 
     }
 }
 
-template <bool HAS_COL>
-__global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, uint64_t *tmp, int64_t nnz_cap, int32_t *ent_dst,
-                                                         int32_t *ent_src, float *ent_val, int32_t *ent_col) {
-    __shared__ int32_t cnt[CSR_TILES];
-    __shared__ int32_t wsum[CSR_BLOCK / 64];
-    __shared__ uint64_t win[CSR_WIN];
-    if ((int)blockIdx.x >= c.n_frames) {
-        clear_unused(c, nnz_cap, ent_dst, (int)blockIdx.x - c.n_frames);
-        return;
+// Exclusive scan of the TILES LDS tile counters in place (1024 threads):
+// cnt[t] = start of tile t.
+template <int TILES>
+__device__ __forceinline__ void tile_scan(int32_t *cnt, int32_t *wsum) {
+    constexpr int CSR_PER_THREAD = TILES / CSR_BLOCK;
+    int32_t v[CSR_PER_THREAD];
+    int32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < CSR_PER_THREAD; ++q) {
+        v[q] = cnt[threadIdx.x * CSR_PER_THREAD + q];
+        sum += v[q];
     }
-    const int f = blockIdx.x;
-    const int64_t e0 = c.frame_off[f];
-    const int64_t cap_end = c.frame_off[f + 1];
-    int64_t e1 = cap_end;
-    if (c.frame_nnz) {
-        const int64_t n = c.frame_nnz[f];
-        e1 = e0 + n < cap_end ? e0 + n : cap_end;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int32_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
     }
-    const int64_t kbase = (int64_t)f * c.keys_per_frame;
-    const int n_tiles = (int)(((c.keys_per_frame - 1) >> c.log_tile) + 1);
-    for (int t = threadIdx.x; t < CSR_TILES; t += CSR_BLOCK) cnt[t] = 0;
+    if (lane == 63) wsum[wid] = x;
     __syncthreads();
-    // 1. histogram
-    for (int64_t b = e0 + threadIdx.x; b < e1; b += (int64_t)CSR_BLOCK * CSR_BATCH) {
-        int32_t key[CSR_BATCH];
-        keys_batch<HAS_COL>(c, b, e1, key);
+    int32_t run = x - sum;
+    for (int w = 0; w < wid; ++w) run += wsum[w];
 #pragma unroll
-        for (int u = 0; u < CSR_BATCH; ++u) {
-            const int64_t k = (int64_t)key[u] - kbase;
-            if (key[u] >= 0 && k >= 0 && k < c.keys_per_frame) atomicAdd(&cnt[k >> c.log_tile], 1);
-        }
+    for (int q = 0; q < CSR_PER_THREAD; ++q) {
+        cnt[threadIdx.x * CSR_PER_THREAD + q] = run;
+        run += v[q];
     }
-    __syncthreads();
-    // 2. exclusive scan: thread j owns tiles [j*16, j*16+16)
-    {
-        int32_t v[CSR_PER_THREAD];
-        int32_t sum = 0;
-#pragma unroll
-        for (int q = 0; q < CSR_PER_THREAD; ++q) {
-            v[q] = cnt[threadIdx.x * CSR_PER_THREAD + q];
-            sum += v[q];
-        }
-        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-        int32_t x = sum;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) wsum[wid] = x;
-        __syncthreads();
-        int32_t run = x - sum;
-        for (int w = 0; w < wid; ++w) run += wsum[w];
-#pragma unroll
-        for (int q = 0; q < CSR_PER_THREAD; ++q) {
-            cnt[threadIdx.x * CSR_PER_THREAD + q] = run;
-            run += v[q];
-        }
-    }
-    __syncthreads();
-    // 3. placement of (destination << 32 | entry): cnt[t] advances from start(t) to end(t) = start(t+1)
-    for (int64_t b = e0 + threadIdx.x; b < e1; b += (int64_t)CSR_BLOCK * CSR_BATCH) {
-        int32_t key[CSR_BATCH];
-        keys_batch<HAS_COL>(c, b, e1, key);
-#pragma unroll
-        for (int u = 0; u < CSR_BATCH; ++u) {
-            const int64_t k = (int64_t)key[u] - kbase;
-            const int64_t e = b + (int64_t)u * CSR_BLOCK;
-            if (key[u] >= 0 && k >= 0 && k < c.keys_per_frame)
-                tmp[e0 + atomicAdd(&cnt[k >> c.log_tile], 1)] = ((uint64_t)(uint32_t)key[u] << 32) | (uint32_t)e;
-        }
-    }
-    block_publish();  // tmp was written by other waves of this workgroup through memory
-    const int32_t n_valid = cnt[n_tiles - 1];
-    // With identity columns every TF order collapses to entry order, so the
-    // packed (destination, entry) word alone sorts the tile.
+}
+
+// Rank fix-up + emission. words[0, n_valid) hold packed (destination << 32 |
+// entry) words grouped by destination tile (cnt[t] = end of tile t, tiles of
+// 2^log_tile destinations from kbase); each entry counts the tile entries
+// that precede it in (destination, TF order, entry), which makes the order
+// stable and sorted, and is written to out_base + its rank with its source
+// row, value and column. With identity columns (or ORDER_ENTRY) the packed
+// word alone orders a tile and the words are staged in LDS windows, so the
+// quadratic count reads LDS, not HBM.
+template <bool HAS_COL, int CSR_WIN>
+__device__ void emit_sorted(const CsrIn &c, const uint64_t *words, int32_t n_valid, int64_t out_base, int64_t kbase,
+                            int log_tile, const int32_t *cnt, uint64_t *win, int32_t *ent_dst, int32_t *ent_src,
+                            float *ent_val, int32_t *ent_col) {
+    // With identity columns every TF order collapses to entry order.
     const bool entry_order = c.order == SHPL_ORDER_ENTRY || !HAS_COL;
-    // 4. rank fix-up
     if (entry_order) {
         for (int32_t w0 = 0; w0 < n_valid; w0 += CSR_WIN) {
             const int32_t w1 = w0 + CSR_WIN < n_valid ? w0 + CSR_WIN : n_valid;
-            for (int32_t s = w0 + threadIdx.x; s < w1; s += CSR_BLOCK) win[s - w0] = tmp[e0 + s];
+            for (int32_t s = w0 + threadIdx.x; s < w1; s += CSR_BLOCK) win[s - w0] = words[s];
             __syncthreads();
             for (int32_t s0 = w0 + threadIdx.x; s0 < w1; s0 += CSR_BLOCK * CSR_BATCH) {
                 int32_t d[CSR_BATCH], ee[CSR_BATCH], kk[CSR_BATCH], key[CSR_BATCH];
@@ -254,14 +222,14 @@ __global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, uint64_t *tmp,
                     const uint64_t me = win[s - w0];
                     key[u] = (int32_t)(me >> 32);
                     ee[u] = (int32_t)(uint32_t)me;
-                    const int t = (int)((key[u] - kbase) >> c.log_tile);
+                    const int t = (int)((key[u] - kbase) >> log_tile);
                     const int32_t a = t ? cnt[t - 1] : 0, b = cnt[t];
                     int32_t rank = 0;
                     if (b - a > 1) {
                         if (a >= w0 && b <= w1) {
                             for (int32_t x = a; x < b; ++x) rank += win[x - w0] < me ? 1 : 0;
                         } else {  // tile straddles the window edge
-                            for (int32_t x = a; x < b; ++x) rank += tmp[e0 + x] < me ? 1 : 0;
+                            for (int32_t x = a; x < b; ++x) rank += words[x] < me ? 1 : 0;
                         }
                     }
                     d[u] = a + rank;
@@ -279,7 +247,7 @@ __global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, uint64_t *tmp,
 #pragma unroll
                 for (int u = 0; u < CSR_BATCH; ++u) {
                     if (d[u] < 0) continue;
-                    const int64_t o = e0 + d[u];
+                    const int64_t o = out_base + d[u];
                     ent_dst[o] = key[u];
                     ent_src[o] = src[u];
                     ent_val[o] = val[u];
@@ -290,15 +258,15 @@ __global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, uint64_t *tmp,
         }
     } else {
         for (int32_t s = threadIdx.x; s < n_valid; s += CSR_BLOCK) {
-            const uint64_t me = tmp[e0 + s];
+            const uint64_t me = words[s];
             const int32_t key = (int32_t)(me >> 32);
             const int32_t e = (int32_t)(uint32_t)me;
-            const int t = (int)((key - kbase) >> c.log_tile);
+            const int t = (int)((key - kbase) >> log_tile);
             const int32_t a = t ? cnt[t - 1] : 0, b = cnt[t];
             int32_t rank = 0;
             const uint64_t ke = order_key(c, e);
             for (int32_t u = a; u < b; ++u) {
-                const uint64_t ot = tmp[e0 + u];
+                const uint64_t ot = words[u];
                 const int32_t ko = (int32_t)(ot >> 32), o = (int32_t)(uint32_t)ot;
                 bool before = ko < key;
                 if (ko == key && o != e) {
@@ -307,7 +275,7 @@ __global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, uint64_t *tmp,
                 }
                 rank += before ? 1 : 0;
             }
-            const int64_t d = e0 + a + rank;
+            const int64_t d = out_base + a + rank;
             const int32_t k = col_of(c, e);
             ent_dst[d] = key;
             ent_src[d] = c.direction == SHPL_BY_CELL ? c.pix[k] : c.cell[e];
@@ -315,12 +283,281 @@ __global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, uint64_t *tmp,
             if (ent_col) ent_col[d] = k;
         }
     }
-    // Slots of invalid entries (flagged upstream) become empty here; the unused
-    // capacity past the frame's live entries is cleared by the launch's extra
-    // workgroups (frame_nnz given), or here (no frame_nnz: the frame's capacity
-    // is all live, so only invalid entries leave slots).
+}
+
+// Live entry range [e0, e1) and capacity end of frame f.
+__device__ __forceinline__ void frame_range(const CsrIn &c, int f, int64_t &e0, int64_t &e1, int64_t &cap_end) {
+    e0 = c.frame_off[f];
+    cap_end = c.frame_off[f + 1];
+    e1 = cap_end;
+    if (c.frame_nnz) {
+        const int64_t n = c.frame_nnz[f];
+        e1 = e0 + n < cap_end ? e0 + n : cap_end;
+    }
+}
+
+// Slots of invalid entries (flagged upstream) become empty; the unused
+// capacity past the frame's live entries is cleared by the launch's extra
+// workgroups (frame_nnz given), or here (no frame_nnz: the frame's capacity
+// is all live, so only invalid entries leave slots).
+__device__ __forceinline__ void clear_holes(const CsrIn &c, int f, int64_t from, int64_t e1, int64_t cap_end,
+                                            int64_t nnz_cap, int32_t *ent_dst) {
     const int64_t hole_end = c.frame_nnz ? e1 : (f == c.n_frames - 1 ? nnz_cap : cap_end);
-    for (int64_t d = e0 + n_valid + threadIdx.x; d < hole_end; d += CSR_BLOCK) ent_dst[d] = -1;
+    for (int64_t d = from + threadIdx.x; d < hole_end; d += CSR_BLOCK) ent_dst[d] = -1;
+}
+
+template <bool HAS_COL>
+__global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, uint64_t *tmp, int64_t nnz_cap, int32_t *ent_dst,
+                                                         int32_t *ent_src, float *ent_val, int32_t *ent_col) {
+    __shared__ int32_t cnt[CSR_TILES];
+    __shared__ int32_t wsum[CSR_BLOCK / 64];
+    __shared__ uint64_t win[CSR_WIN];
+    if ((int)blockIdx.x >= c.n_frames) {
+        clear_unused(c, nnz_cap, ent_dst, (int)blockIdx.x - c.n_frames);
+        return;
+    }
+    const int f = blockIdx.x;
+    int64_t e0, e1, cap_end;
+    frame_range(c, f, e0, e1, cap_end);
+    const int64_t kbase = (int64_t)f * c.keys_per_frame;
+    const int n_tiles = (int)(((c.keys_per_frame - 1) >> c.log_tile) + 1);
+    for (int t = threadIdx.x; t < CSR_TILES; t += CSR_BLOCK) cnt[t] = 0;
+    __syncthreads();
+    // 1. histogram
+    for (int64_t b = e0 + threadIdx.x; b < e1; b += (int64_t)CSR_BLOCK * CSR_BATCH) {
+        int32_t key[CSR_BATCH];
+        keys_batch<HAS_COL>(c, b, e1, key);
+#pragma unroll
+        for (int u = 0; u < CSR_BATCH; ++u) {
+            const int64_t k = (int64_t)key[u] - kbase;
+            if (key[u] >= 0 && k >= 0 && k < c.keys_per_frame) atomicAdd(&cnt[k >> c.log_tile], 1);
+        }
+    }
+    __syncthreads();
+    // 2. exclusive scan
+    tile_scan<CSR_TILES>(cnt, wsum);
+    __syncthreads();
+    // 3. placement of (destination << 32 | entry): cnt[t] advances from start(t) to end(t) = start(t+1)
+    for (int64_t b = e0 + threadIdx.x; b < e1; b += (int64_t)CSR_BLOCK * CSR_BATCH) {
+        int32_t key[CSR_BATCH];
+        keys_batch<HAS_COL>(c, b, e1, key);
+#pragma unroll
+        for (int u = 0; u < CSR_BATCH; ++u) {
+            const int64_t k = (int64_t)key[u] - kbase;
+            const int64_t e = b + (int64_t)u * CSR_BLOCK;
+            if (key[u] >= 0 && k >= 0 && k < c.keys_per_frame)
+                tmp[e0 + atomicAdd(&cnt[k >> c.log_tile], 1)] = ((uint64_t)(uint32_t)key[u] << 32) | (uint32_t)e;
+        }
+    }
+    block_publish();  // tmp was written by other waves of this workgroup through memory
+    const int32_t n_valid = cnt[n_tiles - 1];
+    // 4. rank fix-up
+    emit_sorted<HAS_COL, CSR_WIN>(c, tmp + e0, n_valid, e0, kbase, c.log_tile, cnt, win, ent_dst, ent_src, ent_val, ent_col);
+    clear_holes(c, f, e0 + n_valid, e1, cap_end, nnz_cap, ent_dst);
+}
+
+// ---------------------------------------------------------------- segmented CSR
+// For batches too small to fill the chip with one workgroup per frame (config
+// 3: 4 frames), each frame's destinations are cut into S segments holding
+// about the same number of entries, sorted by S workgroups:
+//   k_csr_count   every entry's destination -> kbuf; a histogram of the
+//                 frame's destinations over n_bins bins of 2^log_bin
+//   k_csr_bucket  bins -> balanced segments (bin b goes to segment
+//                 excl(b) * S / total); entries scattered to their segment's
+//                 bucket (any order)
+//   k_csr_segment one workgroup per (frame, segment): the frame kernel's tile
+//                 histogram / placement / rank fix-up over its bucket
+// Segments are contiguous destination ranges, so the result is identical to
+// k_csr_frame's. Balancing matters: image points crowd a few rows around the
+// horizon, and equal destination ranges left one segment with most of a
+// frame (measured: pixel CSR 50 us with equal ranges at config 3).
+constexpr int SEG_BLOCK = 256;
+constexpr int SEG_MAX = 1024;   // bins per frame (LDS histogram of count / bucket / segment)
+constexpr int SEG_BATCH = 4;    // entries per thread in flight
+constexpr int SEG_TILES = 4096; // tile counters of a segment workgroup (16 KiB)
+constexpr int SEG_WIN = 4096;   // rank fix-up window of a segment workgroup (32 KiB): two per CU
+
+struct SegIn {
+    int S;              // segments per frame
+    int n_bins;         // destination bins per frame (<= SEG_MAX)
+    int log_bin;        // destinations per bin = 1 << log_bin
+    int32_t *hist;      // [n_frames * n_bins] entries per bin
+    int32_t *cur;       // [n_frames * S] bucket fill cursors
+    int32_t *kbuf;      // [nnz_cap] destination of each entry slot (-1: invalid)
+    uint64_t *bucket;   // [nnz_cap] words grouped by segment
+    uint64_t *sorted;   // [nnz_cap] words grouped by tile inside a segment
+};
+
+// Zeroes the bin and cursor counters (a kernel node: cheaper than a memset
+// node inside the bench's captured graph).
+__global__ __launch_bounds__(SEG_BLOCK) void k_zero32(int32_t *p, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * SEG_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * SEG_BLOCK) p[i] = 0;
+}
+
+template <bool HAS_COL>
+__global__ __launch_bounds__(SEG_BLOCK) void k_csr_count(CsrIn c, SegIn g) {
+    __shared__ int32_t h[SEG_MAX];
+    const int f = blockIdx.y;
+    int64_t e0, e1, cap_end;
+    frame_range(c, f, e0, e1, cap_end);
+    const int64_t kbase = (int64_t)f * c.keys_per_frame;
+    for (int b = threadIdx.x; b < g.n_bins; b += SEG_BLOCK) h[b] = 0;
+    __syncthreads();
+    const int64_t step = (int64_t)gridDim.x * SEG_BLOCK;
+    for (int64_t b = e0 + (int64_t)blockIdx.x * SEG_BLOCK + threadIdx.x; b < e1; b += step * SEG_BATCH) {
+        int32_t r[SEG_BATCH], k[SEG_BATCH], p[SEG_BATCH];
+#pragma unroll
+        for (int u = 0; u < SEG_BATCH; ++u) {
+            const int64_t e = b + u * step;
+            const bool ok = e < e1;
+            r[u] = ok ? c.cell[e] : -1;
+            k[u] = ok ? (HAS_COL ? c.col[e] : (int32_t)e) : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < SEG_BATCH; ++u) p[u] = k[u] >= 0 ? c.pix[k[u]] : -1;
+#pragma unroll
+        for (int u = 0; u < SEG_BATCH; ++u) {
+            const int64_t e = b + u * step;
+            if (e >= e1) continue;
+            int32_t key = (r[u] < 0 || k[u] < 0 || p[u] < 0) ? -1 : (c.direction == SHPL_BY_CELL ? r[u] : p[u]);
+            const int64_t kk = (int64_t)key - kbase;
+            if (key >= 0 && (kk < 0 || kk >= c.keys_per_frame)) key = -1;  // outside the frame: left out
+            g.kbuf[e] = key;
+            if (key >= 0) atomicAdd(&h[(int)(kk >> g.log_bin)], 1);
+        }
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < g.n_bins; b += SEG_BLOCK)
+        if (h[b]) atomicAdd(&g.hist[(int64_t)f * g.n_bins + b], h[b]);
+}
+
+// Balanced segments of frame f from its bin histogram (BLOCK threads, every
+// thread calls): seg_of[b] for each bin; per segment its first entry offset
+// in the frame (seg_start), entry count (seg_n), first bin (seg_lo) and bin
+// count (seg_nb). Returns the frame's entry total.
+template <int BLOCK>
+__device__ int32_t seg_map(const SegIn &g, int f, int32_t *seg_of, int32_t *seg_start, int32_t *seg_n,
+                           int32_t *seg_lo, int32_t *seg_nb, int32_t *wsum) {
+    constexpr int PER = SEG_MAX / BLOCK;
+    const int32_t *hist = g.hist + (int64_t)f * g.n_bins;
+    int32_t v[PER], sum = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int b = threadIdx.x * PER + q;
+        v[q] = b < g.n_bins ? hist[b] : 0;
+        sum += v[q];
+    }
+    for (int s = threadIdx.x; s < g.S; s += BLOCK) {
+        seg_n[s] = 0;
+        seg_nb[s] = 0;
+        seg_start[s] = 0;
+        seg_lo[s] = 0;
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int32_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    int32_t run = x - sum, total = 0;
+    for (int w = 0; w < BLOCK / 64; ++w) {
+        if (w < wid) run += wsum[w];
+        total += wsum[w];
+    }
+    const int64_t S = g.S;
+    auto seg_at = [&](int32_t excl) { return total ? (int)min(S - 1, (int64_t)excl * S / total) : 0; };
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int b = threadIdx.x * PER + q;
+        if (b < g.n_bins) {
+            const int sg = seg_at(run);
+            seg_of[b] = sg;
+            const bool first = b == 0 || seg_at(run - (q ? v[q - 1] : hist[b - 1])) != sg;
+            if (first) {
+                seg_start[sg] = run;
+                seg_lo[sg] = b;
+            }
+            atomicAdd(&seg_n[sg], v[q]);
+            atomicAdd(&seg_nb[sg], 1);
+        }
+        run += v[q];
+    }
+    __syncthreads();
+    return total;
+}
+
+__global__ __launch_bounds__(SEG_BLOCK) void k_csr_bucket(CsrIn c, SegIn g) {
+    __shared__ int32_t seg_of[SEG_MAX], seg_start[SEG_MAX], seg_n[SEG_MAX], seg_lo[SEG_MAX], seg_nb[SEG_MAX];
+    __shared__ int32_t h[SEG_MAX], base[SEG_MAX];
+    __shared__ int32_t wsum[SEG_BLOCK / 64];
+    const int f = blockIdx.y;
+    int64_t e0, e1, cap_end;
+    frame_range(c, f, e0, e1, cap_end);
+    const int64_t kbase = (int64_t)f * c.keys_per_frame;
+    seg_map<SEG_BLOCK>(g, f, seg_of, seg_start, seg_n, seg_lo, seg_nb, wsum);
+    const int64_t step = (int64_t)gridDim.x * SEG_BLOCK;
+    // uniform trip count: every thread takes part in every round's barriers
+    for (int64_t b0 = e0 + (int64_t)blockIdx.x * SEG_BLOCK; b0 < e1; b0 += step) {
+        for (int s = threadIdx.x; s < g.S; s += SEG_BLOCK) h[s] = 0;
+        __syncthreads();
+        const int64_t e = b0 + threadIdx.x;
+        const int32_t key = e < e1 ? g.kbuf[e] : -1;
+        int seg = 0, loc = 0;
+        if (key >= 0) {
+            seg = seg_of[(int)((key - kbase) >> g.log_bin)];
+            loc = atomicAdd(&h[seg], 1);
+        }
+        __syncthreads();
+        for (int s = threadIdx.x; s < g.S; s += SEG_BLOCK)
+            if (h[s]) base[s] = atomicAdd(&g.cur[(int64_t)f * g.S + s], h[s]);
+        __syncthreads();
+        if (key >= 0)
+            g.bucket[e0 + seg_start[seg] + base[seg] + loc] = ((uint64_t)(uint32_t)key << 32) | (uint32_t)e;
+        __syncthreads();
+    }
+}
+
+template <bool HAS_COL>
+__global__ __launch_bounds__(CSR_BLOCK) void k_csr_segment(CsrIn c, SegIn g, int64_t nnz_cap, int32_t *ent_dst,
+                                                           int32_t *ent_src, float *ent_val, int32_t *ent_col) {
+    __shared__ int32_t cnt[SEG_TILES];
+    __shared__ int32_t wsum[CSR_BLOCK / 64];
+    __shared__ uint64_t win[SEG_WIN];
+    __shared__ int32_t seg_of[SEG_MAX], seg_start[SEG_MAX], seg_n[SEG_MAX], seg_lo[SEG_MAX], seg_nb[SEG_MAX];
+    if ((int)blockIdx.y >= c.n_frames) {
+        clear_unused(c, nnz_cap, ent_dst, (int)blockIdx.x + (int)(blockIdx.y - c.n_frames) * (int)gridDim.x);
+        return;
+    }
+    const int f = blockIdx.y, s = blockIdx.x;
+    int64_t e0, e1, cap_end;
+    frame_range(c, f, e0, e1, cap_end);
+    const int32_t total = seg_map<CSR_BLOCK>(g, f, seg_of, seg_start, seg_n, seg_lo, seg_nb, wsum);
+    if (s == g.S - 1) clear_holes(c, f, e0 + total, e1, cap_end, nnz_cap, ent_dst);
+    const int32_t n = seg_n[s];
+    if (n == 0) return;  // uniform
+    const int64_t b0 = e0 + seg_start[s];
+    const int64_t kbase = (int64_t)f * c.keys_per_frame + ((int64_t)seg_lo[s] << g.log_bin);
+    const int64_t nkeys = (int64_t)seg_nb[s] << g.log_bin;
+    int log_tile = 0;
+    while (((nkeys - 1) >> log_tile) + 1 > SEG_TILES) ++log_tile;
+    for (int t = threadIdx.x; t < SEG_TILES; t += CSR_BLOCK) cnt[t] = 0;
+    __syncthreads();
+    const uint64_t *in = g.bucket + b0;
+    for (int32_t i = threadIdx.x; i < n; i += CSR_BLOCK)
+        atomicAdd(&cnt[(int)((((int64_t)(in[i] >> 32)) - kbase) >> log_tile)], 1);
+    __syncthreads();
+    tile_scan<SEG_TILES>(cnt, wsum);
+    __syncthreads();
+    for (int32_t i = threadIdx.x; i < n; i += CSR_BLOCK) {
+        const uint64_t w = in[i];
+        g.sorted[b0 + atomicAdd(&cnt[(int)((((int64_t)(w >> 32)) - kbase) >> log_tile)], 1)] = w;
+    }
+    block_publish();  // sorted was written by other waves of this workgroup through memory
+    emit_sorted<HAS_COL, SEG_WIN>(c, g.sorted + b0, n, b0, kbase, log_tile, cnt, win, ent_dst, ent_src, ent_val,
+                                  ent_col);
 }
 
 }  // namespace
@@ -357,9 +594,34 @@ extern "C" int shpl_pack_map(int64_t nnz, const int64_t *d_mij, const float *d_v
     return SHPL_OK;
 }
 
+// Workspace: [tmp words | segmented path: kbuf | sorted words | counters].
+// The segmented path is taken when its counters fit (n_frames * S <=
+// seg_cap, i.e. up to ~4096 frames) -- see csr_plan.
+namespace {
+constexpr int64_t SEG_TARGET = 2048;  // entries per segment the host aims for
+constexpr int SEG_FRAMES = 32;        // batches from this many frames sort one frame per workgroup
+
+int64_t seg_cap_of(int64_t nnz_cap) { return nnz_cap / 16 + 65536; }  // bin + cursor counters
+
+struct CsrLayout {
+    size_t tmp, kbuf, sorted, counters, total;
+};
+
+CsrLayout csr_layout(int64_t nnz_cap) {
+    CsrLayout l;
+    const size_t cap = (size_t)(nnz_cap > 0 ? nnz_cap : 1);
+    l.tmp = 0;
+    l.kbuf = align_up(sizeof(uint64_t) * cap, 256);
+    l.sorted = l.kbuf + align_up(sizeof(int32_t) * cap, 256);
+    l.counters = l.sorted + align_up(sizeof(uint64_t) * cap, 256);
+    l.total = l.counters + align_up(2 * sizeof(int32_t) * (size_t)seg_cap_of(nnz_cap), 256);
+    return l;
+}
+}  // namespace
+
 extern "C" int shpl_csr_workspace_bytes(int64_t n_keys, int64_t nnz_cap, size_t *bytes) {
     if (!bytes || n_keys < 0 || nnz_cap < 0) return SHPL_ERR_ARG;
-    *bytes = align_up(sizeof(uint64_t) * (size_t)(nnz_cap > 0 ? nnz_cap : 1), 256);
+    *bytes = csr_layout(nnz_cap).total;
     return SHPL_OK;
 }
 
@@ -377,21 +639,74 @@ extern "C" int shpl_build_csr(int direction, int order, int n_frames, const int6
     if (nnz_cap == 0) return SHPL_OK;
     if (!d_cell || !d_val || !d_pix || !csr->ent_dst || !csr->ent_src || !csr->ent_val || !d_ws) return SHPL_ERR_ARG;
     if (direction == SHPL_BY_PIXEL && !csr->ent_col) return SHPL_ERR_ARG;
-    size_t need;
-    shpl_csr_workspace_bytes(csr->n_keys, nnz_cap, &need);
-    if (need > ws_bytes) return SHPL_ERR_WORKSPACE;
-    int log_tile = 0;
-    while (((keys_per_frame - 1) >> log_tile) + 1 > CSR_TILES) ++log_tile;
-    CsrIn c{direction, order, n_frames, d_frame_off, d_frame_nnz, keys_per_frame, log_tile, d_cell, d_col, d_pix, d_val};
-    // n_frames sorting workgroups + the workgroups clearing the unused capacity
-    const int64_t spans = d_frame_nnz ? (nnz_cap + HOLE_SPAN - 1) / HOLE_SPAN : 0;
-    const dim3 grid((unsigned)(n_frames + spans));
+    const CsrLayout lay = csr_layout(nnz_cap);
+    hipStream_t st = (hipStream_t)stream;
+    uint8_t *ws = (uint8_t *)d_ws;
+    // segments: about SEG_TARGET entries each (estimated from the capacity per frame)
+    const int64_t est = (nnz_cap + n_frames - 1) / n_frames;
+    int log_bin = 0;
+    while (((keys_per_frame - 1) >> log_bin) + 1 > SEG_MAX) ++log_bin;
+    const int64_t n_bins = ((keys_per_frame - 1) >> log_bin) + 1;
+    int64_t S = (est + SEG_TARGET - 1) / SEG_TARGET;
+    if (S < 1) S = 1;
+    if (S > n_bins) S = n_bins;
+    // Small batches take the segmented path (config 3, 4 frames: 0.305 -> 0.259 ms per step); from
+    // SEG_FRAMES frames on, one workgroup per frame fills enough of the chip and, overlapped with the
+    // dense stream, measured faster (config 2, 64 frames: 2.34 vs 2.42 ms per step).
+    // SHPL_CSR_PATH=frame|segment forces a path (measurements).
+    const char *path = getenv("SHPL_CSR_PATH");
+    const bool want = path ? path[0] == 's' : n_frames < SEG_FRAMES;
+    const bool segmented = want && ws_bytes >= lay.total && (int64_t)n_frames * (n_bins + S) <= seg_cap_of(nnz_cap);
+    if (!segmented) {
+        // one workgroup per frame; needs only the tmp words
+        if (ws_bytes < align_up(sizeof(uint64_t) * (size_t)nnz_cap, 256)) return SHPL_ERR_WORKSPACE;
+        int log_tile = 0;
+        while (((keys_per_frame - 1) >> log_tile) + 1 > CSR_TILES) ++log_tile;
+        CsrIn c{direction, order, n_frames, d_frame_off, d_frame_nnz, keys_per_frame, log_tile,
+                d_cell, d_col, d_pix, d_val};
+        // n_frames sorting workgroups + the workgroups clearing the unused capacity
+        const int64_t spans = d_frame_nnz ? (nnz_cap + HOLE_SPAN - 1) / HOLE_SPAN : 0;
+        const dim3 grid((unsigned)(n_frames + spans));
+        if (d_col)
+            hipLaunchKernelGGL(k_csr_frame<true>, grid, dim3(CSR_BLOCK), 0, st, c, (uint64_t *)ws, nnz_cap,
+                               csr->ent_dst, csr->ent_src, csr->ent_val, csr->ent_col);
+        else
+            hipLaunchKernelGGL(k_csr_frame<false>, grid, dim3(CSR_BLOCK), 0, st, c, (uint64_t *)ws, nnz_cap,
+                               csr->ent_dst, csr->ent_src, csr->ent_val, csr->ent_col);
+        SHPL_LAUNCH_CHECK();
+        return SHPL_OK;
+    }
+    CsrIn c{direction, order, n_frames, d_frame_off, d_frame_nnz, keys_per_frame, 0,
+            d_cell, d_col, d_pix, d_val};
+    SegIn g;
+    g.S = (int)S;
+    g.n_bins = (int)n_bins;
+    g.log_bin = log_bin;
+    g.hist = (int32_t *)(ws + lay.counters);
+    g.cur = g.hist + (int64_t)n_frames * n_bins;
+    g.kbuf = (int32_t *)(ws + lay.kbuf);
+    g.bucket = (uint64_t *)(ws + lay.tmp);
+    g.sorted = (uint64_t *)(ws + lay.sorted);
+    const int64_t n_ctr = (int64_t)n_frames * (n_bins + S);
+    hipLaunchKernelGGL(k_zero32, dim3(grid_for(n_ctr, SEG_BLOCK, 1024)), dim3(SEG_BLOCK), 0, st, g.hist, n_ctr);
+    SHPL_LAUNCH_CHECK();
+    const int gx = (int)(est / 1024 < 1 ? 1 : (est / 1024 > 1024 ? 1024 : est / 1024));
+    const dim3 grid_fr((unsigned)gx, (unsigned)n_frames);
     if (d_col)
-        hipLaunchKernelGGL(k_csr_frame<true>, grid, dim3(CSR_BLOCK), 0, (hipStream_t)stream, c, (uint64_t *)d_ws,
-                           nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_val, csr->ent_col);
+        hipLaunchKernelGGL(k_csr_count<true>, grid_fr, dim3(SEG_BLOCK), 0, st, c, g);
     else
-        hipLaunchKernelGGL(k_csr_frame<false>, grid, dim3(CSR_BLOCK), 0, (hipStream_t)stream, c, (uint64_t *)d_ws,
-                           nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_val, csr->ent_col);
+        hipLaunchKernelGGL(k_csr_count<false>, grid_fr, dim3(SEG_BLOCK), 0, st, c, g);
+    SHPL_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_csr_bucket, grid_fr, dim3(SEG_BLOCK), 0, st, c, g);
+    SHPL_LAUNCH_CHECK();
+    const int64_t spans = d_frame_nnz ? (nnz_cap + HOLE_SPAN - 1) / HOLE_SPAN : 0;
+    const dim3 grid_seg((unsigned)S, (unsigned)(n_frames + (spans + S - 1) / S));
+    if (d_col)
+        hipLaunchKernelGGL(k_csr_segment<true>, grid_seg, dim3(CSR_BLOCK), 0, st, c, g, nnz_cap, csr->ent_dst,
+                           csr->ent_src, csr->ent_val, csr->ent_col);
+    else
+        hipLaunchKernelGGL(k_csr_segment<false>, grid_seg, dim3(CSR_BLOCK), 0, st, c, g, nnz_cap, csr->ent_dst,
+                           csr->ent_src, csr->ent_val, csr->ent_col);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
 }

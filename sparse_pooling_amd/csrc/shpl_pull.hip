@@ -166,100 +166,248 @@ __device__ __forceinline__ void fma_free_accumulate(float (&acc)[VEC], float w, 
 #define SHPL_WALK_PRED 0
 #endif
 constexpr int WALK = SHPL_WALK;
+// Runs longer than LONG_RUN entries (config 3: up to 54 image points on one
+// pixel) are left to k_sparse_long, which batches LONG_WALK entries per
+// feature round trip with the index words staged in LDS; k_sparse then never walks more than LONG_RUN / WALK
+// steps, and the common short runs keep its low register count.
+constexpr int LONG_RUN = 8;
+constexpr int LONG_WALK = 16;
 
-template <typename T, int VEC, bool GROUP>
-__global__ __launch_bounds__(SHPL_BLOCK) void k_sparse(const Feat f, const Ents e) {
+// Sum of one destination's run starting at sorted entry s, chunk c (VEC
+// elements of the pooled part), in TF-CPU order: entries in CSR order with
+// separate multiply and add; GROUP (BY_PIXEL): per column partial Q[k] first
+// (ScatterNd's order). W entries per step: their index loads, then their
+// feature loads, are each in flight together.
+template <typename T, int VEC, bool GROUP, int W>
+__device__ __forceinline__ void walk_run(const Feat &f, const Ents &e, int64_t s, int32_t key, uint32_t c,
+                                         float (&acc)[VEC]) {
     typedef Chunk<T, VEC> C;
     const int64_t nnz = e.n;
+    const T *sc = reinterpret_cast<const T *>(f.src) + f.src_off + (int64_t)c * VEC;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] = 0.0f;
+    float q[VEC];  // GROUP: the current column's partial, TF's Q[k]
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) q[j] = 0.0f;
+    int32_t kprev = -1;  // no column yet: the first flush adds a zero partial (0 + 0 = +0)
+    for (int64_t i = s;; i += W) {
+        bool in[W];
+        int32_t d[W], sr[W], kc[W];
+        float w[W];
+#if SHPL_WALK_PRED
+        // src / val / col only for entries of the run (one more latency, fewer loads)
+#pragma unroll
+        for (int u = 0; u < W; ++u) d[u] = i + u < nnz ? e.dst[i + u] : -1;
+#pragma unroll
+        for (int u = 0; u < W; ++u) in[u] = d[u] == key && (u == 0 || in[u - 1]);
+#pragma unroll
+        for (int u = 0; u < W; ++u) {
+            sr[u] = in[u] ? e.src[i + u] : 0;
+            w[u] = in[u] ? e.val[i + u] : 0.0f;
+            kc[u] = (GROUP && in[u]) ? e.col[i + u] : 0;
+        }
+#else
+        // index loads of the batch do not wait for each other (dst need not match yet)
+#pragma unroll
+        for (int u = 0; u < W; ++u) {
+            const bool ok = i + u < nnz;
+            d[u] = ok ? e.dst[i + u] : -1;
+            sr[u] = ok ? e.src[i + u] : 0;
+            w[u] = ok ? e.val[i + u] : 0.0f;
+            kc[u] = (GROUP && ok) ? e.col[i + u] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < W; ++u) in[u] = d[u] == key && (u == 0 || in[u - 1]);
+#endif
+        typename C::raw_t raw[W];
+#pragma unroll
+        for (int u = 0; u < W; ++u)
+            if (in[u]) raw[u] = C::load(sc + (int64_t)sr[u] * f.src_stride);
+#pragma unroll
+        for (int u = 0; u < W; ++u) {
+            if (!in[u]) break;
+            float x[VEC];
+            C::to_f32(raw[u], x);
+            if (GROUP) {
+                // TF: Q[k] = sum of column k's entries; out = 0 + Q[k1] + Q[k2] ... (ScatterNd order)
+                if (kc[u] != kprev) {
+#pragma unroll
+                    for (int j = 0; j < VEC; ++j) {
+                        acc[j] = __fadd_rn(acc[j], q[j]);
+                        q[j] = 0.0f;
+                    }
+                    kprev = kc[u];
+                }
+                fma_free_accumulate<VEC>(q, w[u], x);
+            } else {
+                fma_free_accumulate<VEC>(acc, w[u], x);
+            }
+        }
+        if (!in[W - 1]) break;
+    }
+    if (GROUP) {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(acc[j], q[j]);
+    }
+}
+
+template <typename T, int VEC>
+__device__ __forceinline__ void store_pooled(const Feat &f, int32_t key, uint32_t c, float (&acc)[VEC]) {
+    typedef Chunk<T, VEC> C;
+    if (f.mode == SHPL_OUT_ADD) {
+        const T *pass = reinterpret_cast<const T *>(f.pass) + f.pass_off;
+        float a[VEC];
+        C::to_f32(C::load(pass + (int64_t)key * f.pass_stride + (int64_t)c * VEC), a);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(a[j], acc[j]);
+    }
+    const uint32_t oc = (f.mode == SHPL_OUT_CONCAT ? f.cpass : 0u) + c;
+    C::store_nt(reinterpret_cast<T *>(f.out) + (int64_t)key * f.out_stride + (int64_t)oc * VEC, C::from_f32(acc));
+}
+
+// One thread per (sorted entry, chunk); the thread on the first entry of a
+// destination's run sums it and writes the pooled chunk -- for runs of at
+// most LONG_RUN entries (SPLIT) or all runs (!SPLIT).
+template <typename T, int VEC, bool GROUP, bool SPLIT>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_sparse(const Feat f, const Ents e) {
+    const int64_t nnz = e.n;
     const int64_t total = nnz * (int64_t)f.cpool;
-    const T *src = reinterpret_cast<const T *>(f.src) + f.src_off;
-    const T *pass = reinterpret_cast<const T *>(f.pass) + f.pass_off;
     for (int64_t t = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x; t < total;
          t += (int64_t)gridDim.x * SHPL_BLOCK) {
         const int64_t s = t / f.cpool;
         const uint32_t c = (uint32_t)(t - s * f.cpool);
+        // the three index loads are independent: one round trip
         const int32_t key = e.dst[s];
-        if (key < 0 || (s > 0 && e.dst[s - 1] == key)) continue;  // empty, or not the first entry of key
-        const T *sc = src + (int64_t)c * VEC;
+        const int32_t prev = s > 0 ? e.dst[s - 1] : -1;
+        const int32_t ahead = (SPLIT && s + LONG_RUN < nnz) ? e.dst[s + LONG_RUN] : -1;
+        if (key < 0 || prev == key) continue;  // empty, or not the first entry of key
+        if (SPLIT && ahead == key) continue;   // a run longer than LONG_RUN: k_sparse_long's
         float acc[VEC];
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) acc[j] = 0.0f;
-        // Walk the destination's run WALK entries at a time: the index loads
-        // and the feature loads of a batch are all issued before the first
-        // add, then the adds run in TF order (a run of length L costs
-        // about 2*ceil(L/WALK) memory latencies instead of 3*L).
-        float q[VEC];  // GROUP: the current column's partial, TF's Q[k]
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) q[j] = 0.0f;
-        int32_t kprev = -1;  // no column yet: the first flush adds a zero partial (0 + 0 = +0)
-        for (int64_t i = s;; i += WALK) {
-            bool in[WALK];
-            int32_t d[WALK], sr[WALK], kc[WALK];
-            float w[WALK];
-#if SHPL_WALK_PRED
-            // src / val / col only for entries of the run (one more latency, fewer loads)
-#pragma unroll
-            for (int u = 0; u < WALK; ++u) d[u] = i + u < nnz ? e.dst[i + u] : -1;
-#pragma unroll
-            for (int u = 0; u < WALK; ++u) in[u] = d[u] == key && (u == 0 || in[u - 1]);
-#pragma unroll
-            for (int u = 0; u < WALK; ++u) {
-                sr[u] = in[u] ? e.src[i + u] : 0;
-                w[u] = in[u] ? e.val[i + u] : 0.0f;
-                kc[u] = (GROUP && in[u]) ? e.col[i + u] : 0;
-            }
-#else
-            // index loads of the batch do not wait for each other (dst need not match yet)
-#pragma unroll
-            for (int u = 0; u < WALK; ++u) {
-                const bool ok = i + u < nnz;
-                d[u] = ok ? e.dst[i + u] : -1;
-                sr[u] = ok ? e.src[i + u] : 0;
-                w[u] = ok ? e.val[i + u] : 0.0f;
-                kc[u] = (GROUP && ok) ? e.col[i + u] : 0;
-            }
-#pragma unroll
-            for (int u = 0; u < WALK; ++u) in[u] = d[u] == key && (u == 0 || in[u - 1]);
-#endif
-            typename C::raw_t raw[WALK];
-#pragma unroll
-            for (int u = 0; u < WALK; ++u)
-                if (in[u]) raw[u] = C::load(sc + (int64_t)sr[u] * f.src_stride);
-#pragma unroll
-            for (int u = 0; u < WALK; ++u) {
-                if (!in[u]) break;
-                float x[VEC];
-                C::to_f32(raw[u], x);
-                if (GROUP) {
-                    // TF: Q[k] = sum of column k's entries; out = 0 + Q[k1] + Q[k2] ... (ScatterNd order)
-                    if (kc[u] != kprev) {
-#pragma unroll
-                        for (int j = 0; j < VEC; ++j) {
-                            acc[j] = __fadd_rn(acc[j], q[j]);
-                            q[j] = 0.0f;
-                        }
-                        kprev = kc[u];
-                    }
-                    fma_free_accumulate<VEC>(q, w[u], x);
-                } else {
-                    fma_free_accumulate<VEC>(acc, w[u], x);
+        walk_run<T, VEC, GROUP, WALK>(f, e, s, key, c, acc);
+        store_pooled<T, VEC>(f, key, c, acc);
+    }
+}
+
+// The runs longer than LONG_RUN. Each workgroup lists the long runs that
+// start among its LONG_SLOTS entry slots and stages, in one round trip, the
+// index words (dst, src, val, col) of the LONG_IDX entries from its first
+// long run on; its threads then take (run, chunk) pairs in parallel and walk
+// them LONG_WALK entries per step with the index read from LDS (global past
+// the staged range), so a step costs one feature round trip. (Measured and
+// dropped: staging the feature rows of one run at a time in LDS -- the runs
+// of a workgroup then go in series; at config 3 a quarter of the pixel runs
+// are long.)
+constexpr int LONG_IDX = 512;
+constexpr int LONG_SLOTS = 64;  // entry slots per workgroup when the grid is not capped: few runs each
+constexpr int LONG_GRID = 2048; // workgroups of k_sparse_long at most (config 2: ~625 slots each)
+template <typename T, int VEC, bool GROUP>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_sparse_long(const Feat f, const Ents e, int64_t per_block) {
+    typedef Chunk<T, VEC> C;
+    __shared__ int32_t s_run[SHPL_BLOCK];
+    __shared__ int32_t s_dst[LONG_IDX], s_src[LONG_IDX], s_col[GROUP ? LONG_IDX : 1];
+    __shared__ float s_val[LONG_IDX];
+    __shared__ int s_n, s_first;
+    const int64_t nnz = e.n;
+    const int64_t r_end = (int64_t)(blockIdx.x + 1) * per_block < nnz ? (int64_t)(blockIdx.x + 1) * per_block : nnz;
+    const T *sc0 = reinterpret_cast<const T *>(f.src) + f.src_off;
+    // the block's slots, up to SHPL_BLOCK per round (uniform trip count)
+    const int64_t span = per_block < SHPL_BLOCK ? per_block : SHPL_BLOCK;
+    for (int64_t blk = (int64_t)blockIdx.x * per_block; blk < r_end; blk += span) {
+        if (threadIdx.x == 0) {
+            s_n = 0;
+            s_first = SHPL_BLOCK;
+        }
+        __syncthreads();
+        if ((int64_t)threadIdx.x < span) {
+            const int64_t s = blk + threadIdx.x;
+            if (s < r_end) {
+                const int32_t key = e.dst[s];
+                const int32_t prev = s > 0 ? e.dst[s - 1] : -1;
+                const int32_t ahead = s + LONG_RUN < nnz ? e.dst[s + LONG_RUN] : -1;
+                if (key >= 0 && prev != key && ahead == key) {
+                    s_run[atomicAdd(&s_n, 1)] = (int32_t)threadIdx.x;
+                    atomicMin(&s_first, (int)threadIdx.x);
                 }
             }
-            if (!in[WALK - 1]) break;
         }
-        if (GROUP) {
+        __syncthreads();
+        const int n_run = s_n;
+        if (n_run == 0) continue;  // uniform
+        const int64_t base = blk + s_first;
+        for (int j = threadIdx.x; j < LONG_IDX; j += SHPL_BLOCK) {
+            const int64_t i = base + j;
+            const bool ok = i < nnz;
+            s_dst[j] = ok ? e.dst[i] : -1;
+            s_src[j] = ok ? e.src[i] : 0;
+            s_val[j] = ok ? e.val[i] : 0.0f;
+            if (GROUP) s_col[j] = ok ? e.col[i] : 0;
+        }
+        __syncthreads();
+        for (int p = threadIdx.x; p < n_run * (int)f.cpool; p += SHPL_BLOCK) {
+            const int r = p / (int)f.cpool;
+            const uint32_t c = (uint32_t)(p - r * (int)f.cpool);
+            const int64_t s0 = blk + s_run[r];
+            const T *sc = sc0 + (int64_t)c * VEC;
+            const int32_t key = s_dst[s0 - base];
+            float acc[VEC], q[VEC];
 #pragma unroll
-            for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(acc[j], q[j]);
-        }
-        if (f.mode == SHPL_OUT_ADD) {
-            float a[VEC];
-            C::to_f32(C::load(pass + (int64_t)key * f.pass_stride + (int64_t)c * VEC), a);
+            for (int j = 0; j < VEC; ++j) acc[j] = q[j] = 0.0f;
+            int32_t kprev = -1;
+            for (int64_t i = s0;; i += LONG_WALK) {
+                bool in[LONG_WALK];
+                int32_t sr[LONG_WALK], kc[LONG_WALK];
+                float w[LONG_WALK];
 #pragma unroll
-            for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(a[j], acc[j]);
+                for (int u = 0; u < LONG_WALK; ++u) {
+                    const int64_t x = i + u, j = x - base;
+                    int32_t d;
+                    if (j < LONG_IDX) {
+                        d = s_dst[j];
+                        sr[u] = s_src[j];
+                        w[u] = s_val[j];
+                        kc[u] = GROUP ? s_col[j] : 0;
+                    } else {
+                        const bool ok = x < nnz;
+                        d = ok ? e.dst[x] : -1;
+                        sr[u] = ok ? e.src[x] : 0;
+                        w[u] = ok ? e.val[x] : 0.0f;
+                        kc[u] = (GROUP && ok) ? e.col[x] : 0;
+                    }
+                    in[u] = d == key && (u == 0 || in[u - 1]);
+                }
+                typename C::raw_t raw[LONG_WALK];
+#pragma unroll
+                for (int u = 0; u < LONG_WALK; ++u)
+                    if (in[u]) raw[u] = C::load(sc + (int64_t)sr[u] * f.src_stride);
+#pragma unroll
+                for (int u = 0; u < LONG_WALK; ++u) {
+                    if (!in[u]) break;
+                    float x[VEC];
+                    C::to_f32(raw[u], x);
+                    if (GROUP) {
+                        // TF: Q[k] = sum of column k's entries; out = 0 + Q[k1] + Q[k2] ... (ScatterNd order)
+                        if (kc[u] != kprev) {
+#pragma unroll
+                            for (int j = 0; j < VEC; ++j) {
+                                acc[j] = __fadd_rn(acc[j], q[j]);
+                                q[j] = 0.0f;
+                            }
+                            kprev = kc[u];
+                        }
+                        fma_free_accumulate<VEC>(q, w[u], x);
+                    } else {
+                        fma_free_accumulate<VEC>(acc, w[u], x);
+                    }
+                }
+                if (!in[LONG_WALK - 1]) break;
+            }
+            if (GROUP) {
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(acc[j], q[j]);
+            }
+            store_pooled<T, VEC>(f, key, c, acc);
         }
-        const uint32_t oc = (f.mode == SHPL_OUT_CONCAT ? f.cpass : 0u) + c;
-        C::store_nt(reinterpret_cast<T *>(f.out) + (int64_t)key * f.out_stride + (int64_t)oc * VEC,
-                    C::from_f32(acc));
+        __syncthreads();  // s_run / s_dst are refilled for the next slots
     }
 }
 
@@ -338,17 +486,31 @@ int dense(const Plan &pl, hipStream_t s) {
     return pl.v16 ? dense_t<uint16_t, 8>(pl, s) : dense_t<uint16_t, 1>(pl, s);
 }
 
+template <typename T, int VEC, bool GROUP>
+int sparse_tg(const Plan &pl, const Ents &e, int64_t nnz_cap, hipStream_t s) {
+    // one thread per (entry, chunk) of the capacity; the live count is read on the device
+    const int grid = grid_for(nnz_cap * (int64_t)pl.f.cpool, SHPL_BLOCK, 1 << 20);
+    if (nnz_cap <= LONG_RUN) {
+        hipLaunchKernelGGL((k_sparse<T, VEC, GROUP, false>), dim3(grid), dim3(SHPL_BLOCK), 0, s, pl.f, e);
+        SHPL_LAUNCH_CHECK();
+        return SHPL_OK;
+    }
+    hipLaunchKernelGGL((k_sparse<T, VEC, GROUP, true>), dim3(grid), dim3(SHPL_BLOCK), 0, s, pl.f, e);
+    SHPL_LAUNCH_CHECK();
+    // a bounded grid: each workgroup scans per_block slots, LONG_SLOTS at a time
+    int64_t lgrid = (nnz_cap + LONG_SLOTS - 1) / LONG_SLOTS;
+    if (lgrid > LONG_GRID) lgrid = LONG_GRID;
+    const int64_t per_block = (nnz_cap + lgrid - 1) / lgrid;
+    hipLaunchKernelGGL((k_sparse_long<T, VEC, GROUP>), dim3((unsigned)lgrid), dim3(SHPL_BLOCK), 0, s, pl.f, e,
+                       per_block);
+    SHPL_LAUNCH_CHECK();
+    return SHPL_OK;
+}
+
 template <typename T, int VEC>
 int sparse_t(const Plan &pl, const shpl_csr *csr, bool group, hipStream_t s) {
     Ents e{csr->nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_col, csr->ent_val};
-    // one thread per (entry, chunk) of the capacity; the live count is read on the device
-    const int grid = grid_for(csr->nnz_cap * (int64_t)pl.f.cpool, SHPL_BLOCK, 1 << 20);
-    if (group)
-        hipLaunchKernelGGL((k_sparse<T, VEC, true>), dim3(grid), dim3(SHPL_BLOCK), 0, s, pl.f, e);
-    else
-        hipLaunchKernelGGL((k_sparse<T, VEC, false>), dim3(grid), dim3(SHPL_BLOCK), 0, s, pl.f, e);
-    SHPL_LAUNCH_CHECK();
-    return SHPL_OK;
+    return group ? sparse_tg<T, VEC, true>(pl, e, csr->nnz_cap, s) : sparse_tg<T, VEC, false>(pl, e, csr->nnz_cap, s);
 }
 
 int sparse(const Plan &pl, const shpl_csr *csr, int direction, hipStream_t s) {
