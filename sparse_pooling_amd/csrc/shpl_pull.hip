@@ -178,9 +178,26 @@ constexpr int LONG_WALK = 16;
 // separate multiply and add; GROUP (BY_PIXEL): per column partial Q[k] first
 // (ScatterNd's order). W entries per step: their index loads, then their
 // feature loads, are each in flight together.
+// Index words of W consecutive entries from i (past nnz: dst -1).
+template <bool GROUP, int W>
+struct IdxBatch {
+    int32_t d[W], sr[W], kc[W];
+    float w[W];
+    __device__ __forceinline__ void load(const Ents &e, int64_t i) {
+#pragma unroll
+        for (int u = 0; u < W; ++u) {
+            const bool ok = i + u < e.n;
+            d[u] = ok ? e.dst[i + u] : -1;
+            sr[u] = ok ? e.src[i + u] : 0;
+            w[u] = ok ? e.val[i + u] : 0.0f;
+            kc[u] = (GROUP && ok) ? e.col[i + u] : 0;
+        }
+    }
+};
+
 template <typename T, int VEC, bool GROUP, int W>
 __device__ __forceinline__ void walk_run(const Feat &f, const Ents &e, int64_t s, int32_t key, uint32_t c,
-                                         float (&acc)[VEC]) {
+                                         float (&acc)[VEC], const IdxBatch<GROUP, W> *first = nullptr) {
     typedef Chunk<T, VEC> C;
     const int64_t nnz = e.n;
     const T *sc = reinterpret_cast<const T *>(f.src) + f.src_off + (int64_t)c * VEC;
@@ -207,14 +224,19 @@ __device__ __forceinline__ void walk_run(const Feat &f, const Ents &e, int64_t s
             kc[u] = (GROUP && in[u]) ? e.col[i + u] : 0;
         }
 #else
-        // index loads of the batch do not wait for each other (dst need not match yet)
+        // index loads of the batch do not wait for each other (dst need not match yet);
+        // the first batch may come preloaded (issued with the caller's head test)
+        IdxBatch<GROUP, W> b;
+        if (first && i == s)
+            b = *first;
+        else
+            b.load(e, i);
 #pragma unroll
         for (int u = 0; u < W; ++u) {
-            const bool ok = i + u < nnz;
-            d[u] = ok ? e.dst[i + u] : -1;
-            sr[u] = ok ? e.src[i + u] : 0;
-            w[u] = ok ? e.val[i + u] : 0.0f;
-            kc[u] = (GROUP && ok) ? e.col[i + u] : 0;
+            d[u] = b.d[u];
+            sr[u] = b.sr[u];
+            w[u] = b.w[u];
+            kc[u] = b.kc[u];
         }
 #pragma unroll
         for (int u = 0; u < W; ++u) in[u] = d[u] == key && (u == 0 || in[u - 1]);
@@ -276,14 +298,17 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse(const Feat f, const Ents 
          t += (int64_t)gridDim.x * SHPL_BLOCK) {
         const int64_t s = t / f.cpool;
         const uint32_t c = (uint32_t)(t - s * f.cpool);
-        // the three index loads are independent: one round trip
-        const int32_t key = e.dst[s];
+        // the head test's loads and the walk's first index batch are
+        // independent: one round trip
+        IdxBatch<GROUP, WALK> b0;
+        b0.load(e, s);
+        const int32_t key = b0.d[0];
         const int32_t prev = s > 0 ? e.dst[s - 1] : -1;
         const int32_t ahead = (SPLIT && s + LONG_RUN < nnz) ? e.dst[s + LONG_RUN] : -1;
         if (key < 0 || prev == key) continue;  // empty, or not the first entry of key
         if (SPLIT && ahead == key) continue;   // a run longer than LONG_RUN: k_sparse_long's
         float acc[VEC];
-        walk_run<T, VEC, GROUP, WALK>(f, e, s, key, c, acc);
+        walk_run<T, VEC, GROUP, WALK>(f, e, s, key, c, acc, &b0);
         store_pooled<T, VEC>(f, key, c, acc);
     }
 }
