@@ -357,18 +357,57 @@ int shpl_conv3x3(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a,
                  int act, void *d_out, int64_t out_stride, double *d_stats, void *d_ws,
                  size_t ws_bytes, void *stream);
 
-/* BatchNorm in training mode over rows x c (in place), from d_stats of
- * shpl_conv3x3 and count = rows: mean = sum/count, var = sumsq/count - mean^2,
- * x = act((x - mean) * gamma / sqrt(var + eps) + beta); moving averages
- * m -= (m - v) * (1 - decay) with the Bessel-corrected variance (TF
- * FusedBatchNorm, slim.batch_norm defaults eps 1e-3, decay 0.999, gamma
- * NULL = 1). d_batch_mean / d_batch_var (optional) receive the batch
- * moments (variance Bessel-corrected, as FusedBatchNorm's outputs).
- * d_ws: 2*c floats. */
-int shpl_batch_norm(int dtype, int64_t rows, void *d_x, int64_t stride, int64_t c, const double *d_stats,
-                    double count, float eps, const float *d_gamma, const float *d_beta, int act,
-                    float *d_moving_mean, float *d_moving_var, float decay, float *d_batch_mean,
+/* BatchNorm in training mode over rows x c, from d_stats of shpl_conv3x3 and
+ * count = rows: mean = sum/count, var = sumsq/count - mean^2,
+ * y = act((x - mean) * gamma / sqrt(var + eps) + beta), written to d_y
+ * (NULL: in place over d_x); moving averages m -= (m - v) * (1 - decay) with
+ * the Bessel-corrected variance (TF FusedBatchNorm, slim.batch_norm defaults
+ * eps 1e-3, decay 0.999, gamma NULL = 1). d_batch_mean / d_batch_var
+ * (optional) receive the batch moments (variance Bessel-corrected, as
+ * FusedBatchNorm's outputs). d_ws: 2*c floats; on return it holds the mean
+ * and scale = gamma / sqrt(var + eps) that shpl_batch_norm_backward takes. */
+int shpl_batch_norm(int dtype, int64_t rows, void *d_x, void *d_y, int64_t stride, int64_t c,
+                    const double *d_stats, double count, float eps, const float *d_gamma, const float *d_beta,
+                    int act, float *d_moving_mean, float *d_moving_var, float decay, float *d_batch_mean,
                     float *d_batch_var, float *d_ws, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Post-fusion conv backward (the TF autodiff of rpn_model.py:338-354)
+ * ------------------------------------------------------------------------- */
+
+/* BatchNorm (+ ReLU) backward over rows x c. g_bn = g * [y > 0] when act is
+ * SHPL_ACT_RELU (d_y = the layer output), xhat = (raw - mean) * scale / gamma
+ * (d_raw = the conv output). Per channel (f64, fixed order):
+ * dbeta = sum g_bn, dgamma = sum g_bn * xhat; then
+ *   training:  g_raw = scale * (g_bn - dbeta / rows - xhat * dgamma / rows)
+ *   inference: g_raw = scale * g_bn   (mean / scale from the moving statistics)
+ * d_mean / d_scale NULL: 0 / 1 -- a conv bias instead of BatchNorm (dbeta is
+ * then the bias gradient). Workspace: shpl_batch_norm_backward_workspace_bytes. */
+int shpl_batch_norm_backward_workspace_bytes(int64_t rows, int64_t c, size_t *bytes);
+int shpl_batch_norm_backward(int dtype, int64_t rows, const void *d_y, const void *d_raw, const void *d_gy,
+                             int64_t stride, int64_t c, const float *d_mean, const float *d_scale,
+                             const float *d_gamma, int act, int training, void *d_graw, float *d_dbeta,
+                             float *d_dgamma, void *d_ws, size_t ws_bytes, void *stream);
+
+/* Input gradient: dx = conv3x3_SAME(gy, W') with W'[ky][kx][co][ci] =
+ * W[2-ky][2-kx][ci][co], the forward conv kernel on transposed packed
+ * weights. d_weights: the forward's HWIO [3][3][c_dx][c_gy]. Workspace:
+ * shpl_conv3x3_workspace_bytes(dtype, n_frames, h, w, c_gy, 0, c_dx, 0, 0). */
+int shpl_conv3x3_dgrad(int dtype, int n_frames, int64_t h, int64_t w, const void *d_gy, int64_t gy_stride,
+                       int64_t c_gy, const void *d_weights, int64_t c_dx, void *d_dx, int64_t dx_stride,
+                       void *d_ws, size_t ws_bytes, void *stream);
+
+/* Weight gradient: dw[ky][kx][ci][co] = sum over pixels of x[p + (ky-1, kx-1)][ci]
+ * * gy[p][co], x given exactly as shpl_conv3x3's input (A channels, then B
+ * channels, dense or pooled from the CSR -- recomputed, never stored). f32
+ * MFMA (bf16 inputs widened), per-workgroup partials summed in a fixed order
+ * (f64): deterministic. d_dw: f32 HWIO [3][3][c_a+c_b][c_out]. */
+int shpl_conv3x3_wgrad_workspace_bytes(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_t c_b,
+                                       int64_t c_out, int pooled, size_t *bytes);
+int shpl_conv3x3_wgrad(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a, int64_t a_stride,
+                       int64_t a_off, int64_t c_a, const void *d_b, int64_t b_stride, int64_t b_off, int64_t c_b,
+                       const shpl_csr *pool, const int64_t *d_frame_off, const void *d_gy, int64_t gy_stride,
+                       int64_t c_out, float *d_dw, void *d_ws, size_t ws_bytes, void *stream);
 
 #ifdef __cplusplus
 }

@@ -590,3 +590,78 @@ void shplo_bn_train(const double *raw, int64_t rows, int64_t C, double eps, cons
         if (batch_var) batch_var[c] = vu;
     }
 }
+
+/* Weight gradient of the 3x3 SAME conv: dw[ky][kx][ci][co] =
+ * sum over (f, y, x) of in[f, y+ky-1, x+kx-1, ci] * g[f, y, x, co]
+ * (zero outside the map), summed in double. */
+void shplo_conv3x3_wgrad(const float *in, int64_t B, int64_t H, int64_t W, int64_t Cin, const float *g,
+                         int64_t Cout, double *dw)
+{
+    memset(dw, 0, sizeof(double) * (size_t)(9 * Cin * Cout));
+    for (int64_t f = 0; f < B; ++f)
+        for (int64_t y = 0; y < H; ++y)
+            for (int64_t x = 0; x < W; ++x) {
+                const float *gr = g + ((f * H + y) * W + x) * Cout;
+                for (int64_t ky = 0; ky < 3; ++ky) {
+                    const int64_t yy = y + ky - 1;
+                    if (yy < 0 || yy >= H) continue;
+                    for (int64_t kx = 0; kx < 3; ++kx) {
+                        const int64_t xx = x + kx - 1;
+                        if (xx < 0 || xx >= W) continue;
+                        const float *a = in + ((f * H + yy) * W + xx) * Cin;
+                        double *d = dw + (ky * 3 + kx) * Cin * Cout;
+                        for (int64_t ci = 0; ci < Cin; ++ci) {
+                            const double av = a[ci];
+                            for (int64_t co = 0; co < Cout; ++co) d[ci * Cout + co] += av * (double)gr[co];
+                        }
+                    }
+                }
+            }
+}
+
+/* BatchNorm + ReLU backward in double. raw: the conv output (pre-BN), g: the
+ * gradient of the layer output. training: batch moments (biased variance)
+ * normalise, as in the forward; otherwise mean / var are the moving
+ * statistics (constants). Writes d_raw, dbeta = sum g_bn, dgamma =
+ * sum g_bn * xhat, with g_bn = g * [y > 0] (ReLU) and
+ *   training:  d_raw = gamma r / N (N g_bn - dbeta - xhat dgamma)
+ *   inference: d_raw = gamma r g_bn,     r = 1 / sqrt(var + eps). */
+void shplo_bn_bwd(const double *raw, const float *g, int64_t rows, int64_t C, int training, const double *mean_in,
+                  const double *var_in, double eps, const float *gamma, const float *beta, int relu, double *d_raw,
+                  double *dbeta, double *dgamma)
+{
+    for (int64_t c = 0; c < C; ++c) {
+        double mean, var;
+        if (training) {
+            double s = 0.0, s2 = 0.0;
+            for (int64_t r = 0; r < rows; ++r) s += raw[r * C + c];
+            mean = s / (double)rows;
+            for (int64_t r = 0; r < rows; ++r) {
+                const double d = raw[r * C + c] - mean;
+                s2 += d * d;
+            }
+            var = s2 / (double)rows;
+        } else {
+            mean = mean_in[c];
+            var = var_in[c];
+        }
+        const double rr = 1.0 / sqrt(var + eps);
+        const double gm = gamma ? gamma[c] : 1.0, bt = beta ? beta[c] : 0.0;
+        double db = 0.0, dg = 0.0;
+        for (int64_t r = 0; r < rows; ++r) {
+            const double xh = (raw[r * C + c] - mean) * rr;
+            const double y = gm * xh + bt;
+            const double gb = (relu && !(y > 0.0)) ? 0.0 : g[r * C + c];
+            db += gb;
+            dg += gb * xh;
+        }
+        dbeta[c] = db;
+        dgamma[c] = dg;
+        for (int64_t r = 0; r < rows; ++r) {
+            const double xh = (raw[r * C + c] - mean) * rr;
+            const double y = gm * xh + bt;
+            const double gb = (relu && !(y > 0.0)) ? 0.0 : g[r * C + c];
+            d_raw[r * C + c] = training ? gm * rr / (double)rows * ((double)rows * gb - db - xh * dg) : gm * rr * gb;
+        }
+    }
+}

@@ -57,6 +57,10 @@ def lib():
                                           p, p]
         _lib.shplo_conv3x3.restype = None
         _lib.shplo_conv3x3.argtypes = [p, i64, i64, i64, i64, p, i64, p, p, p, ctypes.c_int, p, p]
+        _lib.shplo_conv3x3_wgrad.restype = None
+        _lib.shplo_conv3x3_wgrad.argtypes = [p, i64, i64, i64, i64, p, i64, p]
+        _lib.shplo_bn_bwd.restype = None
+        _lib.shplo_bn_bwd.argtypes = [p, p, i64, i64, ctypes.c_int, p, p, d, p, p, ctypes.c_int, p, p, p]
         _lib.shplo_bn_train.restype = None
         _lib.shplo_bn_train.argtypes = [p, i64, i64, d, p, p, ctypes.c_int, p, p, p, d, p, p]
     return _lib
@@ -344,3 +348,40 @@ def batch_norm_train(raw, eps=1e-3, gamma=None, beta=None, relu=True, moving_mea
                          int(bool(relu)), _p(out), None if mm is None else _p(mm), None if mv is None else _p(mv),
                          float(decay), _p(bm), _p(bv))
     return out, bm, bv, mm, mv
+
+
+def conv3x3_dgrad(g, w):
+    """Input gradient of the SAME 3x3 conv: the conv of ``g`` [B,H,W,Cout] with
+    the flipped, transposed weights W'[ky][kx][co][ci] = W[2-ky][2-kx][ci][co]
+    (double sums, rounded once)."""
+    wt = np.ascontiguousarray(np.asarray(w, np.float32)[::-1, ::-1].transpose(0, 1, 3, 2))
+    return conv3x3(g, wt)
+
+
+def conv3x3_wgrad(x, g):
+    """Weight gradient [3,3,Cin,Cout] (double) of the SAME 3x3 conv."""
+    x = _c(x, np.float32)
+    g = _c(g, np.float32)
+    B, H, W, Cin = x.shape
+    Cout = g.shape[3]
+    dw = np.empty((3, 3, Cin, Cout), np.float64)
+    lib().shplo_conv3x3_wgrad(_p(x), B, H, W, Cin, _p(g), Cout, _p(dw))
+    return dw
+
+
+def batch_norm_backward(raw, g, training=True, mean=None, var=None, eps=1e-3, gamma=None, beta=None, relu=True):
+    """(d_raw, dbeta, dgamma) in double of BatchNorm (+ ReLU) over [..., C]."""
+    raw = _c(raw, np.float64)
+    g = _c(g, np.float32)
+    C = raw.shape[-1]
+    rows = raw.size // C
+    d_raw = np.empty(raw.shape, np.float64)
+    db, dg = np.empty(C, np.float64), np.empty(C, np.float64)
+    m = None if mean is None else _c(mean, np.float64)
+    v = None if var is None else _c(var, np.float64)
+    gm = None if gamma is None else _c(gamma, np.float32)
+    bt = None if beta is None else _c(beta, np.float32)
+    lib().shplo_bn_bwd(_p(raw), _p(g), rows, C, int(bool(training)), None if m is None else _p(m),
+                       None if v is None else _p(v), float(eps), None if gm is None else _p(gm),
+                       None if bt is None else _p(bt), int(bool(relu)), _p(d_raw), _p(db), _p(dg))
+    return d_raw, db, dg

@@ -155,24 +155,154 @@ __device__ __forceinline__ void pool_run(const ConvArgs &p, const T *img, int c0
     }
 }
 
+// The halo tile's runs of CSR entries in LDS (POOLED): one run per occupied
+// halo cell, with its first entry's source row and weight.
+struct HaloRuns {
+    int32_t *lo, *pre;                    // [HH], [HH+1]: entry range of each halo row
+    int32_t *pix, *e, *end, *src;         // [HH*HWD]
+    float *val;                           // [HH*HWD]
+    uint8_t *occ;                         // [HH*HWD]: cell holds a run
+    int64_t *scan;                        // [SHPL_BLOCK/64+1]
+};
+
+// Lists the runs of the halo tile of output tile (f, y0, x0): per halo row
+// the entry range of cells [x0-1, x0+TW+1) (row pointers + binary search),
+// then one block scan in entry order. Every thread of the 256 calls it.
+__device__ int find_runs(const ConvArgs &p, int f, int y0, int x0, const HaloRuns &r) {
+    constexpr int NPIX = HH * HWD;
+    const int tid = threadIdx.x;
+    const int H = p.h, W = p.w;
+    const int64_t frame_row0 = (int64_t)f * H * W;
+    for (int j = tid; j < NPIX; j += CONV_BLOCK) r.occ[j] = 0;
+    if (tid < HH) {
+        const int y = y0 - 1 + tid;
+        int32_t lo = 0, hi = 0;
+        if (y >= 0 && y < H) {
+            const int32_t ra = p.row_ptr[(int64_t)f * (H + 1) + y];
+            const int32_t rb = p.row_ptr[(int64_t)f * (H + 1) + y + 1];
+            const int32_t kl = (int32_t)(frame_row0 + (int64_t)y * W + (x0 > 0 ? x0 - 1 : 0));
+            const int32_t kh = (int32_t)(frame_row0 + (int64_t)y * W + (x0 + TW + 1 < W ? x0 + TW + 1 : W));
+            lo = lower_bound(p.ent_dst, ra, rb, kl);
+            hi = lower_bound(p.ent_dst, lo, rb, kh);
+        }
+        r.lo[tid] = lo;
+        r.pre[tid + 1] = hi - lo;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        r.pre[0] = 0;
+        for (int k = 0; k < HH; ++k) r.pre[k + 1] += r.pre[k];
+    }
+    __syncthreads();
+    const int n_ent = r.pre[HH];
+    int n_run = 0, n_tail = 0;
+    for (int base = 0; base < n_ent; base += CONV_BLOCK) {
+        const int j = base + tid;
+        int64_t flags = 0;
+        int32_t e = 0, pix = 0;
+        if (j < n_ent) {
+            int k = 0;
+            while (j >= r.pre[k + 1]) ++k;
+            e = r.lo[k] + (j - r.pre[k]);
+            const int32_t last = r.lo[k] + (r.pre[k + 1] - r.pre[k]) - 1;
+            const int32_t d = p.ent_dst[e];
+            const bool head = j == r.pre[k] || p.ent_dst[e - 1] != d;
+            const bool tail = e == last || p.ent_dst[e + 1] != d;
+            flags = (head ? 1 : 0) | (tail ? (int64_t)1 << 32 : 0);
+            const int y = y0 - 1 + k;
+            pix = k * HWD + (int)((int64_t)d - frame_row0 - (int64_t)y * W) - (x0 - 1);
+        }
+        int64_t tot;
+        const int64_t ex = block_excl_scan(flags, r.scan, &tot);
+        if (flags & 1) {
+            const int k = n_run + (int)(ex & 0xffffffff);
+            r.e[k] = e;
+            r.pix[k] = pix;
+            r.occ[pix] = 1;
+            r.src[k] = p.ent_src[e];
+            r.val[k] = p.ent_val[e];
+        }
+        if (flags >> 32) r.end[n_tail + (int)(ex >> 32)] = e + 1;
+        n_run += (int)(tot & 0xffffffff);
+        n_tail += (int)(tot >> 32);  // a run may open in one round and close in the next
+    }
+    __syncthreads();
+    return n_run;
+}
+
+// Stages input chunk q (channels of A, then of B) of the 10 x 34 halo of
+// output tile (f, y0, x0) into s_in ([pixel][chunk], PSTR-byte rows); zero
+// outside the map. Pooled chunks: zeros where no entry lands, each run's sum
+// elsewhere (disjoint cells: no barrier between the two). The caller
+// synchronises after.
+template <typename T, bool POOLED>
+__device__ __forceinline__ void stage_halo(const ConvArgs &p, int q, int f, int y0, int x0, uint8_t *s_in,
+                                           const HaloRuns &r, int n_run) {
+    typedef Elem<T> E;
+    constexpr int CK = E::CK, HE = E::HE, NP = E::NP, PSTR = E::PSTR;
+    constexpr int IN_PIECES = HH * HWD * NP;
+    constexpr int IN_IT = (IN_PIECES + CONV_BLOCK - 1) / CONV_BLOCK;
+    const int tid = threadIdx.x;
+    const int H = p.h, W = p.w;
+    const int64_t frame_row0 = (int64_t)f * H * W;
+    const bool from_a = q < p.qa;
+    if (from_a || !POOLED) {
+        const T *src = reinterpret_cast<const T *>(from_a ? p.a : p.b) + (from_a ? p.a_off : p.b_off);
+        const int64_t stride = from_a ? p.a_stride : p.b_stride;
+        const int c_src = from_a ? p.c_a : p.c_b;
+        const int c0 = (from_a ? q : q - p.qa) * CK;
+        const bool vec = from_a ? p.vec_a : p.vec_b;
+        u32x4 v[IN_IT];
+#pragma unroll
+        for (int u = 0; u < IN_IT; ++u) {
+            const int j = tid + u * CONV_BLOCK;
+            v[u] = u32x4{0u, 0u, 0u, 0u};
+            if (j < IN_PIECES) {
+                const int pix = j / NP, hr = pix / HWD, hc = pix - hr * HWD;
+                const int y = y0 - 1 + hr, x = x0 - 1 + hc;
+                if (y >= 0 && y < H && x >= 0 && x < W)
+                    v[u] = load_piece<T>(src + (frame_row0 + (int64_t)y * W + x) * stride, c0 + (j % NP) * HE, c_src,
+                                         vec);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < IN_IT; ++u) {
+            const int j = tid + u * CONV_BLOCK;
+            if (j < IN_PIECES) *reinterpret_cast<u32x4 *>(s_in + (j / NP) * PSTR + (j % NP) * 16) = v[u];
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < IN_IT; ++u) {
+            const int j = tid + u * CONV_BLOCK;
+            if (j < IN_PIECES && !r.occ[j / NP])
+                *reinterpret_cast<u32x4 *>(s_in + (j / NP) * PSTR + (j % NP) * 16) = u32x4{0u, 0u, 0u, 0u};
+        }
+        const T *img = reinterpret_cast<const T *>(p.b) + p.b_off;
+        for (int k = tid; k < n_run; k += CONV_BLOCK)
+            pool_run<T>(p, img, (q - p.qa) * CK, r.e[k], r.end[k], r.src[k], r.val[k], s_in + r.pix[k] * PSTR);
+    }
+}
+
+#define SHPL_HALO_RUNS_LDS(POOLED)                                                                            \
+    __shared__ int32_t s_lo[HH], s_pre[HH + 1];                                                              \
+    __shared__ int32_t s_run_pix[POOLED ? HH * HWD : 1], s_run_e[POOLED ? HH * HWD : 1],                     \
+        s_run_end[POOLED ? HH * HWD : 1], s_run_src[POOLED ? HH * HWD : 1];                                 \
+    __shared__ float s_run_val[POOLED ? HH * HWD : 1];                                                       \
+    __shared__ uint8_t s_occ[POOLED ? HH * HWD : 1];                                                         \
+    __shared__ int64_t s_scan[SHPL_BLOCK / 64 + 1];                                                          \
+    const HaloRuns runs{s_lo, s_pre, s_run_pix, s_run_e, s_run_end, s_run_src, s_run_val, s_occ, s_scan};
+
 template <typename T, bool POOLED, bool STATS>
 __global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3(const ConvArgs p) {
     typedef Elem<T> E;
     constexpr int CK = E::CK, HE = E::HE, NP = E::NP, PSTR = E::PSTR;
-    constexpr int NPIX = HH * HWD;  // halo cells; at most one run of entries per cell
-    constexpr int IN_PIECES = NPIX * NP, W_PIECES = W_ROWS * NP;
-    constexpr int IN_IT = (IN_PIECES + CONV_BLOCK - 1) / CONV_BLOCK;
+    constexpr int NPIX = HH * HWD;
+    constexpr int W_PIECES = W_ROWS * NP;
     constexpr int W_IT = (W_PIECES + CONV_BLOCK - 1) / CONV_BLOCK;
     __shared__ __attribute__((aligned(16))) uint8_t s_in[NPIX * PSTR];
     __shared__ __attribute__((aligned(16))) uint8_t s_w[W_ROWS * PSTR];
-    // POOLED: the halo tile's runs of CSR entries (one run = one occupied cell)
-    __shared__ int32_t s_lo[HH], s_pre[HH + 1];
-    __shared__ int32_t s_run_pix[POOLED ? NPIX : 1], s_run_e[POOLED ? NPIX : 1], s_run_end[POOLED ? NPIX : 1];
-    __shared__ int32_t s_run_src[POOLED ? NPIX : 1];
-    __shared__ float s_run_val[POOLED ? NPIX : 1];
-    __shared__ uint8_t s_occ[POOLED ? NPIX : 1];
-    __shared__ int64_t s_scan[SHPL_BLOCK / 64 + 1];
     __shared__ float s_red[4][2][NCO];
+    SHPL_HALO_RUNS_LDS(POOLED)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int pl = lane & 31, hf = lane >> 5;
@@ -186,67 +316,7 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3(const ConvArgs p) {
     const int64_t frame_row0 = (int64_t)f * H * W;
     const int Q = p.qa + p.qb;
 
-    int n_run = 0;
-    if (POOLED) {
-        // 1. entry range of each halo row: cells [x0-1, x0+TW+1) of row y, from
-        //    the per-row entry pointers and a binary search inside the row
-        for (int j = tid; j < NPIX; j += CONV_BLOCK) s_occ[j] = 0;
-        if (tid < HH) {
-            const int y = y0 - 1 + tid;
-            int32_t lo = 0, hi = 0;
-            if (y >= 0 && y < H) {
-                const int32_t ra = p.row_ptr[(int64_t)f * (H + 1) + y];
-                const int32_t rb = p.row_ptr[(int64_t)f * (H + 1) + y + 1];
-                const int32_t kl = (int32_t)(frame_row0 + (int64_t)y * W + (x0 > 0 ? x0 - 1 : 0));
-                const int32_t kh = (int32_t)(frame_row0 + (int64_t)y * W + (x0 + TW + 1 < W ? x0 + TW + 1 : W));
-                lo = lower_bound(p.ent_dst, ra, rb, kl);
-                hi = lower_bound(p.ent_dst, lo, rb, kh);
-            }
-            s_lo[tid] = lo;
-            s_pre[tid + 1] = hi - lo;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            s_pre[0] = 0;
-            for (int r = 0; r < HH; ++r) s_pre[r + 1] += s_pre[r];
-        }
-        __syncthreads();
-        // 2. runs (first / one-past-last entry of each occupied cell) in entry
-        //    order, with the source row and weight of their first entry
-        const int n_ent = s_pre[HH];
-        int n_tail = 0;
-        for (int base = 0; base < n_ent; base += CONV_BLOCK) {
-            const int j = base + tid;
-            int64_t flags = 0;
-            int32_t e = 0, pix = 0;
-            if (j < n_ent) {
-                int r = 0;
-                while (j >= s_pre[r + 1]) ++r;
-                e = s_lo[r] + (j - s_pre[r]);
-                const int32_t last = s_lo[r] + (s_pre[r + 1] - s_pre[r]) - 1;
-                const int32_t d = p.ent_dst[e];
-                const bool head = j == s_pre[r] || p.ent_dst[e - 1] != d;
-                const bool tail = e == last || p.ent_dst[e + 1] != d;
-                flags = (head ? 1 : 0) | (tail ? (int64_t)1 << 32 : 0);
-                const int y = y0 - 1 + r;
-                pix = r * HWD + (int)((int64_t)d - frame_row0 - (int64_t)y * W) - (x0 - 1);
-            }
-            int64_t tot;
-            const int64_t ex = block_excl_scan(flags, s_scan, &tot);
-            if (flags & 1) {
-                const int k = n_run + (int)(ex & 0xffffffff);
-                s_run_e[k] = e;
-                s_run_pix[k] = pix;
-                s_occ[pix] = 1;
-                s_run_src[k] = p.ent_src[e];
-                s_run_val[k] = p.ent_val[e];
-            }
-            if (flags >> 32) s_run_end[n_tail + (int)(ex >> 32)] = e + 1;
-            n_run += (int)(tot & 0xffffffff);
-            n_tail += (int)(tot >> 32);  // a run may open in one round and close in the next
-        }
-        __syncthreads();
-    }
+    const int n_run = POOLED ? find_runs(p, f, y0, x0, runs) : 0;
 
     f32x16 acc[2];
 #pragma unroll
@@ -255,7 +325,6 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3(const ConvArgs p) {
         for (int i = 0; i < 16; ++i) acc[m][i] = 0.0f;
 
     const T *wq = reinterpret_cast<const T *>(p.wp) + (int64_t)cob * Q * W_ROWS * CK;
-    const T *img = reinterpret_cast<const T *>(p.b) + p.b_off;
     for (int q = 0; q < Q; ++q) {
         // ---- stage chunk q in LDS, synchronously: the other workgroups on the
         // CU keep the MFMAs busy meanwhile (a register-staged prefetch of chunk
@@ -273,8 +342,14 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3(const ConvArgs p) {
                 if (j < W_PIECES) *reinterpret_cast<u32x4 *>(s_w + (j / NP) * PSTR + (j % NP) * 16) = v[u];
             }
         }
-        const bool from_a = q < p.qa;
-        if (from_a || !POOLED) {
+        if constexpr (POOLED) {
+            stage_halo<T, POOLED>(p, q, f, y0, x0, s_in, runs, n_run);
+        } else {
+            // the dense form of stage_halo, written out: inlined through the
+            // helper it costs 16 more VGPRs here (5 -> 4 waves per SIMD)
+            constexpr int IN_PIECES = NPIX * NP;
+            constexpr int IN_IT = (IN_PIECES + CONV_BLOCK - 1) / CONV_BLOCK;
+            const bool from_a = q < p.qa;
             const T *src = reinterpret_cast<const T *>(from_a ? p.a : p.b) + (from_a ? p.a_off : p.b_off);
             const int64_t stride = from_a ? p.a_stride : p.b_stride;
             const int c_src = from_a ? p.c_a : p.c_b;
@@ -298,18 +373,6 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3(const ConvArgs p) {
                 const int j = tid + u * CONV_BLOCK;
                 if (j < IN_PIECES) *reinterpret_cast<u32x4 *>(s_in + (j / NP) * PSTR + (j % NP) * 16) = v[u];
             }
-        } else {
-            // pooled chunk: zeros where no entry lands, each run's sum elsewhere
-            // (disjoint cells: no barrier between the two)
-#pragma unroll
-            for (int u = 0; u < IN_IT; ++u) {
-                const int j = tid + u * CONV_BLOCK;
-                if (j < IN_PIECES && !s_occ[j / NP])
-                    *reinterpret_cast<u32x4 *>(s_in + (j / NP) * PSTR + (j % NP) * 16) = u32x4{0u, 0u, 0u, 0u};
-            }
-            for (int k = tid; k < n_run; k += CONV_BLOCK)
-                pool_run<T>(p, img, (q - p.qa) * CK, s_run_e[k], s_run_end[k], s_run_src[k], s_run_val[k],
-                            s_in + s_run_pix[k] * PSTR);
         }
         __syncthreads();
         // ---- 9 taps of MFMA over the chunk
@@ -391,10 +454,12 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3(const ConvArgs p) {
 }
 
 // Packed weights: HWIO [3][3][c_a+c_b][c_out] -> [co_block][chunk][tap][32][CK],
-// chunks of A's channels first, then B's, zero padded.
+// chunks of A's channels first, then B's, zero padded. transpose (the input
+// gradient): w is the forward's HWIO [3][3][c_out][c_a+c_b] and the packed
+// tap t takes W[8-t] transposed (W'[ky][kx][co][ci] = W[2-ky][2-kx][ci][co]).
 template <typename T>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_pack_w(const T *w, int c_a, int qa, int c_b, int qb, int c_out,
-                                                       int n_cob, T *wp) {
+                                                       int n_cob, int transpose, T *wp) {
     constexpr int CK = Elem<T>::CK;
     const int Q = qa + qb;
     const int64_t total = (int64_t)n_cob * Q * W_ROWS * CK;
@@ -420,7 +485,9 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_pack_w(const T *w, int c_a, int 
             ci = c_a + cb;
             ok = cb < c_b;
         }
-        wp[t] = (ok && co < c_out) ? w[((int64_t)tap * cin + ci) * c_out + co] : T(0);
+        const int64_t src = transpose ? ((int64_t)(8 - tap) * c_out + co) * cin + ci
+                                      : ((int64_t)tap * cin + ci) * c_out + co;
+        wp[t] = (ok && co < c_out) ? w[src] : T(0);
     }
 }
 
@@ -490,7 +557,7 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_finalize(const double *stats,
 }
 
 template <typename T>
-__global__ __launch_bounds__(SHPL_BLOCK) void k_bn_apply(T *x, int64_t rows, int64_t stride, int c,
+__global__ __launch_bounds__(SHPL_BLOCK) void k_bn_apply(const T *x, T *y, int64_t rows, int64_t stride, int c,
                                                          const float *mean, const float *scale, const float *beta,
                                                          int act) {
     const int64_t total = rows * c;
@@ -498,11 +565,217 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_apply(T *x, int64_t rows, int
          t += (int64_t)gridDim.x * SHPL_BLOCK) {
         const int64_t r = t / c;
         const int ch = (int)(t - r * c);
-        T *px = x + r * stride + ch;
-        float v = __fmul_rn(__fsub_rn(Elem<T>::f(*px), mean[ch]), scale[ch]);
+        float v = __fmul_rn(__fsub_rn(Elem<T>::f(x[r * stride + ch]), mean[ch]), scale[ch]);
         if (beta) v = __fadd_rn(v, beta[ch]);
         if (act == 1) v = v > 0.0f ? v : 0.0f;
-        *px = Elem<T>::back(v);
+        y[r * stride + ch] = Elem<T>::back(v);
+    }
+}
+
+// ---------------------------------------------------------------- backward
+// BatchNorm (+ ReLU) backward. g_bn = g * [y > 0] (act), xhat = (raw - mean)
+// * scale / gamma; per-channel sums dbeta = sum g_bn, dgamma = sum g_bn xhat
+// over rows in a fixed order (f64 partials per block, then per channel), and
+//   training:  g_raw = scale * (g_bn - dbeta / N - xhat * dgamma / N)
+//   inference: g_raw = scale * g_bn     (moving statistics are constants)
+// mean / scale NULL: 0 / 1 (a conv bias instead of BN: g_raw = g_bn).
+template <typename T>
+__device__ __forceinline__ float bn_gbn(const T *y, const T *gy, int64_t o, int act) {
+    const float gv = Elem<T>::f(gy[o]);
+    return (act == 1 && !(Elem<T>::f(y[o]) > 0.0f)) ? 0.0f : gv;
+}
+
+template <typename T>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_partial(const T *y, const T *raw, const T *gy, int64_t rows,
+                                                               int64_t stride, int c, const float *mean,
+                                                               const float *scale, const float *gamma, int act,
+                                                               int64_t rows_per_block, double *part) {
+    __shared__ double red[2][SHPL_BLOCK];
+    int cc_n = 1;
+    while (cc_n * 2 <= c && cc_n * 2 <= SHPL_BLOCK) cc_n *= 2;  // channels per pass (a power of two)
+    const int rl_n = SHPL_BLOCK / cc_n, rl = threadIdx.x / cc_n, cc = threadIdx.x % cc_n;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
+    for (int c0 = 0; c0 < c; c0 += cc_n) {
+        const int ch = c0 + cc;
+        double s1 = 0.0, s2 = 0.0;
+        if (ch < c) {
+            const float m = mean ? mean[ch] : 0.0f;
+            const float inv = scale ? __fdiv_rn(scale[ch], gamma ? gamma[ch] : 1.0f) : 1.0f;
+            for (int64_t r = r0 + rl; r < r1; r += rl_n) {
+                const int64_t o = r * stride + ch;
+                const float gb = bn_gbn(y, gy, o, act);
+                const float xh = __fmul_rn(__fsub_rn(Elem<T>::f(raw[o]), m), inv);
+                s1 += (double)gb;
+                s2 += (double)gb * (double)xh;
+            }
+        }
+        red[0][threadIdx.x] = s1;
+        red[1][threadIdx.x] = s2;
+        __syncthreads();
+        if ((int)threadIdx.x < cc_n && c0 + (int)threadIdx.x < c) {
+            double a = 0.0, b = 0.0;
+            for (int k = 0; k < rl_n; ++k) {
+                a += red[0][k * cc_n + threadIdx.x];
+                b += red[1][k * cc_n + threadIdx.x];
+            }
+            part[((int64_t)blockIdx.x * 2 + 0) * c + c0 + threadIdx.x] = a;
+            part[((int64_t)blockIdx.x * 2 + 1) * c + c0 + threadIdx.x] = b;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_finalize(const double *part, int n_blocks, int c,
+                                                                double count, float *dbeta, float *dgamma,
+                                                                float *mean_terms) {
+    for (int ch = blockIdx.x * SHPL_BLOCK + threadIdx.x; ch < c; ch += gridDim.x * SHPL_BLOCK) {
+        double a = 0.0, b = 0.0;
+        for (int k = 0; k < n_blocks; ++k) {
+            a += part[((int64_t)k * 2 + 0) * c + ch];
+            b += part[((int64_t)k * 2 + 1) * c + ch];
+        }
+        if (dbeta) dbeta[ch] = (float)a;
+        if (dgamma) dgamma[ch] = (float)b;
+        mean_terms[ch] = (float)(a / count);
+        mean_terms[c + ch] = (float)(b / count);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_apply(const T *y, const T *raw, const T *gy, int64_t rows,
+                                                             int64_t stride, int c, const float *mean,
+                                                             const float *scale, const float *gamma, int act,
+                                                             int training, const float *mean_terms, T *graw) {
+    const int64_t total = rows * c;
+    for (int64_t t = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * SHPL_BLOCK) {
+        const int64_t r = t / c;
+        const int ch = (int)(t - r * c);
+        const int64_t o = r * stride + ch;
+        const float gb = bn_gbn(y, gy, o, act);
+        const float sc = scale ? scale[ch] : 1.0f;
+        float v;
+        if (training) {
+            const float inv = __fdiv_rn(sc, gamma ? gamma[ch] : 1.0f);
+            const float xh = __fmul_rn(__fsub_rn(Elem<T>::f(raw[o]), mean ? mean[ch] : 0.0f), inv);
+            v = __fmul_rn(sc, __fsub_rn(__fsub_rn(gb, mean_terms[ch]), __fmul_rn(xh, mean_terms[c + ch])));
+        } else {
+            v = __fmul_rn(sc, gb);
+        }
+        graw[o] = Elem<T>::back(v);
+    }
+}
+
+// Weight gradient: dW[tap][ci][co] = sum over pixels p of x[p + tap offset][ci] * g[p][co].
+// One workgroup per (group of output tiles, 32 input channels, 32 output
+// channels): per tile it stages the input halo of its 32 channels (the
+// forward's stage_halo: the pooled channels are recomputed from the CSR, so
+// bv_fused need not exist) and the 8x32-pixel gradient tile (as f32), and
+// wave w accumulates the 9 taps over tile rows 2w, 2w+1 with
+// v_mfma_f32_32x32x2_f32 (M = input channel, N = output channel, K = pixel
+// pairs). The four waves' sums and then the groups' partials are added in a
+// fixed order (k_wgrad_reduce): deterministic.
+constexpr int WG_GSTR = NCO + 1;  // floats per pixel of the staged gradient tile
+
+struct WgArgs {
+    const void *gy;
+    int64_t gy_stride;
+    int n_cib, n_cob, tiles_per_group;
+    float *part;  // [((group * n_cib + cib) * n_cob + cob)][9][32][32]
+};
+
+template <typename T, bool POOLED>
+__global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3_wgrad(const ConvArgs p, const WgArgs g) {
+    typedef Elem<T> E;
+    constexpr int CK = E::CK, PSTR = E::PSTR, NQ = 32 / CK;
+    constexpr int NPIX = HH * HWD;
+    __shared__ __attribute__((aligned(16))) uint8_t s_x[NQ * NPIX * PSTR];
+    __shared__ float s_g[TH * TW * WG_GSTR];
+    SHPL_HALO_RUNS_LDS(POOLED)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int pl = lane & 31, hf = lane >> 5;
+    const int grp = blockIdx.x, cib = blockIdx.y, cob = blockIdx.z;
+    const int Q = p.qa + p.qb;
+    const int H = p.h, W = p.w;
+    const T *gy = reinterpret_cast<const T *>(g.gy);
+    f32x16 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[t][i] = 0.0f;
+    const int t0 = grp * g.tiles_per_group;
+    const int t1 = t0 + g.tiles_per_group < p.n_tiles ? t0 + g.tiles_per_group : p.n_tiles;
+    // this lane's input channel: chunk ci / CK of the block, element ci % CK
+    const int a_off = (pl / CK) * NPIX * PSTR + (pl % CK) * (int)sizeof(T);
+    for (int tile = t0; tile < t1; ++tile) {
+        const int f = tile / p.tiles_per_frame;
+        const int t_in = tile - f * p.tiles_per_frame;
+        const int ty = t_in / p.tiles_x, tx = t_in - ty * p.tiles_x;
+        const int y0 = ty * TH, x0 = tx * TW;
+        const int64_t frame_row0 = (int64_t)f * H * W;
+        const int n_run = POOLED ? find_runs(p, f, y0, x0, runs) : 0;
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+            const int q = cib * NQ + j;
+            if (q < Q) stage_halo<T, POOLED>(p, q, f, y0, x0, s_x + j * NPIX * PSTR, runs, n_run);
+        }
+        for (int i = tid; i < TH * TW * NCO; i += CONV_BLOCK) {
+            const int pix = i / NCO, col = i - pix * NCO;
+            const int y = y0 + pix / TW, x = x0 + (pix % TW), co = cob * NCO + col;
+            float v = 0.0f;
+            if (y < H && x < W && co < p.c_out) v = E::f(gy[(frame_row0 + (int64_t)y * W + x) * g.gy_stride + co]);
+            s_g[pix * WG_GSTR + col] = v;
+        }
+        __syncthreads();
+        for (int sp = 0; sp < TW; ++sp) {  // 32 pixel pairs of the wave's 64 pixels
+            const int pp = 2 * sp + hf;
+            const int r = 2 * wave + (pp / TW), c = pp % TW;
+            const float bv = s_g[(r * TW + c) * WG_GSTR + pl];
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const int hp = (r + t / 3) * HWD + c + t % 3;
+                const float av = E::f(*reinterpret_cast<const T *>(s_x + a_off + hp * PSTR));
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[t], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+    // the four waves' sums, in wave order, into this workgroup's partial
+    float *red = reinterpret_cast<float *>(s_x);  // 4 x 1024 floats
+    float *out = g.part + (((int64_t)grp * g.n_cib + cib) * g.n_cob + cob) * (9 * NCO * NCO);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int ci = (i & 3) + 8 * (i >> 2) + 4 * hf;
+            red[wave * 1024 + ci * NCO + pl] = acc[t][i];
+        }
+        __syncthreads();
+        for (int e = tid; e < NCO * NCO; e += CONV_BLOCK)
+            out[t * 1024 + e] = __fadd_rn(__fadd_rn(__fadd_rn(red[e], red[1024 + e]), red[2048 + e]), red[3072 + e]);
+        __syncthreads();
+    }
+}
+
+// dW (f32, HWIO [3][3][c_a+c_b][c_out]) = the groups' partials summed in
+// group order (f64), channels mapped back from the chunk layout.
+__global__ __launch_bounds__(SHPL_BLOCK) void k_wgrad_reduce(const float *part, int n_groups, int n_cib, int n_cob,
+                                                             int c_a, int c_b, int qa, int ck, int c_out, float *dw) {
+    const int cin = c_a + c_b;
+    const int64_t total = (int64_t)9 * cin * c_out;
+    for (int64_t t = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * SHPL_BLOCK) {
+        const int co = (int)(t % c_out);
+        const int ci = (int)((t / c_out) % cin);
+        const int tap = (int)(t / ((int64_t)c_out * cin));
+        const int cs = ci < c_a ? ci : qa * ck + (ci - c_a);  // channel in the chunk layout
+        const int cib = cs / 32, cil = cs % 32, cob = co / NCO, col = co % NCO;
+        double sum = 0.0;
+        for (int k = 0; k < n_groups; ++k)
+            sum += (double)part[(((int64_t)k * n_cib + cib) * n_cob + cob) * (9 * NCO * NCO) + tap * 1024 + cil * NCO +
+                                col];
+        dw[t] = (float)sum;
     }
 }
 
@@ -539,11 +812,11 @@ bool aligned16(const void *ptr) { return ((uintptr_t)ptr & 15u) == 0; }
 
 template <typename T>
 int conv_launch(const ConvPlan &pl, ConvArgs &a, bool pooled, bool stats, const void *w, const int64_t *frame_off,
-                double *d_stats, hipStream_t s) {
+                double *d_stats, hipStream_t s, int transpose = 0) {
     T *wp = reinterpret_cast<T *>(const_cast<void *>(a.wp));
     const int64_t wtot = (int64_t)pl.n_cob * (pl.qa + pl.qb) * W_ROWS * Elem<T>::CK;
     hipLaunchKernelGGL(k_pack_w<T>, dim3(grid_for(wtot, SHPL_BLOCK, 4096)), dim3(SHPL_BLOCK), 0, s,
-                       reinterpret_cast<const T *>(w), a.c_a, pl.qa, a.c_b, pl.qb, a.c_out, pl.n_cob, wp);
+                       reinterpret_cast<const T *>(w), a.c_a, pl.qa, a.c_b, pl.qb, a.c_out, pl.n_cob, transpose, wp);
     SHPL_LAUNCH_CHECK();
     if (pooled) {
         hipLaunchKernelGGL(k_row_ptr, dim3(16, a.n_frames), dim3(SHPL_BLOCK), 0, s, a.ent_dst, frame_off, a.h, a.w,
@@ -649,14 +922,15 @@ extern "C" int shpl_conv3x3(int dtype, int n_frames, int64_t h, int64_t w, const
     return conv_launch<uint16_t>(pl, a, pooled, stats, d_weights, d_frame_off, d_stats, s);
 }
 
-extern "C" int shpl_batch_norm(int dtype, int64_t rows, void *d_x, int64_t stride, int64_t c, const double *d_stats,
-                               double count, float eps, const float *d_gamma, const float *d_beta, int act,
-                               float *d_moving_mean, float *d_moving_var, float decay, float *d_batch_mean,
-                               float *d_batch_var, float *d_ws, void *stream) {
+extern "C" int shpl_batch_norm(int dtype, int64_t rows, void *d_x, void *d_y, int64_t stride, int64_t c,
+                               const double *d_stats, double count, float eps, const float *d_gamma,
+                               const float *d_beta, int act, float *d_moving_mean, float *d_moving_var, float decay,
+                               float *d_batch_mean, float *d_batch_var, float *d_ws, void *stream) {
     if (dtype != SHPL_F32 && dtype != SHPL_BF16) return SHPL_ERR_ARG;
     if (rows < 0 || c < 1 || stride < c || c > (1 << 16)) return SHPL_ERR_BAD_SHAPE;
     if (act != 0 && act != 1) return SHPL_ERR_ARG;
     if (!d_stats || !d_ws || (rows > 0 && !d_x) || !(count > 0.0)) return SHPL_ERR_ARG;
+    if (!d_y) d_y = d_x;
     hipStream_t s = (hipStream_t)stream;
     float *mean = d_ws, *scale = d_ws + c;
     hipLaunchKernelGGL(k_bn_finalize, dim3(1), dim3(SHPL_BLOCK), 0, s, d_stats, count, (int)c, eps, d_gamma, mean,
@@ -665,11 +939,231 @@ extern "C" int shpl_batch_norm(int dtype, int64_t rows, void *d_x, int64_t strid
     if (rows == 0) return SHPL_OK;
     const int grid = grid_for(rows * c, SHPL_BLOCK, 1 << 16);
     if (dtype == SHPL_F32)
-        hipLaunchKernelGGL(k_bn_apply<float>, dim3(grid), dim3(SHPL_BLOCK), 0, s, reinterpret_cast<float *>(d_x), rows,
-                           stride, (int)c, mean, scale, d_beta, act);
+        hipLaunchKernelGGL(k_bn_apply<float>, dim3(grid), dim3(SHPL_BLOCK), 0, s, reinterpret_cast<const float *>(d_x),
+                           reinterpret_cast<float *>(d_y), rows, stride, (int)c, mean, scale, d_beta, act);
     else
-        hipLaunchKernelGGL(k_bn_apply<uint16_t>, dim3(grid), dim3(SHPL_BLOCK), 0, s, reinterpret_cast<uint16_t *>(d_x),
-                           rows, stride, (int)c, mean, scale, d_beta, act);
+        hipLaunchKernelGGL(k_bn_apply<uint16_t>, dim3(grid), dim3(SHPL_BLOCK), 0, s,
+                           reinterpret_cast<const uint16_t *>(d_x), reinterpret_cast<uint16_t *>(d_y), rows, stride,
+                           (int)c, mean, scale, d_beta, act);
+    SHPL_LAUNCH_CHECK();
+    return SHPL_OK;
+}
+
+namespace {
+int bn_bwd_blocks(int64_t rows) {
+    int64_t nb = (rows + 4095) / 4096;
+    if (nb < 1) nb = 1;
+    if (nb > 1024) nb = 1024;
+    return (int)nb;
+}
+}  // namespace
+
+extern "C" int shpl_batch_norm_backward_workspace_bytes(int64_t rows, int64_t c, size_t *bytes) {
+    if (!bytes || rows < 0 || c < 1) return SHPL_ERR_ARG;
+    *bytes = align_up((size_t)bn_bwd_blocks(rows) * 2 * c * sizeof(double), 256) + align_up(2 * c * sizeof(float), 256);
+    return SHPL_OK;
+}
+
+extern "C" int shpl_batch_norm_backward(int dtype, int64_t rows, const void *d_y, const void *d_raw,
+                                        const void *d_gy, int64_t stride, int64_t c, const float *d_mean,
+                                        const float *d_scale, const float *d_gamma, int act, int training,
+                                        void *d_graw, float *d_dbeta, float *d_dgamma, void *d_ws, size_t ws_bytes,
+                                        void *stream) {
+    if (dtype != SHPL_F32 && dtype != SHPL_BF16) return SHPL_ERR_ARG;
+    if (rows < 0 || c < 1 || stride < c || c > (1 << 16)) return SHPL_ERR_BAD_SHAPE;
+    if (act != 0 && act != 1) return SHPL_ERR_ARG;
+    size_t need;
+    shpl_batch_norm_backward_workspace_bytes(rows, c, &need);
+    if (!d_ws || ws_bytes < need) return SHPL_ERR_WORKSPACE;
+    if (rows > 0 && (!d_gy || !d_graw || (act == 1 && !d_y) || (training && !d_raw))) return SHPL_ERR_ARG;
+    if (rows == 0) return SHPL_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const int nb = bn_bwd_blocks(rows);
+    const int64_t rpb = (rows + nb - 1) / nb;
+    double *part = reinterpret_cast<double *>(d_ws);
+    float *mt = reinterpret_cast<float *>((uint8_t *)d_ws + align_up((size_t)nb * 2 * c * sizeof(double), 256));
+    const int grid = grid_for(rows * c, SHPL_BLOCK, 1 << 16);
+    // the sums need xhat only for dgamma: without raw (inference) they use raw := y's input... pass raw or y
+    const void *rw = d_raw ? d_raw : d_gy;
+    if (dtype == SHPL_F32) {
+        const float *y = (const float *)d_y, *r = (const float *)rw, *g = (const float *)d_gy;
+        hipLaunchKernelGGL(k_bn_bwd_partial<float>, dim3(nb), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride, (int)c,
+                           d_mean, d_scale, d_gamma, act, rpb, part);
+        SHPL_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(grid_for(c, SHPL_BLOCK, 256)), dim3(SHPL_BLOCK), 0, s, part, nb,
+                           (int)c, (double)rows, d_dbeta, d_raw ? d_dgamma : nullptr, mt);
+        SHPL_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_bn_bwd_apply<float>, dim3(grid), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride, (int)c,
+                           d_mean, d_scale, d_gamma, act, training, mt, (float *)d_graw);
+    } else {
+        const uint16_t *y = (const uint16_t *)d_y, *r = (const uint16_t *)rw, *g = (const uint16_t *)d_gy;
+        hipLaunchKernelGGL(k_bn_bwd_partial<uint16_t>, dim3(nb), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride,
+                           (int)c, d_mean, d_scale, d_gamma, act, rpb, part);
+        SHPL_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(grid_for(c, SHPL_BLOCK, 256)), dim3(SHPL_BLOCK), 0, s, part, nb,
+                           (int)c, (double)rows, d_dbeta, d_raw ? d_dgamma : nullptr, mt);
+        SHPL_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_bn_bwd_apply<uint16_t>, dim3(grid), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride,
+                           (int)c, d_mean, d_scale, d_gamma, act, training, mt, (uint16_t *)d_graw);
+    }
+    SHPL_LAUNCH_CHECK();
+    return SHPL_OK;
+}
+
+extern "C" int shpl_conv3x3_dgrad(int dtype, int n_frames, int64_t h, int64_t w, const void *d_gy, int64_t gy_stride,
+                                  int64_t c_gy, const void *d_weights, int64_t c_dx, void *d_dx, int64_t dx_stride,
+                                  void *d_ws, size_t ws_bytes, void *stream) {
+    ConvPlan pl;
+    int rc = conv_plan(dtype, n_frames, h, w, c_gy, 0, c_dx, false, false, &pl);
+    if (rc) return rc;
+    if (!d_weights || (ws_bytes > 0 && !d_ws)) return SHPL_ERR_ARG;
+    if (ws_bytes < pl.total) return SHPL_ERR_WORKSPACE;
+    if (gy_stride < c_gy || dx_stride < c_dx) return SHPL_ERR_BAD_SHAPE;
+    if (pl.n_tiles == 0) return SHPL_OK;
+    if (!d_gy || !d_dx) return SHPL_ERR_ARG;
+    const int esz = dtype == SHPL_F32 ? 4 : 2, he = 16 / esz;
+    ConvArgs a = {};
+    a.n_frames = n_frames;
+    a.h = (int)h;
+    a.w = (int)w;
+    a.tiles_x = pl.tiles_x;
+    a.tiles_per_frame = pl.tiles_per_frame;
+    a.n_tiles = (int)pl.n_tiles;
+    a.a = d_gy;
+    a.a_stride = gy_stride;
+    a.a_off = 0;
+    a.c_a = (int)c_gy;
+    a.qa = pl.qa;
+    a.vec_a = aligned16(d_gy) && gy_stride % he == 0;
+    a.wp = d_ws;
+    a.act = 0;
+    a.out = d_dx;
+    a.out_stride = dx_stride;
+    a.c_out = (int)c_dx;
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == SHPL_F32) return conv_launch<float>(pl, a, false, false, d_weights, nullptr, nullptr, s, 1);
+    return conv_launch<uint16_t>(pl, a, false, false, d_weights, nullptr, nullptr, s, 1);
+}
+
+namespace {
+struct WgPlan {
+    ConvPlan cp;
+    int n_cib, n_groups, tiles_per_group;
+    size_t rp_bytes, part_bytes, total;
+};
+
+int wgrad_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_t c_b, int64_t c_out, bool pooled,
+               WgPlan *wp) {
+    int rc = conv_plan(dtype, n_frames, h, w, c_a, c_b, c_out, pooled, false, &wp->cp);
+    if (rc) return rc;
+    const int Q = wp->cp.qa + wp->cp.qb;
+    wp->n_cib = (Q * wp->cp.ck + 31) / 32;
+    const int64_t blocks_per_group = (int64_t)wp->n_cib * wp->cp.n_cob;
+    int64_t ng = 512 / blocks_per_group;
+    if (ng < 1) ng = 1;
+    if (ng > wp->cp.n_tiles) ng = wp->cp.n_tiles > 0 ? wp->cp.n_tiles : 1;
+    wp->tiles_per_group = (int)((wp->cp.n_tiles + ng - 1) / ng);
+    if (wp->tiles_per_group < 1) wp->tiles_per_group = 1;
+    wp->n_groups = (int)((wp->cp.n_tiles + wp->tiles_per_group - 1) / wp->tiles_per_group);
+    if (wp->n_groups < 1) wp->n_groups = 1;
+    wp->rp_bytes = wp->cp.rp_bytes;
+    wp->part_bytes = align_up((size_t)wp->n_groups * blocks_per_group * 9 * NCO * NCO * sizeof(float), 256);
+    wp->total = wp->rp_bytes + wp->part_bytes;
+    return SHPL_OK;
+}
+}  // namespace
+
+extern "C" int shpl_conv3x3_wgrad_workspace_bytes(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a,
+                                                  int64_t c_b, int64_t c_out, int pooled, size_t *bytes) {
+    if (!bytes) return SHPL_ERR_ARG;
+    WgPlan wp;
+    const int rc = wgrad_plan(dtype, n_frames, h, w, c_a, c_b, c_out, pooled != 0, &wp);
+    if (rc) return rc;
+    *bytes = wp.total;
+    return SHPL_OK;
+}
+
+extern "C" int shpl_conv3x3_wgrad(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a, int64_t a_stride,
+                                  int64_t a_off, int64_t c_a, const void *d_b, int64_t b_stride, int64_t b_off,
+                                  int64_t c_b, const shpl_csr *pool, const int64_t *d_frame_off, const void *d_gy,
+                                  int64_t gy_stride, int64_t c_out, float *d_dw, void *d_ws, size_t ws_bytes,
+                                  void *stream) {
+    const bool pooled = pool != nullptr;
+    WgPlan wp;
+    int rc = wgrad_plan(dtype, n_frames, h, w, c_a, c_b, c_out, pooled, &wp);
+    if (rc) return rc;
+    if (!d_dw || (ws_bytes > 0 && !d_ws)) return SHPL_ERR_ARG;
+    if (ws_bytes < wp.total) return SHPL_ERR_WORKSPACE;
+    if (a_stride < a_off + c_a || a_off < 0 || b_off < 0 || gy_stride < c_out) return SHPL_ERR_BAD_SHAPE;
+    if (c_b > 0 && b_stride < b_off + c_b) return SHPL_ERR_BAD_SHAPE;
+    if (pooled) {
+        if (!d_frame_off || c_b < 1 || !d_b) return SHPL_ERR_ARG;
+        if (pool->n_keys != (int64_t)n_frames * h * w) return SHPL_ERR_BAD_SHAPE;
+        if (pool->nnz_cap > 0 && (!pool->ent_dst || !pool->ent_src || !pool->ent_val)) return SHPL_ERR_ARG;
+    } else if (c_b > 0 && !d_b) {
+        return SHPL_ERR_ARG;
+    }
+    if ((c_a > 0 && !d_a) || !d_gy) return SHPL_ERR_ARG;
+    const ConvPlan &pl = wp.cp;
+    const int esz = dtype == SHPL_F32 ? 4 : 2, he = 16 / esz;
+    hipStream_t s = (hipStream_t)stream;
+    if (pl.n_tiles == 0) {  // no pixels: dW = 0
+        SHPL_HIP_CHECK(hipMemsetAsync(d_dw, 0, sizeof(float) * 9 * (size_t)(c_a + c_b) * c_out, s));
+        return SHPL_OK;
+    }
+    ConvArgs a = {};
+    a.n_frames = n_frames;
+    a.h = (int)h;
+    a.w = (int)w;
+    a.tiles_x = pl.tiles_x;
+    a.tiles_per_frame = pl.tiles_per_frame;
+    a.n_tiles = (int)pl.n_tiles;
+    a.a = d_a;
+    a.a_stride = a_stride;
+    a.a_off = a_off;
+    a.c_a = (int)c_a;
+    a.qa = pl.qa;
+    a.b = d_b;
+    a.b_stride = b_stride;
+    a.b_off = b_off;
+    a.c_b = (int)c_b;
+    a.qb = pl.qb;
+    a.vec_a = aligned16(d_a) && a_stride % he == 0 && a_off % he == 0;
+    a.vec_b = aligned16(d_b) && b_stride % he == 0 && b_off % he == 0;
+    a.ent_dst = pooled ? pool->ent_dst : nullptr;
+    a.ent_src = pooled ? pool->ent_src : nullptr;
+    a.ent_val = pooled ? pool->ent_val : nullptr;
+    uint8_t *ws = reinterpret_cast<uint8_t *>(d_ws);
+    a.row_ptr = pooled ? reinterpret_cast<const int32_t *>(ws) : nullptr;
+    a.c_out = (int)c_out;
+    WgArgs g;
+    g.gy = d_gy;
+    g.gy_stride = gy_stride;
+    g.n_cib = wp.n_cib;
+    g.n_cob = pl.n_cob;
+    g.tiles_per_group = wp.tiles_per_group;
+    g.part = reinterpret_cast<float *>(ws + wp.rp_bytes);
+    if (pooled) {
+        hipLaunchKernelGGL(k_row_ptr, dim3(16, n_frames), dim3(SHPL_BLOCK), 0, s, a.ent_dst, d_frame_off, a.h, a.w,
+                           const_cast<int32_t *>(a.row_ptr));
+        SHPL_LAUNCH_CHECK();
+    }
+    const dim3 grid((unsigned)wp.n_groups, (unsigned)wp.n_cib, (unsigned)pl.n_cob);
+    if (dtype == SHPL_F32) {
+        if (pooled)
+            hipLaunchKernelGGL((k_conv3x3_wgrad<float, true>), grid, dim3(CONV_BLOCK), 0, s, a, g);
+        else
+            hipLaunchKernelGGL((k_conv3x3_wgrad<float, false>), grid, dim3(CONV_BLOCK), 0, s, a, g);
+    } else {
+        if (pooled)
+            hipLaunchKernelGGL((k_conv3x3_wgrad<uint16_t, true>), grid, dim3(CONV_BLOCK), 0, s, a, g);
+        else
+            hipLaunchKernelGGL((k_conv3x3_wgrad<uint16_t, false>), grid, dim3(CONV_BLOCK), 0, s, a, g);
+    }
+    SHPL_LAUNCH_CHECK();
+    const int64_t n_out = 9 * (c_a + c_b) * c_out;
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3(grid_for(n_out, SHPL_BLOCK, 1024)), dim3(SHPL_BLOCK), 0, s, g.part,
+                       wp.n_groups, wp.n_cib, pl.n_cob, (int)c_a, (int)c_b, pl.qa, pl.ck, (int)c_out, d_dw);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
 }

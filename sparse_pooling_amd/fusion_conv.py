@@ -20,7 +20,11 @@ averages with the Bessel-corrected variance).
 ``FusionConv.fused(bev, img, smap)`` computes the BEV conv of
 [bev || pool(img)] straight from the img->BEV CSR (shpl_conv3x3 with a
 pool CSR): bv_fused never reaches HBM, and the result is bitwise the conv of
-the materialised map. Forward only: there is no autograd rule yet.
+the materialised map. The backward (TF autodiff of the same graph) runs on
+the device too: BatchNorm/ReLU backward, the input gradient (the same conv
+kernel on transposed weights) and the weight gradient (an MFMA reduction over
+pixels that recomputes the pooled channels from the CSR), then the SHPL pull
+that carries the pooled channels' gradient back to the image map.
 """
 from __future__ import annotations
 
@@ -30,6 +34,7 @@ import numpy as np
 import torch
 
 from . import _lib as L
+from . import shpl_map as sm
 
 
 def conv_ws_bytes(dtype, n_frames, h, w, c_a, c_b, c_out, pooled, stats):
@@ -82,16 +87,146 @@ def conv3x3(a, weights, b=None, pool=None, frame_off=None, center=None, scale=No
 
 
 def batch_norm_train(x, stats, count, eps=1e-3, gamma=None, beta=None, relu=True, moving_mean=None,
-                     moving_var=None, decay=0.999, batch_mean=None, batch_var=None):
-    """In-place FusedBatchNorm (is_training) of x [..., C] from conv3x3's stats."""
+                     moving_var=None, decay=0.999, batch_mean=None, batch_var=None, out=None, ws=None):
+    """FusedBatchNorm (is_training) of x [..., C] from conv3x3's stats into
+    ``out`` (None: in place). ``ws`` (2*C floats) receives the batch mean and
+    scale the backward needs."""
     C = int(x.shape[-1])
     rows = x.numel() // C
-    ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
-    L.check(L.lib().shpl_batch_norm(L.dtype_code(x), rows, L.ptr(x), C, C, L.ptr(stats), float(count), float(eps),
-                                    L.ptr(gamma), L.ptr(beta), L.ACT_RELU if relu else L.ACT_NONE,
+    if ws is None:
+        ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+    L.check(L.lib().shpl_batch_norm(L.dtype_code(x), rows, L.ptr(x), L.ptr(out), C, C, L.ptr(stats), float(count),
+                                    float(eps), L.ptr(gamma), L.ptr(beta), L.ACT_RELU if relu else L.ACT_NONE,
                                     L.ptr(moving_mean), L.ptr(moving_var), float(decay), L.ptr(batch_mean),
                                     L.ptr(batch_var), L.ptr(ws), L.stream_of(x.device)), "shpl_batch_norm")
-    return x
+    return x if out is None else out
+
+
+def batch_norm_backward(gy, y=None, raw=None, mean=None, scale=None, gamma=None, relu=True, training=True):
+    """(g_raw, dbeta, dgamma) of BatchNorm (+ ReLU) over [..., C]; mean / scale
+    None -> 0 / 1 (a conv bias: dbeta is the bias gradient)."""
+    C = int(gy.shape[-1])
+    rows = gy.numel() // C
+    out = torch.empty_like(gy)
+    dbeta = torch.empty(C, dtype=torch.float32, device=gy.device)
+    dgamma = torch.empty(C, dtype=torch.float32, device=gy.device)
+    nb = ctypes.c_size_t()
+    L.check(L.lib().shpl_batch_norm_backward_workspace_bytes(rows, C, ctypes.byref(nb)),
+            "shpl_batch_norm_backward_workspace_bytes")
+    ws = L.workspace(nb.value, gy.device)
+    L.check(L.lib().shpl_batch_norm_backward(L.dtype_code(gy), rows, L.ptr(y), L.ptr(raw), L.ptr(gy), C, C,
+                                             L.ptr(mean), L.ptr(scale), L.ptr(gamma),
+                                             L.ACT_RELU if relu else L.ACT_NONE, int(bool(training)), L.ptr(out),
+                                             L.ptr(dbeta), L.ptr(dgamma), L.ptr(ws), ws.numel(),
+                                             L.stream_of(gy.device)), "shpl_batch_norm_backward")
+    return out, dbeta, dgamma
+
+
+def conv3x3_dgrad(gy, weights, c_dx):
+    """Input gradient [B,H,W,c_dx] of the SAME 3x3 conv with HWIO ``weights``."""
+    gy = gy.contiguous()
+    B, H, W, Cg = (int(s) for s in gy.shape)
+    weights = weights.to(gy.dtype).contiguous()
+    dx = torch.empty((B, H, W, int(c_dx)), dtype=gy.dtype, device=gy.device)
+    ws = L.workspace(conv_ws_bytes(L.dtype_code(gy), B, H, W, Cg, 0, c_dx, False, False), gy.device)
+    L.check(L.lib().shpl_conv3x3_dgrad(L.dtype_code(gy), B, H, W, L.ptr(gy), Cg, Cg, L.ptr(weights), int(c_dx),
+                                       L.ptr(dx), int(c_dx), L.ptr(ws), ws.numel(), L.stream_of(gy.device)),
+            "shpl_conv3x3_dgrad")
+    return dx
+
+
+def conv3x3_wgrad(a, gy, b=None, pool=None, frame_off=None):
+    """Weight gradient (f32 HWIO [3,3,Ca+Cb,Cout]) of the SAME 3x3 conv of
+    [a || b] (b dense, or the image map pooled through ``pool``)."""
+    a = a.contiguous()
+    gy = gy.contiguous()
+    dt = L.dtype_code(a)
+    B, H, W, Ca = (int(s) for s in a.shape)
+    Cb = 0 if b is None else int(b.shape[-1])
+    if b is not None:
+        b = b.contiguous()
+    Cout = int(gy.shape[-1])
+    dw = torch.empty((3, 3, Ca + Cb, Cout), dtype=torch.float32, device=a.device)
+    nb = ctypes.c_size_t()
+    L.check(L.lib().shpl_conv3x3_wgrad_workspace_bytes(dt, B, H, W, Ca, Cb, Cout, int(pool is not None),
+                                                       ctypes.byref(nb)), "shpl_conv3x3_wgrad_workspace_bytes")
+    ws = L.workspace(nb.value, a.device)
+    L.check(L.lib().shpl_conv3x3_wgrad(dt, B, H, W, L.ptr(a), Ca, 0, Ca, L.ptr(b), Cb, 0, Cb,
+                                       None if pool is None else pool.ref(), L.ptr(frame_off), L.ptr(gy), Cout,
+                                       Cout, L.ptr(dw), L.ptr(ws), ws.numel(), L.stream_of(a.device)),
+            "shpl_conv3x3_wgrad")
+    return dw
+
+
+class _FusionConvFn(torch.autograd.Function):
+    """FusionConv forward + its TF-autodiff backward, all on the device.
+    Inputs: a [B,H,W,Ca]; b: a dense [B,H,W,Cb], or the image map pooled
+    through smap (pooled=True), or None; the conv weights; beta / bias."""
+
+    @staticmethod
+    def forward(ctx, a, b, weights, beta, bias, conv, smap, pooled, is_training, out):
+        a = a.contiguous()
+        b = None if b is None else b.contiguous()
+        B, H, W, Ca = (int(s) for s in a.shape)
+        Cb = 0 if b is None else int(b.shape[-1])
+        dt = L.dtype_code(a)
+        pool = smap.csr(L.BY_CELL, L.ORDER_ENTRY) if pooled else None
+        frame_off = smap.frame_off if pooled else None
+        train_bn = conv.batch_norm and is_training
+        ws = conv._ws_for((dt, B, H, W, Cb, pooled, train_bn),
+                          conv_ws_bytes(dt, B, H, W, Ca, Cb, conv.c_out, pooled, train_bn))
+        raw, mean, scale = None, None, None
+        if not train_bn:
+            center, scale, shift = conv._inference_epilogue()
+            mean = center
+            if not conv.batch_norm:
+                shift = bias
+            y = conv3x3(a, weights, b=b, pool=pool, frame_off=frame_off, center=center, scale=scale, shift=shift,
+                        relu=conv.relu, out=out, ws=ws)
+        else:
+            stats = torch.empty((2, conv.c_out), dtype=torch.float64, device=a.device)
+            raw = conv3x3(a, weights, b=b, pool=pool, frame_off=frame_off, relu=False, stats=stats, ws=ws)
+            bn_ws = torch.empty(2 * conv.c_out, dtype=torch.float32, device=a.device)
+            y = out if out is not None else torch.empty_like(raw)
+            batch_norm_train(raw, stats, B * H * W, eps=conv.eps, beta=beta, relu=conv.relu,
+                             moving_mean=conv.moving_mean, moving_var=conv.moving_var, decay=conv.decay, out=y,
+                             ws=bn_ws)
+            mean, scale = bn_ws[:conv.c_out], bn_ws[conv.c_out:]
+        ctx.conv, ctx.smap, ctx.pooled, ctx.train_bn = conv, smap, pooled, train_bn
+        ctx.shapes = (Ca, Cb)
+        ctx.save_for_backward(a, b, weights, y, raw, mean, scale)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        a, b, weights, y, raw, mean, scale = ctx.saved_tensors
+        conv, smap, pooled = ctx.conv, ctx.smap, ctx.pooled
+        Ca, Cb = ctx.shapes
+        gy = gy.contiguous().to(y.dtype)
+        if conv.batch_norm or conv.bias is not None or conv.relu:
+            g_raw, dbeta, _ = batch_norm_backward(
+                gy, y=y, raw=raw, mean=mean if (conv.batch_norm or ctx.train_bn) else None,
+                scale=scale if conv.batch_norm else None, relu=conv.relu, training=ctx.train_bn)
+        else:
+            g_raw, dbeta = gy, None
+        need_x = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        d_a = d_b = dw = None
+        if need_x:
+            dx = conv3x3_dgrad(g_raw, weights, Ca + Cb)
+            if ctx.needs_input_grad[0]:
+                d_a = dx[..., :Ca].contiguous()
+            if b is not None and ctx.needs_input_grad[1]:
+                if pooled:  # the pooled channels' gradient back to the image (a8's TF gradient)
+                    d_b = torch.empty(b.shape, dtype=dx.dtype, device=dx.device)
+                    sm.pull(smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, dx, Ca + Cb, Ca, Cb, d_b, Cb)
+                else:
+                    d_b = dx[..., Ca:].contiguous()
+        if ctx.needs_input_grad[2]:
+            dw = conv3x3_wgrad(a, g_raw, b=b, pool=smap.csr(L.BY_CELL, L.ORDER_ENTRY) if pooled else None,
+                               frame_off=smap.frame_off if pooled else None).to(weights.dtype)
+        d_beta = dbeta if (conv.batch_norm and ctx.needs_input_grad[3]) else None
+        d_bias = dbeta if (not conv.batch_norm and ctx.needs_input_grad[4]) else None
+        return d_a, d_b, dw, d_beta, d_bias, None, None, None, None, None
 
 
 class FusionConv:
@@ -145,16 +280,28 @@ class FusionConv:
         return batch_norm_train(y, stats, B * H * W, eps=self.eps, beta=self.beta, relu=self.relu,
                                 moving_mean=self.moving_mean, moving_var=self.moving_var, decay=self.decay)
 
+    def _grad_wanted(self, *tensors):
+        return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in
+                                               (*tensors, self.weights, self.beta, self.bias))
+
     def __call__(self, x, is_training=False, out=None):
         """The conv of a materialised map (bv_fused, img_fused, or img)."""
+        if self._grad_wanted(x):
+            return _FusionConvFn.apply(x, None, self.weights, self.beta, self.bias, self, None, False, is_training,
+                                       out)
         return self._run(x, None, None, None, is_training, out)
 
     def fused(self, bev, img, smap, is_training=False, out=None):
         """The conv of [bev || _sparse_pool_op(M, img)] without writing the
-        concat: ``smap`` is the ShplMap of the frames of ``bev``."""
+        concat: ``smap`` is the ShplMap of the frames of ``bev``. Differentiable
+        in bev, img, the weights and beta / bias."""
+        if self._grad_wanted(bev, img):
+            return _FusionConvFn.apply(bev, img, self.weights, self.beta, self.bias, self, smap, True, is_training,
+                                       out)
         return self.fused_csr(bev, img, smap.csr(L.BY_CELL, L.ORDER_ENTRY), smap.frame_off, is_training, out)
 
     def fused_csr(self, bev, img, csr, frame_off, is_training=False, out=None):
         """fused() over an already built cell-keyed CSR (``_lib.Csr``) and the
-        per-frame entry slots ``frame_off`` (FusedPipeline.csr / .frame_off)."""
+        per-frame entry slots ``frame_off`` (FusedPipeline.csr / .frame_off);
+        forward only."""
         return self._run(bev, img, csr, frame_off, is_training, out)

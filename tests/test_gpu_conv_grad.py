@@ -1,0 +1,175 @@
+"""Backward of the post-fusion conv (shpl_conv3x3_dgrad / _wgrad,
+shpl_batch_norm_backward, FusionConv autograd) vs the CPU oracle on MI355X.
+
+Tolerances as in test_gpu_conv.py: 1e-5 plus the f32 summation error of the
+products involved, 2^-19 * sum |a*b| for the 9*C-term dot products of the
+input gradient, 2^-16 * sum |x*g| for the weight gradient (a reduction over
+every pixel of the batch, summed in f32 per workgroup and in f64 across
+workgroups). The oracle (double sums) is cross-checked against torch's CPU
+autograd in tests/test_oracle_conv.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import shpl_oracle as orc
+from sparse_pooling_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+ACC = 2.0 ** -19
+ACC_W = 2.0 ** -16
+DEV = "cuda"
+
+
+def _np(t):
+    return t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t)
+
+
+def _t(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def _weights(cin, cout, seed):
+    rng = np.random.default_rng(seed)
+    lim = np.sqrt(6.0 / (9 * cin + 9 * cout))
+    return (3.0 * rng.uniform(-lim, lim, (3, 3, cin, cout))).astype(np.float32)
+
+
+def _check(got, ref, bound, what):
+    err = np.abs(_np(got).astype(np.float64) - ref)
+    assert (err <= bound).all(), (what, float(err.max()), float((err / bound).max()))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from sparse_pooling_amd import _lib as L
+    L.lib()
+    assert torch.cuda.is_available()
+
+
+@pytest.mark.parametrize("shape", [(2, 9, 35, 24, 33), (1, 16, 64, 64, 32), (1, 3, 5, 5, 7)])
+def test_dgrad_and_wgrad_dense(shape):
+    from sparse_pooling_amd import fusion_conv as fc
+    B, H, W, Cin, Cout = shape
+    x = synth.make_features((B, H, W, Cin), 1)
+    w = _weights(Cin, Cout, 2)
+    g = synth.make_features((B, H, W, Cout), 3)
+    dx = fc.conv3x3_dgrad(_t(g), _t(w), Cin)
+    wt = np.ascontiguousarray(w[::-1, ::-1].transpose(0, 1, 3, 2))
+    _, ab = orc.conv3x3(np.abs(g), np.abs(wt), raw=True)
+    _check(dx, orc.conv3x3_dgrad(g, w), TOL + ACC * ab, "dx")
+    dw = fc.conv3x3_wgrad(_t(x), _t(g))
+    _check(dw, orc.conv3x3_wgrad(x, g), TOL + ACC_W * orc.conv3x3_wgrad(np.abs(x), np.abs(g)), "dw")
+
+
+def test_wgrad_two_sources_and_pooled():
+    """wgrad of [a || b] with b dense, and with b pooled from the CSR (the
+    pooled channels recomputed in the staging), == wgrad of the concat."""
+    from sparse_pooling_amd import fusion_conv as fc, pipeline, shpl_map as sm
+    spec = synth.CONFIGS[1]
+    frames = [synth.make_frame(spec, seed=700 + f, n_outside=10) for f in range(2)]
+    pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
+    ib = sm.build_index_batch(pts, vox, off, P, spec.im_size, spec.bv_size, spec.stride, maxp)
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    bev = synth.make_features((2, Hb, Wb, 16), 4)
+    img = synth.make_features((2, Hi, Wi, 12), 5)
+    g = synth.make_features((2, Hb, Wb, 40), 6)
+    bv = sm.pool_img_to_bev(ib.map, _t(img), (2, Hb, Wb, 16), bev=_t(bev))
+    x = _np(bv)
+    ref = orc.conv3x3_wgrad(x, g)
+    bound = TOL + ACC_W * orc.conv3x3_wgrad(np.abs(x), np.abs(g))
+    _check(fc.conv3x3_wgrad(_t(x), _t(g)), ref, bound, "concat")
+    _check(fc.conv3x3_wgrad(_t(bev), _t(g), b=_t(x[..., 16:])), ref, bound, "two dense")
+    pooled = fc.conv3x3_wgrad(_t(bev), _t(g), b=_t(img), pool=ib.map.csr(0, 0), frame_off=ib.map.frame_off)
+    _check(pooled, ref, bound, "pooled")
+
+
+@pytest.mark.parametrize("training", [True, False])
+def test_batch_norm_backward(training):
+    from sparse_pooling_amd import fusion_conv as fc
+    rng = np.random.default_rng(7)
+    raw = (rng.standard_normal((3, 11, 13, 40)) * 2.0 + 0.5).astype(np.float32)
+    g = rng.standard_normal(raw.shape).astype(np.float32)
+    beta = rng.standard_normal(40).astype(np.float32)
+    if training:
+        mean = raw.reshape(-1, 40).astype(np.float64).mean(0)
+        var = raw.reshape(-1, 40).astype(np.float64).var(0)
+    else:
+        mean = rng.standard_normal(40)
+        var = rng.uniform(0.5, 2.0, 40)
+    scale = (1.0 / np.sqrt(var + 1e-3)).astype(np.float32)
+    y = np.maximum((raw - mean) * scale + beta, 0.0).astype(np.float32)
+    gr, db, _ = fc.batch_norm_backward(_t(g), y=_t(y), raw=_t(raw), mean=_t(mean.astype(np.float32)),
+                                       scale=_t(scale), relu=True, training=training)
+    e_raw, e_db, _ = orc.batch_norm_backward(raw.astype(np.float64), g, training, mean, var, 1e-3, None, beta, True)
+    # values of order |scale * g|; the training form subtracts two O(1) means in f32
+    _check(gr, e_raw, 1e-5 + 1e-5 * np.abs(scale) * (np.abs(g) + 1.0), "g_raw")
+    _check(db, e_db, 1e-4 + 1e-6 * np.abs(g).reshape(-1, 40).sum(0), "dbeta")
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_fused_conv_autograd_vs_oracle(train):
+    """d(bev), d(img), d(weights), d(beta) of FusionConv.fused (pooling inside
+    the conv) against the oracle chain: pooled map -> conv -> BatchNorm ->
+    ReLU forward, and its TF gradients (BN / conv backward, then the
+    gradient of _sparse_pool_op for the image)."""
+    from sparse_pooling_amd import fusion_conv as fc, pipeline, shpl_map as sm
+    spec = synth.CONFIGS[1]
+    fr = synth.make_frame(spec, seed=900, n_outside=10)
+    gen = orc.gen_sparse_pooling_input_avod(fr.points, fr.voxel_indices, fr.P, list(spec.im_size),
+                                            tuple(spec.bv_size))
+    ref = orc.produce_sparse_pooling_input(gen, stride=spec.stride)
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    Cb, Ci = spec.c_bev, spec.c_img
+    bev = synth.make_features((1, Hb, Wb, Cb), 11)
+    img = synth.make_features((1, Hi, Wi, Ci), 12)
+    w = _weights(Cb + Ci, Ci, 13)
+    rng = np.random.default_rng(14)
+    beta = (0.1 * rng.standard_normal(Ci)).astype(np.float32)
+    mm = (0.1 * rng.standard_normal(Ci)).astype(np.float32)
+    mv = rng.uniform(0.5, 2.0, Ci).astype(np.float32)
+    g = rng.standard_normal((1, Hb, Wb, Ci)).astype(np.float32)
+    smap = sm.pack_map(_t(ref["Mij_pool"]), _t(ref["M_val"].astype(np.float32)), ref["M_size"],
+                       _t(ref["img_index_flip_pool"]), img.shape)
+    conv = fc.FusionConv(Cb + Ci, Ci, device=DEV)
+    conv.weights = _t(w).requires_grad_(True)
+    conv.beta = _t(beta).requires_grad_(True)
+    conv.moving_mean, conv.moving_var = _t(mm), _t(mv)
+    tb, ti = _t(bev).requires_grad_(True), _t(img).requires_grad_(True)
+    y = conv.fused(tb, ti, smap, is_training=train)
+    y.backward(_t(g))
+    # oracle chain
+    eb, _ = orc.sparse_pool_layer(bev, img, ref["Mij_pool"], ref["M_val"], ref["M_size"], ref["img_index_flip_pool"])
+    _, raw = orc.conv3x3(eb, w, raw=True)
+    mean = None if train else mm.astype(np.float64)
+    var = None if train else mv.astype(np.float64)
+    if train:
+        ey, _, bvar, _, _ = orc.batch_norm_train(raw, 1e-3, None, beta, True)
+        var_b = raw.reshape(-1, Ci).var(0)
+        scale = 1.0 / np.sqrt(var_b + 1e-3)
+    else:
+        scale = 1.0 / np.sqrt(mv.astype(np.float64) + 1e-3)
+        ey = np.maximum((raw - mm) * scale + beta, 0.0)
+    g_raw, e_db, _ = orc.batch_norm_backward(raw, g, train, mean, var, 1e-3, None, beta, True)
+    g_raw32 = g_raw.astype(np.float32)
+    d_bv = orc.conv3x3_dgrad(g_raw32, w).astype(np.float64)
+    d_img = orc.sparse_pool_grad_img(ref["Mij_pool"], ref["M_val"], ref["M_size"],
+                                     np.ascontiguousarray(d_bv[0, ..., Cb:].astype(np.float32)).reshape(-1, Ci),
+                                     ref["img_index_flip_pool"], img.shape)
+    d_w = orc.conv3x3_wgrad(eb, g_raw32)
+    _, ab_y = orc.conv3x3(np.abs(eb), np.abs(w), raw=True)
+    _check(y, ey, TOL + ACC * ab_y * np.abs(scale) + 1e-5 * np.abs(ey), "y")
+    # g_raw is within ~1e-5 relative of the oracle's; the products carry it
+    gr_mag = np.abs(g_raw) + 1e-3
+    wt = np.ascontiguousarray(w[::-1, ::-1].transpose(0, 1, 3, 2))
+    _, ab_dx = orc.conv3x3(gr_mag.astype(np.float32), np.abs(wt), raw=True)
+    _check(tb.grad, d_bv[..., :Cb], TOL + 2e-5 * ab_dx[..., :Cb], "d_bev")
+    # d_img sums several d_bv rows (TF order, f32) per pixel
+    _check(ti.grad, d_img, 1e-4 + 1e-4 * np.abs(d_img), "d_img")
+    _, ab_w = None, orc.conv3x3_wgrad(np.abs(eb), gr_mag.astype(np.float32))
+    _check(conv.weights.grad, d_w, TOL + 2e-5 * ab_w, "d_w")
+    _check(conv.beta.grad, e_db, 1e-4 + 1e-6 * np.abs(g).reshape(-1, Ci).sum(0), "d_beta")

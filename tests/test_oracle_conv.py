@@ -49,3 +49,27 @@ def test_oracle_batch_norm_training_matches_torch():
     np.testing.assert_allclose(emm, rm.numpy().astype(np.float32), rtol=1e-6, atol=1e-7)
     np.testing.assert_allclose(emv, rv.numpy().astype(np.float32), rtol=1e-6, atol=1e-7)
     np.testing.assert_allclose(bv, raw.reshape(-1, 6).var(0, ddof=1), rtol=1e-12)
+
+
+def test_oracle_conv_and_bn_backward_match_torch_autograd():
+    rng = np.random.default_rng(2)
+    B, H, W, Cin, Cout = 2, 5, 7, 6, 4
+    x = rng.standard_normal((B, H, W, Cin)).astype(np.float32)
+    w = rng.standard_normal((3, 3, Cin, Cout)).astype(np.float32)
+    g = rng.standard_normal((B, H, W, Cout)).astype(np.float32)
+    tx = torch.from_numpy(x).double().permute(0, 3, 1, 2).requires_grad_()
+    tw = torch.from_numpy(w).double().permute(3, 2, 0, 1).requires_grad_()
+    torch.nn.functional.conv2d(tx, tw, padding=1).backward(torch.from_numpy(g).double().permute(0, 3, 1, 2))
+    np.testing.assert_allclose(orc.conv3x3_dgrad(g, w), tx.grad.permute(0, 2, 3, 1).numpy(), rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(orc.conv3x3_wgrad(x, g), tw.grad.permute(2, 3, 1, 0).numpy(), rtol=1e-12, atol=1e-12)
+    raw = rng.standard_normal((B, H, W, Cout)) * 2 + 1
+    beta = rng.standard_normal(Cout).astype(np.float32)
+    t = torch.from_numpy(raw).permute(0, 3, 1, 2).requires_grad_()
+    tb = torch.from_numpy(beta).double().requires_grad_()
+    tg = torch.ones(Cout, dtype=torch.float64, requires_grad=True)
+    yy = torch.relu(torch.nn.functional.batch_norm(t, None, None, tg, tb, training=True, eps=1e-3))
+    yy.backward(torch.from_numpy(g).double().permute(0, 3, 1, 2))
+    dr, db, dg = orc.batch_norm_backward(raw, g, True, eps=1e-3, beta=beta)
+    np.testing.assert_allclose(dr, t.grad.permute(0, 2, 3, 1).numpy(), rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(db, tb.grad.numpy(), rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(dg, tg.grad.numpy(), rtol=1e-10, atol=1e-12)
