@@ -71,6 +71,9 @@ def parse():
                          "pooling fused into the conv (SURVEY §8f row 4)")
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"], help="conv workload storage dtype")
     ap.add_argument("--train-bn", action="store_true", help="conv workload: BatchNorm in training mode")
+    ap.add_argument("--train", action="store_true",
+                    help="conv workload: training step (batch-statistics BatchNorm forward + the whole backward: "
+                         "BN/ReLU, input and weight gradients of the conv, the pooled channels' gradient to the image)")
     ap.add_argument("--scan-points", type=int, default=120000, help="points per velodyne scan (frames)")
     return ap.parse_args()
 
@@ -489,6 +492,70 @@ def cpu_baseline_conv(spec, frames_np, budget_s):
                        f"{os.cpu_count()} host cpus visible")}
 
 
+def run_conv_train(args, world, rank, dev, spec, F, dtype, pl, pts, vox, off, P, bev, img, conv):
+    """Training step of the fused SHPL + post-fusion conv: index build, then
+    FusionConv.fused with batch-statistics BatchNorm, then its backward
+    (autograd over the device kernels): gradients of bev, img, the weights and
+    beta. Eager launches (autograd allocates per step)."""
+    from sparse_pooling_amd import dist as sd
+    Hb, Wb = spec.bev_feat_hw
+    cb, ci = spec.c_bev, spec.c_img
+    esz = 2 if dtype == torch.bfloat16 else 4
+    conv.weights.requires_grad_(True)
+    conv.beta.requires_grad_(True)
+    tb, ti = bev.clone().requires_grad_(True), img.clone().requires_grad_(True)
+    g = torch.Generator(device=dev)
+    g.manual_seed(99 + rank)
+    gy = torch.randn((F, Hb, Wb, ci), device=dev, generator=g).to(dtype)
+
+    def step(ev=None):
+        pl.build_index(pts, vox, off, P)
+        smap = pl.map()
+        for t in (tb, ti, conv.weights, conv.beta):
+            t.grad = None
+        if ev is not None:
+            ev[0].record()
+        y = conv.fused(tb, ti, smap, is_training=True)
+        if ev is not None:
+            ev[1].record()
+        y.backward(gy)
+        if ev is not None:
+            ev[2].record()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    elapsed = sd.timed(lambda k: step(), args.steps, device=dev)
+    n_ev = min(args.steps, 5)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(n_ev)]
+    for k in range(n_ev):
+        step(evs[k])
+    torch.cuda.synchronize()
+    fwd_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / n_ev
+    bwd_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / n_ev
+    flops = 3 * 2.0 * F * Hb * Wb * 9 * (cb + ci) * ci  # forward, input gradient, weight gradient
+    dname = "bf16" if esz == 2 else "f32"
+    tflops = flops / ((fwd_ms + bwd_ms) * 1e-3) / 1e12
+    if rank == 0:
+        print(json.dumps({
+            "metric": "SHPL + post-fusion conv training frames/sec (fwd + bwd), 1/2/4/8 GPU",
+            "value": round(F * world * args.steps / elapsed, 2), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dname,
+            "data": "synthetic (seeded KITTI-shaped frames, xavier-initialised conv weights)",
+            "config": {"workload": (f"conv training: config2 -> index -> conv3x3 {cb + ci}->{ci} + BatchNorm (batch "
+                                    "statistics) + ReLU of [bev || pool(img)] (pooling inside the conv), backward to "
+                                    "bev, img, weights, beta"),
+                       "frames_per_gpu_per_step": F, "hip_graph": False, "parallelism": f"frame-sharded x{world}"},
+            "roofline": {"bound": "mfma", "kernel": "fwd + input-gradient + weight-gradient convs (3x the forward flops) "
+                         "over the forward + backward time (BN, ReLU and the pooling gradient included)",
+                         "achieved": round(tflops, 2), "peak": MFMA_PEAK_TFS[dname], "unit": "TFLOP/s",
+                         "frac": round(tflops / MFMA_PEAK_TFS[dname], 4), "traffic": None,
+                         "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4)},
+            "cpu_baseline": None,
+        }), flush=True)
+
+
 def run_conv(args, world, rank, dev):
     """Config 2 + the post-fusion conv: index build -> cell CSR ->
     conv3x3(BN, ReLU) of [bev || pool(img)] with the pooling inside the conv's staging
@@ -513,6 +580,9 @@ def run_conv(args, world, rank, dev):
     out = torch.empty((F, Hb, Wb, ci), dtype=dtype, device=dev)
     out_unf = torch.empty_like(out)
     train = args.train_bn
+    if args.train:
+        run_conv_train(args, world, rank, dev, spec, F, dtype, pl, pts, vox, off, P, bev, img, conv)
+        return
 
     def step(ev=None):
         pl.build_index(pts, vox, off, P)

@@ -115,17 +115,6 @@ __device__ __forceinline__ int xcd_tile(int bid, int n) {
     return xcd < r ? xcd * (q + 1) + i : r * (q + 1) + (xcd - r) * q + i;
 }
 
-__device__ __forceinline__ int32_t lower_bound(const int32_t *v, int32_t lo, int32_t hi, int32_t key) {
-    while (lo < hi) {
-        const int32_t mid = lo + ((hi - lo) >> 1);
-        if ((uint32_t)v[mid] < (uint32_t)key)  // empty slots (-1) sort last
-            lo = mid + 1;
-        else
-            hi = mid;
-    }
-    return lo;
-}
-
 // Pooled vector of one occupied cell for the channels [c0, c0 + CK) of the
 // chunk: sum over the cell's run of CSR entries [e0, e1) of val * img[src],
 // in entry order with separate multiply and add from 0 -- the arithmetic of
@@ -166,27 +155,49 @@ struct HaloRuns {
 };
 
 // Lists the runs of the halo tile of output tile (f, y0, x0): per halo row
-// the entry range of cells [x0-1, x0+TW+1) (row pointers + binary search),
-// then one block scan in entry order. Every thread of the 256 calls it.
+// the entry range of cells [x0-1, x0+TW+1) (row pointers + counting the
+// row's sorted entries below each bound), then one block scan in entry
+// order. Every thread of the 256 calls it.
 __device__ int find_runs(const ConvArgs &p, int f, int y0, int x0, const HaloRuns &r) {
     constexpr int NPIX = HH * HWD;
     const int tid = threadIdx.x;
     const int H = p.h, W = p.w;
     const int64_t frame_row0 = (int64_t)f * H * W;
     for (int j = tid; j < NPIX; j += CONV_BLOCK) r.occ[j] = 0;
-    if (tid < HH) {
-        const int y = y0 - 1 + tid;
-        int32_t lo = 0, hi = 0;
-        if (y >= 0 && y < H) {
-            const int32_t ra = p.row_ptr[(int64_t)f * (H + 1) + y];
-            const int32_t rb = p.row_ptr[(int64_t)f * (H + 1) + y + 1];
-            const int32_t kl = (int32_t)(frame_row0 + (int64_t)y * W + (x0 > 0 ? x0 - 1 : 0));
-            const int32_t kh = (int32_t)(frame_row0 + (int64_t)y * W + (x0 + TW + 1 < W ? x0 + TW + 1 : W));
-            lo = lower_bound(p.ent_dst, ra, rb, kl);
-            hi = lower_bound(p.ent_dst, lo, rb, kh);
+    // wave w takes halo rows w, w+4, w+8; a row's sorted entries are counted
+    // 64 at a time against the two cell bounds (ballots), the rows' loads in
+    // flight together: two round trips for rows of up to 64 entries.
+    const int lane = tid & 63, wave = tid >> 6;
+    constexpr int RPW = (HH + 3) / 4;  // rows per wave
+    int32_t ra[RPW], rb[RPW], kl[RPW], kh[RPW];
+#pragma unroll
+    for (int u = 0; u < RPW; ++u) {
+        const int k = wave + 4 * u, y = y0 - 1 + k;
+        ra[u] = rb[u] = 0;
+        kl[u] = kh[u] = 0;
+        if (k < HH && y >= 0 && y < H) {
+            ra[u] = p.row_ptr[(int64_t)f * (H + 1) + y];
+            rb[u] = p.row_ptr[(int64_t)f * (H + 1) + y + 1];
+            kl[u] = (int32_t)(frame_row0 + (int64_t)y * W + (x0 > 0 ? x0 - 1 : 0));
+            kh[u] = (int32_t)(frame_row0 + (int64_t)y * W + (x0 + TW + 1 < W ? x0 + TW + 1 : W));
         }
-        r.lo[tid] = lo;
-        r.pre[tid + 1] = hi - lo;
+    }
+    int32_t d[RPW];
+#pragma unroll
+    for (int u = 0; u < RPW; ++u) d[u] = ra[u] + lane < rb[u] ? p.ent_dst[ra[u] + lane] : 0x7fffffff;
+#pragma unroll
+    for (int u = 0; u < RPW; ++u) {
+        const int k = wave + 4 * u;
+        int32_t n_lo = __popcll(__ballot(d[u] < kl[u])), n_hi = __popcll(__ballot(d[u] < kh[u]));
+        for (int32_t base = ra[u] + 64; base < rb[u] && n_hi == base - ra[u]; base += 64) {  // rows over 64 entries
+            const int32_t dd = base + lane < rb[u] ? p.ent_dst[base + lane] : 0x7fffffff;
+            n_lo += __popcll(__ballot(dd < kl[u]));
+            n_hi += __popcll(__ballot(dd < kh[u]));
+        }
+        if (lane == 0 && k < HH) {
+            r.lo[k] = ra[u] + n_lo;
+            r.pre[k + 1] = n_hi - n_lo;
+        }
     }
     __syncthreads();
     if (tid == 0) {
@@ -235,11 +246,11 @@ __device__ int find_runs(const ConvArgs &p, int f, int y0, int x0, const HaloRun
 // outside the map. Pooled chunks: zeros where no entry lands, each run's sum
 // elsewhere (disjoint cells: no barrier between the two). The caller
 // synchronises after.
-template <typename T, bool POOLED>
+template <typename T, bool POOLED, int PSTR = Elem<T>::PSTR>
 __device__ __forceinline__ void stage_halo(const ConvArgs &p, int q, int f, int y0, int x0, uint8_t *s_in,
                                            const HaloRuns &r, int n_run) {
     typedef Elem<T> E;
-    constexpr int CK = E::CK, HE = E::HE, NP = E::NP, PSTR = E::PSTR;
+    constexpr int CK = E::CK, HE = E::HE, NP = E::NP;
     constexpr int IN_PIECES = HH * HWD * NP;
     constexpr int IN_IT = (IN_PIECES + CONV_BLOCK - 1) / CONV_BLOCK;
     const int tid = threadIdx.x;
@@ -670,44 +681,57 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_apply(const T *y, const T
 // Weight gradient: dW[tap][ci][co] = sum over pixels p of x[p + tap offset][ci] * g[p][co].
 // One workgroup per (group of output tiles, 32 input channels, 32 output
 // channels): per tile it stages the input halo of its 32 channels (the
-// forward's stage_halo: the pooled channels are recomputed from the CSR, so
-// bv_fused need not exist) and the 8x32-pixel gradient tile (as f32), and
-// wave w accumulates the 9 taps over tile rows 2w, 2w+1 with
-// v_mfma_f32_32x32x2_f32 (M = input channel, N = output channel, K = pixel
-// pairs). The four waves' sums and then the groups' partials are added in a
-// fixed order (k_wgrad_reduce): deterministic.
-constexpr int WG_GSTR = NCO + 1;  // floats per pixel of the staged gradient tile
+// forward's stage_halo with unpadded 32-byte rows; the pooled channels are
+// recomputed from the CSR, so bv_fused need not exist) and the 8x32-pixel
+// gradient tile (f32, channel-major, 258-float rows: conflict-free reads),
+// and wave w accumulates the 9 taps over tile rows 2w, 2w+1 with
+// v_mfma_f32_16x16x4_f32 (M = 16 input channels, N = 16 output channels,
+// K = 4 pixels; 2 x 2 blocks per tap). ~76 KB of LDS (f32): two workgroups
+// per CU, so one stages while the other multiplies. (Measured: 32 channels
+// per workgroup with padded rows, one workgroup per CU, 3.3x the forward's
+// time; 16 channels per workgroup, 2x -- the gradient tile and the run list
+// were staged once per 16 channels.) The four waves' sums and then the
+// groups' partials are added in a fixed order (k_wgrad_reduce): deterministic.
+constexpr int WG_CI = 32;            // input channels per workgroup
+constexpr int WG_GPS = TH * TW + 2;  // floats per output channel of the staged gradient tile (258)
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 struct WgArgs {
     const void *gy;
     int64_t gy_stride;
     int n_cib, n_cob, tiles_per_group;
+    bool vec_g;
     float *part;  // [((group * n_cib + cib) * n_cob + cob)][9][32][32]
 };
 
 template <typename T, bool POOLED>
-__global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3_wgrad(const ConvArgs p, const WgArgs g) {
+__global__ __launch_bounds__(CONV_BLOCK, 2) void k_conv3x3_wgrad(const ConvArgs p, const WgArgs g) {
     typedef Elem<T> E;
-    constexpr int CK = E::CK, PSTR = E::PSTR, NQ = 32 / CK;
+    constexpr int CK = E::CK, HE = E::HE, CB = E::CB, NQ = WG_CI / CK;
     constexpr int NPIX = HH * HWD;
-    __shared__ __attribute__((aligned(16))) uint8_t s_x[NQ * NPIX * PSTR];
-    __shared__ float s_g[TH * TW * WG_GSTR];
+    __shared__ __attribute__((aligned(16))) uint8_t s_x[NQ * NPIX * CB];
+    __shared__ float s_g[NCO * WG_GPS];
     SHPL_HALO_RUNS_LDS(POOLED)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int pl = lane & 31, hf = lane >> 5;
+    const int l16 = lane & 15, kq = lane >> 4;
     const int grp = blockIdx.x, cib = blockIdx.y, cob = blockIdx.z;
     const int Q = p.qa + p.qb;
     const int H = p.h, W = p.w;
     const T *gy = reinterpret_cast<const T *>(g.gy);
-    f32x16 acc[9];
+    f32x4v acc[9][2][2];  // [tap][input-channel half][output-channel half]
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc[t][i] = 0.0f;
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int o = 0; o < 2; ++o) acc[t][h][o] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
     const int t0 = grp * g.tiles_per_group;
     const int t1 = t0 + g.tiles_per_group < p.n_tiles ? t0 + g.tiles_per_group : p.n_tiles;
-    // this lane's input channel: chunk ci / CK of the block, element ci % CK
-    const int a_off = (pl / CK) * NPIX * PSTR + (pl % CK) * (int)sizeof(T);
+    // this lane's input channels (rows of A): h*16 + l16 -> chunk (h*16 + l16) / CK, element % CK
+    int a_off[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) a_off[h] = ((h * 16 + l16) / CK) * NPIX * CB + ((h * 16 + l16) % CK) * (int)sizeof(T);
     for (int tile = t0; tile < t1; ++tile) {
         const int f = tile / p.tiles_per_frame;
         const int t_in = tile - f * p.tiles_per_frame;
@@ -718,41 +742,63 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3_wgrad(const ConvArgs p, 
 #pragma unroll
         for (int j = 0; j < NQ; ++j) {
             const int q = cib * NQ + j;
-            if (q < Q) stage_halo<T, POOLED>(p, q, f, y0, x0, s_x + j * NPIX * PSTR, runs, n_run);
+            if (q < Q) stage_halo<T, POOLED, CB>(p, q, f, y0, x0, s_x + j * NPIX * CB, runs, n_run);
         }
-        for (int i = tid; i < TH * TW * NCO; i += CONV_BLOCK) {
-            const int pix = i / NCO, col = i - pix * NCO;
-            const int y = y0 + pix / TW, x = x0 + (pix % TW), co = cob * NCO + col;
-            float v = 0.0f;
-            if (y < H && x < W && co < p.c_out) v = E::f(gy[(frame_row0 + (int64_t)y * W + x) * g.gy_stride + co]);
-            s_g[pix * WG_GSTR + col] = v;
+        // gradient tile -> [co][pixel] f32, 16-byte pieces of HE channels
+        for (int i = tid; i < TH * TW * (NCO / HE); i += CONV_BLOCK) {
+            const int pix = i / (NCO / HE), pc = i - pix * (NCO / HE);
+            const int y = y0 + pix / TW, x = x0 + (pix % TW), co0 = cob * NCO + pc * HE;
+            float v[HE];
+#pragma unroll
+            for (int k = 0; k < HE; ++k) v[k] = 0.0f;
+            if (y < H && x < W) {
+                const T *row = gy + (frame_row0 + (int64_t)y * W + x) * g.gy_stride;
+                const u32x4 raw = load_piece<T>(row, co0, p.c_out, g.vec_g);
+                T e[HE];
+                __builtin_memcpy(e, &raw, 16);
+#pragma unroll
+                for (int k = 0; k < HE; ++k) v[k] = E::f(e[k]);
+            }
+#pragma unroll
+            for (int k = 0; k < HE; ++k) s_g[(pc * HE + k) * WG_GPS + pix] = v[k];
         }
         __syncthreads();
-        for (int sp = 0; sp < TW; ++sp) {  // 32 pixel pairs of the wave's 64 pixels
-            const int pp = 2 * sp + hf;
+#pragma unroll 1
+        for (int sp = 0; sp < 16; ++sp) {  // 16 steps of 4 pixels over the wave's 64
+            const int pp = 4 * sp + kq;
             const int r = 2 * wave + (pp / TW), c = pp % TW;
-            const float bv = s_g[(r * TW + c) * WG_GSTR + pl];
+            float b[2];
+#pragma unroll
+            for (int o = 0; o < 2; ++o) b[o] = s_g[(o * 16 + l16) * WG_GPS + r * TW + c];
 #pragma unroll
             for (int t = 0; t < 9; ++t) {
                 const int hp = (r + t / 3) * HWD + c + t % 3;
-                const float av = E::f(*reinterpret_cast<const T *>(s_x + a_off + hp * PSTR));
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[t], 0, 0, 0);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const float av = E::f(*reinterpret_cast<const T *>(s_x + a_off[h] + hp * CB));
+#pragma unroll
+                    for (int o = 0; o < 2; ++o)
+                        acc[t][h][o] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b[o], acc[t][h][o], 0, 0, 0);
+                }
             }
         }
         __syncthreads();
     }
     // the four waves' sums, in wave order, into this workgroup's partial
+    // (D of 16x16x4: column = lane & 15 (output channel), row = 4 (lane >> 4) + reg (input channel))
     float *red = reinterpret_cast<float *>(s_x);  // 4 x 1024 floats
-    float *out = g.part + (((int64_t)grp * g.n_cib + cib) * g.n_cob + cob) * (9 * NCO * NCO);
+    float *out = g.part + (((int64_t)grp * g.n_cib + cib) * g.n_cob + cob) * (9 * WG_CI * NCO);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int ci = (i & 3) + 8 * (i >> 2) + 4 * hf;
-            red[wave * 1024 + ci * NCO + pl] = acc[t][i];
-        }
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int o = 0; o < 2; ++o)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    red[wave * 1024 + (h * 16 + 4 * kq + i) * NCO + o * 16 + l16] = acc[t][h][o][i];
         __syncthreads();
-        for (int e = tid; e < NCO * NCO; e += CONV_BLOCK)
+        for (int e = tid; e < WG_CI * NCO; e += CONV_BLOCK)
             out[t * 1024 + e] = __fadd_rn(__fadd_rn(__fadd_rn(red[e], red[1024 + e]), red[2048 + e]), red[3072 + e]);
         __syncthreads();
     }
@@ -770,11 +816,11 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_wgrad_reduce(const float *part, 
         const int ci = (int)((t / c_out) % cin);
         const int tap = (int)(t / ((int64_t)c_out * cin));
         const int cs = ci < c_a ? ci : qa * ck + (ci - c_a);  // channel in the chunk layout
-        const int cib = cs / 32, cil = cs % 32, cob = co / NCO, col = co % NCO;
+        const int cib = cs / WG_CI, cil = cs % WG_CI, cob = co / NCO, col = co % NCO;
         double sum = 0.0;
         for (int k = 0; k < n_groups; ++k)
-            sum += (double)part[(((int64_t)k * n_cib + cib) * n_cob + cob) * (9 * NCO * NCO) + tap * 1024 + cil * NCO +
-                                col];
+            sum += (double)part[(((int64_t)k * n_cib + cib) * n_cob + cob) * (9 * WG_CI * NCO) + tap * (WG_CI * NCO) +
+                                cil * NCO + col];
         dw[t] = (float)sum;
     }
 }
@@ -1057,9 +1103,9 @@ int wgrad_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64
     int rc = conv_plan(dtype, n_frames, h, w, c_a, c_b, c_out, pooled, false, &wp->cp);
     if (rc) return rc;
     const int Q = wp->cp.qa + wp->cp.qb;
-    wp->n_cib = (Q * wp->cp.ck + 31) / 32;
+    wp->n_cib = (Q * wp->cp.ck + WG_CI - 1) / WG_CI;
     const int64_t blocks_per_group = (int64_t)wp->n_cib * wp->cp.n_cob;
-    int64_t ng = 512 / blocks_per_group;
+    int64_t ng = 1024 / blocks_per_group;
     if (ng < 1) ng = 1;
     if (ng > wp->cp.n_tiles) ng = wp->cp.n_tiles > 0 ? wp->cp.n_tiles : 1;
     wp->tiles_per_group = (int)((wp->cp.n_tiles + ng - 1) / ng);
@@ -1067,7 +1113,7 @@ int wgrad_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64
     wp->n_groups = (int)((wp->cp.n_tiles + wp->tiles_per_group - 1) / wp->tiles_per_group);
     if (wp->n_groups < 1) wp->n_groups = 1;
     wp->rp_bytes = wp->cp.rp_bytes;
-    wp->part_bytes = align_up((size_t)wp->n_groups * blocks_per_group * 9 * NCO * NCO * sizeof(float), 256);
+    wp->part_bytes = align_up((size_t)wp->n_groups * blocks_per_group * 9 * WG_CI * NCO * sizeof(float), 256);
     wp->total = wp->rp_bytes + wp->part_bytes;
     return SHPL_OK;
 }
@@ -1142,6 +1188,7 @@ extern "C" int shpl_conv3x3_wgrad(int dtype, int n_frames, int64_t h, int64_t w,
     g.n_cib = wp.n_cib;
     g.n_cob = pl.n_cob;
     g.tiles_per_group = wp.tiles_per_group;
+    g.vec_g = aligned16(d_gy) && gy_stride % he == 0;
     g.part = reinterpret_cast<float *>(ws + wp.rp_bytes);
     if (pooled) {
         hipLaunchKernelGGL(k_row_ptr, dim3(16, n_frames), dim3(SHPL_BLOCK), 0, s, a.ent_dst, d_frame_off, a.h, a.w,

@@ -222,8 +222,15 @@ class _FusionConvFn(torch.autograd.Function):
                 else:
                     d_b = dx[..., Ca:].contiguous()
         if ctx.needs_input_grad[2]:
-            dw = conv3x3_wgrad(a, g_raw, b=b, pool=smap.csr(L.BY_CELL, L.ORDER_ENTRY) if pooled else None,
-                               frame_off=smap.frame_off if pooled else None).to(weights.dtype)
+            if pooled:
+                # the pooled channels once into HBM (shpl_pull): the dense two-source weight gradient
+                # runs at twice the waves per SIMD of the one that recomputes them per tile (257 vs
+                # 214 registers); conv3x3_wgrad(..., pool=...) stays the memory-lean form
+                xb = sm.pool_img_to_bev(smap, b, tuple(a.shape[:3]) + (Cb,))
+                dw = conv3x3_wgrad(a, g_raw, b=xb)
+            else:
+                dw = conv3x3_wgrad(a, g_raw, b=b)
+            dw = dw.to(weights.dtype)
         d_beta = dbeta if (conv.batch_norm and ctx.needs_input_grad[3]) else None
         d_bias = dbeta if (not conv.batch_norm and ctx.needs_input_grad[4]) else None
         return d_a, d_b, dw, d_beta, d_bias, None, None, None, None, None
