@@ -391,11 +391,15 @@ int shpl_batch_norm_backward(int dtype, int64_t rows, const void *d_y, const voi
 
 /* Input gradient: dx = conv3x3_SAME(gy, W') with W'[ky][kx][co][ci] =
  * W[2-ky][2-kx][ci][co], the forward conv kernel on transposed packed
- * weights. d_weights: the forward's HWIO [3][3][c_dx][c_gy]. Workspace:
+ * weights. d_weights: the forward's HWIO [3][3][c_dx][c_gy]. With d_dx_b
+ * set, channels [0, c_split) go to d_dx and [c_split, c_dx) to d_dx_b (the
+ * gradients of the conv's two sources, e.g. BEV and pooled image channels,
+ * as separate dense maps); with d_dx_b NULL, c_split is ignored. Workspace:
  * shpl_conv3x3_workspace_bytes(dtype, n_frames, h, w, c_gy, 0, c_dx, 0, 0). */
 int shpl_conv3x3_dgrad(int dtype, int n_frames, int64_t h, int64_t w, const void *d_gy, int64_t gy_stride,
                        int64_t c_gy, const void *d_weights, int64_t c_dx, void *d_dx, int64_t dx_stride,
-                       void *d_ws, size_t ws_bytes, void *stream);
+                       int64_t c_split, void *d_dx_b, int64_t dx_b_stride, void *d_ws, size_t ws_bytes,
+                       void *stream);
 
 /* Weight gradient: dw[ky][kx][ci][co] = sum over pixels of x[p + (ky-1, kx-1)][ci]
  * * gy[p][co], x given exactly as shpl_conv3x3's input (A channels, then B

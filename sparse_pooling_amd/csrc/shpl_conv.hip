@@ -92,6 +92,10 @@ struct ConvArgs {
     void *out;
     int64_t out_stride;
     int c_out;
+    // channels >= c_split go to out2 (channel co - c_split), when out2 is set
+    void *out2;
+    int64_t out2_stride;
+    int c_split;
     double *part;  // STATS: [(co_block*32 + co)*2 + stat][n_tiles]
 };
 
@@ -427,6 +431,13 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3(const ConvArgs p) {
         if (p.shift) sft = p.shift[co];
     }
     T *out = reinterpret_cast<T *>(p.out);
+    int64_t ostr = p.out_stride;
+    int oc = co;
+    if (p.out2 && co >= p.c_split) {
+        out = reinterpret_cast<T *>(p.out2);
+        ostr = p.out2_stride;
+        oc = co - p.c_split;
+    }
     float s1 = 0.0f, s2 = 0.0f;
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
@@ -444,7 +455,7 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3(const ConvArgs p) {
             if (p.scale) v = __fmul_rn(v, scl);
             if (p.shift) v = __fadd_rn(v, sft);
             if (p.act == 1) v = v > 0.0f ? v : 0.0f;
-            out[(frame_row0 + (int64_t)y * W + x) * p.out_stride + co] = E::back(v);
+            out[(frame_row0 + (int64_t)y * W + x) * ostr + oc] = E::back(v);
         }
     }
     if (STATS) {
@@ -583,6 +594,57 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_apply(const T *x, T *y, int64
     }
 }
 
+// 16-byte pieces of a row (VEC channels): the vector forms of the BatchNorm
+// streams, used when rows and channel counts are multiples of VEC and aligned.
+template <typename T, int VEC>
+struct Piece {
+    static __device__ __forceinline__ void load(const T *p, float (&x)[VEC]) {
+        const u32x4 r = *reinterpret_cast<const u32x4 *>(p);
+        T e[VEC];
+        __builtin_memcpy(e, &r, 16);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) x[k] = Elem<T>::f(e[k]);
+    }
+    static __device__ __forceinline__ void store(T *p, const float (&x)[VEC]) {
+        T e[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) e[k] = Elem<T>::back(x[k]);
+        u32x4 r;
+        __builtin_memcpy(&r, e, 16);
+        *reinterpret_cast<u32x4 *>(p) = r;
+    }
+};
+
+// Thread layout of the vector forms: c / VEC piece lanes (a power of two
+// dividing the block) times SHPL_BLOCK / (c / VEC) row lanes, so each thread
+// keeps one channel group and its per-channel coefficients in registers.
+template <typename T>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_bn_apply_vec(const T *x, T *y, int64_t rows, int64_t stride, int c,
+                                                             const float *mean, const float *scale, const float *beta,
+                                                             int act) {
+    constexpr int VEC = 16 / sizeof(T);
+    const int pr = c / VEC, rpb = SHPL_BLOCK / pr;
+    const int ch0 = (threadIdx.x % pr) * VEC;
+    float m[VEC], sc[VEC], b[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+        m[k] = mean[ch0 + k];
+        sc[k] = scale[ch0 + k];
+        b[k] = beta ? beta[ch0 + k] : 0.0f;
+    }
+    for (int64_t r = (int64_t)blockIdx.x * rpb + threadIdx.x / pr; r < rows; r += (int64_t)gridDim.x * rpb) {
+        float v[VEC];
+        Piece<T, VEC>::load(x + r * stride + ch0, v);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            float u = __fmul_rn(__fsub_rn(v[k], m[k]), sc[k]);
+            if (beta) u = __fadd_rn(u, b[k]);
+            v[k] = (act == 1 && !(u > 0.0f)) ? 0.0f : u;
+        }
+        Piece<T, VEC>::store(y + r * stride + ch0, v);
+    }
+}
+
 // ---------------------------------------------------------------- backward
 // BatchNorm (+ ReLU) backward. g_bn = g * [y > 0] (act), xhat = (raw - mean)
 // * scale / gamma; per-channel sums dbeta = sum g_bn, dgamma = sum g_bn xhat
@@ -637,6 +699,100 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_partial(const T *y, const
     }
 }
 
+// Vector form of k_bn_bwd_partial: thread (row lane rl, channel group cg)
+// reads VEC channels of every rl_n-th row; c / VEC a power of two <= 256.
+template <typename T>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_partial_vec(const T *y, const T *raw, const T *gy,
+                                                                   int64_t rows, int64_t stride, int c,
+                                                                   const float *mean, const float *scale,
+                                                                   const float *gamma, int act,
+                                                                   int64_t rows_per_block, double *part) {
+    constexpr int VEC = 16 / sizeof(T);
+    __shared__ double red[2][SHPL_BLOCK * VEC];
+    const int cg_n = c / VEC, rl_n = SHPL_BLOCK / cg_n;
+    const int rl = threadIdx.x / cg_n, cg = threadIdx.x % cg_n, ch0 = cg * VEC;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
+    float m[VEC], inv[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+        m[k] = mean ? mean[ch0 + k] : 0.0f;
+        inv[k] = scale ? __fdiv_rn(scale[ch0 + k], gamma ? gamma[ch0 + k] : 1.0f) : 1.0f;
+    }
+    double s1[VEC], s2[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) s1[k] = s2[k] = 0.0;
+    for (int64_t r = r0 + rl; r < r1; r += rl_n) {
+        const int64_t o = r * stride + ch0;
+        float gv[VEC], xv[VEC], yv[VEC];
+        Piece<T, VEC>::load(gy + o, gv);
+        Piece<T, VEC>::load(raw + o, xv);
+        if (act == 1) Piece<T, VEC>::load(y + o, yv);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const float gb = (act == 1 && !(yv[k] > 0.0f)) ? 0.0f : gv[k];
+            const float xh = __fmul_rn(__fsub_rn(xv[k], m[k]), inv[k]);
+            s1[k] += (double)gb;
+            s2[k] += (double)gb * (double)xh;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+        red[0][threadIdx.x * VEC + k] = s1[k];
+        red[1][threadIdx.x * VEC + k] = s2[k];
+    }
+    __syncthreads();
+    for (int ch = threadIdx.x; ch < c; ch += SHPL_BLOCK) {
+        const int g2 = ch / VEC, k = ch % VEC;
+        double a = 0.0, b = 0.0;
+        for (int q = 0; q < rl_n; ++q) {
+            a += red[0][(q * cg_n + g2) * VEC + k];
+            b += red[1][(q * cg_n + g2) * VEC + k];
+        }
+        part[((int64_t)blockIdx.x * 2 + 0) * c + ch] = a;
+        part[((int64_t)blockIdx.x * 2 + 1) * c + ch] = b;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_apply_vec(const T *y, const T *raw, const T *gy,
+                                                                 int64_t rows, int64_t stride, int c,
+                                                                 const float *mean, const float *scale,
+                                                                 const float *gamma, int act, int training,
+                                                                 const float *mean_terms, T *graw) {
+    constexpr int VEC = 16 / sizeof(T);
+    const int pr = c / VEC, rpb = SHPL_BLOCK / pr;
+    const int ch0 = (threadIdx.x % pr) * VEC;
+    float sc[VEC], m[VEC], inv[VEC], t0[VEC], t1[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+        const int ch = ch0 + k;
+        sc[k] = scale ? scale[ch] : 1.0f;
+        m[k] = mean ? mean[ch] : 0.0f;
+        inv[k] = __fdiv_rn(sc[k], gamma ? gamma[ch] : 1.0f);
+        t0[k] = training ? mean_terms[ch] : 0.0f;
+        t1[k] = training ? mean_terms[c + ch] : 0.0f;
+    }
+    for (int64_t r = (int64_t)blockIdx.x * rpb + threadIdx.x / pr; r < rows; r += (int64_t)gridDim.x * rpb) {
+        const int64_t o = r * stride + ch0;
+        float gv[VEC], yv[VEC], xv[VEC], out[VEC];
+        Piece<T, VEC>::load(gy + o, gv);
+        if (act == 1) Piece<T, VEC>::load(y + o, yv);
+        if (training) Piece<T, VEC>::load(raw + o, xv);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const float gb = (act == 1 && !(yv[k] > 0.0f)) ? 0.0f : gv[k];
+            if (training) {
+                const float xh = __fmul_rn(__fsub_rn(xv[k], m[k]), inv[k]);
+                out[k] = __fmul_rn(sc[k], __fsub_rn(__fsub_rn(gb, t0[k]), __fmul_rn(xh, t1[k])));
+            } else {
+                out[k] = __fmul_rn(sc[k], gb);
+            }
+        }
+        Piece<T, VEC>::store(graw + o, out);
+    }
+}
+
 __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_finalize(const double *part, int n_blocks, int c,
                                                                 double count, float *dbeta, float *dgamma,
                                                                 float *mean_terms) {
@@ -680,20 +836,23 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_apply(const T *y, const T
 
 // Weight gradient: dW[tap][ci][co] = sum over pixels p of x[p + tap offset][ci] * g[p][co].
 // One workgroup per (group of output tiles, 32 input channels, 32 output
-// channels): per tile it stages the input halo of its 32 channels (the
-// forward's stage_halo with unpadded 32-byte rows; the pooled channels are
-// recomputed from the CSR, so bv_fused need not exist) and the 8x32-pixel
-// gradient tile (f32, channel-major, 258-float rows: conflict-free reads),
-// and wave w accumulates the 9 taps over tile rows 2w, 2w+1 with
-// v_mfma_f32_16x16x4_f32 (M = 16 input channels, N = 16 output channels,
-// K = 4 pixels; 2 x 2 blocks per tap). ~76 KB of LDS (f32): two workgroups
-// per CU, so one stages while the other multiplies. (Measured: 32 channels
-// per workgroup with padded rows, one workgroup per CU, 3.3x the forward's
-// time; 16 channels per workgroup, 2x -- the gradient tile and the run list
-// were staged once per 16 channels.) The four waves' sums and then the
-// groups' partials are added in a fixed order (k_wgrad_reduce): deterministic.
-constexpr int WG_CI = 32;            // input channels per workgroup
-constexpr int WG_GPS = TH * TW + 2;  // floats per output channel of the staged gradient tile (258)
+// channels). Per tile it stages the input halo of its 32 channels ([chunk]
+// [pixel][32 B], unpadded) and the 8x32-pixel gradient tile ([pixel][32
+// channels], raw) in LDS -- dense sources by LDS-DMA, the whole tile in one
+// round trip; pooled channels recomputed from the CSR by stage_halo, so
+// bv_fused need not exist -- and wave w accumulates the 9 taps over tile
+// rows 2w, 2w+1 with v_mfma_f32_16x16x4_f32 (M = 16 input channels, N = 16
+// output channels, K = 4 pixels; 2 x 2 blocks per tap). Lane group kq walks
+// 16 consecutive pixels of one row, so the three kx taps of a (ky, channel)
+// are a sliding window: one new LDS read per (ky, channel half) per step.
+// ~76 KB of LDS (f32): two workgroups per CU, so one stages while the
+// other multiplies. The four waves' sums and then the groups' partials are
+// added in a fixed order (k_wgrad_reduce): deterministic. Measured and
+// dropped: 32 channels per workgroup with padded rows at one workgroup per
+// CU (3.3x the forward's time), 16 channels per workgroup (2x: the gradient
+// tile and the run list staged once per 16 channels), a register-staged
+// prefetch of the next tile's halo (2 %: 256 registers).
+constexpr int WG_CI = 32;  // input channels per workgroup
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
@@ -702,8 +861,86 @@ struct WgArgs {
     int64_t gy_stride;
     int n_cib, n_cob, tiles_per_group;
     bool vec_g;
+    bool whole;   // every 16-byte piece of A, B and gy lies inside its row: unmasked vector loads
     float *part;  // [((group * n_cib + cib) * n_cob + cob)][9][32][32]
 };
+
+// A 16-byte word of zeros in global memory: the LDS-DMA source of halo pieces
+// outside the map (an LDS-DMA writes what it reads; it cannot write zeros).
+__device__ u32x4 g_zero_piece;
+
+// Stages one tile's inputs of the weight gradient in LDS, as 16-byte pieces:
+// HALO: the 10x34 halo of the workgroup's WG_CI input channels (dense
+// sources), s_x [chunk][pixel][CB bytes]; always: the 8x32 gradient tile of
+// output channels [cob*32, cob*32+32), s_g [pixel][32 channels] raw. With
+// g.whole (every piece inside its row) each piece is one LDS-DMA
+// (global_load_lds_dwordx4: no registers, the whole tile in one round trip,
+// the destination lane-linear per wave); otherwise masked loads + ds_write.
+// The caller waits (vmcnt(0)) and synchronises.
+template <typename T, bool HALO>
+__device__ __forceinline__ void wg_stage(const ConvArgs &p, const WgArgs &g, int f, int y0, int x0, int cib, int cob,
+                                         uint8_t *s_x, uint8_t *s_g) {
+    typedef Elem<T> E;
+    constexpr int CK = E::CK, HE = E::HE, NP = E::NP, CB = E::CB, NQ = WG_CI / CK;
+    constexpr int NPIX = HH * HWD, IN_PIECES = NPIX * NP;
+    constexpr int GPP = NCO / HE, G_PIECES = TH * TW * GPP;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int H = p.h, W = p.w;
+    const int64_t frame_row0 = (int64_t)f * H * W;
+    const u32x4 *zero = &g_zero_piece;
+    const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+    if constexpr (HALO) {
+        const int Q = p.qa + p.qb;
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+            const int q = cib * NQ + j;
+            // chunks past the last (q >= Q) are zeros, addressed in a source that exists
+            const bool from_a = p.c_a > 0 && (q < p.qa || q >= Q);
+            const T *src = reinterpret_cast<const T *>(from_a ? p.a : p.b) + (from_a ? p.a_off : p.b_off);
+            const int64_t stride = from_a ? p.a_stride : p.b_stride;
+            const int c_src = from_a ? p.c_a : p.c_b;
+            const int c0 = (from_a ? q : q - p.qa) * CK;
+            const bool vec = from_a ? p.vec_a : p.vec_b;
+#pragma unroll
+            for (int u = 0; u < (IN_PIECES + CONV_BLOCK - 1) / CONV_BLOCK; ++u) {
+                const int base = u * CONV_BLOCK + wave * 64;  // the wave's first piece
+                if (base >= IN_PIECES) break;
+                const int jj = base + lane;
+                const int pix = jj / NP, hr = pix / HWD, hc = pix - hr * HWD;
+                const int y = y0 - 1 + hr, xx = x0 - 1 + hc;
+                const bool ok = q < Q && jj < IN_PIECES && y >= 0 && y < H && xx >= 0 && xx < W;
+                const int64_t row = frame_row0 + (int64_t)y * W + xx;
+                const int c = c0 + (jj % NP) * HE;
+                uint8_t *dst = s_x + j * NPIX * CB + base * 16;
+                if (jj < IN_PIECES) {
+                    if (g.whole)
+                        __builtin_amdgcn_global_load_lds(ok ? reinterpret_cast<const u32x4 *>(src + row * stride + c) : zero,
+                                                         dst, 16, 0, 0);
+                    else
+                        *reinterpret_cast<u32x4 *>(dst + lane * 16) = ok ? load_piece<T>(src + row * stride, c, c_src, vec) : z;
+                }
+            }
+        }
+    }
+    const T *gy = reinterpret_cast<const T *>(g.gy);
+#pragma unroll
+    for (int u = 0; u < G_PIECES / CONV_BLOCK; ++u) {
+        const int base = u * CONV_BLOCK + wave * 64;
+        const int i = base + lane;
+        const int pix = i / GPP, pc = i - pix * GPP;
+        const int y = y0 + pix / TW, xx = x0 + pix % TW;
+        const bool ok = y < H && xx < W;
+        const int64_t row = frame_row0 + (int64_t)y * W + xx;
+        const int c = cob * NCO + pc * HE;
+        uint8_t *dst = s_g + base * 16;
+        if (g.whole)
+            __builtin_amdgcn_global_load_lds(ok ? reinterpret_cast<const u32x4 *>(gy + row * g.gy_stride + c) : zero, dst,
+                                             16, 0, 0);
+        else
+            *reinterpret_cast<u32x4 *>(dst + lane * 16) = ok ? load_piece<T>(gy + row * g.gy_stride, c, p.c_out, g.vec_g) : z;
+    }
+    static_assert(G_PIECES % CONV_BLOCK == 0, "gradient pieces");
+}
 
 template <typename T, bool POOLED>
 __global__ __launch_bounds__(CONV_BLOCK, 2) void k_conv3x3_wgrad(const ConvArgs p, const WgArgs g) {
@@ -711,14 +948,12 @@ __global__ __launch_bounds__(CONV_BLOCK, 2) void k_conv3x3_wgrad(const ConvArgs 
     constexpr int CK = E::CK, HE = E::HE, CB = E::CB, NQ = WG_CI / CK;
     constexpr int NPIX = HH * HWD;
     __shared__ __attribute__((aligned(16))) uint8_t s_x[NQ * NPIX * CB];
-    __shared__ float s_g[NCO * WG_GPS];
+    __shared__ __attribute__((aligned(16))) uint8_t s_g[TH * TW * NCO * sizeof(T)];
     SHPL_HALO_RUNS_LDS(POOLED)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l16 = lane & 15, kq = lane >> 4;
     const int grp = blockIdx.x, cib = blockIdx.y, cob = blockIdx.z;
     const int Q = p.qa + p.qb;
-    const int H = p.h, W = p.w;
-    const T *gy = reinterpret_cast<const T *>(g.gy);
     f32x4v acc[9][2][2];  // [tap][input-channel half][output-channel half]
 #pragma unroll
     for (int t = 0; t < 9; ++t)
@@ -737,50 +972,58 @@ __global__ __launch_bounds__(CONV_BLOCK, 2) void k_conv3x3_wgrad(const ConvArgs 
         const int t_in = tile - f * p.tiles_per_frame;
         const int ty = t_in / p.tiles_x, tx = t_in - ty * p.tiles_x;
         const int y0 = ty * TH, x0 = tx * TW;
-        const int64_t frame_row0 = (int64_t)f * H * W;
-        const int n_run = POOLED ? find_runs(p, f, y0, x0, runs) : 0;
+        if constexpr (POOLED) {
+            const int n_run = find_runs(p, f, y0, x0, runs);
 #pragma unroll
-        for (int j = 0; j < NQ; ++j) {
-            const int q = cib * NQ + j;
-            if (q < Q) stage_halo<T, POOLED, CB>(p, q, f, y0, x0, s_x + j * NPIX * CB, runs, n_run);
-        }
-        // gradient tile -> [co][pixel] f32, 16-byte pieces of HE channels
-        for (int i = tid; i < TH * TW * (NCO / HE); i += CONV_BLOCK) {
-            const int pix = i / (NCO / HE), pc = i - pix * (NCO / HE);
-            const int y = y0 + pix / TW, x = x0 + (pix % TW), co0 = cob * NCO + pc * HE;
-            float v[HE];
-#pragma unroll
-            for (int k = 0; k < HE; ++k) v[k] = 0.0f;
-            if (y < H && x < W) {
-                const T *row = gy + (frame_row0 + (int64_t)y * W + x) * g.gy_stride;
-                const u32x4 raw = load_piece<T>(row, co0, p.c_out, g.vec_g);
-                T e[HE];
-                __builtin_memcpy(e, &raw, 16);
-#pragma unroll
-                for (int k = 0; k < HE; ++k) v[k] = E::f(e[k]);
+            for (int j = 0; j < NQ; ++j) {
+                const int q = cib * NQ + j;
+                if (q < Q) stage_halo<T, POOLED, CB>(p, q, f, y0, x0, s_x + j * NPIX * CB, runs, n_run);
             }
-#pragma unroll
-            for (int k = 0; k < HE; ++k) s_g[(pc * HE + k) * WG_GPS + pix] = v[k];
         }
+        wg_stage<T, !POOLED>(p, g, f, y0, x0, cib, cob, s_x, s_g);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMAs have landed
         __syncthreads();
-#pragma unroll 1
-        for (int sp = 0; sp < 16; ++sp) {  // 16 steps of 4 pixels over the wave's 64
-            const int pp = 4 * sp + kq;
-            const int r = 2 * wave + (pp / TW), c = pp % TW;
+        // lane group kq walks tile row 2w + (kq >> 1), columns (kq & 1) * 16 + sp, sp = 0..15: the
+        // three kx taps of a (ky, channel) are a sliding window over the halo row, so each
+        // step reads one new input value per (ky, channel half) instead of three
+        const int r = 2 * wave + (kq >> 1), cb = (kq & 1) * 16;
+        float win[3][2][3];  // [ky][h][kx]: x at halo (r + ky, cb + sp + kx), channel h*16 + l16
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int kx = 0; kx < 2; ++kx)
+                    win[ky][h][kx] = E::f(*reinterpret_cast<const T *>(s_x + a_off[h] + ((r + ky) * HWD + cb + kx) * CB));
+#pragma unroll 2
+        for (int sp = 0; sp < 16; ++sp) {
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    win[ky][h][2] =
+                        E::f(*reinterpret_cast<const T *>(s_x + a_off[h] + ((r + ky) * HWD + cb + sp + 2) * CB));
             float b[2];
 #pragma unroll
-            for (int o = 0; o < 2; ++o) b[o] = s_g[(o * 16 + l16) * WG_GPS + r * TW + c];
+            for (int o = 0; o < 2; ++o)
+                b[o] = E::f(reinterpret_cast<const T *>(s_g)[(r * TW + cb + sp) * NCO + o * 16 + l16]);
 #pragma unroll
-            for (int t = 0; t < 9; ++t) {
-                const int hp = (r + t / 3) * HWD + c + t % 3;
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+#pragma unroll
+                        for (int o = 0; o < 2; ++o)
+                            acc[ky * 3 + kx][h][o] =
+                                __builtin_amdgcn_mfma_f32_16x16x4f32(win[ky][h][kx], b[o], acc[ky * 3 + kx][h][o], 0, 0, 0);
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const float av = E::f(*reinterpret_cast<const T *>(s_x + a_off[h] + hp * CB));
-#pragma unroll
-                    for (int o = 0; o < 2; ++o)
-                        acc[t][h][o] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b[o], acc[t][h][o], 0, 0, 0);
+                    win[ky][h][0] = win[ky][h][1];
+                    win[ky][h][1] = win[ky][h][2];
                 }
-            }
         }
         __syncthreads();
     }
@@ -983,14 +1226,30 @@ extern "C" int shpl_batch_norm(int dtype, int64_t rows, void *d_x, void *d_y, in
                        scale, d_moving_mean, d_moving_var, decay, d_batch_mean, d_batch_var);
     SHPL_LAUNCH_CHECK();
     if (rows == 0) return SHPL_OK;
-    const int grid = grid_for(rows * c, SHPL_BLOCK, 1 << 16);
-    if (dtype == SHPL_F32)
-        hipLaunchKernelGGL(k_bn_apply<float>, dim3(grid), dim3(SHPL_BLOCK), 0, s, reinterpret_cast<const float *>(d_x),
-                           reinterpret_cast<float *>(d_y), rows, stride, (int)c, mean, scale, d_beta, act);
-    else
-        hipLaunchKernelGGL(k_bn_apply<uint16_t>, dim3(grid), dim3(SHPL_BLOCK), 0, s,
-                           reinterpret_cast<const uint16_t *>(d_x), reinterpret_cast<uint16_t *>(d_y), rows, stride,
-                           (int)c, mean, scale, d_beta, act);
+    const int vec = dtype == SHPL_F32 ? 4 : 8;
+    const int pr = (int)(c / vec);
+    const bool vform = c % vec == 0 && stride % vec == 0 && pr <= SHPL_BLOCK && (pr & (pr - 1)) == 0 &&
+                       aligned16(d_x) && aligned16(d_y);
+    const int grid = grid_for(rows * c / (vform ? vec : 1), SHPL_BLOCK, 1 << 16);
+    if (dtype == SHPL_F32) {
+        if (vform)
+            hipLaunchKernelGGL(k_bn_apply_vec<float>, dim3(grid), dim3(SHPL_BLOCK), 0, s,
+                               reinterpret_cast<const float *>(d_x), reinterpret_cast<float *>(d_y), rows, stride,
+                               (int)c, mean, scale, d_beta, act);
+        else
+            hipLaunchKernelGGL(k_bn_apply<float>, dim3(grid), dim3(SHPL_BLOCK), 0, s,
+                               reinterpret_cast<const float *>(d_x), reinterpret_cast<float *>(d_y), rows, stride,
+                               (int)c, mean, scale, d_beta, act);
+    } else {
+        if (vform)
+            hipLaunchKernelGGL(k_bn_apply_vec<uint16_t>, dim3(grid), dim3(SHPL_BLOCK), 0, s,
+                               reinterpret_cast<const uint16_t *>(d_x), reinterpret_cast<uint16_t *>(d_y), rows,
+                               stride, (int)c, mean, scale, d_beta, act);
+        else
+            hipLaunchKernelGGL(k_bn_apply<uint16_t>, dim3(grid), dim3(SHPL_BLOCK), 0, s,
+                               reinterpret_cast<const uint16_t *>(d_x), reinterpret_cast<uint16_t *>(d_y), rows,
+                               stride, (int)c, mean, scale, d_beta, act);
+    }
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
 }
@@ -1028,45 +1287,54 @@ extern "C" int shpl_batch_norm_backward(int dtype, int64_t rows, const void *d_y
     const int64_t rpb = (rows + nb - 1) / nb;
     double *part = reinterpret_cast<double *>(d_ws);
     float *mt = reinterpret_cast<float *>((uint8_t *)d_ws + align_up((size_t)nb * 2 * c * sizeof(double), 256));
-    const int grid = grid_for(rows * c, SHPL_BLOCK, 1 << 16);
-    // the sums need xhat only for dgamma: without raw (inference) they use raw := y's input... pass raw or y
+    // x-hat needs raw only in training (dgamma); otherwise any row-shaped input stands in
     const void *rw = d_raw ? d_raw : d_gy;
-    if (dtype == SHPL_F32) {
-        const float *y = (const float *)d_y, *r = (const float *)rw, *g = (const float *)d_gy;
-        hipLaunchKernelGGL(k_bn_bwd_partial<float>, dim3(nb), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride, (int)c,
-                           d_mean, d_scale, d_gamma, act, rpb, part);
-        SHPL_LAUNCH_CHECK();
+    const int vec = dtype == SHPL_F32 ? 4 : 8;
+    const int cg = (int)(c / vec);
+    const bool vform = c % vec == 0 && stride % vec == 0 && cg <= SHPL_BLOCK && (cg & (cg - 1)) == 0 &&
+                       aligned16(d_gy) && aligned16(rw) && aligned16(d_graw) && (act != 1 || aligned16(d_y));
+    const int grid = grid_for(rows * c / (vform ? vec : 1), SHPL_BLOCK, 1 << 16);
+    auto launch = [&](auto tag) {
+        typedef decltype(tag) T;
+        const T *y = (const T *)d_y, *r = (const T *)rw, *g = (const T *)d_gy;
+        if (vform)
+            hipLaunchKernelGGL(k_bn_bwd_partial_vec<T>, dim3(nb), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride,
+                               (int)c, d_mean, d_scale, d_gamma, act, rpb, part);
+        else
+            hipLaunchKernelGGL(k_bn_bwd_partial<T>, dim3(nb), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride, (int)c,
+                               d_mean, d_scale, d_gamma, act, rpb, part);
         hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(grid_for(c, SHPL_BLOCK, 256)), dim3(SHPL_BLOCK), 0, s, part, nb,
                            (int)c, (double)rows, d_dbeta, d_raw ? d_dgamma : nullptr, mt);
-        SHPL_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_bn_bwd_apply<float>, dim3(grid), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride, (int)c,
-                           d_mean, d_scale, d_gamma, act, training, mt, (float *)d_graw);
-    } else {
-        const uint16_t *y = (const uint16_t *)d_y, *r = (const uint16_t *)rw, *g = (const uint16_t *)d_gy;
-        hipLaunchKernelGGL(k_bn_bwd_partial<uint16_t>, dim3(nb), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride,
-                           (int)c, d_mean, d_scale, d_gamma, act, rpb, part);
-        SHPL_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(grid_for(c, SHPL_BLOCK, 256)), dim3(SHPL_BLOCK), 0, s, part, nb,
-                           (int)c, (double)rows, d_dbeta, d_raw ? d_dgamma : nullptr, mt);
-        SHPL_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_bn_bwd_apply<uint16_t>, dim3(grid), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride,
-                           (int)c, d_mean, d_scale, d_gamma, act, training, mt, (uint16_t *)d_graw);
-    }
+        if (vform)
+            hipLaunchKernelGGL(k_bn_bwd_apply_vec<T>, dim3(grid), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride,
+                               (int)c, d_mean, d_scale, d_gamma, act, training, mt, (T *)d_graw);
+        else
+            hipLaunchKernelGGL(k_bn_bwd_apply<T>, dim3(grid), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride, (int)c,
+                               d_mean, d_scale, d_gamma, act, training, mt, (T *)d_graw);
+    };
+    if (dtype == SHPL_F32)
+        launch(float());
+    else
+        launch(uint16_t());
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
 }
 
 extern "C" int shpl_conv3x3_dgrad(int dtype, int n_frames, int64_t h, int64_t w, const void *d_gy, int64_t gy_stride,
                                   int64_t c_gy, const void *d_weights, int64_t c_dx, void *d_dx, int64_t dx_stride,
-                                  void *d_ws, size_t ws_bytes, void *stream) {
+                                  int64_t c_split, void *d_dx_b, int64_t dx_b_stride, void *d_ws, size_t ws_bytes,
+                                  void *stream) {
     ConvPlan pl;
     int rc = conv_plan(dtype, n_frames, h, w, c_gy, 0, c_dx, false, false, &pl);
     if (rc) return rc;
     if (!d_weights || (ws_bytes > 0 && !d_ws)) return SHPL_ERR_ARG;
     if (ws_bytes < pl.total) return SHPL_ERR_WORKSPACE;
-    if (gy_stride < c_gy || dx_stride < c_dx) return SHPL_ERR_BAD_SHAPE;
+    if (!d_dx_b) c_split = c_dx;
+    if (c_split < 0 || c_split > c_dx) return SHPL_ERR_BAD_SHAPE;
+    if (gy_stride < c_gy || dx_stride < c_split || (d_dx_b && dx_b_stride < c_dx - c_split))
+        return SHPL_ERR_BAD_SHAPE;
     if (pl.n_tiles == 0) return SHPL_OK;
-    if (!d_gy || !d_dx) return SHPL_ERR_ARG;
+    if (!d_gy || (c_split > 0 && !d_dx)) return SHPL_ERR_ARG;
     const int esz = dtype == SHPL_F32 ? 4 : 2, he = 16 / esz;
     ConvArgs a = {};
     a.n_frames = n_frames;
@@ -1086,6 +1354,9 @@ extern "C" int shpl_conv3x3_dgrad(int dtype, int n_frames, int64_t h, int64_t w,
     a.out = d_dx;
     a.out_stride = dx_stride;
     a.c_out = (int)c_dx;
+    a.out2 = d_dx_b;
+    a.out2_stride = dx_b_stride;
+    a.c_split = (int)c_split;
     hipStream_t s = (hipStream_t)stream;
     if (dtype == SHPL_F32) return conv_launch<float>(pl, a, false, false, d_weights, nullptr, nullptr, s, 1);
     return conv_launch<uint16_t>(pl, a, false, false, d_weights, nullptr, nullptr, s, 1);
@@ -1189,6 +1460,8 @@ extern "C" int shpl_conv3x3_wgrad(int dtype, int n_frames, int64_t h, int64_t w,
     g.n_cob = pl.n_cob;
     g.tiles_per_group = wp.tiles_per_group;
     g.vec_g = aligned16(d_gy) && gy_stride % he == 0;
+    g.whole = (c_a == 0 || (a.vec_a && c_a % pl.ck == 0)) && (c_b == 0 || (a.vec_b && c_b % pl.ck == 0)) &&
+              g.vec_g && c_out % NCO == 0;
     g.part = reinterpret_cast<float *>(ws + wp.rp_bytes);
     if (pooled) {
         hipLaunchKernelGGL(k_row_ptr, dim3(16, n_frames), dim3(SHPL_BLOCK), 0, s, a.ent_dst, d_frame_off, a.h, a.w,

@@ -122,17 +122,23 @@ def batch_norm_backward(gy, y=None, raw=None, mean=None, scale=None, gamma=None,
     return out, dbeta, dgamma
 
 
-def conv3x3_dgrad(gy, weights, c_dx):
-    """Input gradient [B,H,W,c_dx] of the SAME 3x3 conv with HWIO ``weights``."""
+def conv3x3_dgrad(gy, weights, c_dx, split=None):
+    """Input gradient [B,H,W,c_dx] of the SAME 3x3 conv with HWIO ``weights``;
+    with ``split`` = c, the pair (channels [0, c), channels [c, c_dx)) as two
+    dense maps written by the kernel's epilogue (no slicing copies)."""
     gy = gy.contiguous()
     B, H, W, Cg = (int(s) for s in gy.shape)
     weights = weights.to(gy.dtype).contiguous()
-    dx = torch.empty((B, H, W, int(c_dx)), dtype=gy.dtype, device=gy.device)
+    c_dx = int(c_dx)
+    c0 = c_dx if split is None else int(split)
+    dx = torch.empty((B, H, W, c0), dtype=gy.dtype, device=gy.device)
+    dx_b = None if split is None else torch.empty((B, H, W, c_dx - c0), dtype=gy.dtype, device=gy.device)
     ws = L.workspace(conv_ws_bytes(L.dtype_code(gy), B, H, W, Cg, 0, c_dx, False, False), gy.device)
-    L.check(L.lib().shpl_conv3x3_dgrad(L.dtype_code(gy), B, H, W, L.ptr(gy), Cg, Cg, L.ptr(weights), int(c_dx),
-                                       L.ptr(dx), int(c_dx), L.ptr(ws), ws.numel(), L.stream_of(gy.device)),
+    L.check(L.lib().shpl_conv3x3_dgrad(L.dtype_code(gy), B, H, W, L.ptr(gy), Cg, Cg, L.ptr(weights), c_dx,
+                                       L.ptr(dx), max(c0, 1), c0, L.ptr(dx_b), max(c_dx - c0, 1), L.ptr(ws),
+                                       ws.numel(), L.stream_of(gy.device)),
             "shpl_conv3x3_dgrad")
-    return dx
+    return dx if split is None else (dx, dx_b)
 
 
 def conv3x3_wgrad(a, gy, b=None, pool=None, frame_off=None):
@@ -212,15 +218,18 @@ class _FusionConvFn(torch.autograd.Function):
         need_x = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         d_a = d_b = dw = None
         if need_x:
-            dx = conv3x3_dgrad(g_raw, weights, Ca + Cb)
-            if ctx.needs_input_grad[0]:
-                d_a = dx[..., :Ca].contiguous()
-            if b is not None and ctx.needs_input_grad[1]:
-                if pooled:  # the pooled channels' gradient back to the image (a8's TF gradient)
-                    d_b = torch.empty(b.shape, dtype=dx.dtype, device=dx.device)
-                    sm.pull(smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, dx, Ca + Cb, Ca, Cb, d_b, Cb)
-                else:
-                    d_b = dx[..., Ca:].contiguous()
+            if b is None:
+                d_a = conv3x3_dgrad(g_raw, weights, Ca)
+            else:  # the epilogue writes the two sources' gradients as separate dense maps
+                d_a, dx_b = conv3x3_dgrad(g_raw, weights, Ca + Cb, split=Ca)
+                if ctx.needs_input_grad[1]:
+                    if pooled:  # the pooled channels' gradient back to the image (a8's TF gradient)
+                        d_b = torch.empty(b.shape, dtype=dx_b.dtype, device=dx_b.device)
+                        sm.pull(smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, dx_b, Cb, 0, Cb, d_b, Cb)
+                    else:
+                        d_b = dx_b
+            if not ctx.needs_input_grad[0]:
+                d_a = None
         if ctx.needs_input_grad[2]:
             if pooled:
                 # the pooled channels once into HBM (shpl_pull): the dense two-source weight gradient

@@ -60,6 +60,11 @@ def test_dgrad_and_wgrad_dense(shape):
     wt = np.ascontiguousarray(w[::-1, ::-1].transpose(0, 1, 3, 2))
     _, ab = orc.conv3x3(np.abs(g), np.abs(wt), raw=True)
     _check(dx, orc.conv3x3_dgrad(g, w), TOL + ACC * ab, "dx")
+    # the two-output epilogue (the gradients of the conv's two sources) == one map, split
+    c = Cin // 3
+    da, db = fc.conv3x3_dgrad(_t(g), _t(w), Cin, split=c)
+    assert da.shape[-1] == c and db.shape[-1] == Cin - c
+    assert torch.equal(torch.cat([da, db], -1), dx)
     dw = fc.conv3x3_wgrad(_t(x), _t(g))
     _check(dw, orc.conv3x3_wgrad(x, g), TOL + ACC_W * orc.conv3x3_wgrad(np.abs(x), np.abs(g)), "dw")
 
