@@ -18,9 +18,9 @@
 // v_mfma_f32_32x32x16_bf16 for bf16 storage, f32 accumulation in both).
 // The input channels are walked in chunks (8 f32 / 16 bf16 channels): a
 // chunk of the 10 x 34 halo tile and the chunk's 9 x 32 weights are staged
-// in LDS (rows padded by 16 B: conflict-free ds_read_b128), then 9 taps of
-// MFMAs consume them. Staging is synchronous; 4-5 workgroups per CU keep
-// the MFMAs busy across each other's staging.
+// in LDS as 32-byte rows, unpadded and swizzled (conflict-free ds_read_b128)
+// by LDS-DMA, then 9 taps of MFMAs consume them. Staging is synchronous;
+// 5 workgroups per CU keep the MFMAs busy across each other's staging.
 //
 // Input channels [0, c_a) come from tensor A (the BEV map), [c_a, c_a+c_b)
 // from tensor B. B is either a dense tensor (the materialised pooled map, or
@@ -50,15 +50,13 @@ constexpr int W_ROWS = 9 * NCO;             // weight rows of a chunk (tap, out 
 // One chunk = the input channels staged per LDS round, 32 B per pixel: 8
 // f32 channels (4 f32 MFMAs of K=2 per tap) or 16 bf16 channels (one bf16
 // MFMA of K=16 per tap). 64 B bf16 chunks measured slower (fewer workgroups
-// per CU). LDS rows are padded by 16 B: ds_read_b128 of 16 consecutive
-// pixels then hits 16 distinct bank quads.
+// per CU).
 template <typename T>
 struct Elem {
     static constexpr int CB = 32;                        // chunk bytes per pixel
     static constexpr int CK = CB / sizeof(T);            // channels per chunk
     static constexpr int HE = 16 / sizeof(T);            // channels per 16-byte piece
     static constexpr int NP = CB / 16;                   // pieces per pixel
-    static constexpr int PSTR = CB + 16;                 // LDS row stride
     static __device__ __forceinline__ float f(T v) {
         if constexpr (sizeof(T) == 4)
             return v;
@@ -112,6 +110,41 @@ __device__ __forceinline__ u32x4 load_piece(const T *row, int c, int c_src, bool
     return r;
 }
 
+// A 16-byte word of zeros in global memory: the LDS-DMA source of pieces
+// outside the map (an LDS-DMA writes what it reads; it cannot write zeros).
+__device__ u32x4 g_zero_piece;
+
+// One LDS-DMA of 16 bytes per lane: lane l's piece lands at wave_dst + 16 l.
+__device__ __forceinline__ void dma16(const void *src, uint8_t *wave_dst) {
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const u32x4 *>(src), wave_dst, 16, 0, 0);
+}
+
+// Piece g (0/1) of LDS row `row` (32-byte rows: two 16-byte pieces). SWZ: the
+// unpadded, swizzled image the forward conv reads with ds_read_b128 -- slot
+// 2 row + (g ^ bit 3 of row): any 16 consecutive rows of one half fall on 16
+// distinct bank quads -- which an LDS-DMA can fill (its destination is
+// lane-linear; the swizzle goes on the source side). Otherwise rows of PSTR bytes.
+template <bool SWZ, int PSTR>
+__device__ __forceinline__ int piece_off(int row, int g) {
+    if constexpr (SWZ)
+        return (2 * row + (g ^ ((row >> 3) & 1))) * 16;
+    else
+        return row * PSTR + g * 16;
+}
+
+// The piece of channels [c, c + HE) of `row` (NULL: outside the map) into the
+// lane's LDS slot: an LDS-DMA when the piece is whole or all padding, a
+// masked load + ds_write when it straddles the channel count (or the rows are
+// not 16-byte aligned).
+template <typename T>
+__device__ __forceinline__ void piece_to_lds(const T *row, int c, int c_src, bool vec, uint8_t *wave_dst, int lane) {
+    constexpr int HE = Elem<T>::HE;
+    if (!row || c >= c_src || (vec && c + HE <= c_src))
+        dma16(row && c < c_src ? static_cast<const void *>(row + c) : &g_zero_piece, wave_dst);
+    else
+        *reinterpret_cast<u32x4 *>(wave_dst + lane * 16) = load_piece<T>(row, c, c_src, vec);
+}
+
 // blockIdx -> tile, so that each XCD (blocks b, b+8, ...) gets one contiguous
 // run of tiles: neighbouring tiles share halo rows through that XCD's L2.
 __device__ __forceinline__ int xcd_tile(int bid, int n) {
@@ -123,9 +156,9 @@ __device__ __forceinline__ int xcd_tile(int bid, int n) {
 // chunk: sum over the cell's run of CSR entries [e0, e1) of val * img[src],
 // in entry order with separate multiply and add from 0 -- the arithmetic of
 // k_sparse (shpl_pull.hip) -- written to the cell's LDS row.
-template <typename T>
+template <typename T, bool SWZ, int PSTR>
 __device__ __forceinline__ void pool_run(const ConvArgs &p, const T *img, int c0, int32_t e0, int32_t e1,
-                                         int32_t src0, float val0, uint8_t *dst) {
+                                         int32_t src0, float val0, uint8_t *s_base, int pix) {
     typedef Elem<T> E;
     constexpr int HE = E::HE;
     for (int g = 0; g < E::NP; ++g) {  // one 16-byte piece (4 f32 / 8 bf16 channels) at a time
@@ -144,7 +177,7 @@ __device__ __forceinline__ void pool_run(const ConvArgs &p, const T *img, int c0
         T o[HE];
 #pragma unroll
         for (int c = 0; c < HE; ++c) o[c] = E::back(sum[c]);
-        __builtin_memcpy(dst + g * 16, o, 16);
+        __builtin_memcpy(s_base + piece_off<SWZ, PSTR>(pix, g), o, 16);
     }
 }
 
@@ -246,11 +279,11 @@ __device__ int find_runs(const ConvArgs &p, int f, int y0, int x0, const HaloRun
 }
 
 // Stages input chunk q (channels of A, then of B) of the 10 x 34 halo of
-// output tile (f, y0, x0) into s_in ([pixel][chunk], PSTR-byte rows); zero
+// output tile (f, y0, x0) into s_in ([pixel][chunk] rows, piece_off); zero
 // outside the map. Pooled chunks: zeros where no entry lands, each run's sum
 // elsewhere (disjoint cells: no barrier between the two). The caller
 // synchronises after.
-template <typename T, bool POOLED, int PSTR = Elem<T>::PSTR>
+template <typename T, bool POOLED, int PSTR, bool SWZ = false>
 __device__ __forceinline__ void stage_halo(const ConvArgs &p, int q, int f, int y0, int x0, uint8_t *s_in,
                                            const HaloRuns &r, int n_run) {
     typedef Elem<T> E;
@@ -283,18 +316,18 @@ __device__ __forceinline__ void stage_halo(const ConvArgs &p, int q, int f, int 
 #pragma unroll
         for (int u = 0; u < IN_IT; ++u) {
             const int j = tid + u * CONV_BLOCK;
-            if (j < IN_PIECES) *reinterpret_cast<u32x4 *>(s_in + (j / NP) * PSTR + (j % NP) * 16) = v[u];
+            if (j < IN_PIECES) *reinterpret_cast<u32x4 *>(s_in + piece_off<SWZ, PSTR>(j / NP, j % NP)) = v[u];
         }
     } else {
 #pragma unroll
         for (int u = 0; u < IN_IT; ++u) {
             const int j = tid + u * CONV_BLOCK;
             if (j < IN_PIECES && !r.occ[j / NP])
-                *reinterpret_cast<u32x4 *>(s_in + (j / NP) * PSTR + (j % NP) * 16) = u32x4{0u, 0u, 0u, 0u};
+                *reinterpret_cast<u32x4 *>(s_in + piece_off<SWZ, PSTR>(j / NP, j % NP)) = u32x4{0u, 0u, 0u, 0u};
         }
         const T *img = reinterpret_cast<const T *>(p.b) + p.b_off;
         for (int k = tid; k < n_run; k += CONV_BLOCK)
-            pool_run<T>(p, img, (q - p.qa) * CK, r.e[k], r.end[k], r.src[k], r.val[k], s_in + r.pix[k] * PSTR);
+            pool_run<T, SWZ, PSTR>(p, img, (q - p.qa) * CK, r.e[k], r.end[k], r.src[k], r.val[k], s_in, r.pix[k]);
     }
 }
 
@@ -307,15 +340,59 @@ __device__ __forceinline__ void stage_halo(const ConvArgs &p, int q, int f, int 
     __shared__ int64_t s_scan[SHPL_BLOCK / 64 + 1];                                                          \
     const HaloRuns runs{s_lo, s_pre, s_run_pix, s_run_e, s_run_end, s_run_src, s_run_val, s_occ, s_scan};
 
-template <typename T, bool POOLED, bool STATS>
-__global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3(const ConvArgs p) {
+// Stages input chunk q of output tile (f, y0, x0) -- its 9x32 weight rows
+// and its 10x34 halo -- into one LDS buffer pair (swizzled 32-byte rows).
+// Weights and dense halo chunks are LDS-DMAs (lane k of the wave fills slot
+// k: it loads the piece the swizzle puts there); pooled chunks are computed
+// (stage_halo). The caller waits and synchronises.
+template <typename T, bool POOLED>
+__device__ __forceinline__ void conv_stage(const ConvArgs &p, int q, int f, int y0, int x0, const T *wq, uint8_t *s_in,
+                                           uint8_t *s_w, const HaloRuns &runs, int n_run) {
     typedef Elem<T> E;
-    constexpr int CK = E::CK, HE = E::HE, NP = E::NP, PSTR = E::PSTR;
-    constexpr int NPIX = HH * HWD;
-    constexpr int W_PIECES = W_ROWS * NP;
-    constexpr int W_IT = (W_PIECES + CONV_BLOCK - 1) / CONV_BLOCK;
-    __shared__ __attribute__((aligned(16))) uint8_t s_in[NPIX * PSTR];
-    __shared__ __attribute__((aligned(16))) uint8_t s_w[W_ROWS * PSTR];
+    constexpr int CK = E::CK, HE = E::HE, NP = E::NP;
+    constexpr int IN_PIECES = HH * HWD * NP, W_PIECES = W_ROWS * NP;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int u = 0; u < (W_PIECES + CONV_BLOCK - 1) / CONV_BLOCK; ++u) {
+        const int base = u * CONV_BLOCK + wave * 64;  // the wave's first slot
+        if (base >= W_PIECES) break;
+        const int k = base + lane, row = k >> 1, g = (k & 1) ^ ((row >> 3) & 1);
+        if (k < W_PIECES) dma16(wq + ((int64_t)q * W_ROWS + row) * CK + g * HE, s_w + base * 16);
+    }
+    if (!POOLED || q < p.qa) {
+        const int H = p.h, W = p.w;
+        const int64_t frame_row0 = (int64_t)f * H * W;
+        const bool from_a = q < p.qa;
+        const T *src = reinterpret_cast<const T *>(from_a ? p.a : p.b) + (from_a ? p.a_off : p.b_off);
+        const int64_t stride = from_a ? p.a_stride : p.b_stride;
+        const int c_src = from_a ? p.c_a : p.c_b;
+        const int c0 = (from_a ? q : q - p.qa) * CK;
+        const bool vec = from_a ? p.vec_a : p.vec_b;
+#pragma unroll
+        for (int u = 0; u < (IN_PIECES + CONV_BLOCK - 1) / CONV_BLOCK; ++u) {
+            const int base = u * CONV_BLOCK + wave * 64;
+            if (base >= IN_PIECES) break;
+            const int k = base + lane, pix = k >> 1, g = (k & 1) ^ ((pix >> 3) & 1);
+            const int hr = pix / HWD, hc = pix - hr * HWD;
+            const int y = y0 - 1 + hr, x = x0 - 1 + hc;
+            const bool ok = y >= 0 && y < H && x >= 0 && x < W;
+            if (k < IN_PIECES)
+                piece_to_lds<T>(ok ? src + (frame_row0 + (int64_t)y * W + x) * stride : nullptr, c0 + g * HE, c_src, vec,
+                                s_in + base * 16, lane);
+        }
+    } else {
+        stage_halo<T, true, E::CB, true>(p, q, f, y0, x0, s_in, runs, n_run);
+    }
+}
+
+template <typename T, bool POOLED, bool STATS>
+__global__ __launch_bounds__(CONV_BLOCK, 4) void k_conv3x3(const ConvArgs p) {
+    typedef Elem<T> E;
+    constexpr int CK = E::CK, NP = E::NP;
+    static_assert(NP == 2, "two 16-byte pieces per LDS row (the swizzle)");
+    constexpr int IN_BYTES = HH * HWD * NP * 16, W_BYTES = W_ROWS * NP * 16;
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[IN_BYTES];
+    __shared__ __attribute__((aligned(16))) uint8_t s_w[W_BYTES];
     __shared__ float s_red[4][2][NCO];
     SHPL_HALO_RUNS_LDS(POOLED)
 
@@ -341,64 +418,24 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3(const ConvArgs p) {
 
     const T *wq = reinterpret_cast<const T *>(p.wp) + (int64_t)cob * Q * W_ROWS * CK;
     for (int q = 0; q < Q; ++q) {
-        // ---- stage chunk q in LDS, synchronously: the other workgroups on the
-        // CU keep the MFMAs busy meanwhile (a register-staged prefetch of chunk
-        // q+1 cost more occupancy than it hid latency)
-        {
-            u32x4 v[W_IT];  // weights: 288 rows, contiguous in the packed array
-#pragma unroll
-            for (int u = 0; u < W_IT; ++u) {
-                const int j = tid + u * CONV_BLOCK;
-                if (j < W_PIECES) v[u] = *reinterpret_cast<const u32x4 *>(wq + ((int64_t)q * W_ROWS * NP + j) * HE);
-            }
-#pragma unroll
-            for (int u = 0; u < W_IT; ++u) {
-                const int j = tid + u * CONV_BLOCK;
-                if (j < W_PIECES) *reinterpret_cast<u32x4 *>(s_w + (j / NP) * PSTR + (j % NP) * 16) = v[u];
-            }
-        }
-        if constexpr (POOLED) {
-            stage_halo<T, POOLED>(p, q, f, y0, x0, s_in, runs, n_run);
-        } else {
-            // the dense form of stage_halo, written out: inlined through the
-            // helper it costs 16 more VGPRs here (5 -> 4 waves per SIMD)
-            constexpr int IN_PIECES = NPIX * NP;
-            constexpr int IN_IT = (IN_PIECES + CONV_BLOCK - 1) / CONV_BLOCK;
-            const bool from_a = q < p.qa;
-            const T *src = reinterpret_cast<const T *>(from_a ? p.a : p.b) + (from_a ? p.a_off : p.b_off);
-            const int64_t stride = from_a ? p.a_stride : p.b_stride;
-            const int c_src = from_a ? p.c_a : p.c_b;
-            const int c0 = (from_a ? q : q - p.qa) * CK;
-            const bool vec = from_a ? p.vec_a : p.vec_b;
-            u32x4 v[IN_IT];
-#pragma unroll
-            for (int u = 0; u < IN_IT; ++u) {
-                const int j = tid + u * CONV_BLOCK;
-                v[u] = u32x4{0u, 0u, 0u, 0u};
-                if (j < IN_PIECES) {
-                    const int pix = j / NP, hr = pix / HWD, hc = pix - hr * HWD;
-                    const int y = y0 - 1 + hr, x = x0 - 1 + hc;
-                    if (y >= 0 && y < H && x >= 0 && x < W)
-                        v[u] = load_piece<T>(src + (frame_row0 + (int64_t)y * W + x) * stride, c0 + (j % NP) * HE,
-                                             c_src, vec);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < IN_IT; ++u) {
-                const int j = tid + u * CONV_BLOCK;
-                if (j < IN_PIECES) *reinterpret_cast<u32x4 *>(s_in + (j / NP) * PSTR + (j % NP) * 16) = v[u];
-            }
-        }
+        // ---- stage chunk q, synchronously: the other workgroups on the CU (5
+        // at f32) keep the MFMAs busy meanwhile. Measured and dropped: two LDS
+        // buffers with chunk q+1's LDS-DMAs in flight under chunk q's MFMAs
+        // (3 workgroups per CU: f32 fused 11.3 -> 12.1 ms), and a register-staged
+        // prefetch (VGPRs 62 -> 86-168: 11.8 -> 12.5 ms)
+        conv_stage<T, POOLED>(p, q, f, y0, x0, wq, s_in, s_w, runs, n_run);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMAs have landed
         __syncthreads();
-        // ---- 9 taps of MFMA over the chunk
+        const uint8_t *si = s_in, *sw = s_w;
+        // ---- 9 taps of MFMA over chunk q
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky) {
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
-                const uint8_t *wrow = s_w + ((ky * 3 + kx) * NCO + pl) * PSTR + hf * 16;
+                const uint8_t *wrow = sw + piece_off<true, 0>((ky * 3 + kx) * NCO + pl, hf);
 #pragma unroll
                 for (int m = 0; m < 2; ++m) {
-                    const uint8_t *arow = s_in + ((2 * wave + m + ky) * HWD + pl + kx) * PSTR + hf * 16;
+                    const uint8_t *arow = si + piece_off<true, 0>((2 * wave + m + ky) * HWD + pl + kx, hf);
                     if constexpr (sizeof(T) == 4) {
                         // lane half h supplies channels 4h+s of the chunk to MFMA s (A and B alike)
                         const f32x4 a4 = *reinterpret_cast<const f32x4 *>(arow);
@@ -407,18 +444,15 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv3x3(const ConvArgs p) {
                         for (int s = 0; s < 4; ++s)
                             acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[s], b4[s], acc[m], 0, 0, 0);
                     } else {
-                        // k-step s covers channels 16s .. 16s+15; lane half h holds 16s+8h .. +7
-#pragma unroll
-                        for (int s = 0; s < NP / 2; ++s) {
-                            const bf16x8 a8 = *reinterpret_cast<const bf16x8 *>(arow + 32 * s);
-                            const bf16x8 b8 = *reinterpret_cast<const bf16x8 *>(wrow + 32 * s);
-                            acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a8, b8, acc[m], 0, 0, 0);
-                        }
+                        // channels 0..15 of the chunk; lane half h holds 8h .. 8h+7
+                        const bf16x8 a8 = *reinterpret_cast<const bf16x8 *>(arow);
+                        const bf16x8 b8 = *reinterpret_cast<const bf16x8 *>(wrow);
+                        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a8, b8, acc[m], 0, 0, 0);
                     }
                 }
             }
         }
-        __syncthreads();
+        __syncthreads();  // the chunk's buffers are restaged next
     }
 
     // ---- epilogue: acc element i of subtile m is pixel (y0+2w+m, x0+(i&3)+8(i>>2)+4h), channel pl
@@ -864,10 +898,6 @@ struct WgArgs {
     bool whole;   // every 16-byte piece of A, B and gy lies inside its row: unmasked vector loads
     float *part;  // [((group * n_cib + cib) * n_cob + cob)][9][32][32]
 };
-
-// A 16-byte word of zeros in global memory: the LDS-DMA source of halo pieces
-// outside the map (an LDS-DMA writes what it reads; it cannot write zeros).
-__device__ u32x4 g_zero_piece;
 
 // Stages one tile's inputs of the weight gradient in LDS, as 16-byte pieces:
 // HALO: the 10x34 halo of the workgroup's WG_CI input channels (dense
