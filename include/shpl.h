@@ -376,7 +376,9 @@ int shpl_batch_norm(int dtype, int64_t rows, void *d_x, void *d_y, int64_t strid
  * ------------------------------------------------------------------------- */
 
 /* BatchNorm (+ ReLU) backward over rows x c. g_bn = g * [y > 0] when act is
- * SHPL_ACT_RELU (d_y = the layer output), xhat = (raw - mean) * scale / gamma
+ * SHPL_ACT_RELU (d_y = the layer output; d_y NULL: y recomputed from d_raw
+ * as (raw - mean) * scale + beta with the forward's rounding -- the same mask,
+ * one map less to read), xhat = (raw - mean) * scale / gamma
  * (d_raw = the conv output). Per channel (f64, fixed order):
  * dbeta = sum g_bn, dgamma = sum g_bn * xhat; then
  *   training:  g_raw = scale * (g_bn - dbeta / rows - xhat * dgamma / rows)
@@ -386,8 +388,8 @@ int shpl_batch_norm(int dtype, int64_t rows, void *d_x, void *d_y, int64_t strid
 int shpl_batch_norm_backward_workspace_bytes(int64_t rows, int64_t c, size_t *bytes);
 int shpl_batch_norm_backward(int dtype, int64_t rows, const void *d_y, const void *d_raw, const void *d_gy,
                              int64_t stride, int64_t c, const float *d_mean, const float *d_scale,
-                             const float *d_gamma, int act, int training, void *d_graw, float *d_dbeta,
-                             float *d_dgamma, void *d_ws, size_t ws_bytes, void *stream);
+                             const float *d_gamma, const float *d_beta, int act, int training, void *d_graw,
+                             float *d_dbeta, float *d_dgamma, void *d_ws, size_t ws_bytes, void *stream);
 
 /* Input gradient: dx = conv3x3_SAME(gy, W') with W'[ky][kx][co][ci] =
  * W[2-ky][2-kx][ci][co], the forward conv kernel on transposed packed

@@ -686,17 +686,30 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_apply_vec(const T *x, T *y, i
 //   training:  g_raw = scale * (g_bn - dbeta / N - xhat * dgamma / N)
 //   inference: g_raw = scale * g_bn     (moving statistics are constants)
 // mean / scale NULL: 0 / 1 (a conv bias instead of BN: g_raw = g_bn).
+// The ReLU mask [y > 0] is read from y, or (y NULL) recomputed from the BN
+// input with the forward's rounded operations, u = (raw - mean) * scale
+// (+ beta), so that it is bitwise the forward's: [u > 0] == [y > 0].
+__device__ __forceinline__ float bn_pre_act(float x, float m, float sc, const float *beta, int ch) {
+    const float u = __fmul_rn(__fsub_rn(x, m), sc);
+    return beta ? __fadd_rn(u, beta[ch]) : u;
+}
+
 template <typename T>
-__device__ __forceinline__ float bn_gbn(const T *y, const T *gy, int64_t o, int act) {
+__device__ __forceinline__ float bn_gbn(const T *y, const T *raw, const T *gy, int64_t o, int ch, int act,
+                                        const float *mean, const float *scale, const float *beta) {
     const float gv = Elem<T>::f(gy[o]);
-    return (act == 1 && !(Elem<T>::f(y[o]) > 0.0f)) ? 0.0f : gv;
+    if (act != 1) return gv;
+    const float yv = y ? Elem<T>::f(y[o])
+                       : bn_pre_act(Elem<T>::f(raw[o]), mean ? mean[ch] : 0.0f, scale ? scale[ch] : 1.0f, beta, ch);
+    return yv > 0.0f ? gv : 0.0f;
 }
 
 template <typename T>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_partial(const T *y, const T *raw, const T *gy, int64_t rows,
                                                                int64_t stride, int c, const float *mean,
-                                                               const float *scale, const float *gamma, int act,
-                                                               int64_t rows_per_block, double *part) {
+                                                               const float *scale, const float *gamma,
+                                                               const float *beta, int act, int64_t rows_per_block,
+                                                               double *part) {
     __shared__ double red[2][SHPL_BLOCK];
     int cc_n = 1;
     while (cc_n * 2 <= c && cc_n * 2 <= SHPL_BLOCK) cc_n *= 2;  // channels per pass (a power of two)
@@ -711,7 +724,7 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_partial(const T *y, const
             const float inv = scale ? __fdiv_rn(scale[ch], gamma ? gamma[ch] : 1.0f) : 1.0f;
             for (int64_t r = r0 + rl; r < r1; r += rl_n) {
                 const int64_t o = r * stride + ch;
-                const float gb = bn_gbn(y, gy, o, act);
+                const float gb = bn_gbn(y, raw, gy, o, ch, act, mean, scale, beta);
                 const float xh = __fmul_rn(__fsub_rn(Elem<T>::f(raw[o]), m), inv);
                 s1 += (double)gb;
                 s2 += (double)gb * (double)xh;
@@ -739,7 +752,7 @@ template <typename T>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_partial_vec(const T *y, const T *raw, const T *gy,
                                                                    int64_t rows, int64_t stride, int c,
                                                                    const float *mean, const float *scale,
-                                                                   const float *gamma, int act,
+                                                                   const float *gamma, const float *beta, int act,
                                                                    int64_t rows_per_block, double *part) {
     constexpr int VEC = 16 / sizeof(T);
     __shared__ double red[2][SHPL_BLOCK * VEC];
@@ -747,11 +760,13 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_partial_vec(const T *y, c
     const int rl = threadIdx.x / cg_n, cg = threadIdx.x % cg_n, ch0 = cg * VEC;
     const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
     const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
-    float m[VEC], inv[VEC];
+    float m[VEC], inv[VEC], sc[VEC], b[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
         m[k] = mean ? mean[ch0 + k] : 0.0f;
+        sc[k] = scale ? scale[ch0 + k] : 1.0f;
         inv[k] = scale ? __fdiv_rn(scale[ch0 + k], gamma ? gamma[ch0 + k] : 1.0f) : 1.0f;
+        b[k] = beta ? beta[ch0 + k] : 0.0f;
     }
     double s1[VEC], s2[VEC];
 #pragma unroll
@@ -761,9 +776,13 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_partial_vec(const T *y, c
         float gv[VEC], xv[VEC], yv[VEC];
         Piece<T, VEC>::load(gy + o, gv);
         Piece<T, VEC>::load(raw + o, xv);
-        if (act == 1) Piece<T, VEC>::load(y + o, yv);
+        if (act == 1 && y) Piece<T, VEC>::load(y + o, yv);
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
+            if (act == 1 && !y) {
+                const float u = __fmul_rn(__fsub_rn(xv[k], m[k]), sc[k]);
+                yv[k] = beta ? __fadd_rn(u, b[k]) : u;
+            }
             const float gb = (act == 1 && !(yv[k] > 0.0f)) ? 0.0f : gv[k];
             const float xh = __fmul_rn(__fsub_rn(xv[k], m[k]), inv[k]);
             s1[k] += (double)gb;
@@ -792,15 +811,16 @@ template <typename T>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_apply_vec(const T *y, const T *raw, const T *gy,
                                                                  int64_t rows, int64_t stride, int c,
                                                                  const float *mean, const float *scale,
-                                                                 const float *gamma, int act, int training,
-                                                                 const float *mean_terms, T *graw) {
+                                                                 const float *gamma, const float *beta, int act,
+                                                                 int training, const float *mean_terms, T *graw) {
     constexpr int VEC = 16 / sizeof(T);
     const int pr = c / VEC, rpb = SHPL_BLOCK / pr;
     const int ch0 = (threadIdx.x % pr) * VEC;
-    float sc[VEC], m[VEC], inv[VEC], t0[VEC], t1[VEC];
+    float sc[VEC], m[VEC], inv[VEC], t0[VEC], t1[VEC], b[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
         const int ch = ch0 + k;
+        b[k] = beta ? beta[ch] : 0.0f;
         sc[k] = scale ? scale[ch] : 1.0f;
         m[k] = mean ? mean[ch] : 0.0f;
         inv[k] = __fdiv_rn(sc[k], gamma ? gamma[ch] : 1.0f);
@@ -811,10 +831,14 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_apply_vec(const T *y, con
         const int64_t o = r * stride + ch0;
         float gv[VEC], yv[VEC], xv[VEC], out[VEC];
         Piece<T, VEC>::load(gy + o, gv);
-        if (act == 1) Piece<T, VEC>::load(y + o, yv);
-        if (training) Piece<T, VEC>::load(raw + o, xv);
+        if (act == 1 && y) Piece<T, VEC>::load(y + o, yv);
+        if (training || !y) Piece<T, VEC>::load(raw + o, xv);
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
+            if (act == 1 && !y) {
+                const float u = __fmul_rn(__fsub_rn(xv[k], m[k]), sc[k]);
+                yv[k] = beta ? __fadd_rn(u, b[k]) : u;
+            }
             const float gb = (act == 1 && !(yv[k] > 0.0f)) ? 0.0f : gv[k];
             if (training) {
                 const float xh = __fmul_rn(__fsub_rn(xv[k], m[k]), inv[k]);
@@ -846,15 +870,15 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_finalize(const double *pa
 template <typename T>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_apply(const T *y, const T *raw, const T *gy, int64_t rows,
                                                              int64_t stride, int c, const float *mean,
-                                                             const float *scale, const float *gamma, int act,
-                                                             int training, const float *mean_terms, T *graw) {
+                                                             const float *scale, const float *gamma, const float *beta,
+                                                             int act, int training, const float *mean_terms, T *graw) {
     const int64_t total = rows * c;
     for (int64_t t = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x; t < total;
          t += (int64_t)gridDim.x * SHPL_BLOCK) {
         const int64_t r = t / c;
         const int ch = (int)(t - r * c);
         const int64_t o = r * stride + ch;
-        const float gb = bn_gbn(y, gy, o, act);
+        const float gb = bn_gbn(y, raw, gy, o, ch, act, mean, scale, beta);
         const float sc = scale ? scale[ch] : 1.0f;
         float v;
         if (training) {
@@ -1301,16 +1325,16 @@ extern "C" int shpl_batch_norm_backward_workspace_bytes(int64_t rows, int64_t c,
 
 extern "C" int shpl_batch_norm_backward(int dtype, int64_t rows, const void *d_y, const void *d_raw,
                                         const void *d_gy, int64_t stride, int64_t c, const float *d_mean,
-                                        const float *d_scale, const float *d_gamma, int act, int training,
-                                        void *d_graw, float *d_dbeta, float *d_dgamma, void *d_ws, size_t ws_bytes,
-                                        void *stream) {
+                                        const float *d_scale, const float *d_gamma, const float *d_beta, int act,
+                                        int training, void *d_graw, float *d_dbeta, float *d_dgamma, void *d_ws,
+                                        size_t ws_bytes, void *stream) {
     if (dtype != SHPL_F32 && dtype != SHPL_BF16) return SHPL_ERR_ARG;
     if (rows < 0 || c < 1 || stride < c || c > (1 << 16)) return SHPL_ERR_BAD_SHAPE;
     if (act != 0 && act != 1) return SHPL_ERR_ARG;
     size_t need;
     shpl_batch_norm_backward_workspace_bytes(rows, c, &need);
     if (!d_ws || ws_bytes < need) return SHPL_ERR_WORKSPACE;
-    if (rows > 0 && (!d_gy || !d_graw || (act == 1 && !d_y) || (training && !d_raw))) return SHPL_ERR_ARG;
+    if (rows > 0 && (!d_gy || !d_graw || (act == 1 && !d_y && !d_raw) || (training && !d_raw))) return SHPL_ERR_ARG;
     if (rows == 0) return SHPL_OK;
     hipStream_t s = (hipStream_t)stream;
     const int nb = bn_bwd_blocks(rows);
@@ -1322,25 +1346,27 @@ extern "C" int shpl_batch_norm_backward(int dtype, int64_t rows, const void *d_y
     const int vec = dtype == SHPL_F32 ? 4 : 8;
     const int cg = (int)(c / vec);
     const bool vform = c % vec == 0 && stride % vec == 0 && cg <= SHPL_BLOCK && (cg & (cg - 1)) == 0 &&
-                       aligned16(d_gy) && aligned16(rw) && aligned16(d_graw) && (act != 1 || aligned16(d_y));
+                       aligned16(d_gy) && aligned16(rw) && aligned16(d_graw) && (!d_y || aligned16(d_y));
+    // y NULL: the ReLU mask from raw (bn_pre_act), so only the y argument of the kernels changes
+    const float *beta = act == 1 && !d_y ? d_beta : nullptr;
     const int grid = grid_for(rows * c / (vform ? vec : 1), SHPL_BLOCK, 1 << 16);
     auto launch = [&](auto tag) {
         typedef decltype(tag) T;
         const T *y = (const T *)d_y, *r = (const T *)rw, *g = (const T *)d_gy;
         if (vform)
             hipLaunchKernelGGL(k_bn_bwd_partial_vec<T>, dim3(nb), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride,
-                               (int)c, d_mean, d_scale, d_gamma, act, rpb, part);
+                               (int)c, d_mean, d_scale, d_gamma, beta, act, rpb, part);
         else
             hipLaunchKernelGGL(k_bn_bwd_partial<T>, dim3(nb), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride, (int)c,
-                               d_mean, d_scale, d_gamma, act, rpb, part);
+                               d_mean, d_scale, d_gamma, beta, act, rpb, part);
         hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(grid_for(c, SHPL_BLOCK, 256)), dim3(SHPL_BLOCK), 0, s, part, nb,
                            (int)c, (double)rows, d_dbeta, d_raw ? d_dgamma : nullptr, mt);
         if (vform)
             hipLaunchKernelGGL(k_bn_bwd_apply_vec<T>, dim3(grid), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride,
-                               (int)c, d_mean, d_scale, d_gamma, act, training, mt, (T *)d_graw);
+                               (int)c, d_mean, d_scale, d_gamma, beta, act, training, mt, (T *)d_graw);
         else
             hipLaunchKernelGGL(k_bn_bwd_apply<T>, dim3(grid), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride, (int)c,
-                               d_mean, d_scale, d_gamma, act, training, mt, (T *)d_graw);
+                               d_mean, d_scale, d_gamma, beta, act, training, mt, (T *)d_graw);
     };
     if (dtype == SHPL_F32)
         launch(float());

@@ -102,9 +102,11 @@ def batch_norm_train(x, stats, count, eps=1e-3, gamma=None, beta=None, relu=True
     return x if out is None else out
 
 
-def batch_norm_backward(gy, y=None, raw=None, mean=None, scale=None, gamma=None, relu=True, training=True):
+def batch_norm_backward(gy, y=None, raw=None, mean=None, scale=None, gamma=None, relu=True, training=True,
+                        beta=None):
     """(g_raw, dbeta, dgamma) of BatchNorm (+ ReLU) over [..., C]; mean / scale
-    None -> 0 / 1 (a conv bias: dbeta is the bias gradient)."""
+    None -> 0 / 1 (a conv bias: dbeta is the bias gradient). With y None the
+    ReLU mask is recomputed from raw (and beta), bitwise the forward's."""
     C = int(gy.shape[-1])
     rows = gy.numel() // C
     out = torch.empty_like(gy)
@@ -115,7 +117,7 @@ def batch_norm_backward(gy, y=None, raw=None, mean=None, scale=None, gamma=None,
             "shpl_batch_norm_backward_workspace_bytes")
     ws = L.workspace(nb.value, gy.device)
     L.check(L.lib().shpl_batch_norm_backward(L.dtype_code(gy), rows, L.ptr(y), L.ptr(raw), L.ptr(gy), C, C,
-                                             L.ptr(mean), L.ptr(scale), L.ptr(gamma),
+                                             L.ptr(mean), L.ptr(scale), L.ptr(gamma), L.ptr(beta),
                                              L.ACT_RELU if relu else L.ACT_NONE, int(bool(training)), L.ptr(out),
                                              L.ptr(dbeta), L.ptr(dgamma), L.ptr(ws), ws.numel(),
                                              L.stream_of(gy.device)), "shpl_batch_norm_backward")
@@ -200,19 +202,21 @@ class _FusionConvFn(torch.autograd.Function):
             mean, scale = bn_ws[:conv.c_out], bn_ws[conv.c_out:]
         ctx.conv, ctx.smap, ctx.pooled, ctx.train_bn = conv, smap, pooled, train_bn
         ctx.shapes = (Ca, Cb)
-        ctx.save_for_backward(a, b, weights, y, raw, mean, scale)
+        # training BN: the backward recomputes the ReLU mask from raw and beta (bitwise y's), so y is not kept
+        ctx.save_for_backward(a, b, weights, None if train_bn else y, raw, mean, scale,
+                              beta if train_bn else None)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        a, b, weights, y, raw, mean, scale = ctx.saved_tensors
+        a, b, weights, y, raw, mean, scale, beta = ctx.saved_tensors
         conv, smap, pooled = ctx.conv, ctx.smap, ctx.pooled
         Ca, Cb = ctx.shapes
-        gy = gy.contiguous().to(y.dtype)
+        gy = gy.contiguous().to(a.dtype)
         if conv.batch_norm or conv.bias is not None or conv.relu:
             g_raw, dbeta, _ = batch_norm_backward(
                 gy, y=y, raw=raw, mean=mean if (conv.batch_norm or ctx.train_bn) else None,
-                scale=scale if conv.batch_norm else None, relu=conv.relu, training=ctx.train_bn)
+                scale=scale if conv.batch_norm else None, relu=conv.relu, training=ctx.train_bn, beta=beta)
         else:
             g_raw, dbeta = gy, None
         need_x = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]

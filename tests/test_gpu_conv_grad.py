@@ -113,6 +113,15 @@ def test_batch_norm_backward(training):
     # values of order |scale * g|; the training form subtracts two O(1) means in f32
     _check(gr, e_raw, 1e-5 + 1e-5 * np.abs(scale) * (np.abs(g) + 1.0), "g_raw")
     _check(db, e_db, 1e-4 + 1e-6 * np.abs(g).reshape(-1, 40).sum(0), "dbeta")
+    # the ReLU mask recomputed from raw (y not read) with the forward's rounding, (raw - mean) * scale + beta
+    # one rounded op at a time (as torch's separate kernels do): bitwise the same result as reading y
+    t_raw, t_mean, t_scale, t_beta = _t(raw), _t(mean.astype(np.float32)), _t(scale), _t(beta)
+    y_dev = torch.clamp_min((t_raw - t_mean) * t_scale + t_beta, 0.0)
+    a1 = fc.batch_norm_backward(_t(g), y=y_dev, raw=t_raw, mean=t_mean, scale=t_scale, relu=True, training=training)
+    a2 = fc.batch_norm_backward(_t(g), y=None, raw=t_raw, mean=t_mean, scale=t_scale, relu=True, training=training,
+                                beta=t_beta)
+    for u, v in zip(a1, a2):
+        assert torch.equal(u, v)
 
 
 @pytest.mark.parametrize("train", [True, False])
