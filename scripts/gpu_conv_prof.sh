@@ -14,7 +14,7 @@ rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 i=0
 for c in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVES"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex 'k_conv3x3' -d gpurun_out/pmc_conv_${DT}_$i -o run \
+  timeout -s KILL 180 rocprofv3 --pmc $c --kernel-include-regex 'k_conv3x3' -d gpurun_out/pmc_conv_${DT}_$i -o run \
     --output-format csv -- python3 $B > gpurun_out/pmc_conv_${DT}_$i.log 2>&1
   rc=$?; echo "pmc '$c' rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done

@@ -17,6 +17,9 @@ run bench_c3 300 python bench.py --config 3
 run bench_c5 400 python bench.py --config 5
 run bench_frames 400 python bench.py --workload frames
 run bench_noov 300 python bench.py --no-overlap --no-graph --no-cpu-baseline
+run bench_conv 400 python bench.py --workload conv
+run bench_conv_bf16 300 python bench.py --workload conv --dtype bf16 --no-cpu-baseline
+run bench_conv_train 300 python bench.py --workload conv --train
 for c in 3 5; do
   run prof_c$c 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c$c -o run --output-format csv -- \
     python3 bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline

@@ -26,7 +26,7 @@ for s in $STEPS; do
       # HBM traffic of the SHPL kernels: FETCH_SIZE and WRITE_SIZE in separate passes
       # (they do not fit one TCC pass), kernel filter on the shpl kernels only.
       for c in FETCH_SIZE WRITE_SIZE; do
-        timeout -k 10 600 rocprofv3 --pmc $c --kernel-include-regex 'k_dense|k_sparse|k_csr_frame|k_compact|k_count' \
+        timeout -s KILL 180 rocprofv3 --pmc $c --kernel-include-regex 'k_dense|k_sparse|k_csr_frame|k_compact|k_count' \
           -d gpurun_out/pmc_$c -o run --output-format csv -- \
           python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/pmc_$c.log 2>&1
         rc=$?; echo "pmc $c rc=$rc"; tail -1 gpurun_out/pmc_$c.log | cut -c1-200; ok $rc || exit $rc
