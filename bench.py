@@ -222,7 +222,7 @@ def main():
         if backward:
             if ev is not None:
                 ev[4].record()
-            pl.backward(g_bv, g_img, d_bev, d_img, side2=side2)
+            pl.backward(g_bv, g_img, d_bev, d_img, side2=None if args.no_overlap else side2)
             if ev is not None:
                 ev[5].record()
 

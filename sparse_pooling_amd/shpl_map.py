@@ -84,6 +84,12 @@ class ShplMap:
         self._csr[key] = c
         return c
 
+    def csr_tensors(self, direction, order):
+        """(ent_dst, ent_src, ent_val, ent_col or None) of csr(direction, order):
+        the CSR as the tensors the torch.ops.shpl operators take (ops.py)."""
+        c = self.csr(direction, order)
+        return c.ent_dst, c.ent_src, c.ent_val, c.ent_col
+
 
 def pack_map(mij, values, m_size, idx, img_shape, validate=True):
     """Reference-format M (Mij [nnz,2] i64, M_val [nnz], M_size [2]) and the
@@ -126,72 +132,41 @@ def pull(smap, direction, order, src, src_stride, src_off, c_pool, out, out_stri
     return out
 
 
+def op_pull(smap, direction, order, src, out_shape, src_off=0, c_pool=None, pass_=None, pass_off=0, c_pass=None,
+            mode=L.OUT_POOL):
+    """torch.ops.shpl.pull through smap's CSR (ops.py): a new output tensor."""
+    from . import ops  # noqa: F401 -- registers torch.ops.shpl
+    c_pool = int(src.shape[-1]) - src_off if c_pool is None else int(c_pool)
+    if c_pass is None:
+        c_pass = 0 if pass_ is None else int(pass_.shape[-1]) - pass_off
+    return torch.ops.shpl.pull(src, *smap.csr_tensors(direction, order), direction, [int(v) for v in out_shape],
+                               int(src_off), c_pool, pass_, int(pass_off), int(c_pass), mode)
+
+
 def pool_img_to_bev(smap, img, bev_shape, bev=None):
     """img [.., Ci] -> [B,Hb,Wb,Ci] (or [bev || pooled] when ``bev`` is given)."""
     Ci = img.shape[-1]
     if bev is None:
-        out = torch.empty(tuple(bev_shape[:3]) + (Ci,), dtype=img.dtype, device=img.device)
-        return pull(smap, L.BY_CELL, L.ORDER_ENTRY, img, Ci, 0, Ci, out, Ci)
+        return op_pull(smap, L.BY_CELL, L.ORDER_ENTRY, img, tuple(bev_shape[:3]) + (Ci,))
     Cb = bev.shape[-1]
-    out = torch.empty(tuple(bev.shape[:3]) + (Cb + Ci,), dtype=img.dtype, device=img.device)
-    return pull(smap, L.BY_CELL, L.ORDER_ENTRY, img, Ci, 0, Ci, out, Cb + Ci,
-                pass_=bev, pass_stride=Cb, c_pass=Cb, mode=L.OUT_CONCAT)
+    return op_pull(smap, L.BY_CELL, L.ORDER_ENTRY, img, tuple(bev.shape[:3]) + (Cb + Ci,), pass_=bev,
+                   mode=L.OUT_CONCAT)
 
 
 def pool_bev_to_img(smap, bev, img_shape, img=None):
     """bev [.., Cb] -> [B,Hi,Wi,Cb] (or [img || pooled] when ``img`` is given)."""
     Cb = bev.shape[-1]
     if img is None:
-        out = torch.empty(tuple(img_shape[:3]) + (Cb,), dtype=bev.dtype, device=bev.device)
-        return pull(smap, L.BY_PIXEL, L.ORDER_COL_ROW, bev, Cb, 0, Cb, out, Cb)
+        return op_pull(smap, L.BY_PIXEL, L.ORDER_COL_ROW, bev, tuple(img_shape[:3]) + (Cb,))
     Ci = img.shape[-1]
-    out = torch.empty(tuple(img.shape[:3]) + (Ci + Cb,), dtype=bev.dtype, device=bev.device)
-    return pull(smap, L.BY_PIXEL, L.ORDER_COL_ROW, bev, Cb, 0, Cb, out, Ci + Cb,
-                pass_=img, pass_stride=Ci, c_pass=Ci, mode=L.OUT_CONCAT)
+    return op_pull(smap, L.BY_PIXEL, L.ORDER_COL_ROW, bev, tuple(img.shape[:3]) + (Ci + Cb,), pass_=img,
+                   mode=L.OUT_CONCAT)
 
 
 # ------------------------------------------------------------------ autograd
 
 def _c(t):
     return t if t.is_contiguous() else t.contiguous()
-
-
-class _PoolFn(torch.autograd.Function):
-    """_sparse_pool_op: gather_nd + sparse_tensor_dense_matmul + reshape."""
-
-    @staticmethod
-    def forward(ctx, img, smap, bev_shape):
-        ctx.smap = smap
-        ctx.img_shape = img.shape
-        return pool_img_to_bev(smap, _c(img), bev_shape)
-
-    @staticmethod
-    def backward(ctx, g):
-        g = _c(g)
-        C = g.shape[-1]
-        d = torch.empty(ctx.img_shape, dtype=g.dtype, device=g.device)
-        # TF: scatter_nd(idx, matmul(M, dY, adjoint_a=True))
-        pull(ctx.smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, g, C, 0, C, d, C)
-        return d, None, None
-
-
-class _TransFn(torch.autograd.Function):
-    """_sparse_pool_trans_op: sparse_transpose + matmul + scatter_nd."""
-
-    @staticmethod
-    def forward(ctx, bev, smap, img_shape):
-        ctx.smap = smap
-        ctx.bev_shape = bev.shape
-        return pool_bev_to_img(smap, _c(bev), img_shape)
-
-    @staticmethod
-    def backward(ctx, g):
-        g = _c(g)
-        C = g.shape[-1]
-        d = torch.empty(ctx.bev_shape, dtype=g.dtype, device=g.device)
-        # TF: matmul(sparse_transpose(M), gather_nd(dZ, idx), adjoint_a=True)
-        pull(ctx.smap, L.BY_CELL, L.ORDER_COL_ENTRY, g, C, 0, C, d, C)
-        return d, None, None
 
 
 class _PoolConcatFn(torch.autograd.Function):
@@ -208,8 +183,7 @@ class _PoolConcatFn(torch.autograd.Function):
     def backward(ctx, g):
         g = _c(g)
         Cb, Ci = ctx.Cb, ctx.img_shape[-1]
-        d_img = torch.empty(ctx.img_shape, dtype=g.dtype, device=g.device)
-        pull(ctx.smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, g, Cb + Ci, Cb, Ci, d_img, Ci)
+        d_img = op_pull(ctx.smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, g, ctx.img_shape, src_off=Cb, c_pool=Ci)
         return g[..., :Cb].contiguous(), d_img, None
 
 
@@ -232,31 +206,22 @@ class _DualFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_bv, g_img):
         smap, Cb, Ci = ctx.smap, ctx.Cb, ctx.Ci
-        ref = g_bv if g_bv is not None else g_img
-        dev, dt = ref.device, ref.dtype
-        w = Cb + Ci
-        d_bev = torch.empty(ctx.bev_shape, dtype=dt, device=dev)
-        d_img = torch.empty(ctx.img_shape, dtype=dt, device=dev)
         if g_bv is not None:
             g_bv = _c(g_bv)
         if g_img is not None:
             g_img = _c(g_img)
         # d_bev = g_bv[..., :Cb] + matmul(sparse_transpose(M), gather_nd(g_img[..., Ci:]), adjoint_a)
         if g_img is None:
-            d_bev.copy_(g_bv[..., :Cb])
-        elif g_bv is None:
-            pull(smap, L.BY_CELL, L.ORDER_COL_ENTRY, g_img, w, Ci, Cb, d_bev, Cb)
+            d_bev = g_bv[..., :Cb].contiguous()
         else:
-            pull(smap, L.BY_CELL, L.ORDER_COL_ENTRY, g_img, w, Ci, Cb, d_bev, Cb,
-                 pass_=g_bv, pass_stride=w, c_pass=Cb, mode=L.OUT_ADD)
+            d_bev = op_pull(smap, L.BY_CELL, L.ORDER_COL_ENTRY, g_img, ctx.bev_shape, src_off=Ci, c_pool=Cb,
+                            pass_=g_bv, c_pass=Cb, mode=L.OUT_POOL if g_bv is None else L.OUT_ADD)
         # d_img = g_img[..., :Ci] + scatter_nd(idx, matmul(M, g_bv[..., Cb:], adjoint_a))
         if g_bv is None:
-            d_img.copy_(g_img[..., :Ci])
-        elif g_img is None:
-            pull(smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, g_bv, w, Cb, Ci, d_img, Ci)
+            d_img = g_img[..., :Ci].contiguous()
         else:
-            pull(smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, g_bv, w, Cb, Ci, d_img, Ci,
-                 pass_=g_img, pass_stride=w, c_pass=Ci, mode=L.OUT_ADD)
+            d_img = op_pull(smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, g_bv, ctx.img_shape, src_off=Cb, c_pool=Ci,
+                            pass_=g_img, c_pass=Ci, mode=L.OUT_POOL if g_img is None else L.OUT_ADD)
         return d_bev, d_img, None
 
 
@@ -268,11 +233,15 @@ def layer(bev, img, smap, dual=False):
 
 
 def pool_op(img, smap, bev_shape):
-    return _PoolFn.apply(img, smap, tuple(bev_shape))
+    """_sparse_pool_op: torch.ops.shpl.spmm (ops.py), gradient = the pixel-keyed pull."""
+    from . import ops
+    return ops.sparse_pool(_c(img), smap, tuple(bev_shape))
 
 
 def trans_op(bev, smap, img_shape):
-    return _TransFn.apply(bev, smap, tuple(img_shape))
+    """_sparse_pool_trans_op: torch.ops.shpl.spmm, gradient = the cell-keyed pull."""
+    from . import ops
+    return ops.sparse_pool_trans(_c(bev), smap, tuple(img_shape))
 
 
 # --------------------------------------------------------------- index build
