@@ -69,6 +69,27 @@ def test_dgrad_and_wgrad_dense(shape):
     _check(dw, orc.conv3x3_wgrad(x, g), TOL + ACC_W * orc.conv3x3_wgrad(np.abs(x), np.abs(g)), "dw")
 
 
+def test_dgrad_and_wgrad_bf16():
+    """bf16 storage: products of bf16 values are exact in f32, so the weight
+    gradient keeps the f32 bound; the input gradient is stored in bf16 (plus
+    half a bf16 ulp of the result: 2^-8 relative, 7 stored mantissa bits)."""
+    from sparse_pooling_amd import fusion_conv as fc
+    B, H, W, Cin, Cout = 2, 11, 37, 48, 32
+    bf = lambda a: torch.from_numpy(a).to(torch.bfloat16)  # noqa: E731
+    x = bf(synth.make_features((B, H, W, Cin), 41))
+    w = bf(_weights(Cin, Cout, 42))
+    g = bf(synth.make_features((B, H, W, Cout), 43))
+    xf, wf, gf = (t.float().numpy() for t in (x, w, g))
+    dx = fc.conv3x3_dgrad(g.to(DEV), w.to(DEV), Cin)
+    assert dx.dtype == torch.bfloat16
+    ref = orc.conv3x3_dgrad(gf, wf)
+    wt = np.ascontiguousarray(wf[::-1, ::-1].transpose(0, 1, 3, 2))
+    _, ab = orc.conv3x3(np.abs(gf), np.abs(wt), raw=True)
+    _check(dx.float(), ref, TOL + ACC * ab + 2.0 ** -8 * np.abs(ref), "dx bf16")
+    dw = fc.conv3x3_wgrad(x.to(DEV), g.to(DEV))
+    _check(dw, orc.conv3x3_wgrad(xf, gf), TOL + ACC_W * orc.conv3x3_wgrad(np.abs(xf), np.abs(gf)), "dw bf16")
+
+
 def test_wgrad_two_sources_and_pooled():
     """wgrad of [a || b] with b dense, and with b pooled from the CSR (the
     pooled channels recomputed in the staging), == wgrad of the concat."""
@@ -92,19 +113,20 @@ def test_wgrad_two_sources_and_pooled():
     _check(pooled, ref, bound, "pooled")
 
 
-@pytest.mark.parametrize("training", [True, False])
-def test_batch_norm_backward(training):
+@pytest.mark.parametrize("training,C", [(True, 40), (False, 40), (True, 7), (False, 7)])
+def test_batch_norm_backward(training, C):
+    """C = 40: the 16-byte vector kernels; C = 7: the scalar ones."""
     from sparse_pooling_amd import fusion_conv as fc
     rng = np.random.default_rng(7)
-    raw = (rng.standard_normal((3, 11, 13, 40)) * 2.0 + 0.5).astype(np.float32)
+    raw = (rng.standard_normal((3, 11, 13, C)) * 2.0 + 0.5).astype(np.float32)
     g = rng.standard_normal(raw.shape).astype(np.float32)
-    beta = rng.standard_normal(40).astype(np.float32)
+    beta = rng.standard_normal(C).astype(np.float32)
     if training:
-        mean = raw.reshape(-1, 40).astype(np.float64).mean(0)
-        var = raw.reshape(-1, 40).astype(np.float64).var(0)
+        mean = raw.reshape(-1, C).astype(np.float64).mean(0)
+        var = raw.reshape(-1, C).astype(np.float64).var(0)
     else:
-        mean = rng.standard_normal(40)
-        var = rng.uniform(0.5, 2.0, 40)
+        mean = rng.standard_normal(C)
+        var = rng.uniform(0.5, 2.0, C)
     scale = (1.0 / np.sqrt(var + 1e-3)).astype(np.float32)
     y = np.maximum((raw - mean) * scale + beta, 0.0).astype(np.float32)
     gr, db, _ = fc.batch_norm_backward(_t(g), y=_t(y), raw=_t(raw), mean=_t(mean.astype(np.float32)),
@@ -112,7 +134,7 @@ def test_batch_norm_backward(training):
     e_raw, e_db, _ = orc.batch_norm_backward(raw.astype(np.float64), g, training, mean, var, 1e-3, None, beta, True)
     # values of order |scale * g|; the training form subtracts two O(1) means in f32
     _check(gr, e_raw, 1e-5 + 1e-5 * np.abs(scale) * (np.abs(g) + 1.0), "g_raw")
-    _check(db, e_db, 1e-4 + 1e-6 * np.abs(g).reshape(-1, 40).sum(0), "dbeta")
+    _check(db, e_db, 1e-4 + 1e-6 * np.abs(g).reshape(-1, C).sum(0), "dbeta")
     # the ReLU mask recomputed from raw (y not read) with the forward's rounding, (raw - mean) * scale + beta
     # one rounded op at a time (as torch's separate kernels do): bitwise the same result as reading y
     t_raw, t_mean, t_scale, t_beta = _t(raw), _t(mean.astype(np.float32)), _t(scale), _t(beta)
