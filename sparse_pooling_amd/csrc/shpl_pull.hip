@@ -118,32 +118,35 @@ struct Feat {  // strided feature rows: row r, element c at base + r*stride + of
     uint32_t cpass;  // chunks of the pass-through half (CONCAT)
     uint32_t cpool;  // chunks of the pooled part
     int mode;
+    int cpr_shift;   // log2(cpr) when cpr is a power of two, else -1
 };
 
 // ---------------------------------------------------------------- k_dense
-template <typename T, int VEC>
+template <typename T, int VEC, bool POW2>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_dense(const Feat f, uint32_t row0, uint32_t n_rows) {
     typedef Chunk<T, VEC> C;
     const uint32_t g = blockIdx.x * SHPL_BLOCK + threadIdx.x;
     if (g >= n_rows * f.cpr) return;
-    const uint32_t r = g / f.cpr;
+    const uint32_t r = POW2 ? g >> f.cpr_shift : g / f.cpr;  // a shift instead of a division when it can
     const uint32_t ch = g - r * f.cpr;
-    const int64_t row = (int64_t)row0 + r;
+    // row < 2^32 and row widths < 2^31 (plan() checks): 32 x 32 -> 64-bit offsets
+    const uint32_t row = row0 + r;
     const T *pass = reinterpret_cast<const T *>(f.pass) + f.pass_off;
+    const uint64_t pass_at = (uint64_t)row * (uint32_t)f.pass_stride + ch * VEC;
     typename C::raw_t v;
     if (f.mode == SHPL_OUT_ADD) {
         // pass + 0.0f: TF's add_n with an all-zero scatter turns -0 into +0
         float a[VEC];
-        C::to_f32(C::load_nt(pass + row * f.pass_stride + (int64_t)ch * VEC), a);
+        C::to_f32(C::load_nt(pass + pass_at), a);
 #pragma unroll
         for (int j = 0; j < VEC; ++j) a[j] = __fadd_rn(a[j], 0.0f);
         v = C::from_f32(a);
     } else if (f.mode == SHPL_OUT_CONCAT && ch < f.cpass) {
-        v = C::load_nt(pass + row * f.pass_stride + (int64_t)ch * VEC);
+        v = C::load_nt(pass + pass_at);
     } else {
         v = C::zero();
     }
-    C::store_nt(reinterpret_cast<T *>(f.out) + row * f.out_stride + (int64_t)ch * VEC, v);
+    C::store_nt(reinterpret_cast<T *>(f.out) + ((uint64_t)row * (uint32_t)f.out_stride + ch * VEC), v);
 }
 
 // ---------------------------------------------------------------- k_sparse
@@ -290,13 +293,14 @@ __device__ __forceinline__ void store_pooled(const Feat &f, int32_t key, uint32_
 // One thread per (sorted entry, chunk); the thread on the first entry of a
 // destination's run sums it and writes the pooled chunk -- for runs of at
 // most LONG_RUN entries (SPLIT) or all runs (!SPLIT).
-template <typename T, int VEC, bool GROUP, bool SPLIT>
-__global__ __launch_bounds__(SHPL_BLOCK) void k_sparse(const Feat f, const Ents e) {
+template <typename T, int VEC, bool GROUP, bool SPLIT, bool POW2>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_sparse(const Feat f, const Ents e, int cpool_shift) {
     const int64_t nnz = e.n;
     const int64_t total = nnz * (int64_t)f.cpool;
     for (int64_t t = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x; t < total;
          t += (int64_t)gridDim.x * SHPL_BLOCK) {
-        const int64_t s = t / f.cpool;
+        // a shift, not a 64-bit division, when the chunk count is a power of two
+        const int64_t s = POW2 ? t >> cpool_shift : t / f.cpool;
         const uint32_t c = (uint32_t)(t - s * f.cpool);
         // the head test's loads and the walk's first index batch are
         // independent: one round trip
@@ -463,6 +467,8 @@ int plan(int direction, int dtype, const shpl_csr *csr, const void *d_src, int64
     if (out_stride < width || (c_pool > 0 && src_stride < src_off + c_pool) ||
         (mode != SHPL_OUT_POOL && pass_stride < pass_off + c_pass))
         return SHPL_ERR_BAD_SHAPE;
+    const int64_t row_max = (int64_t)1 << 31;  // row widths index in 32 bits (k_dense)
+    if (out_stride >= row_max || src_stride >= row_max || pass_stride >= row_max) return SHPL_ERR_BAD_SHAPE;
     const int64_t esz = dtype == SHPL_F32 ? 4 : 2;
     const int64_t vec = 16 / esz;
     // 16-byte chunks need every row start and every channel split on a 16-byte boundary
@@ -484,6 +490,9 @@ int plan(int direction, int dtype, const shpl_csr *csr, const void *d_src, int64
     f.cpr = (uint32_t)(width / v);
     f.cpass = mode == SHPL_OUT_CONCAT ? (uint32_t)(c_pass / v) : 0u;
     f.cpool = (uint32_t)(c_pool / v);
+    f.cpr_shift = -1;
+    for (int k = 0; k < 31; ++k)
+        if (f.cpr == (1u << k)) f.cpr_shift = k;
     pl->n_dst = n_dst;
     pl->v16 = v16;
     pl->dtype = dtype;
@@ -498,8 +507,12 @@ int dense_t(const Plan &pl, hipStream_t s) {
     for (int64_t r0 = 0; r0 < pl.n_dst; r0 += rows_per_launch) {
         const int64_t nr = (pl.n_dst - r0) < rows_per_launch ? (pl.n_dst - r0) : rows_per_launch;
         const int64_t blocks = (nr * pl.f.cpr + SHPL_BLOCK - 1) / SHPL_BLOCK;
-        hipLaunchKernelGGL((k_dense<T, VEC>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, s, pl.f, (uint32_t)r0,
-                           (uint32_t)nr);
+        if (pl.f.cpr_shift >= 0)
+            hipLaunchKernelGGL((k_dense<T, VEC, true>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, s, pl.f,
+                               (uint32_t)r0, (uint32_t)nr);
+        else
+            hipLaunchKernelGGL((k_dense<T, VEC, false>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, s, pl.f,
+                               (uint32_t)r0, (uint32_t)nr);
         SHPL_LAUNCH_CHECK();
     }
     return SHPL_OK;
@@ -515,13 +528,20 @@ template <typename T, int VEC, bool GROUP>
 int sparse_tg(const Plan &pl, const Ents &e, int64_t nnz_cap, hipStream_t s) {
     // one thread per (entry, chunk) of the capacity; the live count is read on the device
     const int grid = grid_for(nnz_cap * (int64_t)pl.f.cpool, SHPL_BLOCK, 1 << 20);
-    if (nnz_cap <= LONG_RUN) {
-        hipLaunchKernelGGL((k_sparse<T, VEC, GROUP, false>), dim3(grid), dim3(SHPL_BLOCK), 0, s, pl.f, e);
-        SHPL_LAUNCH_CHECK();
-        return SHPL_OK;
+    int shift = -1;
+    for (int k = 0; k < 31; ++k)
+        if (pl.f.cpool == (1u << k)) shift = k;
+    const bool split = nnz_cap > LONG_RUN;
+#define SHPL_SPARSE(SPLIT, POW2) \
+    hipLaunchKernelGGL((k_sparse<T, VEC, GROUP, SPLIT, POW2>), dim3(grid), dim3(SHPL_BLOCK), 0, s, pl.f, e, shift)
+    if (split) {
+        if (shift >= 0) SHPL_SPARSE(true, true); else SHPL_SPARSE(true, false);
+    } else {
+        if (shift >= 0) SHPL_SPARSE(false, true); else SHPL_SPARSE(false, false);
     }
-    hipLaunchKernelGGL((k_sparse<T, VEC, GROUP, true>), dim3(grid), dim3(SHPL_BLOCK), 0, s, pl.f, e);
+#undef SHPL_SPARSE
     SHPL_LAUNCH_CHECK();
+    if (!split) return SHPL_OK;
     // a bounded grid: each workgroup scans per_block slots, LONG_SLOTS at a time
     int64_t lgrid = (nnz_cap + LONG_SLOTS - 1) / LONG_SLOTS;
     if (lgrid > LONG_GRID) lgrid = LONG_GRID;
