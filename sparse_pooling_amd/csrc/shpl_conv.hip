@@ -1101,6 +1101,146 @@ __global__ __launch_bounds__(CONV_BLOCK, 2) void k_conv3x3_wgrad(const ConvArgs 
     }
 }
 
+// bf16 weight gradient on bf16 MFMA (v_mfma_f32_16x16x32_bf16: M = 16 input
+// channels, N = 16 output channels, K = 32 pixels of one tile row). K runs
+// along each lane's registers, so the staging transposes: the halo goes to
+// LDS as [kx][channel][halo row][32 columns] -- three copies shifted by the
+// tap's kx, so that every A fragment (8 pixels of one channel) is one
+// aligned ds_read_b128 -- and the gradient tile as [co][row][32 columns]; the
+// channel pitches are padded by 16 bytes (16 lanes' reads on distinct bank
+// quads). Dense sources only (the pooled form stays on k_conv3x3_wgrad).
+// Products of bf16 values are exact in f32; sums in f32 per workgroup, the
+// same partials and k_wgrad_reduce as k_conv3x3_wgrad. Staging goes through
+// registers, synchronously (one round trip per tile; two workgroups per CU).
+// Measured and dropped: loading the next tile's pieces under this tile's
+// MFMAs (4.50 -> 4.57 ms, 167 -> 197 VGPRs).
+constexpr int WB_CIP = HH * TW * 2 + 16;  // bytes per input channel of one kx copy (10 rows x 32 bf16 + pad)
+constexpr int WB_KXS = WG_CI * WB_CIP;    // bytes per kx copy
+constexpr int WB_COP = TH * TW * 2 + 16;  // bytes per output channel of the gradient tile
+
+__global__ __launch_bounds__(CONV_BLOCK, 2) void k_wgrad_bf16(const ConvArgs p, const WgArgs g) {
+    typedef Elem<uint16_t> E;
+    constexpr int CK = E::CK, HE = E::HE, NQ = WG_CI / CK;  // 16 channels per chunk, 2 chunks
+    constexpr int IN_PIECES = NQ * HH * HWD * 2;              // (chunk, halo pixel, 8-channel piece)
+    constexpr int IN_IT = (IN_PIECES + CONV_BLOCK - 1) / CONV_BLOCK;
+    constexpr int G_PIECES = TH * TW * (NCO / HE);            // (pixel, 8-channel piece)
+    constexpr int G_IT = G_PIECES / CONV_BLOCK;
+    __shared__ __attribute__((aligned(16))) uint8_t s_x[3 * WB_KXS];
+    __shared__ __attribute__((aligned(16))) uint8_t s_g[NCO * WB_COP];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int l16 = lane & 15, kq = lane >> 4;
+    const int grp = blockIdx.x, cib = blockIdx.y, cob = blockIdx.z;
+    const int Q = p.qa + p.qb;
+    const int H = p.h, W = p.w;
+    const uint16_t *gy = reinterpret_cast<const uint16_t *>(g.gy);
+    // wave w owns input-channel half h = w >> 1 and output-channel half o = w & 1, all 8 rows and 9 taps
+    const int h = wave >> 1, o = wave & 1;
+    f32x4v acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+    const int t0 = grp * g.tiles_per_group;
+    const int t1 = t0 + g.tiles_per_group < p.n_tiles ? t0 + g.tiles_per_group : p.n_tiles;
+    const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+    u32x4 xv[IN_IT], gv[G_IT];
+    // the tile's pieces into registers, issued together
+    auto load = [&](int tile) {
+        const int f = tile / p.tiles_per_frame;
+        const int t_in = tile - f * p.tiles_per_frame;
+        const int ty = t_in / p.tiles_x, tx = t_in - ty * p.tiles_x;
+        const int y0 = ty * TH, x0 = tx * TW;
+        const int64_t frame_row0 = (int64_t)f * H * W;
+#pragma unroll
+        for (int u = 0; u < IN_IT; ++u) {
+            const int j = tid + u * CONV_BLOCK;
+            const int q = cib * NQ + j / (HH * HWD * 2);
+            const int rem = j % (HH * HWD * 2), pix = rem >> 1, pc = rem & 1;
+            const int hr = pix / HWD, hc = pix - hr * HWD;
+            const int y = y0 - 1 + hr, x = x0 - 1 + hc;
+            const bool ok = j < IN_PIECES && q < Q && y >= 0 && y < H && x >= 0 && x < W;
+            const bool from_a = p.c_a > 0 && (q < p.qa || q >= Q);
+            const uint16_t *src = reinterpret_cast<const uint16_t *>(from_a ? p.a : p.b) + (from_a ? p.a_off : p.b_off);
+            const int64_t row = ok ? frame_row0 + (int64_t)y * W + x : frame_row0;
+            const int c = ok ? (from_a ? q : q - p.qa) * CK + pc * HE : 0;
+            if (g.whole) {  // unmasked, branch-free: out-of-map pieces read row 0 and are zeroed
+                const u32x4 v = *reinterpret_cast<const u32x4 *>(src + row * (from_a ? p.a_stride : p.b_stride) + c);
+                xv[u] = ok ? v : z;
+            } else {
+                xv[u] = ok ? load_piece<uint16_t>(src + row * (from_a ? p.a_stride : p.b_stride), c,
+                                                  from_a ? p.c_a : p.c_b, from_a ? p.vec_a : p.vec_b)
+                           : z;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < G_IT; ++u) {
+            const int i = tid + u * CONV_BLOCK;
+            const int pix = i / (NCO / HE), pc = i % (NCO / HE);
+            const int y = y0 + pix / TW, x = x0 + pix % TW;
+            const bool ok = y < H && x < W;
+            const int64_t row = ok ? frame_row0 + (int64_t)y * W + x : frame_row0;
+            if (g.whole) {
+                const u32x4 v = *reinterpret_cast<const u32x4 *>(gy + row * g.gy_stride + cob * NCO + pc * HE);
+                gv[u] = ok ? v : z;
+            } else {
+                gv[u] = ok ? load_piece<uint16_t>(gy + row * g.gy_stride, cob * NCO + pc * HE, p.c_out, g.vec_g) : z;
+            }
+        }
+    };
+    for (int tile = t0; tile < t1; ++tile) {
+        load(tile);
+        // ---- transposed writes: halo pixel (hr, hc) feeds column hc - kx of copy kx
+#pragma unroll
+        for (int u = 0; u < IN_IT; ++u) {
+            const int j = tid + u * CONV_BLOCK;
+            if (j >= IN_PIECES) continue;
+            const int jq = j / (HH * HWD * 2);
+            const int rem = j % (HH * HWD * 2), pix = rem >> 1, pc = rem & 1;
+            const int hr = pix / HWD, hc = pix - hr * HWD;
+            uint16_t e[HE];
+            __builtin_memcpy(e, &xv[u], 16);
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                const int c = hc - kx;
+                if (c < 0 || c >= TW) continue;
+                uint8_t *base = s_x + kx * WB_KXS + (jq * CK + pc * HE) * WB_CIP + (hr * TW + c) * 2;
+#pragma unroll
+                for (int k = 0; k < HE; ++k) *reinterpret_cast<uint16_t *>(base + k * WB_CIP) = e[k];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < G_IT; ++u) {
+            const int i = tid + u * CONV_BLOCK;
+            const int pix = i / (NCO / HE), pc = i % (NCO / HE);
+            uint16_t e[HE];
+            __builtin_memcpy(e, &gv[u], 16);
+            uint8_t *base = s_g + (pc * HE) * WB_COP + pix * 2;
+#pragma unroll
+            for (int k = 0; k < HE; ++k) *reinterpret_cast<uint16_t *>(base + k * WB_COP) = e[k];
+        }
+        __syncthreads();
+        // ---- one K step (the 32 pixels of a tile row) per row and tap
+#pragma unroll 2
+        for (int r = 0; r < TH; ++r) {
+            const bf16x8 b = *reinterpret_cast<const bf16x8 *>(s_g + (o * 16 + l16) * WB_COP + (r * TW + kq * 8) * 2);
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    const bf16x8 a = *reinterpret_cast<const bf16x8 *>(
+                        s_x + kx * WB_KXS + (h * 16 + l16) * WB_CIP + ((r + ky) * TW + kq * 8) * 2);
+                    acc[ky * 3 + kx] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[ky * 3 + kx], 0, 0, 0);
+                }
+        }
+        __syncthreads();
+    }
+    // this wave's block of the workgroup's partial
+    // (D of 16x16x32: column = lane & 15 (output channel), row = 4 (lane >> 4) + reg (input channel))
+    float *out = g.part + (((int64_t)grp * g.n_cib + cib) * g.n_cob + cob) * (9 * WG_CI * NCO);
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) out[t * 1024 + (h * 16 + 4 * kq + i) * NCO + o * 16 + l16] = acc[t][i];
+}
+
 // dW (f32, HWIO [3][3][c_a+c_b][c_out]) = the groups' partials summed in
 // group order (f64), channels mapped back from the chunk layout.
 __global__ __launch_bounds__(SHPL_BLOCK) void k_wgrad_reduce(const float *part, int n_groups, int n_cib, int n_cob,
@@ -1227,7 +1367,7 @@ extern "C" int shpl_conv3x3(int dtype, int n_frames, int64_t h, int64_t w, const
     if (pl.n_tiles == 0) return SHPL_OK;
     if (!d_out || (c_a > 0 && !d_a)) return SHPL_ERR_ARG;
     const int esz = dtype == SHPL_F32 ? 4 : 2, he = 16 / esz;
-    ConvArgs a;
+    ConvArgs a = {};  // every field the forward does not set (out2: the dgrad split) is zero
     a.n_frames = n_frames;
     a.h = (int)h;
     a.w = (int)w;
@@ -1509,7 +1649,7 @@ extern "C" int shpl_conv3x3_wgrad(int dtype, int n_frames, int64_t h, int64_t w,
     uint8_t *ws = reinterpret_cast<uint8_t *>(d_ws);
     a.row_ptr = pooled ? reinterpret_cast<const int32_t *>(ws) : nullptr;
     a.c_out = (int)c_out;
-    WgArgs g;
+    WgArgs g = {};
     g.gy = d_gy;
     g.gy_stride = gy_stride;
     g.n_cib = wp.n_cib;
@@ -1534,7 +1674,7 @@ extern "C" int shpl_conv3x3_wgrad(int dtype, int n_frames, int64_t h, int64_t w,
         if (pooled)
             hipLaunchKernelGGL((k_conv3x3_wgrad<uint16_t, true>), grid, dim3(CONV_BLOCK), 0, s, a, g);
         else
-            hipLaunchKernelGGL((k_conv3x3_wgrad<uint16_t, false>), grid, dim3(CONV_BLOCK), 0, s, a, g);
+            hipLaunchKernelGGL(k_wgrad_bf16, grid, dim3(CONV_BLOCK), 0, s, a, g);
     }
     SHPL_LAUNCH_CHECK();
     const int64_t n_out = 9 * (c_a + c_b) * c_out;

@@ -608,7 +608,7 @@ struct CsrLayout {
 };
 
 CsrLayout csr_layout(int64_t nnz_cap) {
-    CsrLayout l;
+    CsrLayout l = {};
     const size_t cap = (size_t)(nnz_cap > 0 ? nnz_cap : 1);
     l.tmp = 0;
     l.kbuf = align_up(sizeof(uint64_t) * cap, 256);
@@ -678,7 +678,7 @@ extern "C" int shpl_build_csr(int direction, int order, int n_frames, const int6
     }
     CsrIn c{direction, order, n_frames, d_frame_off, d_frame_nnz, keys_per_frame, 0,
             d_cell, d_col, d_pix, d_val};
-    SegIn g;
+    SegIn g = {};
     g.S = (int)S;
     g.n_bins = (int)n_bins;
     g.log_bin = log_bin;

@@ -46,7 +46,7 @@ struct Geometry {
 };
 
 Geometry make_geometry(double im_w, double im_h, double bv_h, double bv_w, double s_img, double s_bv) {
-    Geometry g;
+    Geometry g = {};
     g.im_w = im_w;
     g.im_h = im_h;
     g.s_img = s_img;
@@ -70,7 +70,7 @@ struct Produced {
 
 __device__ __forceinline__ Produced produce(const Geometry &g, double ur, double vr, int64_t vx,
                                             int64_t vz) {
-    Produced o;
+    Produced o = {};
     double u = floor(__ddiv_rn(ur, g.s_img));
     double v = floor(__ddiv_rn(vr, g.s_img));
     if (u >= g.wq) u = g.wq - 1.0;
@@ -95,7 +95,7 @@ struct FusedStage {
     const void *vox;
     int64_t vstride;
     const double *P;
-    Geometry g;
+    Geometry g = {};
     const float *mval;
     int32_t *cell, *pix;
     float *val;
@@ -191,7 +191,7 @@ struct ProduceStage {  // produce_sparse_pooling_input (in-place img_index updat
     int64_t bstride;
     double *img;  // 3 rows, stride ld
     int64_t ld;
-    Geometry g;
+    Geometry g = {};
     int64_t *mij, *flip;
     int32_t *cell, *pix;
     uint32_t *err;

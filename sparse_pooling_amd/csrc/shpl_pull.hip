@@ -443,7 +443,7 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse_long(const Feat f, const 
 bool aligned(const void *ptr, int64_t a) { return ((uintptr_t)ptr) % (uintptr_t)a == 0; }
 
 struct Plan {
-    Feat f;
+    Feat f = {};
     int64_t n_dst;
     bool v16;
     int dtype;
