@@ -239,9 +239,10 @@ extern "C" int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, con
     uint64_t *srt = (uint64_t *)((char *)d_ws + half);
     hipStream_t s = (hipStream_t)stream;
     const int64_t per_map = (int64_t)g.nx * g.nz;
+    // the maps' zeros: a streaming kernel (hipMemsetAsync's fill ran at ~2.2 TB/s, beside k_dense)
     if (d_height_maps)
-        SHPL_HIP_CHECK(hipMemsetAsync(d_height_maps, 0, sizeof(double) * (size_t)(per_map * num_slices * n_frames), s));
-    if (d_density_map) SHPL_HIP_CHECK(hipMemsetAsync(d_density_map, 0, sizeof(double) * (size_t)(per_map * n_frames), s));
+        SHPL_HIP_CHECK(zero_fill(d_height_maps, sizeof(double) * (size_t)(per_map * num_slices * n_frames), s));
+    if (d_density_map) SHPL_HIP_CHECK(zero_fill(d_density_map, sizeof(double) * (size_t)(per_map * n_frames), s));
     if (points_dtype == SHPL_F64)
         hipLaunchKernelGGL(k_bev_frame<double>, dim3(n_frames), dim3(BEV_BLOCK), 0, s, g, d_point_offsets,
                            d_point_counts, d_points,

@@ -104,4 +104,32 @@ inline int grid_for(int64_t work, int64_t per_block, int cap) {
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+namespace {
+// Zeros at the streaming rate: one nontemporal 16-byte store per thread over
+// a full grid (hipMemsetAsync's fill kernel ran at ~2.2 TB/s on MI355X; this
+// shape measured 6.7 TB/s, scripts/calib.hip). Sizes in 8-byte words.
+__global__ __launch_bounds__(SHPL_BLOCK) void k_zero_fill(uint64_t *p, uint64_t n8) {
+    const uint64_t i = (uint64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x;
+    typedef uint32_t u32x4z __attribute__((ext_vector_type(4)));
+    if (2 * i + 1 < n8) {
+        __builtin_nontemporal_store(u32x4z{0u, 0u, 0u, 0u}, reinterpret_cast<u32x4z *>(p) + i);
+    } else if (2 * i < n8) {
+        p[2 * i] = 0;  // an odd word count's last word
+    }
+}
+
+// Zero `bytes` (a multiple of 8) at `ptr` on `s`; hipMemsetAsync when the
+// pointer is not 16-byte aligned or the size not a whole number of words.
+inline hipError_t zero_fill(void *ptr, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return hipSuccess;
+    if (((uintptr_t)ptr & 15u) || (bytes & 7u)) return hipMemsetAsync(ptr, 0, bytes, s);
+    const uint64_t n8 = bytes / 8, threads = (n8 + 1) / 2;
+    const uint64_t blocks = (threads + SHPL_BLOCK - 1) / SHPL_BLOCK;
+    if (blocks >= (1ull << 31)) return hipMemsetAsync(ptr, 0, bytes, s);
+    hipLaunchKernelGGL(k_zero_fill, dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, s, reinterpret_cast<uint64_t *>(ptr),
+                       n8);
+    return hipGetLastError();
+}
+}  // namespace
+
 }  // namespace shpl

@@ -997,9 +997,9 @@ __device__ __forceinline__ void wg_stage(const ConvArgs &p, const WgArgs &g, int
 }
 
 template <typename T, bool POOLED>
-__global__ __launch_bounds__(CONV_BLOCK, 2) void k_conv3x3_wgrad(const ConvArgs p, const WgArgs g) {
+__global__ __launch_bounds__(CONV_BLOCK, POOLED ? 1 : 2) void k_conv3x3_wgrad(const ConvArgs p, const WgArgs g) {
     typedef Elem<T> E;
-    constexpr int CK = E::CK, HE = E::HE, CB = E::CB, NQ = WG_CI / CK;
+    constexpr int CK = E::CK, CB = E::CB, NQ = WG_CI / CK;
     constexpr int NPIX = HH * HWD;
     __shared__ __attribute__((aligned(16))) uint8_t s_x[NQ * NPIX * CB];
     __shared__ __attribute__((aligned(16))) uint8_t s_g[TH * TW * NCO * sizeof(T)];

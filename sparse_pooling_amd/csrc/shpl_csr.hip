@@ -55,7 +55,6 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_pack(int64_t nnz, const int64_t 
 // ------------------------------------------------------------------ CSR
 constexpr int CSR_BLOCK = 1024;           // one workgroup per frame
 constexpr int CSR_TILES = 16384;          // LDS tile counters (64 KiB)
-constexpr int CSR_PER_THREAD = CSR_TILES / CSR_BLOCK;
 
 struct CsrIn {
     int direction, order, n_frames;

@@ -202,7 +202,6 @@ template <typename T, int VEC, bool GROUP, int W>
 __device__ __forceinline__ void walk_run(const Feat &f, const Ents &e, int64_t s, int32_t key, uint32_t c,
                                          float (&acc)[VEC], const IdxBatch<GROUP, W> *first = nullptr) {
     typedef Chunk<T, VEC> C;
-    const int64_t nnz = e.n;
     const T *sc = reinterpret_cast<const T *>(f.src) + f.src_off + (int64_t)c * VEC;
 #pragma unroll
     for (int j = 0; j < VEC; ++j) acc[j] = 0.0f;
