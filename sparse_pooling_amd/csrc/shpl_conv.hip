@@ -94,6 +94,7 @@ struct ConvArgs {
     void *out2;
     int64_t out2_stride;
     int c_split;
+    bool vec_out;  // out (and out2) rows and c_split 16-byte aligned: 16-byte stores
     double *part;  // STATS: [(co_block*32 + co)*2 + stat][n_tiles]
 };
 
@@ -191,12 +192,13 @@ struct HaloRuns {
     int64_t *scan;                        // [SHPL_BLOCK/64+1]
 };
 
-// Lists the runs of the halo tile of output tile (f, y0, x0): per halo row
-// the entry range of cells [x0-1, x0+TW+1) (row pointers + counting the
+// Lists the runs of the HHT-row halo of output tile (f, y0, x0): per halo
+// row the entry range of cells [x0-1, x0+TW+1) (row pointers + counting the
 // row's sorted entries below each bound), then one block scan in entry
 // order. Every thread of the 256 calls it.
+template <int HHT = HH>
 __device__ int find_runs(const ConvArgs &p, int f, int y0, int x0, const HaloRuns &r) {
-    constexpr int NPIX = HH * HWD;
+    constexpr int NPIX = HHT * HWD;
     const int tid = threadIdx.x;
     const int H = p.h, W = p.w;
     const int64_t frame_row0 = (int64_t)f * H * W;
@@ -205,14 +207,14 @@ __device__ int find_runs(const ConvArgs &p, int f, int y0, int x0, const HaloRun
     // 64 at a time against the two cell bounds (ballots), the rows' loads in
     // flight together: two round trips for rows of up to 64 entries.
     const int lane = tid & 63, wave = tid >> 6;
-    constexpr int RPW = (HH + 3) / 4;  // rows per wave
+    constexpr int RPW = (HHT + 3) / 4;  // rows per wave
     int32_t ra[RPW], rb[RPW], kl[RPW], kh[RPW];
 #pragma unroll
     for (int u = 0; u < RPW; ++u) {
         const int k = wave + 4 * u, y = y0 - 1 + k;
         ra[u] = rb[u] = 0;
         kl[u] = kh[u] = 0;
-        if (k < HH && y >= 0 && y < H) {
+        if (k < HHT && y >= 0 && y < H) {
             ra[u] = p.row_ptr[(int64_t)f * (H + 1) + y];
             rb[u] = p.row_ptr[(int64_t)f * (H + 1) + y + 1];
             kl[u] = (int32_t)(frame_row0 + (int64_t)y * W + (x0 > 0 ? x0 - 1 : 0));
@@ -231,7 +233,7 @@ __device__ int find_runs(const ConvArgs &p, int f, int y0, int x0, const HaloRun
             n_lo += __popcll(__ballot(dd < kl[u]));
             n_hi += __popcll(__ballot(dd < kh[u]));
         }
-        if (lane == 0 && k < HH) {
+        if (lane == 0 && k < HHT) {
             r.lo[k] = ra[u] + n_lo;
             r.pre[k + 1] = n_hi - n_lo;
         }
@@ -239,10 +241,10 @@ __device__ int find_runs(const ConvArgs &p, int f, int y0, int x0, const HaloRun
     __syncthreads();
     if (tid == 0) {
         r.pre[0] = 0;
-        for (int k = 0; k < HH; ++k) r.pre[k + 1] += r.pre[k];
+        for (int k = 0; k < HHT; ++k) r.pre[k + 1] += r.pre[k];
     }
     __syncthreads();
-    const int n_ent = r.pre[HH];
+    const int n_ent = r.pre[HHT];
     int n_run = 0, n_tail = 0;
     for (int base = 0; base < n_ent; base += CONV_BLOCK) {
         const int j = base + tid;
@@ -283,12 +285,12 @@ __device__ int find_runs(const ConvArgs &p, int f, int y0, int x0, const HaloRun
 // outside the map. Pooled chunks: zeros where no entry lands, each run's sum
 // elsewhere (disjoint cells: no barrier between the two). The caller
 // synchronises after.
-template <typename T, bool POOLED, int PSTR, bool SWZ = false>
+template <typename T, bool POOLED, int PSTR, bool SWZ = false, int HHT = HH>
 __device__ __forceinline__ void stage_halo(const ConvArgs &p, int q, int f, int y0, int x0, uint8_t *s_in,
                                            const HaloRuns &r, int n_run) {
     typedef Elem<T> E;
     constexpr int CK = E::CK, HE = E::HE, NP = E::NP;
-    constexpr int IN_PIECES = HH * HWD * NP;
+    constexpr int IN_PIECES = HHT * HWD * NP;
     constexpr int IN_IT = (IN_PIECES + CONV_BLOCK - 1) / CONV_BLOCK;
     const int tid = threadIdx.x;
     const int H = p.h, W = p.w;
@@ -331,17 +333,31 @@ __device__ __forceinline__ void stage_halo(const ConvArgs &p, int q, int f, int 
     }
 }
 
-#define SHPL_HALO_RUNS_LDS(POOLED)                                                                            \
-    __shared__ int32_t s_lo[HH], s_pre[HH + 1];                                                              \
-    __shared__ int32_t s_run_pix[POOLED ? HH * HWD : 1], s_run_e[POOLED ? HH * HWD : 1],                     \
-        s_run_end[POOLED ? HH * HWD : 1], s_run_src[POOLED ? HH * HWD : 1];                                 \
-    __shared__ float s_run_val[POOLED ? HH * HWD : 1];                                                       \
-    __shared__ uint8_t s_occ[POOLED ? HH * HWD : 1];                                                         \
+#define SHPL_HALO_RUNS_LDS(POOLED, HHT)                                                                       \
+    __shared__ int32_t s_lo[HHT], s_pre[HHT + 1];                                                            \
+    __shared__ int32_t s_run_pix[POOLED ? HHT * HWD : 1], s_run_e[POOLED ? HHT * HWD : 1],                   \
+        s_run_end[POOLED ? HHT * HWD : 1], s_run_src[POOLED ? HHT * HWD : 1];                               \
+    __shared__ float s_run_val[POOLED ? HHT * HWD : 1];                                                      \
+    __shared__ uint8_t s_occ[POOLED ? HHT * HWD : 1];                                                        \
     __shared__ int64_t s_scan[SHPL_BLOCK / 64 + 1];                                                          \
     const HaloRuns runs{s_lo, s_pre, s_run_pix, s_run_e, s_run_end, s_run_src, s_run_val, s_occ, s_scan};
 
+// Forward tile shape: output rows per wave, 2 at f32 (8 x 32 tiles) and 4 at
+// bf16 (16 x 32 tiles). A bf16 chunk's MFMAs are 16x faster than an f32
+// chunk's: the taller tile halves the staging round trips, halo rows and
+// weight rows per output pixel, and each wave reuses every A operand it reads
+// for up to three kernel rows (0.75 KB of LDS reads per MFMA instead of 1.5).
+#ifndef SHPL_BF16_RPW
+#define SHPL_BF16_RPW 2
+#endif
+template <typename T>
+struct ConvTile {
+    static constexpr int RPW = sizeof(T) == 2 ? SHPL_BF16_RPW : 2;
+    static constexpr int TH = 4 * RPW, HH = TH + 2;
+};
+
 // Stages input chunk q of output tile (f, y0, x0) -- its 9x32 weight rows
-// and its 10x34 halo -- into one LDS buffer pair (swizzled 32-byte rows).
+// and its HH x 34 halo -- into one LDS buffer pair (swizzled 32-byte rows).
 // Weights and dense halo chunks are LDS-DMAs (lane k of the wave fills slot
 // k: it loads the piece the swizzle puts there); pooled chunks are computed
 // (stage_halo). The caller waits and synchronises.
@@ -349,8 +365,8 @@ template <typename T, bool POOLED>
 __device__ __forceinline__ void conv_stage(const ConvArgs &p, int q, int f, int y0, int x0, const T *wq, uint8_t *s_in,
                                            uint8_t *s_w, const HaloRuns &runs, int n_run) {
     typedef Elem<T> E;
-    constexpr int CK = E::CK, HE = E::HE, NP = E::NP;
-    constexpr int IN_PIECES = HH * HWD * NP, W_PIECES = W_ROWS * NP;
+    constexpr int CK = E::CK, HE = E::HE, NP = E::NP, HHT = ConvTile<T>::HH;
+    constexpr int IN_PIECES = HHT * HWD * NP, W_PIECES = W_ROWS * NP;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int u = 0; u < (W_PIECES + CONV_BLOCK - 1) / CONV_BLOCK; ++u) {
@@ -381,20 +397,24 @@ __device__ __forceinline__ void conv_stage(const ConvArgs &p, int q, int f, int 
                                 s_in + base * 16, lane);
         }
     } else {
-        stage_halo<T, true, E::CB, true>(p, q, f, y0, x0, s_in, runs, n_run);
+        stage_halo<T, true, E::CB, true, HHT>(p, q, f, y0, x0, s_in, runs, n_run);
     }
 }
 
 template <typename T, bool POOLED, bool STATS>
 __global__ __launch_bounds__(CONV_BLOCK, 4) void k_conv3x3(const ConvArgs p) {
     typedef Elem<T> E;
-    constexpr int CK = E::CK, NP = E::NP;
+    constexpr int CK = E::CK, NP = E::NP, RPW = ConvTile<T>::RPW, HHT = ConvTile<T>::HH;
     static_assert(NP == 2, "two 16-byte pieces per LDS row (the swizzle)");
-    constexpr int IN_BYTES = HH * HWD * NP * 16, W_BYTES = W_ROWS * NP * 16;
-    __shared__ __attribute__((aligned(16))) uint8_t s_in[IN_BYTES];
-    __shared__ __attribute__((aligned(16))) uint8_t s_w[W_BYTES];
+    constexpr int IN_BYTES = HHT * HWD * NP * 16, W_BYTES = W_ROWS * NP * 16;
+    // the output rows' transpose (epilogue) reuses the chunk buffers: 4 waves x 32 pixels x OPITCH
+    constexpr int OPITCH = NCO * (int)sizeof(T) + 16;
+    static_assert(4 * 32 * OPITCH <= IN_BYTES + W_BYTES, "epilogue rows fit the chunk buffers");
+    __shared__ __attribute__((aligned(16))) uint8_t s_buf[IN_BYTES + W_BYTES];
+    uint8_t *const s_in = s_buf, *const s_w = s_buf + IN_BYTES;
     __shared__ float s_red[4][2][NCO];
-    SHPL_HALO_RUNS_LDS(POOLED)
+    __shared__ __attribute__((aligned(16))) float s_par[3][NCO];  // center, scale, shift of the block's channels
+    SHPL_HALO_RUNS_LDS(POOLED, HHT)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int pl = lane & 31, hf = lane >> 5;
@@ -403,16 +423,21 @@ __global__ __launch_bounds__(CONV_BLOCK, 4) void k_conv3x3(const ConvArgs p) {
     const int f = tile / p.tiles_per_frame;
     const int t_in = tile - f * p.tiles_per_frame;
     const int ty = t_in / p.tiles_x, tx = t_in - ty * p.tiles_x;
-    const int y0 = ty * TH, x0 = tx * TW;
+    const int y0 = ty * ConvTile<T>::TH, x0 = tx * TW;
     const int H = p.h, W = p.w;
     const int64_t frame_row0 = (int64_t)f * H * W;
     const int Q = p.qa + p.qb;
 
-    const int n_run = POOLED ? find_runs(p, f, y0, x0, runs) : 0;
+    if (tid < 3 * NCO) {
+        const int k = tid >> 5, c = cob * NCO + (tid & 31);
+        const float *src = k == 0 ? p.center : k == 1 ? p.scale : p.shift;
+        s_par[k][tid & 31] = src && c < p.c_out ? src[c] : 0.0f;
+    }
+    const int n_run = POOLED ? find_runs<HHT>(p, f, y0, x0, runs) : 0;  // (s_par: published by the next barrier)
 
-    f32x16 acc[2];
+    f32x16 acc[RPW];
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int m = 0; m < RPW; ++m)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[m][i] = 0.0f;
 
@@ -428,83 +453,144 @@ __global__ __launch_bounds__(CONV_BLOCK, 4) void k_conv3x3(const ConvArgs p) {
         __syncthreads();
         const uint8_t *si = s_in, *sw = s_w;
         // ---- 9 taps of MFMA over chunk q
+        if constexpr (sizeof(T) == 4) {
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
+            for (int ky = 0; ky < 3; ++ky) {
 #pragma unroll
-            for (int kx = 0; kx < 3; ++kx) {
-                const uint8_t *wrow = sw + piece_off<true, 0>((ky * 3 + kx) * NCO + pl, hf);
+                for (int kx = 0; kx < 3; ++kx) {
+                    const uint8_t *wrow = sw + piece_off<true, 0>((ky * 3 + kx) * NCO + pl, hf);
 #pragma unroll
-                for (int m = 0; m < 2; ++m) {
-                    const uint8_t *arow = si + piece_off<true, 0>((2 * wave + m + ky) * HWD + pl + kx, hf);
-                    if constexpr (sizeof(T) == 4) {
-                        // lane half h supplies channels 4h+s of the chunk to MFMA s (A and B alike)
+                    for (int m = 0; m < RPW; ++m) {
+                        const uint8_t *arow = si + piece_off<true, 0>((RPW * wave + m + ky) * HWD + pl + kx, hf);
+                        // lane half h supplies channels 4h+s of the chunk to MFMA s (both operands)
                         const f32x4 a4 = *reinterpret_cast<const f32x4 *>(arow);
                         const f32x4 b4 = *reinterpret_cast<const f32x4 *>(wrow);
 #pragma unroll
                         for (int s = 0; s < 4; ++s)
-                            acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[s], b4[s], acc[m], 0, 0, 0);
-                    } else {
-                        // channels 0..15 of the chunk; lane half h holds 8h .. 8h+7
-                        const bf16x8 a8 = *reinterpret_cast<const bf16x8 *>(arow);
-                        const bf16x8 b8 = *reinterpret_cast<const bf16x8 *>(wrow);
-                        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a8, b8, acc[m], 0, 0, 0);
+                            acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(b4[s], a4[s], acc[m], 0, 0, 0);
                     }
+                }
+            }
+        } else {
+            // channels 0..15 of the chunk; lane half h holds 8h .. 8h+7. Per kernel
+            // column kx: the three kernel rows' weights, then each of the wave's
+            // RPW + 2 halo rows read once and fed to every output row it reaches.
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                bf16x8 b8[3];
+#pragma unroll
+                for (int ky = 0; ky < 3; ++ky)
+                    b8[ky] = *reinterpret_cast<const bf16x8 *>(sw + piece_off<true, 0>((ky * 3 + kx) * NCO + pl, hf));
+#pragma unroll
+                for (int r = 0; r < RPW + 2; ++r) {
+                    const bf16x8 a8 = *reinterpret_cast<const bf16x8 *>(
+                        si + piece_off<true, 0>((RPW * wave + r) * HWD + pl + kx, hf));
+#pragma unroll
+                    for (int ky = 0; ky < 3; ++ky)
+                        if (r - ky >= 0 && r - ky < RPW)
+                            acc[r - ky] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b8[ky], a8, acc[r - ky], 0, 0, 0);
                 }
             }
         }
         __syncthreads();  // the chunk's buffers are restaged next
     }
 
-    // ---- epilogue: acc element i of subtile m is pixel (y0+2w+m, x0+(i&3)+8(i>>2)+4h), channel pl
-    const int co = cob * NCO + pl;
-    const bool co_ok = co < p.c_out;
-    float cen = 0.0f, scl = 1.0f, sft = 0.0f;
-    if (co_ok) {
-        if (p.center) cen = p.center[co];
-        if (p.scale) scl = p.scale[co];
-        if (p.shift) sft = p.shift[co];
-    }
-    T *out = reinterpret_cast<T *>(p.out);
-    int64_t ostr = p.out_stride;
-    int oc = co;
-    if (p.out2 && co >= p.c_split) {
-        out = reinterpret_cast<T *>(p.out2);
-        ostr = p.out2_stride;
-        oc = co - p.c_split;
-    }
-    float s1 = 0.0f, s2 = 0.0f;
+    // ---- epilogue. The MFMAs take the weights as A and the pixels as B (D =
+    // W^T X^T), so acc element i of subtile m is channel cob*32 + 8(i>>2) +
+    // 4h + (i&3) of pixel (y0 + RPW w + m, x0 + pl): four runs of 4 channels
+    // per lane. A row of 32 pixels goes through LDS (wave-private, rows of
+    // OPITCH bytes) and out as 16-byte pieces, consecutive lanes on
+    // consecutive pieces: 2 (bf16) / 4 (f32) store instructions per row, each
+    // one contiguous 1 KB, instead of 16 two- or four-byte stores (the texture
+    // addresser was the bf16 conv's busiest unit). Blocks whose channels are not
+    // whole or whose rows are not 16-byte aligned store channel by channel.
+    constexpr int HE = E::HE, PPP = NCO / HE;  // channels per piece, pieces per pixel
+    const int x = x0 + pl;
+    const bool fast = p.vec_out && cob * NCO + NCO <= p.c_out;
+    uint8_t *const s_o = s_buf + wave * 32 * OPITCH;
+    float s1[16], s2[16];
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
-        const int y = y0 + 2 * wave + m;
+    for (int i = 0; i < 16; ++i) s1[i] = s2[i] = 0.0f;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int x = x0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
-            if (!(co_ok && y < H && x < W)) continue;
-            float v = acc[m][i];
-            if (STATS) {
-                s1 = __fadd_rn(s1, v);
-                s2 = __fadd_rn(s2, __fmul_rn(v, v));
+    for (int m = 0; m < RPW; ++m) {
+        const int y = y0 + RPW * wave + m;
+        const bool ok = y < H && x < W;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int cl = 8 * g + 4 * hf, c = cob * NCO + cl;  // first channel of the run
+            const f32x4 cen = *reinterpret_cast<const f32x4 *>(&s_par[0][cl]);
+            const f32x4 scl = *reinterpret_cast<const f32x4 *>(&s_par[1][cl]);
+            const f32x4 sft = *reinterpret_cast<const f32x4 *>(&s_par[2][cl]);
+            T o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float v = acc[m][4 * g + j];
+                if (STATS && ok) {
+                    s1[4 * g + j] = __fadd_rn(s1[4 * g + j], v);
+                    s2[4 * g + j] = __fadd_rn(s2[4 * g + j], __fmul_rn(v, v));
+                }
+                if (p.center) v = __fsub_rn(v, cen[j]);
+                if (p.scale) v = __fmul_rn(v, scl[j]);
+                if (p.shift) v = __fadd_rn(v, sft[j]);
+                if (p.act == 1) v = v > 0.0f ? v : 0.0f;
+                o[j] = E::back(v);
             }
-            if (p.center) v = __fsub_rn(v, cen);
-            if (p.scale) v = __fmul_rn(v, scl);
-            if (p.shift) v = __fadd_rn(v, sft);
-            if (p.act == 1) v = v > 0.0f ? v : 0.0f;
-            out[(frame_row0 + (int64_t)y * W + x) * ostr + oc] = E::back(v);
+            if (fast) {
+                __builtin_memcpy(s_o + pl * OPITCH + cl * sizeof(T), o, sizeof(o));
+            } else if (ok) {
+                const int64_t row = frame_row0 + (int64_t)y * W + x;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (c + j >= p.c_out) break;
+                    T *d = p.out2 && c + j >= p.c_split
+                               ? reinterpret_cast<T *>(p.out2) + row * p.out2_stride + (c + j - p.c_split)
+                               : reinterpret_cast<T *>(p.out) + row * p.out_stride + c + j;
+                    *d = o[j];
+                }
+            }
+        }
+        if (fast) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's row is in LDS (one wave: in order)
+#pragma unroll
+            for (int k = 0; k < 32 * PPP / 64; ++k) {
+                const int pc = lane + 64 * k, px = pc / PPP, pi = pc % PPP;
+                const u32x4 v = *reinterpret_cast<const u32x4 *>(s_o + px * OPITCH + pi * 16);
+                if (y < H && x0 + px < W) {
+                    const int64_t row = frame_row0 + (int64_t)y * W + x0 + px;
+                    const int c = cob * NCO + pi * HE;
+                    T *d = p.out2 && c >= p.c_split
+                               ? reinterpret_cast<T *>(p.out2) + row * p.out2_stride + (c - p.c_split)
+                               : reinterpret_cast<T *>(p.out) + row * p.out_stride + c;
+                    *reinterpret_cast<u32x4 *>(d) = v;
+                }
+            }
         }
     }
     if (STATS) {
-        s1 = __fadd_rn(s1, __shfl_xor(s1, 32, 64));
-        s2 = __fadd_rn(s2, __shfl_xor(s2, 32, 64));
-        if (hf == 0) {
-            s_red[wave][0][pl] = s1;
-            s_red[wave][1][pl] = s2;
+        // per channel: sum over the 32 pixels of the lane half (butterfly), then
+        // over the 4 waves in double
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+#pragma unroll
+            for (int off = 1; off < 32; off <<= 1) {
+                s1[i] = __fadd_rn(s1[i], __shfl_xor(s1[i], off, 64));
+                s2[i] = __fadd_rn(s2[i], __shfl_xor(s2[i], off, 64));
+            }
+        }
+        if (pl == 0) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int cl = 8 * (i >> 2) + 4 * hf + (i & 3);
+                s_red[wave][0][cl] = s1[i];
+                s_red[wave][1][cl] = s2[i];
+            }
         }
         __syncthreads();
         if (tid < 2 * NCO) {
             const int st = tid >> 5, c = tid & 31;
-            double s = 0.0;
-            for (int w = 0; w < 4; ++w) s += (double)s_red[w][st][c];
-            p.part[((int64_t)(cob * NCO + c) * 2 + st) * p.n_tiles + tile] = s;
+            double sum = 0.0;
+            for (int w = 0; w < 4; ++w) sum += (double)s_red[w][st][c];
+            p.part[((int64_t)(cob * NCO + c) * 2 + st) * p.n_tiles + tile] = sum;
         }
     }
 }
@@ -1003,7 +1089,7 @@ __global__ __launch_bounds__(CONV_BLOCK, POOLED ? 1 : 2) void k_conv3x3_wgrad(co
     constexpr int NPIX = HH * HWD;
     __shared__ __attribute__((aligned(16))) uint8_t s_x[NQ * NPIX * CB];
     __shared__ __attribute__((aligned(16))) uint8_t s_g[TH * TW * NCO * sizeof(T)];
-    SHPL_HALO_RUNS_LDS(POOLED)
+    SHPL_HALO_RUNS_LDS(POOLED, HH)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l16 = lane & 15, kq = lane >> 4;
     const int grp = blockIdx.x, cib = blockIdx.y, cob = blockIdx.z;
@@ -1268,8 +1354,10 @@ struct ConvPlan {
     size_t wp_bytes, rp_bytes, part_bytes, total;
 };
 
+// th: output tile rows -- the forward's ConvTile (8 f32, 16 bf16) unless the
+// weight gradient asks for its own 8.
 int conv_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_t c_b, int64_t c_out, bool pooled,
-              bool stats, ConvPlan *pl) {
+              bool stats, ConvPlan *pl, int th = 0) {
     if (dtype != SHPL_F32 && dtype != SHPL_BF16) return SHPL_ERR_ARG;
     if (n_frames < 0 || h < 0 || w < 0 || c_a < 0 || c_b < 0 || c_out < 1 || c_a + c_b < 1) return SHPL_ERR_BAD_SHAPE;
     if (h > (1 << 20) || w > (1 << 20) || c_a + c_b > (1 << 16) || c_out > (1 << 16)) return SHPL_ERR_BAD_SHAPE;
@@ -1280,7 +1368,8 @@ int conv_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_
     pl->qb = (int)((c_b + pl->ck - 1) / pl->ck);
     pl->n_cob = (int)((c_out + NCO - 1) / NCO);
     pl->tiles_x = (int)((w + TW - 1) / TW);
-    pl->tiles_y = (int)((h + TH - 1) / TH);
+    if (th == 0) th = dtype == SHPL_F32 ? ConvTile<float>::TH : ConvTile<uint16_t>::TH;
+    pl->tiles_y = (int)((h + th - 1) / th);
     pl->tiles_per_frame = pl->tiles_x * pl->tiles_y;
     pl->n_tiles = (int64_t)n_frames * pl->tiles_per_frame;
     if (pl->n_tiles >= (1LL << 31) || (int64_t)n_frames * h * w >= (1LL << 31)) return SHPL_ERR_BAD_SHAPE;
@@ -1400,6 +1489,7 @@ extern "C" int shpl_conv3x3(int dtype, int n_frames, int64_t h, int64_t w, const
     a.out = d_out;
     a.out_stride = out_stride;
     a.c_out = (int)c_out;
+    a.vec_out = aligned16(d_out) && out_stride % he == 0;
     hipStream_t s = (hipStream_t)stream;
     if (dtype == SHPL_F32) return conv_launch<float>(pl, a, pooled, stats, d_weights, d_frame_off, d_stats, s);
     return conv_launch<uint16_t>(pl, a, pooled, stats, d_weights, d_frame_off, d_stats, s);
@@ -1553,6 +1643,8 @@ extern "C" int shpl_conv3x3_dgrad(int dtype, int n_frames, int64_t h, int64_t w,
     a.out2 = d_dx_b;
     a.out2_stride = dx_b_stride;
     a.c_split = (int)c_split;
+    a.vec_out = (!d_dx || (aligned16(d_dx) && dx_stride % he == 0)) &&
+                (!d_dx_b || (aligned16(d_dx_b) && dx_b_stride % he == 0 && c_split % he == 0));
     hipStream_t s = (hipStream_t)stream;
     if (dtype == SHPL_F32) return conv_launch<float>(pl, a, false, false, d_weights, nullptr, nullptr, s, 1);
     return conv_launch<uint16_t>(pl, a, false, false, d_weights, nullptr, nullptr, s, 1);
@@ -1567,7 +1659,7 @@ struct WgPlan {
 
 int wgrad_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_t c_b, int64_t c_out, bool pooled,
                WgPlan *wp) {
-    int rc = conv_plan(dtype, n_frames, h, w, c_a, c_b, c_out, pooled, false, &wp->cp);
+    int rc = conv_plan(dtype, n_frames, h, w, c_a, c_b, c_out, pooled, false, &wp->cp, TH);
     if (rc) return rc;
     const int Q = wp->cp.qa + wp->cp.qb;
     wp->n_cib = (Q * wp->cp.ck + WG_CI - 1) / WG_CI;
