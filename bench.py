@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-parallel", action="store_true",
+                    help="skip the frame-parallel (one process per core, up to 16) CPU-baseline sample")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the layer's streaming pass after the index build instead of beside it")
     ap.add_argument("--groups", type=int, default=1,
@@ -145,6 +147,35 @@ def cpu_baseline(spec, frames_np, budget_s, dual, backward=False):
                        + ((" (both directions, forward + gradients, f32)" if backward else
                            " (both directions, forward only)") if dual else "")
                        + f", single thread, {os.cpu_count()} host cpus visible")}
+
+
+def _cpu_worker(q, barrier, spec, frames_np, budget_s, dual, backward):
+    barrier.wait()
+    q.put(cpu_baseline(spec, frames_np, budget_s, dual, backward))
+
+
+def cpu_baseline_parallel(spec, frames_np, budget_s, dual, backward=False):
+    """Frame-parallel form of cpu_baseline (single thread and
+    N-process frame-parallel): one spawned process per host core, up to 16
+    (the CPU share of one GPU on the box), each starting at its own frame,
+    started together; the aggregate is the sum of the processes' rates."""
+    import multiprocessing as mp
+    n = max(1, min(16, len(os.sched_getaffinity(0))))
+    ctx = mp.get_context("spawn")
+    q, bar = ctx.Queue(), ctx.Barrier(n)
+    procs = [ctx.Process(target=_cpu_worker,
+                         args=(q, bar, spec, frames_np[i:] + frames_np[:i], budget_s, dual, backward))
+             for i in range(n)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=10 * budget_s + 300) for _ in procs]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    return {"value": round(sum(r["value"] for r in res), 3), "unit": "frames/s", "cores": n, "processes": n,
+            "sample": f"{n} processes started together, each the single-thread sample ({budget_s:.0f} s) "
+                      f"from its own first frame"}
 
 
 def main():
@@ -288,6 +319,8 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(spec, frames[: min(F, 64)], args.cpu_seconds, dual, backward)
+        if not args.no_cpu_parallel:
+            cpu["parallel"] = cpu_baseline_parallel(spec, frames[: min(F, 64)], args.cpu_seconds, dual, backward)
 
     if rank == 0:
         total_frames = F * world * args.steps
