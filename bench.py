@@ -183,11 +183,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # SHPL_DIST_BACKEND=gloo: rehearsal of the N>1 path with several ranks on
+    # one GPU (ranks share device LOCAL_RANK mod the device count); the
+    # driver's runs use RCCL ("nccl"), one rank per GPU.
+    backend = os.environ.get("SHPL_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from sparse_pooling_amd import dist as sd, pipeline, synth
 

@@ -23,6 +23,16 @@ def frame_seeds(rank, frames_per_rank, base=100000):
     return [base * rank + f for f in range(frames_per_rank)]
 
 
+def _coll_device(device):
+    """Where the control-plane tensors live: on the GPU for RCCL, on the host
+    for gloo (the CPU tests and the one-GPU rehearsal of the N>1 bench)."""
+    if device is None or device.type != "cuda":
+        return "cpu"
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "gloo":
+        return "cpu"
+    return device
+
+
 def _sync(device):
     if device is not None and device.type == "cuda":
         torch.cuda.synchronize(device)
@@ -43,8 +53,7 @@ def timed(fn, steps, device=None):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if on:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device=device if (device is not None and device.type == "cuda") else "cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=_coll_device(device))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed
@@ -53,8 +62,7 @@ def timed(fn, steps, device=None):
 def gather_checksums(value, device=None):
     """All ranks' scalar checksums, rank order."""
     on = dist.is_available() and dist.is_initialized()
-    dev = device if (device is not None and device.type == "cuda") else "cpu"
-    t = torch.tensor([float(value)], dtype=torch.float64, device=dev)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=_coll_device(device))
     if not on:
         return [float(value)]
     out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
