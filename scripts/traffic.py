@@ -55,7 +55,7 @@ def conv(key, dt):
     tj = json.load(open(path)) if os.path.exists(path) else {}
     tj[key] = {"hbm_bytes_per_launch": out[main_k]["fetch_bytes"] + out[main_k]["write_bytes"], "kernels": out,
                "note": (f"{main_k} = the fused conv; FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes; "
-                        "WRITE_SIZE of 4 B/lane stores is uncalibrated (MI355X_MICROARCH.md HBM); mfma_busy_share "
+                        "WRITE_SIZE exact (16 B/lane stores since the LDS-transposed epilogue); mfma_busy_share "
                         "= MFMA busy cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)")}
     json.dump(tj, open(path, "w"), indent=1)
     print(json.dumps(tj[key], indent=1))

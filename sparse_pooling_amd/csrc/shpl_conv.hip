@@ -658,20 +658,44 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_row_ptr(const int32_t *dst, cons
 // Per-channel sum / sum of squares of the pre-activation output, summed over
 // the per-tile partials in a fixed order (deterministic): one block per
 // (channel, statistic).
-__global__ __launch_bounds__(SHPL_BLOCK) void k_stats_reduce(const double *part, int n_tiles, int c_out,
-                                                             double *stats) {
-    __shared__ double red[SHPL_BLOCK];
-    const int ch = blockIdx.x >> 1, st = blockIdx.x & 1;
-    const double *v = part + ((int64_t)ch * 2 + st) * n_tiles;
-    double s = 0.0;
-    for (int i = threadIdx.x; i < n_tiles; i += SHPL_BLOCK) s += v[i];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = SHPL_BLOCK / 2; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-        __syncthreads();
+// Deterministic sums of long strided lists (the per-tile / per-block /
+// per-group partials): thread t adds elements t, t + n_thr, ... into 8
+// independent accumulators (8 loads in flight, then a fixed pairwise
+// combine), the wave and the block then reduce in a fixed order. A thread per
+// list walking it serially (550-4096 dependent loads) cost 0.2-0.3 ms per
+// reduction.
+template <int NT>
+__device__ __forceinline__ double strided_sum(const double *v, int64_t n, int64_t step, int t) {
+    double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    int64_t i = t;
+    for (; i + 7 * NT < n; i += 8 * NT) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc[u] += v[(i + u * NT) * step];
     }
-    if (threadIdx.x == 0 && ch < c_out) stats[st * c_out + ch] = red[0];
+    for (int u = 0; i < n; i += NT, ++u) acc[u & 7] += v[i * step];
+    return ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+}
+
+// Block sum of one double per thread (fixed order); valid in thread 0.
+template <int NT>
+__device__ __forceinline__ double block_sum(double s, double *red) {
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (int w = 1; w < NT / 64; ++w) s += red[w];
+    __syncthreads();
+    return s;
+}
+
+constexpr int RED_BLOCK = 1024;
+__global__ __launch_bounds__(RED_BLOCK) void k_stats_reduce(const double *part, int n_tiles, int c_out,
+                                                            double *stats) {
+    __shared__ double red[RED_BLOCK / 64];
+    const int ch = blockIdx.x >> 1, st = blockIdx.x & 1;
+    const double s = block_sum<RED_BLOCK>(
+        strided_sum<RED_BLOCK>(part + ((int64_t)ch * 2 + st) * n_tiles, n_tiles, 1, threadIdx.x), red);
+    if (threadIdx.x == 0 && ch < c_out) stats[st * c_out + ch] = s;
 }
 
 // BatchNorm (training) from the batch statistics: mean, biased variance for
@@ -937,15 +961,16 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_apply_vec(const T *y, con
     }
 }
 
+// one block per channel (strided_sum / block_sum above)
 __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_finalize(const double *part, int n_blocks, int c,
                                                                 double count, float *dbeta, float *dgamma,
                                                                 float *mean_terms) {
-    for (int ch = blockIdx.x * SHPL_BLOCK + threadIdx.x; ch < c; ch += gridDim.x * SHPL_BLOCK) {
-        double a = 0.0, b = 0.0;
-        for (int k = 0; k < n_blocks; ++k) {
-            a += part[((int64_t)k * 2 + 0) * c + ch];
-            b += part[((int64_t)k * 2 + 1) * c + ch];
-        }
+    __shared__ double red[SHPL_BLOCK / 64];
+    const int ch = blockIdx.x;
+    const double a = block_sum<SHPL_BLOCK>(strided_sum<SHPL_BLOCK>(part + ch, n_blocks, 2 * c, threadIdx.x), red);
+    const double b =
+        block_sum<SHPL_BLOCK>(strided_sum<SHPL_BLOCK>(part + c + ch, n_blocks, 2 * c, threadIdx.x), red);
+    if (threadIdx.x == 0) {
         if (dbeta) dbeta[ch] = (float)a;
         if (dgamma) dgamma[ch] = (float)b;
         mean_terms[ch] = (float)(a / count);
@@ -1329,22 +1354,46 @@ __global__ __launch_bounds__(CONV_BLOCK, 2) void k_wgrad_bf16(const ConvArgs p, 
 
 // dW (f32, HWIO [3][3][c_a+c_b][c_out]) = the groups' partials summed in
 // group order (f64), channels mapped back from the chunk layout.
+// dW[tap][ci][co] = sum over the n_groups partials, in group order. A block
+// takes 32 consecutive outputs; its 8 lane groups walk every 8th group (4
+// independent accumulators each, 4 loads in flight) and their sums are
+// added in lane-group order: deterministic.
+constexpr int WR_OUT = 32, WR_K = SHPL_BLOCK / WR_OUT;
 __global__ __launch_bounds__(SHPL_BLOCK) void k_wgrad_reduce(const float *part, int n_groups, int n_cib, int n_cob,
                                                              int c_a, int c_b, int qa, int ck, int c_out, float *dw) {
+    __shared__ double red[WR_K][WR_OUT];
     const int cin = c_a + c_b;
     const int64_t total = (int64_t)9 * cin * c_out;
-    for (int64_t t = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x; t < total;
-         t += (int64_t)gridDim.x * SHPL_BLOCK) {
-        const int co = (int)(t % c_out);
-        const int ci = (int)((t / c_out) % cin);
-        const int tap = (int)(t / ((int64_t)c_out * cin));
-        const int cs = ci < c_a ? ci : qa * ck + (ci - c_a);  // channel in the chunk layout
-        const int cib = cs / WG_CI, cil = cs % WG_CI, cob = co / NCO, col = co % NCO;
+    const int j = threadIdx.x % WR_OUT, kk = threadIdx.x / WR_OUT;
+    for (int64_t t0 = (int64_t)blockIdx.x * WR_OUT; t0 < total; t0 += (int64_t)gridDim.x * WR_OUT) {
+        const int64_t t = t0 + j;
         double sum = 0.0;
-        for (int k = 0; k < n_groups; ++k)
-            sum += (double)part[(((int64_t)k * n_cib + cib) * n_cob + cob) * (9 * WG_CI * NCO) + tap * (WG_CI * NCO) +
-                                cil * NCO + col];
-        dw[t] = (float)sum;
+        if (t < total) {
+            const int co = (int)(t % c_out);
+            const int ci = (int)((t / c_out) % cin);
+            const int tap = (int)(t / ((int64_t)c_out * cin));
+            const int cs = ci < c_a ? ci : qa * ck + (ci - c_a);  // channel in the chunk layout
+            const int cib = cs / WG_CI, cil = cs % WG_CI, cob = co / NCO, col = co % NCO;
+            const int64_t gstride = (int64_t)n_cib * n_cob * (9 * WG_CI * NCO);  // one group further
+            const float *v = part + ((int64_t)cib * n_cob + cob) * (9 * WG_CI * NCO) + tap * (WG_CI * NCO) +
+                             cil * NCO + col;
+            double acc[4] = {0.0, 0.0, 0.0, 0.0};
+            int k = kk;
+            for (; k + 3 * WR_K < n_groups; k += 4 * WR_K) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc[u] += (double)v[(int64_t)(k + u * WR_K) * gstride];
+            }
+            for (int u = 0; k < n_groups; k += WR_K, ++u) acc[u & 3] += (double)v[(int64_t)k * gstride];
+            sum = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        }
+        red[kk][j] = sum;
+        __syncthreads();
+        if (kk == 0 && t < total) {
+            double s2 = red[0][j];
+            for (int q = 1; q < WR_K; ++q) s2 += red[q][j];
+            dw[t] = (float)s2;
+        }
+        __syncthreads();
     }
 }
 
@@ -1409,7 +1458,7 @@ int conv_launch(const ConvPlan &pl, ConvArgs &a, bool pooled, bool stats, const 
     }
     SHPL_LAUNCH_CHECK();
     if (stats) {
-        hipLaunchKernelGGL(k_stats_reduce, dim3(pl.n_cob * NCO * 2), dim3(SHPL_BLOCK), 0, s, a.part, (int)pl.n_tiles,
+        hipLaunchKernelGGL(k_stats_reduce, dim3(pl.n_cob * NCO * 2), dim3(RED_BLOCK), 0, s, a.part, (int)pl.n_tiles,
                            a.c_out, d_stats);
         SHPL_LAUNCH_CHECK();
     }
@@ -1589,7 +1638,7 @@ extern "C" int shpl_batch_norm_backward(int dtype, int64_t rows, const void *d_y
         else
             hipLaunchKernelGGL(k_bn_bwd_partial<T>, dim3(nb), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride, (int)c,
                                d_mean, d_scale, d_gamma, beta, act, rpb, part);
-        hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(grid_for(c, SHPL_BLOCK, 256)), dim3(SHPL_BLOCK), 0, s, part, nb,
+        hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((unsigned)c), dim3(SHPL_BLOCK), 0, s, part, nb,
                            (int)c, (double)rows, d_dbeta, d_raw ? d_dgamma : nullptr, mt);
         if (vform)
             hipLaunchKernelGGL(k_bn_bwd_apply_vec<T>, dim3(grid), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride,
@@ -1770,7 +1819,7 @@ extern "C" int shpl_conv3x3_wgrad(int dtype, int n_frames, int64_t h, int64_t w,
     }
     SHPL_LAUNCH_CHECK();
     const int64_t n_out = 9 * (c_a + c_b) * c_out;
-    hipLaunchKernelGGL(k_wgrad_reduce, dim3(grid_for(n_out, SHPL_BLOCK, 1024)), dim3(SHPL_BLOCK), 0, s, g.part,
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3(grid_for(n_out, WR_OUT, 4096)), dim3(SHPL_BLOCK), 0, s, g.part,
                        wp.n_groups, wp.n_cib, pl.n_cob, (int)c_a, (int)c_b, pl.qa, pl.ck, (int)c_out, d_dw);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
