@@ -13,6 +13,6 @@ for dt in f32 bf16; do
 import csv,glob,sys
 f=glob.glob(f'gpurun_out/prof_bn_{sys.argv[1]}/**/*kernel_stats.csv',recursive=True)[0]
 for r in csv.DictReader(open(f)):
-    if 'k_bn' in r['Name']: print(' ', r['Name'][:60], r['Calls'], round(float(r['AverageNs'])/1e3,1), 'us')
+    if 'k_bn' in r['Name'] or 'k_conv3x3' in r['Name'] or 'wgrad' in r['Name']: print(' ', r['Name'][30:100], r['Calls'], round(float(r['AverageNs'])/1e3,1), 'us')
 PY
 done
