@@ -595,23 +595,28 @@ __global__ __launch_bounds__(CONV_BLOCK, NCB == 2 ? 3 : 4) void k_conv3x3(const 
         }
     }
     if (STATS) {
-        // per channel: sum over the 32 pixels of the lane half (butterfly), then
-        // over the 4 waves in double
+        // per channel: sum over the 32 pixels of the lane half by a halving
+        // butterfly (each exchange hands the partner the half of the values it
+        // keeps: 8 + 4 + 2 + 1 + 1 shuffles per statistic instead of 16 x 5),
+        // after which lanes 2j and 2j+1 both hold value j; then over the 4
+        // waves in double
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        for (int n = 8, off = 16; n >= 1; n >>= 1, off >>= 1) {
+            const bool up = (pl & off) != 0;
 #pragma unroll
-            for (int off = 1; off < 32; off <<= 1) {
-                s1[i] = __fadd_rn(s1[i], __shfl_xor(s1[i], off, 64));
-                s2[i] = __fadd_rn(s2[i], __shfl_xor(s2[i], off, 64));
+            for (int i = 0; i < n; ++i) {
+                const float g1 = up ? s1[i] : s1[i + n], k1 = up ? s1[i + n] : s1[i];
+                const float g2 = up ? s2[i] : s2[i + n], k2 = up ? s2[i + n] : s2[i];
+                s1[i] = __fadd_rn(k1, __shfl_xor(g1, off, 64));
+                s2[i] = __fadd_rn(k2, __shfl_xor(g2, off, 64));
             }
         }
-        if (pl == 0) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int cl = 8 * (i >> 2) + 4 * hf + (i & 3);
-                s_red[wave][0][cl] = s1[i];
-                s_red[wave][1][cl] = s2[i];
-            }
+        s1[0] = __fadd_rn(s1[0], __shfl_xor(s1[0], 1, 64));
+        s2[0] = __fadd_rn(s2[0], __shfl_xor(s2[0], 1, 64));
+        if ((pl & 1) == 0) {
+            const int i = pl >> 1, cl = 8 * (i >> 2) + 4 * hf + (i & 3);
+            s_red[wave][0][cl] = s1[0];
+            s_red[wave][1][cl] = s2[0];
         }
         __syncthreads();
         if (tid < 2 * NCO) {
