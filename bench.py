@@ -60,6 +60,8 @@ def parse():
                     help="skip the frame-parallel (one process per core, up to 16) CPU-baseline sample")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the layer's streaming pass after the index build instead of beside it")
+    ap.add_argument("--no-split-runs", action="store_true",
+                    help="dual configs: pixel-keyed long runs on the same stream as the short ones")
     ap.add_argument("--groups", type=int, default=1,
                     help="config 2: frame groups of the layer; group g's pooled rows are gathered while "
                          "group g+1 streams (1 = one dense + one sparse launch; measured fastest, "
@@ -229,6 +231,8 @@ def main():
         d_bev, d_img = torch.empty_like(bev), torch.empty_like(img)
     side = torch.cuda.Stream(device=dev)
     side2 = torch.cuda.Stream(device=dev) if dual else None  # pixel-keyed CSR / pulls beside the cell-keyed
+    # the pixel-keyed pulls' long runs (k_sparse_long) beside their short ones
+    aux = torch.cuda.Stream(device=dev) if dual and not args.no_overlap and not args.no_split_runs else None
     grouped = not dual and not args.no_overlap and args.groups > 1
     if grouped:
         host_off = np.concatenate([[0], np.cumsum([f.points.shape[0] for f in frames])])
@@ -258,11 +262,12 @@ def main():
             if ev is not None:
                 ev[3].record()
         else:
-            pl.step_overlapped(pts, vox, off, P, bev, img, side, events=ev[:4] if ev else None, side2=side2)
+            pl.step_overlapped(pts, vox, off, P, bev, img, side, events=ev[:4] if ev else None, side2=side2,
+                               aux=aux)
         if backward:
             if ev is not None:
                 ev[4].record()
-            pl.backward(g_bv, g_img, d_bev, d_img, side2=None if args.no_overlap else side2)
+            pl.backward(g_bv, g_img, d_bev, d_img, side2=None if args.no_overlap else side2, aux=aux)
             if ev is not None:
                 ev[5].record()
 

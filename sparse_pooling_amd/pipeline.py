@@ -95,15 +95,33 @@ class FusedPipeline:
             self._pull(self._lib.shpl_pull_dense, self.pcsr, L.BY_PIXEL, bev, self.Cb, img, self.Ci,
                        self.img_fused, st)
 
-    def layer_sparse(self, bev, img, which=("cell", "pixel")):
-        """Pooled rows, after layer_dense and build_csr."""
-        st = L.stream_of(self.dev)
+    def _sparse(self, args, aux=None):
+        """shpl_pull_sparse(*args) on the current stream. With `aux`, its two
+        run classes go on two streams: the runs of at most 8 entries here, the
+        longer ones (k_sparse_long) on `aux` beside them -- they write disjoint
+        rows -- and the current stream then waits for `aux`."""
+        cur = torch.cuda.current_stream(self.dev)
+        st = ctypes.c_void_p(cur.cuda_stream)
+        if aux is None:
+            L.check(self._lib.shpl_pull_sparse(*args, st), "shpl_pull_sparse")
+            return
+        aux.wait_stream(cur)              # the dense pass of the same output is done
+        L.check(self._lib.shpl_pull_sparse_runs(L.RUNS_LONG, *args, ctypes.c_void_p(aux.cuda_stream)),
+                "shpl_pull_sparse_runs")
+        L.check(self._lib.shpl_pull_sparse_runs(L.RUNS_SHORT, *args, st), "shpl_pull_sparse_runs")
+        cur.wait_stream(aux)
+
+    def _concat_args(self, csr, direction, src, cs, pass_, cp, out):
+        return (direction, L.dtype_code(out), csr.ref(), L.ptr(src), cs, 0, cs, L.ptr(pass_), cp, 0, cp,
+                L.OUT_CONCAT, L.ptr(out), cs + cp)
+
+    def layer_sparse(self, bev, img, which=("cell", "pixel"), aux=None):
+        """Pooled rows, after layer_dense and build_csr. `aux`: a stream for
+        the pixel-keyed pull's long runs (see _sparse)."""
         if "cell" in which:
-            self._pull(self._lib.shpl_pull_sparse, self.csr, L.BY_CELL, img, self.Ci, bev, self.Cb, self.bv_fused,
-                       st)
+            self._sparse(self._concat_args(self.csr, L.BY_CELL, img, self.Ci, bev, self.Cb, self.bv_fused))
         if self.dual and "pixel" in which:
-            self._pull(self._lib.shpl_pull_sparse, self.pcsr, L.BY_PIXEL, bev, self.Cb, img, self.Ci,
-                       self.img_fused, st)
+            self._sparse(self._concat_args(self.pcsr, L.BY_PIXEL, bev, self.Cb, img, self.Ci, self.img_fused), aux)
 
     def layer(self, bev, img):
         """bv_fused = [bev || pool(img)] (+ img_fused = [img || trans(bev)] if dual)."""
@@ -116,11 +134,12 @@ class FusedPipeline:
         self.layer(bev, img)
 
     def step_overlapped(self, points, voxels, point_offsets, P, bev, img, side, mval=None, events=None,
-                        side2=None):
+                        side2=None, aux=None):
         """Same result as step(): the streaming half runs on `side` while the
         current stream builds M and its CSR; the sparse half then waits for it.
         Dual layers with `side2`: the pixel-keyed CSR and pull run on side2,
         beside the cell-keyed ones (they share only M).
+        `aux`: the pixel-keyed pull's long runs beside its short ones.
         `events` (4 timing events) bracket the dense and the sparse launches."""
         main = torch.cuda.current_stream(self.dev)
         side.wait_stream(main)            # inputs / previous step done
@@ -137,7 +156,7 @@ class FusedPipeline:
             with torch.cuda.stream(side2):
                 self.build_csr(("pixel",))
                 side2.wait_stream(side)
-                self.layer_sparse(bev, img, ("pixel",))
+                self.layer_sparse(bev, img, ("pixel",), aux=aux)
         self.build_csr(("cell",) if split else ("cell", "pixel"))
         main.wait_stream(side)            # sparse overwrites rows the dense pass wrote
         if events:
@@ -221,27 +240,29 @@ class FusedPipeline:
         main.wait_stream(sstream)
         main.wait_stream(dstream)
 
-    def backward(self, g_bv, g_img, d_bev, d_img, side2=None):
+    def backward(self, g_bv, g_img, d_bev, d_img, side2=None, aux=None):
         """TF gradient of the dual layer with the concat split and add_n fused:
         d_bev = g_bv[..., :Cb] + M^T-pull of g_img[..., Ci:]
         d_img = g_img[..., :Ci] + scatter of M-pulled g_bv[..., Cb:].
         With the builder's identity columns the forward entry lists already are
         in the gradients' TF order (ORDER_COL_ENTRY == ORDER_ENTRY / COL_ROW).
-        side2: the d_img pull runs there, beside the d_bev pull."""
+        side2: the d_img pull runs there, beside the d_bev pull; aux: the
+        d_img pull's long runs beside its short ones."""
         assert self.dual
         main = torch.cuda.current_stream(self.dev)
         w = self.Cb + self.Ci
         dt = L.dtype_code(d_bev)
+        cell = (L.BY_CELL, dt, self.csr.ref(), L.ptr(g_img), w, self.Ci, self.Cb, L.ptr(g_bv), w, 0, self.Cb,
+                L.OUT_ADD, L.ptr(d_bev), self.Cb)
+        pix = (L.BY_PIXEL, dt, self.pcsr.ref(), L.ptr(g_bv), w, self.Cb, self.Ci, L.ptr(g_img), w, 0, self.Ci,
+               L.OUT_ADD, L.ptr(d_img), self.Ci)
+        pst = side2 if side2 is not None else main
         if side2 is not None:
             side2.wait_stream(main)       # forward done
-            st = ctypes.c_void_p(side2.cuda_stream)
-        else:
-            st = L.stream_of(self.dev)
-        L.check(self._lib.shpl_pull(L.BY_CELL, dt, self.csr.ref(), L.ptr(g_img), w, self.Ci, self.Cb, L.ptr(g_bv),
-                                    w, 0, self.Cb, L.OUT_ADD, L.ptr(d_bev), self.Cb, L.stream_of(self.dev)),
-                "shpl_pull")
-        L.check(self._lib.shpl_pull(L.BY_PIXEL, dt, self.pcsr.ref(), L.ptr(g_bv), w, self.Cb, self.Ci,
-                                    L.ptr(g_img), w, 0, self.Ci, L.OUT_ADD, L.ptr(d_img), self.Ci, st), "shpl_pull")
+        L.check(self._lib.shpl_pull(*cell, L.stream_of(self.dev)), "shpl_pull")
+        with torch.cuda.stream(pst):
+            L.check(self._lib.shpl_pull_dense(*pix, L.stream_of(self.dev)), "shpl_pull_dense")
+            self._sparse(pix, aux)
         if side2 is not None:
             main.wait_stream(side2)
 

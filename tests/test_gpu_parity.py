@@ -392,7 +392,7 @@ def test_full_size_properties_config5():
 
 
 @pytest.mark.parametrize("dtype,mode", [("f32", "eager"), ("bf16", "eager"), ("bf16", "streams"),
-                                        ("f32", "graph")])
+                                        ("f32", "graph"), ("bf16", "split"), ("f32", "split-graph")])
 def test_pipeline_backward_matches_oracle(dtype, mode):
     """FusedPipeline.backward (the config-3 bench gradient) vs the oracle's TF gradients;
     mode streams/graph: the bench's step (side streams for the streaming half and the
@@ -423,12 +423,14 @@ def test_pipeline_backward_matches_oracle(dtype, mode):
         pl.backward(tgb, tgi, d_bev, d_img)
     else:
         side, side2 = torch.cuda.Stream(), torch.cuda.Stream()
+        # split: the pixel-keyed pulls' long runs on a fourth stream
+        aux = torch.cuda.Stream() if mode.startswith("split") else None
 
         def step():
-            pl.step_overlapped(pts, vox, off, P, tb, ti, side, side2=side2)
-            pl.backward(tgb, tgi, d_bev, d_img, side2=side2)
+            pl.step_overlapped(pts, vox, off, P, tb, ti, side, side2=side2, aux=aux)
+            pl.backward(tgb, tgi, d_bev, d_img, side2=side2, aux=aux)
         step()
-        if mode == "graph":
+        if mode.endswith("graph"):
             torch.cuda.synchronize()
             for t in (pl.bv_fused, pl.img_fused, d_bev, d_img):
                 t.fill_(float("nan"))
