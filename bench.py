@@ -60,8 +60,8 @@ def parse():
                     help="skip the frame-parallel (one process per core, up to 16) CPU-baseline sample")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the layer's streaming pass after the index build instead of beside it")
-    ap.add_argument("--no-split-runs", action="store_true",
-                    help="dual configs: pixel-keyed long runs on the same stream as the short ones")
+    ap.add_argument("--split-runs", action="store_true",
+                    help="dual configs: pixel-keyed long runs on a fourth stream beside the short ones (no graph)")
     ap.add_argument("--groups", type=int, default=1,
                     help="config 2: frame groups of the layer; group g's pooled rows are gathered while "
                          "group g+1 streams (1 = one dense + one sparse launch; measured fastest, "
@@ -232,7 +232,8 @@ def main():
     side = torch.cuda.Stream(device=dev)
     side2 = torch.cuda.Stream(device=dev) if dual else None  # pixel-keyed CSR / pulls beside the cell-keyed
     # the pixel-keyed pulls' long runs (k_sparse_long) beside their short ones
-    aux = torch.cuda.Stream(device=dev) if dual and not args.no_overlap and not args.no_split_runs else None
+    # (eager launches only: capturing the fourth stream's fork/join crashed in hipGraph capture_end)
+    aux = torch.cuda.Stream(device=dev) if dual and not args.no_overlap and args.split_runs else None
     grouped = not dual and not args.no_overlap and args.groups > 1
     if grouped:
         host_off = np.concatenate([[0], np.cumsum([f.points.shape[0] for f in frames])])
@@ -283,7 +284,7 @@ def main():
     # the timed loop replays it, so host launch gaps leave the step. Kernel
     # durations for the roofline come from the same step run eagerly with events.
     graph, graph_note = None, None
-    if not args.no_graph:
+    if not args.no_graph and aux is None:
         try:
             gstream = torch.cuda.Stream(device=dev)
             gstream.wait_stream(torch.cuda.current_stream(dev))

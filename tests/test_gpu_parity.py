@@ -392,7 +392,7 @@ def test_full_size_properties_config5():
 
 
 @pytest.mark.parametrize("dtype,mode", [("f32", "eager"), ("bf16", "eager"), ("bf16", "streams"),
-                                        ("f32", "graph"), ("bf16", "split"), ("f32", "split-graph")])
+                                        ("f32", "graph"), ("bf16", "split"), ("f32", "split")])
 def test_pipeline_backward_matches_oracle(dtype, mode):
     """FusedPipeline.backward (the config-3 bench gradient) vs the oracle's TF gradients;
     mode streams/graph: the bench's step (side streams for the streaming half and the
