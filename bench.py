@@ -16,11 +16,17 @@ Other configs: 3 = bf16 dual SHPL forward + backward at the fusion_vgg
 conv4 level (88x100x256 / 45x150x256, 4 frames); 5 = fp32 dual forward,
 40k points, 64 channels.
 
-Frames are independent: each rank draws its own frames and runs
-them with no data-path collective ("scaling": "weak"); the only collectives
-are the barriers around the timed loop, a MAX all-reduce of the elapsed time
-and an all-gather of per-rank checksums. `value` = frames of all ranks / max
-elapsed.
+Multi-GPU (config 4): `--gpus N` without a launcher starts N
+ranks itself (torch.distributed.run, before this process touches HIP); under
+a launcher --gpus must equal WORLD_SIZE. Frames are independent and named by
+global frame id (points, voxel indices and features seeded by it), so ranks
+need no data-path collective. --partition strong (default): a fixed global
+batch of --frames frames (default 64), rank r owning the contiguous block
+[r*G/w, (r+1)*G/w), value = G / max elapsed, "scaling": "strong"; weak: every
+rank --frames frames of a global batch of frames*w. The only collectives are
+the barriers around the timed loop, a MAX all-reduce of the elapsed time and
+an all-gather of per-frame output checksums, compared with the N=1 run's
+(profiles/frame_checksums.json, --write-checksums).
 
 roofline: the SHPL layer kernels (k_dense + k_sparse of every pull in the
 step); algorithmic bytes per step (SURVEY §8d per frame x F) over their
@@ -30,8 +36,10 @@ TF-order pooling + concat), one core, on a bounded sample of the same
 frames (rank 0, N=1 only).
 """
 import argparse
+import hashlib
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -45,6 +53,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 # dense MFMA peaks (MI355X_MICROARCH.md, Matrix cores): f32-input 157.3 TF, bf16 ~2.5 PF
 MFMA_PEAK_TFS = {"f32": 157.3, "bf16": 2500.0}
 DEFAULT_FRAMES = {2: 64, 3: 4, 5: 64}
+CHECKSUM_FILE = os.path.join(HERE, "profiles", "frame_checksums.json")
 
 
 def parse():
@@ -52,7 +61,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=None, help="frames per GPU per step")
+    ap.add_argument("--frames", type=int, default=None,
+                    help="frames per step: the global batch (--partition strong) or per GPU (weak)")
+    ap.add_argument("--partition", default="strong", choices=["strong", "weak"],
+                    help="strong: the global batch split into contiguous blocks over the ranks (config 4); "
+                         "weak: every rank its own --frames frames")
+    ap.add_argument("--write-checksums", action="store_true",
+                    help="store this run's per-frame output checksums in profiles/frame_checksums.json "
+                         "(the N=1 reference the N>1 runs are compared with)")
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -60,8 +76,6 @@ def parse():
                     help="skip the frame-parallel (one process per core, up to 16) CPU-baseline sample")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the layer's streaming pass after the index build instead of beside it")
-    ap.add_argument("--split-runs", action="store_true",
-                    help="dual configs: pixel-keyed long runs on a fourth stream beside the short ones (no graph)")
     ap.add_argument("--groups", type=int, default=1,
                     help="config 2: frame groups of the layer; group g's pooled rows are gathered while "
                          "group g+1 streams (1 = one dense + one sparse launch; measured fastest, "
@@ -156,13 +170,30 @@ def _cpu_worker(q, barrier, spec, frames_np, budget_s, dual, backward):
     q.put(cpu_baseline(spec, frames_np, budget_s, dual, backward))
 
 
+def usable_cores():
+    """Host cores this process may run on: its affinity set, capped by the
+    cgroup CPU quota when one is set (cpu.max; a GPU box's share of a large
+    host shows every CPU in the affinity set but allows only its quota)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, period = fh.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return (min(aff, quota) if quota else aff), aff, quota
+
+
 def cpu_baseline_parallel(spec, frames_np, budget_s, dual, backward=False):
     """Frame-parallel form of cpu_baseline (single thread and
-    N-process frame-parallel): one spawned process per host core, up to 16
-    (the CPU share of one GPU on the box), each starting at its own frame,
-    started together; the aggregate is the sum of the processes' rates."""
+    N-process frame-parallel): one spawned process per usable host core (every
+    core of the affinity set, capped by the cgroup quota), each starting at
+    its own frame, started together; the aggregate is the sum of the
+    processes' rates."""
     import multiprocessing as mp
-    n = max(1, min(16, len(os.sched_getaffinity(0))))
+    n, aff, quota = usable_cores()
     ctx = mp.get_context("spawn")
     q, bar = ctx.Queue(), ctx.Barrier(n)
     procs = [ctx.Process(target=_cpu_worker,
@@ -176,13 +207,56 @@ def cpu_baseline_parallel(spec, frames_np, budget_s, dual, backward=False):
         for p in procs:
             p.join(timeout=60)
     return {"value": round(sum(r["value"] for r in res), 3), "unit": "frames/s", "cores": n, "processes": n,
-            "sample": f"{n} processes started together, each the single-thread sample ({budget_s:.0f} s) "
+            "sample": f"{n} processes started together (all usable cores: affinity set of {aff} cpus, cgroup "
+                      f"quota {quota if quota else 'none'}), each the single-thread sample ({budget_s:.0f} s) "
                       f"from its own first frame"}
+
+
+def self_launch(args):
+    """`--gpus N` (N > 1) without a launcher: start N ranks, one per GPU, as
+    torch.distributed.run children, and wait for them. Nothing in this
+    process has touched HIP (no device call before this point), so it is a
+    plain parent, not an exec of a GPU process."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd)
+
+
+def checksum_report(key, local, dev, rank, args):
+    """All-gather the per-frame checksums (global frame order), compare them
+    with the N=1 run's stored under `key`, store them with --write-checksums."""
+    from sparse_pooling_amd import dist as sd
+    allcs = sd.gather_frame_checksums(local, device=dev)
+    ref = None
+    if os.path.exists(CHECKSUM_FILE):
+        with open(CHECKSUM_FILE) as fh:
+            ref = json.load(fh).get(key)
+    if args.write_checksums and rank == 0:
+        tab = {}
+        if os.path.exists(CHECKSUM_FILE):
+            with open(CHECKSUM_FILE) as fh:
+                tab = json.load(fh)
+        tab[key] = allcs
+        with open(CHECKSUM_FILE, "w") as fh:
+            json.dump(tab, fh, indent=0)
+    return {"key": key, "frames": len(allcs),
+            "digest": hashlib.sha256(json.dumps(allcs).encode()).hexdigest()[:16],
+            "match_n1": None if ref is None else ref == allcs,
+            "first": allcs[:4]}
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch one rank per GPU, or drop the "
+                 "launcher and let --gpus start the ranks)")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # SHPL_DIST_BACKEND=gloo: rehearsal of the N>1 path with several ranks on
@@ -214,26 +288,23 @@ def main():
     backward = cfg == 3
     dtype = torch.bfloat16 if cfg == 3 else torch.float32
     esz = 2 if dtype == torch.bfloat16 else 4
-    F = args.frames or DEFAULT_FRAMES[cfg]
-    frames = [synth.make_frame(spec, seed=s, n_outside=200) for s in sd.frame_seeds(rank, F)]
+    fids = sd.partition(args.frames or DEFAULT_FRAMES[cfg], world, rank, args.partition)
+    F = len(fids)
+    frames = [synth.make_frame(spec, seed=s, n_outside=200) for s in fids]
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, dev)
     pl = pipeline.FusedPipeline(F, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev,
                                 spec.c_img, dtype=dtype, dual=dual, device=dev)
     Hb, Wb = spec.bev_feat_hw
     Hi, Wi = spec.img_feat_hw
-    g = torch.Generator(device=dev)
-    g.manual_seed(1234 + rank)
-    bev = torch.randn((F, Hb, Wb, spec.c_bev), device=dev, generator=g).to(dtype)
-    img = torch.randn((F, Hi, Wi, spec.c_img), device=dev, generator=g).to(dtype)
+    feats = lambda shape, seed: sd.fill_features(torch.empty(shape, dtype=dtype, device=dev), fids, seed)  # noqa
+    bev = feats((F, Hb, Wb, spec.c_bev), 1)
+    img = feats((F, Hi, Wi, spec.c_img), 2)
     if backward:
-        g_bv = torch.randn(tuple(pl.bv_fused.shape), device=dev, generator=g).to(dtype)
-        g_img = torch.randn(tuple(pl.img_fused.shape), device=dev, generator=g).to(dtype)
+        g_bv = feats(tuple(pl.bv_fused.shape), 3)
+        g_img = feats(tuple(pl.img_fused.shape), 4)
         d_bev, d_img = torch.empty_like(bev), torch.empty_like(img)
     side = torch.cuda.Stream(device=dev)
     side2 = torch.cuda.Stream(device=dev) if dual else None  # pixel-keyed CSR / pulls beside the cell-keyed
-    # the pixel-keyed pulls' long runs (k_sparse_long) beside their short ones
-    # (eager launches only: capturing the fourth stream's fork/join crashed in hipGraph capture_end)
-    aux = torch.cuda.Stream(device=dev) if dual and not args.no_overlap and args.split_runs else None
     grouped = not dual and not args.no_overlap and args.groups > 1
     if grouped:
         host_off = np.concatenate([[0], np.cumsum([f.points.shape[0] for f in frames])])
@@ -263,12 +334,11 @@ def main():
             if ev is not None:
                 ev[3].record()
         else:
-            pl.step_overlapped(pts, vox, off, P, bev, img, side, events=ev[:4] if ev else None, side2=side2,
-                               aux=aux)
+            pl.step_overlapped(pts, vox, off, P, bev, img, side, events=ev[:4] if ev else None, side2=side2)
         if backward:
             if ev is not None:
                 ev[4].record()
-            pl.backward(g_bv, g_img, d_bev, d_img, side2=None if args.no_overlap else side2, aux=aux)
+            pl.backward(g_bv, g_img, d_bev, d_img, side2=None if args.no_overlap else side2)
             if ev is not None:
                 ev[5].record()
 
@@ -284,7 +354,7 @@ def main():
     # the timed loop replays it, so host launch gaps leave the step. Kernel
     # durations for the roofline come from the same step run eagerly with events.
     graph, graph_note = None, None
-    if not args.no_graph and aux is None:
+    if not args.no_graph:
         try:
             gstream = torch.cuda.Stream(device=dev)
             gstream.wait_stream(torch.cuda.current_stream(dev))
@@ -308,7 +378,9 @@ def main():
     else:
         elapsed = sd.timed(lambda k: step(evs[k]), args.steps, device=dev)
     args_steps_ev = n_ev
-    checksums = sd.gather_checksums(pl.bv_fused[..., spec.c_bev:].double().sum().item(), device=dev)
+    outs = [pl.bv_fused] + ([pl.img_fused] if dual else []) + ([d_bev, d_img] if backward else [])
+    checks = checksum_report(f"layer_config{cfg}_frames{F * world}", sum(sd.frame_checksums(t) for t in outs),
+                             dev, rank, args)
     nbytes = step_bytes(cfg, spec, nnz, u_pix, u_cell, F, esz)
     kernels = {}
     if grouped:
@@ -358,7 +430,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.partition,
             "vs_baseline": None,
             "dtype": "bf16" if esz == 2 else "f32",
             "data": "synthetic (seeded KITTI-shaped frames; no dataset on the box)",
@@ -366,7 +438,9 @@ def main():
                 "workload": (f"config{cfg}: {spec.n_points} pts/frame, BEV {Hb}x{Wb}x{spec.c_bev}, "
                              f"img {Hi}x{Wi}x{spec.c_img}, {what}; step = device index build + sorted M "
                              "+ fused layer" + (" + gradient" if backward else "")),
+                "global_batch": F * world,
                 "frames_per_gpu_per_step": F,
+                "partition": (f"{args.partition}: rank r owns global frames [r*{F}, (r+1)*{F}) of {F * world}"),
                 "nnz_per_step_rank0": nnz,
                 "unique_src_pixels_rank0": u_pix,
                 "unique_cells_rank0": u_cell,
@@ -396,7 +470,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "index_errors": err,
-            "pooled_checksum_per_rank": [round(c, 3) for c in checksums],
+            "frame_checksums": checks,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -445,18 +519,17 @@ def run_frames(args, world, rank, dev):
     """Raw-scan workload: the whole per-frame SHPL path of kitti_dataset.py:285-379 +
     rpn_model.py's fused layer, from velodyne scans resident in HBM."""
     from sparse_pooling_amd import dist as sd, kitti, pipeline, synth
-    F = args.frames or 64
+    fids = sd.partition(args.frames or 64, world, rank, args.partition)
+    F = len(fids)
     C = 32
     h, w = synth.KITTI_IMAGE_SHAPE
     im_size = (w, h)
-    fr = kitti.synthetic_frames(F, args.scan_points, seed=1000 + rank, device=dev)
+    fr = kitti.synthetic_frames(F, args.scan_points, seed=1000, device=dev, frame_ids=fids)
     pl = pipeline.FramePipeline(F, fr.total_points, im_size, synth.AREA_EXTENTS, synth.VOXEL_SIZE,
                                 synth.HEIGHT_LO, synth.HEIGHT_HI, synth.NUM_SLICES, (1, 1), C, C, device=dev,
                                 max_points_per_frame=fr.max_points)
-    g = torch.Generator(device=dev)
-    g.manual_seed(4321 + rank)
-    bev = torch.randn((F, pl.Hb, pl.Wb, C), device=dev, generator=g)
-    img = torch.randn((F, pl.Hi, pl.Wi, C), device=dev, generator=g)
+    bev = sd.fill_features(torch.empty((F, pl.Hb, pl.Wb, C), device=dev), fids, 5)
+    img = sd.fill_features(torch.empty((F, pl.Hi, pl.Wi, C), device=dev), fids, 6)
     side = torch.cuda.Stream(device=dev)
     for _ in range(args.warmup):
         pl.velo_step(fr, bev, img, side=side)
@@ -474,6 +547,8 @@ def run_frames(args, world, rank, dev):
               "csr_ms": mean(5, 6), "k_dense_ms": dense_ms, "k_sparse_ms": sparse_ms}
     nbytes = pull_bytes(F * pl.Hb * pl.Wb, C, C, u_pix, nnz, 4, 2 * C)
     achieved = nbytes / ((dense_ms + sparse_ms) * 1e-3) / 1e9
+    checks = checksum_report(f"frames_{args.scan_points}_frames{F * world}", sd.frame_checksums(pl.bv_fused), dev,
+                             rank, args)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         scans = [fr.xyzi[int(fr.point_offsets[f]):int(fr.point_offsets[f + 1])].cpu().numpy() for f in range(min(F, 8))]
@@ -488,14 +563,16 @@ def run_frames(args, world, rank, dev):
             "metric": "SHPL frames/sec from raw velodyne scans (loader + BEV slices + index + fused layer)",
             "value": round(F * world * args.steps / elapsed, 2), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": args.partition, "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded 64-beam-like velodyne scans, KITTI calib; no dataset on the box)",
             "config": {"workload": (f"frames: {args.scan_points} pts/scan -> {n_cam / F:.0f} FOV pts -> "
                                     f"{n_vox / F:.0f} BEV voxel pts -> {nnz / F:.0f} M entries; BEV "
                                     f"{pl.Hb}x{pl.Wb}x{C} (5 slices + density maps), img {pl.Hi}x{pl.Wi}x{C}, "
                                     "img->BEV fused layer"),
-                       "frames_per_gpu_per_step": F, "parallelism": f"frame-sharded x{world}"},
+                       "global_batch": F * world, "frames_per_gpu_per_step": F,
+                       "parallelism": f"frame-sharded x{world}"},
             "stages_ms": {k: round(v, 4) for k, v in stages.items()},
+            "frame_checksums": checks,
             "roofline": {"bound": "hbm", "kernel": "k_dense + k_sparse (fused layer)", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None, "algorithmic_bytes_per_launch": nbytes},
@@ -540,21 +617,22 @@ def cpu_baseline_conv(spec, frames_np, budget_s):
                        f"{os.cpu_count()} host cpus visible")}
 
 
-def run_conv_train(args, world, rank, dev, spec, F, dtype, pl, pts, vox, off, P, bev, img, conv):
+def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off, P, bev, img, conv):
     """Training step of the fused SHPL + post-fusion conv: index build, then
     FusionConv.fused with batch-statistics BatchNorm, then its backward
     (autograd over the device kernels): gradients of bev, img, the weights and
-    beta. Eager launches (autograd allocates per step)."""
+    beta. Eager launches (autograd allocates per step). BatchNorm statistics
+    are the rank's own frames' (no cross-rank sync; data-parallel weight
+    gradients would need an all-reduce, out of scope per SURVEY §8e)."""
     from sparse_pooling_amd import dist as sd
+    F = len(fids)
     Hb, Wb = spec.bev_feat_hw
     cb, ci = spec.c_bev, spec.c_img
     esz = 2 if dtype == torch.bfloat16 else 4
     conv.weights.requires_grad_(True)
     conv.beta.requires_grad_(True)
     tb, ti = bev.clone().requires_grad_(True), img.clone().requires_grad_(True)
-    g = torch.Generator(device=dev)
-    g.manual_seed(99 + rank)
-    gy = torch.randn((F, Hb, Wb, ci), device=dev, generator=g).to(dtype)
+    gy = sd.fill_features(torch.empty((F, Hb, Wb, ci), dtype=dtype, device=dev), fids, 7)
 
     def step(ev=None):
         pl.build_index(pts, vox, off, P)
@@ -589,12 +667,13 @@ def run_conv_train(args, world, rank, dev, spec, F, dtype, pl, pts, vox, off, P,
             "metric": "SHPL + post-fusion conv training frames/sec (fwd + bwd), 1/2/4/8 GPU",
             "value": round(F * world * args.steps / elapsed, 2), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dname,
+            "higher_is_better": True, "scaling": args.partition, "vs_baseline": None, "dtype": dname,
             "data": "synthetic (seeded KITTI-shaped frames, xavier-initialised conv weights)",
             "config": {"workload": (f"conv training: config2 -> index -> conv3x3 {cb + ci}->{ci} + BatchNorm (batch "
                                     "statistics) + ReLU of [bev || pool(img)] (pooling inside the conv), backward to "
                                     "bev, img, weights, beta"),
-                       "frames_per_gpu_per_step": F, "hip_graph": False, "parallelism": f"frame-sharded x{world}"},
+                       "global_batch": F * world, "frames_per_gpu_per_step": F, "hip_graph": False,
+                       "bn_statistics": "per rank (no cross-rank sync)", "parallelism": f"frame-sharded x{world}"},
             "roofline": {"bound": "mfma", "kernel": "fwd + input-gradient + weight-gradient convs (3x the forward flops) "
                          "over the forward + backward time (BN, ReLU and the pooling gradient included)",
                          "achieved": round(tflops, 2), "peak": MFMA_PEAK_TFS[dname], "unit": "TFLOP/s",
@@ -611,25 +690,24 @@ def run_conv(args, world, rank, dev):
     timed beside it."""
     from sparse_pooling_amd import dist as sd, fusion_conv as fc, pipeline, synth
     spec = synth.CONFIG2
-    F = args.frames or 64
+    fids = sd.partition(args.frames or 64, world, rank, args.partition)
+    F = len(fids)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    frames = [synth.make_frame(spec, seed=s, n_outside=200) for s in sd.frame_seeds(rank, F)]
+    frames = [synth.make_frame(spec, seed=s, n_outside=200) for s in fids]
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, dev)
     pl = pipeline.FusedPipeline(F, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev, spec.c_img,
                                 dtype=dtype, device=dev)
     Hb, Wb = spec.bev_feat_hw
     Hi, Wi = spec.img_feat_hw
     cb, ci = spec.c_bev, spec.c_img
-    g = torch.Generator(device=dev)
-    g.manual_seed(1234 + rank)
-    bev = torch.randn((F, Hb, Wb, cb), device=dev, generator=g).to(dtype)
-    img = torch.randn((F, Hi, Wi, ci), device=dev, generator=g).to(dtype)
-    conv = fc.FusionConv(cb + ci, ci, dtype=dtype, device=dev, seed=rank)
+    bev = sd.fill_features(torch.empty((F, Hb, Wb, cb), dtype=dtype, device=dev), fids, 1)
+    img = sd.fill_features(torch.empty((F, Hi, Wi, ci), dtype=dtype, device=dev), fids, 2)
+    conv = fc.FusionConv(cb + ci, ci, dtype=dtype, device=dev, seed=0)  # the same weights on every rank
     out = torch.empty((F, Hb, Wb, ci), dtype=dtype, device=dev)
     out_unf = torch.empty_like(out)
     train = args.train_bn
     if args.train:
-        run_conv_train(args, world, rank, dev, spec, F, dtype, pl, pts, vox, off, P, bev, img, conv)
+        run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off, P, bev, img, conv)
         return
 
     def step(ev=None):
@@ -684,6 +762,8 @@ def run_conv(args, world, rank, dev):
     u_pix = int(torch.unique(pl.pix[pl.pix >= 0]).numel())
     hbm_bytes = F * Hb * Wb * (cb + ci) * esz + u_pix * ci * esz + 12 * nnz  # read bev, write out, gather
     tflops = flops / (conv_ms * 1e-3) / 1e12
+    checks = None if train else checksum_report(f"conv_{args.dtype}_frames{F * world}", sd.frame_checksums(out),
+                                                dev, rank, args)
     traffic, mfma_busy = None, None
     tpath = os.path.join(HERE, "profiles", "traffic.json")
     if os.path.exists(tpath):
@@ -701,14 +781,15 @@ def run_conv(args, world, rank, dev):
             "metric": "SHPL + post-fusion conv frames/sec (MFMA roofline), 1/2/4/8 GPU",
             "value": round(F * world * args.steps / elapsed, 2), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dname,
+            "higher_is_better": True, "scaling": args.partition, "vs_baseline": None, "dtype": dname,
             "data": "synthetic (seeded KITTI-shaped frames, xavier-initialised conv weights; no dataset on the box)",
             "config": {"workload": (f"conv: config2 ({spec.n_points} pts/frame, BEV {Hb}x{Wb}x{cb}, img {Hi}x{Wi}x{ci})"
                                     f" -> index -> cell CSR -> conv3x3 {cb + ci}->{ci} + BatchNorm "
                                     f"({'training' if train else 'inference'}) + ReLU of [bev || pool(img)], pooling "
                                     "fused into the conv's staging (rpn_model.py:338-346)"),
-                       "frames_per_gpu_per_step": F, "hip_graph": graph is not None,
+                       "global_batch": F * world, "frames_per_gpu_per_step": F, "hip_graph": graph is not None,
                        "parallelism": f"frame-sharded x{world}"},
+            "frame_checksums": checks,
             "roofline": {"bound": "mfma", "kernel": "k_conv3x3 (fused pooling), MFMA "
                          + ("v_mfma_f32_32x32x16_bf16" if esz == 2 else "v_mfma_f32_32x32x2_f32"),
                          "achieved": round(tflops, 2), "peak": MFMA_PEAK_TFS[dname], "unit": "TFLOP/s",

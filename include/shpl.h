@@ -313,19 +313,6 @@ int shpl_pull_sparse(int direction, int dtype, const shpl_csr *csr, const void *
                      int64_t pass_stride, int64_t pass_off, int64_t c_pass, int mode, void *d_out,
                      int64_t out_stride, void *stream);
 
-/* shpl_pull_sparse restricted to one class of destination runs: runs of at
- * most 8 entries (SHPL_RUNS_SHORT: k_sparse) or longer ones
- * (SHPL_RUNS_LONG: k_sparse_long). The two classes write disjoint rows, so a
- * caller may issue them on two streams, both after the dense pass; SHORT +
- * LONG == shpl_pull_sparse bit for bit. At config 3 the pixel-keyed long runs
- * (up to 54 image points on one pixel) take as long as all short ones, but
- * the two on two streams measured slower than in series. */
-typedef enum { SHPL_RUNS_ALL = 0, SHPL_RUNS_SHORT = 1, SHPL_RUNS_LONG = 2 } shpl_runs;
-int shpl_pull_sparse_runs(int runs, int direction, int dtype, const shpl_csr *csr, const void *d_src,
-                          int64_t src_stride, int64_t src_off, int64_t c_pool, const void *d_pass,
-                          int64_t pass_stride, int64_t pass_off, int64_t c_pass, int mode, void *d_out,
-                          int64_t out_stride, void *stream);
-
 /* ---------------------------------------------------------------------------
  * Post-fusion 3x3 convolution
  * ------------------------------------------------------------------------- */

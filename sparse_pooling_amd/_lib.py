@@ -20,7 +20,6 @@ I32, I64 = 0, 1
 BY_CELL, BY_PIXEL = 0, 1
 ORDER_ENTRY, ORDER_COL_ROW, ORDER_COL_ENTRY = 0, 1, 2
 OUT_POOL, OUT_CONCAT, OUT_ADD = 0, 1, 2
-RUNS_ALL, RUNS_SHORT, RUNS_LONG = 0, 1, 2
 ACT_NONE, ACT_RELU = 0, 1
 
 _lib = None
@@ -85,7 +84,6 @@ def _declare(lib):
         "shpl_pull": (i32, pull_args),
         "shpl_pull_dense": (i32, pull_args),
         "shpl_pull_sparse": (i32, pull_args),
-        "shpl_pull_sparse_runs": (i32, [i32] + pull_args),
         "shpl_conv3x3_workspace_bytes": (i32, [i32, i32, i64, i64, i64, i64, i64, i32, i32, psz]),
         "shpl_conv3x3": (i32, [i32, i32, i64, i64, p, i64, i64, i64, p, i64, i64, i64,
                                ctypes.POINTER(ShplCsr), p, p, i64, p, p, p, i32, p, i64, p, p, sz, p]),

@@ -524,7 +524,7 @@ int dense(const Plan &pl, hipStream_t s) {
 }
 
 template <typename T, int VEC, bool GROUP>
-int sparse_tg(const Plan &pl, const Ents &e, int64_t nnz_cap, int part, hipStream_t s) {
+int sparse_tg(const Plan &pl, const Ents &e, int64_t nnz_cap, hipStream_t s) {
     // one thread per (entry, chunk) of the capacity; the live count is read on the device
     const int grid = grid_for(nnz_cap * (int64_t)pl.f.cpool, SHPL_BLOCK, 1 << 20);
     int shift = -1;
@@ -532,18 +532,16 @@ int sparse_tg(const Plan &pl, const Ents &e, int64_t nnz_cap, int part, hipStrea
         if (pl.f.cpool == (1u << k)) shift = k;
     // without a run longer than LONG_RUN possible, k_sparse takes every run (the short part)
     const bool split = nnz_cap > LONG_RUN;
-    if (part != SHPL_RUNS_LONG) {
 #define SHPL_SPARSE(SPLIT, POW2) \
     hipLaunchKernelGGL((k_sparse<T, VEC, GROUP, SPLIT, POW2>), dim3(grid), dim3(SHPL_BLOCK), 0, s, pl.f, e, shift)
-        if (split) {
-            if (shift >= 0) SHPL_SPARSE(true, true); else SHPL_SPARSE(true, false);
-        } else {
-            if (shift >= 0) SHPL_SPARSE(false, true); else SHPL_SPARSE(false, false);
-        }
-#undef SHPL_SPARSE
-        SHPL_LAUNCH_CHECK();
+    if (split) {
+        if (shift >= 0) SHPL_SPARSE(true, true); else SHPL_SPARSE(true, false);
+    } else {
+        if (shift >= 0) SHPL_SPARSE(false, true); else SHPL_SPARSE(false, false);
     }
-    if (!split || part == SHPL_RUNS_SHORT) return SHPL_OK;
+#undef SHPL_SPARSE
+    SHPL_LAUNCH_CHECK();
+    if (!split) return SHPL_OK;
     // a bounded grid: each workgroup scans per_block slots, LONG_SLOTS at a time
     int64_t lgrid = (nnz_cap + LONG_SLOTS - 1) / LONG_SLOTS;
     if (lgrid > LONG_GRID) lgrid = LONG_GRID;
@@ -555,18 +553,18 @@ int sparse_tg(const Plan &pl, const Ents &e, int64_t nnz_cap, int part, hipStrea
 }
 
 template <typename T, int VEC>
-int sparse_t(const Plan &pl, const shpl_csr *csr, bool group, int part, hipStream_t s) {
+int sparse_t(const Plan &pl, const shpl_csr *csr, bool group, hipStream_t s) {
     Ents e{csr->nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_col, csr->ent_val};
-    return group ? sparse_tg<T, VEC, true>(pl, e, csr->nnz_cap, part, s)
-                 : sparse_tg<T, VEC, false>(pl, e, csr->nnz_cap, part, s);
+    return group ? sparse_tg<T, VEC, true>(pl, e, csr->nnz_cap, s)
+                 : sparse_tg<T, VEC, false>(pl, e, csr->nnz_cap, s);
 }
 
-int sparse(const Plan &pl, const shpl_csr *csr, int direction, int part, hipStream_t s) {
+int sparse(const Plan &pl, const shpl_csr *csr, int direction, hipStream_t s) {
     if (pl.n_dst == 0 || pl.f.cpool == 0 || csr->nnz_cap == 0) return SHPL_OK;
     const bool group = direction == SHPL_BY_PIXEL;
     if (pl.dtype == SHPL_F32)
-        return pl.v16 ? sparse_t<float, 4>(pl, csr, group, part, s) : sparse_t<float, 1>(pl, csr, group, part, s);
-    return pl.v16 ? sparse_t<uint16_t, 8>(pl, csr, group, part, s) : sparse_t<uint16_t, 1>(pl, csr, group, part, s);
+        return pl.v16 ? sparse_t<float, 4>(pl, csr, group, s) : sparse_t<float, 1>(pl, csr, group, s);
+    return pl.v16 ? sparse_t<uint16_t, 8>(pl, csr, group, s) : sparse_t<uint16_t, 1>(pl, csr, group, s);
 }
 
 }  // namespace
@@ -588,7 +586,7 @@ extern "C" int shpl_pull(SHPL_PULL_ARGS) {
     SHPL_PLAN();
     rc = dense(pl, (hipStream_t)stream);
     if (rc) return rc;
-    return sparse(pl, csr, direction, SHPL_RUNS_ALL, (hipStream_t)stream);
+    return sparse(pl, csr, direction, (hipStream_t)stream);
 }
 
 extern "C" int shpl_pull_dense(SHPL_PULL_ARGS) {
@@ -598,11 +596,5 @@ extern "C" int shpl_pull_dense(SHPL_PULL_ARGS) {
 
 extern "C" int shpl_pull_sparse(SHPL_PULL_ARGS) {
     SHPL_PLAN();
-    return sparse(pl, csr, direction, SHPL_RUNS_ALL, (hipStream_t)stream);
-}
-
-extern "C" int shpl_pull_sparse_runs(int runs, SHPL_PULL_ARGS) {
-    if (runs != SHPL_RUNS_ALL && runs != SHPL_RUNS_SHORT && runs != SHPL_RUNS_LONG) return SHPL_ERR_ARG;
-    SHPL_PLAN();
-    return sparse(pl, csr, direction, runs, (hipStream_t)stream);
+    return sparse(pl, csr, direction, (hipStream_t)stream);
 }

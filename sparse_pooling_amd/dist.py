@@ -1,11 +1,22 @@
 """Frame-parallel orchestration across GPUs.
 
 SHPL frames are independent -- no parameters, no cross-frame state, no
-halo -- so a node scales by giving every rank its own frames. The only
-collectives are control-plane: barriers around the timed region, one MAX
-all-reduce of the elapsed time and one all-gather of per-rank output
-checksums (a few bytes over RCCL/xGMI). Backend "nccl" (RCCL) on the GPUs,
-"gloo" in the CPU tests.
+halo -- so a node scales by splitting the frames of a batch over the ranks.
+Every frame is named by its global frame id, and everything drawn for it
+(points, voxel indices, feature maps) is seeded by that id, so a frame's
+output does not depend on which rank computes it or on how many frames share
+its launch.
+
+Partitioning (config 4, BASELINE.json configs[3]):
+* ``strong`` (default): a fixed global batch of G frames; rank r of w owns
+  the contiguous block [r*G/w, (r+1)*G/w) (G must divide by w).
+* ``weak``: every rank owns F frames of a global batch of F*w: rank r the
+  block [r*F, (r+1)*F).
+
+The only collectives are control-plane (RCCL over xGMI on the GPUs, gloo in
+the CPU tests): barriers around the timed region, one MAX all-reduce of the
+elapsed time and one all-gather of the per-frame output checksums (8 B per
+frame), which must equal the N=1 run's.
 """
 import os
 import time
@@ -18,9 +29,50 @@ def world():
     return int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
 
 
-def frame_seeds(rank, frames_per_rank, base=100000):
-    """Disjoint seeds per rank: rank r owns frames [r*base, r*base + F)."""
-    return [base * rank + f for f in range(frames_per_rank)]
+def partition(frames, world_size, rank, mode="strong"):
+    """Global frame ids owned by `rank`.
+
+    strong: `frames` is the global batch, split into contiguous blocks of
+    frames / world_size; weak: `frames` is the per-rank count."""
+    if mode == "strong":
+        if frames % world_size:
+            raise ValueError(f"strong partitioning: the global batch of {frames} frames does not split "
+                             f"over {world_size} ranks (use a multiple, or --partition weak)")
+        per = frames // world_size
+        return list(range(rank * per, (rank + 1) * per))
+    if mode == "weak":
+        return list(range(rank * frames, (rank + 1) * frames))
+    raise ValueError(f"unknown partition mode {mode!r}")
+
+
+def frame_seeds(rank, frames_per_rank):
+    """Weak partitioning's global frame ids of `rank` (seed = global frame id)."""
+    return partition(frames_per_rank, rank + 1, rank, "weak")
+
+
+def fill_features(out, frame_ids, seed_base):
+    """out[i] = N(0,1) drawn on out's device by a generator seeded with
+    (seed_base, frame_ids[i]): a frame's features are the same whichever rank
+    draws them and however many frames share the tensor."""
+    assert out.shape[0] == len(frame_ids)
+    g = torch.Generator(device=out.device)
+    tmp = torch.empty(out.shape[1:], dtype=torch.float32, device=out.device)
+    for i, fid in enumerate(frame_ids):
+        g.manual_seed(int(seed_base) * 1_000_003 + int(fid))
+        torch.randn(tmp.shape, generator=g, out=tmp, device=out.device)
+        out[i].copy_(tmp)
+    return out
+
+
+def frame_checksums(t):
+    """Per-frame checksum of a [F, ...] f32/bf16 map: the int64 sum of its
+    elements' bit patterns. Integer sums are exact in any order, so the value
+    is independent of the reduction's launch shape (and of the batch)."""
+    bits = {4: torch.int32, 2: torch.int16}[t.element_size()]
+    out = torch.empty(t.shape[0], dtype=torch.int64, device=t.device)
+    for i in range(t.shape[0]):
+        out[i] = t[i].contiguous().view(bits).to(torch.int64).sum()
+    return out
 
 
 def _coll_device(device):
@@ -68,3 +120,17 @@ def gather_checksums(value, device=None):
     out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(out, t)
     return [float(x.item()) for x in out]
+
+
+def gather_frame_checksums(local, device=None):
+    """All-gather the ranks' per-frame checksums (int64 [F_rank], every rank
+    the same F_rank) into one list in rank order -- global frame order for
+    both partitionings."""
+    local = local.to(torch.int64)
+    on = dist.is_available() and dist.is_initialized()
+    if not on:
+        return [int(x) for x in local.cpu().tolist()]
+    t = local.to(_coll_device(device))
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [int(x) for o in out for x in o.cpu().tolist()]

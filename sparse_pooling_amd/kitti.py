@@ -227,8 +227,10 @@ class KittiFrames:
                                  flip=self.flip, max_points_per_frame=self.max_points, ws=ws, out=out)
 
 
-def synthetic_frames(n_frames, points_per_scan, seed=0, device="cuda", flips=None):
-    """Seeded synthetic KITTI samples (synth.synthetic_scan, synth.KITTI_CALIB) for the bench."""
+def synthetic_frames(n_frames, points_per_scan, seed=0, device="cuda", flips=None, frame_ids=None):
+    """Seeded synthetic KITTI samples (synth.synthetic_scan, synth.KITTI_CALIB) for the bench.
+    frame_ids: scan i is drawn from a generator seeded with (seed, frame_ids[i]), so a
+    frame is the same whichever batch holds it; None: one generator for all scans."""
     from . import synth
     rng = np.random.default_rng(seed)
     fc = FrameCalibrationData()
@@ -236,7 +238,11 @@ def synthetic_frames(n_frames, points_per_scan, seed=0, device="cuda", flips=Non
     fc.p0, fc.p1, fc.p2, fc.p3 = (np.array(c[k]).reshape(3, 4) for k in ("P0", "P1", "P2", "P3"))
     fc.r0_rect = np.array(c["R0_rect"]).reshape(3, 3)
     fc.tr_velodyne_to_cam = np.array(c["Tr_velo_to_cam"]).reshape(3, 4)
-    scans = [synth.synthetic_scan(rng, points_per_scan) for _ in range(n_frames)]
+    if frame_ids is None:
+        scans = [synth.synthetic_scan(rng, points_per_scan) for _ in range(n_frames)]
+    else:
+        assert len(frame_ids) == n_frames
+        scans = [synth.synthetic_scan(np.random.default_rng([seed, int(f)]), points_per_scan) for f in frame_ids]
     plane = synth.KITTI_PLANE / np.linalg.norm(synth.KITTI_PLANE[:3])
     return KittiFrames(scans, [fc] * n_frames, [plane] * n_frames, [synth.KITTI_IMAGE_SHAPE] * n_frames,
                        flips, device)

@@ -95,33 +95,20 @@ class FusedPipeline:
             self._pull(self._lib.shpl_pull_dense, self.pcsr, L.BY_PIXEL, bev, self.Cb, img, self.Ci,
                        self.img_fused, st)
 
-    def _sparse(self, args, aux=None):
-        """shpl_pull_sparse(*args) on the current stream. With `aux`, its two
-        run classes go on two streams: the runs of at most 8 entries here, the
-        longer ones (k_sparse_long) on `aux` beside them -- they write disjoint
-        rows -- and the current stream then waits for `aux`."""
-        cur = torch.cuda.current_stream(self.dev)
-        st = ctypes.c_void_p(cur.cuda_stream)
-        if aux is None:
-            L.check(self._lib.shpl_pull_sparse(*args, st), "shpl_pull_sparse")
-            return
-        aux.wait_stream(cur)              # the dense pass of the same output is done
-        L.check(self._lib.shpl_pull_sparse_runs(L.RUNS_LONG, *args, ctypes.c_void_p(aux.cuda_stream)),
-                "shpl_pull_sparse_runs")
-        L.check(self._lib.shpl_pull_sparse_runs(L.RUNS_SHORT, *args, st), "shpl_pull_sparse_runs")
-        cur.wait_stream(aux)
+    def _sparse(self, args):
+        """shpl_pull_sparse(*args) on the current stream."""
+        L.check(self._lib.shpl_pull_sparse(*args, L.stream_of(self.dev)), "shpl_pull_sparse")
 
     def _concat_args(self, csr, direction, src, cs, pass_, cp, out):
         return (direction, L.dtype_code(out), csr.ref(), L.ptr(src), cs, 0, cs, L.ptr(pass_), cp, 0, cp,
                 L.OUT_CONCAT, L.ptr(out), cs + cp)
 
-    def layer_sparse(self, bev, img, which=("cell", "pixel"), aux=None):
-        """Pooled rows, after layer_dense and build_csr. `aux`: a stream for
-        the pixel-keyed pull's long runs (see _sparse)."""
+    def layer_sparse(self, bev, img, which=("cell", "pixel")):
+        """Pooled rows, after layer_dense and build_csr."""
         if "cell" in which:
             self._sparse(self._concat_args(self.csr, L.BY_CELL, img, self.Ci, bev, self.Cb, self.bv_fused))
         if self.dual and "pixel" in which:
-            self._sparse(self._concat_args(self.pcsr, L.BY_PIXEL, bev, self.Cb, img, self.Ci, self.img_fused), aux)
+            self._sparse(self._concat_args(self.pcsr, L.BY_PIXEL, bev, self.Cb, img, self.Ci, self.img_fused))
 
     def layer(self, bev, img):
         """bv_fused = [bev || pool(img)] (+ img_fused = [img || trans(bev)] if dual)."""
@@ -134,12 +121,11 @@ class FusedPipeline:
         self.layer(bev, img)
 
     def step_overlapped(self, points, voxels, point_offsets, P, bev, img, side, mval=None, events=None,
-                        side2=None, aux=None):
+                        side2=None):
         """Same result as step(): the streaming half runs on `side` while the
         current stream builds M and its CSR; the sparse half then waits for it.
         Dual layers with `side2`: the pixel-keyed CSR and pull run on side2,
         beside the cell-keyed ones (they share only M).
-        `aux`: the pixel-keyed pull's long runs beside its short ones.
         `events` (4 timing events) bracket the dense and the sparse launches."""
         main = torch.cuda.current_stream(self.dev)
         side.wait_stream(main)            # inputs / previous step done
@@ -156,7 +142,7 @@ class FusedPipeline:
             with torch.cuda.stream(side2):
                 self.build_csr(("pixel",))
                 side2.wait_stream(side)
-                self.layer_sparse(bev, img, ("pixel",), aux=aux)
+                self.layer_sparse(bev, img, ("pixel",))
         self.build_csr(("cell",) if split else ("cell", "pixel"))
         main.wait_stream(side)            # sparse overwrites rows the dense pass wrote
         if events:
@@ -240,14 +226,13 @@ class FusedPipeline:
         main.wait_stream(sstream)
         main.wait_stream(dstream)
 
-    def backward(self, g_bv, g_img, d_bev, d_img, side2=None, aux=None):
+    def backward(self, g_bv, g_img, d_bev, d_img, side2=None):
         """TF gradient of the dual layer with the concat split and add_n fused:
         d_bev = g_bv[..., :Cb] + M^T-pull of g_img[..., Ci:]
         d_img = g_img[..., :Ci] + scatter of M-pulled g_bv[..., Cb:].
         With the builder's identity columns the forward entry lists already are
         in the gradients' TF order (ORDER_COL_ENTRY == ORDER_ENTRY / COL_ROW).
-        side2: the d_img pull runs there, beside the d_bev pull; aux: the
-        d_img pull's long runs beside its short ones."""
+        side2: the d_img pull runs there, beside the d_bev pull."""
         assert self.dual
         main = torch.cuda.current_stream(self.dev)
         w = self.Cb + self.Ci
@@ -262,7 +247,7 @@ class FusedPipeline:
         L.check(self._lib.shpl_pull(*cell, L.stream_of(self.dev)), "shpl_pull")
         with torch.cuda.stream(pst):
             L.check(self._lib.shpl_pull_dense(*pix, L.stream_of(self.dev)), "shpl_pull_dense")
-            self._sparse(pix, aux)
+            self._sparse(pix)
         if side2 is not None:
             main.wait_stream(side2)
 

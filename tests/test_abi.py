@@ -87,12 +87,6 @@ def test_argument_validation_is_host_side():
                   N) == L.ERR_BAD_SHAPE
         assert fn(L.BY_CELL, L.F32, ctypes.byref(csr), P, 32, 0, 32, N, 32, 0, 32, L.OUT_CONCAT, P, 64,
                   N) == L.ERR_ARG
-    # run classes: an unknown class, then the pull's own argument checks
-    assert lib.shpl_pull_sparse_runs(3, L.BY_CELL, L.F32, ctypes.byref(csr), P, 32, 0, 32, P, 32, 0, 32,
-                                     L.OUT_CONCAT, P, 64, N) == L.ERR_ARG
-    for runs in (L.RUNS_ALL, L.RUNS_SHORT, L.RUNS_LONG):
-        assert lib.shpl_pull_sparse_runs(runs, L.BY_CELL, L.F32, ctypes.byref(csr), P, 32, 0, 32, P, 32, 0, 32,
-                                         L.OUT_CONCAT, P, 48, N) == L.ERR_BAD_SHAPE
     # velodyne loader: P2 without image size, misaligned scan
     assert lib.shpl_velo_to_cam(1, P, 10, P, P, P, N, math.nan, N, P, P, N, P, 1 << 20, N) == L.ERR_ARG
     assert lib.shpl_velo_to_cam(1, P, 10, ctypes.c_void_p(260), P, N, N, math.nan, N, P, P, N, P, 1 << 20,

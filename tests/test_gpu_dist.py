@@ -1,0 +1,49 @@
+"""Config 4 on the GPU: bench.py's strong partition over 2 ranks
+on one device (gloo control plane, SHPL_DIST_BACKEND=gloo; the driver's
+scaling runs use RCCL, one rank per GPU) computes per-frame outputs identical
+to the single-rank run of the same global batch. The 2-rank run goes
+through bench.py's own `--gpus 2` self-launch."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+COMMON = ["--frames", "4", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+
+
+def _bench(args, env_extra=None, timeout=240):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", **(env_extra or {}))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("extra", [[], ["--config", "3"]])
+def test_strong_partition_two_ranks_matches_one(extra):
+    one = _bench(["--gpus", "1", *COMMON, *extra])
+    two = _bench(["--gpus", "2", *COMMON, *extra], {"SHPL_DIST_BACKEND": "gloo"})
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert two["scaling"] == "strong" and two["config"]["global_batch"] == 4
+    assert two["config"]["frames_per_gpu_per_step"] == 2
+    c1, c2 = one["frame_checksums"], two["frame_checksums"]
+    assert c1["frames"] == c2["frames"] == 4
+    assert c1["digest"] == c2["digest"], (c1, c2)
+    assert one["index_errors"] == 0 and two["index_errors"] == 0
+
+
+def test_weak_partition_is_the_global_batch_of_frames_times_ranks():
+    one = _bench(["--gpus", "1", *COMMON])
+    two = _bench(["--gpus", "2", "--frames", "2", "--partition", "weak", "--steps", "2", "--warmup", "1",
+                  "--no-cpu-baseline"], {"SHPL_DIST_BACKEND": "gloo"})
+    assert two["scaling"] == "weak" and two["config"]["global_batch"] == 4
+    assert one["frame_checksums"]["digest"] == two["frame_checksums"]["digest"]

@@ -391,18 +391,26 @@ def test_full_size_properties_config5():
         (frames[0].voxel_indices[:, 1] >= spec.bv_size[0]).sum())
 
 
-@pytest.mark.parametrize("dtype,mode", [("f32", "eager"), ("bf16", "eager"), ("bf16", "streams"),
-                                        ("f32", "graph"), ("bf16", "split"), ("f32", "split")])
-def test_pipeline_backward_matches_oracle(dtype, mode):
-    """FusedPipeline.backward (the config-3 bench gradient) vs the oracle's TF gradients;
-    mode streams/graph: the bench's step (side streams for the streaming half and the
-    pixel-keyed chain), launched eagerly or replayed from a captured HIP graph."""
+@pytest.mark.parametrize("cfg,dtype,mode", [(1, "f32", "eager"), (1, "bf16", "eager"), (1, "bf16", "streams"),
+                                            (1, "f32", "graph"), (3, "bf16", "eager"), (3, "bf16", "graph")])
+def test_pipeline_backward_matches_oracle(cfg, dtype, mode):
+    """FusedPipeline forward + backward (the config-3 bench step) vs the oracle's TF
+    forward and gradients; mode streams/graph: the bench's step (side streams for the
+    streaming half and the pixel-keyed chain), launched eagerly or replayed from a
+    captured HIP graph. cfg 3 is the bench's own shape: bf16, 256 channels (32 chunks
+    per pooled row, the power-of-two path), stride 8, pixel runs far longer than
+    k_sparse's 8 entries (k_sparse_long with per-column partials in OUT_ADD mode)."""
     from sparse_pooling_amd import pipeline
-    spec = synth.CONFIGS[1]
-    frames = [synth.make_frame(spec, seed=60 + f, n_outside=10) for f in range(2)]
+    spec = synth.CONFIGS[cfg]
+    B = 2 if cfg == 1 else 4
+    frames = [synth.make_frame(spec, seed=60 + f, n_outside=10) for f in range(B)]
+    refs = [_oracle_frame(fr, spec.stride) for fr in frames]
+    if cfg == 3:  # the long-run path is really exercised
+        runs = max(np.unique(r["img_index_flip_pool"][:, 1:], axis=0, return_counts=True)[1].max() for r in refs)
+        assert runs > 16, runs
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
     tdt = torch.float32 if dtype == "f32" else torch.bfloat16
-    pl = pipeline.FusedPipeline(2, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev, spec.c_img,
+    pl = pipeline.FusedPipeline(B, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev, spec.c_img,
                                 dtype=tdt, dual=True)
     Hb, Wb = spec.bev_feat_hw
     Hi, Wi = spec.img_feat_hw
@@ -413,24 +421,22 @@ def test_pipeline_backward_matches_oracle(dtype, mode):
         if dtype == "bf16":
             x = orc.from_bf16_bits(orc.to_bf16_bits(x)).reshape(shape)
         return x, torch.from_numpy(x).to(DEV).to(tdt)
-    bev, tb = mk((2, Hb, Wb, Cb), 1)
-    img, ti = mk((2, Hi, Wi, Ci), 2)
-    gb, tgb = mk((2, Hb, Wb, Cb + Ci), 3)
-    gi, tgi = mk((2, Hi, Wi, Ci + Cb), 4)
+    bev, tb = mk((B, Hb, Wb, Cb), 1)
+    img, ti = mk((B, Hi, Wi, Ci), 2)
+    gb, tgb = mk((B, Hb, Wb, Cb + Ci), 3)
+    gi, tgi = mk((B, Hi, Wi, Ci + Cb), 4)
     d_bev, d_img = torch.empty_like(tb), torch.empty_like(ti)
     if mode == "eager":
         pl.step(pts, vox, off, P, tb, ti)
         pl.backward(tgb, tgi, d_bev, d_img)
     else:
         side, side2 = torch.cuda.Stream(), torch.cuda.Stream()
-        # split: the pixel-keyed pulls' long runs on a fourth stream
-        aux = torch.cuda.Stream() if mode.startswith("split") else None
 
         def step():
-            pl.step_overlapped(pts, vox, off, P, tb, ti, side, side2=side2, aux=aux)
-            pl.backward(tgb, tgi, d_bev, d_img, side2=side2, aux=aux)
+            pl.step_overlapped(pts, vox, off, P, tb, ti, side, side2=side2)
+            pl.backward(tgb, tgi, d_bev, d_img, side2=side2)
         step()
-        if mode.endswith("graph"):
+        if mode == "graph":
             torch.cuda.synchronize()
             for t in (pl.bv_fused, pl.img_fused, d_bev, d_img):
                 t.fill_(float("nan"))
@@ -442,29 +448,24 @@ def test_pipeline_backward_matches_oracle(dtype, mode):
             g.replay()
             g.replay()
     torch.cuda.synchronize()
-    if mode != "eager":  # the forward outputs as well
-        for f, fr in enumerate(frames):
-            ref = _oracle_frame(fr, spec.stride)
-            eb, ei = orc.sparse_pool_layer(bev[f:f + 1], img[f:f + 1], ref["Mij_pool"], ref["M_val"],
-                                           ref["M_size"], ref["img_index_flip_pool"], dual=True)
-            if dtype == "f32":
-                _close_and_exact(pl.bv_fused[f:f + 1], eb)
-                _close_and_exact(pl.img_fused[f:f + 1], ei)
-    for f, fr in enumerate(frames):
-        ref = _oracle_frame(fr, spec.stride)
+
+    def same(got, want):
+        if dtype == "f32":
+            _close_and_exact(got, want)
+        else:
+            np.testing.assert_array_equal(_np(got.view(torch.int16)).view(np.uint16),
+                                          orc.to_bf16_bits(want.astype(np.float32)))
+    for f, ref in enumerate(refs):
         mij, mval, msize, idx = ref["Mij_pool"], ref["M_val"], ref["M_size"], ref["img_index_flip_pool"]
+        eb, ei = orc.sparse_pool_layer(bev[f:f + 1], img[f:f + 1], mij, mval, msize, idx, dual=True)
+        same(pl.bv_fused[f:f + 1], eb)
+        same(pl.img_fused[f:f + 1], ei)
         e_img = gi[f:f + 1, ..., :Ci] + orc.sparse_pool_grad_img(
             mij, mval, msize, gb[f, ..., Cb:].reshape(-1, Ci), idx, (1, Hi, Wi, Ci))
         e_bev = gb[f:f + 1, ..., :Cb] + orc.sparse_pool_trans_grad_bev(
             mij, mval, msize, np.ascontiguousarray(gi[f:f + 1, ..., Ci:]), idx).reshape(1, Hb, Wb, Cb)
-        if dtype == "f32":
-            _close_and_exact(d_img[f:f + 1], e_img)
-            _close_and_exact(d_bev[f:f + 1], e_bev)
-        else:
-            got_i = _np(d_img[f:f + 1].view(torch.int16)).view(np.uint16)
-            got_b = _np(d_bev[f:f + 1].view(torch.int16)).view(np.uint16)
-            np.testing.assert_array_equal(got_i, orc.to_bf16_bits(e_img.astype(np.float32)))
-            np.testing.assert_array_equal(got_b, orc.to_bf16_bits(e_bev.astype(np.float32)))
+        same(d_img[f:f + 1], e_img)
+        same(d_bev[f:f + 1], e_bev)
 
 
 # ---------------------------------------------------------------- BEV voxelizer
