@@ -50,20 +50,30 @@
 #define SHPLO_ERR_SHAPE 1
 
 /* ---- a1: projectToImage (avod/avod/utils/transform.py:3-26) -----------------
- * numpy evaluates np.dot(P, [x;y;z;1]) through OpenBLAS dgemm, which
- * accumulates the K=4 products as one fused-multiply-add chain in k order.
- * That chain was checked bit-exact against np.dot on 2M random points
- * (every column count >= 2; a single column goes through dgemv instead). */
-static void project(const double *P, double x, double y, double z, double *u, double *v)
+ * numpy evaluates np.dot(P, [x;y;z;1]) through OpenBLAS. With two or more
+ * columns that is dgemm, which accumulates the K=4 products as one
+ * fused-multiply-add chain in k order (checked bit-exact against np.dot on 2M
+ * random points, column counts 2 .. 120000). With ONE column (a frame of one
+ * point, or one survivor of the clip) numpy calls dgemv, which sums
+ * (a0*x0 + a2*x2) + (a1*x1 + a3*x3) with every product rounded (probed
+ * against np.dot for 3x4 and 4x4 matrices; pinned by tests/golden/
+ * index_single_*.npz, index_one_survivor.npz, kitti_single.npz). */
+static double dot4(const double *p, const double *a, int gemv)
+{
+    if (gemv)
+        return (p[0] * a[0] + p[2] * a[2]) + (p[1] * a[1] + p[3] * a[3]);
+    double s = p[0] * a[0];
+    for (int k = 1; k < 4; ++k)
+        s = fma(p[k], a[k], s);
+    return s;
+}
+
+static void project(const double *P, double x, double y, double z, int gemv, double *u, double *v)
 {
     const double a[4] = {x, y, z, 1.0};
     double r[3];
-    for (int i = 0; i < 3; ++i) {
-        double s = P[4 * i] * a[0];
-        for (int k = 1; k < 4; ++k)
-            s = fma(P[4 * i + k], a[k], s);
-        r[i] = s;
-    }
+    for (int i = 0; i < 3; ++i)
+        r[i] = dot4(P + 4 * i, a, gemv);
     *u = r[0] / r[2];
     *v = r[1] / r[2];
 }
@@ -77,22 +87,35 @@ static int inside_image(double u, double v, double w_img, double h_img)
 /* a3: gen_sparse_pooling_input_avod (sparse_pool_utils.py:6-20).
  * pts: n x 3 (camera frame), vox: n x 2, P: 3 x 4 (row-major).
  * Outputs (capacity n): bv_index nv x 2, img_index 3 rows of stride `ld`
- * ([u; v; 0], rounded half-to-even like np.round). Returns nv. */
+ * ([u; v; 0], rounded half-to-even like np.round). Returns nv.
+ * Two projections as in the reference: the clip over all n columns (:13),
+ * then projectToImage over the nv survivors (:16) -- dgemv when either
+ * count is one. */
 int64_t shplo_gen_index(int64_t n, const double *pts, const int64_t *vox, const double *P,
                         double im_w, double im_h, int64_t *bv_index, double *img_index, int64_t ld)
 {
     int64_t nv = 0;
     for (int64_t i = 0; i < n; ++i) {
         double u, v;
-        project(P, pts[3 * i], pts[3 * i + 1], pts[3 * i + 2], &u, &v);
+        project(P, pts[3 * i], pts[3 * i + 1], pts[3 * i + 2], n == 1, &u, &v);
         if (!inside_image(u, v, im_w, im_h))
             continue;
         bv_index[2 * nv] = vox[2 * i];
         bv_index[2 * nv + 1] = vox[2 * i + 1];
         img_index[nv] = (double)(int64_t)nearbyint(u);
         img_index[ld + nv] = (double)(int64_t)nearbyint(v);
-        img_index[2 * ld + nv] = 0.0;
+        img_index[2 * ld + nv] = (double)i;  /* the survivor's point, re-projected below */
         ++nv;
+    }
+    for (int64_t j = 0; j < nv; ++j) {
+        const int64_t i = (int64_t)img_index[2 * ld + j];
+        img_index[2 * ld + j] = 0.0;
+        if (nv != 1 || n == 1)
+            continue;  /* same order as the clip's projection */
+        double u, v;
+        project(P, pts[3 * i], pts[3 * i + 1], pts[3 * i + 2], 1, &u, &v);
+        img_index[j] = (double)(int64_t)nearbyint(u);
+        img_index[ld + j] = (double)(int64_t)nearbyint(v);
     }
     return nv;
 }
@@ -471,8 +494,10 @@ int64_t shplo_mv3d_voxels(int64_t n, const double *pts, int64_t stride, const in
  *   lidar_to_cam_frame (calib_utils.py:371-410): p_cam = (R0_rect4 . Tr_velo_to_cam4) . [x;y;z;1]
  *     -- `rect` is that 4x4 product's rows 0-2, computed by numpy on the host; the
  *     per-point np.dot is OpenBLAS dgemm, i.e. the same FMA chain as project()
- *     (checked bit-exact against numpy for N = 2 .. 120000);
- *   keep z > 0 (:250), project with P2 (calib_utils.project_to_image :281-298),
+ *     (checked bit-exact against numpy for N = 2 .. 120000), dgemv's order for a
+ *     one-point scan (dot4);
+ *   keep z > 0 (:250), project with P2 (calib_utils.project_to_image :281-298;
+ *   dgemv's order when exactly one point has z > 0),
  *   keep 0 < u < W and 0 < v < H (strict, :256-259), im_size = [W, H].
  * has_filter = 0 mirrors im_size=None (every point, :244-246).
  * min_intensity (NaN = none): the reference compares the intensities of ALL
@@ -485,21 +510,22 @@ int64_t shplo_mv3d_voxels(int64_t n, const double *pts, int64_t stride, const in
 int64_t shplo_velo_to_cam(int64_t n, const float *xyzi, const double *rect, const double *P, int has_filter,
                           double im_w, double im_h, double min_intensity, int flip, double *out)
 {
-    int64_t k = 0;
+    int64_t k = 0, front = 0;
+    for (int64_t pass = has_filter ? 0 : 1; pass < 2; ++pass)
     for (int64_t i = 0; i < n; ++i) {
         const double a[4] = {(double)xyzi[4 * i], (double)xyzi[4 * i + 1], (double)xyzi[4 * i + 2], 1.0};
         double c[3];
-        for (int r = 0; r < 3; ++r) {
-            double s = rect[4 * r] * a[0];
-            for (int q = 1; q < 4; ++q)
-                s = fma(rect[4 * r + q], a[q], s);
-            c[r] = s;
+        for (int r = 0; r < 3; ++r)
+            c[r] = dot4(rect + 4 * r, a, n == 1);
+        if (pass == 0) {  /* the columns of project_to_image: points with z > 0 */
+            front += c[2] > 0.0;
+            continue;
         }
         if (has_filter) {
             if (!(c[2] > 0.0))
                 continue;
             double u, v;
-            project(P, c[0], c[1], c[2], &u, &v);
+            project(P, c[0], c[1], c[2], front == 1, &u, &v);
             if (!(u > 0.0 && u < im_w && v > 0.0 && v < im_h))
                 continue;
             if (!isnan(min_intensity) && !((double)xyzi[4 * i + 3] > min_intensity))

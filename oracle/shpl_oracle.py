@@ -15,7 +15,9 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "build", "libshpl_oracle.so")
+# SHPL_ORACLE_LIB: an alternative build of the same source, e.g. the
+# ASan/UBSan one (`make -C oracle san`, tests/test_oracle_sanitized.py)
+_LIB_PATH = os.environ.get("SHPL_ORACLE_LIB") or os.path.join(_HERE, "build", "libshpl_oracle.so")
 _lib = None
 
 

@@ -87,10 +87,25 @@ __device__ __forceinline__ double dot4_chain(const double *row, double a0, doubl
     return __fma_rn(row[3], 1.0, s);
 }
 
+// The same row product when np.dot has ONE column (a frame of one point, one
+// clip survivor): numpy calls OpenBLAS dgemv, which sums the rounded products
+// as (p0*a0 + p2*a2) + (p1*a1 + p3*a3) (probed against np.dot; pinned by
+// tests/golden/index_single_*, index_one_survivor, kitti_single).
+__device__ __forceinline__ double dot4_gemv(const double *row, double a0, double a1, double a2) {
+    return __dadd_rn(__dadd_rn(__dmul_rn(row[0], a0), __dmul_rn(row[2], a2)),
+                     __dadd_rn(__dmul_rn(row[1], a1), row[3]));
+}
+
+__device__ __forceinline__ double dot4(const double *row, double a0, double a1, double a2, bool gemv) {
+    return gemv ? dot4_gemv(row, a0, a1, a2) : dot4_chain(row, a0, a1, a2);
+}
+
 // projectToImage (avod/avod/utils/transform.py:3-26; calib_utils.project_to_image
-// :281-298): [u;v;w] = P [x;y;z;1]; u/=w; v/=w (IEEE division).
-__device__ __forceinline__ void project(const double *P, double x, double y, double z, double &u, double &v) {
-    const double r0 = dot4_chain(P, x, y, z), r1 = dot4_chain(P + 4, x, y, z), r2 = dot4_chain(P + 8, x, y, z);
+// :281-298): [u;v;w] = P [x;y;z;1]; u/=w; v/=w (IEEE division). gemv: the
+// product had one column (see dot4_gemv).
+__device__ __forceinline__ void project(const double *P, double x, double y, double z, double &u, double &v,
+                                        bool gemv = false) {
+    const double r0 = dot4(P, x, y, z, gemv), r1 = dot4(P + 4, x, y, z, gemv), r2 = dot4(P + 8, x, y, z, gemv);
     u = __ddiv_rn(r0, r2);
     v = __ddiv_rn(r1, r2);
 }

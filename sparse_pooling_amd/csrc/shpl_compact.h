@@ -6,9 +6,21 @@
 //                earlier chunks, in point order; each chunk also writes the
 //                sentinels of the unused capacity in its stretch of slots, and
 //                the frame's last chunk the frame's count.
-// A Stage provides: In/Payload types, load(i, in), eval(f, i, in, pl) -> keep,
-// touch(f, i, pl, keep) (every point, write pass), emit(f, i, pos, fstart, pl)
-// and hole(pos).
+// A Stage provides: In/Payload types, load(i, in), eval(ctx, f, i, in, pl) ->
+// flag mask, touch(f, i, pl, keep) (every point, write pass), emit(f, i, pos,
+// fstart, pl) and hole(pos).
+//
+// Column counts. numpy's np.dot over a frame's points evaluates a row product
+// in one order for two or more columns (dgemm) and in another for exactly one
+// (dgemv; shpl_common.h dot4_gemv). A stage's products therefore depend on
+// per-frame counts: ctx.n_live (the frame's points, known up front) and
+// ctx.n_aux (how many points pass the stage's first filter -- the columns of
+// its second product; -1 = not yet known, in k_count). eval returns
+//   KEEP_MULTI -- kept, when the second product has >= 2 columns (or none)
+//   KEEP_ONE   -- kept, when it has exactly one (n_aux == 1)
+//   AUX        -- the point is one of the second product's columns
+// k_count counts all three per chunk; k_compact sums the AUX counts of the
+// frame first, then uses the matching KEEP count and passes n_aux to eval.
 #pragma once
 
 #include "shpl_common.h"
@@ -20,10 +32,17 @@ constexpr int IDX_BLOCK = 1024;
 constexpr int IDX_BATCH = 4;                      // point rows per thread whose loads are in flight together
 constexpr int IDX_CHUNK = IDX_BLOCK * IDX_BATCH;  // points per workgroup: one round
 
+constexpr uint32_t KEEP_MULTI = 1u, KEEP_ONE = 2u, AUX = 4u;
+
+struct Ctx {
+    int64_t n_live;  // live points of the frame
+    int64_t n_aux;   // points of the frame with AUX set; -1 = unknown (k_count)
+};
+
 struct Frames {
     const int64_t *pt_off, *pt_count;
     int n_frames, n_chunks;  // chunks of IDX_CHUNK points per frame (grid.x)
-    int32_t *chunk_kept;     // [n_frames][n_chunks] workspace
+    int32_t *chunk_kept;     // [3][n_frames][n_chunks] workspace: KEEP_MULTI, KEEP_ONE, AUX counts
     int64_t *frame_nnz, *frame_out_off;
     uint32_t *err;
 };
@@ -35,37 +54,43 @@ __device__ __forceinline__ void frame_range(const Frames &fr, int f, int64_t &p0
     p1 = fr.pt_count ? (p0 + fr.pt_count[f] < cap_end ? p0 + fr.pt_count[f] : cap_end) : cap_end;
 }
 
-// Pass 1 (grid n_chunks x n_frames): kept points per chunk.
+// Pass 1 (grid n_chunks x n_frames): KEEP_MULTI / KEEP_ONE / AUX points per chunk.
 template <typename Stage>
 __global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr) {
-    __shared__ int32_t wsum[IDX_BLOCK / 64];
+    __shared__ int32_t wsum[3][IDX_BLOCK / 64];
     const int f = blockIdx.y, j = blockIdx.x;
     int64_t p0, p1, cap_end;
     frame_range(fr, f, p0, p1, cap_end);
     const int64_t base = p0 + (int64_t)j * IDX_CHUNK;
     if (j == fr.n_chunks - 1 && p1 > base + IDX_CHUNK && threadIdx.x == 0 && fr.err)
         atomicOr(fr.err, SHPL_EBIT_CAPACITY);  // frame larger than max_points_per_frame
+    const Ctx ctx{p1 - p0, -1};
     typename Stage::In in[IDX_BATCH];
 #pragma unroll
     for (int u = 0; u < IDX_BATCH; ++u) {
         const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
         if (i < p1) st.load(i, in[u]);
     }
-    int32_t n = 0;
+    int32_t n[3] = {0, 0, 0};
 #pragma unroll
     for (int u = 0; u < IDX_BATCH; ++u) {
         const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
         typename Stage::Payload pl;
-        if (i < p1 && st.eval(f, i, in[u], pl)) ++n;
+        const uint32_t m = i < p1 ? st.eval(ctx, f, i, in[u], pl) : 0u;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) n[k] += (m >> k) & 1u;
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = n;
+    for (int k = 0; k < 3; ++k) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) n[k] += __shfl_xor(n[k], o, 64);
+        if ((threadIdx.x & 63) == 0) wsum[k][threadIdx.x >> 6] = n[k];
+    }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 3) {
         int32_t t = 0;
-        for (int w = 0; w < IDX_BLOCK / 64; ++w) t += wsum[w];
-        fr.chunk_kept[(int64_t)f * fr.n_chunks + j] = t;
+        for (int w = 0; w < IDX_BLOCK / 64; ++w) t += wsum[threadIdx.x][w];
+        fr.chunk_kept[((int64_t)threadIdx.x * fr.n_frames + f) * fr.n_chunks + j] = t;
     }
 }
 
@@ -77,15 +102,29 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr) {
 template <typename Stage>
 __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr) {
     __shared__ int32_t wsum[IDX_BATCH][IDX_BLOCK / 64];
-    __shared__ int32_t pre[IDX_BLOCK / 64], all[IDX_BLOCK / 64];
+    __shared__ int32_t pre[IDX_BLOCK / 64], all[IDX_BLOCK / 64], naux[IDX_BLOCK / 64];
     const int f = blockIdx.y, j = blockIdx.x;
     int64_t p0, p1, cap_end;
     frame_range(fr, f, p0, p1, cap_end);
     const int wid = threadIdx.x >> 6;
+    // the frame's AUX count picks the KEEP count (and the stage's product order)
+    const int32_t *aux_c = fr.chunk_kept + ((int64_t)2 * fr.n_frames + f) * fr.n_chunks;
+    int32_t na = 0;
+    for (int q = threadIdx.x; q < fr.n_chunks; q += IDX_BLOCK) na += aux_c[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) na += __shfl_xor(na, o, 64);
+    if ((threadIdx.x & 63) == 0) naux[wid] = na;
+    __syncthreads();
+    int64_t n_aux = 0;
+    for (int w = 0; w < IDX_BLOCK / 64; ++w) n_aux += naux[w];
+    const Ctx ctx{p1 - p0, n_aux};
+    const int variant = n_aux == 1 ? 1 : 0;
+    const uint32_t keep_bit = variant ? KEEP_ONE : KEEP_MULTI;
     // kept points of the earlier chunks, and of the whole frame
+    const int32_t *kept_c = fr.chunk_kept + ((int64_t)variant * fr.n_frames + f) * fr.n_chunks;
     int32_t mine = 0, every = 0;
     for (int q = threadIdx.x; q < fr.n_chunks; q += IDX_BLOCK) {
-        const int32_t c = fr.chunk_kept[(int64_t)f * fr.n_chunks + q];
+        const int32_t c = kept_c[q];
         mine += q < j ? c : 0;
         every += c;
     }
@@ -113,7 +152,7 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr) {
         const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
         keep[u] = false;
         if (i < p1) {
-            keep[u] = st.eval(f, i, in[u], pl[u]);
+            keep[u] = (st.eval(ctx, f, i, in[u], pl[u]) & keep_bit) != 0;
             st.touch(f, i, pl[u], keep[u]);
         }
         m[u] = __ballot(keep[u]);
@@ -158,7 +197,7 @@ int n_chunks_for(int64_t max_points) {
 constexpr size_t IDX_WS_HEAD = 256;  // single-frame [0, n] offsets
 
 size_t index_ws_bytes(int n_frames, int64_t max_points) {
-    return IDX_WS_HEAD + align_up(sizeof(int32_t) * (size_t)n_frames * (size_t)n_chunks_for(max_points), 256);
+    return IDX_WS_HEAD + align_up(3 * sizeof(int32_t) * (size_t)n_frames * (size_t)n_chunks_for(max_points), 256);
 }
 
 template <typename Stage>

@@ -13,8 +13,12 @@
 // the next frame is filled with -1 sentinels that every consumer skips, so no
 // cross-frame scan is needed.
 // Projection runs in f64 with the exact operation order numpy uses (an FMA
-// chain over k for np.dot, IEEE division, rint = round-half-even), so the
-// integer outputs are bit-identical to the reference (tests/golden/index_*).
+// chain over k for np.dot, dgemv's order when the product has one column,
+// IEEE division, rint = round-half-even), so the integer outputs are
+// bit-identical to the reference (tests/golden/index_*). The reference
+// projects twice: the clip over the frame's N points (transform.py:34 via
+// sparse_pool_utils.py:13), then projectToImage over the clip's survivors
+// (:16) -- one column each when N == 1, resp. when one point survives.
 #include "shpl_compact.h"
 
 namespace shpl {
@@ -115,14 +119,16 @@ struct FusedStage {
         in.vx = load_idx<VT>(vox, i * vstride);
         in.vz = load_idx<VT>(vox, i * vstride + 1);
     }
-    __device__ bool eval(int f, int64_t, const In &in, Payload &pl) const {
+    // AUX = inside the clip (the columns of the second projection)
+    __device__ uint32_t eval(const Ctx &c, int f, int64_t, const In &in, Payload &pl) const {
         double u, v;
-        project(P + 12 * f, in.x, in.y, in.z, u, v);
-        if (!in_image(u, v, g.im_w, g.im_h)) return false;
+        project(P + 12 * f, in.x, in.y, in.z, u, v, c.n_live == 1);
+        if (!in_image(u, v, g.im_w, g.im_h)) return 0u;
+        if (c.n_aux == 1 && c.n_live != 1) project(P + 12 * f, in.x, in.y, in.z, u, v, true);
         const double ur = (double)(int64_t)rint(u);
         const double vr = (double)(int64_t)rint(v);
         pl.pr = produce(g, ur, vr, in.vx, in.vz);
-        return pl.pr.inside;
+        return AUX | (pl.pr.inside ? KEEP_MULTI | KEEP_ONE : 0u);
     }
     __device__ void touch(int, int64_t, const Payload &, bool) const {}
     __device__ void emit(int f, int64_t i, int64_t pos, int64_t fstart, const Payload &pl) const {
@@ -170,9 +176,11 @@ struct GenStage {  // gen_sparse_pooling_input_avod
     };
 
     __device__ void load(int64_t i, In &in) const { load_point<PT>(pts, i, in.x, in.y, in.z); }
-    __device__ bool eval(int f, int64_t, const In &in, Payload &pl) const {
-        project(P + 12 * f, in.x, in.y, in.z, pl.u, pl.v);
-        return in_image(pl.u, pl.v, im_w, im_h);
+    __device__ uint32_t eval(const Ctx &c, int f, int64_t, const In &in, Payload &pl) const {
+        project(P + 12 * f, in.x, in.y, in.z, pl.u, pl.v, c.n_live == 1);
+        if (!in_image(pl.u, pl.v, im_w, im_h)) return 0u;
+        if (c.n_aux == 1 && c.n_live != 1) project(P + 12 * f, in.x, in.y, in.z, pl.u, pl.v, true);
+        return AUX | KEEP_MULTI | KEEP_ONE;
     }
     __device__ void touch(int, int64_t, const Payload &, bool) const {}
     __device__ void emit(int, int64_t i, int64_t pos, int64_t, const Payload &pl) const {
@@ -212,10 +220,10 @@ struct ProduceStage {  // produce_sparse_pooling_input (in-place img_index updat
         in.vx = load_idx<VT>(bv, i * bstride);
         in.vz = load_idx<VT>(bv, i * bstride + 1);
     }
-    __device__ bool eval(int, int64_t, const In &in, Payload &pl) const {
+    __device__ uint32_t eval(const Ctx &, int, int64_t, const In &in, Payload &pl) const {
         pl.pr = produce(g, in.u, in.v, in.vx, in.vz);
         pl.w = in.w;
-        return pl.pr.inside;
+        return pl.pr.inside ? KEEP_MULTI | KEEP_ONE : 0u;
     }
     // img_index[0:2] = floor(img_index/stride), clamped -- for EVERY point
     // (sparse_pool_utils.py:30-34), after this thread has read its own value.

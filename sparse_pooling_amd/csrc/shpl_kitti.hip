@@ -9,8 +9,10 @@
 //     (applied to the camera-frame cloud, kitti_dataset.py:305-306)
 // Per point: p_cam = rect . [x; y; z; 1] where rect = rows 0-2 of
 // R0_rect4 . Tr_velo_to_cam4 (numpy's 4x4 product, done on the host), as the
-// dgemm FMA chain numpy uses; with an image size: keep z > 0, project with P2
-// and keep 0 < u < W, 0 < v < H (strict). The kept points are compacted in
+// dgemm FMA chain numpy uses (dgemv's order for a one-point scan); with an
+// image size: keep z > 0, project with P2 (dgemv's order when exactly one
+// point has z > 0: the projection's only column) and keep 0 < u < W,
+// 0 < v < H (strict). The kept points are compacted in
 // scan order by the chunked stable compaction of shpl_compact.h.
 // File parsing (read_calibration, read_lidar, get_road_plane) is host code
 // (sparse_pooling_amd/kitti.py); the scans arrive here as one [N,4] f32 batch.
@@ -43,19 +45,26 @@ struct VeloStage {
         in.z = v[2];
         in.i = v[3];
     }
-    __device__ bool eval(int f, int64_t, const In &in, Payload &pl) const {
+    // AUX = z > 0 (the columns of project_to_image); KEEP_MULTI / KEEP_ONE: the
+    // image filter with the projection in dgemm / dgemv order
+    __device__ uint32_t eval(const Ctx &c, int f, int64_t, const In &in, Payload &pl) const {
         const double *r = rect + 12 * f;
         const double x = (double)in.x, y = (double)in.y, z = (double)in.z;
-        pl.c[0] = dot4_chain(r, x, y, z);
-        pl.c[1] = dot4_chain(r + 4, x, y, z);
-        pl.c[2] = dot4_chain(r + 8, x, y, z);
-        if (!P) return true;  // im_size=None: every point (obj_utils.py:244-246)
-        if (!(pl.c[2] > 0.0)) return false;
-        double u, v;
-        project(P + 12 * f, pl.c[0], pl.c[1], pl.c[2], u, v);
+        const bool one = c.n_live == 1;
+        pl.c[0] = dot4(r, x, y, z, one);
+        pl.c[1] = dot4(r + 4, x, y, z, one);
+        pl.c[2] = dot4(r + 8, x, y, z, one);
+        if (!P) return KEEP_MULTI | KEEP_ONE;  // im_size=None: every point (obj_utils.py:244-246)
+        if (!(pl.c[2] > 0.0)) return 0u;
+        if (!(isnan(min_int) || (double)in.i > min_int)) return AUX;
         const double w = im[2 * f], h = im[2 * f + 1];
-        if (!(u > 0.0 && u < w && v > 0.0 && v < h)) return false;
-        return isnan(min_int) || (double)in.i > min_int;
+        uint32_t m = AUX;
+        double u, v;
+        project(P + 12 * f, pl.c[0], pl.c[1], pl.c[2], u, v, false);
+        if (u > 0.0 && u < w && v > 0.0 && v < h) m |= KEEP_MULTI;
+        project(P + 12 * f, pl.c[0], pl.c[1], pl.c[2], u, v, true);
+        if (u > 0.0 && u < w && v > 0.0 && v < h) m |= KEEP_ONE;
+        return m;
     }
     __device__ void touch(int, int64_t, const Payload &, bool) const {}
     __device__ void emit(int f, int64_t, int64_t pos, int64_t, const Payload &pl) const {

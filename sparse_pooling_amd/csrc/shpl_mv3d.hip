@@ -32,9 +32,11 @@ struct Mv3dGeom {
 };
 
 // projectToImage + np.round (minibatch_mv3d_img.py:88-91)
-__device__ __forceinline__ void project_round(const double *P, double x, double y, double z, int64_t &u, int64_t &v) {
+// (gemv: the frame has one point, so np.dot has one column -- dgemv's order)
+__device__ __forceinline__ void project_round(const double *P, double x, double y, double z, int64_t &u, int64_t &v,
+                                              bool gemv) {
     double uf, vf;
-    project(P, x, y, z, uf, vf);
+    project(P, x, y, z, uf, vf, gemv);
     u = (int64_t)rint(uf);
     v = (int64_t)rint(vf);
 }
@@ -135,7 +137,7 @@ __global__ __launch_bounds__(TS_BLOCK) void k_mv3d_frame(Mv3dGeom g, const int64
             voxel_key(g, q[0], q[1], q[2], si, fi);
             int64_t u, v;
             if (g.has_proj) {
-                project_round(P + 12 * f, q[0], q[1], q[2], u, v);
+                project_round(P + 12 * f, q[0], q[1], q[2], u, v, p1 - p0 == 1);
             } else {
                 u = img2[i];
                 v = img2[img2_ld + i];

@@ -8,6 +8,9 @@
 * ``sparse_pool`` mirrors the ``@layer sparse_pool`` of
   MV3D_TF_release/lib/networks/network.py:243-246:
   ``input = [M, img_features, img_index_flip]``.
+* ``calib_to_P`` / ``calib_to_L2C`` mirror MV3D_TF_release/lib/utils/
+  transform.py:13-30: the camera matrix the minibatch projects with
+  (minibatch_mv3d_img.py:89) from the imdb's 4x12 calib rows.
 
 M_val here is the MV3D voxel weight 1/count (construct_voxel.py:160); it is
 carried unchanged to the pull kernels, which then compute per-voxel means
@@ -29,6 +32,37 @@ def produce_sparse_pooling_input(img_index, im_size, bv_index, bv_size, M_val=No
 def sparse_pool(input, pooled_size):  # noqa: A002 (reference signature)
     """0 is the sparse matrix M, 1 the source feature map, 2 the pooling index."""
     return spu._sparse_pool_op(input[0], input[1], input[2], pooled_size)
+
+
+def calib_to_P(calib, from_camera=False):
+    """Lidar (or camera, from_camera=True) coordinates -> image: the 3x4 P with
+    uvw = P [X; Y; Z; 1]. calib rows (imdb layout): 0 = P2 (3x4), 2 = R0 read
+    as 4x3 and closed by the column [0, 0, 0, 1], 3 = Tr_velo_to_cam (3x4)
+    closed by the row [0, 0, 0, 1]; P = (P2 . R0) . C2V, evaluated in that
+    association (numpy matmul) like transform.py:22-23."""
+    import numpy as np
+    calib = np.asarray(calib, dtype=np.float64)
+    p2 = calib[0].reshape(3, 4)
+    if from_camera:
+        return p2
+    return np.matmul(np.matmul(p2, _r0_4x4(calib)), _c2v_4x4(calib))
+
+
+def calib_to_L2C(calib):
+    """Lidar -> camera frame: R0 . C2V (transform.py:26-30), both closed to 4x4."""
+    import numpy as np
+    calib = np.asarray(calib, dtype=np.float64)
+    return np.matmul(_r0_4x4(calib), _c2v_4x4(calib))
+
+
+def _r0_4x4(calib):
+    import numpy as np
+    return np.concatenate([calib[2].reshape(4, 3), np.array([[0.0], [0.0], [0.0], [1.0]])], axis=1)
+
+
+def _c2v_4x4(calib):
+    import numpy as np
+    return np.concatenate([calib[3].reshape(3, 4), np.array([[0.0, 0.0, 0.0, 1.0]])], axis=0)
 
 
 # MV3D voxel config (MV3D_TF_release/lib/utils/config_voxels.py:49-59, DETECT_OBJ != 'Car')

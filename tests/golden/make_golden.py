@@ -185,6 +185,122 @@ KITTI_CALIB = synth.KITTI_CALIB
 synthetic_scan = synth.synthetic_scan
 
 
+# ---- single-column products: np.dot(A, x) with x of one column goes through
+# OpenBLAS dgemv, whose sum order ((a0*x0 + a2*x2) + (a1*x1 + a3*x3)) differs
+# from dgemm's FMA chain. The searches below look for points where the two
+# orders give different integer outputs (rounded pixel, clip decision), so the
+# goldens discriminate; the reference then runs on them as on any frame.
+def _fma(a, b, c):
+    from fractions import Fraction
+    return float(Fraction(a) * Fraction(b) + Fraction(c))
+
+
+def _dot_chain(p, a):
+    return _fma(p[3], a[3], _fma(p[2], a[2], _fma(p[1], a[1], p[0] * a[0])))
+
+
+def _dot_gemv(p, a):
+    return (p[0] * a[0] + p[2] * a[2]) + (p[1] * a[1] + p[3] * a[3])
+
+
+def _uv(P, pt, dot):
+    a = (pt[0], pt[1], pt[2], 1.0)
+    r = [dot(P[i], a) for i in range(3)]
+    return r[0] / r[2], r[1] / r[2]
+
+
+def _search_x(P, y, z, target, pred, rng, span=600):
+    """x near the point whose u equals `target` (y, z given; z nudged until one is
+    found) with pred(u_chain, u_gemv) true: a linear walk over x's neighbours."""
+    for _ in range(200):
+        base = (target * (P[2, 2] * z + P[2, 3]) - P[0, 2] * z - P[0, 3]) / P[0, 0]
+        lo = base
+        for _ in range(span):
+            lo = np.nextafter(lo, -np.inf)
+        x = lo
+        for _ in range(2 * span):
+            uc, _ = _uv(P, (x, y, z), _dot_chain)
+            ug, _ = _uv(P, (x, y, z), _dot_gemv)
+            if pred(uc, ug):
+                return x
+            x = np.nextafter(x, np.inf)
+        z = z + rng.uniform(0.01, 0.5)
+    raise RuntimeError("no discriminating point found")
+
+
+def _single_case():
+    """Frames whose projections go through dgemv (transform.py:17-19 with one column):
+    single_tie  -- one point, round(u) differs between the two orders;
+    single_clip -- one point, u < W-1 under one order and not the other;
+    one_survivor -- 40 points, exactly one inside the clip, at a rounding tie (the clip
+                    runs as dgemm over all columns, the projection of the survivor as dgemv)."""
+    rng = np.random.default_rng(31)
+    P = synth.KITTI_P2
+    im, bv = (1200, 360), (704, 800)
+    spec = synth.FrameSpec(1, im, bv)
+
+    def frame(pts, vox):
+        return synth.Frame(np.asarray(pts, dtype=np.float64).reshape(-1, 3), np.asarray(vox, dtype=np.int64),
+                           P, spec)
+    y, z = 0.7, 23.0
+    tie = lambda uc, ug: np.round(uc) != np.round(ug) and 0 <= min(uc, ug) and max(uc, ug) < im[0] - 1  # noqa
+    x = _search_x(P, y, z, 500.5, tie, rng)
+    _index_case("single_tie", frame([x, y, z], [[300, 400]]), im, bv, (1, 1))
+    clip = lambda uc, ug: (uc < im[0] - 1) != (ug < im[0] - 1)  # noqa
+    x = _search_x(P, -1.1, 31.0, im[0] - 1.0, clip, rng)
+    _index_case("single_clip", frame([x, -1.1, 31.0], [[10, 20]]), im, bv, (1, 1))
+    x = _search_x(P, 0.3, 12.0, 731.5, tie, rng)
+    out = np.stack([rng.uniform(60, 90, 39), rng.uniform(-2, 2, 39), rng.uniform(5, 10, 39)], 1)
+    pts = np.insert(out, 17, [x, 0.3, 12.0], axis=0)
+    vox = np.stack([rng.integers(0, bv[1], 40), rng.integers(0, bv[0], 40)], 1)
+    _index_case("one_survivor", frame(pts, vox), im, bv, (2, 2))
+
+
+def _mv3d_calib_case():
+    """MV3D transform.calib_to_P / calib_to_L2C (MV3D_TF_release/lib/utils/transform.py:13-30)
+    on a random imdb-layout calib (4 x 12 rows)."""
+    import importlib
+    tr = importlib.import_module("utils.transform")
+    rng = np.random.default_rng(51)
+    calib = rng.normal(0, 1, (4, 12)) * np.array([700, 1, 600, 40, 1, 700, 170, 0.2, 1, 1, 1, 0.003])
+    np.savez_compressed(os.path.join(HERE, "mv3d_calib.npz"), calib=calib, P=tr.calib_to_P(calib.copy()),
+                        P_cam=tr.calib_to_P(calib.copy(), from_camera=True), L2C=tr.calib_to_L2C(calib.copy()))
+    print("mv3d_calib: P", tr.calib_to_P(calib.copy()).shape)
+
+
+def _kitti_single_case():
+    """get_lidar_point_cloud on scans whose products are single-column (dgemv):
+    a one-point scan (lidar_to_cam_frame with one column, then the FOV projection),
+    and a scan whose only point in front of the camera is its one FOV candidate."""
+    import tempfile
+    from wavedata.tools.core import calib_utils
+    from wavedata.tools.obj_detection import obj_utils
+    rng = np.random.default_rng(41)
+    rec = {}
+    text = "".join(f"{k}: " + " ".join(f"{v:.12e}" for v in vals) + "\n" for k, vals in KITTI_CALIB.items())
+    shape = (375, 1242)
+    with tempfile.TemporaryDirectory() as d:
+        for sub in ("calib", "velodyne"):
+            os.makedirs(os.path.join(d, sub))
+        scans = {0: np.array([[11.3, 1.7, -0.4, 0.5]], np.float32)}
+        behind = np.stack([rng.uniform(-30, -5, 30), rng.uniform(-5, 5, 30), rng.uniform(-1, 1, 30),
+                           rng.uniform(0, 1, 30)], 1).astype(np.float32)
+        scans[1] = np.insert(behind, 11, [9.6, -2.2, 0.3, 0.9], axis=0)
+        for idx, scan in scans.items():
+            with open(os.path.join(d, "calib", "%06d.txt" % idx), "w") as fh:
+                fh.write(text)
+            scan.tofile(os.path.join(d, "velodyne", "%06d.bin" % idx))
+            pc = obj_utils.get_lidar_point_cloud(idx, os.path.join(d, "calib"), os.path.join(d, "velodyne"),
+                                                 im_size=[shape[1], shape[0]])
+            pc_all = obj_utils.get_lidar_point_cloud(idx, os.path.join(d, "calib"), os.path.join(d, "velodyne"))
+            fc = calib_utils.read_calibration(os.path.join(d, "calib"), idx)
+            rec.update({f"{idx}_velo": scan, f"{idx}_point_cloud": pc, f"{idx}_point_cloud_all": pc_all,
+                        f"{idx}_p2": fc.p2, f"{idx}_r0_rect": fc.r0_rect, f"{idx}_tr": fc.tr_velodyne_to_cam})
+            print(f"kitti_single {idx}: scan {scan.shape[0]} -> FOV {pc.shape[1]}")
+    rec["image_shape"] = np.array(shape)
+    np.savez_compressed(os.path.join(HERE, "kitti_single.npz"), **rec)
+
+
 def _kitti_case():
     """obj_utils.get_lidar_point_cloud / calib_utils.read_calibration /
     get_road_plane + the kitti_aug flips on synthetic KITTI files."""
@@ -252,10 +368,13 @@ def main():
         _index_case("empty", e, s0.im_size, s0.bv_size, s0.stride)
     except Exception as ex:  # record what the reference does with no points
         print("empty frame: reference raised", type(ex).__name__, ex)
+    _single_case()
     _bev_slices_case()
     _mv3d_voxel_case()
     _mv3d_voxel_case(dense=True)
     _kitti_case()
+    _kitti_single_case()
+    _mv3d_calib_case()
 
 
 if __name__ == "__main__":

@@ -101,3 +101,13 @@ def test_parses_every_reference_config():
     assert n > 10
     shpl = C.load_shpl_config(open(os.path.join(REF_CFG, "retinanet_car_SHPL.config")).read())
     assert C.retinanet_uses_sparse_pooling(shpl)
+
+
+def test_mv3d_calib_to_P_matches_reference(golden_dir):
+    """MV3D transform.calib_to_P / calib_to_L2C (transform.py:13-30) vs the reference run."""
+    import numpy as np
+    from sparse_pooling_amd import mv3d
+    g = np.load(os.path.join(golden_dir, "mv3d_calib.npz"))
+    np.testing.assert_array_equal(mv3d.calib_to_P(g["calib"]), g["P"])
+    np.testing.assert_array_equal(mv3d.calib_to_P(g["calib"], from_camera=True), g["P_cam"])
+    np.testing.assert_array_equal(mv3d.calib_to_L2C(g["calib"]), g["L2C"])

@@ -648,6 +648,47 @@ def test_kitti_loader_batch_vs_oracle():
         assert int(b.err.item()) == 0
 
 
+def test_kitti_loader_single_column_vs_reference_golden(golden_dir):
+    """One-point scan / one point in front of the camera: numpy's products have one
+    column there (OpenBLAS dgemv's order), reproduced on the device, in a batch with
+    an ordinary scan."""
+    from sparse_pooling_amd import kitti
+    g = np.load(os.path.join(golden_dir, "kitti_single.npz"))
+    h, w = g["image_shape"]
+    fc = kitti.FrameCalibrationData()
+    fc.r0_rect, fc.tr_velodyne_to_cam = g["0_r0_rect"], g["0_tr"]
+    rect = kitti.rect_matrix(fc)
+    big = synth.synthetic_scan(np.random.default_rng(3), 5000)
+    scans = [g["0_velo"], big, g["1_velo"]]
+    off = np.concatenate([[0], np.cumsum([len(x) for x in scans])]).astype(np.int64)
+    xyzi = torch.from_numpy(np.concatenate(scans)).to(DEV)
+    for filt in (True, False):
+        b = kitti.velo_to_cam_batch(xyzi, torch.from_numpy(off).to(DEV), np.stack([rect] * 3),
+                                    np.stack([g["0_p2"]] * 3) if filt else None, [[w, h]] * 3 if filt else None)
+        torch.cuda.synchronize()
+        n = _np(b.counts)
+        key = "point_cloud" if filt else "point_cloud_all"
+        for f, want in ((0, g[f"0_{key}"]), (2, g[f"1_{key}"])):
+            np.testing.assert_array_equal(_np(b.points[off[f]:off[f] + n[f]]).T, want)
+        e = orc.velo_to_cam(big, rect, g["0_p2"] if filt else None, [w, h] if filt else None)
+        np.testing.assert_array_equal(_np(b.points[off[1]:off[1] + n[1]]).T, e)
+
+
+def test_mv3d_one_point_frame_projects_like_numpy():
+    """MV3D with img_index2 projected on the device: a one-point frame is np.dot with
+    one column (dgemv's order), as minibatch_mv3d_img.py:88-90 computes it."""
+    from sparse_pooling_amd import mv3d
+    t = np.load(os.path.join(GOLD, "index_single_tie.npz"))
+    pts = np.array([[*t["points"][0], 0.5]])
+    mat = np.vstack((pts[:, :3].T, np.ones((1, 1))))
+    uvw = np.dot(synth.KITTI_P2, mat)          # the reference's projectToImage, one column
+    want = np.round(uvw[:2] / uvw[2]).astype(np.int64)
+    img_p, bv, _ = mv3d.mv3d_sparse_pooling_input(pts, P=synth.KITTI_P2)
+    img_r, _, _ = mv3d.mv3d_sparse_pooling_input(pts, img_index2=want)
+    assert _np(bv).shape[0] == 1
+    np.testing.assert_array_equal(_np(img_p), _np(img_r))
+
+
 def test_velodyne_to_fused_layer_pipeline(kitti_dir):
     """KITTI files -> device velodyne loader -> BEV slices -> index -> sorted M -> fused
     layer (kitti_dataset.py:285-379), against the oracle chain."""

@@ -199,3 +199,44 @@ def test_kitti_oracle_vs_reference_golden(kitti_dir):
         np.testing.assert_array_equal(orc.velo_to_cam(g[f"{idx}_velo"], rect), g[f"{idx}_point_cloud_all"])
         np.testing.assert_array_equal(orc.velo_to_cam(g[f"{idx}_velo"], rect, g[f"{idx}_p2"], [w, h], flip=True),
                                       g[f"{idx}_flip_point_cloud"])
+
+
+def test_kitti_single_column_oracle_vs_reference_golden(golden_dir):
+    """One-point scan and a scan with one point in front of the camera: numpy's
+    products have one column (dgemv order) -- pinned by the reference's output."""
+    g = np.load(os.path.join(golden_dir, "kitti_single.npz"))
+    h, w = g["image_shape"]
+    for idx in (0, 1):
+        rect = orc.rect_matrix(g[f"{idx}_r0_rect"], g[f"{idx}_tr"])
+        np.testing.assert_array_equal(orc.velo_to_cam(g[f"{idx}_velo"], rect, g[f"{idx}_p2"], [w, h]),
+                                      g[f"{idx}_point_cloud"])
+        np.testing.assert_array_equal(orc.velo_to_cam(g[f"{idx}_velo"], rect), g[f"{idx}_point_cloud_all"])
+
+
+def test_single_column_goldens_discriminate_the_order(golden_dir):
+    """The single-column goldens are not satisfied by dgemm's FMA chain: evaluated
+    that way the one-point frames round / clip differently, and the one-point scan's
+    camera coordinates differ -- so passing them pins dgemv's order."""
+    from fractions import Fraction
+
+    def chain(p, a):
+        s = p[0] * a[0]
+        for k in range(1, 4):
+            s = float(Fraction(p[k]) * Fraction(a[k]) + Fraction(s))
+        return s
+    for name in ("index_single_tie.npz", "index_single_clip.npz"):
+        g = np.load(os.path.join(golden_dir, name))
+        a = [*g["points"][0], 1.0]
+        u = chain(g["P"][0], a) / chain(g["P"][2], a)
+        v = chain(g["P"][1], a) / chain(g["P"][2], a)
+        W, H = g["im_size"]
+        inside = 0 <= u < W - 1 and 0 <= v < H - 1
+        if not inside:
+            assert g["gen_bv_index"].reshape(-1, 2).shape[0] == 1   # the reference kept it
+        else:
+            assert np.round(u) != g["gen_img_index"].reshape(3, -1)[0, 0]
+    k = np.load(os.path.join(golden_dir, "kitti_single.npz"))
+    rect = orc.rect_matrix(k["0_r0_rect"], k["0_tr"])
+    a = [float(x) for x in k["0_velo"][0, :3]] + [1.0]
+    cam = [chain(rect[r], a) for r in range(3)]
+    assert cam != list(k["0_point_cloud_all"][:, 0])
