@@ -257,6 +257,9 @@ typedef struct {
     int32_t *ent_col;  /* [nnz_cap] column k of each sorted entry (SHPL_BY_PIXEL; else NULL) */
     int64_t n_keys;    /* destination rows (all frames)                                      */
     int64_t nnz_cap;   /* capacity of the entry arrays                                       */
+    int32_t *key_range; /* optional [n_keys][2]: (first, end) sorted entry of each destination's
+                           run (first == end: no entry). NULL: not built. When set,
+                           shpl_build_csr fills it and shpl_pull runs one row-keyed launch. */
 } shpl_csr;
 
 /* Sort the entries of every frame by destination (cell for SHPL_BY_CELL,
@@ -269,7 +272,12 @@ typedef struct {
  * [f*keys_per_frame, (f+1)*keys_per_frame); one workgroup sorts one frame
  * (LDS tile histogram + stable rank inside each tile). d_col NULL means
  * col[e] = e. Entries whose row, column or pixel is -1 or whose destination
- * lies outside the frame are left out. */
+ * lies outside the frame are left out.
+ * With csr->key_range set (or for small batches of frames with at most 65536
+ * destinations each) the sort is ONE launch of one workgroup per (frame, range
+ * of 1024 destinations): each reads its frame's entries, counts its
+ * destinations and the entries below them, places and ranks its own -- no
+ * workgroup waits for another -- and writes key_range for its destinations. */
 int shpl_csr_workspace_bytes(int64_t n_keys, int64_t nnz_cap, size_t *bytes);
 int shpl_build_csr(int direction, int order, int n_frames, const int64_t *d_frame_off,
                    const int64_t *d_frame_nnz, int64_t keys_per_frame, const int32_t *d_cell,
@@ -297,6 +305,12 @@ int shpl_build_csr(int direction, int order, int n_frames, const int64_t *d_fram
  * pooled part. shpl_pull = shpl_pull_dense + shpl_pull_sparse on one stream;
  * the split entry points let a caller start the dense pass before M is built
  * (the sparse pass must follow the dense pass of the same output).
+ * With csr->key_range set, shpl_pull is instead ONE launch keyed by output row
+ * (k_rows: a group of lanes per row writes its pass-through chunks and walks
+ * the row's run from key_range for the pooled ones) -- for small, latency-bound
+ * layers (config 3), where two dependent launches and a thread per
+ * (entry, chunk) cost more than the extra key_range read per row. Results are
+ * bitwise the same. shpl_pull_dense / shpl_pull_sparse ignore key_range.
  * Replaces: _sparse_pool_op + concat  (sparse_pool_utils.py:96-103, :72)  -> BY_CELL, CONCAT
  *           _sparse_pool_trans_op + concat (sparse_pool_utils.py:105-117, :87) -> BY_PIXEL, CONCAT
  *           their TF autodiff gradients                       -> the other direction */

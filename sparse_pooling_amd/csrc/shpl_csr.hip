@@ -559,6 +559,221 @@ __global__ __launch_bounds__(CSR_BLOCK) void k_csr_segment(CsrIn c, SegIn g, int
                                   ent_col);
 }
 
+// ---------------------------------------------------------------- range CSR
+// One launch, no workgroup waiting for another: one workgroup per (frame,
+// range of RANGE_KEYS destinations). Small batches of frames with few
+// destinations (config 3: 4 frames of 8,800 cells / 6,750 pixels) sort in
+// one launch instead of four, and the per-destination (first, end) ranges the
+// row-keyed pull reads (csr->key_range) come out of the same pass:
+//   1. every workgroup reads all of its frame's entries once (L2-resident,
+//      8-12 B each, RANGE_BATCH in flight per thread): the entries of its
+//      range go to an LDS list as 32-bit words (local destination << 24 |
+//      entry offset in the frame; wave-aggregated slots), with LDS counts per
+//      destination; the valid entries below its range are counted (its
+//      output offset inside the frame);
+//   2. exclusive scan of the counts: each destination's start;
+//   3. the list placed by destination (LDS atomics: any order inside one);
+//   4. each word's rank among its destination's words in (TF order, entry)
+//      order -> its sorted slot; emitted with source row, value and column;
+//   5. key_range of its destinations; the frame's last range clears the
+//      frame's unused capacity (and, for the last frame, the slots after it).
+// A range holding more than RANGE_LIST entries (a pathological frame) reads
+// its frame a second time and places 64-bit words in its own stretch of the
+// workspace instead.
+constexpr int RANGE_KEYS = 256;
+constexpr int RANGE_LIST = 10240;  // words of one range in LDS (2 arrays, 80 KiB)
+constexpr int RANGE_BATCH = 16;    // entries per thread whose loads are in flight together
+
+// Rank of entry `me` (order key `ke` if !entry_order) among words[a, z) of one
+// destination and the emission of entry e at slot o. W(i) -> (entry, word
+// compare value); entry_order: the words' numeric order is TF's.
+template <bool HAS_COL, typename W>
+__device__ __forceinline__ void range_emit(const CsrIn &c, int32_t total, const int32_t *beg, const int32_t *endk,
+                                           int64_t k0, int64_t out0, W words, int32_t *ent_dst, int32_t *ent_src,
+                                           float *ent_val, int32_t *ent_col) {
+    const bool entry_order = c.order == SHPL_ORDER_ENTRY || !HAS_COL;
+    for (int32_t s0 = threadIdx.x; s0 < total; s0 += CSR_BLOCK * CSR_BATCH) {
+        int32_t d[CSR_BATCH], ee[CSR_BATCH], key[CSR_BATCH], kk[CSR_BATCH], src[CSR_BATCH];
+        float val[CSR_BATCH];
+#pragma unroll
+        for (int u = 0; u < CSR_BATCH; ++u) {
+            const int32_t sl = s0 + u * CSR_BLOCK;
+            d[u] = -1;
+            if (sl >= total) continue;
+            int32_t t;
+            const uint64_t me = words.get(sl, t, ee[u]);
+            key[u] = (int32_t)(k0 + t);
+            const int32_t a = beg[t], z = endk[t];
+            int32_t rank = 0;
+            if (z - a > 1) {
+                if (entry_order) {
+                    for (int32_t y = a; y < z; ++y) rank += words.cmp(y) < me ? 1 : 0;
+                } else {
+                    const uint64_t ke = order_key(c, ee[u]);
+                    for (int32_t y = a; y < z; ++y) {
+                        int32_t ty, o;
+                        words.get(y, ty, o);
+                        if (o == ee[u]) continue;
+                        const uint64_t oo = order_key(c, o);
+                        rank += (oo < ke || (oo == ke && o < ee[u])) ? 1 : 0;
+                    }
+                }
+            }
+            d[u] = a + rank;
+        }
+#pragma unroll
+        for (int u = 0; u < CSR_BATCH; ++u) kk[u] = d[u] >= 0 ? (HAS_COL ? c.col[ee[u]] : ee[u]) : 0;
+#pragma unroll
+        for (int u = 0; u < CSR_BATCH; ++u) {
+            if (d[u] < 0) continue;
+            src[u] = c.direction == SHPL_BY_CELL ? c.pix[kk[u]] : c.cell[ee[u]];
+            val[u] = c.val[ee[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < CSR_BATCH; ++u) {
+            if (d[u] < 0) continue;
+            const int64_t o = out0 + d[u];
+            ent_dst[o] = key[u];
+            ent_src[o] = src[u];
+            ent_val[o] = val[u];
+            if (ent_col) ent_col[o] = kk[u];
+        }
+    }
+}
+
+struct LdsWords {  // (local destination << 24 | entry - e0) words in LDS
+    const uint32_t *w;
+    int64_t e0;
+    __device__ __forceinline__ uint64_t get(int32_t i, int32_t &t, int32_t &e) const {
+        const uint32_t x = w[i];
+        t = (int32_t)(x >> 24);
+        e = (int32_t)(e0 + (x & 0xffffffu));
+        return x;
+    }
+    __device__ __forceinline__ uint64_t cmp(int32_t i) const { return w[i]; }
+};
+
+struct GlobalWords {  // (destination << 32 | entry) words in the workspace
+    const uint64_t *w;
+    int64_t k0;
+    __device__ __forceinline__ uint64_t get(int32_t i, int32_t &t, int32_t &e) const {
+        const uint64_t x = w[i];
+        t = (int32_t)((int64_t)(x >> 32) - k0);
+        e = (int32_t)(uint32_t)x;
+        return x;
+    }
+    __device__ __forceinline__ uint64_t cmp(int32_t i) const { return w[i]; }
+};
+
+template <bool HAS_COL>
+__global__ __launch_bounds__(CSR_BLOCK) void k_csr_range(CsrIn c, uint64_t *tmp, int64_t nnz_cap, int64_t n_keys,
+                                                         int n_ranges, int32_t *ent_dst, int32_t *ent_src,
+                                                         float *ent_val, int32_t *ent_col, int32_t *key_range) {
+    __shared__ int32_t cnt[RANGE_KEYS], beg[RANGE_KEYS];
+    __shared__ int32_t wsum[CSR_BLOCK / 64];
+    __shared__ int32_t n_list;
+    __shared__ uint32_t list[RANGE_LIST], srt[RANGE_LIST];
+    const int f = blockIdx.y, r = blockIdx.x;
+    int64_t e0, e1, cap_end;
+    frame_range(c, f, e0, e1, cap_end);
+    const int64_t kf = (int64_t)f * c.keys_per_frame, kend = kf + c.keys_per_frame;
+    const int64_t k0 = kf + (int64_t)r * RANGE_KEYS;
+    const int nk = (int)(k0 + RANGE_KEYS < kend ? RANGE_KEYS : kend - k0);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int t = threadIdx.x; t < RANGE_KEYS; t += CSR_BLOCK) cnt[t] = 0;
+    if (threadIdx.x == 0) n_list = 0;
+    __syncthreads();
+    // 1. this range's entries -> LDS list + counts; valid entries below the range
+    int32_t below = 0;
+    for (int64_t b = e0 + threadIdx.x; b < e1; b += (int64_t)CSR_BLOCK * RANGE_BATCH) {
+        int32_t key[RANGE_BATCH];
+        keys_batch<HAS_COL>(c, b, e1, key);
+#pragma unroll
+        for (int u = 0; u < RANGE_BATCH; ++u) {
+            const int64_t k = key[u];
+            below += (k >= kf && k < k0) ? 1 : 0;  // invalid (-1) or outside the frame: left out
+            const bool in = k >= k0 && k < k0 + nk;
+            const uint64_t m = __ballot(in);
+            if (m == 0) continue;  // wave-uniform
+            int32_t base = 0;
+            if (lane == 0) base = atomicAdd(&n_list, (int32_t)__popcll(m));
+            base = __shfl(base, 0, 64);
+            if (!in) continue;
+            const int32_t slot = base + (int32_t)lane_rank(m);
+            const int32_t t = (int32_t)(k - k0);
+            if (slot < RANGE_LIST) list[slot] = ((uint32_t)t << 24) | (uint32_t)(b + (int64_t)u * CSR_BLOCK - e0);
+            atomicAdd(&cnt[t], 1);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) below += __shfl_xor(below, o, 64);
+    if (lane == 0) wsum[wid] = below;
+    __syncthreads();
+    below = 0;
+    for (int w = 0; w < CSR_BLOCK / 64; ++w) below += wsum[w];
+    const int32_t total = n_list;
+    __syncthreads();  // wsum is reused by the scan
+    // 2. exclusive scan: beg[t] = start of destination k0 + t; cnt becomes the fill cursor
+    const int32_t v = threadIdx.x < RANGE_KEYS ? cnt[threadIdx.x] : 0;
+    int32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    int32_t run = x - v;
+    for (int w = 0; w < wid; ++w) run += wsum[w];
+    if (threadIdx.x < RANGE_KEYS) {
+        beg[threadIdx.x] = run;
+        cnt[threadIdx.x] = run;
+    }
+    __syncthreads();
+    const int64_t out0 = e0 + below;
+    // 3. placement by destination; 4. rank + emission (cnt[t] ends up at the end of destination k0 + t)
+    if (total <= RANGE_LIST) {
+        for (int32_t s = threadIdx.x; s < total; s += CSR_BLOCK) {
+            const uint32_t w = list[s];
+            srt[atomicAdd(&cnt[w >> 24], 1)] = w;
+        }
+        __syncthreads();
+        range_emit<HAS_COL>(c, total, beg, cnt, k0, out0, LdsWords{srt, e0}, ent_dst, ent_src, ent_val, ent_col);
+    } else {
+        uint64_t *words = tmp + out0;  // this range's stretch of the frame's slots
+        for (int64_t b = e0 + threadIdx.x; b < e1; b += (int64_t)CSR_BLOCK * RANGE_BATCH) {
+            int32_t key[RANGE_BATCH];
+            keys_batch<HAS_COL>(c, b, e1, key);
+#pragma unroll
+            for (int u = 0; u < RANGE_BATCH; ++u) {
+                const int64_t k = key[u];
+                if (k < k0 || k >= k0 + nk) continue;
+                words[atomicAdd(&cnt[k - k0], 1)] =
+                    ((uint64_t)(uint32_t)k << 32) | (uint32_t)(b + (int64_t)u * CSR_BLOCK);
+            }
+        }
+        block_publish();  // the words went through memory to the other waves
+        range_emit<HAS_COL>(c, total, beg, cnt, k0, out0, GlobalWords{words, k0}, ent_dst, ent_src, ent_val,
+                            ent_col);
+    }
+    // 5. key ranges; holes after the frame's valid entries (the frame's last range)
+    if (key_range) {
+        for (int t = threadIdx.x; t < nk; t += CSR_BLOCK) {
+            key_range[2 * (k0 + t)] = (int32_t)(out0 + beg[t]);
+            key_range[2 * (k0 + t) + 1] = (int32_t)(out0 + cnt[t]);
+        }
+    }
+    if (r != n_ranges - 1) return;
+    for (int64_t h = out0 + total + threadIdx.x; h < cap_end; h += CSR_BLOCK) ent_dst[h] = -1;
+    if (f != c.n_frames - 1) return;
+    for (int64_t h = cap_end + threadIdx.x; h < nnz_cap; h += CSR_BLOCK) ent_dst[h] = -1;
+    if (key_range)
+        for (int64_t k = kend + threadIdx.x; k < n_keys; k += CSR_BLOCK) {
+            key_range[2 * k] = 0;
+            key_range[2 * k + 1] = 0;
+        }
+}
+
 }  // namespace
 }  // namespace shpl
 
@@ -599,6 +814,7 @@ extern "C" int shpl_pack_map(int64_t nnz, const int64_t *d_mij, const float *d_v
 namespace {
 constexpr int64_t SEG_TARGET = 2048;  // entries per segment the host aims for
 constexpr int SEG_FRAMES = 32;        // batches from this many frames sort one frame per workgroup
+constexpr int64_t RANGE_MAX_KEYS = 65536;  // destinations per frame up to which small batches take the range CSR
 
 int64_t seg_cap_of(int64_t nnz_cap) { return nnz_cap / 16 + 65536; }  // bin + cursor counters
 
@@ -641,6 +857,34 @@ extern "C" int shpl_build_csr(int direction, int order, int n_frames, const int6
     const CsrLayout lay = csr_layout(nnz_cap);
     hipStream_t st = (hipStream_t)stream;
     uint8_t *ws = (uint8_t *)d_ws;
+    // The range CSR: always when key ranges are asked for; by default for batches under
+    // SEG_FRAMES frames of at most RANGE_MAX_KEYS destinations (each workgroup reads its
+    // whole frame, so many ranges per frame would multiply those reads).
+    const char *path = getenv("SHPL_CSR_PATH");
+    // (entry offsets inside a frame travel in 24 bits: capacities under 2^24 entries)
+    const bool small_cap = nnz_cap < ((int64_t)1 << 24);
+    if (csr->key_range && !small_cap) return SHPL_ERR_BAD_SHAPE;
+    const bool ranged = csr->key_range != nullptr ||
+                        (small_cap && (path ? path[0] == 'r'
+                                            : (n_frames < SEG_FRAMES && keys_per_frame <= RANGE_MAX_KEYS)));
+    if (ranged) {
+        if (ws_bytes < align_up(sizeof(uint64_t) * (size_t)nnz_cap, 256)) return SHPL_ERR_WORKSPACE;
+        const int64_t n_ranges = (keys_per_frame + RANGE_KEYS - 1) / RANGE_KEYS;
+        if (n_ranges > 65535) return SHPL_ERR_BAD_SHAPE;
+        CsrIn c{direction, order, n_frames, d_frame_off, d_frame_nnz, keys_per_frame, 0,
+                d_cell, d_col, d_pix, d_val};
+        const dim3 grid((unsigned)n_ranges, (unsigned)n_frames);
+        if (d_col)
+            hipLaunchKernelGGL(k_csr_range<true>, grid, dim3(CSR_BLOCK), 0, st, c, (uint64_t *)ws, nnz_cap,
+                               csr->n_keys, (int)n_ranges, csr->ent_dst, csr->ent_src, csr->ent_val, csr->ent_col,
+                               csr->key_range);
+        else
+            hipLaunchKernelGGL(k_csr_range<false>, grid, dim3(CSR_BLOCK), 0, st, c, (uint64_t *)ws, nnz_cap,
+                               csr->n_keys, (int)n_ranges, csr->ent_dst, csr->ent_src, csr->ent_val, csr->ent_col,
+                               csr->key_range);
+        SHPL_LAUNCH_CHECK();
+        return SHPL_OK;
+    }
     // segments: about SEG_TARGET entries each (estimated from the capacity per frame)
     const int64_t est = (nnz_cap + n_frames - 1) / n_frames;
     int log_bin = 0;
@@ -652,8 +896,7 @@ extern "C" int shpl_build_csr(int direction, int order, int n_frames, const int6
     // Small batches take the segmented path (config 3, 4 frames: 0.305 -> 0.259 ms per step); from
     // SEG_FRAMES frames on, one workgroup per frame fills enough of the chip and, overlapped with the
     // dense stream, measured faster (config 2, 64 frames: 2.34 vs 2.42 ms per step).
-    // SHPL_CSR_PATH=frame|segment forces a path (measurements).
-    const char *path = getenv("SHPL_CSR_PATH");
+    // SHPL_CSR_PATH=frame|segment|range forces a path (measurements).
     const bool want = path ? path[0] == 's' : n_frames < SEG_FRAMES;
     const bool segmented = want && ws_bytes >= lay.total && (int64_t)n_frames * (n_bins + S) <= seg_cap_of(nnz_cap);
     if (!segmented) {

@@ -439,6 +439,110 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse_long(const Feat f, const 
     }
 }
 
+// ---------------------------------------------------------------- k_rows
+// The whole pull in ONE launch keyed by output row, for CSRs that carry
+// key_range (small, latency-bound layers: config 3). A group of G lanes owns a
+// row (64 / G rows per wave): lane g copies pass-through chunks g, g+G, ...
+// and sums pooled chunks g, g+G, ... over the row's run [first, end) in TF
+// order. The run's index words are loaded G at a time, one entry per lane,
+// and handed to the group's lanes by shuffles; ROWS_WALK feature rows are in
+// flight per step. Trip counts are wave-uniform (the longest run of the
+// wave's rows), so the shuffles always see every lane. Arithmetic is
+// k_sparse's: bitwise the same output as k_dense + k_sparse.
+constexpr int ROWS_WALK = 16;
+
+template <typename T, int VEC, bool GROUP, int G>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_rows(const Feat f, const Ents e, const int32_t *key_range,
+                                                     int64_t n_rows) {
+    typedef Chunk<T, VEC> C;
+    constexpr int RPW = SHPL_WAVE / G;
+    const int lane = threadIdx.x & 63, lg = lane & (G - 1), gbase = lane & ~(G - 1);
+    const int64_t row = ((int64_t)blockIdx.x * (SHPL_BLOCK / SHPL_WAVE) + (threadIdx.x >> 6)) * RPW + lane / G;
+    const bool live = row < n_rows;
+    int32_t first = 0, end = 0;
+    if (live) {
+        first = key_range[2 * row];
+        end = key_range[2 * row + 1];
+    }
+    T *out = reinterpret_cast<T *>(f.out);
+    const T *pass = reinterpret_cast<const T *>(f.pass) + f.pass_off;
+    if (live && f.mode == SHPL_OUT_CONCAT)
+        for (uint32_t c = lg; c < f.cpass; c += G)
+            C::store_nt(out + (row * f.out_stride + (int64_t)c * VEC), C::load_nt(pass + (row * f.pass_stride + (int64_t)c * VEC)));
+    // longest run among the wave's rows: the walk's trip count
+    int32_t len = end - first, wlen = len;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wlen = max(wlen, __shfl_xor(wlen, o, 64));
+    const T *src = reinterpret_cast<const T *>(f.src) + f.src_off;
+    const uint32_t oc0 = f.mode == SHPL_OUT_CONCAT ? f.cpass : 0u;
+    for (uint32_t pc0 = 0; pc0 < f.cpool; pc0 += G) {
+        const uint32_t pc = pc0 + lg;
+        const bool mine = live && pc < f.cpool;
+        float acc[VEC], q[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) acc[j] = q[j] = 0.0f;
+        int32_t kprev = -1;
+        for (int32_t j0 = 0; j0 < wlen; j0 += G) {
+            // index words of entries first + j0 + lg of this lane's row
+            const bool has = j0 + lg < len;
+            const int32_t my_src = has ? e.src[first + j0 + lg] : 0;
+            const float my_val = has ? e.val[first + j0 + lg] : 0.0f;
+            const int32_t my_col = (GROUP && has) ? e.col[first + j0 + lg] : 0;
+            const int32_t n = min(G, wlen - j0);
+            for (int32_t u0 = 0; u0 < n; u0 += ROWS_WALK) {
+                typename C::raw_t raw[ROWS_WALK];
+                int32_t sr[ROWS_WALK];
+#pragma unroll
+                for (int u = 0; u < ROWS_WALK; ++u) {
+                    const int srcl = gbase + ((u0 + u) & (G - 1));
+                    sr[u] = __shfl(my_src, srcl, 64);
+                    if (mine && j0 + u0 + u < len && u0 + u < G) raw[u] = C::load(src + ((int64_t)sr[u] * f.src_stride + (int64_t)pc * VEC));
+                }
+#pragma unroll
+                for (int u = 0; u < ROWS_WALK; ++u) {
+                    const int srcl = gbase + ((u0 + u) & (G - 1));
+                    const float w = __shfl(my_val, srcl, 64);
+                    const int32_t kc = GROUP ? __shfl(my_col, srcl, 64) : 0;
+                    if (!(mine && j0 + u0 + u < len && u0 + u < G)) continue;
+                    float x[VEC];
+                    C::to_f32(raw[u], x);
+                    if (GROUP) {
+                        // TF: Q[k] = sum of column k's entries; out = 0 + Q[k1] + Q[k2] ... (ScatterNd order)
+                        if (kc != kprev) {
+#pragma unroll
+                            for (int j = 0; j < VEC; ++j) {
+                                acc[j] = __fadd_rn(acc[j], q[j]);
+                                q[j] = 0.0f;
+                            }
+                            kprev = kc;
+                        }
+                        fma_free_accumulate<VEC>(q, w, x);
+                    } else {
+                        fma_free_accumulate<VEC>(acc, w, x);
+                    }
+                }
+            }
+        }
+        if (!mine) continue;
+        if (GROUP) {
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(acc[j], q[j]);
+        }
+        if (len == 0 && f.mode != SHPL_OUT_ADD) {
+            C::store_nt(out + (row * f.out_stride + (int64_t)(oc0 + pc) * VEC), C::zero());
+            continue;
+        }
+        if (f.mode == SHPL_OUT_ADD) {
+            // pass + pooled (pass + 0.0f for an empty row: k_dense's -0 -> +0)
+            float a[VEC];
+            C::to_f32(C::load(pass + (row * f.pass_stride + (int64_t)pc * VEC)), a);
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(a[j], acc[j]);
+        }
+        C::store_nt(out + (row * f.out_stride + (int64_t)(oc0 + pc) * VEC), C::from_f32(acc));
+    }
+}
+
 bool aligned(const void *ptr, int64_t a) { return ((uintptr_t)ptr) % (uintptr_t)a == 0; }
 
 struct Plan {
@@ -567,6 +671,42 @@ int sparse(const Plan &pl, const shpl_csr *csr, int direction, hipStream_t s) {
     return pl.v16 ? sparse_t<uint16_t, 8>(pl, csr, group, s) : sparse_t<uint16_t, 1>(pl, csr, group, s);
 }
 
+template <typename T, int VEC, bool GROUP>
+int rows_t(const Plan &pl, const shpl_csr *csr, hipStream_t s) {
+    Ents e{csr->nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_col, csr->ent_val};
+    // lanes per row: the pooled chunks of a row, at least 8 (index words come G at a time), at most a wave
+    int G = 8;
+    while (G < 64 && (uint32_t)G < pl.f.cpool) G <<= 1;
+    const int64_t rows_per_block = (int64_t)(SHPL_BLOCK / G);
+    const int64_t blocks = (pl.n_dst + rows_per_block - 1) / rows_per_block;
+    if (blocks > 0x7fffffffLL) return SHPL_ERR_BAD_SHAPE;
+#define SHPL_ROWS(GG) \
+    hipLaunchKernelGGL((k_rows<T, VEC, GROUP, GG>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, s, pl.f, e, \
+                       (const int32_t *)csr->key_range, pl.n_dst)
+    switch (G) {
+        case 8: SHPL_ROWS(8); break;
+        case 16: SHPL_ROWS(16); break;
+        case 32: SHPL_ROWS(32); break;
+        default: SHPL_ROWS(64); break;
+    }
+#undef SHPL_ROWS
+    SHPL_LAUNCH_CHECK();
+    return SHPL_OK;
+}
+
+template <typename T, int VEC>
+int rows_tv(const Plan &pl, const shpl_csr *csr, bool group, hipStream_t s) {
+    return group ? rows_t<T, VEC, true>(pl, csr, s) : rows_t<T, VEC, false>(pl, csr, s);
+}
+
+int rows(const Plan &pl, const shpl_csr *csr, int direction, hipStream_t s) {
+    if (pl.n_dst == 0) return SHPL_OK;
+    const bool group = direction == SHPL_BY_PIXEL;
+    if (pl.dtype == SHPL_F32)
+        return pl.v16 ? rows_tv<float, 4>(pl, csr, group, s) : rows_tv<float, 1>(pl, csr, group, s);
+    return pl.v16 ? rows_tv<uint16_t, 8>(pl, csr, group, s) : rows_tv<uint16_t, 1>(pl, csr, group, s);
+}
+
 }  // namespace
 }  // namespace shpl
 
@@ -584,6 +724,7 @@ using namespace shpl;
 
 extern "C" int shpl_pull(SHPL_PULL_ARGS) {
     SHPL_PLAN();
+    if (csr->key_range) return rows(pl, csr, direction, (hipStream_t)stream);
     rc = dense(pl, (hipStream_t)stream);
     if (rc) return rc;
     return sparse(pl, csr, direction, (hipStream_t)stream);

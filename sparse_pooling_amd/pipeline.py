@@ -23,8 +23,12 @@ from .shpl_map import ShplMap
 
 
 class FusedPipeline:
+    # row-keyed pulls (one launch per pull, shpl_csr.key_range) for batches under this many frames whose
+    # maps have at most ROWS_MAX_KEYS destinations per frame: latency-bound layers (config 3)
+    ROWS_FRAMES, ROWS_MAX_KEYS = 32, 65536
+
     def __init__(self, n_frames, max_points_per_frame, total_points, im_size, bv_size, stride,
-                 c_bev, c_img, dtype=torch.float32, device="cuda", dual=False):
+                 c_bev, c_img, dtype=torch.float32, device="cuda", dual=False, rows=None):
         dev = torch.device(device)
         self.dev, self.dtype, self.dual = dev, dtype, dual
         self.B = int(n_frames)
@@ -39,6 +43,9 @@ class FusedPipeline:
         self.Wi = int(np.floor(im_size[0] / self.stride[0]))
         self.n_cells = self.B * self.Hb * self.Wb
         self.n_pix = self.B * self.Hi * self.Wi
+        if rows is None:
+            rows = self.B < self.ROWS_FRAMES and max(self.Hb * self.Wb, self.Hi * self.Wi) <= self.ROWS_MAX_KEYS
+        self.rows = bool(rows)
         N = max(self.N, 1)
         i32 = dict(dtype=torch.int32, device=dev)
         self.cell = torch.empty(N, **i32)
@@ -48,10 +55,10 @@ class FusedPipeline:
         self.frame_off = torch.empty(self.B + 1, dtype=torch.int64, device=dev)
         self.err = torch.zeros(1, **i32)
         self.index_ws = L.workspace(L.index_ws_bytes(self.B, self.max_points), dev)
-        self.csr = L.Csr(self.n_cells, self.N, dev, with_col=False)  # BEV-cell CSR (img -> BEV)
+        self.csr = L.Csr(self.n_cells, self.N, dev, with_col=False, key_range=self.rows)  # BEV-cell CSR (img -> BEV)
         self.bv_fused = torch.empty((self.B, self.Hb, self.Wb, self.Cb + self.Ci), dtype=dtype, device=dev)
         if dual:
-            self.pcsr = L.Csr(self.n_pix, self.N, dev, with_col=True)  # pixel CSR (BEV -> img)
+            self.pcsr = L.Csr(self.n_pix, self.N, dev, with_col=True, key_range=self.rows)  # pixel CSR (BEV -> img)
             self.img_fused = torch.empty((self.B, self.Hi, self.Wi, self.Ci + self.Cb), dtype=dtype,
                                          device=dev)
         self._lib = L.lib()
@@ -88,7 +95,10 @@ class FusedPipeline:
                    L.OUT_CONCAT, L.ptr(out), cs + cp, st), "shpl_pull")
 
     def layer_dense(self, bev, img):
-        """Streaming half of the layer (needs no M): pass-through copy + zeros."""
+        """Streaming half of the layer (needs no M): pass-through copy + zeros.
+        Row-keyed pulls (self.rows) have no separate streaming half."""
+        if self.rows:
+            return
         st = L.stream_of(self.dev)
         self._pull(self._lib.shpl_pull_dense, self.csr, L.BY_CELL, img, self.Ci, bev, self.Cb, self.bv_fused, st)
         if self.dual:
@@ -96,7 +106,11 @@ class FusedPipeline:
                        self.img_fused, st)
 
     def _sparse(self, args):
-        """shpl_pull_sparse(*args) on the current stream."""
+        """shpl_pull_sparse(*args) on the current stream; with row-keyed CSRs the
+        whole pull (shpl_pull's one launch)."""
+        if self.rows:
+            L.check(self._lib.shpl_pull(*args, L.stream_of(self.dev)), "shpl_pull")
+            return
         L.check(self._lib.shpl_pull_sparse(*args, L.stream_of(self.dev)), "shpl_pull_sparse")
 
     def _concat_args(self, csr, direction, src, cs, pass_, cp, out):
@@ -246,7 +260,8 @@ class FusedPipeline:
             side2.wait_stream(main)       # forward done
         L.check(self._lib.shpl_pull(*cell, L.stream_of(self.dev)), "shpl_pull")
         with torch.cuda.stream(pst):
-            L.check(self._lib.shpl_pull_dense(*pix, L.stream_of(self.dev)), "shpl_pull_dense")
+            if not self.rows:
+                L.check(self._lib.shpl_pull_dense(*pix, L.stream_of(self.dev)), "shpl_pull_dense")
             self._sparse(pix)
         if side2 is not None:
             main.wait_stream(side2)

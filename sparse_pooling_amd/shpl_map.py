@@ -70,12 +70,21 @@ class ShplMap:
             raise InvalidArgumentError("; ".join(what))
 
     # ------------------------------------------------------------------ CSR
+    # Row-keyed pulls (shpl_csr.key_range: one launch per pull) for maps of fewer
+    # than ROWS_FRAMES frames with at most ROWS_MAX_KEYS destinations per frame;
+    # ROW_PULLS = True / False forces the form (tests).
+    ROWS_FRAMES, ROWS_MAX_KEYS = 32, 65536
+    ROW_PULLS = None
+
     def csr(self, direction, order):
         key = (direction, order)
         if key in self._csr:
             return self._csr[key]
         n_keys = self.n_cells if direction == L.BY_CELL else self.n_pix
-        c = L.Csr(n_keys, self.nnz_cap, self.device, with_col=direction == L.BY_PIXEL)
+        rows = self.ROW_PULLS
+        if rows is None:
+            rows = self.n_frames < self.ROWS_FRAMES and n_keys // max(self.n_frames, 1) <= self.ROWS_MAX_KEYS
+        c = L.Csr(n_keys, self.nnz_cap, self.device, with_col=direction == L.BY_PIXEL, key_range=rows)
         L.check(L.lib().shpl_build_csr(direction, order, self.n_frames, L.ptr(self.frame_off),
                                        L.ptr(self.frame_nnz), n_keys // self.n_frames,
                                        L.ptr(self.cell), L.ptr(self.col), L.ptr(self.val),

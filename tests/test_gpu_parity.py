@@ -252,6 +252,61 @@ def test_noncanonical_M_weights_and_collisions():
     _close_and_exact(tb.grad, d_bev)
 
 
+@pytest.mark.parametrize("c", [3, 8, 64])
+def test_row_keyed_pulls_noncanonical_M(c):
+    """k_rows (shpl_pull over a CSR with key_range) == k_dense + k_sparse == the oracle,
+    bitwise, on a non-canonical M: shuffled nnz, repeated columns (TF's per-column
+    partials), negative weights, a 160-entry run, 3 / 8 / 64 channels (scalar path,
+    one chunk per lane, groups of 16 lanes), every direction / order / output mode."""
+    from sparse_pooling_amd import _lib as L
+    from sparse_pooling_amd import shpl_map as sm
+    rng = np.random.default_rng(22)
+    n, R, hb, wb, h, w = 500, 600, 20, 30, 15, 17
+    idx = np.stack([np.zeros(n, np.int64), rng.integers(0, h, n), rng.integers(0, w, n)], 1)
+    idx[: n // 4, 1:] = idx[0, 1:]
+    rows = rng.integers(0, R, n)
+    rows[100:260] = rows[100]
+    extra = np.stack([rng.integers(0, R, 300), rng.integers(0, n, 300)], 1)
+    mij = np.concatenate([np.stack([rows, np.arange(n)], 1), extra]).astype(np.int64)
+    mij = mij[rng.permutation(len(mij))]
+    mval = rng.uniform(-2, 2, len(mij)).astype(np.float32)
+    img = rng.standard_normal((1, h, w, c)).astype(np.float32)
+    bev = rng.standard_normal((1, hb, wb, c)).astype(np.float32)
+    ti, tb = torch.from_numpy(img).to(DEV), torch.from_numpy(bev).to(DEV)
+    outs = {}
+    for rows_mode in (True, False):
+        sm.ShplMap.ROW_PULLS = rows_mode
+        try:
+            smap = sm.pack_map(torch.from_numpy(mij).to(DEV), torch.from_numpy(mval).to(DEV),
+                               np.array([R, n]), torch.from_numpy(idx).to(DEV), img.shape)
+            res = []
+            for direction, order, src, pas, nrow in ((L.BY_CELL, L.ORDER_ENTRY, ti, tb, R),
+                                                     (L.BY_PIXEL, L.ORDER_COL_ROW, tb, ti, h * w),
+                                                     (L.BY_PIXEL, L.ORDER_COL_ENTRY, tb, ti, h * w),
+                                                     (L.BY_CELL, L.ORDER_COL_ENTRY, ti, tb, R)):
+                pool = torch.full((nrow, c), float("nan"), device=DEV)
+                sm.pull(smap, direction, order, src, c, 0, c, pool, c)
+                p2 = pas.reshape(nrow, c)
+                cat = torch.full((nrow, 2 * c), float("nan"), device=DEV)
+                sm.pull(smap, direction, order, src, c, 0, c, cat, 2 * c, pass_=p2, pass_stride=c, c_pass=c,
+                        mode=L.OUT_CONCAT)
+                add = torch.full((nrow, c), float("nan"), device=DEV)
+                sm.pull(smap, direction, order, src, c, 0, c, add, c, pass_=p2, pass_stride=c, c_pass=c,
+                        mode=L.OUT_ADD)
+                res += [cat, add, pool]
+            torch.cuda.synchronize()
+            outs[rows_mode] = [_np(t) for t in res]
+        finally:
+            sm.ShplMap.ROW_PULLS = None
+    for a, b in zip(outs[True], outs[False]):
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+    # against the oracle: img -> BEV (TF entry order) and BEV -> img (transpose + ScatterNd)
+    _close_and_exact(outs[True][2], orc.sparse_pool_op(mij, mval, [R, n], img, idx).reshape(R, c))
+    _close_and_exact(outs[True][5], orc.sparse_pool_trans_op(mij, mval, [R, n], bev.reshape(-1, c), idx,
+                                                             img.shape).reshape(h * w, c))
+    _close_and_exact(outs[True][0][:, :c], bev.reshape(R, c))
+
+
 def test_invalid_indices_raise():
     from sparse_pooling_amd import sparse_pool_utils as spu
     from sparse_pooling_amd.errors import InvalidArgumentError
@@ -391,15 +446,19 @@ def test_full_size_properties_config5():
         (frames[0].voxel_indices[:, 1] >= spec.bv_size[0]).sum())
 
 
-@pytest.mark.parametrize("cfg,dtype,mode", [(1, "f32", "eager"), (1, "bf16", "eager"), (1, "bf16", "streams"),
-                                            (1, "f32", "graph"), (3, "bf16", "eager"), (3, "bf16", "graph")])
-def test_pipeline_backward_matches_oracle(cfg, dtype, mode):
+@pytest.mark.parametrize("cfg,dtype,mode,rows", [
+    (1, "f32", "eager", False), (1, "bf16", "eager", False), (1, "bf16", "streams", False), (1, "f32", "graph", False),
+    (3, "bf16", "eager", False), (3, "bf16", "graph", False),
+    (1, "f32", "eager", True), (1, "bf16", "streams", True), (1, "f32", "graph", True),
+    (3, "bf16", "eager", True), (3, "bf16", "graph", True), (3, "f32", "streams", True)])
+def test_pipeline_backward_matches_oracle(cfg, dtype, mode, rows):
     """FusedPipeline forward + backward (the config-3 bench step) vs the oracle's TF
     forward and gradients; mode streams/graph: the bench's step (side streams for the
     streaming half and the pixel-keyed chain), launched eagerly or replayed from a
     captured HIP graph. cfg 3 is the bench's own shape: bf16, 256 channels (32 chunks
     per pooled row, the power-of-two path), stride 8, pixel runs far longer than
-    k_sparse's 8 entries (k_sparse_long with per-column partials in OUT_ADD mode)."""
+    k_sparse's 8 entries (k_sparse_long with per-column partials in OUT_ADD mode).
+    rows: the CSRs carry key_range and every pull is one row-keyed launch (k_rows)."""
     from sparse_pooling_amd import pipeline
     spec = synth.CONFIGS[cfg]
     B = 2 if cfg == 1 else 4
@@ -411,7 +470,7 @@ def test_pipeline_backward_matches_oracle(cfg, dtype, mode):
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
     tdt = torch.float32 if dtype == "f32" else torch.bfloat16
     pl = pipeline.FusedPipeline(B, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev, spec.c_img,
-                                dtype=tdt, dual=True)
+                                dtype=tdt, dual=True, rows=rows)
     Hb, Wb = spec.bev_feat_hw
     Hi, Wi = spec.img_feat_hw
     Cb, Ci = spec.c_bev, spec.c_img
