@@ -10,7 +10,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libshpl.so")
+# SHPL_LIB: an alternative build of the same sources (A/B measurements of compile-time variants)
+LIB_PATH = os.environ.get("SHPL_LIB") or os.path.join(_HERE, "libshpl.so")
 
 # enums of include/shpl.h
 OK, ERR_BAD_SHAPE, ERR_INDEX_OOB, ERR_HIP, ERR_WORKSPACE, ERR_ARG = range(6)

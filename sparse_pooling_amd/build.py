@@ -20,29 +20,36 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=o
          "-Wall", "-Wno-unused-function"]
 
 
-def _compile(src):
-    obj = os.path.join(OBJ, os.path.basename(src).replace(".hip", ".o"))
+def _compile(src, obj_dir=OBJ, extra=()):
+    obj = os.path.join(obj_dir, os.path.basename(src).replace(".hip", ".o"))
     deps = [src, *glob.glob(os.path.join(CSRC, "*.h")),
             os.path.join(os.path.dirname(HERE), "include", "shpl.h")]
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return obj
-    subprocess.run([HIPCC, *FLAGS, "-c", src, "-o", obj], check=True)
+    subprocess.run([HIPCC, *FLAGS, *extra, "-c", src, "-o", obj], check=True)
     return obj
 
 
-def build(verbose=False):
-    os.makedirs(OBJ, exist_ok=True)
+def build(verbose=False, out=OUT, defines=()):
+    """defines: extra -D flags for an A/B variant (with `out` elsewhere, loaded through SHPL_LIB)."""
+    obj_dir = OBJ if not defines else os.path.join(OBJ, "variant_" + "_".join(d.replace("=", "") for d in defines))
+    os.makedirs(obj_dir, exist_ok=True)
+    extra = [f"-D{d}" for d in defines]
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(_compile, srcs))
-    if not os.path.exists(OUT) or os.path.getmtime(OUT) < max(os.path.getmtime(o) for o in objs):
-        subprocess.run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", OUT],
+        objs = list(ex.map(lambda s: _compile(s, obj_dir, extra), srcs))
+    if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(o) for o in objs):
+        subprocess.run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", out],
                        check=True)
     if verbose:
-        print("built", OUT)
-    return OUT
+        print("built", out)
+    return out
 
 
 if __name__ == "__main__":
-    build(verbose=True)
+    # python -m sparse_pooling_amd.build [OUT.so NAME=VALUE ...]: an A/B variant
+    if len(sys.argv) > 2:
+        build(verbose=True, out=os.path.abspath(sys.argv[1]), defines=tuple(sys.argv[2:]))
+    else:
+        build(verbose=True)
     sys.exit(0)

@@ -29,7 +29,10 @@ namespace shpl {
 namespace {
 
 constexpr int IDX_BLOCK = 1024;
-constexpr int IDX_BATCH = 4;                      // point rows per thread whose loads are in flight together
+#ifndef SHPL_IDX_BATCH
+#define SHPL_IDX_BATCH 1
+#endif
+constexpr int IDX_BATCH = SHPL_IDX_BATCH;         // point rows per thread whose loads are in flight together
 constexpr int IDX_CHUNK = IDX_BLOCK * IDX_BATCH;  // points per workgroup: one round
 
 constexpr uint32_t KEEP_MULTI = 1u, KEEP_ONE = 2u, AUX = 4u;

@@ -580,7 +580,10 @@ __global__ __launch_bounds__(CSR_BLOCK) void k_csr_segment(CsrIn c, SegIn g, int
 // A range holding more than RANGE_LIST entries (a pathological frame) reads
 // its frame a second time and places 64-bit words in its own stretch of the
 // workspace instead.
-constexpr int RANGE_KEYS = 256;
+#ifndef SHPL_RANGE_KEYS
+#define SHPL_RANGE_KEYS 128
+#endif
+constexpr int RANGE_KEYS = SHPL_RANGE_KEYS;
 constexpr int RANGE_LIST = 10240;  // words of one range in LDS (2 arrays, 80 KiB)
 constexpr int RANGE_BATCH = 16;    // entries per thread whose loads are in flight together
 

@@ -446,10 +446,16 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse_long(const Feat f, const 
 // and sums pooled chunks g, g+G, ... over the row's run [first, end) in TF
 // order. The run's index words are loaded G at a time, one entry per lane,
 // and handed to the group's lanes by shuffles; ROWS_WALK feature rows are in
-// flight per step. Trip counts are wave-uniform (the longest run of the
-// wave's rows), so the shuffles always see every lane. Arithmetic is
-// k_sparse's: bitwise the same output as k_dense + k_sparse.
-constexpr int ROWS_WALK = 16;
+// flight per step (8: ~90 VGPRs, 5 waves per SIMD -- rows in flight matter
+// more than entries in flight when the average run is ~3 entries). The first
+// pass-through chunk and the ADD operand are loaded with the row's range, so
+// their latency overlaps the index loads. Trip counts are wave-uniform (the
+// longest run of the wave's rows), so the shuffles always see every lane.
+// Arithmetic is k_sparse's: bitwise the same output as k_dense + k_sparse.
+#ifndef SHPL_ROWS_WALK
+#define SHPL_ROWS_WALK 8
+#endif
+constexpr int ROWS_WALK = SHPL_ROWS_WALK;
 
 template <typename T, int VEC, bool GROUP, int G>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_rows(const Feat f, const Ents e, const int32_t *key_range,
@@ -459,22 +465,31 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_rows(const Feat f, const Ents e,
     const int lane = threadIdx.x & 63, lg = lane & (G - 1), gbase = lane & ~(G - 1);
     const int64_t row = ((int64_t)blockIdx.x * (SHPL_BLOCK / SHPL_WAVE) + (threadIdx.x >> 6)) * RPW + lane / G;
     const bool live = row < n_rows;
+    T *out = reinterpret_cast<T *>(f.out);
+    const T *pass = reinterpret_cast<const T *>(f.pass) + f.pass_off;
+    const T *src = reinterpret_cast<const T *>(f.src) + f.src_off;
+    const bool concat = f.mode == SHPL_OUT_CONCAT, add = f.mode == SHPL_OUT_ADD;
+    const uint32_t oc0 = concat ? f.cpass : 0u;
+    // the row's range, its first pass-through chunk and its first ADD operand: one round trip
     int32_t first = 0, end = 0;
+    typename C::raw_t pv, av;
+    const bool p0 = live && concat && (uint32_t)lg < f.cpass;
+    const bool a0 = live && add && (uint32_t)lg < f.cpool;
     if (live) {
         first = key_range[2 * row];
         end = key_range[2 * row + 1];
     }
-    T *out = reinterpret_cast<T *>(f.out);
-    const T *pass = reinterpret_cast<const T *>(f.pass) + f.pass_off;
-    if (live && f.mode == SHPL_OUT_CONCAT)
-        for (uint32_t c = lg; c < f.cpass; c += G)
-            C::store_nt(out + (row * f.out_stride + (int64_t)c * VEC), C::load_nt(pass + (row * f.pass_stride + (int64_t)c * VEC)));
-    // longest run among the wave's rows: the walk's trip count
-    int32_t len = end - first, wlen = len;
+    if (p0) pv = C::load_nt(pass + (row * f.pass_stride + (int64_t)lg * VEC));
+    if (a0) av = C::load(pass + (row * f.pass_stride + (int64_t)lg * VEC));
+    const int32_t len = end - first;
+    int32_t wlen = len;  // longest run among the wave's rows: the walk's trip count
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) wlen = max(wlen, __shfl_xor(wlen, o, 64));
-    const T *src = reinterpret_cast<const T *>(f.src) + f.src_off;
-    const uint32_t oc0 = f.mode == SHPL_OUT_CONCAT ? f.cpass : 0u;
+    if (p0) C::store_nt(out + (row * f.out_stride + (int64_t)lg * VEC), pv);
+    if (live && concat)
+        for (uint32_t c = lg + G; c < f.cpass; c += G)
+            C::store_nt(out + (row * f.out_stride + (int64_t)c * VEC),
+                        C::load_nt(pass + (row * f.pass_stride + (int64_t)c * VEC)));
     for (uint32_t pc0 = 0; pc0 < f.cpool; pc0 += G) {
         const uint32_t pc = pc0 + lg;
         const bool mine = live && pc < f.cpool;
@@ -491,12 +506,11 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_rows(const Feat f, const Ents e,
             const int32_t n = min(G, wlen - j0);
             for (int32_t u0 = 0; u0 < n; u0 += ROWS_WALK) {
                 typename C::raw_t raw[ROWS_WALK];
-                int32_t sr[ROWS_WALK];
 #pragma unroll
                 for (int u = 0; u < ROWS_WALK; ++u) {
-                    const int srcl = gbase + ((u0 + u) & (G - 1));
-                    sr[u] = __shfl(my_src, srcl, 64);
-                    if (mine && j0 + u0 + u < len && u0 + u < G) raw[u] = C::load(src + ((int64_t)sr[u] * f.src_stride + (int64_t)pc * VEC));
+                    const int32_t sr = __shfl(my_src, gbase + ((u0 + u) & (G - 1)), 64);
+                    if (mine && j0 + u0 + u < len && u0 + u < G)
+                        raw[u] = C::load(src + ((int64_t)sr * f.src_stride + (int64_t)pc * VEC));
                 }
 #pragma unroll
                 for (int u = 0; u < ROWS_WALK; ++u) {
@@ -528,16 +542,15 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_rows(const Feat f, const Ents e,
 #pragma unroll
             for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(acc[j], q[j]);
         }
-        if (len == 0 && f.mode != SHPL_OUT_ADD) {
-            C::store_nt(out + (row * f.out_stride + (int64_t)(oc0 + pc) * VEC), C::zero());
-            continue;
-        }
-        if (f.mode == SHPL_OUT_ADD) {
+        if (add) {
             // pass + pooled (pass + 0.0f for an empty row: k_dense's -0 -> +0)
             float a[VEC];
-            C::to_f32(C::load(pass + (row * f.pass_stride + (int64_t)pc * VEC)), a);
+            C::to_f32(pc0 == 0 ? av : C::load(pass + (row * f.pass_stride + (int64_t)pc * VEC)), a);
 #pragma unroll
             for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(a[j], acc[j]);
+        } else if (len == 0) {
+            C::store_nt(out + (row * f.out_stride + (int64_t)(oc0 + pc) * VEC), C::zero());
+            continue;
         }
         C::store_nt(out + (row * f.out_stride + (int64_t)(oc0 + pc) * VEC), C::from_f32(acc));
     }
