@@ -80,6 +80,8 @@ def parse():
                     help="config 2: frame groups of the layer; group g's pooled rows are gathered while "
                          "group g+1 streams (1 = one dense + one sparse launch; measured fastest, "
                          "profiles/r01_groups.log)")
+    ap.add_argument("--no-interleave", action="store_true",
+                    help="dual configs: start both sparse passes after both dense passes (A/B of the overlap)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step eagerly instead of replaying one captured HIP graph of it")
     ap.add_argument("--workload", default="layer", choices=["layer", "frames", "conv"],
@@ -305,6 +307,7 @@ def main():
         d_bev, d_img = torch.empty_like(bev), torch.empty_like(img)
     side = torch.cuda.Stream(device=dev)
     side2 = torch.cuda.Stream(device=dev) if dual else None  # pixel-keyed CSR / pulls beside the cell-keyed
+    pl.interleave = not args.no_interleave
     grouped = not dual and not args.no_overlap and args.groups > 1
     if grouped:
         host_off = np.concatenate([[0], np.cumsum([f.points.shape[0] for f in frames])])
@@ -383,6 +386,7 @@ def main():
                              dev, rank, args)
     nbytes = step_bytes(cfg, spec, nnz, u_pix, u_cell, F, esz)
     kernels = {}
+    interleaved = dual and not args.no_overlap and not pl.rows and pl.interleave
     if grouped:
         # the layer's window: first k_dense start -> last k_sparse end (the two overlap)
         layer_ms = sum(e["span"][0].elapsed_time(e["span"][1]) for e in evs) / args_steps_ev
@@ -401,6 +405,10 @@ def main():
         sparse_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args_steps_ev
         bwd_ms = sum(e[4].elapsed_time(e[5]) for e in evs) / args_steps_ev if backward else 0.0
         layer_ms = dense_ms + sparse_ms + bwd_ms
+        if interleaved:
+            # the cell-keyed sparse pass runs beside img_fused's dense pass: the layer's window
+            # (first k_dense start -> last k_sparse end) instead of the summed durations
+            layer_ms = sum(e[0].elapsed_time(e[3]) for e in evs) / args_steps_ev + bwd_ms
     achieved = nbytes / (layer_ms * 1e-3) / 1e9
 
     cpu = None
@@ -454,8 +462,11 @@ def main():
                 "kernel": ("SHPL layer: k_dense (concat stream) + k_sparse (pooled gather) in "
                            f"{G} frame groups, gathers of group g beside the stream of group g+1; achieved "
                            "over the layer's window (first k_dense start to last k_sparse end)") if grouped else
-                          ("SHPL layer pulls: k_dense (concat stream) + k_sparse (pooled gather); "
-                           "achieved over their summed durations"),
+                          ("SHPL layer pulls: k_dense (concat stream) + k_sparse (pooled gather); achieved over "
+                           + ("the layer's window (first k_dense start to last k_sparse end: the cell-keyed gathers "
+                              "run beside img_fused's stream)" if interleaved else "their summed durations")
+                           + ("; step pulls are row-keyed k_rows (one launch per pull), timed as the sparse and "
+                              "backward brackets" if pl.rows else "")),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

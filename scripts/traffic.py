@@ -86,3 +86,42 @@ if __name__ == "__main__":
         conv(key, key.split("_")[1])
     else:
         main(key)
+
+
+def step_traffic(key, tag, layer_kernels=("k_dense", "k_sparse", "k_sparse_long", "k_rows")):
+    """Per-step HBM bytes of the layer kernels of one bench workload from the
+    scripts/r02_pmc.sh passes (gpurun_out/pmc_<tag>_FETCH_SIZE, _WRITE_SIZE):
+    every launch's counters summed, divided by the steps profiled (the number of
+    k_count launches: one index build per step)."""
+    def launches(counter):
+        files = glob.glob(os.path.join(ROOT, "gpurun_out", f"pmc_{tag}_{counter}", "**", "*counter_collection.csv"),
+                          recursive=True)
+        acc = defaultdict(lambda: [0.0, 0])
+        for f in files:
+            for r in csv.DictReader(open(f)):
+                if r.get("Counter_Name") != counter:
+                    continue
+                name = r["Kernel_Name"]
+                short = next((s for k, s in SHORT if k in name), None)
+                if short is None:
+                    short = "k_rows" if "k_rows" in name else ("k_csr_range" if "k_csr_range" in name else name[:40])
+                acc[short][0] += float(r["Counter_Value"])
+                acc[short][1] += 1
+        return acc
+    fetch, write = launches("FETCH_SIZE"), launches("WRITE_SIZE")
+    steps = fetch.get("k_count", [0, 0])[1] or 1
+    out = {}
+    for k in sorted(set(fetch) | set(write)):
+        f_b = 2 * fetch.get(k, [0, 0])[0] * 1024 / steps
+        w_b = write.get(k, [0, 0])[0] * 1024 / steps
+        out[k] = {"fetch_bytes_per_step": f_b, "write_bytes_per_step": w_b,
+                  "launches_per_step": fetch.get(k, [0, 0])[1] / steps}
+    layer = sum(v["fetch_bytes_per_step"] + v["write_bytes_per_step"] for k, v in out.items() if k in layer_kernels)
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    tj = json.load(open(path)) if os.path.exists(path) else {}
+    tj[key] = {"hbm_bytes_per_launch": layer, "steps_profiled": steps, "kernels": out,
+               "note": ("layer = " + " + ".join(layer_kernels) + " per step (every launch of the step summed); "
+                        "FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes; scripts/r02_pmc.sh")}
+    json.dump(tj, open(path, "w"), indent=1)
+    print(key, f"{layer / 1e9:.4f} GB per step", {k: round((v['fetch_bytes_per_step'] + v['write_bytes_per_step']) / 1e6, 2)
+                                                   for k, v in out.items()})

@@ -46,6 +46,8 @@ class FusedPipeline:
         if rows is None:
             rows = self.B < self.ROWS_FRAMES and max(self.Hb * self.Wb, self.Hi * self.Wi) <= self.ROWS_MAX_KEYS
         self.rows = bool(rows)
+        # dual layers in step_overlapped: the cell-keyed sparse pass beside img_fused's stream
+        self.interleave = True
         N = max(self.N, 1)
         i32 = dict(dtype=torch.int32, device=dev)
         self.cell = torch.empty(N, **i32)
@@ -94,14 +96,16 @@ class FusedPipeline:
         L.check(fn(direction, L.dtype_code(out), csr.ref(), L.ptr(src), cs, 0, cs, L.ptr(pass_), cp, 0, cp,
                    L.OUT_CONCAT, L.ptr(out), cs + cp, st), "shpl_pull")
 
-    def layer_dense(self, bev, img):
+    def layer_dense(self, bev, img, which=("cell", "pixel")):
         """Streaming half of the layer (needs no M): pass-through copy + zeros.
         Row-keyed pulls (self.rows) have no separate streaming half."""
         if self.rows:
             return
         st = L.stream_of(self.dev)
-        self._pull(self._lib.shpl_pull_dense, self.csr, L.BY_CELL, img, self.Ci, bev, self.Cb, self.bv_fused, st)
-        if self.dual:
+        if "cell" in which:
+            self._pull(self._lib.shpl_pull_dense, self.csr, L.BY_CELL, img, self.Ci, bev, self.Cb, self.bv_fused,
+                       st)
+        if self.dual and "pixel" in which:
             self._pull(self._lib.shpl_pull_dense, self.pcsr, L.BY_PIXEL, bev, self.Cb, img, self.Ci,
                        self.img_fused, st)
 
@@ -143,14 +147,20 @@ class FusedPipeline:
         `events` (4 timing events) bracket the dense and the sparse launches."""
         main = torch.cuda.current_stream(self.dev)
         side.wait_stream(main)            # inputs / previous step done
+        split = self.dual and side2 is not None
+        # dual layers: the cell-keyed sparse pass needs only bv_fused's stream, so it runs
+        # beside img_fused's stream (the gathers overlap the second dense pass)
+        cell_streamed = torch.cuda.Event() if split and not self.rows and self.interleave else None
         with torch.cuda.stream(side):
             if events:
                 events[0].record(side)
-            self.layer_dense(bev, img)
+            self.layer_dense(bev, img, ("cell",))
+            if cell_streamed is not None:
+                cell_streamed.record(side)
+            self.layer_dense(bev, img, ("pixel",))
             if events:
                 events[1].record(side)
         self.build_index(points, voxels, point_offsets, P, mval)
-        split = self.dual and side2 is not None
         if split:
             side2.wait_stream(main)       # M built
             with torch.cuda.stream(side2):
@@ -158,12 +168,16 @@ class FusedPipeline:
                 side2.wait_stream(side)
                 self.layer_sparse(bev, img, ("pixel",))
         self.build_csr(("cell",) if split else ("cell", "pixel"))
-        main.wait_stream(side)            # sparse overwrites rows the dense pass wrote
+        if cell_streamed is not None:
+            main.wait_event(cell_streamed)  # the cell-keyed sparse pass overwrites rows bv_fused's stream wrote
+        else:
+            main.wait_stream(side)        # sparse overwrites rows the dense pass wrote
         if events:
             events[2].record(main)
         self.layer_sparse(bev, img, ("cell",) if split else ("cell", "pixel"))
         if split:
             main.wait_stream(side2)
+        main.wait_stream(side)
         if events:
             events[3].record(main)
 
