@@ -55,11 +55,14 @@ __device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t *lds, int6
     return r;
 }
 
-// f32 -> bf16 round-to-nearest-even; NaN stays NaN (quiet).
+// f32 -> bf16 round-to-nearest-even; NaN stays NaN (quiet): gfx950's
+// v_cvt_pk_bf16_f32 (one instruction instead of five integer ones -- the bf16
+// conv epilogue converts 64 values per wave and output row).
 __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
-    const uint32_t u = __float_as_uint(f);
-    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
-    return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+    const __bf16 b = (__bf16)f;
+    uint16_t u;
+    __builtin_memcpy(&u, &b, 2);
+    return u;
 }
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
