@@ -542,8 +542,17 @@ def run_frames(args, world, rank, dev):
     bev = sd.fill_features(torch.empty((F, pl.Hb, pl.Wb, C), device=dev), fids, 5)
     img = sd.fill_features(torch.empty((F, pl.Hi, pl.Wi, C), device=dev), fids, 6)
     side = torch.cuda.Stream(device=dev)
+    # the index chain on a high-priority stream: its 1024-thread workgroups otherwise wait for
+    # whole CUs to drain of k_dense's workgroups (BEV slices 1.07 -> 0.68 ms, step 2.86 -> 2.84 ms,
+    # profiles/r02_priority.log; the step is then bound by k_dense + the sparse pass)
+    chain = torch.cuda.Stream(device=dev, priority=-1)
+
+    def velo_step(ev=None):
+        with torch.cuda.stream(chain):
+            pl.velo_step(fr, bev, img, side=side, events=ev)
+
     for _ in range(args.warmup):
-        pl.velo_step(fr, bev, img, side=side)
+        velo_step()
     torch.cuda.synchronize()
     nnz = int(pl.frame_nnz.sum().item())
     u_pix = int(torch.unique(pl.pix[pl.pix >= 0]).numel())
@@ -551,7 +560,7 @@ def run_frames(args, world, rank, dev):
     n_vox = int(pl.bev.frame_nvox.sum().item())
     errs = int(pl.err.item()) | int(pl.bev.err.item()) | int(pl.velo.err.item())
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(9)] for _ in range(args.steps)]
-    elapsed = sd.timed(lambda k: pl.velo_step(fr, bev, img, side=side, events=evs[k]), args.steps, device=dev)
+    elapsed = sd.timed(lambda k: velo_step(evs[k]), args.steps, device=dev)
     mean = lambda i, j: sum(e[i].elapsed_time(e[j]) for e in evs) / args.steps  # noqa: E731
     dense_ms, sparse_ms = mean(0, 1), mean(7, 8)
     stages = {"velo_to_cam_ms": mean(2, 3), "bev_slices_ms": mean(3, 4), "index_ms": mean(4, 5),
