@@ -110,6 +110,35 @@ def layer_bytes(spec, nnz, u_pix, frames, esz=4):
     return pull_bytes(frames * Hb * Wb, spec.c_bev, spec.c_img, u_pix, nnz, esz, spec.c_bev + spec.c_img)
 
 
+def pool_fwd_report(pl, img, spec, F, u_pix, nnz, esz, dev, reps=10):
+    """SURVEY §8d's pool_fwd beside the official layer_fwd: the img->BEV pooling
+    alone (shpl_pull, SHPL_OUT_POOL: k_dense writing the zeros, then k_sparse)
+    into a [F, Hb, Wb, Ci] map, over the CSR the step just built; HIP events
+    around `reps` launches, after the timed loop. Checked bitwise against the
+    pooled half of bv_fused."""
+    from sparse_pooling_amd import _lib as L
+    Hb, Wb = spec.bev_feat_hw
+    ci = spec.c_img
+    out = torch.empty((F, Hb, Wb, ci), dtype=pl.bv_fused.dtype, device=dev)
+    lib = L.lib()
+
+    def run():
+        L.check(lib.shpl_pull(L.BY_CELL, L.dtype_code(out), pl.csr.ref(), L.ptr(img), ci, 0, ci, None, 0, 0, 0,
+                              L.OUT_POOL, L.ptr(out), ci, L.stream_of(dev)), "shpl_pull")
+    run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    nb = pull_bytes(F * Hb * Wb, 0, ci, u_pix, nnz, esz, ci)
+    return {"algorithmic_bytes_per_launch": nb, "ms": round(ms, 4), "achieved_GBps": round(nb / (ms * 1e-3) / 1e9, 1),
+            "frac": round(nb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "equals_layer_pooled_half": bool(torch.equal(out, pl.bv_fused[..., spec.c_bev:]))}
+
+
 def step_bytes(cfg, spec, nnz, u_pix, u_cell, F, esz):
     Hb, Wb = spec.bev_feat_hw
     Hi, Wi = spec.img_feat_hw
@@ -410,6 +439,7 @@ def main():
             # (first k_dense start -> last k_sparse end) instead of the summed durations
             layer_ms = sum(e[0].elapsed_time(e[3]) for e in evs) / args_steps_ev + bwd_ms
     achieved = nbytes / (layer_ms * 1e-3) / 1e9
+    pool = pool_fwd_report(pl, img, spec, F, u_pix, nnz, esz, dev) if cfg == 2 and not grouped else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -478,6 +508,7 @@ def main():
                 "k_sparse_ms": round(sparse_ms, 4),
                 "backward_ms": round(bwd_ms, 4),
                 **({"kernels": kernels} if kernels else {}),
+                **({"pool_fwd": pool} if pool else {}),
             },
             "cpu_baseline": cpu,
             "index_errors": err,

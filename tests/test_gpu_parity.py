@@ -529,6 +529,105 @@ def test_pipeline_backward_matches_oracle(cfg, dtype, mode, rows):
 
 # ---------------------------------------------------------------- BEV voxelizer
 
+def _ragged_frames(base, sizes, seed):
+    """Frames of the given inside-point counts: 0 = no points at all, negative =
+    -n points that all fall outside the image (no survivor)."""
+    frames = []
+    for f, n in enumerate(sizes):
+        if n == 0:
+            frames.append(synth.Frame(np.zeros((0, 3)), np.zeros((0, 2), dtype=np.int64), synth.KITTI_P2,
+                                      synth.FrameSpec(0, base.im_size, base.bv_size, base.stride, base.c_bev,
+                                                      base.c_img)))
+            continue
+        spec = synth.FrameSpec(max(n, 0), base.im_size, base.bv_size, base.stride, base.c_bev, base.c_img)
+        frames.append(synth.make_frame(spec, seed=seed + f, n_outside=-n if n < 0 else 13 * f))
+    return frames
+
+
+def _ragged_pipeline_run(cfg, sizes, dtype, paths):
+    """FusedPipeline forward + backward over a ragged batch, once per CSR path
+    (SHPL_CSR_PATH: frame / segment / range; None = the default), each compared
+    with the oracle frame by frame (f32: bitwise; bf16: bitwise on the bf16 bits)."""
+    from sparse_pooling_amd import pipeline
+    base = synth.CONFIGS[cfg]
+    frames = _ragged_frames(base, sizes, 500)
+    refs = [_oracle_frame(fr, base.stride) for fr in frames]
+    B = len(frames)
+    pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
+    tdt = torch.float32 if dtype == "f32" else torch.bfloat16
+    Hb, Wb = base.bev_feat_hw
+    Hi, Wi = base.img_feat_hw
+    Cb, Ci = base.c_bev, base.c_img
+
+    def mk(shape, seed):
+        x = synth.make_features(shape, seed)
+        if dtype == "bf16":
+            x = orc.from_bf16_bits(orc.to_bf16_bits(x)).reshape(shape)
+        return x, torch.from_numpy(x).to(DEV).to(tdt)
+    bev, tb = mk((B, Hb, Wb, Cb), 1)
+    img, ti = mk((B, Hi, Wi, Ci), 2)
+    gb, tgb = mk((B, Hb, Wb, Cb + Ci), 3)
+    gi, tgi = mk((B, Hi, Wi, Ci + Cb), 4)
+    want = []
+    for f, ref in enumerate(refs):
+        mij, mval, msize, idx = ref["Mij_pool"], ref["M_val"], ref["M_size"], ref["img_index_flip_pool"]
+        eb, ei = orc.sparse_pool_layer(bev[f:f + 1], img[f:f + 1], mij, mval, msize, idx, dual=True)
+        e_img = gi[f:f + 1, ..., :Ci] + orc.sparse_pool_grad_img(
+            mij, mval, msize, gb[f, ..., Cb:].reshape(-1, Ci), idx, (1, Hi, Wi, Ci))
+        e_bev = gb[f:f + 1, ..., :Cb] + orc.sparse_pool_trans_grad_bev(
+            mij, mval, msize, np.ascontiguousarray(gi[f:f + 1, ..., Ci:]), idx).reshape(1, Hb, Wb, Cb)
+        want.append((eb, ei, e_bev, e_img))
+
+    def same(got, exp):
+        if dtype == "f32":
+            _close_and_exact(got, exp)
+        else:
+            np.testing.assert_array_equal(_np(got.view(torch.int16)).view(np.uint16),
+                                          orc.to_bf16_bits(exp.astype(np.float32)))
+    old = os.environ.get("SHPL_CSR_PATH")
+    try:
+        for path in paths:
+            if path is None:
+                os.environ.pop("SHPL_CSR_PATH", None)
+            else:
+                os.environ["SHPL_CSR_PATH"] = path
+            pl = pipeline.FusedPipeline(B, maxp, N, base.im_size, base.bv_size, base.stride, Cb, Ci, dtype=tdt,
+                                        dual=True)
+            d_bev, d_img = torch.empty_like(tb), torch.empty_like(ti)
+            pl.step(pts, vox, off, P, tb, ti)
+            pl.backward(tgb, tgi, d_bev, d_img)
+            torch.cuda.synchronize()
+            assert int(pl.err.item()) == 0
+            nnz = _np(pl.frame_nnz)
+            for f, (eb, ei, e_bev, e_img) in enumerate(want):
+                assert nnz[f] == refs[f]["M_size"][1], (path, f)
+                same(pl.bv_fused[f:f + 1], eb)
+                same(pl.img_fused[f:f + 1], ei)
+                same(d_bev[f:f + 1], e_bev)
+                same(d_img[f:f + 1], e_img)
+            del pl
+    finally:
+        if old is None:
+            os.environ.pop("SHPL_CSR_PATH", None)
+        else:
+            os.environ["SHPL_CSR_PATH"] = old
+
+
+def test_pipeline_ragged_batch_every_csr_path():
+    """Empty and ragged inputs through the whole batched path (index -> both CSRs
+    -> dual layer -> both gradients) at config-2 shape: a frame without points,
+    a one-point frame, a frame whose points all fall outside the image, frames
+    straddling the index builder's chunks -- under each CSR builder (per-frame
+    workgroup, segments, destination ranges), bitwise against the oracle."""
+    _ragged_pipeline_run(2, [0, 1, -40, 1025, 20000, 2], "f32", ["frame", "segment", "range"])
+
+
+def test_pipeline_ragged_batch_row_keyed_bf16():
+    """The same ragged batch at config-3 shape (bf16, 256 channels, row-keyed
+    pulls over key_range CSRs), bitwise on the bf16 bits."""
+    _ragged_pipeline_run(3, [0, 1, -40, 1025, 20000, 2], "bf16", [None])
+
+
 def test_bev_slices_vs_reference_golden():
     from sparse_pooling_amd import bev
     g = np.load(os.path.join(GOLD, "bev_slices.npz"))
