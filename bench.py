@@ -402,8 +402,17 @@ def main():
         evs = [new_events() for _ in range(n_ev)]
     else:
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(n_ev)]
+    issue_ms = None
     if graph is not None:
         elapsed = sd.timed(lambda k: graph.replay(), args.steps, device=dev)
+        # host cost of one replay: issue the replays without waiting (after the timed loop); well
+        # under the step at every config (0.03 ms at config 3), so the timed loop is not launch-bound
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            graph.replay()
+        issue_ms = 1e3 * (time.perf_counter() - t0) / args.steps
+        torch.cuda.synchronize()
         for k in range(n_ev):
             step(evs[k])
         torch.cuda.synchronize()
@@ -484,6 +493,7 @@ def main():
                 "unique_cells_rank0": u_cell,
                 "overlap_index_build": not args.no_overlap,
                 "hip_graph": graph is not None,
+                **({"graph_issue_ms_per_replay": round(issue_ms, 4)} if issue_ms is not None else {}),
                 **({"graph_note": graph_note} if graph_note else {}),
                 "parallelism": f"frame-sharded x{world}",
             },
