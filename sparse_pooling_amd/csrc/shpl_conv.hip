@@ -182,6 +182,49 @@ __device__ __forceinline__ void pool_run(const ConvArgs &p, const T *img, int c0
     }
 }
 
+// One 16-byte piece (channels [c, c + HE)) of an occupied cell's pooled
+// vector: pool_run's sum for one piece, its entries' loads issued
+// POOL_BATCH at a time (one round trip for runs of up to POOL_BATCH entries)
+// and summed in entry order.
+#ifndef SHPL_POOL_PIECES
+#define SHPL_POOL_PIECES 1
+#endif
+constexpr int POOL_BATCH = 4;
+template <typename T, bool SWZ, int PSTR>
+__device__ __forceinline__ void pool_piece(const ConvArgs &p, const T *img, int c, int32_t e0, int32_t e1,
+                                           int32_t src0, float val0, uint8_t *s_base, int pix, int g) {
+    typedef Elem<T> E;
+    constexpr int HE = E::HE;
+    float sum[HE];
+#pragma unroll
+    for (int j = 0; j < HE; ++j) sum[j] = 0.0f;
+    for (int32_t i0 = e0; i0 < e1; i0 += POOL_BATCH) {
+        u32x4 raw[POOL_BATCH];
+        float wv[POOL_BATCH];
+#pragma unroll
+        for (int u = 0; u < POOL_BATCH; ++u) {
+            const int32_t i = i0 + u;
+            if (i < e1) {
+                const int32_t sr = i == e0 ? src0 : p.ent_src[i];
+                wv[u] = i == e0 ? val0 : p.ent_val[i];
+                raw[u] = load_piece<T>(img + (int64_t)sr * p.b_stride, c, p.c_b, p.vec_b);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < POOL_BATCH; ++u) {
+            if (i0 + u >= e1) break;
+            T x[HE];
+            __builtin_memcpy(x, &raw[u], sizeof(raw[u]));
+#pragma unroll
+            for (int j = 0; j < HE; ++j) sum[j] = __fadd_rn(sum[j], __fmul_rn(wv[u], E::f(x[j])));
+        }
+    }
+    T o[HE];
+#pragma unroll
+    for (int j = 0; j < HE; ++j) o[j] = E::back(sum[j]);
+    __builtin_memcpy(s_base + piece_off<SWZ, PSTR>(pix, g), o, 16);
+}
+
 // The halo tile's runs of CSR entries in LDS (POOLED): one run per occupied
 // halo cell, with its first entry's source row and weight.
 struct HaloRuns {
@@ -328,8 +371,15 @@ __device__ __forceinline__ void stage_halo(const ConvArgs &p, int q, int f, int 
                 *reinterpret_cast<u32x4 *>(s_in + piece_off<SWZ, PSTR>(j / NP, j % NP)) = u32x4{0u, 0u, 0u, 0u};
         }
         const T *img = reinterpret_cast<const T *>(p.b) + p.b_off;
+#if SHPL_POOL_PIECES
+        // one (run, 16-byte piece) pair per thread, POOL_BATCH entries' loads in flight per round trip
+        for (int t = tid; t < n_run * NP; t += CONV_BLOCK)
+            pool_piece<T, SWZ, PSTR>(p, img, (q - p.qa) * CK + (t % NP) * HE, r.e[t / NP], r.end[t / NP],
+                                     r.src[t / NP], r.val[t / NP], s_in, r.pix[t / NP], t % NP);
+#else
         for (int k = tid; k < n_run; k += CONV_BLOCK)
             pool_run<T, SWZ, PSTR>(p, img, (q - p.qa) * CK, r.e[k], r.end[k], r.src[k], r.val[k], s_in, r.pix[k]);
+#endif
     }
 }
 
