@@ -356,14 +356,19 @@ typedef enum { SHPL_ACT_NONE = 0, SHPL_ACT_RELU = 1 } shpl_act;
  * the pre-epilogue output, for BatchNorm in training mode (shpl_batch_norm).
  * f32: v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulation);
  * SHPL_BF16: bf16 storage, v_mfma_f32_32x32x16_bf16, f32 accumulation, one
- * rounding at the store. Workspace: shpl_conv3x3_workspace_bytes.
+ * rounding at the store. Workspace: shpl_conv3x3_workspace_bytes, with
+ * pool_nnz_cap = pool->nnz_cap for a pooled call and -1 without a pool.
+ * bf16 inputs of at most 64 channels (c_a, c_b multiples of 8, 16-byte rows)
+ * without d_stats run the row-streaming kernel; pooled, the pooled vector of
+ * each occupied cell is computed once into the workspace (shpl_pull's
+ * arithmetic) and gathered by the conv's staging.
  * Replaces: bv_fused = sparse_pool_layer(...) (sparse_pool_utils.py:61-92)
  *   followed by slim.conv2d(bv_fused, Ci, [3,3], normalizer_fn=slim.batch_norm)
  *   (avod/avod/core/models/rpn_model.py:338-346, scope pyramid_fusion_pooled_bev;
  *   the img side :347-354) and slim.conv2d(bev_fused, 256, [3,3])
  *   (avod/avod/core/models/retinanet_model.py:343-348). */
 int shpl_conv3x3_workspace_bytes(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_t c_b,
-                                 int64_t c_out, int pooled, int stats, size_t *bytes);
+                                 int64_t c_out, int64_t pool_nnz_cap, int stats, size_t *bytes);
 int shpl_conv3x3(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a, int64_t a_stride,
                  int64_t a_off, int64_t c_a, const void *d_b, int64_t b_stride, int64_t b_off,
                  int64_t c_b, const shpl_csr *pool, const int64_t *d_frame_off, const void *d_weights,
@@ -411,7 +416,7 @@ int shpl_batch_norm_backward(int dtype, int64_t rows, const void *d_y, const voi
  * set, channels [0, c_split) go to d_dx and [c_split, c_dx) to d_dx_b (the
  * gradients of the conv's two sources, e.g. BEV and pooled image channels,
  * as separate dense maps); with d_dx_b NULL, c_split is ignored. Workspace:
- * shpl_conv3x3_workspace_bytes(dtype, n_frames, h, w, c_gy, 0, c_dx, 0, 0). */
+ * shpl_conv3x3_workspace_bytes(dtype, n_frames, h, w, c_gy, 0, c_dx, -1, 0). */
 int shpl_conv3x3_dgrad(int dtype, int n_frames, int64_t h, int64_t w, const void *d_gy, int64_t gy_stride,
                        int64_t c_gy, const void *d_weights, int64_t c_dx, void *d_dx, int64_t dx_stride,
                        int64_t c_split, void *d_dx_b, int64_t dx_b_stride, void *d_ws, size_t ws_bytes,

@@ -37,11 +37,13 @@ from . import _lib as L
 from . import shpl_map as sm
 
 
-def conv_ws_bytes(dtype, n_frames, h, w, c_a, c_b, c_out, pooled, stats):
+def conv_ws_bytes(dtype, n_frames, h, w, c_a, c_b, c_out, pool_cap, stats):
+    """Workspace of shpl_conv3x3; pool_cap: the pooling CSR's entry capacity
+    (``Csr.nnz_cap``), or None without a pool."""
     out = ctypes.c_size_t()
     L.check(L.lib().shpl_conv3x3_workspace_bytes(dtype, int(n_frames), int(h), int(w), int(c_a), int(c_b),
-                                                 int(c_out), int(bool(pooled)), int(bool(stats)),
-                                                 ctypes.byref(out)), "shpl_conv3x3_workspace_bytes")
+                                                 int(c_out), -1 if pool_cap is None else int(pool_cap),
+                                                 int(bool(stats)), ctypes.byref(out)), "shpl_conv3x3_workspace_bytes")
     return out.value
 
 
@@ -75,7 +77,8 @@ def conv3x3(a, weights, b=None, pool=None, frame_off=None, center=None, scale=No
     if out is None:
         out = torch.empty((B, H, W, Cout), dtype=a.dtype, device=a.device)
     if ws is None:
-        ws = L.workspace(conv_ws_bytes(dt, B, H, W, Ca, Cb, Cout, pool is not None, stats is not None), a.device)
+        ws = L.workspace(conv_ws_bytes(dt, B, H, W, Ca, Cb, Cout, None if pool is None else pool.nnz_cap,
+                                       stats is not None), a.device)
     f32 = [None if v is None else v.to(device=a.device, dtype=torch.float32).contiguous()
            for v in (center, scale, shift)]
     L.check(L.lib().shpl_conv3x3(dt, B, H, W, L.ptr(a), Ca, 0, Ca, L.ptr(b), Cb, 0, Cb,
@@ -135,7 +138,7 @@ def conv3x3_dgrad(gy, weights, c_dx, split=None):
     c0 = c_dx if split is None else int(split)
     dx = torch.empty((B, H, W, c0), dtype=gy.dtype, device=gy.device)
     dx_b = None if split is None else torch.empty((B, H, W, c_dx - c0), dtype=gy.dtype, device=gy.device)
-    ws = L.workspace(conv_ws_bytes(L.dtype_code(gy), B, H, W, Cg, 0, c_dx, False, False), gy.device)
+    ws = L.workspace(conv_ws_bytes(L.dtype_code(gy), B, H, W, Cg, 0, c_dx, None, False), gy.device)
     L.check(L.lib().shpl_conv3x3_dgrad(L.dtype_code(gy), B, H, W, L.ptr(gy), Cg, Cg, L.ptr(weights), c_dx,
                                        L.ptr(dx), max(c0, 1), c0, L.ptr(dx_b), max(c_dx - c0, 1), L.ptr(ws),
                                        ws.numel(), L.stream_of(gy.device)),
@@ -181,8 +184,8 @@ class _FusionConvFn(torch.autograd.Function):
         pool = smap.csr(L.BY_CELL, L.ORDER_ENTRY) if pooled else None
         frame_off = smap.frame_off if pooled else None
         train_bn = conv.batch_norm and is_training
-        ws = conv._ws_for((dt, B, H, W, Cb, pooled, train_bn),
-                          conv_ws_bytes(dt, B, H, W, Ca, Cb, conv.c_out, pooled, train_bn))
+        cap = pool.nnz_cap if pooled else None
+        ws = conv._ws_for((dt, B, H, W, Cb, cap, train_bn), conv_ws_bytes(dt, B, H, W, Ca, Cb, conv.c_out, cap, train_bn))
         raw, mean, scale = None, None, None
         if not train_bn:
             center, scale, shift = conv._inference_epilogue()
@@ -289,8 +292,9 @@ class FusionConv:
         Cb = 0 if b is None else int(b.shape[-1])
         dt = L.dtype_code(a)
         train_bn = self.batch_norm and is_training
-        ws = self._ws_for((dt, B, H, W, Cb, pool is not None, train_bn),
-                          conv_ws_bytes(dt, B, H, W, int(a.shape[-1]), Cb, self.c_out, pool is not None, train_bn))
+        cap = None if pool is None else pool.nnz_cap
+        ws = self._ws_for((dt, B, H, W, Cb, cap, train_bn),
+                          conv_ws_bytes(dt, B, H, W, int(a.shape[-1]), Cb, self.c_out, cap, train_bn))
         if not train_bn:
             center, scale, shift = self._inference_epilogue()
             return conv3x3(a, self.weights, b=b, pool=pool, frame_off=frame_off, center=center, scale=scale,

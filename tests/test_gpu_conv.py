@@ -257,6 +257,71 @@ def test_bf16_conv_and_fused():
             np.testing.assert_array_equal(_np(y_fus.float()), _np(y_unf.float()))
 
 
+ROWS_SHAPES = [  # bf16, <= 64 input channels, whole 32-channel output blocks: the row-streaming kernel
+    (2, 16, 64, 64, 32),   # one band, two strips
+    (3, 17, 70, 24, 64),   # a partial strip, two output blocks, a channel tail inside chunk 2
+    (1, 1, 5, 8, 32),      # one row, one partial strip
+    (2, 130, 40, 48, 32),  # three bands (band edges inside the map)
+    (1, 61, 33, 16, 32),   # one band of 61 rows (every ring slot phase at the band end)
+]
+
+
+@pytest.mark.parametrize("shape", ROWS_SHAPES, ids=[str(s) for s in ROWS_SHAPES])
+def test_bf16_rows_conv_dense(shape):
+    """k_conv_rows (bf16, weights resident in VGPRs, per-wave LDS-DMA ring) vs
+    the oracle, with the BatchNorm-inference epilogue; a two-source split on
+    the chunk grid is bitwise the one-source conv."""
+    from sparse_pooling_amd import fusion_conv as fc
+    B, H, W, Cin, Cout = shape
+    x = orc.from_bf16_bits(orc.to_bf16_bits(synth.make_features((B, H, W, Cin), 41)))
+    w = orc.from_bf16_bits(orc.to_bf16_bits(_weights(Cin, Cout, 42)))
+    rng = np.random.default_rng(43)
+    center = rng.standard_normal(Cout).astype(np.float32)
+    scale = rng.uniform(0.5, 2.0, Cout).astype(np.float32)
+    shift = rng.standard_normal(Cout).astype(np.float32)
+    y = fc.conv3x3(_bf16(x), _bf16(w), center=_t(center), scale=_t(scale), shift=_t(shift), relu=True)
+    ref = orc.conv3x3(x, w, center, scale, shift, True)
+    _assert_within(y.float(), ref, _bound(x, w, scale) + np.abs(ref) * 2.0 ** -8)
+    if Cin % 32 == 0:
+        h = Cin // 2
+        y2 = fc.conv3x3(_bf16(np.ascontiguousarray(x[..., :h])), _bf16(w), b=_bf16(np.ascontiguousarray(x[..., h:])),
+                        center=_t(center), scale=_t(scale), shift=_t(shift), relu=True)
+        np.testing.assert_array_equal(_np(y2.float()), _np(y.float()))
+
+
+def test_bf16_rows_fused_config2():
+    """Config 2 in bf16 (32 + 32 -> 32 channels: k_conv_rows with the pooled
+    half gathered from the compact run buffer): fused == the conv of the
+    materialised bv_fused bitwise, and within the bf16 bound of the oracle's
+    conv of the oracle's bv_fused on a band of rows."""
+    from sparse_pooling_amd import fusion_conv as fc, shpl_map as sm
+    spec, frames, ib = _batch_map(2, 2, 700)
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    Cb, Ci = spec.c_bev, spec.c_img
+    bev = orc.from_bf16_bits(orc.to_bf16_bits(synth.make_features((2, Hb, Wb, Cb), 51)))
+    img = orc.from_bf16_bits(orc.to_bf16_bits(synth.make_features((2, Hi, Wi, Ci), 52)))
+    w = orc.from_bf16_bits(orc.to_bf16_bits(_weights(Cb + Ci, Ci, 53)))
+    tb, ti, tw = _bf16(bev), _bf16(img), _bf16(w)
+    conv = fc.FusionConv(Cb + Ci, Ci, dtype=torch.bfloat16, device=DEV, seed=3)
+    conv.weights = tw
+    conv.moving_mean = _t(np.random.default_rng(1).standard_normal(Ci).astype(np.float32) * 0.1)
+    conv.beta = _t(np.random.default_rng(2).standard_normal(Ci).astype(np.float32) * 0.1)
+    bv_fused = sm.pool_img_to_bev(ib.map, ti, tb.shape, bev=tb)
+    y_unf = conv(bv_fused)
+    y_fus = conv.fused(tb, ti, ib.map)
+    torch.cuda.synchronize()
+    assert ib.map.error_bits() == 0
+    np.testing.assert_array_equal(_np(y_fus.float()), _np(y_unf.float()))
+    center, scale, shift = (_np(v) for v in conv._inference_epilogue())
+    y0, y1 = 296, 344
+    for f in range(2):
+        x = _np(bv_fused[f:f + 1, y0 - 1:y1 + 1].float())
+        ref = orc.conv3x3(x, w, center, scale, shift, True)[:, 1:-1]
+        bound = (_bound(x, w, scale) + np.abs(orc.conv3x3(x, w, center, scale, shift, True)) * 2.0 ** -8)[:, 1:-1]
+        _assert_within(y_fus[f:f + 1, y0:y1].float(), ref, bound)
+
+
 def test_conv_argument_errors():
     from sparse_pooling_amd import fusion_conv as fc, _lib as L
     x = _t(synth.make_features((1, 4, 4, 8), 1))
