@@ -694,12 +694,14 @@ __global__ __launch_bounds__(CONV_BLOCK, NCB == 2 ? 3 : 4) void k_conv3x3(const 
 // no barrier anywhere (one wave). Two waves per SIMD (8 per CU) each run
 // their own ring: one's MFMAs cover the other's waits.
 //
-// Slot layout: 40 pixels (34 used) x 128 bytes = 8 pieces of 16 bytes (piece
-// g = 2 chunk + half: channels 16 chunk + 8 half); piece g of pixel p sits at
-// p*128 + 16 (g ^ ((p >> 1) & 7)): the 16 lanes of any ds_read_b128 lane group
-// read 16 consecutive-mod-16 pixels of one piece and hit 16 distinct bank
-// quads. An LDS-DMA fills 8 pixels (lane k: pixel k/8, slot piece k%8, which
-// loads the logical piece the swizzle puts there).
+// Slot layout: [piece][40 pixels] of 16 bytes (piece g = 2 chunk + half:
+// channels 16 chunk + 8 half; pixels 34..39 unused): the lanes of a
+// ds_read_b128 read 16 consecutive pixels of one piece (16 distinct bank quads,
+// no swizzle), and every pixel-operand read of a row is one base register plus
+// an immediate (kx: 16 bytes, chunk: 1280). An LDS-DMA fills 64 consecutive
+// 16-byte slots (lane k: slot 64 i + k = piece (64 i + k) / 40, pixel
+// (64 i + k) % 40); each lane's source offsets for the 5 DMAs are computed
+// once per band.
 //
 // Pooled B channels (CMP): the pooled vectors of the occupied cells, computed
 // once by k_pool_runs with shpl_pull's arithmetic into a compact buffer (one
@@ -709,12 +711,16 @@ __global__ __launch_bounds__(CONV_BLOCK, NCB == 2 ? 3 : 4) void k_conv3x3(const 
 // fused form is bitwise the conv of [bev || shpl_pull(...)] through this same
 // kernel.
 constexpr int RING = 3;                    // ring slots per wave = the row loop's unroll
+#ifndef SHPL_ROWS_PRIO
+#define SHPL_ROWS_PRIO 0  // 1: s_setprio 1 over each row's MFMAs; 2: over its epilogue and staging
+#endif
 #ifndef SHPL_ROWS_PROBE
 #define SHPL_ROWS_PROBE 0  // timing probes (wrong results): 1 no ring DMAs in the loop, 2 no MFMAs, 3 no output stores
 #endif
-constexpr int RPIX = 40;                   // pixels per ring slot (34 used)
-constexpr int RSLOT = RPIX * 128;          // bytes per ring slot
-constexpr int RDMA = RPIX / 8;             // LDS-DMAs per staged row
+constexpr int RPIX = 40;                   // pixels per piece row of a ring slot (34 used)
+constexpr int RPIECE = RPIX * 16;          // bytes per piece row
+constexpr int RSLOT = 8 * RPIECE;          // bytes per ring slot (8 pieces)
+constexpr int RDMA = RSLOT / 1024;         // LDS-DMAs per staged row
 constexpr int REPI = NCO * 2 + 16;         // epilogue transpose row pitch (bytes per pixel)
 constexpr int OCC_MAX_WORDS = 32768;       // k_occ_frame's LDS mask: up to 1M cells per frame
 
@@ -842,7 +848,6 @@ struct RowArgs {
     int h, w, strips, band, n_bands, n_items;
     const uint16_t *wp;          // packed weights [co_block][chunk][tap][32][16]
     const float *center, *scale, *shift;
-    int act;
     uint16_t *out;
     int64_t out_stride;
     const uint32_t *occ;         // CMP: occupancy words, prefix counts, compact pooled rows, entry slots
@@ -862,54 +867,55 @@ __device__ __forceinline__ void dma16_ring(const void *src, const uint8_t *wave_
     asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(lds) : "memory");
 }
 
-// Lane's piece of an LDS-DMA: pixel 8 i + lane/8 of the staged row, slot piece
-// lane%8, logical piece g = lane%8 ^ ((pixel >> 1) & 7) = lane%8 ^ lane/16 ^
-// 4 (i & 1). Its source: channel q*16 + 8 (g & 1) of A (q = g/2 < qa), of B
-// (q < Q), or nothing (-1). Encoded as channel | (1 << 30) for B.
-template <int Q>
-__device__ __forceinline__ int rows_piece_src(const RowArgs &r, int lane, int parity) {
-    const int g = (lane & 7) ^ (lane >> 4) ^ (4 * parity), q = g >> 1, c8 = (g & 1) * 8;
-    if (q < r.qa) return q * 16 + c8 < r.c_a ? q * 16 + c8 : -1;
-    if (q < Q) return (q - r.qa) * 16 + c8 < r.c_b ? ((q - r.qa) * 16 + c8) | (1 << 30) : -1;
-    return -1;
-}
-
-// The lane id, opaque to the optimizer: the per-lane offsets derived from it
-// are recomputed in every row (a few VALU) instead of being hoisted out of the
-// row loop into ~30 live registers beside 144 weight and 48 accumulator ones.
-__device__ __forceinline__ int lane_now(int lane) {
-    asm volatile("" : "+v"(lane));
-    return lane;
-}
-
-// Stages input row y into a ring slot: RDMA LDS-DMAs, every lane issuing
-// (the vmcnt arithmetic counts whole instructions); pieces outside the map,
-// the channels or the band read the zero piece. pix0: global pixel row of the
-// slot's pixel 0 (uniform: 64-bit bases in SGPRs, 32-bit lane offsets).
+// Per band, per lane and DMA i: where slot 64 i + lane's piece comes from.
+// Dense: bit 31 = B, bits 0..30 = the element offset from the row's pixel 0
+// (pixel * stride + channel). CMP B pieces: bit 31, pixel << 16 | channel.
+// valid: bit i set when the piece lies inside the map's columns and channels.
 template <int Q, bool CMP>
-__device__ __forceinline__ void rows_stage(const RowArgs &r, int64_t pix0, int x0, bool yok, uint64_t occ,
-                                           int32_t first, uint8_t *slot, int lane_in) {
-    const int lane = lane_now(lane_in);
-    const int src_e = rows_piece_src<Q>(r, lane, 0), src_o = rows_piece_src<Q>(r, lane, 1);
+__device__ __forceinline__ void rows_lane_src(const RowArgs &r, int x0, int lane, int (&off)[RDMA], int &valid) {
+    valid = 0;
+#pragma unroll
+    for (int i = 0; i < RDMA; ++i) {
+        const int sl = 64 * i + lane, g = sl / RPIX, px = sl - g * RPIX, x = x0 - 1 + px;
+        const int q = g >> 1, c8 = (g & 1) * 8;
+        const bool in_x = px < HWD && x >= 0 && x < r.w;
+        int o = 0;
+        bool ok = false;
+        if (q < r.qa) {
+            ok = q * 16 + c8 < r.c_a;
+            o = px * (int)r.a_stride + q * 16 + c8;
+        } else if (q < Q) {
+            const int c = (q - r.qa) * 16 + c8;
+            ok = c < r.c_b;
+            o = (int)(0x80000000u | (uint32_t)(CMP ? (px << 16) | c : px * (int)r.b_stride + c));
+        }
+        off[i] = o;
+        valid |= (ok && in_x ? 1 : 0) << i;
+    }
+}
+
+// Stages input row y (its pixel 0 at global pixel pix0) into a ring slot:
+// RDMA LDS-DMAs, every lane issuing (the vmcnt arithmetic counts whole
+// instructions); pieces outside the map, the channels or the band read the
+// zero piece.
+template <bool CMP>
+__device__ __forceinline__ void rows_stage(const RowArgs &r, int64_t pix0, bool yok, uint64_t occ, int32_t first,
+                                           const int (&off)[RDMA], int valid, uint8_t *slot) {
     const uint16_t *row_a = r.a + pix0 * r.a_stride;
     const uint16_t *row_b = CMP ? r.cmp : r.b + pix0 * r.b_stride;
 #pragma unroll
     for (int i = 0; i < RDMA; ++i) {
-        const int px = 8 * i + (lane >> 3), x = x0 - 1 + px;
-        const int src = (i & 1) ? src_o : src_e;
-        const int ch = src & 0xffff;
-        const bool is_b = (src >> 30) & 1;
-        // bitwise & throughout: selects, not branches
-        bool ok = yok & (src >= 0) & (px < HWD) & (x >= 0) & (x < r.w);
-        int off_b;
+        const int o = off[i];
+        const bool is_b = o < 0;
+        bool ok = yok & (bool)((valid >> i) & 1);
+        int e = o & 0x7fffffff;
         if constexpr (CMP) {
+            const int px = (o >> 16) & 63;
+            const int rank = first + (int)__popcll(occ & ((1ull << px) - 1));
             ok = ok & (!is_b | (bool)((occ >> px) & 1));
-            off_b = (first + (int)__popcll(occ & ((1ull << px) - 1))) * r.c_b + ch;
-        } else {
-            off_b = px * (int)r.b_stride + ch;
+            e = is_b ? rank * r.c_b + (o & 0xffff) : e;
         }
-        const int off = is_b ? off_b : px * (int)r.a_stride + ch;
-        const uint16_t *ps = (is_b ? row_b : row_a) + off;
+        const uint16_t *ps = (is_b ? row_b : row_a) + (uint32_t)e;
         dma16_ring(ok ? static_cast<const void *>(ps) : static_cast<const void *>(&g_zero_piece), slot + i * 1024);
     }
 }
@@ -919,33 +925,36 @@ __device__ __forceinline__ void rows_stage(const RowArgs &r, int64_t pix0, int x
 // is one of the band's rows; its accumulator is cleared either way), then
 // stage input row j + RING into the slot just read. Rows outside the band
 // feed accumulators that are cleared or never stored.
-template <int Q, bool CMP, int U>
+template <int Q, bool CMP, bool RELU, int U>
 __device__ __forceinline__ void rows_step(const RowArgs &r, const bf16x8r (&wr)[Q][9], f32x16 (&acc)[3],
-                                          const float (*s_par)[NCO], uint8_t *s_ring, uint8_t *s_o, int64_t frame_row0,
-                                          int x0, int ya, int n_in, int n_out, int cob, int j,
-                                          const uint64_t *s_occ, const int32_t *s_first, int lane_in) {
+                                          const float (*s_par)[NCO], const uint8_t *rd, uint8_t *s_ring,
+                                          uint8_t *s_o, int64_t frame_row0, int x0, int ya, int n_in, int n_out,
+                                          int cob, int j, const uint64_t *s_occ, const int32_t *s_first,
+                                          const int (&off)[RDMA], int valid, int lane) {
     // rows j+1 .. j+RING-1 may still be in flight: RDMA DMAs each (stores in between only add to the count)
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RDMA * (RING - 1)) : "memory");
-    const int lane = lane_now(lane_in), pl = lane & 31, hf = lane >> 5;
-    const uint8_t *slot = s_ring + U * RSLOT;
     f32x16 &a0 = acc[(U + 1) % 3], &a1 = acc[U], &a2 = acc[(U + 2) % 3];
+    if (SHPL_ROWS_PRIO == 1) __builtin_amdgcn_s_setprio(1);
+    if (SHPL_ROWS_PRIO == 2) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx) {
-        const int px = pl + kx, sw = hf ^ ((px >> 1) & 7);
-        const uint8_t *prow = slot + px * 128;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            const bf16x8r xv = *reinterpret_cast<const bf16x8r *>(prow + ((sw ^ (2 * q)) << 4));
+            // rd: this lane's pixel pl, piece hf of slot 0; + slot U, kx pixels, 2 q pieces
+            const bf16x8r xv = *reinterpret_cast<const bf16x8r *>(rd + U * RSLOT + kx * 16 + 2 * q * RPIECE);
             if (SHPL_ROWS_PROBE == 2) continue;
             a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[q][kx], xv, a0, 0, 0, 0);
             a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[q][3 + kx], xv, a1, 0, 0, 0);
             a2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[q][6 + kx], xv, a2, 0, 0, 0);
         }
     }
+    if (SHPL_ROWS_PRIO == 1) __builtin_amdgcn_s_setprio(0);
+    if (SHPL_ROWS_PRIO == 2) __builtin_amdgcn_s_setprio(1);
     const int b = j - 2;  // band output row finished by this input row
     if (b >= 0 && b < n_out) {
         // epilogue: (acc - center) * scale + shift, ReLU, bf16; the lane's 4 runs of 4 channels to the
         // wave's LDS rows, then 2 x 16-byte stores per lane (consecutive lanes, consecutive pieces)
+        const int pl = lane & 31, hf = lane >> 5;
         const int y = ya + b;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -957,7 +966,7 @@ __device__ __forceinline__ void rows_step(const RowArgs &r, const bf16x8r (&wr)[
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 float v = __fadd_rn(__fmul_rn(__fsub_rn(a2[4 * g + k], cen[k]), scl[k]), sft[k]);
-                if (r.act == 1) v = v > 0.0f ? v : 0.0f;
+                if (RELU) v = __builtin_fmaxf(v, 0.0f);
                 o[k] = f32_to_bf16(v);
             }
             __builtin_memcpy(s_o + pl * REPI + cl * 2, o, sizeof(o));
@@ -979,24 +988,28 @@ __device__ __forceinline__ void rows_step(const RowArgs &r, const bf16x8r (&wr)[
     for (int i = 0; i < 16; ++i) a2[i] = 0.0f;
     // the slot's reads are done (their MFMAs consumed them): stage row j + RING into it
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (SHPL_ROWS_PROBE == 1) return;
     const int jn = j + RING, y = ya - 1 + jn;
     const bool live = jn < n_in;
     uint64_t occ = 0;
     int32_t first = 0;
-    if (SHPL_ROWS_PROBE == 1) return;
     if (CMP && live) {  // uniform LDS words (the band's halo-row windows)
         occ = s_occ[jn];
         first = s_first[jn];
     }
-    rows_stage<Q, CMP>(r, frame_row0 + (int64_t)y * r.w + x0 - 1, x0, live && y >= 0 && y < r.h, occ, first,
-                       s_ring + U * RSLOT, lane);
+    rows_stage<CMP>(r, frame_row0 + (int64_t)y * r.w + x0 - 1, live && y >= 0 && y < r.h, occ, first, off, valid,
+                    s_ring + U * RSLOT);
 }
 
-template <int Q, bool CMP>
+template <int Q, bool CMP, bool RELU>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_rows(const RowArgs r) {
     __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING * RSLOT];
     __shared__ __attribute__((aligned(16))) uint8_t s_o[32 * REPI];
     __shared__ __attribute__((aligned(16))) float s_par[3][NCO];
+    // the halo rows' occupancy windows (entry j: input row ya - 1 + j): cells x0-1 .. x0+32 as bits 0..33, and
+    // the frame-slot run index of the first of them
+    __shared__ uint64_t s_occ[CMP ? 64 : 1];
+    __shared__ int32_t s_first[CMP ? 64 : 1];
     const int lane = threadIdx.x;
     const int item = xcd_tile(blockIdx.x, r.n_items);  // (frame, band, strip), strips fastest
     const int strip = item % r.strips, fb = item / r.strips;
@@ -1012,10 +1025,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         s_par[1][lane] = r.scale ? r.scale[c] : 1.0f;
         s_par[2][lane] = r.shift ? r.shift[c] : 0.0f;
     }
-    // the halo rows' occupancy windows (entry j: input row ya - 1 + j): cells x0-1 .. x0+32 as bits 0..33, and
-    // the frame-slot run index of the first of them
-    __shared__ uint64_t s_occ[CMP ? 64 : 1];
-    __shared__ int32_t s_first[CMP ? 64 : 1];
     if constexpr (CMP) {
         const int y = ya - 1 + lane, w0 = x0 >> 5;
         uint64_t occ_row = 0;
@@ -1032,12 +1041,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         s_first[lane] = first_row;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own LDS writes, in order
     }
+    int off[RDMA], valid;
+    rows_lane_src<Q, CMP>(r, x0, lane, off, valid);
     // prologue: input rows 0 .. RING-1 in flight
 #pragma unroll
     for (int j = 0; j < RING; ++j) {
         const int y = ya - 1 + j;
-        rows_stage<Q, CMP>(r, frame_row0 + (int64_t)y * r.w + x0 - 1, x0, j < n_in && y >= 0 && y < H,
-                           CMP ? s_occ[j] : 0, CMP ? s_first[j] : 0, s_ring + j * RSLOT, lane);
+        rows_stage<CMP>(r, frame_row0 + (int64_t)y * r.w + x0 - 1, j < n_in && y >= 0 && y < H,
+                        CMP ? s_occ[j] : 0, CMP ? s_first[j] : 0, off, valid, s_ring + j * RSLOT);
     }
     // the chunk weights of all taps stay in registers: A operands (32 output x 16 input channels)
     bf16x8r wr[Q][9];
@@ -1052,15 +1063,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     for (int k = 0; k < 3; ++k)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[k][i] = 0.0f;
+    // B operand (pixels): lane (pl, hf) reads pixel pl (+ kx) of piece 2 q + hf
+    const uint8_t *rd = s_ring + (lane >> 5) * RPIECE + (lane & 31) * 16;
     for (int j = 0; j < n_in; j += RING) {
-        rows_step<Q, CMP, 0>(r, wr, acc, s_par, s_ring, s_o, frame_row0, x0, ya, n_in, n_out, cob, j, s_occ,
-                             s_first, lane);
+        rows_step<Q, CMP, RELU, 0>(r, wr, acc, s_par, rd, s_ring, s_o, frame_row0, x0, ya, n_in, n_out, cob, j, s_occ,
+                                   s_first, off, valid, lane);
         if (j + 1 >= n_in) break;
-        rows_step<Q, CMP, 1>(r, wr, acc, s_par, s_ring, s_o, frame_row0, x0, ya, n_in, n_out, cob, j + 1, s_occ,
-                             s_first, lane);
+        rows_step<Q, CMP, RELU, 1>(r, wr, acc, s_par, rd, s_ring, s_o, frame_row0, x0, ya, n_in, n_out, cob, j + 1,
+                                   s_occ, s_first, off, valid, lane);
         if (j + 2 >= n_in) break;
-        rows_step<Q, CMP, 2>(r, wr, acc, s_par, s_ring, s_o, frame_row0, x0, ya, n_in, n_out, cob, j + 2, s_occ,
-                             s_first, lane);
+        rows_step<Q, CMP, RELU, 2>(r, wr, acc, s_par, rd, s_ring, s_o, frame_row0, x0, ya, n_in, n_out, cob, j + 2,
+                                   s_occ, s_first, off, valid, lane);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing DMAs land before the wave's LDS is released
 }
@@ -1958,7 +1971,6 @@ int conv_rows_launch(const ConvPlan &pl, const ConvArgs &a, bool pooled, const i
     r.center = a.center;
     r.scale = a.scale;
     r.shift = a.shift;
-    r.act = a.act;
     r.out = reinterpret_cast<uint16_t *>(a.out);
     r.out_stride = a.out_stride;
     r.wpr = pl.wpr;
@@ -1985,18 +1997,20 @@ int conv_rows_launch(const ConvPlan &pl, const ConvArgs &a, bool pooled, const i
         r.cmp = cmp;
     }
     const dim3 grid((unsigned)r.n_items, (unsigned)pl.n_cob);
-    switch (pl.qa + pl.qb) {
-#define SHPL_ROWS_CASE(QQ)                                                       \
-    case QQ:                                                                     \
-        if (pooled)                                                              \
-            hipLaunchKernelGGL((k_conv_rows<QQ, true>), grid, dim3(64), 0, s, r);  \
-        else                                                                     \
-            hipLaunchKernelGGL((k_conv_rows<QQ, false>), grid, dim3(64), 0, s, r); \
+    const bool relu = a.act == 1;
+    switch ((pl.qa + pl.qb) * 4 + (pooled ? 2 : 0) + (relu ? 1 : 0)) {
+#define SHPL_ROWS_CASE(QQ, CMP, RELU)                                                       \
+    case QQ * 4 + (CMP ? 2 : 0) + (RELU ? 1 : 0):                                           \
+        hipLaunchKernelGGL((k_conv_rows<QQ, CMP, RELU>), grid, dim3(64), 0, s, r);            \
         break;
-        SHPL_ROWS_CASE(1)
-        SHPL_ROWS_CASE(2)
-        SHPL_ROWS_CASE(3)
-        SHPL_ROWS_CASE(4)
+#define SHPL_ROWS_CASES(QQ)                                                                 \
+    SHPL_ROWS_CASE(QQ, false, false)                                                        \
+    SHPL_ROWS_CASE(QQ, false, true) SHPL_ROWS_CASE(QQ, true, false) SHPL_ROWS_CASE(QQ, true, true)
+        SHPL_ROWS_CASES(1)
+        SHPL_ROWS_CASES(2)
+        SHPL_ROWS_CASES(3)
+        SHPL_ROWS_CASES(4)
+#undef SHPL_ROWS_CASES
 #undef SHPL_ROWS_CASE
         default:
             return SHPL_ERR_ARG;
