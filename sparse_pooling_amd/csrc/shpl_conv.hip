@@ -32,6 +32,7 @@
 // add), so the conv of the fused form is bitwise the conv of
 // [bev || shpl_pull(...)] and bv_fused never reaches HBM.
 #include "shpl_common.h"
+#include "shpl_conv_rows.h"
 
 namespace shpl {
 namespace {
@@ -676,406 +677,6 @@ __global__ __launch_bounds__(CONV_BLOCK, NCB == 2 ? 3 : 4) void k_conv3x3(const 
             p.part[((int64_t)(cob0 * NCO + c) * 2 + st) * p.n_tiles + tile] = sum;
         }
     }
-}
-
-// ---------------------------------------------------------------------------
-// Row-streaming bf16 conv (k_conv_rows): the forward for inputs of at most 64
-// channels (Q <= 4 chunks of 16), where the tiled kernel above is bound by its
-// per-tile chain of staging round trips, not by MFMA or HBM.
-//
-// One wave per workgroup walks a band of output rows of one 32-column strip
-// (and one block of 32 output channels). The chunk weights of all 9 taps sit
-// in VGPRs for the whole band (9 Q bf16x8 A operands: 144 registers at Q = 4),
-// so the LDS holds only pixels. Input row r of the halo contributes to output
-// rows r+1, r, r-1 (ky = 0, 1, 2): three f32 accumulators roll over the band,
-// and each input row is staged, read and multiplied once: 12 ds_read_b128 per
-// 36 MFMAs at Q = 4. Rows arrive by LDS-DMA into a per-wave ring of RING
-// slots, RING-1 rows ahead of the MFMAs, behind counted `s_waitcnt vmcnt` --
-// no barrier anywhere (one wave). Two waves per SIMD (8 per CU) each run
-// their own ring: one's MFMAs cover the other's waits.
-//
-// Slot layout: [piece][40 pixels] of 16 bytes (piece g = 2 chunk + half:
-// channels 16 chunk + 8 half; pixels 34..39 unused): the lanes of a
-// ds_read_b128 read 16 consecutive pixels of one piece (16 distinct bank quads,
-// no swizzle), and every pixel-operand read of a row is one base register plus
-// an immediate (kx: 16 bytes, chunk: 1280). An LDS-DMA fills 64 consecutive
-// 16-byte slots (lane k: slot 64 i + k = piece (64 i + k) / 40, pixel
-// (64 i + k) % 40); each lane's source offsets for the 5 DMAs are computed
-// once per band.
-//
-// Pooled B channels (CMP): the pooled vectors of the occupied cells, computed
-// once by k_pool_runs with shpl_pull's arithmetic into a compact buffer (one
-// row per run of the cell-keyed CSR), are gathered by the same DMAs: cell
-// (y, x) holds run  occ_base[word] + popc(occ[word] below bit x%32)  of its
-// frame (k_occ_frame), unoccupied cells read a zero piece. The conv of the
-// fused form is bitwise the conv of [bev || shpl_pull(...)] through this same
-// kernel.
-constexpr int RING = 3;                    // ring slots per wave = the row loop's unroll
-#ifndef SHPL_ROWS_PRIO
-#define SHPL_ROWS_PRIO 0  // 1: s_setprio 1 over each row's MFMAs; 2: over its epilogue and staging
-#endif
-#ifndef SHPL_ROWS_PROBE
-#define SHPL_ROWS_PROBE 0  // timing probes (wrong results): 1 no ring DMAs in the loop, 2 no MFMAs, 3 no output stores
-#endif
-constexpr int RPIX = 40;                   // pixels per piece row of a ring slot (34 used)
-constexpr int RPIECE = RPIX * 16;          // bytes per piece row
-constexpr int RSLOT = 8 * RPIECE;          // bytes per ring slot (8 pieces)
-constexpr int RDMA = RSLOT / 1024;         // LDS-DMAs per staged row
-constexpr int REPI = NCO * 2 + 16;         // epilogue transpose row pitch (bytes per pixel)
-constexpr int OCC_MAX_WORDS = 32768;       // k_occ_frame's LDS mask: up to 1M cells per frame
-
-typedef __bf16 bf16x8r __attribute__((ext_vector_type(8)));
-
-// Occupancy of the cell-keyed CSR per frame: bit x%32 of word (f, y, x/32) is
-// set when cell (y, x) of frame f has entries; occ_base[word] counts the
-// frame's occupied cells before the word (row-major). One 1024-thread
-// workgroup per frame: run heads set bits of an LDS mask, then a blocked
-// exclusive scan of popcounts; every word written once.
-__global__ __launch_bounds__(1024) void k_occ_frame(const int32_t *ent_dst, const int64_t *frame_off, int H, int W,
-                                                    int wpr, uint32_t *occ, int32_t *occ_base) {
-    __shared__ uint32_t s_mask[OCC_MAX_WORDS];
-    __shared__ int32_t s_tot[17];
-    const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int nw = H * wpr;
-    for (int i = tid; i < nw; i += 1024) s_mask[i] = 0u;
-    __syncthreads();
-    const int64_t e0 = frame_off[f], e1 = frame_off[f + 1];
-    const int64_t cell0 = (int64_t)f * H * W;
-    for (int64_t e = e0 + tid; e < e1; e += 1024) {
-        const int32_t d = ent_dst[e];
-        if (d < 0) continue;
-        if (e == e0 || ent_dst[e - 1] != d) {
-            const int c = (int)(d - cell0), y = c / W, x = c - y * W;
-            atomicOr(&s_mask[y * wpr + (x >> 5)], 1u << (x & 31));
-        }
-    }
-    __syncthreads();
-    uint32_t *om = occ + (int64_t)f * nw;
-    int32_t *ob = occ_base + (int64_t)f * nw;
-    int32_t carry = 0;
-    for (int base = 0; base < nw; base += 1024) {  // 1024 consecutive words per round: coalesced stores
-        const int i = base + tid;
-        const uint32_t m = i < nw ? s_mask[i] : 0u;
-        int32_t x = __popc(m);
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) s_tot[wave] = x;
-        __syncthreads();
-        if (tid == 0) {
-            int32_t s = 0;
-            for (int w = 0; w < 16; ++w) {
-                const int32_t t = s_tot[w];
-                s_tot[w] = s;
-                s += t;
-            }
-            s_tot[16] = s;
-        }
-        __syncthreads();
-        if (i < nw) {
-            om[i] = m;
-            ob[i] = carry + s_tot[wave] + x - __popc(m);
-        }
-        carry += s_tot[16];
-        __syncthreads();
-    }
-}
-
-// The pooled vector of every run of the cell-keyed CSR into its compact row
-// frame_off[f] + (run rank in frame f): one thread per (entry, 16-byte piece);
-// the thread on a run's first entry sums the run in entry order with separate
-// multiply and add from 0 and rounds once -- shpl_pull's (k_sparse's) and
-// pool_piece's arithmetic, bit for bit.
-__global__ __launch_bounds__(SHPL_BLOCK) void k_pool_runs(const int32_t *ent_dst, const int32_t *ent_src,
-                                                          const float *ent_val, int64_t nnz_cap, const uint16_t *img,
-                                                          int64_t img_stride, int64_t img_off, int c_b, int np,
-                                                          int H, int W, int wpr, const uint32_t *occ,
-                                                          const int32_t *occ_base, const int64_t *frame_off,
-                                                          uint16_t *cmp) {
-    const int64_t t = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x;
-    const int64_t e = t / np;
-    const int g = (int)(t - e * np);
-    if (e >= nnz_cap) return;
-    const int32_t d = ent_dst[e];
-    if (d < 0 || (e > 0 && ent_dst[e - 1] == d)) return;
-    const int64_t cells = (int64_t)H * W;
-    const int f = (int)(d / cells);
-    const int c = (int)(d - f * cells), y = c / W, x = c - y * W;
-    const int64_t wi = ((int64_t)f * H + y) * wpr + (x >> 5);
-    const int32_t rid = occ_base[wi] + __popc(occ[wi] & ((1u << (x & 31)) - 1u));
-    float sum[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sum[j] = 0.0f;
-    for (int64_t i0 = e; i0 < nnz_cap; i0 += POOL_BATCH) {
-        u32x4 raw[POOL_BATCH];
-        float wv[POOL_BATCH];
-        bool live[POOL_BATCH];
-#pragma unroll
-        for (int u = 0; u < POOL_BATCH; ++u) {
-            const int64_t i = i0 + u;
-            live[u] = i < nnz_cap && ent_dst[i] == d;
-            if (live[u]) {
-                wv[u] = ent_val[i];
-                raw[u] = *reinterpret_cast<const u32x4 *>(img + (int64_t)ent_src[i] * img_stride + img_off + g * 8);
-            }
-        }
-        bool more = true;
-#pragma unroll
-        for (int u = 0; u < POOL_BATCH; ++u) {
-            if (!live[u]) {
-                more = false;
-                break;
-            }
-            uint16_t xv[8];
-            __builtin_memcpy(xv, &raw[u], 16);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) sum[j] = __fadd_rn(sum[j], __fmul_rn(wv[u], bf16_to_f32(xv[j])));
-        }
-        if (!more) break;
-    }
-    uint16_t o[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f32_to_bf16(sum[j]);
-    *reinterpret_cast<u32x4 *>(cmp + (frame_off[f] + rid) * (int64_t)c_b + g * 8) = *reinterpret_cast<u32x4 *>(o);
-}
-
-struct RowArgs {
-    const uint16_t *a, *b;     // A / B rows (the channel offsets applied)
-    int64_t a_stride, b_stride;  // elements
-    int c_a, c_b, qa;
-    int h, w, strips, band, n_bands, n_items;
-    const uint16_t *wp;          // packed weights [co_block][chunk][tap][32][16]
-    const float *center, *scale, *shift;
-    uint16_t *out;
-    int64_t out_stride;
-    const uint32_t *occ;         // CMP: occupancy words, prefix counts, compact pooled rows, entry slots
-    const int32_t *occ_base;
-    int wpr;
-    const uint16_t *cmp;
-    const int64_t *frame_off;
-};
-
-// An LDS-DMA the compiler does not see: k_conv_rows waits for its ring slots
-// itself (counted vmcnt), while the compiler, seeing an LDS write by DMA,
-// would drain every outstanding DMA (vmcnt(0)) before each ds_read -- the
-// whole prefetch ring. M0 holds the wave's LDS destination (one wait state
-// before the DMA reads it).
-__device__ __forceinline__ void dma16_ring(const void *src, const uint8_t *wave_dst) {
-    const uint32_t lds = (uint32_t)(uintptr_t)wave_dst;
-    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(lds) : "memory");
-}
-
-// Per band, per lane and DMA i: where slot 64 i + lane's piece comes from.
-// Dense: bit 31 = B, bits 0..30 = the element offset from the row's pixel 0
-// (pixel * stride + channel). CMP B pieces: bit 31, pixel << 16 | channel.
-// valid: bit i set when the piece lies inside the map's columns and channels.
-template <int Q, bool CMP>
-__device__ __forceinline__ void rows_lane_src(const RowArgs &r, int x0, int lane, int (&off)[RDMA], int &valid) {
-    valid = 0;
-#pragma unroll
-    for (int i = 0; i < RDMA; ++i) {
-        const int sl = 64 * i + lane, g = sl / RPIX, px = sl - g * RPIX, x = x0 - 1 + px;
-        const int q = g >> 1, c8 = (g & 1) * 8;
-        const bool in_x = px < HWD && x >= 0 && x < r.w;
-        int o = 0;
-        bool ok = false;
-        if (q < r.qa) {
-            ok = q * 16 + c8 < r.c_a;
-            o = px * (int)r.a_stride + q * 16 + c8;
-        } else if (q < Q) {
-            const int c = (q - r.qa) * 16 + c8;
-            ok = c < r.c_b;
-            o = (int)(0x80000000u | (uint32_t)(CMP ? (px << 16) | c : px * (int)r.b_stride + c));
-        }
-        off[i] = o;
-        valid |= (ok && in_x ? 1 : 0) << i;
-    }
-}
-
-// Stages input row y (its pixel 0 at global pixel pix0) into a ring slot:
-// RDMA LDS-DMAs, every lane issuing (the vmcnt arithmetic counts whole
-// instructions); pieces outside the map, the channels or the band read the
-// zero piece.
-template <bool CMP>
-__device__ __forceinline__ void rows_stage(const RowArgs &r, int64_t pix0, bool yok, uint64_t occ, int32_t first,
-                                           const int (&off)[RDMA], int valid, uint8_t *slot) {
-    const uint16_t *row_a = r.a + pix0 * r.a_stride;
-    const uint16_t *row_b = CMP ? r.cmp : r.b + pix0 * r.b_stride;
-#pragma unroll
-    for (int i = 0; i < RDMA; ++i) {
-        const int o = off[i];
-        const bool is_b = o < 0;
-        bool ok = yok & (bool)((valid >> i) & 1);
-        int e = o & 0x7fffffff;
-        if constexpr (CMP) {
-            const int px = (o >> 16) & 63;
-            const int rank = first + (int)__popcll(occ & ((1ull << px) - 1));
-            ok = ok & (!is_b | (bool)((occ >> px) & 1));
-            e = is_b ? rank * r.c_b + (o & 0xffff) : e;
-        }
-        const uint16_t *ps = (is_b ? row_b : row_a) + (uint32_t)e;
-        dma16_ring(ok ? static_cast<const void *>(ps) : static_cast<const void *>(&g_zero_piece), slot + i * 1024);
-    }
-}
-
-// One staged input row j (j % RING == U) of the band: wait for its slot, 3 kx
-// x Q chunks x 3 ky MFMAs, finish output row j-2 of the band (stores when it
-// is one of the band's rows; its accumulator is cleared either way), then
-// stage input row j + RING into the slot just read. Rows outside the band
-// feed accumulators that are cleared or never stored.
-template <int Q, bool CMP, bool RELU, int U>
-__device__ __forceinline__ void rows_step(const RowArgs &r, const bf16x8r (&wr)[Q][9], f32x16 (&acc)[3],
-                                          const float (*s_par)[NCO], const uint8_t *rd, uint8_t *s_ring,
-                                          uint8_t *s_o, int64_t frame_row0, int x0, int ya, int n_in, int n_out,
-                                          int cob, int j, const uint64_t *s_occ, const int32_t *s_first,
-                                          const int (&off)[RDMA], int valid, int lane) {
-    // rows j+1 .. j+RING-1 may still be in flight: RDMA DMAs each (stores in between only add to the count)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RDMA * (RING - 1)) : "memory");
-    f32x16 &a0 = acc[(U + 1) % 3], &a1 = acc[U], &a2 = acc[(U + 2) % 3];
-    if (SHPL_ROWS_PRIO == 1) __builtin_amdgcn_s_setprio(1);
-    if (SHPL_ROWS_PRIO == 2) __builtin_amdgcn_s_setprio(0);
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            // rd: this lane's pixel pl, piece hf of slot 0; + slot U, kx pixels, 2 q pieces
-            const bf16x8r xv = *reinterpret_cast<const bf16x8r *>(rd + U * RSLOT + kx * 16 + 2 * q * RPIECE);
-            if (SHPL_ROWS_PROBE == 2) continue;
-            a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[q][kx], xv, a0, 0, 0, 0);
-            a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[q][3 + kx], xv, a1, 0, 0, 0);
-            a2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[q][6 + kx], xv, a2, 0, 0, 0);
-        }
-    }
-    if (SHPL_ROWS_PRIO == 1) __builtin_amdgcn_s_setprio(0);
-    if (SHPL_ROWS_PRIO == 2) __builtin_amdgcn_s_setprio(1);
-    const int b = j - 2;  // band output row finished by this input row
-    if (b >= 0 && b < n_out) {
-        // epilogue: (acc - center) * scale + shift, ReLU, bf16; the lane's 4 runs of 4 channels to the
-        // wave's LDS rows, then 2 x 16-byte stores per lane (consecutive lanes, consecutive pieces)
-        const int pl = lane & 31, hf = lane >> 5;
-        const int y = ya + b;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int cl = 8 * g + 4 * hf;
-            const f32x4 cen = *reinterpret_cast<const f32x4 *>(&s_par[0][cl]);
-            const f32x4 scl = *reinterpret_cast<const f32x4 *>(&s_par[1][cl]);
-            const f32x4 sft = *reinterpret_cast<const f32x4 *>(&s_par[2][cl]);
-            uint16_t o[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                float v = __fadd_rn(__fmul_rn(__fsub_rn(a2[4 * g + k], cen[k]), scl[k]), sft[k]);
-                if (RELU) v = __builtin_fmaxf(v, 0.0f);
-                o[k] = f32_to_bf16(v);
-            }
-            __builtin_memcpy(s_o + pl * REPI + cl * 2, o, sizeof(o));
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        uint16_t *orow = r.out + (frame_row0 + (int64_t)y * r.w + x0) * r.out_stride + cob * NCO;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {  // 32 pixels x 4 pieces of 8 channels
-            const int pc = lane + 64 * k, px = pc >> 2, pi = pc & 3;
-            const u32x4 v = *reinterpret_cast<const u32x4 *>(s_o + px * REPI + pi * 16);
-            if (SHPL_ROWS_PROBE == 3) {
-                asm volatile("" ::"v"(v));
-                continue;
-            }
-            if (x0 + px < r.w) *reinterpret_cast<u32x4 *>(orow + px * (int)r.out_stride + pi * 8) = v;
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) a2[i] = 0.0f;
-    // the slot's reads are done (their MFMAs consumed them): stage row j + RING into it
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (SHPL_ROWS_PROBE == 1) return;
-    const int jn = j + RING, y = ya - 1 + jn;
-    const bool live = jn < n_in;
-    uint64_t occ = 0;
-    int32_t first = 0;
-    if (CMP && live) {  // uniform LDS words (the band's halo-row windows)
-        occ = s_occ[jn];
-        first = s_first[jn];
-    }
-    rows_stage<CMP>(r, frame_row0 + (int64_t)y * r.w + x0 - 1, live && y >= 0 && y < r.h, occ, first, off, valid,
-                    s_ring + U * RSLOT);
-}
-
-template <int Q, bool CMP, bool RELU>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_rows(const RowArgs r) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING * RSLOT];
-    __shared__ __attribute__((aligned(16))) uint8_t s_o[32 * REPI];
-    __shared__ __attribute__((aligned(16))) float s_par[3][NCO];
-    // the halo rows' occupancy windows (entry j: input row ya - 1 + j): cells x0-1 .. x0+32 as bits 0..33, and
-    // the frame-slot run index of the first of them
-    __shared__ uint64_t s_occ[CMP ? 64 : 1];
-    __shared__ int32_t s_first[CMP ? 64 : 1];
-    const int lane = threadIdx.x;
-    const int item = xcd_tile(blockIdx.x, r.n_items);  // (frame, band, strip), strips fastest
-    const int strip = item % r.strips, fb = item / r.strips;
-    const int band = fb % r.n_bands, f = fb / r.n_bands;
-    const int cob = blockIdx.y;
-    const int H = r.h;
-    const int x0 = strip * TW, ya = band * r.band;
-    const int n_out = min(r.band, H - ya), n_in = n_out + 2;
-    const int64_t frame_row0 = (int64_t)f * H * r.w;
-    if (lane < NCO) {  // 0 / 1 / 0 where a coefficient is absent
-        const int c = cob * NCO + lane;
-        s_par[0][lane] = r.center ? r.center[c] : 0.0f;
-        s_par[1][lane] = r.scale ? r.scale[c] : 1.0f;
-        s_par[2][lane] = r.shift ? r.shift[c] : 0.0f;
-    }
-    if constexpr (CMP) {
-        const int y = ya - 1 + lane, w0 = x0 >> 5;
-        uint64_t occ_row = 0;
-        int32_t first_row = 0;
-        if (lane < n_in && y >= 0 && y < H) {
-            const int64_t wrow = ((int64_t)f * H + y) * r.wpr;
-            const uint32_t ml = w0 > 0 ? r.occ[wrow + w0 - 1] : 0u, mc = r.occ[wrow + w0];
-            const uint32_t mr = w0 + 1 < r.wpr ? r.occ[wrow + w0 + 1] : 0u;
-            const int32_t b = r.occ_base[wrow + (w0 > 0 ? w0 - 1 : w0)];
-            occ_row = (uint64_t)(ml >> 31) | ((uint64_t)mc << 1) | ((uint64_t)(mr & 1u) << 33);
-            first_row = (int32_t)r.frame_off[f] + b + (w0 > 0 ? __popc(ml & 0x7fffffffu) : 0);
-        }
-        s_occ[lane] = occ_row;
-        s_first[lane] = first_row;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own LDS writes, in order
-    }
-    int off[RDMA], valid;
-    rows_lane_src<Q, CMP>(r, x0, lane, off, valid);
-    // prologue: input rows 0 .. RING-1 in flight
-#pragma unroll
-    for (int j = 0; j < RING; ++j) {
-        const int y = ya - 1 + j;
-        rows_stage<CMP>(r, frame_row0 + (int64_t)y * r.w + x0 - 1, j < n_in && y >= 0 && y < H,
-                        CMP ? s_occ[j] : 0, CMP ? s_first[j] : 0, off, valid, s_ring + j * RSLOT);
-    }
-    // the chunk weights of all taps stay in registers: A operands (32 output x 16 input channels)
-    bf16x8r wr[Q][9];
-    const uint16_t *wq = r.wp + (int64_t)cob * Q * W_ROWS * 16;
-#pragma unroll
-    for (int q = 0; q < Q; ++q)
-#pragma unroll
-        for (int t = 0; t < 9; ++t)
-            wr[q][t] = *reinterpret_cast<const bf16x8r *>(wq + ((q * 9 + t) * NCO + (lane & 31)) * 16 + (lane >> 5) * 8);
-    f32x16 acc[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[k][i] = 0.0f;
-    // B operand (pixels): lane (pl, hf) reads pixel pl (+ kx) of piece 2 q + hf
-    const uint8_t *rd = s_ring + (lane >> 5) * RPIECE + (lane & 31) * 16;
-    for (int j = 0; j < n_in; j += RING) {
-        rows_step<Q, CMP, RELU, 0>(r, wr, acc, s_par, rd, s_ring, s_o, frame_row0, x0, ya, n_in, n_out, cob, j, s_occ,
-                                   s_first, off, valid, lane);
-        if (j + 1 >= n_in) break;
-        rows_step<Q, CMP, RELU, 1>(r, wr, acc, s_par, rd, s_ring, s_o, frame_row0, x0, ya, n_in, n_out, cob, j + 1,
-                                   s_occ, s_first, off, valid, lane);
-        if (j + 2 >= n_in) break;
-        rows_step<Q, CMP, RELU, 2>(r, wr, acc, s_par, rd, s_ring, s_o, frame_row0, x0, ya, n_in, n_out, cob, j + 2,
-                                   s_occ, s_first, off, valid, lane);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing DMAs land before the wave's LDS is released
 }
 
 // Packed weights: HWIO [3][3][c_a+c_b][c_out] -> [co_block][chunk][tap][32][CK],
@@ -1895,7 +1496,7 @@ struct ConvPlan {
     // occupancy words per BEV row; the pooled runs' buffers (pooled only)
     bool rows;
     int band, n_bands, wpr;
-    size_t occ_bytes, cmp_bytes;
+    size_t occ_bytes, cmp_bytes, junk_bytes;
     int64_t pool_cap;
 };
 
@@ -1932,7 +1533,8 @@ int conv_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_
     pl->part_bytes = stats ? align_up((size_t)pl->n_cob * NCO * 2 * pl->n_tiles * 8, 256) : 0;
     pl->wpr = (int)((w + 31) / 32);
     pl->rows = SHPL_CONV_ROWS && dtype == SHPL_BF16 && !stats && pl->qa + pl->qb <= 4 && c_a % 8 == 0 && c_b % 8 == 0 && h > 0 &&
-               w > 0 && (!pooled || h * pl->wpr <= OCC_MAX_WORDS);
+               w > 0 && rows::supported(pl->qa + pl->qb, pl->qa) &&
+               (!pooled || (h * pl->wpr <= rows::OCC_MAX_WORDS && pool_cap * c_b * esz < (1LL << 31)));
     pl->n_bands = (int)((h + 59) / 60);
     pl->band = (int)((h + pl->n_bands - 1) / pl->n_bands);
     if (SHPL_ROWS_BAND > 0 && SHPL_ROWS_BAND <= 62) {
@@ -1943,24 +1545,24 @@ int conv_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_
     pl->occ_bytes = pl->rows && pooled ? 2 * align_up((size_t)n_frames * h * pl->wpr * 4, 256) : 0;
     pl->pool_cap = pool_cap;
     pl->cmp_bytes = pl->rows && pooled ? align_up((size_t)pool_cap * c_b * esz, 256) : 0;
-    pl->total = pl->wp_bytes + pl->rp_bytes + pl->part_bytes + pl->occ_bytes + pl->cmp_bytes;
+    pl->junk_bytes = pl->rows ? 32 * NCO * 2 : 0;
+    pl->total = pl->wp_bytes + pl->rp_bytes + pl->part_bytes + pl->occ_bytes + pl->cmp_bytes + pl->junk_bytes;
     return SHPL_OK;
 }
 
 bool aligned16(const void *ptr) { return ((uintptr_t)ptr & 15u) == 0; }
 
-// k_conv_rows and, pooled, its two preparatory launches (occupancy words +
-// prefix counts per frame; the pooled vector of every run into the compact
-// buffer). The packed weights are already in a.wp.
+// k_conv_rows (shpl_conv_rows.hip) and, pooled, its two preparatory launches
+// (occupancy words + prefix counts per frame; the pooled vector of every run
+// into the compact buffer). The packed weights are already in a.wp.
 int conv_rows_launch(const ConvPlan &pl, const ConvArgs &a, bool pooled, const int64_t *frame_off, hipStream_t s) {
-    RowArgs r = {};
+    rows::RowArgs r = {};
     r.a = reinterpret_cast<const uint16_t *>(a.a) + a.a_off;
     r.b = reinterpret_cast<const uint16_t *>(a.b) + a.b_off;
     r.a_stride = a.a_stride;
     r.b_stride = a.b_stride;
     r.c_a = a.c_a;
     r.c_b = a.c_b;
-    r.qa = pl.qa;
     r.h = a.h;
     r.w = a.w;
     r.strips = pl.tiles_x;
@@ -1975,48 +1577,21 @@ int conv_rows_launch(const ConvPlan &pl, const ConvArgs &a, bool pooled, const i
     r.out_stride = a.out_stride;
     r.wpr = pl.wpr;
     r.frame_off = frame_off;
+    uint8_t *ws = reinterpret_cast<uint8_t *>(const_cast<void *>(a.wp)) + pl.wp_bytes + pl.rp_bytes + pl.part_bytes;
+    r.junk = reinterpret_cast<uint16_t *>(ws + pl.occ_bytes + pl.cmp_bytes);
     if (pooled) {
-        uint8_t *ws = reinterpret_cast<uint8_t *>(const_cast<void *>(a.wp)) + pl.wp_bytes + pl.rp_bytes + pl.part_bytes;
         uint32_t *occ = reinterpret_cast<uint32_t *>(ws);
         int32_t *occ_base = reinterpret_cast<int32_t *>(ws + pl.occ_bytes / 2);
         uint16_t *cmp = reinterpret_cast<uint16_t *>(ws + pl.occ_bytes);
-        hipLaunchKernelGGL(k_occ_frame, dim3(a.n_frames), dim3(1024), 0, s, a.ent_dst, frame_off, a.h, a.w, pl.wpr,
-                           occ, occ_base);
-        SHPL_LAUNCH_CHECK();
-        const int np = a.c_b / 8;
-        if (pl.pool_cap > 0 && np > 0) {
-            const int64_t threads = pl.pool_cap * np;
-            hipLaunchKernelGGL(k_pool_runs, dim3((unsigned)((threads + SHPL_BLOCK - 1) / SHPL_BLOCK)), dim3(SHPL_BLOCK),
-                               0, s, a.ent_dst, a.ent_src, a.ent_val, pl.pool_cap,
-                               reinterpret_cast<const uint16_t *>(a.b), a.b_stride, a.b_off, a.c_b, np, a.h, a.w,
-                               pl.wpr, occ, occ_base, frame_off, cmp);
-            SHPL_LAUNCH_CHECK();
-        }
+        const int rc = rows::prep_pooled(a.n_frames, a.h, a.w, pl.wpr, a.ent_dst, a.ent_src, a.ent_val, pl.pool_cap,
+                                         frame_off, reinterpret_cast<const uint16_t *>(a.b), a.b_stride, a.b_off,
+                                         a.c_b, occ, occ_base, cmp, s);
+        if (rc) return rc;
         r.occ = occ;
         r.occ_base = occ_base;
         r.cmp = cmp;
     }
-    const dim3 grid((unsigned)r.n_items, (unsigned)pl.n_cob);
-    const bool relu = a.act == 1;
-    switch ((pl.qa + pl.qb) * 4 + (pooled ? 2 : 0) + (relu ? 1 : 0)) {
-#define SHPL_ROWS_CASE(QQ, CMP, RELU)                                                       \
-    case QQ * 4 + (CMP ? 2 : 0) + (RELU ? 1 : 0):                                           \
-        hipLaunchKernelGGL((k_conv_rows<QQ, CMP, RELU>), grid, dim3(64), 0, s, r);            \
-        break;
-#define SHPL_ROWS_CASES(QQ)                                                                 \
-    SHPL_ROWS_CASE(QQ, false, false)                                                        \
-    SHPL_ROWS_CASE(QQ, false, true) SHPL_ROWS_CASE(QQ, true, false) SHPL_ROWS_CASE(QQ, true, true)
-        SHPL_ROWS_CASES(1)
-        SHPL_ROWS_CASES(2)
-        SHPL_ROWS_CASES(3)
-        SHPL_ROWS_CASES(4)
-#undef SHPL_ROWS_CASES
-#undef SHPL_ROWS_CASE
-        default:
-            return SHPL_ERR_ARG;
-    }
-    SHPL_LAUNCH_CHECK();
-    return SHPL_OK;
+    return rows::launch(r, pl.qa + pl.qb, pl.qa, pooled, a.act == 1, pl.n_cob, s);
 }
 
 template <typename T>

@@ -1,0 +1,43 @@
+// shpl_conv_rows.h -- the row-streaming bf16 conv (shpl_conv_rows.hip) as the
+// tiled conv's host code (shpl_conv.hip) launches it.
+#pragma once
+
+#include "shpl_common.h"
+
+namespace shpl {
+namespace rows {
+
+constexpr int OCC_MAX_WORDS = 32768;  // k_occ_frame's LDS mask: up to 1M cells per frame
+
+struct RowArgs {
+    const uint16_t *a, *b;       // A / B rows (the channel offsets applied)
+    int64_t a_stride, b_stride;  // elements
+    int c_a, c_b;
+    int h, w, strips, band, n_bands, n_items;
+    const uint16_t *wp;          // packed weights [co_block][chunk][tap][32][16] (k_pack_w)
+    const float *center, *scale, *shift;
+    uint16_t *out;
+    int64_t out_stride;
+    const uint32_t *occ;         // CMP: occupancy words, their prefix counts, compact pooled rows, entry slots
+    const int32_t *occ_base;
+    int wpr;
+    const uint16_t *cmp;
+    const int64_t *frame_off;
+    uint16_t *junk;              // 32 x 32 channels: stores of rows / pixels outside the map land here
+};
+
+// k_conv_rows has an instantiation for q chunks of which qa come from A.
+bool supported(int q, int qa);
+
+// Occupancy words + prefix counts of the cell-keyed CSR per frame, then the
+// pooled vector of every run into its compact row (shpl_pull's arithmetic).
+int prep_pooled(int n_frames, int h, int w, int wpr, const int32_t *ent_dst, const int32_t *ent_src,
+                const float *ent_val, int64_t nnz_cap, const int64_t *frame_off, const uint16_t *img,
+                int64_t img_stride, int64_t img_off, int c_b, uint32_t *occ, int32_t *occ_base, uint16_t *cmp,
+                hipStream_t s);
+
+// The conv: grid (n_items, n_cob) of one-wave workgroups.
+int launch(const RowArgs &r, int q, int qa, bool cmp, bool relu, int n_cob, hipStream_t s);
+
+}  // namespace rows
+}  // namespace shpl

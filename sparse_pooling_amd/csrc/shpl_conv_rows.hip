@@ -1,0 +1,479 @@
+// shpl_conv_rows.hip -- the row-streaming bf16 3x3 conv (k_conv_rows): the
+// forward of shpl_conv3x3 (avod/avod/core/models/
+// rpn_model.py:338-346) for bf16 inputs of at most 64 channels, where the
+// tiled kernel of shpl_conv.hip is bound by its per-tile chain of staging
+// round trips, not by MFMA or HBM.
+//
+// One wave per workgroup walks a band of output rows of one 32-column strip
+// (and one block of 32 output channels). The chunk weights of all 9 taps sit
+// in VGPRs for the whole band (9 Q bf16x8 A operands: 144 registers at Q =
+// 4), so the LDS holds only pixels. Input row r of the halo contributes to
+// output rows r+1, r, r-1 (ky = 0, 1, 2): three f32 accumulators roll over the
+// band, and each input row is staged, read and multiplied once: 12
+// ds_read_b128 per 36 MFMAs at Q = 4. Rows arrive by LDS-DMA into a per-wave
+// ring of RING slots, RING-1 rows ahead of the MFMAs, behind counted
+// `s_waitcnt vmcnt` -- no barrier anywhere (one wave). Two waves per SIMD (8
+// per CU) each run their own ring.
+//
+// The loop is vector-issue-bound before it is MFMA-bound (an MFMA holds the
+// SIMD's vector issue for 8 of its 32 cycles, a VALU op for 4, an LDS-DMA for
+// ~60), so the staging does no per-row address arithmetic for dense sources:
+// each row is one uniform buffer descriptor (its base pointer; num_records 0
+// for rows outside the map) and every lane's 32-bit offset into it is fixed for
+// the band; pieces outside the map or the channels carry an offset past
+// num_records and read as zeros.
+//
+// Slot layout: A pieces (g = 2 chunk + half: channels 16 chunk + 8 half) as
+// [g][34 pixels] of 16 bytes from slot 0, B pieces likewise from slot RB (the
+// next multiple of 64 slots), so that every DMA (64 consecutive slots) reads
+// one tensor. The lanes of a ds_read_b128 read 16 consecutive pixels of one
+// piece (16 distinct bank quads), and every pixel-operand read of a row is one
+// base register plus an immediate. After a row's MFMAs its slot holds the
+// epilogue's transpose until the next DMA into it.
+//
+// Pooled B channels (CMP): the pooled vectors of the occupied cells, computed
+// once by k_pool_runs with shpl_pull's arithmetic into a compact buffer (one
+// row per run of the cell-keyed CSR), are gathered by the B DMAs: cell (y, x)
+// holds run  occ_base[word] + popc(occ[word] below bit x%32)  of its frame
+// (k_occ_frame), unoccupied cells read zeros. The conv of the fused form is
+// bitwise the conv of [bev || shpl_pull(...)] through this same kernel.
+#include "shpl_conv_rows.h"
+
+namespace shpl {
+namespace rows {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int NCO = 32;           // output channels per wave
+constexpr int TW = 32;            // strip width (output pixels)
+constexpr int HWD = TW + 2;       // halo row (pixels)
+constexpr int W_ROWS = 9 * NCO;   // packed weight rows of a chunk
+constexpr int RING = 3;           // ring slots per wave = the row loop's unroll (accumulator roles)
+constexpr int REPI = NCO * 2 + 16;  // epilogue transpose pitch (bytes per pixel)
+constexpr int RSTORES = 2;        // output stores per row step, always issued (the vmcnt arithmetic)
+constexpr uint32_t OOB = 0x80000000u;  // an offset past every descriptor's num_records: reads zeros
+constexpr int POOL_BATCH = 4;     // k_pool_runs: entries' loads in flight per round trip
+
+template <int Q, int QA>
+struct Layout {
+    static constexpr int QB = Q - QA;
+    static constexpr int NA = (2 * QA * HWD + 63) / 64;  // A DMAs (the last one: TA lanes)
+    static constexpr int TA = 2 * QA * HWD - 64 * (NA - 1);
+    static constexpr int RB = 64 * NA;                   // first B slot
+    static constexpr int NB = (2 * QB * HWD + 63) / 64;
+    static constexpr int TB = QB ? 2 * QB * HWD - 64 * (NB - 1) : 0;
+    static constexpr int NDMA = NA + NB;
+    static constexpr int DATA = (QB ? RB + 2 * QB * HWD : 2 * QA * HWD) * 16;  // bytes of pieces
+    static constexpr int SLOT = DATA > 32 * REPI ? DATA : 32 * REPI;  // also the epilogue's transpose
+};
+
+// Occupancy of the cell-keyed CSR per frame: bit x%32 of word (f, y, x/32) is
+// set when cell (y, x) of frame f has entries; occ_base[word] counts the
+// frame's occupied cells before the word (row-major). One 1024-thread
+// workgroup per frame: run heads set bits of an LDS mask, then a blocked
+// exclusive scan of popcounts; every word written once.
+__global__ __launch_bounds__(1024) void k_occ_frame(const int32_t *ent_dst, const int64_t *frame_off, int H, int W,
+                                                    int wpr, uint32_t *occ, int32_t *occ_base) {
+    __shared__ uint32_t s_mask[OCC_MAX_WORDS];
+    __shared__ int32_t s_tot[17];
+    const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nw = H * wpr;
+    for (int i = tid; i < nw; i += 1024) s_mask[i] = 0u;
+    __syncthreads();
+    const int64_t e0 = frame_off[f], e1 = frame_off[f + 1];
+    const int64_t cell0 = (int64_t)f * H * W;
+    for (int64_t e = e0 + tid; e < e1; e += 1024) {
+        const int32_t d = ent_dst[e];
+        if (d < 0) continue;
+        if (e == e0 || ent_dst[e - 1] != d) {
+            const int c = (int)(d - cell0), y = c / W, x = c - y * W;
+            atomicOr(&s_mask[y * wpr + (x >> 5)], 1u << (x & 31));
+        }
+    }
+    __syncthreads();
+    uint32_t *om = occ + (int64_t)f * nw;
+    int32_t *ob = occ_base + (int64_t)f * nw;
+    int32_t carry = 0;
+    for (int base = 0; base < nw; base += 1024) {  // 1024 consecutive words per round: coalesced stores
+        const int i = base + tid;
+        const uint32_t m = i < nw ? s_mask[i] : 0u;
+        int32_t x = __popc(m);
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_tot[wave] = x;
+        __syncthreads();
+        if (tid == 0) {
+            int32_t sum = 0;
+            for (int w = 0; w < 16; ++w) {
+                const int32_t t = s_tot[w];
+                s_tot[w] = sum;
+                sum += t;
+            }
+            s_tot[16] = sum;
+        }
+        __syncthreads();
+        if (i < nw) {
+            om[i] = m;
+            ob[i] = carry + s_tot[wave] + x - __popc(m);
+        }
+        carry += s_tot[16];
+        __syncthreads();
+    }
+}
+
+// The pooled vector of every run of the cell-keyed CSR into its compact row
+// frame_off[f] + (run rank in frame f): one thread per (entry, 16-byte piece);
+// the thread on a run's first entry sums the run in entry order with separate
+// multiply and add from 0 and rounds once -- shpl_pull's (k_sparse's)
+// arithmetic, bit for bit.
+__global__ __launch_bounds__(SHPL_BLOCK) void k_pool_runs(const int32_t *ent_dst, const int32_t *ent_src,
+                                                          const float *ent_val, int64_t nnz_cap, const uint16_t *img,
+                                                          int64_t img_stride, int64_t img_off, int c_b, int np,
+                                                          int H, int W, int wpr, const uint32_t *occ,
+                                                          const int32_t *occ_base, const int64_t *frame_off,
+                                                          uint16_t *cmp) {
+    const int64_t t = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x;
+    const int64_t e = t / np;
+    const int g = (int)(t - e * np);
+    if (e >= nnz_cap) return;
+    const int32_t d = ent_dst[e];
+    if (d < 0 || (e > 0 && ent_dst[e - 1] == d)) return;
+    const int64_t cells = (int64_t)H * W;
+    const int f = (int)(d / cells);
+    const int c = (int)(d - f * cells), y = c / W, x = c - y * W;
+    const int64_t wi = ((int64_t)f * H + y) * wpr + (x >> 5);
+    const int32_t rid = occ_base[wi] + __popc(occ[wi] & ((1u << (x & 31)) - 1u));
+    float sum[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sum[j] = 0.0f;
+    for (int64_t i0 = e; i0 < nnz_cap; i0 += POOL_BATCH) {
+        u32x4 raw[POOL_BATCH];
+        float wv[POOL_BATCH];
+        bool live[POOL_BATCH];
+#pragma unroll
+        for (int u = 0; u < POOL_BATCH; ++u) {
+            const int64_t i = i0 + u;
+            live[u] = i < nnz_cap && ent_dst[i] == d;
+            if (live[u]) {
+                wv[u] = ent_val[i];
+                raw[u] = *reinterpret_cast<const u32x4 *>(img + (int64_t)ent_src[i] * img_stride + img_off + g * 8);
+            }
+        }
+        bool more = true;
+#pragma unroll
+        for (int u = 0; u < POOL_BATCH; ++u) {
+            if (!live[u]) {
+                more = false;
+                break;
+            }
+            uint16_t xv[8];
+            __builtin_memcpy(xv, &raw[u], 16);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sum[j] = __fadd_rn(sum[j], __fmul_rn(wv[u], bf16_to_f32(xv[j])));
+        }
+        if (!more) break;
+    }
+    uint16_t o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f32_to_bf16(sum[j]);
+    *reinterpret_cast<u32x4 *>(cmp + (frame_off[f] + rid) * (int64_t)c_b + g * 8) = *reinterpret_cast<u32x4 *>(o);
+}
+
+// A raw buffer descriptor (gfx9: dword 3 = 0x00020000) over `bytes` bytes from `base`.
+__device__ __forceinline__ i32x4 rsrc(const void *base, uint32_t bytes) {
+    const uint64_t b = (uint64_t)base;
+    return i32x4{(int32_t)(uint32_t)b, (int32_t)((b >> 32) & 0xffffu), (int32_t)bytes, 0x00020000};
+}
+
+// One LDS-DMA of 16 bytes per lane from buffer offset voff (lane k's piece
+// lands at wave_dst + 16 k), hidden from the compiler: the kernel waits for
+// its ring slots itself (counted vmcnt), while the compiler, seeing an LDS
+// write by DMA, would drain every outstanding DMA (vmcnt(0)) before each
+// ds_read -- the whole prefetch ring. M0 holds the LDS destination (one wait
+// state before the DMA reads it).
+__device__ __forceinline__ void dma16(i32x4 rs, uint32_t voff, const uint8_t *wave_dst) {
+    const uint32_t lds = (uint32_t)(uintptr_t)wave_dst;
+    asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "{m0}"(lds) : "memory");
+}
+
+// Per band, per lane: the byte offset of the lane's piece in each DMA's row
+// (dense), or for pooled B pieces pixel << 16 | channel (-1: outside).
+template <int Q, int QA, bool CMP>
+__device__ __forceinline__ void lane_offsets(const RowArgs &r, int x0, int lane, uint32_t (&offa)[Layout<Q, QA>::NA],
+                                             int32_t (&offb)[Layout<Q, QA>::NB > 0 ? Layout<Q, QA>::NB : 1]) {
+    typedef Layout<Q, QA> L;
+#pragma unroll
+    for (int i = 0; i < L::NA; ++i) {
+        const int sl = 64 * i + lane, g = sl / HWD, px = sl - g * HWD, x = x0 - 1 + px;
+        const int ch = (g >> 1) * 16 + (g & 1) * 8;
+        const bool ok = sl < 2 * QA * HWD && x >= 0 && x < r.w && ch < r.c_a;
+        offa[i] = ok ? (uint32_t)((px * (int)r.a_stride + ch) * 2) : OOB;
+    }
+#pragma unroll
+    for (int i = 0; i < L::NB; ++i) {
+        const int sl = 64 * i + lane, g = sl / HWD, px = sl - g * HWD, x = x0 - 1 + px;
+        const int ch = (g >> 1) * 16 + (g & 1) * 8;
+        const bool ok = sl < 2 * L::QB * HWD && x >= 0 && x < r.w && ch < r.c_b;
+        if constexpr (CMP)
+            offb[i] = ok ? (px << 16) | ch : -1;
+        else
+            offb[i] = ok ? (int32_t)((px * (int)r.b_stride + ch) * 2) : (int32_t)OOB;
+    }
+}
+
+// Stages input row y (its pixel 0 at global pixel pix0) into a ring slot:
+// NDMA LDS-DMAs, always issued (the vmcnt arithmetic counts instructions).
+template <int Q, int QA, bool CMP>
+__device__ __forceinline__ void stage(const RowArgs &r, int64_t pix0, bool yok, uint64_t occ, int32_t first,
+                                      const uint32_t (&offa)[Layout<Q, QA>::NA],
+                                      const int32_t (&offb)[Layout<Q, QA>::NB > 0 ? Layout<Q, QA>::NB : 1],
+                                      uint8_t *slot, int lane) {
+    typedef Layout<Q, QA> L;
+    const uint32_t nrec = yok ? OOB : 0u;
+    const i32x4 ra = rsrc(r.a + pix0 * r.a_stride, nrec);
+#pragma unroll
+    for (int i = 0; i < L::NA; ++i)
+        if (i < L::NA - 1 || lane < L::TA) dma16(ra, offa[i], slot + i * 1024);
+    if constexpr (L::QB > 0) {
+        const i32x4 rb = CMP ? rsrc(r.cmp, nrec) : rsrc(r.b + pix0 * r.b_stride, nrec);
+#pragma unroll
+        for (int i = 0; i < L::NB; ++i) {
+            uint32_t o = (uint32_t)offb[i];
+            if constexpr (CMP) {
+                const int px = (offb[i] >> 16) & 63;
+                const bool hit = offb[i] >= 0 && ((occ >> px) & 1);
+                const int rank = first + (int)__popcll(occ & ((1ull << px) - 1));
+                o = hit ? (uint32_t)((rank * r.c_b + (offb[i] & 0xffff)) * 2) : OOB;
+            }
+            if (i < L::NB - 1 || lane < L::TB) dma16(rb, o, slot + (L::RB + 64 * i) * 16);
+        }
+    }
+}
+
+// One staged input row j (j % RING == U: its slot and the accumulators'
+// roles) of the band: wait for its slot, 3 kx x Q chunks x 3 ky MFMAs, the
+// epilogue of output row j-2 of the band (always stored: rows and pixels
+// outside the map go to the junk line; its accumulator is cleared), then
+// stage input row j + RING into the slot just read.
+template <int Q, int QA, bool CMP, bool RELU, int U>
+__device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9], f32x16 (&acc)[3],
+                                     const float (*s_par)[NCO], const uint8_t *rd, uint8_t *s_ring,
+                                     int64_t frame_row0, int x0, int ya, int n_in, int n_out, int cob, int j,
+                                     const uint64_t *s_occ, const int32_t *s_first,
+                                     const uint32_t (&offa)[Layout<Q, QA>::NA],
+                                     const int32_t (&offb)[Layout<Q, QA>::NB > 0 ? Layout<Q, QA>::NB : 1],
+                                     int lane) {
+    typedef Layout<Q, QA> L;
+    // rows j+1 .. j+RING-1 may still be in flight: per later step RSTORES stores and NDMA DMAs
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L::NDMA + RSTORES) * (RING - 1)) : "memory");
+    f32x16 &a0 = acc[(U + 1) % 3], &a1 = acc[U], &a2 = acc[(U + 2) % 3];
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int off = U * L::SLOT + kx * 16 + (q < QA ? 2 * q * HWD * 16 : (L::RB + 2 * (q - QA) * HWD) * 16);
+            const bf16x8 xv = *reinterpret_cast<const bf16x8 *>(rd + off);
+            a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[q][kx], xv, a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[q][3 + kx], xv, a1, 0, 0, 0);
+            a2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[q][6 + kx], xv, a2, 0, 0, 0);
+        }
+    }
+    // epilogue of band output row b: acc * scale + (shift - center * scale), ReLU on the bf16 pairs;
+    // the lane's 4 runs of 4 channels to rows of the slot just read, then 2 x 16-byte stores per lane
+    // (consecutive lanes, consecutive pieces)
+    const int b = j - 2;
+    uint8_t *s_o = s_ring + U * L::SLOT;
+    const int pl = lane & 31, hf = lane >> 5;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the MFMAs' operand reads of the slot are done
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int cl = 8 * g + 4 * hf;
+        uint32_t pk[2];
+#pragma unroll
+        for (int k = 0; k < 4; k += 2) {
+            const float v0 = __builtin_fmaf(a2[4 * g + k], s_par[0][cl + k], s_par[1][cl + k]);
+            const float v1 = __builtin_fmaf(a2[4 * g + k + 1], s_par[0][cl + k + 1], s_par[1][cl + k + 1]);
+            uint32_t w = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
+            if (RELU) {  // max(x, 0) on bf16 bit patterns as signed 16-bit integers (negatives and -0 -> +0)
+                s16x2 h;
+                __builtin_memcpy(&h, &w, 4);
+                h = __builtin_elementwise_max(h, s16x2{0, 0});
+                __builtin_memcpy(&w, &h, 4);
+            }
+            pk[k >> 1] = w;
+        }
+        __builtin_memcpy(s_o + pl * REPI + cl * 2, pk, sizeof(pk));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const bool row_ok = b >= 0 && b < n_out;
+    uint16_t *orow = r.out + (frame_row0 + (int64_t)(ya + b) * r.w + x0) * r.out_stride + cob * NCO;
+#pragma unroll
+    for (int k = 0; k < RSTORES; ++k) {  // 32 pixels x 4 pieces of 8 channels
+        const int pc = lane + 64 * k, px = pc >> 2, pi = pc & 3;
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(s_o + px * REPI + pi * 16);
+        uint16_t *dst = row_ok && x0 + px < r.w ? orow + px * (int)r.out_stride + pi * 8 : r.junk + pc * 8;
+        *reinterpret_cast<u32x4 *>(dst) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) a2[i] = 0.0f;
+    // stage row j + RING into the slot (the transpose's reads of it are done first)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int jn = j + RING, y = ya - 1 + jn;
+    const bool live = jn < n_in;
+    uint64_t occ = 0;
+    int32_t first = 0;
+    if (CMP && live) {  // uniform LDS words (the band's halo-row windows)
+        occ = s_occ[jn];
+        first = s_first[jn];
+    }
+    stage<Q, QA, CMP>(r, frame_row0 + (int64_t)y * r.w + x0 - 1, live && y >= 0 && y < r.h, occ, first, offa, offb,
+                      s_ring + U * L::SLOT, lane);
+}
+
+template <int Q, int QA, bool CMP, bool RELU>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_rows(const RowArgs r) {
+    typedef Layout<Q, QA> L;
+    __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING * L::SLOT];
+    __shared__ __attribute__((aligned(16))) float s_par[2][NCO];
+    // the halo rows' occupancy windows (entry j: input row ya - 1 + j): cells x0-1 .. x0+32 as bits 0..33, and
+    // the frame-slot run index of the first of them
+    __shared__ uint64_t s_occ[CMP ? 64 : 1];
+    __shared__ int32_t s_first[CMP ? 64 : 1];
+    const int lane = threadIdx.x;
+    const int item = blockIdx.x;  // (frame, band, strip), strips fastest
+    const int strip = item % r.strips, fb = item / r.strips;
+    const int band = fb % r.n_bands, f = fb / r.n_bands;
+    const int cob = blockIdx.y;
+    const int H = r.h;
+    const int x0 = strip * TW, ya = band * r.band;
+    const int n_out = min(r.band, H - ya), n_in = n_out + 2;
+    const int64_t frame_row0 = (int64_t)f * H * r.w;
+    if (lane < NCO) {  // scale (1 when absent) and shift - center * scale
+        const int c = cob * NCO + lane;
+        const float sc = r.scale ? r.scale[c] : 1.0f;
+        const float ce = r.center ? r.center[c] : 0.0f;
+        const float sh = r.shift ? r.shift[c] : 0.0f;
+        s_par[0][lane] = sc;
+        s_par[1][lane] = __fsub_rn(sh, __fmul_rn(ce, sc));
+    }
+    if constexpr (CMP) {
+        const int y = ya - 1 + lane, w0 = x0 >> 5;
+        uint64_t occ_row = 0;
+        int32_t first_row = 0;
+        if (lane < n_in && y >= 0 && y < H) {
+            const int64_t wrow = ((int64_t)f * H + y) * r.wpr;
+            const uint32_t ml = w0 > 0 ? r.occ[wrow + w0 - 1] : 0u, mc = r.occ[wrow + w0];
+            const uint32_t mr = w0 + 1 < r.wpr ? r.occ[wrow + w0 + 1] : 0u;
+            const int32_t bs = r.occ_base[wrow + (w0 > 0 ? w0 - 1 : w0)];
+            occ_row = (uint64_t)(ml >> 31) | ((uint64_t)mc << 1) | ((uint64_t)(mr & 1u) << 33);
+            first_row = (int32_t)r.frame_off[f] + bs + (w0 > 0 ? __popc(ml & 0x7fffffffu) : 0);
+        }
+        s_occ[lane] = occ_row;
+        s_first[lane] = first_row;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own LDS writes, in order
+    }
+    uint32_t offa[L::NA];
+    int32_t offb[L::NB > 0 ? L::NB : 1];
+    lane_offsets<Q, QA, CMP>(r, x0, lane, offa, offb);
+    // prologue: input rows 0 .. RING-1 in flight
+#pragma unroll
+    for (int j = 0; j < RING; ++j) {
+        const int y = ya - 1 + j;
+        stage<Q, QA, CMP>(r, frame_row0 + (int64_t)y * r.w + x0 - 1, j < n_in && y >= 0 && y < H, CMP ? s_occ[j] : 0,
+                          CMP ? s_first[j] : 0, offa, offb, s_ring + j * L::SLOT, lane);
+    }
+    // the chunk weights of all taps stay in registers: A operands (32 output x 16 input channels)
+    bf16x8 wr[Q][9];
+    const uint16_t *wq = r.wp + (int64_t)cob * Q * W_ROWS * 16;
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+            wr[q][t] = *reinterpret_cast<const bf16x8 *>(wq + ((q * 9 + t) * NCO + (lane & 31)) * 16 + (lane >> 5) * 8);
+    f32x16 acc[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[k][i] = 0.0f;
+    // B operand (pixels): lane (pl, hf) reads pixel pl (+ kx) of piece 2 q + hf
+    const uint8_t *rd = s_ring + (lane >> 5) * HWD * 16 + (lane & 31) * 16;
+    for (int j = 0; j < n_in; j += RING) {
+#define SHPL_ROWS_STEP(UU)                                                                                          \
+    if (j + UU >= n_in) break;                                                                                      \
+    step<Q, QA, CMP, RELU, UU>(r, wr, acc, s_par, rd, s_ring, frame_row0, x0, ya, n_in, n_out, cob, j + UU, s_occ, \
+                               s_first, offa, offb, lane);
+        SHPL_ROWS_STEP(0)
+        SHPL_ROWS_STEP(1)
+        SHPL_ROWS_STEP(2)
+#undef SHPL_ROWS_STEP
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing DMAs land before the wave's LDS is released
+}
+
+}  // namespace
+
+bool supported(int q, int qa) {
+    if (q < 1 || q > 4 || qa < 1 || qa > q) return false;
+    return qa == q || q - qa >= 1;
+}
+
+int prep_pooled(int n_frames, int h, int w, int wpr, const int32_t *ent_dst, const int32_t *ent_src,
+                const float *ent_val, int64_t nnz_cap, const int64_t *frame_off, const uint16_t *img,
+                int64_t img_stride, int64_t img_off, int c_b, uint32_t *occ, int32_t *occ_base, uint16_t *cmp,
+                hipStream_t s) {
+    hipLaunchKernelGGL(k_occ_frame, dim3(n_frames), dim3(1024), 0, s, ent_dst, frame_off, h, w, wpr, occ, occ_base);
+    SHPL_LAUNCH_CHECK();
+    const int np = c_b / 8;
+    if (nnz_cap > 0 && np > 0) {
+        const int64_t threads = nnz_cap * np;
+        hipLaunchKernelGGL(k_pool_runs, dim3((unsigned)((threads + SHPL_BLOCK - 1) / SHPL_BLOCK)), dim3(SHPL_BLOCK),
+                           0, s, ent_dst, ent_src, ent_val, nnz_cap, img, img_stride, img_off, c_b, np, h, w, wpr, occ,
+                           occ_base, frame_off, cmp);
+        SHPL_LAUNCH_CHECK();
+    }
+    return SHPL_OK;
+}
+
+int launch(const RowArgs &r, int q, int qa, bool cmp, bool relu, int n_cob, hipStream_t s) {
+    if (!supported(q, qa) || (cmp && qa == q)) return SHPL_ERR_ARG;
+    const dim3 grid((unsigned)r.n_items, (unsigned)n_cob);
+    const int key = ((q * 8 + qa) * 2 + (cmp ? 1 : 0)) * 2 + (relu ? 1 : 0);
+    switch (key) {
+#define SHPL_ROWS_CASE(QQ, QQA, CMP, RELU)                                              \
+    case ((QQ * 8 + QQA) * 2 + CMP) * 2 + RELU:                                         \
+        hipLaunchKernelGGL((k_conv_rows<QQ, QQA, CMP, RELU>), grid, dim3(64), 0, s, r); \
+        break;
+#define SHPL_ROWS_DENSE(QQ) SHPL_ROWS_CASE(QQ, QQ, 0, 0) SHPL_ROWS_CASE(QQ, QQ, 0, 1)
+#define SHPL_ROWS_TWO(QQ, QQA)                                                                        \
+    SHPL_ROWS_CASE(QQ, QQA, 0, 0)                                                                    \
+    SHPL_ROWS_CASE(QQ, QQA, 0, 1) SHPL_ROWS_CASE(QQ, QQA, 1, 0) SHPL_ROWS_CASE(QQ, QQA, 1, 1)
+        SHPL_ROWS_DENSE(1)
+        SHPL_ROWS_DENSE(2)
+        SHPL_ROWS_DENSE(3)
+        SHPL_ROWS_DENSE(4)
+        SHPL_ROWS_TWO(2, 1)
+        SHPL_ROWS_TWO(3, 1)
+        SHPL_ROWS_TWO(3, 2)
+        SHPL_ROWS_TWO(4, 1)
+        SHPL_ROWS_TWO(4, 2)
+        SHPL_ROWS_TWO(4, 3)
+#undef SHPL_ROWS_TWO
+#undef SHPL_ROWS_DENSE
+#undef SHPL_ROWS_CASE
+        default:
+            return SHPL_ERR_ARG;
+    }
+    SHPL_LAUNCH_CHECK();
+    return SHPL_OK;
+}
+
+}  // namespace rows
+}  // namespace shpl
