@@ -267,7 +267,7 @@ template <int Q, int QA, bool CMP, bool RELU, int U>
 __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9], f32x16 (&acc)[3],
                                      const float (*s_par)[NCO], const uint8_t *rd, uint8_t *s_ring,
                                      int64_t frame_row0, int x0, int ya, int n_in, int n_out, int cob, int j,
-                                     const uint64_t *s_occ, const int32_t *s_first,
+                                     const uint64_t *s_occ, const int32_t *s_first, uint64_t b_rows,
                                      const uint32_t (&offa)[Layout<Q, QA>::NA],
                                      const int32_t (&offb)[Layout<Q, QA>::NB > 0 ? Layout<Q, QA>::NB : 1],
                                      int lane) {
@@ -275,15 +275,31 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
     // rows j+1 .. j+RING-1 may still be in flight: per later step RSTORES stores and NDMA DMAs
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L::NDMA + RSTORES) * (RING - 1)) : "memory");
     f32x16 &a0 = acc[(U + 1) % 3], &a1 = acc[U], &a2 = acc[(U + 2) % 3];
+    // chunk-major (q outer): a split of the channels between A and B, and the skipped pooled chunks below,
+    // leave every accumulator's summation order unchanged
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
+    for (int q = 0; q < QA; ++q) {
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const int off = U * L::SLOT + kx * 16 + (q < QA ? 2 * q * HWD * 16 : (L::RB + 2 * (q - QA) * HWD) * 16);
-            const bf16x8 xv = *reinterpret_cast<const bf16x8 *>(rd + off);
+        for (int kx = 0; kx < 3; ++kx) {
+            const bf16x8 xv = *reinterpret_cast<const bf16x8 *>(rd + U * L::SLOT + kx * 16 + 2 * q * HWD * 16);
             a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[q][kx], xv, a0, 0, 0, 0);
             a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[q][3 + kx], xv, a1, 0, 0, 0);
             a2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[q][6 + kx], xv, a2, 0, 0, 0);
+        }
+    }
+    // pooled rows without an occupied cell in the window are all zeros: their MFMAs would add exact zeros
+    // to accumulators that are never -0, so skipping them is bitwise the same
+    if (L::QB > 0 && (!CMP || ((b_rows >> j) & 1))) {
+#pragma unroll
+        for (int q = QA; q < Q; ++q) {
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                const bf16x8 xv = *reinterpret_cast<const bf16x8 *>(rd + U * L::SLOT + kx * 16 +
+                                                                    (L::RB + 2 * (q - QA) * HWD) * 16);
+                a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[q][kx], xv, a0, 0, 0, 0);
+                a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[q][3 + kx], xv, a1, 0, 0, 0);
+                a2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[q][6 + kx], xv, a2, 0, 0, 0);
+            }
         }
     }
     // epilogue of band output row b: acc * scale + (shift - center * scale), ReLU on the bf16 pairs;
@@ -364,6 +380,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         s_par[0][lane] = sc;
         s_par[1][lane] = __fsub_rn(sh, __fmul_rn(ce, sc));
     }
+    uint64_t b_rows = ~0ull;
     if constexpr (CMP) {
         const int y = ya - 1 + lane, w0 = x0 >> 5;
         uint64_t occ_row = 0;
@@ -378,6 +395,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         }
         s_occ[lane] = occ_row;
         s_first[lane] = first_row;
+        b_rows = __ballot(occ_row != 0);  // input rows with an occupied cell in their window
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own LDS writes, in order
     }
     uint32_t offa[L::NA];
@@ -409,7 +427,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #define SHPL_ROWS_STEP(UU)                                                                                          \
     if (j + UU >= n_in) break;                                                                                      \
     step<Q, QA, CMP, RELU, UU>(r, wr, acc, s_par, rd, s_ring, frame_row0, x0, ya, n_in, n_out, cob, j + UU, s_occ, \
-                               s_first, offa, offb, lane);
+                               s_first, b_rows, offa, offb, lane);
         SHPL_ROWS_STEP(0)
         SHPL_ROWS_STEP(1)
         SHPL_ROWS_STEP(2)
