@@ -7,7 +7,7 @@
 namespace shpl {
 namespace rows {
 
-constexpr int OCC_MAX_WORDS = 32768;  // k_occ_frame's LDS mask: up to 1M cells per frame
+constexpr int OCC_MAX_WORDS = 18432;  // k_occ_frame's LDS mask and prefixes: up to 589,824 cells per frame
 
 struct RowArgs {
     const uint16_t *a, *b;       // A / B rows (the channel offsets applied)

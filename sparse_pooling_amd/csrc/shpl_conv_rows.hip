@@ -57,7 +57,6 @@ constexpr int RING = 3;           // ring slots per wave = the row loop's unroll
 constexpr int REPI = NCO * 2 + 16;  // epilogue transpose pitch (bytes per pixel)
 constexpr int RSTORES = 2;        // output stores per row step, always issued (the vmcnt arithmetic)
 constexpr uint32_t OOB = 0x80000000u;  // an offset past every descriptor's num_records: reads zeros
-constexpr int POOL_BATCH = 4;     // k_pool_runs: entries' loads in flight per round trip
 
 template <int Q, int QA>
 struct Layout {
@@ -75,11 +74,13 @@ struct Layout {
 // Occupancy of the cell-keyed CSR per frame: bit x%32 of word (f, y, x/32) is
 // set when cell (y, x) of frame f has entries; occ_base[word] counts the
 // frame's occupied cells before the word (row-major). One 1024-thread
-// workgroup per frame: run heads set bits of an LDS mask, then a blocked
-// exclusive scan of popcounts; every word written once.
+// workgroup per frame: run heads set bits of an LDS mask; each thread sums
+// the popcounts of a contiguous run of words, one block scan, the prefixes
+// written back to LDS beside the mask, then both copied out coalesced.
 __global__ __launch_bounds__(1024) void k_occ_frame(const int32_t *ent_dst, const int64_t *frame_off, int H, int W,
                                                     int wpr, uint32_t *occ, int32_t *occ_base) {
     __shared__ uint32_t s_mask[OCC_MAX_WORDS];
+    __shared__ int32_t s_base[OCC_MAX_WORDS];
     __shared__ int32_t s_tot[17];
     const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nw = H * wpr;
@@ -96,53 +97,52 @@ __global__ __launch_bounds__(1024) void k_occ_frame(const int32_t *ent_dst, cons
         }
     }
     __syncthreads();
+    const int per = (nw + 1023) / 1024, w0 = tid * per, w1 = min(w0 + per, nw);
+    int32_t cnt = 0;
+    for (int i = w0; i < w1; ++i) cnt += __popc(s_mask[i]);
+    int32_t x = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_tot[wave] = x;
+    __syncthreads();
+    if (tid == 0) {
+        int32_t sum = 0;
+        for (int w = 0; w < 16; ++w) {
+            const int32_t t = s_tot[w];
+            s_tot[w] = sum;
+            sum += t;
+        }
+    }
+    __syncthreads();
+    int32_t run = s_tot[wave] + x - cnt;
+    for (int i = w0; i < w1; ++i) {
+        s_base[i] = run;
+        run += __popc(s_mask[i]);
+    }
+    __syncthreads();
     uint32_t *om = occ + (int64_t)f * nw;
     int32_t *ob = occ_base + (int64_t)f * nw;
-    int32_t carry = 0;
-    for (int base = 0; base < nw; base += 1024) {  // 1024 consecutive words per round: coalesced stores
-        const int i = base + tid;
-        const uint32_t m = i < nw ? s_mask[i] : 0u;
-        int32_t x = __popc(m);
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) s_tot[wave] = x;
-        __syncthreads();
-        if (tid == 0) {
-            int32_t sum = 0;
-            for (int w = 0; w < 16; ++w) {
-                const int32_t t = s_tot[w];
-                s_tot[w] = sum;
-                sum += t;
-            }
-            s_tot[16] = sum;
-        }
-        __syncthreads();
-        if (i < nw) {
-            om[i] = m;
-            ob[i] = carry + s_tot[wave] + x - __popc(m);
-        }
-        carry += s_tot[16];
-        __syncthreads();
+    for (int i = tid; i < nw; i += 1024) {
+        om[i] = s_mask[i];
+        ob[i] = s_base[i];
     }
 }
 
 // The pooled vector of every run of the cell-keyed CSR into its compact row
-// frame_off[f] + (run rank in frame f): one thread per (entry, 16-byte piece);
-// the thread on a run's first entry sums the run in entry order with separate
-// multiply and add from 0 and rounds once -- shpl_pull's (k_sparse's)
-// arithmetic, bit for bit.
+// frame_off[f] + (run rank in frame f): one thread per entry; the thread on a
+// run's first entry sums the run in entry order with separate multiply and add
+// from 0 and rounds once per channel -- shpl_pull's (k_sparse's) arithmetic,
+// bit for bit -- all NP 16-byte pieces of each entry's row in flight together.
+template <int NP>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_pool_runs(const int32_t *ent_dst, const int32_t *ent_src,
                                                           const float *ent_val, int64_t nnz_cap, const uint16_t *img,
-                                                          int64_t img_stride, int64_t img_off, int c_b, int np,
-                                                          int H, int W, int wpr, const uint32_t *occ,
-                                                          const int32_t *occ_base, const int64_t *frame_off,
-                                                          uint16_t *cmp) {
-    const int64_t t = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x;
-    const int64_t e = t / np;
-    const int g = (int)(t - e * np);
+                                                          int64_t img_stride, int64_t img_off, int c_b, int H, int W,
+                                                          int wpr, const uint32_t *occ, const int32_t *occ_base,
+                                                          const int64_t *frame_off, uint16_t *cmp) {
+    const int64_t e = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x;
     if (e >= nnz_cap) return;
     const int32_t d = ent_dst[e];
     if (d < 0 || (e > 0 && ent_dst[e - 1] == d)) return;
@@ -151,40 +151,33 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_pool_runs(const int32_t *ent_dst
     const int c = (int)(d - f * cells), y = c / W, x = c - y * W;
     const int64_t wi = ((int64_t)f * H + y) * wpr + (x >> 5);
     const int32_t rid = occ_base[wi] + __popc(occ[wi] & ((1u << (x & 31)) - 1u));
-    float sum[8];
+    float sum[NP][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) sum[j] = 0.0f;
-    for (int64_t i0 = e; i0 < nnz_cap; i0 += POOL_BATCH) {
-        u32x4 raw[POOL_BATCH];
-        float wv[POOL_BATCH];
-        bool live[POOL_BATCH];
+    for (int g = 0; g < NP; ++g)
 #pragma unroll
-        for (int u = 0; u < POOL_BATCH; ++u) {
-            const int64_t i = i0 + u;
-            live[u] = i < nnz_cap && ent_dst[i] == d;
-            if (live[u]) {
-                wv[u] = ent_val[i];
-                raw[u] = *reinterpret_cast<const u32x4 *>(img + (int64_t)ent_src[i] * img_stride + img_off + g * 8);
-            }
-        }
-        bool more = true;
+        for (int j = 0; j < 8; ++j) sum[g][j] = 0.0f;
+    for (int64_t i = e; i < nnz_cap && ent_dst[i] == d; ++i) {
+        const float wv = ent_val[i];
+        const uint16_t *row = img + (int64_t)ent_src[i] * img_stride + img_off;
+        u32x4 raw[NP];
 #pragma unroll
-        for (int u = 0; u < POOL_BATCH; ++u) {
-            if (!live[u]) {
-                more = false;
-                break;
-            }
+        for (int g = 0; g < NP; ++g) raw[g] = *reinterpret_cast<const u32x4 *>(row + g * 8);
+#pragma unroll
+        for (int g = 0; g < NP; ++g) {
             uint16_t xv[8];
-            __builtin_memcpy(xv, &raw[u], 16);
+            __builtin_memcpy(xv, &raw[g], 16);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) sum[j] = __fadd_rn(sum[j], __fmul_rn(wv[u], bf16_to_f32(xv[j])));
+            for (int j = 0; j < 8; ++j) sum[g][j] = __fadd_rn(sum[g][j], __fmul_rn(wv, bf16_to_f32(xv[j])));
         }
-        if (!more) break;
     }
-    uint16_t o[8];
+    uint16_t *o = cmp + (frame_off[f] + rid) * (int64_t)c_b;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f32_to_bf16(sum[j]);
-    *reinterpret_cast<u32x4 *>(cmp + (frame_off[f] + rid) * (int64_t)c_b + g * 8) = *reinterpret_cast<u32x4 *>(o);
+    for (int g = 0; g < NP; ++g) {
+        uint16_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = f32_to_bf16(sum[g][j]);
+        *reinterpret_cast<u32x4 *>(o + g * 8) = *reinterpret_cast<u32x4 *>(v);
+    }
 }
 
 // A raw buffer descriptor (gfx9: dword 3 = 0x00020000) over `bytes` bytes from `base`.
@@ -451,10 +444,25 @@ int prep_pooled(int n_frames, int h, int w, int wpr, const int32_t *ent_dst, con
     SHPL_LAUNCH_CHECK();
     const int np = c_b / 8;
     if (nnz_cap > 0 && np > 0) {
-        const int64_t threads = nnz_cap * np;
-        hipLaunchKernelGGL(k_pool_runs, dim3((unsigned)((threads + SHPL_BLOCK - 1) / SHPL_BLOCK)), dim3(SHPL_BLOCK),
-                           0, s, ent_dst, ent_src, ent_val, nnz_cap, img, img_stride, img_off, c_b, np, h, w, wpr, occ,
-                           occ_base, frame_off, cmp);
+        const dim3 grid((unsigned)((nnz_cap + SHPL_BLOCK - 1) / SHPL_BLOCK));
+        switch (np) {
+#define SHPL_POOL_RUNS(NP)                                                                                       \
+    case NP:                                                                                                     \
+        hipLaunchKernelGGL(k_pool_runs<NP>, grid, dim3(SHPL_BLOCK), 0, s, ent_dst, ent_src, ent_val, nnz_cap, img, \
+                           img_stride, img_off, c_b, h, w, wpr, occ, occ_base, frame_off, cmp);                   \
+        break;
+            SHPL_POOL_RUNS(1)
+            SHPL_POOL_RUNS(2)
+            SHPL_POOL_RUNS(3)
+            SHPL_POOL_RUNS(4)
+            SHPL_POOL_RUNS(5)
+            SHPL_POOL_RUNS(6)
+            SHPL_POOL_RUNS(7)
+            SHPL_POOL_RUNS(8)
+#undef SHPL_POOL_RUNS
+            default:
+                return SHPL_ERR_ARG;
+        }
         SHPL_LAUNCH_CHECK();
     }
     return SHPL_OK;
