@@ -180,10 +180,13 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_pool_runs(const int32_t *ent_dst
     }
 }
 
-// A raw buffer descriptor (gfx9: dword 3 = 0x00020000) over `bytes` bytes from `base`.
+// A raw buffer descriptor (gfx9: dword 3 = 0x00020000) over `bytes` bytes from
+// `base` (wave-uniform; readfirstlane pins it to SGPRs for the asm operand).
 __device__ __forceinline__ i32x4 rsrc(const void *base, uint32_t bytes) {
     const uint64_t b = (uint64_t)base;
-    return i32x4{(int32_t)(uint32_t)b, (int32_t)((b >> 32) & 0xffffu), (int32_t)bytes, 0x00020000};
+    return i32x4{__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)b),
+                 __builtin_amdgcn_readfirstlane((int32_t)((b >> 32) & 0xffffu)),
+                 __builtin_amdgcn_readfirstlane((int32_t)bytes), 0x00020000};
 }
 
 // One LDS-DMA of 16 bytes per lane from buffer offset voff (lane k's piece
@@ -301,6 +304,8 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
     const int b = j - 2;
     uint8_t *s_o = s_ring + U * L::SLOT;
     const int pl = lane & 31, hf = lane >> 5;
+    const bool row_ok = b >= 0 && b < n_out;
+    uint16_t *orow = r.out + (frame_row0 + (int64_t)(ya + b) * r.w + x0) * r.out_stride + cob * NCO;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the MFMAs' operand reads of the slot are done
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -322,10 +327,8 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
         __builtin_memcpy(s_o + pl * REPI + cl * 2, pk, sizeof(pk));
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const bool row_ok = b >= 0 && b < n_out;
-    uint16_t *orow = r.out + (frame_row0 + (int64_t)(ya + b) * r.w + x0) * r.out_stride + cob * NCO;
 #pragma unroll
-    for (int k = 0; k < RSTORES; ++k) {  // 32 pixels x 4 pieces of 8 channels
+    for (int k = 0; k < 2; ++k) {  // 32 pixels x 4 pieces of 8 channels
         const int pc = lane + 64 * k, px = pc >> 2, pi = pc & 3;
         const u32x4 v = *reinterpret_cast<const u32x4 *>(s_o + px * REPI + pi * 16);
         uint16_t *dst = row_ok && x0 + px < r.w ? orow + px * (int)r.out_stride + pi * 8 : r.junk + pc * 8;
