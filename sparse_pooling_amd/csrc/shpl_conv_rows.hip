@@ -55,6 +55,9 @@ constexpr int HWD = TW + 2;       // halo row (pixels)
 constexpr int W_ROWS = 9 * NCO;   // packed weight rows of a chunk
 constexpr int RING = 3;           // ring slots per wave = the row loop's unroll (accumulator roles)
 constexpr int REPI = NCO * 2 + 16;  // epilogue transpose pitch (bytes per pixel)
+#ifndef SHPL_ROWS_XCD
+#define SHPL_ROWS_XCD 1  // XCD-contiguous item order (0: blockIdx order)
+#endif
 constexpr int RSTORES = 2;        // output stores per row step, always issued (the vmcnt arithmetic)
 constexpr uint32_t OOB = 0x80000000u;  // an offset past every descriptor's num_records: reads zeros
 
@@ -360,7 +363,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     __shared__ uint64_t s_occ[CMP ? 64 : 1];
     __shared__ int32_t s_first[CMP ? 64 : 1];
     const int lane = threadIdx.x;
-    const int item = blockIdx.x;  // (frame, band, strip), strips fastest
+    // (frame, band, strip), strips fastest; each XCD (blocks b, b+8, ...) takes one contiguous run of items,
+    // so neighbouring strips share their halo columns and neighbouring bands their halo rows in that L2
+#if SHPL_ROWS_XCD
+    const int item = [](int bid, int n) {
+        const int q = n >> 3, rr = n & 7, xcd = bid & 7, i = bid >> 3;
+        return xcd < rr ? xcd * (q + 1) + i : rr * (q + 1) + (xcd - rr) * q + i;
+    }(blockIdx.x, r.n_items);
+#else
+    const int item = blockIdx.x;
+#endif
     const int strip = item % r.strips, fb = item / r.strips;
     const int band = fb % r.n_bands, f = fb / r.n_bands;
     const int cob = blockIdx.y;
