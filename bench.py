@@ -832,7 +832,7 @@ def run_conv(args, world, rank, dev):
             tj = json.load(fh).get(f"conv_{args.dtype}_F{F}")
         if tj:
             traffic = tj["hbm_bytes_per_launch"]
-            mfma_busy = tj["kernels"].get(f"k_conv3x3_pooled_{args.dtype}", {}).get("mfma_busy_share")
+            mfma_busy = tj.get("mfma_busy_share")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_conv(spec, frames[:1], args.cpu_seconds)
@@ -851,8 +851,12 @@ def run_conv(args, world, rank, dev):
                        "global_batch": F * world, "frames_per_gpu_per_step": F, "hip_graph": graph is not None,
                        "parallelism": f"frame-sharded x{world}"},
             "frame_checksums": checks,
-            "roofline": {"bound": "mfma", "kernel": "k_conv3x3 (fused pooling), MFMA "
-                         + ("v_mfma_f32_32x32x16_bf16" if esz == 2 else "v_mfma_f32_32x32x2_f32"),
+            "roofline": {"bound": "mfma",
+                         "kernel": ("shpl_conv3x3 call = k_pack_w + k_occ_frame + k_pool_runs + k_conv_rows "
+                                    "(row-streaming, pooled half gathered from the per-run buffer), MFMA "
+                                    "v_mfma_f32_32x32x16_bf16" if esz == 2 else
+                                    "shpl_conv3x3 call = k_pack_w + k_row_ptr + k_conv3x3 (tiled, pooling in the "
+                                    "staging), MFMA v_mfma_f32_32x32x2_f32"),
                          "achieved": round(tflops, 2), "peak": MFMA_PEAK_TFS[dname], "unit": "TFLOP/s",
                          "frac": round(tflops / MFMA_PEAK_TFS[dname], 4), "traffic": traffic,
                          "mfma_busy_share_pmc": mfma_busy,

@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 evidence for the post-fusion conv workload (bench.py --workload conv):
 # kernel-trace stats, then one PMC pass per counter group (FETCH_SIZE and
-# WRITE_SIZE do not fit one TCC pass), kernel filter on k_conv3x3.
+# WRITE_SIZE do not fit one TCC pass), kernel filter on the conv call's kernels.
 # Each pass has its own time limit; a failure ends the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -14,7 +14,7 @@ rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 i=0
 for c in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVES"; do
   i=$((i+1))
-  timeout -s KILL 180 rocprofv3 --pmc $c --kernel-include-regex 'k_conv3x3' -d gpurun_out/pmc_conv_${DT}_$i -o run \
+  timeout -s KILL 180 rocprofv3 --pmc $c --kernel-include-regex 'k_conv3x3|k_conv_rows|k_pool_runs|k_occ_frame|k_pack_w' -d gpurun_out/pmc_conv_${DT}_$i -o run \
     --output-format csv -- python3 $B > gpurun_out/pmc_conv_${DT}_$i.log 2>&1
   rc=$?; echo "pmc '$c' rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done

@@ -14,7 +14,9 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-SHORT = (("k_conv3x3<float, true", "k_conv3x3_pooled_f32"), ("k_conv3x3<float, false", "k_conv3x3_dense_f32"),
+SHORT = (("k_conv_rows<4, 2, true", "k_conv_rows_pooled_bf16"), ("k_conv_rows<4, 4, false", "k_conv_rows_dense_bf16"),
+         ("k_pool_runs", "k_pool_runs"), ("k_occ_frame", "k_occ_frame"), ("k_pack_w", "k_pack_w"),
+         ("k_conv3x3<float, true", "k_conv3x3_pooled_f32"), ("k_conv3x3<float, false", "k_conv3x3_dense_f32"),
          ("k_conv3x3<unsigned short, true", "k_conv3x3_pooled_bf16"),
          ("k_conv3x3<unsigned short, false", "k_conv3x3_dense_bf16"),
          ("k_dense", "k_dense"), ("k_sparse_long", "k_sparse_long"), ("k_sparse", "k_sparse"), ("k_csr_frame", "k_csr_frame"), ("k_compact", "k_compact"),
@@ -50,12 +52,16 @@ def conv(key, dt):
                   "raw_WRITE_SIZE_KiB": write.get(k), "SQ_VALU_MFMA_BUSY_CYCLES": mfma.get(k),
                   "GRBM_GUI_ACTIVE": grbm.get(k),
                   "mfma_busy_share": mfma.get(k, 0.0) / (1024 * cyc) if cyc else None}
-    main_k = f"k_conv3x3_pooled_{dt}"
+    # bf16: the fused call is k_pack_w + k_occ_frame + k_pool_runs + k_conv_rows (row-streaming kernel);
+    # f32: k_pack_w + k_row_ptr + k_conv3x3 (tiled)
+    main_k = "k_conv_rows_pooled_bf16" if dt == "bf16" else f"k_conv3x3_pooled_{dt}"
+    call = [main_k] + (["k_pool_runs", "k_occ_frame", "k_pack_w"] if dt == "bf16" else [])
     path = os.path.join(ROOT, "profiles", "traffic.json")
     tj = json.load(open(path)) if os.path.exists(path) else {}
-    tj[key] = {"hbm_bytes_per_launch": out[main_k]["fetch_bytes"] + out[main_k]["write_bytes"], "kernels": out,
-               "note": (f"{main_k} = the fused conv; FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes; "
-                        "WRITE_SIZE exact (16 B/lane stores since the LDS-transposed epilogue); mfma_busy_share "
+    tj[key] = {"hbm_bytes_per_launch": sum(out[k]["fetch_bytes"] + out[k]["write_bytes"] for k in call if k in out),
+               "main_kernel": main_k, "mfma_busy_share": out[main_k]["mfma_busy_share"], "kernels": out,
+               "note": (f"hbm_bytes_per_launch: the fused conv call ({' + '.join(call)}); FETCH_SIZE x2 (gfx950 "
+                        "wide-read correction), KiB -> bytes; WRITE_SIZE exact (16 B/lane stores); mfma_busy_share "
                         "= MFMA busy cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)")}
     json.dump(tj, open(path, "w"), indent=1)
     print(json.dumps(tj[key], indent=1))
