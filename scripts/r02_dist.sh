@@ -10,7 +10,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_dist.py tests/test_gpu_pari
   -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/dist_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -12 gpurun_out/dist_tests.log; [ $rc -le 1 ] || exit $rc
 i=0
-for w in "" "--config 3" "--config 5" "--workload frames" "--workload conv"; do
+for w in "" "--config 3" "--config 5" "--workload frames" "--workload conv" "--workload conv --dtype bf16"; do
   i=$((i+1))
   timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --write-checksums $w > gpurun_out/n1_$i.log 2>&1 || { tail -5 gpurun_out/n1_$i.log; exit 1; }
   grep '^{' gpurun_out/n1_$i.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('N=1 [$w]', d['value'], d['ms_per_step'], d['frame_checksums'])"
@@ -18,7 +18,7 @@ done
 cp profiles/frame_checksums.json gpurun_out/frame_checksums.json
 export SHPL_DIST_BACKEND=gloo
 i=0
-for w in "" "--config 3" "--config 5" "--workload frames" "--workload conv" "--workload conv --train"; do
+for w in "" "--config 3" "--config 5" "--workload frames" "--workload conv" "--workload conv --dtype bf16" "--workload conv --train"; do
   i=$((i+1))
   timeout -k 10 300 python bench.py --gpus 2 --steps 5 --warmup 2 $w > gpurun_out/n2_$i.log 2>&1 || { tail -20 gpurun_out/n2_$i.log; exit 1; }
   grep '^{' gpurun_out/n2_$i.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('N=2 [$w]', d['value'], d['ms_per_step'], d['scaling'], d.get('frame_checksums'))"
