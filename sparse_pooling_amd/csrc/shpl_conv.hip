@@ -1532,7 +1532,7 @@ int conv_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_
     pl->rp_bytes = pooled ? align_up((size_t)n_frames * (h + 1) * 4, 256) : 0;
     pl->part_bytes = stats ? align_up((size_t)pl->n_cob * NCO * 2 * pl->n_tiles * 8, 256) : 0;
     pl->wpr = (int)((w + 31) / 32);
-    pl->rows = SHPL_CONV_ROWS && dtype == SHPL_BF16 && !stats && pl->qa + pl->qb <= 4 && c_a % 8 == 0 && c_b % 8 == 0 && h > 0 &&
+    pl->rows = SHPL_CONV_ROWS && dtype == SHPL_BF16 && pl->qa + pl->qb <= 4 && c_a % 8 == 0 && c_b % 8 == 0 && h > 0 &&
                w > 0 && rows::supported(pl->qa + pl->qb, pl->qa) &&
                (!pooled || (h * pl->wpr <= rows::OCC_MAX_WORDS && pool_cap * c_b * esz < (1LL << 31)));
     pl->n_bands = (int)((h + 59) / 60);
@@ -1555,7 +1555,8 @@ bool aligned16(const void *ptr) { return ((uintptr_t)ptr & 15u) == 0; }
 // k_conv_rows (shpl_conv_rows.hip) and, pooled, its two preparatory launches
 // (occupancy words + prefix counts per frame; the pooled vector of every run
 // into the compact buffer). The packed weights are already in a.wp.
-int conv_rows_launch(const ConvPlan &pl, const ConvArgs &a, bool pooled, const int64_t *frame_off, hipStream_t s) {
+int conv_rows_launch(const ConvPlan &pl, const ConvArgs &a, bool pooled, bool stats, const int64_t *frame_off,
+                     double *d_stats, hipStream_t s) {
     rows::RowArgs r = {};
     r.a = reinterpret_cast<const uint16_t *>(a.a) + a.a_off;
     r.b = reinterpret_cast<const uint16_t *>(a.b) + a.b_off;
@@ -1577,6 +1578,11 @@ int conv_rows_launch(const ConvPlan &pl, const ConvArgs &a, bool pooled, const i
     r.out_stride = a.out_stride;
     r.wpr = pl.wpr;
     r.frame_off = frame_off;
+    r.out2 = reinterpret_cast<uint16_t *>(a.out2);
+    r.out2_stride = a.out2_stride;
+    r.c_split = a.c_split;
+    r.n_cob = pl.n_cob;
+    r.part = stats ? a.part : nullptr;  // n_items <= n_tiles: the tiled plan's partials hold the rows kernel's
     uint8_t *ws = reinterpret_cast<uint8_t *>(const_cast<void *>(a.wp)) + pl.wp_bytes + pl.rp_bytes + pl.part_bytes;
     r.junk = reinterpret_cast<uint16_t *>(ws + pl.occ_bytes + pl.cmp_bytes);
     if (pooled) {
@@ -1591,7 +1597,12 @@ int conv_rows_launch(const ConvPlan &pl, const ConvArgs &a, bool pooled, const i
         r.occ_base = occ_base;
         r.cmp = cmp;
     }
-    return rows::launch(r, pl.qa + pl.qb, pl.qa, pooled, a.act == 1, pl.n_cob, s);
+    int rc = rows::launch(r, pl.qa + pl.qb, pl.qa, pooled, a.act == 1, stats, s);
+    if (rc || !stats) return rc;
+    hipLaunchKernelGGL(k_stats_reduce, dim3(pl.n_cob * NCO * 2), dim3(RED_BLOCK), 0, s, a.part, r.n_items, a.c_out,
+                       d_stats);
+    SHPL_LAUNCH_CHECK();
+    return SHPL_OK;
 }
 
 template <typename T>
@@ -1603,10 +1614,12 @@ int conv_launch(const ConvPlan &pl, ConvArgs &a, bool pooled, bool stats, const 
                        reinterpret_cast<const T *>(w), a.c_a, pl.qa, a.c_b, pl.qb, a.c_out, pl.n_cob, transpose, wp);
     SHPL_LAUNCH_CHECK();
     if constexpr (sizeof(T) == 2) {
-        // bf16 with at most 64 input channels: the row-streaming kernel (k_conv_rows)
-        if (pl.rows && a.vec_a && (a.c_b == 0 || a.vec_b) && !a.out2 && a.vec_out && a.c_out % NCO == 0 &&
-            a.n_frames > 0)
-            return conv_rows_launch(pl, a, pooled, frame_off, s);
+        // bf16 with at most 64 input channels: the row-streaming kernel (k_conv_rows), also for the input
+        // gradient's two maps (split at a whole output block) and the training forward's statistics
+        if (pl.rows && a.vec_a && (a.c_b == 0 || a.vec_b) && (!a.out2 || a.c_split % NCO == 0) && a.vec_out &&
+            a.c_out % NCO == 0 && a.n_frames > 0 &&
+            (!stats || (a.act == 0 && rows::supported_st(pl.qa + pl.qb, pl.qa, pooled))))
+            return conv_rows_launch(pl, a, pooled, stats, frame_off, d_stats, s);
     }
     if (pooled) {
         hipLaunchKernelGGL(k_row_ptr, dim3(16, a.n_frames), dim3(SHPL_BLOCK), 0, s, a.ent_dst, frame_off, a.h, a.w,

@@ -24,10 +24,17 @@ struct RowArgs {
     const uint16_t *cmp;
     const int64_t *frame_off;
     uint16_t *junk;              // 32 x 32 channels: stores of rows / pixels outside the map land here
+    uint16_t *out2;              // output blocks from channel c_split on go here (the input gradient's two maps)
+    int64_t out2_stride;
+    int c_split;                 // a multiple of 32 when out2 is set
+    int n_cob;                   // output blocks (the fastest index of a workgroup's item)
+    double *part;                // ST: per-item channel sums [(co * 2 + stat) * n_items + item]
 };
 
-// k_conv_rows has an instantiation for q chunks of which qa come from A.
+// k_conv_rows has an instantiation for q chunks of which qa come from A
+// (supported_st: with the batch-statistics epilogue).
 bool supported(int q, int qa);
+bool supported_st(int q, int qa, bool cmp);
 
 // Occupancy words + prefix counts of the cell-keyed CSR per frame, then the
 // pooled vector of every run into its compact row (shpl_pull's arithmetic).
@@ -36,8 +43,9 @@ int prep_pooled(int n_frames, int h, int w, int wpr, const int32_t *ent_dst, con
                 int64_t img_stride, int64_t img_off, int c_b, uint32_t *occ, int32_t *occ_base, uint16_t *cmp,
                 hipStream_t s);
 
-// The conv: grid (n_items, n_cob) of one-wave workgroups.
-int launch(const RowArgs &r, int q, int qa, bool cmp, bool relu, int n_cob, hipStream_t s);
+// The conv: n_items * n_cob one-wave workgroups (ST: also the per-item
+// channel sums of the pre-activation output, for k_stats_reduce).
+int launch(const RowArgs &r, int q, int qa, bool cmp, bool relu, bool st, hipStream_t s);
 
 }  // namespace rows
 }  // namespace shpl

@@ -47,6 +47,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int NCO = 32;           // output channels per wave
@@ -60,8 +62,9 @@ constexpr int REPI = NCO * 2 + 16;  // epilogue transpose pitch (bytes per pixel
 #endif
 constexpr int RSTORES = 2;        // output stores per row step, always issued (the vmcnt arithmetic)
 constexpr uint32_t OOB = 0x80000000u;  // an offset past every descriptor's num_records: reads zeros
+constexpr int SPF = NCO + 4;      // ST: f32 transpose pitch (floats per pixel; 16-byte rows, conflict-free b64 reads)
 
-template <int Q, int QA>
+template <int Q, int QA, bool ST = false>
 struct Layout {
     static constexpr int QB = Q - QA;
     static constexpr int NA = (2 * QA * HWD + 63) / 64;  // A DMAs (the last one: TA lanes)
@@ -71,7 +74,8 @@ struct Layout {
     static constexpr int TB = QB ? 2 * QB * HWD - 64 * (NB - 1) : 0;
     static constexpr int NDMA = NA + NB;
     static constexpr int DATA = (QB ? RB + 2 * QB * HWD : 2 * QA * HWD) * 16;  // bytes of pieces
-    static constexpr int SLOT = DATA > 32 * REPI ? DATA : 32 * REPI;  // also the epilogue's transpose
+    static constexpr int SLOT0 = DATA > 32 * REPI ? DATA : 32 * REPI;  // also the epilogue's transpose
+    static constexpr int SLOT = ST && SLOT0 < 32 * SPF * 4 ? 32 * SPF * 4 : SLOT0;  // ... and ST's f32 one
 };
 
 // Occupancy of the cell-keyed CSR per frame: bit x%32 of word (f, y, x/32) is
@@ -262,15 +266,16 @@ __device__ __forceinline__ void stage(const RowArgs &r, int64_t pix0, bool yok, 
 // epilogue of output row j-2 of the band (always stored: rows and pixels
 // outside the map go to the junk line; its accumulator is cleared), then
 // stage input row j + RING into the slot just read.
-template <int Q, int QA, bool CMP, bool RELU, int U>
+template <int Q, int QA, bool CMP, bool RELU, bool ST, int U>
 __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9], f32x16 (&acc)[3],
                                      const float (*s_par)[NCO], const uint8_t *rd, uint8_t *s_ring,
-                                     int64_t frame_row0, int x0, int ya, int n_in, int n_out, int cob, int j,
+                                     int64_t frame_row0, int x0, int ya, int n_in, int n_out, uint16_t *obase,
+                                     int64_t ostr, f32x4 *s_st, int j,
                                      const uint64_t *s_occ, const int32_t *s_first, uint64_t b_rows,
                                      const uint32_t (&offa)[Layout<Q, QA>::NA],
                                      const int32_t (&offb)[Layout<Q, QA>::NB > 0 ? Layout<Q, QA>::NB : 1],
                                      int lane) {
-    typedef Layout<Q, QA> L;
+    typedef Layout<Q, QA, ST> L;
     // rows j+1 .. j+RING-1 may still be in flight: per later step RSTORES stores and NDMA DMAs
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L::NDMA + RSTORES) * (RING - 1)) : "memory");
     f32x16 &a0 = acc[(U + 1) % 3], &a1 = acc[U], &a2 = acc[(U + 2) % 3];
@@ -308,7 +313,7 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
     uint8_t *s_o = s_ring + U * L::SLOT;
     const int pl = lane & 31, hf = lane >> 5;
     const bool row_ok = b >= 0 && b < n_out;
-    uint16_t *orow = r.out + (frame_row0 + (int64_t)(ya + b) * r.w + x0) * r.out_stride + cob * NCO;
+    uint16_t *orow = obase + (frame_row0 + (int64_t)(ya + b) * r.w + x0) * ostr;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the MFMAs' operand reads of the slot are done
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -334,8 +339,39 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
     for (int k = 0; k < 2; ++k) {  // 32 pixels x 4 pieces of 8 channels
         const int pc = lane + 64 * k, px = pc >> 2, pi = pc & 3;
         const u32x4 v = *reinterpret_cast<const u32x4 *>(s_o + px * REPI + pi * 16);
-        uint16_t *dst = row_ok && x0 + px < r.w ? orow + px * (int)r.out_stride + pi * 8 : r.junk + pc * 8;
+        uint16_t *dst = row_ok && x0 + px < r.w ? orow + px * (int)ostr + pi * 8 : r.junk + pc * 8;
         *reinterpret_cast<u32x4 *>(dst) = v;
+    }
+    if constexpr (ST) {
+        // batch statistics of the pre-activation row (f32, as the tiled kernel): the accumulator through a
+        // second transpose in the slot ([pixel][SPF floats]; LDS runs one wave's operations in order, so the
+        // bf16 transpose's reads above are done first), then lane (cp, qt) sums channels 2cp, 2cp+1 over
+        // pixels 8qt .. 8qt+7 of the row into its band sums (kept in LDS: the pooled form has no VGPR to spare)
+        float *s_f = reinterpret_cast<float *>(s_o);
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<f32x4 *>(s_f + pl * SPF + 8 * g + 4 * hf) =
+                f32x4{a2[4 * g], a2[4 * g + 1], a2[4 * g + 2], a2[4 * g + 3]};
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (row_ok) {
+            const int cp = lane & 15, qt = lane >> 4, nv = r.w - x0;
+            float t[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (k == 4) asm volatile("" ::: "memory");  // two batches of reads (transient registers)
+                const int px = 8 * qt + k;
+                f32x2 v = *reinterpret_cast<const f32x2 *>(s_f + px * SPF + 2 * cp);
+                if (px >= nv) v = f32x2{0.0f, 0.0f};
+                t[0] = __fadd_rn(t[0], v[0]);
+                t[1] = __fadd_rn(t[1], v[1]);
+                t[2] = __fadd_rn(t[2], __fmul_rn(v[0], v[0]));
+                t[3] = __fadd_rn(t[3], __fmul_rn(v[1], v[1]));
+            }
+            f32x4 a = s_st[lane];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = __fadd_rn(a[i], t[i]);
+            s_st[lane] = a;
+        }
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) a2[i] = 0.0f;
@@ -353,9 +389,9 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
                       s_ring + U * L::SLOT, lane);
 }
 
-template <int Q, int QA, bool CMP, bool RELU>
+template <int Q, int QA, bool CMP, bool RELU, bool ST>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_rows(const RowArgs r) {
-    typedef Layout<Q, QA> L;
+    typedef Layout<Q, QA, ST> L;
     __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING * L::SLOT];
     __shared__ __attribute__((aligned(16))) float s_par[2][NCO];
     // the halo rows' occupancy windows (entry j: input row ya - 1 + j): cells x0-1 .. x0+32 as bits 0..33, and
@@ -363,19 +399,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     __shared__ uint64_t s_occ[CMP ? 64 : 1];
     __shared__ int32_t s_first[CMP ? 64 : 1];
     const int lane = threadIdx.x;
-    // (frame, band, strip), strips fastest; each XCD (blocks b, b+8, ...) takes one contiguous run of items,
-    // so neighbouring strips share their halo columns and neighbouring bands their halo rows in that L2
+    // (frame, band, strip, output block), output blocks fastest, then strips; each XCD (blocks b, b+8, ...)
+    // takes one contiguous run of them, so the blocks of a strip read its rows together, and neighbouring
+    // strips share their halo columns and neighbouring bands their halo rows, in that L2
 #if SHPL_ROWS_XCD
-    const int item = [](int bid, int n) {
+    const int wi = [](int bid, int n) {
         const int q = n >> 3, rr = n & 7, xcd = bid & 7, i = bid >> 3;
         return xcd < rr ? xcd * (q + 1) + i : rr * (q + 1) + (xcd - rr) * q + i;
-    }(blockIdx.x, r.n_items);
+    }(blockIdx.x, r.n_items * r.n_cob);
 #else
-    const int item = blockIdx.x;
+    const int wi = blockIdx.x;
 #endif
+    const int cob = wi % r.n_cob, item = wi / r.n_cob;
     const int strip = item % r.strips, fb = item / r.strips;
     const int band = fb % r.n_bands, f = fb / r.n_bands;
-    const int cob = blockIdx.y;
+    const bool second = r.out2 && cob * NCO >= r.c_split;
+    uint16_t *const obase = second ? r.out2 + (cob * NCO - r.c_split) : r.out + cob * NCO;
+    const int64_t ostr = second ? r.out2_stride : r.out_stride;
+    // ST: lane (cp, qt)'s band sums of channels 2cp, 2cp+1 (sum, sum; square sum, square sum)
+    __shared__ f32x4 s_st[ST ? 64 : 1];
+    if constexpr (ST) s_st[lane] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     const int H = r.h;
     const int x0 = strip * TW, ya = band * r.band;
     const int n_out = min(r.band, H - ya), n_in = n_out + 2;
@@ -434,14 +477,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     for (int j = 0; j < n_in; j += RING) {
 #define SHPL_ROWS_STEP(UU)                                                                                          \
     if (j + UU >= n_in) break;                                                                                      \
-    step<Q, QA, CMP, RELU, UU>(r, wr, acc, s_par, rd, s_ring, frame_row0, x0, ya, n_in, n_out, cob, j + UU, s_occ, \
-                               s_first, b_rows, offa, offb, lane);
+    step<Q, QA, CMP, RELU, ST, UU>(r, wr, acc, s_par, rd, s_ring, frame_row0, x0, ya, n_in, n_out, obase, ostr, s_st, \
+                                   j + UU, s_occ, s_first, b_rows, offa, offb, lane);
         SHPL_ROWS_STEP(0)
         SHPL_ROWS_STEP(1)
         SHPL_ROWS_STEP(2)
 #undef SHPL_ROWS_STEP
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing DMAs land before the wave's LDS is released
+    if constexpr (ST) {  // the band's sums over the 4 pixel quarters, then one double per (channel, statistic)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const f32x4 a = s_st[lane];
+        float sst[4] = {a[0], a[1], a[2], a[3]};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            sst[i] = __fadd_rn(sst[i], __shfl_xor(sst[i], 16, 64));
+            sst[i] = __fadd_rn(sst[i], __shfl_xor(sst[i], 32, 64));
+        }
+        if (lane < 16) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int c = cob * NCO + 2 * lane + (i & 1), st = i >> 1;
+                r.part[((int64_t)c * 2 + st) * r.n_items + item] = (double)sst[i];
+            }
+        }
+    }
 }
 
 }  // namespace
@@ -450,6 +510,10 @@ bool supported(int q, int qa) {
     if (q < 1 || q > 4 || qa < 1 || qa > q) return false;
     return qa == q || q - qa >= 1;
 }
+
+// Statistics: dense sources only, and not at 3 chunks from two sources (those spill at 256 VGPRs; the
+// pooled form spills too -- its callers materialise the pooled map, which their backward needs anyway).
+bool supported_st(int q, int qa, bool cmp) { return supported(q, qa) && !cmp && !(q == 3 && qa < 3); }
 
 int prep_pooled(int n_frames, int h, int w, int wpr, const int32_t *ent_dst, const int32_t *ent_src,
                 const float *ent_val, int64_t nnz_cap, const int64_t *frame_off, const uint16_t *img,
@@ -483,19 +547,23 @@ int prep_pooled(int n_frames, int h, int w, int wpr, const int32_t *ent_dst, con
     return SHPL_OK;
 }
 
-int launch(const RowArgs &r, int q, int qa, bool cmp, bool relu, int n_cob, hipStream_t s) {
-    if (!supported(q, qa) || (cmp && qa == q)) return SHPL_ERR_ARG;
-    const dim3 grid((unsigned)r.n_items, (unsigned)n_cob);
-    const int key = ((q * 8 + qa) * 2 + (cmp ? 1 : 0)) * 2 + (relu ? 1 : 0);
+int launch(const RowArgs &r, int q, int qa, bool cmp, bool relu, bool st, hipStream_t s) {
+    if (!supported(q, qa) || (cmp && qa == q) || (st && (relu || !r.part || !supported_st(q, qa, cmp))) || r.n_cob < 1)
+        return SHPL_ERR_ARG;
+    if ((int64_t)r.n_items * r.n_cob >= (1LL << 31)) return SHPL_ERR_BAD_SHAPE;
+    if (r.out2 && r.c_split % NCO != 0) return SHPL_ERR_ARG;
+    const dim3 grid((unsigned)(r.n_items * r.n_cob));
+    const int key = (((q * 8 + qa) * 2 + (cmp ? 1 : 0)) * 2 + (relu ? 1 : 0)) * 2 + (st ? 1 : 0);
     switch (key) {
-#define SHPL_ROWS_CASE(QQ, QQA, CMP, RELU)                                              \
-    case ((QQ * 8 + QQA) * 2 + CMP) * 2 + RELU:                                         \
-        hipLaunchKernelGGL((k_conv_rows<QQ, QQA, CMP, RELU>), grid, dim3(64), 0, s, r); \
+#define SHPL_ROWS_CASE(QQ, QQA, CMP, RELU, ST)                                              \
+    case (((QQ * 8 + QQA) * 2 + CMP) * 2 + RELU) * 2 + ST:                                  \
+        hipLaunchKernelGGL((k_conv_rows<QQ, QQA, CMP, RELU, ST>), grid, dim3(64), 0, s, r); \
         break;
-#define SHPL_ROWS_DENSE(QQ) SHPL_ROWS_CASE(QQ, QQ, 0, 0) SHPL_ROWS_CASE(QQ, QQ, 0, 1)
-#define SHPL_ROWS_TWO(QQ, QQA)                                                                        \
-    SHPL_ROWS_CASE(QQ, QQA, 0, 0)                                                                    \
-    SHPL_ROWS_CASE(QQ, QQA, 0, 1) SHPL_ROWS_CASE(QQ, QQA, 1, 0) SHPL_ROWS_CASE(QQ, QQA, 1, 1)
+    // statistics only beside the plain epilogue (the training forward writes the pre-activation output)
+#define SHPL_ROWS_DENSE(QQ) SHPL_ROWS_CASE(QQ, QQ, 0, 0, 0) SHPL_ROWS_CASE(QQ, QQ, 0, 1, 0) SHPL_ROWS_CASE(QQ, QQ, 0, 0, 1)
+#define SHPL_ROWS_TWO(QQ, QQA)                                                                                 \
+    SHPL_ROWS_CASE(QQ, QQA, 0, 0, 0)                                                                          \
+    SHPL_ROWS_CASE(QQ, QQA, 0, 1, 0) SHPL_ROWS_CASE(QQ, QQA, 1, 0, 0) SHPL_ROWS_CASE(QQ, QQA, 1, 1, 0)
         SHPL_ROWS_DENSE(1)
         SHPL_ROWS_DENSE(2)
         SHPL_ROWS_DENSE(3)
@@ -506,6 +574,10 @@ int launch(const RowArgs &r, int q, int qa, bool cmp, bool relu, int n_cob, hipS
         SHPL_ROWS_TWO(4, 1)
         SHPL_ROWS_TWO(4, 2)
         SHPL_ROWS_TWO(4, 3)
+        SHPL_ROWS_CASE(2, 1, 0, 0, 1)
+        SHPL_ROWS_CASE(4, 1, 0, 0, 1)
+        SHPL_ROWS_CASE(4, 2, 0, 0, 1)
+        SHPL_ROWS_CASE(4, 3, 0, 0, 1)
 #undef SHPL_ROWS_TWO
 #undef SHPL_ROWS_DENSE
 #undef SHPL_ROWS_CASE

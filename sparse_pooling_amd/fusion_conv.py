@@ -184,7 +184,14 @@ class _FusionConvFn(torch.autograd.Function):
         pool = smap.csr(L.BY_CELL, L.ORDER_ENTRY) if pooled else None
         frame_off = smap.frame_off if pooled else None
         train_bn = conv.batch_norm and is_training
-        cap = pool.nnz_cap if pooled else None
+        xb, b_img = None, b
+        if pooled and train_bn and ctx.needs_input_grad[2]:
+            # the weight gradient needs the pooled channels in HBM (see backward): pooled here, once, the
+            # forward is the dense two-source conv whose statistics epilogue runs on the row-streaming
+            # bf16 kernel (the pooled form spills there)
+            xb = sm.pool_img_to_bev(smap, b, (B, H, W, Cb))
+            b, pool, frame_off = xb, None, None
+        cap = pool.nnz_cap if pool is not None else None
         ws = conv._ws_for((dt, B, H, W, Cb, cap, train_bn), conv_ws_bytes(dt, B, H, W, Ca, Cb, conv.c_out, cap, train_bn))
         raw, mean, scale = None, None, None
         if not train_bn:
@@ -205,6 +212,8 @@ class _FusionConvFn(torch.autograd.Function):
             mean, scale = bn_ws[:conv.c_out], bn_ws[conv.c_out:]
         ctx.conv, ctx.smap, ctx.pooled, ctx.train_bn = conv, smap, pooled, train_bn
         ctx.shapes = (Ca, Cb)
+        ctx.xb = xb
+        b = b_img
         # training BN: the backward recomputes the ReLU mask from raw and beta (bitwise y's), so y is not kept
         ctx.save_for_backward(a, b, weights, None if train_bn else y, raw, mean, scale,
                               beta if train_bn else None)
@@ -242,7 +251,7 @@ class _FusionConvFn(torch.autograd.Function):
                 # the pooled channels once into HBM (shpl_pull): the dense two-source weight gradient
                 # runs at twice the waves per SIMD of the one that recomputes them per tile (257 vs
                 # 214 registers); conv3x3_wgrad(..., pool=...) stays the memory-lean form
-                xb = sm.pool_img_to_bev(smap, b, tuple(a.shape[:3]) + (Cb,))
+                xb = ctx.xb if ctx.xb is not None else sm.pool_img_to_bev(smap, b, tuple(a.shape[:3]) + (Cb,))
                 dw = conv3x3_wgrad(a, g_raw, b=xb)
             else:
                 dw = conv3x3_wgrad(a, g_raw, b=b)

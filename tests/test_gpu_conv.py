@@ -289,6 +289,44 @@ def test_bf16_rows_conv_dense(shape):
         np.testing.assert_array_equal(_np(y2.float()), _np(y.float()))
 
 
+STATS_SHAPES = [  # bf16 training forward on k_conv_rows: statistics epilogue (dense sources)
+    (2, 16, 64, 64, 32),   # two sources of 32 (the training workload's Q = 4, QA = 2)
+    (3, 17, 70, 24, 64),   # partial strip (masked pixels), two output blocks
+    (2, 130, 40, 32, 32),  # three bands
+]
+
+
+@pytest.mark.parametrize("shape", STATS_SHAPES, ids=[str(s) for s in STATS_SHAPES])
+def test_bf16_rows_conv_stats(shape):
+    """The batch statistics of k_conv_rows' statistics epilogue (per band: f32
+    sums of the f32 accumulators, per item a double; k_stats_reduce in a fixed
+    order) vs the oracle's double sums of its double conv; the pre-activation
+    output within the bf16 bound; a two-source split bitwise the one-source conv
+    (output and statistics)."""
+    from sparse_pooling_amd import fusion_conv as fc
+    B, H, W, Cin, Cout = shape
+    x = orc.from_bf16_bits(orc.to_bf16_bits(synth.make_features((B, H, W, Cin), 61) + 0.25))
+    w = orc.from_bf16_bits(orc.to_bf16_bits(_weights(Cin, Cout, 62)))
+    stats = torch.empty((2, Cout), dtype=torch.float64, device=DEV)
+    y = fc.conv3x3(_bf16(x), _bf16(w), relu=False, stats=stats)
+    _, raw = orc.conv3x3(x, w, raw=True)
+    bound = _bound(x, w)
+    _assert_within(y.float(), raw, bound + np.abs(raw) * 2.0 ** -8)
+    r2 = raw.reshape(-1, Cout)
+    b2 = bound.reshape(-1, Cout)
+    s = _np(stats)
+    # per value the accumulator's error (bound), plus the f32 summation of the band sums
+    _assert_within(s[0], r2.sum(0), b2.sum(0) + 1e-5 * np.abs(r2).sum(0))
+    _assert_within(s[1], (r2 * r2).sum(0), (2.0 * np.abs(r2) * b2 + b2 * b2).sum(0) + 1e-5 * (r2 * r2).sum(0))
+    if Cin % 32 == 0:
+        h = Cin // 2
+        st2 = torch.empty_like(stats)
+        y2 = fc.conv3x3(_bf16(np.ascontiguousarray(x[..., :h])), _bf16(w), b=_bf16(np.ascontiguousarray(x[..., h:])),
+                        relu=False, stats=st2)
+        np.testing.assert_array_equal(_np(y2.float()), _np(y.float()))
+        np.testing.assert_array_equal(_np(st2), s)
+
+
 def test_bf16_rows_fused_config2():
     """Config 2 in bf16 (32 + 32 -> 32 channels: k_conv_rows with the pooled
     half gathered from the compact run buffer): fused == the conv of the

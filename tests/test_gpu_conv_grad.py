@@ -90,6 +90,81 @@ def test_dgrad_and_wgrad_bf16():
     _check(dw, orc.conv3x3_wgrad(xf, gf), TOL + ACC_W * orc.conv3x3_wgrad(np.abs(xf), np.abs(gf)), "dw bf16")
 
 
+@pytest.mark.parametrize("shape,split", [((2, 16, 64, 32, 64), 32), ((1, 61, 70, 32, 64), 32),
+                                         ((2, 9, 35, 32, 64), 16)])
+def test_dgrad_bf16_two_maps(shape, split):
+    """The bf16 input gradient of a 64-channel input from a 32-channel output
+    gradient (the training workload's): k_conv_rows with two output blocks
+    (blocks fastest in the item order, one per map when the split is at 32),
+    vs the oracle within the bf16 bound; both maps bitwise the one-map form
+    (a split inside an output block takes the tiled kernel: oracle bound only)."""
+    from sparse_pooling_amd import fusion_conv as fc
+    B, H, W, Cout, Cin = shape
+    bf = lambda a: torch.from_numpy(a).to(torch.bfloat16)  # noqa: E731
+    w = bf(_weights(Cin, Cout, 52))
+    g = bf(synth.make_features((B, H, W, Cout), 53))
+    wf, gf = (t.float().numpy() for t in (w, g))
+    ref = orc.conv3x3_dgrad(gf, wf)
+    wt = np.ascontiguousarray(wf[::-1, ::-1].transpose(0, 1, 3, 2))
+    _, ab = orc.conv3x3(np.abs(gf), np.abs(wt), raw=True)
+    bound = TOL + ACC * ab + 2.0 ** -8 * np.abs(ref)
+    dx = fc.conv3x3_dgrad(g.to(DEV), w.to(DEV), Cin)
+    _check(dx.float(), ref, bound, "dx bf16")
+    da, db = fc.conv3x3_dgrad(g.to(DEV), w.to(DEV), Cin, split=split)
+    _check(torch.cat([da, db], -1).float(), ref, bound, "dx bf16 split")
+    if split % 32 == 0:
+        assert torch.equal(torch.cat([da, db], -1), dx)
+
+
+def test_fused_conv_training_bf16_rows():
+    """bf16 FusionConv.fused in training (the bench's --train --dtype bf16 form
+    at config-1 geometry, 32 + 32 -> 32 channels): the pooled map is built once
+    in the forward and the conv runs dense on k_conv_rows with the statistics
+    epilogue; output and every gradient bitwise those of the same autograd
+    graph over the materialised bv_fused (conv(bv_fused) with the pooled
+    channels' gradient pulled back to the image), and the output within the
+    bf16 bound of the oracle chain."""
+    from sparse_pooling_amd import fusion_conv as fc, shpl_map as sm
+    spec = synth.CONFIGS[1]
+    fr = synth.make_frame(spec, seed=910, n_outside=10)
+    gen = orc.gen_sparse_pooling_input_avod(fr.points, fr.voxel_indices, fr.P, list(spec.im_size),
+                                            tuple(spec.bv_size))
+    ref = orc.produce_sparse_pooling_input(gen, stride=spec.stride)
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    Cb = Ci = 32
+    bf = lambda a: torch.from_numpy(a).to(torch.bfloat16)  # noqa: E731
+    bev = bf(synth.make_features((1, Hb, Wb, Cb), 21)).to(DEV)
+    img = bf(synth.make_features((1, Hi, Wi, Ci), 22)).to(DEV)
+    w = bf(_weights(Cb + Ci, Ci, 23)).to(DEV)
+    g = bf(np.random.default_rng(24).standard_normal((1, Hb, Wb, Ci)).astype(np.float32)).to(DEV)
+    smap = sm.pack_map(_t(ref["Mij_pool"]), _t(ref["M_val"].astype(np.float32)), ref["M_size"],
+                       _t(ref["img_index_flip_pool"]), tuple(img.shape))
+    beta = _t((0.1 * np.random.default_rng(25).standard_normal(Ci)).astype(np.float32))
+
+    def run(fused):
+        conv = fc.FusionConv(Cb + Ci, Ci, dtype=torch.bfloat16, device=DEV)
+        conv.weights = w.clone().requires_grad_(True)
+        conv.beta = beta.clone().requires_grad_(True)
+        tb, ti = bev.clone().requires_grad_(True), img.clone().requires_grad_(True)
+        if fused:
+            y = conv.fused(tb, ti, smap, is_training=True)
+        else:
+            y = conv(sm.layer(tb, ti, smap)[0], is_training=True)
+        y.backward(g)
+        return y, tb.grad, ti.grad, conv.weights.grad, conv.beta.grad, conv.moving_mean, conv.moving_var
+
+    got, want = run(True), run(False)
+    for name, u, v in zip(("y", "d_bev", "d_img", "d_w", "d_beta", "moving_mean", "moving_var"), got, want):
+        assert torch.equal(u, v), name
+    eb, _ = orc.sparse_pool_layer(bev.float().cpu().numpy(), img.float().cpu().numpy(), ref["Mij_pool"],
+                                  ref["M_val"], ref["M_size"], ref["img_index_flip_pool"])
+    eb = orc.from_bf16_bits(orc.to_bf16_bits(eb))
+    _, raw = orc.conv3x3(eb, w.float().cpu().numpy(), raw=True)
+    ey, _, bvar, _, _ = orc.batch_norm_train(raw, 1e-3, None, beta.cpu().numpy(), True)
+    _check(got[0].float(), ey, 1e-2 + 2.0 ** -7 * np.abs(ey), "y bf16")
+
+
 def test_wgrad_two_sources_and_pooled():
     """wgrad of [a || b] with b dense, and with b pooled from the CSR (the
     pooled channels recomputed in the staging), == wgrad of the concat."""
