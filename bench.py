@@ -731,8 +731,8 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
             "higher_is_better": True, "scaling": args.partition, "vs_baseline": None, "dtype": dname,
             "data": "synthetic (seeded KITTI-shaped frames, xavier-initialised conv weights)",
             "config": {"workload": (f"conv training: config2 -> index -> conv3x3 {cb + ci}->{ci} + BatchNorm (batch "
-                                    "statistics) + ReLU of [bev || pool(img)] (pooling inside the conv), backward to "
-                                    "bev, img, weights, beta"),
+                                    "statistics) + ReLU of [bev || pool(img)] (the pooled map built once in the forward, "
+                                    "reused by the weight gradient), backward to bev, img, weights, beta"),
                        "global_batch": F * world, "frames_per_gpu_per_step": F, "hip_graph": False,
                        "bn_statistics": "per rank (no cross-rank sync)", "parallelism": f"frame-sharded x{world}"},
             "roofline": {"bound": "mfma", "kernel": "fwd + input-gradient + weight-gradient convs (3x the forward flops) "

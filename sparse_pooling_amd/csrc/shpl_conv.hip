@@ -1895,6 +1895,9 @@ struct WgPlan {
     ConvPlan cp;
     int n_cib, n_groups, tiles_per_group;
     size_t rp_bytes, part_bytes, total;
+    bool rows;  // bf16, dense: k_wgrad_rows when the pointers are 16-byte aligned
+    int r_groups;
+    size_t r_part_bytes, r_part2_bytes;
 };
 
 int wgrad_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_t c_b, int64_t c_out, bool pooled,
@@ -1914,6 +1917,19 @@ int wgrad_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64
     wp->rp_bytes = wp->cp.rp_bytes;
     wp->part_bytes = align_up((size_t)wp->n_groups * blocks_per_group * 9 * WG_CI * NCO * sizeof(float), 256);
     wp->total = wp->rp_bytes + wp->part_bytes;
+    // the row-streaming bf16 weight gradient: bands and strips of the forward's row kernel
+    const int n_bands = (int)((h + 59) / 60);
+    const int64_t n_items = (int64_t)n_frames * n_bands * ((w + TW - 1) / TW);
+    wp->rows = SHPL_CONV_ROWS && dtype == SHPL_BF16 && !pooled && h > 0 && w > 0 && n_items > 0 &&
+               n_items < (1LL << 31) && rows::wgrad_supported((int)c_a, (int)c_b, (int)c_out);
+    if (wp->rows) {
+        rows::wgrad_sizes((int)n_items, (int)c_a, (int)c_b, (int)c_out, &wp->r_groups, &wp->r_part_bytes,
+                          &wp->r_part2_bytes);
+        wp->r_part_bytes = align_up(wp->r_part_bytes, 256);
+        wp->r_part2_bytes = align_up(wp->r_part2_bytes, 256);
+        const size_t rt = wp->r_part_bytes + wp->r_part2_bytes;
+        if (rt > wp->total) wp->total = rt;
+    }
     return SHPL_OK;
 }
 }  // namespace
@@ -1955,6 +1971,32 @@ extern "C" int shpl_conv3x3_wgrad(int dtype, int n_frames, int64_t h, int64_t w,
     if (pl.n_tiles == 0) {  // no pixels: dW = 0
         SHPL_HIP_CHECK(hipMemsetAsync(d_dw, 0, sizeof(float) * 9 * (size_t)(c_a + c_b) * c_out, s));
         return SHPL_OK;
+    }
+    if (wp.rows && (c_a == 0 || (aligned16(d_a) && a_stride % he == 0 && a_off % he == 0)) &&
+        (c_b == 0 || (aligned16(d_b) && b_stride % he == 0 && b_off % he == 0)) && aligned16(d_gy) &&
+        gy_stride % he == 0) {
+        rows::WgRowArgs r = {};
+        r.a = reinterpret_cast<const uint16_t *>(d_a) + a_off;
+        r.b = c_b > 0 ? reinterpret_cast<const uint16_t *>(d_b) + b_off : nullptr;
+        r.a_stride = a_stride;
+        r.b_stride = b_stride;
+        r.c_a = (int)c_a;
+        r.c_b = (int)c_b;
+        r.gy = reinterpret_cast<const uint16_t *>(d_gy);
+        r.gy_stride = gy_stride;
+        r.c_out = (int)c_out;
+        r.h = (int)h;
+        r.w = (int)w;
+        r.strips = (int)((w + TW - 1) / TW);
+        r.n_bands = (int)((h + 59) / 60);
+        r.band = (int)((h + r.n_bands - 1) / r.n_bands);
+        r.n_items = n_frames * r.n_bands * r.strips;
+        r.n_cit = (int)((c_a + 31) / 32 + (c_b + 31) / 32);
+        r.n_cot = (int)((c_out + 31) / 32);
+        r.n_groups = wp.r_groups;
+        uint8_t *ws = reinterpret_cast<uint8_t *>(d_ws);
+        r.part = reinterpret_cast<float *>(ws);
+        return rows::wgrad_launch(r, d_dw, reinterpret_cast<double *>(ws + wp.r_part_bytes), s);
     }
     ConvArgs a = {};
     a.n_frames = n_frames;

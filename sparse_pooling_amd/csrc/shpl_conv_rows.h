@@ -47,5 +47,23 @@ int prep_pooled(int n_frames, int h, int w, int wpr, const int32_t *ent_dst, con
 // channel sums of the pre-activation output, for k_stats_reduce).
 int launch(const RowArgs &r, int q, int qa, bool cmp, bool relu, bool st, hipStream_t s);
 
+// The bf16 weight gradient (k_wgrad_rows): dense sources, input tiles of 32
+// channels within one source, outputs in tiles of 32.
+struct WgRowArgs {
+    const uint16_t *a, *b;
+    int64_t a_stride, b_stride;
+    int c_a, c_b;
+    const uint16_t *gy;
+    int64_t gy_stride;
+    int c_out;
+    int h, w, strips, band, n_bands, n_items;
+    int n_cit, n_cot, n_groups;
+    float *part;  // [group][cot][cit][9][32 co][32 ci]
+};
+
+bool wgrad_supported(int c_a, int c_b, int c_out);
+void wgrad_sizes(int n_items, int c_a, int c_b, int c_out, int *n_groups, size_t *part_bytes, size_t *part2_bytes);
+int wgrad_launch(const WgRowArgs &r, float *dw, double *part2, hipStream_t s);
+
 }  // namespace rows
 }  // namespace shpl

@@ -504,6 +504,205 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     }
 }
 
+
+// ---- The bf16 weight gradient, row-streaming (k_wgrad_rows) ----
+//
+// dW[ky][kx][ci][co] = sum over pixels of X[y+ky-1][x+kx-1][ci] * G[y][x][co]
+// as MFMAs with the pixels as K: D[ci][co] += Xᵀ[ci][px] G[px][co]. Both
+// operands want 8 consecutive pixels of one channel per lane, i.e. the NHWC
+// rows transposed; ds_read_b64_tr_b16 reads them so straight from the rows as
+// the LDS-DMA lands them ([pixel][32 channels], 64 B per pixel: 4 rows of a
+// read cover the 64 banks once). One wave per workgroup owns one 32-channel
+// input tile x one 32-channel output tile, keeps the 9 taps' accumulators
+// (144 VGPRs) for a whole run of items (frame, band, strip), and streams the
+// band's input rows j through the per-wave ring of the forward (3 slots, 2
+// rows ahead, counted vmcnt): row j of X (34 halo pixels) and row j of G
+// arrive together; X row j meets G rows j, j-1, j-2 (ky = 0, 1, 2; the two
+// older G fragments stay in registers), so each staged row is read once: 16
+// transposed reads per 18 MFMAs. G rows outside the band read zeros (exact
+// zero products). Per wave one f32 partial of the 9 x 32 x 32 tile; two
+// fixed-order reductions (f64) give dW: deterministic.
+constexpr int WX_PIECES = HWD * 4;                  // X row: 34 pixels x 4 pieces of 8 channels
+constexpr int WG_PIECES = TW * 4;                   // G row: 32 pixels x 4 pieces
+constexpr int WSLOT = (WX_PIECES + WG_PIECES) * 16;  // 4224 B
+constexpr int WNX = (WX_PIECES + 63) / 64, WTX = WX_PIECES - 64 * (WNX - 1);  // 3 DMAs, the last one 8 lanes
+constexpr int WNG = WG_PIECES / 64;                                         // 2 DMAs
+constexpr int WNDMA = WNX + WNG;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+// The 32x16 operand fragment at pixel p0 (+ 8h + 4t + q) of an LDS image [pixel][64 B]: two transposed reads
+// (lane 4q+p of 16-lane group g: row q, channels 16 (g & 1) + 4p .. + 3; lane i of the group gets channel
+// 16 (g & 1) + i). `lb` holds the lane's part of the address; p0 a compile-time pixel offset.
+template <int P0>
+__device__ __forceinline__ bf16x8 tr_frag(const uint8_t *lb) {
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(lb + P0 * 64));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(lb + (P0 + 4) * 64));
+    const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    bf16x8 out;
+    __builtin_memcpy(&out, &v, 16);
+    return out;
+}
+
+__device__ __forceinline__ void wstage(const WgRowArgs &r, const uint16_t *xsrc, int64_t xstride, int64_t pix0,
+                                       bool xok, int64_t gpix, bool gok, const uint32_t (&offx)[WNX],
+                                       const uint32_t (&offg)[WNG], uint8_t *slot, int lane) {
+    const i32x4 rx = rsrc(xsrc + pix0 * xstride, xok ? OOB : 0u);
+#pragma unroll
+    for (int i = 0; i < WNX; ++i)
+        if (i < WNX - 1 || lane < WTX) dma16(rx, offx[i], slot + i * 1024);
+    const i32x4 rg = rsrc(r.gy + gpix * r.gy_stride, gok ? OOB : 0u);
+#pragma unroll
+    for (int i = 0; i < WNG; ++i) dma16(rg, offg[i], slot + WX_PIECES * 16 + i * 1024);
+}
+
+// One input row j of the band (slot U = j % 3): 16 transposed reads, 18 MFMAs, then row j + 3 staged.
+template <int U>
+__device__ __forceinline__ void wstep(const WgRowArgs &r, f32x16 (&acc)[9], bf16x8 (&g1)[2], bf16x8 (&g2)[2],
+                                      uint8_t *s_ring, const uint8_t *lb, const uint16_t *xsrc, int64_t xstride,
+                                      int64_t frame_row0, int x0, int ya, int n_in, int n_out, int j,
+                                      const uint32_t (&offx)[WNX], const uint32_t (&offg)[WNG], int lane) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WNDMA * 2) : "memory");  // rows j+1, j+2 may still be in flight
+    const uint8_t *xs = lb + U * WSLOT, *gs = xs + WX_PIECES * 16;
+    bf16x8 g0[2];
+    g0[0] = tr_frag<0>(gs);
+    g0[1] = tr_frag<16>(gs);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+            const bf16x8 xa = kx == 0 ? tr_frag<0>(xs + s * 1024) : kx == 1 ? tr_frag<1>(xs + s * 1024)
+                                                                             : tr_frag<2>(xs + s * 1024);
+            acc[kx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa, g0[s], acc[kx], 0, 0, 0);
+            acc[3 + kx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa, g1[s], acc[3 + kx], 0, 0, 0);
+            acc[6 + kx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa, g2[s], acc[6 + kx], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        g2[s] = g1[s];
+        g1[s] = g0[s];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done before the DMAs refill it
+    const int jn = j + RING, y = ya - 1 + jn;
+    wstage(r, xsrc, xstride, frame_row0 + (int64_t)y * r.w + x0 - 1, jn < n_in && y >= 0 && y < r.h,
+           frame_row0 + (int64_t)(ya + jn) * r.w + x0, jn < n_out, offx, offg, s_ring + U * WSLOT, lane);
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_wgrad_rows(const WgRowArgs r) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING * WSLOT];
+    const int lane = threadIdx.x;
+    const int n_tiles = r.n_cit * r.n_cot, total = r.n_groups * n_tiles;
+    // (group, output tile, input tile), input tiles fastest (they share the G rows), each XCD one contiguous run
+    const int wi = [](int bid, int n) {
+        const int q = n >> 3, rr = n & 7, xcd = bid & 7, i = bid >> 3;
+        return xcd < rr ? xcd * (q + 1) + i : rr * (q + 1) + (xcd - rr) * q + i;
+    }(blockIdx.x, total);
+    const int cit = wi % r.n_cit, cot = (wi / r.n_cit) % r.n_cot, grp = wi / n_tiles;
+    const int na = r.c_a / 32 + (r.c_a % 32 ? 1 : 0);  // input tiles of A (c_a % 32 == 0 when B is present)
+    const bool from_a = cit < na;
+    const uint16_t *xsrc = from_a ? r.a + cit * 32 : r.b + (cit - na) * 32;
+    const int64_t xstride = from_a ? r.a_stride : r.b_stride;
+    const int cn = from_a ? r.c_a - cit * 32 : r.c_b - (cit - na) * 32;  // channels of the tile (>= 32: whole)
+    const int cg = r.c_out - cot * 32;
+    const uint16_t *gsrc = r.gy + cot * 32;
+    WgRowArgs rr = r;
+    rr.gy = gsrc;
+    const int64_t i0 = (int64_t)grp * r.n_items / r.n_groups, i1 = (int64_t)(grp + 1) * r.n_items / r.n_groups;
+    // lane address part of the transposed reads: row q = (lane & 15) >> 2, channel 16 ((lane >> 4) & 1) + 4 (lane & 3),
+    // pixel base 8 h (h = lane >> 5)
+    const uint8_t *lb = s_ring + (8 * (lane >> 5) + ((lane & 15) >> 2)) * 64 + 32 * ((lane >> 4) & 1) + 8 * (lane & 3);
+    f32x16 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[t][i] = 0.0f;
+    for (int64_t it = i0; it < i1; ++it) {
+        const int item = (int)it;
+        const int strip = item % r.strips, fb = item / r.strips;
+        const int band = fb % r.n_bands, f = fb / r.n_bands;
+        const int x0 = strip * TW, ya = band * r.band;
+        const int n_out = min(r.band, r.h - ya), n_in = n_out + 2;
+        const int64_t frame_row0 = (int64_t)f * r.h * r.w;
+        uint32_t offx[WNX], offg[WNG];
+#pragma unroll
+        for (int i = 0; i < WNX; ++i) {
+            const int pc = 64 * i + lane, px = pc >> 2, cq = pc & 3, x = x0 - 1 + px;
+            const bool ok = pc < WX_PIECES && x >= 0 && x < r.w && 8 * cq < cn;
+            offx[i] = ok ? (uint32_t)((px * (int)xstride + 8 * cq) * 2) : OOB;
+        }
+#pragma unroll
+        for (int i = 0; i < WNG; ++i) {
+            const int pc = 64 * i + lane, px = pc >> 2, cq = pc & 3, x = x0 + px;
+            offg[i] = x < r.w && 8 * cq < cg ? (uint32_t)((px * (int)r.gy_stride + 8 * cq) * 2) : OOB;
+        }
+#pragma unroll
+        for (int j = 0; j < RING; ++j) {
+            const int y = ya - 1 + j;
+            wstage(rr, xsrc, xstride, frame_row0 + (int64_t)y * r.w + x0 - 1, j < n_in && y >= 0 && y < r.h,
+                   frame_row0 + (int64_t)(ya + j) * r.w + x0, j < n_out, offx, offg, s_ring + j * WSLOT, lane);
+        }
+        bf16x8 g1[2], g2[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) g1[s][i] = g2[s][i] = (__bf16)0.0f;
+        for (int j = 0; j < n_in; j += RING) {
+#define SHPL_WROWS_STEP(UU)                                                                                  \
+    if (j + UU >= n_in) break;                                                                               \
+    wstep<UU>(rr, acc, g1, g2, s_ring, lb, xsrc, xstride, frame_row0, x0, ya, n_in, n_out, j + UU, offx, offg, \
+              lane);
+            SHPL_WROWS_STEP(0)
+            SHPL_WROWS_STEP(1)
+            SHPL_WROWS_STEP(2)
+#undef SHPL_WROWS_STEP
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing DMAs land before the next item's prologue
+    }
+    // partial [group][cot][cit][tap][co][ci]: lane (co = lane & 31, h) holds ci 8 (i >> 2) + 4 h + (i & 3)
+    float *out = r.part + (((int64_t)grp * r.n_cot + cot) * r.n_cit + cit) * (9 * 1024) + (lane & 31) * 32 +
+                 4 * (lane >> 5);
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<f32x4 *>(out + t * 1024 + 8 * g) =
+                f32x4{acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]};
+}
+
+// Level 1: entries e of the partial tile set, summed over groups [c*WGC, (c+1)*WGC) in order (f64).
+constexpr int WGC = 32;
+__global__ __launch_bounds__(SHPL_BLOCK) void k_wgrad_rows_sum(const float *part, int64_t n_ent, int n_groups,
+                                                               double *part2) {
+    const int64_t e = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x;
+    if (e >= n_ent) return;
+    const int c = blockIdx.y, g0 = c * WGC, g1 = min(g0 + WGC, n_groups);
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    int g = g0;
+    for (; g + 3 < g1; g += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[u] += (double)part[(int64_t)(g + u) * n_ent + e];
+    }
+    for (int u = 0; g < g1; ++g, ++u) acc[u] += (double)part[(int64_t)g * n_ent + e];
+    part2[(int64_t)c * n_ent + e] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+}
+
+// Level 2: dW (HWIO f32) from the chunk sums, in order.
+__global__ __launch_bounds__(SHPL_BLOCK) void k_wgrad_rows_final(const double *part2, int n_chunks, int64_t n_ent,
+                                                                 int c_a, int c_b, int c_out, int n_cit, int n_cot,
+                                                                 float *dw) {
+    const int cin = c_a + c_b;
+    const int64_t o = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x;
+    if (o >= (int64_t)9 * cin * c_out) return;
+    const int co = (int)(o % c_out), ci = (int)((o / c_out) % cin), tap = (int)(o / ((int64_t)c_out * cin));
+    const int na = c_a / 32 + (c_a % 32 ? 1 : 0);
+    const int cit = ci < c_a ? ci / 32 : na + (ci - c_a) / 32, lci = ci < c_a ? ci % 32 : (ci - c_a) % 32;
+    const int64_t e = ((int64_t)(co / 32) * n_cit + cit) * (9 * 1024) + tap * 1024 + (co % 32) * 32 + lci;
+    double s = 0.0;
+    for (int c = 0; c < n_chunks; ++c) s += part2[(int64_t)c * n_ent + e];
+    dw[o] = (float)s;
+}
 }  // namespace
 
 bool supported(int q, int qa) {
@@ -584,6 +783,40 @@ int launch(const RowArgs &r, int q, int qa, bool cmp, bool relu, bool st, hipStr
         default:
             return SHPL_ERR_ARG;
     }
+    SHPL_LAUNCH_CHECK();
+    return SHPL_OK;
+}
+
+
+bool wgrad_supported(int c_a, int c_b, int c_out) {
+    if (c_a < 0 || c_b < 0 || c_a + c_b < 1 || c_out < 1) return false;
+    if (c_a % 8 || c_b % 8 || c_out % 8) return false;
+    return c_b == 0 || c_a % 32 == 0;  // an input tile never straddles the two sources
+}
+
+void wgrad_sizes(int n_items, int c_a, int c_b, int c_out, int *n_groups, size_t *part_bytes, size_t *part2_bytes) {
+    const int n_cit = (c_a + 31) / 32 + (c_b + 31) / 32, n_cot = (c_out + 31) / 32;
+    int g = 2048 / (n_cit * n_cot);  // 8 waves per CU
+    if (g < 1) g = 1;
+    if (g > n_items) g = n_items > 0 ? n_items : 1;
+    *n_groups = g;
+    const int64_t n_ent = (int64_t)n_cit * n_cot * 9 * 1024;
+    *part_bytes = (size_t)g * n_ent * 4;
+    *part2_bytes = (size_t)((g + WGC - 1) / WGC) * n_ent * 8;
+}
+
+int wgrad_launch(const WgRowArgs &r, float *dw, double *part2, hipStream_t s) {
+    const int total = r.n_groups * r.n_cit * r.n_cot;
+    hipLaunchKernelGGL(k_wgrad_rows, dim3((unsigned)total), dim3(64), 0, s, r);
+    SHPL_LAUNCH_CHECK();
+    const int64_t n_ent = (int64_t)r.n_cit * r.n_cot * 9 * 1024;
+    const int n_chunks = (r.n_groups + WGC - 1) / WGC;
+    hipLaunchKernelGGL(k_wgrad_rows_sum, dim3((unsigned)((n_ent + SHPL_BLOCK - 1) / SHPL_BLOCK), (unsigned)n_chunks),
+                       dim3(SHPL_BLOCK), 0, s, r.part, n_ent, r.n_groups, part2);
+    SHPL_LAUNCH_CHECK();
+    const int64_t n_out = (int64_t)9 * (r.c_a + r.c_b) * r.c_out;
+    hipLaunchKernelGGL(k_wgrad_rows_final, dim3((unsigned)((n_out + SHPL_BLOCK - 1) / SHPL_BLOCK)), dim3(SHPL_BLOCK),
+                       0, s, part2, n_chunks, n_ent, r.c_a, r.c_b, r.c_out, r.n_cit, r.n_cot, dw);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
 }

@@ -116,6 +116,36 @@ def test_dgrad_bf16_two_maps(shape, split):
         assert torch.equal(torch.cat([da, db], -1), dx)
 
 
+WGRAD_ROWS = [  # B, H, W, c_a, c_b, c_out: bf16 dense weight gradients on k_wgrad_rows
+    (2, 16, 64, 32, 32, 32),   # the training workload's two sources
+    (1, 130, 70, 64, 0, 64),   # three bands, a partial strip, two output tiles
+    (3, 9, 33, 16, 0, 40),     # channel tails in both tiles (16 of 32 inputs, 8 of the second 32 outputs)
+    (1, 61, 32, 32, 16, 32),   # one band of 61 rows; B's tile is a tail
+]
+
+
+@pytest.mark.parametrize("shape", WGRAD_ROWS, ids=[str(s) for s in WGRAD_ROWS])
+def test_wgrad_bf16_rows(shape):
+    """k_wgrad_rows (transposed LDS reads of the NHWC rows, the 9 taps'
+    accumulators resident over a run of bands, two fixed-order f64 reductions)
+    vs the oracle's double sums: bf16 products are exact, so the f32 bound
+    holds; two sources == their concat bitwise when A ends on a 32-channel tile."""
+    from sparse_pooling_amd import fusion_conv as fc
+    B, H, W, ca, cb, co = shape
+    bf = lambda a: torch.from_numpy(a).to(torch.bfloat16)  # noqa: E731
+    x = bf(synth.make_features((B, H, W, ca + cb), 71))
+    g = bf(synth.make_features((B, H, W, co), 72))
+    xf, gf = x.float().numpy(), g.float().numpy()
+    bound = TOL + ACC_W * orc.conv3x3_wgrad(np.abs(xf), np.abs(gf))
+    dw = fc.conv3x3_wgrad(x.to(DEV), g.to(DEV))
+    _check(dw, orc.conv3x3_wgrad(xf, gf), bound, "dw bf16 rows")
+    if cb > 0:
+        xa = x[..., :ca].contiguous().to(DEV)
+        xb = x[..., ca:].contiguous().to(DEV)
+        dw2 = fc.conv3x3_wgrad(xa, g.to(DEV), b=xb)
+        assert torch.equal(dw2, dw)
+
+
 def test_fused_conv_training_bf16_rows():
     """bf16 FusionConv.fused in training (the bench's --train --dtype bf16 form
     at config-1 geometry, 32 + 32 -> 32 channels): the pooled map is built once
