@@ -608,6 +608,13 @@ def run_frames(args, world, rank, dev):
               "csr_ms": mean(5, 6), "k_dense_ms": dense_ms, "k_sparse_ms": sparse_ms}
     nbytes = pull_bytes(F * pl.Hb * pl.Wb, C, C, u_pix, nnz, 4, 2 * C)
     achieved = nbytes / ((dense_ms + sparse_ms) * 1e-3) / 1e9
+    # the whole step's algorithmic bytes: scans in (16 B/point), camera-frame points out and back in (24 B),
+    # the BEV maps out (5 height slices + density, f64), voxel indices + unique points (40 B/voxel), the index
+    # (~16 B/entry out, 40 B/point in), the CSR (~40 B/entry) and the layer
+    n_maps = synth.NUM_SLICES + 1
+    step_bytes = (nbytes + 16 * int(fr.total_points) + 2 * 24 * n_cam + F * pl.Hb * pl.Wb * n_maps * 8
+                  + 40 * n_vox + 40 * n_vox + 56 * nnz)
+    step_gbs = step_bytes / (elapsed / args.steps) / 1e9
     checks = checksum_report(f"frames_{args.scan_points}_frames{F * world}", sd.frame_checksums(pl.bv_fused), dev,
                              rank, args)
     cpu = None
@@ -636,7 +643,9 @@ def run_frames(args, world, rank, dev):
             "frame_checksums": checks,
             "roofline": {"bound": "hbm", "kernel": "k_dense + k_sparse (fused layer)", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "algorithmic_bytes_per_launch": nbytes},
+                         "traffic": None, "algorithmic_bytes_per_launch": nbytes,
+                         "step_algorithmic_bytes": step_bytes, "step_GBps": round(step_gbs, 1),
+                         "step_frac": round(step_gbs / HBM_PEAK_GBS, 4)},
             "cpu_baseline": cpu,
             "index_errors": errs,
         }
@@ -722,7 +731,23 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
     bwd_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / n_ev
     flops = 3 * 2.0 * F * Hb * Wb * 9 * (cb + ci) * ci  # forward, input gradient, weight gradient
     dname = "bf16" if esz == 2 else "f32"
-    tflops = flops / ((fwd_ms + bwd_ms) * 1e-3) / 1e12
+    step_s = (fwd_ms + bwd_ms) * 1e-3
+    tflops = flops / step_s / 1e12
+    # algorithmic HBM bytes of the step's passes: pooled map written once (+ gathers), conv forward
+    # reads [bev || pooled] and writes the pre-activation map, BN apply reads / writes it, BN backward reads gy and
+    # raw twice and writes g_raw, the input gradient reads g_raw and writes both sources' gradients, the pooled
+    # channels' gradient is gathered back to the image, the weight gradient reads [bev || pooled] and g_raw
+    nnz = int(pl.frame_nnz.sum().item())
+    ents = pl.cell[pl.cell >= 0]
+    u_cell = int(torch.unique(ents).numel())
+    u_pix = int(torch.unique(pl.pix[pl.pix >= 0]).numel())
+    Hi, Wi = spec.img_feat_hw
+    px = F * Hb * Wb * esz
+    hbm_bytes = (px * (ci + (cb + ci + ci) + 2 * ci + 2 * ci + 3 * ci + (ci + cb + ci) + (cb + ci + ci))
+                 + F * Hi * Wi * ci * esz + (u_pix + u_cell) * ci * esz + 2 * 12 * nnz)
+    hbm_gbs = hbm_bytes / step_s / 1e9
+    # the bound: the larger of the two floors (f32: MFMA; bf16: HBM)
+    hbm_bound = hbm_bytes / (HBM_PEAK_GBS * 1e9) > flops / (MFMA_PEAK_TFS[dname] * 1e12)
     if rank == 0:
         print(json.dumps({
             "metric": "SHPL + post-fusion conv training frames/sec (fwd + bwd), 1/2/4/8 GPU",
@@ -735,11 +760,19 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
                                     "reused by the weight gradient), backward to bev, img, weights, beta"),
                        "global_batch": F * world, "frames_per_gpu_per_step": F, "hip_graph": False,
                        "bn_statistics": "per rank (no cross-rank sync)", "parallelism": f"frame-sharded x{world}"},
-            "roofline": {"bound": "mfma", "kernel": "fwd + input-gradient + weight-gradient convs (3x the forward flops) "
-                         "over the forward + backward time (BN, ReLU and the pooling gradient included)",
-                         "achieved": round(tflops, 2), "peak": MFMA_PEAK_TFS[dname], "unit": "TFLOP/s",
-                         "frac": round(tflops / MFMA_PEAK_TFS[dname], 4), "traffic": None,
-                         "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4)},
+            "roofline": ({"bound": "hbm", "kernel": "the whole forward + backward step: algorithmic bytes of its passes "
+                          "(pooled map, conv fwd, BN apply, BN backward x2, input and weight gradients, image "
+                          "gradient) over the forward + backward time",
+                          "achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(hbm_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                          "algorithmic_bytes_per_step": hbm_bytes, "mfma_tflops": round(tflops, 2),
+                          "mfma_frac": round(tflops / MFMA_PEAK_TFS[dname], 4)} if hbm_bound else
+                         {"bound": "mfma", "kernel": "fwd + input-gradient + weight-gradient convs (3x the forward "
+                          "flops) over the forward + backward time (BN, ReLU and the pooling gradient included)",
+                          "achieved": round(tflops, 2), "peak": MFMA_PEAK_TFS[dname], "unit": "TFLOP/s",
+                          "frac": round(tflops / MFMA_PEAK_TFS[dname], 4), "traffic": None,
+                          "algorithmic_bytes_per_step": hbm_bytes, "hbm_GBps": round(hbm_gbs, 1)}),
+            "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4),
             "cpu_baseline": None,
         }), flush=True)
 
@@ -862,7 +895,11 @@ def run_conv(args, world, rank, dev):
                          "mfma_busy_share_pmc": mfma_busy,
                          "algorithmic_flops_per_launch": flops, "kernel_ms": round(conv_ms, 4),
                          "hbm_algorithmic_bytes_per_launch": hbm_bytes,
-                         "hbm_GBps": round(hbm_bytes / (conv_ms * 1e-3) / 1e9, 1)},
+                         "hbm_GBps": round(hbm_bytes / (conv_ms * 1e-3) / 1e9, 1),
+                         "hbm_frac": round(hbm_bytes / (conv_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         # time at each peak: bf16 sits between the two (HBM's floor the higher), f32 is MFMA-bound
+                         "floor_ms": {"mfma": round(flops / (MFMA_PEAK_TFS[dname] * 1e12) * 1e3, 4),
+                                      "hbm": round(hbm_bytes / (HBM_PEAK_GBS * 1e9) * 1e3, 4)}},
             "unfused": {"pull_ms": round(pull_ms, 4), "conv_ms": round(uconv_ms, 4),
                         "total_ms": round(pull_ms + uconv_ms, 4), "fused_conv_ms": round(conv_ms, 4),
                         "bitwise_equal": same},

@@ -522,6 +522,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 // transposed reads per 18 MFMAs. G rows outside the band read zeros (exact
 // zero products). Per wave one f32 partial of the 9 x 32 x 32 tile; two
 // fixed-order reductions (f64) give dW: deterministic.
+#ifndef SHPL_WG_PROBE
+#define SHPL_WG_PROBE 0
+#endif
 constexpr int WX_PIECES = HWD * 4;                  // X row: 34 pixels x 4 pieces of 8 channels
 constexpr int WG_PIECES = TW * 4;                   // G row: 32 pixels x 4 pieces
 constexpr int WSLOT = (WX_PIECES + WG_PIECES) * 16;  // 4224 B
@@ -586,6 +589,7 @@ __device__ __forceinline__ void wstep(const WgRowArgs &r, f32x16 (&acc)[9], bf16
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done before the DMAs refill it
     const int jn = j + RING, y = ya - 1 + jn;
+    if (SHPL_WG_PROBE == 1) return;  // timing probe: no staging in the loop (wrong results)
     wstage(r, xsrc, xstride, frame_row0 + (int64_t)y * r.w + x0 - 1, jn < n_in && y >= 0 && y < r.h,
            frame_row0 + (int64_t)(ya + jn) * r.w + x0, jn < n_out, offx, offg, s_ring + U * WSLOT, lane);
 }
