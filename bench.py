@@ -743,8 +743,12 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
     u_pix = int(torch.unique(pl.pix[pl.pix >= 0]).numel())
     Hi, Wi = spec.img_feat_hw
     px = F * Hb * Wb * esz
-    hbm_bytes = (px * (ci + (cb + ci + ci) + 2 * ci + 2 * ci + 3 * ci + (ci + cb + ci) + (cb + ci + ci))
-                 + F * Hi * Wi * ci * esz + (u_pix + u_cell) * ci * esz + 2 * 12 * nnz)
+    if esz == 2:  # bf16: both convs gather the pooled rows (compact per-run buffer), bv_fused is never stored
+        hbm_bytes = (px * ((cb + ci) + 2 * ci + 2 * ci + 3 * ci + (ci + cb + ci) + (cb + ci))
+                     + F * Hi * Wi * ci * esz + (2 * u_pix + u_cell) * ci * esz + 3 * 12 * nnz)
+    else:  # f32: the pooled map written once in the forward, read by the forward and the weight gradient
+        hbm_bytes = (px * (ci + (cb + ci + ci) + 2 * ci + 2 * ci + 3 * ci + (ci + cb + ci) + (cb + ci + ci))
+                     + F * Hi * Wi * ci * esz + (u_pix + u_cell) * ci * esz + 2 * 12 * nnz)
     hbm_gbs = hbm_bytes / step_s / 1e9
     # the bound: the larger of the two floors (f32: MFMA; bf16: HBM)
     hbm_bound = hbm_bytes / (HBM_PEAK_GBS * 1e9) > flops / (MFMA_PEAK_TFS[dname] * 1e12)
@@ -756,8 +760,9 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
             "higher_is_better": True, "scaling": args.partition, "vs_baseline": None, "dtype": dname,
             "data": "synthetic (seeded KITTI-shaped frames, xavier-initialised conv weights)",
             "config": {"workload": (f"conv training: config2 -> index -> conv3x3 {cb + ci}->{ci} + BatchNorm (batch "
-                                    "statistics) + ReLU of [bev || pool(img)] (the pooled map built once in the forward, "
-                                    "reused by the weight gradient), backward to bev, img, weights, beta"),
+                                    "statistics) + ReLU of [bev || pool(img)] (bf16: pooling inside the forward conv and "
+                                    "the weight gradient, bv_fused never stored; f32: the pooled map built once in the "
+                                    "forward, reused by the weight gradient), backward to bev, img, weights, beta"),
                        "global_batch": F * world, "frames_per_gpu_per_step": F, "hip_graph": False,
                        "bn_statistics": "per rank (no cross-rank sync)", "parallelism": f"frame-sharded x{world}"},
             "roofline": ({"bound": "hbm", "kernel": "the whole forward + backward step: algorithmic bytes of its passes "

@@ -425,10 +425,13 @@ int shpl_conv3x3_dgrad(int dtype, int n_frames, int64_t h, int64_t w, const void
 /* Weight gradient: dw[ky][kx][ci][co] = sum over pixels of x[p + (ky-1, kx-1)][ci]
  * * gy[p][co], x given exactly as shpl_conv3x3's input (A channels, then B
  * channels, dense or pooled from the CSR -- recomputed, never stored). f32
- * MFMA (bf16 inputs widened), per-workgroup partials summed in a fixed order
- * (f64): deterministic. d_dw: f32 HWIO [3][3][c_a+c_b][c_out]. */
+ * MFMA (bf16: bf16 MFMA, exact products, f32 accumulation), per-workgroup
+ * partials summed in a fixed order (f64): deterministic. d_dw: f32 HWIO
+ * [3][3][c_a+c_b][c_out]. Workspace: pool_nnz_cap as shpl_conv3x3's (-1: B
+ * dense or absent; with a pool, its CSR's nnz_cap, which sizes the compact
+ * buffer of pooled runs of the bf16 form). */
 int shpl_conv3x3_wgrad_workspace_bytes(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_t c_b,
-                                       int64_t c_out, int pooled, size_t *bytes);
+                                       int64_t c_out, int64_t pool_nnz_cap, size_t *bytes);
 int shpl_conv3x3_wgrad(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a, int64_t a_stride,
                        int64_t a_off, int64_t c_a, const void *d_b, int64_t b_stride, int64_t b_off, int64_t c_b,
                        const shpl_csr *pool, const int64_t *d_frame_off, const void *d_gy, int64_t gy_stride,

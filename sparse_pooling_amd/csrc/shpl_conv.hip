@@ -1895,13 +1895,13 @@ struct WgPlan {
     ConvPlan cp;
     int n_cib, n_groups, tiles_per_group;
     size_t rp_bytes, part_bytes, total;
-    bool rows;  // bf16, dense: k_wgrad_rows when the pointers are 16-byte aligned
+    bool rows;  // bf16: k_wgrad_rows when the pointers are 16-byte aligned
     int r_groups;
-    size_t r_part_bytes, r_part2_bytes;
+    size_t r_part_bytes, r_part2_bytes, r_occ_bytes, r_cmp_bytes;
 };
 
 int wgrad_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_t c_b, int64_t c_out, bool pooled,
-               WgPlan *wp) {
+               WgPlan *wp, int64_t pool_cap = 0) {
     int rc = conv_plan(dtype, n_frames, h, w, c_a, c_b, c_out, pooled, false, &wp->cp, TH);
     if (rc) return rc;
     const int Q = wp->cp.qa + wp->cp.qb;
@@ -1920,14 +1920,20 @@ int wgrad_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64
     // the row-streaming bf16 weight gradient: bands and strips of the forward's row kernel
     const int n_bands = (int)((h + 59) / 60);
     const int64_t n_items = (int64_t)n_frames * n_bands * ((w + TW - 1) / TW);
-    wp->rows = SHPL_CONV_ROWS && dtype == SHPL_BF16 && !pooled && h > 0 && w > 0 && n_items > 0 &&
-               n_items < (1LL << 31) && rows::wgrad_supported((int)c_a, (int)c_b, (int)c_out);
+    // pooled: B gathered from the compact pooled rows of prep_pooled (the forward's k_occ_frame + k_pool_runs)
+    const int64_t wpr = (w + 31) / 32;
+    wp->rows = SHPL_CONV_ROWS && dtype == SHPL_BF16 && h > 0 && w > 0 && n_items > 0 && n_items < (1LL << 31) &&
+               rows::wgrad_supported((int)c_a, (int)c_b, (int)c_out) &&
+               (!pooled || (c_a > 0 && c_b <= 64 && h * wpr <= rows::OCC_MAX_WORDS && pool_cap >= 0 &&
+                            pool_cap * c_b * 2 < (1LL << 31)));
     if (wp->rows) {
         rows::wgrad_sizes((int)n_items, (int)c_a, (int)c_b, (int)c_out, &wp->r_groups, &wp->r_part_bytes,
                           &wp->r_part2_bytes);
         wp->r_part_bytes = align_up(wp->r_part_bytes, 256);
         wp->r_part2_bytes = align_up(wp->r_part2_bytes, 256);
-        const size_t rt = wp->r_part_bytes + wp->r_part2_bytes;
+        wp->r_occ_bytes = pooled ? 2 * align_up((size_t)n_frames * h * wpr * 4, 256) : 0;
+        wp->r_cmp_bytes = pooled ? align_up((size_t)pool_cap * c_b * 2, 256) : 0;
+        const size_t rt = wp->r_part_bytes + wp->r_part2_bytes + wp->r_occ_bytes + wp->r_cmp_bytes;
         if (rt > wp->total) wp->total = rt;
     }
     return SHPL_OK;
@@ -1935,10 +1941,11 @@ int wgrad_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64
 }  // namespace
 
 extern "C" int shpl_conv3x3_wgrad_workspace_bytes(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a,
-                                                  int64_t c_b, int64_t c_out, int pooled, size_t *bytes) {
+                                                  int64_t c_b, int64_t c_out, int64_t pool_nnz_cap, size_t *bytes) {
     if (!bytes) return SHPL_ERR_ARG;
     WgPlan wp;
-    const int rc = wgrad_plan(dtype, n_frames, h, w, c_a, c_b, c_out, pooled != 0, &wp);
+    const bool pooled = pool_nnz_cap >= 0;
+    const int rc = wgrad_plan(dtype, n_frames, h, w, c_a, c_b, c_out, pooled, &wp, pooled ? pool_nnz_cap : 0);
     if (rc) return rc;
     *bytes = wp.total;
     return SHPL_OK;
@@ -1951,7 +1958,7 @@ extern "C" int shpl_conv3x3_wgrad(int dtype, int n_frames, int64_t h, int64_t w,
                                   void *stream) {
     const bool pooled = pool != nullptr;
     WgPlan wp;
-    int rc = wgrad_plan(dtype, n_frames, h, w, c_a, c_b, c_out, pooled, &wp);
+    int rc = wgrad_plan(dtype, n_frames, h, w, c_a, c_b, c_out, pooled, &wp, pooled ? pool->nnz_cap : 0);
     if (rc) return rc;
     if (!d_dw || (ws_bytes > 0 && !d_ws)) return SHPL_ERR_ARG;
     if (ws_bytes < wp.total) return SHPL_ERR_WORKSPACE;
@@ -1974,7 +1981,7 @@ extern "C" int shpl_conv3x3_wgrad(int dtype, int n_frames, int64_t h, int64_t w,
     }
     if (wp.rows && (c_a == 0 || (aligned16(d_a) && a_stride % he == 0 && a_off % he == 0)) &&
         (c_b == 0 || (aligned16(d_b) && b_stride % he == 0 && b_off % he == 0)) && aligned16(d_gy) &&
-        gy_stride % he == 0) {
+        gy_stride % he == 0 && (!pooled || c_a % 32 == 0)) {
         rows::WgRowArgs r = {};
         r.a = reinterpret_cast<const uint16_t *>(d_a) + a_off;
         r.b = c_b > 0 ? reinterpret_cast<const uint16_t *>(d_b) + b_off : nullptr;
@@ -1996,6 +2003,24 @@ extern "C" int shpl_conv3x3_wgrad(int dtype, int n_frames, int64_t h, int64_t w,
         r.n_groups = wp.r_groups;
         uint8_t *ws = reinterpret_cast<uint8_t *>(d_ws);
         r.part = reinterpret_cast<float *>(ws);
+        if (pooled) {  // the pooled vector of every run once into the compact buffer (the forward's prep)
+            uint8_t *po = ws + wp.r_part_bytes + wp.r_part2_bytes;
+            uint32_t *occ = reinterpret_cast<uint32_t *>(po);
+            int32_t *occ_base = reinterpret_cast<int32_t *>(po + wp.r_occ_bytes / 2);
+            uint16_t *cmp = reinterpret_cast<uint16_t *>(po + wp.r_occ_bytes);
+            const int wpr = (int)((w + 31) / 32);
+            rc = rows::prep_pooled(n_frames, (int)h, (int)w, wpr, pool->ent_dst, pool->ent_src, pool->ent_val,
+                                   pool->nnz_cap, d_frame_off, reinterpret_cast<const uint16_t *>(d_b), b_stride,
+                                   b_off, (int)c_b, occ, occ_base, cmp, s);
+            if (rc) return rc;
+            r.b = nullptr;
+            r.cmp = cmp;
+            r.cmp_stride = (int)c_b;
+            r.occ = occ;
+            r.occ_base = occ_base;
+            r.wpr = wpr;
+            r.frame_off = d_frame_off;
+        }
         return rows::wgrad_launch(r, d_dw, reinterpret_cast<double *>(ws + wp.r_part_bytes), s);
     }
     ConvArgs a = {};

@@ -59,6 +59,14 @@ struct WgRowArgs {
     int h, w, strips, band, n_bands, n_items;
     int n_cit, n_cot, n_groups;
     float *part;  // [group][cot][cit][9][32 co][32 ci]
+    // pooled B (cmp set): the compact pooled rows of prep_pooled (cmp_stride = c_b channels per row), their
+    // occupancy words and prefix counts, the frames' entry slots
+    const uint16_t *cmp;
+    int cmp_stride;
+    const uint32_t *occ;
+    const int32_t *occ_base;
+    int wpr;
+    const int64_t *frame_off;
 };
 
 bool wgrad_supported(int c_a, int c_b, int c_out);

@@ -277,7 +277,7 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
                                      const uint64_t *s_occ, const int32_t *s_first, uint64_t b_rows,
                                      const uint32_t (&offa)[Layout<Q, QA>::NA],
                                      const int32_t (&offb)[Layout<Q, QA>::NB > 0 ? Layout<Q, QA>::NB : 1],
-                                     int lane) {
+                                     const uint32_t *s_offs, int lane) {
     typedef Layout<Q, QA, ST> L;
     // rows j+1 .. j+RING-1 may still be in flight: per later step RSTORES stores and NDMA DMAs
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L::NDMA + RSTORES) * (RING - 1)) : "memory");
@@ -393,7 +393,14 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
         occ = s_occ[jn];
         first = s_first[jn];
     }
-    stage<Q, QA, CMP>(r, frame_row0 + (int64_t)y * r.w + x0 - 1, live && y >= 0 && y < r.h, occ, first, offa, offb,
+    // the pooled form with statistics keeps the lane offsets in LDS (OFFL: 6 VGPRs it does not have)
+    uint32_t oa[L::NA];
+    int32_t ob[L::NB > 0 ? L::NB : 1];
+#pragma unroll
+    for (int i = 0; i < L::NA; ++i) oa[i] = (ST && CMP) ? s_offs[i * 64 + lane] : offa[i];
+#pragma unroll
+    for (int i = 0; i < (L::NB > 0 ? L::NB : 1); ++i) ob[i] = (ST && CMP) ? (int32_t)s_offs[(L::NA + i) * 64 + lane] : offb[i];
+    stage<Q, QA, CMP>(r, frame_row0 + (int64_t)y * r.w + x0 - 1, live && y >= 0 && y < r.h, occ, first, oa, ob,
                       s_ring + U * L::SLOT, lane);
 }
 
@@ -460,6 +467,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     uint32_t offa[L::NA];
     int32_t offb[L::NB > 0 ? L::NB : 1];
     lane_offsets<Q, QA, CMP>(r, x0, lane, offa, offb);
+    __shared__ uint32_t s_offs[(ST && CMP) ? (L::NA + L::NB) * 64 : 1];
+    if constexpr (ST && CMP) {
+#pragma unroll
+        for (int i = 0; i < L::NA; ++i) s_offs[i * 64 + lane] = offa[i];
+#pragma unroll
+        for (int i = 0; i < L::NB; ++i) s_offs[(L::NA + i) * 64 + lane] = (uint32_t)offb[i];
+    }
     // prologue: input rows 0 .. RING-1 in flight
 #pragma unroll
     for (int j = 0; j < RING; ++j) {
@@ -486,7 +500,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #define SHPL_ROWS_STEP(UU)                                                                                          \
     if (j + UU >= n_in) break;                                                                                      \
     step<Q, QA, CMP, RELU, ST, UU>(r, wr, acc, s_par, rd, s_ring, frame_row0, x0, ya, n_in, n_out, obase, ostr, s_st, \
-                                   j + UU, s_occ, s_first, b_rows, offa, offb, lane);
+                                   j + UU, s_occ, s_first, b_rows, offa, offb, s_offs, lane);
         SHPL_ROWS_STEP(0)
         SHPL_ROWS_STEP(1)
         SHPL_ROWS_STEP(2)
@@ -557,24 +571,42 @@ __device__ __forceinline__ bf16x8 tr_frag(const uint8_t *lb) {
     return out;
 }
 
+// pooled: X is the tile of the compact pooled rows (k_pool_runs): offx holds pixel << 16 | channel (-1: outside),
+// cell pixel px of the row holds run  first + popc(occ below bit px)  when bit px of occ is set, else zeros.
+template <bool CMP>
 __device__ __forceinline__ void wstage(const WgRowArgs &r, const uint16_t *xsrc, int64_t xstride, int64_t pix0,
                                        bool xok, int64_t gpix, bool gok, const uint32_t (&offx)[WNX],
-                                       const uint32_t (&offg)[WNG], uint8_t *slot, int lane) {
-    const i32x4 rx = rsrc(xsrc + pix0 * xstride, xok ? OOB : 0u);
+                                       const uint32_t (&offg)[WNG], uint8_t *slot, int lane, bool pooled,
+                                       uint64_t occ, int32_t first) {
+    if (CMP && pooled) {
+        const i32x4 rx = rsrc(r.cmp, xok ? OOB : 0u);
 #pragma unroll
-    for (int i = 0; i < WNX; ++i)
-        if (i < WNX - 1 || lane < WTX) dma16(rx, offx[i], slot + i * 1024);
+        for (int i = 0; i < WNX; ++i) {
+            const int32_t e = (int32_t)offx[i];
+            const int px = (e >> 16) & 63;
+            const bool hit = e >= 0 && ((occ >> px) & 1);
+            const int rank = first + (int)__popcll(occ & ((1ull << px) - 1));
+            const uint32_t o = hit ? (uint32_t)((rank * r.cmp_stride + (e & 0xffff)) * 2) : OOB;
+            if (i < WNX - 1 || lane < WTX) dma16(rx, o, slot + i * 1024);
+        }
+    } else {
+        const i32x4 rx = rsrc(xsrc + pix0 * xstride, xok ? OOB : 0u);
+#pragma unroll
+        for (int i = 0; i < WNX; ++i)
+            if (i < WNX - 1 || lane < WTX) dma16(rx, offx[i], slot + i * 1024);
+    }
     const i32x4 rg = rsrc(r.gy + gpix * r.gy_stride, gok ? OOB : 0u);
 #pragma unroll
     for (int i = 0; i < WNG; ++i) dma16(rg, offg[i], slot + WX_PIECES * 16 + i * 1024);
 }
 
 // One input row j of the band (slot U = j % 3): 16 transposed reads, 18 MFMAs, then row j + 3 staged.
-template <int U>
+template <bool CMP, int U>
 __device__ __forceinline__ void wstep(const WgRowArgs &r, f32x16 (&acc)[9], bf16x8 (&g1)[2], bf16x8 (&g2)[2],
                                       uint8_t *s_ring, const uint8_t *lb, const uint16_t *xsrc, int64_t xstride,
                                       int64_t frame_row0, int x0, int ya, int n_in, int n_out, int j,
-                                      const uint32_t (&offx)[WNX], const uint32_t (&offg)[WNG], int lane) {
+                                      const uint32_t (&offx)[WNX], const uint32_t (&offg)[WNG], int lane,
+                                      bool pooled, const uint64_t *s_occ, const int32_t *s_first) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WNDMA * 2) : "memory");  // rows j+1, j+2 may still be in flight
     const uint8_t *xs = lb + U * WSLOT, *gs = xs + WX_PIECES * 16;
     bf16x8 g0[2];
@@ -599,12 +631,22 @@ __device__ __forceinline__ void wstep(const WgRowArgs &r, f32x16 (&acc)[9], bf16
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done before the DMAs refill it
     const int jn = j + RING, y = ya - 1 + jn;
     if (SHPL_WG_PROBE == 1) return;  // timing probe: no staging in the loop (wrong results)
-    wstage(r, xsrc, xstride, frame_row0 + (int64_t)y * r.w + x0 - 1, jn < n_in && y >= 0 && y < r.h,
-           frame_row0 + (int64_t)(ya + jn) * r.w + x0, jn < n_out, offx, offg, s_ring + U * WSLOT, lane);
+    uint64_t occ = 0;
+    int32_t first = 0;
+    if (CMP && pooled && jn < n_in) {
+        occ = s_occ[jn];
+        first = s_first[jn];
+    }
+    wstage<CMP>(r, xsrc, xstride, frame_row0 + (int64_t)y * r.w + x0 - 1, jn < n_in && y >= 0 && y < r.h,
+                frame_row0 + (int64_t)(ya + jn) * r.w + x0, jn < n_out, offx, offg, s_ring + U * WSLOT, lane, pooled,
+                occ, first);
 }
 
+template <bool CMP>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_wgrad_rows(const WgRowArgs r) {
     __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING * WSLOT];
+    __shared__ uint64_t s_occ[CMP ? 64 : 1];  // pooled tile: the band rows' occupancy windows (as k_conv_rows)
+    __shared__ int32_t s_first[CMP ? 64 : 1];
     const int lane = threadIdx.x;
     const int n_tiles = r.n_cit * r.n_cot, total = r.n_groups * n_tiles;
     // (group, output tile, input tile), input tiles fastest (they share the G rows), each XCD one contiguous run
@@ -618,6 +660,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const uint16_t *xsrc = from_a ? r.a + cit * 32 : r.b + (cit - na) * 32;
     const int64_t xstride = from_a ? r.a_stride : r.b_stride;
     const int cn = from_a ? r.c_a - cit * 32 : r.c_b - (cit - na) * 32;  // channels of the tile (>= 32: whole)
+    const bool pooled = CMP && !from_a;  // B pooled from the image through the cell-keyed CSR
     const int cg = r.c_out - cot * 32;
     const uint16_t *gsrc = r.gy + cot * 32;
     WgRowArgs rr = r;
@@ -643,7 +686,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         for (int i = 0; i < WNX; ++i) {
             const int pc = 64 * i + lane, px = pc >> 2, cq = pc & 3, x = x0 - 1 + px;
             const bool ok = pc < WX_PIECES && x >= 0 && x < r.w && 8 * cq < cn;
-            offx[i] = ok ? (uint32_t)((px * (int)xstride + 8 * cq) * 2) : OOB;
+            if (pooled)
+                offx[i] = ok ? (uint32_t)((px << 16) | ((cit - na) * 32 + 8 * cq)) : 0xffffffffu;
+            else
+                offx[i] = ok ? (uint32_t)((px * (int)xstride + 8 * cq) * 2) : OOB;
+        }
+        if (pooled) {  // lane j: halo row j's window (cells x0-1 .. x0+32 as bits 0..33) and its first run
+            const int y = ya - 1 + lane, w0 = x0 >> 5;
+            uint64_t occ_row = 0;
+            int32_t first_row = 0;
+            if (lane < n_in && y >= 0 && y < r.h) {
+                const int64_t wrow = ((int64_t)f * r.h + y) * r.wpr;
+                const uint32_t ml = w0 > 0 ? r.occ[wrow + w0 - 1] : 0u, mc = r.occ[wrow + w0];
+                const uint32_t mr = w0 + 1 < r.wpr ? r.occ[wrow + w0 + 1] : 0u;
+                const int32_t bs = r.occ_base[wrow + (w0 > 0 ? w0 - 1 : w0)];
+                occ_row = (uint64_t)(ml >> 31) | ((uint64_t)mc << 1) | ((uint64_t)(mr & 1u) << 33);
+                first_row = (int32_t)r.frame_off[f] + bs + (w0 > 0 ? __popc(ml & 0x7fffffffu) : 0);
+            }
+            s_occ[lane] = occ_row;
+            s_first[lane] = first_row;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own LDS writes, in order
         }
 #pragma unroll
         for (int i = 0; i < WNG; ++i) {
@@ -653,8 +715,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
         for (int j = 0; j < RING; ++j) {
             const int y = ya - 1 + j;
-            wstage(rr, xsrc, xstride, frame_row0 + (int64_t)y * r.w + x0 - 1, j < n_in && y >= 0 && y < r.h,
-                   frame_row0 + (int64_t)(ya + j) * r.w + x0, j < n_out, offx, offg, s_ring + j * WSLOT, lane);
+            wstage<CMP>(rr, xsrc, xstride, frame_row0 + (int64_t)y * r.w + x0 - 1, j < n_in && y >= 0 && y < r.h,
+                        frame_row0 + (int64_t)(ya + j) * r.w + x0, j < n_out, offx, offg, s_ring + j * WSLOT, lane,
+                        pooled, pooled ? s_occ[j] : 0, pooled ? s_first[j] : 0);
         }
         bf16x8 g1[2], g2[2];
 #pragma unroll
@@ -664,8 +727,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         for (int j = 0; j < n_in; j += RING) {
 #define SHPL_WROWS_STEP(UU)                                                                                  \
     if (j + UU >= n_in) break;                                                                               \
-    wstep<UU>(rr, acc, g1, g2, s_ring, lb, xsrc, xstride, frame_row0, x0, ya, n_in, n_out, j + UU, offx, offg, \
-              lane);
+    wstep<CMP, UU>(rr, acc, g1, g2, s_ring, lb, xsrc, xstride, frame_row0, x0, ya, n_in, n_out, j + UU, offx, offg, \
+                   lane, pooled, s_occ, s_first);
             SHPL_WROWS_STEP(0)
             SHPL_WROWS_STEP(1)
             SHPL_WROWS_STEP(2)
@@ -723,9 +786,12 @@ bool supported(int q, int qa) {
     return qa == q || q - qa >= 1;
 }
 
-// Statistics: dense sources only, and not at 3 chunks from two sources (those spill at 256 VGPRs; the
-// pooled form spills too -- its callers materialise the pooled map, which their backward needs anyway).
-bool supported_st(int q, int qa, bool cmp) { return supported(q, qa) && !cmp && !(q == 3 && qa < 3); }
+// Statistics: not at 3 chunks from two sources (those spill at 256 VGPRs); pooled at 2 + 2 and 1 + 1 chunks
+// (the lane offsets in LDS).
+bool supported_st(int q, int qa, bool cmp) {
+    if (!supported(q, qa)) return false;
+    return cmp ? (q == 4 && qa == 2) || (q == 2 && qa == 1) : !(q == 3 && qa < 3);
+}
 
 int prep_pooled(int n_frames, int h, int w, int wpr, const int32_t *ent_dst, const int32_t *ent_src,
                 const float *ent_val, int64_t nnz_cap, const int64_t *frame_off, const uint16_t *img,
@@ -790,6 +856,8 @@ int launch(const RowArgs &r, int q, int qa, bool cmp, bool relu, bool st, hipStr
         SHPL_ROWS_CASE(4, 1, 0, 0, 1)
         SHPL_ROWS_CASE(4, 2, 0, 0, 1)
         SHPL_ROWS_CASE(4, 3, 0, 0, 1)
+        SHPL_ROWS_CASE(2, 1, 1, 0, 1)
+        SHPL_ROWS_CASE(4, 2, 1, 0, 1)
 #undef SHPL_ROWS_TWO
 #undef SHPL_ROWS_DENSE
 #undef SHPL_ROWS_CASE
@@ -820,7 +888,10 @@ void wgrad_sizes(int n_items, int c_a, int c_b, int c_out, int *n_groups, size_t
 
 int wgrad_launch(const WgRowArgs &r, float *dw, double *part2, hipStream_t s) {
     const int total = r.n_groups * r.n_cit * r.n_cot;
-    hipLaunchKernelGGL(k_wgrad_rows, dim3((unsigned)total), dim3(64), 0, s, r);
+    if (r.cmp)
+        hipLaunchKernelGGL(k_wgrad_rows<true>, dim3((unsigned)total), dim3(64), 0, s, r);
+    else
+        hipLaunchKernelGGL(k_wgrad_rows<false>, dim3((unsigned)total), dim3(64), 0, s, r);
     SHPL_LAUNCH_CHECK();
     const int64_t n_ent = (int64_t)r.n_cit * r.n_cot * 9 * 1024;
     const int n_chunks = (r.n_groups + WGC - 1) / WGC;

@@ -159,7 +159,7 @@ def conv3x3_wgrad(a, gy, b=None, pool=None, frame_off=None):
     Cout = int(gy.shape[-1])
     dw = torch.empty((3, 3, Ca + Cb, Cout), dtype=torch.float32, device=a.device)
     nb = ctypes.c_size_t()
-    L.check(L.lib().shpl_conv3x3_wgrad_workspace_bytes(dt, B, H, W, Ca, Cb, Cout, int(pool is not None),
+    L.check(L.lib().shpl_conv3x3_wgrad_workspace_bytes(dt, B, H, W, Ca, Cb, Cout, -1 if pool is None else pool.nnz_cap,
                                                        ctypes.byref(nb)), "shpl_conv3x3_wgrad_workspace_bytes")
     ws = L.workspace(nb.value, a.device)
     L.check(L.lib().shpl_conv3x3_wgrad(dt, B, H, W, L.ptr(a), Ca, 0, Ca, L.ptr(b), Cb, 0, Cb,
@@ -185,10 +185,9 @@ class _FusionConvFn(torch.autograd.Function):
         frame_off = smap.frame_off if pooled else None
         train_bn = conv.batch_norm and is_training
         xb, b_img = None, b
-        if pooled and train_bn and ctx.needs_input_grad[2]:
-            # the weight gradient needs the pooled channels in HBM (see backward): pooled here, once, the
-            # forward is the dense two-source conv whose statistics epilogue runs on the row-streaming
-            # bf16 kernel (the pooled form spills there)
+        if pooled and train_bn and ctx.needs_input_grad[2] and a.dtype != torch.bfloat16:
+            # f32: the weight gradient needs the pooled channels in HBM (see backward): pooled here, once, the
+            # forward is the dense two-source conv (bf16 pools inside both convs: k_conv_rows / k_wgrad_rows)
             xb = sm.pool_img_to_bev(smap, b, (B, H, W, Cb))
             b, pool, frame_off = xb, None, None
         cap = pool.nnz_cap if pool is not None else None
@@ -247,8 +246,11 @@ class _FusionConvFn(torch.autograd.Function):
             if not ctx.needs_input_grad[0]:
                 d_a = None
         if ctx.needs_input_grad[2]:
-            if pooled:
-                # the pooled channels once into HBM (shpl_pull): the dense two-source weight gradient
+            if pooled and a.dtype == torch.bfloat16:
+                # k_wgrad_rows gathers the pooled rows from a compact per-run buffer: bv_fused never stored
+                dw = conv3x3_wgrad(a, g_raw, b=b, pool=smap.csr(L.BY_CELL, L.ORDER_ENTRY), frame_off=smap.frame_off)
+            elif pooled:
+                # f32: the pooled channels once into HBM (shpl_pull): the dense two-source weight gradient
                 # runs at twice the waves per SIMD of the one that recomputes them per tile (257 vs
                 # 214 registers); conv3x3_wgrad(..., pool=...) stays the memory-lean form
                 xb = ctx.xb if ctx.xb is not None else sm.pool_img_to_bev(smap, b, tuple(a.shape[:3]) + (Cb,))

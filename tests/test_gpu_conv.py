@@ -327,6 +327,42 @@ def test_bf16_rows_conv_stats(shape):
         np.testing.assert_array_equal(_np(st2), s)
 
 
+@pytest.mark.parametrize("cb,ci", [(32, 32), (16, 16)])
+def test_bf16_rows_pooled_stats_and_wgrad(cb, ci):
+    """The bf16 training pair without bv_fused: the pooled forward with the
+    statistics epilogue (k_conv_rows, compact run buffer, lane offsets in LDS)
+    and the pooled weight gradient (k_wgrad_rows gathering the same compact
+    rows) are bitwise the dense two-source forms over the materialised pooled
+    map (config 2 geometry, two frames; 16 + 16 -> 32 takes the 1 + 1 chunk
+    instantiation). The dense forms are checked against the oracle elsewhere."""
+    from sparse_pooling_amd import fusion_conv as fc, shpl_map as sm
+    spec, frames, ib = _batch_map(2, 2, 800)
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    bev = orc.from_bf16_bits(orc.to_bf16_bits(synth.make_features((2, Hb, Wb, cb), 81)))
+    img = orc.from_bf16_bits(orc.to_bf16_bits(synth.make_features((2, Hi, Wi, ci), 82)))
+    w = orc.from_bf16_bits(orc.to_bf16_bits(_weights(cb + ci, 32, 83)))
+    tb, ti, tw = _bf16(bev), _bf16(img), _bf16(w)
+    csr, foff = ib.map.csr(0, 0), ib.map.frame_off
+    xb = sm.pool_img_to_bev(ib.map, ti, (2, Hb, Wb, ci))
+    st_f = torch.empty((2, 32), dtype=torch.float64, device=DEV)
+    st_d = torch.empty_like(st_f)
+    y_f = fc.conv3x3(tb, tw, b=ti, pool=csr, frame_off=foff, relu=False, stats=st_f)
+    y_d = fc.conv3x3(tb, tw, b=xb, relu=False, stats=st_d)
+    torch.cuda.synchronize()
+    assert ib.map.error_bits() == 0
+    assert torch.equal(y_f, y_d)
+    assert torch.equal(st_f, st_d)
+    g = _bf16(synth.make_features((2, Hb, Wb, 32), 84))
+    dw_f = fc.conv3x3_wgrad(tb, g, b=ti, pool=csr, frame_off=foff)
+    dw_d = fc.conv3x3_wgrad(tb, g, b=xb)
+    if cb % 32 == 0:
+        assert torch.equal(dw_f, dw_d)
+    else:  # A ends inside an input tile: the tiled kernels (their own summation orders), within the f32 bound
+        ab = fc.conv3x3_wgrad(tb.abs(), g.abs(), b=xb.abs())
+        _assert_within(dw_f, _np(dw_d).astype(np.float64), 1e-5 + 2.0 ** -15 * _np(ab))
+
+
 def test_bf16_rows_fused_config2():
     """Config 2 in bf16 (32 + 32 -> 32 channels: k_conv_rows with the pooled
     half gathered from the compact run buffer): fused == the conv of the
