@@ -831,10 +831,12 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_apply(const T *x, T *y, int64
 // apply 2.68 -> 2.35 ms; bf16 at 2 rows per thread was 1.7x slower than at 8.
 constexpr int64_t bn_rows_per_thread(int esz) { return esz == 4 ? 4 : 8; }
 
+// 16-byte pieces of the BatchNorm streams, nontemporal (each byte is touched
+// once per pass; the maps are far larger than the caches).
 template <typename T, int VEC>
 struct Piece {
     static __device__ __forceinline__ void load(const T *p, float (&x)[VEC]) {
-        const u32x4 r = *reinterpret_cast<const u32x4 *>(p);
+        const u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
         T e[VEC];
         __builtin_memcpy(e, &r, 16);
 #pragma unroll
@@ -846,9 +848,11 @@ struct Piece {
         for (int k = 0; k < VEC; ++k) e[k] = Elem<T>::back(x[k]);
         u32x4 r;
         __builtin_memcpy(&r, e, 16);
-        *reinterpret_cast<u32x4 *>(p) = r;
+        __builtin_nontemporal_store(r, reinterpret_cast<u32x4 *>(p));
     }
 };
+
+constexpr int BN_U = 4;  // rows per iteration of the vector apply kernels: their loads in flight together
 
 // Thread layout of the vector forms: c / VEC piece lanes (a power of two
 // dividing the block) times SHPL_BLOCK / (c / VEC) row lanes, so each thread
@@ -867,16 +871,23 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_apply_vec(const T *x, T *y, i
         sc[k] = scale[ch0 + k];
         b[k] = beta ? beta[ch0 + k] : 0.0f;
     }
-    for (int64_t r = (int64_t)blockIdx.x * rpb + threadIdx.x / pr; r < rows; r += (int64_t)gridDim.x * rpb) {
-        float v[VEC];
-        Piece<T, VEC>::load(x + r * stride + ch0, v);
+    const int64_t step = (int64_t)gridDim.x * rpb;
+    for (int64_t r0 = (int64_t)blockIdx.x * rpb + threadIdx.x / pr; r0 < rows; r0 += BN_U * step) {
+        float v[BN_U][VEC];
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            float u = __fmul_rn(__fsub_rn(v[k], m[k]), sc[k]);
-            if (beta) u = __fadd_rn(u, b[k]);
-            v[k] = (act == 1 && !(u > 0.0f)) ? 0.0f : u;
+        for (int u = 0; u < BN_U; ++u)
+            if (r0 + u * step < rows) Piece<T, VEC>::load(x + (r0 + u * step) * stride + ch0, v[u]);
+#pragma unroll
+        for (int u = 0; u < BN_U; ++u) {
+            if (r0 + u * step >= rows) break;
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                float t = __fmul_rn(__fsub_rn(v[u][k], m[k]), sc[k]);
+                if (beta) t = __fadd_rn(t, b[k]);
+                v[u][k] = (act == 1 && !(t > 0.0f)) ? 0.0f : t;
+            }
+            Piece<T, VEC>::store(y + (r0 + u * step) * stride + ch0, v[u]);
         }
-        Piece<T, VEC>::store(y + r * stride + ch0, v);
     }
 }
 
@@ -972,22 +983,32 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_partial_vec(const T *y, c
     double s1[VEC], s2[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) s1[k] = s2[k] = 0.0;
-    for (int64_t r = r0 + rl; r < r1; r += rl_n) {
-        const int64_t o = r * stride + ch0;
-        float gv[VEC], xv[VEC], yv[VEC];
-        Piece<T, VEC>::load(gy + o, gv);
-        Piece<T, VEC>::load(raw + o, xv);
-        if (act == 1 && y) Piece<T, VEC>::load(y + o, yv);
+    constexpr int U = BN_U / 2;
+    for (int64_t rb = r0 + rl; rb < r1; rb += U * rl_n) {
+        float gv[U][VEC], xv[U][VEC], yv[U][VEC];
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            if (act == 1 && !y) {
-                const float u = __fmul_rn(__fsub_rn(xv[k], m[k]), sc[k]);
-                yv[k] = beta ? __fadd_rn(u, b[k]) : u;
+        for (int u = 0; u < U; ++u) {
+            if (rb + u * rl_n >= r1) break;
+            const int64_t o = (rb + u * rl_n) * stride + ch0;
+            Piece<T, VEC>::load(gy + o, gv[u]);
+            Piece<T, VEC>::load(raw + o, xv[u]);
+            if (act == 1 && y) Piece<T, VEC>::load(y + o, yv[u]);
+        }
+        // the sums in row order, as before
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (rb + u * rl_n >= r1) break;
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                if (act == 1 && !y) {
+                    const float t = __fmul_rn(__fsub_rn(xv[u][k], m[k]), sc[k]);
+                    yv[u][k] = beta ? __fadd_rn(t, b[k]) : t;
+                }
+                const float gb = (act == 1 && !(yv[u][k] > 0.0f)) ? 0.0f : gv[u][k];
+                const float xh = __fmul_rn(__fsub_rn(xv[u][k], m[k]), inv[k]);
+                s1[k] += (double)gb;
+                s2[k] += (double)gb * (double)xh;
             }
-            const float gb = (act == 1 && !(yv[k] > 0.0f)) ? 0.0f : gv[k];
-            const float xh = __fmul_rn(__fsub_rn(xv[k], m[k]), inv[k]);
-            s1[k] += (double)gb;
-            s2[k] += (double)gb * (double)xh;
         }
     }
 #pragma unroll
@@ -1028,27 +1049,38 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_apply_vec(const T *y, con
         t0[k] = training ? mean_terms[ch] : 0.0f;
         t1[k] = training ? mean_terms[c + ch] : 0.0f;
     }
-    for (int64_t r = (int64_t)blockIdx.x * rpb + threadIdx.x / pr; r < rows; r += (int64_t)gridDim.x * rpb) {
-        const int64_t o = r * stride + ch0;
-        float gv[VEC], yv[VEC], xv[VEC], out[VEC];
-        Piece<T, VEC>::load(gy + o, gv);
-        if (act == 1 && y) Piece<T, VEC>::load(y + o, yv);
-        if (training || !y) Piece<T, VEC>::load(raw + o, xv);
+    const int64_t step = (int64_t)gridDim.x * rpb;
+    constexpr int U = BN_U / 2;  // two or three streams in per row
+    for (int64_t r0 = (int64_t)blockIdx.x * rpb + threadIdx.x / pr; r0 < rows; r0 += U * step) {
+        float gv[U][VEC], yv[U][VEC], xv[U][VEC];
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            if (act == 1 && !y) {
-                const float u = __fmul_rn(__fsub_rn(xv[k], m[k]), sc[k]);
-                yv[k] = beta ? __fadd_rn(u, b[k]) : u;
-            }
-            const float gb = (act == 1 && !(yv[k] > 0.0f)) ? 0.0f : gv[k];
-            if (training) {
-                const float xh = __fmul_rn(__fsub_rn(xv[k], m[k]), inv[k]);
-                out[k] = __fmul_rn(sc[k], __fsub_rn(__fsub_rn(gb, t0[k]), __fmul_rn(xh, t1[k])));
-            } else {
-                out[k] = __fmul_rn(sc[k], gb);
-            }
+        for (int u = 0; u < U; ++u) {
+            if (r0 + u * step >= rows) break;
+            const int64_t o = (r0 + u * step) * stride + ch0;
+            Piece<T, VEC>::load(gy + o, gv[u]);
+            if (act == 1 && y) Piece<T, VEC>::load(y + o, yv[u]);
+            if (training || !y) Piece<T, VEC>::load(raw + o, xv[u]);
         }
-        Piece<T, VEC>::store(graw + o, out);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (r0 + u * step >= rows) break;
+            float out[VEC];
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                if (act == 1 && !y) {
+                    const float t = __fmul_rn(__fsub_rn(xv[u][k], m[k]), sc[k]);
+                    yv[u][k] = beta ? __fadd_rn(t, b[k]) : t;
+                }
+                const float gb = (act == 1 && !(yv[u][k] > 0.0f)) ? 0.0f : gv[u][k];
+                if (training) {
+                    const float xh = __fmul_rn(__fsub_rn(xv[u][k], m[k]), inv[k]);
+                    out[k] = __fmul_rn(sc[k], __fsub_rn(__fsub_rn(gb, t0[k]), __fmul_rn(xh, t1[k])));
+                } else {
+                    out[k] = __fmul_rn(sc[k], gb);
+                }
+            }
+            Piece<T, VEC>::store(graw + (r0 + u * step) * stride + ch0, out);
+        }
     }
 }
 
