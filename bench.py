@@ -615,6 +615,13 @@ def run_frames(args, world, rank, dev):
     step_bytes = (nbytes + 16 * int(fr.total_points) + 2 * 24 * n_cam + F * pl.Hb * pl.Wb * n_maps * 8
                   + 40 * n_vox + 40 * n_vox + 56 * nnz)
     step_gbs = step_bytes / (elapsed / args.steps) / 1e9
+    traffic, step_traffic = None, None  # PMC (scripts/r02_pmc.sh TAG=frames, traffic.py step frames_F64 ...)
+    tpath = os.path.join(HERE, "profiles", "traffic.json")
+    if os.path.exists(tpath):
+        with open(tpath) as fh:
+            tj = json.load(fh).get(f"frames_F{F}")
+        if tj:
+            traffic, step_traffic = tj["hbm_bytes_per_launch"], tj.get("step_bytes_all_kernels")
     checks = checksum_report(f"frames_{args.scan_points}_frames{F * world}", sd.frame_checksums(pl.bv_fused), dev,
                              rank, args)
     cpu = None
@@ -643,8 +650,8 @@ def run_frames(args, world, rank, dev):
             "frame_checksums": checks,
             "roofline": {"bound": "hbm", "kernel": "k_dense + k_sparse (fused layer)", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "algorithmic_bytes_per_launch": nbytes,
-                         "step_algorithmic_bytes": step_bytes, "step_GBps": round(step_gbs, 1),
+                         "traffic": traffic, "algorithmic_bytes_per_launch": nbytes,
+                         "step_traffic": step_traffic, "step_algorithmic_bytes": step_bytes, "step_GBps": round(step_gbs, 1),
                          "step_frac": round(step_gbs / HBM_PEAK_GBS, 4)},
             "cpu_baseline": cpu,
             "index_errors": errs,
@@ -752,6 +759,13 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
     hbm_gbs = hbm_bytes / step_s / 1e9
     # the bound: the larger of the two floors (f32: MFMA; bf16: HBM)
     hbm_bound = hbm_bytes / (HBM_PEAK_GBS * 1e9) > flops / (MFMA_PEAK_TFS[dname] * 1e12)
+    traffic = None  # PMC bytes of every SHPL kernel of a step (scripts/r02_pmc.sh TAG=train..., traffic.py step)
+    tpath = os.path.join(HERE, "profiles", "traffic.json")
+    if os.path.exists(tpath):
+        with open(tpath) as fh:
+            tj = json.load(fh).get(f"train_{dname}_F{F}")
+        if tj:
+            traffic = tj["hbm_bytes_per_launch"]
     if rank == 0:
         print(json.dumps({
             "metric": "SHPL + post-fusion conv training frames/sec (fwd + bwd), 1/2/4/8 GPU",
@@ -769,14 +783,15 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
                           "(pooled map, conv fwd, BN apply, BN backward x2, input and weight gradients, image "
                           "gradient) over the forward + backward time",
                           "achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                          "frac": round(hbm_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                          "frac": round(hbm_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
                           "algorithmic_bytes_per_step": hbm_bytes, "mfma_tflops": round(tflops, 2),
                           "mfma_frac": round(tflops / MFMA_PEAK_TFS[dname], 4)} if hbm_bound else
                          {"bound": "mfma", "kernel": "fwd + input-gradient + weight-gradient convs (3x the forward "
                           "flops) over the forward + backward time (BN, ReLU and the pooling gradient included)",
                           "achieved": round(tflops, 2), "peak": MFMA_PEAK_TFS[dname], "unit": "TFLOP/s",
                           "frac": round(tflops / MFMA_PEAK_TFS[dname], 4), "traffic": None,
-                          "algorithmic_bytes_per_step": hbm_bytes, "hbm_GBps": round(hbm_gbs, 1)}),
+                          "algorithmic_bytes_per_step": hbm_bytes, "hbm_GBps": round(hbm_gbs, 1),
+                          "hbm_traffic_per_step": traffic}),
             "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4),
             "cpu_baseline": None,
         }), flush=True)

@@ -8,6 +8,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -86,15 +87,7 @@ def main(key):
     print(json.dumps(tj[key], indent=1))
 
 
-if __name__ == "__main__":
-    key = sys.argv[1] if len(sys.argv) > 1 else "config2_F64"
-    if key.startswith("conv_"):
-        conv(key, key.split("_")[1])
-    else:
-        main(key)
-
-
-def step_traffic(key, tag, layer_kernels=("k_dense", "k_sparse", "k_sparse_long", "k_rows")):
+def step_traffic(key, tag, layer_kernels=("k_dense", "k_sparse", "k_sparse_long", "k_rows"), anchor="k_count"):
     """Per-step HBM bytes of the layer kernels of one bench workload from the
     scripts/r02_pmc.sh passes (gpurun_out/pmc_<tag>_FETCH_SIZE, _WRITE_SIZE):
     every launch's counters summed, divided by the steps profiled (the number of
@@ -110,24 +103,42 @@ def step_traffic(key, tag, layer_kernels=("k_dense", "k_sparse", "k_sparse_long"
                 name = r["Kernel_Name"]
                 short = next((s for k, s in SHORT if k in name), None)
                 if short is None:
-                    short = "k_rows" if "k_rows" in name else ("k_csr_range" if "k_csr_range" in name else name[:40])
+                    m = re.search(r"(k_[A-Za-z0-9_]+)", name)
+                    short = m.group(1) if m else name[:40]
                 acc[short][0] += float(r["Counter_Value"])
                 acc[short][1] += 1
         return acc
     fetch, write = launches("FETCH_SIZE"), launches("WRITE_SIZE")
-    steps = fetch.get("k_count", [0, 0])[1] or 1
+    steps = fetch.get(anchor, [0, 0])[1] or 1
     out = {}
     for k in sorted(set(fetch) | set(write)):
         f_b = 2 * fetch.get(k, [0, 0])[0] * 1024 / steps
         w_b = write.get(k, [0, 0])[0] * 1024 / steps
         out[k] = {"fetch_bytes_per_step": f_b, "write_bytes_per_step": w_b,
                   "launches_per_step": fetch.get(k, [0, 0])[1] / steps}
-    layer = sum(v["fetch_bytes_per_step"] + v["write_bytes_per_step"] for k, v in out.items() if k in layer_kernels)
+    total = sum(v["fetch_bytes_per_step"] + v["write_bytes_per_step"] for v in out.values())
+    layer = sum(v["fetch_bytes_per_step"] + v["write_bytes_per_step"] for k, v in out.items()
+                if layer_kernels is None or k in layer_kernels)
     path = os.path.join(ROOT, "profiles", "traffic.json")
     tj = json.load(open(path)) if os.path.exists(path) else {}
-    tj[key] = {"hbm_bytes_per_launch": layer, "steps_profiled": steps, "kernels": out,
-               "note": ("layer = " + " + ".join(layer_kernels) + " per step (every launch of the step summed); "
-                        "FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes; scripts/r02_pmc.sh")}
+    tj[key] = {"hbm_bytes_per_launch": layer, "step_bytes_all_kernels": total, "steps_profiled": steps,
+               "kernels": out,
+               "note": ("layer = " + (" + ".join(layer_kernels) if layer_kernels else "every profiled kernel")
+                        + " per step (every launch of the step summed); FETCH_SIZE x2 (gfx950 wide-read "
+                        "correction), KiB -> bytes; scripts/r02_pmc.sh")}
     json.dump(tj, open(path, "w"), indent=1)
     print(key, f"{layer / 1e9:.4f} GB per step", {k: round((v['fetch_bytes_per_step'] + v['write_bytes_per_step']) / 1e6, 2)
                                                    for k, v in out.items()})
+
+
+if __name__ == "__main__":
+    key = sys.argv[1] if len(sys.argv) > 1 else "config2_F64"
+    if key == "step":  # traffic.py step KEY TAG [all] [ANCHOR]: per-step bytes of a bench workload's PMC passes
+        every = len(sys.argv) > 4 and sys.argv[4] == "all"
+        step_traffic(sys.argv[2], sys.argv[3], None if every else ("k_dense", "k_sparse", "k_sparse_long", "k_rows"),
+                     sys.argv[5] if len(sys.argv) > 5 else "k_count")
+        sys.exit(0)
+    if key.startswith("conv_"):
+        conv(key, key.split("_")[1])
+    else:
+        main(key)
