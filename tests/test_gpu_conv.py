@@ -204,6 +204,28 @@ def test_fused_conv_empty_map():
     _assert_within(y, orc.conv3x3(x, wts), _bound(x, wts))
 
 
+def test_bf16_rows_empty_map_stats_and_wgrad():
+    """An empty map through the bf16 pooled forms (k_conv_rows CMP + statistics, k_wgrad_rows with a pooled
+    tile): every pooled chunk is zero, so both equal the dense forms over a zero second source, bitwise."""
+    from sparse_pooling_amd import fusion_conv as fc, shpl_map as sm
+    bev = orc.from_bf16_bits(orc.to_bf16_bits(synth.make_features((1, 6, 37, 32), 2)))
+    img = orc.from_bf16_bits(orc.to_bf16_bits(synth.make_features((1, 9, 11, 32), 1)))
+    smap = sm.pack_map(torch.zeros((0, 2), dtype=torch.int64, device=DEV), torch.zeros(0, device=DEV), [222, 0],
+                       torch.zeros((0, 3), dtype=torch.int32, device=DEV), img.shape)
+    w = _bf16(orc.from_bf16_bits(orc.to_bf16_bits(_weights(64, 32, 3))))
+    tb, ti = _bf16(bev), _bf16(img)
+    zero = torch.zeros_like(tb)
+    st_f, st_d = (torch.empty((2, 32), dtype=torch.float64, device=DEV) for _ in range(2))
+    y_f = fc.conv3x3(tb, w, b=ti, pool=smap.csr(0, 0), frame_off=smap.frame_off, relu=False, stats=st_f)
+    y_d = fc.conv3x3(tb, w, b=zero, relu=False, stats=st_d)
+    assert torch.equal(y_f, y_d) and torch.equal(st_f, st_d)
+    g = _bf16(synth.make_features((1, 6, 37, 32), 4))
+    dw_f = fc.conv3x3_wgrad(tb, g, b=ti, pool=smap.csr(0, 0), frame_off=smap.frame_off)
+    dw_d = fc.conv3x3_wgrad(tb, g, b=zero)
+    assert torch.equal(dw_f, dw_d)
+    assert not dw_f[:, :, 32:].any()
+
+
 def test_batch_norm_training_vs_oracle():
     """is_training: conv statistics -> batch moments -> normalise + ReLU in
     place, moving averages with the Bessel-corrected variance."""

@@ -121,6 +121,8 @@ WGRAD_ROWS = [  # B, H, W, c_a, c_b, c_out: bf16 dense weight gradients on k_wgr
     (1, 130, 70, 64, 0, 64),   # three bands, a partial strip, two output tiles
     (3, 9, 33, 16, 0, 40),     # channel tails in both tiles (16 of 32 inputs, 8 of the second 32 outputs)
     (1, 61, 32, 32, 16, 32),   # one band of 61 rows; B's tile is a tail
+    (1, 1, 1, 32, 0, 32),      # one pixel: every halo pixel and row outside the map
+    (2, 2, 3, 8, 0, 8),        # 8-channel tiles, two frames of 2 rows
 ]
 
 
