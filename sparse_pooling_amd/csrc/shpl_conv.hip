@@ -1574,6 +1574,12 @@ int conv_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_
         pl->n_bands = (int)((h + pl->band - 1) / pl->band);
     }
     if ((int64_t)n_frames * pl->n_bands * pl->tiles_x >= (1LL << 31)) pl->rows = false;
+    // statistics partials: one per tile (tiled kernel) or per item (k_conv_rows, SHPL_ROWS_BAND may cut more
+    // bands than there are tile rows)
+    if (stats && pl->rows) {
+        const int64_t n_items = (int64_t)n_frames * pl->n_bands * pl->tiles_x;
+        if (n_items > pl->n_tiles) pl->part_bytes = align_up((size_t)pl->n_cob * NCO * 2 * n_items * 8, 256);
+    }
     pl->occ_bytes = pl->rows && pooled ? 2 * align_up((size_t)n_frames * h * pl->wpr * 4, 256) : 0;
     pl->pool_cap = pool_cap;
     pl->cmp_bytes = pl->rows && pooled ? align_up((size_t)pool_cap * c_b * esz, 256) : 0;
