@@ -13,7 +13,18 @@ generate_bev's slice filter keeps points strictly inside the extents
 (obj_utils.py:465-470), so the KAT's z = 0 corners, on the extents' boundary,
 drop out: that edge is part of what is checked.
 
-The CPU case checks the oracle; the GPU case runs the device voxelizer
+Two more of the reference's unit tests sit on this path and are restated the
+same way: get_point_filter's offset planes (obj_utils_test.py:65-94: the
+points (0, 1, 0), (0, -1, 0), (5, 1, 5), (-5, 1, 5), the plane [0, -1, 0, 0],
+[-2, 2] extents, offsets 0.5 and 2.0 keeping 1 and 2 points), which
+create_slice_filter xors into a slice (kitti_utils.py:97-107); and
+dist_to_plane's signed, normalised distance (geometry_utils_test.py:9-37:
+point (1, 1, 1), distance 1 from the axis planes, sqrt(3) from [1, 1, 1, 0],
+-sqrt(3) from [-1, -1, -1, 0]), which sets the voxel heights
+(voxel_grid_2d.py:111) while the slice filter compares the unnormalised
+plane product (obj_utils.py:479-483).
+
+The CPU cases check the oracle; the GPU cases run the device voxelizer
 (shpl_bev_slices through bev.BevSlices) on the same inputs.
 """
 import types
@@ -80,11 +91,12 @@ def test_voxel_grid_extents_oracle():
     _check_random(hm, vox, cells)
 
 
-def _device(pts, ext):
+def _device(pts, ext, plane=PLANE, lo=-5.0, hi=5.0):
     import torch
     from sparse_pooling_amd import bev
-    cfg = types.SimpleNamespace(height_lo=-5.0, height_hi=5.0, num_slices=1)
-    maps, vox, upts = bev.BevSlices(cfg).generate_bev("lidar", pts.T, PLANE, ext, VS, output_indices=True)
+    cfg = types.SimpleNamespace(height_lo=lo, height_hi=hi, num_slices=1)
+    maps, vox, upts = bev.BevSlices(cfg).generate_bev("lidar", pts.T, np.asarray(plane, np.float64), ext, VS,
+                                                      output_indices=True)
     torch.cuda.synchronize()
     f = lambda t: t.cpu().numpy() if hasattr(t, "cpu") else np.asarray(t)
     return np.stack([f(m) for m in maps["height_maps"]]), f(maps["density_map"]), f(vox), f(upts)
@@ -105,3 +117,70 @@ def test_voxel_grid_extents_device():
     np.testing.assert_array_equal(upts, oupts)
     np.testing.assert_array_equal(hm, ohm)
     np.testing.assert_array_equal(dm, odm)
+
+
+# ---- get_point_filter (obj_utils_test.py:65-94) and dist_to_plane (geometry_utils_test.py:9-37)
+
+FILTER_POINTS = np.array([[0.0, 1, 0], [0, -1, 0], [5, 1, 5], [-5, 1, 5]])
+EXT2 = np.array([[-2.0, 2.0], [-2.0, 2.0], [-2.0, 2.0]])
+CELL2 = (20, 20, 19)  # (0, *, 0): x index 0 - floor(-2 / 0.1) = 20, BEV row nz - z = 40 - 20, map row nz - 1 - z
+
+# (slice low, high) -> the points kept (get_point_filter(high) xor get_point_filter(low)): offset 0.5 keeps
+# (0, 1, 0) (height -1), offset 2.0 adds (0, -1, 0) (height 1); (5, 1, 5) and (-5, 1, 5) are outside the extents
+FILTER_CASES = {(-10.0, 0.5): [[0.0, 1, 0]], (-10.0, 2.0): [[0.0, 1, 0], [0, -1, 0]], (0.5, 2.0): [[0.0, -1, 0]]}
+
+
+def _check_filter(lo, hi, hm, dm, vox, upts):
+    kept = np.array(FILTER_CASES[(lo, hi)])
+    x, row, mrow = CELL2
+    np.testing.assert_array_equal(np.asarray(vox), [[x, row]])
+    top = kept[np.argmin(kept[:, 1])]  # the cell's lowest-y point
+    np.testing.assert_array_equal(np.asarray(upts), [top])
+    eh = np.zeros((1, 40, 40))
+    eh[0, mrow, x] = (-top[1] - lo) / (hi - lo)
+    ed = np.zeros((40, 40))
+    ed[mrow, x] = min(1.0, np.log(len(kept) + 1) / np.log(16))
+    np.testing.assert_allclose(np.asarray(hm), eh, rtol=1e-14, atol=0)
+    np.testing.assert_allclose(np.asarray(dm), ed, rtol=1e-14, atol=0)
+
+
+# plane -> (slice low, high, the point's distance): the filter compares a.x + d - offset < 0 (unnormalised), the
+# height is the normalised signed distance
+PLANE_CASES = [([0.0, 0, 1, 0], -2.0, 2.0, 1.0), ([0.0, 1, 0, 0], -2.0, 2.0, 1.0), ([1.0, 0, 0, 0], -2.0, 2.0, 1.0),
+               ([1.0, 1, 1, 0], 0.0, 4.0, np.sqrt(3)), ([0.0, 0, -1, 0], -2.0, 2.0, -1.0),
+               ([-1.0, -1, -1, 0], -4.0, 0.0, -np.sqrt(3))]
+
+
+def _check_plane(lo, hi, dist, hm, vox):
+    np.testing.assert_array_equal(np.asarray(vox), [[30, 40 - 30]])  # (1, 1, 1): x, z index 10 + 20
+    eh = np.zeros((1, 40, 40))
+    eh[0, 39 - 30, 30] = (dist - lo) / (hi - lo)
+    np.testing.assert_allclose(np.asarray(hm), eh, rtol=1e-14, atol=0)
+
+
+@pytest.mark.parametrize("lohi", list(FILTER_CASES), ids=str)
+def test_point_filter_kat_oracle(lohi):
+    lo, hi = lohi
+    _check_filter(lo, hi, *orc.bev_slices(FILTER_POINTS.T, [0.0, -1, 0, 0], EXT2, VS, lo, hi, 1))
+
+
+@pytest.mark.parametrize("case", PLANE_CASES, ids=str)
+def test_dist_to_plane_kat_oracle(case):
+    plane, lo, hi, dist = case
+    hm, _, vox, _ = orc.bev_slices(np.array([[1.0], [1.0], [1.0]]), plane, EXT2, VS, lo, hi, 1)
+    _check_plane(lo, hi, dist, hm, vox)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lohi", list(FILTER_CASES), ids=str)
+def test_point_filter_kat_device(lohi):
+    lo, hi = lohi
+    _check_filter(lo, hi, *_device(FILTER_POINTS, EXT2, [0.0, -1, 0, 0], lo, hi))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", PLANE_CASES, ids=str)
+def test_dist_to_plane_kat_device(case):
+    plane, lo, hi, dist = case
+    hm, _, vox, _ = _device(np.array([[1.0, 1.0, 1.0]]), EXT2, plane, lo, hi)
+    _check_plane(lo, hi, dist, hm, vox)
