@@ -260,7 +260,16 @@ typedef struct {
     int32_t *key_range; /* optional [n_keys][2]: (first, end) sorted entry of each destination's
                            run (first == end: no entry). NULL: not built. When set,
                            shpl_build_csr fills it and shpl_pull runs one row-keyed launch. */
+    /* optional, read by the sparse pass only (n_frames 0: it walks the whole capacity): the frame
+       layout shpl_build_csr was given, so that it walks only the live entries -- frame f's
+       [frame_off[f], frame_off[f] + min(frame_nnz[f], frame_off[f+1] - frame_off[f])) -- when
+       most of the capacity is empty (raw scans: ~9 k voxel points in 120 k slots per frame).
+       At most SHPL_LIVE_MAX_FRAMES frames. */
+    const int64_t *frame_off; /* [n_frames + 1] */
+    const int64_t *frame_nnz; /* [n_frames]     */
+    int64_t n_frames;
 } shpl_csr;
+#define SHPL_LIVE_MAX_FRAMES 1024
 
 /* Sort the entries of every frame by destination (cell for SHPL_BY_CELL,
  * pix[col] for SHPL_BY_PIXEL) keeping `order` among equal destinations, and

@@ -30,11 +30,15 @@ class ShplLibraryError(RuntimeError):
     pass
 
 
+LIVE_MAX_FRAMES = 1024  # SHPL_LIVE_MAX_FRAMES
+
+
 class ShplCsr(ctypes.Structure):
     """struct shpl_csr of include/shpl.h (device pointers + sizes)."""
     _fields_ = [("ent_dst", ctypes.c_void_p), ("ent_src", ctypes.c_void_p),
                 ("ent_val", ctypes.c_void_p), ("ent_col", ctypes.c_void_p),
-                ("n_keys", ctypes.c_int64), ("nnz_cap", ctypes.c_int64), ("key_range", ctypes.c_void_p)]
+                ("n_keys", ctypes.c_int64), ("nnz_cap", ctypes.c_int64), ("key_range", ctypes.c_void_p),
+                ("frame_off", ctypes.c_void_p), ("frame_nnz", ctypes.c_void_p), ("n_frames", ctypes.c_int64)]
 
 
 class Csr:
@@ -55,6 +59,20 @@ class Csr:
         self.struct = ShplCsr(self.ent_dst.data_ptr(), self.ent_src.data_ptr(), self.ent_val.data_ptr(),
                               self.ent_col.data_ptr() if with_col else None, self.n_keys, self.nnz_cap,
                               self.key_range.data_ptr() if key_range else None)
+
+    def live_frames(self, frame_off, frame_nnz):
+        """Hand the sparse pass the frame layout the CSR was built with (device i64 [F+1] / [F],
+        kept alive here): it then walks only the live entries of each frame's capacity."""
+        if frame_nnz is None or frame_nnz.numel() > LIVE_MAX_FRAMES:
+            self._frames = None
+            self.struct.frame_off, self.struct.frame_nnz, self.struct.n_frames = None, None, 0
+            return self
+        assert frame_off.dtype == torch.int64 and frame_nnz.dtype == torch.int64
+        assert frame_off.numel() == frame_nnz.numel() + 1
+        self._frames = (frame_off, frame_nnz)
+        self.struct.frame_off, self.struct.frame_nnz = frame_off.data_ptr(), frame_nnz.data_ptr()
+        self.struct.n_frames = int(frame_nnz.numel())
+        return self
 
     def ref(self):
         return ctypes.byref(self.struct)

@@ -154,7 +154,54 @@ struct Ents {
     int64_t n;  // capacity; empty slots carry dst = -1
     const int32_t *dst, *src, *col;
     const float *val;
+    // optional frame layout (n_frames > 0): frame f's live entries are the first frame_nnz[f] slots of
+    // [frame_off[f], frame_off[f+1]), the rest of the capacity is empty
+    const int64_t *frame_off, *frame_nnz;
+    int n_frames;
 };
+
+// The live-entry table of a frame layout in LDS (one per workgroup): s_off[f] = frame f's first slot
+// (s_off[F] = the end of the last frame), s_pre[f] = live entries of the frames before f (s_pre[F] =
+// all). Returns the live total.
+constexpr int LIVE_MAX_FRAMES = SHPL_LIVE_MAX_FRAMES;
+__device__ __forceinline__ int32_t live_table(const Ents &e, int32_t *s_off, int32_t *s_pre, int64_t *s_scan) {
+    const int F = e.n_frames;
+    int32_t cnt[LIVE_MAX_FRAMES / SHPL_BLOCK];
+    int64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < LIVE_MAX_FRAMES / SHPL_BLOCK; ++k) {
+        const int fi = (LIVE_MAX_FRAMES / SHPL_BLOCK) * threadIdx.x + k;
+        cnt[k] = 0;
+        if (fi < F) {
+            const int64_t o0 = e.frame_off[fi], o1 = e.frame_off[fi + 1], n = e.frame_nnz[fi];
+            cnt[k] = (int32_t)(n < 0 ? 0 : (n < o1 - o0 ? n : o1 - o0));
+            s_off[fi] = (int32_t)o0;
+            if (fi == F - 1) s_off[F] = (int32_t)o1;
+        }
+        sum += cnt[k];
+    }
+    int64_t total;
+    int64_t run = block_excl_scan(sum, s_scan, &total);
+#pragma unroll
+    for (int k = 0; k < LIVE_MAX_FRAMES / SHPL_BLOCK; ++k) {
+        const int fi = (LIVE_MAX_FRAMES / SHPL_BLOCK) * threadIdx.x + k;
+        if (fi < F) s_pre[fi] = (int32_t)run;
+        run += cnt[k];
+    }
+    if (threadIdx.x == 0) s_pre[F] = (int32_t)total;
+    __syncthreads();
+    return (int32_t)total;
+}
+
+// The frame holding live entry L (0 <= L < s_pre[F]): the last f with s_pre[f] <= L (never an empty one).
+__device__ __forceinline__ int live_frame(const int32_t *s_pre, int F, int64_t L) {
+    int lo = 0, hi = F;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (s_pre[mid] <= L) lo = mid; else hi = mid;
+    }
+    return lo;
+}
 
 template <int VEC>
 __device__ __forceinline__ void fma_free_accumulate(float (&acc)[VEC], float w, const float (&x)[VEC]) {
@@ -292,15 +339,25 @@ __device__ __forceinline__ void store_pooled(const Feat &f, int32_t key, uint32_
 // One thread per (sorted entry, chunk); the thread on the first entry of a
 // destination's run sums it and writes the pooled chunk -- for runs of at
 // most LONG_RUN entries (SPLIT) or all runs (!SPLIT).
-template <typename T, int VEC, bool GROUP, bool SPLIT, bool POW2>
+// LIVE: with a frame layout, threads walk (live entry, chunk) pairs of a grid sized for the GPU, not
+// the capacity's (entry, chunk) pairs (the empty slots' waves cost more than the work at raw-scan
+// occupancy); the sums and stores are the same.
+template <typename T, int VEC, bool GROUP, bool SPLIT, bool POW2, bool LIVE>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse(const Feat f, const Ents e, int cpool_shift) {
+    __shared__ int32_t s_off[LIVE ? LIVE_MAX_FRAMES + 1 : 1], s_pre[LIVE ? LIVE_MAX_FRAMES + 1 : 1];
+    __shared__ int64_t s_scan[SHPL_BLOCK / 64 + 1];
     const int64_t nnz = e.n;
-    const int64_t total = nnz * (int64_t)f.cpool;
+    const int64_t total = (LIVE ? (int64_t)live_table(e, s_off, s_pre, s_scan) : nnz) * (int64_t)f.cpool;
     for (int64_t t = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x; t < total;
          t += (int64_t)gridDim.x * SHPL_BLOCK) {
         // a shift, not a 64-bit division, when the chunk count is a power of two
-        const int64_t s = POW2 ? t >> cpool_shift : t / f.cpool;
-        const uint32_t c = (uint32_t)(t - s * f.cpool);
+        const int64_t l = POW2 ? t >> cpool_shift : t / f.cpool;
+        const uint32_t c = (uint32_t)(t - l * f.cpool);
+        int64_t s = l;
+        if (LIVE) {
+            const int fr = live_frame(s_pre, e.n_frames, l);
+            s = (int64_t)s_off[fr] + (l - s_pre[fr]);
+        }
         // the head test's loads and the walk's first index batch are
         // independent: one round trip
         IdxBatch<GROUP, WALK> b0;
@@ -328,9 +385,12 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse(const Feat f, const Ents 
 constexpr int LONG_IDX = 512;
 constexpr int LONG_SLOTS = 64;  // entry slots per workgroup when the grid is not capped: few runs each
 constexpr int LONG_GRID = 2048; // workgroups of k_sparse_long at most (config 2: ~625 slots each)
-template <typename T, int VEC, bool GROUP>
+template <typename T, int VEC, bool GROUP, bool LIVE>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse_long(const Feat f, const Ents e, int64_t per_block) {
     typedef Chunk<T, VEC> C;
+    __shared__ int32_t s_off[LIVE ? LIVE_MAX_FRAMES + 1 : 1], s_pre[LIVE ? LIVE_MAX_FRAMES + 1 : 1];
+    __shared__ int64_t s_scan[SHPL_BLOCK / 64 + 1];
+    if (LIVE) live_table(e, s_off, s_pre, s_scan);
     __shared__ int32_t s_run[SHPL_BLOCK];
     __shared__ int32_t s_dst[LONG_IDX], s_src[LONG_IDX], s_col[GROUP ? LONG_IDX : 1];
     __shared__ float s_val[LONG_IDX];
@@ -341,6 +401,17 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse_long(const Feat f, const 
     // the block's slots, up to SHPL_BLOCK per round (uniform trip count)
     const int64_t span = per_block < SHPL_BLOCK ? per_block : SHPL_BLOCK;
     for (int64_t blk = (int64_t)blockIdx.x * per_block; blk < r_end; blk += span) {
+        if (LIVE) {  // slots [blk, blk + span) all empty (past a frame's live entries, within the frame): next
+            const int F = e.n_frames;
+            if (blk >= s_off[F]) break;
+            int lo = 0, hi = F;  // the last frame starting at or before blk
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (s_off[mid] <= blk) lo = mid; else hi = mid;
+            }
+            if (blk >= s_off[lo] && blk - s_off[lo] >= s_pre[lo + 1] - s_pre[lo] && blk + span <= s_off[lo + 1])
+                continue;
+        }
         if (threadIdx.x == 0) {
             s_n = 0;
             s_first = SHPL_BLOCK;
@@ -640,44 +711,67 @@ int dense(const Plan &pl, hipStream_t s) {
     return pl.v16 ? dense_t<uint16_t, 8>(pl, s) : dense_t<uint16_t, 1>(pl, s);
 }
 
-template <typename T, int VEC, bool GROUP>
-int sparse_tg(const Plan &pl, const Ents &e, int64_t nnz_cap, hipStream_t s) {
-    // one thread per (entry, chunk) of the capacity; the live count is read on the device
-    const int grid = grid_for(nnz_cap * (int64_t)pl.f.cpool, SHPL_BLOCK, 1 << 20);
-    int shift = -1;
-    for (int k = 0; k < 31; ++k)
-        if (pl.f.cpool == (1u << k)) shift = k;
-    // without a run longer than LONG_RUN possible, k_sparse takes every run (the short part)
-    const bool split = nnz_cap > LONG_RUN;
-#define SHPL_SPARSE(SPLIT, POW2) \
-    hipLaunchKernelGGL((k_sparse<T, VEC, GROUP, SPLIT, POW2>), dim3(grid), dim3(SHPL_BLOCK), 0, s, pl.f, e, shift)
+#ifndef SHPL_LIVE_GRID
+#define SHPL_LIVE_GRID 4096  // workgroups of the live-entry k_sparse at most (a grid-stride loop)
+#endif
+
+template <typename T, int VEC, bool GROUP, bool LIVE>
+void sparse_launch(const Plan &pl, const Ents &e, int grid, int shift, bool split, hipStream_t s) {
+#define SHPL_SPARSE(SPLIT, POW2)                                                                                   \
+    hipLaunchKernelGGL((k_sparse<T, VEC, GROUP, SPLIT, POW2, LIVE>), dim3(grid), dim3(SHPL_BLOCK), 0, s, pl.f, e, \
+                       shift)
     if (split) {
         if (shift >= 0) SHPL_SPARSE(true, true); else SHPL_SPARSE(true, false);
     } else {
         if (shift >= 0) SHPL_SPARSE(false, true); else SHPL_SPARSE(false, false);
     }
 #undef SHPL_SPARSE
+}
+
+template <typename T, int VEC, bool GROUP>
+int sparse_tg(const Plan &pl, const Ents &e, int64_t nnz_cap, hipStream_t s) {
+    // one thread per (entry, chunk) of the capacity (the live count is read on the device), or, with a
+    // frame layout, a bounded grid walking the live entries' (entry, chunk) pairs
+    const bool live = e.n_frames > 0;
+    int grid = grid_for(nnz_cap * (int64_t)pl.f.cpool, SHPL_BLOCK, 1 << 20);
+    if (live && grid > SHPL_LIVE_GRID) grid = SHPL_LIVE_GRID;
+    int shift = -1;
+    for (int k = 0; k < 31; ++k)
+        if (pl.f.cpool == (1u << k)) shift = k;
+    // without a run longer than LONG_RUN possible, k_sparse takes every run (the short part)
+    const bool split = nnz_cap > LONG_RUN;
+    if (live)
+        sparse_launch<T, VEC, GROUP, true>(pl, e, grid, shift, split, s);
+    else
+        sparse_launch<T, VEC, GROUP, false>(pl, e, grid, shift, split, s);
     SHPL_LAUNCH_CHECK();
     if (!split) return SHPL_OK;
     // a bounded grid: each workgroup scans per_block slots, LONG_SLOTS at a time
     int64_t lgrid = (nnz_cap + LONG_SLOTS - 1) / LONG_SLOTS;
     if (lgrid > LONG_GRID) lgrid = LONG_GRID;
     const int64_t per_block = (nnz_cap + lgrid - 1) / lgrid;
-    hipLaunchKernelGGL((k_sparse_long<T, VEC, GROUP>), dim3((unsigned)lgrid), dim3(SHPL_BLOCK), 0, s, pl.f, e,
-                       per_block);
+    if (live)
+        hipLaunchKernelGGL((k_sparse_long<T, VEC, GROUP, true>), dim3((unsigned)lgrid), dim3(SHPL_BLOCK), 0, s, pl.f,
+                           e, per_block);
+    else
+        hipLaunchKernelGGL((k_sparse_long<T, VEC, GROUP, false>), dim3((unsigned)lgrid), dim3(SHPL_BLOCK), 0, s, pl.f,
+                           e, per_block);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
 }
 
 template <typename T, int VEC>
 int sparse_t(const Plan &pl, const shpl_csr *csr, bool group, hipStream_t s) {
-    Ents e{csr->nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_col, csr->ent_val};
+    const bool live = csr->n_frames > 0 && csr->frame_off && csr->frame_nnz;
+    Ents e{csr->nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_col, csr->ent_val,
+           live ? csr->frame_off : nullptr, live ? csr->frame_nnz : nullptr, live ? (int)csr->n_frames : 0};
     return group ? sparse_tg<T, VEC, true>(pl, e, csr->nnz_cap, s)
                  : sparse_tg<T, VEC, false>(pl, e, csr->nnz_cap, s);
 }
 
 int sparse(const Plan &pl, const shpl_csr *csr, int direction, hipStream_t s) {
     if (pl.n_dst == 0 || pl.f.cpool == 0 || csr->nnz_cap == 0) return SHPL_OK;
+    if (csr->n_frames < 0 || csr->n_frames > LIVE_MAX_FRAMES) return SHPL_ERR_ARG;
     const bool group = direction == SHPL_BY_PIXEL;
     if (pl.dtype == SHPL_F32)
         return pl.v16 ? sparse_t<float, 4>(pl, csr, group, s) : sparse_t<float, 1>(pl, csr, group, s);

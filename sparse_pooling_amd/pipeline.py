@@ -28,7 +28,10 @@ class FusedPipeline:
     ROWS_FRAMES, ROWS_MAX_KEYS = 32, 65536
 
     def __init__(self, n_frames, max_points_per_frame, total_points, im_size, bv_size, stride,
-                 c_bev, c_img, dtype=torch.float32, device="cuda", dual=False, rows=None):
+                 c_bev, c_img, dtype=torch.float32, device="cuda", dual=False, rows=None, live=False):
+        """live: the sparse passes walk each frame's live entries (shpl_csr frame layout) instead of the
+        whole capacity -- for capacities far above the entry counts (FramePipeline: raw-scan slots per
+        voxel point); at config 2 (capacity = entries) the capacity walk is faster (2.22 vs 2.24 ms)."""
         dev = torch.device(device)
         self.dev, self.dtype, self.dual = dev, dtype, dual
         self.B = int(n_frames)
@@ -63,6 +66,10 @@ class FusedPipeline:
             self.pcsr = L.Csr(self.n_pix, self.N, dev, with_col=True, key_range=self.rows)  # pixel CSR (BEV -> img)
             self.img_fused = torch.empty((self.B, self.Hi, self.Wi, self.Ci + self.Cb), dtype=dtype,
                                          device=dev)
+        if live:
+            for c in (self.csr, self.pcsr if dual else None):
+                if c is not None:
+                    c.live_frames(self.frame_off, self.frame_nnz)
         self._lib = L.lib()
 
     # ------------------------------------------------------------------ steps
@@ -313,7 +320,7 @@ class FramePipeline(FusedPipeline):
         # a frame holds at most as many voxels as points (capacity layout)
         maxp = total_points if max_points_per_frame is None else max_points_per_frame
         super().__init__(n_frames, maxp, total_points, im_size, (nz, nx), stride, c_bev, c_img,
-                         dtype=dtype, device=device, dual=dual)
+                         dtype=dtype, device=device, dual=dual, live=True)
         self.bev_args = (area_extents, voxel_size, height_lo, height_hi, num_slices)
         self.maps = maps
         import ctypes

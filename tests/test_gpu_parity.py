@@ -879,3 +879,48 @@ def test_velodyne_to_fused_layer_pipeline(kitti_dir):
                                        ref["img_index_flip_pool"], dual=True)
         _close_and_exact(out[f:f + 1], eb)
         _close_and_exact(iout[f:f + 1], ei)
+
+
+@pytest.mark.parametrize("cfg,dtype,counts", [
+    (1, "f32", (1.0, 0.0, 0.5)), (3, "bf16", (0.3, 1.0, 0.0, 0.7)), (1, "f32", (0.0, 0.0)), (1, "bf16", (0.2,))])
+def test_sparse_live_entries_equal_capacity_walk(cfg, dtype, counts):
+    """The sparse passes with the CSR's frame layout (Csr.live_frames: k_sparse walks the live entries
+    of each frame with a bounded grid, k_sparse_long skips empty stretches) against the capacity walk,
+    forward (both directions) and backward, bitwise: frames whose live points are a fraction of their
+    slots (point_counts), empty frames, a frame alone; cfg 3 has pixel runs longer than k_sparse's 8
+    entries (k_sparse_long). The capacity walk is the oracle-pinned path of the other tests."""
+    from sparse_pooling_amd import pipeline
+    spec = synth.CONFIGS[cfg]
+    B = len(counts)
+    frames = [synth.make_frame(spec, seed=700 + f, n_outside=10) for f in range(B)]
+    pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
+    n = np.diff(_np(off))
+    cnt = torch.tensor([int(round(c * k)) for c, k in zip(counts, n)], dtype=torch.int64, device=DEV)
+    tdt = torch.float32 if dtype == "f32" else torch.bfloat16
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    Cb, Ci = spec.c_bev, spec.c_img
+    g = torch.Generator(device=DEV).manual_seed(5)
+    bev = torch.randn((B, Hb, Wb, Cb), device=DEV, generator=g).to(tdt)
+    img = torch.randn((B, Hi, Wi, Ci), device=DEV, generator=g).to(tdt)
+    gb = torch.randn((B, Hb, Wb, Cb + Ci), device=DEV, generator=g).to(tdt)
+    gi = torch.randn((B, Hi, Wi, Ci + Cb), device=DEV, generator=g).to(tdt)
+    outs = []
+    for live in (False, True):
+        pl = pipeline.FusedPipeline(B, maxp, N, spec.im_size, spec.bv_size, spec.stride, Cb, Ci, dtype=tdt,
+                                    dual=True, rows=False, live=live)
+        assert (pl.csr.struct.n_frames > 0) == live
+        pl.build_index(pts, vox, off, P, point_counts=cnt)
+        pl.build_csr()
+        pl.layer(bev, img)
+        d_bev, d_img = torch.empty_like(bev), torch.empty_like(img)
+        pl.backward(gb, gi, d_bev, d_img)
+        torch.cuda.synchronize()
+        assert int(pl.err.item()) == 0
+        if cfg == 3 and live:  # a long run is really there
+            e = pl.pcsr.ent_dst[pl.pcsr.ent_dst >= 0]
+            assert int(torch.unique_consecutive(e, return_counts=True)[1].max().item()) > 8
+        outs.append([t.clone() for t in (pl.bv_fused, pl.img_fused, d_bev, d_img)])
+    for a, b in zip(*outs):
+        assert torch.equal(a.view(torch.int16) if a.dtype == torch.bfloat16 else a.view(torch.int32),
+                           b.view(torch.int16) if b.dtype == torch.bfloat16 else b.view(torch.int32))
