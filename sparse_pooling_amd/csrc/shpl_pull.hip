@@ -341,7 +341,8 @@ __device__ __forceinline__ void store_pooled(const Feat &f, int32_t key, uint32_
 // most LONG_RUN entries (SPLIT) or all runs (!SPLIT).
 // LIVE: with a frame layout, threads walk (live entry, chunk) pairs of a grid sized for the GPU, not
 // the capacity's (entry, chunk) pairs (the empty slots' waves cost more than the work at raw-scan
-// occupancy); the sums and stores are the same.
+// occupancy), and take every run (no k_sparse_long pass over the capacity); the sums and stores are
+// the same.
 template <typename T, int VEC, bool GROUP, bool SPLIT, bool POW2, bool LIVE>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse(const Feat f, const Ents e, int cpool_shift) {
     __shared__ int32_t s_off[LIVE ? LIVE_MAX_FRAMES + 1 : 1], s_pre[LIVE ? LIVE_MAX_FRAMES + 1 : 1];
@@ -385,12 +386,9 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse(const Feat f, const Ents 
 constexpr int LONG_IDX = 512;
 constexpr int LONG_SLOTS = 64;  // entry slots per workgroup when the grid is not capped: few runs each
 constexpr int LONG_GRID = 2048; // workgroups of k_sparse_long at most (config 2: ~625 slots each)
-template <typename T, int VEC, bool GROUP, bool LIVE>
+template <typename T, int VEC, bool GROUP>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse_long(const Feat f, const Ents e, int64_t per_block) {
     typedef Chunk<T, VEC> C;
-    __shared__ int32_t s_off[LIVE ? LIVE_MAX_FRAMES + 1 : 1], s_pre[LIVE ? LIVE_MAX_FRAMES + 1 : 1];
-    __shared__ int64_t s_scan[SHPL_BLOCK / 64 + 1];
-    if (LIVE) live_table(e, s_off, s_pre, s_scan);
     __shared__ int32_t s_run[SHPL_BLOCK];
     __shared__ int32_t s_dst[LONG_IDX], s_src[LONG_IDX], s_col[GROUP ? LONG_IDX : 1];
     __shared__ float s_val[LONG_IDX];
@@ -401,17 +399,6 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse_long(const Feat f, const 
     // the block's slots, up to SHPL_BLOCK per round (uniform trip count)
     const int64_t span = per_block < SHPL_BLOCK ? per_block : SHPL_BLOCK;
     for (int64_t blk = (int64_t)blockIdx.x * per_block; blk < r_end; blk += span) {
-        if (LIVE) {  // slots [blk, blk + span) all empty (past a frame's live entries, within the frame): next
-            const int F = e.n_frames;
-            if (blk >= s_off[F]) break;
-            int lo = 0, hi = F;  // the last frame starting at or before blk
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (s_off[mid] <= blk) lo = mid; else hi = mid;
-            }
-            if (blk >= s_off[lo] && blk - s_off[lo] >= s_pre[lo + 1] - s_pre[lo] && blk + span <= s_off[lo + 1])
-                continue;
-        }
         if (threadIdx.x == 0) {
             s_n = 0;
             s_first = SHPL_BLOCK;
@@ -738,8 +725,10 @@ int sparse_tg(const Plan &pl, const Ents &e, int64_t nnz_cap, hipStream_t s) {
     int shift = -1;
     for (int k = 0; k < 31; ++k)
         if (pl.f.cpool == (1u << k)) shift = k;
-    // without a run longer than LONG_RUN possible, k_sparse takes every run (the short part)
-    const bool split = nnz_cap > LONG_RUN;
+    // without a run longer than LONG_RUN possible, k_sparse takes every run (the short part); so it does
+    // over live entries (raw scans: runs of at most a few voxel points per cell -- k_sparse_long would only
+    // scan the capacity)
+    const bool split = !live && nnz_cap > LONG_RUN;
     if (live)
         sparse_launch<T, VEC, GROUP, true>(pl, e, grid, shift, split, s);
     else
@@ -750,12 +739,8 @@ int sparse_tg(const Plan &pl, const Ents &e, int64_t nnz_cap, hipStream_t s) {
     int64_t lgrid = (nnz_cap + LONG_SLOTS - 1) / LONG_SLOTS;
     if (lgrid > LONG_GRID) lgrid = LONG_GRID;
     const int64_t per_block = (nnz_cap + lgrid - 1) / lgrid;
-    if (live)
-        hipLaunchKernelGGL((k_sparse_long<T, VEC, GROUP, true>), dim3((unsigned)lgrid), dim3(SHPL_BLOCK), 0, s, pl.f,
-                           e, per_block);
-    else
-        hipLaunchKernelGGL((k_sparse_long<T, VEC, GROUP, false>), dim3((unsigned)lgrid), dim3(SHPL_BLOCK), 0, s, pl.f,
-                           e, per_block);
+    hipLaunchKernelGGL((k_sparse_long<T, VEC, GROUP>), dim3((unsigned)lgrid), dim3(SHPL_BLOCK), 0, s, pl.f, e,
+                       per_block);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
 }
