@@ -924,3 +924,21 @@ def test_sparse_live_entries_equal_capacity_walk(cfg, dtype, counts):
     for a, b in zip(*outs):
         assert torch.equal(a.view(torch.int16) if a.dtype == torch.bfloat16 else a.view(torch.int32),
                            b.view(torch.int16) if b.dtype == torch.bfloat16 else b.view(torch.int32))
+
+
+def test_sparse_live_frame_limit():
+    """shpl_csr.n_frames above SHPL_LIVE_MAX_FRAMES (or negative) is an argument error of the sparse
+    pass, raised before any launch; Csr.live_frames keeps the capacity walk for such batches."""
+    from sparse_pooling_amd import _lib as L
+    F = L.LIVE_MAX_FRAMES + 1
+    c = L.Csr(8, 64, DEV, with_col=False)
+    off = torch.zeros(F + 1, dtype=torch.int64, device=DEV)
+    nnz = torch.zeros(F, dtype=torch.int64, device=DEV)
+    assert c.live_frames(off, nnz).struct.n_frames == 0  # too many frames: capacity walk
+    src = torch.zeros((8, 4), device=DEV)
+    out = torch.zeros((8, 4), device=DEV)
+    for bad in (F, -1):
+        c.struct.frame_off, c.struct.frame_nnz, c.struct.n_frames = off.data_ptr(), nnz.data_ptr(), bad
+        rc = L.lib().shpl_pull_sparse(L.BY_CELL, L.F32, c.ref(), L.ptr(src), 4, 0, 4, None, 0, 0, 0, L.OUT_POOL,
+                                      L.ptr(out), 4, L.stream_of(torch.device(DEV)))
+        assert rc == L.ERR_ARG, rc
