@@ -154,8 +154,13 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_pool_runs(const int32_t *ent_dst
                                                           const int64_t *frame_off, uint16_t *cmp) {
     const int64_t e = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x;
     if (e >= nnz_cap) return;
+    // the head test, the first entry's index words and the next entry's destination in one round trip
     const int32_t d = ent_dst[e];
-    if (d < 0 || (e > 0 && ent_dst[e - 1] == d)) return;
+    const int32_t prev = e > 0 ? ent_dst[e - 1] : -1;
+    int32_t dn = e + 1 < nnz_cap ? ent_dst[e + 1] : -1;
+    float wv = ent_val[e];
+    int32_t src = ent_src[e];
+    if (d < 0 || prev == d) return;
     const int64_t cells = (int64_t)H * W;
     const int f = (int)(d / cells);
     const int c = (int)(d - f * cells), y = c / W, x = c - y * W;
@@ -166,12 +171,20 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_pool_runs(const int32_t *ent_dst
     for (int g = 0; g < NP; ++g)
 #pragma unroll
         for (int j = 0; j < 8; ++j) sum[g][j] = 0.0f;
-    for (int64_t i = e; i < nnz_cap && ent_dst[i] == d; ++i) {
-        const float wv = ent_val[i];
-        const uint16_t *row = img + (int64_t)ent_src[i] * img_stride + img_off;
+    // entry i's row loads go out with entry i+1's index words (one round trip per entry, not two)
+    for (int64_t i = e;; ++i) {
+        const uint16_t *row = img + (int64_t)src * img_stride + img_off;
         u32x4 raw[NP];
 #pragma unroll
         for (int g = 0; g < NP; ++g) raw[g] = *reinterpret_cast<const u32x4 *>(row + g * 8);
+        const bool more = dn == d;  // entry i+1 is in the run (dn is -1 past the capacity)
+        float wn = 0.0f;
+        int32_t sn = 0, dnn = -1;
+        if (more) {
+            wn = ent_val[i + 1];
+            sn = ent_src[i + 1];
+            dnn = i + 2 < nnz_cap ? ent_dst[i + 2] : -1;
+        }
 #pragma unroll
         for (int g = 0; g < NP; ++g) {
             uint16_t xv[8];
@@ -179,6 +192,10 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_pool_runs(const int32_t *ent_dst
 #pragma unroll
             for (int j = 0; j < 8; ++j) sum[g][j] = __fadd_rn(sum[g][j], __fmul_rn(wv, bf16_to_f32(xv[j])));
         }
+        if (!more) break;
+        wv = wn;
+        src = sn;
+        dn = dnn;
     }
     uint16_t *o = cmp + (frame_off[f] + rid) * (int64_t)c_b;
 #pragma unroll
