@@ -983,7 +983,9 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_partial_vec(const T *y, c
     double s1[VEC], s2[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) s1[k] = s2[k] = 0.0;
-    constexpr int U = BN_U / 2;
+    // rows in flight per iteration (the sums stay in row order): bf16 4 (0.81 -> 0.73 ms per 64-frame
+    // step; the apply kernels are slower with more, profiles/r02_bn_sweep.log)
+    constexpr int U = sizeof(T) == 2 ? 4 : BN_U / 2;
     for (int64_t rb = r0 + rl; rb < r1; rb += U * rl_n) {
         float gv[U][VEC], xv[U][VEC], yv[U][VEC];
 #pragma unroll
