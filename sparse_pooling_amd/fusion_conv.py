@@ -184,6 +184,8 @@ class _FusionConvFn(torch.autograd.Function):
         pool = smap.csr(L.BY_CELL, L.ORDER_ENTRY) if pooled else None
         frame_off = smap.frame_off if pooled else None
         train_bn = conv.batch_norm and is_training
+        if pooled and ctx.needs_input_grad[1]:  # the image gradient's pixel-keyed CSR sorts beside the forward
+            smap.prefetch_csr(L.BY_PIXEL, L.ORDER_COL_ENTRY)
         xb, b_img = None, b
         if pooled and train_bn and ctx.needs_input_grad[2] and a.dtype != torch.bfloat16:
             # f32: the weight gradient needs the pooled channels in HBM (see backward): pooled here, once, the

@@ -26,6 +26,9 @@ def _i32(n, device):
     return torch.empty(max(int(n), 1), dtype=torch.int32, device=device)
 
 
+_SIDE = {}  # device -> the side stream of ShplMap.prefetch_csr
+
+
 class ShplMap:
     """M on the device. Entries are grouped by frame: frame f owns entry slots
     [frame_off[f], frame_off[f+1]) of which the first frame_nnz[f] are live
@@ -46,6 +49,7 @@ class ShplMap:
         self.frame_off, self.frame_nnz = frame_off, frame_nnz
         self.err = err if err is not None else torch.zeros(1, dtype=torch.int32, device=device)
         self._csr = {}
+        self._pending = {}  # key -> event of a csr() built on a side stream (prefetch_csr)
 
     # ---------------------------------------------------------------- checks
     def error_bits(self):
@@ -79,7 +83,14 @@ class ShplMap:
     def csr(self, direction, order):
         key = (direction, order)
         if key in self._csr:
-            return self._csr[key]
+            c = self._csr[key]
+            if key in self._pending:  # built on a side stream: the current one waits for it, and owns its buffers
+                cur = torch.cuda.current_stream(self.device)
+                cur.wait_event(self._pending.pop(key))
+                for t in (c.ent_dst, c.ent_src, c.ent_val, c.ent_col, c.key_range, c.ws):
+                    if t is not None:
+                        t.record_stream(cur)
+            return c
         n_keys = self.n_cells if direction == L.BY_CELL else self.n_pix
         rows = self.ROW_PULLS
         if rows is None:
@@ -92,6 +103,28 @@ class ShplMap:
                                        L.stream_of(self.device)), "shpl_build_csr")
         self._csr[key] = c
         return c
+
+    def prefetch_csr(self, direction, order):
+        """Start csr(direction, order) on a side stream (after the current stream's work so far: the
+        map's arrays); the first csr() of that key later makes its stream wait for it. The training
+        forward of FusionConv.fused starts the pixel-keyed CSR of the image gradient this way, so that it
+        sorts beside the forward conv instead of on the backward's critical path."""
+        key = (direction, order)
+        if key in self._csr or torch.cuda.is_current_stream_capturing():
+            return
+        dev = torch.device(self.device)
+        side = _SIDE.get(dev)
+        if side is None:
+            side = _SIDE[dev] = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        for t in (self.cell, self.col, self.val, self.pix, self.frame_off, self.frame_nnz):
+            if isinstance(t, torch.Tensor):
+                t.record_stream(side)  # read there: not reused before the side stream is done with them
+        with torch.cuda.stream(side):
+            self.csr(direction, order)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        self._pending[key] = ev
 
     def csr_tensors(self, direction, order):
         """(ent_dst, ent_src, ent_val, ent_col or None) of csr(direction, order):
