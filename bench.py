@@ -153,9 +153,17 @@ def step_bytes(cfg, spec, nnz, u_pix, u_cell, F, esz):
     return b
 
 
-def cpu_baseline(spec, frames_np, budget_s, dual, backward=False):
-    """Oracle (C port of the reference path) on one core, bounded sample."""
-    from oracle import shpl_oracle as orc
+def cpu_baseline(spec, frames_np, budget_s, dual, backward=False, impl="c"):
+    """The reference CPU path on one core, bounded sample (frames cycled until the budget):
+    impl "numpy": the numpy restatement of the reference's own numpy index builder and of
+    TF 1.8's sequential CPU pooling kernels (oracle/shpl_numpy.py: np.dot / np.round / masks,
+    np.add.at); impl "c": the C port of the same path (oracle/shpl_oracle.c)."""
+    if impl == "numpy":
+        from oracle import shpl_numpy as orc
+        what = "oracle/shpl_numpy.py (numpy: the reference's index builder, TF-CPU-order np.add.at pooling)"
+    else:
+        from oracle import shpl_oracle as orc
+        what = "oracle/shpl_oracle.c (C port)"
     Hb, Wb = spec.bev_feat_hw
     Hi, Wi = spec.img_feat_hw
     rng = np.random.default_rng(0)
@@ -188,12 +196,25 @@ def cpu_baseline(spec, frames_np, budget_s, dual, backward=False):
         done += 1
     total = t_index + t_pool
     return {"value": round(done / total, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": (f"{done} frames of this workload ({spec.n_points} pts) through oracle/shpl_oracle.c: "
+            "index_ms_per_frame": round(1e3 * t_index / done, 3), "pool_ms_per_frame": round(1e3 * t_pool / done, 3),
+            "sample": (f"{done} frames of this workload ({spec.n_points} pts) through {what}: "
                        f"index build {1e3 * t_index / done:.2f} ms/frame + TF-order pooling and concat "
                        f"{1e3 * t_pool / done:.2f} ms/frame"
                        + ((" (both directions, forward + gradients, f32)" if backward else
                            " (both directions, forward only)") if dual else "")
                        + f", single thread, {os.cpu_count()} host cpus visible")}
+
+
+def cpu_baselines(spec, frames_np, budget_s, dual, backward, parallel):
+    """SURVEY §8d's CPU baseline: the numpy restatement of the reference path (the
+    headline `value`), the C port beside it, and the C port frame-parallel over the
+    usable cores."""
+    npy = cpu_baseline(spec, frames_np, budget_s, dual, backward, impl="numpy")
+    port = cpu_baseline(spec, frames_np, budget_s, dual, backward, impl="c")
+    out = dict(npy, numpy=dict(npy), port=port)
+    if parallel:
+        out["parallel"] = cpu_baseline_parallel(spec, frames_np, budget_s, dual, backward)
+    return out
 
 
 def _cpu_worker(q, barrier, spec, frames_np, budget_s, dual, backward):
@@ -257,27 +278,58 @@ def self_launch(args):
     return subprocess.call(cmd)
 
 
-def checksum_report(key, local, dev, rank, args):
-    """All-gather the per-frame checksums (global frame order), compare them
-    with the N=1 run's stored under `key`, store them with --write-checksums."""
+def checksum_report(base, local, fids, dev, rank, args):
+    """All-gather the per-frame checksums and their global frame ids (rank order),
+    compare each frame with the N=1 run's checksum of the same global frame id
+    (profiles/frame_checksums.json: tables `<base>_frames<n>`, frame i at index i;
+    a frame's output does not depend on its rank or on what shares its launch, so
+    any partition or sub-batch is checked), store them with --write-checksums."""
     from sparse_pooling_amd import dist as sd
     allcs = sd.gather_frame_checksums(local, device=dev)
-    ref = None
+    allfids = sd.gather_frame_checksums(torch.as_tensor(fids, dtype=torch.int64, device=dev), device=dev)
+    tab = {}
     if os.path.exists(CHECKSUM_FILE):
         with open(CHECKSUM_FILE) as fh:
-            ref = json.load(fh).get(key)
+            tab = json.load(fh)
+    tables = [(k, v) for k, v in tab.items() if k.startswith(base + "_frames")]
+    ref_key, ref = max(tables, key=lambda kv: len(kv[1])) if tables else (None, None)
+    match = None
+    if ref is not None and allfids and max(allfids) < len(ref):
+        match = all(ref[f] == c for f, c in zip(allfids, allcs))
     if args.write_checksums and rank == 0:
-        tab = {}
-        if os.path.exists(CHECKSUM_FILE):
-            with open(CHECKSUM_FILE) as fh:
-                tab = json.load(fh)
-        tab[key] = allcs
+        if allfids != list(range(len(allfids))):
+            raise SystemExit("--write-checksums needs the frames 0..n-1 of a whole batch")
+        tab[f"{base}_frames{len(allcs)}"] = allcs
         with open(CHECKSUM_FILE, "w") as fh:
             json.dump(tab, fh, indent=0)
-    return {"key": key, "frames": len(allcs),
+    return {"key": base, "frames": len(allcs), "frame_ids": [min(allfids), max(allfids)] if allfids else None,
+            "compared_with": ref_key,
             "digest": hashlib.sha256(json.dumps(allcs).encode()).hexdigest()[:16],
-            "match_n1": None if ref is None else ref == allcs,
-            "first": allcs[:4]}
+            "match_n1": match, "first": allcs[:4]}
+
+
+def lib_sha256():
+    """Content hash of the HIP library this run loaded (traffic provenance)."""
+    from sparse_pooling_amd import _lib as L
+    with open(L.LIB_PATH, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
+
+
+def traffic_lookup(key, field="hbm_bytes_per_launch"):
+    """PMC HBM bytes of `key` in profiles/traffic.json, only when they were
+    measured on the library this run loaded: (value, note, entry)."""
+    tpath = os.path.join(HERE, "profiles", "traffic.json")
+    if not os.path.exists(tpath):
+        return None, "no profiles/traffic.json", None
+    with open(tpath) as fh:
+        tj = json.load(fh).get(key)
+    if not tj:
+        return None, f"no PMC entry {key}", None
+    here = lib_sha256()
+    if tj.get("lib_sha256") != here:
+        return None, (f"stale: {key} was measured on libshpl.so {tj.get('lib_sha256')} "
+                      f"(commit {tj.get('commit')}), this run loaded {here}"), None
+    return tj[field], f"PMC of {key}, libshpl.so {here}, commit {tj.get('commit')}", tj
 
 
 def main():
@@ -420,8 +472,8 @@ def main():
         elapsed = sd.timed(lambda k: step(evs[k]), args.steps, device=dev)
     args_steps_ev = n_ev
     outs = [pl.bv_fused] + ([pl.img_fused] if dual else []) + ([d_bev, d_img] if backward else [])
-    checks = checksum_report(f"layer_config{cfg}_frames{F * world}", sum(sd.frame_checksums(t) for t in outs),
-                             dev, rank, args)
+    checks = checksum_report(f"layer_config{cfg}", sum(sd.frame_checksums(t) for t in outs), fids, dev, rank, args)
+    comm = sd.comm_report(dev)
     nbytes = step_bytes(cfg, spec, nnz, u_pix, u_cell, F, esz)
     kernels = {}
     interleaved = dual and not args.no_overlap and not pl.rows and pl.interleave
@@ -452,20 +504,11 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(spec, frames[: min(F, 64)], args.cpu_seconds, dual, backward)
-        if not args.no_cpu_parallel:
-            cpu["parallel"] = cpu_baseline_parallel(spec, frames[: min(F, 64)], args.cpu_seconds, dual, backward)
+        cpu = cpu_baselines(spec, frames[: min(F, 64)], args.cpu_seconds, dual, backward, not args.no_cpu_parallel)
 
     if rank == 0:
         total_frames = F * world * args.steps
-        traffic = None
-        tpath = os.path.join(HERE, "profiles", "traffic.json")
-        if os.path.exists(tpath):
-            with open(tpath) as fh:
-                tj = json.load(fh)
-            key = f"config{cfg}_F{F}"
-            if key in tj:
-                traffic = tj[key]["hbm_bytes_per_launch"]
+        traffic, traffic_note, _ = traffic_lookup(f"config{cfg}_F{F}")
         what = {2: "img->BEV SHPL fwd", 3: "dual SHPL fwd + bwd (bf16 storage, f32 accumulate)",
                 5: "dual SHPL fwd (img->BEV and BEV->img)"}[cfg]
         out = {
@@ -512,6 +555,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_note": traffic_note,
                 "algorithmic_bytes_per_launch": nbytes,
                 "kernel_ms": round(layer_ms, 4),
                 "k_dense_ms": round(dense_ms, 4),
@@ -523,6 +567,8 @@ def main():
             "cpu_baseline": cpu,
             "index_errors": err,
             "frame_checksums": checks,
+            "comm": comm,
+            "lib_sha256": lib_sha256(),
         }
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -615,15 +661,11 @@ def run_frames(args, world, rank, dev):
     step_bytes = (nbytes + 16 * int(fr.total_points) + 2 * 24 * n_cam + F * pl.Hb * pl.Wb * n_maps * 8
                   + 40 * n_vox + 40 * n_vox + 56 * nnz)
     step_gbs = step_bytes / (elapsed / args.steps) / 1e9
-    traffic, step_traffic = None, None  # PMC (scripts/r02_pmc.sh TAG=frames, traffic.py step frames_F64 ...)
-    tpath = os.path.join(HERE, "profiles", "traffic.json")
-    if os.path.exists(tpath):
-        with open(tpath) as fh:
-            tj = json.load(fh).get(f"frames_F{F}")
-        if tj:
-            traffic, step_traffic = tj["hbm_bytes_per_launch"], tj.get("step_bytes_all_kernels")
-    checks = checksum_report(f"frames_{args.scan_points}_frames{F * world}", sd.frame_checksums(pl.bv_fused), dev,
-                             rank, args)
+    # PMC (scripts/r02_pmc.sh TAG=frames, traffic.py step frames_F64 ...), when measured on this library
+    traffic, traffic_note, tj = traffic_lookup(f"frames_F{F}")
+    step_traffic = tj.get("step_bytes_all_kernels") if tj else None
+    checks = checksum_report(f"frames_{args.scan_points}", sd.frame_checksums(pl.bv_fused), fids, dev, rank, args)
+    comm = sd.comm_report(dev)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         scans = [fr.xyzi[int(fr.point_offsets[f]):int(fr.point_offsets[f + 1])].cpu().numpy() for f in range(min(F, 8))]
@@ -650,11 +692,13 @@ def run_frames(args, world, rank, dev):
             "frame_checksums": checks,
             "roofline": {"bound": "hbm", "kernel": "k_dense + k_sparse (fused layer)", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "algorithmic_bytes_per_launch": nbytes,
+                         "traffic": traffic, "traffic_note": traffic_note, "algorithmic_bytes_per_launch": nbytes,
                          "step_traffic": step_traffic, "step_algorithmic_bytes": step_bytes, "step_GBps": round(step_gbs, 1),
                          "step_frac": round(step_gbs / HBM_PEAK_GBS, 4)},
             "cpu_baseline": cpu,
             "index_errors": errs,
+            "comm": comm,
+            "lib_sha256": lib_sha256(),
         }
         print(json.dumps(out), flush=True)
 
@@ -759,13 +803,9 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
     hbm_gbs = hbm_bytes / step_s / 1e9
     # the bound: the larger of the two floors (f32: MFMA; bf16: HBM)
     hbm_bound = hbm_bytes / (HBM_PEAK_GBS * 1e9) > flops / (MFMA_PEAK_TFS[dname] * 1e12)
-    traffic = None  # PMC bytes of every SHPL kernel of a step (scripts/r02_pmc.sh TAG=train..., traffic.py step)
-    tpath = os.path.join(HERE, "profiles", "traffic.json")
-    if os.path.exists(tpath):
-        with open(tpath) as fh:
-            tj = json.load(fh).get(f"train_{dname}_F{F}")
-        if tj:
-            traffic = tj["hbm_bytes_per_launch"]
+    # PMC bytes of every SHPL kernel of a step (scripts/r02_pmc.sh TAG=train..., traffic.py step)
+    traffic, traffic_note, _ = traffic_lookup(f"train_{dname}_F{F}")
+    comm = sd.comm_report(dev)
     if rank == 0:
         print(json.dumps({
             "metric": "SHPL + post-fusion conv training frames/sec (fwd + bwd), 1/2/4/8 GPU",
@@ -783,7 +823,7 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
                           "(pooled map, conv fwd, BN apply, BN backward x2, input and weight gradients, image "
                           "gradient) over the forward + backward time",
                           "achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                          "frac": round(hbm_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                          "frac": round(hbm_gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_note": traffic_note,
                           "algorithmic_bytes_per_step": hbm_bytes, "mfma_tflops": round(tflops, 2),
                           "mfma_frac": round(tflops / MFMA_PEAK_TFS[dname], 4)} if hbm_bound else
                          {"bound": "mfma", "kernel": "fwd + input-gradient + weight-gradient convs (3x the forward "
@@ -791,9 +831,11 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
                           "achieved": round(tflops, 2), "peak": MFMA_PEAK_TFS[dname], "unit": "TFLOP/s",
                           "frac": round(tflops / MFMA_PEAK_TFS[dname], 4), "traffic": None,
                           "algorithmic_bytes_per_step": hbm_bytes, "hbm_GBps": round(hbm_gbs, 1),
-                          "hbm_traffic_per_step": traffic}),
+                          "hbm_traffic_per_step": traffic, "traffic_note": traffic_note}),
             "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4),
             "cpu_baseline": None,
+            "comm": comm,
+            "lib_sha256": lib_sha256(),
         }), flush=True)
 
 
@@ -876,16 +918,10 @@ def run_conv(args, world, rank, dev):
     u_pix = int(torch.unique(pl.pix[pl.pix >= 0]).numel())
     hbm_bytes = F * Hb * Wb * (cb + ci) * esz + u_pix * ci * esz + 12 * nnz  # read bev, write out, gather
     tflops = flops / (conv_ms * 1e-3) / 1e12
-    checks = None if train else checksum_report(f"conv_{args.dtype}_frames{F * world}", sd.frame_checksums(out),
-                                                dev, rank, args)
-    traffic, mfma_busy = None, None
-    tpath = os.path.join(HERE, "profiles", "traffic.json")
-    if os.path.exists(tpath):
-        with open(tpath) as fh:
-            tj = json.load(fh).get(f"conv_{args.dtype}_F{F}")
-        if tj:
-            traffic = tj["hbm_bytes_per_launch"]
-            mfma_busy = tj.get("mfma_busy_share")
+    checks = None if train else checksum_report(f"conv_{args.dtype}", sd.frame_checksums(out), fids, dev, rank, args)
+    comm = sd.comm_report(dev)
+    traffic, traffic_note, tj = traffic_lookup(f"conv_{args.dtype}_F{F}")
+    mfma_busy = tj.get("mfma_busy_share") if tj else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_conv(spec, frames[:1], args.cpu_seconds)
@@ -912,7 +948,7 @@ def run_conv(args, world, rank, dev):
                                     "staging), MFMA v_mfma_f32_32x32x2_f32"),
                          "achieved": round(tflops, 2), "peak": MFMA_PEAK_TFS[dname], "unit": "TFLOP/s",
                          "frac": round(tflops / MFMA_PEAK_TFS[dname], 4), "traffic": traffic,
-                         "mfma_busy_share_pmc": mfma_busy,
+                         "traffic_note": traffic_note, "mfma_busy_share_pmc": mfma_busy,
                          "algorithmic_flops_per_launch": flops, "kernel_ms": round(conv_ms, 4),
                          "hbm_algorithmic_bytes_per_launch": hbm_bytes,
                          "hbm_GBps": round(hbm_bytes / (conv_ms * 1e-3) / 1e9, 1),
@@ -925,6 +961,8 @@ def run_conv(args, world, rank, dev):
                         "bitwise_equal": same},
             "cpu_baseline": cpu,
             "index_errors": err,
+            "comm": comm,
+            "lib_sha256": lib_sha256(),
         }
         print(json.dumps(out_j), flush=True)
 

@@ -292,6 +292,20 @@ int shpl_build_csr(int direction, int order, int n_frames, const int64_t *d_fram
                    const int64_t *d_frame_nnz, int64_t keys_per_frame, const int32_t *d_cell,
                    const int32_t *d_col, const float *d_val, const int32_t *d_pix,
                    const shpl_csr *csr, void *d_ws, size_t ws_bytes, void *stream);
+/* The same sort with the builder chosen explicitly instead of by batch shape
+ * (tests and measurements; every builder yields the same entry lists):
+ * SHPL_CSR_AUTO = shpl_build_csr's choice, SHPL_CSR_FRAME one workgroup per
+ * frame, SHPL_CSR_SEGMENT balanced destination segments, SHPL_CSR_RANGE one
+ * workgroup per (frame, destination range). A key_range CSR always takes the
+ * range builder. Same arguments and errors as shpl_build_csr otherwise. */
+#define SHPL_CSR_AUTO 0
+#define SHPL_CSR_FRAME 1
+#define SHPL_CSR_SEGMENT 2
+#define SHPL_CSR_RANGE 3
+int shpl_build_csr_path(int path, int direction, int order, int n_frames, const int64_t *d_frame_off,
+                        const int64_t *d_frame_nnz, int64_t keys_per_frame, const int32_t *d_cell,
+                        const int32_t *d_col, const float *d_val, const int32_t *d_pix,
+                        const shpl_csr *csr, void *d_ws, size_t ws_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Pull kernels: the sparse gather / scatter-add of SHPL

@@ -16,7 +16,17 @@
  *                    GatherNd                  copy params[idx[k]] -> P[k]; OOB is InvalidArgument
  *                    SparseTensorDenseMatMul   out = 0; for i in nnz order: out[m] += a_i * B[k]
  *                                              (adjoint_a swaps m/k; separate mul and add, the
- *                                              pip TF 1.8 binaries are built without FMA)
+ *                                              pip TF 1.8 binaries are built without FMA).
+ *                                              TF 1.8's sparse_tensor_dense_matmul_op.cc has two
+ *                                              CPU branches: below kNumVectorize = 32 right-hand
+ *                                              columns a scalar loop `out(m, n) += a * b(k, n)`;
+ *                                              from 32 on (config 2: Ci = 32; config 3: 256) the
+ *                                              Eigen form `out.chip<0>(m) += b.chip(k) * a`, a
+ *                                              coefficient-wise padd(out, pmul(b, a)) -- Eigen
+ *                                              emits pmadd only inside its GEMM kernels, and the
+ *                                              AVX-only build cannot contract. Both branches walk
+ *                                              nnz in order and round the product before the add,
+ *                                              so one restatement covers both.
  *                    SparseTranspose           permute index columns, then SparseReorder:
  *                                              lexicographic (col,row) order; equal keys keep
  *                                              input order here (TF's std::sort leaves them unspecified)

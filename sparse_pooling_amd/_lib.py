@@ -22,6 +22,7 @@ BY_CELL, BY_PIXEL = 0, 1
 ORDER_ENTRY, ORDER_COL_ROW, ORDER_COL_ENTRY = 0, 1, 2
 OUT_POOL, OUT_CONCAT, OUT_ADD = 0, 1, 2
 ACT_NONE, ACT_RELU = 0, 1
+CSR_AUTO, CSR_FRAME, CSR_SEGMENT, CSR_RANGE = 0, 1, 2, 3
 
 _lib = None
 
@@ -104,6 +105,8 @@ def _declare(lib):
         "shpl_csr_workspace_bytes": (i32, [i64, i64, psz]),
         "shpl_build_csr": (i32, [i32, i32, i32, p, p, i64, p, p, p, p, ctypes.POINTER(ShplCsr), p, sz,
                                  p]),
+        "shpl_build_csr_path": (i32, [i32, i32, i32, i32, p, p, i64, p, p, p, p, ctypes.POINTER(ShplCsr), p,
+                                      sz, p]),
         "shpl_pull": (i32, pull_args),
         "shpl_pull_dense": (i32, pull_args),
         "shpl_pull_sparse": (i32, pull_args),

@@ -15,8 +15,6 @@
 // a few entries each, so the quadratic rank costs less than a sort pass.
 #include "shpl_common.h"
 
-#include <stdlib.h>
-
 namespace shpl {
 namespace {
 
@@ -843,10 +841,11 @@ extern "C" int shpl_csr_workspace_bytes(int64_t n_keys, int64_t nnz_cap, size_t 
     return SHPL_OK;
 }
 
-extern "C" int shpl_build_csr(int direction, int order, int n_frames, const int64_t *d_frame_off,
-                              const int64_t *d_frame_nnz, int64_t keys_per_frame, const int32_t *d_cell,
-                              const int32_t *d_col, const float *d_val, const int32_t *d_pix, const shpl_csr *csr,
-                              void *d_ws, size_t ws_bytes, void *stream) {
+extern "C" int shpl_build_csr_path(int path, int direction, int order, int n_frames, const int64_t *d_frame_off,
+                                   const int64_t *d_frame_nnz, int64_t keys_per_frame, const int32_t *d_cell,
+                                   const int32_t *d_col, const float *d_val, const int32_t *d_pix,
+                                   const shpl_csr *csr, void *d_ws, size_t ws_bytes, void *stream) {
+    if (path < SHPL_CSR_AUTO || path > SHPL_CSR_RANGE) return SHPL_ERR_ARG;
     if (!csr || !d_frame_off || n_frames < 1) return SHPL_ERR_ARG;
     if (direction != SHPL_BY_CELL && direction != SHPL_BY_PIXEL) return SHPL_ERR_ARG;
     if (order < SHPL_ORDER_ENTRY || order > SHPL_ORDER_COL_ENTRY) return SHPL_ERR_ARG;
@@ -854,7 +853,14 @@ extern "C" int shpl_build_csr(int direction, int order, int n_frames, const int6
     if (keys_per_frame < 1 || nnz_cap < 0 || csr->n_keys < (int64_t)n_frames * keys_per_frame ||
         csr->n_keys >= 2147483647LL || nnz_cap >= 2147483647LL)
         return SHPL_ERR_BAD_SHAPE;
-    if (nnz_cap == 0) return SHPL_OK;
+    if (nnz_cap == 0) {
+        // an empty map: every destination's run is empty (first == end == 0)
+        if (csr->key_range && csr->n_keys > 0 &&
+            hipMemsetAsync(csr->key_range, 0, sizeof(int32_t) * 2 * (size_t)csr->n_keys, (hipStream_t)stream) !=
+                hipSuccess)
+            return SHPL_ERR_HIP;
+        return SHPL_OK;
+    }
     if (!d_cell || !d_val || !d_pix || !csr->ent_dst || !csr->ent_src || !csr->ent_val || !d_ws) return SHPL_ERR_ARG;
     if (direction == SHPL_BY_PIXEL && !csr->ent_col) return SHPL_ERR_ARG;
     const CsrLayout lay = csr_layout(nnz_cap);
@@ -863,13 +869,13 @@ extern "C" int shpl_build_csr(int direction, int order, int n_frames, const int6
     // The range CSR: always when key ranges are asked for; by default for batches under
     // SEG_FRAMES frames of at most RANGE_MAX_KEYS destinations (each workgroup reads its
     // whole frame, so many ranges per frame would multiply those reads).
-    const char *path = getenv("SHPL_CSR_PATH");
     // (entry offsets inside a frame travel in 24 bits: capacities under 2^24 entries)
     const bool small_cap = nnz_cap < ((int64_t)1 << 24);
     if (csr->key_range && !small_cap) return SHPL_ERR_BAD_SHAPE;
     const bool ranged = csr->key_range != nullptr ||
-                        (small_cap && (path ? path[0] == 'r'
-                                            : (n_frames < SEG_FRAMES && keys_per_frame <= RANGE_MAX_KEYS)));
+                        (small_cap && (path != SHPL_CSR_AUTO
+                                           ? path == SHPL_CSR_RANGE
+                                           : (n_frames < SEG_FRAMES && keys_per_frame <= RANGE_MAX_KEYS)));
     if (ranged) {
         if (ws_bytes < align_up(sizeof(uint64_t) * (size_t)nnz_cap, 256)) return SHPL_ERR_WORKSPACE;
         const int64_t n_ranges = (keys_per_frame + RANGE_KEYS - 1) / RANGE_KEYS;
@@ -899,8 +905,8 @@ extern "C" int shpl_build_csr(int direction, int order, int n_frames, const int6
     // Small batches take the segmented path (config 3, 4 frames: 0.305 -> 0.259 ms per step); from
     // SEG_FRAMES frames on, one workgroup per frame fills enough of the chip and, overlapped with the
     // dense stream, measured faster (config 2, 64 frames: 2.34 vs 2.42 ms per step).
-    // SHPL_CSR_PATH=frame|segment|range forces a path (measurements).
-    const bool want = path ? path[0] == 's' : n_frames < SEG_FRAMES;
+    // shpl_build_csr_path(SHPL_CSR_FRAME | _SEGMENT | _RANGE, ...) forces a path (tests, measurements).
+    const bool want = path != SHPL_CSR_AUTO ? path == SHPL_CSR_SEGMENT : n_frames < SEG_FRAMES;
     const bool segmented = want && ws_bytes >= lay.total && (int64_t)n_frames * (n_bins + S) <= seg_cap_of(nnz_cap);
     if (!segmented) {
         // one workgroup per frame; needs only the tmp words
@@ -954,4 +960,12 @@ extern "C" int shpl_build_csr(int direction, int order, int n_frames, const int6
                            csr->ent_src, csr->ent_val, csr->ent_col);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
+}
+
+extern "C" int shpl_build_csr(int direction, int order, int n_frames, const int64_t *d_frame_off,
+                              const int64_t *d_frame_nnz, int64_t keys_per_frame, const int32_t *d_cell,
+                              const int32_t *d_col, const float *d_val, const int32_t *d_pix, const shpl_csr *csr,
+                              void *d_ws, size_t ws_bytes, void *stream) {
+    return shpl_build_csr_path(SHPL_CSR_AUTO, direction, order, n_frames, d_frame_off, d_frame_nnz, keys_per_frame,
+                               d_cell, d_col, d_val, d_pix, csr, d_ws, ws_bytes, stream);
 }

@@ -816,7 +816,9 @@ using namespace shpl;
 
 extern "C" int shpl_pull(SHPL_PULL_ARGS) {
     SHPL_PLAN();
-    if (csr->key_range) return rows(pl, csr, direction, (hipStream_t)stream);
+    // row-keyed form only over a built CSR: an empty map (nnz_cap == 0) has no sorted entries and
+    // shpl_build_csr leaves nothing for k_rows to walk -- the streaming pass alone is the whole pull
+    if (csr->key_range && csr->nnz_cap > 0) return rows(pl, csr, direction, (hipStream_t)stream);
     rc = dense(pl, (hipStream_t)stream);
     if (rc) return rc;
     return sparse(pl, csr, direction, (hipStream_t)stream);

@@ -92,7 +92,13 @@ def _sync(device):
 
 def timed(fn, steps, device=None):
     """Run ``fn`` ``steps`` times between barriers + device syncs; returns the
-    elapsed seconds maximised over ranks."""
+    elapsed seconds maximised over ranks.
+
+    Each rank's clock runs from after the opening barrier and device sync to
+    its closing device sync; the closing barrier comes after the clock stops,
+    so a collective's own latency (a visible share of an 8-rank run's ~6 ms
+    window) is never timed. The MAX over ranks is then the slowest rank's
+    compute span, all ranks having started together."""
     on = dist.is_available() and dist.is_initialized()
     if on:
         dist.barrier()
@@ -101,9 +107,9 @@ def timed(fn, steps, device=None):
     for k in range(steps):
         fn(k)
     _sync(device)
+    elapsed = time.perf_counter() - t0
     if on:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     if on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=_coll_device(device))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -134,3 +140,39 @@ def gather_frame_checksums(local, device=None):
     out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(out, t)
     return [int(x) for o in out for x in o.cpu().tolist()]
+
+
+def device_identity(device):
+    """This rank's device: ordinal, PCI location and name (for the bench line's
+    evidence that the ranks ran on distinct GPUs)."""
+    if device is None or device.type != "cuda":
+        return {"device": "cpu"}
+    p = torch.cuda.get_device_properties(device)
+    pci = None
+    if hasattr(p, "pci_bus_id"):
+        pci = f"{getattr(p, 'pci_domain_id', 0):04x}:{p.pci_bus_id:02x}:{getattr(p, 'pci_device_id', 0):02x}"
+    return {"ordinal": device.index, "pci": pci, "uuid": str(getattr(p, "uuid", "")) or None,
+            "name": p.name, "visible": os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")}
+
+
+def comm_report(device):
+    """Control-plane evidence: backend, world size, RCCL version and every
+    rank's device identity (all-gathered, rank order)."""
+    on = dist.is_available() and dist.is_initialized()
+    me = dict(device_identity(device), rank=dist.get_rank() if on else 0, host_pid=os.getpid())
+    ranks = [me]
+    if on:
+        ranks = [None] * dist.get_world_size()
+        dist.all_gather_object(ranks, me)
+    rccl = None
+    try:
+        v = torch.cuda.nccl.version()
+        rccl = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception:  # noqa: BLE001 -- no RCCL in this build
+        pass
+    pcis = [r.get("pci") or r.get("uuid") for r in ranks]
+    return {"backend": dist.get_backend() if on else None,
+            "world_size": dist.get_world_size() if on else 1,
+            "rccl_version": rccl,
+            "distinct_devices": len(set(pcis)) if all(pcis) else None,
+            "ranks": ranks}

@@ -25,7 +25,7 @@ from .shpl_map import ShplMap
 class FusedPipeline:
     # row-keyed pulls (one launch per pull, shpl_csr.key_range) for batches under this many frames whose
     # maps have at most ROWS_MAX_KEYS destinations per frame: latency-bound layers (config 3)
-    ROWS_FRAMES, ROWS_MAX_KEYS = 32, 65536
+    ROWS_FRAMES, ROWS_MAX_KEYS, ROWS_MAX_CAP = 32, 65536, 1 << 24
 
     def __init__(self, n_frames, max_points_per_frame, total_points, im_size, bv_size, stride,
                  c_bev, c_img, dtype=torch.float32, device="cuda", dual=False, rows=None, live=False):
@@ -47,7 +47,8 @@ class FusedPipeline:
         self.n_cells = self.B * self.Hb * self.Wb
         self.n_pix = self.B * self.Hi * self.Wi
         if rows is None:
-            rows = self.B < self.ROWS_FRAMES and max(self.Hb * self.Wb, self.Hi * self.Wi) <= self.ROWS_MAX_KEYS
+            rows = (self.B < self.ROWS_FRAMES and max(self.Hb * self.Wb, self.Hi * self.Wi) <= self.ROWS_MAX_KEYS
+                    and self.N < self.ROWS_MAX_CAP)  # the range CSR's 24-bit entry offsets
         self.rows = bool(rows)
         # dual layers in step_overlapped: the cell-keyed sparse pass beside img_fused's stream
         self.interleave = True
@@ -86,16 +87,19 @@ class FusedPipeline:
             L.ptr(self.pix), L.ptr(self.val), None, None, L.ptr(self.frame_nnz), L.ptr(self.frame_off),
             L.ptr(self.err), L.ptr(self.index_ws), self.index_ws.numel(), st), "shpl_build_index")
 
+    # shpl_build_csr_path's builder (L.CSR_AUTO: chosen by batch shape; tests force the others)
+    csr_path = L.CSR_AUTO
+
     def build_csr(self, which=("cell", "pixel")):
         st = L.stream_of(self.dev)
         args = (self.B, L.ptr(self.frame_off), L.ptr(self.frame_nnz))
         if "cell" in which:
-            L.check(self._lib.shpl_build_csr(
-                L.BY_CELL, L.ORDER_ENTRY, *args, self.Hb * self.Wb, L.ptr(self.cell), None, L.ptr(self.val),
+            L.check(self._lib.shpl_build_csr_path(
+                self.csr_path, L.BY_CELL, L.ORDER_ENTRY, *args, self.Hb * self.Wb, L.ptr(self.cell), None, L.ptr(self.val),
                 L.ptr(self.pix), self.csr.ref(), L.ptr(self.csr.ws), self.csr.ws.numel(), st), "shpl_build_csr")
         if self.dual and "pixel" in which:
-            L.check(self._lib.shpl_build_csr(
-                L.BY_PIXEL, L.ORDER_COL_ROW, *args, self.Hi * self.Wi, L.ptr(self.cell), None, L.ptr(self.val),
+            L.check(self._lib.shpl_build_csr_path(
+                self.csr_path, L.BY_PIXEL, L.ORDER_COL_ROW, *args, self.Hi * self.Wi, L.ptr(self.cell), None, L.ptr(self.val),
                 L.ptr(self.pix), self.pcsr.ref(), L.ptr(self.pcsr.ws), self.pcsr.ws.numel(), st),
                 "shpl_build_csr")
 

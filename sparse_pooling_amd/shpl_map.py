@@ -77,7 +77,7 @@ class ShplMap:
     # Row-keyed pulls (shpl_csr.key_range: one launch per pull) for maps of fewer
     # than ROWS_FRAMES frames with at most ROWS_MAX_KEYS destinations per frame;
     # ROW_PULLS = True / False forces the form (tests).
-    ROWS_FRAMES, ROWS_MAX_KEYS = 32, 65536
+    ROWS_FRAMES, ROWS_MAX_KEYS, ROWS_MAX_CAP = 32, 65536, 1 << 24
     ROW_PULLS = None
 
     def csr(self, direction, order):
@@ -94,7 +94,9 @@ class ShplMap:
         n_keys = self.n_cells if direction == L.BY_CELL else self.n_pix
         rows = self.ROW_PULLS
         if rows is None:
-            rows = self.n_frames < self.ROWS_FRAMES and n_keys // max(self.n_frames, 1) <= self.ROWS_MAX_KEYS
+            # (the range CSR carries entry offsets in 24 bits: capacities under 2^24 slots)
+            rows = (self.n_frames < self.ROWS_FRAMES and n_keys // max(self.n_frames, 1) <= self.ROWS_MAX_KEYS
+                    and self.nnz_cap < self.ROWS_MAX_CAP)
         c = L.Csr(n_keys, self.nnz_cap, self.device, with_col=direction == L.BY_PIXEL, key_range=rows)
         L.check(L.lib().shpl_build_csr(direction, order, self.n_frames, L.ptr(self.frame_off),
                                        L.ptr(self.frame_nnz), n_keys // self.n_frames,

@@ -50,6 +50,9 @@ def _worker(rank, world, port, q):
     out = _frame_outputs(fids)
     el = sd.timed(lambda k: time.sleep(0.05 * (rank + 1)), 2)   # rank 1 is slower on purpose
     cs = sd.gather_frame_checksums(sd.frame_checksums(out))
+    comm = sd.comm_report(None)
+    assert comm["backend"] == "gloo" and comm["world_size"] == world
+    assert [r["rank"] for r in comm["ranks"]] == list(range(world))
     q.put((rank, fids, el, cs))
     dist.destroy_process_group()
 

@@ -39,6 +39,31 @@ def test_strong_partition_two_ranks_matches_one(extra):
     assert c1["frames"] == c2["frames"] == 4
     assert c1["digest"] == c2["digest"], (c1, c2)
     assert one["index_errors"] == 0 and two["index_errors"] == 0
+    assert two["comm"]["backend"] == "gloo" and two["comm"]["world_size"] == 2
+    assert [r["rank"] for r in two["comm"]["ranks"]] == [0, 1]
+    assert one["comm"]["world_size"] == 1 and one["lib_sha256"] == two["lib_sha256"]
+
+
+def test_eight_frame_rank_shape_matches_stored_n1_table():
+    """One rank of the driver's N=8 config-4 run owns 8 frames (the segmented CSR
+    path): its per-frame checksums equal frames 0-7 of the stored 64-frame N=1
+    table (profiles/frame_checksums.json), compared by global frame id."""
+    one = _bench(["--gpus", "1", "--frames", "8", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"])
+    c = one["frame_checksums"]
+    assert c["frames"] == 8 and c["frame_ids"] == [0, 7]
+    assert c["compared_with"] == "layer_config2_frames64"
+    assert c["match_n1"] is True, c
+    assert one["config"]["frames_per_gpu_per_step"] == 8 and one["index_errors"] == 0
+
+
+def test_sub_batch_over_two_ranks_matches_stored_n1_table():
+    """A 32-frame global batch over 2 ranks on one device (16 frames per rank, the
+    N=4 rank shape): every gathered frame matches the 64-frame N=1 table by its
+    global frame id."""
+    two = _bench(["--gpus", "2", "--frames", "32", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+                  "--partition", "strong"], {"SHPL_DIST_BACKEND": "gloo"})
+    c = two["frame_checksums"]
+    assert c["frames"] == 32 and c["frame_ids"] == [0, 31] and c["match_n1"] is True, c
 
 
 def test_weak_partition_is_the_global_batch_of_frames_times_ranks():

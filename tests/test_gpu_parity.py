@@ -344,6 +344,75 @@ def test_empty_M():
     assert not out[..., 4:].any()
 
 
+@pytest.mark.parametrize("rows_mode", [True, False])
+def test_empty_map_pulls_every_form(rows_mode):
+    """pack_map with nnz = 0, pulled through the row-keyed (key_range CSR) and the
+    dense + sparse forms, every output mode: the pooled part is zeros, CONCAT copies
+    the pass-through half, ADD is pass + 0 (-0 -> +0), no uninitialised key_range
+    is walked (the outputs start as NaN)."""
+    from sparse_pooling_amd import _lib as L
+    from sparse_pooling_amd import shpl_map as sm
+    c, R, h, w = 8, 42, 9, 11
+    img = synth.make_features((1, h, w, c), 1)
+    bev = synth.make_features((1, 6, 7, c), 2)
+    bev.flat[0] = -0.0
+    ti, tb = torch.from_numpy(img).to(DEV), torch.from_numpy(bev).to(DEV)
+    sm.ShplMap.ROW_PULLS = rows_mode
+    try:
+        smap = sm.pack_map(torch.zeros((0, 2), dtype=torch.int64, device=DEV), torch.zeros(0, device=DEV),
+                           np.array([R, 0]), torch.zeros((0, 3), dtype=torch.int64, device=DEV), img.shape)
+        for direction, order, src, pas, nrow in ((L.BY_CELL, L.ORDER_ENTRY, ti, tb, R),
+                                                 (L.BY_PIXEL, L.ORDER_COL_ROW, tb, ti, h * w)):
+            p2 = pas.reshape(nrow, c)
+            pool = torch.full((nrow, c), float("nan"), device=DEV)
+            sm.pull(smap, direction, order, src, c, 0, c, pool, c)
+            cat = torch.full((nrow, 2 * c), float("nan"), device=DEV)
+            sm.pull(smap, direction, order, src, c, 0, c, cat, 2 * c, pass_=p2, pass_stride=c, c_pass=c,
+                    mode=L.OUT_CONCAT)
+            add = torch.full((nrow, c), float("nan"), device=DEV)
+            sm.pull(smap, direction, order, src, c, 0, c, add, c, pass_=p2, pass_stride=c, c_pass=c,
+                    mode=L.OUT_ADD)
+            torch.cuda.synchronize()
+            zero = np.zeros((nrow, c), np.float32)
+            np.testing.assert_array_equal(_np(pool).view(np.uint32), zero.view(np.uint32))
+            np.testing.assert_array_equal(_np(cat)[:, :c].view(np.uint32), _np(p2).view(np.uint32))
+            np.testing.assert_array_equal(_np(cat)[:, c:].view(np.uint32), zero.view(np.uint32))
+            np.testing.assert_array_equal(_np(add).view(np.uint32), (_np(p2) + np.float32(0)).view(np.uint32))
+    finally:
+        sm.ShplMap.ROW_PULLS = None
+
+
+@pytest.mark.parametrize("n", [3000, 20000])
+def test_range_csr_one_long_run(n):
+    """Every entry of a frame on ONE destination (all points on one cell and one
+    pixel): the range CSR's degenerate case (one run longer than its LDS list at
+    n = 20000), row-keyed pulls in both directions against the oracle, bitwise."""
+    from sparse_pooling_amd import _lib as L
+    from sparse_pooling_amd import shpl_map as sm
+    rng = np.random.default_rng(5)
+    c, R, h, w = 8, 64, 6, 7
+    idx = np.tile(np.array([[0, 2, 3]], np.int64), (n, 1))
+    mij = np.stack([np.full(n, 17), np.arange(n)], 1).astype(np.int64)
+    mval = rng.uniform(-1, 1, n).astype(np.float32)
+    img = rng.standard_normal((1, h, w, c)).astype(np.float32)
+    bev = rng.standard_normal((1, 8, 8, c)).astype(np.float32)
+    ti, tb = torch.from_numpy(img).to(DEV), torch.from_numpy(bev).to(DEV)
+    sm.ShplMap.ROW_PULLS = True
+    try:
+        smap = sm.pack_map(torch.from_numpy(mij).to(DEV), torch.from_numpy(mval).to(DEV), np.array([R, n]),
+                           torch.from_numpy(idx).to(DEV), img.shape)
+        pool = torch.full((R, c), float("nan"), device=DEV)
+        sm.pull(smap, L.BY_CELL, L.ORDER_ENTRY, ti, c, 0, c, pool, c)
+        trans = torch.full((h * w, c), float("nan"), device=DEV)
+        sm.pull(smap, L.BY_PIXEL, L.ORDER_COL_ROW, tb, c, 0, c, trans, c)
+        torch.cuda.synchronize()
+    finally:
+        sm.ShplMap.ROW_PULLS = None
+    _close_and_exact(_np(pool), orc.sparse_pool_op(mij, mval, [R, n], img, idx).reshape(R, c))
+    _close_and_exact(_np(trans), orc.sparse_pool_trans_op(mij, mval, [R, n], bev.reshape(-1, c), idx,
+                                                          img.shape).reshape(h * w, c))
+
+
 def test_bf16_storage_fp32_accumulate():
     """Config 3 storage: bf16 in/out, f32 accumulation, rounded once (RNE)."""
     from sparse_pooling_amd import sparse_pool_utils as spu
@@ -546,7 +615,7 @@ def _ragged_frames(base, sizes, seed):
 
 def _ragged_pipeline_run(cfg, sizes, dtype, paths):
     """FusedPipeline forward + backward over a ragged batch, once per CSR path
-    (SHPL_CSR_PATH: frame / segment / range; None = the default), each compared
+    (shpl_build_csr_path: frame / segment / range; None = the default), each compared
     with the oracle frame by frame (f32: bitwise; bf16: bitwise on the bf16 bits)."""
     from sparse_pooling_amd import pipeline
     base = synth.CONFIGS[cfg]
@@ -584,33 +653,24 @@ def _ragged_pipeline_run(cfg, sizes, dtype, paths):
         else:
             np.testing.assert_array_equal(_np(got.view(torch.int16)).view(np.uint16),
                                           orc.to_bf16_bits(exp.astype(np.float32)))
-    old = os.environ.get("SHPL_CSR_PATH")
-    try:
-        for path in paths:
-            if path is None:
-                os.environ.pop("SHPL_CSR_PATH", None)
-            else:
-                os.environ["SHPL_CSR_PATH"] = path
-            pl = pipeline.FusedPipeline(B, maxp, N, base.im_size, base.bv_size, base.stride, Cb, Ci, dtype=tdt,
-                                        dual=True)
-            d_bev, d_img = torch.empty_like(tb), torch.empty_like(ti)
-            pl.step(pts, vox, off, P, tb, ti)
-            pl.backward(tgb, tgi, d_bev, d_img)
-            torch.cuda.synchronize()
-            assert int(pl.err.item()) == 0
-            nnz = _np(pl.frame_nnz)
-            for f, (eb, ei, e_bev, e_img) in enumerate(want):
-                assert nnz[f] == refs[f]["M_size"][1], (path, f)
-                same(pl.bv_fused[f:f + 1], eb)
-                same(pl.img_fused[f:f + 1], ei)
-                same(d_bev[f:f + 1], e_bev)
-                same(d_img[f:f + 1], e_img)
-            del pl
-    finally:
-        if old is None:
-            os.environ.pop("SHPL_CSR_PATH", None)
-        else:
-            os.environ["SHPL_CSR_PATH"] = old
+    codes = {None: L.CSR_AUTO, "frame": L.CSR_FRAME, "segment": L.CSR_SEGMENT, "range": L.CSR_RANGE}
+    for path in paths:
+        pl = pipeline.FusedPipeline(B, maxp, N, base.im_size, base.bv_size, base.stride, Cb, Ci, dtype=tdt,
+                                    dual=True)
+        pl.csr_path = codes[path]
+        d_bev, d_img = torch.empty_like(tb), torch.empty_like(ti)
+        pl.step(pts, vox, off, P, tb, ti)
+        pl.backward(tgb, tgi, d_bev, d_img)
+        torch.cuda.synchronize()
+        assert int(pl.err.item()) == 0
+        nnz = _np(pl.frame_nnz)
+        for f, (eb, ei, e_bev, e_img) in enumerate(want):
+            assert nnz[f] == refs[f]["M_size"][1], (path, f)
+            same(pl.bv_fused[f:f + 1], eb)
+            same(pl.img_fused[f:f + 1], ei)
+            same(d_bev[f:f + 1], e_bev)
+            same(d_img[f:f + 1], e_img)
+        del pl
 
 
 def test_pipeline_ragged_batch_every_csr_path():
