@@ -82,6 +82,8 @@ def parse():
                          "profiles/r01_groups.log)")
     ap.add_argument("--no-interleave", action="store_true",
                     help="dual configs: start both sparse passes after both dense passes (A/B of the overlap)")
+    ap.add_argument("--csr-path", default="auto", choices=["auto", "frame", "segment", "range", "bucket"],
+                    help="layer workloads: force the CSR builder (shpl_build_csr_path; A/B measurements)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step eagerly instead of replaying one captured HIP graph of it")
     ap.add_argument("--workload", default="layer", choices=["layer", "frames", "conv"],
@@ -389,6 +391,9 @@ def main():
     side = torch.cuda.Stream(device=dev)
     side2 = torch.cuda.Stream(device=dev) if dual else None  # pixel-keyed CSR / pulls beside the cell-keyed
     pl.interleave = not args.no_interleave
+    from sparse_pooling_amd import _lib as L
+    pl.csr_path = {"auto": L.CSR_AUTO, "frame": L.CSR_FRAME, "segment": L.CSR_SEGMENT, "range": L.CSR_RANGE,
+                   "bucket": L.CSR_BUCKET}[args.csr_path]
     grouped = not dual and not args.no_overlap and args.groups > 1
     if grouped:
         host_off = np.concatenate([[0], np.cumsum([f.points.shape[0] for f in frames])])

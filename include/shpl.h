@@ -296,12 +296,17 @@ int shpl_build_csr(int direction, int order, int n_frames, const int64_t *d_fram
  * (tests and measurements; every builder yields the same entry lists):
  * SHPL_CSR_AUTO = shpl_build_csr's choice, SHPL_CSR_FRAME one workgroup per
  * frame, SHPL_CSR_SEGMENT balanced destination segments, SHPL_CSR_RANGE one
- * workgroup per (frame, destination range). A key_range CSR always takes the
- * range builder. Same arguments and errors as shpl_build_csr otherwise. */
+ * workgroup per (frame, destination range) reading the whole frame,
+ * SHPL_CSR_BUCKET the range builder over stable per-range buckets (three
+ * launches: chunk histograms, stable bucketing, one sort per bucket; entry
+ * order only -- identity columns or SHPL_ORDER_ENTRY -- else the range
+ * builder). A key_range CSR always takes a range builder (bucket when it
+ * applies). Same arguments and errors as shpl_build_csr otherwise. */
 #define SHPL_CSR_AUTO 0
 #define SHPL_CSR_FRAME 1
 #define SHPL_CSR_SEGMENT 2
 #define SHPL_CSR_RANGE 3
+#define SHPL_CSR_BUCKET 4
 int shpl_build_csr_path(int path, int direction, int order, int n_frames, const int64_t *d_frame_off,
                         const int64_t *d_frame_nnz, int64_t keys_per_frame, const int32_t *d_cell,
                         const int32_t *d_col, const float *d_val, const int32_t *d_pix,

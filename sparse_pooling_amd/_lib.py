@@ -22,7 +22,7 @@ BY_CELL, BY_PIXEL = 0, 1
 ORDER_ENTRY, ORDER_COL_ROW, ORDER_COL_ENTRY = 0, 1, 2
 OUT_POOL, OUT_CONCAT, OUT_ADD = 0, 1, 2
 ACT_NONE, ACT_RELU = 0, 1
-CSR_AUTO, CSR_FRAME, CSR_SEGMENT, CSR_RANGE = 0, 1, 2, 3
+CSR_AUTO, CSR_FRAME, CSR_SEGMENT, CSR_RANGE, CSR_BUCKET = 0, 1, 2, 3, 4
 
 _lib = None
 

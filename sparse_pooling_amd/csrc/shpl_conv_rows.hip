@@ -60,12 +60,40 @@ constexpr int REPI = NCO * 2 + 16;  // epilogue transpose pitch (bytes per pixel
 #ifndef SHPL_ROWS_XCD
 #define SHPL_ROWS_XCD 1  // XCD-contiguous item order (0: blockIdx order)
 #endif
-constexpr int RSTORES = 2;        // output stores per row step, always issued (the vmcnt arithmetic)
+#ifndef SHPL_ROWS_RSTORES
+#define SHPL_ROWS_RSTORES 2
+#endif
+constexpr int RSTORES = SHPL_ROWS_RSTORES;  // output stores per row step, always issued (the vmcnt arithmetic)
 constexpr uint32_t OOB = 0x80000000u;  // an offset past every descriptor's num_records: reads zeros
 #ifndef SHPL_ROWS_PROBE
 #define SHPL_ROWS_PROBE 0  // timing probes of k_conv_rows (wrong results): 1 no epilogue, 2 no in-loop DMAs
 #endif
 constexpr int SPF = NCO + 4;      // ST: f32 transpose pitch (floats per pixel; 16-byte rows, conflict-free b64 reads)
+#ifndef SHPL_ROWS_EPI8
+#define SHPL_ROWS_EPI8 0  // the dropped 8-byte-store epilogue (wrong results; kept only for the ISA guard's record)
+#endif
+#ifndef SHPL_ROWS_WPE
+#define SHPL_ROWS_WPE 2  // waves per SIMD of the row kernels (tests/test_isa_guard.py forces 4: spills)
+#endif
+
+// The ring's counted wait: vmcnt(K) leaves the K most recent vector-memory operations -- the DMAs and
+// stores of the RING-1 later steps -- in flight. expcnt(6) is a no-op in a compute kernel (no exports)
+// that marks the wait as this one, so tests/test_isa_guard.py can find it in the disassembly and
+// check that every path between two of them issues exactly K / (RING-1) vector-memory operations.
+#ifndef SHPL_ROWS_DRAIN
+#define SHPL_ROWS_DRAIN 0  // 1: every ring wait drains (vmcnt(0); probes of the epilogue variants only)
+#endif
+#if SHPL_ROWS_DRAIN
+#define SHPL_RING_WAIT(K) asm volatile("s_waitcnt vmcnt(0) expcnt(6)" ::: "memory")
+#else
+#define SHPL_RING_WAIT(K) asm volatile("s_waitcnt vmcnt(%0) expcnt(6)" ::"n"(K) : "memory")
+#endif
+
+// Pooled forms whose per-lane DMA offsets live in LDS instead of VGPRs (one ds_read_b32 each per row):
+// with statistics, and Q = 4 / QA = 1 (both would otherwise spill to scratch, whose reloads inside the
+// loop drain the ring).
+template <int Q, int QA, bool CMP, bool ST>
+constexpr bool offsets_in_lds() { return CMP && (ST || (Q == 4 && QA == 1)); }
 
 template <int Q, int QA, bool ST = false>
 struct Layout {
@@ -297,7 +325,7 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
                                      const uint32_t *s_offs, int lane) {
     typedef Layout<Q, QA, ST> L;
     // rows j+1 .. j+RING-1 may still be in flight: per later step RSTORES stores and NDMA DMAs
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L::NDMA + RSTORES) * (RING - 1)) : "memory");
+    SHPL_RING_WAIT((L::NDMA + RSTORES) * (RING - 1));
     f32x16 &a0 = acc[(U + 1) % 3], &a1 = acc[U], &a2 = acc[(U + 2) % 3];
     // chunk-major (q outer): a split of the channels between A and B, and the skipped pooled chunks below,
     // leave every accumulator's summation order unchanged
@@ -338,6 +366,24 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
         const bool row_ok = b >= 0 && b < n_out;
         uint16_t *orow = obase + (frame_row0 + (int64_t)(ya + b) * r.w + x0) * ostr;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the MFMAs' operand reads of the slot are done
+#if SHPL_ROWS_EPI8
+        // the dropped round-2 form (never shipped; tests/test_isa_guard.py's record of why it failed):
+        // 8-byte stores straight from the accumulators -- 4 per lane and row instead of RSTORES = 2, so the
+        // ring's counted wait leaves 2 of the next row's DMAs unwaited-for and the MFMAs read a stale slot
+    #pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int cl = 8 * g + 4 * hf;
+            uint32_t pk[2];
+    #pragma unroll
+            for (int k = 0; k < 4; k += 2) {
+                const float v0 = __builtin_fmaf(a2[4 * g + k], s_par[0][cl + k], s_par[1][cl + k]);
+                const float v1 = __builtin_fmaf(a2[4 * g + k + 1], s_par[0][cl + k + 1], s_par[1][cl + k + 1]);
+                pk[k >> 1] = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
+            }
+            uint16_t *dst = row_ok && x0 + pl < r.w ? orow + pl * (int)ostr + cl : r.junk + lane * 16 + 4 * g;
+            __builtin_memcpy(dst, pk, sizeof(pk));
+        }
+#else
     #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int cl = 8 * g + 4 * hf;
@@ -365,6 +411,7 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
             uint16_t *dst = row_ok && x0 + px < r.w ? orow + px * (int)ostr + pi * 8 : r.junk + pc * 8;
             *reinterpret_cast<u32x4 *>(dst) = v;
         }
+#endif
         if constexpr (ST) {
             // batch statistics of the pre-activation row (f32, as the tiled kernel): the accumulator through a
             // second transpose in the slot ([pixel][SPF floats]; LDS runs one wave's operations in order, so the
@@ -414,15 +461,17 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
     uint32_t oa[L::NA];
     int32_t ob[L::NB > 0 ? L::NB : 1];
 #pragma unroll
-    for (int i = 0; i < L::NA; ++i) oa[i] = (ST && CMP) ? s_offs[i * 64 + lane] : offa[i];
+    for (int i = 0; i < L::NA; ++i) oa[i] = offsets_in_lds<Q, QA, CMP, ST>() ? s_offs[i * 64 + lane] : offa[i];
 #pragma unroll
-    for (int i = 0; i < (L::NB > 0 ? L::NB : 1); ++i) ob[i] = (ST && CMP) ? (int32_t)s_offs[(L::NA + i) * 64 + lane] : offb[i];
+    for (int i = 0; i < (L::NB > 0 ? L::NB : 1); ++i)
+        ob[i] = offsets_in_lds<Q, QA, CMP, ST>() ? (int32_t)s_offs[(L::NA + i) * 64 + lane] : offb[i];
     stage<Q, QA, CMP>(r, frame_row0 + (int64_t)y * r.w + x0 - 1, live && y >= 0 && y < r.h, occ, first, oa, ob,
                       s_ring + U * L::SLOT, lane);
 }
 
 template <int Q, int QA, bool CMP, bool RELU, bool ST>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_rows(const RowArgs r) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS_WPE, SHPL_ROWS_WPE))) void k_conv_rows(
+    const RowArgs r) {
     typedef Layout<Q, QA, ST> L;
     __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING * L::SLOT];
     __shared__ __attribute__((aligned(16))) float s_par[2][NCO];
@@ -484,8 +533,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     uint32_t offa[L::NA];
     int32_t offb[L::NB > 0 ? L::NB : 1];
     lane_offsets<Q, QA, CMP>(r, x0, lane, offa, offb);
-    __shared__ uint32_t s_offs[(ST && CMP) ? (L::NA + L::NB) * 64 : 1];
-    if constexpr (ST && CMP) {
+    __shared__ uint32_t s_offs[offsets_in_lds<Q, QA, CMP, ST>() ? (L::NA + L::NB) * 64 : 1];
+    if constexpr (offsets_in_lds<Q, QA, CMP, ST>()) {
 #pragma unroll
         for (int i = 0; i < L::NA; ++i) s_offs[i * 64 + lane] = offa[i];
 #pragma unroll
@@ -595,22 +644,21 @@ __device__ __forceinline__ void wstage(const WgRowArgs &r, const uint16_t *xsrc,
                                        bool xok, int64_t gpix, bool gok, const uint32_t (&offx)[WNX],
                                        const uint32_t (&offg)[WNG], uint8_t *slot, int lane, bool pooled,
                                        uint64_t occ, int32_t first) {
-    if (CMP && pooled) {
-        const i32x4 rx = rsrc(r.cmp, xok ? OOB : 0u);
+    // one set of X DMAs whichever the source (selects, no branch: every path issues WNDMA DMAs)
+    const bool cmp = CMP && pooled;
+    const i32x4 rx = rsrc(cmp ? static_cast<const void *>(r.cmp) : static_cast<const void *>(xsrc + pix0 * xstride),
+                          xok ? OOB : 0u);
 #pragma unroll
-        for (int i = 0; i < WNX; ++i) {
+    for (int i = 0; i < WNX; ++i) {
+        uint32_t o = offx[i];
+        if (cmp) {
             const int32_t e = (int32_t)offx[i];
             const int px = (e >> 16) & 63;
             const bool hit = e >= 0 && ((occ >> px) & 1);
             const int rank = first + (int)__popcll(occ & ((1ull << px) - 1));
-            const uint32_t o = hit ? (uint32_t)((rank * r.cmp_stride + (e & 0xffff)) * 2) : OOB;
-            if (i < WNX - 1 || lane < WTX) dma16(rx, o, slot + i * 1024);
+            o = hit ? (uint32_t)((rank * r.cmp_stride + (e & 0xffff)) * 2) : OOB;
         }
-    } else {
-        const i32x4 rx = rsrc(xsrc + pix0 * xstride, xok ? OOB : 0u);
-#pragma unroll
-        for (int i = 0; i < WNX; ++i)
-            if (i < WNX - 1 || lane < WTX) dma16(rx, offx[i], slot + i * 1024);
+        if (i < WNX - 1 || lane < WTX) dma16(rx, o, slot + i * 1024);
     }
     const i32x4 rg = rsrc(r.gy + gpix * r.gy_stride, gok ? OOB : 0u);
 #pragma unroll
@@ -624,7 +672,7 @@ __device__ __forceinline__ void wstep(const WgRowArgs &r, f32x16 (&acc)[9], bf16
                                       int64_t frame_row0, int x0, int ya, int n_in, int n_out, int j,
                                       const uint32_t (&offx)[WNX], const uint32_t (&offg)[WNG], int lane,
                                       bool pooled, const uint64_t *s_occ, const int32_t *s_first) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WNDMA * 2) : "memory");  // rows j+1, j+2 may still be in flight
+    SHPL_RING_WAIT(WNDMA * (RING - 1));  // rows j+1, j+2 may still be in flight
     const uint8_t *xs = lb + U * WSLOT, *gs = xs + WX_PIECES * 16;
     bf16x8 g0[2];
     g0[0] = tr_frag<0>(gs);
@@ -660,7 +708,8 @@ __device__ __forceinline__ void wstep(const WgRowArgs &r, f32x16 (&acc)[9], bf16
 }
 
 template <bool CMP>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_wgrad_rows(const WgRowArgs r) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS_WPE, SHPL_ROWS_WPE))) void k_wgrad_rows(
+    const WgRowArgs r) {
     __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING * WSLOT];
     __shared__ uint64_t s_occ[CMP ? 64 : 1];  // pooled tile: the band rows' occupancy windows (as k_conv_rows)
     __shared__ int32_t s_first[CMP ? 64 : 1];

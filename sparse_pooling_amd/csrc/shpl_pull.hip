@@ -40,6 +40,7 @@ namespace {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+
 template <int BYTES>
 struct Raw;
 template <>

@@ -617,6 +617,7 @@ def _ragged_pipeline_run(cfg, sizes, dtype, paths):
     """FusedPipeline forward + backward over a ragged batch, once per CSR path
     (shpl_build_csr_path: frame / segment / range; None = the default), each compared
     with the oracle frame by frame (f32: bitwise; bf16: bitwise on the bf16 bits)."""
+    from sparse_pooling_amd import _lib as L
     from sparse_pooling_amd import pipeline
     base = synth.CONFIGS[cfg]
     frames = _ragged_frames(base, sizes, 500)
@@ -653,7 +654,8 @@ def _ragged_pipeline_run(cfg, sizes, dtype, paths):
         else:
             np.testing.assert_array_equal(_np(got.view(torch.int16)).view(np.uint16),
                                           orc.to_bf16_bits(exp.astype(np.float32)))
-    codes = {None: L.CSR_AUTO, "frame": L.CSR_FRAME, "segment": L.CSR_SEGMENT, "range": L.CSR_RANGE}
+    codes = {None: L.CSR_AUTO, "frame": L.CSR_FRAME, "segment": L.CSR_SEGMENT, "range": L.CSR_RANGE,
+             "bucket": L.CSR_BUCKET}
     for path in paths:
         pl = pipeline.FusedPipeline(B, maxp, N, base.im_size, base.bv_size, base.stride, Cb, Ci, dtype=tdt,
                                     dual=True)
@@ -678,14 +680,14 @@ def test_pipeline_ragged_batch_every_csr_path():
     -> dual layer -> both gradients) at config-2 shape: a frame without points,
     a one-point frame, a frame whose points all fall outside the image, frames
     straddling the index builder's chunks -- under each CSR builder (per-frame
-    workgroup, segments, destination ranges), bitwise against the oracle."""
-    _ragged_pipeline_run(2, [0, 1, -40, 1025, 20000, 2], "f32", ["frame", "segment", "range"])
+    workgroup, segments, destination ranges, range buckets), bitwise against the oracle."""
+    _ragged_pipeline_run(2, [0, 1, -40, 1025, 20000, 2], "f32", ["frame", "segment", "range", "bucket"])
 
 
 def test_pipeline_ragged_batch_row_keyed_bf16():
     """The same ragged batch at config-3 shape (bf16, 256 channels, row-keyed
     pulls over key_range CSRs), bitwise on the bf16 bits."""
-    _ragged_pipeline_run(3, [0, 1, -40, 1025, 20000, 2], "bf16", [None])
+    _ragged_pipeline_run(3, [0, 1, -40, 1025, 20000, 2], "bf16", [None, "range"])
 
 
 def test_bev_slices_vs_reference_golden():
