@@ -175,6 +175,21 @@ int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, const int64_t 
                     int32_t *d_voxel_indices, double *d_pts_in_voxel, int64_t *d_frame_nvox,
                     double *d_height_maps, double *d_density_map, uint32_t *d_err, void *d_ws,
                     size_t ws_bytes, void *stream);
+/* The height and density maps of the last shpl_bev_slices call that used the
+ * same workspace d_ws (and the same frames, points and geometry), from the
+ * sorted words it left there: a caller can run the voxelizer without maps
+ * (d_height_maps = d_density_map = NULL) where its outputs are on a critical
+ * path, and write the maps -- ~27 MB of f64 per frame, almost all zeros --
+ * later, on another stream (FramePipeline.velo_step: after the layer's
+ * streaming pass). zero != 0 first zero-fills both maps (shpl_bev_slices'
+ * maps arrive zero-filled; here the caller may have zeroed them itself).
+ * Same values as shpl_bev_slices' maps, bit for bit. */
+int shpl_bev_maps(int n_frames, const int64_t *d_point_offsets, int64_t total_points, const void *d_points,
+                  int points_dtype, const double *d_planes, const double *area_extents, double voxel_size,
+                  int num_slices, const double *slice_lo, const double *slice_hi, double density_lo,
+                  double density_hi, double height_per_division, const double *density_table,
+                  double *d_height_maps, double *d_density_map, int zero, const void *d_ws,
+                  size_t ws_bytes, void *stream);
 
 /* MV3D_TF's producer point_cloud_2_top_sparse
  * (MV3D_TF_release/lib/utils/construct_voxel.py:37-162), n_frames at once:

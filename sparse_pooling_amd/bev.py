@@ -45,9 +45,24 @@ def grid_divisions(area_extents, voxel_size):
 
 
 class BevBatch:
-    def __init__(self, voxel_indices, pts_in_voxel, frame_nvox, height_maps, density_map, err):
+    def __init__(self, voxel_indices, pts_in_voxel, frame_nvox, height_maps, density_map, err, call=None):
         self.voxel_indices, self.pts_in_voxel, self.frame_nvox = voxel_indices, pts_in_voxel, frame_nvox
         self.height_maps, self.density_map, self.err = height_maps, density_map, err
+        self._call = call  # the voxelizer call's arguments, for write_maps
+
+    def write_maps(self, height_maps, density_map, zero=True):
+        """The height / density maps of this batch (shpl_bev_maps) into the given [F,S,nz,nx] /
+        [F,nz,nx] f64 tensors, on the current stream, from the sorted words the voxelizer left in its
+        workspace (the workspace must not be reused in between): bitwise the maps bev_slices_batch
+        writes with maps=True."""
+        c = self._call
+        L.check(L.lib().shpl_bev_maps(c["F"], L.ptr(c["off"]), c["N"], L.ptr(c["pts"]), L.F64, L.ptr(c["planes"]),
+                                      c["p"](c["ext"]), c["vs"], c["S"], c["p"](c["lo"]), c["p"](c["hi"]), c["hlo"],
+                                      c["hhi"], c["hpd"], c["p"](c["table"]), L.ptr(height_maps),
+                                      L.ptr(density_map), int(bool(zero)), L.ptr(c["ws"]), c["ws"].numel(),
+                                      L.stream_of(c["pts"].device)), "shpl_bev_maps")
+        self.height_maps, self.density_map = height_maps, density_map
+        return height_maps, density_map
 
 
 def bev_slices_batch(points, point_offsets, planes, area_extents, voxel_size, height_lo, height_hi,
@@ -87,7 +102,10 @@ def bev_slices_batch(points, point_offsets, planes, area_extents, voxel_size, he
                                     float(height_hi), float(hpd), p(table), L.ptr(vox), L.ptr(upts), L.ptr(nvox),
                                     L.ptr(hm), L.ptr(dm), L.ptr(err), L.ptr(ws), ws.numel(),
                                     L.stream_of(dev)), "shpl_bev_slices")
-    return BevBatch(vox, upts, nvox, hm, dm, err)
+    call = dict(F=F, off=point_offsets, N=N, pts=points, planes=planes, p=p, ext=ext, vs=float(voxel_size),
+                S=int(num_slices), lo=lo_a, hi=hi_a, hlo=float(height_lo), hhi=float(height_hi), hpd=float(hpd),
+                table=table, ws=ws)
+    return BevBatch(vox, upts, nvox, hm, dm, err, call)
 
 
 class BevSlices:

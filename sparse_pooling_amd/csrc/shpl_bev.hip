@@ -95,7 +95,7 @@ __global__ __launch_bounds__(BEV_BLOCK) void k_bev_frame(BevGeom g, const int64_
                                                          const double *planes, uint64_t *tmp, uint64_t *srt,
                                                          int64_t ent_per_point, int32_t *vox_out, double *pts_out,
                                                          int64_t *frame_nvox, double *hmaps, double *dmap,
-                                                         uint32_t *err) {
+                                                         int32_t *frame_nent, uint32_t *err) {
     __shared__ TileSortLds lds;
     const int f = blockIdx.x;
     const int64_t p0 = pt_off[f], cap_end = pt_off[f + 1];
@@ -174,40 +174,65 @@ __global__ __launch_bounds__(BEV_BLOCK) void k_bev_frame(BevGeom g, const int64_
         kept += tot;
         __syncthreads();
     }
-    if (threadIdx.x == 0) frame_nvox[f] = kept < cap ? kept : cap;
+    if (threadIdx.x == 0) {
+        frame_nvox[f] = kept < cap ? kept : cap;
+        frame_nent[f] = n_ent;  // the sorted words stay in the workspace for shpl_bev_maps
+    }
 }
 
-}  // namespace
-}  // namespace shpl
+// The height and density maps from the sorted words a k_bev_frame launch left in the workspace
+// (shpl_bev_maps): the same values step 5 above writes, by a grid of BEV_MAP_SPLIT workgroups per
+// frame over its words -- a cell's first word writes its height (slices) or count-derived density.
+constexpr int BEV_MAP_SPLIT = 16;
+template <typename PT>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_bev_maps(BevGeom g, const int64_t *pt_off, const void *pts,
+                                                        const double *planes, const uint64_t *srt,
+                                                        int64_t ent_per_point, const int32_t *frame_nent,
+                                                        double *hmaps, double *dmap) {
+    const int f = blockIdx.y;
+    const int64_t p0 = pt_off[f], t0 = p0 * ent_per_point;
+    const int32_t n_ent = frame_nent[f];
+    const int64_t n_cells = (int64_t)g.nx * g.nz;
+    const double *plane = planes + 4 * f;
+    const double a = plane[0], b = plane[1], c = plane[2], d = plane[3];
+    const double norm = sqrt(__dadd_rn(__dadd_rn(__dmul_rn(a, a), __dmul_rn(b, b)), __dmul_rn(c, c)));
+    for (int32_t s = blockIdx.x * SHPL_BLOCK + threadIdx.x; s < n_ent; s += BEV_MAP_SPLIT * SHPL_BLOCK) {
+        const uint64_t me = srt[t0 + s];
+        const uint64_t key = me >> KEY_SHIFT;
+        if (s > 0 && (srt[t0 + s - 1] >> KEY_SHIFT) == key) continue;  // not the cell's first word
+        const int v = (int)((int64_t)key / n_cells);
+        const int64_t cell = (int64_t)key - (int64_t)v * n_cells;
+        const int xi = (int)(cell / g.nz), zi = (int)(cell - (int64_t)xi * g.nz);
+        const int64_t pix = (int64_t)(g.nz - 1 - zi) * g.nx + xi;  // np.flip(map.T, axis=0)
+        if (v < g.num_slices) {
+            if (!hmaps) continue;
+            double x, y, z;
+            Pt<PT>::load(pts, p0 + (int64_t)(uint32_t)me, x, y, z);
+            const double dist =
+                __ddiv_rn(__dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(a, x), __dmul_rn(b, y)), __dmul_rn(c, z)), d), norm);
+            hmaps[((int64_t)f * g.num_slices + v) * n_cells + pix] = __ddiv_rn(__dsub_rn(dist, g.lo[v]), g.hpd);
+        } else if (dmap) {
+            int32_t n = 1;
+            while (s + n < n_ent && (srt[t0 + s + n] >> KEY_SHIFT) == key) ++n;
+            dmap[(int64_t)f * n_cells + pix] = n < 16 ? g.dens[n] : 1.0;
+        }
+    }
+}
 
-using namespace shpl;
+constexpr int BEV_MAX_FRAMES = 4096;  // frames of one call (the per-frame word counts in the workspace)
 
-extern "C" int shpl_bev_workspace_bytes(int64_t total_points, int num_slices, size_t *bytes) {
-    if (!bytes || total_points < 0 || num_slices < 1 || num_slices > BEV_MAX_SLICES) return SHPL_ERR_ARG;
+size_t bev_half_bytes(int64_t total_points, int num_slices) {
     const size_t n = (size_t)(total_points > 0 ? total_points : 1) * (size_t)(num_slices + 1);
-    *bytes = 2 * align_up(n * sizeof(uint64_t), 256);
-    return SHPL_OK;
+    return align_up(n * sizeof(uint64_t), 256);
 }
 
-extern "C" int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, const int64_t *d_point_counts,
-                               int64_t total_points,
-                               const void *d_points, int points_dtype, const double *d_planes,
-                               const double *area_extents, double voxel_size, int num_slices,
-                               const double *slice_lo, const double *slice_hi, double density_lo,
-                               double density_hi, double height_per_division, const double *density_table,
-                               int32_t *d_voxel_indices, double *d_pts_in_voxel, int64_t *d_frame_nvox,
-                               double *d_height_maps, double *d_density_map, uint32_t *d_err, void *d_ws,
-                               size_t ws_bytes, void *stream) {
-    if (n_frames < 1 || !d_point_offsets || !d_planes || !area_extents || !slice_lo || !slice_hi ||
-        !density_table || !d_frame_nvox || !d_ws)
-        return SHPL_ERR_ARG;
+// BevGeom of the call's host arguments (SHPL_OK or a status).
+int bev_geom(const double *area_extents, double voxel_size, int num_slices, const double *slice_lo,
+             const double *slice_hi, double density_lo, double density_hi, double height_per_division,
+             const double *density_table, BevGeom &g) {
+    if (!area_extents || !slice_lo || !slice_hi || !density_table) return SHPL_ERR_ARG;
     if (num_slices < 1 || num_slices > BEV_MAX_SLICES || !(voxel_size > 0)) return SHPL_ERR_BAD_SHAPE;
-    if (total_points > 0 && (!d_points || !d_voxel_indices || !d_pts_in_voxel)) return SHPL_ERR_ARG;
-    if (total_points >= ((int64_t)1 << 31)) return SHPL_ERR_BAD_SHAPE;
-    size_t need;
-    shpl_bev_workspace_bytes(total_points, num_slices, &need);
-    if (need > ws_bytes) return SHPL_ERR_WORKSPACE;
-    BevGeom g{};
+    g = BevGeom{};
     for (int i = 0; i < 3; ++i) {
         g.ext[i][0] = area_extents[2 * i];
         g.ext[i][1] = area_extents[2 * i + 1];
@@ -234,9 +259,46 @@ extern "C" int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, con
     if (n_keys >= ((int64_t)1 << 22)) return SHPL_ERR_BAD_SHAPE;  // key field of the packed word
     g.log_tile = 0;
     while (((n_keys - 1) >> g.log_tile) + 1 > BEV_TILES) ++g.log_tile;
-    const size_t half = need / 2;
+    return SHPL_OK;
+}
+
+}  // namespace
+}  // namespace shpl
+
+using namespace shpl;
+
+extern "C" int shpl_bev_workspace_bytes(int64_t total_points, int num_slices, size_t *bytes) {
+    if (!bytes || total_points < 0 || num_slices < 1 || num_slices > BEV_MAX_SLICES) return SHPL_ERR_ARG;
+    *bytes = 2 * bev_half_bytes(total_points, num_slices) + align_up(sizeof(int32_t) * BEV_MAX_FRAMES, 256);
+    return SHPL_OK;
+}
+
+extern "C" int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, const int64_t *d_point_counts,
+                               int64_t total_points,
+                               const void *d_points, int points_dtype, const double *d_planes,
+                               const double *area_extents, double voxel_size, int num_slices,
+                               const double *slice_lo, const double *slice_hi, double density_lo,
+                               double density_hi, double height_per_division, const double *density_table,
+                               int32_t *d_voxel_indices, double *d_pts_in_voxel, int64_t *d_frame_nvox,
+                               double *d_height_maps, double *d_density_map, uint32_t *d_err, void *d_ws,
+                               size_t ws_bytes, void *stream) {
+    if (n_frames < 1 || !d_point_offsets || !d_planes || !area_extents || !slice_lo || !slice_hi ||
+        !density_table || !d_frame_nvox || !d_ws)
+        return SHPL_ERR_ARG;
+    if (num_slices < 1 || num_slices > BEV_MAX_SLICES || !(voxel_size > 0)) return SHPL_ERR_BAD_SHAPE;
+    if (total_points > 0 && (!d_points || !d_voxel_indices || !d_pts_in_voxel)) return SHPL_ERR_ARG;
+    if (total_points >= ((int64_t)1 << 31) || n_frames > BEV_MAX_FRAMES) return SHPL_ERR_BAD_SHAPE;
+    size_t need;
+    shpl_bev_workspace_bytes(total_points, num_slices, &need);
+    if (need > ws_bytes) return SHPL_ERR_WORKSPACE;
+    BevGeom g;
+    const int rc = bev_geom(area_extents, voxel_size, num_slices, slice_lo, slice_hi, density_lo, density_hi,
+                            height_per_division, density_table, g);
+    if (rc) return rc;
+    const size_t half = bev_half_bytes(total_points, num_slices);
     uint64_t *tmp = (uint64_t *)d_ws;
     uint64_t *srt = (uint64_t *)((char *)d_ws + half);
+    int32_t *nent = (int32_t *)((char *)d_ws + 2 * half);
     hipStream_t s = (hipStream_t)stream;
     const int64_t per_map = (int64_t)g.nx * g.nz;
     // the maps' zeros: a streaming kernel (hipMemsetAsync's fill ran at ~2.2 TB/s, beside k_dense)
@@ -247,9 +309,42 @@ extern "C" int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, con
         hipLaunchKernelGGL(k_bev_frame<double>, dim3(n_frames), dim3(BEV_BLOCK), 0, s, g, d_point_offsets,
                            d_point_counts, d_points,
                            d_planes, tmp, srt, (int64_t)(num_slices + 1), d_voxel_indices, d_pts_in_voxel,
-                           d_frame_nvox, d_height_maps, d_density_map, d_err);
+                           d_frame_nvox, d_height_maps, d_density_map, nent, d_err);
     else
         return SHPL_ERR_ARG;
+    SHPL_LAUNCH_CHECK();
+    return SHPL_OK;
+}
+
+extern "C" int shpl_bev_maps(int n_frames, const int64_t *d_point_offsets, int64_t total_points, const void *d_points,
+                             int points_dtype, const double *d_planes, const double *area_extents, double voxel_size,
+                             int num_slices, const double *slice_lo, const double *slice_hi, double density_lo,
+                             double density_hi, double height_per_division, const double *density_table,
+                             double *d_height_maps, double *d_density_map, int zero, const void *d_ws,
+                             size_t ws_bytes, void *stream) {
+    if (n_frames < 1 || !d_point_offsets || !d_planes || !d_ws) return SHPL_ERR_ARG;
+    if (points_dtype != SHPL_F64 || (total_points > 0 && !d_points)) return SHPL_ERR_ARG;
+    if (total_points < 0 || total_points >= ((int64_t)1 << 31) || n_frames > BEV_MAX_FRAMES) return SHPL_ERR_BAD_SHAPE;
+    BevGeom g;
+    const int rc = bev_geom(area_extents, voxel_size, num_slices, slice_lo, slice_hi, density_lo, density_hi,
+                            height_per_division, density_table, g);
+    if (rc) return rc;
+    size_t need;
+    shpl_bev_workspace_bytes(total_points, num_slices, &need);
+    if (need > ws_bytes) return SHPL_ERR_WORKSPACE;
+    const size_t half = bev_half_bytes(total_points, num_slices);
+    const uint64_t *srt = (const uint64_t *)((const char *)d_ws + half);
+    const int32_t *nent = (const int32_t *)((const char *)d_ws + 2 * half);
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t per_map = (int64_t)g.nx * g.nz;
+    if (zero) {
+        if (d_height_maps)
+            SHPL_HIP_CHECK(zero_fill(d_height_maps, sizeof(double) * (size_t)(per_map * num_slices * n_frames), s));
+        if (d_density_map) SHPL_HIP_CHECK(zero_fill(d_density_map, sizeof(double) * (size_t)(per_map * n_frames), s));
+    }
+    if (!d_height_maps && !d_density_map) return SHPL_OK;
+    hipLaunchKernelGGL(k_bev_maps<double>, dim3(BEV_MAP_SPLIT, n_frames), dim3(SHPL_BLOCK), 0, s, g, d_point_offsets,
+                       d_points, d_planes, srt, (int64_t)(num_slices + 1), nent, d_height_maps, d_density_map);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
 }

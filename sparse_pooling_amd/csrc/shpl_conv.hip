@@ -473,7 +473,8 @@ __global__ __launch_bounds__(CONV_BLOCK, NCB == 2 ? 3 : 4) void k_conv3x3(const 
     __shared__ __attribute__((aligned(16))) uint8_t s_buf[IN_BYTES + W_BYTES];
     uint8_t *const s_in = s_buf, *const s_w = s_buf + IN_BYTES;
     __shared__ float s_red[4][2][NCO];
-    __shared__ __attribute__((aligned(16))) float s_par[NCB][3][NCO];  // center, scale, shift of the block's channels
+    __shared__ __attribute__((aligned(16))) float s_par[NCB][2][NCO];  // scale, shift - center * scale of the block's channels
+    const bool affine = p.center || p.scale || p.shift;
     SHPL_HALO_RUNS_LDS(POOLED, HHT)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -488,10 +489,16 @@ __global__ __launch_bounds__(CONV_BLOCK, NCB == 2 ? 3 : 4) void k_conv3x3(const 
     const int64_t frame_row0 = (int64_t)f * H * W;
     const int Q = p.qa + p.qb;
 
-    if (tid < 3 * NCO * NCB) {
-        const int cb = tid / (3 * NCO), k = (tid >> 5) % 3, c = (cob0 + cb) * NCO + (tid & 31);
-        const float *src = k == 0 ? p.center : k == 1 ? p.scale : p.shift;
-        s_par[cb][k][tid & 31] = src && c < p.c_out ? src[c] : 0.0f;
+    // epilogue coefficients, as k_conv_rows: scale (1 when absent) and shift - center * scale, applied
+    // as one fma -- the two kernels give the same bits for the same call
+    if (tid < NCO * NCB) {
+        const int cb = tid / NCO, c = (cob0 + cb) * NCO + (tid & 31);
+        const bool in = c < p.c_out;
+        const float sc = p.scale && in ? p.scale[c] : 1.0f;
+        const float ce = p.center && in ? p.center[c] : 0.0f;
+        const float sh = p.shift && in ? p.shift[c] : 0.0f;
+        s_par[cb][0][tid & 31] = sc;
+        s_par[cb][1][tid & 31] = __fsub_rn(sh, __fmul_rn(ce, sc));
     }
     const int n_run = POOLED ? find_runs<HHT>(p, f, y0, x0, runs) : 0;  // (s_par: published by the next barrier)
 
@@ -596,9 +603,8 @@ __global__ __launch_bounds__(CONV_BLOCK, NCB == 2 ? 3 : 4) void k_conv3x3(const 
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const int cl = 8 * g + 4 * hf, c = cob * NCO + cl;  // first channel of the run
-                const f32x4 cen = *reinterpret_cast<const f32x4 *>(&s_par[cb][0][cl]);
-                const f32x4 scl = *reinterpret_cast<const f32x4 *>(&s_par[cb][1][cl]);
-                const f32x4 sft = *reinterpret_cast<const f32x4 *>(&s_par[cb][2][cl]);
+                const f32x4 scl = *reinterpret_cast<const f32x4 *>(&s_par[cb][0][cl]);
+                const f32x4 sft = *reinterpret_cast<const f32x4 *>(&s_par[cb][1][cl]);
                 T o[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -607,10 +613,8 @@ __global__ __launch_bounds__(CONV_BLOCK, NCB == 2 ? 3 : 4) void k_conv3x3(const 
                         s1[4 * g + j] = __fadd_rn(s1[4 * g + j], v);
                         s2[4 * g + j] = __fadd_rn(s2[4 * g + j], __fmul_rn(v, v));
                     }
-                    if (p.center) v = __fsub_rn(v, cen[j]);
-                    if (p.scale) v = __fmul_rn(v, scl[j]);
-                    if (p.shift) v = __fadd_rn(v, sft[j]);
-                    if (p.act == 1) v = v > 0.0f ? v : 0.0f;
+                    if (affine) v = __builtin_fmaf(v, scl[j], sft[j]);
+                    if (p.act == 1) v = __builtin_fmaxf(v, 0.0f);
                     o[j] = E::back(v);
                 }
                 if (fast) {

@@ -335,11 +335,22 @@ class FramePipeline(FusedPipeline):
         self.bev = None
         self._velo_ws = None
 
-    def build_bev(self, points, point_offsets, planes, point_counts=None):
+    def build_bev(self, points, point_offsets, planes, point_counts=None, maps=None):
         from . import bev as _bev
-        self.bev = _bev.bev_slices_batch(points, point_offsets, planes, *self.bev_args, maps=self.maps,
-                                         ws=self.bev_ws, point_counts=point_counts)
+        self.bev = _bev.bev_slices_batch(points, point_offsets, planes, *self.bev_args,
+                                         maps=self.maps if maps is None else maps, ws=self.bev_ws,
+                                         point_counts=point_counts)
         return self.bev
+
+    def _map_buffers(self):
+        """The step's height / density maps, allocated once (velo_step writes them off the chain)."""
+        if getattr(self, "_maps", None) is None:
+            from . import bev as _bev
+            area, vs, _, _, S = self.bev_args
+            nx, nz = _bev.grid_divisions(area, vs)
+            f64 = dict(dtype=torch.float64, device=self.dev)
+            self._maps = (torch.empty((self.B, int(S), nz, nx), **f64), torch.empty((self.B, nz, nx), **f64))
+        return self._maps
 
     def frame_step(self, points, point_offsets, planes, P, bev_feat, img_feat, point_counts=None):
         b = self.build_bev(points, point_offsets, planes, point_counts)
@@ -354,12 +365,17 @@ class FramePipeline(FusedPipeline):
         the index chain. events: 9 timing events (dense start/end on `side`; then
         velo, bev, index, csr boundaries, sparse start/end on the current stream)."""
         if side is not None:
+            # the 1.7 GB of f64 maps (64 frames) are written on `side` after the streaming pass, from the
+            # voxelizer's sorted words (shpl_bev_maps): off the index chain, and streaming after the
+            # stream instead of beside it
             main = torch.cuda.current_stream(self.dev)
             side.wait_stream(main)
+            dense_done, bev_done = torch.cuda.Event(), torch.cuda.Event()
             with torch.cuda.stream(side):
                 if events:
                     events[0].record(side)
                 self.layer_dense(bev_feat, img_feat)
+                dense_done.record(side)
                 if events:
                     events[1].record(side)
             if events:
@@ -367,7 +383,13 @@ class FramePipeline(FusedPipeline):
             self._velo(frames)
             if events:
                 events[3].record(main)
-            b = self.build_bev(self.velo.points, frames.point_offsets, frames.planes, self.velo.counts)
+            b = self.build_bev(self.velo.points, frames.point_offsets, frames.planes, self.velo.counts,
+                               maps=False)
+            bev_done.record(main)
+            if self.maps:
+                side.wait_event(bev_done)
+                with torch.cuda.stream(side):
+                    b.write_maps(*self._map_buffers(), zero=True)
             if events:
                 events[4].record(main)
             self.build_index(b.pts_in_voxel, b.voxel_indices, frames.point_offsets, frames.P2,
@@ -377,12 +399,13 @@ class FramePipeline(FusedPipeline):
             self.build_csr()
             if events:
                 events[6].record(main)
-            main.wait_stream(side)
+            main.wait_event(dense_done)  # the sparse pass overwrites rows the streaming pass wrote
             if events:
                 events[7].record(main)
             self.layer_sparse(bev_feat, img_feat)
             if events:
                 events[8].record(main)
+            main.wait_stream(side)  # the maps
             return
         self._velo(frames)
         self.frame_step(self.velo.points, frames.point_offsets, frames.planes, frames.P2, bev_feat, img_feat,

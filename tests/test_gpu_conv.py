@@ -311,6 +311,37 @@ def test_bf16_rows_conv_dense(shape):
         np.testing.assert_array_equal(_np(y2.float()), _np(y.float()))
 
 
+@pytest.mark.parametrize("relu", [True, False])
+def test_bf16_rows_epilogue_equals_tiled(relu):
+    """The same bf16 conv through k_conv_rows (16-byte aligned output) and the tiled
+    k_conv3x3 (an output view 2 bytes off 16-byte alignment): bitwise the same with
+    center, scale and shift all set (fma(acc, scale, shift - center * scale), then
+    fmax(., 0)), a NaN input pixel included (ReLU of NaN is 0 in both). The two
+    kernels sum the MFMA products in different orders, so inputs and weights are
+    small integers: every accumulator is exact in f32 and only the epilogue can
+    differ."""
+    from sparse_pooling_amd import fusion_conv as fc
+    B, H, W, Cin, Cout = 2, 16, 40, 32, 32
+    rng = np.random.default_rng(53)
+    x = rng.integers(-3, 4, (B, H, W, Cin)).astype(np.float32)
+    x[1, 7, 9, 3] = np.nan
+    w = rng.integers(-2, 3, (3, 3, Cin, Cout)).astype(np.float32)
+    center = rng.standard_normal(Cout).astype(np.float32)
+    scale = rng.uniform(0.5, 2.0, Cout).astype(np.float32)
+    shift = rng.standard_normal(Cout).astype(np.float32)
+    n = B * H * W * Cout
+    flat = torch.empty(n + 16, dtype=torch.bfloat16, device=DEV)
+    outs = []
+    for off in (0, 1):  # 0: 16-byte aligned (row kernel), 1: 2 bytes off (tiled kernel)
+        o = flat[off:off + n].view(B, H, W, Cout)
+        fc.conv3x3(_bf16(x), _bf16(w), center=_t(center), scale=_t(scale), shift=_t(shift), relu=relu, out=o)
+        torch.cuda.synchronize()
+        outs.append(_np(o.view(torch.int16)).copy())
+    np.testing.assert_array_equal(outs[0], outs[1])
+    if relu:
+        assert not np.isnan(orc.from_bf16_bits(outs[0].view(np.uint16))).any()
+
+
 STATS_SHAPES = [  # bf16 training forward on k_conv_rows: statistics epilogue (dense sources)
     (2, 16, 64, 64, 32),   # two sources of 32 (the training workload's Q = 4, QA = 2)
     (3, 17, 70, 24, 64),   # partial strip (masked pixels), two output blocks

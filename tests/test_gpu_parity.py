@@ -943,6 +943,32 @@ def test_velodyne_to_fused_layer_pipeline(kitti_dir):
         _close_and_exact(iout[f:f + 1], ei)
 
 
+def test_velodyne_pipeline_overlapped_maps_equal_sequential(kitti_dir):
+    """velo_step with a side stream (the streaming pass beside the index chain, the BEV maps written
+    after it by shpl_bev_maps from the voxelizer's sorted words) == the sequential step (maps written
+    by shpl_bev_slices itself), bitwise: layer outputs, height and density maps."""
+    from sparse_pooling_amd import kitti, pipeline
+    d, g = kitti_dir
+    shapes = [tuple(g["7_image_shape"]), tuple(g["8_image_shape"])]
+    fr = kitti.KittiFrames.from_dirs(os.path.join(d, "calib"), os.path.join(d, "velodyne"), os.path.join(d, "planes"),
+                                     [7, 8], shapes, flips=[False, True])
+    im_size, stride, C = (1242, 375), (4, 4), 8
+    outs = []
+    for side in (None, torch.cuda.Stream()):
+        pl = pipeline.FramePipeline(2, fr.total_points, im_size, synth.AREA_EXTENTS, synth.VOXEL_SIZE,
+                                    synth.HEIGHT_LO, synth.HEIGHT_HI, synth.NUM_SLICES, stride, C, C, dual=True,
+                                    max_points_per_frame=fr.max_points)
+        bev = torch.from_numpy(synth.make_features((2, pl.Hb, pl.Wb, C), 3)).to(DEV)
+        img = torch.from_numpy(synth.make_features((2, pl.Hi, pl.Wi, C), 4)).to(DEV)
+        for _ in range(2):  # the second step reuses every workspace
+            pl.velo_step(fr, bev, img, side=side)
+        torch.cuda.synchronize()
+        assert int(pl.err.item()) == 0 and int(pl.bev.err.item()) == 0
+        outs.append([_np(t).copy() for t in (pl.bv_fused, pl.img_fused, pl.bev.height_maps, pl.bev.density_map)])
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
 @pytest.mark.parametrize("cfg,dtype,counts", [
     (1, "f32", (1.0, 0.0, 0.5)), (3, "bf16", (0.3, 1.0, 0.0, 0.7)), (1, "f32", (0.0, 0.0)), (1, "bf16", (0.2,))])
 def test_sparse_live_entries_equal_capacity_walk(cfg, dtype, counts):
