@@ -97,6 +97,9 @@ def parse():
                     help="conv workload: training step (batch-statistics BatchNorm forward + the whole backward: "
                          "BN/ReLU, input and weight gradients of the conv, the pooled channels' gradient to the image)")
     ap.add_argument("--scan-points", type=int, default=120000, help="points per velodyne scan (frames)")
+    ap.add_argument("--maps-after", default="stream", choices=["stream", "chain"],
+                    help="frames: write the BEV maps after the streaming pass (side stream) or after the CSR "
+                         "(index chain)")
     return ap.parse_args()
 
 
@@ -631,6 +634,7 @@ def run_frames(args, world, rank, dev):
     pl = pipeline.FramePipeline(F, fr.total_points, im_size, synth.AREA_EXTENTS, synth.VOXEL_SIZE,
                                 synth.HEIGHT_LO, synth.HEIGHT_HI, synth.NUM_SLICES, (1, 1), C, C, device=dev,
                                 max_points_per_frame=fr.max_points)
+    pl.maps_after = args.maps_after
     bev = sd.fill_features(torch.empty((F, pl.Hb, pl.Wb, C), device=dev), fids, 5)
     img = sd.fill_features(torch.empty((F, pl.Hi, pl.Wi, C), device=dev), fids, 6)
     side = torch.cuda.Stream(device=dev)

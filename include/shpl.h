@@ -315,8 +315,11 @@ int shpl_build_csr(int direction, int order, int n_frames, const int64_t *d_fram
  * SHPL_CSR_BUCKET the range builder over stable per-range buckets (three
  * launches: chunk histograms, stable bucketing, one sort per bucket; entry
  * order only -- identity columns or SHPL_ORDER_ENTRY -- else the range
- * builder). A key_range CSR always takes a range builder (bucket when it
- * applies). Same arguments and errors as shpl_build_csr otherwise. */
+ * builder); linear in every run length, where the range builder's in-run
+ * rank is quadratic in a run's length (a frame with all its points on one
+ * cell), but three launches instead of one (slower at config 3). A key_range
+ * CSR always takes a range builder (the bucket one only on request). Same
+ * arguments and errors as shpl_build_csr otherwise. */
 #define SHPL_CSR_AUTO 0
 #define SHPL_CSR_FRAME 1
 #define SHPL_CSR_SEGMENT 2

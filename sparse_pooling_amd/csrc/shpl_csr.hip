@@ -803,7 +803,7 @@ __global__ __launch_bounds__(CSR_BLOCK) void k_csr_range(CsrIn c, uint64_t *tmp,
 constexpr int BKT_CHUNK = 1024;        // entries per count / place workgroup (one per thread)
 constexpr int BKT_MAX_RANGES = 512;    // ranges per frame: 65536 destinations of RANGE_KEYS
 constexpr int BKT_MAX_FRAMES = 1024;   // frames of one build (one per thread of the chunk prefix)
-constexpr int BKT_SORT = 256;          // threads of a sort workgroup
+constexpr int BKT_SORT = 512;          // threads of a sort workgroup
 constexpr int BKT_RBITS = 9;           // range bits matched by the place multisplit (BKT_MAX_RANGES)
 static_assert(RANGE_KEYS == 128, "the sort multisplit matches 7 destination bits");
 
@@ -901,17 +901,36 @@ __global__ __launch_bounds__(BKT_CHUNK) void k_bkt_place(CsrIn c, BktIn k) {
     frame_range(c, f, e0, e1, cap_end);
     const int nc = s_pre[f + 1] - s_pre[f], nr = k.n_ranges;
     const int wid = threadIdx.x >> 6;
-    // 1. each range's entries in the frame's earlier chunks and in all of them
-    for (int q = threadIdx.x; q < nr; q += BKT_CHUNK) {
-        const int32_t *col = k.counts + (int64_t)s_pre[f] * nr + q;
+    // 1. each range's entries in the frame's earlier chunks and in all of them: np = BKT_CHUNK / nr
+    //    threads per range, each summing every np-th chunk (their loads in flight together), partial
+    //    sums combined in LDS (s_w doubles as the table)
+    {
+        const int np = BKT_CHUNK / nr, part = threadIdx.x / nr, q = threadIdx.x - part * nr;
         int32_t tot = 0, bef = 0;
-        for (int jj = 0; jj < nc; ++jj) {
-            const int32_t v = col[(int64_t)jj * nr];
-            tot += v;
-            bef += jj < j ? v : 0;
+        if (part < np) {
+            const int32_t *col = k.counts + (int64_t)s_pre[f] * nr + q;
+            for (int jj = part; jj < nc; jj += np) {
+                const int32_t v = col[(int64_t)jj * nr];
+                tot += v;
+                bef += jj < j ? v : 0;
+            }
         }
-        s_tot[q] = tot;
-        s_off[q] = bef;
+        int32_t *pt = &s_w[0][0], *pb = pt + BKT_CHUNK;  // [np][nr] partial totals / partial befores
+        if (part < np) {
+            pt[part * nr + q] = tot;
+            pb[part * nr + q] = bef;
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < nr) {
+            int32_t t = 0, b = 0;
+            for (int i = 0; i < np; ++i) {
+                t += pt[i * nr + threadIdx.x];
+                b += pb[i * nr + threadIdx.x];
+            }
+            s_tot[threadIdx.x] = t;
+            s_off[threadIdx.x] = b;
+        }
+        __syncthreads();
     }
     for (int i = threadIdx.x; i < (BKT_CHUNK / 64) * nr; i += BKT_CHUNK) s_w[i / nr][i % nr] = 0;
     __syncthreads();
@@ -1171,11 +1190,13 @@ extern "C" int shpl_build_csr_path(int path, int direction, int order, int n_fra
                         (small_cap && (path != SHPL_CSR_AUTO
                                            ? (path == SHPL_CSR_RANGE || path == SHPL_CSR_BUCKET)
                                            : (n_frames < SEG_FRAMES && keys_per_frame <= RANGE_MAX_KEYS)));
-    // the bucket form when the order inside a destination is entry order (it keeps the bucket's) and
-    // its tables fit; SHPL_CSR_RANGE forces k_csr_range
+    // the bucket form on request (SHPL_CSR_BUCKET), when the order inside a destination is entry order
+    // (it keeps the bucket's) and its tables fit. Linear in every run length, where k_csr_range ranks an
+    // entry among its destination's (quadratic in a run), but slower at config 3 (three launches per key:
+    // step 0.132-0.134 ms against 0.123-0.125 with k_csr_range), so not the default.
     const int64_t n_ranges_b = (keys_per_frame + RANGE_KEYS - 1) / RANGE_KEYS;
     const int64_t n_chunks_b = nnz_cap / BKT_CHUNK + n_frames + 1;
-    const bool bucket = ranged && path != SHPL_CSR_RANGE && (d_col == nullptr || order == SHPL_ORDER_ENTRY) &&
+    const bool bucket = ranged && path == SHPL_CSR_BUCKET && (d_col == nullptr || order == SHPL_ORDER_ENTRY) &&
                         n_frames <= BKT_MAX_FRAMES && n_ranges_b <= BKT_MAX_RANGES &&
                         n_chunks_b * n_ranges_b + 2 * (int64_t)n_frames * n_ranges_b <= lay.bkt_ints &&
                         ws_bytes >= lay.total && n_chunks_b < 0x7fffffffLL;

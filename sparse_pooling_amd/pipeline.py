@@ -335,6 +335,10 @@ class FramePipeline(FusedPipeline):
         self.bev = None
         self._velo_ws = None
 
+    # velo_step with a side stream: where the BEV maps are written (shpl_bev_maps) -- "stream": on the
+    # side stream after the layer's streaming pass; "chain": on the index chain after the CSR
+    maps_after = "stream"
+
     def build_bev(self, points, point_offsets, planes, point_counts=None, maps=None):
         from . import bev as _bev
         self.bev = _bev.bev_slices_batch(points, point_offsets, planes, *self.bev_args,
@@ -386,7 +390,7 @@ class FramePipeline(FusedPipeline):
             b = self.build_bev(self.velo.points, frames.point_offsets, frames.planes, self.velo.counts,
                                maps=False)
             bev_done.record(main)
-            if self.maps:
+            if self.maps and self.maps_after == "stream":
                 side.wait_event(bev_done)
                 with torch.cuda.stream(side):
                     b.write_maps(*self._map_buffers(), zero=True)
@@ -399,6 +403,8 @@ class FramePipeline(FusedPipeline):
             self.build_csr()
             if events:
                 events[6].record(main)
+            if self.maps and self.maps_after == "chain":
+                b.write_maps(*self._map_buffers(), zero=True)
             main.wait_event(dense_done)  # the sparse pass overwrites rows the streaming pass wrote
             if events:
                 events[7].record(main)

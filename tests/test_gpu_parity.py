@@ -386,7 +386,8 @@ def test_empty_map_pulls_every_form(rows_mode):
 def test_range_csr_one_long_run(n):
     """Every entry of a frame on ONE destination (all points on one cell and one
     pixel): the range CSR's degenerate case (one run longer than its LDS list at
-    n = 20000), row-keyed pulls in both directions against the oracle, bitwise."""
+    n = 20000), row-keyed pulls in both directions against the oracle, bitwise;
+    the bucket builder (linear in the run) gives the same cell-keyed entry list."""
     from sparse_pooling_amd import _lib as L
     from sparse_pooling_amd import shpl_map as sm
     rng = np.random.default_rng(5)
@@ -411,6 +412,17 @@ def test_range_csr_one_long_run(n):
     _close_and_exact(_np(pool), orc.sparse_pool_op(mij, mval, [R, n], img, idx).reshape(R, c))
     _close_and_exact(_np(trans), orc.sparse_pool_trans_op(mij, mval, [R, n], bev.reshape(-1, c), idx,
                                                           img.shape).reshape(h * w, c))
+    lists = []
+    for path in (L.CSR_RANGE, L.CSR_BUCKET):
+        cs = L.Csr(smap.n_cells, smap.nnz_cap, DEV, with_col=False, key_range=True)
+        L.check(L.lib().shpl_build_csr_path(path, L.BY_CELL, L.ORDER_ENTRY, 1, L.ptr(smap.frame_off),
+                                            L.ptr(smap.frame_nnz), smap.n_cells, L.ptr(smap.cell), L.ptr(smap.col),
+                                            L.ptr(smap.val), L.ptr(smap.pix), cs.ref(), L.ptr(cs.ws), cs.ws.numel(),
+                                            L.stream_of(torch.device(DEV))), "shpl_build_csr_path")
+        torch.cuda.synchronize()
+        lists.append([_np(t).copy() for t in (cs.ent_dst, cs.ent_src, cs.ent_val, cs.key_range)])
+    for a, b in zip(*lists):
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
 def test_bf16_storage_fp32_accumulate():
