@@ -97,7 +97,7 @@ def parse():
                     help="conv workload: training step (batch-statistics BatchNorm forward + the whole backward: "
                          "BN/ReLU, input and weight gradients of the conv, the pooled channels' gradient to the image)")
     ap.add_argument("--scan-points", type=int, default=120000, help="points per velodyne scan (frames)")
-    ap.add_argument("--maps-after", default="stream", choices=["stream", "chain"],
+    ap.add_argument("--maps-after", default="chain", choices=["stream", "chain"],
                     help="frames: write the BEV maps after the streaming pass (side stream) or after the CSR "
                          "(index chain)")
     return ap.parse_args()

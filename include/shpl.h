@@ -379,9 +379,15 @@ int shpl_pull_sparse(int direction, int dtype, const shpl_csr *csr, const void *
 
 typedef enum { SHPL_ACT_NONE = 0, SHPL_ACT_RELU = 1 } shpl_act;
 
-/* out[f,y,x,co] = act((sum_{ky,kx,ci} in[f, y+ky-1, x+kx-1, ci] * W[ky,kx,ci,co]
- *                      - center[co]) * scale[co] + shift[co])
- * SAME padding (zeros outside the map), stride 1, n_frames frames of h x w
+/* out[f,y,x,co] = act(round(fma(acc, scale[co], shift[co] - center[co]*scale[co])))
+ *   acc = sum_{ky,kx,ci} in[f, y+ky-1, x+kx-1, ci] * W[ky,kx,ci,co]
+ * i.e. (acc - center) * scale + shift with one fused rounding (the per-channel
+ * shift - center*scale rounded once in f32); round = to the storage dtype;
+ * act RELU = max(bits, 0) on the stored value's bit pattern as a signed
+ * integer (negatives, -0 and -NaN -> +0, +NaN stays NaN). Every kernel behind
+ * this call (row-streaming or tiled) applies exactly this epilogue, so the
+ * same call gives the same bits whichever runs, up to the accumulation order
+ * of acc (the kernels sum the MFMA products in different orders). SAME padding (zeros outside the map), stride 1, n_frames frames of h x w
  * pixels, NHWC rows of global id (f*h + y)*w + x. Input channels
  * [0, c_a) are row r of d_a (element r*a_stride + a_off + c), channels
  * [c_a, c_a + c_b) come from d_b:

@@ -14,7 +14,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run 
   python3 bench.py --config 3 --steps 20 --warmup 2 --no-cpu-baseline --no-graph > gpurun_out/prof_c3.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fr -o run --output-format csv -- \
   python3 bench.py --workload frames --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/prof_fr.log 2>&1 || exit 1
-for v in epi8 epi8r4 epi8drain; do
+for v in epi8; do
   SHPL_LIB=$PWD/sparse_pooling_amd/variants/$v.so timeout -k 10 400 python -u -m pytest tests/test_gpu_conv.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -k rows > gpurun_out/$v.log 2>&1
   echo "$v rows tests rc=$?"; tail -2 gpurun_out/$v.log
 done

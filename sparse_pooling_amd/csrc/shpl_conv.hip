@@ -72,6 +72,16 @@ struct Elem {
     }
 };
 
+// ReLU of a stored value as max(bits, 0) on its bit pattern as a signed integer of its width: negatives,
+// -0 and -NaN become +0, +NaN stays -- k_conv_rows' packed 16-bit max, so both kernels give the same bits.
+__device__ __forceinline__ float relu_bits(float v, bool on) {
+    const int32_t b = __float_as_int(v);
+    return on ? __int_as_float(b > 0 ? b : 0) : v;
+}
+__device__ __forceinline__ uint16_t relu_bits(uint16_t v, bool on) {
+    return on ? ((int16_t)v > 0 ? v : (uint16_t)0) : v;
+}
+
 struct ConvArgs {
     int n_frames, h, w;
     int tiles_x, tiles_per_frame, n_tiles;
@@ -474,7 +484,6 @@ __global__ __launch_bounds__(CONV_BLOCK, NCB == 2 ? 3 : 4) void k_conv3x3(const 
     uint8_t *const s_in = s_buf, *const s_w = s_buf + IN_BYTES;
     __shared__ float s_red[4][2][NCO];
     __shared__ __attribute__((aligned(16))) float s_par[NCB][2][NCO];  // scale, shift - center * scale of the block's channels
-    const bool affine = p.center || p.scale || p.shift;
     SHPL_HALO_RUNS_LDS(POOLED, HHT)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -613,9 +622,7 @@ __global__ __launch_bounds__(CONV_BLOCK, NCB == 2 ? 3 : 4) void k_conv3x3(const 
                         s1[4 * g + j] = __fadd_rn(s1[4 * g + j], v);
                         s2[4 * g + j] = __fadd_rn(s2[4 * g + j], __fmul_rn(v, v));
                     }
-                    if (affine) v = __builtin_fmaf(v, scl[j], sft[j]);
-                    if (p.act == 1) v = __builtin_fmaxf(v, 0.0f);
-                    o[j] = E::back(v);
+                    o[j] = relu_bits(E::back(__builtin_fmaf(v, scl[j], sft[j])), p.act == 1);
                 }
                 if (fast) {
                     __builtin_memcpy(s_o + pl * OPITCH + cl * sizeof(T), o, sizeof(o));

@@ -364,7 +364,6 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
     } else {
         const int pl = lane & 31, hf = lane >> 5;
         const bool row_ok = b >= 0 && b < n_out;
-        const bool affine = r.scale || r.center || r.shift;
         uint16_t *orow = obase + (frame_row0 + (int64_t)(ya + b) * r.w + x0) * ostr;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the MFMAs' operand reads of the slot are done
 #if SHPL_ROWS_EPI8
@@ -377,16 +376,16 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
             uint32_t pk[2];
     #pragma unroll
             for (int k = 0; k < 4; k += 2) {
-                float v0 = a2[4 * g + k], v1 = a2[4 * g + k + 1];
-                if (affine) {
-                    v0 = __builtin_fmaf(v0, s_par[0][cl + k], s_par[1][cl + k]);
-                    v1 = __builtin_fmaf(v1, s_par[0][cl + k + 1], s_par[1][cl + k + 1]);
-                }
+                const float v0 = __builtin_fmaf(a2[4 * g + k], s_par[0][cl + k], s_par[1][cl + k]);
+                const float v1 = __builtin_fmaf(a2[4 * g + k + 1], s_par[0][cl + k + 1], s_par[1][cl + k + 1]);
+                uint32_t w = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
                 if (RELU) {
-                    v0 = __builtin_fmaxf(v0, 0.0f);
-                    v1 = __builtin_fmaxf(v1, 0.0f);
+                    s16x2 h;
+                    __builtin_memcpy(&h, &w, 4);
+                    h = __builtin_elementwise_max(h, s16x2{0, 0});
+                    __builtin_memcpy(&w, &h, 4);
                 }
-                pk[k >> 1] = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
+                pk[k >> 1] = w;
             }
             uint16_t *dst = row_ok && x0 + pl < r.w ? orow + pl * (int)ostr + cl : r.junk + lane * 16 + 4 * g;
             __builtin_memcpy(dst, pk, sizeof(pk));
@@ -398,18 +397,19 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
             uint32_t pk[2];
     #pragma unroll
             for (int k = 0; k < 4; k += 2) {
-                // the tiled kernel's epilogue, operation for operation (same bits for the same call):
-                // fma(acc, scale, shift - center * scale) when any coefficient is given, then fmax(., 0)
-                float v0 = a2[4 * g + k], v1 = a2[4 * g + k + 1];
-                if (affine) {
-                    v0 = __builtin_fmaf(v0, s_par[0][cl + k], s_par[1][cl + k]);
-                    v1 = __builtin_fmaf(v1, s_par[0][cl + k + 1], s_par[1][cl + k + 1]);
-                }
+                // fma(acc, scale, shift - center * scale) (scale 1 / shift 0 when absent), rounded to bf16,
+                // ReLU as max(bits, 0) on the bf16 bit patterns as signed 16-bit integers (negatives, -0
+                // and -NaN -> +0, +NaN kept): the tiled kernel's epilogue, bit for bit (shpl.h)
+                const float v0 = __builtin_fmaf(a2[4 * g + k], s_par[0][cl + k], s_par[1][cl + k]);
+                const float v1 = __builtin_fmaf(a2[4 * g + k + 1], s_par[0][cl + k + 1], s_par[1][cl + k + 1]);
+                uint32_t w = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
                 if (RELU) {
-                    v0 = __builtin_fmaxf(v0, 0.0f);
-                    v1 = __builtin_fmaxf(v1, 0.0f);
+                    s16x2 h;
+                    __builtin_memcpy(&h, &w, 4);
+                    h = __builtin_elementwise_max(h, s16x2{0, 0});
+                    __builtin_memcpy(&w, &h, 4);
                 }
-                pk[k >> 1] = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
+                pk[k >> 1] = w;
             }
             __builtin_memcpy(s_o + pl * REPI + cl * 2, pk, sizeof(pk));
         }

@@ -335,9 +335,10 @@ class FramePipeline(FusedPipeline):
         self.bev = None
         self._velo_ws = None
 
-    # velo_step with a side stream: where the BEV maps are written (shpl_bev_maps) -- "stream": on the
-    # side stream after the layer's streaming pass; "chain": on the index chain after the CSR
-    maps_after = "stream"
+    # velo_step with a side stream: where the BEV maps are written (shpl_bev_maps) -- "chain": on the
+    # index chain after the CSR, beside the end of the streaming pass (step 2.66-2.67 ms); "stream": on the
+    # side stream after the streaming pass (2.68-2.69 ms; profiles/r03_frames_maps_ab.log)
+    maps_after = "chain"
 
     def build_bev(self, points, point_offsets, planes, point_counts=None, maps=None):
         from . import bev as _bev

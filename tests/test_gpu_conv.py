@@ -315,8 +315,8 @@ def test_bf16_rows_conv_dense(shape):
 def test_bf16_rows_epilogue_equals_tiled(relu):
     """The same bf16 conv through k_conv_rows (16-byte aligned output) and the tiled
     k_conv3x3 (an output view 2 bytes off 16-byte alignment): bitwise the same with
-    center, scale and shift all set (fma(acc, scale, shift - center * scale), then
-    fmax(., 0)), a NaN input pixel included (ReLU of NaN is 0 in both). The two
+    center, scale and shift all set (fma(acc, scale, shift - center * scale), rounded,
+    then ReLU as an integer max on the bf16 bits), a NaN input pixel included. The two
     kernels sum the MFMA products in different orders, so inputs and weights are
     small integers: every accumulator is exact in f32 and only the epilogue can
     differ."""
@@ -338,8 +338,8 @@ def test_bf16_rows_epilogue_equals_tiled(relu):
         torch.cuda.synchronize()
         outs.append(_np(o.view(torch.int16)).copy())
     np.testing.assert_array_equal(outs[0], outs[1])
-    if relu:
-        assert not np.isnan(orc.from_bf16_bits(outs[0].view(np.uint16))).any()
+    if not relu:  # the NaN pixel reached the outputs (the MFMA's NaN is negative: ReLU makes it +0)
+        assert np.isnan(orc.from_bf16_bits(outs[0].view(np.uint16))).any()
 
 
 STATS_SHAPES = [  # bf16 training forward on k_conv_rows: statistics epilogue (dense sources)
