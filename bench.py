@@ -84,6 +84,9 @@ def parse():
                     help="dual configs: start both sparse passes after both dense passes (A/B of the overlap)")
     ap.add_argument("--csr-path", default="auto", choices=["auto", "frame", "segment", "range", "bucket"],
                     help="layer workloads: force the CSR builder (shpl_build_csr_path; A/B measurements)")
+    ap.add_argument("--no-buckets", action="store_true",
+                    help="row-keyed layers (config 3): range CSRs + one k_rows launch per pull on two streams "
+                         "instead of the index build's buckets + one shpl_pull_buckets launch per pull pair")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step eagerly instead of replaying one captured HIP graph of it")
     ap.add_argument("--workload", default="layer", choices=["layer", "frames", "conv"],
@@ -381,7 +384,8 @@ def main():
     frames = [synth.make_frame(spec, seed=s, n_outside=200) for s in fids]
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, dev)
     pl = pipeline.FusedPipeline(F, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev,
-                                spec.c_img, dtype=dtype, dual=dual, device=dev)
+                                spec.c_img, dtype=dtype, dual=dual, device=dev,
+                                buckets=False if args.no_buckets else None)
     Hb, Wb = spec.bev_feat_hw
     Hi, Wi = spec.img_feat_hw
     feats = lambda shape, seed: sd.fill_features(torch.empty(shape, dtype=dtype, device=dev), fids, seed)  # noqa
@@ -556,7 +560,10 @@ def main():
                           ("SHPL layer pulls: k_dense (concat stream) + k_sparse (pooled gather); achieved over "
                            + ("the layer's window (first k_dense start to last k_sparse end: the cell-keyed gathers "
                               "run beside img_fused's stream)" if interleaved else "their summed durations")
-                           + ("; step pulls are row-keyed k_rows (one launch per pull), timed as the sparse and "
+                           + ("; each pull pair is ONE shpl_pull_buckets launch over the index build's "
+                              "destination buckets (one stream), timed as the sparse and backward brackets"
+                              if pl.buckets else
+                              "; step pulls are row-keyed k_rows (one launch per pull), timed as the sparse and "
                               "backward brackets" if pl.rows else "")),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,

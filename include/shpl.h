@@ -374,6 +374,70 @@ int shpl_pull_sparse(int direction, int dtype, const shpl_csr *csr, const void *
                      int64_t out_stride, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * Bucketed pulls: the index build hands the pulls M already cut by
+ * destination (small batches, one stream, no CSR launch)
+ * ------------------------------------------------------------------------- */
+
+/* shpl_build_index, and in the same two launches the destination buckets of
+ * both keys in d_bkt: per key (BEV cell, image pixel) every frame's
+ * destinations are cut into ranges of 128, and each (frame, range) bucket
+ * lists the frame's entries of that range in entry order -- TF's accumulation
+ * order inside every destination, for both directions (the builder's columns
+ * are the identity: SHPL_ORDER_ENTRY == SHPL_ORDER_COL_ROW). The count launch
+ * adds per-chunk range histograms, the placement launch a stable multisplit.
+ * No d_mij / d_flip outputs; nnz_cap = the point capacity (d_cell's length).
+ * Limits (SHPL_ERR_BAD_SHAPE otherwise): at most 65536 cells and 65536 pixels
+ * per frame, max_points_per_frame below 2^24.
+ * Replaces what shpl_build_index + two shpl_build_csr calls feed the pulls
+ * (kitti_dataset.py:374-379, then rpn_model.py:330-331's SparseTensor). */
+int shpl_bucket_workspace_bytes(int n_frames, int64_t max_points_per_frame, int64_t nnz_cap,
+                                int64_t cells_per_frame, int64_t pix_per_frame, size_t *bytes);
+int shpl_build_index_buckets(int n_frames, const int64_t *d_point_offsets, const int64_t *d_point_counts,
+                             int64_t max_points_per_frame, const void *d_points, int points_dtype,
+                             const void *d_voxels, int voxels_itype, int64_t vox_stride, const double *d_P,
+                             double im_w, double im_h, double bv_h, double bv_w, double s_img, double s_bv,
+                             const float *d_mval, int32_t *d_cell, int32_t *d_pix, float *d_val,
+                             int64_t *d_frame_nnz, int64_t *d_frame_out_off, uint32_t *d_err, void *d_ws,
+                             size_t ws_bytes, int64_t nnz_cap, void *d_bkt, size_t bkt_bytes, void *stream);
+
+/* The map shpl_build_index_buckets left: its frame layout, index arrays and
+ * bucket workspace (the same sizes as that call). */
+typedef struct {
+    int n_frames;
+    int64_t max_points_per_frame, nnz_cap;
+    int64_t cells_per_frame, pix_per_frame;
+    const int64_t *frame_off, *frame_nnz; /* [n_frames + 1], [n_frames] */
+    const int32_t *cell, *pix;            /* [nnz_cap] global rows, as shpl_build_index writes them */
+    const float *val;                     /* [nnz_cap] */
+    void *ws;                             /* the bucket workspace (also the pull's sort scratch) */
+    size_t ws_bytes;
+} shpl_buckets;
+
+/* One pull of shpl_pull_buckets: the arguments of shpl_pull after its csr. */
+typedef struct {
+    int dtype;
+    const void *src;
+    int64_t src_stride, src_off, c_pool;
+    const void *pass;
+    int64_t pass_stride, pass_off, c_pass;
+    int mode;
+    void *out;
+    int64_t out_stride;
+} shpl_pull_desc;
+
+/* The cell-keyed pull (by_cell: destination = BEV cell, sources = image
+ * pixels) and the pixel-keyed pull (by_pixel: destination = pixel, sources =
+ * BEV cells) over the buckets, in ONE launch (either may be NULL): a
+ * workgroup per (pull, frame, range part) reads its bucket, sorts its part's
+ * entries by destination in LDS, and writes its output rows as shpl_pull
+ * would -- same values, bit for bit, as shpl_pull over the CSRs
+ * shpl_build_csr makes of the same index arrays. Both pulls take one dtype.
+ * Replaces the forward pair (sparse_pool_utils.py:96-117 + the concats of
+ * :72, :87) or, with SHPL_OUT_ADD, its gradient pair. */
+int shpl_pull_buckets(const shpl_buckets *bk, const shpl_pull_desc *by_cell, const shpl_pull_desc *by_pixel,
+                      void *stream);
+
+/* ---------------------------------------------------------------------------
  * Post-fusion 3x3 convolution
  * ------------------------------------------------------------------------- */
 

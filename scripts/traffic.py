@@ -24,6 +24,28 @@ SHORT = (("k_conv_rows<4, 2, true", "k_conv_rows_pooled_bf16"), ("k_conv_rows<4,
          ("k_count", "k_count"))
 
 
+def stamp(*logs):
+    """Provenance of a PMC entry: the lib_sha256 the profiled bench run printed (the library it loaded),
+    the commit it was measured at (this tree's HEAD) and the pass logs it came from."""
+    sha = None
+    for name in logs:
+        f = os.path.join(ROOT, "gpurun_out", name)
+        if not os.path.exists(f):
+            continue
+        for line in open(f, errors="replace"):
+            if line.startswith("{") and '"lib_sha256"' in line:
+                sha = json.loads(line).get("lib_sha256") or sha
+    if sha is None:
+        sys.exit(f"traffic.py: no lib_sha256 in {logs}: the entry would not be bound to a library")
+    try:
+        import subprocess
+        commit = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
+                                text=True).stdout.strip() or None
+    except OSError:
+        commit = None
+    return {"lib_sha256": sha, "commit": commit, "pass_logs": list(logs)}
+
+
 def per_kernel(counter, pattern=None):
     pattern = pattern or f"pmc_{counter}"
     files = glob.glob(os.path.join(ROOT, "gpurun_out", pattern, "**", "*counter_collection.csv"), recursive=True)
@@ -60,6 +82,7 @@ def conv(key, dt):
     path = os.path.join(ROOT, "profiles", "traffic.json")
     tj = json.load(open(path)) if os.path.exists(path) else {}
     tj[key] = {"hbm_bytes_per_launch": sum(out[k]["fetch_bytes"] + out[k]["write_bytes"] for k in call if k in out),
+               **stamp(f"pmc_conv_{dt}_1.log", f"pmc_conv_{dt}_2.log"),
                "main_kernel": main_k, "mfma_busy_share": out[main_k]["mfma_busy_share"], "kernels": out,
                "note": (f"hbm_bytes_per_launch: the fused conv call ({' + '.join(call)}); FETCH_SIZE x2 (gfx950 "
                         "wide-read correction), KiB -> bytes; WRITE_SIZE exact (16 B/lane stores); mfma_busy_share "
@@ -87,7 +110,10 @@ def main(key):
     print(json.dumps(tj[key], indent=1))
 
 
-def step_traffic(key, tag, layer_kernels=("k_dense", "k_sparse", "k_sparse_long", "k_rows"), anchor="k_count"):
+LAYER = ("k_dense", "k_sparse", "k_sparse_long", "k_rows", "k_bpull")
+
+
+def step_traffic(key, tag, layer_kernels=LAYER, anchor="k_count"):
     """Per-step HBM bytes of the layer kernels of one bench workload from the
     scripts/r02_pmc.sh passes (gpurun_out/pmc_<tag>_FETCH_SIZE, _WRITE_SIZE):
     every launch's counters summed, divided by the steps profiled (the number of
@@ -122,10 +148,10 @@ def step_traffic(key, tag, layer_kernels=("k_dense", "k_sparse", "k_sparse_long"
     path = os.path.join(ROOT, "profiles", "traffic.json")
     tj = json.load(open(path)) if os.path.exists(path) else {}
     tj[key] = {"hbm_bytes_per_launch": layer, "step_bytes_all_kernels": total, "steps_profiled": steps,
-               "kernels": out,
+               **stamp(f"pmc_{tag}_FETCH_SIZE.log", f"pmc_{tag}_WRITE_SIZE.log"), "kernels": out,
                "note": ("layer = " + (" + ".join(layer_kernels) if layer_kernels else "every profiled kernel")
                         + " per step (every launch of the step summed); FETCH_SIZE x2 (gfx950 wide-read "
-                        "correction), KiB -> bytes; scripts/r02_pmc.sh")}
+                        "correction), KiB -> bytes; scripts/r03_pmc.sh")}
     json.dump(tj, open(path, "w"), indent=1)
     print(key, f"{layer / 1e9:.4f} GB per step", {k: round((v['fetch_bytes_per_step'] + v['write_bytes_per_step']) / 1e6, 2)
                                                    for k, v in out.items()})
@@ -135,8 +161,7 @@ if __name__ == "__main__":
     key = sys.argv[1] if len(sys.argv) > 1 else "config2_F64"
     if key == "step":  # traffic.py step KEY TAG [all] [ANCHOR]: per-step bytes of a bench workload's PMC passes
         every = len(sys.argv) > 4 and sys.argv[4] == "all"
-        step_traffic(sys.argv[2], sys.argv[3], None if every else ("k_dense", "k_sparse", "k_sparse_long", "k_rows"),
-                     sys.argv[5] if len(sys.argv) > 5 else "k_count")
+        step_traffic(sys.argv[2], sys.argv[3], None if every else LAYER, sys.argv[5] if len(sys.argv) > 5 else "k_count")
         sys.exit(0)
     if key.startswith("conv_"):
         conv(key, key.split("_")[1])

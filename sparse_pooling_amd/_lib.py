@@ -79,6 +79,30 @@ class Csr:
         return ctypes.byref(self.struct)
 
 
+class ShplBuckets(ctypes.Structure):
+    """struct shpl_buckets of include/shpl.h."""
+    _fields_ = [("n_frames", ctypes.c_int), ("max_points_per_frame", ctypes.c_int64), ("nnz_cap", ctypes.c_int64),
+                ("cells_per_frame", ctypes.c_int64), ("pix_per_frame", ctypes.c_int64),
+                ("frame_off", ctypes.c_void_p), ("frame_nnz", ctypes.c_void_p), ("cell", ctypes.c_void_p),
+                ("pix", ctypes.c_void_p), ("val", ctypes.c_void_p), ("ws", ctypes.c_void_p),
+                ("ws_bytes", ctypes.c_size_t)]
+
+
+class ShplPullDesc(ctypes.Structure):
+    """struct shpl_pull_desc of include/shpl.h: shpl_pull's arguments after its csr."""
+    _fields_ = [("dtype", ctypes.c_int), ("src", ctypes.c_void_p), ("src_stride", ctypes.c_int64),
+                ("src_off", ctypes.c_int64), ("c_pool", ctypes.c_int64), ("pass_", ctypes.c_void_p),
+                ("pass_stride", ctypes.c_int64), ("pass_off", ctypes.c_int64), ("c_pass", ctypes.c_int64),
+                ("mode", ctypes.c_int), ("out", ctypes.c_void_p), ("out_stride", ctypes.c_int64)]
+
+
+def pull_desc(dtype, src, src_stride, src_off, c_pool, pass_, pass_stride, pass_off, c_pass, mode, out, out_stride):
+    """A ShplPullDesc from tensors (the same argument order as shpl_pull after its csr)."""
+    p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    return ShplPullDesc(dtype, p(src), src_stride, src_off, c_pool, p(pass_), pass_stride, pass_off, c_pass, mode,
+                        p(out), out_stride)
+
+
 def _declare(lib):
     p, i32, i64, d, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double, ctypes.c_size_t
     psz = ctypes.POINTER(ctypes.c_size_t)
@@ -108,6 +132,11 @@ def _declare(lib):
                                  p]),
         "shpl_build_csr_path": (i32, [i32, i32, i32, i32, p, p, i64, p, p, p, p, ctypes.POINTER(ShplCsr), p,
                                       sz, p]),
+        "shpl_bucket_workspace_bytes": (i32, [i32, i64, i64, i64, i64, psz]),
+        "shpl_build_index_buckets": (i32, [i32, p, p, i64, p, i32, p, i32, i64, p, d, d, d, d, d, d, p,
+                                           p, p, p, p, p, p, p, sz, i64, p, sz, p]),
+        "shpl_pull_buckets": (i32, [ctypes.POINTER(ShplBuckets), ctypes.POINTER(ShplPullDesc),
+                                    ctypes.POINTER(ShplPullDesc), p]),
         "shpl_pull": (i32, pull_args),
         "shpl_pull_dense": (i32, pull_args),
         "shpl_pull_sparse": (i32, pull_args),
@@ -190,3 +219,10 @@ def dtype_code(t):
     if t.dtype == torch.bfloat16:
         return BF16
     raise TypeError(f"SHPL features must be float32 or bfloat16, got {t.dtype}")
+
+
+def bucket_ws_bytes(n_frames, max_points, nnz_cap, cells_per_frame, pix_per_frame):
+    out = ctypes.c_size_t()
+    check(lib().shpl_bucket_workspace_bytes(int(n_frames), int(max_points), int(nnz_cap), int(cells_per_frame),
+                                            int(pix_per_frame), ctypes.byref(out)), "shpl_bucket_workspace_bytes")
+    return out.value

@@ -113,14 +113,75 @@ __device__ __forceinline__ void project(const double *P, double x, double y, dou
     v = __ddiv_rn(r1, r2);
 }
 
+// Workgroup bid of n -> logical block, so that each XCD (blocks dealt round
+// robin: bid, bid + 8, ... share one; MI355X_MICROARCH.md §Workgroup dispatch)
+// gets one contiguous run of logical blocks and its L2 sees one stretch of the
+// data. A bijection on [0, n) for any n (the first n % 8 XCDs get one more).
+// Speed only: nothing depends on the placement.
+__device__ __forceinline__ int64_t xcd_block(int64_t bid, int64_t n) {
+    const int64_t q = n >> 3, r = n & 7, xcd = bid & 7, i = bid >> 3;
+    return xcd < r ? xcd * (q + 1) + i : r * (q + 1) + (xcd - r) * q + i;
+}
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// ---------------------------------------------------------------- buckets
+// Destination buckets of the index builder's entries (shpl_build_index_buckets
+// -> shpl_pull_buckets): per key (0 = BEV cells, 1 = image pixels) a frame's
+// destinations are cut into ranges of BK_KEYS; bucket (key, frame, range)
+// lists the frame's entries of that range in entry order -- TF's order inside
+// every destination -- as 32-bit words (local destination << 24 | entry slot
+// - frame start). Workspace, in this order (host-computed, both calls agree):
+//   hist  [2][F][n_chunks][nrmax] i32  entries per (index chunk, range)
+//   ext   [2][F][nrmax][2]        i32  bucket (start from the frame's first slot, entries)
+//   words [2][nnz_cap]            u32  the buckets, frame f's at [off[f], off[f] + nnz_f)
+//   swords / ssrc / sval [2][nnz_cap]  scratch of the pull's sort when a
+//                                      workgroup's entries overflow its LDS
+constexpr int BK_KEYS = 128;        // destinations per range
+constexpr int BK_MAX_RANGES = 512;  // ranges per frame (65536 destinations)
+constexpr int BK_RBITS = 9;         // range bits matched by the placement's multisplit
+
+struct BkLayout {
+    int n_frames, n_chunks, nr[2], nrmax;
+    int64_t nnz_cap, kpf[2];
+    size_t hist, ext, words, swords, ssrc, sval, bytes;  // byte offsets into the workspace, total
+};
+
+inline BkLayout bk_layout(int n_frames, int n_chunks, int64_t nnz_cap, int64_t cells_per_frame,
+                          int64_t pix_per_frame) {
+    BkLayout l = {};
+    l.n_frames = n_frames;
+    l.n_chunks = n_chunks;
+    l.nnz_cap = nnz_cap;
+    l.kpf[0] = cells_per_frame;
+    l.kpf[1] = pix_per_frame;
+    for (int k = 0; k < 2; ++k) l.nr[k] = (int)((l.kpf[k] + BK_KEYS - 1) / BK_KEYS);
+    l.nrmax = l.nr[0] > l.nr[1] ? l.nr[0] : l.nr[1];
+    if (l.nrmax < 1) l.nrmax = 1;
+    const size_t F = (size_t)n_frames, cap = (size_t)(nnz_cap > 0 ? nnz_cap : 1);
+    size_t o = 0;
+    l.hist = o;
+    o = align_up(o + 4 * 2 * F * (size_t)n_chunks * (size_t)l.nrmax, 256);
+    l.ext = o;
+    o = align_up(o + 4 * 2 * F * (size_t)l.nrmax * 2, 256);
+    l.words = o;
+    o = align_up(o + 4 * 2 * cap, 256);
+    l.swords = o;
+    o = align_up(o + 4 * 2 * cap, 256);
+    l.ssrc = o;
+    o = align_up(o + 4 * 2 * cap, 256);
+    l.sval = o;
+    o = align_up(o + 4 * 2 * cap, 256);
+    l.bytes = o;
+    return l;
+}
+
 inline int grid_for(int64_t work, int64_t per_block, int cap) {
     int64_t g = (work + per_block - 1) / per_block;
     if (g < 1) g = 1;
     if (g > cap) g = cap;
     return (int)g;
 }
-
-inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 namespace {
 // Zeros at the streaming rate: one nontemporal 16-byte store per thread over

@@ -8,7 +8,7 @@
 //                the frame's last chunk the frame's count.
 // A Stage provides: In/Payload types, load(i, in), eval(ctx, f, i, in, pl) ->
 // flag mask, touch(f, i, pl, keep) (every point, write pass), emit(f, i, pos,
-// fstart, pl) and hole(pos).
+// fstart, pl), hole(pos) and HAS_BUCKETS (with bucket_keys, see Bkt).
 //
 // Column counts. numpy's np.dot over a frame's points evaluates a row product
 // in one order for two or more columns (dgemm) and in another for exactly one
@@ -50,6 +50,24 @@ struct Frames {
     uint32_t *err;
 };
 
+// Destination buckets of the kept entries (BKT instantiations; shpl_common.h
+// BkLayout): k_count adds per-chunk histograms over each key's destination
+// ranges, k_compact places every kept entry with valid destinations into its
+// (key, range) bucket, stably -- after the frame's earlier ranges and the
+// range's entries of earlier chunks, in chunk order inside the chunk.
+// A Stage with buckets provides bucket_keys(pl, kc, kp): the entry's
+// frame-local destinations (BEV cell, image pixel), false if either is invalid.
+// Frames of at most one entry get no bucket (the pull reads that entry from
+// the index arrays): only there may the second projection's column count
+// (dgemv order) differ from the count k_count assumed.
+struct Bkt {
+    int nr[2], nrmax;
+    int64_t nnz_cap;
+    int32_t *hist;    // [2][F][n_chunks][nrmax]
+    int32_t *ext;     // [2][F][nrmax][2]
+    uint32_t *words;  // [2][nnz_cap]
+};
+
 __device__ __forceinline__ void frame_range(const Frames &fr, int f, int64_t &p0, int64_t &p1, int64_t &cap_end) {
     p0 = fr.pt_off[f];
     cap_end = fr.pt_off[f + 1];
@@ -58,10 +76,14 @@ __device__ __forceinline__ void frame_range(const Frames &fr, int f, int64_t &p0
 }
 
 // Pass 1 (grid n_chunks x n_frames): KEEP_MULTI / KEEP_ONE / AUX points per chunk.
-template <typename Stage>
-__global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr) {
+template <typename Stage, bool BKT = false>
+__global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr, Bkt bk) {
     __shared__ int32_t wsum[3][IDX_BLOCK / 64];
+    __shared__ int32_t hist[BKT ? 2 * BK_MAX_RANGES : 1];
     const int f = blockIdx.y, j = blockIdx.x;
+    if constexpr (BKT) {
+        for (int q = threadIdx.x; q < 2 * BK_MAX_RANGES; q += IDX_BLOCK) hist[q] = 0;
+    }
     int64_t p0, p1, cap_end;
     frame_range(fr, f, p0, p1, cap_end);
     const int64_t base = p0 + (int64_t)j * IDX_CHUNK;
@@ -75,6 +97,7 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr) {
         if (i < p1) st.load(i, in[u]);
     }
     int32_t n[3] = {0, 0, 0};
+    if constexpr (BKT) __syncthreads();  // hist cleared
 #pragma unroll
     for (int u = 0; u < IDX_BATCH; ++u) {
         const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
@@ -82,6 +105,13 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr) {
         const uint32_t m = i < p1 ? st.eval(ctx, f, i, in[u], pl) : 0u;
 #pragma unroll
         for (int k = 0; k < 3; ++k) n[k] += (m >> k) & 1u;
+        if constexpr (BKT) {
+            int32_t kc, kp;
+            if ((m & KEEP_MULTI) && st.bucket_keys(pl, kc, kp)) {
+                atomicAdd(&hist[kc / BK_KEYS], 1);
+                atomicAdd(&hist[BK_MAX_RANGES + kp / BK_KEYS], 1);
+            }
+        }
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -95,6 +125,80 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr) {
         for (int w = 0; w < IDX_BLOCK / 64; ++w) t += wsum[threadIdx.x][w];
         fr.chunk_kept[((int64_t)threadIdx.x * fr.n_frames + f) * fr.n_chunks + j] = t;
     }
+    if constexpr (BKT) {
+        for (int i = threadIdx.x; i < 2 * bk.nrmax; i += IDX_BLOCK) {
+            const int K = i / bk.nrmax, q = i - K * bk.nrmax;
+            bk.hist[(((int64_t)K * fr.n_frames + f) * fr.n_chunks + j) * bk.nrmax + q] =
+                q < bk.nr[K] ? hist[K * BK_MAX_RANGES + q] : 0;
+        }
+    }
+}
+
+// k_compact's bucket placement (BKT), all threads: b_tot / b_bef = thread
+// (key bK, range bq)'s entries in the frame / in its earlier chunks; pos = this
+// point's entry slot in the frame when `keep`.
+template <typename Stage>
+__device__ __forceinline__ void bucket_place(const Stage &st, const Frames &fr, const Bkt &bk, int f, int j,
+                                             int64_t p0, int64_t total, bool keep,
+                                             const typename Stage::Payload &pl, int64_t pos, int32_t b_tot,
+                                             int32_t b_bef, int32_t *s_off, int32_t *s_scan,
+                                             int32_t (*s_w)[IDX_BLOCK / 64][BK_MAX_RANGES]) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int bK = threadIdx.x / BK_MAX_RANGES, bq = threadIdx.x % BK_MAX_RANGES;
+    // 1. each range's start in the frame: exclusive scan of the totals, per key
+    int32_t x = b_tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_scan[wid] = x;
+    __syncthreads();
+    int32_t start = x - b_tot;
+    const int w0 = bK * (BK_MAX_RANGES / 64);  // the key's first wave
+    for (int w = w0; w < wid; ++w) start += s_scan[w];
+    if (bq < bk.nr[bK]) {
+        s_off[threadIdx.x] = start + b_bef;
+        if (j == 0 && total >= 2) {
+            int32_t *x2 = bk.ext + (((int64_t)bK * fr.n_frames + f) * bk.nrmax + bq) * 2;
+            x2[0] = start;
+            x2[1] = b_tot;
+        }
+    }
+    // 2. stable multisplit of the chunk's entries by range, per key (wave ballots over the range bits)
+    int32_t kk[2] = {0, 0};
+    const bool ok = total >= 2 && keep && st.bucket_keys(pl, kk[0], kk[1]);
+    int32_t rank[2];
+#pragma unroll
+    for (int K = 0; K < 2; ++K) {
+        const int r = ok ? kk[K] / BK_KEYS : 0;
+        uint64_t peers = __ballot(ok);
+#pragma unroll
+        for (int bit = 0; bit < BK_RBITS; ++bit) {
+            const uint64_t bm = __ballot(ok && ((r >> bit) & 1));
+            peers &= ((r >> bit) & 1) ? bm : ~bm;
+        }
+        rank[K] = (int32_t)lane_rank(peers);
+        if (ok && rank[K] == 0) s_w[K][wid][r] = (int32_t)__popcll(peers);
+    }
+    __syncthreads();
+    if (bq < bk.nr[bK]) {  // waves' exclusive prefix per (key, range)
+        int32_t run = 0;
+#pragma unroll
+        for (int w = 0; w < IDX_BLOCK / 64; ++w) {
+            const int32_t v = s_w[bK][w][bq];
+            s_w[bK][w][bq] = run;
+            run += v;
+        }
+    }
+    __syncthreads();
+    if (!ok) return;
+#pragma unroll
+    for (int K = 0; K < 2; ++K) {
+        const int r = kk[K] / BK_KEYS;
+        const int64_t slot = p0 + s_off[K * BK_MAX_RANGES + r] + s_w[K][wid][r] + rank[K];
+        bk.words[(int64_t)K * bk.nnz_cap + slot] = ((uint32_t)(kk[K] % BK_KEYS) << 24) | (uint32_t)pos;
+    }
 }
 
 // Pass 2 (same grid): the chunk's kept points land after those of the
@@ -102,14 +206,33 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr) {
 // chunk are ranked in order by wave ballots + an LDS prefix. Each chunk also
 // writes the sentinels of the unused capacity that falls in its stretch of
 // slots, and the frame's last chunk the frame's entry count.
-template <typename Stage>
-__global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr) {
+template <typename Stage, bool BKT = false>
+__global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr, Bkt bk) {
+    static_assert(!BKT || IDX_BATCH == 1, "bucket placement ranks one point per thread");
     __shared__ int32_t wsum[IDX_BATCH][IDX_BLOCK / 64];
     __shared__ int32_t pre[IDX_BLOCK / 64], all[IDX_BLOCK / 64], naux[IDX_BLOCK / 64];
+    __shared__ int32_t s_off[BKT ? 2 * BK_MAX_RANGES : 1], s_scan[IDX_BLOCK / 64];
+    __shared__ int32_t s_w[BKT ? 2 : 1][IDX_BLOCK / 64][BKT ? BK_MAX_RANGES : 1];  // per-wave range counts
     const int f = blockIdx.y, j = blockIdx.x;
     int64_t p0, p1, cap_end;
     frame_range(fr, f, p0, p1, cap_end);
     const int wid = threadIdx.x >> 6;
+    // buckets: each (key, range) thread's entries in all of the frame's chunks and in the earlier ones
+    // (loads issued first, beside the point loads)
+    int32_t b_tot = 0, b_bef = 0;
+    const int bK = threadIdx.x / BK_MAX_RANGES, bq = threadIdx.x % BK_MAX_RANGES;
+    if constexpr (BKT) {
+        static_assert(IDX_BLOCK == 2 * BK_MAX_RANGES, "one thread per (key, range)");
+        if (bq < bk.nr[bK]) {
+            const int32_t *h = bk.hist + ((int64_t)bK * fr.n_frames + f) * fr.n_chunks * bk.nrmax + bq;
+            for (int jj = 0; jj < fr.n_chunks; ++jj) {
+                const int32_t v = h[(int64_t)jj * bk.nrmax];
+                b_tot += v;
+                b_bef += jj < j ? v : 0;
+            }
+        }
+        for (int i = threadIdx.x; i < 2 * (IDX_BLOCK / 64) * BK_MAX_RANGES; i += IDX_BLOCK) (&s_w[0][0][0])[i] = 0;
+    }
     // the frame's AUX count picks the KEEP count (and the stage's product order)
     const int32_t *aux_c = fr.chunk_kept + ((int64_t)2 * fr.n_frames + f) * fr.n_chunks;
     int32_t na = 0;
@@ -150,6 +273,7 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr) {
         if (i < p1) st.load(i, in[u]);
     }
     uint64_t m[IDX_BATCH];
+    int64_t b_pos = 0;  // BKT: this point's entry slot in the frame
 #pragma unroll
     for (int u = 0; u < IDX_BATCH; ++u) {
         const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
@@ -174,11 +298,14 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr) {
         }
         const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
         if (keep[u]) st.emit(f, i, p0 + kept + before + lane_rank(m[u]), p0, pl[u]);
+        if constexpr (BKT) b_pos = kept + before + lane_rank(m[u]);
         kept += tot;
     }
     // sentinels of the unused capacity [p0 + total, cap_end), each chunk its own stretch
     int64_t total = 0;
     for (int w = 0; w < IDX_BLOCK / 64; ++w) total += all[w];
+    if constexpr (BKT) bucket_place(st, fr, bk, f, j, p0, total, keep[0], pl[0], b_pos, b_tot, b_bef, s_off, s_scan,
+                                    s_w);
     const int64_t h0 = p0 + total > base ? p0 + total : base;
     const int64_t h1 = j == fr.n_chunks - 1 ? cap_end : (base + IDX_CHUNK < cap_end ? base + IDX_CHUNK : cap_end);
     for (int64_t pos = h0 + threadIdx.x; pos < h1; pos += IDX_BLOCK) st.hole(pos);
@@ -206,14 +333,25 @@ size_t index_ws_bytes(int n_frames, int64_t max_points) {
 template <typename Stage>
 int run_compaction(const Stage &st, int n_frames, int64_t max_points, const int64_t *pt_off,
                    const int64_t *pt_count, int64_t *frame_nnz, int64_t *frame_out_off, uint32_t *err, void *ws,
-                   size_t ws_bytes, hipStream_t stream) {
+                   size_t ws_bytes, hipStream_t stream, const Bkt *bk = nullptr) {
     if (ws_bytes < index_ws_bytes(n_frames, max_points)) return SHPL_ERR_WORKSPACE;
     Frames fr{pt_off, pt_count, n_frames, n_chunks_for(max_points),
               (int32_t *)((char *)ws + IDX_WS_HEAD), frame_nnz, frame_out_off, err};
     const dim3 grid(fr.n_chunks, n_frames);
-    hipLaunchKernelGGL(k_count<Stage>, grid, dim3(IDX_BLOCK), 0, stream, st, fr);
+    if constexpr (Stage::HAS_BUCKETS) {
+        if (bk) {
+            hipLaunchKernelGGL((k_count<Stage, true>), grid, dim3(IDX_BLOCK), 0, stream, st, fr, *bk);
+            SHPL_LAUNCH_CHECK();
+            hipLaunchKernelGGL((k_compact<Stage, true>), grid, dim3(IDX_BLOCK), 0, stream, st, fr, *bk);
+            SHPL_LAUNCH_CHECK();
+            return SHPL_OK;
+        }
+    } else {
+        if (bk) return SHPL_ERR_ARG;
+    }
+    hipLaunchKernelGGL((k_count<Stage, false>), grid, dim3(IDX_BLOCK), 0, stream, st, fr, Bkt{});
     SHPL_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_compact<Stage>, grid, dim3(IDX_BLOCK), 0, stream, st, fr);
+    hipLaunchKernelGGL((k_compact<Stage, false>), grid, dim3(IDX_BLOCK), 0, stream, st, fr, Bkt{});
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
 }

@@ -157,12 +157,9 @@ __device__ __forceinline__ void piece_to_lds(const T *row, int c, int c_src, boo
         *reinterpret_cast<u32x4 *>(wave_dst + lane * 16) = load_piece<T>(row, c, c_src, vec);
 }
 
-// blockIdx -> tile, so that each XCD (blocks b, b+8, ...) gets one contiguous
-// run of tiles: neighbouring tiles share halo rows through that XCD's L2.
-__device__ __forceinline__ int xcd_tile(int bid, int n) {
-    const int q = n >> 3, r = n & 7, xcd = bid & 7, i = bid >> 3;
-    return xcd < r ? xcd * (q + 1) + i : r * (q + 1) + (xcd - r) * q + i;
-}
+// blockIdx -> tile, so that each XCD gets one contiguous run of tiles:
+// neighbouring tiles share halo rows through that XCD's L2.
+__device__ __forceinline__ int xcd_tile(int bid, int n) { return (int)xcd_block(bid, n); }
 
 // Pooled vector of one occupied cell for the channels [c0, c0 + CK) of the
 // chunk: sum over the cell's run of CSR entries [e0, e1) of val * img[src],

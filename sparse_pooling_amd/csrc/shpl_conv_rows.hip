@@ -494,10 +494,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS_WP
     // takes one contiguous run of them, so the blocks of a strip read its rows together, and neighbouring
     // strips share their halo columns and neighbouring bands their halo rows, in that L2
 #if SHPL_ROWS_XCD
-    const int wi = [](int bid, int n) {
-        const int q = n >> 3, rr = n & 7, xcd = bid & 7, i = bid >> 3;
-        return xcd < rr ? xcd * (q + 1) + i : rr * (q + 1) + (xcd - rr) * q + i;
-    }(blockIdx.x, r.n_items * r.n_cob);
+    const int wi = (int)xcd_block(blockIdx.x, r.n_items * r.n_cob);
 #else
     const int wi = blockIdx.x;
 #endif
@@ -726,10 +723,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS_WP
     const int lane = threadIdx.x;
     const int n_tiles = r.n_cit * r.n_cot, total = r.n_groups * n_tiles;
     // (group, output tile, input tile), input tiles fastest (they share the G rows), each XCD one contiguous run
-    const int wi = [](int bid, int n) {
-        const int q = n >> 3, rr = n & 7, xcd = bid & 7, i = bid >> 3;
-        return xcd < rr ? xcd * (q + 1) + i : rr * (q + 1) + (xcd - rr) * q + i;
-    }(blockIdx.x, total);
+    const int wi = (int)xcd_block(blockIdx.x, total);
     const int cit = wi % r.n_cit, cot = (wi / r.n_cit) % r.n_cot, grp = wi / n_tiles;
     const int na = r.c_a / 32 + (r.c_a % 32 ? 1 : 0);  // input tiles of A (c_a % 32 == 0 when B is present)
     const bool from_a = cit < na;

@@ -95,6 +95,7 @@ __device__ __forceinline__ Produced produce(const Geometry &g, double ur, double
 
 template <typename PT, typename VT>
 struct FusedStage {
+    static constexpr bool HAS_BUCKETS = true;
     const void *pts;
     const void *vox;
     int64_t vstride;
@@ -155,10 +156,19 @@ struct FusedStage {
         pix[pos] = -1;
         val[pos] = 0.0f;
     }
+    // frame-local destinations of a kept entry (buckets): the cell and pixel emit() writes, unless -1
+    __device__ bool bucket_keys(const Payload &pl, int32_t &kc, int32_t &kp) const {
+        const int64_t r = pl.pr.r, vi = (int64_t)pl.pr.v, ui = (int64_t)pl.pr.u;
+        if (r < 0 || vi < 0 || ui < 0) return false;
+        kc = (int32_t)r;
+        kp = (int32_t)(vi * (int64_t)g.wq + ui);
+        return true;
+    }
 };
 
 template <typename PT, typename VT>
 struct GenStage {  // gen_sparse_pooling_input_avod
+    static constexpr bool HAS_BUCKETS = false;
     const void *pts;
     const void *vox;
     int64_t vstride;
@@ -195,6 +205,7 @@ struct GenStage {  // gen_sparse_pooling_input_avod
 
 template <typename VT>
 struct ProduceStage {  // produce_sparse_pooling_input (in-place img_index update)
+    static constexpr bool HAS_BUCKETS = false;
     const void *bv;
     int64_t bstride;
     double *img;  // 3 rows, stride ld
@@ -268,6 +279,41 @@ extern "C" int shpl_build_index_workspace_bytes(int n_frames, int64_t max_points
     return SHPL_OK;
 }
 
+// shpl_build_index, optionally with the destination buckets (bk != NULL)
+static int build_index(int n_frames, const int64_t *d_point_offsets, const int64_t *d_point_counts,
+                       int64_t max_points_per_frame, const void *d_points, int points_dtype, const void *d_voxels,
+                       int voxels_itype, int64_t vox_stride, const double *d_P, const Geometry &g,
+                       const float *d_mval, int32_t *d_cell, int32_t *d_pix, float *d_val, int64_t *d_mij,
+                       int64_t *d_flip, int64_t *d_frame_nnz, int64_t *d_frame_out_off, uint32_t *d_err, void *d_ws,
+                       size_t ws_bytes, hipStream_t s, const Bkt *bk) {
+#define SHPL_FUSED(PT, VT)                                                                       \
+    {                                                                                            \
+        FusedStage<PT, VT> st{d_points, d_voxels, vox_stride, d_P, g, d_mval, d_cell, d_pix,     \
+                              d_val, d_mij, d_flip, d_err};                                      \
+        return run_compaction(st, n_frames, max_points_per_frame, d_point_offsets, d_point_counts, d_frame_nnz, \
+                              d_frame_out_off, d_err, d_ws, ws_bytes, s, bk);                    \
+    }
+    if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I64) SHPL_FUSED(double, int64_t)
+    if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I32) SHPL_FUSED(double, int32_t)
+    if (points_dtype == SHPL_F32 && voxels_itype == SHPL_I64) SHPL_FUSED(float, int64_t)
+    if (points_dtype == SHPL_F32 && voxels_itype == SHPL_I32) SHPL_FUSED(float, int32_t)
+#undef SHPL_FUSED
+    return SHPL_ERR_ARG;
+}
+
+static int index_args(int n_frames, const int64_t *d_point_offsets, int64_t max_points_per_frame,
+                      const void *d_points, const void *d_voxels, int64_t vox_stride, const double *d_P,
+                      double s_img, double s_bv, const int32_t *d_cell, const int32_t *d_pix, const float *d_val,
+                      const void *d_ws, const Geometry &g) {
+    if (n_frames < 1 || !d_point_offsets || !d_P || !d_ws) return SHPL_ERR_ARG;
+    if (max_points_per_frame > 0 && (!d_points || !d_voxels || !d_cell || !d_pix || !d_val)) return SHPL_ERR_ARG;
+    if (vox_stride < 2 || !(s_img > 0) || !(s_bv > 0)) return SHPL_ERR_BAD_SHAPE;
+    if ((double)n_frames * (double)(g.n_cells > 0 ? g.n_cells : 0) >= 2147483647.0 ||
+        (double)n_frames * (double)(g.n_pix > 0 ? g.n_pix : 0) >= 2147483647.0)
+        return SHPL_ERR_BAD_SHAPE;
+    return SHPL_OK;
+}
+
 extern "C" int shpl_build_index(int n_frames, const int64_t *d_point_offsets, const int64_t *d_point_counts,
                                 int64_t max_points_per_frame,
                                 const void *d_points, int points_dtype, const void *d_voxels,
@@ -277,27 +323,53 @@ extern "C" int shpl_build_index(int n_frames, const int64_t *d_point_offsets, co
                                 int64_t *d_mij, int64_t *d_flip, int64_t *d_frame_nnz,
                                 int64_t *d_frame_out_off, uint32_t *d_err, void *d_ws, size_t ws_bytes,
                                 void *stream) {
-    if (n_frames < 1 || !d_point_offsets || !d_P || !d_ws) return SHPL_ERR_ARG;
-    if (max_points_per_frame > 0 && (!d_points || !d_voxels || !d_cell || !d_pix || !d_val)) return SHPL_ERR_ARG;
-    if (vox_stride < 2 || !(s_img > 0) || !(s_bv > 0)) return SHPL_ERR_BAD_SHAPE;
     const Geometry g = make_geometry(im_w, im_h, bv_h, bv_w, s_img, s_bv);
-    if ((double)n_frames * (double)(g.n_cells > 0 ? g.n_cells : 0) >= 2147483647.0 ||
-        (double)n_frames * (double)(g.n_pix > 0 ? g.n_pix : 0) >= 2147483647.0)
-        return SHPL_ERR_BAD_SHAPE;
-    hipStream_t s = (hipStream_t)stream;
-#define SHPL_FUSED(PT, VT)                                                                       \
-    {                                                                                            \
-        FusedStage<PT, VT> st{d_points, d_voxels, vox_stride, d_P, g, d_mval, d_cell, d_pix,     \
-                              d_val, d_mij, d_flip, d_err};                                      \
-        return run_compaction(st, n_frames, max_points_per_frame, d_point_offsets, d_point_counts, d_frame_nnz, \
-                              d_frame_out_off, d_err, d_ws, ws_bytes, s);                        \
-    }
-    if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I64) SHPL_FUSED(double, int64_t)
-    if (points_dtype == SHPL_F64 && voxels_itype == SHPL_I32) SHPL_FUSED(double, int32_t)
-    if (points_dtype == SHPL_F32 && voxels_itype == SHPL_I64) SHPL_FUSED(float, int64_t)
-    if (points_dtype == SHPL_F32 && voxels_itype == SHPL_I32) SHPL_FUSED(float, int32_t)
-#undef SHPL_FUSED
-    return SHPL_ERR_ARG;
+    const int rc = index_args(n_frames, d_point_offsets, max_points_per_frame, d_points, d_voxels, vox_stride, d_P,
+                              s_img, s_bv, d_cell, d_pix, d_val, d_ws, g);
+    if (rc) return rc;
+    return build_index(n_frames, d_point_offsets, d_point_counts, max_points_per_frame, d_points, points_dtype,
+                       d_voxels, voxels_itype, vox_stride, d_P, g, d_mval, d_cell, d_pix, d_val, d_mij, d_flip,
+                       d_frame_nnz, d_frame_out_off, d_err, d_ws, ws_bytes, (hipStream_t)stream, nullptr);
+}
+
+// bucket limits: 24-bit entry offsets, 512 ranges of BK_KEYS destinations per frame and key
+static bool bucket_shape_ok(int64_t max_points_per_frame, int64_t nnz_cap, int64_t cells, int64_t pix) {
+    return (int64_t)n_chunks_for(max_points_per_frame) * IDX_CHUNK <= ((int64_t)1 << 24) && nnz_cap >= 0 &&
+           nnz_cap < ((int64_t)1 << 31) && cells <= (int64_t)BK_KEYS * BK_MAX_RANGES &&
+           pix <= (int64_t)BK_KEYS * BK_MAX_RANGES;
+}
+
+extern "C" int shpl_bucket_workspace_bytes(int n_frames, int64_t max_points_per_frame, int64_t nnz_cap,
+                                           int64_t cells_per_frame, int64_t pix_per_frame, size_t *bytes) {
+    if (!bytes || n_frames < 1 || max_points_per_frame < 0 || cells_per_frame < 0 || pix_per_frame < 0)
+        return SHPL_ERR_ARG;
+    if (!bucket_shape_ok(max_points_per_frame, nnz_cap, cells_per_frame, pix_per_frame)) return SHPL_ERR_BAD_SHAPE;
+    *bytes = bk_layout(n_frames, n_chunks_for(max_points_per_frame), nnz_cap, cells_per_frame, pix_per_frame).bytes;
+    return SHPL_OK;
+}
+
+extern "C" int shpl_build_index_buckets(int n_frames, const int64_t *d_point_offsets, const int64_t *d_point_counts,
+                                        int64_t max_points_per_frame, const void *d_points, int points_dtype,
+                                        const void *d_voxels, int voxels_itype, int64_t vox_stride, const double *d_P,
+                                        double im_w, double im_h, double bv_h, double bv_w, double s_img,
+                                        double s_bv, const float *d_mval, int32_t *d_cell, int32_t *d_pix,
+                                        float *d_val, int64_t *d_frame_nnz, int64_t *d_frame_out_off,
+                                        uint32_t *d_err, void *d_ws, size_t ws_bytes, int64_t nnz_cap, void *d_bkt,
+                                        size_t bkt_bytes, void *stream) {
+    const Geometry g = make_geometry(im_w, im_h, bv_h, bv_w, s_img, s_bv);
+    int rc = index_args(n_frames, d_point_offsets, max_points_per_frame, d_points, d_voxels, vox_stride, d_P, s_img,
+                        s_bv, d_cell, d_pix, d_val, d_ws, g);
+    if (rc) return rc;
+    if (!d_bkt || !d_frame_nnz) return SHPL_ERR_ARG;
+    if (!bucket_shape_ok(max_points_per_frame, nnz_cap, g.n_cells, g.n_pix)) return SHPL_ERR_BAD_SHAPE;
+    const BkLayout l = bk_layout(n_frames, n_chunks_for(max_points_per_frame), nnz_cap, g.n_cells, g.n_pix);
+    if (bkt_bytes < l.bytes) return SHPL_ERR_WORKSPACE;
+    char *b = (char *)d_bkt;
+    const Bkt bk{{l.nr[0], l.nr[1]}, l.nrmax, nnz_cap, (int32_t *)(b + l.hist), (int32_t *)(b + l.ext),
+                 (uint32_t *)(b + l.words)};
+    return build_index(n_frames, d_point_offsets, d_point_counts, max_points_per_frame, d_points, points_dtype,
+                       d_voxels, voxels_itype, vox_stride, d_P, g, d_mval, d_cell, d_pix, d_val, nullptr, nullptr,
+                       d_frame_nnz, d_frame_out_off, d_err, d_ws, ws_bytes, (hipStream_t)stream, &bk);
 }
 
 // Writes the device [0, n] offsets of a single frame into the workspace tail.

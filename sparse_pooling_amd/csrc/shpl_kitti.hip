@@ -22,6 +22,7 @@ namespace shpl {
 namespace {
 
 struct VeloStage {
+    static constexpr bool HAS_BUCKETS = false;
     const float *xyzi;  // [N,4]
     const double *rect;  // [F,3,4]
     const double *P;     // [F,3,4] or null (no image filter)

@@ -28,10 +28,15 @@ class FusedPipeline:
     ROWS_FRAMES, ROWS_MAX_KEYS, ROWS_MAX_CAP = 32, 65536, 1 << 24
 
     def __init__(self, n_frames, max_points_per_frame, total_points, im_size, bv_size, stride,
-                 c_bev, c_img, dtype=torch.float32, device="cuda", dual=False, rows=None, live=False):
+                 c_bev, c_img, dtype=torch.float32, device="cuda", dual=False, rows=None, live=False,
+                 buckets=None):
         """live: the sparse passes walk each frame's live entries (shpl_csr frame layout) instead of the
         whole capacity -- for capacities far above the entry counts (FramePipeline: raw-scan slots per
-        voxel point); at config 2 (capacity = entries) the capacity walk is faster (2.22 vs 2.24 ms)."""
+        voxel point); at config 2 (capacity = entries) the capacity walk is faster (2.22 vs 2.24 ms).
+        buckets (default: with rows): the index build also cuts M into destination buckets
+        (shpl_build_index_buckets) and both pulls of a step run as ONE launch over them
+        (shpl_pull_buckets) on one stream -- no CSR launch, no cross-stream waits; rows without
+        buckets: the range CSRs + one k_rows launch per pull."""
         dev = torch.device(device)
         self.dev, self.dtype, self.dual = dev, dtype, dual
         self.B = int(n_frames)
@@ -50,6 +55,7 @@ class FusedPipeline:
             rows = (self.B < self.ROWS_FRAMES and max(self.Hb * self.Wb, self.Hi * self.Wi) <= self.ROWS_MAX_KEYS
                     and self.N < self.ROWS_MAX_CAP)  # the range CSR's 24-bit entry offsets
         self.rows = bool(rows)
+        self.buckets = self.rows if buckets is None else bool(buckets) and self.rows
         # dual layers in step_overlapped: the cell-keyed sparse pass beside img_fused's stream
         self.interleave = True
         N = max(self.N, 1)
@@ -72,12 +78,30 @@ class FusedPipeline:
                 if c is not None:
                     c.live_frames(self.frame_off, self.frame_nnz)
         self._lib = L.lib()
+        if self.buckets:
+            nb = L.bucket_ws_bytes(self.B, self.max_points, self.N, self.Hb * self.Wb, self.Hi * self.Wi)
+            self.bkt_ws = L.workspace(nb, dev)
+            self.bkt = L.ShplBuckets(self.B, self.max_points, self.N, self.Hb * self.Wb, self.Hi * self.Wi,
+                                     self.frame_off.data_ptr(), self.frame_nnz.data_ptr(), self.cell.data_ptr(),
+                                     self.pix.data_ptr(), self.val.data_ptr(), self.bkt_ws.data_ptr(),
+                                     self.bkt_ws.numel())
 
     # ------------------------------------------------------------------ steps
     def build_index(self, points, voxels, point_offsets, P, mval=None, point_counts=None):
         assert points.is_contiguous() and point_offsets.is_contiguous() and P.is_contiguous()
         assert voxels.stride(1) == 1, "voxel rows must be contiguous"
         st = L.stream_of(self.dev)
+        if self.buckets:
+            L.check(self._lib.shpl_build_index_buckets(
+                self.B, L.ptr(point_offsets), L.ptr(point_counts), self.max_points, L.ptr(points),
+                L.F64 if points.dtype == torch.float64 else L.F32, L.ptr(voxels),
+                L.I64 if voxels.dtype == torch.int64 else L.I32, int(voxels.stride(0)), L.ptr(P),
+                float(self.im_size[0]), float(self.im_size[1]), float(self.bv_size[0]),
+                float(self.bv_size[1]), self.stride[0], self.stride[1], L.ptr(mval), L.ptr(self.cell),
+                L.ptr(self.pix), L.ptr(self.val), L.ptr(self.frame_nnz), L.ptr(self.frame_off),
+                L.ptr(self.err), L.ptr(self.index_ws), self.index_ws.numel(), self.N, L.ptr(self.bkt_ws),
+                self.bkt_ws.numel(), st), "shpl_build_index_buckets")
+            return
         L.check(self._lib.shpl_build_index(
             self.B, L.ptr(point_offsets), L.ptr(point_counts), self.max_points, L.ptr(points),
             L.F64 if points.dtype == torch.float64 else L.F32, L.ptr(voxels),
@@ -91,6 +115,8 @@ class FusedPipeline:
     csr_path = L.CSR_AUTO
 
     def build_csr(self, which=("cell", "pixel")):
+        if self.buckets:
+            return  # the buckets came with the index build
         st = L.stream_of(self.dev)
         args = (self.B, L.ptr(self.frame_off), L.ptr(self.frame_nnz))
         if "cell" in which:
@@ -132,8 +158,21 @@ class FusedPipeline:
         return (direction, L.dtype_code(out), csr.ref(), L.ptr(src), cs, 0, cs, L.ptr(pass_), cp, 0, cp,
                 L.OUT_CONCAT, L.ptr(out), cs + cp)
 
+    def _pull_buckets(self, cell_desc, pix_desc):
+        L.check(self._lib.shpl_pull_buckets(ctypes.byref(self.bkt), ctypes.byref(cell_desc) if cell_desc else None,
+                                            ctypes.byref(pix_desc) if pix_desc else None,
+                                            L.stream_of(self.dev)), "shpl_pull_buckets")
+
     def layer_sparse(self, bev, img, which=("cell", "pixel")):
-        """Pooled rows, after layer_dense and build_csr."""
+        """Pooled rows, after layer_dense and build_csr (with buckets: both pulls, one launch)."""
+        if self.buckets:
+            dt = L.dtype_code(self.bv_fused)
+            cell = L.pull_desc(dt, img, self.Ci, 0, self.Ci, bev, self.Cb, 0, self.Cb, L.OUT_CONCAT, self.bv_fused,
+                               self.Cb + self.Ci) if "cell" in which else None
+            pix = L.pull_desc(dt, bev, self.Cb, 0, self.Cb, img, self.Ci, 0, self.Ci, L.OUT_CONCAT, self.img_fused,
+                              self.Ci + self.Cb) if self.dual and "pixel" in which else None
+            self._pull_buckets(cell, pix)
+            return
         if "cell" in which:
             self._sparse(self._concat_args(self.csr, L.BY_CELL, img, self.Ci, bev, self.Cb, self.bv_fused))
         if self.dual and "pixel" in which:
@@ -156,6 +195,18 @@ class FusedPipeline:
         Dual layers with `side2`: the pixel-keyed CSR and pull run on side2,
         beside the cell-keyed ones (they share only M).
         `events` (4 timing events) bracket the dense and the sparse launches."""
+        if self.buckets:
+            # one stream: index + buckets (2 launches), both pulls (1 launch); no side-stream waits
+            if events:
+                events[0].record()
+                events[1].record()
+            self.build_index(points, voxels, point_offsets, P, mval)
+            if events:
+                events[2].record()
+            self.layer_sparse(bev, img)
+            if events:
+                events[3].record()
+            return
         main = torch.cuda.current_stream(self.dev)
         side.wait_stream(main)            # inputs / previous step done
         split = self.dual and side2 is not None
@@ -276,6 +327,12 @@ class FusedPipeline:
         main = torch.cuda.current_stream(self.dev)
         w = self.Cb + self.Ci
         dt = L.dtype_code(d_bev)
+        if self.buckets:
+            self._pull_buckets(L.pull_desc(dt, g_img, w, self.Ci, self.Cb, g_bv, w, 0, self.Cb, L.OUT_ADD, d_bev,
+                                           self.Cb),
+                               L.pull_desc(dt, g_bv, w, self.Cb, self.Ci, g_img, w, 0, self.Ci, L.OUT_ADD, d_img,
+                                           self.Ci))
+            return
         cell = (L.BY_CELL, dt, self.csr.ref(), L.ptr(g_img), w, self.Ci, self.Cb, L.ptr(g_bv), w, 0, self.Cb,
                 L.OUT_ADD, L.ptr(d_bev), self.Cb)
         pix = (L.BY_PIXEL, dt, self.pcsr.ref(), L.ptr(g_bv), w, self.Cb, self.Ci, L.ptr(g_img), w, 0, self.Ci,

@@ -87,6 +87,26 @@ def test_argument_validation_is_host_side():
                   N) == L.ERR_BAD_SHAPE
         assert fn(L.BY_CELL, L.F32, ctypes.byref(csr), P, 32, 0, 32, N, 32, 0, 32, L.OUT_CONCAT, P, 64,
                   N) == L.ERR_ARG
+    # buckets: shapes over the limits (65536 destinations per frame, 2^24 points per frame), workspace size,
+    # missing bucket workspace; pull pair: null map, mixed dtypes, the bad-shape checks of shpl_pull
+    nb = ctypes.c_size_t()
+    assert lib.shpl_bucket_workspace_bytes(4, 20000, 80000, 8800, 6750, ctypes.byref(nb)) == L.OK and nb.value > 0
+    assert lib.shpl_bucket_workspace_bytes(4, 20000, 80000, 70000, 6750, ctypes.byref(nb)) == L.ERR_BAD_SHAPE
+    assert lib.shpl_bucket_workspace_bytes(4, (1 << 24) + 1, 80000, 8800, 6750, ctypes.byref(nb)) == L.ERR_BAD_SHAPE
+    args = (4, P, N, 20000, P, L.F64, P, L.I64, 2, P, 1200., 360., 704., 800., 8., 8., N, P, P, P, P, P, P, P,
+            1 << 20, 80000)
+    assert lib.shpl_build_index_buckets(*args, N, 1 << 24, N) == L.ERR_ARG
+    assert lib.shpl_build_index_buckets(*args, P, 64, N) == L.ERR_WORKSPACE
+    assert lib.shpl_build_index_buckets(*args[:14], 1., 1., *args[16:], P, 1 << 24, N) == L.ERR_BAD_SHAPE
+    bk = L.ShplBuckets(4, 20000, 80000, 8800, 6750, 256, 256, 256, 256, 256, 256, nb.value)
+    d32 = L.ShplPullDesc(L.F32, 256, 32, 0, 32, 256, 32, 0, 32, L.OUT_CONCAT, 256, 64)
+    d16 = L.ShplPullDesc(L.BF16, 256, 32, 0, 32, 256, 32, 0, 32, L.OUT_CONCAT, 256, 64)
+    assert lib.shpl_pull_buckets(None, ctypes.byref(d32), None, N) == L.ERR_ARG
+    assert lib.shpl_pull_buckets(ctypes.byref(bk), ctypes.byref(d32), ctypes.byref(d16), N) == L.ERR_BAD_SHAPE
+    narrow = L.ShplPullDesc(L.F32, 256, 32, 0, 32, 256, 32, 0, 32, L.OUT_CONCAT, 256, 48)
+    assert lib.shpl_pull_buckets(ctypes.byref(bk), ctypes.byref(narrow), None, N) == L.ERR_BAD_SHAPE
+    small = L.ShplBuckets(4, 20000, 80000, 8800, 6750, 256, 256, 256, 256, 256, 256, 64)
+    assert lib.shpl_pull_buckets(ctypes.byref(small), ctypes.byref(d32), None, N) == L.ERR_WORKSPACE
     # velodyne loader: P2 without image size, misaligned scan
     assert lib.shpl_velo_to_cam(1, P, 10, P, P, P, N, math.nan, N, P, P, N, P, 1 << 20, N) == L.ERR_ARG
     assert lib.shpl_velo_to_cam(1, P, 10, ctypes.c_void_p(260), P, N, N, math.nan, N, P, P, N, P, 1 << 20,

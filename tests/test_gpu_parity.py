@@ -531,7 +531,8 @@ def test_full_size_properties_config5():
     (1, "f32", "eager", False), (1, "bf16", "eager", False), (1, "bf16", "streams", False), (1, "f32", "graph", False),
     (3, "bf16", "eager", False), (3, "bf16", "graph", False),
     (1, "f32", "eager", True), (1, "bf16", "streams", True), (1, "f32", "graph", True),
-    (3, "bf16", "eager", True), (3, "bf16", "graph", True), (3, "f32", "streams", True)])
+    (3, "bf16", "eager", True), (3, "bf16", "graph", True), (3, "f32", "streams", True),
+    (1, "f32", "graph", "csr"), (3, "bf16", "eager", "csr"), (3, "bf16", "graph", "csr")])
 def test_pipeline_backward_matches_oracle(cfg, dtype, mode, rows):
     """FusedPipeline forward + backward (the config-3 bench step) vs the oracle's TF
     forward and gradients; mode streams/graph: the bench's step (side streams for the
@@ -539,7 +540,9 @@ def test_pipeline_backward_matches_oracle(cfg, dtype, mode, rows):
     captured HIP graph. cfg 3 is the bench's own shape: bf16, 256 channels (32 chunks
     per pooled row, the power-of-two path), stride 8, pixel runs far longer than
     k_sparse's 8 entries (k_sparse_long with per-column partials in OUT_ADD mode).
-    rows: the CSRs carry key_range and every pull is one row-keyed launch (k_rows)."""
+    rows True: the index build cuts M into destination buckets and each pull pair is one
+    launch over them (shpl_pull_buckets, one stream); "csr": the CSRs carry key_range and
+    every pull is one row-keyed launch (k_rows)."""
     from sparse_pooling_amd import pipeline
     spec = synth.CONFIGS[cfg]
     B = 2 if cfg == 1 else 4
@@ -551,7 +554,8 @@ def test_pipeline_backward_matches_oracle(cfg, dtype, mode, rows):
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
     tdt = torch.float32 if dtype == "f32" else torch.bfloat16
     pl = pipeline.FusedPipeline(B, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev, spec.c_img,
-                                dtype=tdt, dual=True, rows=rows)
+                                dtype=tdt, dual=True, rows=bool(rows), buckets=rows is True)
+    assert pl.buckets == (rows is True)
     Hb, Wb = spec.bev_feat_hw
     Hi, Wi = spec.img_feat_hw
     Cb, Ci = spec.c_bev, spec.c_img
@@ -625,14 +629,18 @@ def _ragged_frames(base, sizes, seed):
     return frames
 
 
-def _ragged_pipeline_run(cfg, sizes, dtype, paths):
+def _ragged_pipeline_run(cfg, sizes, dtype, paths, channels=None, frames=None):
     """FusedPipeline forward + backward over a ragged batch, once per CSR path
-    (shpl_build_csr_path: frame / segment / range; None = the default), each compared
-    with the oracle frame by frame (f32: bitwise; bf16: bitwise on the bf16 bits)."""
+    (shpl_build_csr_path: frame / segment / range; None = the default; "buckets": the
+    index build's destination buckets and the one-launch pull pair, shpl_pull_buckets;
+    "csr_rows": range CSRs + k_rows), each compared with the oracle frame by frame
+    (f32: bitwise; bf16: bitwise on the bf16 bits). channels: (Cb, Ci) instead of the config's."""
     from sparse_pooling_amd import _lib as L
     from sparse_pooling_amd import pipeline
     base = synth.CONFIGS[cfg]
-    frames = _ragged_frames(base, sizes, 500)
+    if channels is not None:
+        base = synth.FrameSpec(base.n_points, base.im_size, base.bv_size, base.stride, *channels)
+    frames = _ragged_frames(base, sizes, 500) if frames is None else frames
     refs = [_oracle_frame(fr, base.stride) for fr in frames]
     B = len(frames)
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
@@ -669,9 +677,11 @@ def _ragged_pipeline_run(cfg, sizes, dtype, paths):
     codes = {None: L.CSR_AUTO, "frame": L.CSR_FRAME, "segment": L.CSR_SEGMENT, "range": L.CSR_RANGE,
              "bucket": L.CSR_BUCKET}
     for path in paths:
+        kw = {"buckets": dict(rows=True, buckets=True), "csr_rows": dict(rows=True, buckets=False)}.get(path, {})
         pl = pipeline.FusedPipeline(B, maxp, N, base.im_size, base.bv_size, base.stride, Cb, Ci, dtype=tdt,
-                                    dual=True)
-        pl.csr_path = codes[path]
+                                    dual=True, **kw)
+        assert pl.buckets == (path == "buckets")
+        pl.csr_path = codes.get(path, L.CSR_AUTO)
         d_bev, d_img = torch.empty_like(tb), torch.empty_like(ti)
         pl.step(pts, vox, off, P, tb, ti)
         pl.backward(tgb, tgi, d_bev, d_img)
@@ -685,6 +695,37 @@ def _ragged_pipeline_run(cfg, sizes, dtype, paths):
             same(d_bev[f:f + 1], e_bev)
             same(d_img[f:f + 1], e_img)
         del pl
+
+
+@pytest.mark.parametrize("dtype,cb,ci", [("bf16", 256, 256), ("f32", 256, 256), ("f32", 16, 32), ("bf16", 64, 64),
+                                         ("f32", 3, 5), ("bf16", 8, 24), ("f32", 64, 128)])
+def test_bucket_pulls_ragged_batch(dtype, cb, ci):
+    """The bucketed step (shpl_build_index_buckets -> shpl_pull_buckets: both pulls in one
+    launch, forward then gradients) at config 3's geometry over a ragged batch -- no points,
+    one point, no survivor, one survivor among 14 points (the dgemv projection order: no
+    bucket, the entry read from the index arrays), chunk-straddling and full frames --
+    bitwise against the oracle and against the range CSR + k_rows path, for every lane
+    group width (G = 8 .. 64) and the unvectorised form (3 / 5 f32 channels)."""
+    _ragged_pipeline_run(3, [0, 1, -40, 1025, 20000, 2], dtype, ["buckets", "csr_rows"], channels=(cb, ci))
+
+
+def test_bucket_pulls_overflowing_part():
+    """One frame whose 3000 points are one point repeated (one cell, one pixel: a part far over
+    the pull's 2048-entry LDS sort, which then sorts through the workspace scratch) beside
+    ordinary frames: bitwise against the oracle, f32 and bf16."""
+    base = synth.CONFIGS[3]
+    rng = np.random.default_rng(9)
+    one = synth.make_frame(synth.FrameSpec(1, base.im_size, base.bv_size, base.stride, 32, 32), seed=3)
+    pts = np.repeat(one.points, 3000, axis=0)
+    vox = np.repeat(one.voxel_indices, 3000, axis=0)
+    heavy = synth.Frame(pts, vox, synth.KITTI_P2, base)
+    mixed = synth.make_frame(synth.FrameSpec(4000, base.im_size, base.bv_size, base.stride, 32, 32), seed=4)
+    half = mixed.points.shape[0] // 2  # half of a frame's points on one cell too (a long run among others)
+    mixed.voxel_indices[:half] = mixed.voxel_indices[0]
+    frames = [heavy, synth.make_frame(synth.FrameSpec(3000, base.im_size, base.bv_size, base.stride, 32, 32),
+                                      seed=5, n_outside=int(rng.integers(1, 50))), mixed]
+    for dtype in ("f32", "bf16"):
+        _ragged_pipeline_run(3, None, dtype, ["buckets"], channels=(32, 32), frames=frames)
 
 
 def test_pipeline_ragged_batch_every_csr_path():
