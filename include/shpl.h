@@ -409,11 +409,11 @@ typedef struct {
     const int64_t *frame_off, *frame_nnz; /* [n_frames + 1], [n_frames] */
     const int32_t *cell, *pix;            /* [nnz_cap] global rows, as shpl_build_index writes them */
     const float *val;                     /* [nnz_cap] */
-    void *ws;                             /* the bucket workspace (also the pull's sort scratch) */
+    void *ws;                             /* the bucket workspace */
     size_t ws_bytes;
 } shpl_buckets;
 
-/* One pull of shpl_pull_buckets: the arguments of shpl_pull after its csr. */
+/* One pull of shpl_pull_pair: the arguments of shpl_pull after its csr. */
 typedef struct {
     int dtype;
     const void *src;
@@ -425,17 +425,25 @@ typedef struct {
     int64_t out_stride;
 } shpl_pull_desc;
 
-/* The cell-keyed pull (by_cell: destination = BEV cell, sources = image
- * pixels) and the pixel-keyed pull (by_pixel: destination = pixel, sources =
- * BEV cells) over the buckets, in ONE launch (either may be NULL): a
- * workgroup per (pull, frame, range part) reads its bucket, sorts its part's
- * entries by destination in LDS, and writes its output rows as shpl_pull
- * would -- same values, bit for bit, as shpl_pull over the CSRs
- * shpl_build_csr makes of the same index arrays. Both pulls take one dtype.
- * Replaces the forward pair (sparse_pool_utils.py:96-117 + the concats of
- * :72, :87) or, with SHPL_OUT_ADD, its gradient pair. */
-int shpl_pull_buckets(const shpl_buckets *bk, const shpl_pull_desc *by_cell, const shpl_pull_desc *by_pixel,
-                      void *stream);
+/* Both CSRs of the map (by_cell: SHPL_BY_CELL, SHPL_ORDER_ENTRY; by_pixel:
+ * SHPL_BY_PIXEL, SHPL_ORDER_COL_ROW with ent_col; either may be NULL) from
+ * the buckets, in ONE launch: a workgroup per (key, frame, range) sorts its
+ * bucket by destination, stably (the bucket is in entry order), emits the
+ * sorted entries and key_range (when set) and clears the unused capacity --
+ * the same lists shpl_build_csr makes of the same index arrays. No counting or
+ * bucketing pass: the index build did both. */
+int shpl_build_csr_buckets(const shpl_buckets *bk, const shpl_csr *by_cell, const shpl_csr *by_pixel,
+                           void *stream);
+
+/* Two row-keyed pulls in ONE launch (shpl_pull over CSRs with key_range):
+ * d_cell over by_cell (SHPL_BY_CELL), d_pixel over by_pixel (SHPL_BY_PIXEL);
+ * either pair may be NULL (two launches if their dtypes or vector widths
+ * differ). Same results, bit for bit,
+ * as the two shpl_pull calls. Replaces the forward pair
+ * (sparse_pool_utils.py:96-117, with the concats of :72, :87) or, with
+ * SHPL_OUT_ADD, its gradient pair. */
+int shpl_pull_pair(const shpl_csr *by_cell, const shpl_pull_desc *d_cell, const shpl_csr *by_pixel,
+                   const shpl_pull_desc *d_pixel, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Post-fusion 3x3 convolution

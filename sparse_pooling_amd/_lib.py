@@ -89,7 +89,7 @@ class ShplBuckets(ctypes.Structure):
 
 
 class ShplPullDesc(ctypes.Structure):
-    """struct shpl_pull_desc of include/shpl.h: shpl_pull's arguments after its csr."""
+    """struct shpl_pull_desc of include/shpl.h: shpl_pull's arguments after its csr (shpl_pull_pair)."""
     _fields_ = [("dtype", ctypes.c_int), ("src", ctypes.c_void_p), ("src_stride", ctypes.c_int64),
                 ("src_off", ctypes.c_int64), ("c_pool", ctypes.c_int64), ("pass_", ctypes.c_void_p),
                 ("pass_stride", ctypes.c_int64), ("pass_off", ctypes.c_int64), ("c_pass", ctypes.c_int64),
@@ -135,8 +135,10 @@ def _declare(lib):
         "shpl_bucket_workspace_bytes": (i32, [i32, i64, i64, i64, i64, psz]),
         "shpl_build_index_buckets": (i32, [i32, p, p, i64, p, i32, p, i32, i64, p, d, d, d, d, d, d, p,
                                            p, p, p, p, p, p, p, sz, i64, p, sz, p]),
-        "shpl_pull_buckets": (i32, [ctypes.POINTER(ShplBuckets), ctypes.POINTER(ShplPullDesc),
-                                    ctypes.POINTER(ShplPullDesc), p]),
+        "shpl_build_csr_buckets": (i32, [ctypes.POINTER(ShplBuckets), ctypes.POINTER(ShplCsr),
+                                         ctypes.POINTER(ShplCsr), p]),
+        "shpl_pull_pair": (i32, [ctypes.POINTER(ShplCsr), ctypes.POINTER(ShplPullDesc), ctypes.POINTER(ShplCsr),
+                                 ctypes.POINTER(ShplPullDesc), p]),
         "shpl_pull": (i32, pull_args),
         "shpl_pull_dense": (i32, pull_args),
         "shpl_pull_sparse": (i32, pull_args),

@@ -127,7 +127,7 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // ---------------------------------------------------------------- buckets
 // Destination buckets of the index builder's entries (shpl_build_index_buckets
-// -> shpl_pull_buckets): per key (0 = BEV cells, 1 = image pixels) a frame's
+// -> shpl_build_csr_buckets): per key (0 = BEV cells, 1 = image pixels) a frame's
 // destinations are cut into ranges of BK_KEYS; bucket (key, frame, range)
 // lists the frame's entries of that range in entry order -- TF's order inside
 // every destination -- as 32-bit words (local destination << 24 | entry slot
@@ -135,8 +135,6 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 //   hist  [2][F][n_chunks][nrmax] i32  entries per (index chunk, range)
 //   ext   [2][F][nrmax][2]        i32  bucket (start from the frame's first slot, entries)
 //   words [2][nnz_cap]            u32  the buckets, frame f's at [off[f], off[f] + nnz_f)
-//   swords / ssrc / sval [2][nnz_cap]  scratch of the pull's sort when a
-//                                      workgroup's entries overflow its LDS
 constexpr int BK_KEYS = 128;        // destinations per range
 constexpr int BK_MAX_RANGES = 512;  // ranges per frame (65536 destinations)
 constexpr int BK_RBITS = 9;         // range bits matched by the placement's multisplit
@@ -144,7 +142,7 @@ constexpr int BK_RBITS = 9;         // range bits matched by the placement's mul
 struct BkLayout {
     int n_frames, n_chunks, nr[2], nrmax;
     int64_t nnz_cap, kpf[2];
-    size_t hist, ext, words, swords, ssrc, sval, bytes;  // byte offsets into the workspace, total
+    size_t hist, ext, words, bytes;  // byte offsets into the workspace, total
 };
 
 inline BkLayout bk_layout(int n_frames, int n_chunks, int64_t nnz_cap, int64_t cells_per_frame,
@@ -165,12 +163,6 @@ inline BkLayout bk_layout(int n_frames, int n_chunks, int64_t nnz_cap, int64_t c
     l.ext = o;
     o = align_up(o + 4 * 2 * F * (size_t)l.nrmax * 2, 256);
     l.words = o;
-    o = align_up(o + 4 * 2 * cap, 256);
-    l.swords = o;
-    o = align_up(o + 4 * 2 * cap, 256);
-    l.ssrc = o;
-    o = align_up(o + 4 * 2 * cap, 256);
-    l.sval = o;
     o = align_up(o + 4 * 2 * cap, 256);
     l.bytes = o;
     return l;

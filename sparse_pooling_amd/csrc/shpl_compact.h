@@ -225,10 +225,15 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr, Bkt 
         static_assert(IDX_BLOCK == 2 * BK_MAX_RANGES, "one thread per (key, range)");
         if (bq < bk.nr[bK]) {
             const int32_t *h = bk.hist + ((int64_t)bK * fr.n_frames + f) * fr.n_chunks * bk.nrmax + bq;
-            for (int jj = 0; jj < fr.n_chunks; ++jj) {
-                const int32_t v = h[(int64_t)jj * bk.nrmax];
-                b_tot += v;
-                b_bef += jj < j ? v : 0;
+            for (int j0 = 0; j0 < fr.n_chunks; j0 += 8) {  // 8 loads in flight
+                int32_t v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = j0 + u < fr.n_chunks ? h[(int64_t)(j0 + u) * bk.nrmax] : 0;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    b_tot += v[u];
+                    b_bef += j0 + u < j ? v[u] : 0;
+                }
             }
         }
         for (int i = threadIdx.x; i < 2 * (IDX_BLOCK / 64) * BK_MAX_RANGES; i += IDX_BLOCK) (&s_w[0][0][0])[i] = 0;

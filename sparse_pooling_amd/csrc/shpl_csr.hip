@@ -806,6 +806,7 @@ constexpr int BKT_MAX_FRAMES = 1024;   // frames of one build (one per thread of
 constexpr int BKT_SORT = 512;          // threads of a sort workgroup
 constexpr int BKT_RBITS = 9;           // range bits matched by the place multisplit (BKT_MAX_RANGES)
 static_assert(RANGE_KEYS == 128, "the sort multisplit matches 7 destination bits");
+static_assert(BK_KEYS == RANGE_KEYS, "the index builder's buckets are the sort's ranges");
 
 struct BktIn {
     int n_ranges;         // ranges per frame
@@ -972,29 +973,22 @@ __global__ __launch_bounds__(BKT_CHUNK) void k_bkt_place(CsrIn c, BktIn k) {
     if (ok) k.words[e0 + s_off[r] + s_w[wid][r] + rank] = ((uint32_t)(t % RANGE_KEYS) << 24) | (uint32_t)(e - e0);
 }
 
-template <bool HAS_COL>
-__global__ __launch_bounds__(BKT_SORT) void k_bkt_sort(CsrIn c, BktIn k, int64_t nnz_cap, int64_t n_keys,
-                                                      int32_t *ent_dst, int32_t *ent_src, float *ent_val,
-                                                      int32_t *ent_col, int32_t *key_range) {
+// A bucket's counting sort (k_bkt_sort, k_bsort2): words[0, n) = the bucket of destinations
+// [k0, k0 + nk) (global ids, word = local destination << 24 | entry - e0) in entry order, placed stably
+// by destination at out0.. (rounds of BKT_SORT words in bucket order, wave ballots over the 7 destination
+// bits) with source row, value and column; key_range of its destinations. BY_CELL: source = pix[e];
+// BY_PIXEL: source = cell[e] and column e (the builder's identity columns). Returns nothing; all threads.
+__device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t n, int64_t e0, int64_t out0,
+                                                 int64_t k0, int nk, int direction, const int32_t *col,
+                                                 const int32_t *cell, const int32_t *pix, const float *vals,
+                                                 int32_t *ent_dst, int32_t *ent_src, float *ent_val,
+                                                 int32_t *ent_col, int32_t *key_range) {
     __shared__ int32_t cnt[RANGE_KEYS], cur[RANGE_KEYS], s_w[BKT_SORT / 64][RANGE_KEYS];
-    const int f = blockIdx.y, q = blockIdx.x;
-    int64_t e0, e1, cap_end;
-    frame_range(c, f, e0, e1, cap_end);
-    const int64_t kf = (int64_t)f * c.keys_per_frame, kend = kf + c.keys_per_frame;
-    const int64_t k0 = kf + (int64_t)q * RANGE_KEYS;
-    const int nk = (int)(k0 + RANGE_KEYS < kend ? RANGE_KEYS : kend - k0);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    int32_t start = 0, n = 0;
-    if (e1 > e0) {  // a frame without live entries has no chunk, so no bucket extents
-        const int32_t *x = k.ext + ((int64_t)f * k.n_ranges + q) * 2;
-        start = x[0];
-        n = x[1];
-    }
-    const int64_t out0 = e0 + start;
     for (int i = threadIdx.x; i < (BKT_SORT / 64) * RANGE_KEYS; i += BKT_SORT) s_w[i / RANGE_KEYS][i % RANGE_KEYS] = 0;
     if ((int)threadIdx.x < RANGE_KEYS) cnt[threadIdx.x] = 0;
     __syncthreads();
-    for (int32_t i = threadIdx.x; i < n; i += BKT_SORT) atomicAdd(&cnt[k.words[out0 + i] >> 24], 1);
+    for (int32_t i = threadIdx.x; i < n; i += BKT_SORT) atomicAdd(&cnt[words[i] >> 24], 1);
     __syncthreads();
     // destinations' starts (128 counts: the first two waves)
     if ((int)threadIdx.x < RANGE_KEYS) {
@@ -1024,15 +1018,15 @@ __global__ __launch_bounds__(BKT_SORT) void k_bkt_sort(CsrIn c, BktIn k, int64_t
     for (int32_t b0 = 0; b0 < n; b0 += BKT_SORT) {
         const int32_t i = b0 + threadIdx.x;
         const bool ok = i < n;
-        const uint32_t w = ok ? k.words[out0 + i] : 0u;
+        const uint32_t w = ok ? words[i] : 0u;
         const int t = (int)(w >> 24);
         const int64_t e = e0 + (w & 0xffffffu);
         int32_t kk = 0, src = 0;
         float val = 0.0f;
         if (ok) {  // the emission's loads, in flight during the multisplit
-            kk = HAS_COL ? c.col[e] : (int32_t)e;
-            val = c.val[e];
-            src = c.direction == SHPL_BY_CELL ? c.pix[kk] : c.cell[e];
+            kk = col ? col[e] : (int32_t)e;
+            val = vals[e];
+            src = direction == SHPL_BY_CELL ? pix[kk] : cell[e];
         }
         uint64_t peers = __ballot(ok);
 #pragma unroll
@@ -1068,6 +1062,27 @@ __global__ __launch_bounds__(BKT_SORT) void k_bkt_sort(CsrIn c, BktIn k, int64_t
         }
         __syncthreads();
     }
+}
+
+template <bool HAS_COL>
+__global__ __launch_bounds__(BKT_SORT) void k_bkt_sort(CsrIn c, BktIn k, int64_t nnz_cap, int64_t n_keys,
+                                                      int32_t *ent_dst, int32_t *ent_src, float *ent_val,
+                                                      int32_t *ent_col, int32_t *key_range) {
+    const int f = blockIdx.y, q = blockIdx.x;
+    int64_t e0, e1, cap_end;
+    frame_range(c, f, e0, e1, cap_end);
+    const int64_t kf = (int64_t)f * c.keys_per_frame, kend = kf + c.keys_per_frame;
+    const int64_t k0 = kf + (int64_t)q * RANGE_KEYS;
+    const int nk = (int)(k0 + RANGE_KEYS < kend ? RANGE_KEYS : kend - k0);
+    int32_t start = 0, n = 0;
+    if (e1 > e0) {  // a frame without live entries has no chunk, so no bucket extents
+        const int32_t *x = k.ext + ((int64_t)f * k.n_ranges + q) * 2;
+        start = x[0];
+        n = x[1];
+    }
+    const int64_t out0 = e0 + start;
+    bucket_sort_emit(k.words + out0, n, e0, out0, k0, nk, c.direction, HAS_COL ? c.col : nullptr, c.cell, c.pix,
+                     c.val, ent_dst, ent_src, ent_val, ent_col, key_range);
     // the frame's unused capacity (its last range), the slots and key ranges after the last frame
     if (q != k.n_ranges - 1) return;
     for (int64_t h = out0 + n + threadIdx.x; h < cap_end; h += BKT_SORT) ent_dst[h] = -1;
@@ -1077,6 +1092,80 @@ __global__ __launch_bounds__(BKT_SORT) void k_bkt_sort(CsrIn c, BktIn k, int64_t
         for (int64_t kk = kend + threadIdx.x; kk < n_keys; kk += BKT_SORT) {
             key_range[2 * kk] = 0;
             key_range[2 * kk + 1] = 0;
+        }
+}
+
+// ------------------------------------------------ both CSRs from the index build's buckets
+// (shpl_build_csr_buckets). One launch: a BKT_SORT-thread workgroup per (key, frame, range) sorts its
+// bucket with bucket_sort_emit -- the buckets are the index builder's (shpl_common.h BkLayout), so no
+// counting or bucketing pass precedes it. A frame of at most one entry has no bucket: that entry is
+// read from the index arrays.
+struct BsSide {
+    int nr;            // ranges per frame (0: side absent)
+    int64_t kpf, n_keys, nnz_cap;
+    int32_t *ent_dst, *ent_src;
+    float *ent_val;
+    int32_t *ent_col, *key_range;
+    int64_t blocks;    // n_frames * nr
+};
+
+struct BsIn {
+    const int64_t *frame_off, *frame_nnz;
+    const int32_t *cell, *pix;
+    const float *val;
+    const int32_t *ext;
+    const uint32_t *words;
+    int n_frames, nrmax;
+    int64_t nnz_cap;
+};
+
+__global__ __launch_bounds__(BKT_SORT) void k_bsort2(BsIn in, BsSide s0, BsSide s1) {
+    __shared__ uint32_t one[1];
+    const bool second = (int64_t)blockIdx.x >= s0.blocks;
+    const BsSide &sd = second ? s1 : s0;
+    const int key = second ? 1 : 0;
+    const int64_t b = second ? (int64_t)blockIdx.x - s0.blocks : (int64_t)blockIdx.x;
+    const int f = (int)(b / sd.nr), q = (int)(b - (int64_t)f * sd.nr);
+    const int64_t p0 = in.frame_off[f], cap_end = in.frame_off[f + 1];
+    int64_t nnz = in.frame_nnz[f];
+    nnz = nnz < 0 ? 0 : (nnz > cap_end - p0 ? cap_end - p0 : nnz);
+    const int64_t kf = (int64_t)f * sd.kpf, kend = kf + sd.kpf;
+    const int64_t k0 = kf + (int64_t)q * RANGE_KEYS;
+    const int nk = (int)(k0 + RANGE_KEYS < kend ? RANGE_KEYS : kend - k0);
+    const int direction = key ? SHPL_BY_PIXEL : SHPL_BY_CELL;
+    int32_t start = 0, n = 0, valid = 0;
+    const uint32_t *W = one;
+    if (nnz >= 2) {
+        const int32_t *x = in.ext + (((int64_t)key * in.n_frames + f) * in.nrmax + q) * 2;
+        start = x[0];
+        n = x[1];
+        W = in.words + (int64_t)key * in.nnz_cap + p0 + start;
+        if (q == sd.nr - 1) valid = start + n;  // the frame's entries with valid destinations
+    } else if (nnz == 1) {
+        // no bucket: the frame's one entry, in this range or not
+        const int32_t c = in.cell[p0], p = in.pix[p0];
+        if (c >= 0 && p >= 0) {
+            valid = 1;
+            const int64_t k = key ? p : c;
+            if (k >= k0 && k < k0 + nk) {
+                if (threadIdx.x == 0) one[0] = (uint32_t)(k - k0) << 24;
+                n = 1;
+            }
+        }
+        __syncthreads();
+    }
+    const int64_t out0 = p0 + start;
+    bucket_sort_emit(W, n, p0, out0, k0, nk, direction, nullptr, in.cell, in.pix, in.val, sd.ent_dst, sd.ent_src,
+                     sd.ent_val, sd.ent_col, sd.key_range);
+    // the frame's unused capacity (its last range), the slots and key ranges after the last frame
+    if (q != sd.nr - 1) return;
+    for (int64_t h = p0 + valid + threadIdx.x; h < cap_end; h += BKT_SORT) sd.ent_dst[h] = -1;
+    if (f != in.n_frames - 1) return;
+    for (int64_t h = cap_end + threadIdx.x; h < sd.nnz_cap; h += BKT_SORT) sd.ent_dst[h] = -1;
+    if (sd.key_range)
+        for (int64_t kk = kend + threadIdx.x; kk < sd.n_keys; kk += BKT_SORT) {
+            sd.key_range[2 * kk] = 0;
+            sd.key_range[2 * kk + 1] = 0;
         }
 }
 
@@ -1318,4 +1407,48 @@ extern "C" int shpl_build_csr(int direction, int order, int n_frames, const int6
                               void *d_ws, size_t ws_bytes, void *stream) {
     return shpl_build_csr_path(SHPL_CSR_AUTO, direction, order, n_frames, d_frame_off, d_frame_nnz, keys_per_frame,
                                d_cell, d_col, d_val, d_pix, csr, d_ws, ws_bytes, stream);
+}
+
+extern "C" int shpl_build_csr_buckets(const shpl_buckets *bk, const shpl_csr *by_cell, const shpl_csr *by_pixel,
+                                      void *stream) {
+    if (!bk || bk->n_frames < 1 || !bk->frame_off || !bk->frame_nnz || !bk->ws) return SHPL_ERR_ARG;
+    size_t need = 0;
+    int rc = shpl_bucket_workspace_bytes(bk->n_frames, bk->max_points_per_frame, bk->nnz_cap, bk->cells_per_frame,
+                                         bk->pix_per_frame, &need);
+    if (rc) return rc;
+    if (bk->ws_bytes < need) return SHPL_ERR_WORKSPACE;
+    if (bk->nnz_cap > 0 && (!bk->cell || !bk->pix || !bk->val)) return SHPL_ERR_ARG;
+    const int64_t chunks = (bk->max_points_per_frame + 1023) / 1024;
+    const BkLayout l = bk_layout(bk->n_frames, (int)(chunks < 1 ? 1 : chunks), bk->nnz_cap, bk->cells_per_frame,
+                                 bk->pix_per_frame);
+    const shpl_csr *cs[2] = {by_cell, by_pixel};
+    BsSide s[2] = {};
+    for (int k = 0; k < 2; ++k) {
+        const shpl_csr *c = cs[k];
+        if (!c) continue;
+        if (c->n_keys < (int64_t)bk->n_frames * l.kpf[k] || c->n_keys >= 2147483647LL || c->nnz_cap < bk->nnz_cap)
+            return SHPL_ERR_BAD_SHAPE;
+        if (bk->nnz_cap > 0 && (!c->ent_dst || !c->ent_src || !c->ent_val)) return SHPL_ERR_ARG;
+        if (k == 1 && bk->nnz_cap > 0 && !c->ent_col) return SHPL_ERR_ARG;
+        s[k] = BsSide{l.nr[k], l.kpf[k], c->n_keys, c->nnz_cap, c->ent_dst, c->ent_src, c->ent_val, c->ent_col,
+                      c->key_range, (int64_t)bk->n_frames * l.nr[k]};
+        if (l.nr[k] == 0) s[k].blocks = 0;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    if (bk->nnz_cap == 0) {  // an empty map: empty runs everywhere
+        for (int k = 0; k < 2; ++k)
+            if (cs[k] && cs[k]->key_range && cs[k]->n_keys > 0 &&
+                hipMemsetAsync(cs[k]->key_range, 0, sizeof(int32_t) * 2 * (size_t)cs[k]->n_keys, st) != hipSuccess)
+                return SHPL_ERR_HIP;
+        return SHPL_OK;
+    }
+    const int64_t blocks = s[0].blocks + s[1].blocks;
+    if (blocks == 0) return SHPL_OK;
+    if (blocks > 0x7fffffffLL) return SHPL_ERR_BAD_SHAPE;
+    char *w = (char *)bk->ws;
+    const BsIn in{bk->frame_off, bk->frame_nnz, bk->cell, bk->pix, bk->val, (const int32_t *)(w + l.ext),
+                  (const uint32_t *)(w + l.words), bk->n_frames, l.nrmax, bk->nnz_cap};
+    hipLaunchKernelGGL(k_bsort2, dim3((unsigned)blocks), dim3(BKT_SORT), 0, st, in, s[0], s[1]);
+    SHPL_LAUNCH_CHECK();
+    return SHPL_OK;
 }

@@ -522,18 +522,11 @@ constexpr int ROWS_WALK = SHPL_ROWS_WALK;
 #endif
 
 template <typename T, int VEC, bool GROUP, int G>
-__global__ __launch_bounds__(SHPL_BLOCK) void k_rows(const Feat f, const Ents e, const int32_t *key_range,
-                                                     int64_t n_rows) {
+__device__ __forceinline__ void rows_body(const Feat &f, const Ents &e, const int32_t *key_range, int64_t n_rows,
+                                          int64_t blk) {
     typedef Chunk<T, VEC> C;
     constexpr int RPW = SHPL_WAVE / G;
     const int lane = threadIdx.x & 63, lg = lane & (G - 1), gbase = lane & ~(G - 1);
-#if SHPL_PULL_XCD
-    // each XCD one contiguous stretch of output rows (config 3: half a frame), so the rows its runs
-    // gather (one frame's sources, 3.5-4.5 MB) stay in its L2 instead of every XCD's L2 seeing all frames
-    const int64_t blk = xcd_block(blockIdx.x, gridDim.x);
-#else
-    const int64_t blk = blockIdx.x;
-#endif
     const int64_t row = (blk * (SHPL_BLOCK / SHPL_WAVE) + (threadIdx.x >> 6)) * RPW + lane / G;
     const bool live = row < n_rows;
     T *out = reinterpret_cast<T *>(f.out);
@@ -627,260 +620,33 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_rows(const Feat f, const Ents e,
     }
 }
 
-// ---------------------------------------------------------------- k_bpull
-// Both keyed pulls of a small batch in ONE launch, straight from the index
-// builder's destination buckets (shpl_build_index_buckets): no CSR launch, no
-// second stream. Workgroup = (pull, frame, part of a 128-destination range):
-// a part is the BP_SUB = 16 waves x 64/G rows the workgroup writes.
-//   A. the pass-through chunks of its rows are copied (CONCAT) or loaded (ADD)
-//      first, beside everything below;
-//   B. its bucket (the range's entries in entry order, L2-resident) is read
-//      once; the words of its part go to an LDS list with per-destination
-//      counts (wave-aggregated slots);
-//   C. counting sort in LDS: scan, placement (atomics: any order inside a
-//      destination), then each word's rank inside its destination -- its words'
-//      numeric order is entry order, TF's -- and the entry's source row and
-//      weight loaded into the sorted slot;
-//   D. a group of G lanes per row walks the row's sorted entries, ROWS_WALK
-//      feature rows in flight, k_sparse's arithmetic (separate multiply and
-//      add in entry order; the builder's identity columns make TF's per-column
-//      partials Q[k] single products, so the plain sum is bitwise the same).
-// A part holding more than BP_CAP entries (a pathological frame) sorts through
-// the workspace scratch instead of LDS, same order.
-constexpr int BP_BLOCK = 1024;
-constexpr int BP_CAP = 2048;  // entries of one part sorted in LDS (16 KiB per array)
-constexpr int BP_LOAD = 4;    // bucket words per thread in flight
-#ifndef SHPL_BPULL_XCD
-#define SHPL_BPULL_XCD 0      // 1: XCD-contiguous workgroups (one (pull, frame) per XCD at config 3)
+template <typename T, int VEC, bool GROUP, int G>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_rows(const Feat f, const Ents e, const int32_t *key_range,
+                                                     int64_t n_rows) {
+#if SHPL_PULL_XCD
+    // each XCD one contiguous stretch of output rows (config 3: half a frame), so the rows its runs
+    // gather (one frame's sources, 3.5-4.5 MB) stay in its L2 instead of every XCD's L2 seeing all frames
+    rows_body<T, VEC, GROUP, G>(f, e, key_range, n_rows, xcd_block(blockIdx.x, gridDim.x));
+#else
+    rows_body<T, VEC, GROUP, G>(f, e, key_range, n_rows, blockIdx.x);
 #endif
-
-struct BpSide {
-    Feat f;
-    int key;        // 0: destination = BEV cell, source = pix[e]; 1: destination = pixel, source = cell[e]
-    int nr, subs;   // ranges per frame, parts per range
-    int64_t kpf;    // destinations per frame
-    int64_t blocks; // n_frames * nr * subs
-};
-
-struct BpIn {
-    const int64_t *frame_off, *frame_nnz;
-    const int32_t *cell, *pix;
-    const float *val;
-    const int32_t *ext;
-    const uint32_t *words;
-    uint32_t *swords;
-    int32_t *ssrc;
-    float *sval;
-    int n_frames, nrmax;
-    int64_t nnz_cap, kpf[2];
-};
-
-// D. rows t of the part: pooled chunks from the sorted entries [beg[t], beg[t+1]) of (src_l, val_l)
-template <typename T, int VEC, int G, typename SP, typename VP>
-__device__ __forceinline__ void bp_rows(const Feat &f, int64_t row, bool live, int32_t first, int32_t end,
-                                        SP src_l, VP val_l, typename Chunk<T, VEC>::raw_t av) {
-    typedef Chunk<T, VEC> C;
-    if (!live) return;
-    const int lg = (threadIdx.x & 63) & (G - 1);
-    T *out = reinterpret_cast<T *>(f.out);
-    const T *pass = reinterpret_cast<const T *>(f.pass) + f.pass_off;
-    const T *src = reinterpret_cast<const T *>(f.src) + f.src_off;
-    const bool concat = f.mode == SHPL_OUT_CONCAT, add = f.mode == SHPL_OUT_ADD;
-    const uint32_t oc0 = concat ? f.cpass : 0u;
-    for (uint32_t pc0 = 0; pc0 < f.cpool; pc0 += G) {
-        const uint32_t pc = pc0 + lg;
-        if (pc >= f.cpool) break;
-        float acc[VEC];
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) acc[j] = 0.0f;
-        for (int32_t j0 = first; j0 < end; j0 += ROWS_WALK) {
-            typename C::raw_t raw[ROWS_WALK];
-#pragma unroll
-            for (int u = 0; u < ROWS_WALK; ++u)
-                if (j0 + u < end) raw[u] = C::load(src + ((int64_t)src_l[j0 + u] * f.src_stride + (int64_t)pc * VEC));
-#pragma unroll
-            for (int u = 0; u < ROWS_WALK; ++u) {
-                if (j0 + u >= end) continue;
-                float x[VEC];
-                C::to_f32(raw[u], x);
-                fma_free_accumulate<VEC>(acc, val_l[j0 + u], x);
-            }
-        }
-        if (add) {
-            // pass + pooled (pass + 0.0f for an empty row: k_dense's -0 -> +0)
-            float a[VEC];
-            C::to_f32(pc0 == 0 ? av : C::load(pass + (row * f.pass_stride + (int64_t)pc * VEC)), a);
-#pragma unroll
-            for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(a[j], acc[j]);
-        } else if (end == first) {
-            C::store_nt(out + (row * f.out_stride + (int64_t)(oc0 + pc) * VEC), C::zero());
-            continue;
-        }
-        C::store_nt(out + (row * f.out_stride + (int64_t)(oc0 + pc) * VEC), C::from_f32(acc));
-    }
 }
 
+// Two row-keyed pulls in ONE launch (shpl_pull_pair): blocks [0, blocks0) run the first pull (no per-column
+// partials: the cell-keyed one), the rest the second (with them: the pixel-keyed one) -- k_rows each.
+struct RowsSide {
+    Feat f;
+    Ents e;
+    const int32_t *key_range;
+    int64_t n_rows, blocks;
+};
+
 template <typename T, int VEC, int G>
-__global__ __launch_bounds__(BP_BLOCK) void k_bpull(const BpIn in, const BpSide s0, const BpSide s1) {
-    typedef Chunk<T, VEC> C;
-    constexpr int RPW = SHPL_WAVE / G, SUB = (BP_BLOCK / SHPL_WAVE) * RPW;
-    __shared__ uint32_t s_list[BP_CAP], s_srt[BP_CAP];
-    __shared__ int32_t s_src[BP_CAP];
-    __shared__ float s_val[BP_CAP];
-    __shared__ int32_t s_cnt[SUB], s_beg[SUB + 1], s_scan[2];
-    __shared__ int32_t s_n, s_below;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#if SHPL_BPULL_XCD
-    const int64_t b0 = xcd_block(blockIdx.x, gridDim.x);
-#else
-    const int64_t b0 = blockIdx.x;
-#endif
-    const bool second = b0 >= s0.blocks;
-    const BpSide &sd = second ? s1 : s0;
-    const Feat &f = sd.f;
-    const int64_t b = second ? b0 - s0.blocks : b0;
-    const int per_frame = sd.nr * sd.subs;
-    const int fr = (int)(b / per_frame);
-    const int rem = (int)(b - (int64_t)fr * per_frame);
-    const int q = rem / sd.subs, part = rem - q * sd.subs;
-    const int t_lo = part * SUB;                    // first range-local destination of the part
-    const int64_t k0 = (int64_t)q * BK_KEYS + t_lo; // first frame-local destination
-    const int nk = (int)((sd.kpf - k0) < SUB ? (sd.kpf - k0) : SUB);
-    if (nk <= 0) return;  // the last range's unused parts (uniform)
-    // A. this lane's row: pass-through copy (CONCAT) / first ADD operand, issued first
-    const int t = wid * RPW + lane / G, lg = lane & (G - 1);
-    const bool live = t < nk;
-    const int64_t row = (int64_t)fr * sd.kpf + k0 + t;
-    const T *pass = reinterpret_cast<const T *>(f.pass) + f.pass_off;
-    typename C::raw_t av;
-    if (live && f.mode == SHPL_OUT_ADD && (uint32_t)lg < f.cpool)
-        av = C::load(pass + (row * f.pass_stride + (int64_t)lg * VEC));
-    if (live && f.mode == SHPL_OUT_CONCAT)
-        for (uint32_t c = lg; c < f.cpass; c += G)
-            C::store_nt(reinterpret_cast<T *>(f.out) + (row * f.out_stride + (int64_t)c * VEC),
-                        C::load_nt(pass + (row * f.pass_stride + (int64_t)c * VEC)));
-    // B. the part's entries from the bucket
-    const int64_t p0 = in.frame_off[fr], capf = in.frame_off[fr + 1] - p0;
-    int64_t nnz = in.frame_nnz[fr];
-    nnz = nnz < 0 ? 0 : (nnz > capf ? capf : nnz);
-    if (threadIdx.x < SUB) s_cnt[threadIdx.x] = 0;
-    if (threadIdx.x == 0) {
-        s_n = 0;
-        s_below = 0;
-    }
-    __syncthreads();
-    int32_t start = 0, n = 0;
-    const uint32_t *W = nullptr;
-    if (nnz >= 2) {
-        const int32_t *x = in.ext + (((int64_t)sd.key * in.n_frames + fr) * in.nrmax + q) * 2;
-        start = x[0];
-        n = x[1];
-        W = in.words + (int64_t)sd.key * in.nnz_cap + p0 + start;
-        int32_t below = 0;
-        for (int32_t i0 = threadIdx.x; i0 < n; i0 += BP_BLOCK * BP_LOAD) {
-            uint32_t w[BP_LOAD];
-#pragma unroll
-            for (int u = 0; u < BP_LOAD; ++u) {
-                const int32_t i = i0 + u * BP_BLOCK;
-                w[u] = i < n ? W[i] : 0xffffffffu;
-            }
-#pragma unroll
-            for (int u = 0; u < BP_LOAD; ++u) {
-                const int tl = (int)(w[u] >> 24);  // 255: past the bucket
-                below += (tl < t_lo) ? 1 : 0;
-                const bool mine = tl >= t_lo && tl - t_lo < nk;
-                const uint64_t m = __ballot(mine);
-                if (m == 0) continue;  // wave-uniform
-                int32_t base = 0;
-                if (lane == 0) base = atomicAdd(&s_n, (int32_t)__popcll(m));
-                base = __shfl(base, 0, 64);
-                if (!mine) continue;
-                const int32_t slot = base + (int32_t)lane_rank(m);
-                if (slot < BP_CAP) s_list[slot] = w[u];
-                atomicAdd(&s_cnt[tl - t_lo], 1);
-            }
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) below += __shfl_xor(below, o, 64);
-        if (lane == 0 && below) atomicAdd(&s_below, below);
-    } else if (nnz == 1 && threadIdx.x == 0) {
-        // no bucket (see Bkt): the frame's one entry, from the index arrays
-        const int32_t c = in.cell[p0], p = in.pix[p0];
-        if (c >= 0 && p >= 0) {
-            const int64_t key = sd.key ? p - (int64_t)fr * in.kpf[1] : c - (int64_t)fr * in.kpf[0];
-            const int64_t tt = key - k0;
-            if (tt >= 0 && tt < nk) {
-                s_list[0] = ((uint32_t)(key % BK_KEYS) << 24);
-                s_cnt[tt] = 1;
-                s_n = 1;
-            }
-        }
-    }
-    __syncthreads();
-    const int32_t total = s_n;
-    // C. destinations' starts (SUB <= 128 counts: the first two waves), then placement and ranks
-    int32_t v = 0, x = 0;
-    if (threadIdx.x < 128) {
-        v = (int)threadIdx.x < SUB ? s_cnt[threadIdx.x] : 0;
-        x = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) s_scan[wid] = x;
-    }
-    __syncthreads();
-    if ((int)threadIdx.x < SUB) {
-        const int32_t incl = x + (wid == 1 ? s_scan[0] : 0);
-        s_beg[threadIdx.x] = incl - v;
-        s_cnt[threadIdx.x] = incl - v;  // placement cursor
-        if ((int)threadIdx.x == SUB - 1) s_beg[SUB] = incl;
-    }
-    __syncthreads();
-    const bool over = total > BP_CAP;
-    const int64_t R = (int64_t)sd.key * in.nnz_cap + p0 + start + s_below;  // the part's scratch stretch
-    if (!over) {
-        for (int32_t i = threadIdx.x; i < total; i += BP_BLOCK) {
-            const uint32_t w = s_list[i];
-            s_srt[atomicAdd(&s_cnt[(int)(w >> 24) - t_lo], 1)] = w;
-        }
-        __syncthreads();
-        for (int32_t i = threadIdx.x; i < total; i += BP_BLOCK) {
-            const uint32_t w = s_srt[i];
-            const int tl = (int)(w >> 24) - t_lo;
-            const int32_t a = s_beg[tl], z = s_beg[tl + 1];
-            int32_t rank = 0;
-            for (int32_t y = a; y < z; ++y) rank += s_srt[y] < w ? 1 : 0;
-            const int64_t e = p0 + (w & 0xffffffu);
-            s_src[a + rank] = sd.key ? in.cell[e] : in.pix[e];
-            s_val[a + rank] = in.val[e];
-        }
-        __syncthreads();
-        bp_rows<T, VEC, G>(f, row, live, live ? s_beg[t] : 0, live ? s_beg[t + 1] : 0, s_src, s_val, av);
-        return;
-    }
-    // the same sort through the workspace scratch
-    uint32_t *sw = in.swords + R;
-    for (int32_t i0 = threadIdx.x; i0 < n; i0 += BP_BLOCK) {
-        const uint32_t w = W[i0];
-        const int tl = (int)(w >> 24) - t_lo;
-        if (tl >= 0 && tl < nk) sw[atomicAdd(&s_cnt[tl], 1)] = w;
-    }
-    block_publish();
-    for (int32_t i = threadIdx.x; i < total; i += BP_BLOCK) {
-        const uint32_t w = sw[i];
-        const int tl = (int)(w >> 24) - t_lo;
-        const int32_t a = s_beg[tl], z = s_beg[tl + 1];
-        int32_t rank = 0;
-        for (int32_t y = a; y < z; ++y) rank += sw[y] < w ? 1 : 0;
-        const int64_t e = p0 + (w & 0xffffffu);
-        in.ssrc[R + a + rank] = sd.key ? in.cell[e] : in.pix[e];
-        in.sval[R + a + rank] = in.val[e];
-    }
-    block_publish();
-    bp_rows<T, VEC, G>(f, row, live, live ? s_beg[t] : 0, live ? s_beg[t + 1] : 0,
-                       static_cast<const int32_t *>(in.ssrc + R), static_cast<const float *>(in.sval + R), av);
+__global__ __launch_bounds__(SHPL_BLOCK) void k_rows2(const RowsSide s0, const RowsSide s1) {
+    if ((int64_t)blockIdx.x < s0.blocks)
+        rows_body<T, VEC, false, G>(s0.f, s0.e, s0.key_range, s0.n_rows, blockIdx.x);
+    else
+        rows_body<T, VEC, true, G>(s1.f, s1.e, s1.key_range, s1.n_rows, (int64_t)blockIdx.x - s0.blocks);
 }
 
 bool aligned(const void *ptr, int64_t a) { return ((uintptr_t)ptr) % (uintptr_t)a == 0; }
@@ -1103,36 +869,25 @@ extern "C" int shpl_pull_sparse(SHPL_PULL_ARGS) {
     return sparse(pl, csr, direction, (hipStream_t)stream);
 }
 
-// ---------------------------------------------------------------- bucketed pulls
+// ---------------------------------------------------------------- paired pulls
 namespace shpl {
 namespace {
 
-int bp_side(const shpl_buckets *bk, const shpl_pull_desc *d, int key, int64_t nr, Plan *pl) {
-    shpl_csr c = {};
-    c.n_keys = (int64_t)bk->n_frames * (key ? bk->pix_per_frame : bk->cells_per_frame);
-    return plan(key ? SHPL_BY_PIXEL : SHPL_BY_CELL, d->dtype, &c, d->src, d->src_stride, d->src_off, d->c_pool,
-                d->pass, d->pass_stride, d->pass_off, d->c_pass, d->mode, d->out, d->out_stride, pl);
-}
-
 template <typename T, int VEC>
-int bpull_t(const BpIn &in, BpSide s[2], int G, hipStream_t st) {
-    constexpr int rows16 = BP_BLOCK / SHPL_WAVE;  // rows of a part = 16 waves x 64/G
-    for (int k = 0; k < 2; ++k) {
-        s[k].subs = BK_KEYS / (rows16 * (SHPL_WAVE / G));
-        s[k].blocks = s[k].blocks ? (int64_t)in.n_frames * s[k].nr * s[k].subs : 0;
-    }
+int pair_t(RowsSide s[2], int G, hipStream_t st) {
+    for (int k = 0; k < 2; ++k)
+        if (s[k].n_rows > 0) s[k].blocks = (s[k].n_rows + SHPL_BLOCK / G - 1) / (SHPL_BLOCK / G);
     const int64_t blocks = s[0].blocks + s[1].blocks;
     if (blocks == 0) return SHPL_OK;
     if (blocks > 0x7fffffffLL) return SHPL_ERR_BAD_SHAPE;
-#define SHPL_BPULL(GG) \
-    hipLaunchKernelGGL((k_bpull<T, VEC, GG>), dim3((unsigned)blocks), dim3(BP_BLOCK), 0, st, in, s[0], s[1])
+#define SHPL_ROWS2(GG) hipLaunchKernelGGL((k_rows2<T, VEC, GG>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, s[0], s[1])
     switch (G) {
-        case 8: SHPL_BPULL(8); break;
-        case 16: SHPL_BPULL(16); break;
-        case 32: SHPL_BPULL(32); break;
-        default: SHPL_BPULL(64); break;
+        case 8: SHPL_ROWS2(8); break;
+        case 16: SHPL_ROWS2(16); break;
+        case 32: SHPL_ROWS2(32); break;
+        default: SHPL_ROWS2(64); break;
     }
-#undef SHPL_BPULL
+#undef SHPL_ROWS2
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
 }
@@ -1140,45 +895,50 @@ int bpull_t(const BpIn &in, BpSide s[2], int G, hipStream_t st) {
 }  // namespace
 }  // namespace shpl
 
-extern "C" int shpl_pull_buckets(const shpl_buckets *bk, const shpl_pull_desc *by_cell,
-                                 const shpl_pull_desc *by_pixel, void *stream) {
-    if (!bk || bk->n_frames < 1 || !bk->frame_off || !bk->frame_nnz || !bk->ws) return SHPL_ERR_ARG;
-    if (bk->max_points_per_frame < 0 || bk->nnz_cap < 0 || bk->cells_per_frame < 0 || bk->pix_per_frame < 0)
-        return SHPL_ERR_ARG;
-    size_t need = 0;
-    int rc = shpl_bucket_workspace_bytes(bk->n_frames, bk->max_points_per_frame, bk->nnz_cap, bk->cells_per_frame,
-                                         bk->pix_per_frame, &need);
-    if (rc) return rc;
-    if (bk->ws_bytes < need) return SHPL_ERR_WORKSPACE;
-    if (bk->nnz_cap > 0 && (!bk->cell || !bk->pix || !bk->val)) return SHPL_ERR_ARG;
-    const int64_t chunks = (bk->max_points_per_frame + 1023) / 1024;
-    const BkLayout l = bk_layout(bk->n_frames, (int)(chunks < 1 ? 1 : chunks), bk->nnz_cap, bk->cells_per_frame,
-                                 bk->pix_per_frame);
-    const shpl_pull_desc *d[2] = {by_cell, by_pixel};
+extern "C" int shpl_pull_pair(const shpl_csr *by_cell, const shpl_pull_desc *d_cell, const shpl_csr *by_pixel,
+                              const shpl_pull_desc *d_pixel, void *stream) {
+    const shpl_csr *cs[2] = {by_cell, by_pixel};
+    const shpl_pull_desc *ds[2] = {d_cell, d_pixel};
+    hipStream_t st = (hipStream_t)stream;
     Plan pl[2];
-    BpSide s[2] = {};
-    int dtype = -1, v16 = -1, G = 8;
+    bool on[2] = {false, false};
     for (int k = 0; k < 2; ++k) {
-        if (!d[k]) continue;
-        rc = bp_side(bk, d[k], k, l.nr[k], &pl[k]);
+        if (!ds[k]) continue;
+        const shpl_csr *c = cs[k];
+        if (!c) return SHPL_ERR_ARG;
+        if (!c->key_range && c->nnz_cap > 0) return SHPL_ERR_ARG;  // row-keyed: the CSR must carry key_range
+        const shpl_pull_desc *d = ds[k];
+        const int rc = plan(k ? SHPL_BY_PIXEL : SHPL_BY_CELL, d->dtype, c, d->src, d->src_stride, d->src_off,
+                            d->c_pool, d->pass, d->pass_stride, d->pass_off, d->c_pass, d->mode, d->out, d->out_stride,
+                            &pl[k]);
         if (rc) return rc;
-        if (pl[k].n_dst == 0) continue;
-        if (dtype >= 0 && (dtype != pl[k].dtype || v16 != (int)pl[k].v16)) return SHPL_ERR_BAD_SHAPE;
+        on[k] = pl[k].n_dst > 0;
+        if (on[k] && c->nnz_cap == 0) {  // an empty map: the streaming pass is the whole pull
+            const int r2 = dense(pl[k], st);
+            if (r2) return r2;
+            on[k] = false;
+        }
+    }
+    if (on[0] && on[1] && (pl[0].dtype != pl[1].dtype || pl[0].v16 != pl[1].v16)) {
+        // one template per launch: two launches (shpl_pull's row-keyed form each)
+        for (int k = 0; k < 2; ++k) {
+            const int rc = rows(pl[k], cs[k], k ? SHPL_BY_PIXEL : SHPL_BY_CELL, st);
+            if (rc) return rc;
+        }
+        return SHPL_OK;
+    }
+    RowsSide s[2] = {};
+    int dtype = -1, v16 = 0, G = 8;
+    for (int k = 0; k < 2; ++k) {
+        if (!on[k]) continue;
+        const shpl_csr *c = cs[k];
         dtype = pl[k].dtype;
         v16 = pl[k].v16;
         while (G < 64 && (uint32_t)G < pl[k].f.cpool) G <<= 1;  // lanes per row: the widest pooled row
-        s[k].f = pl[k].f;
-        s[k].key = k;
-        s[k].nr = l.nr[k];
-        s[k].kpf = l.kpf[k];
-        s[k].blocks = 1;  // marks the side as present; bpull_t sizes it
+        s[k] = RowsSide{pl[k].f, Ents{c->nnz_cap, c->ent_dst, c->ent_src, c->ent_col, c->ent_val}, c->key_range,
+                        pl[k].n_dst, 0};
     }
     if (dtype < 0) return SHPL_OK;
-    char *w = (char *)bk->ws;
-    const BpIn in{bk->frame_off, bk->frame_nnz, bk->cell, bk->pix, bk->val, (const int32_t *)(w + l.ext),
-                  (const uint32_t *)(w + l.words), (uint32_t *)(w + l.swords), (int32_t *)(w + l.ssrc),
-                  (float *)(w + l.sval), bk->n_frames, l.nrmax, bk->nnz_cap, {l.kpf[0], l.kpf[1]}};
-    hipStream_t st = (hipStream_t)stream;
-    if (dtype == SHPL_F32) return v16 ? bpull_t<float, 4>(in, s, G, st) : bpull_t<float, 1>(in, s, G, st);
-    return v16 ? bpull_t<uint16_t, 8>(in, s, G, st) : bpull_t<uint16_t, 1>(in, s, G, st);
+    if (dtype == SHPL_F32) return v16 ? pair_t<float, 4>(s, G, st) : pair_t<float, 1>(s, G, st);
+    return v16 ? pair_t<uint16_t, 8>(s, G, st) : pair_t<uint16_t, 1>(s, G, st);
 }

@@ -34,9 +34,10 @@ class FusedPipeline:
         whole capacity -- for capacities far above the entry counts (FramePipeline: raw-scan slots per
         voxel point); at config 2 (capacity = entries) the capacity walk is faster (2.22 vs 2.24 ms).
         buckets (default: with rows): the index build also cuts M into destination buckets
-        (shpl_build_index_buckets) and both pulls of a step run as ONE launch over them
-        (shpl_pull_buckets) on one stream -- no CSR launch, no cross-stream waits; rows without
-        buckets: the range CSRs + one k_rows launch per pull."""
+        (shpl_build_index_buckets), one launch sorts both CSRs out of them (shpl_build_csr_buckets) and
+        each pull pair is one row-keyed launch (shpl_pull_pair), all on one stream; the forward's
+        pass-through halves are copied on the side stream beside the index chain. rows without
+        buckets: the range CSRs (one launch per key) + one k_rows launch per pull, on two streams."""
         dev = torch.device(device)
         self.dev, self.dtype, self.dual = dev, dtype, dual
         self.B = int(n_frames)
@@ -115,9 +116,12 @@ class FusedPipeline:
     csr_path = L.CSR_AUTO
 
     def build_csr(self, which=("cell", "pixel")):
-        if self.buckets:
-            return  # the buckets came with the index build
         st = L.stream_of(self.dev)
+        if self.buckets:  # both CSRs from the index build's buckets, one launch
+            L.check(self._lib.shpl_build_csr_buckets(
+                ctypes.byref(self.bkt), self.csr.ref() if "cell" in which else None,
+                self.pcsr.ref() if self.dual and "pixel" in which else None, st), "shpl_build_csr_buckets")
+            return
         args = (self.B, L.ptr(self.frame_off), L.ptr(self.frame_nnz))
         if "cell" in which:
             L.check(self._lib.shpl_build_csr_path(
@@ -158,20 +162,47 @@ class FusedPipeline:
         return (direction, L.dtype_code(out), csr.ref(), L.ptr(src), cs, 0, cs, L.ptr(pass_), cp, 0, cp,
                 L.OUT_CONCAT, L.ptr(out), cs + cp)
 
-    def _pull_buckets(self, cell_desc, pix_desc):
-        L.check(self._lib.shpl_pull_buckets(ctypes.byref(self.bkt), ctypes.byref(cell_desc) if cell_desc else None,
-                                            ctypes.byref(pix_desc) if pix_desc else None,
-                                            L.stream_of(self.dev)), "shpl_pull_buckets")
+    def _pull_pair(self, cell_desc, pix_desc):
+        L.check(self._lib.shpl_pull_pair(self.csr.ref(), ctypes.byref(cell_desc) if cell_desc else None,
+                                         self.pcsr.ref() if self.dual else None,
+                                         ctypes.byref(pix_desc) if pix_desc else None,
+                                         L.stream_of(self.dev)), "shpl_pull_pair")
+
+    def _pass_copies(self, bev, img, which=("cell", "pixel")):
+        """The forward's pass-through halves alone (shpl_pull_dense over no pooled channels): bv_fused[..., :Cb]
+        = bev, img_fused[..., :Ci] = img; they need no index."""
+        st = L.stream_of(self.dev)
+        dt = L.dtype_code(self.bv_fused)
+        if "cell" in which:
+            L.check(self._lib.shpl_pull_dense(L.BY_CELL, dt, self.csr.ref(), None, 0, 0, 0, L.ptr(bev), self.Cb, 0,
+                                              self.Cb, L.OUT_CONCAT, L.ptr(self.bv_fused), self.Cb + self.Ci, st),
+                    "shpl_pull_dense")
+        if self.dual and "pixel" in which:
+            L.check(self._lib.shpl_pull_dense(L.BY_PIXEL, dt, self.pcsr.ref(), None, 0, 0, 0, L.ptr(img), self.Ci, 0,
+                                              self.Ci, L.OUT_CONCAT, L.ptr(self.img_fused), self.Ci + self.Cb, st),
+                    "shpl_pull_dense")
+
+    def _pooled_descs(self, bev, img, which=("cell", "pixel")):
+        """The forward pair's pooled halves (SHPL_OUT_POOL into the output rows' pooled columns)."""
+        dt = L.dtype_code(self.bv_fused)
+        esz = self.bv_fused.element_size()
+        cell = pix = None
+        if "cell" in which:
+            cell = L.pull_desc(dt, img, self.Ci, 0, self.Ci, None, 0, 0, 0, L.OUT_POOL, self.bv_fused,
+                               self.Cb + self.Ci)
+            cell.out += self.Cb * esz
+        if self.dual and "pixel" in which:
+            pix = L.pull_desc(dt, bev, self.Cb, 0, self.Cb, None, 0, 0, 0, L.OUT_POOL, self.img_fused,
+                              self.Ci + self.Cb)
+            pix.out += self.Ci * esz
+        return cell, pix
 
     def layer_sparse(self, bev, img, which=("cell", "pixel")):
-        """Pooled rows, after layer_dense and build_csr (with buckets: both pulls, one launch)."""
+        """Pooled rows, after layer_dense and build_csr (with buckets: the pass-through halves and
+        then both pooled halves in one launch)."""
         if self.buckets:
-            dt = L.dtype_code(self.bv_fused)
-            cell = L.pull_desc(dt, img, self.Ci, 0, self.Ci, bev, self.Cb, 0, self.Cb, L.OUT_CONCAT, self.bv_fused,
-                               self.Cb + self.Ci) if "cell" in which else None
-            pix = L.pull_desc(dt, bev, self.Cb, 0, self.Cb, img, self.Ci, 0, self.Ci, L.OUT_CONCAT, self.img_fused,
-                              self.Ci + self.Cb) if self.dual and "pixel" in which else None
-            self._pull_buckets(cell, pix)
+            self._pass_copies(bev, img, which)
+            self._pull_pair(*self._pooled_descs(bev, img, which))
             return
         if "cell" in which:
             self._sparse(self._concat_args(self.csr, L.BY_CELL, img, self.Ci, bev, self.Cb, self.bv_fused))
@@ -196,16 +227,24 @@ class FusedPipeline:
         beside the cell-keyed ones (they share only M).
         `events` (4 timing events) bracket the dense and the sparse launches."""
         if self.buckets:
-            # one stream: index + buckets (2 launches), both pulls (1 launch); no side-stream waits
-            if events:
-                events[0].record()
-                events[1].record()
+            # index + buckets (2 launches), both CSRs (1 launch), both pooled halves (1 launch) on the current
+            # stream; the pass-through halves on `side` beside them (no index needed; disjoint columns)
+            main = torch.cuda.current_stream(self.dev)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                if events:
+                    events[0].record(side)
+                self._pass_copies(bev, img)
+                if events:
+                    events[1].record(side)
             self.build_index(points, voxels, point_offsets, P, mval)
+            self.build_csr()
             if events:
-                events[2].record()
-            self.layer_sparse(bev, img)
+                events[2].record(main)
+            self._pull_pair(*self._pooled_descs(bev, img))
             if events:
-                events[3].record()
+                events[3].record(main)
+            main.wait_stream(side)
             return
         main = torch.cuda.current_stream(self.dev)
         side.wait_stream(main)            # inputs / previous step done
@@ -327,11 +366,11 @@ class FusedPipeline:
         main = torch.cuda.current_stream(self.dev)
         w = self.Cb + self.Ci
         dt = L.dtype_code(d_bev)
-        if self.buckets:
-            self._pull_buckets(L.pull_desc(dt, g_img, w, self.Ci, self.Cb, g_bv, w, 0, self.Cb, L.OUT_ADD, d_bev,
-                                           self.Cb),
-                               L.pull_desc(dt, g_bv, w, self.Cb, self.Ci, g_img, w, 0, self.Ci, L.OUT_ADD, d_img,
-                                           self.Ci))
+        if self.buckets:  # both gradient pulls, one launch, current stream
+            self._pull_pair(L.pull_desc(dt, g_img, w, self.Ci, self.Cb, g_bv, w, 0, self.Cb, L.OUT_ADD, d_bev,
+                                        self.Cb),
+                            L.pull_desc(dt, g_bv, w, self.Cb, self.Ci, g_img, w, 0, self.Ci, L.OUT_ADD, d_img,
+                                        self.Ci))
             return
         cell = (L.BY_CELL, dt, self.csr.ref(), L.ptr(g_img), w, self.Ci, self.Cb, L.ptr(g_bv), w, 0, self.Cb,
                 L.OUT_ADD, L.ptr(d_bev), self.Cb)

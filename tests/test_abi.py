@@ -88,7 +88,8 @@ def test_argument_validation_is_host_side():
         assert fn(L.BY_CELL, L.F32, ctypes.byref(csr), P, 32, 0, 32, N, 32, 0, 32, L.OUT_CONCAT, P, 64,
                   N) == L.ERR_ARG
     # buckets: shapes over the limits (65536 destinations per frame, 2^24 points per frame), workspace size,
-    # missing bucket workspace; pull pair: null map, mixed dtypes, the bad-shape checks of shpl_pull
+    # missing bucket workspace; CSRs from buckets: null map, no ent_col for the pixel key, too few keys, small
+    # workspace; pull pair: null CSR, the bad-shape checks of shpl_pull, no key_range
     nb = ctypes.c_size_t()
     assert lib.shpl_bucket_workspace_bytes(4, 20000, 80000, 8800, 6750, ctypes.byref(nb)) == L.OK and nb.value > 0
     assert lib.shpl_bucket_workspace_bytes(4, 20000, 80000, 70000, 6750, ctypes.byref(nb)) == L.ERR_BAD_SHAPE
@@ -99,14 +100,20 @@ def test_argument_validation_is_host_side():
     assert lib.shpl_build_index_buckets(*args, P, 64, N) == L.ERR_WORKSPACE
     assert lib.shpl_build_index_buckets(*args[:14], 1., 1., *args[16:], P, 1 << 24, N) == L.ERR_BAD_SHAPE
     bk = L.ShplBuckets(4, 20000, 80000, 8800, 6750, 256, 256, 256, 256, 256, 256, nb.value)
-    d32 = L.ShplPullDesc(L.F32, 256, 32, 0, 32, 256, 32, 0, 32, L.OUT_CONCAT, 256, 64)
-    d16 = L.ShplPullDesc(L.BF16, 256, 32, 0, 32, 256, 32, 0, 32, L.OUT_CONCAT, 256, 64)
-    assert lib.shpl_pull_buckets(None, ctypes.byref(d32), None, N) == L.ERR_ARG
-    assert lib.shpl_pull_buckets(ctypes.byref(bk), ctypes.byref(d32), ctypes.byref(d16), N) == L.ERR_BAD_SHAPE
-    narrow = L.ShplPullDesc(L.F32, 256, 32, 0, 32, 256, 32, 0, 32, L.OUT_CONCAT, 256, 48)
-    assert lib.shpl_pull_buckets(ctypes.byref(bk), ctypes.byref(narrow), None, N) == L.ERR_BAD_SHAPE
+    ccell = L.ShplCsr(256, 256, 256, None, 4 * 8800, 80000, 256)
+    cpix = L.ShplCsr(256, 256, 256, None, 4 * 6750, 80000, 256)  # no ent_col
+    assert lib.shpl_build_csr_buckets(None, ctypes.byref(ccell), None, N) == L.ERR_ARG
+    assert lib.shpl_build_csr_buckets(ctypes.byref(bk), ctypes.byref(ccell), ctypes.byref(cpix), N) == L.ERR_ARG
+    few = L.ShplCsr(256, 256, 256, None, 100, 80000, 256)  # fewer keys than frames x cells
+    assert lib.shpl_build_csr_buckets(ctypes.byref(bk), ctypes.byref(few), None, N) == L.ERR_BAD_SHAPE
     small = L.ShplBuckets(4, 20000, 80000, 8800, 6750, 256, 256, 256, 256, 256, 256, 64)
-    assert lib.shpl_pull_buckets(ctypes.byref(small), ctypes.byref(d32), None, N) == L.ERR_WORKSPACE
+    assert lib.shpl_build_csr_buckets(ctypes.byref(small), ctypes.byref(ccell), None, N) == L.ERR_WORKSPACE
+    d32 = L.ShplPullDesc(L.F32, 256, 32, 0, 32, 256, 32, 0, 32, L.OUT_CONCAT, 256, 64)
+    narrow = L.ShplPullDesc(L.F32, 256, 32, 0, 32, 256, 32, 0, 32, L.OUT_CONCAT, 256, 48)
+    assert lib.shpl_pull_pair(None, ctypes.byref(d32), None, None, N) == L.ERR_ARG
+    assert lib.shpl_pull_pair(ctypes.byref(ccell), ctypes.byref(narrow), None, None, N) == L.ERR_BAD_SHAPE
+    norange = L.ShplCsr(256, 256, 256, None, 4 * 8800, 80000)  # row-keyed pulls need key_range
+    assert lib.shpl_pull_pair(ctypes.byref(norange), ctypes.byref(d32), None, None, N) == L.ERR_ARG
     # velodyne loader: P2 without image size, misaligned scan
     assert lib.shpl_velo_to_cam(1, P, 10, P, P, P, N, math.nan, N, P, P, N, P, 1 << 20, N) == L.ERR_ARG
     assert lib.shpl_velo_to_cam(1, P, 10, ctypes.c_void_p(260), P, N, N, math.nan, N, P, P, N, P, 1 << 20,

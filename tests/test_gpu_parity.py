@@ -632,8 +632,9 @@ def _ragged_frames(base, sizes, seed):
 def _ragged_pipeline_run(cfg, sizes, dtype, paths, channels=None, frames=None):
     """FusedPipeline forward + backward over a ragged batch, once per CSR path
     (shpl_build_csr_path: frame / segment / range; None = the default; "buckets": the
-    index build's destination buckets and the one-launch pull pair, shpl_pull_buckets;
-    "csr_rows": range CSRs + k_rows), each compared with the oracle frame by frame
+    index build's destination buckets, both CSRs in one launch (shpl_build_csr_buckets) and
+    the one-launch pull pairs (shpl_pull_pair); "csr_rows": range CSRs + k_rows), each
+    compared with the oracle frame by frame
     (f32: bitwise; bf16: bitwise on the bf16 bits). channels: (Cb, Ci) instead of the config's."""
     from sparse_pooling_amd import _lib as L
     from sparse_pooling_amd import pipeline
@@ -677,10 +678,13 @@ def _ragged_pipeline_run(cfg, sizes, dtype, paths, channels=None, frames=None):
     codes = {None: L.CSR_AUTO, "frame": L.CSR_FRAME, "segment": L.CSR_SEGMENT, "range": L.CSR_RANGE,
              "bucket": L.CSR_BUCKET}
     for path in paths:
-        kw = {"buckets": dict(rows=True, buckets=True), "csr_rows": dict(rows=True, buckets=False)}.get(path, {})
+        # a named CSR builder: the CSR pulls (no buckets); None: the pipeline's default
+        kw = {"buckets": dict(rows=True, buckets=True), "csr_rows": dict(rows=True, buckets=False),
+              None: {}}.get(path, dict(buckets=False))
         pl = pipeline.FusedPipeline(B, maxp, N, base.im_size, base.bv_size, base.stride, Cb, Ci, dtype=tdt,
                                     dual=True, **kw)
-        assert pl.buckets == (path == "buckets")
+        if path is not None:
+            assert pl.buckets == (path == "buckets")
         pl.csr_path = codes.get(path, L.CSR_AUTO)
         d_bev, d_img = torch.empty_like(tb), torch.empty_like(ti)
         pl.step(pts, vox, off, P, tb, ti)
@@ -698,21 +702,22 @@ def _ragged_pipeline_run(cfg, sizes, dtype, paths, channels=None, frames=None):
 
 
 @pytest.mark.parametrize("dtype,cb,ci", [("bf16", 256, 256), ("f32", 256, 256), ("f32", 16, 32), ("bf16", 64, 64),
-                                         ("f32", 3, 5), ("bf16", 8, 24), ("f32", 64, 128)])
+                                         ("f32", 3, 5), ("bf16", 8, 24), ("f32", 64, 128), ("f32", 4, 6)])
 def test_bucket_pulls_ragged_batch(dtype, cb, ci):
-    """The bucketed step (shpl_build_index_buckets -> shpl_pull_buckets: both pulls in one
-    launch, forward then gradients) at config 3's geometry over a ragged batch -- no points,
+    """The bucketed step (shpl_build_index_buckets -> shpl_build_csr_buckets -> shpl_pull_pair:
+    both CSRs in one launch, both pulls in one launch, forward then gradients) at config 3's
+    geometry over a ragged batch -- no points,
     one point, no survivor, one survivor among 14 points (the dgemv projection order: no
     bucket, the entry read from the index arrays), chunk-straddling and full frames --
     bitwise against the oracle and against the range CSR + k_rows path, for every lane
-    group width (G = 8 .. 64) and the unvectorised form (3 / 5 f32 channels)."""
+    group width (G = 8 .. 64) and the unvectorised form (3 / 5 and 4 / 6 f32 channels)."""
     _ragged_pipeline_run(3, [0, 1, -40, 1025, 20000, 2], dtype, ["buckets", "csr_rows"], channels=(cb, ci))
 
 
-def test_bucket_pulls_overflowing_part():
-    """One frame whose 3000 points are one point repeated (one cell, one pixel: a part far over
-    the pull's 2048-entry LDS sort, which then sorts through the workspace scratch) beside
-    ordinary frames: bitwise against the oracle, f32 and bf16."""
+def test_bucket_pulls_long_runs():
+    """One frame whose 3000 points are one point repeated (one cell, one pixel: one bucket, one
+    run of 3000 entries, sorted in 12 rounds) beside a frame with half its points on one cell:
+    bitwise against the oracle, f32 and bf16."""
     base = synth.CONFIGS[3]
     rng = np.random.default_rng(9)
     one = synth.make_frame(synth.FrameSpec(1, base.im_size, base.bv_size, base.stride, 32, 32), seed=3)
@@ -738,8 +743,8 @@ def test_pipeline_ragged_batch_every_csr_path():
 
 
 def test_pipeline_ragged_batch_row_keyed_bf16():
-    """The same ragged batch at config-3 shape (bf16, 256 channels, row-keyed
-    pulls over key_range CSRs), bitwise on the bf16 bits."""
+    """The same ragged batch at config-3 shape (bf16, 256 channels): the default
+    (bucketed pulls) and the row-keyed pulls over key_range CSRs, bitwise on the bf16 bits."""
     _ragged_pipeline_run(3, [0, 1, -40, 1025, 20000, 2], "bf16", [None, "range"])
 
 
