@@ -390,6 +390,22 @@ int shpl_pull_sparse(int direction, int dtype, const shpl_csr *csr, const void *
  * per frame, max_points_per_frame below 2^24.
  * Replaces what shpl_build_index + two shpl_build_csr calls feed the pulls
  * (kitti_dataset.py:374-379, then rpn_model.py:330-331's SparseTensor). */
+/* Optional riders of shpl_build_index_buckets: the concat's pass-through half
+ * of a forward pull, which needs no index -- out row r, channels [0,
+ * channels) = src row r (rows: the BEV cells for cell_copy, the pixels for
+ * pixel_copy, all frames). Extra workgroups of the two index launches do the
+ * copies beside the latency-bound index work (one stream, no fork). Rows and
+ * strides 16-byte aligned, channels * element size a multiple of 16
+ * (SHPL_ERR_BAD_SHAPE otherwise). Strides in elements. */
+typedef struct {
+    int dtype;
+    const void *src;
+    int64_t src_stride;
+    void *out;
+    int64_t out_stride;
+    int64_t channels;
+} shpl_pass_copy;
+
 int shpl_bucket_workspace_bytes(int n_frames, int64_t max_points_per_frame, int64_t nnz_cap,
                                 int64_t cells_per_frame, int64_t pix_per_frame, size_t *bytes);
 int shpl_build_index_buckets(int n_frames, const int64_t *d_point_offsets, const int64_t *d_point_counts,
@@ -398,7 +414,8 @@ int shpl_build_index_buckets(int n_frames, const int64_t *d_point_offsets, const
                              double im_w, double im_h, double bv_h, double bv_w, double s_img, double s_bv,
                              const float *d_mval, int32_t *d_cell, int32_t *d_pix, float *d_val,
                              int64_t *d_frame_nnz, int64_t *d_frame_out_off, uint32_t *d_err, void *d_ws,
-                             size_t ws_bytes, int64_t nnz_cap, void *d_bkt, size_t bkt_bytes, void *stream);
+                             size_t ws_bytes, int64_t nnz_cap, void *d_bkt, size_t bkt_bytes,
+                             const shpl_pass_copy *cell_copy, const shpl_pass_copy *pixel_copy, void *stream);
 
 /* The map shpl_build_index_buckets left: its frame layout, index arrays and
  * bucket workspace (the same sizes as that call). */

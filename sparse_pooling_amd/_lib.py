@@ -96,6 +96,12 @@ class ShplPullDesc(ctypes.Structure):
                 ("mode", ctypes.c_int), ("out", ctypes.c_void_p), ("out_stride", ctypes.c_int64)]
 
 
+class ShplPassCopy(ctypes.Structure):
+    """struct shpl_pass_copy of include/shpl.h (a rider of shpl_build_index_buckets)."""
+    _fields_ = [("dtype", ctypes.c_int), ("src", ctypes.c_void_p), ("src_stride", ctypes.c_int64),
+                ("out", ctypes.c_void_p), ("out_stride", ctypes.c_int64), ("channels", ctypes.c_int64)]
+
+
 def pull_desc(dtype, src, src_stride, src_off, c_pool, pass_, pass_stride, pass_off, c_pass, mode, out, out_stride):
     """A ShplPullDesc from tensors (the same argument order as shpl_pull after its csr)."""
     p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
@@ -134,7 +140,8 @@ def _declare(lib):
                                       sz, p]),
         "shpl_bucket_workspace_bytes": (i32, [i32, i64, i64, i64, i64, psz]),
         "shpl_build_index_buckets": (i32, [i32, p, p, i64, p, i32, p, i32, i64, p, d, d, d, d, d, d, p,
-                                           p, p, p, p, p, p, p, sz, i64, p, sz, p]),
+                                           p, p, p, p, p, p, p, sz, i64, p, sz, ctypes.POINTER(ShplPassCopy),
+                                           ctypes.POINTER(ShplPassCopy), p]),
         "shpl_build_csr_buckets": (i32, [ctypes.POINTER(ShplBuckets), ctypes.POINTER(ShplCsr),
                                          ctypes.POINTER(ShplCsr), p]),
         "shpl_pull_pair": (i32, [ctypes.POINTER(ShplCsr), ctypes.POINTER(ShplPullDesc), ctypes.POINTER(ShplCsr),

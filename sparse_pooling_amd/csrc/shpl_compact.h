@@ -60,13 +60,52 @@ struct Frames {
 // Frames of at most one entry get no bucket (the pull reads that entry from
 // the index arrays): only there may the second projection's column count
 // (dgemv order) differ from the count k_count assumed.
+// A rider of the bucketed launches (optional): extra workgroups of each launch
+// copy row bytes [0, row_bytes) of frame f's rows_per_frame rows from src to
+// out (16-byte pieces, nontemporal) -- the concat's pass-through halves, which
+// need no index: k_count copies cp[0], k_compact cp[1], so the copies ride
+// the two latency-bound launches instead of a stream of their own.
+struct PassCopy {
+    const uint8_t *src;
+    uint8_t *out;
+    int64_t src_stride, out_stride, row_bytes, rows_per_frame;  // bytes (16-byte multiples), rows
+};
+
 struct Bkt {
     int nr[2], nrmax;
     int64_t nnz_cap;
     int32_t *hist;    // [2][F][n_chunks][nrmax]
     int32_t *ext;     // [2][F][nrmax][2]
     uint32_t *words;  // [2][nnz_cap]
+    PassCopy cp[2];
+    int cp_blocks;    // rider workgroups per frame in each launch (0: none)
 };
+
+constexpr int CP_BATCH = 8;  // 16-byte pieces per thread in flight
+
+__device__ __forceinline__ void pass_copy(const PassCopy &c, int f, int b, int nb) {
+    typedef uint32_t u32x4c __attribute__((ext_vector_type(4)));
+    const int64_t per_row = c.row_bytes >> 4, total = c.rows_per_frame * per_row;
+    const int64_t r0 = (int64_t)f * c.rows_per_frame;
+    const int64_t step = (int64_t)nb * IDX_BLOCK;
+    for (int64_t i0 = (int64_t)b * IDX_BLOCK + threadIdx.x; i0 < total; i0 += step * CP_BATCH) {
+        u32x4c v[CP_BATCH];
+#pragma unroll
+        for (int u = 0; u < CP_BATCH; ++u) {
+            const int64_t i = i0 + u * step;
+            if (i >= total) continue;
+            const int64_t row = r0 + i / per_row, pc = i - (i / per_row) * per_row;
+            v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4c *>(c.src + row * c.src_stride) + pc);
+        }
+#pragma unroll
+        for (int u = 0; u < CP_BATCH; ++u) {
+            const int64_t i = i0 + u * step;
+            if (i >= total) continue;
+            const int64_t row = r0 + i / per_row, pc = i - (i / per_row) * per_row;
+            __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4c *>(c.out + row * c.out_stride) + pc);
+        }
+    }
+}
 
 __device__ __forceinline__ void frame_range(const Frames &fr, int f, int64_t &p0, int64_t &p1, int64_t &cap_end) {
     p0 = fr.pt_off[f];
@@ -82,6 +121,10 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr, Bkt bk
     __shared__ int32_t hist[BKT ? 2 * BK_MAX_RANGES : 1];
     const int f = blockIdx.y, j = blockIdx.x;
     if constexpr (BKT) {
+        if (j >= fr.n_chunks) {  // a rider workgroup (uniform)
+            pass_copy(bk.cp[0], f, j - fr.n_chunks, bk.cp_blocks);
+            return;
+        }
         for (int q = threadIdx.x; q < 2 * BK_MAX_RANGES; q += IDX_BLOCK) hist[q] = 0;
     }
     int64_t p0, p1, cap_end;
@@ -214,6 +257,12 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr, Bkt 
     __shared__ int32_t s_off[BKT ? 2 * BK_MAX_RANGES : 1], s_scan[IDX_BLOCK / 64];
     __shared__ int32_t s_w[BKT ? 2 : 1][IDX_BLOCK / 64][BKT ? BK_MAX_RANGES : 1];  // per-wave range counts
     const int f = blockIdx.y, j = blockIdx.x;
+    if constexpr (BKT) {
+        if (j >= fr.n_chunks) {  // a rider workgroup (uniform)
+            pass_copy(bk.cp[1], f, j - fr.n_chunks, bk.cp_blocks);
+            return;
+        }
+    }
     int64_t p0, p1, cap_end;
     frame_range(fr, f, p0, p1, cap_end);
     const int wid = threadIdx.x >> 6;
@@ -345,9 +394,10 @@ int run_compaction(const Stage &st, int n_frames, int64_t max_points, const int6
     const dim3 grid(fr.n_chunks, n_frames);
     if constexpr (Stage::HAS_BUCKETS) {
         if (bk) {
-            hipLaunchKernelGGL((k_count<Stage, true>), grid, dim3(IDX_BLOCK), 0, stream, st, fr, *bk);
+            const dim3 gridb(fr.n_chunks + bk->cp_blocks, n_frames);
+            hipLaunchKernelGGL((k_count<Stage, true>), gridb, dim3(IDX_BLOCK), 0, stream, st, fr, *bk);
             SHPL_LAUNCH_CHECK();
-            hipLaunchKernelGGL((k_compact<Stage, true>), grid, dim3(IDX_BLOCK), 0, stream, st, fr, *bk);
+            hipLaunchKernelGGL((k_compact<Stage, true>), gridb, dim3(IDX_BLOCK), 0, stream, st, fr, *bk);
             SHPL_LAUNCH_CHECK();
             return SHPL_OK;
         }

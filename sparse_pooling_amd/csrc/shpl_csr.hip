@@ -975,20 +975,55 @@ __global__ __launch_bounds__(BKT_CHUNK) void k_bkt_place(CsrIn c, BktIn k) {
 
 // A bucket's counting sort (k_bkt_sort, k_bsort2): words[0, n) = the bucket of destinations
 // [k0, k0 + nk) (global ids, word = local destination << 24 | entry - e0) in entry order, placed stably
-// by destination at out0.. (rounds of BKT_SORT words in bucket order, wave ballots over the 7 destination
+// by destination at out0.. (rounds of BLOCK words in bucket order, wave ballots over the 7 destination
 // bits) with source row, value and column; key_range of its destinations. BY_CELL: source = pix[e];
-// BY_PIXEL: source = cell[e] and column e (the builder's identity columns). Returns nothing; all threads.
+// BY_PIXEL: source = cell[e] and column e (the builder's identity columns). All threads call it.
+// Buckets of at most LCAP words are first read into LDS together with their entries' source rows and
+// values (every load of the bucket in flight at once), so the rounds touch only LDS; larger ones load
+// per round.
+template <int BLOCK, int LCAP>
 __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t n, int64_t e0, int64_t out0,
                                                  int64_t k0, int nk, int direction, const int32_t *col,
                                                  const int32_t *cell, const int32_t *pix, const float *vals,
                                                  int32_t *ent_dst, int32_t *ent_src, float *ent_val,
                                                  int32_t *ent_col, int32_t *key_range) {
-    __shared__ int32_t cnt[RANGE_KEYS], cur[RANGE_KEYS], s_w[BKT_SORT / 64][RANGE_KEYS];
+    __shared__ int32_t cnt[RANGE_KEYS], cur[RANGE_KEYS], s_w[BLOCK / 64][RANGE_KEYS];
+    __shared__ uint32_t l_w[LCAP > 0 ? LCAP : 1];
+    __shared__ int32_t l_s[LCAP > 0 ? LCAP : 1];
+    __shared__ float l_v[LCAP > 0 ? LCAP : 1];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < (BKT_SORT / 64) * RANGE_KEYS; i += BKT_SORT) s_w[i / RANGE_KEYS][i % RANGE_KEYS] = 0;
+    const bool staged = n <= LCAP;
+    for (int i = threadIdx.x; i < (BLOCK / 64) * RANGE_KEYS; i += BLOCK) s_w[i / RANGE_KEYS][i % RANGE_KEYS] = 0;
     if ((int)threadIdx.x < RANGE_KEYS) cnt[threadIdx.x] = 0;
     __syncthreads();
-    for (int32_t i = threadIdx.x; i < n; i += BKT_SORT) atomicAdd(&cnt[words[i] >> 24], 1);
+    if (staged) {
+        for (int32_t i0 = threadIdx.x; i0 < n; i0 += 4 * BLOCK) {  // 4 words per thread in flight
+            uint32_t w[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) w[u] = i0 + u * BLOCK < n ? words[i0 + u * BLOCK] : 0u;
+            int32_t sr[4];
+            float vl[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (i0 + u * BLOCK >= n) continue;
+                const int64_t e = e0 + (w[u] & 0xffffffu);
+                const int32_t kk = col ? col[e] : (int32_t)e;
+                vl[u] = vals[e];
+                sr[u] = direction == SHPL_BY_CELL ? pix[kk] : cell[e];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int32_t i = i0 + u * BLOCK;
+                if (i >= n) continue;
+                l_w[i] = w[u];
+                l_s[i] = sr[u];
+                l_v[i] = vl[u];
+                atomicAdd(&cnt[w[u] >> 24], 1);
+            }
+        }
+    } else {
+        for (int32_t i = threadIdx.x; i < n; i += BLOCK) atomicAdd(&cnt[words[i] >> 24], 1);
+    }
     __syncthreads();
     // destinations' starts (128 counts: the first two waves)
     if ((int)threadIdx.x < RANGE_KEYS) {
@@ -1014,20 +1049,28 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
     __syncthreads();
     if ((int)threadIdx.x < RANGE_KEYS) s_w[0][threadIdx.x] = 0;
     __syncthreads();
-    // stable placement, rounds of BKT_SORT words in bucket (= entry) order
-    for (int32_t b0 = 0; b0 < n; b0 += BKT_SORT) {
+    // stable placement, rounds of BLOCK words in bucket (= entry) order
+    for (int32_t b0 = 0; b0 < n; b0 += BLOCK) {
         const int32_t i = b0 + threadIdx.x;
         const bool ok = i < n;
-        const uint32_t w = ok ? words[i] : 0u;
-        const int t = (int)(w >> 24);
-        const int64_t e = e0 + (w & 0xffffffu);
+        uint32_t w = 0u;
         int32_t kk = 0, src = 0;
         float val = 0.0f;
-        if (ok) {  // the emission's loads, in flight during the multisplit
+        if (staged) {
+            if (ok) {
+                w = l_w[i];
+                src = l_s[i];
+                val = l_v[i];
+            }
+        } else if (ok) {  // the emission's loads, in flight during the multisplit
+            w = words[i];
+            const int64_t e = e0 + (w & 0xffffffu);
             kk = col ? col[e] : (int32_t)e;
             val = vals[e];
             src = direction == SHPL_BY_CELL ? pix[kk] : cell[e];
         }
+        const int t = (int)(w >> 24);
+        if (staged && ok && ent_col) kk = col ? col[e0 + (w & 0xffffffu)] : (int32_t)(e0 + (w & 0xffffffu));
         uint64_t peers = __ballot(ok);
 #pragma unroll
         for (int bit = 0; bit < 7; ++bit) {
@@ -1040,7 +1083,7 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
         if ((int)threadIdx.x < RANGE_KEYS) {  // per destination: waves' prefix, then the cursor moves on
             int32_t run = cur[threadIdx.x];
 #pragma unroll
-            for (int v = 0; v < BKT_SORT / 64; ++v) {
+            for (int v = 0; v < BLOCK / 64; ++v) {
                 const int32_t x = s_w[v][threadIdx.x];
                 s_w[v][threadIdx.x] = run;
                 run += x;
@@ -1058,7 +1101,7 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
         __syncthreads();
         if ((int)threadIdx.x < RANGE_KEYS) {
 #pragma unroll
-            for (int v = 0; v < BKT_SORT / 64; ++v) s_w[v][threadIdx.x] = 0;
+            for (int v = 0; v < BLOCK / 64; ++v) s_w[v][threadIdx.x] = 0;
         }
         __syncthreads();
     }
@@ -1081,8 +1124,8 @@ __global__ __launch_bounds__(BKT_SORT) void k_bkt_sort(CsrIn c, BktIn k, int64_t
         n = x[1];
     }
     const int64_t out0 = e0 + start;
-    bucket_sort_emit(k.words + out0, n, e0, out0, k0, nk, c.direction, HAS_COL ? c.col : nullptr, c.cell, c.pix,
-                     c.val, ent_dst, ent_src, ent_val, ent_col, key_range);
+    bucket_sort_emit<BKT_SORT, 0>(k.words + out0, n, e0, out0, k0, nk, c.direction, HAS_COL ? c.col : nullptr,
+                                  c.cell, c.pix, c.val, ent_dst, ent_src, ent_val, ent_col, key_range);
     // the frame's unused capacity (its last range), the slots and key ranges after the last frame
     if (q != k.n_ranges - 1) return;
     for (int64_t h = out0 + n + threadIdx.x; h < cap_end; h += BKT_SORT) ent_dst[h] = -1;
@@ -1096,7 +1139,7 @@ __global__ __launch_bounds__(BKT_SORT) void k_bkt_sort(CsrIn c, BktIn k, int64_t
 }
 
 // ------------------------------------------------ both CSRs from the index build's buckets
-// (shpl_build_csr_buckets). One launch: a BKT_SORT-thread workgroup per (key, frame, range) sorts its
+// (shpl_build_csr_buckets). One launch: a BS_BLOCK-thread workgroup per (key, frame, range) sorts its
 // bucket with bucket_sort_emit -- the buckets are the index builder's (shpl_common.h BkLayout), so no
 // counting or bucketing pass precedes it. A frame of at most one entry has no bucket: that entry is
 // read from the index arrays.
@@ -1119,7 +1162,10 @@ struct BsIn {
     int64_t nnz_cap;
 };
 
-__global__ __launch_bounds__(BKT_SORT) void k_bsort2(BsIn in, BsSide s0, BsSide s1) {
+constexpr int BS_BLOCK = 1024;  // threads of a k_bsort2 workgroup (the horizon's 2 k-entry pixel buckets: 3 rounds)
+constexpr int BS_LCAP = 4096;   // bucket words staged in LDS with their source rows and values (48 KiB)
+
+__global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide s1) {
     __shared__ uint32_t one[1];
     const bool second = (int64_t)blockIdx.x >= s0.blocks;
     const BsSide &sd = second ? s1 : s0;
@@ -1155,15 +1201,15 @@ __global__ __launch_bounds__(BKT_SORT) void k_bsort2(BsIn in, BsSide s0, BsSide 
         __syncthreads();
     }
     const int64_t out0 = p0 + start;
-    bucket_sort_emit(W, n, p0, out0, k0, nk, direction, nullptr, in.cell, in.pix, in.val, sd.ent_dst, sd.ent_src,
-                     sd.ent_val, sd.ent_col, sd.key_range);
+    bucket_sort_emit<BS_BLOCK, BS_LCAP>(W, n, p0, out0, k0, nk, direction, nullptr, in.cell, in.pix, in.val, sd.ent_dst,
+                                        sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range);
     // the frame's unused capacity (its last range), the slots and key ranges after the last frame
     if (q != sd.nr - 1) return;
-    for (int64_t h = p0 + valid + threadIdx.x; h < cap_end; h += BKT_SORT) sd.ent_dst[h] = -1;
+    for (int64_t h = p0 + valid + threadIdx.x; h < cap_end; h += BS_BLOCK) sd.ent_dst[h] = -1;
     if (f != in.n_frames - 1) return;
-    for (int64_t h = cap_end + threadIdx.x; h < sd.nnz_cap; h += BKT_SORT) sd.ent_dst[h] = -1;
+    for (int64_t h = cap_end + threadIdx.x; h < sd.nnz_cap; h += BS_BLOCK) sd.ent_dst[h] = -1;
     if (sd.key_range)
-        for (int64_t kk = kend + threadIdx.x; kk < sd.n_keys; kk += BKT_SORT) {
+        for (int64_t kk = kend + threadIdx.x; kk < sd.n_keys; kk += BS_BLOCK) {
             sd.key_range[2 * kk] = 0;
             sd.key_range[2 * kk + 1] = 0;
         }
@@ -1448,7 +1494,7 @@ extern "C" int shpl_build_csr_buckets(const shpl_buckets *bk, const shpl_csr *by
     char *w = (char *)bk->ws;
     const BsIn in{bk->frame_off, bk->frame_nnz, bk->cell, bk->pix, bk->val, (const int32_t *)(w + l.ext),
                   (const uint32_t *)(w + l.words), bk->n_frames, l.nrmax, bk->nnz_cap};
-    hipLaunchKernelGGL(k_bsort2, dim3((unsigned)blocks), dim3(BKT_SORT), 0, st, in, s[0], s[1]);
+    hipLaunchKernelGGL(k_bsort2, dim3((unsigned)blocks), dim3(BS_BLOCK), 0, st, in, s[0], s[1]);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
 }

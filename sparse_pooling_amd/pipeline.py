@@ -88,7 +88,9 @@ class FusedPipeline:
                                      self.bkt_ws.numel())
 
     # ------------------------------------------------------------------ steps
-    def build_index(self, points, voxels, point_offsets, P, mval=None, point_counts=None):
+    def build_index(self, points, voxels, point_offsets, P, mval=None, point_counts=None, pass_copies=None):
+        """pass_copies (bucketed pipelines): (bev, img) -- the forward's pass-through halves ride the index
+        launches (shpl_pass_copy)."""
         assert points.is_contiguous() and point_offsets.is_contiguous() and P.is_contiguous()
         assert voxels.stride(1) == 1, "voxel rows must be contiguous"
         st = L.stream_of(self.dev)
@@ -101,7 +103,7 @@ class FusedPipeline:
                 float(self.bv_size[1]), self.stride[0], self.stride[1], L.ptr(mval), L.ptr(self.cell),
                 L.ptr(self.pix), L.ptr(self.val), L.ptr(self.frame_nnz), L.ptr(self.frame_off),
                 L.ptr(self.err), L.ptr(self.index_ws), self.index_ws.numel(), self.N, L.ptr(self.bkt_ws),
-                self.bkt_ws.numel(), st), "shpl_build_index_buckets")
+                self.bkt_ws.numel(), *self._copy_riders(pass_copies), st), "shpl_build_index_buckets")
             return
         L.check(self._lib.shpl_build_index(
             self.B, L.ptr(point_offsets), L.ptr(point_counts), self.max_points, L.ptr(points),
@@ -168,6 +170,23 @@ class FusedPipeline:
                                          ctypes.byref(pix_desc) if pix_desc else None,
                                          L.stream_of(self.dev)), "shpl_pull_pair")
 
+    def _copy_riders(self, pass_copies):
+        if pass_copies is None:
+            return None, None
+        bev, img = pass_copies
+        dt = L.dtype_code(self.bv_fused)
+        cell = L.ShplPassCopy(dt, bev.data_ptr(), self.Cb, self.bv_fused.data_ptr(), self.Cb + self.Ci, self.Cb)
+        pix = L.ShplPassCopy(dt, img.data_ptr(), self.Ci, self.img_fused.data_ptr(), self.Ci + self.Cb,
+                             self.Ci) if self.dual else None
+        self._riders = (cell, pix)  # kept alive until the call returns
+        return ctypes.byref(cell), (ctypes.byref(pix) if pix is not None else None)
+
+    def copy_riders_ok(self, bev, img):
+        """The riders' shape rule (16-byte rows and pieces), else the pass-through halves take shpl_pull_dense."""
+        esz = self.bv_fused.element_size()
+        return all((c * esz) % 16 == 0 for c in (self.Cb, self.Ci)) and all(
+            t.data_ptr() % 16 == 0 for t in (bev, img, self.bv_fused) + ((self.img_fused,) if self.dual else ()))
+
     def _pass_copies(self, bev, img, which=("cell", "pixel")):
         """The forward's pass-through halves alone (shpl_pull_dense over no pooled channels): bv_fused[..., :Cb]
         = bev, img_fused[..., :Ci] = img; they need no index."""
@@ -227,24 +246,24 @@ class FusedPipeline:
         beside the cell-keyed ones (they share only M).
         `events` (4 timing events) bracket the dense and the sparse launches."""
         if self.buckets:
-            # index + buckets (2 launches), both CSRs (1 launch), both pooled halves (1 launch) on the current
-            # stream; the pass-through halves on `side` beside them (no index needed; disjoint columns)
+            # one stream: index + buckets with the pass-through halves riding its two launches, both CSRs
+            # (1 launch), both pooled halves (1 launch). (The copies on `side` beside the index chain instead
+            # cost 20-30 us of cross-queue waits per graph replay at config 3: profiles/r03_bpull_ab.log.)
             main = torch.cuda.current_stream(self.dev)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                if events:
-                    events[0].record(side)
+            if events:
+                events[0].record(main)
+            riders = self.copy_riders_ok(bev, img)
+            if not riders:
                 self._pass_copies(bev, img)
-                if events:
-                    events[1].record(side)
-            self.build_index(points, voxels, point_offsets, P, mval)
+            if events:
+                events[1].record(main)
+            self.build_index(points, voxels, point_offsets, P, mval, pass_copies=(bev, img) if riders else None)
             self.build_csr()
             if events:
                 events[2].record(main)
             self._pull_pair(*self._pooled_descs(bev, img))
             if events:
                 events[3].record(main)
-            main.wait_stream(side)
             return
         main = torch.cuda.current_stream(self.dev)
         side.wait_stream(main)            # inputs / previous step done

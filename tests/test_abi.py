@@ -96,9 +96,13 @@ def test_argument_validation_is_host_side():
     assert lib.shpl_bucket_workspace_bytes(4, (1 << 24) + 1, 80000, 8800, 6750, ctypes.byref(nb)) == L.ERR_BAD_SHAPE
     args = (4, P, N, 20000, P, L.F64, P, L.I64, 2, P, 1200., 360., 704., 800., 8., 8., N, P, P, P, P, P, P, P,
             1 << 20, 80000)
-    assert lib.shpl_build_index_buckets(*args, N, 1 << 24, N) == L.ERR_ARG
-    assert lib.shpl_build_index_buckets(*args, P, 64, N) == L.ERR_WORKSPACE
-    assert lib.shpl_build_index_buckets(*args[:14], 1., 1., *args[16:], P, 1 << 24, N) == L.ERR_BAD_SHAPE
+    assert lib.shpl_build_index_buckets(*args, N, 1 << 24, N, N, N) == L.ERR_ARG
+    assert lib.shpl_build_index_buckets(*args, P, 64, N, N, N) == L.ERR_WORKSPACE
+    assert lib.shpl_build_index_buckets(*args[:14], 1., 1., *args[16:], P, 1 << 24, N, N, N) == L.ERR_BAD_SHAPE
+    odd = L.ShplPassCopy(L.BF16, 256, 12, 256, 24, 12)  # 24-byte rows: not 16-byte pieces
+    assert lib.shpl_build_index_buckets(*args, P, 1 << 24, ctypes.byref(odd), N, N) == L.ERR_BAD_SHAPE
+    bad = L.ShplPassCopy(7, 256, 32, 256, 64, 32)
+    assert lib.shpl_build_index_buckets(*args, P, 1 << 24, N, ctypes.byref(bad), N) == L.ERR_ARG
     bk = L.ShplBuckets(4, 20000, 80000, 8800, 6750, 256, 256, 256, 256, 256, 256, nb.value)
     ccell = L.ShplCsr(256, 256, 256, None, 4 * 8800, 80000, 256)
     cpix = L.ShplCsr(256, 256, 256, None, 4 * 6750, 80000, 256)  # no ent_col
