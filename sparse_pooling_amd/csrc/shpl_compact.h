@@ -256,6 +256,7 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr, Bkt 
     __shared__ int32_t pre[IDX_BLOCK / 64], all[IDX_BLOCK / 64], naux[IDX_BLOCK / 64];
     __shared__ int32_t s_off[BKT ? 2 * BK_MAX_RANGES : 1], s_scan[IDX_BLOCK / 64];
     __shared__ int32_t s_w[BKT ? 2 : 1][IDX_BLOCK / 64][BKT ? BK_MAX_RANGES : 1];  // per-wave range counts
+    __shared__ int32_t s_tb[BKT ? 4 * BK_MAX_RANGES : 1];  // per (key, range): entries in the frame, in earlier chunks
     const int f = blockIdx.y, j = blockIdx.x;
     if constexpr (BKT) {
         if (j >= fr.n_chunks) {  // a rider workgroup (uniform)
@@ -268,22 +269,37 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr, Bkt 
     const int wid = threadIdx.x >> 6;
     // buckets: each (key, range) thread's entries in all of the frame's chunks and in the earlier ones
     // (loads issued first, beside the point loads)
-    int32_t b_tot = 0, b_bef = 0;
-    const int bK = threadIdx.x / BK_MAX_RANGES, bq = threadIdx.x % BK_MAX_RANGES;
     if constexpr (BKT) {
+        // (key K, range q) pairs x S slices of the chunks: S adjacent lanes per pair (S a power of two, at
+        // most 64, S x pairs <= the block), each summing every S-th chunk -- all its loads in flight --
+        // then a shuffle reduction; s_tb[K][q] / s_tb[2][K][q] = the pair's entries in all / earlier chunks
         static_assert(IDX_BLOCK == 2 * BK_MAX_RANGES, "one thread per (key, range)");
-        if (bq < bk.nr[bK]) {
-            const int32_t *h = bk.hist + ((int64_t)bK * fr.n_frames + f) * fr.n_chunks * bk.nrmax + bq;
-            for (int j0 = 0; j0 < fr.n_chunks; j0 += 8) {  // 8 loads in flight
+        const int P = 2 * bk.nrmax;
+        int S = 1;
+        while (S < 64 && 2 * S * P <= IDX_BLOCK) S <<= 1;
+        const int pair = threadIdx.x / S, sl = threadIdx.x & (S - 1);
+        const int K = pair / bk.nrmax, q = pair - K * bk.nrmax;
+        int32_t tot = 0, bef = 0;
+        if (pair < P && q < bk.nr[K]) {
+            const int32_t *h = bk.hist + ((int64_t)K * fr.n_frames + f) * fr.n_chunks * bk.nrmax + q;
+            for (int j0 = sl; j0 < fr.n_chunks; j0 += 8 * S) {  // 8 loads in flight
                 int32_t v[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) v[u] = j0 + u < fr.n_chunks ? h[(int64_t)(j0 + u) * bk.nrmax] : 0;
+                for (int u = 0; u < 8; ++u) v[u] = j0 + u * S < fr.n_chunks ? h[(int64_t)(j0 + u * S) * bk.nrmax] : 0;
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
-                    b_tot += v[u];
-                    b_bef += j0 + u < j ? v[u] : 0;
+                    tot += v[u];
+                    bef += j0 + u * S < j ? v[u] : 0;
                 }
             }
+        }
+        for (int o = 1; o < S; o <<= 1) {  // S lanes of one wave (S <= 64, aligned)
+            tot += __shfl_xor(tot, o, 64);
+            bef += __shfl_xor(bef, o, 64);
+        }
+        if (pair < P && sl == 0) {
+            s_tb[K * BK_MAX_RANGES + q] = tot;
+            s_tb[2 * BK_MAX_RANGES + K * BK_MAX_RANGES + q] = bef;
         }
         for (int i = threadIdx.x; i < 2 * (IDX_BLOCK / 64) * BK_MAX_RANGES; i += IDX_BLOCK) (&s_w[0][0][0])[i] = 0;
     }
@@ -358,8 +374,11 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr, Bkt 
     // sentinels of the unused capacity [p0 + total, cap_end), each chunk its own stretch
     int64_t total = 0;
     for (int w = 0; w < IDX_BLOCK / 64; ++w) total += all[w];
-    if constexpr (BKT) bucket_place(st, fr, bk, f, j, p0, total, keep[0], pl[0], b_pos, b_tot, b_bef, s_off, s_scan,
-                                    s_w);
+    if constexpr (BKT) {  // (s_tb written before k_compact's first barrier; entries past nr[K] never)
+        const bool live = (int)(threadIdx.x % BK_MAX_RANGES) < bk.nr[threadIdx.x / BK_MAX_RANGES];
+        bucket_place(st, fr, bk, f, j, p0, total, keep[0], pl[0], b_pos, live ? s_tb[threadIdx.x] : 0,
+                     live ? s_tb[2 * BK_MAX_RANGES + threadIdx.x] : 0, s_off, s_scan, s_w);
+    }
     const int64_t h0 = p0 + total > base ? p0 + total : base;
     const int64_t h1 = j == fr.n_chunks - 1 ? cap_end : (base + IDX_CHUNK < cap_end ? base + IDX_CHUNK : cap_end);
     for (int64_t pos = h0 + threadIdx.x; pos < h1; pos += IDX_BLOCK) st.hole(pos);

@@ -975,32 +975,36 @@ __global__ __launch_bounds__(BKT_CHUNK) void k_bkt_place(CsrIn c, BktIn k) {
 
 // A bucket's counting sort (k_bkt_sort, k_bsort2): words[0, n) = the bucket of destinations
 // [k0, k0 + nk) (global ids, word = local destination << 24 | entry - e0) in entry order, placed stably
-// by destination at out0.. (rounds of BLOCK words in bucket order, wave ballots over the 7 destination
-// bits) with source row, value and column; key_range of its destinations. BY_CELL: source = pix[e];
-// BY_PIXEL: source = cell[e] and column e (the builder's identity columns). All threads call it.
-// Buckets of at most LCAP words are first read into LDS together with their entries' source rows and
-// values (every load of the bucket in flight at once), so the rounds touch only LDS; larger ones load
-// per round.
+// by destination at out0.. with source row, value and column; key_range of its destinations. BY_CELL:
+// source = pix[e]; BY_PIXEL: source = cell[e] and column e (the builder's identity columns). All threads
+// call it. The bucket is cut into one contiguous slice per wave: the slices' per-destination counts
+// (LDS atomics), one exclusive scan over (destination, slice) gives every (slice, destination) its first
+// slot, and each wave then places its own slice in order, 64 words at a time (ballots over the 7
+// destination bits rank a word among its batch's equals, one lane per destination moves the slice's
+// cursor) -- three block barriers whatever the bucket's size. Buckets of at most LCAP words are read
+// into LDS first together with their entries' source rows and values (every load in flight at once).
 template <int BLOCK, int LCAP>
 __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t n, int64_t e0, int64_t out0,
                                                  int64_t k0, int nk, int direction, const int32_t *col,
                                                  const int32_t *cell, const int32_t *pix, const float *vals,
                                                  int32_t *ent_dst, int32_t *ent_src, float *ent_val,
                                                  int32_t *ent_col, int32_t *key_range) {
-    __shared__ int32_t cnt[RANGE_KEYS], cur[RANGE_KEYS], s_w[BLOCK / 64][RANGE_KEYS];
+    constexpr int NW = BLOCK / 64;
+    __shared__ int32_t cnt[NW][RANGE_KEYS], s_tot[RANGE_KEYS];
     __shared__ uint32_t l_w[LCAP > 0 ? LCAP : 1];
     __shared__ int32_t l_s[LCAP > 0 ? LCAP : 1];
     __shared__ float l_v[LCAP > 0 ? LCAP : 1];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const bool staged = n <= LCAP;
-    for (int i = threadIdx.x; i < (BLOCK / 64) * RANGE_KEYS; i += BLOCK) s_w[i / RANGE_KEYS][i % RANGE_KEYS] = 0;
-    if ((int)threadIdx.x < RANGE_KEYS) cnt[threadIdx.x] = 0;
+    const int32_t L = (n + NW - 1) / NW;  // words per wave slice
+    for (int i = threadIdx.x; i < NW * RANGE_KEYS; i += BLOCK) cnt[i / RANGE_KEYS][i % RANGE_KEYS] = 0;
     __syncthreads();
-    if (staged) {
-        for (int32_t i0 = threadIdx.x; i0 < n; i0 += 4 * BLOCK) {  // 4 words per thread in flight
-            uint32_t w[4];
+    // 1. per-slice counts (and, staged, the words with their sources and values into LDS)
+    for (int32_t i0 = threadIdx.x; i0 < n; i0 += 4 * BLOCK) {  // 4 words per thread in flight
+        uint32_t w[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) w[u] = i0 + u * BLOCK < n ? words[i0 + u * BLOCK] : 0u;
+        for (int u = 0; u < 4; ++u) w[u] = i0 + u * BLOCK < n ? words[i0 + u * BLOCK] : 0u;
+        if (staged) {
             int32_t sr[4];
             float vl[4];
 #pragma unroll
@@ -1018,59 +1022,65 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
                 l_w[i] = w[u];
                 l_s[i] = sr[u];
                 l_v[i] = vl[u];
-                atomicAdd(&cnt[w[u] >> 24], 1);
             }
         }
-    } else {
-        for (int32_t i = threadIdx.x; i < n; i += BLOCK) atomicAdd(&cnt[words[i] >> 24], 1);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int32_t i = i0 + u * BLOCK;
+            if (i < n) atomicAdd(&cnt[i / L][w[u] >> 24], 1);
+        }
     }
     __syncthreads();
-    // destinations' starts (128 counts: the first two waves)
+    // 2. (destination, slice) starts: totals per destination, scanned (first two waves), then the slices
     if ((int)threadIdx.x < RANGE_KEYS) {
-        const int32_t v = cnt[threadIdx.x];
+        int32_t v = 0;
+#pragma unroll
+        for (int s = 0; s < NW; ++s) v += cnt[s][threadIdx.x];
         int32_t x = v;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const int32_t y = __shfl_up(x, o, 64);
             if (lane >= o) x += y;
         }
-        s_w[0][threadIdx.x] = x;  // inclusive prefix inside the wave (s_w is cleared again below)
+        s_tot[threadIdx.x] = x;  // inclusive prefix inside the wave
     }
     __syncthreads();
     if ((int)threadIdx.x < RANGE_KEYS) {
-        const int32_t incl = s_w[0][threadIdx.x] + (threadIdx.x >= 64 ? s_w[0][63] : 0);
-        const int32_t beg = incl - cnt[threadIdx.x];
-        cur[threadIdx.x] = beg;
+        const int32_t incl = s_tot[threadIdx.x] + (threadIdx.x >= 64 ? s_tot[63] : 0);
+        int32_t run = incl;
+        for (int s = NW - 1; s >= 0; --s) {  // slice cursors, last slice first (run ends at the start)
+            run -= cnt[s][threadIdx.x];
+            cnt[s][threadIdx.x] = run;
+        }
         if (key_range && (int)threadIdx.x < nk) {
-            key_range[2 * (k0 + threadIdx.x)] = (int32_t)(out0 + beg);
+            key_range[2 * (k0 + threadIdx.x)] = (int32_t)(out0 + run);
             key_range[2 * (k0 + threadIdx.x) + 1] = (int32_t)(out0 + incl);
         }
     }
     __syncthreads();
-    if ((int)threadIdx.x < RANGE_KEYS) s_w[0][threadIdx.x] = 0;
-    __syncthreads();
-    // stable placement, rounds of BLOCK words in bucket (= entry) order
-    for (int32_t b0 = 0; b0 < n; b0 += BLOCK) {
-        const int32_t i = b0 + threadIdx.x;
-        const bool ok = i < n;
+    // 3. each wave places its slice in order, 64 words at a time (no block barrier)
+    const int32_t s0 = wid * L, s1 = min(n, s0 + L);
+    for (int32_t b0 = s0; b0 < s1; b0 += 64) {
+        const int32_t i = b0 + lane;
+        const bool ok = i < s1;
         uint32_t w = 0u;
         int32_t kk = 0, src = 0;
         float val = 0.0f;
-        if (staged) {
-            if (ok) {
+        if (ok) {
+            if (staged) {
                 w = l_w[i];
                 src = l_s[i];
                 val = l_v[i];
+                if (ent_col) kk = col ? col[e0 + (w & 0xffffffu)] : (int32_t)(e0 + (w & 0xffffffu));
+            } else {
+                w = words[i];
+                const int64_t e = e0 + (w & 0xffffffu);
+                kk = col ? col[e] : (int32_t)e;
+                val = vals[e];
+                src = direction == SHPL_BY_CELL ? pix[kk] : cell[e];
             }
-        } else if (ok) {  // the emission's loads, in flight during the multisplit
-            w = words[i];
-            const int64_t e = e0 + (w & 0xffffffu);
-            kk = col ? col[e] : (int32_t)e;
-            val = vals[e];
-            src = direction == SHPL_BY_CELL ? pix[kk] : cell[e];
         }
         const int t = (int)(w >> 24);
-        if (staged && ok && ent_col) kk = col ? col[e0 + (w & 0xffffffu)] : (int32_t)(e0 + (w & 0xffffffu));
         uint64_t peers = __ballot(ok);
 #pragma unroll
         for (int bit = 0; bit < 7; ++bit) {
@@ -1078,32 +1088,17 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
             peers &= ((t >> bit) & 1) ? bm : ~bm;
         }
         const int32_t rank = (int32_t)lane_rank(peers);
-        if (ok && rank == 0) s_w[wid][t] = (int32_t)__popcll(peers);
-        __syncthreads();
-        if ((int)threadIdx.x < RANGE_KEYS) {  // per destination: waves' prefix, then the cursor moves on
-            int32_t run = cur[threadIdx.x];
-#pragma unroll
-            for (int v = 0; v < BLOCK / 64; ++v) {
-                const int32_t x = s_w[v][threadIdx.x];
-                s_w[v][threadIdx.x] = run;
-                run += x;
-            }
-            cur[threadIdx.x] = run;
-        }
-        __syncthreads();
+        const int32_t base = ok ? cnt[wid][t] : 0;
+        // the batch's last lane of each destination moves the slice's cursor (after every lane's read: one
+        // wave's LDS operations complete in order)
+        if (ok && (peers >> lane) == 1ull) cnt[wid][t] = base + (int32_t)__popcll(peers);
         if (ok) {
-            const int64_t o = out0 + s_w[wid][t] + rank;
+            const int64_t o = out0 + base + rank;
             ent_dst[o] = (int32_t)(k0 + t);
             ent_src[o] = src;
             ent_val[o] = val;
             if (ent_col) ent_col[o] = kk;
         }
-        __syncthreads();
-        if ((int)threadIdx.x < RANGE_KEYS) {
-#pragma unroll
-            for (int v = 0; v < BLOCK / 64; ++v) s_w[v][threadIdx.x] = 0;
-        }
-        __syncthreads();
     }
 }
 

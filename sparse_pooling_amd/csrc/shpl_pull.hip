@@ -641,8 +641,12 @@ struct RowsSide {
     int64_t n_rows, blocks;
 };
 
+#ifndef SHPL_ROWS2_WPE
+#define SHPL_ROWS2_WPE 1  // amdgpu_waves_per_eu floor of k_rows2 (1: the compiler's choice)
+#endif
 template <typename T, int VEC, int G>
-__global__ __launch_bounds__(SHPL_BLOCK) void k_rows2(const RowsSide s0, const RowsSide s1) {
+__global__ __launch_bounds__(SHPL_BLOCK) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS2_WPE))) void k_rows2(
+    const RowsSide s0, const RowsSide s1) {
     if ((int64_t)blockIdx.x < s0.blocks)
         rows_body<T, VEC, false, G>(s0.f, s0.e, s0.key_range, s0.n_rows, blockIdx.x);
     else
