@@ -87,6 +87,11 @@ def parse():
     ap.add_argument("--no-buckets", action="store_true",
                     help="row-keyed layers (config 3): range CSRs + one k_rows launch per pull on two streams "
                          "instead of the index build's buckets + one shpl_pull_buckets launch per pull pair")
+    ap.add_argument("--no-records", action="store_true",
+                    help="bucketed config 3: CSRs without per-destination records (k_rows2 instead of k_rows2r)")
+    ap.add_argument("--no-riders", action="store_true",
+                    help="bucketed config 3: copy the forward's pass-through halves with their own launches before the "
+                         "index build instead of as extra workgroups of the index launches")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step eagerly instead of replaying one captured HIP graph of it")
     ap.add_argument("--workload", default="layer", choices=["layer", "frames", "conv"],
@@ -385,7 +390,7 @@ def main():
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, dev)
     pl = pipeline.FusedPipeline(F, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev,
                                 spec.c_img, dtype=dtype, dual=dual, device=dev,
-                                buckets=False if args.no_buckets else None)
+                                buckets=False if args.no_buckets else None, records=not args.no_records)
     Hb, Wb = spec.bev_feat_hw
     Hi, Wi = spec.img_feat_hw
     feats = lambda shape, seed: sd.fill_features(torch.empty(shape, dtype=dtype, device=dev), fids, seed)  # noqa
@@ -398,6 +403,7 @@ def main():
     side = torch.cuda.Stream(device=dev)
     side2 = torch.cuda.Stream(device=dev) if dual else None  # pixel-keyed CSR / pulls beside the cell-keyed
     pl.interleave = not args.no_interleave
+    pl.riders = not args.no_riders
     from sparse_pooling_amd import _lib as L
     pl.csr_path = {"auto": L.CSR_AUTO, "frame": L.CSR_FRAME, "segment": L.CSR_SEGMENT, "range": L.CSR_RANGE,
                    "bucket": L.CSR_BUCKET}[args.csr_path]

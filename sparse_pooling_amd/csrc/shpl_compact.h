@@ -78,6 +78,7 @@ struct Bkt {
     int32_t *ext;     // [2][F][nrmax][2]
     uint32_t *words;  // [2][nnz_cap]
     PassCopy cp[2];
+    int cp_at[2];     // the launch each copy rides: 0 = k_count, 1 = k_compact
     int cp_blocks;    // rider workgroups per frame in each launch (0: none)
 };
 
@@ -122,7 +123,8 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr, Bkt bk
     const int f = blockIdx.y, j = blockIdx.x;
     if constexpr (BKT) {
         if (j >= fr.n_chunks) {  // a rider workgroup (uniform)
-            pass_copy(bk.cp[0], f, j - fr.n_chunks, bk.cp_blocks);
+            for (int c = 0; c < 2; ++c)
+                if (bk.cp_at[c] == 0) pass_copy(bk.cp[c], f, j - fr.n_chunks, bk.cp_blocks);
             return;
         }
         for (int q = threadIdx.x; q < 2 * BK_MAX_RANGES; q += IDX_BLOCK) hist[q] = 0;
@@ -260,7 +262,8 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr, Bkt 
     const int f = blockIdx.y, j = blockIdx.x;
     if constexpr (BKT) {
         if (j >= fr.n_chunks) {  // a rider workgroup (uniform)
-            pass_copy(bk.cp[1], f, j - fr.n_chunks, bk.cp_blocks);
+            for (int c = 0; c < 2; ++c)
+                if (bk.cp_at[c] == 1) pass_copy(bk.cp[c], f, j - fr.n_chunks, bk.cp_blocks);
             return;
         }
     }
@@ -413,10 +416,14 @@ int run_compaction(const Stage &st, int n_frames, int64_t max_points, const int6
     const dim3 grid(fr.n_chunks, n_frames);
     if constexpr (Stage::HAS_BUCKETS) {
         if (bk) {
-            const dim3 gridb(fr.n_chunks + bk->cp_blocks, n_frames);
-            hipLaunchKernelGGL((k_count<Stage, true>), gridb, dim3(IDX_BLOCK), 0, stream, st, fr, *bk);
+            bool rides[2] = {false, false};
+            for (int c = 0; c < 2; ++c)
+                if (bk->cp[c].row_bytes > 0) rides[bk->cp_at[c]] = true;
+            const dim3 grid0(fr.n_chunks + (rides[0] ? bk->cp_blocks : 0), n_frames);
+            const dim3 grid1(fr.n_chunks + (rides[1] ? bk->cp_blocks : 0), n_frames);
+            hipLaunchKernelGGL((k_count<Stage, true>), grid0, dim3(IDX_BLOCK), 0, stream, st, fr, *bk);
             SHPL_LAUNCH_CHECK();
-            hipLaunchKernelGGL((k_compact<Stage, true>), gridb, dim3(IDX_BLOCK), 0, stream, st, fr, *bk);
+            hipLaunchKernelGGL((k_compact<Stage, true>), grid1, dim3(IDX_BLOCK), 0, stream, st, fr, *bk);
             SHPL_LAUNCH_CHECK();
             return SHPL_OK;
         }

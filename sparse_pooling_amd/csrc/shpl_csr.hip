@@ -988,9 +988,9 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
                                                  int64_t k0, int nk, int direction, const int32_t *col,
                                                  const int32_t *cell, const int32_t *pix, const float *vals,
                                                  int32_t *ent_dst, int32_t *ent_src, float *ent_val,
-                                                 int32_t *ent_col, int32_t *key_range) {
+                                                 int32_t *ent_col, int32_t *key_range, int32_t *key_rec = nullptr) {
     constexpr int NW = BLOCK / 64;
-    __shared__ int32_t cnt[NW][RANGE_KEYS], s_tot[RANGE_KEYS];
+    __shared__ int32_t cnt[NW][RANGE_KEYS], s_tot[RANGE_KEYS], s_beg[RANGE_KEYS];
     __shared__ uint32_t l_w[LCAP > 0 ? LCAP : 1];
     __shared__ int32_t l_s[LCAP > 0 ? LCAP : 1];
     __shared__ float l_v[LCAP > 0 ? LCAP : 1];
@@ -1052,9 +1052,14 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
             run -= cnt[s][threadIdx.x];
             cnt[s][threadIdx.x] = run;
         }
+        s_beg[threadIdx.x] = run;
         if (key_range && (int)threadIdx.x < nk) {
             key_range[2 * (k0 + threadIdx.x)] = (int32_t)(out0 + run);
             key_range[2 * (k0 + threadIdx.x) + 1] = (int32_t)(out0 + incl);
+        }
+        if (key_rec && (int)threadIdx.x < nk) {
+            key_rec[8 * (k0 + threadIdx.x)] = (int32_t)(out0 + run);
+            key_rec[8 * (k0 + threadIdx.x) + 1] = (int32_t)(out0 + incl);
         }
     }
     __syncthreads();
@@ -1098,6 +1103,11 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
             ent_src[o] = src;
             ent_val[o] = val;
             if (ent_col) ent_col[o] = kk;
+            const int32_t k = base + rank - s_beg[t];  // the entry's place in its destination's run
+            if (key_rec && k < 3) {
+                key_rec[8 * (k0 + t) + 2 + 2 * k] = src;
+                key_rec[8 * (k0 + t) + 3 + 2 * k] = __float_as_int(val);
+            }
         }
     }
 }
@@ -1145,6 +1155,7 @@ struct BsSide {
     float *ent_val;
     int32_t *ent_col, *key_range;
     int64_t blocks;    // n_frames * nr
+    int32_t *key_rec;  // optional per-destination records
 };
 
 struct BsIn {
@@ -1197,17 +1208,22 @@ __global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide 
     }
     const int64_t out0 = p0 + start;
     bucket_sort_emit<BS_BLOCK, BS_LCAP>(W, n, p0, out0, k0, nk, direction, nullptr, in.cell, in.pix, in.val, sd.ent_dst,
-                                        sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range);
+                                        sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range, sd.key_rec);
     // the frame's unused capacity (its last range), the slots and key ranges after the last frame
     if (q != sd.nr - 1) return;
     for (int64_t h = p0 + valid + threadIdx.x; h < cap_end; h += BS_BLOCK) sd.ent_dst[h] = -1;
     if (f != in.n_frames - 1) return;
     for (int64_t h = cap_end + threadIdx.x; h < sd.nnz_cap; h += BS_BLOCK) sd.ent_dst[h] = -1;
-    if (sd.key_range)
-        for (int64_t kk = kend + threadIdx.x; kk < sd.n_keys; kk += BS_BLOCK) {
+    for (int64_t kk = kend + threadIdx.x; kk < sd.n_keys; kk += BS_BLOCK) {
+        if (sd.key_range) {
             sd.key_range[2 * kk] = 0;
             sd.key_range[2 * kk + 1] = 0;
         }
+        if (sd.key_rec) {
+            sd.key_rec[8 * kk] = 0;
+            sd.key_rec[8 * kk + 1] = 0;
+        }
+    }
 }
 
 }  // namespace
@@ -1472,15 +1488,19 @@ extern "C" int shpl_build_csr_buckets(const shpl_buckets *bk, const shpl_csr *by
         if (bk->nnz_cap > 0 && (!c->ent_dst || !c->ent_src || !c->ent_val)) return SHPL_ERR_ARG;
         if (k == 1 && bk->nnz_cap > 0 && !c->ent_col) return SHPL_ERR_ARG;
         s[k] = BsSide{l.nr[k], l.kpf[k], c->n_keys, c->nnz_cap, c->ent_dst, c->ent_src, c->ent_val, c->ent_col,
-                      c->key_range, (int64_t)bk->n_frames * l.nr[k]};
+                      c->key_range, (int64_t)bk->n_frames * l.nr[k], c->key_rec};
         if (l.nr[k] == 0) s[k].blocks = 0;
     }
     hipStream_t st = (hipStream_t)stream;
     if (bk->nnz_cap == 0) {  // an empty map: empty runs everywhere
-        for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < 2; ++k) {
             if (cs[k] && cs[k]->key_range && cs[k]->n_keys > 0 &&
                 hipMemsetAsync(cs[k]->key_range, 0, sizeof(int32_t) * 2 * (size_t)cs[k]->n_keys, st) != hipSuccess)
                 return SHPL_ERR_HIP;
+            if (cs[k] && cs[k]->key_rec && cs[k]->n_keys > 0 &&
+                hipMemsetAsync(cs[k]->key_rec, 0, sizeof(int32_t) * 8 * (size_t)cs[k]->n_keys, st) != hipSuccess)
+                return SHPL_ERR_HIP;
+        }
         return SHPL_OK;
     }
     const int64_t blocks = s[0].blocks + s[1].blocks;

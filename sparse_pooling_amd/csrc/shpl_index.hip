@@ -366,8 +366,13 @@ extern "C" int shpl_build_index_buckets(int n_frames, const int64_t *d_point_off
     const BkLayout l = bk_layout(n_frames, n_chunks_for(max_points_per_frame), nnz_cap, g.n_cells, g.n_pix);
     if (bkt_bytes < l.bytes) return SHPL_ERR_WORKSPACE;
     char *b = (char *)d_bkt;
+    // which index launch each rider copy rides (SHPL_RIDERS: 0 = cell copy with the count, pixel copy with the
+    // placement; 1 = both with the count; 2 = both with the placement)
+#ifndef SHPL_RIDERS
+#define SHPL_RIDERS 0
+#endif
     Bkt bk{{l.nr[0], l.nr[1]}, l.nrmax, nnz_cap, (int32_t *)(b + l.hist), (int32_t *)(b + l.ext),
-           (uint32_t *)(b + l.words), {}, 0};
+           (uint32_t *)(b + l.words), {}, {SHPL_RIDERS == 2 ? 1 : 0, SHPL_RIDERS == 1 ? 0 : 1}, 0};
     const shpl_pass_copy *cps[2] = {cell_copy, pixel_copy};
     int64_t copy_bytes = 0;
     for (int k = 0; k < 2; ++k) {

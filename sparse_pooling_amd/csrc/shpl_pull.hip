@@ -521,30 +521,19 @@ constexpr int ROWS_WALK = SHPL_ROWS_WALK;
 #define SHPL_PULL_XCD 0
 #endif
 
+// The walk of one row's run [first, end) (all lanes of the wave, wave-uniform trip counts); pv / av: the
+// lane's first pass-through chunk (CONCAT, when p0) and first ADD operand, loaded by the caller.
 template <typename T, int VEC, bool GROUP, int G>
-__device__ __forceinline__ void rows_body(const Feat &f, const Ents &e, const int32_t *key_range, int64_t n_rows,
-                                          int64_t blk) {
+__device__ __forceinline__ void row_walk(const Feat &f, const Ents &e, int64_t row, bool live, int32_t first,
+                                         int32_t end, bool p0, typename Chunk<T, VEC>::raw_t pv,
+                                         typename Chunk<T, VEC>::raw_t av) {
     typedef Chunk<T, VEC> C;
-    constexpr int RPW = SHPL_WAVE / G;
     const int lane = threadIdx.x & 63, lg = lane & (G - 1), gbase = lane & ~(G - 1);
-    const int64_t row = (blk * (SHPL_BLOCK / SHPL_WAVE) + (threadIdx.x >> 6)) * RPW + lane / G;
-    const bool live = row < n_rows;
     T *out = reinterpret_cast<T *>(f.out);
     const T *pass = reinterpret_cast<const T *>(f.pass) + f.pass_off;
     const T *src = reinterpret_cast<const T *>(f.src) + f.src_off;
     const bool concat = f.mode == SHPL_OUT_CONCAT, add = f.mode == SHPL_OUT_ADD;
     const uint32_t oc0 = concat ? f.cpass : 0u;
-    // the row's range, its first pass-through chunk and its first ADD operand: one round trip
-    int32_t first = 0, end = 0;
-    typename C::raw_t pv, av;
-    const bool p0 = live && concat && (uint32_t)lg < f.cpass;
-    const bool a0 = live && add && (uint32_t)lg < f.cpool;
-    if (live) {
-        first = key_range[2 * row];
-        end = key_range[2 * row + 1];
-    }
-    if (p0) pv = C::load_nt(pass + (row * f.pass_stride + (int64_t)lg * VEC));
-    if (a0) av = C::load(pass + (row * f.pass_stride + (int64_t)lg * VEC));
     const int32_t len = end - first;
     int32_t wlen = len;  // longest run among the wave's rows: the walk's trip count
 #pragma unroll
@@ -621,6 +610,29 @@ __device__ __forceinline__ void rows_body(const Feat &f, const Ents &e, const in
 }
 
 template <typename T, int VEC, bool GROUP, int G>
+__device__ __forceinline__ void rows_body(const Feat &f, const Ents &e, const int32_t *key_range, int64_t n_rows,
+                                          int64_t blk) {
+    typedef Chunk<T, VEC> C;
+    constexpr int RPW = SHPL_WAVE / G;
+    const int lane = threadIdx.x & 63, lg = lane & (G - 1);
+    const int64_t row = (blk * (SHPL_BLOCK / SHPL_WAVE) + (threadIdx.x >> 6)) * RPW + lane / G;
+    const bool live = row < n_rows;
+    const T *pass = reinterpret_cast<const T *>(f.pass) + f.pass_off;
+    // the row's range, its first pass-through chunk and its first ADD operand: one round trip
+    int32_t first = 0, end = 0;
+    typename C::raw_t pv = C::zero(), av = C::zero();
+    const bool p0 = live && f.mode == SHPL_OUT_CONCAT && (uint32_t)lg < f.cpass;
+    const bool a0 = live && f.mode == SHPL_OUT_ADD && (uint32_t)lg < f.cpool;
+    if (live) {
+        first = key_range[2 * row];
+        end = key_range[2 * row + 1];
+    }
+    if (p0) pv = C::load_nt(pass + (row * f.pass_stride + (int64_t)lg * VEC));
+    if (a0) av = C::load(pass + (row * f.pass_stride + (int64_t)lg * VEC));
+    row_walk<T, VEC, GROUP, G>(f, e, row, live, first, end, p0, pv, av);
+}
+
+template <typename T, int VEC, bool GROUP, int G>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_rows(const Feat f, const Ents e, const int32_t *key_range,
                                                      int64_t n_rows) {
 #if SHPL_PULL_XCD
@@ -639,6 +651,7 @@ struct RowsSide {
     Ents e;
     const int32_t *key_range;
     int64_t n_rows, blocks;
+    const int32_t *key_rec;  // optional per-destination records (k_rows2r)
 };
 
 #ifndef SHPL_ROWS2_WPE
@@ -651,6 +664,151 @@ __global__ __launch_bounds__(SHPL_BLOCK) __attribute__((amdgpu_waves_per_eu(SHPL
         rows_body<T, VEC, false, G>(s0.f, s0.e, s0.key_range, s0.n_rows, blockIdx.x);
     else
         rows_body<T, VEC, true, G>(s1.f, s1.e, s1.key_range, s1.n_rows, (int64_t)blockIdx.x - s0.blocks);
+}
+
+// ------------------------------------------------------------- k_rows2r
+// The pull pair over CSRs that also carry per-destination records (shpl_csr.key_rec, written by
+// shpl_build_csr_buckets): 8 ints per destination, {first, end, then (source row, weight bits) of its
+// first REC_N entries}. Waves are persistent over "items" (64 / G rows each, both pulls' items in one
+// list) and load the next item's records while they walk the current one, so a wave whose rows all
+// hold at most REC_N entries spends ONE dependent round trip per item -- the feature rows -- where
+// k_rows spends three (range, index words, feature rows). Longer runs take row_walk from the
+// record's (first, end). Every entry of a builder-made map has a column of its own (the identity), so
+// TF's per-column partials are single products and the short form's plain sum is bitwise the same
+// (an accumulator that starts at +0 never becomes -0, so 0 + p and p add alike).
+constexpr int REC_N = 3;
+#ifndef SHPL_ROWS2R_GRID
+#define SHPL_ROWS2R_GRID 1280  // workgroups of k_rows2r at most (4 waves each: ~the chip's resident waves)
+#endif
+
+struct Rec {
+    int32_t first, end, s[REC_N];
+    float v[REC_N];
+};
+
+template <typename T, int VEC, int G>
+__device__ __forceinline__ void rec_fetch(const RowsSide &s0, const RowsSide &s1, int64_t items0, int64_t it,
+                                          Rec &r, typename Chunk<T, VEC>::raw_t &av, bool &live, int64_t &row,
+                                          bool &second) {
+    typedef Chunk<T, VEC> C;
+    constexpr int RPW = SHPL_WAVE / G;
+    const int lane = threadIdx.x & 63, lg = lane & (G - 1);
+    second = it >= items0;
+    const RowsSide &sd = second ? s1 : s0;
+    row = (second ? it - items0 : it) * RPW + lane / G;
+    live = row < sd.n_rows;
+    r.first = r.end = 0;
+    if (live) {
+        typedef int32_t i32x4r __attribute__((ext_vector_type(4)));
+        const i32x4r a = *reinterpret_cast<const i32x4r *>(sd.key_rec + 8 * row);
+        const i32x4r b = *reinterpret_cast<const i32x4r *>(sd.key_rec + 8 * row + 4);
+        r.first = a[0];
+        r.end = a[1];
+        r.s[0] = a[2];
+        r.v[0] = __int_as_float(a[3]);
+        r.s[1] = b[0];
+        r.v[1] = __int_as_float(b[1]);
+        r.s[2] = b[2];
+        r.v[2] = __int_as_float(b[3]);
+    }
+    const Feat &f = sd.f;
+    if (live && f.mode == SHPL_OUT_ADD && (uint32_t)lg < f.cpool)
+        av = C::load(reinterpret_cast<const T *>(f.pass) + f.pass_off + (row * f.pass_stride + (int64_t)lg * VEC));
+}
+
+// A row of at most REC_N entries, from its record (the wave's rows all are).
+template <typename T, int VEC, int G>
+__device__ __forceinline__ void row_short(const Feat &f, int64_t row, bool live, const Rec &r,
+                                          typename Chunk<T, VEC>::raw_t av) {
+    typedef Chunk<T, VEC> C;
+    const int lg = (threadIdx.x & 63) & (G - 1);
+    if (!live) return;
+    T *out = reinterpret_cast<T *>(f.out);
+    const T *pass = reinterpret_cast<const T *>(f.pass) + f.pass_off;
+    const T *src = reinterpret_cast<const T *>(f.src) + f.src_off;
+    const bool concat = f.mode == SHPL_OUT_CONCAT, add = f.mode == SHPL_OUT_ADD;
+    const uint32_t oc0 = concat ? f.cpass : 0u;
+    const int32_t len = r.end - r.first;
+    if (concat)
+        for (uint32_t c = lg; c < f.cpass; c += G)
+            C::store_nt(out + (row * f.out_stride + (int64_t)c * VEC),
+                        C::load_nt(pass + (row * f.pass_stride + (int64_t)c * VEC)));
+    for (uint32_t pc0 = 0; pc0 < f.cpool; pc0 += G) {
+        const uint32_t pc = pc0 + lg;
+        if (pc >= f.cpool) break;
+        typename C::raw_t raw[REC_N];
+#pragma unroll
+        for (int u = 0; u < REC_N; ++u)
+            if (u < len) raw[u] = C::load(src + ((int64_t)r.s[u] * f.src_stride + (int64_t)pc * VEC));
+        float acc[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) acc[j] = 0.0f;
+#pragma unroll
+        for (int u = 0; u < REC_N; ++u) {
+            if (u >= len) continue;
+            float x[VEC];
+            C::to_f32(raw[u], x);
+            fma_free_accumulate<VEC>(acc, r.v[u], x);
+        }
+        if (add) {
+            float a[VEC];
+            C::to_f32(pc0 == 0 ? av : C::load(pass + (row * f.pass_stride + (int64_t)pc * VEC)), a);
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(a[j], acc[j]);
+        } else if (len == 0) {
+            C::store_nt(out + (row * f.out_stride + (int64_t)(oc0 + pc) * VEC), C::zero());
+            continue;
+        }
+        C::store_nt(out + (row * f.out_stride + (int64_t)(oc0 + pc) * VEC), C::from_f32(acc));
+    }
+}
+
+template <typename T, int VEC, int G>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_rows2r(const RowsSide s0, const RowsSide s1, int64_t items0,
+                                                       int64_t items) {
+    typedef Chunk<T, VEC> C;
+    const int lane = threadIdx.x & 63, lg = lane & (G - 1);
+    const int64_t W = (int64_t)gridDim.x * (SHPL_BLOCK / SHPL_WAVE);
+    int64_t it = (int64_t)blockIdx.x * (SHPL_BLOCK / SHPL_WAVE) + (threadIdx.x >> 6);
+    if (it >= items) return;  // wave-uniform
+    Rec cur;
+    typename C::raw_t av = C::zero();
+    bool live, second;
+    int64_t row;
+    rec_fetch<T, VEC, G>(s0, s1, items0, it, cur, av, live, row, second);
+    for (;;) {
+        const int64_t nx = it + W;
+        const bool more = nx < items;  // wave-uniform
+        Rec nr;
+        typename C::raw_t nav = C::zero();
+        bool nlive = false, nsecond = false;
+        int64_t nrow = 0;
+        if (more) rec_fetch<T, VEC, G>(s0, s1, items0, nx, nr, nav, nlive, nrow, nsecond);
+        const int32_t len = cur.end - cur.first;
+        int32_t wlen = len;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) wlen = max(wlen, __shfl_xor(wlen, o, 64));
+        const Feat &f = second ? s1.f : s0.f;
+        if (wlen <= REC_N) {
+            row_short<T, VEC, G>(f, row, live, cur, av);
+        } else {
+            const bool p0 = live && f.mode == SHPL_OUT_CONCAT && (uint32_t)lg < f.cpass;
+            typename C::raw_t pv = C::zero();
+            if (p0) pv = C::load_nt(reinterpret_cast<const T *>(f.pass) + f.pass_off +
+                                    (row * f.pass_stride + (int64_t)lg * VEC));
+            if (second)
+                row_walk<T, VEC, true, G>(s1.f, s1.e, row, live, cur.first, cur.end, p0, pv, av);
+            else
+                row_walk<T, VEC, false, G>(s0.f, s0.e, row, live, cur.first, cur.end, p0, pv, av);
+        }
+        if (!more) break;
+        it = nx;
+        cur = nr;
+        av = nav;
+        live = nlive;
+        row = nrow;
+        second = nsecond;
+    }
 }
 
 bool aligned(const void *ptr, int64_t a) { return ((uintptr_t)ptr) % (uintptr_t)a == 0; }
@@ -884,6 +1042,24 @@ int pair_t(RowsSide s[2], int G, hipStream_t st) {
     const int64_t blocks = s[0].blocks + s[1].blocks;
     if (blocks == 0) return SHPL_OK;
     if (blocks > 0x7fffffffLL) return SHPL_ERR_BAD_SHAPE;
+    const bool recs = (s[0].n_rows == 0 || s[0].key_rec) && (s[1].n_rows == 0 || s[1].key_rec);
+    if (recs) {  // items = waves' worth of rows (64 / G each), both pulls in one list
+        const int64_t rpw = SHPL_WAVE / G;
+        const int64_t items0 = (s[0].n_rows + rpw - 1) / rpw, items = items0 + (s[1].n_rows + rpw - 1) / rpw;
+        int64_t grid = (items + SHPL_BLOCK / SHPL_WAVE - 1) / (SHPL_BLOCK / SHPL_WAVE);
+        if (grid > SHPL_ROWS2R_GRID) grid = SHPL_ROWS2R_GRID;
+#define SHPL_ROWS2R(GG) \
+    hipLaunchKernelGGL((k_rows2r<T, VEC, GG>), dim3((unsigned)grid), dim3(SHPL_BLOCK), 0, st, s[0], s[1], items0, items)
+        switch (G) {
+            case 8: SHPL_ROWS2R(8); break;
+            case 16: SHPL_ROWS2R(16); break;
+            case 32: SHPL_ROWS2R(32); break;
+            default: SHPL_ROWS2R(64); break;
+        }
+#undef SHPL_ROWS2R
+        SHPL_LAUNCH_CHECK();
+        return SHPL_OK;
+    }
 #define SHPL_ROWS2(GG) hipLaunchKernelGGL((k_rows2<T, VEC, GG>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, s[0], s[1])
     switch (G) {
         case 8: SHPL_ROWS2(8); break;
@@ -940,7 +1116,7 @@ extern "C" int shpl_pull_pair(const shpl_csr *by_cell, const shpl_pull_desc *d_c
         v16 = pl[k].v16;
         while (G < 64 && (uint32_t)G < pl[k].f.cpool) G <<= 1;  // lanes per row: the widest pooled row
         s[k] = RowsSide{pl[k].f, Ents{c->nnz_cap, c->ent_dst, c->ent_src, c->ent_col, c->ent_val}, c->key_range,
-                        pl[k].n_dst, 0};
+                        pl[k].n_dst, 0, c->key_rec};
     }
     if (dtype < 0) return SHPL_OK;
     if (dtype == SHPL_F32) return v16 ? pair_t<float, 4>(s, G, st) : pair_t<float, 1>(s, G, st);

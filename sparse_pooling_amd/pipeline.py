@@ -29,15 +29,17 @@ class FusedPipeline:
 
     def __init__(self, n_frames, max_points_per_frame, total_points, im_size, bv_size, stride,
                  c_bev, c_img, dtype=torch.float32, device="cuda", dual=False, rows=None, live=False,
-                 buckets=None):
+                 buckets=None, records=True):
         """live: the sparse passes walk each frame's live entries (shpl_csr frame layout) instead of the
         whole capacity -- for capacities far above the entry counts (FramePipeline: raw-scan slots per
         voxel point); at config 2 (capacity = entries) the capacity walk is faster (2.22 vs 2.24 ms).
         buckets (default: with rows): the index build also cuts M into destination buckets
         (shpl_build_index_buckets), one launch sorts both CSRs out of them (shpl_build_csr_buckets) and
         each pull pair is one row-keyed launch (shpl_pull_pair), all on one stream; the forward's
-        pass-through halves are copied on the side stream beside the index chain. rows without
-        buckets: the range CSRs (one launch per key) + one k_rows launch per pull, on two streams."""
+        pass-through halves ride the index launches. records (bucketed): the CSRs also carry
+        per-destination records and the pull pairs run persistent waves over them (k_rows2r).
+        rows without buckets: the range CSRs (one launch per key) + one k_rows launch per pull,
+        on two streams."""
         dev = torch.device(device)
         self.dev, self.dtype, self.dual = dev, dtype, dual
         self.B = int(n_frames)
@@ -68,10 +70,14 @@ class FusedPipeline:
         self.frame_off = torch.empty(self.B + 1, dtype=torch.int64, device=dev)
         self.err = torch.zeros(1, **i32)
         self.index_ws = L.workspace(L.index_ws_bytes(self.B, self.max_points), dev)
-        self.csr = L.Csr(self.n_cells, self.N, dev, with_col=False, key_range=self.rows)  # BEV-cell CSR (img -> BEV)
+        # rows pulls: with key_range; bucketed: with the per-destination records too (k_rows2r), unless records=False
+        rec = self.buckets and records
+        self.csr = L.Csr(self.n_cells, self.N, dev, with_col=False, key_range=self.rows,
+                         key_rec=rec)  # BEV-cell CSR (img -> BEV)
         self.bv_fused = torch.empty((self.B, self.Hb, self.Wb, self.Cb + self.Ci), dtype=dtype, device=dev)
         if dual:
-            self.pcsr = L.Csr(self.n_pix, self.N, dev, with_col=True, key_range=self.rows)  # pixel CSR (BEV -> img)
+            self.pcsr = L.Csr(self.n_pix, self.N, dev, with_col=True, key_range=self.rows,
+                              key_rec=rec)  # pixel CSR (BEV -> img)
             self.img_fused = torch.empty((self.B, self.Hi, self.Wi, self.Ci + self.Cb), dtype=dtype,
                                          device=dev)
         if live:
@@ -181,10 +187,12 @@ class FusedPipeline:
         self._riders = (cell, pix)  # kept alive until the call returns
         return ctypes.byref(cell), (ctypes.byref(pix) if pix is not None else None)
 
+    riders = True  # bucketed step_overlapped: pass-through halves ride the index launches (False: k_dense copies)
+
     def copy_riders_ok(self, bev, img):
         """The riders' shape rule (16-byte rows and pieces), else the pass-through halves take shpl_pull_dense."""
         esz = self.bv_fused.element_size()
-        return all((c * esz) % 16 == 0 for c in (self.Cb, self.Ci)) and all(
+        return self.riders and all((c * esz) % 16 == 0 for c in (self.Cb, self.Ci)) and all(
             t.data_ptr() % 16 == 0 for t in (bev, img, self.bv_fused) + ((self.img_fused,) if self.dual else ()))
 
     def _pass_copies(self, bev, img, which=("cell", "pixel")):

@@ -679,12 +679,12 @@ def _ragged_pipeline_run(cfg, sizes, dtype, paths, channels=None, frames=None):
              "bucket": L.CSR_BUCKET}
     for path in paths:
         # a named CSR builder: the CSR pulls (no buckets); None: the pipeline's default
-        kw = {"buckets": dict(rows=True, buckets=True), "csr_rows": dict(rows=True, buckets=False),
-              None: {}}.get(path, dict(buckets=False))
+        kw = {"buckets": dict(rows=True, buckets=True), "buckets_norec": dict(rows=True, buckets=True, records=False),
+              "csr_rows": dict(rows=True, buckets=False), None: {}}.get(path, dict(buckets=False))
         pl = pipeline.FusedPipeline(B, maxp, N, base.im_size, base.bv_size, base.stride, Cb, Ci, dtype=tdt,
                                     dual=True, **kw)
         if path is not None:
-            assert pl.buckets == (path == "buckets")
+            assert pl.buckets == path.startswith("buckets")
         pl.csr_path = codes.get(path, L.CSR_AUTO)
         d_bev, d_img = torch.empty_like(tb), torch.empty_like(ti)
         pl.step(pts, vox, off, P, tb, ti)
@@ -705,13 +705,15 @@ def _ragged_pipeline_run(cfg, sizes, dtype, paths, channels=None, frames=None):
                                          ("f32", 3, 5), ("bf16", 8, 24), ("f32", 64, 128), ("f32", 4, 6)])
 def test_bucket_pulls_ragged_batch(dtype, cb, ci):
     """The bucketed step (shpl_build_index_buckets -> shpl_build_csr_buckets -> shpl_pull_pair:
-    both CSRs in one launch, both pulls in one launch, forward then gradients) at config 3's
+    both CSRs in one launch, both pulls in one launch -- over per-destination records, k_rows2r, and
+    without them, k_rows2 --, forward then gradients) at config 3's
     geometry over a ragged batch -- no points,
     one point, no survivor, one survivor among 14 points (the dgemv projection order: no
     bucket, the entry read from the index arrays), chunk-straddling and full frames --
     bitwise against the oracle and against the range CSR + k_rows path, for every lane
     group width (G = 8 .. 64) and the unvectorised form (3 / 5 and 4 / 6 f32 channels)."""
-    _ragged_pipeline_run(3, [0, 1, -40, 1025, 20000, 2], dtype, ["buckets", "csr_rows"], channels=(cb, ci))
+    _ragged_pipeline_run(3, [0, 1, -40, 1025, 20000, 2], dtype, ["buckets", "buckets_norec", "csr_rows"],
+                         channels=(cb, ci))
 
 
 def test_bucket_pulls_long_runs():
@@ -730,7 +732,7 @@ def test_bucket_pulls_long_runs():
     frames = [heavy, synth.make_frame(synth.FrameSpec(3000, base.im_size, base.bv_size, base.stride, 32, 32),
                                       seed=5, n_outside=int(rng.integers(1, 50))), mixed]
     for dtype in ("f32", "bf16"):
-        _ragged_pipeline_run(3, None, dtype, ["buckets"], channels=(32, 32), frames=frames)
+        _ragged_pipeline_run(3, None, dtype, ["buckets", "buckets_norec"], channels=(32, 32), frames=frames)
 
 
 def test_pipeline_ragged_batch_every_csr_path():
