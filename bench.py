@@ -105,6 +105,10 @@ def parse():
                     help="conv workload: training step (batch-statistics BatchNorm forward + the whole backward: "
                          "BN/ReLU, input and weight gradients of the conv, the pooled channels' gradient to the image)")
     ap.add_argument("--scan-points", type=int, default=120000, help="points per velodyne scan (frames)")
+    ap.add_argument("--maps-form", default="f64", choices=["f64", "bev_input"],
+                    help="frames: the BEV maps as the reference's f64 height / density maps, or as the network's "
+                         "f32 BEV input (np.dstack of the maps as its tf.float32 placeholder holds them: half the "
+                         "bytes; shpl_bev_input)")
     ap.add_argument("--maps-after", default="chain", choices=["stream", "chain"],
                     help="frames: write the BEV maps after the streaming pass (side stream) or after the CSR "
                          "(index chain)")
@@ -648,6 +652,7 @@ def run_frames(args, world, rank, dev):
                                 synth.HEIGHT_LO, synth.HEIGHT_HI, synth.NUM_SLICES, (1, 1), C, C, device=dev,
                                 max_points_per_frame=fr.max_points)
     pl.maps_after = args.maps_after
+    pl.maps_form = args.maps_form
     bev = sd.fill_features(torch.empty((F, pl.Hb, pl.Wb, C), device=dev), fids, 5)
     img = sd.fill_features(torch.empty((F, pl.Hi, pl.Wi, C), device=dev), fids, 6)
     side = torch.cuda.Stream(device=dev)
@@ -680,11 +685,12 @@ def run_frames(args, world, rank, dev):
     # the BEV maps out (5 height slices + density, f64), voxel indices + unique points (40 B/voxel), the index
     # (~16 B/entry out, 40 B/point in), the CSR (~40 B/entry) and the layer
     n_maps = synth.NUM_SLICES + 1
-    step_bytes = (nbytes + 16 * int(fr.total_points) + 2 * 24 * n_cam + F * pl.Hb * pl.Wb * n_maps * 8
+    map_esz = 8 if args.maps_form == "f64" else 4
+    step_bytes = (nbytes + 16 * int(fr.total_points) + 2 * 24 * n_cam + F * pl.Hb * pl.Wb * n_maps * map_esz
                   + 40 * n_vox + 40 * n_vox + 56 * nnz)
     step_gbs = step_bytes / (elapsed / args.steps) / 1e9
     # PMC (scripts/r02_pmc.sh TAG=frames, traffic.py step frames_F64 ...), when measured on this library
-    traffic, traffic_note, tj = traffic_lookup(f"frames_F{F}")
+    traffic, traffic_note, tj = traffic_lookup(f"frames_F{F}" if args.maps_form == "f64" else f"frames_bev_input_F{F}")
     step_traffic = tj.get("step_bytes_all_kernels") if tj else None
     checks = checksum_report(f"frames_{args.scan_points}", sd.frame_checksums(pl.bv_fused), fids, dev, rank, args)
     comm = sd.comm_report(dev)
@@ -706,8 +712,11 @@ def run_frames(args, world, rank, dev):
             "data": "synthetic (seeded 64-beam-like velodyne scans, KITTI calib; no dataset on the box)",
             "config": {"workload": (f"frames: {args.scan_points} pts/scan -> {n_cam / F:.0f} FOV pts -> "
                                     f"{n_vox / F:.0f} BEV voxel pts -> {nnz / F:.0f} M entries; BEV "
-                                    f"{pl.Hb}x{pl.Wb}x{C} (5 slices + density maps), img {pl.Hi}x{pl.Wi}x{C}, "
-                                    "img->BEV fused layer"),
+                                    f"{pl.Hb}x{pl.Wb}x{C} (5 slices + density maps"
+                                    + (", f64" if args.maps_form == "f64" else
+                                       " as the network's f32 BEV input [F,nz,nx,6]") + f"), img "
+                                    f"{pl.Hi}x{pl.Wi}x{C}, img->BEV fused layer"),
+                       "maps_form": args.maps_form,
                        "global_batch": F * world, "frames_per_gpu_per_step": F,
                        "parallelism": f"frame-sharded x{world}"},
             "stages_ms": {k: round(v, 4) for k, v in stages.items()},

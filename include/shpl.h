@@ -191,6 +191,21 @@ int shpl_bev_maps(int n_frames, const int64_t *d_point_offsets, int64_t total_po
                   double *d_height_maps, double *d_density_map, int zero, const void *d_ws,
                   size_t ws_bytes, void *stream);
 
+/* The network's BEV input from the same sorted words as shpl_bev_maps: the
+ * tensor KittiDataset.load_samples stacks, bev_input = np.dstack((*height_maps,
+ * density_map)) (avod/avod/datasets/kitti/kitti_dataset.py:368), as the
+ * tf.float32 placeholder receives it (rpn_model.py:185-186, filled at :823):
+ * d_bev_input [n_frames, nz, nx, num_slices + 1] f32, element (f, y, x, v) =
+ * (float) height map v (v < num_slices) or the density map (v = num_slices) of
+ * shpl_bev_maps at (f, y, x), rounded to nearest once -- the feed's cast. Half
+ * the bytes of the f64 maps, already in the layout the BEV feature extractor
+ * reads. Zero-filled first. Same arguments as shpl_bev_maps otherwise. */
+int shpl_bev_input(int n_frames, const int64_t *d_point_offsets, int64_t total_points, const void *d_points,
+                   int points_dtype, const double *d_planes, const double *area_extents, double voxel_size,
+                   int num_slices, const double *slice_lo, const double *slice_hi, double density_lo,
+                   double density_hi, double height_per_division, const double *density_table,
+                   float *d_bev_input, const void *d_ws, size_t ws_bytes, void *stream);
+
 /* MV3D_TF's producer point_cloud_2_top_sparse
  * (MV3D_TF_release/lib/utils/construct_voxel.py:37-162), n_frames at once:
  *   d_points     [N, point_stride] f64 camera-frame points (x, y, z, ...)

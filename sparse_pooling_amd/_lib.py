@@ -130,6 +130,7 @@ def _declare(lib):
         "shpl_bev_slices": (i32, [i32, p, p, i64, p, i32, p, p, d, i32, p, p, d, d, d, p, p, p, p, p, p,
                                   p, p, sz, p]),
         "shpl_bev_maps": (i32, [i32, p, i64, p, i32, p, p, d, i32, p, p, d, d, d, p, p, p, i32, p, sz, p]),
+        "shpl_bev_input": (i32, [i32, p, i64, p, i32, p, p, d, i32, p, p, d, d, d, p, p, p, sz, p]),
         "shpl_velo_workspace_bytes": (i32, [i32, i64, psz]),
         "shpl_velo_to_cam": (i32, [i32, p, i64, p, p, p, p, d, p, p, p, p, p, sz, p]),
         "shpl_gen_index": (i32, [i64, p, i32, p, i32, i64, p, d, d, p, p, i64, p, p, sz, p]),

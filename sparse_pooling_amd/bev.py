@@ -64,6 +64,19 @@ class BevBatch:
         self.height_maps, self.density_map = height_maps, density_map
         return height_maps, density_map
 
+    def write_bev_input(self, bev_input):
+        """The network's BEV input of this batch (shpl_bev_input) into the given [F,nz,nx,S+1] f32 tensor:
+        np.dstack((*height_maps, density_map)) (kitti_dataset.py:368) as the tf.float32 placeholder holds it
+        (each map value rounded to f32 once), from the voxelizer's sorted words like write_maps."""
+        c = self._call
+        assert bev_input.dtype == torch.float32 and bev_input.is_contiguous()
+        L.check(L.lib().shpl_bev_input(c["F"], L.ptr(c["off"]), c["N"], L.ptr(c["pts"]), L.F64, L.ptr(c["planes"]),
+                                       c["p"](c["ext"]), c["vs"], c["S"], c["p"](c["lo"]), c["p"](c["hi"]), c["hlo"],
+                                       c["hhi"], c["hpd"], c["p"](c["table"]), L.ptr(bev_input), L.ptr(c["ws"]),
+                                       c["ws"].numel(), L.stream_of(c["pts"].device)), "shpl_bev_input")
+        self.bev_input = bev_input
+        return bev_input
+
 
 def bev_slices_batch(points, point_offsets, planes, area_extents, voxel_size, height_lo, height_hi,
                      num_slices, norm_value=np.log(16), maps=True, ws=None, point_counts=None):

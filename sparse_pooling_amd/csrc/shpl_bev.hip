@@ -184,11 +184,13 @@ __global__ __launch_bounds__(BEV_BLOCK) void k_bev_frame(BevGeom g, const int64_
 // (shpl_bev_maps): the same values step 5 above writes, by a grid of BEV_MAP_SPLIT workgroups per
 // frame over its words -- a cell's first word writes its height (slices) or count-derived density.
 constexpr int BEV_MAP_SPLIT = 16;
+// bev_in (shpl_bev_input): the same values, rounded to f32, interleaved [F, nz, nx, S + 1] instead of the
+// planar f64 maps (channel v < S: height slice v, channel S: density).
 template <typename PT>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_bev_maps(BevGeom g, const int64_t *pt_off, const void *pts,
                                                         const double *planes, const uint64_t *srt,
                                                         int64_t ent_per_point, const int32_t *frame_nent,
-                                                        double *hmaps, double *dmap) {
+                                                        double *hmaps, double *dmap, float *bev_in) {
     const int f = blockIdx.y;
     const int64_t p0 = pt_off[f], t0 = p0 * ent_per_point;
     const int32_t n_ent = frame_nent[f];
@@ -204,17 +206,22 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bev_maps(BevGeom g, const int64_
         const int64_t cell = (int64_t)key - (int64_t)v * n_cells;
         const int xi = (int)(cell / g.nz), zi = (int)(cell - (int64_t)xi * g.nz);
         const int64_t pix = (int64_t)(g.nz - 1 - zi) * g.nx + xi;  // np.flip(map.T, axis=0)
+        const int64_t in_at = ((int64_t)f * n_cells + pix) * (g.num_slices + 1) + v;  // bev_in element
         if (v < g.num_slices) {
-            if (!hmaps) continue;
+            if (!hmaps && !bev_in) continue;
             double x, y, z;
             Pt<PT>::load(pts, p0 + (int64_t)(uint32_t)me, x, y, z);
             const double dist =
                 __ddiv_rn(__dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(a, x), __dmul_rn(b, y)), __dmul_rn(c, z)), d), norm);
-            hmaps[((int64_t)f * g.num_slices + v) * n_cells + pix] = __ddiv_rn(__dsub_rn(dist, g.lo[v]), g.hpd);
-        } else if (dmap) {
+            const double h = __ddiv_rn(__dsub_rn(dist, g.lo[v]), g.hpd);
+            if (hmaps) hmaps[((int64_t)f * g.num_slices + v) * n_cells + pix] = h;
+            if (bev_in) bev_in[in_at] = __double2float_rn(h);
+        } else if (dmap || bev_in) {
             int32_t n = 1;
             while (s + n < n_ent && (srt[t0 + s + n] >> KEY_SHIFT) == key) ++n;
-            dmap[(int64_t)f * n_cells + pix] = n < 16 ? g.dens[n] : 1.0;
+            const double dn = n < 16 ? g.dens[n] : 1.0;
+            if (dmap) dmap[(int64_t)f * n_cells + pix] = dn;
+            if (bev_in) bev_in[in_at] = __double2float_rn(dn);
         }
     }
 }
@@ -344,7 +351,36 @@ extern "C" int shpl_bev_maps(int n_frames, const int64_t *d_point_offsets, int64
     }
     if (!d_height_maps && !d_density_map) return SHPL_OK;
     hipLaunchKernelGGL(k_bev_maps<double>, dim3(BEV_MAP_SPLIT, n_frames), dim3(SHPL_BLOCK), 0, s, g, d_point_offsets,
-                       d_points, d_planes, srt, (int64_t)(num_slices + 1), nent, d_height_maps, d_density_map);
+                       d_points, d_planes, srt, (int64_t)(num_slices + 1), nent, d_height_maps, d_density_map,
+                       (float *)nullptr);
+    SHPL_LAUNCH_CHECK();
+    return SHPL_OK;
+}
+
+extern "C" int shpl_bev_input(int n_frames, const int64_t *d_point_offsets, int64_t total_points, const void *d_points,
+                              int points_dtype, const double *d_planes, const double *area_extents, double voxel_size,
+                              int num_slices, const double *slice_lo, const double *slice_hi, double density_lo,
+                              double density_hi, double height_per_division, const double *density_table,
+                              float *d_bev_input, const void *d_ws, size_t ws_bytes, void *stream) {
+    if (n_frames < 1 || !d_point_offsets || !d_planes || !d_ws || !d_bev_input) return SHPL_ERR_ARG;
+    if (points_dtype != SHPL_F64 || (total_points > 0 && !d_points)) return SHPL_ERR_ARG;
+    if (total_points < 0 || total_points >= ((int64_t)1 << 31) || n_frames > BEV_MAX_FRAMES) return SHPL_ERR_BAD_SHAPE;
+    BevGeom g;
+    const int rc = bev_geom(area_extents, voxel_size, num_slices, slice_lo, slice_hi, density_lo, density_hi,
+                            height_per_division, density_table, g);
+    if (rc) return rc;
+    size_t need;
+    shpl_bev_workspace_bytes(total_points, num_slices, &need);
+    if (need > ws_bytes) return SHPL_ERR_WORKSPACE;
+    const size_t half = bev_half_bytes(total_points, num_slices);
+    const uint64_t *srt = (const uint64_t *)((const char *)d_ws + half);
+    const int32_t *nent = (const int32_t *)((const char *)d_ws + 2 * half);
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t per_map = (int64_t)g.nx * g.nz;
+    SHPL_HIP_CHECK(zero_fill(d_bev_input, sizeof(float) * (size_t)(per_map * (num_slices + 1) * n_frames), s));
+    hipLaunchKernelGGL(k_bev_maps<double>, dim3(BEV_MAP_SPLIT, n_frames), dim3(SHPL_BLOCK), 0, s, g, d_point_offsets,
+                       d_points, d_planes, srt, (int64_t)(num_slices + 1), nent, (double *)nullptr, (double *)nullptr,
+                       d_bev_input);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
 }

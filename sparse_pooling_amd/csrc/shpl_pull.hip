@@ -779,19 +779,27 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_rows2r(const RowsSide s0, const 
     for (;;) {
         const int64_t nx = it + W;
         const bool more = nx < items;  // wave-uniform
-        Rec nr;
-        typename C::raw_t nav = C::zero();
-        bool nlive = false, nsecond = false;
-        int64_t nrow = 0;
-        if (more) rec_fetch<T, VEC, G>(s0, s1, items0, nx, nr, nav, nlive, nrow, nsecond);
         const int32_t len = cur.end - cur.first;
         int32_t wlen = len;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) wlen = max(wlen, __shfl_xor(wlen, o, 64));
         const Feat &f = second ? s1.f : s0.f;
         if (wlen <= REC_N) {
+            // the next item's records in flight while this one's feature rows load
+            Rec nr;
+            typename C::raw_t nav = C::zero();
+            bool nlive = false, nsecond = false;
+            int64_t nrow = 0;
+            if (more) rec_fetch<T, VEC, G>(s0, s1, items0, nx, nr, nav, nlive, nrow, nsecond);
             row_short<T, VEC, G>(f, row, live, cur, av);
+            if (!more) break;
+            cur = nr;
+            av = nav;
+            live = nlive;
+            row = nrow;
+            second = nsecond;
         } else {
+            // a long run: the walk of k_rows (no prefetch: its registers stay free for the walk)
             const bool p0 = live && f.mode == SHPL_OUT_CONCAT && (uint32_t)lg < f.cpass;
             typename C::raw_t pv = C::zero();
             if (p0) pv = C::load_nt(reinterpret_cast<const T *>(f.pass) + f.pass_off +
@@ -800,14 +808,10 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_rows2r(const RowsSide s0, const 
                 row_walk<T, VEC, true, G>(s1.f, s1.e, row, live, cur.first, cur.end, p0, pv, av);
             else
                 row_walk<T, VEC, false, G>(s0.f, s0.e, row, live, cur.first, cur.end, p0, pv, av);
+            if (!more) break;
+            rec_fetch<T, VEC, G>(s0, s1, items0, nx, cur, av, live, row, second);
         }
-        if (!more) break;
         it = nx;
-        cur = nr;
-        av = nav;
-        live = nlive;
-        row = nrow;
-        second = nsecond;
     }
 }
 

@@ -462,13 +462,36 @@ class FramePipeline(FusedPipeline):
     # index chain after the CSR, beside the end of the streaming pass (step 2.66-2.67 ms); "stream": on the
     # side stream after the streaming pass (2.68-2.69 ms; profiles/r03_frames_maps_ab.log)
     maps_after = "chain"
+    # the form of the BEV maps the steps write: "f64" -- the reference's height / density maps
+    # (BevSlices.generate_bev, [F,S,nz,nx] + [F,nz,nx] f64); "bev_input" -- the network's BEV input as its
+    # tf.float32 placeholder receives it, np.dstack((*height_maps, density_map)) (kitti_dataset.py:368) rounded
+    # to f32 once ([F,nz,nx,S+1]; shpl_bev_input): half the bytes, the layout the BEV extractor reads
+    maps_form = "f64"
 
     def build_bev(self, points, point_offsets, planes, point_counts=None, maps=None):
         from . import bev as _bev
+        want = self.maps if maps is None else maps
         self.bev = _bev.bev_slices_batch(points, point_offsets, planes, *self.bev_args,
-                                         maps=self.maps if maps is None else maps, ws=self.bev_ws,
+                                         maps=want and self.maps_form == "f64", ws=self.bev_ws,
                                          point_counts=point_counts)
+        if want and self.maps_form == "bev_input":
+            self.bev.write_bev_input(self._input_buffer())
         return self.bev
+
+    def _input_buffer(self):
+        """The step's BEV input tensor [F,nz,nx,S+1] f32 (maps_form "bev_input"), allocated once."""
+        if getattr(self, "_bev_input", None) is None:
+            from . import bev as _bev
+            area, vs, _, _, S = self.bev_args
+            nx, nz = _bev.grid_divisions(area, vs)
+            self._bev_input = torch.empty((self.B, nz, nx, int(S) + 1), dtype=torch.float32, device=self.dev)
+        return self._bev_input
+
+    def _write_maps(self, b):
+        if self.maps_form == "bev_input":
+            b.write_bev_input(self._input_buffer())
+        else:
+            b.write_maps(*self._map_buffers(), zero=True)
 
     def _map_buffers(self):
         """The step's height / density maps, allocated once (velo_step writes them off the chain)."""
@@ -517,7 +540,7 @@ class FramePipeline(FusedPipeline):
             if self.maps and self.maps_after == "stream":
                 side.wait_event(bev_done)
                 with torch.cuda.stream(side):
-                    b.write_maps(*self._map_buffers(), zero=True)
+                    self._write_maps(b)
             if events:
                 events[4].record(main)
             self.build_index(b.pts_in_voxel, b.voxel_indices, frames.point_offsets, frames.P2,
@@ -528,7 +551,7 @@ class FramePipeline(FusedPipeline):
             if events:
                 events[6].record(main)
             if self.maps and self.maps_after == "chain":
-                b.write_maps(*self._map_buffers(), zero=True)
+                self._write_maps(b)
             main.wait_event(dense_done)  # the sparse pass overwrites rows the streaming pass wrote
             if events:
                 events[7].record(main)

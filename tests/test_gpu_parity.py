@@ -785,6 +785,15 @@ def test_bev_slices_batch_vs_oracle():
         np.testing.assert_array_equal(_np(b.height_maps[f]), hm)
         np.testing.assert_array_equal(_np(b.density_map[f]), dm)
     assert int(b.err.item()) == 0
+    # the network's BEV input (shpl_bev_input): kitti_dataset.py:368's dstack of the maps, as its tf.float32
+    # placeholder holds it (one rounding), bitwise
+    S = synth.NUM_SLICES
+    bin_ = b.write_bev_input(torch.full((3,) + tuple(b.density_map.shape[1:]) + (S + 1,), float("nan"),
+                                        dtype=torch.float32, device=DEV))
+    torch.cuda.synchronize()
+    for f in range(3):
+        want = np.dstack((*_np(b.height_maps[f]), _np(b.density_map[f]))).astype(np.float32)
+        np.testing.assert_array_equal(_np(bin_[f]).view(np.uint32), want.view(np.uint32))
 
 
 def test_points_to_fused_layer_pipeline():
@@ -1003,10 +1012,12 @@ def test_velodyne_to_fused_layer_pipeline(kitti_dir):
         _close_and_exact(iout[f:f + 1], ei)
 
 
-def test_velodyne_pipeline_overlapped_maps_equal_sequential(kitti_dir):
+@pytest.mark.parametrize("form", ["f64", "bev_input"])
+def test_velodyne_pipeline_overlapped_maps_equal_sequential(kitti_dir, form):
     """velo_step with a side stream (the streaming pass beside the index chain, the BEV maps written
-    after it by shpl_bev_maps from the voxelizer's sorted words) == the sequential step (maps written
-    by shpl_bev_slices itself), bitwise: layer outputs, height and density maps."""
+    after it by shpl_bev_maps / shpl_bev_input from the voxelizer's sorted words) == the sequential step
+    (maps written by shpl_bev_slices itself, or its bev_input), bitwise: layer outputs and the maps in
+    either form (f64 height + density maps; the f32 network input)."""
     from sparse_pooling_amd import kitti, pipeline
     d, g = kitti_dir
     shapes = [tuple(g["7_image_shape"]), tuple(g["8_image_shape"])]
@@ -1018,13 +1029,15 @@ def test_velodyne_pipeline_overlapped_maps_equal_sequential(kitti_dir):
         pl = pipeline.FramePipeline(2, fr.total_points, im_size, synth.AREA_EXTENTS, synth.VOXEL_SIZE,
                                     synth.HEIGHT_LO, synth.HEIGHT_HI, synth.NUM_SLICES, stride, C, C, dual=True,
                                     max_points_per_frame=fr.max_points)
+        pl.maps_form = form
         bev = torch.from_numpy(synth.make_features((2, pl.Hb, pl.Wb, C), 3)).to(DEV)
         img = torch.from_numpy(synth.make_features((2, pl.Hi, pl.Wi, C), 4)).to(DEV)
         for _ in range(2):  # the second step reuses every workspace
             pl.velo_step(fr, bev, img, side=side)
         torch.cuda.synchronize()
         assert int(pl.err.item()) == 0 and int(pl.bev.err.item()) == 0
-        outs.append([_np(t).copy() for t in (pl.bv_fused, pl.img_fused, pl.bev.height_maps, pl.bev.density_map)])
+        maps = (pl.bev.height_maps, pl.bev.density_map) if form == "f64" else (pl.bev.bev_input,)
+        outs.append([_np(t).copy() for t in (pl.bv_fused, pl.img_fused, *maps)])
     for a, b in zip(*outs):
         np.testing.assert_array_equal(a.view(np.uint8), b.view(np.uint8))
 
