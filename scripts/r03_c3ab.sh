@@ -14,6 +14,12 @@ for v in ${VARIANTS:-default} ${VARIANTS:-default}; do
   tail -1 gpurun_out/c3ab_$v.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$v', d['ms_per_step'], r['frac'], r.get('k_sparse_ms'), r.get('backward_ms'), d['frame_checksums']['match_n1'])"
 done
 unset SHPL_LIB
+if [ -n "$FRAMES" ]; then  # the raw-scan step with the BEV maps in each form
+  for m in f64 bev_input f64 bev_input; do
+    timeout -k 10 300 python bench.py --workload frames --steps 20 --no-cpu-baseline --maps-form $m > gpurun_out/fr_$m.log 2>&1 || { tail -5 gpurun_out/fr_$m.log; exit 1; }
+    tail -1 gpurun_out/fr_$m.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('frames $m', d['ms_per_step'], d['roofline']['frac'], d['roofline']['step_frac'], d['stages_ms']['k_dense_ms'], d['frame_checksums']['match_n1'])"
+  done
+fi
 if [ -n "$PROF" ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3ab -o run --output-format csv -- \
     python3 bench.py --config 3 --steps 50 --warmup 2 --no-cpu-baseline > gpurun_out/prof_c3ab.log 2>&1 || exit 1
