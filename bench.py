@@ -87,8 +87,8 @@ def parse():
     ap.add_argument("--no-buckets", action="store_true",
                     help="row-keyed layers (config 3): range CSRs + one k_rows launch per pull on two streams "
                          "instead of the index build's buckets + one shpl_pull_buckets launch per pull pair")
-    ap.add_argument("--no-records", action="store_true",
-                    help="bucketed config 3: CSRs without per-destination records (k_rows2 instead of k_rows2r)")
+    ap.add_argument("--records", action="store_true",
+                    help="bucketed config 3: CSRs with per-destination records (k_rows2r instead of k_rows2)")
     ap.add_argument("--no-riders", action="store_true",
                     help="bucketed config 3: copy the forward's pass-through halves with their own launches before the "
                          "index build instead of as extra workgroups of the index launches")
@@ -394,7 +394,7 @@ def main():
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, dev)
     pl = pipeline.FusedPipeline(F, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev,
                                 spec.c_img, dtype=dtype, dual=dual, device=dev,
-                                buckets=False if args.no_buckets else None, records=not args.no_records)
+                                buckets=False if args.no_buckets else None, records=args.records)
     Hb, Wb = spec.bev_feat_hw
     Hi, Wi = spec.img_feat_hw
     feats = lambda shape, seed: sd.fill_features(torch.empty(shape, dtype=dtype, device=dev), fids, seed)  # noqa

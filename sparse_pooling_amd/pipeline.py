@@ -29,7 +29,7 @@ class FusedPipeline:
 
     def __init__(self, n_frames, max_points_per_frame, total_points, im_size, bv_size, stride,
                  c_bev, c_img, dtype=torch.float32, device="cuda", dual=False, rows=None, live=False,
-                 buckets=None, records=True):
+                 buckets=None, records=False):
         """live: the sparse passes walk each frame's live entries (shpl_csr frame layout) instead of the
         whole capacity -- for capacities far above the entry counts (FramePipeline: raw-scan slots per
         voxel point); at config 2 (capacity = entries) the capacity walk is faster (2.22 vs 2.24 ms).

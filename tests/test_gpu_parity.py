@@ -679,7 +679,8 @@ def _ragged_pipeline_run(cfg, sizes, dtype, paths, channels=None, frames=None):
              "bucket": L.CSR_BUCKET}
     for path in paths:
         # a named CSR builder: the CSR pulls (no buckets); None: the pipeline's default
-        kw = {"buckets": dict(rows=True, buckets=True), "buckets_norec": dict(rows=True, buckets=True, records=False),
+        kw = {"buckets": dict(rows=True, buckets=True, records=True),
+              "buckets_norec": dict(rows=True, buckets=True, records=False),
               "csr_rows": dict(rows=True, buckets=False), None: {}}.get(path, dict(buckets=False))
         pl = pipeline.FusedPipeline(B, maxp, N, base.im_size, base.bv_size, base.stride, Cb, Ci, dtype=tdt,
                                     dual=True, **kw)
