@@ -7,9 +7,11 @@ export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -k "${TESTS:-bucket or backward}" > gpurun_out/c3ab_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/c3ab_tests.log; [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/c3ab_tests.log | head -30; exit $rc; }
 for v in ${VARIANTS:-default} ${VARIANTS:-default}; do
-  # x-<name>: the default library with bench flag --no-<name>; y-<name>: with --<name>
-  x=""; case "$v" in x-*) x="--no-${v#x-}";; y-*) x="--${v#y-}";; esac
-  if [ "$v" = default ] || [ -n "$x" ]; then unset SHPL_LIB; else export SHPL_LIB=$PWD/sparse_pooling_amd/variants/$v.so; fi
+  # x-<name>: the default library with bench flag --no-<name>; y-<name>: with --<name>;
+  # <lib>+<flag>: variants/<lib>.so with --<flag>
+  x=""; lib="$v"
+  case "$v" in x-*) x="--no-${v#x-}"; lib=default;; y-*) x="--${v#y-}"; lib=default;; *+*) x="--${v#*+}"; lib="${v%%+*}";; esac
+  if [ "$lib" = default ]; then unset SHPL_LIB; else export SHPL_LIB=$PWD/sparse_pooling_amd/variants/$lib.so; fi
   timeout -k 10 300 python bench.py --config 3 --steps 200 --no-cpu-baseline $x $BENCH_EXTRA > gpurun_out/c3ab_$v.log 2>&1 || { tail -5 gpurun_out/c3ab_$v.log; exit 1; }
   tail -1 gpurun_out/c3ab_$v.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$v', d['ms_per_step'], r['frac'], r.get('k_sparse_ms'), r.get('backward_ms'), d['frame_checksums']['match_n1'])"
 done

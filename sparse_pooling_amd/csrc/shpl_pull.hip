@@ -678,7 +678,8 @@ __global__ __launch_bounds__(SHPL_BLOCK) __attribute__((amdgpu_waves_per_eu(SHPL
 // (an accumulator that starts at +0 never becomes -0, so 0 + p and p add alike).
 constexpr int REC_N = 3;
 #ifndef SHPL_ROWS2R_GRID
-#define SHPL_ROWS2R_GRID 1280  // workgroups of k_rows2r at most (4 waves each: ~the chip's resident waves)
+// workgroups of k_rows2r at most (4 waves each); past the item count every wave takes one item (no prefetch)
+#define SHPL_ROWS2R_GRID 0x7fffffff
 #endif
 
 struct Rec {
