@@ -816,6 +816,38 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_rows2r(const RowsSide s0, const 
     }
 }
 
+// The same over the records with one item per wave and no prefetch (the form used unless SHPL_ROWS2R_GRID
+// caps the grid): the record replaces the range load, so a wave whose rows hold at most REC_N entries
+// spends two dependent round trips (record, feature rows) instead of three.
+template <typename T, int VEC, int G>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_rows2s(const RowsSide s0, const RowsSide s1, int64_t items0,
+                                                       int64_t items) {
+    typedef Chunk<T, VEC> C;
+    const int lane = threadIdx.x & 63, lg = lane & (G - 1);
+    const int64_t it = (int64_t)blockIdx.x * (SHPL_BLOCK / SHPL_WAVE) + (threadIdx.x >> 6);
+    if (it >= items) return;  // wave-uniform
+    Rec cur;
+    typename C::raw_t av = C::zero();
+    bool live, second;
+    int64_t row;
+    rec_fetch<T, VEC, G>(s0, s1, items0, it, cur, av, live, row, second);
+    int32_t wlen = cur.end - cur.first;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wlen = max(wlen, __shfl_xor(wlen, o, 64));
+    const Feat &f = second ? s1.f : s0.f;
+    if (wlen <= REC_N) {
+        row_short<T, VEC, G>(f, row, live, cur, av);
+        return;
+    }
+    const bool p0 = live && f.mode == SHPL_OUT_CONCAT && (uint32_t)lg < f.cpass;
+    typename C::raw_t pv = C::zero();
+    if (p0) pv = C::load_nt(reinterpret_cast<const T *>(f.pass) + f.pass_off + (row * f.pass_stride + (int64_t)lg * VEC));
+    if (second)
+        row_walk<T, VEC, true, G>(s1.f, s1.e, row, live, cur.first, cur.end, p0, pv, av);
+    else
+        row_walk<T, VEC, false, G>(s0.f, s0.e, row, live, cur.first, cur.end, p0, pv, av);
+}
+
 bool aligned(const void *ptr, int64_t a) { return ((uintptr_t)ptr) % (uintptr_t)a == 0; }
 
 struct Plan {
@@ -1052,9 +1084,15 @@ int pair_t(RowsSide s[2], int G, hipStream_t st) {
         const int64_t rpw = SHPL_WAVE / G;
         const int64_t items0 = (s[0].n_rows + rpw - 1) / rpw, items = items0 + (s[1].n_rows + rpw - 1) / rpw;
         int64_t grid = (items + SHPL_BLOCK / SHPL_WAVE - 1) / (SHPL_BLOCK / SHPL_WAVE);
-        if (grid > SHPL_ROWS2R_GRID) grid = SHPL_ROWS2R_GRID;
-#define SHPL_ROWS2R(GG) \
-    hipLaunchKernelGGL((k_rows2r<T, VEC, GG>), dim3((unsigned)grid), dim3(SHPL_BLOCK), 0, st, s[0], s[1], items0, items)
+        const bool persistent = grid > SHPL_ROWS2R_GRID;
+        if (persistent) grid = SHPL_ROWS2R_GRID;
+#define SHPL_ROWS2R(GG)                                                                                          \
+    if (persistent)                                                                                              \
+        hipLaunchKernelGGL((k_rows2r<T, VEC, GG>), dim3((unsigned)grid), dim3(SHPL_BLOCK), 0, st, s[0], s[1], items0, \
+                           items);                                                                               \
+    else                                                                                                         \
+        hipLaunchKernelGGL((k_rows2s<T, VEC, GG>), dim3((unsigned)grid), dim3(SHPL_BLOCK), 0, st, s[0], s[1], items0, \
+                           items)
         switch (G) {
             case 8: SHPL_ROWS2R(8); break;
             case 16: SHPL_ROWS2R(16); break;
