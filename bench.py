@@ -88,10 +88,13 @@ def parse():
                     help="row-keyed layers (config 3): range CSRs + one k_rows launch per pull on two streams "
                          "instead of the index build's buckets + one shpl_pull_buckets launch per pull pair")
     ap.add_argument("--records", action="store_true",
-                    help="bucketed config 3: CSRs with per-destination records (k_rows2r instead of k_rows2)")
+                    help="bucketed config 3: CSRs with per-destination records (k_rows2s instead of k_rows2)")
     ap.add_argument("--no-riders", action="store_true",
                     help="bucketed config 3: copy the forward's pass-through halves with their own launches before the "
                          "index build instead of as extra workgroups of the index launches")
+    ap.add_argument("--graph-steps", type=int, default=1,
+                    help="layer workloads: consecutive steps captured in one HIP graph (the timed loop replays it "
+                         "steps / graph-steps times; --steps must divide)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step eagerly instead of replaying one captured HIP graph of it")
     ap.add_argument("--workload", default="layer", choices=["layer", "frames", "conv"],
@@ -465,8 +468,11 @@ def main():
             gstream = torch.cuda.Stream(device=dev)
             gstream.wait_stream(torch.cuda.current_stream(dev))
             graph = torch.cuda.CUDAGraph()
+            if args.steps % args.graph_steps:
+                sys.exit(f"bench.py: --steps {args.steps} is not a multiple of --graph-steps {args.graph_steps}")
             with torch.cuda.graph(graph, stream=gstream):
-                step()
+                for _ in range(args.graph_steps):
+                    step()
             graph.replay()
             torch.cuda.synchronize()
         except Exception as e:  # noqa: BLE001 -- report and run eagerly
@@ -478,14 +484,15 @@ def main():
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(n_ev)]
     issue_ms = None
     if graph is not None:
-        elapsed = sd.timed(lambda k: graph.replay(), args.steps, device=dev)
+        replays = args.steps // args.graph_steps
+        elapsed = sd.timed(lambda k: graph.replay(), replays, device=dev)
         # host cost of one replay: issue the replays without waiting (after the timed loop); well
         # under the step at every config (0.03 ms at config 3), so the timed loop is not launch-bound
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(replays):
             graph.replay()
-        issue_ms = 1e3 * (time.perf_counter() - t0) / args.steps
+        issue_ms = 1e3 * (time.perf_counter() - t0) / replays
         torch.cuda.synchronize()
         for k in range(n_ev):
             step(evs[k])
@@ -558,6 +565,7 @@ def main():
                 "unique_cells_rank0": u_cell,
                 "overlap_index_build": not args.no_overlap,
                 "hip_graph": graph is not None,
+                **({"steps_per_graph": args.graph_steps} if graph is not None and args.graph_steps > 1 else {}),
                 **({"graph_issue_ms_per_replay": round(issue_ms, 4)} if issue_ms is not None else {}),
                 **({"graph_note": graph_note} if graph_note else {}),
                 "parallelism": f"frame-sharded x{world}",

@@ -300,8 +300,9 @@ typedef struct {
     int64_t n_frames;
     /* optional [n_keys][8] int32, filled by shpl_build_csr_buckets (the builder's maps: one column per
        entry): per destination {first, end, then (source row, f32 weight bits) of its first three
-       entries}. When every pull of shpl_pull_pair has it, the pair runs persistent waves that load
-       the next rows' records while walking the current ones (k_rows2r). Other builders ignore it. */
+       entries}. When every pull of shpl_pull_pair has it, the pair reads the records instead of the
+       ranges (k_rows2s: a run of at most three entries needs no index-word load). Other builders
+       ignore it. */
     int32_t *key_rec;
 } shpl_csr;
 #define SHPL_LIVE_MAX_FRAMES 1024

@@ -304,7 +304,10 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr, Bkt 
             s_tb[K * BK_MAX_RANGES + q] = tot;
             s_tb[2 * BK_MAX_RANGES + K * BK_MAX_RANGES + q] = bef;
         }
-        for (int i = threadIdx.x; i < 2 * (IDX_BLOCK / 64) * BK_MAX_RANGES; i += IDX_BLOCK) (&s_w[0][0][0])[i] = 0;
+        for (int i = threadIdx.x; i < 2 * (IDX_BLOCK / 64) * bk.nrmax; i += IDX_BLOCK) {  // the ranges in use
+            const int kw = i / bk.nrmax;
+            s_w[kw / (IDX_BLOCK / 64)][kw % (IDX_BLOCK / 64)][i - kw * bk.nrmax] = 0;
+        }
     }
     // the frame's AUX count picks the KEEP count (and the stage's product order)
     const int32_t *aux_c = fr.chunk_kept + ((int64_t)2 * fr.n_frames + f) * fr.n_chunks;

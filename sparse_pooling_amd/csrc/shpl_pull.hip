@@ -651,7 +651,7 @@ struct RowsSide {
     Ents e;
     const int32_t *key_range;
     int64_t n_rows, blocks;
-    const int32_t *key_rec;  // optional per-destination records (k_rows2r)
+    const int32_t *key_rec;  // optional per-destination records (k_rows2s)
 };
 
 #ifndef SHPL_ROWS2_WPE
@@ -666,21 +666,16 @@ __global__ __launch_bounds__(SHPL_BLOCK) __attribute__((amdgpu_waves_per_eu(SHPL
         rows_body<T, VEC, true, G>(s1.f, s1.e, s1.key_range, s1.n_rows, (int64_t)blockIdx.x - s0.blocks);
 }
 
-// ------------------------------------------------------------- k_rows2r
+// ------------------------------------------------------------- k_rows2s
 // The pull pair over CSRs that also carry per-destination records (shpl_csr.key_rec, written by
 // shpl_build_csr_buckets): 8 ints per destination, {first, end, then (source row, weight bits) of its
-// first REC_N entries}. Waves are persistent over "items" (64 / G rows each, both pulls' items in one
-// list) and load the next item's records while they walk the current one, so a wave whose rows all
-// hold at most REC_N entries spends ONE dependent round trip per item -- the feature rows -- where
-// k_rows spends three (range, index words, feature rows). Longer runs take row_walk from the
-// record's (first, end). Every entry of a builder-made map has a column of its own (the identity), so
-// TF's per-column partials are single products and the short form's plain sum is bitwise the same
-// (an accumulator that starts at +0 never becomes -0, so 0 + p and p add alike).
+// first REC_N entries}; "items" of 64 / G rows, both pulls' items in one list. Longer runs take
+// row_walk from the record's (first, end). Every entry of a builder-made map has a column of its own
+// (the identity), so TF's per-column partials are single products and the short form's plain sum is
+// bitwise the same (an accumulator that starts at +0 never becomes -0, so 0 + p and p add alike).
+// Measured slower than k_rows2 at config 3 (0.109 vs 0.107 ms per step; a persistent form that
+// prefetched the next item's records: 0.125 ms; profiles/r03_c3_records_riders_ab.log): opt-in.
 constexpr int REC_N = 3;
-#ifndef SHPL_ROWS2R_GRID
-// workgroups of k_rows2r at most (4 waves each); past the item count every wave takes one item (no prefetch)
-#define SHPL_ROWS2R_GRID 0x7fffffff
-#endif
 
 struct Rec {
     int32_t first, end, s[REC_N];
@@ -764,61 +759,8 @@ __device__ __forceinline__ void row_short(const Feat &f, int64_t row, bool live,
     }
 }
 
-template <typename T, int VEC, int G>
-__global__ __launch_bounds__(SHPL_BLOCK) void k_rows2r(const RowsSide s0, const RowsSide s1, int64_t items0,
-                                                       int64_t items) {
-    typedef Chunk<T, VEC> C;
-    const int lane = threadIdx.x & 63, lg = lane & (G - 1);
-    const int64_t W = (int64_t)gridDim.x * (SHPL_BLOCK / SHPL_WAVE);
-    int64_t it = (int64_t)blockIdx.x * (SHPL_BLOCK / SHPL_WAVE) + (threadIdx.x >> 6);
-    if (it >= items) return;  // wave-uniform
-    Rec cur;
-    typename C::raw_t av = C::zero();
-    bool live, second;
-    int64_t row;
-    rec_fetch<T, VEC, G>(s0, s1, items0, it, cur, av, live, row, second);
-    for (;;) {
-        const int64_t nx = it + W;
-        const bool more = nx < items;  // wave-uniform
-        const int32_t len = cur.end - cur.first;
-        int32_t wlen = len;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) wlen = max(wlen, __shfl_xor(wlen, o, 64));
-        const Feat &f = second ? s1.f : s0.f;
-        if (wlen <= REC_N) {
-            // the next item's records in flight while this one's feature rows load
-            Rec nr;
-            typename C::raw_t nav = C::zero();
-            bool nlive = false, nsecond = false;
-            int64_t nrow = 0;
-            if (more) rec_fetch<T, VEC, G>(s0, s1, items0, nx, nr, nav, nlive, nrow, nsecond);
-            row_short<T, VEC, G>(f, row, live, cur, av);
-            if (!more) break;
-            cur = nr;
-            av = nav;
-            live = nlive;
-            row = nrow;
-            second = nsecond;
-        } else {
-            // a long run: the walk of k_rows (no prefetch: its registers stay free for the walk)
-            const bool p0 = live && f.mode == SHPL_OUT_CONCAT && (uint32_t)lg < f.cpass;
-            typename C::raw_t pv = C::zero();
-            if (p0) pv = C::load_nt(reinterpret_cast<const T *>(f.pass) + f.pass_off +
-                                    (row * f.pass_stride + (int64_t)lg * VEC));
-            if (second)
-                row_walk<T, VEC, true, G>(s1.f, s1.e, row, live, cur.first, cur.end, p0, pv, av);
-            else
-                row_walk<T, VEC, false, G>(s0.f, s0.e, row, live, cur.first, cur.end, p0, pv, av);
-            if (!more) break;
-            rec_fetch<T, VEC, G>(s0, s1, items0, nx, cur, av, live, row, second);
-        }
-        it = nx;
-    }
-}
-
-// The same over the records with one item per wave and no prefetch (the form used unless SHPL_ROWS2R_GRID
-// caps the grid): the record replaces the range load, so a wave whose rows hold at most REC_N entries
-// spends two dependent round trips (record, feature rows) instead of three.
+// One item (64 / G rows) per wave: the record replaces the range load, so a wave whose rows hold at most
+// REC_N entries spends two dependent round trips (record, feature rows) instead of three.
 template <typename T, int VEC, int G>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_rows2s(const RowsSide s0, const RowsSide s1, int64_t items0,
                                                        int64_t items) {
@@ -1083,16 +1025,10 @@ int pair_t(RowsSide s[2], int G, hipStream_t st) {
     if (recs) {  // items = waves' worth of rows (64 / G each), both pulls in one list
         const int64_t rpw = SHPL_WAVE / G;
         const int64_t items0 = (s[0].n_rows + rpw - 1) / rpw, items = items0 + (s[1].n_rows + rpw - 1) / rpw;
-        int64_t grid = (items + SHPL_BLOCK / SHPL_WAVE - 1) / (SHPL_BLOCK / SHPL_WAVE);
-        const bool persistent = grid > SHPL_ROWS2R_GRID;
-        if (persistent) grid = SHPL_ROWS2R_GRID;
+        const int64_t grid = (items + SHPL_BLOCK / SHPL_WAVE - 1) / (SHPL_BLOCK / SHPL_WAVE);
 #define SHPL_ROWS2R(GG)                                                                                          \
-    if (persistent)                                                                                              \
-        hipLaunchKernelGGL((k_rows2r<T, VEC, GG>), dim3((unsigned)grid), dim3(SHPL_BLOCK), 0, st, s[0], s[1], items0, \
-                           items);                                                                               \
-    else                                                                                                         \
-        hipLaunchKernelGGL((k_rows2s<T, VEC, GG>), dim3((unsigned)grid), dim3(SHPL_BLOCK), 0, st, s[0], s[1], items0, \
-                           items)
+    hipLaunchKernelGGL((k_rows2s<T, VEC, GG>), dim3((unsigned)grid), dim3(SHPL_BLOCK), 0, st, s[0], s[1], items0, \
+                       items)
         switch (G) {
             case 8: SHPL_ROWS2R(8); break;
             case 16: SHPL_ROWS2R(16); break;

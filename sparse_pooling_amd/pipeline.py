@@ -37,7 +37,7 @@ class FusedPipeline:
         (shpl_build_index_buckets), one launch sorts both CSRs out of them (shpl_build_csr_buckets) and
         each pull pair is one row-keyed launch (shpl_pull_pair), all on one stream; the forward's
         pass-through halves ride the index launches. records (bucketed): the CSRs also carry
-        per-destination records and the pull pairs run persistent waves over them (k_rows2r).
+        per-destination records and the pull pairs run persistent waves over them (k_rows2s).
         rows without buckets: the range CSRs (one launch per key) + one k_rows launch per pull,
         on two streams."""
         dev = torch.device(device)
@@ -70,7 +70,7 @@ class FusedPipeline:
         self.frame_off = torch.empty(self.B + 1, dtype=torch.int64, device=dev)
         self.err = torch.zeros(1, **i32)
         self.index_ws = L.workspace(L.index_ws_bytes(self.B, self.max_points), dev)
-        # rows pulls: with key_range; bucketed: with the per-destination records too (k_rows2r), unless records=False
+        # rows pulls: with key_range; bucketed: with the per-destination records too (k_rows2s), unless records=False
         rec = self.buckets and records
         self.csr = L.Csr(self.n_cells, self.N, dev, with_col=False, key_range=self.rows,
                          key_rec=rec)  # BEV-cell CSR (img -> BEV)

@@ -706,7 +706,7 @@ def _ragged_pipeline_run(cfg, sizes, dtype, paths, channels=None, frames=None):
                                          ("f32", 3, 5), ("bf16", 8, 24), ("f32", 64, 128), ("f32", 4, 6)])
 def test_bucket_pulls_ragged_batch(dtype, cb, ci):
     """The bucketed step (shpl_build_index_buckets -> shpl_build_csr_buckets -> shpl_pull_pair:
-    both CSRs in one launch, both pulls in one launch -- over per-destination records, k_rows2r, and
+    both CSRs in one launch, both pulls in one launch -- over per-destination records, k_rows2s, and
     without them, k_rows2 --, forward then gradients) at config 3's
     geometry over a ragged batch -- no points,
     one point, no survivor, one survivor among 14 points (the dgemv projection order: no
