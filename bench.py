@@ -92,9 +92,11 @@ def parse():
     ap.add_argument("--no-riders", action="store_true",
                     help="bucketed config 3: copy the forward's pass-through halves with their own launches before the "
                          "index build instead of as extra workgroups of the index launches")
-    ap.add_argument("--graph-steps", type=int, default=1,
+    ap.add_argument("--graph-steps", type=int, default=None,
                     help="layer workloads: consecutive steps captured in one HIP graph (the timed loop replays it "
-                         "steps / graph-steps times; --steps must divide)")
+                         "steps / graph-steps times; --steps must divide). Default: 4 at config 3 when --steps "
+                         "divides (0.107 -> 0.103 ms per step: the replay boundary's ~8 us once per 4 steps), "
+                         "else 1 (config 2: no change, profiles/r03_graph_steps_ab.log)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step eagerly instead of replaying one captured HIP graph of it")
     ap.add_argument("--workload", default="layer", choices=["layer", "frames", "conv"],
@@ -386,6 +388,8 @@ def main():
         return
 
     cfg = args.config
+    if args.graph_steps is None:
+        args.graph_steps = 4 if cfg == 3 and args.steps % 4 == 0 else 1
     spec = synth.CONFIGS[cfg]
     dual = cfg in (3, 5)
     backward = cfg == 3
