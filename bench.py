@@ -86,7 +86,7 @@ def parse():
                     help="layer workloads: force the CSR builder (shpl_build_csr_path; A/B measurements)")
     ap.add_argument("--no-buckets", action="store_true",
                     help="row-keyed layers (config 3): range CSRs + one k_rows launch per pull on two streams "
-                         "instead of the index build's buckets + one shpl_pull_buckets launch per pull pair")
+                         "instead of the index build's buckets, one CSR launch and one shpl_pull_pair launch per pull pair")
     ap.add_argument("--records", action="store_true",
                     help="bucketed config 3: CSRs with per-destination records (k_rows2s instead of k_rows2)")
     ap.add_argument("--no-riders", action="store_true",
@@ -97,6 +97,8 @@ def parse():
                          "steps / graph-steps times; --steps must divide). Default: 4 at config 3 when --steps "
                          "divides (0.107 -> 0.103 ms per step: the replay boundary's ~8 us once per 4 steps), "
                          "else 1 (config 2: no change, profiles/r03_graph_steps_ab.log)")
+    ap.add_argument("--no-pool-report", action="store_true",
+                    help="config 2: skip the separate pool_fwd measurement (PMC passes count the step's launches only)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step eagerly instead of replaying one captured HIP graph of it")
     ap.add_argument("--workload", default="layer", choices=["layer", "frames", "conv"],
@@ -533,7 +535,8 @@ def main():
             # (first k_dense start -> last k_sparse end) instead of the summed durations
             layer_ms = sum(e[0].elapsed_time(e[3]) for e in evs) / args_steps_ev + bwd_ms
     achieved = nbytes / (layer_ms * 1e-3) / 1e9
-    pool = pool_fwd_report(pl, img, spec, F, u_pix, nnz, esz, dev) if cfg == 2 and not grouped else None
+    pool = (pool_fwd_report(pl, img, spec, F, u_pix, nnz, esz, dev)
+            if cfg == 2 and not grouped and not args.no_pool_report else None)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -582,8 +585,10 @@ def main():
                           ("SHPL layer pulls: k_dense (concat stream) + k_sparse (pooled gather); achieved over "
                            + ("the layer's window (first k_dense start to last k_sparse end: the cell-keyed gathers "
                               "run beside img_fused's stream)" if interleaved else "their summed durations")
-                           + ("; each pull pair is ONE shpl_pull_buckets launch over the index build's "
-                              "destination buckets (one stream), timed as the sparse and backward brackets"
+                           + ("; bucketed one-stream step: the forward bracket spans the whole forward "
+                              "(index + buckets with the pass-through copies riding its launches, both CSRs, the "
+                              "pooled pull pair), the backward bracket the gradient pull pair -- every kernel of "
+                              "the step, so achieved = the step's algorithmic bytes over all of its kernel time"
                               if pl.buckets else
                               "; step pulls are row-keyed k_rows (one launch per pull), timed as the sparse and "
                               "backward brackets" if pl.rows else "")),

@@ -258,17 +258,14 @@ class FusedPipeline:
             # (1 launch), both pooled halves (1 launch). (The copies on `side` beside the index chain instead
             # cost 20-30 us of cross-queue waits per graph replay at config 3: profiles/r03_bpull_ab.log.)
             main = torch.cuda.current_stream(self.dev)
-            if events:
-                events[0].record(main)
+            if events:  # no streaming half of its own: the forward bracket [2, 3) is the whole forward
+                for e in events[:3]:
+                    e.record(main)
             riders = self.copy_riders_ok(bev, img)
             if not riders:
                 self._pass_copies(bev, img)
-            if events:
-                events[1].record(main)
             self.build_index(points, voxels, point_offsets, P, mval, pass_copies=(bev, img) if riders else None)
             self.build_csr()
-            if events:
-                events[2].record(main)
             self._pull_pair(*self._pooled_descs(bev, img))
             if events:
                 events[3].record(main)
