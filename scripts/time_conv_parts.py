@@ -6,6 +6,7 @@ current stream. SHPL_LIB selects a variant build (A/B of compile-time switches).
     python scripts/time_conv_parts.py [--frames 64] [--reps 10]
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -46,6 +47,9 @@ def main():
     out["wgrad_two_sources_ms"] = timed(lambda: fc.conv3x3_wgrad(a, gy, b=b), args.reps)
     flops = 2.0 * 9 * (2 * C) * C * B * H * W
     out.update({k.replace("_ms", "_tflops"): round(flops / (v * 1e-3) / 1e12, 1) for k, v in list(out.items())})
+    dw = fc.conv3x3_wgrad(a, gy, b=b)
+    torch.cuda.synchronize()
+    out["wgrad_sha"] = hashlib.sha256(dw.float().cpu().numpy().tobytes()).hexdigest()[:16]  # bitwise A/B check
     out["lib"] = os.environ.get("SHPL_LIB", "default")
     print(json.dumps(out))
 

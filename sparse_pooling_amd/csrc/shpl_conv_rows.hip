@@ -620,15 +620,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS_WP
 #ifndef SHPL_WG_PROBE
 #define SHPL_WG_PROBE 0
 #endif
+#ifndef SHPL_WG_PAIR
+#define SHPL_WG_PAIR 1
+#endif
 
 constexpr int WX_PIECES = HWD * 4;                  // X row: 34 pixels x 4 pieces of 8 channels
 constexpr int WG_PIECES = TW * 4;                   // G row: 32 pixels x 4 pieces
-constexpr int WSLOT = (WX_PIECES + WG_PIECES) * 16;  // 4224 B
+constexpr int WXB = WX_PIECES * 16, WGB = WG_PIECES * 16;  // 2176 + 2048 B
 constexpr int WNX = (WX_PIECES + 63) / 64, WTX = WX_PIECES - 64 * (WNX - 1);  // 3 DMAs, the last one 8 lanes
 constexpr int WNG = WG_PIECES / 64;                                         // 2 DMAs
-constexpr int WNDMA = WNX + WNG;
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+// PAIR: two waves per workgroup, input tiles 2p and 2p+1 of one output tile. They share each staged G row
+// (wave w DMAs its half, pixels 16w .. 16w+15) and run in step: one s_barrier per row, after the ring wait.
+// A ring slot then holds [X of wave 0][X of wave 1][G]; 4 slots, so that the row staged at step j (j + 3) goes
+// into the slot of row j - 1, which both waves finished reading before step j's barrier. Alone (an odd number
+// of input tiles) a wave DMAs the whole G row, and 3 slots suffice (row j + 3 into row j's own slot).
+template <bool PAIR>
+struct WgRing {
+    static constexpr int NSLOT = PAIR ? 4 : 3;
+    static constexpr int SLOT = (PAIR ? 2 : 1) * WXB + WGB;
+    static constexpr int GOFF = (PAIR ? 2 : 1) * WXB;
+    static constexpr int NG = PAIR ? 1 : WNG;  // G DMAs per wave
+    static constexpr int NDMA = WNX + NG;
+};
 
 // The 32x16 operand fragment at pixel p0 (+ 8h + 4t + q) of an LDS image [pixel][64 B]: two transposed reads
 // (lane 4q+p of 16-lane group g: row q, channels 16 (g & 1) + 4p .. + 3; lane i of the group gets channel
@@ -646,12 +662,13 @@ __device__ __forceinline__ bf16x8 tr_frag(const uint8_t *lb) {
 
 // pooled: X is the tile of the compact pooled rows (k_pool_runs): offx holds pixel << 16 | channel (-1: outside),
 // cell pixel px of the row holds run  first + popc(occ below bit px)  when bit px of occ is set, else zeros.
-template <bool CMP>
+// `xslot` is the wave's X part of the slot, `gslot` the G part (PAIR: this wave's half of it).
+template <bool CMP, bool PAIR>
 __device__ __forceinline__ void wstage(const WgRowArgs &r, const uint16_t *xsrc, int64_t xstride, int64_t pix0,
                                        bool xok, int64_t gpix, bool gok, const uint32_t (&offx)[WNX],
-                                       const uint32_t (&offg)[WNG], uint8_t *slot, int lane, bool pooled,
-                                       uint64_t occ, int32_t first) {
-    // one set of X DMAs whichever the source (selects, no branch: every path issues WNDMA DMAs)
+                                       const uint32_t (&offg)[WgRing<PAIR>::NG], uint8_t *xslot, uint8_t *gslot,
+                                       int lane, bool pooled, uint64_t occ, int32_t first) {
+    // one set of X DMAs whichever the source (selects, no branch: every path issues NDMA DMAs)
     const bool cmp = CMP && pooled;
     const i32x4 rx = rsrc(cmp ? static_cast<const void *>(r.cmp) : static_cast<const void *>(xsrc + pix0 * xstride),
                           xok ? OOB : 0u);
@@ -665,22 +682,25 @@ __device__ __forceinline__ void wstage(const WgRowArgs &r, const uint16_t *xsrc,
             const int rank = first + (int)__popcll(occ & ((1ull << px) - 1));
             o = hit ? (uint32_t)((rank * r.cmp_stride + (e & 0xffff)) * 2) : OOB;
         }
-        if (i < WNX - 1 || lane < WTX) dma16(rx, o, slot + i * 1024);
+        if (i < WNX - 1 || lane < WTX) dma16(rx, o, xslot + i * 1024);
     }
     const i32x4 rg = rsrc(r.gy + gpix * r.gy_stride, gok ? OOB : 0u);
 #pragma unroll
-    for (int i = 0; i < WNG; ++i) dma16(rg, offg[i], slot + WX_PIECES * 16 + i * 1024);
+    for (int i = 0; i < WgRing<PAIR>::NG; ++i) dma16(rg, offg[i], gslot + i * 1024);
 }
 
-// One input row j of the band (slot U = j % 3): 16 transposed reads, 18 MFMAs, then row j + 3 staged.
-template <bool CMP, int U>
+// One input row j of the band (slot U = j % NSLOT): 16 transposed reads, 18 MFMAs, then row j + 3 staged.
+template <bool CMP, bool PAIR, int U>
 __device__ __forceinline__ void wstep(const WgRowArgs &r, f32x16 (&acc)[9], bf16x8 (&g1)[2], bf16x8 (&g2)[2],
-                                      uint8_t *s_ring, const uint8_t *lb, const uint16_t *xsrc, int64_t xstride,
-                                      int64_t frame_row0, int x0, int ya, int n_in, int n_out, int j,
-                                      const uint32_t (&offx)[WNX], const uint32_t (&offg)[WNG], int lane,
-                                      bool pooled, const uint64_t *s_occ, const int32_t *s_first) {
-    SHPL_RING_WAIT(WNDMA * (RING - 1));  // rows j+1, j+2 may still be in flight
-    const uint8_t *xs = lb + U * WSLOT, *gs = xs + WX_PIECES * 16;
+                                      uint8_t *s_ring, const uint8_t *lb, int xoff, int goff_w,
+                                      const uint16_t *xsrc, int64_t xstride, int64_t frame_row0, int x0, int ya,
+                                      int n_in, int n_out, int j, const uint32_t (&offx)[WNX],
+                                      const uint32_t (&offg)[WgRing<PAIR>::NG], int lane, bool pooled,
+                                      const uint64_t *s_occ, const int32_t *s_first) {
+    typedef WgRing<PAIR> R;
+    SHPL_RING_WAIT(R::NDMA * (RING - 1));  // rows j+1, j+2 may still be in flight
+    if (PAIR) asm volatile("s_barrier" ::: "memory");  // the other wave's half of G row j has landed too
+    const uint8_t *xs = lb + U * R::SLOT + xoff, *gs = lb + U * R::SLOT + R::GOFF;
     bf16x8 g0[2];
     g0[0] = tr_frag<0>(gs);
     g0[1] = tr_frag<16>(gs);
@@ -700,7 +720,9 @@ __device__ __forceinline__ void wstep(const WgRowArgs &r, f32x16 (&acc)[9], bf16
         g2[s] = g1[s];
         g1[s] = g0[s];
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done before the DMAs refill it
+    // the slot's reads are done before the DMAs refill it (PAIR: before the next barrier, after which the
+    // other wave refills this slot)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const int jn = j + RING, y = ya - 1 + jn;
     if (SHPL_WG_PROBE == 1) return;  // timing probe: no staging in the loop (wrong results)
     uint64_t occ = 0;
@@ -709,22 +731,28 @@ __device__ __forceinline__ void wstep(const WgRowArgs &r, f32x16 (&acc)[9], bf16
         occ = s_occ[jn];
         first = s_first[jn];
     }
-    wstage<CMP>(r, xsrc, xstride, frame_row0 + (int64_t)y * r.w + x0 - 1, jn < n_in && y >= 0 && y < r.h,
-                frame_row0 + (int64_t)(ya + jn) * r.w + x0, jn < n_out, offx, offg, s_ring + U * WSLOT, lane, pooled,
-                occ, first);
+    uint8_t *ns = s_ring + ((U + RING) % R::NSLOT) * R::SLOT;
+    wstage<CMP, PAIR>(r, xsrc, xstride, frame_row0 + (int64_t)y * r.w + x0 - 1, jn < n_in && y >= 0 && y < r.h,
+                      frame_row0 + (int64_t)(ya + jn) * r.w + x0, jn < n_out, offx, offg, ns + xoff,
+                      ns + R::GOFF + goff_w, lane, pooled, occ, first);
 }
 
-template <bool CMP>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS_WPE, SHPL_ROWS_WPE))) void k_wgrad_rows(
-    const WgRowArgs r) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING * WSLOT];
-    __shared__ uint64_t s_occ[CMP ? 64 : 1];  // pooled tile: the band rows' occupancy windows (as k_conv_rows)
-    __shared__ int32_t s_first[CMP ? 64 : 1];
-    const int lane = threadIdx.x;
-    const int n_tiles = r.n_cit * r.n_cot, total = r.n_groups * n_tiles;
-    // (group, output tile, input tile), input tiles fastest (they share the G rows), each XCD one contiguous run
+template <bool CMP, bool PAIR>
+__global__ __launch_bounds__(PAIR ? 128 : 64) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS_WPE, SHPL_ROWS_WPE)))
+void k_wgrad_rows(const WgRowArgs r) {
+    typedef WgRing<PAIR> R;
+    constexpr int NW = PAIR ? 2 : 1;
+    __shared__ __attribute__((aligned(16))) uint8_t s_ring[R::NSLOT * R::SLOT];
+    __shared__ uint64_t s_occ_all[NW][CMP ? 64 : 1];  // pooled tile: the band rows' occupancy windows (as k_conv_rows)
+    __shared__ int32_t s_first_all[NW][CMP ? 64 : 1];
+    const int lane = threadIdx.x & 63, wv = PAIR ? (int)(threadIdx.x >> 6) : 0;
+    uint64_t *s_occ = s_occ_all[wv];
+    int32_t *s_first = s_first_all[wv];
+    const int n_cw = r.n_cit / NW;  // workgroups per (group, output tile)
+    const int total = r.n_groups * r.n_cot * n_cw;
+    // (group, output tile, input tiles), input tiles fastest (they share the G rows), each XCD one contiguous run
     const int wi = (int)xcd_block(blockIdx.x, total);
-    const int cit = wi % r.n_cit, cot = (wi / r.n_cit) % r.n_cot, grp = wi / n_tiles;
+    const int cit = (wi % n_cw) * NW + wv, cot = (wi / n_cw) % r.n_cot, grp = wi / (n_cw * r.n_cot);
     const int na = r.c_a / 32 + (r.c_a % 32 ? 1 : 0);  // input tiles of A (c_a % 32 == 0 when B is present)
     const bool from_a = cit < na;
     const uint16_t *xsrc = from_a ? r.a + cit * 32 : r.b + (cit - na) * 32;
@@ -739,6 +767,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS_WP
     // lane address part of the transposed reads: row q = (lane & 15) >> 2, channel 16 ((lane >> 4) & 1) + 4 (lane & 3),
     // pixel base 8 h (h = lane >> 5)
     const uint8_t *lb = s_ring + (8 * (lane >> 5) + ((lane & 15) >> 2)) * 64 + 32 * ((lane >> 4) & 1) + 8 * (lane & 3);
+    const int xoff = wv * WXB, goff_w = PAIR ? wv * 1024 : 0;
     f32x16 acc[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t)
@@ -751,7 +780,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS_WP
         const int x0 = strip * TW, ya = band * r.band;
         const int n_out = min(r.band, r.h - ya), n_in = n_out + 2;
         const int64_t frame_row0 = (int64_t)f * r.h * r.w;
-        uint32_t offx[WNX], offg[WNG];
+        uint32_t offx[WNX], offg[R::NG];
 #pragma unroll
         for (int i = 0; i < WNX; ++i) {
             const int pc = 64 * i + lane, px = pc >> 2, cq = pc & 3, x = x0 - 1 + px;
@@ -778,35 +807,42 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS_WP
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own LDS writes, in order
         }
 #pragma unroll
-        for (int i = 0; i < WNG; ++i) {
-            const int pc = 64 * i + lane, px = pc >> 2, cq = pc & 3, x = x0 + px;
+        for (int i = 0; i < R::NG; ++i) {
+            const int pc = 64 * (PAIR ? wv : i) + lane, px = pc >> 2, cq = pc & 3, x = x0 + px;
             offg[i] = x < r.w && 8 * cq < cg ? (uint32_t)((px * (int)r.gy_stride + 8 * cq) * 2) : OOB;
         }
 #pragma unroll
         for (int j = 0; j < RING; ++j) {
             const int y = ya - 1 + j;
-            wstage<CMP>(rr, xsrc, xstride, frame_row0 + (int64_t)y * r.w + x0 - 1, j < n_in && y >= 0 && y < r.h,
-                        frame_row0 + (int64_t)(ya + j) * r.w + x0, j < n_out, offx, offg, s_ring + j * WSLOT, lane,
-                        pooled, pooled ? s_occ[j] : 0, pooled ? s_first[j] : 0);
+            uint8_t *sl = s_ring + j * R::SLOT;
+            wstage<CMP, PAIR>(rr, xsrc, xstride, frame_row0 + (int64_t)y * r.w + x0 - 1,
+                              j < n_in && y >= 0 && y < r.h, frame_row0 + (int64_t)(ya + j) * r.w + x0, j < n_out,
+                              offx, offg, sl + xoff, sl + R::GOFF + goff_w, lane, pooled, pooled ? s_occ[j] : 0,
+                              pooled ? s_first[j] : 0);
         }
         bf16x8 g1[2], g2[2];
 #pragma unroll
         for (int s = 0; s < 2; ++s)
 #pragma unroll
             for (int i = 0; i < 8; ++i) g1[s][i] = g2[s][i] = (__bf16)0.0f;
-        for (int j = 0; j < n_in; j += RING) {
-#define SHPL_WROWS_STEP(UU)                                                                                  \
-    if (j + UU >= n_in) break;                                                                               \
-    wstep<CMP, UU>(rr, acc, g1, g2, s_ring, lb, xsrc, xstride, frame_row0, x0, ya, n_in, n_out, j + UU, offx, offg, \
-                   lane, pooled, s_occ, s_first);
+        for (int j = 0; j < n_in; j += R::NSLOT) {
+#define SHPL_WROWS_STEP(UU)                                                                                      \
+    if (UU < R::NSLOT) {                                                                                         \
+        if (j + UU >= n_in) break;                                                                               \
+        wstep<CMP, PAIR, UU % R::NSLOT>(rr, acc, g1, g2, s_ring, lb, xoff, goff_w, xsrc, xstride, frame_row0, x0, \
+                                        ya, n_in, n_out, j + UU, offx, offg, lane, pooled, s_occ, s_first);       \
+    }
             SHPL_WROWS_STEP(0)
             SHPL_WROWS_STEP(1)
             SHPL_WROWS_STEP(2)
+            SHPL_WROWS_STEP(3)
 #undef SHPL_WROWS_STEP
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing DMAs land before the next item's prologue
+        // PAIR: both waves are done with the item's slots before either stages the next item's rows into them
+        if (PAIR) asm volatile("s_barrier" ::: "memory");
     }
-    // partial [group][cot][cit][tap][co][ci]: lane (co = lane & 31, h) holds ci 8 (i >> 2) + 4 h + (i & 3)
+// partial [group][cot][cit][tap][co][ci]: lane (co = lane & 31, h) holds ci 8 (i >> 2) + 4 h + (i & 3)
     float *out = r.part + (((int64_t)grp * r.n_cot + cot) * r.n_cit + cit) * (9 * 1024) + (lane & 31) * 32 +
                  4 * (lane >> 5);
 #pragma unroll
@@ -957,11 +993,21 @@ void wgrad_sizes(int n_items, int c_a, int c_b, int c_out, int *n_groups, size_t
 }
 
 int wgrad_launch(const WgRowArgs &r, float *dw, double *part2, hipStream_t s) {
-    const int total = r.n_groups * r.n_cit * r.n_cot;
-    if (r.cmp)
-        hipLaunchKernelGGL(k_wgrad_rows<true>, dim3((unsigned)total), dim3(64), 0, s, r);
-    else
-        hipLaunchKernelGGL(k_wgrad_rows<false>, dim3((unsigned)total), dim3(64), 0, s, r);
+    // pairs of input tiles share their G rows (SHPL_WG_PAIR 0: one wave per input tile)
+    const bool pair = SHPL_WG_PAIR && r.n_cit % 2 == 0;
+    const int total = r.n_groups * r.n_cot * (pair ? r.n_cit / 2 : r.n_cit);
+    const dim3 grid((unsigned)total), block(pair ? 128 : 64);
+    if (r.cmp) {
+        if (pair)
+            hipLaunchKernelGGL((k_wgrad_rows<true, true>), grid, block, 0, s, r);
+        else
+            hipLaunchKernelGGL((k_wgrad_rows<true, false>), grid, block, 0, s, r);
+    } else {
+        if (pair)
+            hipLaunchKernelGGL((k_wgrad_rows<false, true>), grid, block, 0, s, r);
+        else
+            hipLaunchKernelGGL((k_wgrad_rows<false, false>), grid, block, 0, s, r);
+    }
     SHPL_LAUNCH_CHECK();
     const int64_t n_ent = (int64_t)r.n_cit * r.n_cot * 9 * 1024;
     const int n_chunks = (r.n_groups + WGC - 1) / WGC;
