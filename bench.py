@@ -116,6 +116,8 @@ def parse():
                     help="frames: the BEV maps as the reference's f64 height / density maps, or as the network's "
                          "f32 BEV input (np.dstack of the maps as its tf.float32 placeholder holds them: half the "
                          "bytes; shpl_bev_input)")
+    ap.add_argument("--dense-after", default="start", choices=["start", "velo", "bev", "csr"],
+                    help="frames workload: where the streaming pass starts beside the index chain")
     ap.add_argument("--maps-after", default="chain", choices=["stream", "chain"],
                     help="frames: write the BEV maps after the streaming pass (side stream) or after the CSR "
                          "(index chain)")
@@ -655,6 +657,7 @@ def cpu_baseline_frames(frames_np, calib, plane, im_size, c, budget_s):
                        f"frame; {os.cpu_count()} host cpus visible")}
 
 
+
 def run_frames(args, world, rank, dev):
     """Raw-scan workload: the whole per-frame SHPL path of kitti_dataset.py:285-379 +
     rpn_model.py's fused layer, from velodyne scans resident in HBM."""
@@ -669,6 +672,7 @@ def run_frames(args, world, rank, dev):
                                 synth.HEIGHT_LO, synth.HEIGHT_HI, synth.NUM_SLICES, (1, 1), C, C, device=dev,
                                 max_points_per_frame=fr.max_points)
     pl.maps_after = args.maps_after
+    pl.dense_after = args.dense_after
     pl.maps_form = args.maps_form
     bev = sd.fill_features(torch.empty((F, pl.Hb, pl.Wb, C), device=dev), fids, 5)
     img = sd.fill_features(torch.empty((F, pl.Hi, pl.Wi, C), device=dev), fids, 6)
@@ -734,6 +738,7 @@ def run_frames(args, world, rank, dev):
                                        " as the network's f32 BEV input [F,nz,nx,6]") + f"), img "
                                     f"{pl.Hi}x{pl.Wi}x{C}, img->BEV fused layer"),
                        "maps_form": args.maps_form,
+                       **({"dense_after": args.dense_after} if args.dense_after != "start" else {}),
                        "global_batch": F * world, "frames_per_gpu_per_step": F,
                        "parallelism": f"frame-sharded x{world}"},
             "stages_ms": {k: round(v, 4) for k, v in stages.items()},

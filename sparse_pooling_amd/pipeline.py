@@ -464,6 +464,9 @@ class FramePipeline(FusedPipeline):
     # tf.float32 placeholder receives it, np.dstack((*height_maps, density_map)) (kitti_dataset.py:368) rounded
     # to f32 once ([F,nz,nx,S+1]; shpl_bev_input): half the bytes, the layout the BEV extractor reads
     maps_form = "f64"
+    # where velo_step starts the streaming half: "start" (beside the whole index chain), or after the
+    # chain's "velo" / "bev" / "csr" stage (the chain then runs with the chip to itself until there)
+    dense_after = "start"
 
     def build_bev(self, points, point_offsets, planes, point_counts=None, maps=None):
         from . import bev as _bev
@@ -517,23 +520,33 @@ class FramePipeline(FusedPipeline):
             # voxelizer's sorted words (shpl_bev_maps): off the index chain, and streaming after the
             # stream instead of beside it
             main = torch.cuda.current_stream(self.dev)
-            side.wait_stream(main)
             dense_done, bev_done = torch.cuda.Event(), torch.cuda.Event()
-            with torch.cuda.stream(side):
-                if events:
-                    events[0].record(side)
-                self.layer_dense(bev_feat, img_feat)
-                dense_done.record(side)
-                if events:
-                    events[1].record(side)
+
+            def dense():  # the streaming half on `side`, after what `main` has issued so far
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    if events:
+                        events[0].record(side)
+                    self.layer_dense(bev_feat, img_feat)
+                    dense_done.record(side)
+                    if events:
+                        events[1].record(side)
+
+            at = self.dense_after
+            if at == "start":
+                dense()
             if events:
                 events[2].record(main)
             self._velo(frames)
             if events:
                 events[3].record(main)
+            if at == "velo":
+                dense()
             b = self.build_bev(self.velo.points, frames.point_offsets, frames.planes, self.velo.counts,
                                maps=False)
             bev_done.record(main)
+            if at == "bev":
+                dense()
             if self.maps and self.maps_after == "stream":
                 side.wait_event(bev_done)
                 with torch.cuda.stream(side):
@@ -547,6 +560,8 @@ class FramePipeline(FusedPipeline):
             self.build_csr()
             if events:
                 events[6].record(main)
+            if at == "csr":
+                dense()
             if self.maps and self.maps_after == "chain":
                 self._write_maps(b)
             main.wait_event(dense_done)  # the sparse pass overwrites rows the streaming pass wrote
