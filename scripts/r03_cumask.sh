@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 3: the raw-scan step with the index chain on a CU-masked stream (bench --chain-cus K --cu-layout L
-# [--dense-excl]), f32 BEV input.
+# [--dense-excl]), f32 BEV input. (The bench flags were removed after this A/B: profiles/r03_cumask_ab/summary.log.)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/cm; export TMPDIR=/tmp
 i=0
