@@ -1168,15 +1168,24 @@ struct BsIn {
     int64_t nnz_cap;
 };
 
+#ifndef SHPL_BSORT_ORDER
+#define SHPL_BSORT_ORDER 1  // k_bsort2 runs the pixel-keyed side's buckets first (0: cell-keyed first)
+#endif
 constexpr int BS_BLOCK = 1024;  // threads of a k_bsort2 workgroup (the horizon's 2 k-entry pixel buckets: 3 rounds)
 constexpr int BS_LCAP = 4096;   // bucket words staged in LDS with their source rows and values (48 KiB)
 
 __global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide s1) {
     __shared__ uint32_t one[1];
+#if SHPL_BSORT_ORDER
+    // the pixel-keyed buckets first (the horizon's heavy ones start early instead of forming the tail)
+    const bool second = (int64_t)blockIdx.x < s1.blocks;
+    const int64_t b = second ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - s1.blocks;
+#else
     const bool second = (int64_t)blockIdx.x >= s0.blocks;
+    const int64_t b = second ? (int64_t)blockIdx.x - s0.blocks : (int64_t)blockIdx.x;
+#endif
     const BsSide &sd = second ? s1 : s0;
     const int key = second ? 1 : 0;
-    const int64_t b = second ? (int64_t)blockIdx.x - s0.blocks : (int64_t)blockIdx.x;
     const int f = (int)(b / sd.nr), q = (int)(b - (int64_t)f * sd.nr);
     const int64_t p0 = in.frame_off[f], cap_end = in.frame_off[f + 1];
     int64_t nnz = in.frame_nnz[f];

@@ -654,16 +654,27 @@ struct RowsSide {
     const int32_t *key_rec;  // optional per-destination records (k_rows2s)
 };
 
+#ifndef SHPL_ROWS2_ORDER
+#define SHPL_ROWS2_ORDER 1  // the pixel-keyed side's blocks first in k_rows2 (0: cell-keyed first)
+#endif
 #ifndef SHPL_ROWS2_WPE
 #define SHPL_ROWS2_WPE 1  // amdgpu_waves_per_eu floor of k_rows2 (1: the compiler's choice)
 #endif
 template <typename T, int VEC, int G>
 __global__ __launch_bounds__(SHPL_BLOCK) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS2_WPE))) void k_rows2(
     const RowsSide s0, const RowsSide s1) {
+#if SHPL_ROWS2_ORDER
+    // the pixel-keyed pull's blocks first: its longer runs start early instead of forming the launch's tail
+    if ((int64_t)blockIdx.x < s1.blocks)
+        rows_body<T, VEC, true, G>(s1.f, s1.e, s1.key_range, s1.n_rows, blockIdx.x);
+    else
+        rows_body<T, VEC, false, G>(s0.f, s0.e, s0.key_range, s0.n_rows, (int64_t)blockIdx.x - s1.blocks);
+#else
     if ((int64_t)blockIdx.x < s0.blocks)
         rows_body<T, VEC, false, G>(s0.f, s0.e, s0.key_range, s0.n_rows, blockIdx.x);
     else
         rows_body<T, VEC, true, G>(s1.f, s1.e, s1.key_range, s1.n_rows, (int64_t)blockIdx.x - s0.blocks);
+#endif
 }
 
 // ------------------------------------------------------------- k_rows2s
