@@ -490,18 +490,23 @@ def main():
         evs = [new_events() for _ in range(n_ev)]
     else:
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(n_ev)]
-    issue_ms = None
+    issue_ms = replay_step_ms = None
     if graph is not None:
         replays = args.steps // args.graph_steps
         elapsed = sd.timed(lambda k: graph.replay(), replays, device=dev)
         # host cost of one replay: issue the replays without waiting (after the timed loop); well
         # under the step at every config (0.03 ms at config 3), so the timed loop is not launch-bound
         torch.cuda.synchronize()
+        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        r0.record()
         t0 = time.perf_counter()
         for _ in range(replays):
             graph.replay()
         issue_ms = 1e3 * (time.perf_counter() - t0) / replays
+        r1.record()
         torch.cuda.synchronize()
+        # the replayed step's device time by HIP events on the replay stream (every kernel back to back)
+        replay_step_ms = r0.elapsed_time(r1) / (replays * args.graph_steps)
         for k in range(n_ev):
             step(evs[k])
         torch.cuda.synchronize()
@@ -536,6 +541,12 @@ def main():
             # the cell-keyed sparse pass runs beside img_fused's dense pass: the layer's window
             # (first k_dense start -> last k_sparse end) instead of the summed durations
             layer_ms = sum(e[0].elapsed_time(e[3]) for e in evs) / args_steps_ev + bwd_ms
+    eager_ms = None
+    if getattr(pl, "buckets", False) and replay_step_ms is not None:
+        # the bucketed one-queue step: its brackets span every kernel of the step, and run eagerly they
+        # also hold the host's launch gaps between ~10 us kernels; the replayed step is the same kernels
+        # back to back (rocprof's per-kernel averages sum to it)
+        eager_ms, layer_ms = layer_ms, replay_step_ms
     achieved = nbytes / (layer_ms * 1e-3) / 1e9
     pool = (pool_fwd_report(pl, img, spec, F, u_pix, nnz, esz, dev)
             if cfg == 2 and not grouped and not args.no_pool_report else None)
@@ -590,7 +601,8 @@ def main():
                            + ("; bucketed one-stream step: the forward bracket spans the whole forward "
                               "(index + buckets with the pass-through copies riding its launches, both CSRs, the "
                               "pooled pull pair), the backward bracket the gradient pull pair -- every kernel of "
-                              "the step, so achieved = the step's algorithmic bytes over all of its kernel time"
+                              "the step, so achieved = the step's algorithmic bytes over all of its kernel time, timed as the replayed "
+                              "step (HIP events around the graph replays)"
                               if pl.buckets else
                               "; step pulls are row-keyed k_rows (one launch per pull), timed as the sparse and "
                               "backward brackets" if pl.rows else "")),
@@ -602,6 +614,8 @@ def main():
                 "traffic_note": traffic_note,
                 "algorithmic_bytes_per_launch": nbytes,
                 "kernel_ms": round(layer_ms, 4),
+                **({"kernel_ms_source": "HIP events around the graph replays (per step)",
+                    "eager_brackets_ms": round(eager_ms, 4)} if eager_ms is not None else {}),
                 "k_dense_ms": round(dense_ms, 4),
                 "k_sparse_ms": round(sparse_ms, 4),
                 "backward_ms": round(bwd_ms, 4),
