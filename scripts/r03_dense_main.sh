@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 3: configs 2 / 5 (and the N=8 rank shape) with the streaming half on the main queue and the index
-# chain on the side one (bench --dense-main 1) vs the round-2 layout; the pipeline parity tests first.
+# chain on the side one (bench --dense-main 1) vs the round-2 layout; the pipeline parity tests first. (The flag was removed after this A/B: profiles/r03_dense_main_ab/summary.log.)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/dm; export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dist.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread \
