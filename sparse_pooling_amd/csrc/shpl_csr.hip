@@ -1168,6 +1168,9 @@ struct BsIn {
     int64_t nnz_cap;
 };
 
+#ifndef SHPL_PIX_REV
+#define SHPL_PIX_REV 0  // 1: k_bsort2's pixel-keyed buckets in reverse order
+#endif
 #ifndef SHPL_BSORT_ORDER
 #define SHPL_BSORT_ORDER 1  // k_bsort2 runs the pixel-keyed side's buckets first (0: cell-keyed first)
 #endif
@@ -1179,7 +1182,8 @@ __global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide 
 #if SHPL_BSORT_ORDER
     // the pixel-keyed buckets first (the horizon's heavy ones start early instead of forming the tail)
     const bool second = (int64_t)blockIdx.x < s1.blocks;
-    const int64_t b = second ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - s1.blocks;
+    const int64_t b = second ? (SHPL_PIX_REV ? s1.blocks - 1 - (int64_t)blockIdx.x : (int64_t)blockIdx.x)
+                             : (int64_t)blockIdx.x - s1.blocks;
 #else
     const bool second = (int64_t)blockIdx.x >= s0.blocks;
     const int64_t b = second ? (int64_t)blockIdx.x - s0.blocks : (int64_t)blockIdx.x;

@@ -654,6 +654,9 @@ struct RowsSide {
     const int32_t *key_rec;  // optional per-destination records (k_rows2s)
 };
 
+#ifndef SHPL_PIX_REV
+#define SHPL_PIX_REV 0  // 1: the pixel-keyed side's rows (k_rows2) / buckets (k_bsort2) in reverse order
+#endif
 #ifndef SHPL_ROWS2_ORDER
 #define SHPL_ROWS2_ORDER 1  // the pixel-keyed side's blocks first in k_rows2 (0: cell-keyed first)
 #endif
@@ -666,7 +669,8 @@ __global__ __launch_bounds__(SHPL_BLOCK) __attribute__((amdgpu_waves_per_eu(SHPL
 #if SHPL_ROWS2_ORDER
     // the pixel-keyed pull's blocks first: its longer runs start early instead of forming the launch's tail
     if ((int64_t)blockIdx.x < s1.blocks)
-        rows_body<T, VEC, true, G>(s1.f, s1.e, s1.key_range, s1.n_rows, blockIdx.x);
+        rows_body<T, VEC, true, G>(s1.f, s1.e, s1.key_range, s1.n_rows,
+                                   SHPL_PIX_REV ? s1.blocks - 1 - (int64_t)blockIdx.x : (int64_t)blockIdx.x);
     else
         rows_body<T, VEC, false, G>(s0.f, s0.e, s0.key_range, s0.n_rows, (int64_t)blockIdx.x - s1.blocks);
 #else
