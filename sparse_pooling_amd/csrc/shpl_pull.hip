@@ -654,6 +654,9 @@ struct RowsSide {
     const int32_t *key_rec;  // optional per-destination records (k_rows2s)
 };
 
+#ifndef SHPL_CELL_REV
+#define SHPL_CELL_REV 0  // 1: k_rows2's cell-keyed rows in reverse order
+#endif
 #ifndef SHPL_PIX_REV
 #define SHPL_PIX_REV 0  // 1: the pixel-keyed side's rows (k_rows2) / buckets (k_bsort2) in reverse order
 #endif
@@ -672,7 +675,9 @@ __global__ __launch_bounds__(SHPL_BLOCK) __attribute__((amdgpu_waves_per_eu(SHPL
         rows_body<T, VEC, true, G>(s1.f, s1.e, s1.key_range, s1.n_rows,
                                    SHPL_PIX_REV ? s1.blocks - 1 - (int64_t)blockIdx.x : (int64_t)blockIdx.x);
     else
-        rows_body<T, VEC, false, G>(s0.f, s0.e, s0.key_range, s0.n_rows, (int64_t)blockIdx.x - s1.blocks);
+        rows_body<T, VEC, false, G>(s0.f, s0.e, s0.key_range, s0.n_rows,
+                                    SHPL_CELL_REV ? s0.blocks - 1 - ((int64_t)blockIdx.x - s1.blocks)
+                                                  : (int64_t)blockIdx.x - s1.blocks);
 #else
     if ((int64_t)blockIdx.x < s0.blocks)
         rows_body<T, VEC, false, G>(s0.f, s0.e, s0.key_range, s0.n_rows, blockIdx.x);
