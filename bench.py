@@ -76,19 +76,13 @@ def parse():
                     help="skip the frame-parallel (one process per core, up to 16) CPU-baseline sample")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the layer's streaming pass after the index build instead of beside it")
-    ap.add_argument("--groups", type=int, default=1,
-                    help="config 2: frame groups of the layer; group g's pooled rows are gathered while "
-                         "group g+1 streams (1 = one dense + one sparse launch; measured fastest, "
-                         "profiles/r01_groups.log)")
     ap.add_argument("--no-interleave", action="store_true",
                     help="dual configs: start both sparse passes after both dense passes (A/B of the overlap)")
-    ap.add_argument("--csr-path", default="auto", choices=["auto", "frame", "segment", "range", "bucket"],
+    ap.add_argument("--csr-path", default="auto", choices=["auto", "frame", "segment", "range"],
                     help="layer workloads: force the CSR builder (shpl_build_csr_path; A/B measurements)")
     ap.add_argument("--no-buckets", action="store_true",
                     help="row-keyed layers (config 3): range CSRs + one k_rows launch per pull on two streams "
                          "instead of the index build's buckets, one CSR launch and one shpl_pull_pair launch per pull pair")
-    ap.add_argument("--records", action="store_true",
-                    help="bucketed config 3: CSRs with per-destination records (k_rows2s instead of k_rows2)")
     ap.add_argument("--no-riders", action="store_true",
                     help="bucketed config 3: copy the forward's pass-through halves with their own launches before the "
                          "index build instead of as extra workgroups of the index launches")
@@ -221,7 +215,7 @@ def cpu_baseline(spec, frames_np, budget_s, dual, backward=False, impl="c"):
         t_pool += c - b
         done += 1
     total = t_index + t_pool
-    return {"value": round(done / total, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+    return {"value": round(done / total, 3), "unit": "frames/s", "cores": 1, "kind": impl if impl == "numpy" else "port",
             "index_ms_per_frame": round(1e3 * t_index / done, 3), "pool_ms_per_frame": round(1e3 * t_pool / done, 3),
             "sample": (f"{done} frames of this workload ({spec.n_points} pts) through {what}: "
                        f"index build {1e3 * t_index / done:.2f} ms/frame + TF-order pooling and concat "
@@ -232,12 +226,13 @@ def cpu_baseline(spec, frames_np, budget_s, dual, backward=False, impl="c"):
 
 
 def cpu_baselines(spec, frames_np, budget_s, dual, backward, parallel):
-    """SURVEY §8d's CPU baseline: the numpy restatement of the reference path (the
-    headline `value`), the C port beside it, and the C port frame-parallel over the
-    usable cores."""
+    """SURVEY §8d's CPU baseline: the C port of the reference path (the headline `value`,
+    "kind": "port": the faster of the two single-core legs), the numpy restatement beside
+    it ("kind": "numpy": the reference's own numpy index builder and TF-order np.add.at
+    pooling), and the C port frame-parallel over the usable cores."""
     npy = cpu_baseline(spec, frames_np, budget_s, dual, backward, impl="numpy")
     port = cpu_baseline(spec, frames_np, budget_s, dual, backward, impl="c")
-    out = dict(npy, numpy=dict(npy), port=port)
+    out = dict(port, numpy=npy, port=dict(port))
     if parallel:
         out["parallel"] = cpu_baseline_parallel(spec, frames_np, budget_s, dual, backward)
     return out
@@ -405,7 +400,7 @@ def main():
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, dev)
     pl = pipeline.FusedPipeline(F, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev,
                                 spec.c_img, dtype=dtype, dual=dual, device=dev,
-                                buckets=False if args.no_buckets else None, records=args.records)
+                                buckets=False if args.no_buckets else None)
     Hb, Wb = spec.bev_feat_hw
     Hi, Wi = spec.img_feat_hw
     feats = lambda shape, seed: sd.fill_features(torch.empty(shape, dtype=dtype, device=dev), fids, seed)  # noqa
@@ -420,23 +415,10 @@ def main():
     pl.interleave = not args.no_interleave
     pl.riders = not args.no_riders
     from sparse_pooling_amd import _lib as L
-    pl.csr_path = {"auto": L.CSR_AUTO, "frame": L.CSR_FRAME, "segment": L.CSR_SEGMENT, "range": L.CSR_RANGE,
-                   "bucket": L.CSR_BUCKET}[args.csr_path]
-    grouped = not dual and not args.no_overlap and args.groups > 1
-    if grouped:
-        host_off = np.concatenate([[0], np.cumsum([f.points.shape[0] for f in frames])])
-        G = len(pl.set_frame_layout(host_off, args.groups))
-        sstream = torch.cuda.Stream(device=dev)
-
-        def new_events():
-            e = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
-            return {"span": [e(), e()], "dense": [[e(), e()] for _ in range(G)],
-                    "sparse": [[e(), e()] for _ in range(G)]}
+    pl.csr_path = {"auto": L.CSR_AUTO, "frame": L.CSR_FRAME, "segment": L.CSR_SEGMENT,
+                   "range": L.CSR_RANGE}[args.csr_path]
 
     def step(ev=None):
-        if grouped:
-            pl.step_pipelined(pts, vox, off, P, bev, img, side, sstream, events=ev)
-            return
         # ev: [dense start, dense end, sparse start, sparse end, bwd start, bwd end]
         if args.no_overlap:
             pl.build_index(pts, vox, off, P)
@@ -486,14 +468,12 @@ def main():
         except Exception as e:  # noqa: BLE001 -- report and run eagerly
             graph, graph_note = None, f"graph capture failed, eager launches: {type(e).__name__}: {e}"[:200]
     n_ev = min(args.steps, 10) if graph is not None else args.steps
-    if grouped:
-        evs = [new_events() for _ in range(n_ev)]
-    else:
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(n_ev)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(n_ev)]
     issue_ms = replay_step_ms = None
     if graph is not None:
         replays = args.steps // args.graph_steps
-        elapsed = sd.timed(lambda k: graph.replay(), replays, device=dev)
+        tinfo = {}
+        elapsed = sd.timed(lambda k: graph.replay(), replays, device=dev, info=tinfo)
         # host cost of one replay: issue the replays without waiting (after the timed loop); well
         # under the step at every config (0.03 ms at config 3), so the timed loop is not launch-bound
         torch.cuda.synchronize()
@@ -511,45 +491,36 @@ def main():
             step(evs[k])
         torch.cuda.synchronize()
     else:
-        elapsed = sd.timed(lambda k: step(evs[k]), args.steps, device=dev)
+        tinfo = {}
+        elapsed = sd.timed(lambda k: step(evs[k]), args.steps, device=dev, info=tinfo)
     args_steps_ev = n_ev
     outs = [pl.bv_fused] + ([pl.img_fused] if dual else []) + ([d_bev, d_img] if backward else [])
     checks = checksum_report(f"layer_config{cfg}", sum(sd.frame_checksums(t) for t in outs), fids, dev, rank, args)
     comm = sd.comm_report(dev)
     nbytes = step_bytes(cfg, spec, nnz, u_pix, u_cell, F, esz)
-    kernels = {}
     interleaved = dual and not args.no_overlap and not pl.rows and pl.interleave
-    if grouped:
-        # the layer's window: first k_dense start -> last k_sparse end (the two overlap)
-        layer_ms = sum(e["span"][0].elapsed_time(e["span"][1]) for e in evs) / args_steps_ev
-        dense_ms = sum(sum(d[0].elapsed_time(d[1]) for d in e["dense"]) for e in evs) / args_steps_ev
-        sparse_ms = sum(sum(d[0].elapsed_time(d[1]) for d in e["sparse"]) for e in evs) / args_steps_ev
-        bwd_ms = 0.0
-        dense_bytes = F * Hb * Wb * (2 * spec.c_bev + spec.c_img) * esz  # read bev + write bv_fused
-        kernels = {"k_dense": {"launches_per_step": G, "ms_per_launch": round(dense_ms / G, 4),
-                               "algorithmic_bytes_per_launch": dense_bytes // G,
-                               "GBps": round(dense_bytes / (dense_ms * 1e-3) / 1e9, 1)},
-                   "k_sparse": {"launches_per_step": G, "ms_per_launch": round(sparse_ms / G, 4),
-                                "algorithmic_bytes_per_launch": (nbytes - dense_bytes) // G,
-                                "GBps": round((nbytes - dense_bytes) / (sparse_ms * 1e-3) / 1e9, 1)}}
-    else:
-        dense_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args_steps_ev
-        sparse_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args_steps_ev
-        bwd_ms = sum(e[4].elapsed_time(e[5]) for e in evs) / args_steps_ev if backward else 0.0
-        layer_ms = dense_ms + sparse_ms + bwd_ms
-        if interleaved:
-            # the cell-keyed sparse pass runs beside img_fused's dense pass: the layer's window
-            # (first k_dense start -> last k_sparse end) instead of the summed durations
-            layer_ms = sum(e[0].elapsed_time(e[3]) for e in evs) / args_steps_ev + bwd_ms
+    dense_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args_steps_ev
+    sparse_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args_steps_ev
+    bwd_ms = sum(e[4].elapsed_time(e[5]) for e in evs) / args_steps_ev if backward else 0.0
+    layer_ms = dense_ms + sparse_ms + bwd_ms
+    if interleaved:
+        # the cell-keyed sparse pass runs beside img_fused's dense pass: the layer's window
+        # (first k_dense start -> last k_sparse end) instead of the summed durations
+        layer_ms = sum(e[0].elapsed_time(e[3]) for e in evs) / args_steps_ev + bwd_ms
     eager_ms = None
     if getattr(pl, "buckets", False) and replay_step_ms is not None:
         # the bucketed one-queue step: its brackets span every kernel of the step, and run eagerly they
         # also hold the host's launch gaps between ~10 us kernels; the replayed step is the same kernels
         # back to back (rocprof's per-kernel averages sum to it)
         eager_ms, layer_ms = layer_ms, replay_step_ms
+    # N > 1: every rank's kernel times and bytes; the roofline describes the slowest rank (its own bytes
+    # over its own layer time), the per-rank list beside it
+    per_rank = sd.gather_floats([layer_ms, dense_ms, sparse_ms, bwd_ms, nbytes], device=dev)
+    slow = max(range(len(per_rank)), key=lambda r: per_rank[r][0])
+    layer_ms, dense_ms, sparse_ms, bwd_ms, nbytes = per_rank[slow][:4] + [int(per_rank[slow][4])]
     achieved = nbytes / (layer_ms * 1e-3) / 1e9
     pool = (pool_fwd_report(pl, img, spec, F, u_pix, nnz, esz, dev)
-            if cfg == 2 and not grouped and not args.no_pool_report else None)
+            if cfg == 2 and not args.no_pool_report else None)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -592,10 +563,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": ("SHPL layer: k_dense (concat stream) + k_sparse (pooled gather) in "
-                           f"{G} frame groups, gathers of group g beside the stream of group g+1; achieved "
-                           "over the layer's window (first k_dense start to last k_sparse end)") if grouped else
-                          ("SHPL layer pulls: k_dense (concat stream) + k_sparse (pooled gather); achieved over "
+                "kernel": ("SHPL layer pulls: k_dense (concat stream) + k_sparse (pooled gather); achieved over "
                            + ("the layer's window (first k_dense start to last k_sparse end: the cell-keyed gathers "
                               "run beside img_fused's stream)" if interleaved else "their summed durations")
                            + ("; bucketed one-stream step: the forward bracket spans the whole forward "
@@ -619,11 +587,17 @@ def main():
                 "k_dense_ms": round(dense_ms, 4),
                 "k_sparse_ms": round(sparse_ms, 4),
                 "backward_ms": round(bwd_ms, 4),
-                **({"kernels": kernels} if kernels else {}),
+                "rank": slow,
+                **({"per_rank": [{"rank": r, "kernel_ms": round(v[0], 4), "k_dense_ms": round(v[1], 4),
+                                  "k_sparse_ms": round(v[2], 4), "backward_ms": round(v[3], 4),
+                                  "algorithmic_bytes": int(v[4]),
+                                  "frac": round(v[4] / (v[0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                                 for r, v in enumerate(per_rank)]} if world > 1 else {}),
                 **({"pool_fwd": pool} if pool else {}),
             },
             "cpu_baseline": cpu,
             "index_errors": err,
+            "timing": tinfo,
             "frame_checksums": checks,
             "comm": comm,
             "lib_sha256": lib_sha256(),
@@ -709,7 +683,8 @@ def run_frames(args, world, rank, dev):
     n_vox = int(pl.bev.frame_nvox.sum().item())
     errs = int(pl.err.item()) | int(pl.bev.err.item()) | int(pl.velo.err.item())
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(9)] for _ in range(args.steps)]
-    elapsed = sd.timed(lambda k: velo_step(evs[k]), args.steps, device=dev)
+    tinfo = {}
+    elapsed = sd.timed(lambda k: velo_step(evs[k]), args.steps, device=dev, info=tinfo)
     mean = lambda i, j: sum(e[i].elapsed_time(e[j]) for e in evs) / args.steps  # noqa: E731
     dense_ms, sparse_ms = mean(0, 1), mean(7, 8)
     stages = {"velo_to_cam_ms": mean(2, 3), "bev_slices_ms": mean(3, 4), "index_ms": mean(4, 5),
@@ -764,6 +739,7 @@ def run_frames(args, world, rank, dev):
                          "step_frac": round(step_gbs / HBM_PEAK_GBS, 4)},
             "cpu_baseline": cpu,
             "index_errors": errs,
+            "timing": tinfo,
             "comm": comm,
             "lib_sha256": lib_sha256(),
         }
@@ -839,7 +815,8 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    elapsed = sd.timed(lambda k: step(), args.steps, device=dev)
+    tinfo = {}
+    elapsed = sd.timed(lambda k: step(), args.steps, device=dev, info=tinfo)
     n_ev = min(args.steps, 5)
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(n_ev)]
     for k in range(n_ev):
@@ -901,6 +878,7 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
                           "hbm_traffic_per_step": traffic, "traffic_note": traffic_note}),
             "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4),
             "cpu_baseline": None,
+            "timing": tinfo,
             "comm": comm,
             "lib_sha256": lib_sha256(),
         }), flush=True)
@@ -966,9 +944,11 @@ def run_conv(args, world, rank, dev):
     n_ev = min(args.steps, 10)
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(n_ev)]
     if graph is not None:
-        elapsed = sd.timed(lambda k: graph.replay(), args.steps, device=dev)
+        tinfo = {}
+        elapsed = sd.timed(lambda k: graph.replay(), args.steps, device=dev, info=tinfo)
     else:
-        elapsed = sd.timed(lambda k: step(), args.steps, device=dev)
+        tinfo = {}
+        elapsed = sd.timed(lambda k: step(), args.steps, device=dev, info=tinfo)
     for k in range(n_ev):
         step(evs[k])
     uev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(n_ev)]
@@ -1028,6 +1008,7 @@ def run_conv(args, world, rank, dev):
                         "bitwise_equal": same},
             "cpu_baseline": cpu,
             "index_errors": err,
+            "timing": tinfo,
             "comm": comm,
             "lib_sha256": lib_sha256(),
         }

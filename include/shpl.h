@@ -298,12 +298,6 @@ typedef struct {
     const int64_t *frame_off; /* [n_frames + 1] */
     const int64_t *frame_nnz; /* [n_frames]     */
     int64_t n_frames;
-    /* optional [n_keys][8] int32, filled by shpl_build_csr_buckets (the builder's maps: one column per
-       entry): per destination {first, end, then (source row, f32 weight bits) of its first three
-       entries}. When every pull of shpl_pull_pair has it, the pair reads the records instead of the
-       ranges (k_rows2s: a run of at most three entries needs no index-word load). Other builders
-       ignore it. */
-    int32_t *key_rec;
 } shpl_csr;
 #define SHPL_LIVE_MAX_FRAMES 1024
 
@@ -332,20 +326,15 @@ int shpl_build_csr(int direction, int order, int n_frames, const int64_t *d_fram
  * (tests and measurements; every builder yields the same entry lists):
  * SHPL_CSR_AUTO = shpl_build_csr's choice, SHPL_CSR_FRAME one workgroup per
  * frame, SHPL_CSR_SEGMENT balanced destination segments, SHPL_CSR_RANGE one
- * workgroup per (frame, destination range) reading the whole frame,
- * SHPL_CSR_BUCKET the range builder over stable per-range buckets (three
- * launches: chunk histograms, stable bucketing, one sort per bucket; entry
- * order only -- identity columns or SHPL_ORDER_ENTRY -- else the range
- * builder); linear in every run length, where the range builder's in-run
- * rank is quadratic in a run's length (a frame with all its points on one
- * cell), but three launches instead of one (slower at config 3). A key_range
- * CSR always takes a range builder (the bucket one only on request). Same
- * arguments and errors as shpl_build_csr otherwise. */
+ * workgroup per (frame, destination range) reading the whole frame. Each is
+ * the default of some batch shape (shpl_build_csr picks FRAME from 32 frames
+ * on, SEGMENT below, RANGE for small batches of at most 65536 destinations
+ * per frame); a key_range CSR always takes the range builder. Same arguments
+ * and errors as shpl_build_csr otherwise. */
 #define SHPL_CSR_AUTO 0
 #define SHPL_CSR_FRAME 1
 #define SHPL_CSR_SEGMENT 2
 #define SHPL_CSR_RANGE 3
-#define SHPL_CSR_BUCKET 4
 int shpl_build_csr_path(int path, int direction, int order, int n_frames, const int64_t *d_frame_off,
                         const int64_t *d_frame_nnz, int64_t keys_per_frame, const int32_t *d_cell,
                         const int32_t *d_col, const float *d_val, const int32_t *d_pix,

@@ -22,7 +22,7 @@ BY_CELL, BY_PIXEL = 0, 1
 ORDER_ENTRY, ORDER_COL_ROW, ORDER_COL_ENTRY = 0, 1, 2
 OUT_POOL, OUT_CONCAT, OUT_ADD = 0, 1, 2
 ACT_NONE, ACT_RELU = 0, 1
-CSR_AUTO, CSR_FRAME, CSR_SEGMENT, CSR_RANGE, CSR_BUCKET = 0, 1, 2, 3, 4
+CSR_AUTO, CSR_FRAME, CSR_SEGMENT, CSR_RANGE = 0, 1, 2, 3
 
 _lib = None
 
@@ -39,17 +39,15 @@ class ShplCsr(ctypes.Structure):
     _fields_ = [("ent_dst", ctypes.c_void_p), ("ent_src", ctypes.c_void_p),
                 ("ent_val", ctypes.c_void_p), ("ent_col", ctypes.c_void_p),
                 ("n_keys", ctypes.c_int64), ("nnz_cap", ctypes.c_int64), ("key_range", ctypes.c_void_p),
-                ("frame_off", ctypes.c_void_p), ("frame_nnz", ctypes.c_void_p), ("n_frames", ctypes.c_int64),
-                ("key_rec", ctypes.c_void_p)]
+                ("frame_off", ctypes.c_void_p), ("frame_nnz", ctypes.c_void_p), ("n_frames", ctypes.c_int64)]
 
 
 class Csr:
     """Device buffers of one destination-sorted entry list (owned tensors + the ABI struct)."""
 
-    def __init__(self, n_keys, nnz_cap, device, with_col, key_range=False, key_rec=False):
+    def __init__(self, n_keys, nnz_cap, device, with_col, key_range=False):
         """key_range: also keep the (first, end) entry of every destination
-        (shpl_csr.key_range): shpl_pull then runs its one-launch row-keyed form.
-        key_rec: per-destination records (shpl_csr.key_rec; shpl_build_csr_buckets fills them)."""
+        (shpl_csr.key_range): shpl_pull then runs its one-launch row-keyed form."""
         i32 = dict(dtype=torch.int32, device=device)
         cap = max(int(nnz_cap), 1)
         self.n_keys, self.nnz_cap = int(n_keys), int(nnz_cap)
@@ -58,12 +56,10 @@ class Csr:
         self.ent_val = torch.empty(cap, dtype=torch.float32, device=device)
         self.ent_col = torch.empty(cap, **i32) if with_col else None
         self.key_range = torch.empty((max(self.n_keys, 1), 2), **i32) if key_range else None
-        self.key_rec = torch.empty((max(self.n_keys, 1), 8), **i32) if key_rec else None
         self.ws = workspace(csr_ws_bytes(self.n_keys, self.nnz_cap), device)
         self.struct = ShplCsr(self.ent_dst.data_ptr(), self.ent_src.data_ptr(), self.ent_val.data_ptr(),
                               self.ent_col.data_ptr() if with_col else None, self.n_keys, self.nnz_cap,
                               self.key_range.data_ptr() if key_range else None)
-        self.struct.key_rec = self.key_rec.data_ptr() if key_rec else None
 
     def live_frames(self, frame_off, frame_nnz):
         """Hand the sparse pass the frame layout the CSR was built with (device i64 [F+1] / [F],

@@ -35,10 +35,6 @@ constexpr int IDX_BLOCK = 1024;
 constexpr int IDX_BATCH = SHPL_IDX_BATCH;         // point rows per thread whose loads are in flight together
 constexpr int IDX_CHUNK = IDX_BLOCK * IDX_BATCH;  // points per workgroup: one round
 
-#ifndef SHPL_RIDERS_FIRST
-#define SHPL_RIDERS_FIRST 0  // 1: a launch's rider workgroups come before each frame's chunks in x
-#endif
-
 constexpr uint32_t KEEP_MULTI = 1u, KEEP_ONE = 2u, AUX = 4u;
 
 struct Ctx {
@@ -124,12 +120,11 @@ template <typename Stage, bool BKT = false>
 __global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr, Bkt bk) {
     __shared__ int32_t wsum[3][IDX_BLOCK / 64];
     __shared__ int32_t hist[BKT ? 2 * BK_MAX_RANGES : 1];
-    // rider workgroups (the launch's blocks past n_chunks in x): after the chunks, or before them
-    const int nride = BKT ? (int)gridDim.x - fr.n_chunks : 0;
-    const int f = blockIdx.y, j = SHPL_RIDERS_FIRST ? (int)blockIdx.x - nride : (int)blockIdx.x;
+    // rider workgroups: the launch's blocks past n_chunks in x (before the chunks measured slower)
+    const int f = blockIdx.y, j = (int)blockIdx.x;
     if constexpr (BKT) {
-        if (j < 0 || j >= fr.n_chunks) {  // a rider workgroup (uniform)
-            const int rj = SHPL_RIDERS_FIRST ? (int)blockIdx.x : j - fr.n_chunks;
+        if (j >= fr.n_chunks) {  // a rider workgroup (uniform)
+            const int rj = j - fr.n_chunks;
             for (int c = 0; c < 2; ++c)
                 if (bk.cp_at[c] == 0) pass_copy(bk.cp[c], f, rj, bk.cp_blocks);
             return;
@@ -266,12 +261,11 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr, Bkt 
     __shared__ int32_t s_off[BKT ? 2 * BK_MAX_RANGES : 1], s_scan[IDX_BLOCK / 64];
     __shared__ int32_t s_w[BKT ? 2 : 1][IDX_BLOCK / 64][BKT ? BK_MAX_RANGES : 1];  // per-wave range counts
     __shared__ int32_t s_tb[BKT ? 4 * BK_MAX_RANGES : 1];  // per (key, range): entries in the frame, in earlier chunks
-    // rider workgroups (the launch's blocks past n_chunks in x): after the chunks, or before them
-    const int nride = BKT ? (int)gridDim.x - fr.n_chunks : 0;
-    const int f = blockIdx.y, j = SHPL_RIDERS_FIRST ? (int)blockIdx.x - nride : (int)blockIdx.x;
+    // rider workgroups: the launch's blocks past n_chunks in x (before the chunks measured slower)
+    const int f = blockIdx.y, j = (int)blockIdx.x;
     if constexpr (BKT) {
-        if (j < 0 || j >= fr.n_chunks) {  // a rider workgroup (uniform)
-            const int rj = SHPL_RIDERS_FIRST ? (int)blockIdx.x : j - fr.n_chunks;
+        if (j >= fr.n_chunks) {  // a rider workgroup (uniform)
+            const int rj = j - fr.n_chunks;
             for (int c = 0; c < 2; ++c)
                 if (bk.cp_at[c] == 1) pass_copy(bk.cp[c], f, rj, bk.cp_blocks);
             return;

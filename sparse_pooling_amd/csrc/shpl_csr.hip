@@ -775,205 +775,10 @@ __global__ __launch_bounds__(CSR_BLOCK) void k_csr_range(CsrIn c, uint64_t *tmp,
         }
 }
 
-// --------------------------------------------------------------- bucket CSR
-// Small batches in entry order (the builder's identity columns, ORDER_ENTRY):
-// the destinations of a frame are cut into ranges of RANGE_KEYS; entries are
-// first bucketed by range, stably (entry order inside a bucket), then each
-// (frame, range) workgroup sorts only its own bucket -- k_csr_range read the
-// whole frame in every range workgroup (config 3: 276 workgroups x 20 k
-// entries per key). Three launches, all linear in the entries:
-//   k_bkt_count  one 1024-thread workgroup per chunk of BKT_CHUNK live entries
-//                of a frame: each entry's destination (kept in kbuf), the
-//                chunk's histogram over ranges -> counts[chunk][range]
-//   k_bkt_place  same grid: each range's offset in the frame (earlier ranges'
-//                totals + this range's entries in earlier chunks), then a
-//                stable multisplit of the chunk by range (wave ballots over
-//                the range bits, per-wave counts prefixed over the waves) ->
-//                words[slot] = local destination << 24 | entry - frame start,
-//                in entry order inside each bucket; the frame's chunk 0 writes
-//                the buckets' (start, count)
-//   k_bkt_sort   one 256-thread workgroup per (frame, range): a counting sort
-//                of its bucket by local destination, stable the same way
-//                (rounds of 256 words in bucket order), emitted with source
-//                row, value and column; key_range of its destinations; the
-//                frame's last range clears the frame's unused capacity.
-// A bucket lands at the same slots its sorted entries occupy in the CSR
-// (its frame's first slot + the entries of earlier ranges), so the sort
-// workgroups need no offsets beyond their bucket's.
-constexpr int BKT_CHUNK = 1024;        // entries per count / place workgroup (one per thread)
-constexpr int BKT_MAX_RANGES = 512;    // ranges per frame: 65536 destinations of RANGE_KEYS
-constexpr int BKT_MAX_FRAMES = 1024;   // frames of one build (one per thread of the chunk prefix)
-constexpr int BKT_SORT = 512;          // threads of a sort workgroup
-constexpr int BKT_RBITS = 9;           // range bits matched by the place multisplit (BKT_MAX_RANGES)
 static_assert(RANGE_KEYS == 128, "the sort multisplit matches 7 destination bits");
 static_assert(BK_KEYS == RANGE_KEYS, "the index builder's buckets are the sort's ranges");
 
-struct BktIn {
-    int n_ranges;         // ranges per frame
-    int32_t *kbuf;        // [nnz_cap] local destination of each live slot (-1: left out)
-    int32_t *counts;      // [chunk][n_ranges]
-    int32_t *ext;         // [frame][range][2]: bucket start (slots from the frame's first), entries
-    uint32_t *words;      // [nnz_cap] bucketed words
-};
-
-// Exclusive scan of one int per thread across a 1024-thread workgroup (wsum: 17 ints).
-__device__ __forceinline__ int32_t scan1024(int32_t v, int32_t *wsum, int32_t *total) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    int32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wid] = x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int32_t acc = 0;
-        for (int w = 0; w < 16; ++w) {
-            const int32_t t = wsum[w];
-            wsum[w] = acc;
-            acc += t;
-        }
-        wsum[16] = acc;
-    }
-    __syncthreads();
-    const int32_t r = x - v + wsum[wid];
-    *total = wsum[16];
-    __syncthreads();
-    return r;
-}
-
-// The frame and frame-local chunk of count / place workgroup b (frames' chunks in frame order);
-// s_pre[f] = the first chunk of frame f. False for the grid's spare workgroups.
-__device__ __forceinline__ bool bkt_chunk(const CsrIn &c, int b, int32_t *s_pre, int32_t *wsum, int &f, int &j) {
-    int32_t nch = 0;
-    if ((int)threadIdx.x < c.n_frames) {
-        int64_t e0, e1, cap_end;
-        frame_range(c, threadIdx.x, e0, e1, cap_end);
-        nch = (int32_t)((e1 - e0 + BKT_CHUNK - 1) / BKT_CHUNK);
-    }
-    int32_t total;
-    const int32_t pre = scan1024(nch, wsum, &total);
-    if ((int)threadIdx.x < c.n_frames) s_pre[threadIdx.x] = pre;
-    if (threadIdx.x == 0) s_pre[c.n_frames] = total;
-    __syncthreads();
-    if (b >= total) return false;
-    int lo = 0, hi = c.n_frames;  // the last frame whose first chunk is <= b (frames without chunks skipped)
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (s_pre[mid] <= b) lo = mid; else hi = mid;
-    }
-    f = lo;
-    j = b - s_pre[lo];
-    return true;
-}
-
-template <bool HAS_COL>
-__global__ __launch_bounds__(BKT_CHUNK) void k_bkt_count(CsrIn c, BktIn k) {
-    __shared__ int32_t s_pre[BKT_MAX_FRAMES + 1], wsum[17], hist[BKT_MAX_RANGES];
-    int f, j;
-    if (!bkt_chunk(c, blockIdx.x, s_pre, wsum, f, j)) return;  // uniform
-    int64_t e0, e1, cap_end;
-    frame_range(c, f, e0, e1, cap_end);
-    const int64_t kf = (int64_t)f * c.keys_per_frame;
-    for (int q = threadIdx.x; q < k.n_ranges; q += BKT_CHUNK) hist[q] = 0;
-    __syncthreads();
-    const int64_t e = e0 + (int64_t)j * BKT_CHUNK + threadIdx.x;
-    if (e < e1) {
-        int32_t key[1];
-        keys_batch<HAS_COL, 1>(c, e, e1, key);
-        const int64_t t = (int64_t)key[0] - kf;
-        const bool ok = key[0] >= 0 && t >= 0 && t < c.keys_per_frame;  // invalid / outside the frame: left out
-        k.kbuf[e] = ok ? (int32_t)t : -1;
-        if (ok) atomicAdd(&hist[t / RANGE_KEYS], 1);
-    }
-    __syncthreads();
-    int32_t *row = k.counts + (int64_t)(s_pre[f] + j) * k.n_ranges;
-    for (int q = threadIdx.x; q < k.n_ranges; q += BKT_CHUNK) row[q] = hist[q];
-}
-
-__global__ __launch_bounds__(BKT_CHUNK) void k_bkt_place(CsrIn c, BktIn k) {
-    __shared__ int32_t s_pre[BKT_MAX_FRAMES + 1], wsum[17];
-    __shared__ int32_t s_off[BKT_MAX_RANGES], s_tot[BKT_MAX_RANGES];
-    __shared__ int32_t s_w[BKT_CHUNK / 64][BKT_MAX_RANGES];
-    int f, j;
-    if (!bkt_chunk(c, blockIdx.x, s_pre, wsum, f, j)) return;  // uniform
-    int64_t e0, e1, cap_end;
-    frame_range(c, f, e0, e1, cap_end);
-    const int nc = s_pre[f + 1] - s_pre[f], nr = k.n_ranges;
-    const int wid = threadIdx.x >> 6;
-    // 1. each range's entries in the frame's earlier chunks and in all of them: np = BKT_CHUNK / nr
-    //    threads per range, each summing every np-th chunk (their loads in flight together), partial
-    //    sums combined in LDS (s_w doubles as the table)
-    {
-        const int np = BKT_CHUNK / nr, part = threadIdx.x / nr, q = threadIdx.x - part * nr;
-        int32_t tot = 0, bef = 0;
-        if (part < np) {
-            const int32_t *col = k.counts + (int64_t)s_pre[f] * nr + q;
-            for (int jj = part; jj < nc; jj += np) {
-                const int32_t v = col[(int64_t)jj * nr];
-                tot += v;
-                bef += jj < j ? v : 0;
-            }
-        }
-        int32_t *pt = &s_w[0][0], *pb = pt + BKT_CHUNK;  // [np][nr] partial totals / partial befores
-        if (part < np) {
-            pt[part * nr + q] = tot;
-            pb[part * nr + q] = bef;
-        }
-        __syncthreads();
-        if ((int)threadIdx.x < nr) {
-            int32_t t = 0, b = 0;
-            for (int i = 0; i < np; ++i) {
-                t += pt[i * nr + threadIdx.x];
-                b += pb[i * nr + threadIdx.x];
-            }
-            s_tot[threadIdx.x] = t;
-            s_off[threadIdx.x] = b;
-        }
-        __syncthreads();
-    }
-    for (int i = threadIdx.x; i < (BKT_CHUNK / 64) * nr; i += BKT_CHUNK) s_w[i / nr][i % nr] = 0;
-    __syncthreads();
-    // 2. ranges' starts: exclusive scan of the totals (nr <= 512 <= threads)
-    int32_t all;
-    const int32_t base = scan1024((int)threadIdx.x < nr ? s_tot[threadIdx.x] : 0, wsum, &all);
-    if ((int)threadIdx.x < nr) {
-        s_off[threadIdx.x] += base;
-        if (j == 0) {
-            int32_t *x = k.ext + ((int64_t)f * nr + threadIdx.x) * 2;
-            x[0] = base;
-            x[1] = s_tot[threadIdx.x];
-        }
-    }
-    // 3. stable multisplit of this chunk by range
-    const int64_t e = e0 + (int64_t)j * BKT_CHUNK + threadIdx.x;
-    const int32_t t = e < e1 ? k.kbuf[e] : -1;
-    const bool ok = t >= 0;
-    const int r = ok ? t / RANGE_KEYS : 0;
-    uint64_t peers = __ballot(ok);
-#pragma unroll
-    for (int bit = 0; bit < BKT_RBITS; ++bit) {
-        const uint64_t bm = __ballot(ok && ((r >> bit) & 1));
-        peers &= ((r >> bit) & 1) ? bm : ~bm;
-    }
-    const int32_t rank = (int32_t)lane_rank(peers);
-    if (ok && rank == 0) s_w[wid][r] = (int32_t)__popcll(peers);
-    __syncthreads();
-    for (int q = threadIdx.x; q < nr; q += BKT_CHUNK) {
-        int32_t run = 0;
-#pragma unroll
-        for (int w = 0; w < BKT_CHUNK / 64; ++w) {
-            const int32_t v = s_w[w][q];
-            s_w[w][q] = run;
-            run += v;
-        }
-    }
-    __syncthreads();
-    if (ok) k.words[e0 + s_off[r] + s_w[wid][r] + rank] = ((uint32_t)(t % RANGE_KEYS) << 24) | (uint32_t)(e - e0);
-}
-
-// A bucket's counting sort (k_bkt_sort, k_bsort2): words[0, n) = the bucket of destinations
+// A bucket's counting sort (k_bsort2): words[0, n) = the bucket of destinations
 // [k0, k0 + nk) (global ids, word = local destination << 24 | entry - e0) in entry order, placed stably
 // by destination at out0.. with source row, value and column; key_range of its destinations. BY_CELL:
 // source = pix[e]; BY_PIXEL: source = cell[e] and column e (the builder's identity columns). All threads
@@ -988,7 +793,7 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
                                                  int64_t k0, int nk, int direction, const int32_t *col,
                                                  const int32_t *cell, const int32_t *pix, const float *vals,
                                                  int32_t *ent_dst, int32_t *ent_src, float *ent_val,
-                                                 int32_t *ent_col, int32_t *key_range, int32_t *key_rec = nullptr) {
+                                                 int32_t *ent_col, int32_t *key_range) {
     constexpr int NW = BLOCK / 64;
     __shared__ int32_t cnt[NW][RANGE_KEYS], s_tot[RANGE_KEYS], s_beg[RANGE_KEYS];
     __shared__ uint32_t l_w[LCAP > 0 ? LCAP : 1];
@@ -1057,10 +862,6 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
             key_range[2 * (k0 + threadIdx.x)] = (int32_t)(out0 + run);
             key_range[2 * (k0 + threadIdx.x) + 1] = (int32_t)(out0 + incl);
         }
-        if (key_rec && (int)threadIdx.x < nk) {
-            key_rec[8 * (k0 + threadIdx.x)] = (int32_t)(out0 + run);
-            key_rec[8 * (k0 + threadIdx.x) + 1] = (int32_t)(out0 + incl);
-        }
     }
     __syncthreads();
     // 3. each wave places its slice in order, 64 words at a time (no block barrier)
@@ -1103,44 +904,8 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
             ent_src[o] = src;
             ent_val[o] = val;
             if (ent_col) ent_col[o] = kk;
-            const int32_t k = base + rank - s_beg[t];  // the entry's place in its destination's run
-            if (key_rec && k < 3) {
-                key_rec[8 * (k0 + t) + 2 + 2 * k] = src;
-                key_rec[8 * (k0 + t) + 3 + 2 * k] = __float_as_int(val);
-            }
         }
     }
-}
-
-template <bool HAS_COL>
-__global__ __launch_bounds__(BKT_SORT) void k_bkt_sort(CsrIn c, BktIn k, int64_t nnz_cap, int64_t n_keys,
-                                                      int32_t *ent_dst, int32_t *ent_src, float *ent_val,
-                                                      int32_t *ent_col, int32_t *key_range) {
-    const int f = blockIdx.y, q = blockIdx.x;
-    int64_t e0, e1, cap_end;
-    frame_range(c, f, e0, e1, cap_end);
-    const int64_t kf = (int64_t)f * c.keys_per_frame, kend = kf + c.keys_per_frame;
-    const int64_t k0 = kf + (int64_t)q * RANGE_KEYS;
-    const int nk = (int)(k0 + RANGE_KEYS < kend ? RANGE_KEYS : kend - k0);
-    int32_t start = 0, n = 0;
-    if (e1 > e0) {  // a frame without live entries has no chunk, so no bucket extents
-        const int32_t *x = k.ext + ((int64_t)f * k.n_ranges + q) * 2;
-        start = x[0];
-        n = x[1];
-    }
-    const int64_t out0 = e0 + start;
-    bucket_sort_emit<BKT_SORT, 0>(k.words + out0, n, e0, out0, k0, nk, c.direction, HAS_COL ? c.col : nullptr,
-                                  c.cell, c.pix, c.val, ent_dst, ent_src, ent_val, ent_col, key_range);
-    // the frame's unused capacity (its last range), the slots and key ranges after the last frame
-    if (q != k.n_ranges - 1) return;
-    for (int64_t h = out0 + n + threadIdx.x; h < cap_end; h += BKT_SORT) ent_dst[h] = -1;
-    if (f != c.n_frames - 1) return;
-    for (int64_t h = cap_end + threadIdx.x; h < nnz_cap; h += BKT_SORT) ent_dst[h] = -1;
-    if (key_range)
-        for (int64_t kk = kend + threadIdx.x; kk < n_keys; kk += BKT_SORT) {
-            key_range[2 * kk] = 0;
-            key_range[2 * kk + 1] = 0;
-        }
 }
 
 // ------------------------------------------------ both CSRs from the index build's buckets
@@ -1155,7 +920,6 @@ struct BsSide {
     float *ent_val;
     int32_t *ent_col, *key_range;
     int64_t blocks;    // n_frames * nr
-    int32_t *key_rec;  // optional per-destination records
 };
 
 struct BsIn {
@@ -1168,26 +932,14 @@ struct BsIn {
     int64_t nnz_cap;
 };
 
-#ifndef SHPL_PIX_REV
-#define SHPL_PIX_REV 0  // 1: k_bsort2's pixel-keyed buckets in reverse order
-#endif
-#ifndef SHPL_BSORT_ORDER
-#define SHPL_BSORT_ORDER 1  // k_bsort2 runs the pixel-keyed side's buckets first (0: cell-keyed first)
-#endif
 constexpr int BS_BLOCK = 1024;  // threads of a k_bsort2 workgroup (the horizon's 2 k-entry pixel buckets: 3 rounds)
 constexpr int BS_LCAP = 4096;   // bucket words staged in LDS with their source rows and values (48 KiB)
 
 __global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide s1) {
     __shared__ uint32_t one[1];
-#if SHPL_BSORT_ORDER
     // the pixel-keyed buckets first (the horizon's heavy ones start early instead of forming the tail)
     const bool second = (int64_t)blockIdx.x < s1.blocks;
-    const int64_t b = second ? (SHPL_PIX_REV ? s1.blocks - 1 - (int64_t)blockIdx.x : (int64_t)blockIdx.x)
-                             : (int64_t)blockIdx.x - s1.blocks;
-#else
-    const bool second = (int64_t)blockIdx.x >= s0.blocks;
-    const int64_t b = second ? (int64_t)blockIdx.x - s0.blocks : (int64_t)blockIdx.x;
-#endif
+    const int64_t b = second ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - s1.blocks;
     const BsSide &sd = second ? s1 : s0;
     const int key = second ? 1 : 0;
     const int f = (int)(b / sd.nr), q = (int)(b - (int64_t)f * sd.nr);
@@ -1221,22 +973,17 @@ __global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide 
     }
     const int64_t out0 = p0 + start;
     bucket_sort_emit<BS_BLOCK, BS_LCAP>(W, n, p0, out0, k0, nk, direction, nullptr, in.cell, in.pix, in.val, sd.ent_dst,
-                                        sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range, sd.key_rec);
+                                        sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range);
     // the frame's unused capacity (its last range), the slots and key ranges after the last frame
     if (q != sd.nr - 1) return;
     for (int64_t h = p0 + valid + threadIdx.x; h < cap_end; h += BS_BLOCK) sd.ent_dst[h] = -1;
     if (f != in.n_frames - 1) return;
     for (int64_t h = cap_end + threadIdx.x; h < sd.nnz_cap; h += BS_BLOCK) sd.ent_dst[h] = -1;
-    for (int64_t kk = kend + threadIdx.x; kk < sd.n_keys; kk += BS_BLOCK) {
-        if (sd.key_range) {
+    if (sd.key_range)
+        for (int64_t kk = kend + threadIdx.x; kk < sd.n_keys; kk += BS_BLOCK) {
             sd.key_range[2 * kk] = 0;
             sd.key_range[2 * kk + 1] = 0;
         }
-        if (sd.key_rec) {
-            sd.key_rec[8 * kk] = 0;
-            sd.key_rec[8 * kk + 1] = 0;
-        }
-    }
 }
 
 }  // namespace
@@ -1284,15 +1031,8 @@ constexpr int64_t RANGE_MAX_KEYS = 65536;  // destinations per frame up to which
 int64_t seg_cap_of(int64_t nnz_cap) { return nnz_cap / 16 + 65536; }  // bin + cursor counters
 
 struct CsrLayout {
-    size_t tmp, kbuf, sorted, counters, bkt, total;
-    int64_t bkt_ints;  // int32 slots of the bucket CSR's chunk counts + bucket extents
+    size_t tmp, kbuf, sorted, counters, total;
 };
-
-// Bucket tables: counts [chunks][ranges] with chunks <= cap / BKT_CHUNK + frames + 1 and ranges <= 512,
-// extents [frames][ranges][2]; frames * ranges <= n_keys / RANGE_KEYS + frames, frames <= BKT_MAX_FRAMES.
-int64_t bkt_ints_of(int64_t n_keys, int64_t nnz_cap) {
-    return (nnz_cap / BKT_CHUNK + 2) * BKT_MAX_RANGES + 3 * (n_keys / RANGE_KEYS + BKT_MAX_FRAMES);
-}
 
 CsrLayout csr_layout(int64_t n_keys, int64_t nnz_cap) {
     CsrLayout l = {};
@@ -1301,9 +1041,7 @@ CsrLayout csr_layout(int64_t n_keys, int64_t nnz_cap) {
     l.kbuf = align_up(sizeof(uint64_t) * cap, 256);
     l.sorted = l.kbuf + align_up(sizeof(int32_t) * cap, 256);
     l.counters = l.sorted + align_up(sizeof(uint64_t) * cap, 256);
-    l.bkt = l.counters + align_up(2 * sizeof(int32_t) * (size_t)seg_cap_of(nnz_cap), 256);
-    l.bkt_ints = bkt_ints_of(n_keys, nnz_cap);
-    l.total = l.bkt + align_up(sizeof(int32_t) * (size_t)l.bkt_ints, 256);
+    l.total = l.counters + align_up(2 * sizeof(int32_t) * (size_t)seg_cap_of(nnz_cap), 256);
     return l;
 }
 }  // namespace
@@ -1318,7 +1056,7 @@ extern "C" int shpl_build_csr_path(int path, int direction, int order, int n_fra
                                    const int64_t *d_frame_nnz, int64_t keys_per_frame, const int32_t *d_cell,
                                    const int32_t *d_col, const float *d_val, const int32_t *d_pix,
                                    const shpl_csr *csr, void *d_ws, size_t ws_bytes, void *stream) {
-    if (path < SHPL_CSR_AUTO || path > SHPL_CSR_BUCKET) return SHPL_ERR_ARG;
+    if (path < SHPL_CSR_AUTO || path > SHPL_CSR_RANGE) return SHPL_ERR_ARG;
     if (!csr || !d_frame_off || n_frames < 1) return SHPL_ERR_ARG;
     if (direction != SHPL_BY_CELL && direction != SHPL_BY_PIXEL) return SHPL_ERR_ARG;
     if (order < SHPL_ORDER_ENTRY || order > SHPL_ORDER_COL_ENTRY) return SHPL_ERR_ARG;
@@ -1347,44 +1085,8 @@ extern "C" int shpl_build_csr_path(int path, int direction, int order, int n_fra
     if (csr->key_range && !small_cap) return SHPL_ERR_BAD_SHAPE;
     const bool ranged = csr->key_range != nullptr ||
                         (small_cap && (path != SHPL_CSR_AUTO
-                                           ? (path == SHPL_CSR_RANGE || path == SHPL_CSR_BUCKET)
+                                           ? path == SHPL_CSR_RANGE
                                            : (n_frames < SEG_FRAMES && keys_per_frame <= RANGE_MAX_KEYS)));
-    // the bucket form on request (SHPL_CSR_BUCKET), when the order inside a destination is entry order
-    // (it keeps the bucket's) and its tables fit. Linear in every run length, where k_csr_range ranks an
-    // entry among its destination's (quadratic in a run), but slower at config 3 (three launches per key:
-    // step 0.132-0.134 ms against 0.123-0.125 with k_csr_range), so not the default.
-    const int64_t n_ranges_b = (keys_per_frame + RANGE_KEYS - 1) / RANGE_KEYS;
-    const int64_t n_chunks_b = nnz_cap / BKT_CHUNK + n_frames + 1;
-    const bool bucket = ranged && path == SHPL_CSR_BUCKET && (d_col == nullptr || order == SHPL_ORDER_ENTRY) &&
-                        n_frames <= BKT_MAX_FRAMES && n_ranges_b <= BKT_MAX_RANGES &&
-                        n_chunks_b * n_ranges_b + 2 * (int64_t)n_frames * n_ranges_b <= lay.bkt_ints &&
-                        ws_bytes >= lay.total && n_chunks_b < 0x7fffffffLL;
-    if (bucket) {
-        CsrIn c{direction, order, n_frames, d_frame_off, d_frame_nnz, keys_per_frame, 0,
-                d_cell, d_col, d_pix, d_val};
-        BktIn k;
-        k.n_ranges = (int)n_ranges_b;
-        k.kbuf = (int32_t *)(ws + lay.kbuf);
-        k.words = (uint32_t *)(ws + lay.sorted);
-        k.counts = (int32_t *)(ws + lay.bkt);
-        k.ext = k.counts + n_chunks_b * n_ranges_b;
-        if (d_col)
-            hipLaunchKernelGGL(k_bkt_count<true>, dim3((unsigned)n_chunks_b), dim3(BKT_CHUNK), 0, st, c, k);
-        else
-            hipLaunchKernelGGL(k_bkt_count<false>, dim3((unsigned)n_chunks_b), dim3(BKT_CHUNK), 0, st, c, k);
-        SHPL_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_bkt_place, dim3((unsigned)n_chunks_b), dim3(BKT_CHUNK), 0, st, c, k);
-        SHPL_LAUNCH_CHECK();
-        const dim3 grid((unsigned)n_ranges_b, (unsigned)n_frames);
-        if (d_col)
-            hipLaunchKernelGGL(k_bkt_sort<true>, grid, dim3(BKT_SORT), 0, st, c, k, nnz_cap, csr->n_keys,
-                               csr->ent_dst, csr->ent_src, csr->ent_val, csr->ent_col, csr->key_range);
-        else
-            hipLaunchKernelGGL(k_bkt_sort<false>, grid, dim3(BKT_SORT), 0, st, c, k, nnz_cap, csr->n_keys,
-                               csr->ent_dst, csr->ent_src, csr->ent_val, csr->ent_col, csr->key_range);
-        SHPL_LAUNCH_CHECK();
-        return SHPL_OK;
-    }
     if (ranged) {
         if (ws_bytes < align_up(sizeof(uint64_t) * (size_t)nnz_cap, 256)) return SHPL_ERR_WORKSPACE;
         const int64_t n_ranges = (keys_per_frame + RANGE_KEYS - 1) / RANGE_KEYS;
@@ -1501,7 +1203,7 @@ extern "C" int shpl_build_csr_buckets(const shpl_buckets *bk, const shpl_csr *by
         if (bk->nnz_cap > 0 && (!c->ent_dst || !c->ent_src || !c->ent_val)) return SHPL_ERR_ARG;
         if (k == 1 && bk->nnz_cap > 0 && !c->ent_col) return SHPL_ERR_ARG;
         s[k] = BsSide{l.nr[k], l.kpf[k], c->n_keys, c->nnz_cap, c->ent_dst, c->ent_src, c->ent_val, c->ent_col,
-                      c->key_range, (int64_t)bk->n_frames * l.nr[k], c->key_rec};
+                      c->key_range, (int64_t)bk->n_frames * l.nr[k]};
         if (l.nr[k] == 0) s[k].blocks = 0;
     }
     hipStream_t st = (hipStream_t)stream;
@@ -1509,9 +1211,6 @@ extern "C" int shpl_build_csr_buckets(const shpl_buckets *bk, const shpl_csr *by
         for (int k = 0; k < 2; ++k) {
             if (cs[k] && cs[k]->key_range && cs[k]->n_keys > 0 &&
                 hipMemsetAsync(cs[k]->key_range, 0, sizeof(int32_t) * 2 * (size_t)cs[k]->n_keys, st) != hipSuccess)
-                return SHPL_ERR_HIP;
-            if (cs[k] && cs[k]->key_rec && cs[k]->n_keys > 0 &&
-                hipMemsetAsync(cs[k]->key_rec, 0, sizeof(int32_t) * 8 * (size_t)cs[k]->n_keys, st) != hipSuccess)
                 return SHPL_ERR_HIP;
         }
         return SHPL_OK;

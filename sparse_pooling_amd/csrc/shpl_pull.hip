@@ -213,9 +213,6 @@ __device__ __forceinline__ void fma_free_accumulate(float (&acc)[VEC], float w, 
 #ifndef SHPL_WALK
 #define SHPL_WALK 2
 #endif
-#ifndef SHPL_WALK_PRED
-#define SHPL_WALK_PRED 0
-#endif
 constexpr int WALK = SHPL_WALK;
 // Runs longer than LONG_RUN entries (config 3: up to 54 image points on one
 // pixel) are left to k_sparse_long, which batches LONG_WALK entries per
@@ -261,19 +258,6 @@ __device__ __forceinline__ void walk_run(const Feat &f, const Ents &e, int64_t s
         bool in[W];
         int32_t d[W], sr[W], kc[W];
         float w[W];
-#if SHPL_WALK_PRED
-        // src / val / col only for entries of the run (one more latency, fewer loads)
-#pragma unroll
-        for (int u = 0; u < W; ++u) d[u] = i + u < nnz ? e.dst[i + u] : -1;
-#pragma unroll
-        for (int u = 0; u < W; ++u) in[u] = d[u] == key && (u == 0 || in[u - 1]);
-#pragma unroll
-        for (int u = 0; u < W; ++u) {
-            sr[u] = in[u] ? e.src[i + u] : 0;
-            w[u] = in[u] ? e.val[i + u] : 0.0f;
-            kc[u] = (GROUP && in[u]) ? e.col[i + u] : 0;
-        }
-#else
         // index loads of the batch do not wait for each other (dst need not match yet);
         // the first batch may come preloaded (issued with the caller's head test)
         IdxBatch<GROUP, W> b;
@@ -290,7 +274,6 @@ __device__ __forceinline__ void walk_run(const Feat &f, const Ents &e, int64_t s
         }
 #pragma unroll
         for (int u = 0; u < W; ++u) in[u] = d[u] == key && (u == 0 || in[u - 1]);
-#endif
         typename C::raw_t raw[W];
 #pragma unroll
         for (int u = 0; u < W; ++u)
@@ -515,11 +498,6 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse_long(const Feat f, const 
 #define SHPL_ROWS_WALK 8
 #endif
 constexpr int ROWS_WALK = SHPL_ROWS_WALK;
-#ifndef SHPL_PULL_XCD
-// 1: XCD-contiguous row blocks (xcd_block). Measured slower at config 3 (pixel-keyed pull 27.3 -> 29.6 us,
-// step 0.124 -> 0.127 ms: the long horizon runs then crowd a few XCDs), so blockIdx order is the default
-#define SHPL_PULL_XCD 0
-#endif
 
 // The walk of one row's run [first, end) (all lanes of the wave, wave-uniform trip counts); pv / av: the
 // lane's first pass-through chunk (CONCAT, when p0) and first ADD operand, loaded by the caller.
@@ -635,13 +613,7 @@ __device__ __forceinline__ void rows_body(const Feat &f, const Ents &e, const in
 template <typename T, int VEC, bool GROUP, int G>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_rows(const Feat f, const Ents e, const int32_t *key_range,
                                                      int64_t n_rows) {
-#if SHPL_PULL_XCD
-    // each XCD one contiguous stretch of output rows (config 3: half a frame), so the rows its runs
-    // gather (one frame's sources, 3.5-4.5 MB) stay in its L2 instead of every XCD's L2 seeing all frames
-    rows_body<T, VEC, GROUP, G>(f, e, key_range, n_rows, xcd_block(blockIdx.x, gridDim.x));
-#else
     rows_body<T, VEC, GROUP, G>(f, e, key_range, n_rows, blockIdx.x);
-#endif
 }
 
 // Two row-keyed pulls in ONE launch (shpl_pull_pair): blocks [0, blocks0) run the first pull (no per-column
@@ -651,163 +623,17 @@ struct RowsSide {
     Ents e;
     const int32_t *key_range;
     int64_t n_rows, blocks;
-    const int32_t *key_rec;  // optional per-destination records (k_rows2s)
 };
 
-#ifndef SHPL_CELL_REV
-#define SHPL_CELL_REV 0  // 1: k_rows2's cell-keyed rows in reverse order
-#endif
-#ifndef SHPL_PIX_REV
-#define SHPL_PIX_REV 0  // 1: the pixel-keyed side's rows (k_rows2) / buckets (k_bsort2) in reverse order
-#endif
-#ifndef SHPL_ROWS2_ORDER
-#define SHPL_ROWS2_ORDER 1  // the pixel-keyed side's blocks first in k_rows2 (0: cell-keyed first)
-#endif
-#ifndef SHPL_ROWS2_WPE
-#define SHPL_ROWS2_WPE 1  // amdgpu_waves_per_eu floor of k_rows2 (1: the compiler's choice)
-#endif
+// The pixel-keyed pull's blocks come first: its longer runs (6.7 entries on average at config 3, up to 54 at
+// the horizon) then start early instead of forming the launch's tail (k_rows2 31.1 -> 24.0 us per pair,
+// profiles/r03_pixel_first_ab.log; reversing the order inside either side measured within noise).
 template <typename T, int VEC, int G>
-__global__ __launch_bounds__(SHPL_BLOCK) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS2_WPE))) void k_rows2(
-    const RowsSide s0, const RowsSide s1) {
-#if SHPL_ROWS2_ORDER
-    // the pixel-keyed pull's blocks first: its longer runs start early instead of forming the launch's tail
+__global__ __launch_bounds__(SHPL_BLOCK) void k_rows2(const RowsSide s0, const RowsSide s1) {
     if ((int64_t)blockIdx.x < s1.blocks)
-        rows_body<T, VEC, true, G>(s1.f, s1.e, s1.key_range, s1.n_rows,
-                                   SHPL_PIX_REV ? s1.blocks - 1 - (int64_t)blockIdx.x : (int64_t)blockIdx.x);
+        rows_body<T, VEC, true, G>(s1.f, s1.e, s1.key_range, s1.n_rows, (int64_t)blockIdx.x);
     else
-        rows_body<T, VEC, false, G>(s0.f, s0.e, s0.key_range, s0.n_rows,
-                                    SHPL_CELL_REV ? s0.blocks - 1 - ((int64_t)blockIdx.x - s1.blocks)
-                                                  : (int64_t)blockIdx.x - s1.blocks);
-#else
-    if ((int64_t)blockIdx.x < s0.blocks)
-        rows_body<T, VEC, false, G>(s0.f, s0.e, s0.key_range, s0.n_rows, blockIdx.x);
-    else
-        rows_body<T, VEC, true, G>(s1.f, s1.e, s1.key_range, s1.n_rows, (int64_t)blockIdx.x - s0.blocks);
-#endif
-}
-
-// ------------------------------------------------------------- k_rows2s
-// The pull pair over CSRs that also carry per-destination records (shpl_csr.key_rec, written by
-// shpl_build_csr_buckets): 8 ints per destination, {first, end, then (source row, weight bits) of its
-// first REC_N entries}; "items" of 64 / G rows, both pulls' items in one list. Longer runs take
-// row_walk from the record's (first, end). Every entry of a builder-made map has a column of its own
-// (the identity), so TF's per-column partials are single products and the short form's plain sum is
-// bitwise the same (an accumulator that starts at +0 never becomes -0, so 0 + p and p add alike).
-// Measured slower than k_rows2 at config 3 (0.109 vs 0.107 ms per step; a persistent form that
-// prefetched the next item's records: 0.125 ms; profiles/r03_c3_records_riders_ab.log): opt-in.
-constexpr int REC_N = 3;
-
-struct Rec {
-    int32_t first, end, s[REC_N];
-    float v[REC_N];
-};
-
-template <typename T, int VEC, int G>
-__device__ __forceinline__ void rec_fetch(const RowsSide &s0, const RowsSide &s1, int64_t items0, int64_t it,
-                                          Rec &r, typename Chunk<T, VEC>::raw_t &av, bool &live, int64_t &row,
-                                          bool &second) {
-    typedef Chunk<T, VEC> C;
-    constexpr int RPW = SHPL_WAVE / G;
-    const int lane = threadIdx.x & 63, lg = lane & (G - 1);
-    second = it >= items0;
-    const RowsSide &sd = second ? s1 : s0;
-    row = (second ? it - items0 : it) * RPW + lane / G;
-    live = row < sd.n_rows;
-    r.first = r.end = 0;
-    if (live) {
-        typedef int32_t i32x4r __attribute__((ext_vector_type(4)));
-        const i32x4r a = *reinterpret_cast<const i32x4r *>(sd.key_rec + 8 * row);
-        const i32x4r b = *reinterpret_cast<const i32x4r *>(sd.key_rec + 8 * row + 4);
-        r.first = a[0];
-        r.end = a[1];
-        r.s[0] = a[2];
-        r.v[0] = __int_as_float(a[3]);
-        r.s[1] = b[0];
-        r.v[1] = __int_as_float(b[1]);
-        r.s[2] = b[2];
-        r.v[2] = __int_as_float(b[3]);
-    }
-    const Feat &f = sd.f;
-    if (live && f.mode == SHPL_OUT_ADD && (uint32_t)lg < f.cpool)
-        av = C::load(reinterpret_cast<const T *>(f.pass) + f.pass_off + (row * f.pass_stride + (int64_t)lg * VEC));
-}
-
-// A row of at most REC_N entries, from its record (the wave's rows all are).
-template <typename T, int VEC, int G>
-__device__ __forceinline__ void row_short(const Feat &f, int64_t row, bool live, const Rec &r,
-                                          typename Chunk<T, VEC>::raw_t av) {
-    typedef Chunk<T, VEC> C;
-    const int lg = (threadIdx.x & 63) & (G - 1);
-    if (!live) return;
-    T *out = reinterpret_cast<T *>(f.out);
-    const T *pass = reinterpret_cast<const T *>(f.pass) + f.pass_off;
-    const T *src = reinterpret_cast<const T *>(f.src) + f.src_off;
-    const bool concat = f.mode == SHPL_OUT_CONCAT, add = f.mode == SHPL_OUT_ADD;
-    const uint32_t oc0 = concat ? f.cpass : 0u;
-    const int32_t len = r.end - r.first;
-    if (concat)
-        for (uint32_t c = lg; c < f.cpass; c += G)
-            C::store_nt(out + (row * f.out_stride + (int64_t)c * VEC),
-                        C::load_nt(pass + (row * f.pass_stride + (int64_t)c * VEC)));
-    for (uint32_t pc0 = 0; pc0 < f.cpool; pc0 += G) {
-        const uint32_t pc = pc0 + lg;
-        if (pc >= f.cpool) break;
-        typename C::raw_t raw[REC_N];
-#pragma unroll
-        for (int u = 0; u < REC_N; ++u)
-            if (u < len) raw[u] = C::load(src + ((int64_t)r.s[u] * f.src_stride + (int64_t)pc * VEC));
-        float acc[VEC];
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) acc[j] = 0.0f;
-#pragma unroll
-        for (int u = 0; u < REC_N; ++u) {
-            if (u >= len) continue;
-            float x[VEC];
-            C::to_f32(raw[u], x);
-            fma_free_accumulate<VEC>(acc, r.v[u], x);
-        }
-        if (add) {
-            float a[VEC];
-            C::to_f32(pc0 == 0 ? av : C::load(pass + (row * f.pass_stride + (int64_t)pc * VEC)), a);
-#pragma unroll
-            for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(a[j], acc[j]);
-        } else if (len == 0) {
-            C::store_nt(out + (row * f.out_stride + (int64_t)(oc0 + pc) * VEC), C::zero());
-            continue;
-        }
-        C::store_nt(out + (row * f.out_stride + (int64_t)(oc0 + pc) * VEC), C::from_f32(acc));
-    }
-}
-
-// One item (64 / G rows) per wave: the record replaces the range load, so a wave whose rows hold at most
-// REC_N entries spends two dependent round trips (record, feature rows) instead of three.
-template <typename T, int VEC, int G>
-__global__ __launch_bounds__(SHPL_BLOCK) void k_rows2s(const RowsSide s0, const RowsSide s1, int64_t items0,
-                                                       int64_t items) {
-    typedef Chunk<T, VEC> C;
-    const int lane = threadIdx.x & 63, lg = lane & (G - 1);
-    const int64_t it = (int64_t)blockIdx.x * (SHPL_BLOCK / SHPL_WAVE) + (threadIdx.x >> 6);
-    if (it >= items) return;  // wave-uniform
-    Rec cur;
-    typename C::raw_t av = C::zero();
-    bool live, second;
-    int64_t row;
-    rec_fetch<T, VEC, G>(s0, s1, items0, it, cur, av, live, row, second);
-    int32_t wlen = cur.end - cur.first;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) wlen = max(wlen, __shfl_xor(wlen, o, 64));
-    const Feat &f = second ? s1.f : s0.f;
-    if (wlen <= REC_N) {
-        row_short<T, VEC, G>(f, row, live, cur, av);
-        return;
-    }
-    const bool p0 = live && f.mode == SHPL_OUT_CONCAT && (uint32_t)lg < f.cpass;
-    typename C::raw_t pv = C::zero();
-    if (p0) pv = C::load_nt(reinterpret_cast<const T *>(f.pass) + f.pass_off + (row * f.pass_stride + (int64_t)lg * VEC));
-    if (second)
-        row_walk<T, VEC, true, G>(s1.f, s1.e, row, live, cur.first, cur.end, p0, pv, av);
-    else
-        row_walk<T, VEC, false, G>(s0.f, s0.e, row, live, cur.first, cur.end, p0, pv, av);
+        rows_body<T, VEC, false, G>(s0.f, s0.e, s0.key_range, s0.n_rows, (int64_t)blockIdx.x - s1.blocks);
 }
 
 bool aligned(const void *ptr, int64_t a) { return ((uintptr_t)ptr) % (uintptr_t)a == 0; }
@@ -1041,24 +867,6 @@ int pair_t(RowsSide s[2], int G, hipStream_t st) {
     const int64_t blocks = s[0].blocks + s[1].blocks;
     if (blocks == 0) return SHPL_OK;
     if (blocks > 0x7fffffffLL) return SHPL_ERR_BAD_SHAPE;
-    const bool recs = (s[0].n_rows == 0 || s[0].key_rec) && (s[1].n_rows == 0 || s[1].key_rec);
-    if (recs) {  // items = waves' worth of rows (64 / G each), both pulls in one list
-        const int64_t rpw = SHPL_WAVE / G;
-        const int64_t items0 = (s[0].n_rows + rpw - 1) / rpw, items = items0 + (s[1].n_rows + rpw - 1) / rpw;
-        const int64_t grid = (items + SHPL_BLOCK / SHPL_WAVE - 1) / (SHPL_BLOCK / SHPL_WAVE);
-#define SHPL_ROWS2R(GG)                                                                                          \
-    hipLaunchKernelGGL((k_rows2s<T, VEC, GG>), dim3((unsigned)grid), dim3(SHPL_BLOCK), 0, st, s[0], s[1], items0, \
-                       items)
-        switch (G) {
-            case 8: SHPL_ROWS2R(8); break;
-            case 16: SHPL_ROWS2R(16); break;
-            case 32: SHPL_ROWS2R(32); break;
-            default: SHPL_ROWS2R(64); break;
-        }
-#undef SHPL_ROWS2R
-        SHPL_LAUNCH_CHECK();
-        return SHPL_OK;
-    }
 #define SHPL_ROWS2(GG) hipLaunchKernelGGL((k_rows2<T, VEC, GG>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, s[0], s[1])
     switch (G) {
         case 8: SHPL_ROWS2(8); break;
@@ -1115,7 +923,7 @@ extern "C" int shpl_pull_pair(const shpl_csr *by_cell, const shpl_pull_desc *d_c
         v16 = pl[k].v16;
         while (G < 64 && (uint32_t)G < pl[k].f.cpool) G <<= 1;  // lanes per row: the widest pooled row
         s[k] = RowsSide{pl[k].f, Ents{c->nnz_cap, c->ent_dst, c->ent_src, c->ent_col, c->ent_val}, c->key_range,
-                        pl[k].n_dst, 0, c->key_rec};
+                        pl[k].n_dst, 0};
     }
     if (dtype < 0) return SHPL_OK;
     if (dtype == SHPL_F32) return v16 ? pair_t<float, 4>(s, G, st) : pair_t<float, 1>(s, G, st);

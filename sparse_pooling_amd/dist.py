@@ -90,7 +90,11 @@ def _sync(device):
         torch.cuda.synchronize(device)
 
 
-def timed(fn, steps, device=None):
+TIMING_METHOD = ("per-rank span from after the opening barrier + device sync to the rank's closing device "
+                 "sync (the closing barrier is not timed); MAX over ranks")
+
+
+def timed(fn, steps, device=None, info=None):
     """Run ``fn`` ``steps`` times between barriers + device syncs; returns the
     elapsed seconds maximised over ranks.
 
@@ -98,7 +102,10 @@ def timed(fn, steps, device=None):
     its closing device sync; the closing barrier comes after the clock stops,
     so a collective's own latency (a visible share of an 8-rank run's ~6 ms
     window) is never timed. The MAX over ranks is then the slowest rank's
-    compute span, all ranks having started together."""
+    compute span, all ranks having started together.
+    info (a dict, optional) receives the method and, for comparison with
+    rounds 1-2 (whose clock stopped after the closing barrier), the
+    barrier-inclusive elapsed time, MAX over ranks."""
     on = dist.is_available() and dist.is_initialized()
     if on:
         dist.barrier()
@@ -110,11 +117,25 @@ def timed(fn, steps, device=None):
     elapsed = time.perf_counter() - t0
     if on:
         dist.barrier()
+    with_barrier = time.perf_counter() - t0
     if on:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=_coll_device(device))
+        t = torch.tensor([elapsed, with_barrier], dtype=torch.float64, device=_coll_device(device))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, with_barrier = float(t[0].item()), float(t[1].item())
+    if info is not None:
+        info.update(method=TIMING_METHOD, elapsed_s=elapsed, barrier_inclusive_s=with_barrier)
     return elapsed
+
+
+def gather_floats(values, device=None):
+    """All ranks' lists of floats (every rank the same length), rank order."""
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=_coll_device(device))
+    on = dist.is_available() and dist.is_initialized()
+    if not on:
+        return [[float(x) for x in t.cpu().tolist()]]
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [[float(x) for x in o.cpu().tolist()] for o in out]
 
 
 def gather_checksums(value, device=None):

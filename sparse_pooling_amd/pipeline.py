@@ -29,15 +29,14 @@ class FusedPipeline:
 
     def __init__(self, n_frames, max_points_per_frame, total_points, im_size, bv_size, stride,
                  c_bev, c_img, dtype=torch.float32, device="cuda", dual=False, rows=None, live=False,
-                 buckets=None, records=False):
+                 buckets=None):
         """live: the sparse passes walk each frame's live entries (shpl_csr frame layout) instead of the
         whole capacity -- for capacities far above the entry counts (FramePipeline: raw-scan slots per
         voxel point); at config 2 (capacity = entries) the capacity walk is faster (2.22 vs 2.24 ms).
         buckets (default: with rows): the index build also cuts M into destination buckets
         (shpl_build_index_buckets), one launch sorts both CSRs out of them (shpl_build_csr_buckets) and
         each pull pair is one row-keyed launch (shpl_pull_pair), all on one stream; the forward's
-        pass-through halves ride the index launches. records (bucketed): the CSRs also carry
-        per-destination records and the pull pairs run persistent waves over them (k_rows2s).
+        pass-through halves ride the index launches.
         rows without buckets: the range CSRs (one launch per key) + one k_rows launch per pull,
         on two streams."""
         dev = torch.device(device)
@@ -70,14 +69,11 @@ class FusedPipeline:
         self.frame_off = torch.empty(self.B + 1, dtype=torch.int64, device=dev)
         self.err = torch.zeros(1, **i32)
         self.index_ws = L.workspace(L.index_ws_bytes(self.B, self.max_points), dev)
-        # rows pulls: with key_range; bucketed: with the per-destination records too (k_rows2s), unless records=False
-        rec = self.buckets and records
-        self.csr = L.Csr(self.n_cells, self.N, dev, with_col=False, key_range=self.rows,
-                         key_rec=rec)  # BEV-cell CSR (img -> BEV)
+        # rows pulls: with key_range
+        self.csr = L.Csr(self.n_cells, self.N, dev, with_col=False, key_range=self.rows)  # BEV-cell CSR (img -> BEV)
         self.bv_fused = torch.empty((self.B, self.Hb, self.Wb, self.Cb + self.Ci), dtype=dtype, device=dev)
         if dual:
-            self.pcsr = L.Csr(self.n_pix, self.N, dev, with_col=True, key_range=self.rows,
-                              key_rec=rec)  # pixel CSR (BEV -> img)
+            self.pcsr = L.Csr(self.n_pix, self.N, dev, with_col=True, key_range=self.rows)  # pixel CSR (BEV -> img)
             self.img_fused = torch.empty((self.B, self.Hi, self.Wi, self.Ci + self.Cb), dtype=dtype,
                                          device=dev)
         if live:
@@ -306,79 +302,6 @@ class FusedPipeline:
         if events:
             events[3].record(main)
 
-    # ----------------------------------------------- frame-group pipelining
-    def set_frame_layout(self, host_point_offsets, groups=4):
-        """Host copy of the point offsets (the entry slots of each frame), for
-        step_pipelined: the batch is cut into `groups` frame groups whose
-        pooled rows are filled while the next group's rows stream."""
-        off = np.asarray(host_point_offsets, dtype=np.int64)
-        assert off.shape == (self.B + 1,)
-        G = max(1, min(int(groups), self.B))
-        bounds = [round(g * self.B / G) for g in range(G + 1)]
-        cells = self.Hb * self.Wb
-        self._groups = []
-        for g in range(G):
-            f0, f1 = bounds[g], bounds[g + 1]
-            e0, e1 = int(off[f0]), int(off[f1])
-            c = self.csr
-            sp = L.ShplCsr(c.ent_dst.data_ptr() + 4 * e0, c.ent_src.data_ptr() + 4 * e0,
-                           c.ent_val.data_ptr() + 4 * e0, None, c.n_keys, e1 - e0)
-            dn = L.ShplCsr(c.ent_dst.data_ptr(), c.ent_src.data_ptr(), c.ent_val.data_ptr(), None,
-                           (f1 - f0) * cells, max(e1 - e0, 1))
-            self._groups.append(dict(sparse=sp, dense=dn, rows=(f0 * cells, f1 * cells), frames=(f0, f1),
-                                     entries=(e0, e1)))
-        return self._groups
-
-    def step_pipelined(self, points, voxels, point_offsets, P, bev, img, dstream, sstream, mval=None,
-                       events=None):
-        """step() with the layer cut into frame groups (set_frame_layout): group g's
-        streaming rows (k_dense) run on `dstream` back to back, and its pooled rows
-        (k_sparse) on `sstream` as soon as group g streamed and M is sorted -- the
-        gathers of group g overlap the streaming of group g+1. The index build and
-        the CSR run on the current stream beside the first groups.
-        events: None or dict of lists 'dense' / 'sparse' ([start, end] per group)
-        and 'span' ([start on dstream, end on sstream])."""
-        assert not self.dual, "frame-group pipelining covers the img->BEV layer"
-        main = torch.cuda.current_stream(self.dev)
-        dstream.wait_stream(main)
-        sstream.wait_stream(main)
-        width = self.Cb + self.Ci
-        esz = self.bv_fused.element_size()
-        dt = L.dtype_code(self.bv_fused)
-        ds, ss = ctypes.c_void_p(dstream.cuda_stream), ctypes.c_void_p(sstream.cuda_stream)
-        done = []
-        if events:
-            events["span"][0].record(dstream)
-        for g, grp in enumerate(self._groups):
-            r0 = grp["rows"][0]
-            if events:
-                events["dense"][g][0].record(dstream)
-            L.check(self._lib.shpl_pull_dense(
-                L.BY_CELL, dt, ctypes.byref(grp["dense"]), L.ptr(img), self.Ci, 0, self.Ci,
-                ctypes.c_void_p(bev.data_ptr() + r0 * self.Cb * esz), self.Cb, 0, self.Cb, L.OUT_CONCAT,
-                ctypes.c_void_p(self.bv_fused.data_ptr() + r0 * width * esz), width, ds), "shpl_pull_dense")
-            ev = torch.cuda.Event()
-            ev.record(dstream)
-            done.append(ev)
-            if events:
-                events["dense"][g][1].record(dstream)
-        self.build_index(points, voxels, point_offsets, P, mval)
-        self.build_csr()
-        sstream.wait_stream(main)  # M sorted
-        for g, grp in enumerate(self._groups):
-            sstream.wait_event(done[g])
-            if events:
-                events["sparse"][g][0].record(sstream)
-            L.check(self._lib.shpl_pull_sparse(
-                L.BY_CELL, dt, ctypes.byref(grp["sparse"]), L.ptr(img), self.Ci, 0, self.Ci, L.ptr(bev), self.Cb, 0,
-                self.Cb, L.OUT_CONCAT, L.ptr(self.bv_fused), width, ss), "shpl_pull_sparse")
-            if events:
-                events["sparse"][g][1].record(sstream)
-        if events:
-            events["span"][1].record(sstream)
-        main.wait_stream(sstream)
-        main.wait_stream(dstream)
-
     def backward(self, g_bv, g_img, d_bev, d_img, side2=None):
         """TF gradient of the dual layer with the concat split and add_n fused:
         d_bev = g_bv[..., :Cb] + M^T-pull of g_img[..., Ci:]
@@ -467,6 +390,7 @@ class FramePipeline(FusedPipeline):
     # where velo_step starts the streaming half: "start" (beside the whole index chain), or after the
     # chain's "velo" / "bev" / "csr" stage (the chain then runs with the chip to itself until there)
     dense_after = "start"
+    DENSE_AFTER, MAPS_AFTER, MAPS_FORMS = ("start", "velo", "bev", "csr"), ("stream", "chain"), ("f64", "bev_input")
 
     def build_bev(self, points, point_offsets, planes, point_counts=None, maps=None):
         from . import bev as _bev
@@ -515,6 +439,12 @@ class FramePipeline(FusedPipeline):
         side: a stream for the layer's streaming half (it needs no index), run beside
         the index chain. events: 9 timing events (dense start/end on `side`; then
         velo, bev, index, csr boundaries, sparse start/end on the current stream)."""
+        if self.dense_after not in self.DENSE_AFTER:
+            raise ValueError(f"dense_after must be one of {self.DENSE_AFTER}, not {self.dense_after!r}")
+        if self.maps_after not in self.MAPS_AFTER:
+            raise ValueError(f"maps_after must be one of {self.MAPS_AFTER}, not {self.maps_after!r}")
+        if self.maps_form not in self.MAPS_FORMS:
+            raise ValueError(f"maps_form must be one of {self.MAPS_FORMS}, not {self.maps_form!r}")
         if side is not None:
             # the 1.7 GB of f64 maps (64 frames) are written on `side` after the streaming pass, from the
             # voxelizer's sorted words (shpl_bev_maps): off the index chain, and streaming after the

@@ -48,7 +48,11 @@ def _worker(rank, world, port, q):
     import time
     fids = sd.partition(GLOBAL, world, rank, "strong")
     out = _frame_outputs(fids)
-    el = sd.timed(lambda k: time.sleep(0.05 * (rank + 1)), 2)   # rank 1 is slower on purpose
+    info = {}
+    el = sd.timed(lambda k: time.sleep(0.05 * (rank + 1)), 2, info=info)   # rank 1 is slower on purpose
+    assert info["elapsed_s"] == el and info["barrier_inclusive_s"] >= el and "MAX over ranks" in info["method"]
+    # the bench's per-rank kernel times: every rank's list, rank order
+    assert sd.gather_floats([rank, 0.5 * rank]) == [[float(r), 0.5 * r] for r in range(world)]
     cs = sd.gather_frame_checksums(sd.frame_checksums(out))
     comm = sd.comm_report(None)
     assert comm["backend"] == "gloo" and comm["world_size"] == world

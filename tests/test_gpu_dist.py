@@ -42,6 +42,13 @@ def test_strong_partition_two_ranks_matches_one(extra):
     assert two["comm"]["backend"] == "gloo" and two["comm"]["world_size"] == 2
     assert [r["rank"] for r in two["comm"]["ranks"]] == [0, 1]
     assert one["comm"]["world_size"] == 1 and one["lib_sha256"] == two["lib_sha256"]
+    # the N > 1 roofline describes the slowest rank, every rank's kernel times beside it
+    per = two["roofline"]["per_rank"]
+    assert [r["rank"] for r in per] == [0, 1]
+    assert two["roofline"]["kernel_ms"] == max(r["kernel_ms"] for r in per)
+    assert two["roofline"]["rank"] == max(per, key=lambda r: r["kernel_ms"])["rank"]
+    assert "per_rank" not in one["roofline"]
+    assert two["timing"]["barrier_inclusive_s"] >= two["timing"]["elapsed_s"] > 0
 
 
 def test_eight_frame_rank_shape_matches_stored_n1_table():

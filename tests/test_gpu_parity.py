@@ -387,7 +387,7 @@ def test_range_csr_one_long_run(n):
     """Every entry of a frame on ONE destination (all points on one cell and one
     pixel): the range CSR's degenerate case (one run longer than its LDS list at
     n = 20000), row-keyed pulls in both directions against the oracle, bitwise;
-    the bucket builder (linear in the run) gives the same cell-keyed entry list."""
+    the per-frame builder (tile sort, no key ranges) gives the same cell-keyed entry list."""
     from sparse_pooling_amd import _lib as L
     from sparse_pooling_amd import shpl_map as sm
     rng = np.random.default_rng(5)
@@ -413,14 +413,14 @@ def test_range_csr_one_long_run(n):
     _close_and_exact(_np(trans), orc.sparse_pool_trans_op(mij, mval, [R, n], bev.reshape(-1, c), idx,
                                                           img.shape).reshape(h * w, c))
     lists = []
-    for path in (L.CSR_RANGE, L.CSR_BUCKET):
-        cs = L.Csr(smap.n_cells, smap.nnz_cap, DEV, with_col=False, key_range=True)
+    for path in (L.CSR_RANGE, L.CSR_FRAME):
+        cs = L.Csr(smap.n_cells, smap.nnz_cap, DEV, with_col=False, key_range=path == L.CSR_RANGE)
         L.check(L.lib().shpl_build_csr_path(path, L.BY_CELL, L.ORDER_ENTRY, 1, L.ptr(smap.frame_off),
                                             L.ptr(smap.frame_nnz), smap.n_cells, L.ptr(smap.cell), L.ptr(smap.col),
                                             L.ptr(smap.val), L.ptr(smap.pix), cs.ref(), L.ptr(cs.ws), cs.ws.numel(),
                                             L.stream_of(torch.device(DEV))), "shpl_build_csr_path")
         torch.cuda.synchronize()
-        lists.append([_np(t).copy() for t in (cs.ent_dst, cs.ent_src, cs.ent_val, cs.key_range)])
+        lists.append([_np(t).copy() for t in (cs.ent_dst, cs.ent_src, cs.ent_val)])
     for a, b in zip(*lists):
         np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
 
@@ -467,38 +467,6 @@ def test_pipeline_batch_matches_oracle(cfg, dual):
         _close_and_exact(out[f:f + 1], eb)
         if dual:
             _close_and_exact(iout[f:f + 1], ei)
-
-
-@pytest.mark.parametrize("groups", [2, 3])
-def test_pipelined_frame_groups_match_oracle(groups):
-    """step_pipelined (the bench's config-2 step: layer cut into frame groups,
-    gathers on a second stream beside the next group's stream) == oracle, twice
-    in a row (buffers reused across steps)."""
-    from sparse_pooling_amd import pipeline
-    spec = synth.CONFIGS[2]
-    F = 5
-    frames = [synth.make_frame(spec, seed=60 + f, n_outside=31 * f) for f in range(F)]
-    pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
-    pl = pipeline.FusedPipeline(F, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev, spec.c_img)
-    host_off = np.concatenate([[0], np.cumsum([f.points.shape[0] for f in frames])])
-    pl.set_frame_layout(host_off, groups)
-    Hb, Wb = spec.bev_feat_hw
-    Hi, Wi = spec.img_feat_hw
-    bev = torch.from_numpy(synth.make_features((F, Hb, Wb, spec.c_bev), 3)).to(DEV)
-    img = torch.from_numpy(synth.make_features((F, Hi, Wi, spec.c_img), 4)).to(DEV)
-    d, s_ = torch.cuda.Stream(), torch.cuda.Stream()
-    pl.step_pipelined(pts, vox, off, P, bev, img, d, s_)
-    first = pl.bv_fused.clone()
-    pl.bv_fused.fill_(float("nan"))
-    pl.step_pipelined(pts, vox, off, P, bev, img, d, s_)
-    torch.cuda.synchronize()
-    assert torch.equal(first, pl.bv_fused)
-    out = _np(pl.bv_fused)
-    for f in (0, F - 1):
-        ref = _oracle_frame(frames[f], spec.stride)
-        eb, _ = orc.sparse_pool_layer(_np(bev[f:f + 1]), _np(img[f:f + 1]), ref["Mij_pool"], ref["M_val"],
-                                      ref["M_size"], ref["img_index_flip_pool"])
-        _close_and_exact(out[f:f + 1], eb)
 
 
 def test_full_size_properties_config5():
@@ -675,12 +643,10 @@ def _ragged_pipeline_run(cfg, sizes, dtype, paths, channels=None, frames=None):
         else:
             np.testing.assert_array_equal(_np(got.view(torch.int16)).view(np.uint16),
                                           orc.to_bf16_bits(exp.astype(np.float32)))
-    codes = {None: L.CSR_AUTO, "frame": L.CSR_FRAME, "segment": L.CSR_SEGMENT, "range": L.CSR_RANGE,
-             "bucket": L.CSR_BUCKET}
+    codes = {None: L.CSR_AUTO, "frame": L.CSR_FRAME, "segment": L.CSR_SEGMENT, "range": L.CSR_RANGE}
     for path in paths:
         # a named CSR builder: the CSR pulls (no buckets); None: the pipeline's default
-        kw = {"buckets": dict(rows=True, buckets=True, records=True),
-              "buckets_norec": dict(rows=True, buckets=True, records=False),
+        kw = {"buckets": dict(rows=True, buckets=True),
               "csr_rows": dict(rows=True, buckets=False), None: {}}.get(path, dict(buckets=False))
         pl = pipeline.FusedPipeline(B, maxp, N, base.im_size, base.bv_size, base.stride, Cb, Ci, dtype=tdt,
                                     dual=True, **kw)
@@ -706,14 +672,13 @@ def _ragged_pipeline_run(cfg, sizes, dtype, paths, channels=None, frames=None):
                                          ("f32", 3, 5), ("bf16", 8, 24), ("f32", 64, 128), ("f32", 4, 6)])
 def test_bucket_pulls_ragged_batch(dtype, cb, ci):
     """The bucketed step (shpl_build_index_buckets -> shpl_build_csr_buckets -> shpl_pull_pair:
-    both CSRs in one launch, both pulls in one launch -- over per-destination records, k_rows2s, and
-    without them, k_rows2 --, forward then gradients) at config 3's
+    both CSRs in one launch, both pulls in one launch (k_rows2), forward then gradients) at config 3's
     geometry over a ragged batch -- no points,
     one point, no survivor, one survivor among 14 points (the dgemv projection order: no
     bucket, the entry read from the index arrays), chunk-straddling and full frames --
     bitwise against the oracle and against the range CSR + k_rows path, for every lane
     group width (G = 8 .. 64) and the unvectorised form (3 / 5 and 4 / 6 f32 channels)."""
-    _ragged_pipeline_run(3, [0, 1, -40, 1025, 20000, 2], dtype, ["buckets", "buckets_norec", "csr_rows"],
+    _ragged_pipeline_run(3, [0, 1, -40, 1025, 20000, 2], dtype, ["buckets", "csr_rows"],
                          channels=(cb, ci))
 
 
@@ -733,7 +698,7 @@ def test_bucket_pulls_long_runs():
     frames = [heavy, synth.make_frame(synth.FrameSpec(3000, base.im_size, base.bv_size, base.stride, 32, 32),
                                       seed=5, n_outside=int(rng.integers(1, 50))), mixed]
     for dtype in ("f32", "bf16"):
-        _ragged_pipeline_run(3, None, dtype, ["buckets", "buckets_norec"], channels=(32, 32), frames=frames)
+        _ragged_pipeline_run(3, None, dtype, ["buckets"], channels=(32, 32), frames=frames)
 
 
 def test_pipeline_ragged_batch_every_csr_path():
@@ -741,8 +706,8 @@ def test_pipeline_ragged_batch_every_csr_path():
     -> dual layer -> both gradients) at config-2 shape: a frame without points,
     a one-point frame, a frame whose points all fall outside the image, frames
     straddling the index builder's chunks -- under each CSR builder (per-frame
-    workgroup, segments, destination ranges, range buckets), bitwise against the oracle."""
-    _ragged_pipeline_run(2, [0, 1, -40, 1025, 20000, 2], "f32", ["frame", "segment", "range", "bucket"])
+    workgroup, segments, destination ranges), bitwise against the oracle."""
+    _ragged_pipeline_run(2, [0, 1, -40, 1025, 20000, 2], "f32", ["frame", "segment", "range"])
 
 
 def test_pipeline_ragged_batch_row_keyed_bf16():
