@@ -183,7 +183,9 @@ int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, const int64_t 
  * later, on another stream (FramePipeline.velo_step: after the layer's
  * streaming pass). zero != 0 first zero-fills both maps (shpl_bev_slices'
  * maps arrive zero-filled; here the caller may have zeroed them itself).
- * Same values as shpl_bev_slices' maps, bit for bit. */
+ * Same values as shpl_bev_slices' maps, bit for bit. At most 4096 frames (a
+ * shpl_bev_slices call over more frames keeps no per-frame word counts in the
+ * workspace: SHPL_ERR_BAD_SHAPE here; its own maps are unaffected). */
 int shpl_bev_maps(int n_frames, const int64_t *d_point_offsets, int64_t total_points, const void *d_points,
                   int points_dtype, const double *d_planes, const double *area_extents, double voxel_size,
                   int num_slices, const double *slice_lo, const double *slice_hi, double density_lo,

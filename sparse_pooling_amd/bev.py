@@ -56,6 +56,12 @@ class BevBatch:
         workspace (the workspace must not be reused in between): bitwise the maps bev_slices_batch
         writes with maps=True."""
         c = self._call
+        nx, nz = grid_divisions(c["ext"].reshape(3, 2), c["vs"])
+        for t, shape in ((height_maps, (c["F"], c["S"], nz, nx)), (density_map, (c["F"], nz, nx))):
+            if t is not None and (t.dtype != torch.float64 or not t.is_contiguous() or tuple(t.shape) != shape
+                                  or t.device != c["pts"].device):
+                raise ValueError(f"map tensors must be contiguous f64 {shape} on {c['pts'].device}, "
+                                 f"got {tuple(t.shape)} {t.dtype}")
         L.check(L.lib().shpl_bev_maps(c["F"], L.ptr(c["off"]), c["N"], L.ptr(c["pts"]), L.F64, L.ptr(c["planes"]),
                                       c["p"](c["ext"]), c["vs"], c["S"], c["p"](c["lo"]), c["p"](c["hi"]), c["hlo"],
                                       c["hhi"], c["hpd"], c["p"](c["table"]), L.ptr(height_maps),
@@ -69,7 +75,12 @@ class BevBatch:
         np.dstack((*height_maps, density_map)) (kitti_dataset.py:368) as the tf.float32 placeholder holds it
         (each map value rounded to f32 once), from the voxelizer's sorted words like write_maps."""
         c = self._call
-        assert bev_input.dtype == torch.float32 and bev_input.is_contiguous()
+        nx, nz = grid_divisions(c["ext"].reshape(3, 2), c["vs"])
+        shape = (c["F"], nz, nx, c["S"] + 1)
+        if (bev_input.dtype != torch.float32 or not bev_input.is_contiguous() or tuple(bev_input.shape) != shape
+                or bev_input.device != c["pts"].device):
+            raise ValueError(f"bev_input must be a contiguous f32 {shape} tensor on {c['pts'].device}, "
+                             f"got {tuple(bev_input.shape)} {bev_input.dtype}")
         L.check(L.lib().shpl_bev_input(c["F"], L.ptr(c["off"]), c["N"], L.ptr(c["pts"]), L.F64, L.ptr(c["planes"]),
                                        c["p"](c["ext"]), c["vs"], c["S"], c["p"](c["lo"]), c["p"](c["hi"]), c["hlo"],
                                        c["hhi"], c["hpd"], c["p"](c["table"]), L.ptr(bev_input), L.ptr(c["ws"]),

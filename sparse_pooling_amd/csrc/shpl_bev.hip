@@ -176,7 +176,7 @@ __global__ __launch_bounds__(BEV_BLOCK) void k_bev_frame(BevGeom g, const int64_
     }
     if (threadIdx.x == 0) {
         frame_nvox[f] = kept < cap ? kept : cap;
-        frame_nent[f] = n_ent;  // the sorted words stay in the workspace for shpl_bev_maps
+        if (frame_nent) frame_nent[f] = n_ent;  // the sorted words stay in the workspace for shpl_bev_maps
     }
 }
 
@@ -226,7 +226,9 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bev_maps(BevGeom g, const int64_
     }
 }
 
-constexpr int BEV_MAX_FRAMES = 4096;  // frames of one call (the per-frame word counts in the workspace)
+// frames of one call whose sorted words shpl_bev_maps / shpl_bev_input can read back (the per-frame word
+// counts in the workspace); a larger shpl_bev_slices call works as before but leaves no counts
+constexpr int BEV_MAX_FRAMES = 4096;
 
 size_t bev_half_bytes(int64_t total_points, int num_slices) {
     const size_t n = (size_t)(total_points > 0 ? total_points : 1) * (size_t)(num_slices + 1);
@@ -294,7 +296,7 @@ extern "C" int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, con
         return SHPL_ERR_ARG;
     if (num_slices < 1 || num_slices > BEV_MAX_SLICES || !(voxel_size > 0)) return SHPL_ERR_BAD_SHAPE;
     if (total_points > 0 && (!d_points || !d_voxel_indices || !d_pts_in_voxel)) return SHPL_ERR_ARG;
-    if (total_points >= ((int64_t)1 << 31) || n_frames > BEV_MAX_FRAMES) return SHPL_ERR_BAD_SHAPE;
+    if (total_points >= ((int64_t)1 << 31)) return SHPL_ERR_BAD_SHAPE;
     size_t need;
     shpl_bev_workspace_bytes(total_points, num_slices, &need);
     if (need > ws_bytes) return SHPL_ERR_WORKSPACE;
@@ -305,7 +307,7 @@ extern "C" int shpl_bev_slices(int n_frames, const int64_t *d_point_offsets, con
     const size_t half = bev_half_bytes(total_points, num_slices);
     uint64_t *tmp = (uint64_t *)d_ws;
     uint64_t *srt = (uint64_t *)((char *)d_ws + half);
-    int32_t *nent = (int32_t *)((char *)d_ws + 2 * half);
+    int32_t *nent = n_frames <= BEV_MAX_FRAMES ? (int32_t *)((char *)d_ws + 2 * half) : nullptr;
     hipStream_t s = (hipStream_t)stream;
     const int64_t per_map = (int64_t)g.nx * g.nz;
     // the maps' zeros: a streaming kernel (hipMemsetAsync's fill ran at ~2.2 TB/s, beside k_dense)

@@ -760,6 +760,41 @@ def test_bev_slices_batch_vs_oracle():
     for f in range(3):
         want = np.dstack((*_np(b.height_maps[f]), _np(b.density_map[f]))).astype(np.float32)
         np.testing.assert_array_equal(_np(bin_[f]).view(np.uint32), want.view(np.uint32))
+    # output tensors of the wrong shape / dtype / layout are refused before any device write
+    nz, nx = b.density_map.shape[1:]
+    f64 = dict(dtype=torch.float64, device=DEV)
+    for hm, dm in [(torch.empty((3, S, nz, nx - 1), **f64), torch.empty((3, nz, nx), **f64)),
+                   (torch.empty((3, S, nz, nx), **f64), torch.empty((3, nz, nx), dtype=torch.float32, device=DEV)),
+                   (torch.empty((3, S, nx, nz), **f64).transpose(2, 3), torch.empty((3, nz, nx), **f64))]:
+        with pytest.raises(ValueError):
+            b.write_maps(hm, dm)
+    with pytest.raises(ValueError):
+        b.write_bev_input(torch.empty((3, nz, nx, S), dtype=torch.float32, device=DEV))
+
+
+def test_bev_slices_more_frames_than_map_table():
+    """shpl_bev_slices over more frames than shpl_bev_maps can read back (4096): the voxelizer and its own
+    maps work (the round-3 API regression fixed), only the deferred maps call refuses the batch."""
+    from sparse_pooling_amd import bev
+    F = 4100
+    cloud = synth.make_cloud(64, seed=7)
+    pts = torch.from_numpy(np.ascontiguousarray(np.tile(cloud.T, (F, 1)))).to(DEV)
+    off = torch.arange(F + 1, dtype=torch.int64, device=DEV) * cloud.shape[1]
+    pl = torch.from_numpy(np.tile(synth.GROUND_PLANE, (F, 1))).to(DEV)
+    b = bev.bev_slices_batch(pts, off, pl, synth.AREA_EXTENTS, synth.VOXEL_SIZE, synth.HEIGHT_LO,
+                             synth.HEIGHT_HI, synth.NUM_SLICES, maps=False)  # 4100 frames of maps: 92 GB
+    torch.cuda.synchronize()
+    hm, dm, vox, upts = orc.bev_slices(cloud, synth.GROUND_PLANE, synth.AREA_EXTENTS, synth.VOXEL_SIZE,
+                                       synth.HEIGHT_LO, synth.HEIGHT_HI, synth.NUM_SLICES)
+    n = _np(b.frame_nvox)
+    assert (n == vox.shape[0]).all() and int(b.err.item()) == 0
+    for f in (0, F // 2, F - 1):
+        a = f * cloud.shape[1]
+        np.testing.assert_array_equal(_np(b.voxel_indices[a:a + n[f]]), vox)
+        np.testing.assert_array_equal(_np(b.pts_in_voxel[a:a + n[f]]), upts)
+    from sparse_pooling_amd import _lib as L
+    with pytest.raises(L.ShplLibraryError, match="shpl_bev_maps"):
+        b.write_maps(None, None)  # the deferred maps call: SHPL_ERR_BAD_SHAPE
 
 
 def test_points_to_fused_layer_pipeline():
