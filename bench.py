@@ -83,6 +83,9 @@ def parse():
     ap.add_argument("--no-buckets", action="store_true",
                     help="row-keyed layers (config 3): range CSRs + one k_rows launch per pull on two streams "
                          "instead of the index build's buckets, one CSR launch and one shpl_pull_pair launch per pull pair")
+    ap.add_argument("--pixel-cols", action="store_true",
+                    help="bucketed config 3: the pixel-keyed CSR keeps ent_col (per-column partials in its pulls) "
+                         "instead of the identity-column form")
     ap.add_argument("--no-riders", action="store_true",
                     help="bucketed config 3: copy the forward's pass-through halves with their own launches before the "
                          "index build instead of as extra workgroups of the index launches")
@@ -398,6 +401,7 @@ def main():
     F = len(fids)
     frames = [synth.make_frame(spec, seed=s, n_outside=200) for s in fids]
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, dev)
+    pipeline.FusedPipeline.PIXEL_COLS = args.pixel_cols
     pl = pipeline.FusedPipeline(F, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev,
                                 spec.c_img, dtype=dtype, dual=dual, device=dev,
                                 buckets=False if args.no_buckets else None)
@@ -896,6 +900,7 @@ def run_conv(args, world, rank, dev):
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     frames = [synth.make_frame(spec, seed=s, n_outside=200) for s in fids]
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, dev)
+    pipeline.FusedPipeline.PIXEL_COLS = args.pixel_cols
     pl = pipeline.FusedPipeline(F, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev, spec.c_img,
                                 dtype=dtype, device=dev)
     Hb, Wb = spec.bev_feat_hw

@@ -286,7 +286,10 @@ typedef struct {
     int32_t *ent_dst;  /* [nnz_cap] destination row of each sorted entry (-1 = empty slot) */
     int32_t *ent_src;  /* [nnz_cap] source row of each sorted entry                        */
     float *ent_val;    /* [nnz_cap] M value of each sorted entry                           */
-    int32_t *ent_col;  /* [nnz_cap] column k of each sorted entry (SHPL_BY_PIXEL; else NULL) */
+    int32_t *ent_col;  /* [nnz_cap] column k of each sorted entry (SHPL_BY_PIXEL; else NULL). A pixel-keyed
+                          CSR of shpl_build_csr_buckets may leave it NULL: every entry of the index builder's
+                          maps is a column of its own, and the pulls then sum without per-column partials
+                          (bitwise the same: each partial is one product) */
     int64_t n_keys;    /* destination rows (all frames)                                      */
     int64_t nnz_cap;   /* capacity of the entry arrays                                       */
     int32_t *key_range; /* optional [n_keys][2]: (first, end) sorted entry of each destination's
@@ -456,7 +459,7 @@ typedef struct {
 } shpl_pull_desc;
 
 /* Both CSRs of the map (by_cell: SHPL_BY_CELL, SHPL_ORDER_ENTRY; by_pixel:
- * SHPL_BY_PIXEL, SHPL_ORDER_COL_ROW with ent_col; either may be NULL) from
+ * SHPL_BY_PIXEL, SHPL_ORDER_COL_ROW, ent_col optional; either may be NULL) from
  * the buckets, in ONE launch: a workgroup per (key, frame, range) sorts its
  * bucket by destination, stably (the bucket is in entry order), emits the
  * sorted entries and key_range (when set) and clears the unused capacity --

@@ -498,6 +498,9 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse_long(const Feat f, const 
 #define SHPL_ROWS_WALK 8
 #endif
 constexpr int ROWS_WALK = SHPL_ROWS_WALK;
+#ifndef SHPL_RPROBE
+#define SHPL_RPROBE 0  // timing probes of the row walk (wrong results): 1 every gather from the first 64 rows, 2 no stores
+#endif
 
 // The walk of one row's run [first, end) (all lanes of the wave, wave-uniform trip counts); pv / av: the
 // lane's first pass-through chunk (CONCAT, when p0) and first ADD operand, loaded by the caller.
@@ -541,7 +544,7 @@ __device__ __forceinline__ void row_walk(const Feat &f, const Ents &e, int64_t r
                 for (int u = 0; u < ROWS_WALK; ++u) {
                     const int32_t sr = __shfl(my_src, gbase + ((u0 + u) & (G - 1)), 64);
                     if (mine && j0 + u0 + u < len && u0 + u < G)
-                        raw[u] = C::load(src + ((int64_t)sr * f.src_stride + (int64_t)pc * VEC));
+                        raw[u] = C::load(src + ((int64_t)(SHPL_RPROBE == 1 ? (sr & 63) : sr) * f.src_stride + (int64_t)pc * VEC));
                 }
 #pragma unroll
                 for (int u = 0; u < ROWS_WALK; ++u) {
@@ -581,6 +584,10 @@ __device__ __forceinline__ void row_walk(const Feat &f, const Ents &e, int64_t r
             for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(a[j], acc[j]);
         } else if (len == 0) {
             C::store_nt(out + (row * f.out_stride + (int64_t)(oc0 + pc) * VEC), C::zero());
+            continue;
+        }
+        if (SHPL_RPROBE == 2) {  // timing probe: no pooled stores (wrong results)
+            if (acc[0] == 1234.5f) C::store_nt(out, C::from_f32(acc));
             continue;
         }
         C::store_nt(out + (row * f.out_stride + (int64_t)(oc0 + pc) * VEC), C::from_f32(acc));
@@ -693,11 +700,11 @@ __device__ __forceinline__ bool sched_locate(const Sched &sc, const RowsSide &s0
 // The pixel-keyed pull's blocks come first: its longer runs (6.7 entries on average at config 3, up to 54 at
 // the horizon) then start early instead of forming the launch's tail (k_rows2 31.1 -> 24.0 us per pair,
 // profiles/r03_pixel_first_ab.log; reversing the order inside either side measured within noise).
-template <typename T, int VEC, int G>
+template <typename T, int VEC, int G, bool GR1>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_rows2(const RowsSide s0, const RowsSide s1, const Sched sc) {
     if (sc.mode == SCHED_ROUND_ROBIN) {
         if ((int64_t)blockIdx.x < s1.blocks)
-            rows_body<T, VEC, true, G>(s1.f, s1.e, s1.key_range, 0, s1.n_rows, (int64_t)blockIdx.x);
+            rows_body<T, VEC, GR1, G>(s1.f, s1.e, s1.key_range, 0, s1.n_rows, (int64_t)blockIdx.x);
         else
             rows_body<T, VEC, false, G>(s0.f, s0.e, s0.key_range, 0, s0.n_rows, (int64_t)blockIdx.x - s1.blocks);
         return;
@@ -706,7 +713,7 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_rows2(const RowsSide s0, const R
     int64_t frame, j;
     if (!sched_locate(sc, s0, s1, blockIdx.x, side, frame, j)) return;  // uniform
     if (side)
-        rows_body<T, VEC, true, G>(s1.f, s1.e, s1.key_range, frame * s1.kpf, (frame + 1) * s1.kpf, j);
+        rows_body<T, VEC, GR1, G>(s1.f, s1.e, s1.key_range, frame * s1.kpf, (frame + 1) * s1.kpf, j);
     else
         rows_body<T, VEC, false, G>(s0.f, s0.e, s0.key_range, frame * s0.kpf, (frame + 1) * s0.kpf, j);
 }
@@ -725,7 +732,6 @@ int plan(int direction, int dtype, const shpl_csr *csr, const void *d_src, int64
          void *d_out, int64_t out_stride, Plan *pl) {
     if (!csr) return SHPL_ERR_ARG;
     if (direction != SHPL_BY_CELL && direction != SHPL_BY_PIXEL) return SHPL_ERR_ARG;
-    if (direction == SHPL_BY_PIXEL && csr->nnz_cap > 0 && !csr->ent_col) return SHPL_ERR_ARG;
     if (dtype != SHPL_F32 && dtype != SHPL_BF16) return SHPL_ERR_ARG;
     if (mode < SHPL_OUT_POOL || mode > SHPL_OUT_ADD) return SHPL_ERR_ARG;
     const int64_t n_dst = csr->n_keys;
@@ -851,10 +857,16 @@ int sparse_t(const Plan &pl, const shpl_csr *csr, bool group, hipStream_t s) {
                  : sparse_tg<T, VEC, false>(pl, e, csr->nnz_cap, s);
 }
 
+// Per-column partials (TF's Q[k]) only where columns can repeat: a pixel-keyed CSR without ent_col has every
+// entry in a column of its own (the index builder's maps), where Q[k] is one product and the plain sum is
+// bitwise the same (0 + p differs from p only for p = -0, and an accumulator that starts at +0 never becomes
+// -0, so adding +0 or -0 to it gives the same bits).
+bool grouped(const shpl_csr *csr, int direction) { return direction == SHPL_BY_PIXEL && csr->ent_col != nullptr; }
+
 int sparse(const Plan &pl, const shpl_csr *csr, int direction, hipStream_t s) {
     if (pl.n_dst == 0 || pl.f.cpool == 0 || csr->nnz_cap == 0) return SHPL_OK;
     if (csr->n_frames < 0 || csr->n_frames > LIVE_MAX_FRAMES) return SHPL_ERR_ARG;
-    const bool group = direction == SHPL_BY_PIXEL;
+    const bool group = grouped(csr, direction);
     if (pl.dtype == SHPL_F32)
         return pl.v16 ? sparse_t<float, 4>(pl, csr, group, s) : sparse_t<float, 1>(pl, csr, group, s);
     return pl.v16 ? sparse_t<uint16_t, 8>(pl, csr, group, s) : sparse_t<uint16_t, 1>(pl, csr, group, s);
@@ -890,7 +902,7 @@ int rows_tv(const Plan &pl, const shpl_csr *csr, bool group, hipStream_t s) {
 
 int rows(const Plan &pl, const shpl_csr *csr, int direction, hipStream_t s) {
     if (pl.n_dst == 0) return SHPL_OK;
-    const bool group = direction == SHPL_BY_PIXEL;
+    const bool group = grouped(csr, direction);
     if (pl.dtype == SHPL_F32)
         return pl.v16 ? rows_tv<float, 4>(pl, csr, group, s) : rows_tv<float, 1>(pl, csr, group, s);
     return pl.v16 ? rows_tv<uint16_t, 8>(pl, csr, group, s) : rows_tv<uint16_t, 1>(pl, csr, group, s);
@@ -979,8 +991,13 @@ int pair_t(RowsSide s[2], int G, int n_frames, hipStream_t st) {
     int64_t blocks;
     const Sched sc = pair_sched(s, n_frames, rpb, &blocks);
     if (blocks > 0x7fffffffLL) return SHPL_ERR_BAD_SHAPE;
-#define SHPL_ROWS2(GG) \
-    hipLaunchKernelGGL((k_rows2<T, VEC, GG>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, s[0], s[1], sc)
+    const bool gr1 = s[1].e.col != nullptr;  // the pixel-keyed side's per-column partials (grouped())
+#define SHPL_ROWS2(GG)                                                                                              \
+    if (gr1)                                                                                                        \
+        hipLaunchKernelGGL((k_rows2<T, VEC, GG, true>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, s[0], s[1], \
+                           sc);                                                                                     \
+    else                                                                                                            \
+        hipLaunchKernelGGL((k_rows2<T, VEC, GG, false>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, s[0], s[1], sc)
     switch (G) {
         case 8: SHPL_ROWS2(8); break;
         case 16: SHPL_ROWS2(16); break;

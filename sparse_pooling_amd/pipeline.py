@@ -26,6 +26,8 @@ class FusedPipeline:
     # row-keyed pulls (one launch per pull, shpl_csr.key_range) for batches under this many frames whose
     # maps have at most ROWS_MAX_KEYS destinations per frame: latency-bound layers (config 3)
     ROWS_FRAMES, ROWS_MAX_KEYS, ROWS_MAX_CAP = 32, 65536, 1 << 24
+    # bucketed pixel-keyed CSRs with ent_col (per-column partials in the pulls; A/B of the identity-column form)
+    PIXEL_COLS = False
 
     def __init__(self, n_frames, max_points_per_frame, total_points, im_size, bv_size, stride,
                  c_bev, c_img, dtype=torch.float32, device="cuda", dual=False, rows=None, live=False,
@@ -73,7 +75,9 @@ class FusedPipeline:
         self.csr = L.Csr(self.n_cells, self.N, dev, with_col=False, key_range=self.rows)  # BEV-cell CSR (img -> BEV)
         self.bv_fused = torch.empty((self.B, self.Hb, self.Wb, self.Cb + self.Ci), dtype=dtype, device=dev)
         if dual:
-            self.pcsr = L.Csr(self.n_pix, self.N, dev, with_col=True, key_range=self.rows)  # pixel CSR (BEV -> img)
+            # pixel CSR (BEV -> img); from the buckets without ent_col: every entry its own column (shpl.h)
+            self.pcsr = L.Csr(self.n_pix, self.N, dev, with_col=not self.buckets or self.PIXEL_COLS,
+                              key_range=self.rows)
             self.img_fused = torch.empty((self.B, self.Hi, self.Wi, self.Ci + self.Cb), dtype=dtype,
                                          device=dev)
         if live:

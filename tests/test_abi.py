@@ -88,7 +88,7 @@ def test_argument_validation_is_host_side():
         assert fn(L.BY_CELL, L.F32, ctypes.byref(csr), P, 32, 0, 32, N, 32, 0, 32, L.OUT_CONCAT, P, 64,
                   N) == L.ERR_ARG
     # buckets: shapes over the limits (65536 destinations per frame, 2^24 points per frame), workspace size,
-    # missing bucket workspace; CSRs from buckets: null map, no ent_col for the pixel key, too few keys, small
+    # missing bucket workspace; CSRs from buckets: null map, too few keys, small
     # workspace; pull pair: null CSR, the bad-shape checks of shpl_pull, no key_range
     nb = ctypes.c_size_t()
     assert lib.shpl_bucket_workspace_bytes(4, 20000, 80000, 8800, 6750, ctypes.byref(nb)) == L.OK and nb.value > 0
@@ -105,9 +105,7 @@ def test_argument_validation_is_host_side():
     assert lib.shpl_build_index_buckets(*args, P, 1 << 24, N, ctypes.byref(bad), N) == L.ERR_ARG
     bk = L.ShplBuckets(4, 20000, 80000, 8800, 6750, 256, 256, 256, 256, 256, 256, nb.value)
     ccell = L.ShplCsr(256, 256, 256, None, 4 * 8800, 80000, 256)
-    cpix = L.ShplCsr(256, 256, 256, None, 4 * 6750, 80000, 256)  # no ent_col
     assert lib.shpl_build_csr_buckets(None, ctypes.byref(ccell), None, N) == L.ERR_ARG
-    assert lib.shpl_build_csr_buckets(ctypes.byref(bk), ctypes.byref(ccell), ctypes.byref(cpix), N) == L.ERR_ARG
     few = L.ShplCsr(256, 256, 256, None, 100, 80000, 256)  # fewer keys than frames x cells
     assert lib.shpl_build_csr_buckets(ctypes.byref(bk), ctypes.byref(few), None, N) == L.ERR_BAD_SHAPE
     small = L.ShplBuckets(4, 20000, 80000, 8800, 6750, 256, 256, 256, 256, 256, 256, 64)
