@@ -299,8 +299,7 @@ typedef struct {
        layout shpl_build_csr was given, so that it walks only the live entries -- frame f's
        [frame_off[f], frame_off[f] + min(frame_nnz[f], frame_off[f+1] - frame_off[f])) -- when
        most of the capacity is empty (raw scans: ~9 k voxel points in 120 k slots per frame).
-       At most SHPL_LIVE_MAX_FRAMES frames. n_frames alone (frame_off NULL) only names the batch's frame
-       count for shpl_pull_pair, which then places each frame's rows on XCDs of their own. */
+       At most SHPL_LIVE_MAX_FRAMES frames. */
     const int64_t *frame_off; /* [n_frames + 1] */
     const int64_t *frame_nnz; /* [n_frames]     */
     int64_t n_frames;

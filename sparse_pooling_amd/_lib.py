@@ -75,13 +75,6 @@ class Csr:
         self.struct.n_frames = int(frame_nnz.numel())
         return self
 
-    def pair_frames(self, n_frames):
-        """Name the frame count of a row-keyed CSR (shpl_csr.n_frames without a frame layout): shpl_pull_pair
-        then places each frame's rows on XCDs of their own (keys_per_frame = n_keys / n_frames)."""
-        if not self.struct.frame_off:  # a live-entry frame layout (live_frames) already names them
-            self.struct.n_frames = int(n_frames)
-        return self
-
     def ref(self):
         return ctypes.byref(self.struct)
 

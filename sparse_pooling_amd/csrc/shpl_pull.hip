@@ -499,7 +499,13 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse_long(const Feat f, const 
 #endif
 constexpr int ROWS_WALK = SHPL_ROWS_WALK;
 #ifndef SHPL_RPROBE
-#define SHPL_RPROBE 0  // timing probes of the row walk (wrong results): 1 every gather from the first 64 rows, 2 no stores
+// timing probes of the row walk: 1 every gather from the first 64 rows, 2 no stores (wrong results); 3 each
+// k_rows2 wave's start / end s_memrealtime stamps into g_probe (read by shpl_probe_stamps)
+#define SHPL_RPROBE 0
+#endif
+#if SHPL_RPROBE == 3
+constexpr int64_t PROBE_WAVES = 1 << 16;
+__device__ uint64_t g_probe[2 * PROBE_WAVES];
 #endif
 
 // The walk of one row's run [first, end) (all lanes of the wave, wave-uniform trip counts); pv / av: the
@@ -631,91 +637,30 @@ struct RowsSide {
     Ents e;
     const int32_t *key_range;
     int64_t n_rows, blocks;
-    int64_t kpf, bpf;  // keys and row blocks per frame (XCD schedules)
 };
-
-// Where the pair's blocks run. Workgroups are dealt round-robin over the 8 XCDs (block b shares an XCD,
-// and its 4 MB L2, with b + 8, b + 16, ...; MI355X_MICROARCH.md), so a schedule is a map from
-// (b % 8, b / 8) to a row block:
-//   ROUND_ROBIN  s1's blocks, then s0's, in block order: every XCD's L2 sees every frame's sources
-//   UNITS        a unit = (side, frame): the pixel-keyed rows of frame f gather BEV rows of f only, the
-//                cell-keyed rows image rows of f only. With U = 2 * n_frames units and U | 8, unit u runs on
-//                the q = 8 / U XCDs 8u/U .., its blocks interleaved over them; with 8 | U, XCD x runs units
-//                x, x + 8, ... (pixel-keyed ones first) -- each XCD's L2 sees one frame's sources of one side
-//   FRAMES       frame f's pixel-keyed then cell-keyed blocks on the 8 / n_frames XCDs of frame f (n_frames | 8),
-//                or XCD x runs frames x, x + 8, ... (8 | n_frames)
-enum { SCHED_ROUND_ROBIN = 0, SCHED_UNITS = 1, SCHED_FRAMES = 2 };
-struct Sched {
-    int mode, n_frames;
-    int q;  // XCDs per unit / frame (q >= 1), or 0: several units / frames per XCD
-};
-
-#ifndef SHPL_ROWS2_SCHED
-#define SHPL_ROWS2_SCHED 0
-#endif
-
-// The row block of workgroup b under a unit / frame schedule: side (0: s0, 1: s1), frame, block in the
-// frame's side; false when b has no work (its XCD's list is shorter than the grid's longest).
-__device__ __forceinline__ bool sched_locate(const Sched &sc, const RowsSide &s0, const RowsSide &s1, int64_t b,
-                                             int &side, int64_t &frame, int64_t &j) {
-    const int x = (int)(b & 7);
-    int64_t k = b >> 3;
-    const int64_t B = sc.n_frames;
-    if (sc.mode == SCHED_UNITS) {
-        if (sc.q > 0) {  // one unit per q XCDs
-            const int64_t u = x / sc.q, r = x % sc.q;
-            side = u < B ? 1 : 0;
-            frame = u < B ? u : u - B;
-            j = r + k * sc.q;
-            return j < (side ? s1.bpf : s0.bpf);
-        }
-        for (int64_t u = x; u < 2 * B; u += 8) {  // units x, x + 8, ... in order (pixel-keyed first)
-            side = u < B ? 1 : 0;
-            frame = u < B ? u : u - B;
-            const int64_t n = side ? s1.bpf : s0.bpf;
-            if (k < n) {
-                j = k;
-                return true;
-            }
-            k -= n;
-        }
-        return false;
-    }
-    const int64_t nf = s0.bpf + s1.bpf;  // SCHED_FRAMES: a frame's list is its pixel-keyed then cell-keyed blocks
-    int64_t jj;
-    if (sc.q > 0) {
-        frame = x / sc.q;
-        jj = x % sc.q + k * sc.q;
-    } else {
-        frame = x + 8 * (k / nf);
-        jj = k % nf;
-        if (frame >= B) return false;
-    }
-    if (jj >= nf) return false;
-    side = jj < s1.bpf ? 1 : 0;
-    j = side ? jj : jj - s1.bpf;
-    return true;
-}
 
 // The pixel-keyed pull's blocks come first: its longer runs (6.7 entries on average at config 3, up to 54 at
 // the horizon) then start early instead of forming the launch's tail (k_rows2 31.1 -> 24.0 us per pair,
 // profiles/r03_pixel_first_ab.log; reversing the order inside either side measured within noise).
 template <typename T, int VEC, int G, bool GR1>
-__global__ __launch_bounds__(SHPL_BLOCK) void k_rows2(const RowsSide s0, const RowsSide s1, const Sched sc) {
-    if (sc.mode == SCHED_ROUND_ROBIN) {
-        if ((int64_t)blockIdx.x < s1.blocks)
-            rows_body<T, VEC, GR1, G>(s1.f, s1.e, s1.key_range, 0, s1.n_rows, (int64_t)blockIdx.x);
-        else
-            rows_body<T, VEC, false, G>(s0.f, s0.e, s0.key_range, 0, s0.n_rows, (int64_t)blockIdx.x - s1.blocks);
-        return;
-    }
-    int side;
-    int64_t frame, j;
-    if (!sched_locate(sc, s0, s1, blockIdx.x, side, frame, j)) return;  // uniform
-    if (side)
-        rows_body<T, VEC, GR1, G>(s1.f, s1.e, s1.key_range, frame * s1.kpf, (frame + 1) * s1.kpf, j);
+__global__ __launch_bounds__(SHPL_BLOCK) void k_rows2(const RowsSide s0, const RowsSide s1) {
+#if SHPL_RPROBE == 3
+    uint64_t t0;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+#endif
+    if ((int64_t)blockIdx.x < s1.blocks)
+        rows_body<T, VEC, GR1, G>(s1.f, s1.e, s1.key_range, 0, s1.n_rows, (int64_t)blockIdx.x);
     else
-        rows_body<T, VEC, false, G>(s0.f, s0.e, s0.key_range, frame * s0.kpf, (frame + 1) * s0.kpf, j);
+        rows_body<T, VEC, false, G>(s0.f, s0.e, s0.key_range, 0, s0.n_rows, (int64_t)blockIdx.x - s1.blocks);
+#if SHPL_RPROBE == 3
+    uint64_t t1;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+    const int64_t w = (int64_t)blockIdx.x * (SHPL_BLOCK / SHPL_WAVE) + (threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0 && w < PROBE_WAVES) {
+        g_probe[2 * w] = t0;
+        g_probe[2 * w + 1] = t1;
+    }
+#endif
 }
 
 bool aligned(const void *ptr, int64_t a) { return ((uintptr_t)ptr) % (uintptr_t)a == 0; }
@@ -947,57 +892,20 @@ extern "C" int shpl_pull_sparse(SHPL_PULL_ARGS) {
 namespace shpl {
 namespace {
 
-// The XCD schedule of a pair over n_frames frames (0: unknown), its grid in *grid.
-Sched pair_sched(RowsSide s[2], int n_frames, int rpb, int64_t *grid) {
-    Sched sc{SCHED_ROUND_ROBIN, n_frames, 0};
-    *grid = s[0].blocks + s[1].blocks;
-    const int mode = SHPL_ROWS2_SCHED;
-    if (mode == SCHED_ROUND_ROBIN || n_frames < 1 || s[0].n_rows == 0 || s[1].n_rows == 0) return sc;
-    for (int k = 0; k < 2; ++k) {
-        if (s[k].n_rows % n_frames) return sc;
-        s[k].kpf = s[k].n_rows / n_frames;
-        s[k].bpf = (s[k].kpf + rpb - 1) / rpb;
-    }
-    const int64_t units = mode == SCHED_UNITS ? 2 * (int64_t)n_frames : n_frames;
-    int64_t per_xcd;  // row blocks of the busiest XCD
-    if (8 % units == 0) {
-        sc.q = (int)(8 / units);
-        const int64_t longest = mode == SCHED_UNITS ? (s[0].bpf > s[1].bpf ? s[0].bpf : s[1].bpf)
-                                                    : s[0].bpf + s[1].bpf;
-        per_xcd = (longest + sc.q - 1) / sc.q;
-    } else if (units % 8 == 0) {
-        sc.q = 0;
-        per_xcd = mode == SCHED_UNITS ? 0 : (units / 8) * (s[0].bpf + s[1].bpf);
-        if (mode == SCHED_UNITS)
-            for (int x = 0; x < 8; ++x) {
-                int64_t n = 0;
-                for (int64_t u = x; u < units; u += 8) n += u < n_frames ? s[1].bpf : s[0].bpf;
-                per_xcd = n > per_xcd ? n : per_xcd;
-            }
-    } else {
-        return sc;  // no even split over the XCDs: round robin
-    }
-    sc.mode = mode;
-    *grid = 8 * per_xcd;
-    return sc;
-}
-
 template <typename T, int VEC>
-int pair_t(RowsSide s[2], int G, int n_frames, hipStream_t st) {
+int pair_t(RowsSide s[2], int G, hipStream_t st) {
     const int rpb = SHPL_BLOCK / G;
     for (int k = 0; k < 2; ++k)
         if (s[k].n_rows > 0) s[k].blocks = (s[k].n_rows + rpb - 1) / rpb;
-    if (s[0].blocks + s[1].blocks == 0) return SHPL_OK;
-    int64_t blocks;
-    const Sched sc = pair_sched(s, n_frames, rpb, &blocks);
+    const int64_t blocks = s[0].blocks + s[1].blocks;
+    if (blocks == 0) return SHPL_OK;
     if (blocks > 0x7fffffffLL) return SHPL_ERR_BAD_SHAPE;
     const bool gr1 = s[1].e.col != nullptr;  // the pixel-keyed side's per-column partials (grouped())
 #define SHPL_ROWS2(GG)                                                                                              \
     if (gr1)                                                                                                        \
-        hipLaunchKernelGGL((k_rows2<T, VEC, GG, true>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, s[0], s[1], \
-                           sc);                                                                                     \
+        hipLaunchKernelGGL((k_rows2<T, VEC, GG, true>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, s[0], s[1]); \
     else                                                                                                            \
-        hipLaunchKernelGGL((k_rows2<T, VEC, GG, false>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, s[0], s[1], sc)
+        hipLaunchKernelGGL((k_rows2<T, VEC, GG, false>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, s[0], s[1])
     switch (G) {
         case 8: SHPL_ROWS2(8); break;
         case 16: SHPL_ROWS2(16); break;
@@ -1053,13 +961,19 @@ extern "C" int shpl_pull_pair(const shpl_csr *by_cell, const shpl_pull_desc *d_c
         v16 = pl[k].v16;
         while (G < 64 && (uint32_t)G < pl[k].f.cpool) G <<= 1;  // lanes per row: the widest pooled row
         s[k] = RowsSide{pl[k].f, Ents{c->nnz_cap, c->ent_dst, c->ent_src, c->ent_col, c->ent_val}, c->key_range,
-                        pl[k].n_dst, 0, 0, 0};
+                        pl[k].n_dst, 0};
     }
     if (dtype < 0) return SHPL_OK;
-    // the frames of the pair (XCD schedules): both CSRs must name the same count
-    int nf = 0;
-    if (on[0] && on[1] && cs[0]->n_frames > 0 && cs[0]->n_frames == cs[1]->n_frames && cs[0]->n_frames < 65536)
-        nf = (int)cs[0]->n_frames;
-    if (dtype == SHPL_F32) return v16 ? pair_t<float, 4>(s, G, nf, st) : pair_t<float, 1>(s, G, nf, st);
-    return v16 ? pair_t<uint16_t, 8>(s, G, nf, st) : pair_t<uint16_t, 1>(s, G, nf, st);
+    if (dtype == SHPL_F32) return v16 ? pair_t<float, 4>(s, G, st) : pair_t<float, 1>(s, G, st);
+    return v16 ? pair_t<uint16_t, 8>(s, G, st) : pair_t<uint16_t, 1>(s, G, st);
 }
+
+#if SHPL_RPROBE == 3
+// probe builds only: the last k_rows2 launch's per-wave (start, end) stamps, 100 MHz ticks
+extern "C" int shpl_probe_stamps(uint64_t *host, size_t n_waves) {
+    if (n_waves > (size_t)PROBE_WAVES) n_waves = PROBE_WAVES;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_probe), 16 * n_waves, 0, hipMemcpyDeviceToHost) == hipSuccess
+               ? SHPL_OK
+               : SHPL_ERR_HIP;
+}
+#endif

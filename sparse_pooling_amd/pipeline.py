@@ -85,9 +85,6 @@ class FusedPipeline:
                 if c is not None:
                     c.live_frames(self.frame_off, self.frame_nnz)
         self._lib = L.lib()
-        if self.rows and dual:  # the pull pairs' XCD schedule (shpl_pull_pair): frames of the batch
-            self.csr.pair_frames(self.B)
-            self.pcsr.pair_frames(self.B)
         if self.buckets:
             nb = L.bucket_ws_bytes(self.B, self.max_points, self.N, self.Hb * self.Wb, self.Hi * self.Wi)
             self.bkt_ws = L.workspace(nb, dev)
