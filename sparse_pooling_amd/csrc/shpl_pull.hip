@@ -510,7 +510,8 @@ __device__ uint64_t g_probe[2 * PROBE_WAVES];
 
 // The walk of one row's run [first, end) (all lanes of the wave, wave-uniform trip counts); pv / av: the
 // lane's first pass-through chunk (CONCAT, when p0) and first ADD operand, loaded by the caller.
-template <typename T, int VEC, bool GROUP, int G>
+// MODE: the output mode at compile time (SHPL_OUT_*), or -1: f.mode at run time.
+template <typename T, int VEC, bool GROUP, int G, int MODE = -1>
 __device__ __forceinline__ void row_walk(const Feat &f, const Ents &e, int64_t row, bool live, int32_t first,
                                          int32_t end, bool p0, typename Chunk<T, VEC>::raw_t pv,
                                          typename Chunk<T, VEC>::raw_t av) {
@@ -519,7 +520,8 @@ __device__ __forceinline__ void row_walk(const Feat &f, const Ents &e, int64_t r
     T *out = reinterpret_cast<T *>(f.out);
     const T *pass = reinterpret_cast<const T *>(f.pass) + f.pass_off;
     const T *src = reinterpret_cast<const T *>(f.src) + f.src_off;
-    const bool concat = f.mode == SHPL_OUT_CONCAT, add = f.mode == SHPL_OUT_ADD;
+    const int mode = MODE >= 0 ? MODE : f.mode;
+    const bool concat = mode == SHPL_OUT_CONCAT, add = mode == SHPL_OUT_ADD;
     const uint32_t oc0 = concat ? f.cpass : 0u;
     const int32_t len = end - first;
     int32_t wlen = len;  // longest run among the wave's rows: the walk's trip count
@@ -601,7 +603,7 @@ __device__ __forceinline__ void row_walk(const Feat &f, const Ents &e, int64_t r
 }
 
 // Rows [row0 + blk * rows per block, ...) of a pull, those below row_end live.
-template <typename T, int VEC, bool GROUP, int G>
+template <typename T, int VEC, bool GROUP, int G, int MODE = -1>
 __device__ __forceinline__ void rows_body(const Feat &f, const Ents &e, const int32_t *key_range, int64_t row0,
                                           int64_t row_end, int64_t blk) {
     typedef Chunk<T, VEC> C;
@@ -613,15 +615,16 @@ __device__ __forceinline__ void rows_body(const Feat &f, const Ents &e, const in
     // the row's range, its first pass-through chunk and its first ADD operand: one round trip
     int32_t first = 0, end = 0;
     typename C::raw_t pv = C::zero(), av = C::zero();
-    const bool p0 = live && f.mode == SHPL_OUT_CONCAT && (uint32_t)lg < f.cpass;
-    const bool a0 = live && f.mode == SHPL_OUT_ADD && (uint32_t)lg < f.cpool;
+    const int mode = MODE >= 0 ? MODE : f.mode;
+    const bool p0 = live && mode == SHPL_OUT_CONCAT && (uint32_t)lg < f.cpass;
+    const bool a0 = live && mode == SHPL_OUT_ADD && (uint32_t)lg < f.cpool;
     if (live) {
         first = key_range[2 * row];
         end = key_range[2 * row + 1];
     }
     if (p0) pv = C::load_nt(pass + (row * f.pass_stride + (int64_t)lg * VEC));
     if (a0) av = C::load(pass + (row * f.pass_stride + (int64_t)lg * VEC));
-    row_walk<T, VEC, GROUP, G>(f, e, row, live, first, end, p0, pv, av);
+    row_walk<T, VEC, GROUP, G, MODE>(f, e, row, live, first, end, p0, pv, av);
 }
 
 template <typename T, int VEC, bool GROUP, int G>
@@ -642,16 +645,23 @@ struct RowsSide {
 // The pixel-keyed pull's blocks come first: its longer runs (6.7 entries on average at config 3, up to 54 at
 // the horizon) then start early instead of forming the launch's tail (k_rows2 31.1 -> 24.0 us per pair,
 // profiles/r03_pixel_first_ab.log; reversing the order inside either side measured within noise).
-template <typename T, int VEC, int G, bool GR1>
-__global__ __launch_bounds__(SHPL_BLOCK) void k_rows2(const RowsSide s0, const RowsSide s1) {
+#ifndef SHPL_ROWS2_WPE
+#define SHPL_ROWS2_WPE 0
+#endif
+template <typename T, int VEC, int G, bool GR1, int MODE>
+__global__ __launch_bounds__(SHPL_BLOCK)
+#if SHPL_ROWS2_WPE
+__attribute__((amdgpu_waves_per_eu(SHPL_ROWS2_WPE, SHPL_ROWS2_WPE)))
+#endif
+void k_rows2(const RowsSide s0, const RowsSide s1) {
 #if SHPL_RPROBE == 3
     uint64_t t0;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
 #endif
     if ((int64_t)blockIdx.x < s1.blocks)
-        rows_body<T, VEC, GR1, G>(s1.f, s1.e, s1.key_range, 0, s1.n_rows, (int64_t)blockIdx.x);
+        rows_body<T, VEC, GR1, G, MODE>(s1.f, s1.e, s1.key_range, 0, s1.n_rows, (int64_t)blockIdx.x);
     else
-        rows_body<T, VEC, false, G>(s0.f, s0.e, s0.key_range, 0, s0.n_rows, (int64_t)blockIdx.x - s1.blocks);
+        rows_body<T, VEC, false, G, MODE>(s0.f, s0.e, s0.key_range, 0, s0.n_rows, (int64_t)blockIdx.x - s1.blocks);
 #if SHPL_RPROBE == 3
     uint64_t t1;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
@@ -901,11 +911,24 @@ int pair_t(RowsSide s[2], int G, hipStream_t st) {
     if (blocks == 0) return SHPL_OK;
     if (blocks > 0x7fffffffLL) return SHPL_ERR_BAD_SHAPE;
     const bool gr1 = s[1].e.col != nullptr;  // the pixel-keyed side's per-column partials (grouped())
-#define SHPL_ROWS2(GG)                                                                                              \
-    if (gr1)                                                                                                        \
-        hipLaunchKernelGGL((k_rows2<T, VEC, GG, true>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, s[0], s[1]); \
-    else                                                                                                            \
-        hipLaunchKernelGGL((k_rows2<T, VEC, GG, false>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, s[0], s[1])
+    // the output mode at compile time when both pulls share it (the forward pair's pooled halves, the gradient
+    // pair's add): the other modes' preloaded operands leave the registers (config 3: 78 -> VGPRs below)
+    int mode = -1;
+    if (s[0].n_rows == 0 || s[1].n_rows == 0 || s[0].f.mode == s[1].f.mode)
+        mode = s[0].n_rows ? s[0].f.mode : s[1].f.mode;
+    if (mode == SHPL_OUT_CONCAT) mode = -1;
+#define SHPL_ROWS2_M(GG, GR, M) \
+    hipLaunchKernelGGL((k_rows2<T, VEC, GG, GR, M>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, s[0], s[1])
+#define SHPL_ROWS2_G(GG, GR)                                                \
+    if (mode == SHPL_OUT_POOL) SHPL_ROWS2_M(GG, GR, SHPL_OUT_POOL);        \
+    else if (mode == SHPL_OUT_ADD) SHPL_ROWS2_M(GG, GR, SHPL_OUT_ADD);     \
+    else SHPL_ROWS2_M(GG, GR, -1);
+#define SHPL_ROWS2(GG)              \
+    if (gr1) {                      \
+        SHPL_ROWS2_G(GG, true)      \
+    } else {                        \
+        SHPL_ROWS2_G(GG, false)     \
+    }
     switch (G) {
         case 8: SHPL_ROWS2(8); break;
         case 16: SHPL_ROWS2(16); break;
@@ -913,6 +936,8 @@ int pair_t(RowsSide s[2], int G, hipStream_t st) {
         default: SHPL_ROWS2(64); break;
     }
 #undef SHPL_ROWS2
+#undef SHPL_ROWS2_G
+#undef SHPL_ROWS2_M
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
 }
