@@ -82,28 +82,36 @@ struct Bkt {
     int cp_blocks;    // rider workgroups per frame in each launch (0: none)
 };
 
-constexpr int CP_BATCH = 8;  // 16-byte pieces per thread in flight
+#ifndef SHPL_CP_BATCH
+#define SHPL_CP_BATCH 8
+#endif
+constexpr int CP_BATCH = SHPL_CP_BATCH;  // 16-byte pieces per thread in flight
 
+// 32-bit piece arithmetic (a frame's pieces < 2^31, checked on the host; a shift when a row holds a power of
+// two of pieces): the 64-bit divisions of an earlier form held the rider path at 111 / 122 VGPRs, and with it
+// the whole launch at one 1024-thread workgroup per CU.
 __device__ __forceinline__ void pass_copy(const PassCopy &c, int f, int b, int nb) {
     typedef uint32_t u32x4c __attribute__((ext_vector_type(4)));
-    const int64_t per_row = c.row_bytes >> 4, total = c.rows_per_frame * per_row;
-    const int64_t r0 = (int64_t)f * c.rows_per_frame;
-    const int64_t step = (int64_t)nb * IDX_BLOCK;
-    for (int64_t i0 = (int64_t)b * IDX_BLOCK + threadIdx.x; i0 < total; i0 += step * CP_BATCH) {
+    const uint32_t per_row = (uint32_t)(c.row_bytes >> 4), total = (uint32_t)c.rows_per_frame * per_row;
+    const int sh = per_row & (per_row - 1) ? -1 : __builtin_ctz(per_row);
+    const uint8_t *src = c.src + (int64_t)f * c.rows_per_frame * c.src_stride;
+    uint8_t *out = c.out + (int64_t)f * c.rows_per_frame * c.out_stride;
+    const uint32_t step = (uint32_t)nb * IDX_BLOCK;
+    for (uint32_t i0 = (uint32_t)b * IDX_BLOCK + threadIdx.x; i0 < total; i0 += step * CP_BATCH) {
         u32x4c v[CP_BATCH];
 #pragma unroll
         for (int u = 0; u < CP_BATCH; ++u) {
-            const int64_t i = i0 + u * step;
+            const uint32_t i = i0 + u * step;
             if (i >= total) continue;
-            const int64_t row = r0 + i / per_row, pc = i - (i / per_row) * per_row;
-            v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4c *>(c.src + row * c.src_stride) + pc);
+            const uint32_t row = sh >= 0 ? i >> sh : i / per_row, pc = i - row * per_row;
+            v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4c *>(src + (uint64_t)row * c.src_stride) + pc);
         }
 #pragma unroll
         for (int u = 0; u < CP_BATCH; ++u) {
-            const int64_t i = i0 + u * step;
+            const uint32_t i = i0 + u * step;
             if (i >= total) continue;
-            const int64_t row = r0 + i / per_row, pc = i - (i / per_row) * per_row;
-            __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4c *>(c.out + row * c.out_stride) + pc);
+            const uint32_t row = sh >= 0 ? i >> sh : i / per_row, pc = i - row * per_row;
+            __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4c *>(out + (uint64_t)row * c.out_stride) + pc);
         }
     }
 }

@@ -383,7 +383,8 @@ extern "C" int shpl_build_index_buckets(int n_frames, const int64_t *d_point_off
         const int64_t esz = c->dtype == SHPL_F32 ? 4 : 2;
         const int64_t rb = c->channels * esz;
         if (rb % 16 || (c->src_stride * esz) % 16 || (c->out_stride * esz) % 16 || ((uintptr_t)c->src & 15) ||
-            ((uintptr_t)c->out & 15) || c->src_stride < c->channels || c->out_stride < c->channels)
+            ((uintptr_t)c->out & 15) || c->src_stride < c->channels || c->out_stride < c->channels ||
+            (rb / 16) * (k ? g.n_pix : g.n_cells) >= ((int64_t)1 << 31))  // a frame's pieces in 32 bits
             return SHPL_ERR_BAD_SHAPE;
         bk.cp[k] = PassCopy{(const uint8_t *)c->src, (uint8_t *)c->out, c->src_stride * esz, c->out_stride * esz, rb,
                             k ? g.n_pix : g.n_cells};
