@@ -916,12 +916,12 @@ int pair_t(RowsSide s[2], int G, hipStream_t st) {
     int mode = -1;
     if (s[0].n_rows == 0 || s[1].n_rows == 0 || s[0].f.mode == s[1].f.mode)
         mode = s[0].n_rows ? s[0].f.mode : s[1].f.mode;
-    if (mode == SHPL_OUT_CONCAT) mode = -1;
 #define SHPL_ROWS2_M(GG, GR, M) \
     hipLaunchKernelGGL((k_rows2<T, VEC, GG, GR, M>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, s[0], s[1])
-#define SHPL_ROWS2_G(GG, GR)                                                \
-    if (mode == SHPL_OUT_POOL) SHPL_ROWS2_M(GG, GR, SHPL_OUT_POOL);        \
-    else if (mode == SHPL_OUT_ADD) SHPL_ROWS2_M(GG, GR, SHPL_OUT_ADD);     \
+#define SHPL_ROWS2_G(GG, GR)                                                  \
+    if (mode == SHPL_OUT_POOL) SHPL_ROWS2_M(GG, GR, SHPL_OUT_POOL);          \
+    else if (mode == SHPL_OUT_ADD) SHPL_ROWS2_M(GG, GR, SHPL_OUT_ADD);       \
+    else if (mode == SHPL_OUT_CONCAT) SHPL_ROWS2_M(GG, GR, SHPL_OUT_CONCAT); \
     else SHPL_ROWS2_M(GG, GR, -1);
 #define SHPL_ROWS2(GG)              \
     if (gr1) {                      \
