@@ -66,11 +66,28 @@ constexpr int REPI = NCO * 2 + 16;  // epilogue transpose pitch (bytes per pixel
 constexpr int RSTORES = SHPL_ROWS_RSTORES;  // output stores per row step, always issued (the vmcnt arithmetic)
 constexpr uint32_t OOB = 0x80000000u;  // an offset past every descriptor's num_records: reads zeros
 #ifndef SHPL_ROWS_PROBE
-#define SHPL_ROWS_PROBE 0  // timing probes of k_conv_rows (wrong results): 1 no epilogue, 2 no in-loop DMAs
+// timing probes of k_conv_rows: 1 no epilogue, 2 no in-loop DMAs (wrong results); 3 s_memtime stamps of each
+// row step's phases (ring wait, operand reads + MFMA issue, epilogue, staging) summed per wave into g_cprobe
+// (shpl_probe_conv_phases reads them; the stamps' lgkmcnt(0) waits cost a few % of the loop)
+#define SHPL_ROWS_PROBE 0
+#endif
+#if SHPL_ROWS_PROBE == 3
+constexpr int CPROBE_WAVES = 1 << 17;
+__device__ uint64_t g_cprobe[CPROBE_WAVES * 10];
+#define SHPL_RSTAMP(t) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory")
+#define SHPL_STAMP(t)                                                                  \
+    do {                                                                               \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");     \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+    } while (0)
 #endif
 constexpr int SPF = NCO + 4;      // ST: f32 transpose pitch (floats per pixel; 16-byte rows, conflict-free b64 reads)
 #ifndef SHPL_ROWS_EPI8
 #define SHPL_ROWS_EPI8 0  // the dropped 8-byte-store epilogue (wrong results; kept only for the ISA guard's record)
+#endif
+#ifndef SHPL_ROWS_WLATE
+#define SHPL_ROWS_WLATE 0  // 1: no wait for the weights before the loop (the round-3 form, A/B)
 #endif
 #ifndef SHPL_ROWS_WPE
 #define SHPL_ROWS_WPE 2  // waves per SIMD of the row kernels (tests/test_isa_guard.py forces 4: spills)
@@ -322,10 +339,17 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
                                      const uint64_t *s_occ, const int32_t *s_first, uint64_t b_rows,
                                      const uint32_t (&offa)[Layout<Q, QA>::NA],
                                      const int32_t (&offb)[Layout<Q, QA>::NB > 0 ? Layout<Q, QA>::NB : 1],
-                                     const uint32_t *s_offs, int lane) {
+                                     const uint32_t *s_offs, int lane, uint64_t (&ph)[5]) {
     typedef Layout<Q, QA, ST> L;
+#if SHPL_ROWS_PROBE == 3
+    uint64_t t0, t1, t2, t3, t4;
+    SHPL_STAMP(t0);
+#endif
     // rows j+1 .. j+RING-1 may still be in flight: per later step RSTORES stores and NDMA DMAs
     SHPL_RING_WAIT((L::NDMA + RSTORES) * (RING - 1));
+#if SHPL_ROWS_PROBE == 3
+    SHPL_STAMP(t1);
+#endif
     f32x16 &a0 = acc[(U + 1) % 3], &a1 = acc[U], &a2 = acc[(U + 2) % 3];
     // chunk-major (q outer): a split of the channels between A and B, and the skipped pooled chunks below,
     // leave every accumulator's summation order unchanged
@@ -354,6 +378,9 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
             }
         }
     }
+#if SHPL_ROWS_PROBE == 3
+    SHPL_STAMP(t2);
+#endif
     // epilogue of band output row b: acc * scale + (shift - center * scale), ReLU on the bf16 pairs;
     // the lane's 4 runs of 4 channels to rows of the slot just read, then 2 x 16-byte stores per lane
     // (consecutive lanes, consecutive pieces)
@@ -458,6 +485,9 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
     for (int i = 0; i < 16; ++i) a2[i] = 0.0f;
     // stage row j + RING into the slot (the transpose's reads of it are done first)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#if SHPL_ROWS_PROBE == 3
+    SHPL_STAMP(t3);
+#endif
     if (SHPL_ROWS_PROBE == 2) return;
     const int jn = j + RING, y = ya - 1 + jn;
     const bool live = jn < n_in;
@@ -477,12 +507,24 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
         ob[i] = offsets_in_lds<Q, QA, CMP, ST>() ? (int32_t)s_offs[(L::NA + i) * 64 + lane] : offb[i];
     stage<Q, QA, CMP>(r, frame_row0 + (int64_t)y * r.w + x0 - 1, live && y >= 0 && y < r.h, occ, first, oa, ob,
                       s_ring + U * L::SLOT, lane);
+#if SHPL_ROWS_PROBE == 3
+    SHPL_STAMP(t4);
+    ph[0] += t1 - t0;
+    ph[1] += t2 - t1;
+    ph[2] += t3 - t2;
+    ph[3] += t4 - t3;
+#endif
+    (void)ph;
 }
 
 template <int Q, int QA, bool CMP, bool RELU, bool ST>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS_WPE, SHPL_ROWS_WPE))) void k_conv_rows(
     const RowArgs r) {
     typedef Layout<Q, QA, ST> L;
+#if SHPL_ROWS_PROBE == 3
+    uint64_t rt0;
+    SHPL_RSTAMP(rt0);
+#endif
     __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING * L::SLOT];
     __shared__ __attribute__((aligned(16))) float s_par[2][NCO];
     // the halo rows' occupancy windows (entry j: input row ya - 1 + j): cells x0-1 .. x0+32 as bits 0..33, and
@@ -562,6 +604,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS_WP
 #pragma unroll
         for (int t = 0; t < 9; ++t)
             wr[q][t] = *reinterpret_cast<const bf16x8 *>(wq + ((q * 9 + t) * NCO + (lane & 31)) * 16 + (lane >> 5) * 8);
+#if !SHPL_ROWS_WLATE
+    // the weights have landed before the loop, as the compiler's wait model must know: its waitcnt pass
+    // does not see the ring's asm DMAs, so weights still "pending" at the loop header made it put a ladder of
+    // vmcnt waits down to vmcnt(0) among every row step's MFMAs -- draining the ring (the DMAs of the next two
+    // rows and the stores) every row. The builtin clears its scoreboard (the prologue's DMAs land too)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#endif
     f32x16 acc[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k)
@@ -569,17 +618,40 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS_WP
         for (int i = 0; i < 16; ++i) acc[k][i] = 0.0f;
     // B operand (pixels): lane (pl, hf) reads pixel pl (+ kx) of piece 2 q + hf
     const uint8_t *rd = s_ring + (lane >> 5) * HWD * 16 + (lane & 31) * 16;
+    uint64_t ph[5] = {0, 0, 0, 0, 0};
+#if SHPL_ROWS_PROBE == 3
+    uint64_t tk0, rt1;
+    SHPL_STAMP(tk0);
+    SHPL_RSTAMP(rt1);
+#endif
     for (int j = 0; j < n_in; j += RING) {
 #define SHPL_ROWS_STEP(UU)                                                                                          \
     if (j + UU >= n_in) break;                                                                                      \
     step<Q, QA, CMP, RELU, ST, UU>(r, wr, acc, s_par, rd, s_ring, frame_row0, x0, ya, n_in, n_out, obase, ostr, s_st, \
-                                   j + UU, s_occ, s_first, b_rows, offa, offb, s_offs, lane);
+                                   j + UU, s_occ, s_first, b_rows, offa, offb, s_offs, lane, ph);
         SHPL_ROWS_STEP(0)
         SHPL_ROWS_STEP(1)
         SHPL_ROWS_STEP(2)
 #undef SHPL_ROWS_STEP
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing DMAs land before the wave's LDS is released
+    asm volatile("s_waitcnt vmcnt(0) expcnt(5)" ::: "memory");  // the trailing DMAs land before the wave's LDS is released (expcnt(5): the ISA guard's exit marker)
+#if SHPL_ROWS_PROBE == 3
+    uint64_t tk1, rt2;
+    SHPL_STAMP(tk1);
+    SHPL_RSTAMP(rt2);
+    if (lane == 0 && blockIdx.x < CPROBE_WAVES) {
+        uint64_t *o = g_cprobe + 10 * (int64_t)blockIdx.x;
+        o[6] = rt0;
+        o[7] = rt1;
+        o[8] = rt2;
+        o[0] = ph[0];
+        o[1] = ph[1];
+        o[2] = ph[2];
+        o[3] = ph[3];
+        o[4] = tk1 - tk0;
+        o[5] = (uint64_t)n_in;
+    }
+#endif
     if constexpr (ST) {  // the band's sums over the 4 pixel quarters, then one double per (channel, statistic)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const f32x4 a = s_st[lane];
@@ -838,7 +910,7 @@ void k_wgrad_rows(const WgRowArgs r) {
             SHPL_WROWS_STEP(3)
 #undef SHPL_WROWS_STEP
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing DMAs land before the next item's prologue
+        asm volatile("s_waitcnt vmcnt(0) expcnt(5)" ::: "memory");  // the trailing DMAs land before the next item's prologue (exit marker)
         // PAIR: both waves are done with the item's slots before either stages the next item's rows into them
         if (PAIR) asm volatile("s_barrier" ::: "memory");
     }
@@ -1023,3 +1095,16 @@ int wgrad_launch(const WgRowArgs &r, float *dw, double *part2, hipStream_t s) {
 
 }  // namespace rows
 }  // namespace shpl
+
+#if SHPL_ROWS_PROBE == 3
+// probe builds only: the last k_conv_rows launch's per-wave phase sums (s_memtime cycles: ring wait, operand
+// reads + MFMA issue, epilogue, staging, whole loop; input rows; s_memrealtime at the wave's start, loop start
+// and loop end)
+extern "C" int shpl_probe_conv_phases(uint64_t *host, size_t n_waves) {
+    if (n_waves > (size_t)shpl::rows::CPROBE_WAVES) n_waves = shpl::rows::CPROBE_WAVES;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(shpl::rows::g_cprobe), 80 * n_waves, 0, hipMemcpyDeviceToHost) ==
+                   hipSuccess
+               ? SHPL_OK
+               : SHPL_ERR_HIP;
+}
+#endif

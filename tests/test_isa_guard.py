@@ -12,6 +12,10 @@ read a slot before its DMA landed. For every instantiation in the shipped
 library this test asserts:
   * no scratch: .private_segment_fixed_size 0, no VGPR spills, no scratch_*
     instruction;
+  * no other vmcnt wait on those paths: the compiler's waitcnt pass does not
+    see the ring's asm DMAs, so a load it still counts as pending (weights
+    loaded in the prologue without a builtin wait) makes it place vmcnt waits
+    down to vmcnt(0) among a step's MFMAs -- the ring drained every row;
   * every path from one marked wait to the next issues exactly K / 2 vector
     memory instructions (buffer_*, global_*, flat_*, scratch_*): uniform
     branches both ways; exec-mask branches as with active lanes (execz not
@@ -34,6 +38,7 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 KERNELS = re.compile(r"k_conv_rowsI|k_wgrad_rowsI")
 VMEM = re.compile(r"^(buffer_|global_|scratch_|flat_)")
 MARK = re.compile(r"^s_waitcnt vmcnt\((\d+)\) expcnt\(6\)$")
+EXIT = re.compile(r"^s_waitcnt vmcnt\(0\) expcnt\(5\)$")  # the loop's exit drain (expcnt(5): its marker)
 RING = 3
 
 pytestmark = pytest.mark.skipif(not os.path.exists(os.path.join(LLVM, "llvm-objdump")), reason="no ROCm LLVM tools")
@@ -133,7 +138,7 @@ def ring_violations(name, ins):
         return [i + 1]
 
     mark_set = set(marks)
-    counts = set()
+    counts, stray = set(), set()
     for w in marks:
         stack, seen = [(w + 1, 0)], set()
         while stack:
@@ -145,8 +150,10 @@ def ring_violations(name, ins):
             if i in mark_set:
                 counts.add(c)
                 continue
-            if re.match(r"s_waitcnt vmcnt\(0\)", t):  # the loop's exit drains the ring
+            if EXIT.match(t):  # the loop's exit drains the ring
                 continue
+            if t.startswith("s_waitcnt") and "vmcnt" in t:  # any other vmcnt wait drains (part of) the ring
+                stray.add(t)
             if VMEM.match(t):
                 c += 1
                 if c > 4 * per_step:
@@ -155,6 +162,8 @@ def ring_violations(name, ins):
             stack.extend((s, c) for s in succ(i))
     if counts != {per_step}:
         bad.append(f"vector-memory operations between ring waits {sorted(counts)}, expected {per_step} (K={k})")
+    if stray:
+        bad.append(f"compiler vmcnt waits between ring waits {sorted(stray)[:4]} (they drain the ring every step)")
     return bad
 
 
@@ -208,3 +217,19 @@ def test_guard_rejects_a_forced_spill(tmp_path):
     assert seen >= 40
     flagged = [k for k, v in report.items() if any("scratch" in p or "spill" in p or "private" in p for p in v)]
     assert flagged, "a forced spill went unnoticed"
+
+
+def test_guard_rejects_a_drained_ring(tmp_path):
+    """The round-3 form (the prologue's weight loads left pending in the compiler's model: -DSHPL_ROWS_WLATE=1)
+    has vmcnt waits among every row step's MFMAs; the checks must reject it."""
+    out = tmp_path / "rows_wlate.o"
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                    "--cuda-device-only", "-DSHPL_ROWS_WLATE=1", "-c",
+                    os.path.join(ROOT, "sparse_pooling_amd", "csrc", "shpl_conv_rows.hip"), "-o", str(out)],
+                   check=True, capture_output=True)
+    blob = out.read_bytes()
+    cos = gfx950_code_objects(blob) or [blob]
+    report, seen = check_code_objects(cos)
+    assert seen >= 40
+    flagged = [k for k, v in report.items() if any("compiler vmcnt waits" in p for p in v)]
+    assert any("k_conv_rows" in k for k in flagged), "a drained ring went unnoticed"
