@@ -835,9 +835,7 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
     # algorithmic HBM bytes of the step's passes: pooled map written once (+ gathers), conv forward
     # reads [bev || pooled] and writes the pre-activation map, BN apply reads / writes it, BN backward reads gy and
     # raw twice and writes g_raw, the input gradient reads g_raw and writes both sources' gradients, the pooled
-    # channels' gradient is gathered back to the image, the weight gradient reads [bev || pooled] and g_raw.
-    # bf16 with <= 32 channels: the BN backward's second pass runs inside the input gradient
-    # (shpl_batch_norm_backward_dgrad), which reads gy and raw and writes g_raw: one ci pass less
+    # channels' gradient is gathered back to the image, the weight gradient reads [bev || pooled] and g_raw
     nnz = int(pl.frame_nnz.sum().item())
     ents = pl.cell[pl.cell >= 0]
     u_cell = int(torch.unique(ents).numel())
@@ -845,9 +843,7 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
     Hi, Wi = spec.img_feat_hw
     px = F * Hb * Wb * esz
     if esz == 2:  # bf16: both convs gather the pooled rows (compact per-run buffer), bv_fused is never stored
-        bnb = 17 <= ci <= 32 and ci % 8 == 0
-        bn_bwd = (2 * ci + 2 * ci + ci + (cb + ci)) if bnb else (2 * ci + 3 * ci + ci + (cb + ci))
-        hbm_bytes = (px * (((cb + ci) + ci) + 2 * ci + bn_bwd + ((cb + ci) + ci))
+        hbm_bytes = (px * ((cb + ci) + 2 * ci + 2 * ci + 3 * ci + (ci + cb + ci) + (cb + ci))
                      + F * Hi * Wi * ci * esz + (2 * u_pix + u_cell) * ci * esz + 3 * 12 * nnz)
     else:  # f32: the pooled map written once in the forward, read by the forward and the weight gradient
         hbm_bytes = (px * (ci + (cb + ci + ci) + 2 * ci + 2 * ci + 3 * ci + (ci + cb + ci) + (cb + ci + ci))

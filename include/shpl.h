@@ -578,29 +578,6 @@ int shpl_conv3x3_dgrad(int dtype, int n_frames, int64_t h, int64_t w, const void
                        int64_t c_split, void *d_dx_b, int64_t dx_b_stride, void *d_ws, size_t ws_bytes,
                        void *stream);
 
-/* BatchNorm (+ ReLU) backward and the input gradient of the conv that fed it,
- * in one call: the results of
- *   shpl_batch_norm_backward(dtype, n_frames*h*w, NULL, d_raw, d_gy, stride, c, ...,
- *                            d_graw, d_dbeta, d_dgamma, ...)   (the ReLU mask from raw and beta)
- *   shpl_conv3x3_dgrad(dtype, n_frames, h, w, d_graw, stride, c, d_weights, c_dx, d_dx, ...)
- * bit for bit. bf16 with 17 .. 32 channels, 16-byte rows and whole 32-channel
- * output blocks: the BatchNorm backward runs inside the input gradient's
- * staging (each staged row of gy and raw turned into g_raw in LDS), so g_raw
- * is written once (d_graw: the weight gradient's input) and never re-read by
- * this call -- one streaming pass over gy / raw / g_raw less than the two calls;
- * otherwise the two calls run. Workspace:
- * shpl_batch_norm_backward_dgrad_workspace_bytes. Replaces the TF autodiff of
- * slim.batch_norm + slim.conv2d (avod/avod/core/models/rpn_model.py:338-354). */
-int shpl_batch_norm_backward_dgrad_workspace_bytes(int dtype, int n_frames, int64_t h, int64_t w, int64_t c,
-                                                   int64_t c_dx, size_t *bytes);
-int shpl_batch_norm_backward_dgrad(int dtype, int n_frames, int64_t h, int64_t w, const void *d_raw,
-                                   const void *d_gy, int64_t stride, int64_t c, const float *d_mean,
-                                   const float *d_scale, const float *d_gamma, const float *d_beta, int act,
-                                   int training, void *d_graw, float *d_dbeta, float *d_dgamma,
-                                   const void *d_weights, int64_t c_dx, void *d_dx, int64_t dx_stride,
-                                   int64_t c_split, void *d_dx_b, int64_t dx_b_stride, void *d_ws, size_t ws_bytes,
-                                   void *stream);
-
 /* Weight gradient: dw[ky][kx][ci][co] = sum over pixels of x[p + (ky-1, kx-1)][ci]
  * * gy[p][co], x given exactly as shpl_conv3x3's input (A channels, then B
  * channels, dense or pooled from the CSR -- recomputed, never stored). f32

@@ -1841,24 +1841,30 @@ extern "C" int shpl_batch_norm_backward_workspace_bytes(int64_t rows, int64_t c,
     return SHPL_OK;
 }
 
-namespace {
-// The BatchNorm backward's launches: per-block partial sums, the per-channel totals and mean terms, then (apply)
-// g_raw. Arguments checked by the callers.
-int bn_bwd_launch(int dtype, int64_t rows, const void *d_y, const void *d_raw, const void *d_gy, int64_t stride,
-                  int64_t c, const float *d_mean, const float *d_scale, const float *d_gamma, const float *d_beta,
-                  int act, int training, void *d_graw, float *d_dbeta, float *d_dgamma, void *d_ws, bool apply,
-                  float **terms, hipStream_t s) {
+extern "C" int shpl_batch_norm_backward(int dtype, int64_t rows, const void *d_y, const void *d_raw,
+                                        const void *d_gy, int64_t stride, int64_t c, const float *d_mean,
+                                        const float *d_scale, const float *d_gamma, const float *d_beta, int act,
+                                        int training, void *d_graw, float *d_dbeta, float *d_dgamma, void *d_ws,
+                                        size_t ws_bytes, void *stream) {
+    if (dtype != SHPL_F32 && dtype != SHPL_BF16) return SHPL_ERR_ARG;
+    if (rows < 0 || c < 1 || stride < c || c > (1 << 16)) return SHPL_ERR_BAD_SHAPE;
+    if (act != 0 && act != 1) return SHPL_ERR_ARG;
+    size_t need;
+    shpl_batch_norm_backward_workspace_bytes(rows, c, &need);
+    if (!d_ws || ws_bytes < need) return SHPL_ERR_WORKSPACE;
+    if (rows > 0 && (!d_gy || !d_graw || (act == 1 && !d_y && !d_raw) || (training && !d_raw))) return SHPL_ERR_ARG;
+    if (rows == 0) return SHPL_OK;
+    hipStream_t s = (hipStream_t)stream;
     const int nb = bn_bwd_blocks(rows);
     const int64_t rpb = (rows + nb - 1) / nb;
     double *part = reinterpret_cast<double *>(d_ws);
     float *mt = reinterpret_cast<float *>((uint8_t *)d_ws + align_up((size_t)nb * 2 * c * sizeof(double), 256));
-    if (terms) *terms = mt;
     // x-hat needs raw only in training (dgamma); otherwise any row-shaped input stands in
     const void *rw = d_raw ? d_raw : d_gy;
     const int vec = dtype == SHPL_F32 ? 4 : 8;
     const int cg = (int)(c / vec);
     const bool vform = c % vec == 0 && stride % vec == 0 && cg <= SHPL_BLOCK && (cg & (cg - 1)) == 0 &&
-                       aligned16(d_gy) && aligned16(rw) && (!apply || aligned16(d_graw)) && (!d_y || aligned16(d_y));
+                       aligned16(d_gy) && aligned16(rw) && aligned16(d_graw) && (!d_y || aligned16(d_y));
     // y NULL: the ReLU mask from raw (bn_pre_act), so only the y argument of the kernels changes
     const float *beta = act == 1 && !d_y ? d_beta : nullptr;
     const int grid = grid_for(rows * c / (vform ? vec : 1), SHPL_BLOCK * bn_rows_per_thread(16 / vec), 1 << 22);
@@ -1873,7 +1879,6 @@ int bn_bwd_launch(int dtype, int64_t rows, const void *d_y, const void *d_raw, c
                                d_mean, d_scale, d_gamma, beta, act, rpb, part);
         hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((unsigned)c), dim3(SHPL_BLOCK), 0, s, part, nb,
                            (int)c, (double)rows, d_dbeta, d_raw ? d_dgamma : nullptr, mt);
-        if (!apply) return;
         if (vform)
             hipLaunchKernelGGL(k_bn_bwd_apply_vec<T>, dim3(grid), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride,
                                (int)c, d_mean, d_scale, d_gamma, beta, act, training, mt, (T *)d_graw);
@@ -1887,24 +1892,6 @@ int bn_bwd_launch(int dtype, int64_t rows, const void *d_y, const void *d_raw, c
         launch(uint16_t());
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
-}
-}  // namespace
-
-extern "C" int shpl_batch_norm_backward(int dtype, int64_t rows, const void *d_y, const void *d_raw,
-                                        const void *d_gy, int64_t stride, int64_t c, const float *d_mean,
-                                        const float *d_scale, const float *d_gamma, const float *d_beta, int act,
-                                        int training, void *d_graw, float *d_dbeta, float *d_dgamma, void *d_ws,
-                                        size_t ws_bytes, void *stream) {
-    if (dtype != SHPL_F32 && dtype != SHPL_BF16) return SHPL_ERR_ARG;
-    if (rows < 0 || c < 1 || stride < c || c > (1 << 16)) return SHPL_ERR_BAD_SHAPE;
-    if (act != 0 && act != 1) return SHPL_ERR_ARG;
-    size_t need;
-    shpl_batch_norm_backward_workspace_bytes(rows, c, &need);
-    if (!d_ws || ws_bytes < need) return SHPL_ERR_WORKSPACE;
-    if (rows > 0 && (!d_gy || !d_graw || (act == 1 && !d_y && !d_raw) || (training && !d_raw))) return SHPL_ERR_ARG;
-    if (rows == 0) return SHPL_OK;
-    return bn_bwd_launch(dtype, rows, d_y, d_raw, d_gy, stride, c, d_mean, d_scale, d_gamma, d_beta, act, training,
-                         d_graw, d_dbeta, d_dgamma, d_ws, true, nullptr, (hipStream_t)stream);
 }
 
 extern "C" int shpl_conv3x3_dgrad(int dtype, int n_frames, int64_t h, int64_t w, const void *d_gy, int64_t gy_stride,
@@ -1949,95 +1936,6 @@ extern "C" int shpl_conv3x3_dgrad(int dtype, int n_frames, int64_t h, int64_t w,
     hipStream_t s = (hipStream_t)stream;
     if (dtype == SHPL_F32) return conv_launch<float>(pl, a, false, false, d_weights, nullptr, nullptr, s, 1);
     return conv_launch<uint16_t>(pl, a, false, false, d_weights, nullptr, nullptr, s, 1);
-}
-
-extern "C" int shpl_batch_norm_backward_dgrad_workspace_bytes(int dtype, int n_frames, int64_t h, int64_t w,
-                                                              int64_t c, int64_t c_dx, size_t *bytes) {
-    if (!bytes || n_frames < 0 || h < 0 || w < 0) return SHPL_ERR_ARG;
-    size_t bn;
-    int rc = shpl_batch_norm_backward_workspace_bytes((int64_t)n_frames * h * w, c, &bn);
-    if (rc) return rc;
-    ConvPlan pl;
-    rc = conv_plan(dtype, n_frames, h, w, c, 0, c_dx, false, false, &pl);
-    if (rc) return rc;
-    *bytes = align_up(bn, 256) + pl.total;
-    return SHPL_OK;
-}
-
-extern "C" int shpl_batch_norm_backward_dgrad(int dtype, int n_frames, int64_t h, int64_t w, const void *d_raw,
-                                              const void *d_gy, int64_t stride, int64_t c, const float *d_mean,
-                                              const float *d_scale, const float *d_gamma, const float *d_beta,
-                                              int act, int training, void *d_graw, float *d_dbeta, float *d_dgamma,
-                                              const void *d_weights, int64_t c_dx, void *d_dx, int64_t dx_stride,
-                                              int64_t c_split, void *d_dx_b, int64_t dx_b_stride, void *d_ws,
-                                              size_t ws_bytes, void *stream) {
-    size_t need;
-    int rc = shpl_batch_norm_backward_dgrad_workspace_bytes(dtype, n_frames, h, w, c, c_dx, &need);
-    if (rc) return rc;
-    if (!d_ws || ws_bytes < need) return SHPL_ERR_WORKSPACE;
-    const int64_t rows = (int64_t)n_frames * h * w;
-    size_t bn_bytes;
-    shpl_batch_norm_backward_workspace_bytes(rows, c, &bn_bytes);
-    bn_bytes = align_up(bn_bytes, 256);
-    uint8_t *ws = reinterpret_cast<uint8_t *>(d_ws);
-    ConvPlan pl;
-    conv_plan(dtype, n_frames, h, w, c, 0, c_dx, false, false, &pl);
-    if (!d_dx_b) c_split = c_dx;
-    const bool fused = dtype == SHPL_BF16 && pl.rows && pl.qb == 0 && rows::bnb_supported(pl.qa) && n_frames > 0 &&
-                       c_dx % NCO == 0 && (!d_dx_b || c_split % NCO == 0) && d_raw && d_gy && d_graw && d_weights &&
-                       (act == 0 || act == 1) && stride >= c && stride % 8 == 0 && aligned16(d_raw) &&
-                       aligned16(d_gy) && aligned16(d_graw) && (!d_dx || (aligned16(d_dx) && dx_stride % 8 == 0)) &&
-                       (!d_dx_b || (aligned16(d_dx_b) && dx_b_stride % 8 == 0)) && c_split >= 0 && c_split <= c_dx &&
-                       dx_stride >= c_split && (!d_dx_b || dx_b_stride >= c_dx - c_split) && (c_split == 0 || d_dx);
-    hipStream_t s = (hipStream_t)stream;
-    if (!fused) {  // the two calls (same results: the fused form applies the same arithmetic to each staged row)
-        rc = shpl_batch_norm_backward(dtype, rows, nullptr, d_raw, d_gy, stride, c, d_mean, d_scale, d_gamma, d_beta,
-                                      act, training, d_graw, d_dbeta, d_dgamma, ws, bn_bytes, stream);
-        if (rc) return rc;
-        return shpl_conv3x3_dgrad(dtype, n_frames, h, w, d_graw, stride, c, d_weights, c_dx, d_dx, dx_stride,
-                                  d_dx_b ? c_split : c_dx, d_dx_b, dx_b_stride, ws + bn_bytes, ws_bytes - bn_bytes,
-                                  stream);
-    }
-    float *terms = nullptr;
-    rc = bn_bwd_launch(dtype, rows, nullptr, d_raw, d_gy, stride, c, d_mean, d_scale, d_gamma, d_beta, act, training,
-                       d_graw, d_dbeta, d_dgamma, ws, false, &terms, s);
-    if (rc) return rc;
-    // the transposed packed weights, then k_conv_pair with the BatchNorm backward in its staging
-    uint16_t *wp = reinterpret_cast<uint16_t *>(ws + bn_bytes);
-    const int64_t wtot = (int64_t)pl.n_cob * pl.qa * W_ROWS * Elem<uint16_t>::CK;
-    hipLaunchKernelGGL(k_pack_w<uint16_t>, dim3(grid_for(wtot, SHPL_BLOCK, 4096)), dim3(SHPL_BLOCK), 0, s,
-                       reinterpret_cast<const uint16_t *>(d_weights), (int)c, pl.qa, 0, 0, (int)c_dx, pl.n_cob, 1, wp);
-    SHPL_LAUNCH_CHECK();
-    rows::RowArgs r = {};
-    r.a = reinterpret_cast<const uint16_t *>(d_gy);
-    r.b = reinterpret_cast<const uint16_t *>(d_raw);
-    r.a_stride = r.b_stride = stride;
-    r.c_a = r.c_b = (int)c;
-    r.h = (int)h;
-    r.w = (int)w;
-    r.strips = pl.tiles_x;
-    r.band = pl.band;
-    r.n_bands = pl.n_bands;
-    r.n_items = n_frames * pl.n_bands * pl.tiles_x;
-    r.wp = wp;
-    r.out = reinterpret_cast<uint16_t *>(d_dx);
-    r.out_stride = dx_stride;
-    r.out2 = reinterpret_cast<uint16_t *>(d_dx_b);
-    r.out2_stride = dx_b_stride;
-    r.c_split = (int)c_split;
-    r.n_cob = pl.n_cob;
-    r.junk = reinterpret_cast<uint16_t *>(ws + bn_bytes + pl.wp_bytes + pl.rp_bytes + pl.part_bytes + pl.occ_bytes +
-                                          pl.cmp_bytes);
-    r.bn_mean = d_mean;
-    r.bn_scale = d_scale;
-    r.bn_gamma = d_gamma;
-    r.bn_beta = act == 1 ? d_beta : nullptr;
-    r.bn_terms = terms;
-    r.bn_act = act;
-    r.bn_training = training;
-    r.graw = reinterpret_cast<uint16_t *>(d_graw);
-    r.graw_stride = stride;
-    return rows::launch_bnb(r, pl.qa, s);
 }
 
 namespace {

@@ -29,12 +29,6 @@ struct RowArgs {
     int c_split;                 // a multiple of 32 when out2 is set
     int n_cob;                   // output blocks (the fastest index of a workgroup's item)
     double *part;                // ST: per-item channel sums [(co * 2 + stat) * n_items + item]
-    // BatchNorm backward folded into the input gradient (launch_bnb): a = gy, b = raw (b_stride), c_a = c_b = c;
-    // the coefficients of k_bn_bwd_apply_vec (NULL: 0 / 1 / none), the mean terms [2][c] of k_bn_bwd_finalize
-    const float *bn_mean, *bn_scale, *bn_gamma, *bn_beta, *bn_terms;
-    int bn_act, bn_training;
-    uint16_t *graw;              // g_raw out (the weight gradient's input): rows of graw_stride elements
-    int64_t graw_stride;
 };
 
 // k_conv_rows has an instantiation for q chunks of which qa come from A
@@ -52,12 +46,6 @@ int prep_pooled(int n_frames, int h, int w, int wpr, const int32_t *ent_dst, con
 // The conv: n_items * n_cob one-wave workgroups (ST: also the per-item
 // channel sums of the pre-activation output, for k_stats_reduce).
 int launch(const RowArgs &r, int q, int qa, bool cmp, bool relu, bool st, hipStream_t s);
-
-// The input gradient of a conv whose output went through BatchNorm (+ ReLU) in training: k_conv_pair staging gy
-// and raw, the BatchNorm backward applied to each staged row (g_raw also written to r.graw), then the conv
-// (k_pack_w'd transposed weights in r.wp). q = 2: 17 .. 32 channels.
-bool bnb_supported(int q);
-int launch_bnb(const RowArgs &r, int q, hipStream_t s);
 
 // The bf16 weight gradient (k_wgrad_rows): dense sources, input tiles of 32
 // channels within one source, outputs in tiles of 32.

@@ -777,88 +777,26 @@ __device__ __forceinline__ void pair_stage(const RowArgs &r, int64_t pix0, bool 
     }
 }
 
-// BNB: the BatchNorm backward of staged row j in place -- gy pieces (A) and raw pieces (B) in, g_raw over the gy
-// pieces out, with k_bn_bwd_apply_vec's arithmetic bit for bit (shpl_conv.hip; the ReLU mask recomputed from raw,
-// as there with y NULL). Wave w takes pixels 17w .. 17w+16 of the 34, lane (q, cp) channels 2cp, 2cp+1 of pixels
-// 17w + q + 4k (k < 5; the fifth only for q = 0): one dword of gy and of raw each, its 2 channels' coefficients
-// in registers (bc: mean, scale, scale / gamma, beta, and the two mean terms). Pixels outside the map, channels
-// past c and rows outside the frame give 0 (SAME padding of the conv's input). The band's own rows and the strip's
-// own pixels of g_raw also go to HBM (output block 0 only) for the weight gradient: 5 stores per step, always
-// issued (the counted ring wait), junk when not wanted.
-constexpr int BNB_STORES = 5;
-__device__ __forceinline__ void bnb_row(const RowArgs &r, uint8_t *slot, const float (&bc)[6][2], bool rok,
-                                        bool wrow, int64_t gpix0, int x0, int w, int lane) {
-    constexpr int PA = 2 * 2 * HWD;  // Q = 2: the gy pieces, then the raw pieces
-    const int cp = lane & 15, g = cp >> 2;
-    const bool ch_ok = 2 * cp < r.c_a;
-#pragma unroll
-    for (int k = 0; k < BNB_STORES; ++k) {
-        const int pl = (lane >> 4) + 4 * k;
-        const bool live = pl < 17;
-        const int p = 17 * w + (live ? pl : 16);
-        uint8_t *a = slot + (g * HWD + p) * 16 + (cp & 3) * 4;
-        const int x = x0 - 1 + p;
-        const bool ok = rok && ch_ok && x >= 0 && x < r.w;
-        uint32_t gv, xv;
-        __builtin_memcpy(&gv, a, 4);
-        __builtin_memcpy(&xv, a + PA * 16, 4);
-        uint32_t o = 0;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const float xf = bf16_to_f32((uint16_t)(xv >> (16 * i))), gf = bf16_to_f32((uint16_t)(gv >> (16 * i)));
-            const float m = bc[0][i], sc = bc[1][i];
-            const float t = __fmul_rn(__fsub_rn(xf, m), sc);
-            const float yv = r.bn_beta ? __fadd_rn(t, bc[3][i]) : t;
-            const float gb = (r.bn_act == 1 && !(yv > 0.0f)) ? 0.0f : gf;
-            float v;
-            if (r.bn_training) {
-                const float xh = __fmul_rn(__fsub_rn(xf, m), bc[2][i]);
-                v = __fmul_rn(sc, __fsub_rn(__fsub_rn(gb, bc[4][i]), __fmul_rn(xh, bc[5][i])));
-            } else {
-                v = __fmul_rn(sc, gb);
-            }
-            o |= (uint32_t)f32_to_bf16(v) << (16 * i);
-        }
-        o = ok ? o : 0u;
-        if (live) __builtin_memcpy(a, &o, 4);
-        const bool st = live && wrow && ok && p >= 1 && p <= TW;
-        uint16_t *dst = st ? r.graw + (gpix0 + p - 1) * r.graw_stride + 2 * cp : r.junk + (w * 64 + lane) * 2;
-        __builtin_memcpy(dst, &o, 4);
-    }
-}
-
-// The DMA layout of a row: BNB stages gy (A) and raw (B), Q chunks each.
-template <int Q, int QA, bool BNB>
-using PDma = PLayout<BNB ? 2 * Q : Q, BNB ? Q : QA>;
-
-// One staged input row j (U = j % 3: the accumulators' roles) of the band: ring wait, barrier (BNB: the row's
-// BatchNorm backward and a second barrier), Q / 2 chunks x 2 pixel halves x 3 kx operand reads and 3 ky MFMAs
-// each, the epilogue of output row j - 2 (always stored; rows and pixels outside the map go to the junk line),
-// then the wave's DMAs of row j + 3.
-template <int Q, int QA, bool CMP, bool RELU, bool ST, bool BNB, int U>
+// One staged input row j (U = j % 3: the accumulators' roles) of the band: ring wait, barrier, NC chunks x 2
+// pixel halves x 3 kx operand reads and 3 ky MFMAs each, the epilogue of output row j - 2 (always stored; rows
+// and pixels outside the map go to the junk line), then the wave's DMAs of row j + 3.
+template <int Q, int QA, bool CMP, bool RELU, bool ST, int U>
 __device__ __forceinline__ void pair_step(const RowArgs &r, const bf16x8 (&wr)[Q / 2][9], f32x4 (&acc)[2][3],
                                           const uint8_t *rdb, uint8_t *s_ring, const float (&sc)[4], const float (&sh)[4],
                                           float (&st_s)[4], float (&st_q)[4], int64_t frame_row0, int x0, int ya,
                                           int n_in, int n_out, uint16_t *obase, int64_t ostr, int j,
                                           const uint64_t *s_occ, const int32_t *s_first, uint64_t b_rows,
-                                          const int32_t (&off)[PDma<Q, QA, BNB>::ND], const float (&bc)[6][2],
-                                          bool wblk, int w, int lane) {
-    typedef PDma<Q, QA, BNB> L;
-    // rows j+1, j+2 may still be in flight: per later step 2 stores (BNB: and the g_raw stores) and ND DMAs
-    SHPL_RING_WAIT((L::ND + 2 + (BNB ? BNB_STORES : 0)) * 2);
+                                          const int32_t (&off)[PLayout<Q, QA>::ND], int w, int lane) {
+    typedef PLayout<Q, QA> L;
+    // rows j+1, j+2 may still be in flight: per later step 2 stores and ND DMAs
+    SHPL_RING_WAIT((L::ND + 2) * 2);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if constexpr (BNB) {
-        const int y = ya - 1 + j;
-        bnb_row(r, s_ring + (j & 3) * L::SLOT, bc, y >= 0 && y < r.h, wblk && j >= 1 && j <= n_out,
-                frame_row0 + (int64_t)y * r.w + x0, x0, w, lane);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the whole row transformed
-    }
     const uint8_t *rd = rdb + (j & 3) * L::SLOT;
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {
         f32x4 &a0 = acc[nb][(U + 1) % 3], &a1 = acc[nb][U], &a2 = acc[nb][(U + 2) % 3];
 #pragma unroll
-        for (int c = 0; c < Q / 2; ++c) {
+        for (int c = 0; c < L::NC; ++c) {
             // pooled rows without an occupied cell in the window are all zeros: a chunk of B pieces only adds
             // exact zeros to accumulators that are never -0 (k_conv_rows)
             if (CMP && 4 * c >= 2 * QA && !((b_rows >> j) & 1)) continue;
@@ -920,14 +858,13 @@ __device__ __forceinline__ void pair_step(const RowArgs &r, const bf16x8 (&wr)[Q
     uint8_t *slot = s_ring + (jn & 3) * L::SLOT;
     const int64_t pix0 = frame_row0 + (int64_t)y * r.w + x0 - 1;
     const bool yok = live && y >= 0 && y < r.h;
-    pair_stage<BNB ? 2 * Q : Q, BNB ? Q : QA, CMP>(r, pix0, yok, occ, first, off, slot, w, lane);
+    pair_stage<Q, QA, CMP>(r, pix0, yok, occ, first, off, slot, w, lane);
 }
 
-template <int Q, int QA, bool CMP, bool RELU, bool ST, bool BNB = false>
+template <int Q, int QA, bool CMP, bool RELU, bool ST>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SHPL_PAIR_WPE, SHPL_PAIR_WPE))) void k_conv_pair(
     const RowArgs r) {
-    typedef PDma<Q, QA, BNB> L;
-    constexpr int DQ = BNB ? 2 * Q : Q, DQA = BNB ? Q : QA;
+    typedef PLayout<Q, QA> L;
     __shared__ __attribute__((aligned(16))) uint8_t s_ring[PRING * L::SLOT];
     __shared__ uint64_t s_occ[CMP ? 64 : 1];
     __shared__ int32_t s_first[CMP ? 64 : 1];
@@ -974,23 +911,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SHPL_PAIR_W
         b_rows = __ballot(s_occ[lane] != 0);  // input rows with an occupied cell in their window
     }
     int32_t off[L::ND];
-    pair_offsets<DQ, DQA, CMP>(r, x0, w, lane, off);
-    // BNB: the lane's two channels' BatchNorm-backward coefficients (k_bn_bwd_apply_vec's)
-    float bc[6][2] = {};
-    if constexpr (BNB) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int ch = 2 * (lane & 15) + i;
-            if (ch < r.c_a) {
-                bc[0][i] = r.bn_mean ? r.bn_mean[ch] : 0.0f;
-                bc[1][i] = r.bn_scale ? r.bn_scale[ch] : 1.0f;
-                bc[2][i] = __fdiv_rn(bc[1][i], r.bn_gamma ? r.bn_gamma[ch] : 1.0f);
-                bc[3][i] = r.bn_beta ? r.bn_beta[ch] : 0.0f;
-                bc[4][i] = r.bn_training ? r.bn_terms[ch] : 0.0f;
-                bc[5][i] = r.bn_training ? r.bn_terms[r.c_a + ch] : 0.0f;
-            }
-        }
-    }
+    pair_offsets<Q, QA, CMP>(r, x0, w, lane, off);
     // prologue: input rows 0 .. 2 in flight
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
@@ -999,7 +920,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SHPL_PAIR_W
         const bool yok = j < n_in && y >= 0 && y < H;
         const uint64_t occ = CMP ? s_occ[j] : 0;
         const int32_t first = CMP ? s_first[j] : 0;
-        pair_stage<DQ, DQA, CMP>(r, pix0, yok, occ, first, off, s_ring + j * L::SLOT, w, lane);
+        pair_stage<Q, QA, CMP>(r, pix0, yok, occ, first, off, s_ring + j * L::SLOT, w, lane);
     }
     // the wave's weights, A operands of K-chunk c (16 output x 32 input channels): lane (co = lane & 15,
     // k = 8 (lane >> 4) ..) reads 16-channel chunk 2c + (lane >> 5), half (lane >> 4) & 1, of output channel
@@ -1024,9 +945,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SHPL_PAIR_W
     for (int j = 0; j < n_in; j += 3) {
 #define SHPL_PAIR_STEP(UU)                                                                                           \
     if (j + UU >= n_in) break;                                                                                       \
-    pair_step<Q, QA, CMP, RELU, ST, BNB, UU>(r, wr, acc, rdb, s_ring, sc, sh, st_s, st_q, frame_row0, x0, ya, n_in,  \
-                                             n_out, obase, ostr, j + UU, s_occ, s_first, b_rows, off, bc, cob == 0, w, \
-                                             lane);
+    pair_step<Q, QA, CMP, RELU, ST, UU>(r, wr, acc, rdb, s_ring, sc, sh, st_s, st_q, frame_row0, x0, ya, n_in, n_out, \
+                                        obase, ostr, j + UU, s_occ, s_first, b_rows, off, w, lane);
         SHPL_PAIR_STEP(0)
         SHPL_PAIR_STEP(1)
         SHPL_PAIR_STEP(2)
@@ -1452,21 +1372,6 @@ int launch(const RowArgs &r, int q, int qa, bool cmp, bool relu, bool st, hipStr
     return SHPL_OK;
 }
 
-#ifndef SHPL_BNB
-#define SHPL_BNB 1  // 0: shpl_batch_norm_backward_dgrad runs its two calls (A/B)
-#endif
-bool bnb_supported(int q) { return SHPL_CONV_PAIR && SHPL_BNB && q == 2; }
-
-int launch_bnb(const RowArgs &r, int q, hipStream_t s) {
-    if (!bnb_supported(q) || r.n_cob < 1 || !r.graw || r.c_b != r.c_a || r.c_a > 32 || (r.bn_training && !r.bn_terms))
-        return SHPL_ERR_ARG;
-    if ((int64_t)r.n_items * r.n_cob >= (1LL << 31)) return SHPL_ERR_BAD_SHAPE;
-    if (r.out2 && r.c_split % NCO != 0) return SHPL_ERR_ARG;
-    hipLaunchKernelGGL((k_conv_pair<2, 2, false, false, false, true>), dim3((unsigned)(r.n_items * r.n_cob)), dim3(128),
-                       0, s, r);
-    SHPL_LAUNCH_CHECK();
-    return SHPL_OK;
-}
 
 bool wgrad_supported(int c_a, int c_b, int c_out) {
     if (c_a < 0 || c_b < 0 || c_a + c_b < 1 || c_out < 1) return false;

@@ -146,37 +146,6 @@ def conv3x3_dgrad(gy, weights, c_dx, split=None):
     return dx if split is None else (dx, dx_b)
 
 
-def batch_norm_backward_dgrad(gy, raw, weights, c_dx, split=None, mean=None, scale=None, gamma=None, beta=None,
-                              relu=True, training=True):
-    """batch_norm_backward(gy, raw=raw, ...) (the ReLU mask from raw and beta)
-    followed by conv3x3_dgrad(g_raw, weights, c_dx, split) in one call
-    (shpl_batch_norm_backward_dgrad: bf16 <= 32 channels folds the BatchNorm
-    backward into the input gradient's staging). Returns (g_raw, dbeta,
-    dgamma, dx) with dx as conv3x3_dgrad's (a pair when split is set)."""
-    gy = gy.contiguous()
-    raw = raw.contiguous()
-    B, H, W, C = (int(s) for s in gy.shape)
-    weights = weights.to(gy.dtype).contiguous()
-    c_dx = int(c_dx)
-    c0 = c_dx if split is None else int(split)
-    g_raw = torch.empty_like(gy)
-    dbeta = torch.empty(C, dtype=torch.float32, device=gy.device)
-    dgamma = torch.empty(C, dtype=torch.float32, device=gy.device)
-    dx = torch.empty((B, H, W, c0), dtype=gy.dtype, device=gy.device)
-    dx_b = None if split is None else torch.empty((B, H, W, c_dx - c0), dtype=gy.dtype, device=gy.device)
-    nb = ctypes.c_size_t()
-    dt = L.dtype_code(gy)
-    L.check(L.lib().shpl_batch_norm_backward_dgrad_workspace_bytes(dt, B, H, W, C, c_dx, ctypes.byref(nb)),
-            "shpl_batch_norm_backward_dgrad_workspace_bytes")
-    ws = L.workspace(nb.value, gy.device)
-    L.check(L.lib().shpl_batch_norm_backward_dgrad(
-        dt, B, H, W, L.ptr(raw), L.ptr(gy), C, C, L.ptr(mean), L.ptr(scale), L.ptr(gamma), L.ptr(beta),
-        L.ACT_RELU if relu else L.ACT_NONE, int(bool(training)), L.ptr(g_raw), L.ptr(dbeta), L.ptr(dgamma),
-        L.ptr(weights), c_dx, L.ptr(dx), max(c0, 1), c0, L.ptr(dx_b), max(c_dx - c0, 1), L.ptr(ws), ws.numel(),
-        L.stream_of(gy.device)), "shpl_batch_norm_backward_dgrad")
-    return g_raw, dbeta, dgamma, (dx if split is None else (dx, dx_b))
-
-
 def conv3x3_wgrad(a, gy, b=None, pool=None, frame_off=None):
     """Weight gradient (f32 HWIO [3,3,Ca+Cb,Cout]) of the SAME 3x3 conv of
     [a || b] (b dense, or the image map pooled through ``pool``)."""
@@ -257,25 +226,19 @@ class _FusionConvFn(torch.autograd.Function):
         conv, smap, pooled = ctx.conv, ctx.smap, ctx.pooled
         Ca, Cb = ctx.shapes
         gy = gy.contiguous().to(a.dtype)
-        need_x = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
-        dx_pair = None
-        if ctx.train_bn and need_x and raw is not None:
-            # BatchNorm backward folded into the input gradient (one pass over g_raw less)
-            g_raw, dbeta, _, dx_pair = batch_norm_backward_dgrad(
-                gy, raw, weights, Ca + Cb, split=None if b is None else Ca, mean=mean, scale=scale, beta=beta,
-                relu=conv.relu, training=True)
-        elif conv.batch_norm or conv.bias is not None or conv.relu:
+        if conv.batch_norm or conv.bias is not None or conv.relu:
             g_raw, dbeta, _ = batch_norm_backward(
                 gy, y=y, raw=raw, mean=mean if (conv.batch_norm or ctx.train_bn) else None,
                 scale=scale if conv.batch_norm else None, relu=conv.relu, training=ctx.train_bn, beta=beta)
         else:
             g_raw, dbeta = gy, None
+        need_x = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         d_a = d_b = dw = None
         if need_x:
             if b is None:
-                d_a = dx_pair if dx_pair is not None else conv3x3_dgrad(g_raw, weights, Ca)
+                d_a = conv3x3_dgrad(g_raw, weights, Ca)
             else:  # the epilogue writes the two sources' gradients as separate dense maps
-                d_a, dx_b = dx_pair if dx_pair is not None else conv3x3_dgrad(g_raw, weights, Ca + Cb, split=Ca)
+                d_a, dx_b = conv3x3_dgrad(g_raw, weights, Ca + Cb, split=Ca)
                 if ctx.needs_input_grad[1]:
                     if pooled:  # the pooled channels' gradient back to the image (a8's TF gradient)
                         d_b = torch.empty(b.shape, dtype=dx_b.dtype, device=dx_b.device)

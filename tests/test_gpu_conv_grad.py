@@ -253,45 +253,6 @@ def test_batch_norm_backward(training, C):
         assert torch.equal(u, v)
 
 
-BNB_SHAPES = [  # B, H, W, C, c_dx, split, training, relu, beta
-    (2, 16, 64, 32, 64, 32, True, True, True),      # the training workload's form: two maps
-    (1, 61, 70, 32, 64, 32, True, True, False),     # one band of 61 rows, a partial strip, no beta
-    (3, 130, 40, 32, 64, None, True, False, True),  # three bands, no ReLU, one map
-    (2, 9, 35, 24, 32, None, False, True, True),    # a channel tail (24 of 32), inference form
-    (1, 1, 5, 32, 32, None, True, True, True),      # one row: every halo row outside the map
-]
-
-
-@pytest.mark.parametrize("shape", BNB_SHAPES, ids=[str(s) for s in BNB_SHAPES])
-def test_batch_norm_backward_dgrad_bf16(shape):
-    """shpl_batch_norm_backward_dgrad (the BatchNorm backward applied to each
-    row the input gradient stages, g_raw written once) == shpl_batch_norm_backward
-    followed by shpl_conv3x3_dgrad, bitwise: g_raw, dbeta, dgamma and the input
-    gradient (both maps). The two-call form is checked against the oracle above."""
-    from sparse_pooling_amd import fusion_conv as fc
-    B, H, W, C, cdx, split, training, relu, with_beta = shape
-    rng = np.random.default_rng(91)
-    bf = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(torch.bfloat16).to(DEV)  # noqa
-    raw = bf(rng.standard_normal((B, H, W, C)) * 2.0 + 0.3)
-    gy = bf(rng.standard_normal((B, H, W, C)))
-    w = bf(_weights(cdx, C, 92))
-    mean = _t(rng.standard_normal(C).astype(np.float32) * 0.2)
-    scale = _t(rng.uniform(0.5, 2.0, C).astype(np.float32))
-    beta = _t(rng.standard_normal(C).astype(np.float32) * 0.3) if with_beta else None
-    g1, db1, dg1 = fc.batch_norm_backward(gy, raw=raw, mean=mean, scale=scale, relu=relu, training=training,
-                                          beta=beta)
-    dx1 = fc.conv3x3_dgrad(g1, w, cdx, split=split)
-    g2, db2, dg2, dx2 = fc.batch_norm_backward_dgrad(gy, raw, w, cdx, split=split, mean=mean, scale=scale, beta=beta,
-                                                     relu=relu, training=training)
-    torch.cuda.synchronize()
-    assert torch.equal(g2, g1), "g_raw"
-    assert torch.equal(db2, db1) and torch.equal(dg2, dg1), "dbeta / dgamma"
-    if split is None:
-        assert torch.equal(dx2, dx1), "dx"
-    else:
-        assert torch.equal(dx2[0], dx1[0]) and torch.equal(dx2[1], dx1[1]), "dx pair"
-
-
 @pytest.mark.parametrize("train", [True, False])
 def test_fused_conv_autograd_vs_oracle(train):
     """d(bev), d(img), d(weights), d(beta) of FusionConv.fused (pooling inside
