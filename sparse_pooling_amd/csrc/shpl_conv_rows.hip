@@ -672,306 +672,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS_WP
 }
 
 
-// ---- k_conv_pair: two waves per workgroup, 16 output channels each (v_mfma_f32_16x16x32_bf16) ----
-//
-// k_conv_rows keeps the weights of all 32 output channels in one wave (144 VGPRs at 64 input channels), which
-// holds it at two waves per SIMD, and its per-row chain is longer than the other wave's MFMAs: per row step
-// 1,420 cycles of operand reads and MFMA issue against 930 of epilogue (through an LDS transpose) and 680 of
-// staging (SHPL_ROWS_PROBE=3, profiles/r04_conv_phases.log). Here a workgroup of two waves walks the band and
-// strip together; wave w owns output channels 16w .. 16w+15 of the block (M = 16 of the 16x16x32 MFMA, N = 16
-// pixels twice per strip, K = 32 input channels), so its weights take half the registers (72 at Q = 4) and three
-// waves fit per SIMD. Both waves read every staged row from one ring of PRING slots; each issues half of the
-// row's DMAs (PLayout), and the pair meets once per row at an s_barrier behind each wave's counted ring wait: past
-// it the whole row has landed, and both waves' reads of the previous row are done (lgkmcnt(0) before the
-// barrier), so row j + 3 goes into row j - 1's slot. The epilogue needs no transpose -- a lane holds 4 adjacent
-// output channels of one pixel: one 8-byte store per 16 pixels, scale and shift in registers -- and statistics
-// (ST) are per-lane sums over the band, reduced over the 16 lanes of a channel group at the band's end.
-//
-// Pieces (8 channels x 34 pixels) lie contiguous in a slot, A's then B's, so K-chunk c's lane group g reads piece
-// 4c + g wherever it came from: the summation order depends on the chunk grid only, and a split of the channels
-// between A and B (or pooled B) is bitwise the one-source conv, as in k_conv_rows. Bitwise different from
-// k_conv_rows (K = 32 per MFMA), tolerance-equal.
-constexpr int PRING = 4;  // ring slots of a workgroup: rows j+1, j+2 in flight, j read, j-1 free past the barrier
-#ifndef SHPL_CONV_PAIR
-#define SHPL_CONV_PAIR 1  // 0: every conv on k_conv_rows (A/B)
-#endif
-#ifndef SHPL_PAIR_WPE
-#define SHPL_PAIR_WPE 3
-#endif
-
-template <int Q, int QA>
-struct PLayout {
-    static_assert(Q % 2 == 0, "K-chunks of 32 channels");
-    static constexpr int QB = Q - QA;
-    static constexpr int PA = 2 * QA * HWD, PB = 2 * QB * HWD;  // pieces of a row per source
-    static constexpr int NA0 = (PA + 63) / 64, NB = (PB + 63) / 64;
-    static constexpr int SPLIT = (NA0 + NB) % 2;  // A's first DMA as two of 32 lanes: an even count
-    static constexpr int NA = NA0 + SPLIT;
-    static constexpr int ND = (NA + NB) / 2;      // DMAs per wave and row
-    static constexpr int SLOT = (PA + PB) * 16;
-    static constexpr int NC = Q / 2;              // K-chunks
-    // DMA i of a row: its source (0 A, 1 B), first piece in the slot, pieces (lanes)
-    static constexpr int src(int i) { return i < NA ? 0 : 1; }
-    static constexpr int p0(int i) {
-        return i < NA ? (SPLIT ? (i == 0 ? 0 : i == 1 ? 32 : 64 * (i - 1)) : 64 * i) : PA + 64 * (i - NA);
-    }
-    static constexpr int n(int i) {
-        return i < NA ? (SPLIT && i < 2 ? 32 : (PA - p0(i) < 64 ? PA - p0(i) : 64))
-                      : (PB - 64 * (i - NA) < 64 ? PB - 64 * (i - NA) : 64);
-    }
-};
-
-// Wave w's DMA d of a row: its index in PLayout's list (wave-uniform; no branch on w, so that every path between
-// two ring waits issues the same DMAs, as tests/test_isa_guard.py checks)
-template <int Q, int QA>
-__device__ __forceinline__ void pair_dma(int w, int d, int &src, int &p0, int &n) {
-    typedef PLayout<Q, QA> L;
-    const int i0 = d, i1 = L::ND + d;
-    src = L::src(i0) == L::src(i1) ? L::src(i0) : (w ? L::src(i1) : L::src(i0));
-    p0 = w ? L::p0(i1) : L::p0(i0);
-    n = L::n(i0) == L::n(i1) ? L::n(i0) : (w ? L::n(i1) : L::n(i0));
-}
-
-// Per band: the lane's byte offset into the row (dense) or pixel << 16 | channel (CMP B; -1 outside) of each
-// of wave w's DMAs.
-template <int Q, int QA, bool CMP>
-__device__ __forceinline__ void pair_offsets(const RowArgs &r, int x0, int w, int lane,
-                                             int32_t (&off)[PLayout<Q, QA>::ND]) {
-    typedef PLayout<Q, QA> L;
-#pragma unroll
-    for (int d = 0; d < L::ND; ++d) {
-        int src, p0, n;
-        pair_dma<Q, QA>(w, d, src, p0, n);
-        const int piece = p0 + lane - (src ? L::PA : 0);  // piece of its source
-        const int g = piece / HWD, px = piece - g * HWD, x = x0 - 1 + px;
-        const int ch = (g >> 1) * 16 + (g & 1) * 8;
-        const bool ok = lane < n && x >= 0 && x < r.w && ch < (src ? r.c_b : r.c_a);
-        if (CMP && src)
-            off[d] = ok ? (px << 16) | ch : -1;
-        else
-            off[d] = ok ? (int32_t)((px * (int)(src ? r.b_stride : r.a_stride) + ch) * 2) : (int32_t)OOB;
-    }
-}
-
-// Wave w's share of input row y's DMAs (its pixel 0 at global pixel pix0) into a slot: ND, always issued.
-template <int Q, int QA, bool CMP>
-__device__ __forceinline__ void pair_stage(const RowArgs &r, int64_t pix0, bool yok, uint64_t occ, int32_t first,
-                                           const int32_t (&off)[PLayout<Q, QA>::ND], uint8_t *slot, int w, int lane) {
-    typedef PLayout<Q, QA> L;
-    const uint32_t nrec = yok ? OOB : 0u;
-    const i32x4 ra = rsrc(r.a + pix0 * r.a_stride, nrec);
-    i32x4 rb = ra;
-    if constexpr (L::QB > 0) rb = CMP ? rsrc(r.cmp, nrec) : rsrc(r.b + pix0 * r.b_stride, nrec);
-#pragma unroll
-    for (int d = 0; d < L::ND; ++d) {
-        int src, p0, n;
-        pair_dma<Q, QA>(w, d, src, p0, n);
-        uint32_t o = (uint32_t)off[d];
-        if (CMP && src) {
-            const int px = (off[d] >> 16) & 63;
-            const bool hit = off[d] >= 0 && ((occ >> px) & 1);
-            const int rank = first + (int)__popcll(occ & ((1ull << px) - 1));
-            o = hit ? (uint32_t)((rank * r.c_b + (off[d] & 0xffff)) * 2) : OOB;
-        }
-        if (lane < n) dma16(src ? rb : ra, o, slot + p0 * 16);
-    }
-}
-
-// One staged input row j (U = j % 3: the accumulators' roles) of the band: ring wait, barrier, NC chunks x 2
-// pixel halves x 3 kx operand reads and 3 ky MFMAs each, the epilogue of output row j - 2 (always stored; rows
-// and pixels outside the map go to the junk line), then the wave's DMAs of row j + 3.
-template <int Q, int QA, bool CMP, bool RELU, bool ST, int U>
-__device__ __forceinline__ void pair_step(const RowArgs &r, const bf16x8 (&wr)[Q / 2][9], f32x4 (&acc)[2][3],
-                                          const uint8_t *rdb, uint8_t *s_ring, const float (&sc)[4], const float (&sh)[4],
-                                          float (&st_s)[4], float (&st_q)[4], int64_t frame_row0, int x0, int ya,
-                                          int n_in, int n_out, uint16_t *obase, int64_t ostr, int j,
-                                          const uint64_t *s_occ, const int32_t *s_first, uint64_t b_rows,
-                                          const int32_t (&off)[PLayout<Q, QA>::ND], int w, int lane) {
-    typedef PLayout<Q, QA> L;
-    // rows j+1, j+2 may still be in flight: per later step 2 stores and ND DMAs
-    SHPL_RING_WAIT((L::ND + 2) * 2);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    const uint8_t *rd = rdb + (j & 3) * L::SLOT;
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-        f32x4 &a0 = acc[nb][(U + 1) % 3], &a1 = acc[nb][U], &a2 = acc[nb][(U + 2) % 3];
-#pragma unroll
-        for (int c = 0; c < L::NC; ++c) {
-            // pooled rows without an occupied cell in the window are all zeros: a chunk of B pieces only adds
-            // exact zeros to accumulators that are never -0 (k_conv_rows)
-            if (CMP && 4 * c >= 2 * QA && !((b_rows >> j) & 1)) continue;
-#pragma unroll
-            for (int kx = 0; kx < 3; ++kx) {
-                const bf16x8 xv = *reinterpret_cast<const bf16x8 *>(rd + (4 * c * HWD + 16 * nb + kx) * 16);
-                a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[c][kx], xv, a0, 0, 0, 0);
-                a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[c][3 + kx], xv, a1, 0, 0, 0);
-                a2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[c][6 + kx], xv, a2, 0, 0, 0);
-            }
-        }
-    }
-    // epilogue of band output row b: fma(acc, scale, shift - center * scale), bf16, ReLU as max on the bf16 bits
-    const int b = j - 2;
-    const bool row_ok = b >= 0 && b < n_out;
-    uint16_t *orow = obase + (frame_row0 + (int64_t)(ya + b) * r.w + x0) * ostr;
-    const int cg = lane >> 4, px16 = lane & 15;
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-        f32x4 &a2 = acc[nb][(U + 2) % 3];
-        const int px = 16 * nb + px16;
-        const bool ok = row_ok && x0 + px < r.w;
-        uint32_t pk[2];
-#pragma unroll
-        for (int k = 0; k < 4; k += 2) {
-            const float v0 = __builtin_fmaf(a2[k], sc[k], sh[k]);
-            const float v1 = __builtin_fmaf(a2[k + 1], sc[k + 1], sh[k + 1]);
-            uint32_t v = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
-            if (RELU) {
-                s16x2 h;
-                __builtin_memcpy(&h, &v, 4);
-                h = __builtin_elementwise_max(h, s16x2{0, 0});
-                __builtin_memcpy(&v, &h, 4);
-            }
-            pk[k >> 1] = v;
-        }
-        uint16_t *dst = ok ? orow + px * ostr + 16 * w + 4 * cg : r.junk + ((w * 2 + nb) * 64 + lane) * 4;
-        __builtin_memcpy(dst, pk, sizeof(pk));
-        if constexpr (ST) {  // batch statistics of the pre-activation output (the f32 accumulator)
-            if (ok) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    st_s[i] = __fadd_rn(st_s[i], a2[i]);
-                    st_q[i] = __fadd_rn(st_q[i], __fmul_rn(a2[i], a2[i]));
-                }
-            }
-        }
-        a2 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    }
-    // the wave's DMAs of row j + 3 into row j - 1's slot
-    const int jn = j + 3, y = ya - 1 + jn;
-    const bool live = jn < n_in;
-    uint64_t occ = 0;
-    int32_t first = 0;
-    if (CMP && live) {
-        occ = s_occ[jn];
-        first = s_first[jn];
-    }
-    uint8_t *slot = s_ring + (jn & 3) * L::SLOT;
-    const int64_t pix0 = frame_row0 + (int64_t)y * r.w + x0 - 1;
-    const bool yok = live && y >= 0 && y < r.h;
-    pair_stage<Q, QA, CMP>(r, pix0, yok, occ, first, off, slot, w, lane);
-}
-
-template <int Q, int QA, bool CMP, bool RELU, bool ST>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SHPL_PAIR_WPE, SHPL_PAIR_WPE))) void k_conv_pair(
-    const RowArgs r) {
-    typedef PLayout<Q, QA> L;
-    __shared__ __attribute__((aligned(16))) uint8_t s_ring[PRING * L::SLOT];
-    __shared__ uint64_t s_occ[CMP ? 64 : 1];
-    __shared__ int32_t s_first[CMP ? 64 : 1];
-    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wi = (int)xcd_block(blockIdx.x, r.n_items * r.n_cob);
-    const int cob = wi % r.n_cob, item = wi / r.n_cob;
-    const int strip = item % r.strips, fb = item / r.strips;
-    const int band = fb % r.n_bands, f = fb / r.n_bands;
-    const bool second = r.out2 && cob * NCO >= r.c_split;
-    uint16_t *const obase = second ? r.out2 + (cob * NCO - r.c_split) : r.out + cob * NCO;
-    const int64_t ostr = second ? r.out2_stride : r.out_stride;
-    const int H = r.h;
-    const int x0 = strip * TW, ya = band * r.band;
-    const int n_out = min(r.band, H - ya), n_in = n_out + 2;
-    const int64_t frame_row0 = (int64_t)f * H * r.w;
-    const int cg = lane >> 4, px16 = lane & 15;
-    // the lane's 4 output channels: scale (1 when absent) and shift - center * scale
-    float sc[4], sh[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int c = cob * NCO + 16 * w + 4 * cg + i;
-        const float s = r.scale ? r.scale[c] : 1.0f, ce = r.center ? r.center[c] : 0.0f;
-        sc[i] = s;
-        sh[i] = __fsub_rn(r.shift ? r.shift[c] : 0.0f, __fmul_rn(ce, s));
-    }
-    uint64_t b_rows = ~0ull;
-    if constexpr (CMP) {  // wave 0 lists the halo rows' occupancy windows (as k_conv_rows); the pair shares them
-        if (w == 0) {
-            const int y = ya - 1 + lane, w0 = x0 >> 5;
-            uint64_t occ_row = 0;
-            int32_t first_row = 0;
-            if (lane < n_in && y >= 0 && y < H) {
-                const int64_t wrow = ((int64_t)f * H + y) * r.wpr;
-                const uint32_t ml = w0 > 0 ? r.occ[wrow + w0 - 1] : 0u, mc = r.occ[wrow + w0];
-                const uint32_t mr = w0 + 1 < r.wpr ? r.occ[wrow + w0 + 1] : 0u;
-                const int32_t bs = r.occ_base[wrow + (w0 > 0 ? w0 - 1 : w0)];
-                occ_row = (uint64_t)(ml >> 31) | ((uint64_t)mc << 1) | ((uint64_t)(mr & 1u) << 33);
-                first_row = (int32_t)r.frame_off[f] + bs + (w0 > 0 ? __popc(ml & 0x7fffffffu) : 0);
-            }
-            s_occ[lane] = occ_row;
-            s_first[lane] = first_row;
-        }
-        __syncthreads();
-        b_rows = __ballot(s_occ[lane] != 0);  // input rows with an occupied cell in their window
-    }
-    int32_t off[L::ND];
-    pair_offsets<Q, QA, CMP>(r, x0, w, lane, off);
-    // prologue: input rows 0 .. 2 in flight
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const int y = ya - 1 + j;
-        const int64_t pix0 = frame_row0 + (int64_t)y * r.w + x0 - 1;
-        const bool yok = j < n_in && y >= 0 && y < H;
-        const uint64_t occ = CMP ? s_occ[j] : 0;
-        const int32_t first = CMP ? s_first[j] : 0;
-        pair_stage<Q, QA, CMP>(r, pix0, yok, occ, first, off, s_ring + j * L::SLOT, w, lane);
-    }
-    // the wave's weights, A operands of K-chunk c (16 output x 32 input channels): lane (co = lane & 15,
-    // k = 8 (lane >> 4) ..) reads 16-channel chunk 2c + (lane >> 5), half (lane >> 4) & 1, of output channel
-    // 16 w + co from the packed [chunk][tap][32 co][16 ci] layout
-    bf16x8 wr[Q / 2][9];
-    const uint16_t *wq = r.wp + (int64_t)cob * Q * W_ROWS * 16;
-#pragma unroll
-    for (int c = 0; c < Q / 2; ++c)
-#pragma unroll
-        for (int t = 0; t < 9; ++t)
-            wr[c][t] = *reinterpret_cast<const bf16x8 *>(
-                wq + (((2 * c + (lane >> 5)) * 9 + t) * NCO + 16 * w + px16) * 16 + ((lane >> 4) & 1) * 8);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the weights have landed before the loop (k_conv_rows)
-    f32x4 acc[2][3];
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) acc[nb][k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    float st_s[4] = {0.0f, 0.0f, 0.0f, 0.0f}, st_q[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    // B operand: lane (pixel px16, group cg) reads piece 4c + cg at pixel px16 + 16 nb + kx (immediates)
-    const uint8_t *rdb = s_ring + (cg * HWD + px16) * 16;
-    for (int j = 0; j < n_in; j += 3) {
-#define SHPL_PAIR_STEP(UU)                                                                                           \
-    if (j + UU >= n_in) break;                                                                                       \
-    pair_step<Q, QA, CMP, RELU, ST, UU>(r, wr, acc, rdb, s_ring, sc, sh, st_s, st_q, frame_row0, x0, ya, n_in, n_out, \
-                                        obase, ostr, j + UU, s_occ, s_first, b_rows, off, w, lane);
-        SHPL_PAIR_STEP(0)
-        SHPL_PAIR_STEP(1)
-        SHPL_PAIR_STEP(2)
-#undef SHPL_PAIR_STEP
-    }
-    asm volatile("s_waitcnt vmcnt(0) expcnt(5)" ::: "memory");  // trailing DMAs land before the LDS is released
-    if constexpr (ST) {  // the band's sums over the 16 pixels of each channel group; one double per (channel, stat)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) {
-                st_s[i] = __fadd_rn(st_s[i], __shfl_xor(st_s[i], o, 64));
-                st_q[i] = __fadd_rn(st_q[i], __shfl_xor(st_q[i], o, 64));
-            }
-        if (px16 == 0) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int c = cob * NCO + 16 * w + 4 * cg + i;
-                r.part[((int64_t)c * 2 + 0) * r.n_items + item] = (double)st_s[i];
-                r.part[((int64_t)c * 2 + 1) * r.n_items + item] = (double)st_q[i];
-            }
-        }
-    }
-}
-
 // ---- The bf16 weight gradient, row-streaming (k_wgrad_rows) ----
 //
 // dW[ky][kx][ci][co] = sum over pixels of X[y+ky-1][x+kx-1][ci] * G[y][x][co]
@@ -1310,32 +1010,6 @@ int launch(const RowArgs &r, int q, int qa, bool cmp, bool relu, bool st, hipStr
     if (r.out2 && r.c_split % NCO != 0) return SHPL_ERR_ARG;
     const dim3 grid((unsigned)(r.n_items * r.n_cob));
     const int key = (((q * 8 + qa) * 2 + (cmp ? 1 : 0)) * 2 + (relu ? 1 : 0)) * 2 + (st ? 1 : 0);
-    if (SHPL_CONV_PAIR && q % 2 == 0) {  // even chunk counts: k_conv_pair (two waves per workgroup)
-        switch (key) {
-#define SHPL_PAIR_CASE(QQ, QQA, CMP, RELU, ST)                                              \
-    case (((QQ * 8 + QQA) * 2 + CMP) * 2 + RELU) * 2 + ST:                                  \
-        hipLaunchKernelGGL((k_conv_pair<QQ, QQA, CMP, RELU, ST>), grid, dim3(128), 0, s, r); \
-        break;
-#define SHPL_PAIR_DENSE(QQ) SHPL_PAIR_CASE(QQ, QQ, 0, 0, 0) SHPL_PAIR_CASE(QQ, QQ, 0, 1, 0) SHPL_PAIR_CASE(QQ, QQ, 0, 0, 1)
-#define SHPL_PAIR_TWO(QQ, QQA)                                                                                 \
-    SHPL_PAIR_CASE(QQ, QQA, 0, 0, 0)                                                                          \
-    SHPL_PAIR_CASE(QQ, QQA, 0, 1, 0) SHPL_PAIR_CASE(QQ, QQA, 1, 0, 0) SHPL_PAIR_CASE(QQ, QQA, 1, 1, 0)        \
-    SHPL_PAIR_CASE(QQ, QQA, 0, 0, 1) SHPL_PAIR_CASE(QQ, QQA, 1, 0, 1)
-            SHPL_PAIR_DENSE(2)
-            SHPL_PAIR_DENSE(4)
-            SHPL_PAIR_TWO(2, 1)
-            SHPL_PAIR_TWO(4, 1)
-            SHPL_PAIR_TWO(4, 2)
-            SHPL_PAIR_TWO(4, 3)
-#undef SHPL_PAIR_TWO
-#undef SHPL_PAIR_DENSE
-#undef SHPL_PAIR_CASE
-            default:
-                return SHPL_ERR_ARG;
-        }
-        SHPL_LAUNCH_CHECK();
-        return SHPL_OK;
-    }
     switch (key) {
 #define SHPL_ROWS_CASE(QQ, QQA, CMP, RELU, ST)                                                  \
     case (((QQ * 8 + QQA) * 2 + CMP) * 2 + RELU) * 2 + ST:                                      \

@@ -35,7 +35,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LLVM = "/opt/rocm/lib/llvm/bin"
-KERNELS = re.compile(r"k_conv_rowsI|k_conv_pairI|k_wgrad_rowsI")
+KERNELS = re.compile(r"k_conv_rowsI|k_wgrad_rowsI")
 VMEM = re.compile(r"^(buffer_|global_|scratch_|flat_)")
 MARK = re.compile(r"^s_waitcnt vmcnt\((\d+)\) expcnt\(6\)$")
 EXIT = re.compile(r"^s_waitcnt vmcnt\(0\) expcnt\(5\)$")  # the loop's exit drain (expcnt(5): its marker)
