@@ -843,7 +843,9 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
     Hi, Wi = spec.img_feat_hw
     px = F * Hb * Wb * esz
     if esz == 2:  # bf16: both convs gather the pooled rows (compact per-run buffer), bv_fused is never stored
-        hbm_bytes = (px * ((cb + ci) + 2 * ci + 2 * ci + 3 * ci + (ci + cb + ci) + (cb + ci))
+        # per pixel, in channels: forward (cb + ci) read + ci written, BN apply 2 ci, BN backward 5 ci, input
+        # gradient ci read + (cb + ci) written, weight gradient (cb + ci) + ci read
+        hbm_bytes = (px * (((cb + ci) + ci) + 2 * ci + 5 * ci + (ci + (cb + ci)) + ((cb + ci) + ci))
                      + F * Hi * Wi * ci * esz + (2 * u_pix + u_cell) * ci * esz + 3 * 12 * nnz)
     else:  # f32: the pooled map written once in the forward, read by the forward and the weight gradient
         hbm_bytes = (px * (ci + (cb + ci + ci) + 2 * ci + 2 * ci + 3 * ci + (ci + cb + ci) + (cb + ci + ci))
