@@ -60,8 +60,15 @@ constexpr int REPI = NCO * 2 + 16;  // epilogue transpose pitch (bytes per pixel
 #ifndef SHPL_ROWS_XCD
 #define SHPL_ROWS_XCD 1  // XCD-contiguous item order (0: blockIdx order)
 #endif
+#ifndef SHPL_ROWS_EPI8
+#define SHPL_ROWS_EPI8 0  // 1: 8-byte stores straight from the accumulators (4 per lane and row), no LDS transpose: correct
+                          // with RSTORES = 4, measured 1.2-1.6x slower (profiles/r04_epi_ab.log)
+#endif
+#ifndef SHPL_ROWS_NTSTORE
+#define SHPL_ROWS_NTSTORE 1  // the epilogue's stores nontemporal (0: plain stores, A/B)
+#endif
 #ifndef SHPL_ROWS_RSTORES
-#define SHPL_ROWS_RSTORES 2
+#define SHPL_ROWS_RSTORES (SHPL_ROWS_EPI8 ? 4 : 2)
 #endif
 constexpr int RSTORES = SHPL_ROWS_RSTORES;  // output stores per row step, always issued (the vmcnt arithmetic)
 constexpr uint32_t OOB = 0x80000000u;  // an offset past every descriptor's num_records: reads zeros
@@ -83,9 +90,6 @@ __device__ uint64_t g_cprobe[CPROBE_WAVES * 10];
     } while (0)
 #endif
 constexpr int SPF = NCO + 4;      // ST: f32 transpose pitch (floats per pixel; 16-byte rows, conflict-free b64 reads)
-#ifndef SHPL_ROWS_EPI8
-#define SHPL_ROWS_EPI8 0  // the dropped 8-byte-store epilogue (wrong results; kept only for the ISA guard's record)
-#endif
 #ifndef SHPL_ROWS_WLATE
 #define SHPL_ROWS_WLATE 0  // 1: no wait for the weights before the loop (the round-3 form, A/B)
 #endif
@@ -394,9 +398,8 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
         uint16_t *orow = obase + (frame_row0 + (int64_t)(ya + b) * r.w + x0) * ostr;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the MFMAs' operand reads of the slot are done
 #if SHPL_ROWS_EPI8
-        // the dropped round-2 form (never shipped; tests/test_isa_guard.py's record of why it failed):
-        // 8-byte stores straight from the accumulators -- 4 per lane and row instead of RSTORES = 2, so the
-        // ring's counted wait leaves 2 of the next row's DMAs unwaited-for and the MFMAs read a stale slot
+        // 8-byte stores straight from the accumulators: 4 per lane and row (RSTORES = 4 in the ring's counted
+        // wait; with 2 the wait left two of the next row's DMAs unwaited-for -- the round-2 failure)
     #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int cl = 8 * g + 4 * hf;
@@ -426,7 +429,7 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
             for (int k = 0; k < 4; k += 2) {
                 // fma(acc, scale, shift - center * scale) (scale 1 / shift 0 when absent), rounded to bf16,
                 // ReLU as max(bits, 0) on the bf16 bit patterns as signed 16-bit integers (negatives, -0
-                // and -NaN -> +0, +NaN kept): the tiled kernel's epilogue, bit for bit (shpl.h)
+                // and -NaN -> +0, +NaN kept): the tiled kernel's epilogue, bit for bit (shpl.h).
                 const float v0 = __builtin_fmaf(a2[4 * g + k], s_par[0][cl + k], s_par[1][cl + k]);
                 const float v1 = __builtin_fmaf(a2[4 * g + k + 1], s_par[0][cl + k + 1], s_par[1][cl + k + 1]);
                 uint32_t w = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
@@ -446,7 +449,11 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
             const int pc = lane + 64 * k, px = pc >> 2, pi = pc & 3;
             const u32x4 v = *reinterpret_cast<const u32x4 *>(s_o + px * REPI + pi * 16);
             uint16_t *dst = row_ok && x0 + px < r.w ? orow + px * (int)ostr + pi * 8 : r.junk + pc * 8;
+#if SHPL_ROWS_NTSTORE
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(dst));
+#else
             *reinterpret_cast<u32x4 *>(dst) = v;
+#endif
         }
 #endif
         if constexpr (ST) {
