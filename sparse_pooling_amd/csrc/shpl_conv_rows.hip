@@ -270,7 +270,11 @@ __device__ __forceinline__ i32x4 rsrc(const void *base, uint32_t bytes) {
 // its ring slots itself (counted vmcnt), while the compiler, seeing an LDS
 // write by DMA, would drain every outstanding DMA (vmcnt(0)) before each
 // ds_read -- the whole prefetch ring. M0 holds the LDS destination (one wait
-// state before the DMA reads it).
+// state before the DMA reads it). Measured and not kept: the DMAs nontemporal (`offen nt lds`: the dense conv
+// 1.40 -> 2.10 ms, its rows' re-reads by the halo and the other output block then miss L2;
+// profiles/r04_ntl_ab.log), and a slot layout of 64-byte pixel quads so that each DMA lane quad reads one
+// contiguous segment instead of 4 (dense conv 1.40 -> 1.34 ms, the pooled and training forms 1-2 % slower;
+// profiles/r04_quad_ab.log).
 __device__ __forceinline__ void dma16(i32x4 rs, uint32_t voff, const uint8_t *wave_dst) {
     const uint32_t lds = (uint32_t)(uintptr_t)wave_dst;
     asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "{m0}"(lds) : "memory");
