@@ -1,4 +1,5 @@
 #!/bin/bash
+# (The switch was removed from the sources after this measurement; a rebuild of the variant equals the default.)
 # Nontemporal LDS-DMA loads in the row kernels (SHPL_ROWS_NTLOAD) against the default library: the conv tests on the
 # the variant, then conv and training bench lines with kernel traces.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

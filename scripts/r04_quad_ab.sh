@@ -1,4 +1,5 @@
 #!/bin/bash
+# (The switch was removed from the sources after this measurement; a rebuild of the variant equals the default.)
 # The row kernels' quad layout (SHPL_ROWS_QUAD: each DMA quad of lanes reads one 64-byte segment) against the
 # piece-major layout: conv parity tests on both, then conv and training bench lines with kernel traces.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
