@@ -52,7 +52,7 @@ sys.path.insert(0, HERE)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 # dense MFMA peaks (MI355X_MICROARCH.md, Matrix cores): f32-input 157.3 TF, bf16 ~2.5 PF
 MFMA_PEAK_TFS = {"f32": 157.3, "bf16": 2500.0}
-DEFAULT_FRAMES = {2: 64, 3: 4, 5: 64}
+DEFAULT_FRAMES = {2: 64, 3: 4, 5: 64, 6: 64}
 CHECKSUM_FILE = os.path.join(HERE, "profiles", "frame_checksums.json")
 
 
@@ -69,7 +69,8 @@ def parse():
     ap.add_argument("--write-checksums", action="store_true",
                     help="store this run's per-frame output checksums in profiles/frame_checksums.json "
                          "(the N=1 reference the N>1 runs are compared with)")
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5])
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5, 6],
+                    help="BASELINE configs 2 / 3 / 5; 6: the RetinaNet P2 SHPL shape (stride 4, 256 ch, f32)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cpu-parallel", action="store_true",
@@ -83,6 +84,9 @@ def parse():
     ap.add_argument("--no-buckets", action="store_true",
                     help="row-keyed layers (config 3): range CSRs + one k_rows launch per pull on two streams "
                          "instead of the index build's buckets, one CSR launch and one shpl_pull_pair launch per pull pair")
+    ap.add_argument("--rows", action="store_true",
+                    help="layer workload: the row-keyed pipeline (bucketed index, one launch per pull pair) at any batch "
+                         "(A/B: config 6 1.95-1.99 vs 1.57 ms, profiles/r04_rows_ab.log)")
     ap.add_argument("--pixel-cols", action="store_true",
                     help="bucketed config 3: the pixel-keyed CSR keeps ent_col (per-column partials in its pulls) "
                          "instead of the identity-column form")
@@ -403,7 +407,7 @@ def main():
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, dev)
     pipeline.FusedPipeline.PIXEL_COLS = args.pixel_cols
     pl = pipeline.FusedPipeline(F, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev,
-                                spec.c_img, dtype=dtype, dual=dual, device=dev,
+                                spec.c_img, dtype=dtype, dual=dual, device=dev, rows=True if args.rows else None,
                                 buckets=False if args.no_buckets else None)
     Hb, Wb = spec.bev_feat_hw
     Hi, Wi = spec.img_feat_hw
@@ -534,7 +538,8 @@ def main():
         total_frames = F * world * args.steps
         traffic, traffic_note, _ = traffic_lookup(f"config{cfg}_F{F}")
         what = {2: "img->BEV SHPL fwd", 3: "dual SHPL fwd + bwd (bf16 storage, f32 accumulate)",
-                5: "dual SHPL fwd (img->BEV and BEV->img)"}[cfg]
+                5: "dual SHPL fwd (img->BEV and BEV->img)",
+                6: "img->BEV SHPL fwd at RetinaNet's P2 (stride 4, FPN 256 ch; not a BASELINE config)"}[cfg]
         out = {
             "metric": "SHPL fused frames/sec + achieved HBM GB/s (% of MI355X peak), 1/2/4/8 GPU",
             "value": round(total_frames / elapsed, 2),

@@ -54,7 +54,11 @@ CONFIG1 = FrameSpec(2000, (1200, 360), (704, 800), (4, 4), 16, 16)
 CONFIG2 = FrameSpec(20000, (1200, 360), (704, 800), (1, 1), 32, 32)
 CONFIG3 = FrameSpec(20000, (1200, 360), (704, 800), (8, 8), 256, 256)
 CONFIG5 = FrameSpec(40000, (1200, 360), (704, 800), (1, 1), 64, 64)
-CONFIGS = {1: CONFIG1, 2: CONFIG2, 3: CONFIG3, 5: CONFIG5}
+# Not a BASELINE config: the RetinaNet P2 fusion (avod/avod/core/models/retinanet_model.py:320-348 with
+# configs/retinanet_car_SHPL.config: SHPL at pyramid level P2, stride 4, FPN 256 channels both sides,
+# bv_index None -- the img->BEV direction only), BEV 176x200, image 90x300, f32.
+CONFIG6 = FrameSpec(20000, (1200, 360), (704, 800), (4, 4), 256, 256)
+CONFIGS = {1: CONFIG1, 2: CONFIG2, 3: CONFIG3, 5: CONFIG5, 6: CONFIG6}
 
 
 def _clip_mask(pts, P, im_size):
