@@ -80,7 +80,7 @@ def parse():
     ap.add_argument("--no-interleave", action="store_true",
                     help="dual configs: start both sparse passes after both dense passes (A/B of the overlap)")
     ap.add_argument("--csr-path", default="auto", choices=["auto", "frame", "segment", "range"],
-                    help="layer workloads: force the CSR builder (shpl_build_csr_path; A/B measurements)")
+                    help="force the CSR builder (shpl_build_csr_path; A/B measurements: the conv / training workloads' segmented CSR 115 / 687 us vs 84 / 112 us per frame sort, profiles/r04_csr_ab.log)")
     ap.add_argument("--no-buckets", action="store_true",
                     help="row-keyed layers (config 3): range CSRs + one k_rows launch per pull on two streams "
                          "instead of the index build's buckets, one CSR launch and one shpl_pull_pair launch per pull pair")
@@ -910,6 +910,9 @@ def run_conv(args, world, rank, dev):
     pipeline.FusedPipeline.PIXEL_COLS = args.pixel_cols
     pl = pipeline.FusedPipeline(F, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev, spec.c_img,
                                 dtype=dtype, device=dev)
+    from sparse_pooling_amd import _lib as L, shpl_map as sm
+    pl.csr_path = sm.ShplMap.CSR_PATH = {"auto": L.CSR_AUTO, "frame": L.CSR_FRAME, "segment": L.CSR_SEGMENT,
+                                         "range": L.CSR_RANGE}[args.csr_path]
     Hb, Wb = spec.bev_feat_hw
     Hi, Wi = spec.img_feat_hw
     cb, ci = spec.c_bev, spec.c_img

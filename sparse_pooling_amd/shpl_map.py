@@ -79,6 +79,8 @@ class ShplMap:
     # ROW_PULLS = True / False forces the form (tests).
     ROWS_FRAMES, ROWS_MAX_KEYS, ROWS_MAX_CAP = 32, 65536, 1 << 24
     ROW_PULLS = None
+    # shpl_build_csr_path's builder for the flat CSRs (L.CSR_AUTO: the library's choice by batch shape)
+    CSR_PATH = L.CSR_AUTO
 
     def csr(self, direction, order):
         key = (direction, order)
@@ -98,11 +100,11 @@ class ShplMap:
             rows = (self.n_frames < self.ROWS_FRAMES and n_keys // max(self.n_frames, 1) <= self.ROWS_MAX_KEYS
                     and self.nnz_cap < self.ROWS_MAX_CAP)
         c = L.Csr(n_keys, self.nnz_cap, self.device, with_col=direction == L.BY_PIXEL, key_range=rows)
-        L.check(L.lib().shpl_build_csr(direction, order, self.n_frames, L.ptr(self.frame_off),
-                                       L.ptr(self.frame_nnz), n_keys // self.n_frames,
-                                       L.ptr(self.cell), L.ptr(self.col), L.ptr(self.val),
-                                       L.ptr(self.pix), c.ref(), L.ptr(c.ws), c.ws.numel(),
-                                       L.stream_of(self.device)), "shpl_build_csr")
+        L.check(L.lib().shpl_build_csr_path(self.CSR_PATH, direction, order, self.n_frames, L.ptr(self.frame_off),
+                                            L.ptr(self.frame_nnz), n_keys // self.n_frames,
+                                            L.ptr(self.cell), L.ptr(self.col), L.ptr(self.val),
+                                            L.ptr(self.pix), c.ref(), L.ptr(c.ws), c.ws.numel(),
+                                            L.stream_of(self.device)), "shpl_build_csr_path")
         self._csr[key] = c
         return c
 
