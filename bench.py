@@ -117,6 +117,8 @@ def parse():
                     help="frames: the BEV maps as the reference's f64 height / density maps, or as the network's "
                          "f32 BEV input (np.dstack of the maps as its tf.float32 placeholder holds them: half the "
                          "bytes; shpl_bev_input)")
+    ap.add_argument("--stream-priority", default="chain", choices=["chain", "dense", "both", "none"],
+                    help="frames workload: which of the index chain / the streaming pass runs on a high-priority stream")
     ap.add_argument("--dense-after", default="start", choices=["start", "velo", "bev", "csr"],
                     help="frames workload: where the streaming pass starts beside the index chain")
     ap.add_argument("--maps-after", default="chain", choices=["stream", "chain"],
@@ -673,11 +675,12 @@ def run_frames(args, world, rank, dev):
     pl.maps_form = args.maps_form
     bev = sd.fill_features(torch.empty((F, pl.Hb, pl.Wb, C), device=dev), fids, 5)
     img = sd.fill_features(torch.empty((F, pl.Hi, pl.Wi, C), device=dev), fids, 6)
-    side = torch.cuda.Stream(device=dev)
     # the index chain on a high-priority stream: its 1024-thread workgroups otherwise wait for
     # whole CUs to drain of k_dense's workgroups (BEV slices 1.07 -> 0.68 ms, step 2.86 -> 2.84 ms,
-    # profiles/r02_priority.log; the step is then bound by k_dense + the sparse pass)
-    chain = torch.cuda.Stream(device=dev, priority=-1)
+    # profiles/r02_priority.log; the step is then bound by k_dense + the sparse pass).
+    # --stream-priority dense|both: A/B of the streaming pass at high priority (profiles/r04_prio_ab.log)
+    side = torch.cuda.Stream(device=dev, priority=-1 if args.stream_priority in ("dense", "both") else 0)
+    chain = torch.cuda.Stream(device=dev, priority=-1 if args.stream_priority in ("chain", "both") else 0)
 
     def velo_step(ev=None):
         with torch.cuda.stream(chain):
