@@ -51,6 +51,13 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
+#ifndef SHPL_ROWS_M16
+// 1: even chunk counts multiply with v_mfma_f32_16x16x32_bf16 (K = 32 input channels, the block's 32 output
+// channels as two halves of 16, the row's 32 pixels as two halves of 16) instead of 32x32x16 -- the same
+// cycles per FLOP; under the chip's load-dependent clock the 16x16 shape has measured more FLOP/s
+// (MI355X_MICROARCH.md, DVFS item 7)
+#define SHPL_ROWS_M16 1
+#endif
 constexpr int NCO = 32;           // output channels per wave
 constexpr int TW = 32;            // strip width (output pixels)
 constexpr int HWD = TW + 2;       // halo row (pixels)
@@ -97,6 +104,23 @@ constexpr int SPF = NCO + 4;      // ST: f32 transpose pitch (floats per pixel; 
 #define SHPL_ROWS_WPE 2  // waves per SIMD of the row kernels (tests/test_isa_guard.py forces 4: spills)
 #endif
 
+// The 16x16x32 shape: even chunk counts without statistics (the statistics forms keep 32x32x16: at 4 chunks
+// pooled they would spill). Independent of the A / B split and of pooling, so that those forms stay bitwise
+// equal to each other.
+template <int Q, bool ST>
+constexpr bool m16() { return SHPL_ROWS_M16 && Q % 2 == 0 && !ST; }
+
+// An f32x16 accumulator as four 16x16 tiles (16 output channels x 16 pixels each): tile 2h + nb.
+__device__ __forceinline__ f32x4 tile4(const f32x16 &a, int t) {
+    return f32x4{a[4 * t], a[4 * t + 1], a[4 * t + 2], a[4 * t + 3]};
+}
+__device__ __forceinline__ void set_tile4(f32x16 &a, int t, const f32x4 &v) {
+    a[4 * t] = v[0];
+    a[4 * t + 1] = v[1];
+    a[4 * t + 2] = v[2];
+    a[4 * t + 3] = v[3];
+}
+
 // The ring's counted wait: vmcnt(K) leaves the K most recent vector-memory operations -- the DMAs and
 // stores of the RING-1 later steps -- in flight. expcnt(6) is a no-op in a compute kernel (no exports)
 // that marks the wait as this one, so tests/test_isa_guard.py can find it in the disassembly and
@@ -110,11 +134,11 @@ constexpr int SPF = NCO + 4;      // ST: f32 transpose pitch (floats per pixel; 
 #define SHPL_RING_WAIT(K) asm volatile("s_waitcnt vmcnt(%0) expcnt(6)" ::"n"(K) : "memory")
 #endif
 
-// Pooled forms whose per-lane DMA offsets live in LDS instead of VGPRs (one ds_read_b32 each per row):
-// with statistics, and Q = 4 / QA = 1 (both would otherwise spill to scratch, whose reloads inside the
-// loop drain the ring).
+// Forms whose per-lane DMA offsets live in LDS instead of VGPRs (one ds_read_b32 each per row): pooled with
+// statistics, and every 4-chunk form (they would otherwise spill to scratch, whose reloads inside the loop
+// drain the ring).
 template <int Q, int QA, bool CMP, bool ST>
-constexpr bool offsets_in_lds() { return CMP && (ST || (Q == 4 && QA == 1)); }
+constexpr bool offsets_in_lds() { return (CMP && ST) || (Q == 4 && (CMP || QA == 1)); }
 
 template <int Q, int QA, bool ST = false>
 struct Layout {
@@ -347,7 +371,8 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
                                      const uint64_t *s_occ, const int32_t *s_first, uint64_t b_rows,
                                      const uint32_t (&offa)[Layout<Q, QA>::NA],
                                      const int32_t (&offb)[Layout<Q, QA>::NB > 0 ? Layout<Q, QA>::NB : 1],
-                                     const uint32_t *s_offs, int lane, uint64_t (&ph)[5]) {
+                                     const uint32_t *s_offs, const uint32_t (&rdq)[2], int lane,
+                                     uint64_t (&ph)[5]) {
     typedef Layout<Q, QA, ST> L;
 #if SHPL_ROWS_PROBE == 3
     uint64_t t0, t1, t2, t3, t4;
@@ -359,6 +384,32 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
     SHPL_STAMP(t1);
 #endif
     f32x16 &a0 = acc[(U + 1) % 3], &a1 = acc[U], &a2 = acc[(U + 2) % 3];
+    if constexpr (m16<Q, ST>()) {
+        // K-chunk c (32 channels: pieces 4c .. 4c+3, each lane its piece 4c + lane / 16 from A or B), then kx,
+        // then the pixel half nb; both output halves h per operand read. A split between A and B and the
+        // skipped pooled chunks leave every accumulator's summation order unchanged, as below
+#pragma unroll
+        for (int c = 0; c < Q / 2; ++c) {
+            // a chunk of B pieces only, in a pooled row without an occupied cell in the window: exact zeros
+            if (CMP && 4 * c >= 2 * QA && !((b_rows >> j) & 1)) continue;
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    const bf16x8 xv =
+                        *reinterpret_cast<const bf16x8 *>(s_ring + rdq[c] + (U * L::SLOT + (16 * nb + kx) * 16));
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int t = 2 * h + nb;
+                        set_tile4(a0, t, __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[2 * c + h][kx], xv, tile4(a0, t), 0, 0, 0));
+                        set_tile4(a1, t,
+                                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[2 * c + h][3 + kx], xv, tile4(a1, t), 0, 0, 0));
+                        set_tile4(a2, t,
+                                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[2 * c + h][6 + kx], xv, tile4(a2, t), 0, 0, 0));
+                    }
+                }
+        }
+    } else {
     // chunk-major (q outer): a split of the channels between A and B, and the skipped pooled chunks below,
     // leave every accumulator's summation order unchanged
 #pragma unroll
@@ -385,6 +436,7 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
                 a2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[q][6 + kx], xv, a2, 0, 0, 0);
             }
         }
+    }
     }
 #if SHPL_ROWS_PROBE == 3
     SHPL_STAMP(t2);
@@ -425,6 +477,28 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
             __builtin_memcpy(dst, pk, sizeof(pk));
         }
 #else
+        if constexpr (m16<Q, ST>()) {
+            // tile t = 2h + nb: the lane's 4 consecutive channels 16h + 4 (lane / 16) .. of pixel 16 nb + lane % 16
+    #pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int cl = 16 * (t >> 1) + 4 * (lane >> 4), px = 16 * (t & 1) + (lane & 15);
+                uint32_t pk[2];
+    #pragma unroll
+                for (int k = 0; k < 4; k += 2) {
+                    const float v0 = __builtin_fmaf(a2[4 * t + k], s_par[0][cl + k], s_par[1][cl + k]);
+                    const float v1 = __builtin_fmaf(a2[4 * t + k + 1], s_par[0][cl + k + 1], s_par[1][cl + k + 1]);
+                    uint32_t w = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
+                    if (RELU) {
+                        s16x2 hh;
+                        __builtin_memcpy(&hh, &w, 4);
+                        hh = __builtin_elementwise_max(hh, s16x2{0, 0});
+                        __builtin_memcpy(&w, &hh, 4);
+                    }
+                    pk[k >> 1] = w;
+                }
+                __builtin_memcpy(s_o + px * REPI + cl * 2, pk, sizeof(pk));
+            }
+        } else {
     #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int cl = 8 * g + 4 * hf;
@@ -447,6 +521,7 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
             }
             __builtin_memcpy(s_o + pl * REPI + cl * 2, pk, sizeof(pk));
         }
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     #pragma unroll
         for (int k = 0; k < 2; ++k) {  // 32 pixels x 4 pieces of 8 channels
@@ -466,10 +541,17 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
             // bf16 transpose's reads above are done first), then lane (cp, qt) sums channels 2cp, 2cp+1 over
             // pixels 8qt .. 8qt+7 of the row into its band sums (kept in LDS: the pooled form has no VGPR to spare)
             float *s_f = reinterpret_cast<float *>(s_o);
+            if constexpr (m16<Q, ST>()) {
+    #pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    *reinterpret_cast<f32x4 *>(s_f + (16 * (t & 1) + (lane & 15)) * SPF + 16 * (t >> 1) +
+                                               4 * (lane >> 4)) = tile4(a2, t);
+            } else {
     #pragma unroll
             for (int g = 0; g < 4; ++g)
                 *reinterpret_cast<f32x4 *>(s_f + pl * SPF + 8 * g + 4 * hf) =
                     f32x4{a2[4 * g], a2[4 * g + 1], a2[4 * g + 2], a2[4 * g + 3]};
+            }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (row_ok) {
                 const int cp = lane & 15, qt = lane >> 4, nv = r.w - x0;
@@ -528,8 +610,14 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
     (void)ph;
 }
 
+// Waves per SIMD: SHPL_ROWS_WPE, but the pooled 3 + 1 chunk form without ReLU on the 16x16 shape may drop to
+// one (it needs 257 registers at two; the allocation differs from the ReLU form's by one register).
 template <int Q, int QA, bool CMP, bool RELU, bool ST>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS_WPE, SHPL_ROWS_WPE))) void k_conv_rows(
+constexpr int rows_wpe_min() { return (m16<Q, ST>() && CMP && Q == 4 && QA == 3 && !RELU) ? 1 : SHPL_ROWS_WPE; }
+
+template <int Q, int QA, bool CMP, bool RELU, bool ST>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rows_wpe_min<Q, QA, CMP, RELU, ST>(),
+                                                                    SHPL_ROWS_WPE))) void k_conv_rows(
     const RowArgs r) {
     typedef Layout<Q, QA, ST> L;
 #if SHPL_ROWS_PROBE == 3
@@ -610,11 +698,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS_WP
     // the chunk weights of all taps stay in registers: A operands (32 output x 16 input channels)
     bf16x8 wr[Q][9];
     const uint16_t *wq = r.wp + (int64_t)cob * Q * W_ROWS * 16;
+    if constexpr (m16<Q, ST>()) {
+        // wr[2c + h][t]: the A operand of K-chunk c, output half h (lane: channel 16h + lane % 16, inputs
+        // 8 (lane / 16) .. of the chunk: 16-channel chunk 2c + lane / 32, its half (lane / 16) % 2)
+#pragma unroll
+        for (int c = 0; c < Q / 2; ++c)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int t = 0; t < 9; ++t)
+                    wr[2 * c + h][t] = *reinterpret_cast<const bf16x8 *>(
+                        wq + (((2 * c + (lane >> 5)) * 9 + t) * NCO + 16 * h + (lane & 15)) * 16 + ((lane >> 4) & 1) * 8);
+    } else {
 #pragma unroll
     for (int q = 0; q < Q; ++q)
 #pragma unroll
         for (int t = 0; t < 9; ++t)
             wr[q][t] = *reinterpret_cast<const bf16x8 *>(wq + ((q * 9 + t) * NCO + (lane & 31)) * 16 + (lane >> 5) * 8);
+    }
 #if !SHPL_ROWS_WLATE
     // the weights have landed before the loop, as the compiler's wait model must know: its waitcnt pass
     // does not see the ring's asm DMAs, so weights still "pending" at the loop header made it put a ladder of
@@ -629,6 +730,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS_WP
         for (int i = 0; i < 16; ++i) acc[k][i] = 0.0f;
     // B operand (pixels): lane (pl, hf) reads pixel pl (+ kx) of piece 2 q + hf
     const uint8_t *rd = s_ring + (lane >> 5) * HWD * 16 + (lane & 31) * 16;
+    // 16x16x32 operand reads: K-chunk c's piece 4c + lane / 16 (from A below 2 QA, else B) at pixel lane % 16
+    uint32_t rdq[2];  // byte offsets in s_ring
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const int g = 4 * c + (lane >> 4);
+        rdq[c] = (uint32_t)(((g < 2 * QA ? g * HWD : L::RB + (g - 2 * QA) * HWD) + (lane & 15)) * 16);
+    }
     uint64_t ph[5] = {0, 0, 0, 0, 0};
 #if SHPL_ROWS_PROBE == 3
     uint64_t tk0, rt1;
@@ -639,7 +747,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHPL_ROWS_WP
 #define SHPL_ROWS_STEP(UU)                                                                                          \
     if (j + UU >= n_in) break;                                                                                      \
     step<Q, QA, CMP, RELU, ST, UU>(r, wr, acc, s_par, rd, s_ring, frame_row0, x0, ya, n_in, n_out, obase, ostr, s_st, \
-                                   j + UU, s_occ, s_first, b_rows, offa, offb, s_offs, lane, ph);
+                                   j + UU, s_occ, s_first, b_rows, offa, offb, s_offs, rdq, lane, ph);
         SHPL_ROWS_STEP(0)
         SHPL_ROWS_STEP(1)
         SHPL_ROWS_STEP(2)
