@@ -58,6 +58,9 @@ typedef short s16x2 __attribute__((ext_vector_type(2)));
 // (MI355X_MICROARCH.md, DVFS item 7)
 #define SHPL_ROWS_M16 1
 #endif
+#ifndef SHPL_ROWS_M16_ST
+#define SHPL_ROWS_M16_ST 1  // the statistics forms too (pooled: one operand read ahead of the MFMAs)
+#endif
 constexpr int NCO = 32;           // output channels per wave
 constexpr int TW = 32;            // strip width (output pixels)
 constexpr int HWD = TW + 2;       // halo row (pixels)
@@ -108,7 +111,7 @@ constexpr int SPF = NCO + 4;      // ST: f32 transpose pitch (floats per pixel; 
 // pooled they would spill). Independent of the A / B split and of pooling, so that those forms stay bitwise
 // equal to each other.
 template <int Q, bool ST>
-constexpr bool m16() { return SHPL_ROWS_M16 && Q % 2 == 0 && !ST; }
+constexpr bool m16() { return SHPL_ROWS_M16 && Q % 2 == 0 && (SHPL_ROWS_M16_ST || !ST); }
 
 // An f32x16 accumulator as four 16x16 tiles (16 output channels x 16 pixels each): tile 2h + nb.
 __device__ __forceinline__ f32x4 tile4(const f32x16 &a, int t) {
@@ -407,6 +410,8 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
                         set_tile4(a2, t,
                                   __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[2 * c + h][6 + kx], xv, tile4(a2, t), 0, 0, 0));
                     }
+                    // pooled statistics forms: at most one operand read ahead of the MFMAs (registers)
+                    if constexpr (ST && CMP) asm volatile("" ::: "memory");
                 }
         }
     } else {
