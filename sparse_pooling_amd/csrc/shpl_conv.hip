@@ -31,6 +31,8 @@
 // arithmetic of k_sparse (shpl_pull.hip: TF order, separate multiply and
 // add), so the conv of the fused form is bitwise the conv of
 // [bev || shpl_pull(...)] and bv_fused never reaches HBM.
+#include <type_traits>
+
 #include "shpl_common.h"
 #include "shpl_conv_rows.h"
 
@@ -839,6 +841,20 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_apply(const T *x, T *y, int64
 // apply 2.68 -> 2.35 ms; bf16 at 2 rows per thread was 1.7x slower than at 8.
 constexpr int64_t bn_rows_per_thread(int esz) { return esz == 4 ? 4 : 8; }
 
+// f(std::bool_constant<b0>{}, std::bool_constant<b1>{}, ...) for run-time switches b0, b1, ...: the
+// instance of a vector BatchNorm kernel for one combination of its compile-time forms.
+template <bool... Bs, typename F>
+void bn_forms(F &&f) {
+    f(std::bool_constant<Bs>{}...);
+}
+template <bool... Bs, typename F, typename... R>
+void bn_forms(F &&f, bool b, R... rest) {
+    if (b)
+        bn_forms<Bs..., true>(f, rest...);
+    else
+        bn_forms<Bs..., false>(f, rest...);
+}
+
 // 16-byte pieces of the BatchNorm streams, nontemporal (each byte is touched
 // once per pass; the maps are far larger than the caches).
 template <typename T, int VEC>
@@ -865,10 +881,15 @@ constexpr int BN_U = 4;  // rows per iteration of the vector apply kernels: thei
 // Thread layout of the vector forms: c / VEC piece lanes (a power of two
 // dividing the block) times SHPL_BLOCK / (c / VEC) row lanes, so each thread
 // keeps one channel group and its per-channel coefficients in registers.
-template <typename T>
+// The vector apply kernels take their switches (ReLU, beta, y, training) as
+// template arguments: as run-time flags they put a branch around every element
+// of the unrolled loops (bn_forms picks the instance; bf16 at 64 frames: the
+// backward apply 1,199 -> 1,147 us, the forward apply 777 -> 750 us,
+// profiles/r04_bn_ab.log).
+template <typename T, bool BETA, bool ACT>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_apply_vec(const T *x, T *y, int64_t rows, int64_t stride, int c,
-                                                             const float *mean, const float *scale, const float *beta,
-                                                             int act) {
+                                                             const float *mean, const float *scale,
+                                                             const float *beta) {
     constexpr int VEC = 16 / sizeof(T);
     const int pr = c / VEC, rpb = SHPL_BLOCK / pr;
     const int ch0 = (threadIdx.x % pr) * VEC;
@@ -877,7 +898,7 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_apply_vec(const T *x, T *y, i
     for (int k = 0; k < VEC; ++k) {
         m[k] = mean[ch0 + k];
         sc[k] = scale[ch0 + k];
-        b[k] = beta ? beta[ch0 + k] : 0.0f;
+        b[k] = BETA ? beta[ch0 + k] : 0.0f;
     }
     const int64_t step = (int64_t)gridDim.x * rpb;
     for (int64_t r0 = (int64_t)blockIdx.x * rpb + threadIdx.x / pr; r0 < rows; r0 += BN_U * step) {
@@ -891,8 +912,8 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_apply_vec(const T *x, T *y, i
 #pragma unroll
             for (int k = 0; k < VEC; ++k) {
                 float t = __fmul_rn(__fsub_rn(v[u][k], m[k]), sc[k]);
-                if (beta) t = __fadd_rn(t, b[k]);
-                v[u][k] = (act == 1 && !(t > 0.0f)) ? 0.0f : t;
+                if constexpr (BETA) t = __fadd_rn(t, b[k]);
+                v[u][k] = (ACT && !(t > 0.0f)) ? 0.0f : t;
             }
             Piece<T, VEC>::store(y + (r0 + u * step) * stride + ch0, v[u]);
         }
@@ -1039,12 +1060,12 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_partial_vec(const T *y, c
     }
 }
 
-template <typename T>
+template <typename T, bool ACT, bool HASY, bool BETA, bool TRAIN>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_apply_vec(const T *y, const T *raw, const T *gy,
                                                                  int64_t rows, int64_t stride, int c,
                                                                  const float *mean, const float *scale,
-                                                                 const float *gamma, const float *beta, int act,
-                                                                 int training, const float *mean_terms, T *graw) {
+                                                                 const float *gamma, const float *beta,
+                                                                 const float *mean_terms, T *graw) {
     constexpr int VEC = 16 / sizeof(T);
     const int pr = c / VEC, rpb = SHPL_BLOCK / pr;
     const int ch0 = (threadIdx.x % pr) * VEC;
@@ -1052,12 +1073,12 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_apply_vec(const T *y, con
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
         const int ch = ch0 + k;
-        b[k] = beta ? beta[ch] : 0.0f;
+        b[k] = BETA ? beta[ch] : 0.0f;
         sc[k] = scale ? scale[ch] : 1.0f;
         m[k] = mean ? mean[ch] : 0.0f;
         inv[k] = __fdiv_rn(sc[k], gamma ? gamma[ch] : 1.0f);
-        t0[k] = training ? mean_terms[ch] : 0.0f;
-        t1[k] = training ? mean_terms[c + ch] : 0.0f;
+        t0[k] = TRAIN ? mean_terms[ch] : 0.0f;
+        t1[k] = TRAIN ? mean_terms[c + ch] : 0.0f;
     }
     const int64_t step = (int64_t)gridDim.x * rpb;
     constexpr int U = BN_U / 2;  // two or three streams in per row
@@ -1068,8 +1089,8 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_apply_vec(const T *y, con
             if (r0 + u * step >= rows) break;
             const int64_t o = (r0 + u * step) * stride + ch0;
             Piece<T, VEC>::load(gy + o, gv[u]);
-            if (act == 1 && y) Piece<T, VEC>::load(y + o, yv[u]);
-            if (training || !y) Piece<T, VEC>::load(raw + o, xv[u]);
+            if constexpr (ACT && HASY) Piece<T, VEC>::load(y + o, yv[u]);
+            if constexpr (TRAIN || (ACT && !HASY)) Piece<T, VEC>::load(raw + o, xv[u]);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1077,12 +1098,12 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_bn_bwd_apply_vec(const T *y, con
             float out[VEC];
 #pragma unroll
             for (int k = 0; k < VEC; ++k) {
-                if (act == 1 && !y) {
+                if constexpr (ACT && !HASY) {
                     const float t = __fmul_rn(__fsub_rn(xv[u][k], m[k]), sc[k]);
-                    yv[u][k] = beta ? __fadd_rn(t, b[k]) : t;
+                    yv[u][k] = BETA ? __fadd_rn(t, b[k]) : t;
                 }
-                const float gb = (act == 1 && !(yv[u][k] > 0.0f)) ? 0.0f : gv[u][k];
-                if (training) {
+                const float gb = (ACT && !(yv[u][k] > 0.0f)) ? 0.0f : gv[u][k];
+                if constexpr (TRAIN) {
                     const float xh = __fmul_rn(__fsub_rn(xv[u][k], m[k]), inv[k]);
                     out[k] = __fmul_rn(sc[k], __fsub_rn(__fsub_rn(gb, t0[k]), __fmul_rn(xh, t1[k])));
                 } else {
@@ -1805,18 +1826,22 @@ extern "C" int shpl_batch_norm(int dtype, int64_t rows, void *d_x, void *d_y, in
     const int grid = grid_for(rows * c / (vform ? vec : 1), SHPL_BLOCK * bn_rows_per_thread(16 / vec), 1 << 22);
     if (dtype == SHPL_F32) {
         if (vform)
-            hipLaunchKernelGGL(k_bn_apply_vec<float>, dim3(grid), dim3(SHPL_BLOCK), 0, s,
-                               reinterpret_cast<const float *>(d_x), reinterpret_cast<float *>(d_y), rows, stride,
-                               (int)c, mean, scale, d_beta, act);
+            bn_forms([&](auto B, auto A) {
+                hipLaunchKernelGGL((k_bn_apply_vec<float, B.value, A.value>), dim3(grid), dim3(SHPL_BLOCK), 0, s,
+                                   reinterpret_cast<const float *>(d_x), reinterpret_cast<float *>(d_y), rows, stride,
+                                   (int)c, mean, scale, d_beta);
+            }, d_beta != nullptr, act == 1);
         else
             hipLaunchKernelGGL(k_bn_apply<float>, dim3(grid), dim3(SHPL_BLOCK), 0, s,
                                reinterpret_cast<const float *>(d_x), reinterpret_cast<float *>(d_y), rows, stride,
                                (int)c, mean, scale, d_beta, act);
     } else {
         if (vform)
-            hipLaunchKernelGGL(k_bn_apply_vec<uint16_t>, dim3(grid), dim3(SHPL_BLOCK), 0, s,
-                               reinterpret_cast<const uint16_t *>(d_x), reinterpret_cast<uint16_t *>(d_y), rows,
-                               stride, (int)c, mean, scale, d_beta, act);
+            bn_forms([&](auto B, auto A) {
+                hipLaunchKernelGGL((k_bn_apply_vec<uint16_t, B.value, A.value>), dim3(grid), dim3(SHPL_BLOCK), 0, s,
+                                   reinterpret_cast<const uint16_t *>(d_x), reinterpret_cast<uint16_t *>(d_y), rows,
+                                   stride, (int)c, mean, scale, d_beta);
+            }, d_beta != nullptr, act == 1);
         else
             hipLaunchKernelGGL(k_bn_apply<uint16_t>, dim3(grid), dim3(SHPL_BLOCK), 0, s,
                                reinterpret_cast<const uint16_t *>(d_x), reinterpret_cast<uint16_t *>(d_y), rows,
@@ -1872,6 +1897,7 @@ extern "C" int shpl_batch_norm_backward(int dtype, int64_t rows, const void *d_y
         typedef decltype(tag) T;
         const T *y = (const T *)d_y, *r = (const T *)rw, *g = (const T *)d_gy;
         if (vform)
+            // (its switches as template arguments measured slower: 785 vs 747 us, profiles/r04_bn_ab.log)
             hipLaunchKernelGGL(k_bn_bwd_partial_vec<T>, dim3(nb), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride,
                                (int)c, d_mean, d_scale, d_gamma, beta, act, rpb, part);
         else
@@ -1880,8 +1906,11 @@ extern "C" int shpl_batch_norm_backward(int dtype, int64_t rows, const void *d_y
         hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((unsigned)c), dim3(SHPL_BLOCK), 0, s, part, nb,
                            (int)c, (double)rows, d_dbeta, d_raw ? d_dgamma : nullptr, mt);
         if (vform)
-            hipLaunchKernelGGL(k_bn_bwd_apply_vec<T>, dim3(grid), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride,
-                               (int)c, d_mean, d_scale, d_gamma, beta, act, training, mt, (T *)d_graw);
+            bn_forms([&](auto A, auto Y, auto B, auto TR) {
+                hipLaunchKernelGGL((k_bn_bwd_apply_vec<T, A.value, Y.value, B.value, TR.value>), dim3(grid),
+                                   dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride, (int)c, d_mean, d_scale, d_gamma,
+                                   beta, mt, (T *)d_graw);
+            }, act == 1, d_y != nullptr, beta != nullptr, training != 0);
         else
             hipLaunchKernelGGL(k_bn_bwd_apply<T>, dim3(grid), dim3(SHPL_BLOCK), 0, s, y, r, g, rows, stride, (int)c,
                                d_mean, d_scale, d_gamma, beta, act, training, mt, (T *)d_graw);
