@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 4 evidence on the final tree: the whole GPU suite, smoke, every bench workload, kernel traces of the
-# headline, config 3, the bf16 conv and the bf16 training step.
+# headline, config 3, the bf16 conv and the bf16 training step; the f32 conv's bench line and PMC passes.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -21,6 +21,7 @@ run frames_bev --workload frames --maps-form bev_input
 run conv_bf16 --workload conv --dtype bf16 --no-cpu-baseline
 run train_bf16 --workload conv --train --dtype bf16 --no-cpu-baseline
 run c2f8 --frames 8 --no-cpu-baseline
+run conv_f32 --workload conv --no-cpu-baseline
 trace() {  # name, args...
   local n=$1; shift
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$n -o run --output-format csv -- \
@@ -31,4 +32,5 @@ trace c2 --steps 20 --warmup 2
 trace c3 --config 3 --steps 100
 trace conv_bf16 --workload conv --dtype bf16
 trace train_bf16 --workload conv --train --dtype bf16 --steps 10
+DT=f32 bash scripts/gpu_conv_prof.sh || exit 1
 echo done
