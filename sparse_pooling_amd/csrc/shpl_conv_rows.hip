@@ -61,6 +61,12 @@ typedef short s16x2 __attribute__((ext_vector_type(2)));
 #ifndef SHPL_ROWS_M16_ST
 #define SHPL_ROWS_M16_ST 1  // the statistics forms too (pooled: one operand read ahead of the MFMAs)
 #endif
+#ifndef SHPL_ROWS_STREG
+// 1: the 16x16 statistics forms sum each row straight from the accumulators (a lane's two pixels, then one
+// DPP exchange across lane ^ 8) into per-lane band sums in LDS, reduced over the pixel lanes once per band;
+// 0: each row's f32 accumulators through a transpose in the ring slot (the 32x32 forms always do)
+#define SHPL_ROWS_STREG 1
+#endif
 constexpr int NCO = 32;           // output channels per wave
 constexpr int TW = 32;            // strip width (output pixels)
 constexpr int HWD = TW + 2;       // halo row (pixels)
@@ -112,6 +118,16 @@ constexpr int SPF = NCO + 4;      // ST: f32 transpose pitch (floats per pixel; 
 // equal to each other.
 template <int Q, bool ST>
 constexpr bool m16() { return SHPL_ROWS_M16 && Q % 2 == 0 && (SHPL_ROWS_M16_ST || !ST); }
+
+// The statistics forms that sum from the accumulators (SHPL_ROWS_STREG): the 16x16 ones but the dense 1 + 3
+// chunk form (its registers spill)
+template <int Q, int QA, bool CMP, bool ST>
+constexpr bool streg() { return SHPL_ROWS_STREG && ST && m16<Q, ST>() && !(Q == 4 && QA == 1 && !CMP); }
+
+// v of lane i ^ 8 inside each row of 16 lanes (DPP row_ror:8, no LDS)
+__device__ __forceinline__ float lane_xor8(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xf, 0xf, false));
+}
 
 // An f32x16 accumulator as four 16x16 tiles (16 output channels x 16 pixels each): tile 2h + nb.
 __device__ __forceinline__ f32x4 tile4(const f32x16 &a, int t) {
@@ -375,7 +391,7 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
                                      const uint32_t (&offa)[Layout<Q, QA>::NA],
                                      const int32_t (&offb)[Layout<Q, QA>::NB > 0 ? Layout<Q, QA>::NB : 1],
                                      const uint32_t *s_offs, const uint32_t (&rdq)[2], int lane,
-                                     uint64_t (&ph)[5]) {
+                                     f32x4 (&str)[2], uint64_t (&ph)[5]) {
     typedef Layout<Q, QA, ST> L;
 #if SHPL_ROWS_PROBE == 3
     uint64_t t0, t1, t2, t3, t4;
@@ -540,7 +556,37 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
 #endif
         }
 #endif
-        if constexpr (ST) {
+        if constexpr (streg<Q, QA, CMP, ST>()) {
+            // batch statistics of the pre-activation row (f32): the lane's channels 16h + 4 (lane / 16) + k at its
+            // pixels lane % 16 and 16 + lane % 16 (tiles 2h, 2h + 1) summed, then halves exchanged across lane ^ 8
+            // (bit 3 clear keeps h = 0, set h = 1) and added to the lane's band sums s_st[lane] / s_st[64 + lane]
+            if (row_ok) {
+                const int nv = r.w - x0, p = lane & 15;
+                const bool ok0 = p < nv, ok1 = 16 + p < nv, hi = (lane >> 3) & 1;
+                f32x4 ss = SHPL_ROWS_STREG == 2 ? str[0] : s_st[lane], sq = SHPL_ROWS_STREG == 2 ? str[1] : s_st[64 + lane];
+    #pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    float sv[2], qv[2];
+    #pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const float v0 = ok0 ? a2[4 * (2 * h) + k] : 0.0f, v1 = ok1 ? a2[4 * (2 * h + 1) + k] : 0.0f;
+                        sv[h] = __fadd_rn(v0, v1);
+                        qv[h] = __fadd_rn(__fmul_rn(v0, v0), __fmul_rn(v1, v1));
+                    }
+                    const float ks = hi ? sv[1] : sv[0], gs = hi ? sv[0] : sv[1];
+                    const float kq = hi ? qv[1] : qv[0], gq = hi ? qv[0] : qv[1];
+                    ss[k] = __fadd_rn(ss[k], __fadd_rn(ks, lane_xor8(gs)));
+                    sq[k] = __fadd_rn(sq[k], __fadd_rn(kq, lane_xor8(gq)));
+                }
+                if constexpr (SHPL_ROWS_STREG == 2) {
+                    str[0] = ss;
+                    str[1] = sq;
+                } else {
+                    s_st[lane] = ss;
+                    s_st[64 + lane] = sq;
+                }
+            }
+        } else if constexpr (ST) {
             // batch statistics of the pre-activation row (f32, as the tiled kernel): the accumulator through a
             // second transpose in the slot ([pixel][SPF floats]; LDS runs one wave's operations in order, so the
             // bf16 transpose's reads above are done first), then lane (cp, qt) sums channels 2cp, 2cp+1 over
@@ -650,9 +696,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rows_wpe_min
     const bool second = r.out2 && cob * NCO >= r.c_split;
     uint16_t *const obase = second ? r.out2 + (cob * NCO - r.c_split) : r.out + cob * NCO;
     const int64_t ostr = second ? r.out2_stride : r.out_stride;
-    // ST: lane (cp, qt)'s band sums of channels 2cp, 2cp+1 (sum, sum; square sum, square sum)
-    __shared__ f32x4 s_st[ST ? 64 : 1];
+    // ST: lane (cp, qt)'s band sums of channels 2cp, 2cp+1 (sum, sum; square sum, square sum); with STREG the
+    // lane's sums (s_st[lane]) and square sums (s_st[64 + lane]) of channels 16 ((lane / 8) % 2) + 4 (lane / 16) + k
+    constexpr bool STREG = streg<Q, QA, CMP, ST>();
+    __shared__ f32x4 s_st[ST ? (STREG ? 128 : 64) : 1];
     if constexpr (ST) s_st[lane] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    if constexpr (STREG) s_st[64 + lane] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     const int H = r.h;
     const int x0 = strip * TW, ya = band * r.band;
     const int n_out = min(r.band, H - ya), n_in = n_out + 2;
@@ -743,6 +792,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rows_wpe_min
         rdq[c] = (uint32_t)(((g < 2 * QA ? g * HWD : L::RB + (g - 2 * QA) * HWD) + (lane & 15)) * 16);
     }
     uint64_t ph[5] = {0, 0, 0, 0, 0};
+    f32x4 str[2] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};  // STREG == 2: the band sums
 #if SHPL_ROWS_PROBE == 3
     uint64_t tk0, rt1;
     SHPL_STAMP(tk0);
@@ -752,7 +802,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rows_wpe_min
 #define SHPL_ROWS_STEP(UU)                                                                                          \
     if (j + UU >= n_in) break;                                                                                      \
     step<Q, QA, CMP, RELU, ST, UU>(r, wr, acc, s_par, rd, s_ring, frame_row0, x0, ya, n_in, n_out, obase, ostr, s_st, \
-                                   j + UU, s_occ, s_first, b_rows, offa, offb, s_offs, rdq, lane, ph);
+                                   j + UU, s_occ, s_first, b_rows, offa, offb, s_offs, rdq, lane, str, ph);
         SHPL_ROWS_STEP(0)
         SHPL_ROWS_STEP(1)
         SHPL_ROWS_STEP(2)
@@ -776,7 +826,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rows_wpe_min
         o[5] = (uint64_t)n_in;
     }
 #endif
-    if constexpr (ST) {  // the band's sums over the 4 pixel quarters, then one double per (channel, statistic)
+    if constexpr (STREG) {  // the band's sums over the 8 pixel lanes of each channel group, one double each
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        f32x4 ss = SHPL_ROWS_STREG == 2 ? str[0] : s_st[lane], sq = SHPL_ROWS_STREG == 2 ? str[1] : s_st[64 + lane];
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                ss[k] = __fadd_rn(ss[k], __shfl_xor(ss[k], o, 64));
+                sq[k] = __fadd_rn(sq[k], __shfl_xor(sq[k], o, 64));
+            }
+        if ((lane & 7) == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int c = cob * NCO + 16 * ((lane >> 3) & 1) + 4 * (lane >> 4) + k;
+                r.part[((int64_t)c * 2 + 0) * r.n_items + item] = (double)ss[k];
+                r.part[((int64_t)c * 2 + 1) * r.n_items + item] = (double)sq[k];
+            }
+        }
+    } else if constexpr (ST) {  // the band's sums over the 4 pixel quarters, then one double per (channel, statistic)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const f32x4 a = s_st[lane];
         float sst[4] = {a[0], a[1], a[2], a[3]};
