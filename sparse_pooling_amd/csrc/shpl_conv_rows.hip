@@ -64,8 +64,10 @@ typedef short s16x2 __attribute__((ext_vector_type(2)));
 #ifndef SHPL_ROWS_STREG
 // 1: the 16x16 statistics forms sum each row straight from the accumulators (a lane's two pixels, then one
 // DPP exchange across lane ^ 8) into per-lane band sums in LDS, reduced over the pixel lanes once per band;
-// 0: each row's f32 accumulators through a transpose in the ring slot (the 32x32 forms always do)
-#define SHPL_ROWS_STREG 1
+// 2: the same with the band sums in 8 registers (training forward 1,287-1,313 -> 1,271-1,278 us,
+// profiles/r04_streg2_ab.log); 0: each row's f32 accumulators through a transpose in the ring slot (the
+// 32x32 forms always do)
+#define SHPL_ROWS_STREG 2
 #endif
 constexpr int NCO = 32;           // output channels per wave
 constexpr int TW = 32;            // strip width (output pixels)
