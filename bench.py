@@ -112,6 +112,9 @@ def parse():
     ap.add_argument("--train", action="store_true",
                     help="conv workload: training step (batch-statistics BatchNorm forward + the whole backward: "
                          "BN/ReLU, input and weight gradients of the conv, the pooled channels' gradient to the image)")
+    ap.add_argument("--no-wgrad-reuse", action="store_true",
+                    help="conv training (bf16): the weight gradient prepares its own pooled operand instead of "
+                         "reading the forward's (shpl_conv3x3_wgrad_reuse; A/B)")
     ap.add_argument("--scan-points", type=int, default=120000, help="points per velodyne scan (frames)")
     ap.add_argument("--maps-form", default="f64", choices=["f64", "bev_input"],
                     help="frames: the BEV maps as the reference's f64 height / density maps, or as the network's "
@@ -805,6 +808,7 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
     Hb, Wb = spec.bev_feat_hw
     cb, ci = spec.c_bev, spec.c_img
     esz = 2 if dtype == torch.bfloat16 else 4
+    conv.WGRAD_REUSE = not args.no_wgrad_reuse
     conv.weights.requires_grad_(True)
     conv.beta.requires_grad_(True)
     tb, ti = bev.clone().requires_grad_(True), img.clone().requires_grad_(True)

@@ -593,6 +593,19 @@ int shpl_conv3x3_wgrad(int dtype, int n_frames, int64_t h, int64_t w, const void
                        const shpl_csr *pool, const int64_t *d_frame_off, const void *d_gy, int64_t gy_stride,
                        int64_t c_out, float *d_dw, void *d_ws, size_t ws_bytes, void *stream);
 
+/* shpl_conv3x3_wgrad of the pooled bf16 form reading the pooled operand (the cell-keyed CSR's occupancy maps
+ * and per-run pooled rows) that a forward shpl_conv3x3 call over the same map, image, frames, shape and
+ * channels left in its workspace, instead of preparing it again (k_occ_frame + k_pool_runs): the training
+ * step's weight gradient after its forward. d_fwd_ws / fwd_ws_bytes: that call's workspace, not written since;
+ * fwd_stats: whether that call took statistics (its workspace layout). When that call's plan holds no such
+ * operand (not the row-streaming form) the weight gradient prepares its own. Same results as
+ * shpl_conv3x3_wgrad, bit for bit. */
+int shpl_conv3x3_wgrad_reuse(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a, int64_t a_stride,
+                             int64_t a_off, int64_t c_a, const void *d_b, int64_t b_stride, int64_t b_off,
+                             int64_t c_b, const shpl_csr *pool, const int64_t *d_frame_off, const void *d_gy,
+                             int64_t gy_stride, int64_t c_out, float *d_dw, void *d_ws, size_t ws_bytes,
+                             const void *d_fwd_ws, size_t fwd_ws_bytes, int fwd_stats, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -161,6 +161,8 @@ def _declare(lib):
         "shpl_conv3x3_wgrad_workspace_bytes": (i32, [i32, i32, i64, i64, i64, i64, i64, i64, psz]),
         "shpl_conv3x3_wgrad": (i32, [i32, i32, i64, i64, p, i64, i64, i64, p, i64, i64, i64,
                                      ctypes.POINTER(ShplCsr), p, p, i64, i64, p, p, sz, p]),
+        "shpl_conv3x3_wgrad_reuse": (i32, [i32, i32, i64, i64, p, i64, i64, i64, p, i64, i64, i64,
+                                           ctypes.POINTER(ShplCsr), p, p, i64, i64, p, p, sz, p, sz, i32, p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -2028,11 +2028,14 @@ extern "C" int shpl_conv3x3_wgrad_workspace_bytes(int dtype, int n_frames, int64
     return SHPL_OK;
 }
 
-extern "C" int shpl_conv3x3_wgrad(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a, int64_t a_stride,
-                                  int64_t a_off, int64_t c_a, const void *d_b, int64_t b_stride, int64_t b_off,
-                                  int64_t c_b, const shpl_csr *pool, const int64_t *d_frame_off, const void *d_gy,
-                                  int64_t gy_stride, int64_t c_out, float *d_dw, void *d_ws, size_t ws_bytes,
-                                  void *stream) {
+namespace {
+// shpl_conv3x3_wgrad; d_fwd_ws: the workspace of a pooled bf16 forward shpl_conv3x3 call over the same map
+// (shpl_conv3x3_wgrad_reuse) whose pooled operand the row-streaming form reads instead of preparing its own
+int wgrad_impl(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a, int64_t a_stride, int64_t a_off,
+               int64_t c_a, const void *d_b, int64_t b_stride, int64_t b_off, int64_t c_b, const shpl_csr *pool,
+               const int64_t *d_frame_off, const void *d_gy, int64_t gy_stride, int64_t c_out, float *d_dw,
+               void *d_ws, size_t ws_bytes, const void *d_fwd_ws, size_t fwd_ws_bytes, int fwd_stats,
+               void *stream) {
     const bool pooled = pool != nullptr;
     WgPlan wp;
     int rc = wgrad_plan(dtype, n_frames, h, w, c_a, c_b, c_out, pooled, &wp, pooled ? pool->nnz_cap : 0);
@@ -2086,10 +2089,24 @@ extern "C" int shpl_conv3x3_wgrad(int dtype, int n_frames, int64_t h, int64_t w,
             int32_t *occ_base = reinterpret_cast<int32_t *>(po + wp.r_occ_bytes / 2);
             uint16_t *cmp = reinterpret_cast<uint16_t *>(po + wp.r_occ_bytes);
             const int wpr = (int)((w + 31) / 32);
-            rc = rows::prep_pooled(n_frames, (int)h, (int)w, wpr, pool->ent_dst, pool->ent_src, pool->ent_val,
-                                   pool->nnz_cap, d_frame_off, reinterpret_cast<const uint16_t *>(d_b), b_stride,
-                                   b_off, (int)c_b, occ, occ_base, cmp, s);
-            if (rc) return rc;
+            // the forward call's occupancy maps and pooled runs, where its plan put them (when it has them)
+            ConvPlan fp;
+            const bool reuse = d_fwd_ws &&
+                               conv_plan(dtype, n_frames, h, w, c_a, c_b, c_out, true, fwd_stats != 0, &fp, 0,
+                                         pool->nnz_cap) == SHPL_OK &&
+                               fp.rows && fwd_ws_bytes >= fp.total && fp.wpr == wpr;
+            if (reuse) {
+                uint8_t *fo = reinterpret_cast<uint8_t *>(const_cast<void *>(d_fwd_ws)) + fp.wp_bytes + fp.rp_bytes +
+                              fp.part_bytes;
+                occ = reinterpret_cast<uint32_t *>(fo);
+                occ_base = reinterpret_cast<int32_t *>(fo + fp.occ_bytes / 2);
+                cmp = reinterpret_cast<uint16_t *>(fo + fp.occ_bytes);
+            } else {
+                rc = rows::prep_pooled(n_frames, (int)h, (int)w, wpr, pool->ent_dst, pool->ent_src, pool->ent_val,
+                                       pool->nnz_cap, d_frame_off, reinterpret_cast<const uint16_t *>(d_b), b_stride,
+                                       b_off, (int)c_b, occ, occ_base, cmp, s);
+                if (rc) return rc;
+            }
             r.b = nullptr;
             r.cmp = cmp;
             r.cmp_stride = (int)c_b;
@@ -2158,4 +2175,25 @@ extern "C" int shpl_conv3x3_wgrad(int dtype, int n_frames, int64_t h, int64_t w,
                        wp.n_groups, wp.n_cib, pl.n_cob, (int)c_a, (int)c_b, pl.qa, pl.ck, (int)c_out, d_dw);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
+}
+}  // namespace
+
+extern "C" int shpl_conv3x3_wgrad(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a, int64_t a_stride,
+                                  int64_t a_off, int64_t c_a, const void *d_b, int64_t b_stride, int64_t b_off,
+                                  int64_t c_b, const shpl_csr *pool, const int64_t *d_frame_off, const void *d_gy,
+                                  int64_t gy_stride, int64_t c_out, float *d_dw, void *d_ws, size_t ws_bytes,
+                                  void *stream) {
+    return wgrad_impl(dtype, n_frames, h, w, d_a, a_stride, a_off, c_a, d_b, b_stride, b_off, c_b, pool, d_frame_off,
+                      d_gy, gy_stride, c_out, d_dw, d_ws, ws_bytes, nullptr, 0, 0, stream);
+}
+
+extern "C" int shpl_conv3x3_wgrad_reuse(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a,
+                                        int64_t a_stride, int64_t a_off, int64_t c_a, const void *d_b,
+                                        int64_t b_stride, int64_t b_off, int64_t c_b, const shpl_csr *pool,
+                                        const int64_t *d_frame_off, const void *d_gy, int64_t gy_stride,
+                                        int64_t c_out, float *d_dw, void *d_ws, size_t ws_bytes,
+                                        const void *d_fwd_ws, size_t fwd_ws_bytes, int fwd_stats, void *stream) {
+    if (!pool || !d_fwd_ws || dtype != SHPL_BF16) return SHPL_ERR_ARG;
+    return wgrad_impl(dtype, n_frames, h, w, d_a, a_stride, a_off, c_a, d_b, b_stride, b_off, c_b, pool, d_frame_off,
+                      d_gy, gy_stride, c_out, d_dw, d_ws, ws_bytes, d_fwd_ws, fwd_ws_bytes, fwd_stats, stream);
 }

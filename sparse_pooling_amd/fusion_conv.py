@@ -146,9 +146,11 @@ def conv3x3_dgrad(gy, weights, c_dx, split=None):
     return dx if split is None else (dx, dx_b)
 
 
-def conv3x3_wgrad(a, gy, b=None, pool=None, frame_off=None):
+def conv3x3_wgrad(a, gy, b=None, pool=None, frame_off=None, fwd_ws=None, fwd_stats=False):
     """Weight gradient (f32 HWIO [3,3,Ca+Cb,Cout]) of the SAME 3x3 conv of
-    [a || b] (b dense, or the image map pooled through ``pool``)."""
+    [a || b] (b dense, or the image map pooled through ``pool``). fwd_ws (pooled bf16): the workspace of
+    the forward conv3x3 over the same inputs (taken with statistics: fwd_stats), whose pooled operand is
+    read instead of prepared again (shpl_conv3x3_wgrad_reuse)."""
     a = a.contiguous()
     gy = gy.contiguous()
     dt = L.dtype_code(a)
@@ -162,10 +164,13 @@ def conv3x3_wgrad(a, gy, b=None, pool=None, frame_off=None):
     L.check(L.lib().shpl_conv3x3_wgrad_workspace_bytes(dt, B, H, W, Ca, Cb, Cout, -1 if pool is None else pool.nnz_cap,
                                                        ctypes.byref(nb)), "shpl_conv3x3_wgrad_workspace_bytes")
     ws = L.workspace(nb.value, a.device)
-    L.check(L.lib().shpl_conv3x3_wgrad(dt, B, H, W, L.ptr(a), Ca, 0, Ca, L.ptr(b), Cb, 0, Cb,
-                                       None if pool is None else pool.ref(), L.ptr(frame_off), L.ptr(gy), Cout,
-                                       Cout, L.ptr(dw), L.ptr(ws), ws.numel(), L.stream_of(a.device)),
-            "shpl_conv3x3_wgrad")
+    args = (dt, B, H, W, L.ptr(a), Ca, 0, Ca, L.ptr(b), Cb, 0, Cb, None if pool is None else pool.ref(),
+            L.ptr(frame_off), L.ptr(gy), Cout, Cout, L.ptr(dw), L.ptr(ws), ws.numel())
+    if fwd_ws is not None:
+        L.check(L.lib().shpl_conv3x3_wgrad_reuse(*args, L.ptr(fwd_ws), fwd_ws.numel(), int(bool(fwd_stats)),
+                                                 L.stream_of(a.device)), "shpl_conv3x3_wgrad_reuse")
+    else:
+        L.check(L.lib().shpl_conv3x3_wgrad(*args, L.stream_of(a.device)), "shpl_conv3x3_wgrad")
     return dw
 
 
@@ -193,7 +198,12 @@ class _FusionConvFn(torch.autograd.Function):
             xb = sm.pool_img_to_bev(smap, b, (B, H, W, Cb))
             b, pool, frame_off = xb, None, None
         cap = pool.nnz_cap if pool is not None else None
-        ws = conv._ws_for((dt, B, H, W, Cb, cap, train_bn), conv_ws_bytes(dt, B, H, W, Ca, Cb, conv.c_out, cap, train_bn))
+        # bf16 pooled with a weight gradient to come: a workspace of this call's own, kept for the backward,
+        # whose weight gradient reads the pooled operand the forward prepared in it (shpl_conv3x3_wgrad_reuse)
+        reuse = pooled and conv.WGRAD_REUSE and a.dtype == torch.bfloat16 and ctx.needs_input_grad[2]
+        nbytes = conv_ws_bytes(dt, B, H, W, Ca, Cb, conv.c_out, cap, train_bn)
+        ws = L.workspace(nbytes, a.device) if reuse else conv._ws_for((dt, B, H, W, Cb, cap, train_bn), nbytes)
+        ctx.fwd_ws = ws if reuse else None
         raw, mean, scale = None, None, None
         if not train_bn:
             center, scale, shift = conv._inference_epilogue()
@@ -250,7 +260,8 @@ class _FusionConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[2]:
             if pooled and a.dtype == torch.bfloat16:
                 # k_wgrad_rows gathers the pooled rows from a compact per-run buffer: bv_fused never stored
-                dw = conv3x3_wgrad(a, g_raw, b=b, pool=smap.csr(L.BY_CELL, L.ORDER_ENTRY), frame_off=smap.frame_off)
+                dw = conv3x3_wgrad(a, g_raw, b=b, pool=smap.csr(L.BY_CELL, L.ORDER_ENTRY), frame_off=smap.frame_off,
+                                   fwd_ws=ctx.fwd_ws, fwd_stats=ctx.train_bn)
             elif pooled:
                 # f32: the pooled channels once into HBM (shpl_pull): the dense two-source weight gradient
                 # runs at twice the waves per SIMD of the one that recomputes them per tile (257 vs
@@ -268,6 +279,9 @@ class _FusionConvFn(torch.autograd.Function):
 class FusionConv:
     """slim.conv2d(x, c_out, [3,3]) with slim.batch_norm (or a bias) and ReLU:
     the variables of one ``pyramid_fusion_pooled_*`` scope and its forward."""
+
+    # bf16 fused(): the weight gradient reads the pooled operand its forward prepared (False: prepares its own)
+    WGRAD_REUSE = True
 
     def __init__(self, c_in, c_out, batch_norm=True, bias=False, relu=True, eps=1e-3, decay=0.999,
                  dtype=torch.float32, device="cuda", seed=0):

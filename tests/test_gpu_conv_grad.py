@@ -316,3 +316,35 @@ def test_fused_conv_autograd_vs_oracle(train):
     _, ab_w = None, orc.conv3x3_wgrad(np.abs(eb), gr_mag.astype(np.float32))
     _check(conv.weights.grad, d_w, TOL + 2e-5 * ab_w, "d_w")
     _check(conv.beta.grad, e_db, 1e-4 + 1e-6 * np.abs(g).reshape(-1, Ci).sum(0), "d_beta")
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_fused_bf16_wgrad_reuses_forward_operand(train):
+    """bf16 FusionConv.fused: the weight gradient reading the forward's pooled operand
+    (shpl_conv3x3_wgrad_reuse, WGRAD_REUSE) gives bitwise the gradients of the one that prepares its own.
+    Config 1's geometry with 32 + 32 channels: the row-streaming forward and weight gradient."""
+    from sparse_pooling_amd import fusion_conv as fc, shpl_map as sm
+    spec = synth.FrameSpec(2000, (1200, 360), (704, 800), (4, 4), 32, 32)
+    fr = synth.make_frame(spec, seed=907, n_outside=10)
+    gen = orc.gen_sparse_pooling_input_avod(fr.points, fr.voxel_indices, fr.P, list(spec.im_size),
+                                            tuple(spec.bv_size))
+    ref = orc.produce_sparse_pooling_input(gen, stride=spec.stride)
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    Cb, Ci = spec.c_bev, spec.c_img
+    bev = _t(synth.make_features((1, Hb, Wb, Cb), 31)).to(torch.bfloat16)
+    img = _t(synth.make_features((1, Hi, Wi, Ci), 32)).to(torch.bfloat16)
+    g = _t(np.random.default_rng(33).standard_normal((1, Hb, Wb, Ci)).astype(np.float32)).to(torch.bfloat16)
+    grads = []
+    for reuse in (False, True):
+        smap = sm.pack_map(_t(ref["Mij_pool"]), _t(ref["M_val"].astype(np.float32)), ref["M_size"],
+                           _t(ref["img_index_flip_pool"]), img.shape)
+        conv = fc.FusionConv(Cb + Ci, Ci, dtype=torch.bfloat16, device=DEV, seed=4)
+        conv.WGRAD_REUSE = reuse
+        conv.weights.requires_grad_(True)
+        conv.beta.requires_grad_(True)
+        tb, ti = bev.clone().requires_grad_(True), img.clone().requires_grad_(True)
+        conv.fused(tb, ti, smap, is_training=train).backward(g)
+        grads.append([x.grad.clone() for x in (tb, ti, conv.weights, conv.beta)])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
