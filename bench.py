@@ -855,10 +855,14 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
     Hi, Wi = spec.img_feat_hw
     px = F * Hb * Wb * esz
     if esz == 2:  # bf16: both convs gather the pooled rows (compact per-run buffer), bv_fused is never stored
-        # per pixel, in channels: forward (cb + ci) read + ci written, BN apply 2 ci, BN backward 5 ci, input
-        # gradient ci read + (cb + ci) written, weight gradient (cb + ci) + ci read
-        hbm_bytes = (px * (((cb + ci) + ci) + 2 * ci + 5 * ci + (ci + (cb + ci)) + ((cb + ci) + ci))
-                     + F * Hi * Wi * ci * esz + (2 * u_pix + u_cell) * ci * esz + 3 * 12 * nnz)
+        # per pixel, in channels: forward cb read (the pooled half is gathered: u_pix rows below) + ci written,
+        # BN apply 2 ci, BN backward 5 ci, input gradient ci read + (cb + ci) written, weight gradient cb + ci
+        # read (its pooled half again gathered); the image gradient's ci per image pixel written; the pooled
+        # rows' gathers (once per step with the weight gradient reading the forward's operand, else twice) and
+        # the image gradient's gathers of u_cell rows; the entries read by each of those passes
+        n_pool = 1 if conv.WGRAD_REUSE else 2
+        hbm_bytes = (px * ((cb + ci) + 2 * ci + 5 * ci + (ci + (cb + ci)) + (cb + ci))
+                     + F * Hi * Wi * ci * esz + (n_pool * u_pix + u_cell) * ci * esz + (n_pool + 1) * 12 * nnz)
     else:  # f32: the pooled map written once in the forward, read by the forward and the weight gradient
         hbm_bytes = (px * (ci + (cb + ci + ci) + 2 * ci + 2 * ci + 3 * ci + (ci + cb + ci) + (cb + ci + ci))
                      + F * Hi * Wi * ci * esz + (u_pix + u_cell) * ci * esz + 2 * 12 * nnz)
