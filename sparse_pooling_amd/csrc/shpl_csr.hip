@@ -53,6 +53,9 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_pack(int64_t nnz, const int64_t 
 // ------------------------------------------------------------------ CSR
 constexpr int CSR_BLOCK = 1024;           // one workgroup per frame
 constexpr int CSR_TILES = 16384;          // LDS tile counters (64 KiB)
+#ifndef SHPL_CSR_PROBE
+#define SHPL_CSR_PROBE 0  // timing probes of k_csr_frame (wrong results): 1 return after the scan, 2 after placement
+#endif
 
 struct CsrIn {
     int direction, order, n_frames;
@@ -334,6 +337,7 @@ __global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, uint64_t *tmp,
     // 2. exclusive scan
     tile_scan<CSR_TILES>(cnt, wsum);
     __syncthreads();
+    if (SHPL_CSR_PROBE == 1) return;
     // 3. placement of (destination << 32 | entry): cnt[t] advances from start(t) to end(t) = start(t+1)
     for (int64_t b = e0 + threadIdx.x; b < e1; b += (int64_t)CSR_BLOCK * CSR_BATCH) {
         int32_t key[CSR_BATCH];
@@ -347,6 +351,7 @@ __global__ __launch_bounds__(CSR_BLOCK) void k_csr_frame(CsrIn c, uint64_t *tmp,
         }
     }
     block_publish();  // tmp was written by other waves of this workgroup through memory
+    if (SHPL_CSR_PROBE == 2) return;
     const int32_t n_valid = cnt[n_tiles - 1];
     // 4. rank fix-up
     emit_sorted<HAS_COL, CSR_WIN>(c, tmp + e0, n_valid, e0, kbase, c.log_tile, cnt, win, ent_dst, ent_src, ent_val, ent_col);
