@@ -238,10 +238,11 @@ def cpu_baseline(spec, frames_np, budget_s, dual, backward=False, impl="c"):
 
 
 def cpu_baselines(spec, frames_np, budget_s, dual, backward, parallel):
-    """SURVEY §8d's CPU baseline: the C port of the reference path (the headline `value`,
-    "kind": "port": the faster of the two single-core legs), the numpy restatement beside
-    it ("kind": "numpy": the reference's own numpy index builder and TF-order np.add.at
-    pooling), and the C port frame-parallel over the usable cores."""
+    """SURVEY §8d's CPU baseline: the C port of the reference path is the headline `value`
+    ("kind": "port", since round 4; rounds 1-3 quoted the numpy leg), the numpy restatement
+    beside it ("numpy": "kind": "numpy", the reference's own numpy index builder and TF-order
+    np.add.at pooling), and the C port frame-parallel over the usable cores. Compare rounds by
+    `kind`: the port leg is the faster one on every workload measured."""
     npy = cpu_baseline(spec, frames_np, budget_s, dual, backward, impl="numpy")
     port = cpu_baseline(spec, frames_np, budget_s, dual, backward, impl="c")
     out = dict(port, numpy=npy, port=dict(port))
@@ -336,9 +337,24 @@ def checksum_report(base, local, fids, dev, rank, args):
         with open(CHECKSUM_FILE, "w") as fh:
             json.dump(tab, fh, indent=0)
     return {"key": base, "frames": len(allcs), "frame_ids": [min(allfids), max(allfids)] if allfids else None,
-            "compared_with": ref_key,
+            "compared_with": ref_key, "pinned_to": pinned_to(ref_key), "checksum": CHECKSUM_DEF,
             "digest": hashlib.sha256(json.dumps(allcs).encode()).hexdigest()[:16],
             "match_n1": match, "first": allcs[:4]}
+
+
+CHECKSUM_DEF = "sum_i bits[i]*(2i+1) mod 2^64 per output (row-major), outputs combined as sum_k cs_k*(2k+1)"
+
+
+def pinned_to(key):
+    """What a stored table was computed by: the layer and raw-scan tables by the CPU oracle
+    (tests/golden/make_checksum_tables.py; TF-order arithmetic, so bitwise); the conv tables by a GPU run
+    (TF's Conv2D fixes no summation order, so no oracle checksum exists: the conv is tolerance-tested against
+    the oracle's double-precision conv in tests/test_gpu_conv.py) -- self-referential."""
+    if key is None:
+        return None
+    if key.startswith("layer_config") or key.startswith("frames_"):
+        return "oracle"
+    return "gpu-run (self-referential; parity by tolerance tests, tests/test_gpu_conv.py)"
 
 
 def lib_sha256():
@@ -508,7 +524,8 @@ def main():
         elapsed = sd.timed(lambda k: step(evs[k]), args.steps, device=dev, info=tinfo)
     args_steps_ev = n_ev
     outs = [pl.bv_fused] + ([pl.img_fused] if dual else []) + ([d_bev, d_img] if backward else [])
-    checks = checksum_report(f"layer_config{cfg}", sum(sd.frame_checksums(t) for t in outs), fids, dev, rank, args)
+    checks = checksum_report(f"layer_config{cfg}", sd.combine_checksums([sd.frame_checksums(t) for t in outs]), fids,
+                             dev, rank, args)
     comm = sd.comm_report(dev)
     nbytes = step_bytes(cfg, spec, nnz, u_pix, u_cell, F, esz)
     interleaved = dual and not args.no_overlap and not pl.rows and pl.interleave

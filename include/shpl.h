@@ -287,9 +287,10 @@ typedef struct {
     int32_t *ent_src;  /* [nnz_cap] source row of each sorted entry                        */
     float *ent_val;    /* [nnz_cap] M value of each sorted entry                           */
     int32_t *ent_col;  /* [nnz_cap] column k of each sorted entry (SHPL_BY_PIXEL; else NULL). A pixel-keyed
-                          CSR of shpl_build_csr_buckets may leave it NULL: every entry of the index builder's
-                          maps is a column of its own, and the pulls then sum without per-column partials
-                          (bitwise the same: each partial is one product) */
+                          CSR of shpl_build_csr_buckets may leave it NULL, marked SHPL_CSR_IDENTITY_COLS in
+                          flags: every entry of the index builder's maps is a column of its own, and the pulls
+                          then sum without per-column partials (bitwise the same: each partial is one product).
+                          Any other pixel-keyed CSR without ent_col is SHPL_ERR_ARG for the pulls */
     int64_t n_keys;    /* destination rows (all frames)                                      */
     int64_t nnz_cap;   /* capacity of the entry arrays                                       */
     int32_t *key_range; /* optional [n_keys][2]: (first, end) sorted entry of each destination's
@@ -303,8 +304,11 @@ typedef struct {
     const int64_t *frame_off; /* [n_frames + 1] */
     const int64_t *frame_nnz; /* [n_frames]     */
     int64_t n_frames;
+    int64_t flags;     /* SHPL_CSR_IDENTITY_COLS: a pixel-keyed CSR whose every entry is a column of its own
+                          (built by shpl_build_csr_buckets), so ent_col may be NULL; 0 otherwise */
 } shpl_csr;
 #define SHPL_LIVE_MAX_FRAMES 1024
+#define SHPL_CSR_IDENTITY_COLS 1
 
 /* Sort the entries of every frame by destination (cell for SHPL_BY_CELL,
  * pix[col] for SHPL_BY_PIXEL) keeping `order` among equal destinations, and
@@ -532,6 +536,15 @@ int shpl_conv3x3(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a,
                  int act, void *d_out, int64_t out_stride, double *d_stats, void *d_ws,
                  size_t ws_bytes, void *stream);
 
+/* Whether shpl_conv3x3 with these arguments (d_ws / ws_bytes / d_center / d_scale / d_shift / stream aside;
+ * stats = d_stats != NULL) runs the row-streaming form (*rows_form = 1), whose pooled call leaves the
+ * occupancy maps and per-run pooled rows in its workspace that shpl_conv3x3_wgrad_reuse reads; 0 for the
+ * tiled form, f32, or no pixel. The same predicate shpl_conv3x3 decides by. */
+int shpl_conv3x3_rows_form(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a, int64_t a_stride,
+                           int64_t a_off, int64_t c_a, const void *d_b, int64_t b_stride, int64_t b_off, int64_t c_b,
+                           const shpl_csr *pool, const int64_t *d_frame_off, const void *d_weights, int64_t c_out,
+                           int act, const void *d_out, int64_t out_stride, int stats, int *rows_form);
+
 /* BatchNorm in training mode over rows x c, from d_stats of shpl_conv3x3 and
  * count = rows: mean = sum/count, var = sumsq/count - mean^2,
  * y = act((x - mean) * gamma / sqrt(var + eps) + beta), written to d_y
@@ -597,8 +610,10 @@ int shpl_conv3x3_wgrad(int dtype, int n_frames, int64_t h, int64_t w, const void
  * and per-run pooled rows) that a forward shpl_conv3x3 call over the same map, image, frames, shape and
  * channels left in its workspace, instead of preparing it again (k_occ_frame + k_pool_runs): the training
  * step's weight gradient after its forward. d_fwd_ws / fwd_ws_bytes: that call's workspace, not written since;
- * fwd_stats: whether that call took statistics (its workspace layout). When that call's plan holds no such
- * operand (not the row-streaming form) the weight gradient prepares its own. Same results as
+ * fwd_stats: whether that call took statistics (its workspace layout). Valid only for a forward call for which
+ * shpl_conv3x3_rows_form reported 1 (the caller's to establish: the forward's act and output pointer are not
+ * arguments here); what this call can check of that predicate and finds false is SHPL_ERR_ARG. When the
+ * weight gradient itself does not run the row-streaming form the workspace is not read. Same results as
  * shpl_conv3x3_wgrad, bit for bit. */
 int shpl_conv3x3_wgrad_reuse(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a, int64_t a_stride,
                              int64_t a_off, int64_t c_a, const void *d_b, int64_t b_stride, int64_t b_off,

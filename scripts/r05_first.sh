@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round 5, first GPU pass: the conv tables rewritten under the position-weighted checksum and the hash
+# features (a GPU run: no oracle checksum exists for the conv), then the oracle-pinned tables against the
+# bench, the whole GPU suite, smoke, and the headline bench line.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for dt in bf16 f32; do
+  timeout -k 10 300 python bench.py --workload conv --dtype $dt --steps 2 --warmup 1 --no-cpu-baseline --write-checksums \
+    > gpurun_out/r05_conv_table_$dt.log 2>&1 || { tail -5 gpurun_out/r05_conv_table_$dt.log; exit 1; }
+done
+cp profiles/frame_checksums.json gpurun_out/frame_checksums.json
+timeout -k 10 900 python -u -m pytest tests/test_gpu_checksums_oracle.py tests/test_gpu_conv_grad.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r05_checksums_oracle.log 2>&1
+rc=$?; echo "checksum tests rc=$rc"; tail -3 gpurun_out/r05_checksums_oracle.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r05_checksums_oracle.log | head -20; exit $rc; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r05_gpu_tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_gpu_tests.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/r05_gpu_tests.log | head; exit $rc; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('__SMOKE_OK__')" > gpurun_out/r05_smoke.log 2>&1 || exit 1
+tail -1 gpurun_out/r05_smoke.log
+timeout -k 10 400 python bench.py > gpurun_out/r05_bench_default.log 2>&1 || { tail -5 gpurun_out/r05_bench_default.log; exit 1; }
+grep '^{' gpurun_out/r05_bench_default.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print(d['value'], d['ms_per_step'], r['frac'], d['frame_checksums'])"
+echo done

@@ -23,6 +23,7 @@ ORDER_ENTRY, ORDER_COL_ROW, ORDER_COL_ENTRY = 0, 1, 2
 OUT_POOL, OUT_CONCAT, OUT_ADD = 0, 1, 2
 ACT_NONE, ACT_RELU = 0, 1
 CSR_AUTO, CSR_FRAME, CSR_SEGMENT, CSR_RANGE = 0, 1, 2, 3
+CSR_IDENTITY_COLS = 1
 
 _lib = None
 
@@ -39,15 +40,17 @@ class ShplCsr(ctypes.Structure):
     _fields_ = [("ent_dst", ctypes.c_void_p), ("ent_src", ctypes.c_void_p),
                 ("ent_val", ctypes.c_void_p), ("ent_col", ctypes.c_void_p),
                 ("n_keys", ctypes.c_int64), ("nnz_cap", ctypes.c_int64), ("key_range", ctypes.c_void_p),
-                ("frame_off", ctypes.c_void_p), ("frame_nnz", ctypes.c_void_p), ("n_frames", ctypes.c_int64)]
+                ("frame_off", ctypes.c_void_p), ("frame_nnz", ctypes.c_void_p), ("n_frames", ctypes.c_int64),
+                ("flags", ctypes.c_int64)]
 
 
 class Csr:
     """Device buffers of one destination-sorted entry list (owned tensors + the ABI struct)."""
 
-    def __init__(self, n_keys, nnz_cap, device, with_col, key_range=False):
+    def __init__(self, n_keys, nnz_cap, device, with_col, key_range=False, identity_cols=False):
         """key_range: also keep the (first, end) entry of every destination
-        (shpl_csr.key_range): shpl_pull then runs its one-launch row-keyed form."""
+        (shpl_csr.key_range): shpl_pull then runs its one-launch row-keyed form.
+        identity_cols: a pixel-keyed CSR of shpl_build_csr_buckets without ent_col (SHPL_CSR_IDENTITY_COLS)."""
         i32 = dict(dtype=torch.int32, device=device)
         cap = max(int(nnz_cap), 1)
         self.n_keys, self.nnz_cap = int(n_keys), int(nnz_cap)
@@ -60,6 +63,7 @@ class Csr:
         self.struct = ShplCsr(self.ent_dst.data_ptr(), self.ent_src.data_ptr(), self.ent_val.data_ptr(),
                               self.ent_col.data_ptr() if with_col else None, self.n_keys, self.nnz_cap,
                               self.key_range.data_ptr() if key_range else None)
+        self.struct.flags = CSR_IDENTITY_COLS if identity_cols else 0
 
     def live_frames(self, frame_off, frame_nnz):
         """Hand the sparse pass the frame layout the CSR was built with (device i64 [F+1] / [F],
@@ -153,6 +157,9 @@ def _declare(lib):
         "shpl_conv3x3_workspace_bytes": (i32, [i32, i32, i64, i64, i64, i64, i64, i64, i32, psz]),
         "shpl_conv3x3": (i32, [i32, i32, i64, i64, p, i64, i64, i64, p, i64, i64, i64,
                                ctypes.POINTER(ShplCsr), p, p, i64, p, p, p, i32, p, i64, p, p, sz, p]),
+        "shpl_conv3x3_rows_form": (i32, [i32, i32, i64, i64, p, i64, i64, i64, p, i64, i64, i64,
+                                         ctypes.POINTER(ShplCsr), p, p, i64, i32, p, i64, i32,
+                                         ctypes.POINTER(ctypes.c_int)]),
         "shpl_batch_norm": (i32, [i32, i64, p, p, i64, i64, p, d, ctypes.c_float, p, p, i32, p, p,
                                   ctypes.c_float, p, p, p, p]),
         "shpl_batch_norm_backward_workspace_bytes": (i32, [i64, i64, psz]),

@@ -1674,6 +1674,15 @@ int conv_rows_launch(const ConvPlan &pl, const ConvArgs &a, bool pooled, bool st
     return SHPL_OK;
 }
 
+// Whether a bf16 call with this plan and these arguments runs the row-streaming form (k_conv_rows, and pooled
+// its prep: the occupancy maps and per-run pooled rows in the workspace). The one predicate conv_launch and
+// shpl_conv3x3_rows_form (which the weight gradient's reuse of the forward's workspace hangs on) share.
+bool rows_forward(const ConvPlan &pl, const ConvArgs &a, bool pooled, bool stats) {
+    return pl.rows && a.vec_a && (a.c_b == 0 || a.vec_b) && (!a.out2 || a.c_split % NCO == 0) && a.vec_out &&
+           a.c_out % NCO == 0 && a.n_frames > 0 &&
+           (!stats || (a.act == 0 && rows::supported_st(pl.qa + pl.qb, pl.qa, pooled)));
+}
+
 template <typename T>
 int conv_launch(const ConvPlan &pl, ConvArgs &a, bool pooled, bool stats, const void *w, const int64_t *frame_off,
                 double *d_stats, hipStream_t s, int transpose = 0) {
@@ -1685,10 +1694,7 @@ int conv_launch(const ConvPlan &pl, ConvArgs &a, bool pooled, bool stats, const 
     if constexpr (sizeof(T) == 2) {
         // bf16 with at most 64 input channels: the row-streaming kernel (k_conv_rows), also for the input
         // gradient's two maps (split at a whole output block) and the training forward's statistics
-        if (pl.rows && a.vec_a && (a.c_b == 0 || a.vec_b) && (!a.out2 || a.c_split % NCO == 0) && a.vec_out &&
-            a.c_out % NCO == 0 && a.n_frames > 0 &&
-            (!stats || (a.act == 0 && rows::supported_st(pl.qa + pl.qb, pl.qa, pooled))))
-            return conv_rows_launch(pl, a, pooled, stats, frame_off, d_stats, s);
+        if (rows_forward(pl, a, pooled, stats)) return conv_rows_launch(pl, a, pooled, stats, frame_off, d_stats, s);
     }
     if (pooled) {
         hipLaunchKernelGGL(k_row_ptr, dim3(16, a.n_frames), dim3(SHPL_BLOCK), 0, s, a.ent_dst, frame_off, a.h, a.w,
@@ -1740,19 +1746,21 @@ extern "C" int shpl_conv3x3_workspace_bytes(int dtype, int n_frames, int64_t h, 
     return SHPL_OK;
 }
 
-extern "C" int shpl_conv3x3(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a, int64_t a_stride,
-                            int64_t a_off, int64_t c_a, const void *d_b, int64_t b_stride, int64_t b_off,
-                            int64_t c_b, const shpl_csr *pool, const int64_t *d_frame_off, const void *d_weights,
-                            int64_t c_out, const float *d_center, const float *d_scale, const float *d_shift,
-                            int act, void *d_out, int64_t out_stride, double *d_stats, void *d_ws, size_t ws_bytes,
-                            void *stream) {
-    const bool pooled = pool != nullptr, stats = d_stats != nullptr;
-    ConvPlan pl;
+namespace shpl {
+namespace {
+// shpl_conv3x3's argument checks and kernel arguments (shared with shpl_conv3x3_rows_form). *empty: no pixel.
+int forward_setup(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a, int64_t a_stride, int64_t a_off,
+                  int64_t c_a, const void *d_b, int64_t b_stride, int64_t b_off, int64_t c_b, const shpl_csr *pool,
+                  const int64_t *d_frame_off, const void *d_weights, int64_t c_out, const float *d_center,
+                  const float *d_scale, const float *d_shift, int act, void *d_out, int64_t out_stride,
+                  bool stats, void *d_ws, size_t ws_bytes, bool check_ws, ConvPlan &pl, ConvArgs &a, bool *empty) {
+    const bool pooled = pool != nullptr;
+    *empty = false;
     int rc = conv_plan(dtype, n_frames, h, w, c_a, c_b, c_out, pooled, stats, &pl, 0, pooled ? pool->nnz_cap : 0);
     if (rc) return rc;
     if (act != 0 && act != 1) return SHPL_ERR_ARG;
-    if (!d_weights || (ws_bytes > 0 && !d_ws)) return SHPL_ERR_ARG;
-    if (ws_bytes < pl.total) return SHPL_ERR_WORKSPACE;
+    if (!d_weights || (check_ws && ws_bytes > 0 && !d_ws)) return SHPL_ERR_ARG;
+    if (check_ws && ws_bytes < pl.total) return SHPL_ERR_WORKSPACE;
     if (a_stride < a_off + c_a || out_stride < c_out || a_off < 0 || b_off < 0) return SHPL_ERR_BAD_SHAPE;
     if (c_b > 0 && b_stride < b_off + c_b) return SHPL_ERR_BAD_SHAPE;
     if (pooled) {
@@ -1762,10 +1770,13 @@ extern "C" int shpl_conv3x3(int dtype, int n_frames, int64_t h, int64_t w, const
     } else if (c_b > 0 && !d_b) {
         return SHPL_ERR_ARG;
     }
-    if (pl.n_tiles == 0) return SHPL_OK;
+    if (pl.n_tiles == 0) {
+        *empty = true;
+        return SHPL_OK;
+    }
     if (!d_out || (c_a > 0 && !d_a)) return SHPL_ERR_ARG;
     const int esz = dtype == SHPL_F32 ? 4 : 2, he = 16 / esz;
-    ConvArgs a = {};  // every field the forward does not set (out2: the dgrad split) is zero
+    a = ConvArgs{};  // every field the forward does not set (out2: the dgrad split) is zero
     a.n_frames = n_frames;
     a.h = (int)h;
     a.w = (int)w;
@@ -1789,8 +1800,8 @@ extern "C" int shpl_conv3x3(int dtype, int n_frames, int64_t h, int64_t w, const
     a.ent_val = pooled ? pool->ent_val : nullptr;
     uint8_t *ws = reinterpret_cast<uint8_t *>(d_ws);
     a.wp = ws;
-    a.row_ptr = pooled ? reinterpret_cast<const int32_t *>(ws + pl.wp_bytes) : nullptr;
-    a.part = stats ? reinterpret_cast<double *>(ws + pl.wp_bytes + pl.rp_bytes) : nullptr;
+    a.row_ptr = pooled && ws ? reinterpret_cast<const int32_t *>(ws + pl.wp_bytes) : nullptr;
+    a.part = stats && ws ? reinterpret_cast<double *>(ws + pl.wp_bytes + pl.rp_bytes) : nullptr;
     a.center = d_center;
     a.scale = d_scale;
     a.shift = d_shift;
@@ -1799,9 +1810,46 @@ extern "C" int shpl_conv3x3(int dtype, int n_frames, int64_t h, int64_t w, const
     a.out_stride = out_stride;
     a.c_out = (int)c_out;
     a.vec_out = aligned16(d_out) && out_stride % he == 0;
+    return SHPL_OK;
+}
+}  // namespace
+}  // namespace shpl
+
+extern "C" int shpl_conv3x3(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a, int64_t a_stride,
+                            int64_t a_off, int64_t c_a, const void *d_b, int64_t b_stride, int64_t b_off,
+                            int64_t c_b, const shpl_csr *pool, const int64_t *d_frame_off, const void *d_weights,
+                            int64_t c_out, const float *d_center, const float *d_scale, const float *d_shift,
+                            int act, void *d_out, int64_t out_stride, double *d_stats, void *d_ws, size_t ws_bytes,
+                            void *stream) {
+    const bool pooled = pool != nullptr, stats = d_stats != nullptr;
+    ConvPlan pl;
+    ConvArgs a;
+    bool empty;
+    const int rc = forward_setup(dtype, n_frames, h, w, d_a, a_stride, a_off, c_a, d_b, b_stride, b_off, c_b, pool,
+                                 d_frame_off, d_weights, c_out, d_center, d_scale, d_shift, act, d_out, out_stride,
+                                 stats, d_ws, ws_bytes, true, pl, a, &empty);
+    if (rc || empty) return rc;
     hipStream_t s = (hipStream_t)stream;
     if (dtype == SHPL_F32) return conv_launch<float>(pl, a, pooled, stats, d_weights, d_frame_off, d_stats, s);
     return conv_launch<uint16_t>(pl, a, pooled, stats, d_weights, d_frame_off, d_stats, s);
+}
+
+extern "C" int shpl_conv3x3_rows_form(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a,
+                                      int64_t a_stride, int64_t a_off, int64_t c_a, const void *d_b, int64_t b_stride,
+                                      int64_t b_off, int64_t c_b, const shpl_csr *pool, const int64_t *d_frame_off,
+                                      const void *d_weights, int64_t c_out, int act, const void *d_out,
+                                      int64_t out_stride, int stats, int *rows_form) {
+    if (!rows_form) return SHPL_ERR_ARG;
+    *rows_form = 0;
+    ConvPlan pl;
+    ConvArgs a;
+    bool empty;
+    const int rc = forward_setup(dtype, n_frames, h, w, d_a, a_stride, a_off, c_a, d_b, b_stride, b_off, c_b, pool,
+                                 d_frame_off, d_weights, c_out, nullptr, nullptr, nullptr, act,
+                                 const_cast<void *>(d_out), out_stride, stats != 0, nullptr, 0, false, pl, a, &empty);
+    if (rc) return rc;
+    *rows_form = !empty && dtype == SHPL_BF16 && rows_forward(pl, a, pool != nullptr, stats != 0);
+    return SHPL_OK;
 }
 
 extern "C" int shpl_batch_norm(int dtype, int64_t rows, void *d_x, void *d_y, int64_t stride, int64_t c,
@@ -2094,7 +2142,11 @@ int wgrad_impl(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a, i
             const bool reuse = d_fwd_ws &&
                                conv_plan(dtype, n_frames, h, w, c_a, c_b, c_out, true, fwd_stats != 0, &fp, 0,
                                          pool->nnz_cap) == SHPL_OK &&
-                               fp.rows && fwd_ws_bytes >= fp.total && fp.wpr == wpr;
+                               fp.rows && fwd_ws_bytes >= fp.total && fp.wpr == wpr && c_out % NCO == 0 &&
+                               (fwd_stats == 0 || rows::supported_st(fp.qa + fp.qb, fp.qa, true));
+            // the rest of rows_forward (the forward's act and output alignment) is the caller's to establish
+            // with shpl_conv3x3_rows_form (shpl.h); what is checkable here and fails is an error, not a fallback
+            if (d_fwd_ws && !reuse) return SHPL_ERR_ARG;
             if (reuse) {
                 uint8_t *fo = reinterpret_cast<uint8_t *>(const_cast<void *>(d_fwd_ws)) + fp.wp_bytes + fp.rp_bytes +
                               fp.part_bytes;

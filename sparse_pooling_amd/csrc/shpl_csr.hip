@@ -1206,6 +1206,7 @@ extern "C" int shpl_build_csr_buckets(const shpl_buckets *bk, const shpl_csr *by
         if (c->n_keys < (int64_t)bk->n_frames * l.kpf[k] || c->n_keys >= 2147483647LL || c->nnz_cap < bk->nnz_cap)
             return SHPL_ERR_BAD_SHAPE;
         if (bk->nnz_cap > 0 && (!c->ent_dst || !c->ent_src || !c->ent_val)) return SHPL_ERR_ARG;
+        if (k == 1 && !c->ent_col && !(c->flags & SHPL_CSR_IDENTITY_COLS)) return SHPL_ERR_ARG;
         s[k] = BsSide{l.nr[k], l.kpf[k], c->n_keys, c->nnz_cap, c->ent_dst, c->ent_src, c->ent_val, c->ent_col,
                       c->key_range, (int64_t)bk->n_frames * l.nr[k]};
         if (l.nr[k] == 0) s[k].blocks = 0;

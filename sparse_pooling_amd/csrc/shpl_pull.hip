@@ -693,6 +693,9 @@ int plan(int direction, int dtype, const shpl_csr *csr, const void *d_src, int64
     if (n_dst < 0 || n_dst >= 2147483647LL || c_pool < 0 || c_pass < 0) return SHPL_ERR_BAD_SHAPE;
     if (n_dst > 0 && (!d_out || (c_pool > 0 && !d_src))) return SHPL_ERR_ARG;
     if (csr->nnz_cap > 0 && (!csr->ent_dst || !csr->ent_src || !csr->ent_val)) return SHPL_ERR_ARG;
+    // a pixel-keyed CSR sums per-column partials (TF's Q[k]) unless it is marked as one column per entry
+    if (direction == SHPL_BY_PIXEL && csr->nnz_cap > 0 && !csr->ent_col && !(csr->flags & SHPL_CSR_IDENTITY_COLS))
+        return SHPL_ERR_ARG;
     if (mode != SHPL_OUT_POOL && !d_pass) return SHPL_ERR_ARG;
     if (mode == SHPL_OUT_ADD && c_pass != c_pool) return SHPL_ERR_BAD_SHAPE;
     const int64_t width = mode == SHPL_OUT_CONCAT ? c_pass + c_pool : c_pool;

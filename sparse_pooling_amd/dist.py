@@ -21,6 +21,7 @@ frame), which must equal the N=1 run's.
 import os
 import time
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -50,29 +51,114 @@ def frame_seeds(rank, frames_per_rank):
     return partition(frames_per_rank, rank + 1, rank, "weak")
 
 
+MASK32 = 0xFFFFFFFF
+
+
+def _frame_key(seed_base, fid):
+    """The 32-bit stream key of one frame's features: (seed_base, global frame id)."""
+    return ((int(seed_base) * 1_000_003 + int(fid)) * 0x9E3779B9 + 0x632BE5AB) & MASK32
+
+
+def _mix32(x, mask):
+    """A 32-bit integer mix (xorshift-multiply rounds, multipliers below 2^31 so every product of a 32-bit
+    value fits a signed 64-bit lane): identical on torch int64 (any device) and numpy uint64."""
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & mask
+    x = x ^ (x >> 15)
+    x = (x * 0x2C1B3C6D) & mask
+    x = x ^ (x >> 13)
+    x = (x * 0x297A2D39) & mask
+    return x ^ (x >> 16)
+
+
+def feature_values_np(shape, fid, seed_base):
+    """One frame's features on the host, bit for bit fill_features' (the oracle side of the checksum tables):
+    element i (flat, row-major) = (mix32(i + key) >> 8) * 2^-23 - 1, uniform on [-1, 1) in steps of 2^-23 --
+    integer arithmetic and exact float steps, so every device and numpy agree."""
+    n = int(np.prod(shape))
+    x = (np.arange(n, dtype=np.uint64) + np.uint64(_frame_key(seed_base, fid))) & np.uint64(MASK32)
+    x = _mix32(x, np.uint64(MASK32))
+    return ((x >> np.uint64(8)).astype(np.float32) * np.float32(2.0 ** -23) - np.float32(1.0)).reshape(shape)
+
+
 def fill_features(out, frame_ids, seed_base):
-    """out[i] = N(0,1) drawn on out's device by a generator seeded with
-    (seed_base, frame_ids[i]): a frame's features are the same whichever rank
-    draws them and however many frames share the tensor."""
+    """out[i] = the features of global frame frame_ids[i] for stream seed_base (feature_values_np's values,
+    computed on out's device and rounded once to out's dtype): a frame's features are the same whichever rank
+    draws them, however many frames share the tensor, and on the host."""
     assert out.shape[0] == len(frame_ids)
-    g = torch.Generator(device=out.device)
-    tmp = torch.empty(out.shape[1:], dtype=torch.float32, device=out.device)
+    n = out[0].numel() if out.shape[0] else 0
+    if n == 0:
+        return out
+    idx = torch.arange(n, dtype=torch.int64, device=out.device)
     for i, fid in enumerate(frame_ids):
-        g.manual_seed(int(seed_base) * 1_000_003 + int(fid))
-        torch.randn(tmp.shape, generator=g, out=tmp, device=out.device)
-        out[i].copy_(tmp)
+        x = (idx + _frame_key(seed_base, fid)) & MASK32
+        x = _mix32(x, MASK32)
+        v = (x >> 8).to(torch.float32) * (2.0 ** -23) - 1.0
+        out[i].copy_(v.view(out.shape[1:]))
     return out
+
+
+def _weights(n, device):
+    """2i + 1 for the n elements of a frame (int64), cached per (n, device)."""
+    key = (int(n), str(device))
+    w = _WEIGHTS.get(key)
+    if w is None:
+        w = torch.arange(n, dtype=torch.int64, device=device) * 2 + 1
+        _WEIGHTS.clear()  # one shape at a time: the maps are large
+        _WEIGHTS[key] = w
+    return w
+
+
+_WEIGHTS = {}
 
 
 def frame_checksums(t):
-    """Per-frame checksum of a [F, ...] f32/bf16 map: the int64 sum of its
-    elements' bit patterns. Integer sums are exact in any order, so the value
-    is independent of the reduction's launch shape (and of the batch)."""
+    """Per-frame checksum of a [F, ...] f32/bf16 map: sum_i bits[i] * (2i + 1) mod 2^64 over the frame's
+    elements in row-major order (bits: the element's pattern as a signed integer), as a signed int64.
+    Integer arithmetic mod 2^64 is exact in any order, so the value does not depend on the reduction's launch
+    shape or on the batch; the odd position weights make it see where each value sits -- a row written to the
+    wrong cell or two channels swapped change it (the plain bit sum could not)."""
     bits = {4: torch.int32, 2: torch.int16}[t.element_size()]
     out = torch.empty(t.shape[0], dtype=torch.int64, device=t.device)
+    if t.shape[0] == 0:
+        return out
+    w = _weights(t[0].numel(), t.device)
     for i in range(t.shape[0]):
-        out[i] = t[i].contiguous().view(bits).to(torch.int64).sum()
+        out[i] = (t[i].contiguous().view(bits).reshape(-1).to(torch.int64) * w).sum()
     return out
+
+
+def combine_checksums(per_output):
+    """One checksum per frame over several outputs of a step: sum_k cs_k * (2k + 1) mod 2^64 (int64 tensors,
+    wrapping), so that exchanging two outputs of one shape changes it too."""
+    total = None
+    for k, cs in enumerate(per_output):
+        term = cs.to(torch.int64) * (2 * k + 1)
+        total = term if total is None else total + term
+    return total
+
+
+def frame_checksum_np(a, bf16=False):
+    """frame_checksums of ONE frame on the host (the oracle side): a is the frame's values as f32 (bf16: the
+    values already rounded to bf16, their upper 16 bits taken)."""
+    a = np.ascontiguousarray(a, dtype=np.float32).reshape(-1)
+    if bf16:
+        bits = (a.view(np.uint32) >> np.uint32(16)).astype(np.uint16).view(np.int16)
+    else:
+        bits = a.view(np.int32)
+    s, step = 0, 1 << 22
+    with np.errstate(over="ignore"):
+        for lo in range(0, a.size, step):  # in pieces: the maps run to 10^8 elements
+            b = bits[lo:lo + step].astype(np.int64).astype(np.uint64)
+            w = np.arange(lo, lo + b.size, dtype=np.uint64) * np.uint64(2) + np.uint64(1)
+            s = (s + int((b * w).sum(dtype=np.uint64))) % (1 << 64)
+    return s - (1 << 64) if s >= 1 << 63 else s
+
+
+def combine_checksums_int(per_output):
+    """combine_checksums over Python ints (host side), as a signed int64."""
+    s = sum(int(c) * (2 * k + 1) for k, c in enumerate(per_output)) % (1 << 64)
+    return s - (1 << 64) if s >= 1 << 63 else s
 
 
 def _coll_device(device):

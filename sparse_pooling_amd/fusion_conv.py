@@ -47,6 +47,23 @@ def conv_ws_bytes(dtype, n_frames, h, w, c_a, c_b, c_out, pool_cap, stats):
     return out.value
 
 
+def rows_form(a, weights, b=None, pool=None, frame_off=None, relu=True, stats=False, out=None, c_out=None):
+    """Whether conv3x3 with these arguments runs the row-streaming form (shpl_conv3x3_rows_form): only then
+    does its workspace hold the pooled operand shpl_conv3x3_wgrad_reuse reads. ``out`` None: a fresh
+    contiguous output (16-byte aligned, as torch allocates)."""
+    B, H, W, Ca = (int(s) for s in a.shape)
+    Cb = 0 if b is None else int(b.shape[-1])
+    Cout = int(weights.shape[3]) if c_out is None else int(c_out)
+    flag = ctypes.c_int(0)
+    out_ptr = L.ptr(out) if out is not None else ctypes.c_void_p(256)  # a stand-in aligned address
+    L.check(L.lib().shpl_conv3x3_rows_form(L.dtype_code(a), B, H, W, L.ptr(a), Ca, 0, Ca, L.ptr(b), Cb, 0, Cb,
+                                           None if pool is None else pool.ref(), L.ptr(frame_off), L.ptr(weights),
+                                           Cout, L.ACT_RELU if relu else L.ACT_NONE, out_ptr,
+                                           Cout if out is None else int(out.stride(2)), int(bool(stats)),
+                                           ctypes.byref(flag)), "shpl_conv3x3_rows_form")
+    return bool(flag.value)
+
+
 def conv3x3(a, weights, b=None, pool=None, frame_off=None, center=None, scale=None, shift=None, relu=True,
             stats=None, out=None, ws=None):
     """act((conv3x3_SAME([a || b], weights) - center) * scale + shift).
@@ -200,7 +217,11 @@ class _FusionConvFn(torch.autograd.Function):
         cap = pool.nnz_cap if pool is not None else None
         # bf16 pooled with a weight gradient to come: a workspace of this call's own, kept for the backward,
         # whose weight gradient reads the pooled operand the forward prepared in it (shpl_conv3x3_wgrad_reuse)
-        reuse = pooled and conv.WGRAD_REUSE and a.dtype == torch.bfloat16 and ctx.needs_input_grad[2]
+        # -- only when the forward runs the row-streaming form, which is what leaves that operand there
+        reuse = (pooled and conv.WGRAD_REUSE and a.dtype == torch.bfloat16 and ctx.needs_input_grad[2] and
+                 rows_form(a, weights.to(a.dtype), b=b, pool=pool, frame_off=frame_off,
+                           relu=conv.relu if not train_bn else False, stats=train_bn,
+                           out=out if not train_bn else None, c_out=conv.c_out))
         nbytes = conv_ws_bytes(dt, B, H, W, Ca, Cb, conv.c_out, cap, train_bn)
         ws = L.workspace(nbytes, a.device) if reuse else conv._ws_for((dt, B, H, W, Cb, cap, train_bn), nbytes)
         ctx.fwd_ws = ws if reuse else None

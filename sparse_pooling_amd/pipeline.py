@@ -76,8 +76,9 @@ class FusedPipeline:
         self.bv_fused = torch.empty((self.B, self.Hb, self.Wb, self.Cb + self.Ci), dtype=dtype, device=dev)
         if dual:
             # pixel CSR (BEV -> img); from the buckets without ent_col: every entry its own column (shpl.h)
-            self.pcsr = L.Csr(self.n_pix, self.N, dev, with_col=not self.buckets or self.PIXEL_COLS,
-                              key_range=self.rows)
+            with_col = not self.buckets or self.PIXEL_COLS
+            self.pcsr = L.Csr(self.n_pix, self.N, dev, with_col=with_col, key_range=self.rows,
+                              identity_cols=not with_col)
             self.img_fused = torch.empty((self.B, self.Hi, self.Wi, self.Ci + self.Cb), dtype=dtype,
                                          device=dev)
         if live:

@@ -87,6 +87,22 @@ def test_argument_validation_is_host_side():
                   N) == L.ERR_BAD_SHAPE
         assert fn(L.BY_CELL, L.F32, ctypes.byref(csr), P, 32, 0, 32, N, 32, 0, 32, L.OUT_CONCAT, P, 64,
                   N) == L.ERR_ARG
+    # a pixel-keyed CSR without ent_col only when marked as one column per entry (SHPL_CSR_IDENTITY_COLS):
+    # otherwise the pulls would sum without TF's per-column partials
+    pix = L.ShplCsr(256, 256, 256, None, 100, 10)
+    for fn in (lib.shpl_pull, lib.shpl_pull_dense, lib.shpl_pull_sparse):
+        assert fn(L.BY_PIXEL, L.F32, ctypes.byref(pix), P, 32, 0, 32, P, 32, 0, 32, L.OUT_CONCAT, P, 64,
+                  N) == L.ERR_ARG
+    # the forward conv's row-streaming predicate (shpl_conv3x3_rows_form): f32 never, bf16 at 32 + 32 channels
+    # without statistics yes, with training statistics over 32 + 16 pooled channels no (the tiled kernel)
+    rf = ctypes.c_int(-1)
+    ccell1 = L.ShplCsr(256, 256, 256, None, 176 * 200, 1000)
+    for dt, cb, stats, want in ((L.F32, 32, 0, 0), (L.BF16, 32, 0, 1), (L.BF16, 16, 1, 0), (L.BF16, 32, 1, 1)):
+        assert lib.shpl_conv3x3_rows_form(dt, 1, 176, 200, P, 32, 0, 32, P, cb, 0, cb, ctypes.byref(ccell1), P, P,
+                                          32, L.ACT_NONE, P, 32, stats, ctypes.byref(rf)) == L.OK
+        assert rf.value == want, (dt, cb, stats)
+    assert lib.shpl_conv3x3_rows_form(L.BF16, 1, 176, 200, P, 32, 0, 32, P, 32, 0, 32, ctypes.byref(ccell1), P, P,
+                                      16, L.ACT_NONE, P, 16, 0, ctypes.byref(rf)) == L.OK and rf.value == 0
     # buckets: shapes over the limits (65536 destinations per frame, 2^24 points per frame), workspace size,
     # missing bucket workspace; CSRs from buckets: null map, too few keys, small
     # workspace; pull pair: null CSR, the bad-shape checks of shpl_pull, no key_range
@@ -116,6 +132,9 @@ def test_argument_validation_is_host_side():
     assert lib.shpl_pull_pair(ctypes.byref(ccell), ctypes.byref(narrow), None, None, N) == L.ERR_BAD_SHAPE
     norange = L.ShplCsr(256, 256, 256, None, 4 * 8800, 80000)  # row-keyed pulls need key_range
     assert lib.shpl_pull_pair(ctypes.byref(norange), ctypes.byref(d32), None, None, N) == L.ERR_ARG
+    pnocol = L.ShplCsr(256, 256, 256, None, 4 * 6750, 80000, 256)  # pixel side: neither ent_col nor the flag
+    assert lib.shpl_pull_pair(None, None, ctypes.byref(pnocol), ctypes.byref(d32), N) == L.ERR_ARG
+    assert lib.shpl_build_csr_buckets(ctypes.byref(bk), None, ctypes.byref(pnocol), N) == L.ERR_ARG
     # velodyne loader: P2 without image size, misaligned scan
     assert lib.shpl_velo_to_cam(1, P, 10, P, P, P, N, math.nan, N, P, P, N, P, 1 << 20, N) == L.ERR_ARG
     assert lib.shpl_velo_to_cam(1, P, 10, ctypes.c_void_p(260), P, N, N, math.nan, N, P, P, N, P, 1 << 20,

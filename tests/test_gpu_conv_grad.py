@@ -318,13 +318,18 @@ def test_fused_conv_autograd_vs_oracle(train):
     _check(conv.beta.grad, e_db, 1e-4 + 1e-6 * np.abs(g).reshape(-1, Ci).sum(0), "d_beta")
 
 
-@pytest.mark.parametrize("train", [True, False])
-def test_fused_bf16_wgrad_reuses_forward_operand(train):
+@pytest.mark.parametrize("train,cb,ci,cout", [(True, 32, 32, 32), (False, 32, 32, 32),
+                                               (True, 32, 16, 16), (False, 32, 16, 32), (True, 32, 16, 32),
+                                               (True, 32, 32, 16), (False, 32, 32, 16)])
+def test_fused_bf16_wgrad_reuses_forward_operand(train, cb, ci, cout):
     """bf16 FusionConv.fused: the weight gradient reading the forward's pooled operand
     (shpl_conv3x3_wgrad_reuse, WGRAD_REUSE) gives bitwise the gradients of the one that prepares its own.
-    Config 1's geometry with 32 + 32 channels: the row-streaming forward and weight gradient."""
+    Config 1's geometry. 32 + 32 channels: the row-streaming forward and weight gradient. 32 + 16 with training
+    BatchNorm (a 2 + 1 chunk statistics form k_conv_rows does not have) and c_out = 16 (not a whole output
+    block) run the tiled forward, which leaves no pooled operand: the reuse must not be taken there
+    (shpl_conv3x3_rows_form; ADVICE r04: it was, and dW read an unwritten workspace)."""
     from sparse_pooling_amd import fusion_conv as fc, shpl_map as sm
-    spec = synth.FrameSpec(2000, (1200, 360), (704, 800), (4, 4), 32, 32)
+    spec = synth.FrameSpec(2000, (1200, 360), (704, 800), (4, 4), cb, ci)
     fr = synth.make_frame(spec, seed=907, n_outside=10)
     gen = orc.gen_sparse_pooling_input_avod(fr.points, fr.voxel_indices, fr.P, list(spec.im_size),
                                             tuple(spec.bv_size))
@@ -334,12 +339,12 @@ def test_fused_bf16_wgrad_reuses_forward_operand(train):
     Cb, Ci = spec.c_bev, spec.c_img
     bev = _t(synth.make_features((1, Hb, Wb, Cb), 31)).to(torch.bfloat16)
     img = _t(synth.make_features((1, Hi, Wi, Ci), 32)).to(torch.bfloat16)
-    g = _t(np.random.default_rng(33).standard_normal((1, Hb, Wb, Ci)).astype(np.float32)).to(torch.bfloat16)
+    g = _t(np.random.default_rng(33).standard_normal((1, Hb, Wb, cout)).astype(np.float32)).to(torch.bfloat16)
     grads = []
     for reuse in (False, True):
         smap = sm.pack_map(_t(ref["Mij_pool"]), _t(ref["M_val"].astype(np.float32)), ref["M_size"],
                            _t(ref["img_index_flip_pool"]), img.shape)
-        conv = fc.FusionConv(Cb + Ci, Ci, dtype=torch.bfloat16, device=DEV, seed=4)
+        conv = fc.FusionConv(Cb + Ci, cout, dtype=torch.bfloat16, device=DEV, seed=4)
         conv.WGRAD_REUSE = reuse
         conv.weights.requires_grad_(True)
         conv.beta.requires_grad_(True)
@@ -348,3 +353,37 @@ def test_fused_bf16_wgrad_reuses_forward_operand(train):
         grads.append([x.grad.clone() for x in (tb, ti, conv.weights, conv.beta)])
     for a, b in zip(*grads):
         assert torch.equal(a, b)
+
+
+def test_wgrad_reuse_rejects_a_tiled_forward_workspace():
+    """shpl_conv3x3_wgrad_reuse checks what it can of the forward's row-streaming predicate: a forward with
+    training statistics over 32 + 16 bf16 channels runs the tiled kernel (no pooled operand in its workspace),
+    so handing its workspace over is SHPL_ERR_ARG, not a silent read."""
+    import ctypes
+    from sparse_pooling_amd import _lib as L, fusion_conv as fc, shpl_map as sm
+    spec = synth.FrameSpec(2000, (1200, 360), (704, 800), (4, 4), 32, 16)
+    fr = synth.make_frame(spec, seed=907, n_outside=10)
+    gen = orc.gen_sparse_pooling_input_avod(fr.points, fr.voxel_indices, fr.P, list(spec.im_size),
+                                            tuple(spec.bv_size))
+    ref = orc.produce_sparse_pooling_input(gen, stride=spec.stride)
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    bev = _t(synth.make_features((1, Hb, Wb, 32), 31)).to(torch.bfloat16)
+    img = _t(synth.make_features((1, Hi, Wi, 16), 32)).to(torch.bfloat16)
+    smap = sm.pack_map(_t(ref["Mij_pool"]), _t(ref["M_val"].astype(np.float32)), ref["M_size"],
+                       _t(ref["img_index_flip_pool"]), img.shape)
+    pool = smap.csr(L.BY_CELL, L.ORDER_ENTRY)
+    w = torch.zeros((3, 3, 48, 32), dtype=torch.bfloat16, device=DEV)
+    assert not fc.rows_form(bev, w, b=img, pool=pool, frame_off=smap.frame_off, relu=False, stats=True)
+    assert fc.rows_form(bev, w, b=img, pool=pool, frame_off=smap.frame_off, relu=False, stats=False)
+    fws = L.workspace(fc.conv_ws_bytes(L.BF16, 1, Hb, Wb, 32, 16, 32, pool.nnz_cap, True), DEV)
+    gy = torch.zeros((1, Hb, Wb, 32), dtype=torch.bfloat16, device=DEV)
+    dw = torch.empty((3, 3, 48, 32), dtype=torch.float32, device=DEV)
+    nb = ctypes.c_size_t()
+    L.check(L.lib().shpl_conv3x3_wgrad_workspace_bytes(L.BF16, 1, Hb, Wb, 32, 16, 32, pool.nnz_cap,
+                                                       ctypes.byref(nb)), "ws")
+    ws = L.workspace(nb.value, DEV)
+    rc = L.lib().shpl_conv3x3_wgrad_reuse(L.BF16, 1, Hb, Wb, L.ptr(bev), 32, 0, 32, L.ptr(img), 16, 0, 16, pool.ref(),
+                                          L.ptr(smap.frame_off), L.ptr(gy), 32, 32, L.ptr(dw), L.ptr(ws), ws.numel(),
+                                          L.ptr(fws), fws.numel(), 1, L.stream_of(DEV))
+    assert rc == L.ERR_ARG
