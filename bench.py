@@ -87,6 +87,10 @@ def parse():
     ap.add_argument("--rows", action="store_true",
                     help="layer workload: the row-keyed pipeline (bucketed index, one launch per pull pair) at any batch "
                          "(A/B: config 6 1.95-1.99 vs 1.57 ms, profiles/r04_rows_ab.log)")
+    ap.add_argument("--split", default="auto", choices=["auto", "on", "off"],
+                    help="img->BEV layer: the pass-through copy beside the index chain and the pooled half written once "
+                         "by a row-keyed pull after it, on a high-priority stream (FusedPipeline split); auto: on "
+                         "for 1 KB halves (config 6)")
     ap.add_argument("--pixel-cols", action="store_true",
                     help="bucketed config 3: the pixel-keyed CSR keeps ent_col (per-column partials in its pulls) "
                          "instead of the identity-column form")
@@ -427,9 +431,13 @@ def main():
     frames = [synth.make_frame(spec, seed=s, n_outside=200) for s in fids]
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, dev)
     pipeline.FusedPipeline.PIXEL_COLS = args.pixel_cols
+    esz0 = 2 if dtype == torch.bfloat16 else 4
+    split = (not dual and not args.rows and not args.no_overlap and
+             (args.split == "on" or (args.split == "auto" and min(spec.c_bev, spec.c_img) * esz0 >= 1024)))
     pl = pipeline.FusedPipeline(F, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev,
                                 spec.c_img, dtype=dtype, dual=dual, device=dev, rows=True if args.rows else None,
-                                buckets=False if args.no_buckets else None)
+                                buckets=False if args.no_buckets else None, split=split)
+    chain = torch.cuda.Stream(device=dev, priority=-1) if split else None
     Hb, Wb = spec.bev_feat_hw
     Hi, Wi = spec.img_feat_hw
     feats = lambda shape, seed: sd.fill_features(torch.empty(shape, dtype=dtype, device=dev), fids, seed)  # noqa
@@ -461,6 +469,8 @@ def main():
             pl.layer_sparse(bev, img)
             if ev is not None:
                 ev[3].record()
+        elif split:
+            pl.step_split(pts, vox, off, P, bev, img, side, chain, events=ev[:4] if ev else None)
         else:
             pl.step_overlapped(pts, vox, off, P, bev, img, side, events=ev[:4] if ev else None, side2=side2)
         if backward:
@@ -538,6 +548,12 @@ def main():
         # (first k_dense start -> last k_sparse end) instead of the summed durations
         layer_ms = sum(e[0].elapsed_time(e[3]) for e in evs) / args_steps_ev + bwd_ms
     eager_ms = None
+    if split:
+        # the two halves' passes overlap each other and the chain: the layer's window from the first start to
+        # the last end (eager), or the replayed step (every kernel of it)
+        layer_ms = sum(max(e[0].elapsed_time(e[1]), e[0].elapsed_time(e[3])) for e in evs) / args_steps_ev
+        if replay_step_ms is not None:
+            eager_ms, layer_ms = layer_ms, replay_step_ms
     if getattr(pl, "buckets", False) and replay_step_ms is not None:
         # the bucketed one-queue step: its brackets span every kernel of the step, and run eagerly they
         # also hold the host's launch gaps between ~10 us kernels; the replayed step is the same kernels
@@ -586,6 +602,7 @@ def main():
                 "unique_src_pixels_rank0": u_pix,
                 "unique_cells_rank0": u_cell,
                 "overlap_index_build": not args.no_overlap,
+                **({"split": True} if split else {}),
                 "hip_graph": graph is not None,
                 **({"steps_per_graph": args.graph_steps} if graph is not None and args.graph_steps > 1 else {}),
                 **({"graph_issue_ms_per_replay": round(issue_ms, 4)} if issue_ms is not None else {}),
@@ -597,6 +614,9 @@ def main():
                 "kernel": ("SHPL layer pulls: k_dense (concat stream) + k_sparse (pooled gather); achieved over "
                            + ("the layer's window (first k_dense start to last k_sparse end: the cell-keyed gathers "
                               "run beside img_fused's stream)" if interleaved else "their summed durations")
+                           + ("; split step (the pass-through copy beside the index chain, then the pooled half "
+                              "written once by the row-keyed pull): every kernel of the step, timed as the replayed "
+                              "step (HIP events around the graph replays)" if split else "")
                            + ("; bucketed one-stream step: the forward bracket spans the whole forward "
                               "(index + buckets with the pass-through copies riding its launches, both CSRs, the "
                               "pooled pull pair), the backward bracket the gradient pull pair -- every kernel of "
@@ -778,9 +798,9 @@ def run_frames(args, world, rank, dev):
         print(json.dumps(out), flush=True)
 
 
-def cpu_baseline_conv(spec, frames_np, budget_s):
+def cpu_baseline_conv(spec, frames_np, budget_s, c_out=None, bias=False):
     """Oracle on one core: index build + TF-order pooling + concat of one frame,
-    and the conv/BN/ReLU over a band of rows of it, scaled to the frame."""
+    and the conv/BN/ReLU (bias: bias + ReLU) over a band of rows of it, scaled to the frame."""
     from oracle import shpl_oracle as orc
     Hb, Wb = spec.bev_feat_hw
     Hi, Wi = spec.img_feat_hw
@@ -788,8 +808,10 @@ def cpu_baseline_conv(spec, frames_np, budget_s):
     rng = np.random.default_rng(0)
     bev = rng.standard_normal((1, Hb, Wb, cb), dtype=np.float32)
     img = rng.standard_normal((1, Hi, Wi, ci), dtype=np.float32)
-    w = (rng.standard_normal((3, 3, cb + ci, ci)) * 0.05).astype(np.float32)
-    sc = np.full(ci, 1.0 / np.sqrt(1.0 + 1e-3), np.float32)
+    c_out = ci if c_out is None else c_out
+    w = (rng.standard_normal((3, 3, cb + ci, c_out)) * 0.05).astype(np.float32)
+    sc = None if bias else np.full(c_out, 1.0 / np.sqrt(1.0 + 1e-3), np.float32)
+    shift = np.linspace(-0.5, 0.5, c_out).astype(np.float32) if bias else None
     fr = frames_np[0]
     a = time.perf_counter()
     g = orc.gen_sparse_pooling_input_avod(fr.points, fr.voxel_indices, fr.P, list(spec.im_size), tuple(spec.bv_size))
@@ -801,16 +823,66 @@ def cpu_baseline_conv(spec, frames_np, budget_s):
     band = 8
     while rows < band or (t_conv < budget_s and rows + band <= Hb):
         d = time.perf_counter()
-        orc.conv3x3(eb[:, max(rows - 1, 0):min(rows + band + 1, Hb)], w, None, sc, None, True)
+        orc.conv3x3(eb[:, max(rows - 1, 0):min(rows + band + 1, Hb)], w, None, sc, shift, True)
         t_conv += time.perf_counter() - d
         rows += band
     conv_frame = t_conv * Hb / rows
     total = (b - a) + (c - b) + conv_frame
     return {"value": round(1.0 / total, 4), "unit": "frames/s", "cores": 1, "kind": "port",
             "sample": (f"1 frame ({spec.n_points} pts) through oracle/shpl_oracle.c, single thread: index "
-                       f"{1e3 * (b - a):.1f} ms + TF-order pooling and concat {1e3 * (c - b):.1f} ms + 3x3 conv/BN/"
-                       f"ReLU (double accumulation) timed on {rows} of {Hb} rows, scaled: {1e3 * conv_frame:.0f} ms; "
+                       f"{1e3 * (b - a):.1f} ms + TF-order pooling and concat {1e3 * (c - b):.1f} ms + 3x3 conv "
+                       f"{cb + ci}->{c_out}/{'bias' if bias else 'BN'}/ReLU (double accumulation) timed on {rows} of "
+                       f"{Hb} rows, scaled: {1e3 * conv_frame:.0f} ms; "
                        f"{os.cpu_count()} host cpus visible")}
+
+
+def cpu_baseline_train(spec, frames_np, budget_s):
+    """Oracle on one core, the training step of the conv workload per frame: index build + TF-order pooling
+    and concat (whole frame), the pooled channels' gradient back to the image (whole frame), and over bands
+    of rows, scaled to the frame: the conv forward (double sums), BatchNorm forward with batch statistics +
+    ReLU, BatchNorm / ReLU backward, the input gradient (conv on the flipped, transposed weights) and the
+    weight gradient (oracle/shpl_oracle.c)."""
+    from oracle import shpl_oracle as orc
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    cb, ci = spec.c_bev, spec.c_img
+    rng = np.random.default_rng(0)
+    bev = rng.standard_normal((1, Hb, Wb, cb), dtype=np.float32)
+    img = rng.standard_normal((1, Hi, Wi, ci), dtype=np.float32)
+    w = (rng.standard_normal((3, 3, cb + ci, ci)) * 0.05).astype(np.float32)
+    gy = rng.standard_normal((1, Hb, Wb, ci), dtype=np.float32)
+    fr = frames_np[0]
+    a = time.perf_counter()
+    g = orc.gen_sparse_pooling_input_avod(fr.points, fr.voxel_indices, fr.P, list(spec.im_size), tuple(spec.bv_size))
+    ref = orc.produce_sparse_pooling_input(g, stride=spec.stride)
+    b = time.perf_counter()
+    eb, _ = orc.sparse_pool_layer(bev, img, ref["Mij_pool"], ref["M_val"], ref["M_size"], ref["img_index_flip_pool"])
+    c = time.perf_counter()
+    d_pool = rng.standard_normal((Hb * Wb, ci), dtype=np.float32)
+    orc.sparse_pool_grad_img(ref["Mij_pool"], ref["M_val"], ref["M_size"], d_pool, ref["img_index_flip_pool"],
+                             (1, Hi, Wi, ci))
+    d = time.perf_counter()
+    rows, t_band = 0, 0.0
+    band = 8
+    while rows < band or (t_band < budget_s and rows + band <= Hb):
+        x = eb[:, max(rows - 1, 0):min(rows + band + 1, Hb)]
+        e = time.perf_counter()
+        _, raw = orc.conv3x3(x, w, raw=True)
+        y, mean, var, _, _ = orc.batch_norm_train(raw, relu=True)
+        g_raw, _, _ = orc.batch_norm_backward(raw, gy[:, :raw.shape[1]], True, mean, var, 1e-3, None, None, True)
+        g32 = g_raw.astype(np.float32)
+        orc.conv3x3_dgrad(g32, w)
+        orc.conv3x3_wgrad(x, g32)
+        t_band += time.perf_counter() - e
+        rows += band
+    band_frame = t_band * Hb / rows
+    total = (b - a) + (c - b) + (d - c) + band_frame
+    return {"value": round(1.0 / total, 5), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": (f"1 frame ({spec.n_points} pts) through oracle/shpl_oracle.c, single thread: index "
+                       f"{1e3 * (b - a):.1f} ms + TF-order pooling and concat {1e3 * (c - b):.1f} ms + the pooled "
+                       f"gradient to the image {1e3 * (d - c):.1f} ms + conv forward / BatchNorm (batch statistics) "
+                       f"+ ReLU / their backward / input gradient / weight gradient (double accumulation) timed on "
+                       f"{rows} of {Hb} rows, scaled: {1e3 * band_frame:.0f} ms; {os.cpu_count()} host cpus visible")}
 
 
 def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off, P, bev, img, conv):
@@ -820,7 +892,7 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
     beta. Eager launches (autograd allocates per step). BatchNorm statistics
     are the rank's own frames' (no cross-rank sync; data-parallel weight
     gradients would need an all-reduce, out of scope per SURVEY §8e)."""
-    from sparse_pooling_amd import dist as sd
+    from sparse_pooling_amd import dist as sd, synth
     F = len(fids)
     Hb, Wb = spec.bev_feat_hw
     cb, ci = spec.c_bev, spec.c_img
@@ -889,6 +961,9 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
     # PMC bytes of every SHPL kernel of a step (scripts/r02_pmc.sh TAG=train..., traffic.py step)
     traffic, traffic_note, _ = traffic_lookup(f"train_{dname}_F{F}")
     comm = sd.comm_report(dev)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_train(spec, [synth.make_frame(spec, seed=fids[0], n_outside=200)], args.cpu_seconds)
     if rank == 0:
         print(json.dumps({
             "metric": "SHPL + post-fusion conv training frames/sec (fwd + bwd), 1/2/4/8 GPU",
@@ -916,7 +991,7 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
                           "algorithmic_bytes_per_step": hbm_bytes, "hbm_GBps": round(hbm_gbs, 1),
                           "hbm_traffic_per_step": traffic, "traffic_note": traffic_note}),
             "fwd_ms": round(fwd_ms, 4), "bwd_ms": round(bwd_ms, 4),
-            "cpu_baseline": None,
+            "cpu_baseline": cpu,
             "timing": tinfo,
             "comm": comm,
             "lib_sha256": lib_sha256(),
@@ -929,7 +1004,15 @@ def run_conv(args, world, rank, dev):
     (bv_fused never written). The unfused form (fused layer -> bv_fused -> conv) is
     timed beside it."""
     from sparse_pooling_amd import dist as sd, fusion_conv as fc, pipeline, synth
-    spec = synth.CONFIG2
+    # config 2: rpn_model.py:338-346 (64 -> 32, BatchNorm + ReLU); config 6: retinanet_model.py:334-348, the
+    # RetinaNet P2 SHPL's slim.conv2d(bev_fused, 256, [3, 3]) -- 512 -> 256 channels, bias + ReLU, no normalizer
+    retina = args.config == 6
+    if args.config not in (2, 6):
+        sys.exit("bench.py --workload conv: --config 2 (rpn) or 6 (RetinaNet P2)")
+    if retina and args.train:
+        sys.exit("bench.py --workload conv --config 6: forward only (the reference trains it, but round 5 measures "
+                 "the forward at its shape)")
+    spec = synth.CONFIGS[args.config]
     fids = sd.partition(args.frames or 64, world, rank, args.partition)
     F = len(fids)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
@@ -946,8 +1029,13 @@ def run_conv(args, world, rank, dev):
     cb, ci = spec.c_bev, spec.c_img
     bev = sd.fill_features(torch.empty((F, Hb, Wb, cb), dtype=dtype, device=dev), fids, 1)
     img = sd.fill_features(torch.empty((F, Hi, Wi, ci), dtype=dtype, device=dev), fids, 2)
-    conv = fc.FusionConv(cb + ci, ci, dtype=dtype, device=dev, seed=0)  # the same weights on every rank
-    out = torch.empty((F, Hb, Wb, ci), dtype=dtype, device=dev)
+    c_out = 256 if retina else ci
+    # the same weights on every rank
+    conv = (fc.FusionConv(cb + ci, c_out, batch_norm=False, bias=True, relu=True, dtype=dtype, device=dev, seed=0)
+            if retina else fc.FusionConv(cb + ci, ci, dtype=dtype, device=dev, seed=0))
+    if retina:  # a bias that is not all zeros (slim's zeros initializer would hide the epilogue)
+        conv.bias.copy_(torch.linspace(-0.5, 0.5, c_out, device=dev))
+    out = torch.empty((F, Hb, Wb, c_out), dtype=dtype, device=dev)
     out_unf = torch.empty_like(out)
     train = args.train_bn
     if args.train:
@@ -1003,18 +1091,19 @@ def run_conv(args, world, rank, dev):
     pull_ms = sum(e[0].elapsed_time(e[1]) for e in uev) / n_ev
     uconv_ms = sum(e[1].elapsed_time(e[2]) for e in uev) / n_ev
     esz = 2 if dtype == torch.bfloat16 else 4
-    flops = 2.0 * F * Hb * Wb * 9 * (cb + ci) * ci
+    flops = 2.0 * F * Hb * Wb * 9 * (cb + ci) * c_out
     nnz = int(pl.frame_nnz.sum().item())
     u_pix = int(torch.unique(pl.pix[pl.pix >= 0]).numel())
-    hbm_bytes = F * Hb * Wb * (cb + ci) * esz + u_pix * ci * esz + 12 * nnz  # read bev, write out, gather
+    hbm_bytes = F * Hb * Wb * (cb + c_out) * esz + u_pix * ci * esz + 12 * nnz  # read bev, write out, gather
     tflops = flops / (conv_ms * 1e-3) / 1e12
-    checks = None if train else checksum_report(f"conv_{args.dtype}", sd.frame_checksums(out), fids, dev, rank, args)
+    checks = None if train else checksum_report(f"conv{'_c6' if retina else ''}_{args.dtype}", sd.frame_checksums(out),
+                                                fids, dev, rank, args)
     comm = sd.comm_report(dev)
-    traffic, traffic_note, tj = traffic_lookup(f"conv_{args.dtype}_F{F}")
+    traffic, traffic_note, tj = traffic_lookup(f"conv{'_c6' if retina else ''}_{args.dtype}_F{F}")
     mfma_busy = tj.get("mfma_busy_share") if tj else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline_conv(spec, frames[:1], args.cpu_seconds)
+        cpu = cpu_baseline_conv(spec, frames[:1], args.cpu_seconds, c_out=c_out, bias=retina)
     if rank == 0:
         dname = "bf16" if esz == 2 else "f32"
         out_j = {
@@ -1023,10 +1112,11 @@ def run_conv(args, world, rank, dev):
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
             "higher_is_better": True, "scaling": args.partition, "vs_baseline": None, "dtype": dname,
             "data": "synthetic (seeded KITTI-shaped frames, xavier-initialised conv weights; no dataset on the box)",
-            "config": {"workload": (f"conv: config2 ({spec.n_points} pts/frame, BEV {Hb}x{Wb}x{cb}, img {Hi}x{Wi}x{ci})"
-                                    f" -> index -> cell CSR -> conv3x3 {cb + ci}->{ci} + BatchNorm "
-                                    f"({'training' if train else 'inference'}) + ReLU of [bev || pool(img)], pooling "
-                                    "fused into the conv's staging (rpn_model.py:338-346)"),
+            "config": {"workload": (f"conv: config{args.config} ({spec.n_points} pts/frame, BEV {Hb}x{Wb}x{cb}, img "
+                                    f"{Hi}x{Wi}x{ci}) -> index -> cell CSR -> conv3x3 {cb + ci}->{c_out} + "
+                                    + ("bias + ReLU of [bev || pool(img)] (retinanet_model.py:334-348)" if retina else
+                                       f"BatchNorm ({'training' if train else 'inference'}) + ReLU of [bev || "
+                                       "pool(img)], pooling fused into the conv's staging (rpn_model.py:338-346)")),
                        "global_batch": F * world, "frames_per_gpu_per_step": F, "hip_graph": graph is not None,
                        "parallelism": f"frame-sharded x{world}"},
             "frame_checksums": checks,

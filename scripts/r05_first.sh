@@ -18,4 +18,10 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('__SM
 tail -1 gpurun_out/r05_smoke.log
 timeout -k 10 400 python bench.py > gpurun_out/r05_bench_default.log 2>&1 || { tail -5 gpurun_out/r05_bench_default.log; exit 1; }
 grep '^{' gpurun_out/r05_bench_default.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print(d['value'], d['ms_per_step'], r['frac'], d['frame_checksums'])"
+# config 6: a kernel trace of the default pipeline and of the row-keyed one (--rows: 1.95 ms in round 4, undiagnosed)
+for v in default rows; do
+  extra=""; [ $v = rows ] && extra="--rows"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_prof_c6_$v -o run --output-format csv -- \
+    python3 bench.py --config 6 --no-cpu-baseline --steps 10 $extra > gpurun_out/r05_prof_c6_$v.log 2>&1 || { tail -5 gpurun_out/r05_prof_c6_$v.log; exit 1; }
+done
 echo done

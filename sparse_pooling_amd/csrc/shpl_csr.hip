@@ -396,6 +396,18 @@ __global__ __launch_bounds__(SEG_BLOCK) void k_zero32(int32_t *p, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * SEG_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * SEG_BLOCK) p[i] = 0;
 }
 
+// key_range of a sorted entry list that is not the range builder's (shpl_build_csr_path(SHPL_CSR_FRAME) with
+// key_range): after k_zero32 over key_range (every destination's run empty), each slot that starts a run
+// writes its destination's first entry and each slot that ends one its end.
+__global__ __launch_bounds__(SEG_BLOCK) void k_key_range(const int32_t *ent_dst, int64_t nnz_cap, int32_t *key_range) {
+    for (int64_t s = (int64_t)blockIdx.x * SEG_BLOCK + threadIdx.x; s < nnz_cap; s += (int64_t)gridDim.x * SEG_BLOCK) {
+        const int32_t d = ent_dst[s];
+        if (d < 0) continue;
+        if (s == 0 || ent_dst[s - 1] != d) key_range[2 * (int64_t)d] = (int32_t)s;
+        if (s + 1 == nnz_cap || ent_dst[s + 1] != d) key_range[2 * (int64_t)d + 1] = (int32_t)(s + 1);
+    }
+}
+
 template <bool HAS_COL>
 __global__ __launch_bounds__(SEG_BLOCK) void k_csr_count(CsrIn c, SegIn g) {
     __shared__ int32_t h[SEG_MAX];
@@ -1088,8 +1100,10 @@ extern "C" int shpl_build_csr_path(int path, int direction, int order, int n_fra
     // (entry offsets inside a frame travel in 24 bits: capacities under 2^24 entries)
     const bool small_cap = nnz_cap < ((int64_t)1 << 24);
     if (csr->key_range && !small_cap) return SHPL_ERR_BAD_SHAPE;
-    const bool ranged = csr->key_range != nullptr ||
-                        (small_cap && (path != SHPL_CSR_AUTO
+    // key ranges from the frame builder instead (asked for by name): its sort, then k_key_range
+    const bool frame_ranges = csr->key_range != nullptr && path == SHPL_CSR_FRAME;
+    const bool ranged = (csr->key_range != nullptr && !frame_ranges) ||
+                        (small_cap && !frame_ranges && (path != SHPL_CSR_AUTO
                                            ? path == SHPL_CSR_RANGE
                                            : (n_frames < SEG_FRAMES && keys_per_frame <= RANGE_MAX_KEYS)));
     if (ranged) {
@@ -1124,6 +1138,11 @@ extern "C" int shpl_build_csr_path(int path, int direction, int order, int n_fra
     // shpl_build_csr_path(SHPL_CSR_FRAME | _SEGMENT | _RANGE, ...) forces a path (tests, measurements).
     const bool want = path != SHPL_CSR_AUTO ? path == SHPL_CSR_SEGMENT : n_frames < SEG_FRAMES;
     const bool segmented = want && ws_bytes >= lay.total && (int64_t)n_frames * (n_bins + S) <= seg_cap_of(nnz_cap);
+    if (frame_ranges) {
+        hipLaunchKernelGGL(k_zero32, dim3(grid_for(2 * csr->n_keys, SEG_BLOCK, 4096)), dim3(SEG_BLOCK), 0, st,
+                           csr->key_range, 2 * csr->n_keys);
+        SHPL_LAUNCH_CHECK();
+    }
     if (!segmented) {
         // one workgroup per frame; needs only the tmp words
         if (ws_bytes < align_up(sizeof(uint64_t) * (size_t)nnz_cap, 256)) return SHPL_ERR_WORKSPACE;
@@ -1141,6 +1160,11 @@ extern "C" int shpl_build_csr_path(int path, int direction, int order, int n_fra
             hipLaunchKernelGGL(k_csr_frame<false>, grid, dim3(CSR_BLOCK), 0, st, c, (uint64_t *)ws, nnz_cap,
                                csr->ent_dst, csr->ent_src, csr->ent_val, csr->ent_col);
         SHPL_LAUNCH_CHECK();
+        if (frame_ranges) {
+            hipLaunchKernelGGL(k_key_range, dim3(grid_for(nnz_cap, SEG_BLOCK, 4096)), dim3(SEG_BLOCK), 0, st,
+                               csr->ent_dst, nnz_cap, csr->key_range);
+            SHPL_LAUNCH_CHECK();
+        }
         return SHPL_OK;
     }
     CsrIn c{direction, order, n_frames, d_frame_off, d_frame_nnz, keys_per_frame, 0,

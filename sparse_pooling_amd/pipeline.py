@@ -31,7 +31,7 @@ class FusedPipeline:
 
     def __init__(self, n_frames, max_points_per_frame, total_points, im_size, bv_size, stride,
                  c_bev, c_img, dtype=torch.float32, device="cuda", dual=False, rows=None, live=False,
-                 buckets=None):
+                 buckets=None, split=False):
         """live: the sparse passes walk each frame's live entries (shpl_csr frame layout) instead of the
         whole capacity -- for capacities far above the entry counts (FramePipeline: raw-scan slots per
         voxel point); at config 2 (capacity = entries) the capacity walk is faster (2.22 vs 2.24 ms).
@@ -40,8 +40,17 @@ class FusedPipeline:
         each pull pair is one row-keyed launch (shpl_pull_pair), all on one stream; the forward's
         pass-through halves ride the index launches.
         rows without buckets: the range CSRs (one launch per key) + one k_rows launch per pull,
-        on two streams."""
+        on two streams.
+        split (img->BEV only): the two halves of bv_fused by two passes that need not wait for each other --
+        the pass-through copy (no index) beside the index chain, and the pooled half written once, zeros
+        included, by a row-keyed pull over the frame CSR's key ranges right after the chain (no k_dense zeros
+        for k_sparse to overwrite). For wide channels (config 6: 1 KB halves), where writing half rows costs
+        nothing over whole ones."""
         dev = torch.device(device)
+        self.split = bool(split)
+        if self.split:
+            assert not dual, "split: the img->BEV layer"
+            rows, buckets = False, False
         self.dev, self.dtype, self.dual = dev, dtype, dual
         self.B = int(n_frames)
         self.max_points = int(max_points_per_frame)
@@ -72,7 +81,8 @@ class FusedPipeline:
         self.err = torch.zeros(1, **i32)
         self.index_ws = L.workspace(L.index_ws_bytes(self.B, self.max_points), dev)
         # rows pulls: with key_range
-        self.csr = L.Csr(self.n_cells, self.N, dev, with_col=False, key_range=self.rows)  # BEV-cell CSR (img -> BEV)
+        self.csr = L.Csr(self.n_cells, self.N, dev, with_col=False,
+                         key_range=self.rows or self.split)  # BEV-cell CSR (img -> BEV)
         self.bv_fused = torch.empty((self.B, self.Hb, self.Wb, self.Cb + self.Ci), dtype=dtype, device=dev)
         if dual:
             # pixel CSR (BEV -> img); from the buckets without ent_col: every entry its own column (shpl.h)
@@ -134,7 +144,7 @@ class FusedPipeline:
         args = (self.B, L.ptr(self.frame_off), L.ptr(self.frame_nnz))
         if "cell" in which:
             L.check(self._lib.shpl_build_csr_path(
-                self.csr_path, L.BY_CELL, L.ORDER_ENTRY, *args, self.Hb * self.Wb, L.ptr(self.cell), None, L.ptr(self.val),
+                L.CSR_FRAME if self.split else self.csr_path, L.BY_CELL, L.ORDER_ENTRY, *args, self.Hb * self.Wb, L.ptr(self.cell), None, L.ptr(self.val),
                 L.ptr(self.pix), self.csr.ref(), L.ptr(self.csr.ws), self.csr.ws.numel(), st), "shpl_build_csr")
         if self.dual and "pixel" in which:
             L.check(self._lib.shpl_build_csr_path(
@@ -148,7 +158,10 @@ class FusedPipeline:
 
     def layer_dense(self, bev, img, which=("cell", "pixel")):
         """Streaming half of the layer (needs no M): pass-through copy + zeros.
-        Row-keyed pulls (self.rows) have no separate streaming half."""
+        Row-keyed pulls (self.rows) have no separate streaming half; split: the pass-through copy alone."""
+        if self.split:
+            self._pass_copies(bev, img, ("cell",))
+            return
         if self.rows:
             return
         st = L.stream_of(self.dev)
@@ -232,6 +245,9 @@ class FusedPipeline:
             self._pass_copies(bev, img, which)
             self._pull_pair(*self._pooled_descs(bev, img, which))
             return
+        if self.split:
+            self._pooled_half(img)
+            return
         if "cell" in which:
             self._sparse(self._concat_args(self.csr, L.BY_CELL, img, self.Ci, bev, self.Cb, self.bv_fused))
         if self.dual and "pixel" in which:
@@ -246,6 +262,39 @@ class FusedPipeline:
         self.build_index(points, voxels, point_offsets, P, mval)
         self.build_csr()
         self.layer(bev, img)
+
+    def _pooled_half(self, img):
+        """split: bv_fused[..., Cb:] = pool(img), every row written once (zeros where no entry lands): the
+        row-keyed pull over the cell CSR's key ranges (SHPL_OUT_POOL into the pooled columns)."""
+        esz = self.bv_fused.element_size()
+        out = ctypes.c_void_p(self.bv_fused.data_ptr() + self.Cb * esz)
+        L.check(self._lib.shpl_pull(L.BY_CELL, L.dtype_code(self.bv_fused), self.csr.ref(), L.ptr(img), self.Ci, 0,
+                                    self.Ci, None, 0, 0, 0, L.OUT_POOL, out, self.Cb + self.Ci,
+                                    L.stream_of(self.dev)), "shpl_pull")
+
+    def step_split(self, points, voxels, point_offsets, P, bev, img, side, chain, events=None):
+        """split: the pass-through copy on `side`, the index chain and then the pooled half on `chain` (a
+        high-priority stream, so its latency-bound workgroups are dispatched ahead of the copy's); neither
+        waits for the other (disjoint columns of bv_fused). events: [copy start, copy end, chain start, end]."""
+        main = torch.cuda.current_stream(self.dev)
+        side.wait_stream(main)
+        chain.wait_stream(main)
+        with torch.cuda.stream(side):
+            if events:
+                events[0].record(side)
+            self._pass_copies(bev, img, ("cell",))
+            if events:
+                events[1].record(side)
+        with torch.cuda.stream(chain):
+            if events:
+                events[2].record(chain)
+            self.build_index(points, voxels, point_offsets, P)
+            self.build_csr(("cell",))
+            self._pooled_half(img)
+            if events:
+                events[3].record(chain)
+        main.wait_stream(side)
+        main.wait_stream(chain)
 
     def step_overlapped(self, points, voxels, point_offsets, P, bev, img, side, mval=None, events=None,
                         side2=None):

@@ -164,6 +164,54 @@ def test_fused_pool_conv_is_the_conv_of_bv_fused(cfg, n_frames):
         _assert_within(y_fus[f:f + 1, y0:y1], band[:, sl], bound[:, sl])
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+def test_retinanet_fusion_conv_shape(dtype):
+    """f4's second consumer at its own shape: RetinaNet's P2 SHPL followed by
+    slim.conv2d(bev_fused, 256, [3, 3]) -- 256 BEV + 256 pooled image channels in, 256 out, bias + ReLU, no
+    normalizer (retinanet_model.py:320-348) -- on config 6's 176 x 200 BEV grid, 2 frames. Fused == the conv
+    of the materialised bv_fused (bitwise), and two bands of rows within the conv bound of the oracle's
+    double-precision conv of the oracle's bv_fused (bf16: + one bf16 ulp of the result)."""
+    from sparse_pooling_amd import fusion_conv as fc, shpl_map as sm
+    n_frames = 2
+    spec, frames, ib = _batch_map(6, n_frames, 800)
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    Cb, Ci, Co = spec.c_bev, spec.c_img, 256
+    bf = dtype == "bf16"
+    dt = torch.bfloat16 if bf else torch.float32
+    rd = (lambda a: orc.from_bf16_bits(orc.to_bf16_bits(a))) if bf else (lambda a: a)
+    bev = rd(synth.make_features((n_frames, Hb, Wb, Cb), 61))
+    img = rd(synth.make_features((n_frames, Hi, Wi, Ci), 62))
+    w = rd(_weights(Cb + Ci, Co, 63))
+    tb, ti = _t(bev).to(dt), _t(img).to(dt)
+    conv = fc.FusionConv(Cb + Ci, Co, batch_norm=False, bias=True, relu=True, dtype=dt, device=DEV, seed=3)
+    conv.weights = _t(w).to(dt)
+    conv.bias = _t(np.random.default_rng(4).standard_normal(Co).astype(np.float32) * 0.5)
+    bv_fused = sm.pool_img_to_bev(ib.map, ti, tb.shape, bev=tb)
+    y_unf = conv(bv_fused)
+    y_fus = conv.fused(tb, ti, ib.map)
+    torch.cuda.synchronize()
+    assert ib.map.error_bits() == 0
+    assert torch.equal(y_fus, y_unf)
+    _, _, shift = (None if v is None else _np(v) for v in conv._inference_epilogue())
+    for f, fr in enumerate(frames):
+        gen = orc.gen_sparse_pooling_input_avod(fr.points, fr.voxel_indices, fr.P, list(spec.im_size),
+                                                tuple(spec.bv_size))
+        ref = orc.produce_sparse_pooling_input(gen, stride=spec.stride)
+        eb, _ = orc.sparse_pool_layer(bev[f:f + 1], img[f:f + 1], ref["Mij_pool"], ref["M_val"], ref["M_size"],
+                                      ref["img_index_flip_pool"])
+        eb = rd(eb)
+        np.testing.assert_array_equal(_np(bv_fused[f:f + 1].float()), eb)
+        for y0, y1 in ((0, 5), (70, 76)):
+            lo, hi = max(y0 - 1, 0), min(y1 + 1, Hb)
+            band = orc.conv3x3(eb[:, lo:hi], w, None, None, shift, True)
+            bound = _bound(eb[:, lo:hi], w)
+            if bf:
+                bound = bound + np.abs(band) * 2.0 ** -8
+            sl = slice(y0 - lo, y0 - lo + (y1 - y0))
+            _assert_within(y_fus[f:f + 1, y0:y1].float(), band[:, sl], bound[:, sl])
+
+
 def test_fused_conv_noncanonical_map():
     """Shuffled entries, cells with many entries (the run walk), negative
     weights, an empty frame-less corner, odd channel counts (scalar staging)."""

@@ -469,6 +469,55 @@ def test_pipeline_batch_matches_oracle(cfg, dual):
             _close_and_exact(iout[f:f + 1], ei)
 
 
+@pytest.mark.parametrize("cfg,dtype,graph", [(6, "f32", False), (6, "f32", True), (6, "bf16", False),
+                                             (2, "f32", False)])
+def test_split_pipeline_matches_oracle(cfg, dtype, graph):
+    """FusedPipeline(split=True): the pass-through copy beside the index chain, the frame CSR with key ranges
+    (k_csr_frame + k_key_range) and the pooled half written once by the row-keyed pull -- eager and captured
+    in a HIP graph (two replays) -- bitwise the oracle's bv_fused on 3 frames (one with no point)."""
+    from sparse_pooling_amd import pipeline
+    spec = synth.CONFIGS[cfg]
+    frames = [synth.make_frame(spec, seed=60 + f, n_outside=25) for f in range(2)]
+    frames.insert(1, synth.make_frame(synth.FrameSpec(0, spec.im_size, spec.bv_size, spec.stride, spec.c_bev,
+                                                      spec.c_img), seed=1))
+    pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
+    dt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    pl = pipeline.FusedPipeline(3, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev, spec.c_img,
+                                dtype=dt, split=True)
+    assert pl.split and pl.csr.key_range is not None
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    bev = synth.make_features((3, Hb, Wb, spec.c_bev), 3)
+    img = synth.make_features((3, Hi, Wi, spec.c_img), 4)
+    if dt == torch.bfloat16:
+        bev, img = (orc.from_bf16_bits(orc.to_bf16_bits(a)) for a in (bev, img))
+    tb, ti = torch.from_numpy(bev).to(DEV).to(dt), torch.from_numpy(img).to(DEV).to(dt)
+    side = torch.cuda.Stream(device=DEV)
+    chain = torch.cuda.Stream(device=DEV, priority=-1)
+    pl.bv_fused.fill_(float("nan"))  # every element must be written
+    if graph:
+        g = torch.cuda.CUDAGraph()
+        gs = torch.cuda.Stream(device=DEV)
+        gs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.graph(g, stream=gs):
+            pl.step_split(pts, vox, off, P, tb, ti, side, chain)
+        pl.bv_fused.fill_(float("nan"))
+        g.replay()
+        g.replay()
+    else:
+        pl.step_split(pts, vox, off, P, tb, ti, side, chain)
+    torch.cuda.synchronize()
+    assert int(pl.err.item()) == 0
+    out = pl.bv_fused.float().cpu().numpy()
+    for f, fr in enumerate(frames):
+        ref = _oracle_frame(fr, spec.stride)
+        eb, _ = orc.sparse_pool_layer(bev[f:f + 1], img[f:f + 1], ref["Mij_pool"], ref["M_val"], ref["M_size"],
+                                      ref["img_index_flip_pool"])
+        if dt == torch.bfloat16:
+            eb = orc.from_bf16_bits(orc.to_bf16_bits(eb))
+        _close_and_exact(out[f:f + 1], eb)
+
+
 def test_full_size_properties_config5():
     """Config 5 (40k points, 64 channels, both directions) at full size:
     adjointness <pool(x), y> == <x, trans(y)> and the pass-through halves."""
