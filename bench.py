@@ -91,6 +91,9 @@ def parse():
                     help="img->BEV layer: the pass-through copy beside the index chain and the pooled half written once "
                          "by a row-keyed pull after it, on a high-priority stream (FusedPipeline split); auto: on "
                          "for 1 KB halves (config 6)")
+    ap.add_argument("--split-pull", default="once", choices=["once", "rows"],
+                    help="split layer: the pooled half by shpl_pull_once (sparse walk + the empty rows' zeros) or by "
+                         "the row-keyed k_rows (A/B)")
     ap.add_argument("--pixel-cols", action="store_true",
                     help="bucketed config 3: the pixel-keyed CSR keeps ent_col (per-column partials in its pulls) "
                          "instead of the identity-column form")
@@ -431,6 +434,7 @@ def main():
     frames = [synth.make_frame(spec, seed=s, n_outside=200) for s in fids]
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, dev)
     pipeline.FusedPipeline.PIXEL_COLS = args.pixel_cols
+    pipeline.FusedPipeline.SPLIT_ONCE = args.split_pull == "once"
     esz0 = 2 if dtype == torch.bfloat16 else 4
     split = (not dual and not args.rows and not args.no_overlap and
              (args.split == "on" or (args.split == "auto" and min(spec.c_bev, spec.c_img) * esz0 >= 1024)))
@@ -551,7 +555,7 @@ def main():
     if split:
         # the two halves' passes overlap each other and the chain: the layer's window from the first start to
         # the last end (eager), or the replayed step (every kernel of it)
-        layer_ms = sum(max(e[0].elapsed_time(e[1]), e[0].elapsed_time(e[3])) for e in evs) / args_steps_ev
+        layer_ms = sum(max(e[2].elapsed_time(e[1]), e[2].elapsed_time(e[3])) for e in evs) / args_steps_ev
         if replay_step_ms is not None:
             eager_ms, layer_ms = layer_ms, replay_step_ms
     if getattr(pl, "buckets", False) and replay_step_ms is not None:

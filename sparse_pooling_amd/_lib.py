@@ -154,6 +154,7 @@ def _declare(lib):
         "shpl_pull": (i32, pull_args),
         "shpl_pull_dense": (i32, pull_args),
         "shpl_pull_sparse": (i32, pull_args),
+        "shpl_pull_once": (i32, pull_args),
         "shpl_conv3x3_workspace_bytes": (i32, [i32, i32, i64, i64, i64, i64, i64, i64, i32, psz]),
         "shpl_conv3x3": (i32, [i32, i32, i64, i64, p, i64, i64, i64, p, i64, i64, i64,
                                ctypes.POINTER(ShplCsr), p, p, i64, p, p, p, i32, p, i64, p, p, sz, p]),

@@ -328,13 +328,12 @@ __device__ __forceinline__ void store_pooled(const Feat &f, int32_t key, uint32_
 // occupancy), and take every run (no k_sparse_long pass over the capacity); the sums and stores are
 // the same.
 template <typename T, int VEC, bool GROUP, bool SPLIT, bool POW2, bool LIVE>
-__global__ __launch_bounds__(SHPL_BLOCK) void k_sparse(const Feat f, const Ents e, int cpool_shift) {
+__device__ __forceinline__ void sparse_body(const Feat &f, const Ents &e, int cpool_shift, int64_t bid, int64_t nblk) {
     __shared__ int32_t s_off[LIVE ? LIVE_MAX_FRAMES + 1 : 1], s_pre[LIVE ? LIVE_MAX_FRAMES + 1 : 1];
     __shared__ int64_t s_scan[SHPL_BLOCK / 64 + 1];
     const int64_t nnz = e.n;
     const int64_t total = (LIVE ? (int64_t)live_table(e, s_off, s_pre, s_scan) : nnz) * (int64_t)f.cpool;
-    for (int64_t t = (int64_t)blockIdx.x * SHPL_BLOCK + threadIdx.x; t < total;
-         t += (int64_t)gridDim.x * SHPL_BLOCK) {
+    for (int64_t t = bid * SHPL_BLOCK + threadIdx.x; t < total; t += nblk * SHPL_BLOCK) {
         // a shift, not a 64-bit division, when the chunk count is a power of two
         const int64_t l = POW2 ? t >> cpool_shift : t / f.cpool;
         const uint32_t c = (uint32_t)(t - l * f.cpool);
@@ -355,6 +354,41 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse(const Feat f, const Ents 
         float acc[VEC];
         walk_run<T, VEC, GROUP, WALK>(f, e, s, key, c, acc, &b0);
         store_pooled<T, VEC>(f, key, c, acc);
+    }
+}
+
+template <typename T, int VEC, bool GROUP, bool SPLIT, bool POW2, bool LIVE>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_sparse(const Feat f, const Ents e, int cpool_shift) {
+    sparse_body<T, VEC, GROUP, SPLIT, POW2, LIVE>(f, e, cpool_shift, blockIdx.x, gridDim.x);
+}
+
+// shpl_pull_once: the pooled part of every destination row written exactly once, in ONE launch and with no
+// streaming pass before it. Blocks [0, sblocks) run k_sparse's (entry, chunk) walk over every run (the run
+// heads write the occupied rows); the rest zero the rows whose key_range is empty: a wave per ONCE_ROWS rows,
+// one key_range load for all of them, then their zero chunks stored with nothing to wait for. Rows and
+// stores are disjoint between the two parts.
+constexpr int ONCE_ROWS = 16;
+template <typename T, int VEC, bool GROUP, bool POW2>
+__global__ __launch_bounds__(SHPL_BLOCK) void k_once(const Feat f, const Ents e, int cpool_shift,
+                                                     const int32_t *key_range, int64_t n_rows, int64_t sblocks) {
+    if ((int64_t)blockIdx.x < sblocks) {
+        sparse_body<T, VEC, GROUP, false, POW2, false>(f, e, cpool_shift, blockIdx.x, sblocks);
+        return;
+    }
+    typedef Chunk<T, VEC> C;
+    const int lane = threadIdx.x & 63;
+    const int64_t row0 = (((int64_t)blockIdx.x - sblocks) * (SHPL_BLOCK / SHPL_WAVE) + (threadIdx.x >> 6)) * ONCE_ROWS;
+    bool empty = false;
+    if (lane < ONCE_ROWS && row0 + lane < n_rows)
+        empty = key_range[2 * (row0 + lane)] == key_range[2 * (row0 + lane) + 1];
+    const uint64_t mask = __ballot(empty);
+    if (!mask) return;
+    T *out = reinterpret_cast<T *>(f.out);
+    const uint32_t cp = f.cpool, n = ONCE_ROWS * cp;
+    for (uint32_t q = lane; q < n; q += SHPL_WAVE) {
+        const uint32_t r = POW2 ? q >> cpool_shift : q / cp;
+        const uint32_t c = q - r * cp;
+        if ((mask >> r) & 1) C::store_nt(out + ((row0 + r) * f.out_stride + (int64_t)c * VEC), C::zero());
     }
 }
 
@@ -806,6 +840,30 @@ int sparse_tg(const Plan &pl, const Ents &e, int64_t nnz_cap, hipStream_t s) {
     return SHPL_OK;
 }
 
+template <typename T, int VEC, bool GROUP>
+int once_tg(const Plan &pl, const shpl_csr *csr, hipStream_t s) {
+    Ents e{csr->nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_col, csr->ent_val};
+    const int64_t sblocks = csr->nnz_cap > 0 ? grid_for(csr->nnz_cap * (int64_t)pl.f.cpool, SHPL_BLOCK, 1 << 20) : 0;
+    const int64_t zblocks = (pl.n_dst + ONCE_ROWS * (SHPL_BLOCK / SHPL_WAVE) - 1) / (ONCE_ROWS * (SHPL_BLOCK / SHPL_WAVE));
+    if (sblocks + zblocks > 0x7fffffffLL) return SHPL_ERR_BAD_SHAPE;
+    int shift = -1;
+    for (int k = 0; k < 31; ++k)
+        if (pl.f.cpool == (1u << k)) shift = k;
+    if (shift >= 0)
+        hipLaunchKernelGGL((k_once<T, VEC, GROUP, true>), dim3((unsigned)(sblocks + zblocks)), dim3(SHPL_BLOCK), 0, s,
+                           pl.f, e, shift, (const int32_t *)csr->key_range, pl.n_dst, sblocks);
+    else
+        hipLaunchKernelGGL((k_once<T, VEC, GROUP, false>), dim3((unsigned)(sblocks + zblocks)), dim3(SHPL_BLOCK), 0,
+                           s, pl.f, e, shift, (const int32_t *)csr->key_range, pl.n_dst, sblocks);
+    SHPL_LAUNCH_CHECK();
+    return SHPL_OK;
+}
+
+template <typename T, int VEC>
+int once_t(const Plan &pl, const shpl_csr *csr, bool group, hipStream_t s) {
+    return group ? once_tg<T, VEC, true>(pl, csr, s) : once_tg<T, VEC, false>(pl, csr, s);
+}
+
 template <typename T, int VEC>
 int sparse_t(const Plan &pl, const shpl_csr *csr, bool group, hipStream_t s) {
     const bool live = csr->n_frames > 0 && csr->frame_off && csr->frame_nnz;
@@ -899,6 +957,17 @@ extern "C" int shpl_pull_dense(SHPL_PULL_ARGS) {
 extern "C" int shpl_pull_sparse(SHPL_PULL_ARGS) {
     SHPL_PLAN();
     return sparse(pl, csr, direction, (hipStream_t)stream);
+}
+
+extern "C" int shpl_pull_once(SHPL_PULL_ARGS) {
+    SHPL_PLAN();
+    if (mode != SHPL_OUT_POOL || !csr->key_range) return SHPL_ERR_ARG;
+    if (pl.n_dst == 0 || pl.f.cpool == 0) return SHPL_OK;
+    const bool group = grouped(csr, direction);
+    hipStream_t s = (hipStream_t)stream;
+    if (pl.dtype == SHPL_F32)
+        return pl.v16 ? once_t<float, 4>(pl, csr, group, s) : once_t<float, 1>(pl, csr, group, s);
+    return pl.v16 ? once_t<uint16_t, 8>(pl, csr, group, s) : once_t<uint16_t, 1>(pl, csr, group, s);
 }
 
 // ---------------------------------------------------------------- paired pulls

@@ -28,6 +28,9 @@ class FusedPipeline:
     ROWS_FRAMES, ROWS_MAX_KEYS, ROWS_MAX_CAP = 32, 65536, 1 << 24
     # bucketed pixel-keyed CSRs with ent_col (per-column partials in the pulls; A/B of the identity-column form)
     PIXEL_COLS = False
+    # split: the pooled half by shpl_pull_once (k_sparse's walk + the empty rows' zeros, one launch); False: the
+    # row-keyed k_rows (1.11 ms per 64 frames at config 6, a wave per 1 KB row: latency-bound)
+    SPLIT_ONCE = True
 
     def __init__(self, n_frames, max_points_per_frame, total_points, im_size, bv_size, stride,
                  c_bev, c_img, dtype=torch.float32, device="cuda", dual=False, rows=None, live=False,
@@ -268,9 +271,9 @@ class FusedPipeline:
         row-keyed pull over the cell CSR's key ranges (SHPL_OUT_POOL into the pooled columns)."""
         esz = self.bv_fused.element_size()
         out = ctypes.c_void_p(self.bv_fused.data_ptr() + self.Cb * esz)
-        L.check(self._lib.shpl_pull(L.BY_CELL, L.dtype_code(self.bv_fused), self.csr.ref(), L.ptr(img), self.Ci, 0,
-                                    self.Ci, None, 0, 0, 0, L.OUT_POOL, out, self.Cb + self.Ci,
-                                    L.stream_of(self.dev)), "shpl_pull")
+        fn = self._lib.shpl_pull_once if self.SPLIT_ONCE else self._lib.shpl_pull
+        L.check(fn(L.BY_CELL, L.dtype_code(self.bv_fused), self.csr.ref(), L.ptr(img), self.Ci, 0,
+                   self.Ci, None, 0, 0, 0, L.OUT_POOL, out, self.Cb + self.Ci, L.stream_of(self.dev)), "shpl_pull")
 
     def step_split(self, points, voxels, point_offsets, P, bev, img, side, chain, events=None):
         """split: the pass-through copy on `side`, the index chain and then the pooled half on `chain` (a
@@ -279,12 +282,8 @@ class FusedPipeline:
         main = torch.cuda.current_stream(self.dev)
         side.wait_stream(main)
         chain.wait_stream(main)
-        with torch.cuda.stream(side):
-            if events:
-                events[0].record(side)
-            self._pass_copies(bev, img, ("cell",))
-            if events:
-                events[1].record(side)
+        # the chain is issued (and, in a captured graph, its nodes created) first: its first launch is
+        # dispatched before the copy's workgroups fill the chip
         with torch.cuda.stream(chain):
             if events:
                 events[2].record(chain)
@@ -293,6 +292,12 @@ class FusedPipeline:
             self._pooled_half(img)
             if events:
                 events[3].record(chain)
+        with torch.cuda.stream(side):
+            if events:
+                events[0].record(side)
+            self._pass_copies(bev, img, ("cell",))
+            if events:
+                events[1].record(side)
         main.wait_stream(side)
         main.wait_stream(chain)
 

@@ -90,9 +90,15 @@ def test_argument_validation_is_host_side():
     # a pixel-keyed CSR without ent_col only when marked as one column per entry (SHPL_CSR_IDENTITY_COLS):
     # otherwise the pulls would sum without TF's per-column partials
     pix = L.ShplCsr(256, 256, 256, None, 100, 10)
-    for fn in (lib.shpl_pull, lib.shpl_pull_dense, lib.shpl_pull_sparse):
+    for fn in (lib.shpl_pull, lib.shpl_pull_dense, lib.shpl_pull_sparse, lib.shpl_pull_once):
         assert fn(L.BY_PIXEL, L.F32, ctypes.byref(pix), P, 32, 0, 32, P, 32, 0, 32, L.OUT_CONCAT, P, 64,
                   N) == L.ERR_ARG
+    # shpl_pull_once: SHPL_OUT_POOL over a CSR with key_range only
+    assert lib.shpl_pull_once(L.BY_CELL, L.F32, ctypes.byref(csr), P, 32, 0, 32, N, 0, 0, 0, L.OUT_POOL, P, 32,
+                              N) == L.ERR_ARG  # no key_range
+    kr = L.ShplCsr(256, 256, 256, None, 100, 10, 256)
+    assert lib.shpl_pull_once(L.BY_CELL, L.F32, ctypes.byref(kr), P, 32, 0, 32, P, 32, 0, 32, L.OUT_CONCAT, P, 64,
+                              N) == L.ERR_ARG  # not SHPL_OUT_POOL
     # the forward conv's row-streaming predicate (shpl_conv3x3_rows_form): f32 never, bf16 at 32 + 32 channels
     # without statistics yes, with training statistics over 32 + 16 pooled channels no (the tiled kernel)
     rf = ctypes.c_int(-1)

@@ -469,13 +469,15 @@ def test_pipeline_batch_matches_oracle(cfg, dual):
             _close_and_exact(iout[f:f + 1], ei)
 
 
-@pytest.mark.parametrize("cfg,dtype,graph", [(6, "f32", False), (6, "f32", True), (6, "bf16", False),
-                                             (2, "f32", False)])
-def test_split_pipeline_matches_oracle(cfg, dtype, graph):
+@pytest.mark.parametrize("cfg,dtype,graph,once", [(6, "f32", False, True), (6, "f32", True, True),
+                                                  (6, "bf16", False, True), (2, "f32", False, True),
+                                                  (6, "f32", False, False), (2, "bf16", True, False)])
+def test_split_pipeline_matches_oracle(cfg, dtype, graph, once, monkeypatch):
     """FusedPipeline(split=True): the pass-through copy beside the index chain, the frame CSR with key ranges
-    (k_csr_frame + k_key_range) and the pooled half written once by the row-keyed pull -- eager and captured
+    (k_csr_frame + k_key_range) and the pooled half written once (shpl_pull_once, or the row-keyed k_rows) -- eager and captured
     in a HIP graph (two replays) -- bitwise the oracle's bv_fused on 3 frames (one with no point)."""
     from sparse_pooling_amd import pipeline
+    monkeypatch.setattr(pipeline.FusedPipeline, "SPLIT_ONCE", once)
     spec = synth.CONFIGS[cfg]
     frames = [synth.make_frame(spec, seed=60 + f, n_outside=25) for f in range(2)]
     frames.insert(1, synth.make_frame(synth.FrameSpec(0, spec.im_size, spec.bv_size, spec.stride, spec.c_bev,
