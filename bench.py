@@ -107,6 +107,8 @@ def parse():
                          "else 1 (config 2: no change, profiles/r03_graph_steps_ab.log)")
     ap.add_argument("--no-pool-report", action="store_true",
                     help="config 2: skip the separate pool_fwd measurement (PMC passes count the step's launches only)")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the step in a HIP graph even where the default is eager (the split step)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step eagerly instead of replaying one captured HIP graph of it")
     ap.add_argument("--workload", default="layer", choices=["layer", "frames", "conv"],
@@ -496,7 +498,12 @@ def main():
     # the timed loop replays it, so host launch gaps leave the step. Kernel
     # durations for the roofline come from the same step run eagerly with events.
     graph, graph_note = None, None
-    if not args.no_graph:
+    if split and not args.graph:
+        # a captured graph of the split step ran its two branches nearly in series (the chain's nodes start
+        # after the copy has filled the chip: no stream priority inside a graph): 1.77 vs 1.40 ms eager at
+        # config 6 (profiles/r05_c6b_ab.log); --graph forces the capture
+        graph_note = "split step: eager launches (the chain's high-priority stream; a captured graph serialised it)"
+    elif not args.no_graph:
         try:
             gstream = torch.cuda.Stream(device=dev)
             gstream.wait_stream(torch.cuda.current_stream(dev))

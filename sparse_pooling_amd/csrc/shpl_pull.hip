@@ -367,20 +367,32 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse(const Feat f, const Ents 
 // heads write the occupied rows); the rest zero the rows whose key_range is empty: a wave per ONCE_ROWS rows,
 // one key_range load for all of them, then their zero chunks stored with nothing to wait for. Rows and
 // stores are disjoint between the two parts.
-constexpr int ONCE_ROWS = 16;
+#ifndef SHPL_ONCE_ROWS
+#define SHPL_ONCE_ROWS 16
+#endif
+#ifndef SHPL_ONCE_ZERO_FIRST
+#define SHPL_ONCE_ZERO_FIRST 0  // 1: the zeroing blocks first (A/B)
+#endif
+constexpr int ONCE_ROWS = SHPL_ONCE_ROWS;
 template <typename T, int VEC, bool GROUP, bool POW2>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_once(const Feat f, const Ents e, int cpool_shift,
                                                      const int32_t *key_range, int64_t n_rows, int64_t sblocks) {
-    if ((int64_t)blockIdx.x < sblocks) {
-        sparse_body<T, VEC, GROUP, false, POW2, false>(f, e, cpool_shift, blockIdx.x, sblocks);
+    const int64_t zblocks = (int64_t)gridDim.x - sblocks;
+    const int64_t zb = SHPL_ONCE_ZERO_FIRST ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - sblocks;
+    if (zb < 0 || zb >= zblocks) {
+        sparse_body<T, VEC, GROUP, false, POW2, false>(f, e, cpool_shift,
+                                                       SHPL_ONCE_ZERO_FIRST ? zb - zblocks : (int64_t)blockIdx.x,
+                                                       sblocks);
         return;
     }
     typedef Chunk<T, VEC> C;
     const int lane = threadIdx.x & 63;
-    const int64_t row0 = (((int64_t)blockIdx.x - sblocks) * (SHPL_BLOCK / SHPL_WAVE) + (threadIdx.x >> 6)) * ONCE_ROWS;
+    const int64_t row0 = (zb * (SHPL_BLOCK / SHPL_WAVE) + (threadIdx.x >> 6)) * ONCE_ROWS;
     bool empty = false;
-    if (lane < ONCE_ROWS && row0 + lane < n_rows)
-        empty = key_range[2 * (row0 + lane)] == key_range[2 * (row0 + lane) + 1];
+    if (lane < ONCE_ROWS && row0 + lane < n_rows) {
+        const int2 kr = *reinterpret_cast<const int2 *>(key_range + 2 * (row0 + lane));
+        empty = kr.x == kr.y;
+    }
     const uint64_t mask = __ballot(empty);
     if (!mask) return;
     T *out = reinterpret_cast<T *>(f.out);
