@@ -35,6 +35,7 @@
 
 #include "shpl_common.h"
 #include "shpl_conv_rows.h"
+#include "shpl_conv_wide.h"
 
 namespace shpl {
 namespace {
@@ -1560,11 +1561,18 @@ struct ConvPlan {
     bool rows;
     int band, n_bands, wpr;
     size_t occ_bytes, cmp_bytes, junk_bytes;
+    // k_conv_wide (bf16, input chunks of 64 channels, whole 256-channel output blocks, no statistics); pooled:
+    // the pooled map materialised in the workspace (map_bytes) by shpl_pull first
+    bool wide;
+    size_t map_bytes;
     int64_t pool_cap;
 };
 
 #ifndef SHPL_CONV_ROWS
 #define SHPL_CONV_ROWS 1  // 0: the tiled kernel for every forward (A/B builds)
+#endif
+#ifndef SHPL_CONV_WIDE
+#define SHPL_CONV_WIDE 1  // 0: wide bf16 convs on the tiled kernel (A/B builds)
 #endif
 #ifndef SHPL_ROWS_BAND
 #define SHPL_ROWS_BAND 0  // 0: about 60 rows, equal bands (k_conv_rows stages band + 2 rows, at most 64)
@@ -1615,7 +1623,16 @@ int conv_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_
     pl->pool_cap = pool_cap;
     pl->cmp_bytes = pl->rows && pooled ? align_up((size_t)pool_cap * c_b * esz, 256) : 0;
     pl->junk_bytes = pl->rows ? 32 * NCO * 2 : 0;
-    pl->total = pl->wp_bytes + pl->rp_bytes + pl->part_bytes + pl->occ_bytes + pl->cmp_bytes + pl->junk_bytes;
+    pl->wide = SHPL_CONV_WIDE && dtype == SHPL_BF16 && !stats && !pl->rows && h > 0 && w > 0 &&
+               wide::supported(c_a, c_b, c_out) && (int64_t)n_frames * h * w * (c_b > 0 ? c_b : 1) < (1LL << 40);
+    pl->map_bytes = 0;
+    if (pl->wide) {
+        const size_t wb = align_up(wide::packed_bytes(c_a, c_b, c_out), 256);
+        if (wb > pl->wp_bytes) pl->wp_bytes = wb;
+        pl->map_bytes = pooled ? align_up((size_t)n_frames * h * w * c_b * 2, 256) : 0;
+    }
+    pl->total = pl->wp_bytes + pl->rp_bytes + pl->part_bytes + pl->occ_bytes + pl->cmp_bytes + pl->junk_bytes +
+                pl->map_bytes;
     return SHPL_OK;
 }
 
@@ -1683,9 +1700,48 @@ bool rows_forward(const ConvPlan &pl, const ConvArgs &a, bool pooled, bool stats
            (!stats || (a.act == 0 && rows::supported_st(pl.qa + pl.qb, pl.qa, pooled)));
 }
 
+// The wide bf16 form (k_conv_wide): pooled, the pooled map first into the workspace's last region by
+// shpl_pull (the same arithmetic as the tiled staging: the conv of [a || map] is the fused conv's).
+int conv_wide_launch(const ConvPlan &pl, const ConvArgs &a, const shpl_csr *pool, const void *w, hipStream_t s) {
+    wide::WideArgs r = {};
+    r.a = reinterpret_cast<const uint16_t *>(a.a) + a.a_off;
+    r.a_stride = a.a_stride;
+    r.c_a = a.c_a;
+    r.c_b = a.c_b;
+    if (pool) {
+        uint16_t *map = reinterpret_cast<uint16_t *>(reinterpret_cast<uint8_t *>(const_cast<void *>(a.wp)) + pl.total -
+                                                     pl.map_bytes);
+        const int rc = shpl_pull(SHPL_BY_CELL, SHPL_BF16, pool, a.b, a.b_stride, a.b_off, a.c_b, nullptr, 0, 0, 0,
+                                 SHPL_OUT_POOL, map, a.c_b, s);
+        if (rc) return rc;
+        r.b = map;
+        r.b_stride = a.c_b;
+    } else {
+        r.b = a.c_b > 0 ? reinterpret_cast<const uint16_t *>(a.b) + a.b_off : nullptr;
+        r.b_stride = a.b_stride;
+    }
+    r.n_frames = a.n_frames;
+    r.h = a.h;
+    r.w = a.w;
+    r.center = a.center;
+    r.scale = a.scale;
+    r.shift = a.shift;
+    r.act = a.act;
+    r.out = reinterpret_cast<uint16_t *>(a.out);
+    r.out_stride = a.out_stride;
+    r.c_out = a.c_out;
+    return wide::launch(r, reinterpret_cast<const uint16_t *>(w),
+                        reinterpret_cast<uint16_t *>(const_cast<void *>(a.wp)), s);
+}
+
 template <typename T>
 int conv_launch(const ConvPlan &pl, ConvArgs &a, bool pooled, bool stats, const void *w, const int64_t *frame_off,
-                double *d_stats, hipStream_t s, int transpose = 0) {
+                double *d_stats, hipStream_t s, int transpose = 0, const shpl_csr *pool = nullptr) {
+    if constexpr (sizeof(T) == 2) {
+        if (pl.wide && !stats && !transpose && !a.out2 && a.vec_a && (a.c_b == 0 || a.vec_b) && a.vec_out &&
+            a.n_frames > 0 && (!pooled || pool))
+            return conv_wide_launch(pl, a, pooled ? pool : nullptr, w, s);
+    }
     T *wp = reinterpret_cast<T *>(const_cast<void *>(a.wp));
     const int64_t wtot = (int64_t)pl.n_cob * (pl.qa + pl.qb) * W_ROWS * Elem<T>::CK;
     hipLaunchKernelGGL(k_pack_w<T>, dim3(grid_for(wtot, SHPL_BLOCK, 4096)), dim3(SHPL_BLOCK), 0, s,
@@ -1831,7 +1887,7 @@ extern "C" int shpl_conv3x3(int dtype, int n_frames, int64_t h, int64_t w, const
     if (rc || empty) return rc;
     hipStream_t s = (hipStream_t)stream;
     if (dtype == SHPL_F32) return conv_launch<float>(pl, a, pooled, stats, d_weights, d_frame_off, d_stats, s);
-    return conv_launch<uint16_t>(pl, a, pooled, stats, d_weights, d_frame_off, d_stats, s);
+    return conv_launch<uint16_t>(pl, a, pooled, stats, d_weights, d_frame_off, d_stats, s, 0, pool);
 }
 
 extern "C" int shpl_conv3x3_rows_form(int dtype, int n_frames, int64_t h, int64_t w, const void *d_a,

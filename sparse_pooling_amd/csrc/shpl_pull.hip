@@ -371,7 +371,7 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse(const Feat f, const Ents 
 #define SHPL_ONCE_ROWS 16
 #endif
 #ifndef SHPL_ONCE_ZERO_FIRST
-#define SHPL_ONCE_ZERO_FIRST 0  // 1: the zeroing blocks first (A/B)
+#define SHPL_ONCE_ZERO_FIRST 1  // the zeroing blocks first: 1.401-1.404 vs 1.408-1.410 ms at config 6 (profiles/r05_once_ab.log)
 #endif
 constexpr int ONCE_ROWS = SHPL_ONCE_ROWS;
 template <typename T, int VEC, bool GROUP, bool POW2>

@@ -212,6 +212,40 @@ def test_retinanet_fusion_conv_shape(dtype):
             _assert_within(y_fus[f:f + 1, y0:y1].float(), band[:, sl], bound[:, sl])
 
 
+@pytest.mark.parametrize("shape", [(2, 17, 33, 128, 64, 256, "relu"), (1, 16, 16, 64, 64, 512, "none"),
+                                   (1, 21, 9, 192, 0, 256, "bn"), (3, 5, 40, 64, 128, 256, "relu")])
+def test_bf16_wide_conv_dense(shape):
+    """The wide bf16 kernel (k_conv_wide: input chunks of 64 channels, 256-channel output blocks): partial
+    16 x 16 tiles at every edge, one and two sources (== their concat, bitwise), two output blocks, the
+    epilogue with and without center / scale / shift and ReLU, against the oracle's double-precision conv
+    (bound: the f32 accumulation term + one bf16 ulp of the result)."""
+    from sparse_pooling_amd import fusion_conv as fc
+    B, H, W, ca, cb, co, epi = shape
+    rd = lambda a: orc.from_bf16_bits(orc.to_bf16_bits(a))  # noqa: E731
+    a = rd(synth.make_features((B, H, W, ca), 71))
+    b = rd(synth.make_features((B, H, W, cb), 72)) if cb else None
+    w = rd(_weights(ca + cb, co, 73))
+    rng = np.random.default_rng(74)
+    center = scale = shift = None
+    if epi == "bn":
+        center = rng.standard_normal(co).astype(np.float32) * 0.1
+        scale = rng.uniform(0.5, 2.0, co).astype(np.float32)
+    if epi != "none":
+        shift = rng.standard_normal(co).astype(np.float32) * 0.5
+    relu = epi != "none"
+    ta, tw = _bf16(a), _bf16(w)
+    tb = _bf16(b) if cb else None
+    f32 = lambda v: None if v is None else _t(v)  # noqa: E731
+    y = fc.conv3x3(ta, tw, b=tb, center=f32(center), scale=f32(scale), shift=f32(shift), relu=relu)
+    x = np.concatenate([a, b], -1) if cb else a
+    if cb:  # two sources == one concatenated source, bitwise (the same K order: 64-channel chunks)
+        y1 = fc.conv3x3(_bf16(x), tw, center=f32(center), scale=f32(scale), shift=f32(shift), relu=relu)
+        assert torch.equal(y, y1)
+    ref = orc.conv3x3(x, w, center, scale, shift, relu)
+    bound = _bound(x, w, scale) + np.abs(ref) * 2.0 ** -8
+    _assert_within(y.float(), ref, bound)
+
+
 def test_fused_conv_noncanonical_map():
     """Shuffled entries, cells with many entries (the run walk), negative
     weights, an empty frame-less corner, odd channel counts (scalar staging)."""
