@@ -45,6 +45,16 @@ constexpr int HW_PER_WAVE = (HALO_DMAS + WAVES - 1) / WAVES;  // halo DMAs a wav
 constexpr int WD_PER_WAVE = W_DMAS / WAVES;                     // weight DMAs a wave issues per step (4)
 static_assert(HW_PER_WAVE <= 9, "a chunk's halo DMAs spread one per tap step");
 
+#ifndef SHPL_WIDE_PROBE
+// timing probes (wrong results): 1 no DMAs in the K loop, 2 no barrier in it, 3 no MFMAs
+#define SHPL_WIDE_PROBE 0
+#endif
+#ifndef SHPL_WIDE_VMCNT
+// 1: a step waits for its weight DMAs only (vmcnt(1)); its halo DMA may land during the next step, except at
+// a chunk's last tap (vmcnt(0))
+#define SHPL_WIDE_VMCNT 1
+#endif
+
 __device__ u32x4 g_wide_zero;  // the LDS-DMA source of pieces outside the map
 
 // One LDS-DMA of 16 bytes per lane (lane k's piece lands at dst + 16 k), hidden from the compiler in inline
@@ -175,20 +185,30 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
 #pragma unroll
             for (int i = 0; i < MI; ++i) {
                 // the next step's DMAs among the MFMAs: weights in the first K step, the halo in the second
-                if (ks == 0) issue_w(s_next, i);
+                if (ks == 0 && SHPL_WIDE_PROBE != 1) issue_w(s_next, i);
                 if (ks == 1 && i == 0) {
                     // this wave's halo DMA WAVES t + wave (past the wave's list: its last one again)
                     int k = WAVES * t + wave;
                     k = k < HALO_DMAS ? k : WAVES * ((HALO_DMAS - 1 - wave) / WAVES) + wave;
-                    issue_halo(q_next, k);
+                    if (SHPL_WIDE_PROBE != 1) issue_halo(q_next, k);
                 }
 #pragma unroll
-                for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+                for (int j = 0; j < 8; ++j) {
+                    if (SHPL_WIDE_PROBE == 3)
+                        acc[i][j][0] += (float)av[i][0] * (float)bv[j][0];
+                    else
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+                }
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        if (SHPL_WIDE_VMCNT && t != 8)
+            asm volatile("s_waitcnt vmcnt(1)" ::: "memory");  // the halo DMA issued last may stay in flight
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (SHPL_WIDE_PROBE != 2) __syncthreads();
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
 
     // epilogue: lane (px = tile row 8 wm + j, column l16; channels wn*64 + 16 i + 4 kp .. + 3) -> LDS
     // [pixel][256 channels] bf16, then whole pixel rows out
