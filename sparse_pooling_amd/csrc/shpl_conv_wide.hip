@@ -32,8 +32,13 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int TH = 16, TW = 16;                        // output tile
 constexpr int HH = TH + 2, HW = TW + 2, HPIX = HH * HW;  // 18 x 18 halo
-constexpr int BLOCK = 512, WAVES = BLOCK / 64;
-constexpr int MI = NT / (WAVES / 2) / 16;              // 16-channel tiles per wave (4)
+#ifndef SHPL_WIDE_WAVES
+// 4: one wave per SIMD, 128 channels x 128 pixels each (256 accumulator registers, in AGPRs by inline-asm
+// MFMAs); 8: two per SIMD, 64 x 128 each (128 registers)
+#define SHPL_WIDE_WAVES 4
+#endif
+constexpr int WAVES = SHPL_WIDE_WAVES, BLOCK = 64 * WAVES;
+constexpr int MI = NT / (WAVES / 2) / 16;              // 16-channel tiles per wave (8 / 4)
 constexpr int HALO_DMAS = (HPIX * 8 + 63) / 64;        // 41 DMAs of 1 KB (the last one part padding)
 constexpr int HALO_BYTES = HALO_DMAS * 1024;
 constexpr int W_DMAS = NT * 8 / 64;                    // 32
@@ -41,16 +46,17 @@ constexpr int W_BYTES = NT * KC * 2;                   // 32 KB per (chunk, tap)
 constexpr int LDS_BYTES = 2 * HALO_BYTES + 2 * W_BYTES;
 constexpr int OPITCH = NT * 2 + 16;                    // epilogue transpose: 528 B per pixel
 static_assert(TH * TW * OPITCH <= LDS_BYTES, "epilogue tile fits the staging buffers");
-constexpr int HW_PER_WAVE = (HALO_DMAS + WAVES - 1) / WAVES;  // halo DMAs a wave issues per chunk (at most: 6)
-constexpr int WD_PER_WAVE = W_DMAS / WAVES;                     // weight DMAs a wave issues per step (4)
-static_assert(HW_PER_WAVE <= 9, "a chunk's halo DMAs spread one per tap step");
+constexpr int HW_PER_WAVE = (HALO_DMAS + WAVES - 1) / WAVES;  // halo DMAs a wave issues per chunk (11 / 6)
+constexpr int HS = (HW_PER_WAVE + 8) / 9;                       // halo DMA slots per step (2 / 1)
+constexpr int WD_PER_WAVE = W_DMAS / WAVES;                     // weight DMAs a wave issues per step (8 / 4)
+static_assert(WD_PER_WAVE <= MI && HS <= MI, "the DMAs of a step ride the MFMA groups");
 
 #ifndef SHPL_WIDE_PROBE
 // timing probes (wrong results): 1 no DMAs in the K loop, 2 no barrier in it, 3 no MFMAs
 #define SHPL_WIDE_PROBE 0
 #endif
 #ifndef SHPL_WIDE_VMCNT
-// 1: a step waits for its weight DMAs only (vmcnt(1)); its halo DMA may land during the next step, except at
+// 1: a step waits for its weight DMAs only (vmcnt(HS)); its halo DMAs may land during the next step, except at
 // a chunk's last tap (vmcnt(0))
 #define SHPL_WIDE_VMCNT 1
 #endif
@@ -65,6 +71,17 @@ __device__ u32x4 g_wide_zero;  // the LDS-DMA source of pieces outside the map
 __device__ __forceinline__ void dma(const void *src, uint8_t *dst) {
     const uint32_t lds = (uint32_t)(uintptr_t)dst;
     asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(lds) : "memory");
+}
+
+// acc += A B on v_mfma_f32_16x16x32_bf16. One wave per SIMD: in inline asm with the accumulator in AGPRs (the
+// compiler otherwise keeps the 256 accumulators in VGPRs and spills the operands to AGPRs around every MFMA);
+// volatile, so the MFMAs keep their order among the DMAs; the hazard before reading AGPRs back is the
+// epilogue's (s_nops after the loop).
+__device__ __forceinline__ void mfma(f32x4 &acc, const bf16x8 &a, const bf16x8 &b) {
+    if constexpr (WAVES == 4)
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+    else
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
 }
 
 __device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t n) {
@@ -94,7 +111,7 @@ __global__ __launch_bounds__(256) void k_pack_wide(const uint16_t *w, int c_in, 
     }
 }
 
-__global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
+__global__ __launch_bounds__(BLOCK, WAVES == 4 ? 1 : 2) void k_conv_wide(const WideArgs p) {
     __shared__ __attribute__((aligned(1024))) uint8_t s_lds[LDS_BYTES];
     __shared__ __attribute__((aligned(16))) float s_par[2][NT];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -153,7 +170,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 
-    // fragment read offsets: weights -- output channel wn*64 + 16 i + (lane & 15), K piece 4 ks + lane / 16
+    // fragment read offsets: weights -- output channel wn*16*MI + 16 i + (lane & 15), K piece 4 ks + lane / 16
     // (its row key: lane & 7); pixels -- tile row 8 wm + j, column lane & 15 (+ kx), the same K piece
     const int l16 = lane & 15, kp = lane >> 4;
     uint32_t a_off[2];
@@ -185,10 +202,10 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
 #pragma unroll
             for (int i = 0; i < MI; ++i) {
                 // the next step's DMAs among the MFMAs: weights in the first K step, the halo in the second
-                if (ks == 0 && SHPL_WIDE_PROBE != 1) issue_w(s_next, i);
-                if (ks == 1 && i == 0) {
-                    // this wave's halo DMA WAVES t + wave (past the wave's list: its last one again)
-                    int k = WAVES * t + wave;
+                if (ks == 0 && i < WD_PER_WAVE && SHPL_WIDE_PROBE != 1) issue_w(s_next, i);
+                if (ks == 1 && i < HS) {
+                    // this wave's halo DMA WAVES (t + 9 i) + wave (past the wave's list: its last one again)
+                    int k = WAVES * (t + 9 * i) + wave;
                     k = k < HALO_DMAS ? k : WAVES * ((HALO_DMAS - 1 - wave) / WAVES) + wave;
                     if (SHPL_WIDE_PROBE != 1) issue_halo(q_next, k);
                 }
@@ -197,18 +214,20 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
                     if (SHPL_WIDE_PROBE == 3)
                         acc[i][j][0] += (float)av[i][0] * (float)bv[j][0];
                     else
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+                        mfma(acc[i][j], av[i], bv[j]);
                 }
             }
         }
         if (SHPL_WIDE_VMCNT && t != 8)
-            asm volatile("s_waitcnt vmcnt(1)" ::: "memory");  // the halo DMA issued last may stay in flight
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HS) : "memory");  // the halo DMAs issued last may stay in flight
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (SHPL_WIDE_PROBE != 2) __syncthreads();
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    // the last MFMAs' results before their AGPRs are read (the hazard the compiler cannot see in the asm)
+    if constexpr (WAVES == 4) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 
     // epilogue: lane (px = tile row 8 wm + j, column l16; channels wn*64 + 16 i + 4 kp .. + 3) -> LDS
     // [pixel][256 channels] bf16, then whole pixel rows out
