@@ -1563,7 +1563,7 @@ struct ConvPlan {
     size_t occ_bytes, cmp_bytes, junk_bytes;
     // k_conv_wide (bf16, input chunks of 64 channels, whole 256-channel output blocks, no statistics); pooled:
     // the pooled map materialised in the workspace (map_bytes) by shpl_pull first
-    bool wide;
+    bool wide, wide_cmp;
     size_t map_bytes;
     int64_t pool_cap;
 };
@@ -1626,10 +1626,17 @@ int conv_plan(int dtype, int n_frames, int64_t h, int64_t w, int64_t c_a, int64_
     pl->wide = SHPL_CONV_WIDE && dtype == SHPL_BF16 && !stats && !pl->rows && h > 0 && w > 0 &&
                wide::supported(c_a, c_b, c_out) && (int64_t)n_frames * h * w * (c_b > 0 ? c_b : 1) < (1LL << 40);
     pl->map_bytes = 0;
+    pl->wide_cmp = false;
     if (pl->wide) {
         const size_t wb = align_up(wide::packed_bytes(c_a, c_b, c_out), 256);
         if (wb > pl->wp_bytes) pl->wp_bytes = wb;
-        pl->map_bytes = pooled ? align_up((size_t)n_frames * h * w * c_b * 2, 256) : 0;
+        // pooled: the occupancy words + prefixes and the compact pooled runs (wide::prep), read by the halo
+        // staging -- or, past the occupancy table's limits, the pooled map materialised by shpl_pull
+        pl->wide_cmp = pooled && h * pl->wpr <= rows::OCC_MAX_WORDS && pool_cap * c_b * 2 < (1LL << 31);
+        if (pooled && pl->wide_cmp)
+            pl->map_bytes = 2 * align_up((size_t)n_frames * h * pl->wpr * 4, 256) + align_up((size_t)pool_cap * c_b * 2, 256);
+        else if (pooled)
+            pl->map_bytes = align_up((size_t)n_frames * h * w * c_b * 2, 256);
     }
     pl->total = pl->wp_bytes + pl->rp_bytes + pl->part_bytes + pl->occ_bytes + pl->cmp_bytes + pl->junk_bytes +
                 pl->map_bytes;
@@ -1702,13 +1709,29 @@ bool rows_forward(const ConvPlan &pl, const ConvArgs &a, bool pooled, bool stats
 
 // The wide bf16 form (k_conv_wide): pooled, the pooled map first into the workspace's last region by
 // shpl_pull (the same arithmetic as the tiled staging: the conv of [a || map] is the fused conv's).
-int conv_wide_launch(const ConvPlan &pl, const ConvArgs &a, const shpl_csr *pool, const void *w, hipStream_t s) {
+int conv_wide_launch(const ConvPlan &pl, const ConvArgs &a, const shpl_csr *pool, const int64_t *frame_off,
+                     const void *w, hipStream_t s) {
     wide::WideArgs r = {};
     r.a = reinterpret_cast<const uint16_t *>(a.a) + a.a_off;
     r.a_stride = a.a_stride;
     r.c_a = a.c_a;
     r.c_b = a.c_b;
-    if (pool) {
+    if (pool && pl.wide_cmp) {
+        uint8_t *ws = reinterpret_cast<uint8_t *>(const_cast<void *>(a.wp)) + pl.total - pl.map_bytes;
+        const size_t ob = align_up((size_t)a.n_frames * a.h * pl.wpr * 4, 256);
+        uint32_t *occ = reinterpret_cast<uint32_t *>(ws);
+        int32_t *occ_base = reinterpret_cast<int32_t *>(ws + ob);
+        uint16_t *cmp = reinterpret_cast<uint16_t *>(ws + 2 * ob);
+        const int rc = wide::prep(a.n_frames, a.h, a.w, pl.wpr, pool->ent_dst, pool->ent_src, pool->ent_val,
+                                  pool->nnz_cap, frame_off, reinterpret_cast<const uint16_t *>(a.b), a.b_stride, a.b_off,
+                                  a.c_b, occ, occ_base, cmp, s);
+        if (rc) return rc;
+        r.occ = occ;
+        r.occ_base = occ_base;
+        r.frame_off = frame_off;
+        r.cmp = cmp;
+        r.wpr = pl.wpr;
+    } else if (pool) {
         uint16_t *map = reinterpret_cast<uint16_t *>(reinterpret_cast<uint8_t *>(const_cast<void *>(a.wp)) + pl.total -
                                                      pl.map_bytes);
         const int rc = shpl_pull(SHPL_BY_CELL, SHPL_BF16, pool, a.b, a.b_stride, a.b_off, a.c_b, nullptr, 0, 0, 0,
@@ -1740,7 +1763,7 @@ int conv_launch(const ConvPlan &pl, ConvArgs &a, bool pooled, bool stats, const 
     if constexpr (sizeof(T) == 2) {
         if (pl.wide && !stats && !transpose && !a.out2 && a.vec_a && (a.c_b == 0 || a.vec_b) && a.vec_out &&
             a.n_frames > 0 && (!pooled || pool))
-            return conv_wide_launch(pl, a, pooled ? pool : nullptr, w, s);
+            return conv_wide_launch(pl, a, pooled ? pool : nullptr, frame_off, w, s);
     }
     T *wp = reinterpret_cast<T *>(const_cast<void *>(a.wp));
     const int64_t wtot = (int64_t)pl.n_cob * (pl.qa + pl.qb) * W_ROWS * Elem<T>::CK;

@@ -21,6 +21,14 @@ struct WideArgs {
     uint16_t *out;
     int64_t out_stride;
     int c_out;                   // a multiple of NT
+    // pooled B (cmp set): B's rows are the compact pooled runs of the cell-keyed CSR (prep), gathered per
+    // pixel through the occupancy words: row frame_off[f] + occ_base[word] + popcount(bits below), zeros where
+    // the bit is clear; b / b_stride unused
+    const uint32_t *occ;
+    const int32_t *occ_base;
+    const int64_t *frame_off;
+    const uint16_t *cmp;
+    int wpr;
 };
 
 // Whether the wide kernel takes a bf16 forward of these channel counts (the row kernels' range, at most
@@ -28,6 +36,12 @@ struct WideArgs {
 bool supported(int64_t c_a, int64_t c_b, int64_t c_out);
 // Bytes of its packed weights.
 size_t packed_bytes(int64_t c_a, int64_t c_b, int64_t c_out);
+// The pooled operand of a fused call: occupancy words + prefix counts per frame (rows::prep_pooled's
+// k_occ_frame), then every run's pooled vector into its compact row with shpl_pull's arithmetic -- one thread
+// per (entry, 16-byte piece), so any channel count.
+int prep(int n_frames, int h, int w, int wpr, const int32_t *ent_dst, const int32_t *ent_src, const float *ent_val,
+         int64_t nnz_cap, const int64_t *frame_off, const uint16_t *img, int64_t img_stride, int64_t img_off, int c_b,
+         uint32_t *occ, int32_t *occ_base, uint16_t *cmp, hipStream_t s);
 // Pack the HWIO bf16 weights into wp, then the conv.
 int launch(const WideArgs &a, const uint16_t *w_hwio, uint16_t *wp, hipStream_t s);
 

@@ -21,6 +21,7 @@
 // Epilogue: act(round(fma(acc, scale, shift - center * scale))) -- shpl.h's contract, the tiled and row
 // kernels' arithmetic -- transposed through LDS and stored as whole 512-byte pixel rows.
 #include "shpl_conv_wide.h"
+#include "shpl_conv_rows.h"
 
 namespace shpl {
 namespace wide {
@@ -146,7 +147,9 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
     // (as a byte offset in A's and in B's frame rows, with its logical piece folded in) or -1 outside the map.
     // A chunk's DMA then only adds the chunk's channel offset to a wave-uniform frame base.
     const uint8_t *const fa = reinterpret_cast<const uint8_t *>(p.a + frame_row0 * p.a_stride);
-    const uint8_t *const fb = p.c_b ? reinterpret_cast<const uint8_t *>(p.b + frame_row0 * p.b_stride) : fa;
+    const uint8_t *const fb = p.cmp ? reinterpret_cast<const uint8_t *>(p.cmp)
+                                    : p.c_b ? reinterpret_cast<const uint8_t *>(p.b + frame_row0 * p.b_stride) : fa;
+    const int64_t cmp0 = p.cmp ? p.frame_off[f] : 0;
     int32_t hoff_a[HW_PER_WAVE], hoff_b[HW_PER_WAVE];
 #pragma unroll
     for (int j = 0; j < HW_PER_WAVE; ++j) {
@@ -157,7 +160,19 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
         const bool in = k < HALO_DMAS && hp < HPIX && y >= 0 && y < H && x >= 0 && x < W;
         const int pix = y * W + x, piece = (phys ^ key(hx)) << 4;
         hoff_a[j] = in ? (int32_t)(pix * (int32_t)p.a_stride * 2 + piece) : -1;
-        hoff_b[j] = in ? (int32_t)(pix * (int32_t)p.b_stride * 2 + piece) : -1;
+        if (p.cmp) {  // the pixel's compact pooled row, when a run lands on it
+            int32_t off = -1;
+            if (in) {
+                const int64_t wi = ((int64_t)f * H + y) * p.wpr + (x >> 5);
+                const uint32_t bits = p.occ[wi];
+                if ((bits >> (x & 31)) & 1u)
+                    off = (int32_t)((cmp0 + p.occ_base[wi] + __popc(bits & ((1u << (x & 31)) - 1u))) * p.c_b * 2 +
+                                    piece);
+            }
+            hoff_b[j] = off;
+        } else {
+            hoff_b[j] = in ? (int32_t)(pix * (int32_t)p.b_stride * 2 + piece) : -1;
+        }
     }
     auto issue_halo = [&](int q, int j) {
         const int k = WAVES * j + wave;
@@ -293,7 +308,77 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
     }
 }
 
+// The pooled vector of every run of the cell-keyed CSR, piece g, into its compact row frame_off[f] + (run rank
+// in frame f): one thread per (entry, 16-byte piece); the thread on a run's first entry sums the run in entry
+// order with separate multiply and add from 0 and rounds once -- k_sparse's arithmetic, bit for bit.
+__global__ __launch_bounds__(256) void k_pool_runs_wide(const int32_t *ent_dst, const int32_t *ent_src,
+                                                        const float *ent_val, int64_t nnz_cap, const uint16_t *img,
+                                                        int64_t img_stride, int64_t img_off, int c_b, int np, int H,
+                                                        int W, int wpr, const uint32_t *occ, const int32_t *occ_base,
+                                                        const int64_t *frame_off, uint16_t *cmp) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t e = t / np;
+    const int g = (int)(t - e * np);
+    if (e >= nnz_cap) return;
+    const int32_t d = ent_dst[e];
+    const int32_t prev = e > 0 ? ent_dst[e - 1] : -1;
+    int32_t dn = e + 1 < nnz_cap ? ent_dst[e + 1] : -1;
+    float wv = ent_val[e];
+    int32_t src = ent_src[e];
+    if (d < 0 || prev == d) return;
+    const int64_t cells = (int64_t)H * W;
+    const int f = (int)(d / cells);
+    const int c = (int)(d - f * cells), y = c / W, x = c - y * W;
+    const int64_t wi = ((int64_t)f * H + y) * wpr + (x >> 5);
+    const int32_t rid = occ_base[wi] + __popc(occ[wi] & ((1u << (x & 31)) - 1u));
+    float sum[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sum[j] = 0.0f;
+    // entry i's row piece goes out with entry i+1's index words (one round trip per entry)
+    for (int64_t i = e;; ++i) {
+        const u32x4 raw = *reinterpret_cast<const u32x4 *>(img + (int64_t)src * img_stride + img_off + g * 8);
+        const bool more = dn == d;
+        float wn = 0.0f;
+        int32_t sn = 0, dnn = -1;
+        if (more) {
+            wn = ent_val[i + 1];
+            sn = ent_src[i + 1];
+            dnn = i + 2 < nnz_cap ? ent_dst[i + 2] : -1;
+        }
+        uint16_t xv[8];
+        __builtin_memcpy(xv, &raw, 16);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sum[j] = __fadd_rn(sum[j], __fmul_rn(wv, bf16_to_f32(xv[j])));
+        if (!more) break;
+        wv = wn;
+        src = sn;
+        dn = dnn;
+    }
+    uint16_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = f32_to_bf16(sum[j]);
+    *reinterpret_cast<u32x4 *>(cmp + (frame_off[f] + rid) * (int64_t)c_b + g * 8) = *reinterpret_cast<u32x4 *>(v);
+}
+
 }  // namespace
+
+int prep(int n_frames, int h, int w, int wpr, const int32_t *ent_dst, const int32_t *ent_src, const float *ent_val,
+         int64_t nnz_cap, const int64_t *frame_off, const uint16_t *img, int64_t img_stride, int64_t img_off, int c_b,
+         uint32_t *occ, int32_t *occ_base, uint16_t *cmp, hipStream_t s) {
+    // the occupancy words alone (no pooled channels: rows::prep_pooled's k_occ_frame)
+    int rc = rows::prep_pooled(n_frames, h, w, wpr, ent_dst, ent_src, ent_val, nnz_cap, frame_off, img, img_stride,
+                               img_off, 0, occ, occ_base, cmp, s);
+    if (rc) return rc;
+    const int np = c_b / 8;
+    if (nnz_cap > 0 && np > 0) {
+        const int64_t threads = nnz_cap * np;
+        hipLaunchKernelGGL(k_pool_runs_wide, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, ent_dst,
+                           ent_src, ent_val, nnz_cap, img, img_stride, img_off, c_b, np, h, w, wpr, occ, occ_base,
+                           frame_off, cmp);
+        SHPL_LAUNCH_CHECK();
+    }
+    return SHPL_OK;
+}
 
 bool supported(int64_t c_a, int64_t c_b, int64_t c_out) {
     return c_a > 0 && c_a % KC == 0 && c_b >= 0 && c_b % KC == 0 && c_a + c_b > 64 && c_out > 0 && c_out % NT == 0;
