@@ -49,7 +49,7 @@ static_assert(HW_PER_WAVE <= 9, "a chunk's halo DMAs spread one per tap step");
 #ifndef SHPL_WIDE_M32
 // 1: v_mfma_f32_32x32x16_bf16 (half the MFMA instructions for the same FLOPs: the loop is issue-bound, two
 // waves sharing each SIMD's issue); 0: v_mfma_f32_16x16x32_bf16
-#define SHPL_WIDE_M32 1
+#define SHPL_WIDE_M32 0  // 32x32x16 measured slower: conv 4.47 vs 3.92 ms (profiles/r05_wide_ab3.log)
 #endif
 constexpr bool M32 = SHPL_WIDE_M32;
 constexpr int MT = M32 ? 32 : 16;                      // MFMA tile edge
@@ -59,6 +59,12 @@ constexpr int NJ = 128 / MT;                           // pixel tiles per wave (
 typedef float acc_t __attribute__((ext_vector_type(MT * MT / 64)));
 static_assert(KS * MI >= WD_PER_WAVE + 1, "the DMAs of a step ride its MFMA groups");
 
+#ifndef SHPL_WIDE_RSTAGE
+// 1: the K loop stages the next step's weights and halo pieces through registers (global_load_dwordx4 among
+// the MFMAs, ds_write_b128 at the step's end) instead of LDS-DMA -- an LDS-DMA holds its wave's issue for
+// ~60-185 cycles, and two waves share each SIMD's issue with their MFMAs
+#define SHPL_WIDE_RSTAGE 1
+#endif
 #ifndef SHPL_WIDE_PROBE
 // timing probes (wrong results): 1 no DMAs in the K loop, 2 no barrier in it, 3 no MFMAs
 #define SHPL_WIDE_PROBE 0
@@ -174,16 +180,18 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
             hoff_b[j] = in ? (int32_t)(pix * (int32_t)p.b_stride * 2 + piece) : -1;
         }
     }
-    auto issue_halo = [&](int q, int j) {
-        const int k = WAVES * j + wave;
+    // the global source of this lane's piece of the wave's halo DMA j of chunk q (the zero piece outside the map)
+    auto halo_src = [&](int q, int j) -> const u32x4 * {
         const bool from_a = q < QA;
         int32_t off = -1;  // hoff_[j] by selects: a run-time index into a register array would go to scratch
 #pragma unroll
         for (int jj = 0; jj < HW_PER_WAVE; ++jj)
             if (jj == j) off = from_a ? hoff_a[jj] : hoff_b[jj];
         const uint8_t *base = from_a ? fa + q * KC * 2 : fb + (q - QA) * KC * 2;
-        const void *src = off >= 0 ? static_cast<const void *>(base + off) : static_cast<const void *>(&g_wide_zero);
-        dma(src, hbuf0 + (q & 1) * HALO_BYTES + k * 1024);
+        return off >= 0 ? reinterpret_cast<const u32x4 *>(base + off) : &g_wide_zero;
+    };
+    auto issue_halo = [&](int q, int j) {
+        dma(halo_src(q, j), hbuf0 + (q & 1) * HALO_BYTES + (WAVES * j + wave) * 1024);
     };
     // weight DMA k (0 .. WD_PER_WAVE - 1) of this wave for step s
     auto issue_w = [&](int s, int k) {
@@ -220,6 +228,11 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
+    // register staging (SHPL_WIDE_RSTAGE): the next step's weight pieces, and the halo piece loaded in the
+    // previous step with its LDS byte offset (written one step later, so its HBM latency has a whole step)
+    u32x4 wreg[WD_PER_WAVE];
+    u32x4 hreg = u32x4{0u, 0u, 0u, 0u};
+    uint32_t hdst = 0;
     for (int s = 0; s < steps; ++s) {
         const int q = s / 9, t = s - 9 * q, ky = t / 3, kx = t - 3 * ky;
         const uint8_t *hb = hbuf0 + (q & 1) * HALO_BYTES;
@@ -233,6 +246,19 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
         // this wave's halo DMA of the step: j = t (past the wave's list: its last one again)
         int jh = t < HW_PER_WAVE ? t : HW_PER_WAVE - 1;
         if (WAVES * jh + wave >= HALO_DMAS) jh -= 1;
+#if SHPL_WIDE_RSTAGE
+        // the next step's weight pieces and this step's halo piece (for chunk q_next, written a step later)
+        // issued first; scheduling barriers keep them ahead of the MFMAs and their LDS writes behind them
+        u32x4 hnext = u32x4{0u, 0u, 0u, 0u};
+        if (SHPL_WIDE_PROBE != 1) {
+#pragma unroll
+            for (int g = 0; g < WD_PER_WAVE; ++g)
+                wreg[g] = *reinterpret_cast<const u32x4 *>(wsrc + (size_t)s_next * W_BYTES +
+                                                            (wave * WD_PER_WAVE + g) * 1024 + lane * 16);
+            hnext = *halo_src(q_next, jh);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             bf16x8 av[MI], bv[NJ];
@@ -246,10 +272,11 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
             for (int i = 0; i < MI; ++i) {
                 // the next step's DMAs among the MFMA groups: the weights first, then the halo
                 const int g = ks * MI + i;
-                if (SHPL_WIDE_PROBE != 1) {
+                if (SHPL_WIDE_PROBE != 1 && !SHPL_WIDE_RSTAGE) {
                     if (g < WD_PER_WAVE) issue_w(s_next, g);
                     if (g == WD_PER_WAVE) issue_halo(q_next, jh);
                 }
+
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) {
                     if (SHPL_WIDE_PROBE == 3)
@@ -259,6 +286,23 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
                 }
             }
         }
+#if SHPL_WIDE_RSTAGE
+        __builtin_amdgcn_sched_barrier(0);
+        if (SHPL_WIDE_PROBE != 1) {
+            const uint32_t hdst_next = (q_next & 1) * HALO_BYTES + (WAVES * jh + wave) * 1024 + lane * 16;
+#pragma unroll
+            for (int g = 0; g < WD_PER_WAVE; ++g)
+                *reinterpret_cast<u32x4 *>(wbuf0 + (s_next & 1) * W_BYTES + (wave * WD_PER_WAVE + g) * 1024 +
+                                           lane * 16) = wreg[g];
+            // the piece loaded in the previous step (at t == 0: the previous chunk's last, a repeat of an
+            // already written piece)
+            if (t != 0) *reinterpret_cast<u32x4 *>(hbuf0 + hdst) = hreg;
+            hreg = hnext;
+            hdst = hdst_next;
+        }
+        if (SHPL_WIDE_PROBE != 2) __syncthreads();
+        continue;
+#endif
         // the step's weight DMAs have landed (the halo DMA issued last may stay in flight, but not past the
         // chunk's last tap), and every wave is done with the buffers the next step's DMAs overwrite
         if (t != 8)
