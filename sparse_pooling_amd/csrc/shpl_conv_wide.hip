@@ -63,7 +63,7 @@ static_assert(KS * MI >= WD_PER_WAVE + 1, "the DMAs of a step ride its MFMA grou
 // 1: the K loop stages the next step's weights and halo pieces through registers (global_load_dwordx4 among
 // the MFMAs, ds_write_b128 at the step's end) instead of LDS-DMA -- an LDS-DMA holds its wave's issue for
 // ~60-185 cycles, and two waves share each SIMD's issue with their MFMAs
-#define SHPL_WIDE_RSTAGE 1
+#define SHPL_WIDE_RSTAGE 0  // measured slower: conv 4.33-4.37 vs 3.90-4.03 ms with LDS-DMA (profiles/r05_wide_ab4.log)
 #endif
 #ifndef SHPL_WIDE_PROBE
 // timing probes (wrong results): 1 no DMAs in the K loop, 2 no barrier in it, 3 no MFMAs
