@@ -1,22 +1,24 @@
 // shpl_conv_wide.hip -- the bf16 3x3 conv for wide channel counts: RetinaNet's post-fusion conv,
 // slim.conv2d(bev_fused, 256, [3, 3]) over 256 BEV + 256 pooled image channels with a bias and ReLU
-// (avod/avod/core/models/retinanet_model.py:334-348), on bf16 MFMA.
+// (avod/avod/core/models/retinanet_model.py:334-348), on v_mfma_f32_16x16x32_bf16.
 //
 // Implicit GEMM with the output channels as M and the pixels as N: D[co][px] = sum_k W[co][k] X[k][px],
 // K = 9 taps x the input channels. A 16 x 16 output tile of one frame against all 256 output channels per
-// 512-thread workgroup (one per CU: 148 KB of LDS), so each input row is staged once for every output
-// channel and the weights once per 256 pixels. Wave w owns 64 output channels (w >> 1) x 8 tile rows
-// (w & 1): 128 accumulator registers (two waves per SIMD within 256 registers each), 2 x 4 tiles of
-// v_mfma_f32_32x32x16_bf16 fed per 16-channel K step by 2 weight and 4 pixel fragments (one ds_read_b128 each)
-// for 8 MFMAs (SHPL_WIDE_M32=0: 4 x 8 tiles of 16x16x32).
+// 512-thread workgroup (one per CU), so each input row is staged once for every output channel and the
+// weights once per 256 pixels. Wave w owns 64 output channels (w >> 1) x 8 tile rows (w & 1): 4 x 8 tiles of
+// 16 x 16 (128 accumulator registers: two waves per SIMD within 256 registers each), fed per 32-channel K step
+// by 4 weight and 8 pixel fragments for 32 MFMAs.
 //
 // The K loop walks chunks of 64 input channels (A's, then B's) and, per chunk, the 9 taps. A chunk's 18 x 18
-// halo (128 B per pixel) and a tap's 256 x 64 weights (32 KB) are staged by LDS-DMA into double buffers:
-// step s (chunk q, tap t) multiplies from its buffers while the waves issue step s + 1's weight DMAs and, spread
-// over chunk q's 9 taps, chunk q + 1's halo DMAs; one vmcnt(0) + barrier per step. LDS rows are 128 B (8 pieces
-// of 16 B) with piece c of row r stored at c ^ key(r) -- r the halo column or the output channel -- so every
-// fragment read is conflict-free; the DMA sources carry the
-// swizzle (the destination of an LDS-DMA is lane-linear), and the packed weights come pre-swizzled.
+// halo (128 B per pixel) is staged by LDS-DMA into a double buffer, chunk q + 1's DMAs spread over chunk q's
+// taps. LDS rows are 128 B (8 pieces of 16 B) with piece c of row r at c ^ (r & 7) -- r the halo column or the
+// output channel -- so every 16x16x32 fragment read (16 lanes on consecutive rows, 4 K pieces) is
+// conflict-free; the DMA sources carry the swizzle (the destination of an LDS-DMA is lane-linear).
+// The weights (SHPL_WIDE_AREG, default): each wave loads its own fragments straight from the packed weights
+// (L2-resident: 2.4 MB read by every tile) into registers, one K step ahead, with the vmcnt waits placed by
+// hand; the LDS then holds only the halo and a barrier is needed only where a chunk's halo buffer flips (1 per
+// 9 steps). SHPL_WIDE_AREG=0: a tap's 256 x 64 weights (32 KB) staged by LDS-DMA per step into a second double
+// buffer, one counted vmcnt + barrier per step.
 //
 // Epilogue: act(round(fma(acc, scale, shift - center * scale))) -- shpl.h's contract, the tiled and row
 // kernels' arithmetic -- transposed through LDS and stored as whole 512-byte pixel rows.
@@ -32,67 +34,41 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+#ifndef SHPL_WIDE_AREG
+#define SHPL_WIDE_AREG 1
+#endif
+#ifndef SHPL_WIDE_PROBE
+// timing probes (wrong results): 1 no staging in the K loop, 3 no MFMAs
+#define SHPL_WIDE_PROBE 0
+#endif
+
 constexpr int TH = 16, TW = 16;                        // output tile
 constexpr int HH = TH + 2, HW = TW + 2, HPIX = HH * HW;  // 18 x 18 halo
-constexpr int WAVES = 8, BLOCK = 64 * WAVES;           // two waves per SIMD, 64 channels x 128 pixels each
+constexpr int WAVES = 8, BLOCK = 64 * WAVES;
+constexpr int MI = 4, NJ = 8;                          // 16 x 16 tiles per wave: 64 channels x 128 pixels
+constexpr int KS = KC / 32;                            // 32-channel K steps per chunk
 constexpr int HALO_DMAS = (HPIX * 8 + 63) / 64;        // 41 DMAs of 1 KB (the last one part padding)
 constexpr int HALO_BYTES = HALO_DMAS * 1024;
 constexpr int W_DMAS = NT * 8 / 64;                    // 32
 constexpr int W_BYTES = NT * KC * 2;                   // 32 KB per (chunk, tap)
-constexpr int LDS_BYTES = 2 * HALO_BYTES + 2 * W_BYTES;
+constexpr int LDS_BYTES = 2 * HALO_BYTES + (SHPL_WIDE_AREG ? 0 : 2 * W_BYTES);
 constexpr int OPITCH = NT * 2 + 16;                    // epilogue transpose: 528 B per pixel
-static_assert(TH * TW * OPITCH <= LDS_BYTES, "epilogue tile fits the staging buffers");
+constexpr int LDS_ALLOC = LDS_BYTES > TH * TW * OPITCH ? LDS_BYTES : TH * TW * OPITCH;
 constexpr int HW_PER_WAVE = (HALO_DMAS + WAVES - 1) / WAVES;  // halo DMAs a wave issues per chunk (6)
 constexpr int WD_PER_WAVE = W_DMAS / WAVES;                     // weight DMAs a wave issues per step (4)
 static_assert(HW_PER_WAVE <= 9, "a chunk's halo DMAs spread one per tap step");
 
-#ifndef SHPL_WIDE_M32
-// 1: v_mfma_f32_32x32x16_bf16 (half the MFMA instructions for the same FLOPs: the loop is issue-bound, two
-// waves sharing each SIMD's issue); 0: v_mfma_f32_16x16x32_bf16
-#define SHPL_WIDE_M32 0  // 32x32x16 measured slower: conv 4.47 vs 3.92 ms (profiles/r05_wide_ab3.log)
-#endif
-constexpr bool M32 = SHPL_WIDE_M32;
-constexpr int MT = M32 ? 32 : 16;                      // MFMA tile edge
-constexpr int KS = KC / (M32 ? 16 : 32);               // K steps per 64-channel chunk (4 / 2)
-constexpr int MI = 64 / MT;                            // channel tiles per wave (2 / 4)
-constexpr int NJ = 128 / MT;                           // pixel tiles per wave (4 / 8)
-typedef float acc_t __attribute__((ext_vector_type(MT * MT / 64)));
-static_assert(KS * MI >= WD_PER_WAVE + 1, "the DMAs of a step ride its MFMA groups");
-
-#ifndef SHPL_WIDE_RSTAGE
-// 1: the K loop stages the next step's weights and halo pieces through registers (global_load_dwordx4 among
-// the MFMAs, ds_write_b128 at the step's end) instead of LDS-DMA -- an LDS-DMA holds its wave's issue for
-// ~60-185 cycles, and two waves share each SIMD's issue with their MFMAs
-#define SHPL_WIDE_RSTAGE 0  // measured slower: conv 4.33-4.37 vs 3.90-4.03 ms with LDS-DMA (profiles/r05_wide_ab4.log)
-#endif
-#ifndef SHPL_WIDE_PROBE
-// timing probes (wrong results): 1 no DMAs in the K loop, 2 no barrier in it, 3 no MFMAs
-#define SHPL_WIDE_PROBE 0
-#endif
-
-// Swizzle key of a 128-byte LDS row: piece c of row r at c ^ key(r) -- r the halo column or the output channel.
-// The fragment reads of either MFMA shape (16 lanes on consecutive rows, 2 or 4 pieces) are then
-// conflict-free (checked exhaustively for every tap shift).
-__device__ __forceinline__ constexpr int key(int r) { return M32 ? (r >> 1) & 7 : r & 7; }
+__device__ __forceinline__ constexpr int key(int r) { return r & 7; }
 
 __device__ u32x4 g_wide_zero;  // the LDS-DMA source of pieces outside the map
 
 // One LDS-DMA of 16 bytes per lane (lane k's piece lands at dst + 16 k), hidden from the compiler in inline
-// asm: seeing an LDS write by DMA it would drain every outstanding DMA (vmcnt(0)) before the next ds_read --
-// the prefetch of step s + 1 before step s's second K half. The kernel orders them itself: one counted vmcnt +
-// barrier per step, and no step reads a buffer its own DMAs fill. M0 holds the destination (one wait state
-// before the DMA reads it).
+// asm: seeing an LDS write by DMA it would drain every outstanding DMA (vmcnt(0)) before the next ds_read.
+// The kernel orders them itself (counted vmcnt + barriers; no step reads a buffer its own DMAs fill). M0 holds
+// the destination (one wait state before the DMA reads it).
 __device__ __forceinline__ void dma(const void *src, uint8_t *dst) {
     const uint32_t lds = (uint32_t)(uintptr_t)dst;
     asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(lds) : "memory");
-}
-
-__device__ __forceinline__ void mfma(acc_t &acc, const bf16x8 &a, const bf16x8 &b) {
-#if SHPL_WIDE_M32
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
-#else
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
-#endif
 }
 
 __device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t n) {
@@ -100,30 +76,50 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t n) {
     return xcd < r ? xcd * (q + 1) + i : r * (q + 1) + (xcd - r) * q + i;
 }
 
-// Packed weights: HWIO [3][3][c_a+c_b][c_out] bf16 -> [nb][chunk][tap][co 256][64 channels], piece c of
-// output channel co at (c ^ key(co)) -- the LDS image one (chunk, tap) step DMAs in as it lies.
+// Packed weights, HWIO [3][3][c_a+c_b][c_out] bf16 -> 1 KB blocks of one wave's A fragment, 16 bytes per lane:
+// AREG: block (nb, chunk q, tap t, wave column wn, K step ks, tile i), lane l = output channel
+//   nb*256 + wn*64 + 16 i + (l & 15), channels q*64 + 32 ks + 8 (l >> 4) .. + 7 -- one wave's fragments of a
+//   (step, K step) are 4 KB contiguous;
+// LDS-DMA form: [nb][q][t][co 256][64 channels], piece c of output channel co at c ^ key(co) -- the LDS image a
+//   step DMAs in as it lies.
 __global__ __launch_bounds__(256) void k_pack_wide(const uint16_t *w, int c_in, int c_out, uint16_t *wp) {
     const int64_t n = (int64_t)9 * c_in * c_out;
     const int Q = c_in / KC;
     for (int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x; o < n; o += (int64_t)gridDim.x * 256) {
-        // o indexes the packed array: [nb][q][t][co][slot 8][8]
         const int e = (int)(o & 7);
-        const int slot = (int)((o >> 3) & 7);
-        const int64_t r = o >> 6;
-        const int co = (int)(r % NT);
-        const int64_t r2 = r / NT;
-        const int t = (int)(r2 % 9);
-        const int64_t r3 = r2 / 9;
-        const int q = (int)(r3 % Q);
-        const int nb = (int)(r3 / Q);
-        const int c = slot ^ key(co);
-        const int ci = q * KC + c * 8 + e;
+        int co, ci, t, nb;
+        if (SHPL_WIDE_AREG) {
+            const int l = (int)((o >> 3) & 63);
+            int64_t r = o >> 9;
+            const int i = (int)(r & 3);
+            r >>= 2;
+            const int ks = (int)(r & 1);
+            r >>= 1;
+            const int wn = (int)(r & 3);
+            r >>= 2;
+            t = (int)(r % 9);
+            r /= 9;
+            const int q = (int)(r % Q);
+            nb = (int)(r / Q);
+            co = wn * 64 + 16 * i + (l & 15);
+            ci = q * KC + 32 * ks + 8 * (l >> 4) + e;
+        } else {
+            const int slot = (int)((o >> 3) & 7);
+            const int64_t r = o >> 6;
+            co = (int)(r % NT);
+            const int64_t r2 = r / NT;
+            t = (int)(r2 % 9);
+            const int64_t r3 = r2 / 9;
+            const int q = (int)(r3 % Q);
+            nb = (int)(r3 / Q);
+            ci = q * KC + (slot ^ key(co)) * 8 + e;
+        }
         wp[o] = w[((int64_t)t * c_in + ci) * c_out + nb * NT + co];
     }
 }
 
 __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
-    __shared__ __attribute__((aligned(1024))) uint8_t s_lds[LDS_BYTES];
+    __shared__ __attribute__((aligned(1024))) uint8_t s_lds[LDS_ALLOC];
     __shared__ __attribute__((aligned(16))) float s_par[2][NT];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave & 1, wn = wave >> 1;  // tile rows 8 wm .. + 7, output channels 64 wn .. + 63
@@ -146,12 +142,12 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
         s_par[1][tid] = __fsub_rn(sh, __fmul_rn(ce, sc));
     }
 
-    uint8_t *const hbuf0 = s_lds, *const wbuf0 = s_lds + 2 * HALO_BYTES;
+    uint8_t *const hbuf0 = s_lds;
     const uint8_t *const wsrc = reinterpret_cast<const uint8_t *>(p.wp) + (size_t)nb * Q * 9 * W_BYTES;
 
     // The wave's halo DMAs k = WAVES j + wave (j < HW_PER_WAVE): per lane, once per tile, its LDS slot's pixel
     // (as a byte offset in A's and in B's frame rows, with its logical piece folded in) or -1 outside the map.
-    // A chunk's DMA then only adds the chunk's channel offset to a wave-uniform frame base.
+    // A chunk's piece then only adds the chunk's channel offset to a wave-uniform base.
     const uint8_t *const fa = reinterpret_cast<const uint8_t *>(p.a + frame_row0 * p.a_stride);
     const uint8_t *const fb = p.cmp ? reinterpret_cast<const uint8_t *>(p.cmp)
                                     : p.c_b ? reinterpret_cast<const uint8_t *>(p.b + frame_row0 * p.b_stride) : fa;
@@ -190,153 +186,167 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
         const uint8_t *base = from_a ? fa + q * KC * 2 : fb + (q - QA) * KC * 2;
         return off >= 0 ? reinterpret_cast<const u32x4 *>(base + off) : &g_wide_zero;
     };
-    auto issue_halo = [&](int q, int j) {
-        dma(halo_src(q, j), hbuf0 + (q & 1) * HALO_BYTES + (WAVES * j + wave) * 1024);
-    };
-    // weight DMA k (0 .. WD_PER_WAVE - 1) of this wave for step s
-    auto issue_w = [&](int s, int k) {
-        const int d = wave * WD_PER_WAVE + k;
-        dma(wsrc + (size_t)s * W_BYTES + d * 1024 + lane * 16, wbuf0 + (s & 1) * W_BYTES + d * 1024);
-    };
 
-    // prologue: chunk 0's halo and step 0's weights
+    // prologue: chunk 0's halo (and, LDS-DMA form, step 0's weights)
 #pragma unroll
     for (int j = 0; j < HW_PER_WAVE; ++j)
-        if (WAVES * j + wave < HALO_DMAS) issue_halo(0, j);
-#pragma unroll
-    for (int k = 0; k < WD_PER_WAVE; ++k) issue_w(0, k);
+        if (WAVES * j + wave < HALO_DMAS) dma(halo_src(0, j), hbuf0 + (WAVES * j + wave) * 1024);
 
-    acc_t acc[MI][NJ];
+    f32x4 acc[MI][NJ];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int e = 0; e < MT * MT / 64; ++e) acc[i][j][e] = 0.0f;
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 
-    // fragment reads: lane row lr (an output channel of the A tile, a pixel of the B tile), K piece group kg
-    const int lr = lane & (MT - 1), kg = lane / MT;
-    // B tile pixel lr: tile row (lr / 16) of the tile's pair (M32) and column lr % 16
-    const int prow = M32 ? lr >> 4 : 0, pcol = lane & 15;
+    // fragment reads: B (pixels) -- tile row 8 wm + j, column lane & 15 (+ kx), K piece 4 ks + lane / 16
+    const int l16 = lane & 15, kg = lane >> 4;
+
+#if SHPL_WIDE_AREG
+    // A fragments from the packed weights: (step s, K step ks) -> 4 KB of the wave's column wn
+    const uint8_t *const wlane = wsrc + (size_t)wn * (KS * MI * 1024) + lane * 16;
+    auto load_a = [&](int s, int ks, bf16x8 (&a)[MI]) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+            a[i] = *reinterpret_cast<const bf16x8 *>(wlane + (size_t)s * W_BYTES + (ks * MI + i) * 1024);
+    };
+    bf16x8 a_cur[MI], a_nxt[MI];
+    load_a(0, 0, a_cur);
+    // the halo pieces of chunk q + 1 this wave loads (steps t = 0 .. HW_PER_WAVE - 1) and writes two steps later
+    u32x4 hring[2] = {u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}};
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the prologue DMAs (the compiler does not see them)
+    __syncthreads();
+    for (int q = 0; q < Q; ++q) {
+        const uint8_t *hb = hbuf0 + (q & 1) * HALO_BYTES;
+        uint8_t *hn = hbuf0 + ((q + 1) & 1) * HALO_BYTES;
+        const bool pre = q + 1 < Q;
+#pragma unroll 1
+        for (int t = 0; t < 9; ++t) {
+            const int s = 9 * q + t, ky = t / 3, kx = t - 3 * ky;
+            const int hx = kx + l16;
+            const uint8_t *bbase = hb + ((wm * 8 + ky) * HW + hx) * 128;
+            // halo ring: the piece loaded two steps ago into LDS, this step's into its slot
+            if (SHPL_WIDE_PROBE != 1 && pre) {
+                const int jw = t - 2;
+                if (jw >= 0 && jw < HW_PER_WAVE && WAVES * jw + wave < HALO_DMAS)
+                    *reinterpret_cast<u32x4 *>(hn + (WAVES * jw + wave) * 1024 + lane * 16) = hring[t & 1];
+                if (t < HW_PER_WAVE && WAVES * t + wave < HALO_DMAS) hring[t & 1] = *halo_src(q + 1, t);
+            }
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                // the next K step's A fragments, one K step ahead (past the last step: the last one again)
+                if (SHPL_WIDE_PROBE != 1) {
+                    if (ks + 1 < KS)
+                        load_a(s, ks + 1, a_nxt);
+                    else
+                        load_a(s + 1 < steps ? s + 1 : s, 0, a_nxt);
+                }
+                // the loads stay ahead of this K step's MFMAs (the scheduler would sink them to their use)
+                __builtin_amdgcn_sched_barrier(0);
+                bf16x8 bv[NJ];
+                const int bpiece = ((4 * ks + kg) ^ key(hx)) << 4;
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) bv[j] = *reinterpret_cast<const bf16x8 *>(bbase + j * HW * 128 + bpiece);
+#pragma unroll
+                for (int i = 0; i < MI; ++i)
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) {
+                        if (SHPL_WIDE_PROBE == 3)
+                            acc[i][j][0] += (float)a_cur[i][0] * (float)bv[j][0];
+                        else
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_cur[i], bv[j], acc[i][j], 0, 0, 0);
+                    }
+#pragma unroll
+                for (int i = 0; i < MI; ++i) a_cur[i] = a_nxt[i];
+            }
+        }
+        // chunk q + 1's halo is in LDS (every wave's pieces written, two steps after their loads) and every
+        // wave is done reading chunk q's
+        __syncthreads();
+    }
+#else
+    uint8_t *const wbuf0 = s_lds + 2 * HALO_BYTES;
+    auto issue_w = [&](int s, int k) {  // weight DMA k (0 .. WD_PER_WAVE - 1) of this wave for step s
+        const int d = wave * WD_PER_WAVE + k;
+        dma(wsrc + (size_t)s * W_BYTES + d * 1024 + lane * 16, wbuf0 + (s & 1) * W_BYTES + d * 1024);
+    };
+#pragma unroll
+    for (int k = 0; k < WD_PER_WAVE; ++k) issue_w(0, k);
+    // A fragment reads: output channel wn*64 + 16 i + (lane & 15), K piece 4 ks + lane / 16 (row key lane & 7)
     uint32_t a_off[KS];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-        const int co = wn * 64 + lr;
-        a_off[ks] = (uint32_t)(co * 128 + ((((M32 ? 2 : 4) * ks + kg) ^ key(co)) << 4));
-    }
-
+    for (int ks = 0; ks < KS; ++ks)
+        a_off[ks] = (uint32_t)((wn * 64 + l16) * 128 + (((4 * ks + kg) ^ (lane & 7)) << 4));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-
-    // register staging (SHPL_WIDE_RSTAGE): the next step's weight pieces, and the halo piece loaded in the
-    // previous step with its LDS byte offset (written one step later, so its HBM latency has a whole step)
-    u32x4 wreg[WD_PER_WAVE];
-    u32x4 hreg = u32x4{0u, 0u, 0u, 0u};
-    uint32_t hdst = 0;
     for (int s = 0; s < steps; ++s) {
         const int q = s / 9, t = s - 9 * q, ky = t / 3, kx = t - 3 * ky;
         const uint8_t *hb = hbuf0 + (q & 1) * HALO_BYTES;
         const uint8_t *wb = wbuf0 + (s & 1) * W_BYTES;
-        const int hx = kx + pcol;
-        const uint8_t *bbase = hb + ((wm * 8 + prow + ky) * HW + hx) * 128;
+        const int hx = kx + l16;
+        const uint8_t *bbase = hb + ((wm * 8 + ky) * HW + hx) * 128;
         // the next step's DMAs, issued unconditionally (no branch among the MFMAs): past the last step they
         // repeat the last step's weights / chunk into the buffer nobody reads any more (drained below)
         const int s_next = s + 1 < steps ? s + 1 : s;
         const int q_next = q + 1 < Q ? q + 1 : q;
-        // this wave's halo DMA of the step: j = t (past the wave's list: its last one again)
-        int jh = t < HW_PER_WAVE ? t : HW_PER_WAVE - 1;
+        int jh = t < HW_PER_WAVE ? t : HW_PER_WAVE - 1;  // this wave's halo DMA of the step
         if (WAVES * jh + wave >= HALO_DMAS) jh -= 1;
-#if SHPL_WIDE_RSTAGE
-        // the next step's weight pieces and this step's halo piece (for chunk q_next, written a step later)
-        // issued first; scheduling barriers keep them ahead of the MFMAs and their LDS writes behind them
-        u32x4 hnext = u32x4{0u, 0u, 0u, 0u};
-        if (SHPL_WIDE_PROBE != 1) {
-#pragma unroll
-            for (int g = 0; g < WD_PER_WAVE; ++g)
-                wreg[g] = *reinterpret_cast<const u32x4 *>(wsrc + (size_t)s_next * W_BYTES +
-                                                            (wave * WD_PER_WAVE + g) * 1024 + lane * 16);
-            hnext = *halo_src(q_next, jh);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#endif
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             bf16x8 av[MI], bv[NJ];
-            const int bpiece = ((((M32 ? 2 : 4) * ks + kg) ^ key(hx)) << 4);
+            const int bpiece = ((4 * ks + kg) ^ key(hx)) << 4;
 #pragma unroll
-            for (int i = 0; i < MI; ++i) av[i] = *reinterpret_cast<const bf16x8 *>(wb + a_off[ks] + i * MT * 128);
+            for (int i = 0; i < MI; ++i) av[i] = *reinterpret_cast<const bf16x8 *>(wb + a_off[ks] + i * 16 * 128);
 #pragma unroll
-            for (int j = 0; j < NJ; ++j)
-                bv[j] = *reinterpret_cast<const bf16x8 *>(bbase + j * (M32 ? 2 : 1) * HW * 128 + bpiece);
+            for (int j = 0; j < NJ; ++j) bv[j] = *reinterpret_cast<const bf16x8 *>(bbase + j * HW * 128 + bpiece);
 #pragma unroll
             for (int i = 0; i < MI; ++i) {
                 // the next step's DMAs among the MFMA groups: the weights first, then the halo
                 const int g = ks * MI + i;
-                if (SHPL_WIDE_PROBE != 1 && !SHPL_WIDE_RSTAGE) {
+                if (SHPL_WIDE_PROBE != 1) {
                     if (g < WD_PER_WAVE) issue_w(s_next, g);
-                    if (g == WD_PER_WAVE) issue_halo(q_next, jh);
+                    if (g == WD_PER_WAVE)
+                        dma(halo_src(q_next, jh), hbuf0 + (q_next & 1) * HALO_BYTES + (WAVES * jh + wave) * 1024);
                 }
-
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) {
                     if (SHPL_WIDE_PROBE == 3)
                         acc[i][j][0] += (float)av[i][0] * (float)bv[j][0];
                     else
-                        mfma(acc[i][j], av[i], bv[j]);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
                 }
             }
         }
-#if SHPL_WIDE_RSTAGE
-        __builtin_amdgcn_sched_barrier(0);
-        if (SHPL_WIDE_PROBE != 1) {
-            const uint32_t hdst_next = (q_next & 1) * HALO_BYTES + (WAVES * jh + wave) * 1024 + lane * 16;
-#pragma unroll
-            for (int g = 0; g < WD_PER_WAVE; ++g)
-                *reinterpret_cast<u32x4 *>(wbuf0 + (s_next & 1) * W_BYTES + (wave * WD_PER_WAVE + g) * 1024 +
-                                           lane * 16) = wreg[g];
-            // the piece loaded in the previous step (at t == 0: the previous chunk's last, a repeat of an
-            // already written piece)
-            if (t != 0) *reinterpret_cast<u32x4 *>(hbuf0 + hdst) = hreg;
-            hreg = hnext;
-            hdst = hdst_next;
-        }
-        if (SHPL_WIDE_PROBE != 2) __syncthreads();
-        continue;
-#endif
         // the step's weight DMAs have landed (the halo DMA issued last may stay in flight, but not past the
         // chunk's last tap), and every wave is done with the buffers the next step's DMAs overwrite
         if (t != 8)
             asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (SHPL_WIDE_PROBE != 2) __syncthreads();
+        __syncthreads();
     }
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
-    // epilogue: lane (pixel, 4 consecutive channels per accumulator quad) -> LDS [pixel][256 channels] bf16,
-    // then whole pixel rows out
+    // epilogue: lane (pixel, 4 consecutive channels) -> LDS [pixel][256 channels] bf16, then whole pixel rows out
     uint8_t *const s_out = s_lds;
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
+        const int co = wn * 64 + 16 * i + 4 * kg;
+        const f32x4 sc = *reinterpret_cast<const f32x4 *>(&s_par[0][co]);
+        const f32x4 sh = *reinterpret_cast<const f32x4 *>(&s_par[1][co]);
 #pragma unroll
-        for (int g = 0; g < MT * MT / 256; ++g) {  // accumulator quads: 4 (M32) / 1
-            const int co = wn * 64 + i * MT + 8 * g + 4 * kg;
-            const f32x4 sc = *reinterpret_cast<const f32x4 *>(&s_par[0][co]);
-            const f32x4 sh = *reinterpret_cast<const f32x4 *>(&s_par[1][co]);
+        for (int j = 0; j < NJ; ++j) {
+            uint16_t o[4];
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                uint16_t o[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const uint16_t v = f32_to_bf16(__builtin_fmaf(acc[i][j][4 * g + e], sc[e], sh[e]));
-                    o[e] = (p.act == 1 && (int16_t)v <= 0) ? (uint16_t)0 : v;
-                }
-                u32x2 pk;
-                __builtin_memcpy(&pk, o, 8);
-                const int px = (wm * 8 + j * (M32 ? 2 : 1) + prow) * TW + pcol;
-                *reinterpret_cast<u32x2 *>(s_out + px * OPITCH + co * 2) = pk;
+            for (int e = 0; e < 4; ++e) {
+                const uint16_t v = f32_to_bf16(__builtin_fmaf(acc[i][j][e], sc[e], sh[e]));
+                o[e] = (p.act == 1 && (int16_t)v <= 0) ? (uint16_t)0 : v;
             }
+            u32x2 pk;
+            __builtin_memcpy(&pk, o, 8);
+            const int px = (wm * 8 + j) * TW + l16;
+            *reinterpret_cast<u32x2 *>(s_out + px * OPITCH + co * 2) = pk;
         }
     }
     __syncthreads();
