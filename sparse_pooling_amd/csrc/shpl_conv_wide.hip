@@ -35,7 +35,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 #ifndef SHPL_WIDE_AREG
-#define SHPL_WIDE_AREG 1
+#define SHPL_WIDE_AREG 0  // 1 measured slower: conv 4.06-4.14 vs 3.77-3.88 ms (profiles/r05_wide_ab.log)
 #endif
 #ifndef SHPL_WIDE_PROBE
 // timing probes (wrong results): 1 no staging in the K loop, 3 no MFMAs
@@ -69,6 +69,19 @@ __device__ u32x4 g_wide_zero;  // the LDS-DMA source of pieces outside the map
 __device__ __forceinline__ void dma(const void *src, uint8_t *dst) {
     const uint32_t lds = (uint32_t)(uintptr_t)dst;
     asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(lds) : "memory");
+}
+#ifndef SHPL_WIDE_HNT
+// 1: the halo's DMAs nontemporal (each input row is read by one tile, its edges by two): the 2.4 MB of weights
+// every tile re-reads then keep their place in the XCD's L2
+#define SHPL_WIDE_HNT 0
+#endif
+__device__ __forceinline__ void dma_halo(const void *src, uint8_t *dst) {
+#if SHPL_WIDE_HNT
+    const uint32_t lds = (uint32_t)(uintptr_t)dst;
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(src), "{m0}"(lds) : "memory");
+#else
+    dma(src, dst);
+#endif
 }
 
 __device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t n) {
@@ -190,7 +203,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
     // prologue: chunk 0's halo (and, LDS-DMA form, step 0's weights)
 #pragma unroll
     for (int j = 0; j < HW_PER_WAVE; ++j)
-        if (WAVES * j + wave < HALO_DMAS) dma(halo_src(0, j), hbuf0 + (WAVES * j + wave) * 1024);
+        if (WAVES * j + wave < HALO_DMAS) dma_halo(halo_src(0, j), hbuf0 + (WAVES * j + wave) * 1024);
 
     f32x4 acc[MI][NJ];
 #pragma unroll
@@ -305,7 +318,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
                 if (SHPL_WIDE_PROBE != 1) {
                     if (g < WD_PER_WAVE) issue_w(s_next, g);
                     if (g == WD_PER_WAVE)
-                        dma(halo_src(q_next, jh), hbuf0 + (q_next & 1) * HALO_BYTES + (WAVES * jh + wave) * 1024);
+                        dma_halo(halo_src(q_next, jh), hbuf0 + (q_next & 1) * HALO_BYTES + (WAVES * jh + wave) * 1024);
                 }
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) {
