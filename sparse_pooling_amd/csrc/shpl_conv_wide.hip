@@ -14,11 +14,11 @@
 // taps. LDS rows are 128 B (8 pieces of 16 B) with piece c of row r at c ^ (r & 7) -- r the halo column or the
 // output channel -- so every 16x16x32 fragment read (16 lanes on consecutive rows, 4 K pieces) is
 // conflict-free; the DMA sources carry the swizzle (the destination of an LDS-DMA is lane-linear).
-// The weights (SHPL_WIDE_AREG, default): each wave loads its own fragments straight from the packed weights
-// (L2-resident: 2.4 MB read by every tile) into registers, one K step ahead, with the vmcnt waits placed by
-// hand; the LDS then holds only the halo and a barrier is needed only where a chunk's halo buffer flips (1 per
-// 9 steps). SHPL_WIDE_AREG=0: a tap's 256 x 64 weights (32 KB) staged by LDS-DMA per step into a second double
-// buffer, one counted vmcnt + barrier per step.
+// A tap's 256 x 64 weights (32 KB, pre-swizzled by k_pack_wide) are staged per step by LDS-DMA into a second
+// double buffer; one counted vmcnt + barrier per step. (Measured and dropped, profiles/r05_wide_ab.log: each
+// wave's weight fragments loaded from L2 straight into registers one K step ahead, a barrier per chunk only;
+// register staging of weights and halo; one wave per SIMD with AGPR accumulators; 32x32x16 MFMAs; nontemporal
+// halo DMAs.)
 //
 // Epilogue: act(round(fma(acc, scale, shift - center * scale))) -- shpl.h's contract, the tiled and row
 // kernels' arithmetic -- transposed through LDS and stored as whole 512-byte pixel rows.
@@ -34,9 +34,6 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-#ifndef SHPL_WIDE_AREG
-#define SHPL_WIDE_AREG 0  // 1 measured slower: conv 4.06-4.14 vs 3.77-3.88 ms (profiles/r05_wide_ab.log)
-#endif
 #ifndef SHPL_WIDE_PROBE
 // timing probes (wrong results): 1 no staging in the K loop, 3 no MFMAs
 #define SHPL_WIDE_PROBE 0
@@ -51,7 +48,7 @@ constexpr int HALO_DMAS = (HPIX * 8 + 63) / 64;        // 41 DMAs of 1 KB (the l
 constexpr int HALO_BYTES = HALO_DMAS * 1024;
 constexpr int W_DMAS = NT * 8 / 64;                    // 32
 constexpr int W_BYTES = NT * KC * 2;                   // 32 KB per (chunk, tap)
-constexpr int LDS_BYTES = 2 * HALO_BYTES + (SHPL_WIDE_AREG ? 0 : 2 * W_BYTES);
+constexpr int LDS_BYTES = 2 * HALO_BYTES + 2 * W_BYTES;
 constexpr int OPITCH = NT * 2 + 16;                    // epilogue transpose: 528 B per pixel
 constexpr int LDS_ALLOC = LDS_BYTES > TH * TW * OPITCH ? LDS_BYTES : TH * TW * OPITCH;
 constexpr int HW_PER_WAVE = (HALO_DMAS + WAVES - 1) / WAVES;  // halo DMAs a wave issues per chunk (6)
@@ -70,63 +67,29 @@ __device__ __forceinline__ void dma(const void *src, uint8_t *dst) {
     const uint32_t lds = (uint32_t)(uintptr_t)dst;
     asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(lds) : "memory");
 }
-#ifndef SHPL_WIDE_HNT
-// 1: the halo's DMAs nontemporal (each input row is read by one tile, its edges by two): the 2.4 MB of weights
-// every tile re-reads then keep their place in the XCD's L2
-#define SHPL_WIDE_HNT 0
-#endif
-__device__ __forceinline__ void dma_halo(const void *src, uint8_t *dst) {
-#if SHPL_WIDE_HNT
-    const uint32_t lds = (uint32_t)(uintptr_t)dst;
-    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(src), "{m0}"(lds) : "memory");
-#else
-    dma(src, dst);
-#endif
-}
+__device__ __forceinline__ void dma_halo(const void *src, uint8_t *dst) { dma(src, dst); }
 
 __device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t n) {
     const int64_t q = n >> 3, r = n & 7, xcd = bid & 7, i = bid >> 3;
     return xcd < r ? xcd * (q + 1) + i : r * (q + 1) + (xcd - r) * q + i;
 }
 
-// Packed weights, HWIO [3][3][c_a+c_b][c_out] bf16 -> 1 KB blocks of one wave's A fragment, 16 bytes per lane:
-// AREG: block (nb, chunk q, tap t, wave column wn, K step ks, tile i), lane l = output channel
-//   nb*256 + wn*64 + 16 i + (l & 15), channels q*64 + 32 ks + 8 (l >> 4) .. + 7 -- one wave's fragments of a
-//   (step, K step) are 4 KB contiguous;
-// LDS-DMA form: [nb][q][t][co 256][64 channels], piece c of output channel co at c ^ key(co) -- the LDS image a
-//   step DMAs in as it lies.
+// Packed weights, HWIO [3][3][c_a+c_b][c_out] bf16 -> [nb][chunk q][tap t][co 256][64 channels], piece c of
+// output channel co at c ^ key(co): the LDS image a step DMAs in as it lies.
 __global__ __launch_bounds__(256) void k_pack_wide(const uint16_t *w, int c_in, int c_out, uint16_t *wp) {
     const int64_t n = (int64_t)9 * c_in * c_out;
     const int Q = c_in / KC;
     for (int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x; o < n; o += (int64_t)gridDim.x * 256) {
         const int e = (int)(o & 7);
-        int co, ci, t, nb;
-        if (SHPL_WIDE_AREG) {
-            const int l = (int)((o >> 3) & 63);
-            int64_t r = o >> 9;
-            const int i = (int)(r & 3);
-            r >>= 2;
-            const int ks = (int)(r & 1);
-            r >>= 1;
-            const int wn = (int)(r & 3);
-            r >>= 2;
-            t = (int)(r % 9);
-            r /= 9;
-            const int q = (int)(r % Q);
-            nb = (int)(r / Q);
-            co = wn * 64 + 16 * i + (l & 15);
-            ci = q * KC + 32 * ks + 8 * (l >> 4) + e;
-        } else {
-            const int slot = (int)((o >> 3) & 7);
-            const int64_t r = o >> 6;
-            co = (int)(r % NT);
-            const int64_t r2 = r / NT;
-            t = (int)(r2 % 9);
-            const int64_t r3 = r2 / 9;
-            const int q = (int)(r3 % Q);
-            nb = (int)(r3 / Q);
-            ci = q * KC + (slot ^ key(co)) * 8 + e;
-        }
+        const int slot = (int)((o >> 3) & 7);
+        const int64_t r = o >> 6;
+        const int co = (int)(r % NT);
+        const int64_t r2 = r / NT;
+        const int t = (int)(r2 % 9);
+        const int64_t r3 = r2 / 9;
+        const int q = (int)(r3 % Q);
+        const int nb = (int)(r3 / Q);
+        const int ci = q * KC + (slot ^ key(co)) * 8 + e;
         wp[o] = w[((int64_t)t * c_in + ci) * c_out + nb * NT + co];
     }
 }
@@ -214,69 +177,6 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
     // fragment reads: B (pixels) -- tile row 8 wm + j, column lane & 15 (+ kx), K piece 4 ks + lane / 16
     const int l16 = lane & 15, kg = lane >> 4;
 
-#if SHPL_WIDE_AREG
-    // A fragments from the packed weights: (step s, K step ks) -> 4 KB of the wave's column wn
-    const uint8_t *const wlane = wsrc + (size_t)wn * (KS * MI * 1024) + lane * 16;
-    auto load_a = [&](int s, int ks, bf16x8 (&a)[MI]) {
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-            a[i] = *reinterpret_cast<const bf16x8 *>(wlane + (size_t)s * W_BYTES + (ks * MI + i) * 1024);
-    };
-    bf16x8 a_cur[MI], a_nxt[MI];
-    load_a(0, 0, a_cur);
-    // the halo pieces of chunk q + 1 this wave loads (steps t = 0 .. HW_PER_WAVE - 1) and writes two steps later
-    u32x4 hring[2] = {u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}};
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the prologue DMAs (the compiler does not see them)
-    __syncthreads();
-    for (int q = 0; q < Q; ++q) {
-        const uint8_t *hb = hbuf0 + (q & 1) * HALO_BYTES;
-        uint8_t *hn = hbuf0 + ((q + 1) & 1) * HALO_BYTES;
-        const bool pre = q + 1 < Q;
-#pragma unroll 1
-        for (int t = 0; t < 9; ++t) {
-            const int s = 9 * q + t, ky = t / 3, kx = t - 3 * ky;
-            const int hx = kx + l16;
-            const uint8_t *bbase = hb + ((wm * 8 + ky) * HW + hx) * 128;
-            // halo ring: the piece loaded two steps ago into LDS, this step's into its slot
-            if (SHPL_WIDE_PROBE != 1 && pre) {
-                const int jw = t - 2;
-                if (jw >= 0 && jw < HW_PER_WAVE && WAVES * jw + wave < HALO_DMAS)
-                    *reinterpret_cast<u32x4 *>(hn + (WAVES * jw + wave) * 1024 + lane * 16) = hring[t & 1];
-                if (t < HW_PER_WAVE && WAVES * t + wave < HALO_DMAS) hring[t & 1] = *halo_src(q + 1, t);
-            }
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                // the next K step's A fragments, one K step ahead (past the last step: the last one again)
-                if (SHPL_WIDE_PROBE != 1) {
-                    if (ks + 1 < KS)
-                        load_a(s, ks + 1, a_nxt);
-                    else
-                        load_a(s + 1 < steps ? s + 1 : s, 0, a_nxt);
-                }
-                // the loads stay ahead of this K step's MFMAs (the scheduler would sink them to their use)
-                __builtin_amdgcn_sched_barrier(0);
-                bf16x8 bv[NJ];
-                const int bpiece = ((4 * ks + kg) ^ key(hx)) << 4;
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) bv[j] = *reinterpret_cast<const bf16x8 *>(bbase + j * HW * 128 + bpiece);
-#pragma unroll
-                for (int i = 0; i < MI; ++i)
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j) {
-                        if (SHPL_WIDE_PROBE == 3)
-                            acc[i][j][0] += (float)a_cur[i][0] * (float)bv[j][0];
-                        else
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_cur[i], bv[j], acc[i][j], 0, 0, 0);
-                    }
-#pragma unroll
-                for (int i = 0; i < MI; ++i) a_cur[i] = a_nxt[i];
-            }
-        }
-        // chunk q + 1's halo is in LDS (every wave's pieces written, two steps after their loads) and every
-        // wave is done reading chunk q's
-        __syncthreads();
-    }
-#else
     uint8_t *const wbuf0 = s_lds + 2 * HALO_BYTES;
     auto issue_w = [&](int s, int k) {  // weight DMA k (0 .. WD_PER_WAVE - 1) of this wave for step s
         const int d = wave * WD_PER_WAVE + k;
@@ -337,7 +237,6 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
