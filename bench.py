@@ -1132,7 +1132,11 @@ def run_conv(args, world, rank, dev):
                        "parallelism": f"frame-sharded x{world}"},
             "frame_checksums": checks,
             "roofline": {"bound": "mfma",
-                         "kernel": ("shpl_conv3x3 call = k_pack_w + k_occ_frame + k_pool_runs + k_conv_rows "
+                         "kernel": ("shpl_conv3x3 call = k_pack_wide + k_occ_frame + k_pool_runs_wide + k_conv_wide "
+                                    "(16x16-pixel tiles x 256 output channels per workgroup, halo and weights by "
+                                    "LDS-DMA, pooled half gathered from the per-run buffer), MFMA "
+                                    "v_mfma_f32_16x16x32_bf16" if esz == 2 and retina else
+                                    "shpl_conv3x3 call = k_pack_w + k_occ_frame + k_pool_runs + k_conv_rows "
                                     "(row-streaming, pooled half gathered from the per-run buffer), MFMA "
                                     "v_mfma_f32_32x32x16_bf16" if esz == 2 else
                                     "shpl_conv3x3 call = k_pack_w + k_row_ptr + k_conv3x3 (tiled, pooling in the "
