@@ -124,6 +124,12 @@ def parse():
     ap.add_argument("--no-wgrad-reuse", action="store_true",
                     help="conv training (bf16): the weight gradient prepares its own pooled operand instead of "
                          "reading the forward's (shpl_conv3x3_wgrad_reuse; A/B)")
+    ap.add_argument("--wgrad-side", choices=["on", "off"], default=None,
+                    help="conv training: the weight gradient on a side stream beside the input gradient "
+                         "(FusionConv.WGRAD_SIDE; default: the class's)")
+    ap.add_argument("--img-zero-side", choices=["on", "off"], default=None,
+                    help="conv training: the image gradient's zero rows on a side stream beside the input gradient "
+                         "(FusionConv.IMG_ZERO_SIDE; default: the class's)")
     ap.add_argument("--scan-points", type=int, default=120000, help="points per velodyne scan (frames)")
     ap.add_argument("--maps-form", default="f64", choices=["f64", "bev_input"],
                     help="frames: the BEV maps as the reference's f64 height / density maps, or as the network's "
@@ -909,6 +915,10 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
     cb, ci = spec.c_bev, spec.c_img
     esz = 2 if dtype == torch.bfloat16 else 4
     conv.WGRAD_REUSE = not args.no_wgrad_reuse
+    if args.wgrad_side is not None:
+        conv.WGRAD_SIDE = args.wgrad_side == "on"
+    if args.img_zero_side is not None:
+        conv.IMG_ZERO_SIDE = args.img_zero_side == "on"
     conv.weights.requires_grad_(True)
     conv.beta.requires_grad_(True)
     tb, ti = bev.clone().requires_grad_(True), img.clone().requires_grad_(True)
@@ -987,6 +997,8 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
                                     "the weight gradient, bv_fused never stored; f32: the pooled map built once in the "
                                     "forward, reused by the weight gradient), backward to bev, img, weights, beta"),
                        "global_batch": F * world, "frames_per_gpu_per_step": F, "hip_graph": False,
+                       "wgrad_reuse": conv.WGRAD_REUSE, "wgrad_side_stream": conv.WGRAD_SIDE,
+                       "img_zero_side_stream": conv.IMG_ZERO_SIDE,
                        "bn_statistics": "per rank (no cross-rank sync)", "parallelism": f"frame-sharded x{world}"},
             "roofline": ({"bound": "hbm", "kernel": "the whole forward + backward step: algorithmic bytes of its passes "
                           "(pooled map, conv fwd, BN apply, BN backward x2, input and weight gradients, image "

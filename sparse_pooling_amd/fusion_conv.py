@@ -265,36 +265,83 @@ class _FusionConvFn(torch.autograd.Function):
             g_raw, dbeta = gy, None
         need_x = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         d_a = d_b = dw = None
+        # side stream work beside the input gradient (FusionConv.IMG_ZERO_SIDE / WGRAD_SIDE): the image
+        # gradient's zero rows (they need no index and no input gradient), then the weight gradient (it reads the
+        # same g_raw as the input gradient and writes a disjoint output)
+        side = zeros_done = None
+        img_grad = need_x and pooled and b is not None and ctx.needs_input_grad[1]
+        zero_side = img_grad and conv.IMG_ZERO_SIDE
+        wgrad_side = need_x and ctx.needs_input_grad[2] and conv.WGRAD_SIDE
+        if g_raw.is_cuda and (zero_side or wgrad_side):
+            cur = torch.cuda.current_stream(g_raw.device)
+            side = _side_stream(g_raw.device)
+            side.wait_stream(cur)
+            if zero_side:
+                d_b = torch.empty(b.shape, dtype=a.dtype, device=a.device)
+            with torch.cuda.stream(side):
+                if zero_side:
+                    # (the dense half reads no source rows: any aligned map stands in for dx_b, not written yet)
+                    sm.pull(smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, d_b, Cb, 0, Cb, d_b, Cb, part="dense")
+                    zeros_done = torch.cuda.Event()
+                    zeros_done.record(side)
+                if wgrad_side:
+                    dw = _FusionConvFn._wgrad(ctx, a, b, weights, g_raw)
+            for t in (a, b, g_raw, ctx.fwd_ws, ctx.xb, d_b):
+                if t is not None:
+                    t.record_stream(side)
         if need_x:
             if b is None:
                 d_a = conv3x3_dgrad(g_raw, weights, Ca)
             else:  # the epilogue writes the two sources' gradients as separate dense maps
                 d_a, dx_b = conv3x3_dgrad(g_raw, weights, Ca + Cb, split=Ca)
                 if ctx.needs_input_grad[1]:
-                    if pooled:  # the pooled channels' gradient back to the image (a8's TF gradient)
+                    if pooled and zeros_done is not None:  # its zero rows are on the side stream already
+                        cur.wait_event(zeros_done)
+                        sm.pull(smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, dx_b, Cb, 0, Cb, d_b, Cb, part="sparse")
+                    elif pooled:  # the pooled channels' gradient back to the image (a8's TF gradient)
                         d_b = torch.empty(b.shape, dtype=dx_b.dtype, device=dx_b.device)
                         sm.pull(smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, dx_b, Cb, 0, Cb, d_b, Cb)
                     else:
                         d_b = dx_b
             if not ctx.needs_input_grad[0]:
                 d_a = None
-        if ctx.needs_input_grad[2]:
-            if pooled and a.dtype == torch.bfloat16:
-                # k_wgrad_rows gathers the pooled rows from a compact per-run buffer: bv_fused never stored
-                dw = conv3x3_wgrad(a, g_raw, b=b, pool=smap.csr(L.BY_CELL, L.ORDER_ENTRY), frame_off=smap.frame_off,
-                                   fwd_ws=ctx.fwd_ws, fwd_stats=ctx.train_bn)
-            elif pooled:
-                # f32: the pooled channels once into HBM (shpl_pull): the dense two-source weight gradient
-                # runs at twice the waves per SIMD of the one that recomputes them per tile (257 vs
-                # 214 registers); conv3x3_wgrad(..., pool=...) stays the memory-lean form
-                xb = ctx.xb if ctx.xb is not None else sm.pool_img_to_bev(smap, b, tuple(a.shape[:3]) + (Cb,))
-                dw = conv3x3_wgrad(a, g_raw, b=xb)
-            else:
-                dw = conv3x3_wgrad(a, g_raw, b=b)
-            dw = dw.to(weights.dtype)
+        if side is not None:
+            cur.wait_stream(side)
+            if dw is not None:
+                dw.record_stream(cur)
+        if dw is None and ctx.needs_input_grad[2]:
+            dw = _FusionConvFn._wgrad(ctx, a, b, weights, g_raw)
         d_beta = dbeta if (conv.batch_norm and ctx.needs_input_grad[3]) else None
         d_bias = dbeta if (not conv.batch_norm and ctx.needs_input_grad[4]) else None
         return d_a, d_b, dw, d_beta, d_bias, None, None, None, None, None
+
+    @staticmethod
+    def _wgrad(ctx, a, b, weights, g_raw):
+        smap, pooled = ctx.smap, ctx.pooled
+        if pooled and a.dtype == torch.bfloat16:
+            # k_wgrad_rows gathers the pooled rows from a compact per-run buffer: bv_fused never stored
+            dw = conv3x3_wgrad(a, g_raw, b=b, pool=smap.csr(L.BY_CELL, L.ORDER_ENTRY), frame_off=smap.frame_off,
+                               fwd_ws=ctx.fwd_ws, fwd_stats=ctx.train_bn)
+        elif pooled:
+            # f32: the pooled channels once into HBM (shpl_pull): the dense two-source weight gradient
+            # runs at twice the waves per SIMD of the one that recomputes them per tile (257 vs
+            # 214 registers); conv3x3_wgrad(..., pool=...) stays the memory-lean form
+            xb = ctx.xb if ctx.xb is not None else sm.pool_img_to_bev(smap, b, tuple(a.shape[:3]) + (ctx.shapes[1],))
+            dw = conv3x3_wgrad(a, g_raw, b=xb)
+        else:
+            dw = conv3x3_wgrad(a, g_raw, b=b)
+        return dw.to(weights.dtype)
+
+
+_SIDE = {}
+
+
+def _side_stream(dev):
+    """One side stream per device for the weight gradient (created once: stream creation is not free)."""
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = torch.cuda.Stream(device=dev)
+    return s
 
 
 class FusionConv:
@@ -303,6 +350,11 @@ class FusionConv:
 
     # bf16 fused(): the weight gradient reads the pooled operand its forward prepared (False: prepares its own)
     WGRAD_REUSE = True
+    # backward, beside the input gradient on a side stream: the image gradient's zero rows (IMG_ZERO_SIDE) and
+    # the weight gradient (WGRAD_SIDE; False: after the input gradient on one stream -- the two convs side by
+    # side measured slower: 7.34-7.35 vs 7.14-7.20 ms per bf16 training step, profiles/r05_wside_ab.log)
+    IMG_ZERO_SIDE = True
+    WGRAD_SIDE = False
 
     def __init__(self, c_in, c_out, batch_norm=True, bias=False, relu=True, eps=1e-3, decay=0.999,
                  dtype=torch.float32, device="cuda", seed=0):

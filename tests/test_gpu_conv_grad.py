@@ -355,6 +355,45 @@ def test_fused_bf16_wgrad_reuses_forward_operand(train, cb, ci, cout):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_side_stream_backward_matches_one_stream(dtype):
+    """FusionConv.IMG_ZERO_SIDE / WGRAD_SIDE: the image gradient's zero rows and / or the weight gradient on a
+    side stream beside the input gradient give bitwise the gradients of the one-stream backward, over three
+    steps (the side stream's allocations reused across steps)."""
+    from sparse_pooling_amd import fusion_conv as fc, shpl_map as sm
+    spec = synth.FrameSpec(2000, (1200, 360), (704, 800), (4, 4), 32, 32)
+    fr = synth.make_frame(spec, seed=911, n_outside=10)
+    gen = orc.gen_sparse_pooling_input_avod(fr.points, fr.voxel_indices, fr.P, list(spec.im_size),
+                                            tuple(spec.bv_size))
+    ref = orc.produce_sparse_pooling_input(gen, stride=spec.stride)
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    bev = _t(synth.make_features((1, Hb, Wb, 32), 41)).to(dtype)
+    img = _t(synth.make_features((1, Hi, Wi, 32), 42)).to(dtype)
+    grads = []
+    for zero_side, wgrad_side in ((False, False), (True, False), (False, True), (True, True)):
+        smap = sm.pack_map(_t(ref["Mij_pool"]), _t(ref["M_val"].astype(np.float32)), ref["M_size"],
+                           _t(ref["img_index_flip_pool"]), img.shape)
+        conv = fc.FusionConv(64, 32, dtype=dtype, device=DEV, seed=5)
+        conv.IMG_ZERO_SIDE, conv.WGRAD_SIDE = zero_side, wgrad_side
+        conv.weights.requires_grad_(True)
+        conv.beta.requires_grad_(True)
+        tb, ti = bev.clone().requires_grad_(True), img.clone().requires_grad_(True)
+        out = []
+        for k in range(3):
+            for t in (tb, ti, conv.weights, conv.beta):
+                t.grad = None
+            g = _t(np.random.default_rng(50 + k).standard_normal((1, Hb, Wb, 32)).astype(np.float32)).to(dtype)
+            conv.fused(tb, ti, smap, is_training=True).backward(g)
+            out.append([x.grad.clone() for x in (tb, ti, conv.weights, conv.beta)])
+        torch.cuda.synchronize()
+        grads.append(out)
+    for other in grads[1:]:
+        for s0, s1 in zip(grads[0], other):
+            for a, b in zip(s0, s1):
+                assert torch.equal(a, b)
+
+
 def test_wgrad_reuse_rejects_a_tiled_forward_workspace():
     """shpl_conv3x3_wgrad_reuse checks what it can of the forward's row-streaming predicate: a forward with
     training statistics over 32 + 16 bf16 channels runs the tiled kernel (no pooled operand in its workspace),
