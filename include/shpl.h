@@ -47,6 +47,8 @@ typedef enum {
 #define SHPL_EBIT_PIXEL 4u   /* source index (b,v,u) outside the image */
 #define SHPL_EBIT_VALUES 8u  /* len(M_val) != nnz */
 #define SHPL_EBIT_CAPACITY 16u /* a frame holds more points than max_points_per_frame */
+#define SHPL_EBIT_BARRIER 32u  /* shpl_build_index_buckets' one-launch form gave up waiting at a frame barrier
+                                  (its chunks were not all resident: results of that call are invalid) */
 
 typedef enum { SHPL_F32 = 0, SHPL_BF16 = 1, SHPL_F64 = 2 } shpl_dtype;
 typedef enum { SHPL_I32 = 0, SHPL_I64 = 1 } shpl_itype;
@@ -417,6 +419,11 @@ int shpl_pull_once(int direction, int dtype, const shpl_csr *csr, const void *d_
  * No d_mij / d_flip outputs; nnz_cap = the point capacity (d_cell's length).
  * Limits (SHPL_ERR_BAD_SHAPE otherwise): at most 65536 cells and 65536 pixels
  * per frame, max_points_per_frame below 2^24.
+ * Frames of at most 32 chunks of 1024 points run both passes in ONE launch
+ * (k_index1: a frame barrier between them inside the launch); its barrier
+ * words live at the start of d_bkt, which must be ZEROED once before its first
+ * use -- every call leaves them zero. SHPL_EBIT_BARRIER in *d_err: a barrier
+ * gave up (the call's results are invalid).
  * Replaces what shpl_build_index + two shpl_build_csr calls feed the pulls
  * (kitti_dataset.py:374-379, then rpn_model.py:330-331's SparseTensor). */
 /* Optional riders of shpl_build_index_buckets: the concat's pass-through half

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("SHPL_LIB") or os.path.join(_HERE, "libshpl.so")
 
 # enums of include/shpl.h
 OK, ERR_BAD_SHAPE, ERR_INDEX_OOB, ERR_HIP, ERR_WORKSPACE, ERR_ARG = range(6)
-EBIT_ROW, EBIT_COL, EBIT_PIXEL, EBIT_VALUES, EBIT_CAPACITY = 1, 2, 4, 8, 16
+EBIT_ROW, EBIT_COL, EBIT_PIXEL, EBIT_VALUES, EBIT_CAPACITY, EBIT_BARRIER = 1, 2, 4, 8, 16, 32
 F32, BF16, F64 = 0, 1, 2
 I32, I64 = 0, 1
 BY_CELL, BY_PIXEL = 0, 1

@@ -106,9 +106,14 @@ __device__ __forceinline__ double dot4(const double *row, double a0, double a1, 
 // projectToImage (avod/avod/utils/transform.py:3-26; calib_utils.project_to_image
 // :281-298): [u;v;w] = P [x;y;z;1]; u/=w; v/=w (IEEE division). gemv: the
 // product had one column (see dot4_gemv).
+// P's 12 values are loaded into registers first, all in flight at once: read inside the two summation
+// orders' branches they were 4-8 dependent round trips per point (the index build's longest latency chain).
 __device__ __forceinline__ void project(const double *P, double x, double y, double z, double &u, double &v,
                                         bool gemv = false) {
-    const double r0 = dot4(P, x, y, z, gemv), r1 = dot4(P + 4, x, y, z, gemv), r2 = dot4(P + 8, x, y, z, gemv);
+    double p[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) p[k] = P[k];
+    const double r0 = dot4(p, x, y, z, gemv), r1 = dot4(p + 4, x, y, z, gemv), r2 = dot4(p + 8, x, y, z, gemv);
     u = __ddiv_rn(r0, r2);
     v = __ddiv_rn(r1, r2);
 }
@@ -132,6 +137,8 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // lists the frame's entries of that range in entry order -- TF's order inside
 // every destination -- as 32-bit words (local destination << 24 | entry slot
 // - frame start). Workspace, in this order (host-computed, both calls agree):
+//   bar   [2][F]                  i32  the one-launch index build's frame barrier words (zero between calls:
+//                                        the workspace is zeroed once before its first use)
 //   hist  [2][F][n_chunks][nrmax] i32  entries per (index chunk, range)
 //   ext   [2][F][nrmax][2]        i32  bucket (start from the frame's first slot, entries)
 //   words [2][nnz_cap]            u32  the buckets, frame f's at [off[f], off[f] + nnz_f)
@@ -142,7 +149,7 @@ constexpr int BK_RBITS = 9;         // range bits matched by the placement's mul
 struct BkLayout {
     int n_frames, n_chunks, nr[2], nrmax;
     int64_t nnz_cap, kpf[2];
-    size_t hist, ext, words, bytes;  // byte offsets into the workspace, total
+    size_t bar, hist, ext, words, bytes;  // byte offsets into the workspace, total
 };
 
 inline BkLayout bk_layout(int n_frames, int n_chunks, int64_t nnz_cap, int64_t cells_per_frame,
@@ -158,6 +165,8 @@ inline BkLayout bk_layout(int n_frames, int n_chunks, int64_t nnz_cap, int64_t c
     if (l.nrmax < 1) l.nrmax = 1;
     const size_t F = (size_t)n_frames, cap = (size_t)(nnz_cap > 0 ? nnz_cap : 1);
     size_t o = 0;
+    l.bar = o;
+    o = align_up(o + 4 * 2 * F, 256);
     l.hist = o;
     o = align_up(o + 4 * 2 * F * (size_t)n_chunks * (size_t)l.nrmax, 256);
     l.ext = o;

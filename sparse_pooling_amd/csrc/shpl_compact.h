@@ -80,6 +80,7 @@ struct Bkt {
     PassCopy cp[2];
     int cp_at[2];     // the launch each copy rides: 0 = k_count, 1 = k_compact
     int cp_blocks;    // rider workgroups per frame in each launch (0: none)
+    int32_t *bar;     // [2][F] k_index1's frame barrier words (arrivals, departures): zero between calls
 };
 
 #ifndef SHPL_CP_BATCH
@@ -123,20 +124,53 @@ __device__ __forceinline__ void frame_range(const Frames &fr, int f, int64_t &p0
     p1 = fr.pt_count ? (p0 + fr.pt_count[f] < cap_end ? p0 + fr.pt_count[f] : cap_end) : cap_end;
 }
 
-// Pass 1 (grid n_chunks x n_frames): KEEP_MULTI / KEEP_ONE / AUX points per chunk.
-template <typename Stage, bool BKT = false>
-__global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr, Bkt bk) {
+#ifndef SHPL_IDX1_PROBE
+#define SHPL_IDX1_PROBE 0  // 1: each chunk workgroup's s_memrealtime stamps into g_idx1_probe (probe builds)
+#endif
+#if SHPL_IDX1_PROBE
+constexpr int IDX1_PROBE_BLOCKS = 4096;
+__device__ uint64_t g_idx1_probe[IDX1_PROBE_BLOCKS * 8];
+#define SHPL_IDX1_STAMP(k)                                                                          \
+    do {                                                                                            \
+        if (threadIdx.x == 0 && blockIdx.x < IDX1_PROBE_BLOCKS) {                                            \
+            uint64_t t_;                                                                            \
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
+            g_idx1_probe[blockIdx.x * 8 + (k)] = t_;                                                         \
+        }                                                                                           \
+    } while (0)
+#else
+#define SHPL_IDX1_STAMP(k) \
+    do {                   \
+    } while (0)
+#endif
+// Wave-wide integer sum and inclusive scan (the device library's DPP / swizzle forms: a chain of ds_bpermute
+// shuffles per value was most of the aggregate reads' time in k_index1). Integer sums: any order, same result.
+extern "C" __device__ int __ockl_wfred_add_i32(int);
+extern "C" __device__ int __ockl_wfscan_add_i32(int, bool);
+__device__ __forceinline__ int32_t wave_sum(int32_t v) { return __ockl_wfred_add_i32(v); }
+
+// A block barrier for LDS data only: no wait for the wave's global stores (__syncthreads() drains vmcnt, which
+// after the entries' stores held each barrier of the placement for their round trip to memory).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ void store_agent(int32_t *p, int32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the frame's aggregates are read with sc1 loads (agent scope, past this CU's L1): k_index1's barrier then
+// needs no acquire fence (the guide's hand-off with every handed-off byte stored and loaded sc1)
+__device__ __forceinline__ int32_t load_agent(const int32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Pass 1 of chunk j of frame f: KEEP_MULTI / KEEP_ONE / AUX points, and (BKT) the chunk's histograms over
+// the destination ranges; leaves the chunk's points in `in`.
+template <typename Stage, bool BKT>
+__device__ __forceinline__ void count_phase(const Stage &st, const Frames &fr, const Bkt &bk, int f, int j,
+                                            typename Stage::In (&in)[IDX_BATCH], uint32_t (&m_out)[IDX_BATCH],
+                                            typename Stage::Payload (&pl_out)[IDX_BATCH]) {
     __shared__ int32_t wsum[3][IDX_BLOCK / 64];
     __shared__ int32_t hist[BKT ? 2 * BK_MAX_RANGES : 1];
-    // rider workgroups: the launch's blocks past n_chunks in x (before the chunks measured slower)
-    const int f = blockIdx.y, j = (int)blockIdx.x;
     if constexpr (BKT) {
-        if (j >= fr.n_chunks) {  // a rider workgroup (uniform)
-            const int rj = j - fr.n_chunks;
-            for (int c = 0; c < 2; ++c)
-                if (bk.cp_at[c] == 0) pass_copy(bk.cp[c], f, rj, bk.cp_blocks);
-            return;
-        }
         for (int q = threadIdx.x; q < 2 * BK_MAX_RANGES; q += IDX_BLOCK) hist[q] = 0;
     }
     int64_t p0, p1, cap_end;
@@ -145,7 +179,6 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr, Bkt bk
     if (j == fr.n_chunks - 1 && p1 > base + IDX_CHUNK && threadIdx.x == 0 && fr.err)
         atomicOr(fr.err, SHPL_EBIT_CAPACITY);  // frame larger than max_points_per_frame
     const Ctx ctx{p1 - p0, -1};
-    typename Stage::In in[IDX_BATCH];
 #pragma unroll
     for (int u = 0; u < IDX_BATCH; ++u) {
         const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
@@ -156,8 +189,9 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr, Bkt bk
 #pragma unroll
     for (int u = 0; u < IDX_BATCH; ++u) {
         const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
-        typename Stage::Payload pl;
+        typename Stage::Payload &pl = pl_out[u];
         const uint32_t m = i < p1 ? st.eval(ctx, f, i, in[u], pl) : 0u;
+        m_out[u] = m;
 #pragma unroll
         for (int k = 0; k < 3; ++k) n[k] += (m >> k) & 1u;
         if constexpr (BKT) {
@@ -170,23 +204,43 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr, Bkt bk
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) n[k] += __shfl_xor(n[k], o, 64);
+        n[k] = wave_sum(n[k]);
         if ((threadIdx.x & 63) == 0) wsum[k][threadIdx.x >> 6] = n[k];
     }
     __syncthreads();
+    // the chunk's counts and histograms: write-through stores (sc1), which k_index1's frame barrier hands to
+    // the frame's other chunks with no release fence (the guide's in-launch counter form)
     if (threadIdx.x < 3) {
         int32_t t = 0;
         for (int w = 0; w < IDX_BLOCK / 64; ++w) t += wsum[threadIdx.x][w];
-        fr.chunk_kept[((int64_t)threadIdx.x * fr.n_frames + f) * fr.n_chunks + j] = t;
+        store_agent(fr.chunk_kept + ((int64_t)threadIdx.x * fr.n_frames + f) * fr.n_chunks + j, t);
     }
     if constexpr (BKT) {
         for (int i = threadIdx.x; i < 2 * bk.nrmax; i += IDX_BLOCK) {
             const int K = i / bk.nrmax, q = i - K * bk.nrmax;
-            bk.hist[(((int64_t)K * fr.n_frames + f) * fr.n_chunks + j) * bk.nrmax + q] =
-                q < bk.nr[K] ? hist[K * BK_MAX_RANGES + q] : 0;
+            store_agent(bk.hist + (((int64_t)K * fr.n_frames + f) * fr.n_chunks + j) * bk.nrmax + q,
+                        q < bk.nr[K] ? hist[K * BK_MAX_RANGES + q] : 0);
         }
     }
+}
+
+// Pass 1 (grid n_chunks x n_frames).
+template <typename Stage, bool BKT = false>
+__global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr, Bkt bk) {
+    // rider workgroups: the launch's blocks past n_chunks in x (before the chunks measured slower)
+    const int f = blockIdx.y, j = (int)blockIdx.x;
+    if constexpr (BKT) {
+        if (j >= fr.n_chunks) {  // a rider workgroup (uniform)
+            const int rj = j - fr.n_chunks;
+            for (int c = 0; c < 2; ++c)
+                if (bk.cp_at[c] == 0) pass_copy(bk.cp[c], f, rj, bk.cp_blocks);
+            return;
+        }
+    }
+    typename Stage::In in[IDX_BATCH];
+    uint32_t m[IDX_BATCH];
+    typename Stage::Payload pl[IDX_BATCH];
+    count_phase<Stage, BKT>(st, fr, bk, f, j, in, m, pl);
 }
 
 // k_compact's bucket placement (BKT), all threads: b_tot / b_bef = thread
@@ -197,18 +251,14 @@ __device__ __forceinline__ void bucket_place(const Stage &st, const Frames &fr, 
                                              int64_t p0, int64_t total, bool keep,
                                              const typename Stage::Payload &pl, int64_t pos, int32_t b_tot,
                                              int32_t b_bef, int32_t *s_off, int32_t *s_scan,
-                                             int32_t (*s_w)[IDX_BLOCK / 64][BK_MAX_RANGES]) {
+                                             int16_t (*s_w)[IDX_BLOCK / 64][BK_MAX_RANGES],
+                                             uint64_t (*s_peer)[BK_MAX_RANGES]) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int bK = threadIdx.x / BK_MAX_RANGES, bq = threadIdx.x % BK_MAX_RANGES;
     // 1. each range's start in the frame: exclusive scan of the totals, per key
-    int32_t x = b_tot;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
+    const int32_t x = __ockl_wfscan_add_i32(b_tot, true);  // inclusive, over the wave's 64 (key, range) lanes
     if (lane == 63) s_scan[wid] = x;
-    __syncthreads();
+    lds_barrier();
     int32_t start = x - b_tot;
     const int w0 = bK * (BK_MAX_RANGES / 64);  // the key's first wave
     for (int w = w0; w < wid; ++w) start += s_scan[w];
@@ -220,33 +270,39 @@ __device__ __forceinline__ void bucket_place(const Stage &st, const Frames &fr, 
             x2[1] = b_tot;
         }
     }
-    // 2. stable multisplit of the chunk's entries by range, per key (wave ballots over the range bits)
+    // 2. stable multisplit of the chunk's entries by range, per key: each lane ORs its bit into its wave's word
+    // of its range (s_peer, zero between uses), reads the word back -- the wave's lanes of the same range, its
+    // rank among them = the lanes below it -- and the lanes zero it again. One wave's LDS operations run in
+    // order, so the reads follow every OR of the wave and the zeroing every read. (Measured: a multisplit of
+    // ballots over the range bits spent ~2.4 us of VALU here at config 3.)
     int32_t kk[2] = {0, 0};
     const bool ok = total >= 2 && keep && st.bucket_keys(pl, kk[0], kk[1]);
     int32_t rank[2];
 #pragma unroll
     for (int K = 0; K < 2; ++K) {
         const int r = ok ? kk[K] / BK_KEYS : 0;
-        uint64_t peers = __ballot(ok);
-#pragma unroll
-        for (int bit = 0; bit < BK_RBITS; ++bit) {
-            const uint64_t bm = __ballot(ok && ((r >> bit) & 1));
-            peers &= ((r >> bit) & 1) ? bm : ~bm;
-        }
+        uint64_t peers = 0;
+        if (ok) atomicOr(reinterpret_cast<unsigned long long *>(&s_peer[wid][r]), 1ull << lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (ok) peers = s_peer[wid][r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (ok) s_peer[wid][r] = 0;
         rank[K] = (int32_t)lane_rank(peers);
-        if (ok && rank[K] == 0) s_w[K][wid][r] = (int32_t)__popcll(peers);
+        if (ok && rank[K] == 0) s_w[K][wid][r] = (int16_t)__popcll(peers);
     }
-    __syncthreads();
+    lds_barrier();
+    SHPL_IDX1_STAMP(5);
     if (bq < bk.nr[bK]) {  // waves' exclusive prefix per (key, range)
         int32_t run = 0;
 #pragma unroll
         for (int w = 0; w < IDX_BLOCK / 64; ++w) {
             const int32_t v = s_w[bK][w][bq];
-            s_w[bK][w][bq] = run;
+            s_w[bK][w][bq] = (int16_t)run;
             run += v;
         }
     }
-    __syncthreads();
+    lds_barrier();
+    SHPL_IDX1_STAMP(6);
     if (!ok) return;
 #pragma unroll
     for (int K = 0; K < 2; ++K) {
@@ -261,24 +317,23 @@ __device__ __forceinline__ void bucket_place(const Stage &st, const Frames &fr, 
 // chunk are ranked in order by wave ballots + an LDS prefix. Each chunk also
 // writes the sentinels of the unused capacity that falls in its stretch of
 // slots, and the frame's last chunk the frame's entry count.
-template <typename Stage, bool BKT = false>
-__global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr, Bkt bk) {
+// Pass 2 of chunk j of frame f (`loaded`: its points already in `in`, and pass 1's flags and payloads in
+// flags1 / pay1, from count_phase in the same launch: they are pass 2's own unless the frame has exactly one AUX point --
+// the stage's second product in the other order -- so only then is a point evaluated again).
+template <typename Stage, bool BKT>
+__device__ __forceinline__ void compact_phase(const Stage &st, const Frames &fr, const Bkt &bk, int f, int j,
+                                              typename Stage::In (&in)[IDX_BATCH], bool loaded,
+                                              const uint32_t (&flags1)[IDX_BATCH],
+                                              const typename Stage::Payload (&pay1)[IDX_BATCH]) {
     static_assert(!BKT || IDX_BATCH == 1, "bucket placement ranks one point per thread");
     __shared__ int32_t wsum[IDX_BATCH][IDX_BLOCK / 64];
-    __shared__ int32_t pre[IDX_BLOCK / 64], all[IDX_BLOCK / 64], naux[IDX_BLOCK / 64];
+    __shared__ int32_t pre[2][IDX_BLOCK / 64], all[2][IDX_BLOCK / 64], naux[IDX_BLOCK / 64];
     __shared__ int32_t s_off[BKT ? 2 * BK_MAX_RANGES : 1], s_scan[IDX_BLOCK / 64];
-    __shared__ int32_t s_w[BKT ? 2 : 1][IDX_BLOCK / 64][BKT ? BK_MAX_RANGES : 1];  // per-wave range counts
+    // per-wave range counts, then their prefixes over the waves (at most IDX_BLOCK: 16 bits, so that k_index1's
+    // two phases fit two 1024-thread workgroups per CU)
+    __shared__ int16_t s_w[BKT ? 2 : 1][IDX_BLOCK / 64][BKT ? BK_MAX_RANGES : 1];
     __shared__ int32_t s_tb[BKT ? 4 * BK_MAX_RANGES : 1];  // per (key, range): entries in the frame, in earlier chunks
-    // rider workgroups: the launch's blocks past n_chunks in x (before the chunks measured slower)
-    const int f = blockIdx.y, j = (int)blockIdx.x;
-    if constexpr (BKT) {
-        if (j >= fr.n_chunks) {  // a rider workgroup (uniform)
-            const int rj = j - fr.n_chunks;
-            for (int c = 0; c < 2; ++c)
-                if (bk.cp_at[c] == 1) pass_copy(bk.cp[c], f, rj, bk.cp_blocks);
-            return;
-        }
-    }
+    __shared__ uint64_t s_peer[BKT ? IDX_BLOCK / 64 : 1][BKT ? BK_MAX_RANGES : 1];  // per wave and range: lane bits
     int64_t p0, p1, cap_end;
     frame_range(fr, f, p0, p1, cap_end);
     const int wid = threadIdx.x >> 6;
@@ -300,7 +355,8 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr, Bkt 
             for (int j0 = sl; j0 < fr.n_chunks; j0 += 8 * S) {  // 8 loads in flight
                 int32_t v[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) v[u] = j0 + u * S < fr.n_chunks ? h[(int64_t)(j0 + u * S) * bk.nrmax] : 0;
+                for (int u = 0; u < 8; ++u)
+                    v[u] = j0 + u * S < fr.n_chunks ? load_agent(h + (int64_t)(j0 + u * S) * bk.nrmax) : 0;
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     tot += v[u];
@@ -320,45 +376,51 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr, Bkt 
             const int kw = i / bk.nrmax;
             s_w[kw / (IDX_BLOCK / 64)][kw % (IDX_BLOCK / 64)][i - kw * bk.nrmax] = 0;
         }
+        for (int i = threadIdx.x; i < (IDX_BLOCK / 64) * bk.nrmax; i += IDX_BLOCK)
+            s_peer[i / bk.nrmax][i % bk.nrmax] = 0;
     }
-    // the frame's AUX count picks the KEEP count (and the stage's product order)
+    // the frame's AUX count picks the KEEP count (and the stage's product order): the AUX counts and both
+    // KEEP counts of every chunk in one round trip, then the frame's and the earlier chunks' sums of each
     const int32_t *aux_c = fr.chunk_kept + ((int64_t)2 * fr.n_frames + f) * fr.n_chunks;
-    int32_t na = 0;
-    for (int q = threadIdx.x; q < fr.n_chunks; q += IDX_BLOCK) na += aux_c[q];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) na += __shfl_xor(na, o, 64);
-    if ((threadIdx.x & 63) == 0) naux[wid] = na;
+    const int32_t *k0_c = fr.chunk_kept + (int64_t)f * fr.n_chunks;
+    const int32_t *k1_c = fr.chunk_kept + ((int64_t)fr.n_frames + f) * fr.n_chunks;
+    int32_t na = 0, m0 = 0, e0 = 0, m1 = 0, e1 = 0;
+    for (int q = threadIdx.x; q < fr.n_chunks; q += IDX_BLOCK) {
+        const int32_t a = load_agent(aux_c + q), c0 = load_agent(k0_c + q), c1 = load_agent(k1_c + q);
+        na += a;
+        m0 += q < j ? c0 : 0;
+        e0 += c0;
+        m1 += q < j ? c1 : 0;
+        e1 += c1;
+    }
+    na = wave_sum(na);
+    m0 = wave_sum(m0);
+    e0 = wave_sum(e0);
+    m1 = wave_sum(m1);
+    e1 = wave_sum(e1);
+    if ((threadIdx.x & 63) == 0) {
+        naux[wid] = na;
+        pre[0][wid] = m0;
+        all[0][wid] = e0;
+        pre[1][wid] = m1;
+        all[1][wid] = e1;
+    }
     __syncthreads();
     int64_t n_aux = 0;
     for (int w = 0; w < IDX_BLOCK / 64; ++w) n_aux += naux[w];
+    SHPL_IDX1_STAMP(3);
     const Ctx ctx{p1 - p0, n_aux};
     const int variant = n_aux == 1 ? 1 : 0;
     const uint32_t keep_bit = variant ? KEEP_ONE : KEEP_MULTI;
-    // kept points of the earlier chunks, and of the whole frame
-    const int32_t *kept_c = fr.chunk_kept + ((int64_t)variant * fr.n_frames + f) * fr.n_chunks;
-    int32_t mine = 0, every = 0;
-    for (int q = threadIdx.x; q < fr.n_chunks; q += IDX_BLOCK) {
-        const int32_t c = kept_c[q];
-        mine += q < j ? c : 0;
-        every += c;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        mine += __shfl_xor(mine, o, 64);
-        every += __shfl_xor(every, o, 64);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        pre[wid] = mine;
-        all[wid] = every;
-    }
     const int64_t base = p0 + (int64_t)j * IDX_CHUNK;
-    typename Stage::In in[IDX_BATCH];
     typename Stage::Payload pl[IDX_BATCH];
     bool keep[IDX_BATCH];
+    if (!loaded) {
 #pragma unroll
-    for (int u = 0; u < IDX_BATCH; ++u) {
-        const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
-        if (i < p1) st.load(i, in[u]);
+        for (int u = 0; u < IDX_BATCH; ++u) {
+            const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
+            if (i < p1) st.load(i, in[u]);
+        }
     }
     uint64_t m[IDX_BATCH];
     int64_t b_pos = 0;  // BKT: this point's entry slot in the frame
@@ -367,15 +429,20 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr, Bkt 
         const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
         keep[u] = false;
         if (i < p1) {
-            keep[u] = (st.eval(ctx, f, i, in[u], pl[u]) & keep_bit) != 0;
+            if (loaded && n_aux != 1) {
+                keep[u] = (flags1[u] & keep_bit) != 0;
+                pl[u] = pay1[u];
+            } else {
+                keep[u] = (st.eval(ctx, f, i, in[u], pl[u]) & keep_bit) != 0;
+            }
             st.touch(f, i, pl[u], keep[u]);
         }
         m[u] = __ballot(keep[u]);
         if ((threadIdx.x & 63) == 0) wsum[u][wid] = (int32_t)__popcll(m[u]);
     }
-    __syncthreads();
+    lds_barrier();
     int64_t kept = 0;
-    for (int w = 0; w < IDX_BLOCK / 64; ++w) kept += pre[w];
+    for (int w = 0; w < IDX_BLOCK / 64; ++w) kept += pre[variant][w];
 #pragma unroll
     for (int u = 0; u < IDX_BATCH; ++u) {
         int32_t before = 0, tot = 0;
@@ -391,21 +458,117 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr, Bkt 
     }
     // sentinels of the unused capacity [p0 + total, cap_end), each chunk its own stretch
     int64_t total = 0;
-    for (int w = 0; w < IDX_BLOCK / 64; ++w) total += all[w];
+    for (int w = 0; w < IDX_BLOCK / 64; ++w) total += all[variant][w];
+    SHPL_IDX1_STAMP(4);
     if constexpr (BKT) {  // (s_tb written before k_compact's first barrier; entries past nr[K] never)
         const bool live = (int)(threadIdx.x % BK_MAX_RANGES) < bk.nr[threadIdx.x / BK_MAX_RANGES];
         bucket_place(st, fr, bk, f, j, p0, total, keep[0], pl[0], b_pos, live ? s_tb[threadIdx.x] : 0,
-                     live ? s_tb[2 * BK_MAX_RANGES + threadIdx.x] : 0, s_off, s_scan, s_w);
+                     live ? s_tb[2 * BK_MAX_RANGES + threadIdx.x] : 0, s_off, s_scan, s_w, s_peer);
     }
     const int64_t h0 = p0 + total > base ? p0 + total : base;
     const int64_t h1 = j == fr.n_chunks - 1 ? cap_end : (base + IDX_CHUNK < cap_end ? base + IDX_CHUNK : cap_end);
     for (int64_t pos = h0 + threadIdx.x; pos < h1; pos += IDX_BLOCK) st.hole(pos);
-    if (j != fr.n_chunks - 1) return;
-    if (threadIdx.x == 0) {
+    if (j == fr.n_chunks - 1 && threadIdx.x == 0) {
         if (fr.frame_nnz) fr.frame_nnz[f] = total;
         if (fr.frame_out_off) {
             fr.frame_out_off[f] = p0;
             if (f == fr.n_frames - 1) fr.frame_out_off[fr.n_frames] = cap_end;
+        }
+    }
+}
+
+// Pass 2 (same grid as pass 1).
+template <typename Stage, bool BKT = false>
+__global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr, Bkt bk) {
+    // rider workgroups: the launch's blocks past n_chunks in x (before the chunks measured slower)
+    const int f = blockIdx.y, j = (int)blockIdx.x;
+    if constexpr (BKT) {
+        if (j >= fr.n_chunks) {  // a rider workgroup (uniform)
+            const int rj = j - fr.n_chunks;
+            for (int c = 0; c < 2; ++c)
+                if (bk.cp_at[c] == 1) pass_copy(bk.cp[c], f, rj, bk.cp_blocks);
+            return;
+        }
+    }
+    typename Stage::In in[IDX_BATCH];
+    uint32_t m[IDX_BATCH] = {};
+    typename Stage::Payload pl[IDX_BATCH];
+    compact_phase<Stage, BKT>(st, fr, bk, f, j, in, false, m, pl);
+}
+
+// Both passes of the bucketed index in ONE launch (k_index1, small batches): a 1-D grid, every frame's chunk
+// workgroups first (f = b / n_chunks, j = b % n_chunks), then the rider workgroups of both copies. Between the
+// passes each chunk waits at its frame's barrier -- pass 2 needs the frame's totals (its AUX count, every
+// chunk's kept count and range histogram) -- published by the release / acquire hand-off of the guide's
+// in-launch counter form: the chunk's write-through (sc1) stores, every wave's vmcnt(0), the block barrier and
+// an agent-scope fetch_add on the frame's arrival word (no release fence); one lane polls it (relaxed, agent scope,
+// bounded: SHPL_EBIT_BARRIER on give-up), and every load of the aggregates is an sc1 load (no acquire fence). The chunk's points stay
+// in registers between the passes (no second load). Each chunk then adds to the frame's departure word, and
+// the last to depart zeroes both words for the next call (the words start at zero: the caller's workspace is
+// zeroed once; every call leaves them zero, a timed-out one included). Residency: the barrier waits only for
+// the frame's own chunks, all dispatched before any rider of the launch; the host takes this form only for
+// frames of at most IDX1_MAX_CHUNKS chunks, so a frame's chunks never fill an XCD's workgroup slots.
+constexpr int IDX1_MAX_CHUNKS = 32;
+constexpr uint64_t IDX1_SPIN_TICKS = 2000000;  // 20 ms of s_memrealtime (100 MHz): the barrier's give-up
+
+__device__ __forceinline__ void frame_barrier(const Frames &fr, const Bkt &bk, int f) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through aggregate stores done
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(bk.bar + f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t t0 = wall_clock64();
+        while (__hip_atomic_load(bk.bar + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < fr.n_chunks) {
+            if (wall_clock64() - t0 > IDX1_SPIN_TICKS) {
+                if (fr.err) atomicOr(fr.err, SHPL_EBIT_BARRIER);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();  // (every later load of the frame's aggregates is an sc1 load: no acquire fence)
+}
+
+#ifndef SHPL_IDX1_WPE
+#define SHPL_IDX1_WPE 0  // waves per SIMD asked of the register allocator (8: two workgroups per CU); 0 = its own
+#endif
+template <typename Stage>
+__global__ __launch_bounds__(IDX_BLOCK)
+#if SHPL_IDX1_WPE
+__attribute__((amdgpu_waves_per_eu(SHPL_IDX1_WPE, SHPL_IDX1_WPE)))
+#endif
+void k_index1(Stage st, Frames fr, Bkt bk) {
+    const int64_t b = blockIdx.x, n_ch = (int64_t)fr.n_frames * fr.n_chunks;
+    if (b >= n_ch) {  // a rider workgroup (uniform): copy c's workgroup r of frame f
+        const int64_t rj = b - n_ch;
+        const int per = bk.cp_blocks;
+        const int f = (int)(rj / (2 * per)), c = (int)((rj / per) & 1), r = (int)(rj % per);
+        if (bk.cp[c].row_bytes > 0) pass_copy(bk.cp[c], f, r, per);
+        return;
+    }
+    const int f = (int)(b / fr.n_chunks), j = (int)(b - (int64_t)f * fr.n_chunks);
+    SHPL_IDX1_STAMP(0);
+    // the frame's projection matrix into LDS, its loads in flight beside the frame offsets' (count_phase's first
+    // block barrier precedes every eval): read from global memory inside eval it was one more round trip
+    __shared__ double s_P[12];
+    if (threadIdx.x < 12) s_P[threadIdx.x] = st.P[12 * (int64_t)f + threadIdx.x];
+    Stage sf = st;
+    sf.P_frame = s_P;
+    typename Stage::In in[IDX_BATCH];
+    uint32_t m[IDX_BATCH];
+    typename Stage::Payload pl[IDX_BATCH];
+    count_phase<Stage, true>(sf, fr, bk, f, j, in, m, pl);
+    SHPL_IDX1_STAMP(1);
+    frame_barrier(fr, bk, f);
+    SHPL_IDX1_STAMP(2);
+    compact_phase<Stage, true>(sf, fr, bk, f, j, in, true, m, pl);
+    lds_barrier();  // every wave is past its reads of the frame's aggregates
+    SHPL_IDX1_STAMP(7);
+    if (threadIdx.x == 0) {
+        const int32_t d = __hip_atomic_fetch_add(bk.bar + fr.n_frames + f, 1, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+        if (d == fr.n_chunks - 1) {  // the last to leave: every chunk of the frame is past its poll
+            __hip_atomic_store(bk.bar + f, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(bk.bar + fr.n_frames + f, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -431,6 +594,26 @@ int run_compaction(const Stage &st, int n_frames, int64_t max_points, const int6
     const dim3 grid(fr.n_chunks, n_frames);
     if constexpr (Stage::HAS_BUCKETS) {
         if (bk) {
+#ifndef SHPL_INDEX1
+#define SHPL_INDEX1 1
+#endif
+#ifndef SHPL_IDX1_RIDERS
+#define SHPL_IDX1_RIDERS 240
+#endif
+            if (SHPL_INDEX1 && bk->bar && fr.n_chunks <= IDX1_MAX_CHUNKS) {
+                // rider workgroups per copy and frame: SHPL_IDX1_RIDERS per copy over the batch, at most one per
+                // 64 KiB of a frame's copy (the two-launch form's cp_blocks bound)
+                int per = SHPL_IDX1_RIDERS / n_frames;
+                if (per > bk->cp_blocks) per = bk->cp_blocks;
+                if (per < 1) per = 1;
+                Bkt b1 = *bk;
+                b1.cp_blocks = per;
+                const bool any = bk->cp[0].row_bytes > 0 || bk->cp[1].row_bytes > 0;
+                const int64_t blocks = (int64_t)n_frames * fr.n_chunks + (any ? (int64_t)n_frames * 2 * per : 0);
+                hipLaunchKernelGGL((k_index1<Stage>), dim3((unsigned)blocks), dim3(IDX_BLOCK), 0, stream, st, fr, b1);
+                SHPL_LAUNCH_CHECK();
+                return SHPL_OK;
+            }
             bool rides[2] = {false, false};
             for (int c = 0; c < 2; ++c)
                 if (bk->cp[c].row_bytes > 0) rides[bk->cp_at[c]] = true;

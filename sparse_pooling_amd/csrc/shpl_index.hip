@@ -106,6 +106,7 @@ struct FusedStage {
     float *val;
     int64_t *mij, *flip;
     uint32_t *err;
+    const double *P_frame = nullptr;  // k_index1: this frame's P, staged in LDS at the launch's start
 
     struct Payload {
         Produced pr;
@@ -122,10 +123,17 @@ struct FusedStage {
     }
     // AUX = inside the clip (the columns of the second projection)
     __device__ uint32_t eval(const Ctx &c, int f, int64_t, const In &in, Payload &pl) const {
-        double u, v;
-        project(P + 12 * f, in.x, in.y, in.z, u, v, c.n_live == 1);
+        double u, v, Pf[12];
+        if (P_frame) {  // (LDS: flat loads only on this path; the global one keeps global loads)
+#pragma unroll
+            for (int k = 0; k < 12; ++k) Pf[k] = P_frame[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 12; ++k) Pf[k] = P[12 * f + k];
+        }
+        project(Pf, in.x, in.y, in.z, u, v, c.n_live == 1);
         if (!in_image(u, v, g.im_w, g.im_h)) return 0u;
-        if (c.n_aux == 1 && c.n_live != 1) project(P + 12 * f, in.x, in.y, in.z, u, v, true);
+        if (c.n_aux == 1 && c.n_live != 1) project(Pf, in.x, in.y, in.z, u, v, true);
         const double ur = (double)(int64_t)rint(u);
         const double vr = (double)(int64_t)rint(v);
         pl.pr = produce(g, ur, vr, in.vx, in.vz);
@@ -372,7 +380,8 @@ extern "C" int shpl_build_index_buckets(int n_frames, const int64_t *d_point_off
 #define SHPL_RIDERS 0
 #endif
     Bkt bk{{l.nr[0], l.nr[1]}, l.nrmax, nnz_cap, (int32_t *)(b + l.hist), (int32_t *)(b + l.ext),
-           (uint32_t *)(b + l.words), {}, {SHPL_RIDERS == 2 ? 1 : 0, SHPL_RIDERS == 1 ? 0 : 1}, 0};
+           (uint32_t *)(b + l.words), {}, {SHPL_RIDERS == 2 ? 1 : 0, SHPL_RIDERS == 1 ? 0 : 1}, 0,
+           (int32_t *)(b + l.bar)};
     const shpl_pass_copy *cps[2] = {cell_copy, pixel_copy};
     int64_t copy_bytes = 0;
     for (int k = 0; k < 2; ++k) {
@@ -462,3 +471,14 @@ extern "C" int shpl_produce_index(int64_t nv, const void *d_bv_index, int bv_ity
     }
     return SHPL_ERR_ARG;
 }
+
+#if SHPL_IDX1_PROBE
+// probe builds only: the last k_index1 launch's per-chunk stamps (start, phase 1 done, past the frame barrier,
+// aggregates read, points placed, buckets placed, holes written, end), 100 MHz ticks, chunks in launch order
+extern "C" int shpl_probe_idx1(uint64_t *host, size_t n_blocks) {
+    if (n_blocks > (size_t)shpl::IDX1_PROBE_BLOCKS) n_blocks = shpl::IDX1_PROBE_BLOCKS;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(shpl::g_idx1_probe), 64 * n_blocks, 0, hipMemcpyDeviceToHost) == hipSuccess
+               ? SHPL_OK
+               : SHPL_ERR_HIP;
+}
+#endif

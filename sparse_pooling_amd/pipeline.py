@@ -101,7 +101,8 @@ class FusedPipeline:
         self._lib = L.lib()
         if self.buckets:
             nb = L.bucket_ws_bytes(self.B, self.max_points, self.N, self.Hb * self.Wb, self.Hi * self.Wi)
-            self.bkt_ws = L.workspace(nb, dev)
+            # zeroed once: its frame barrier words start at zero (every call leaves them so)
+            self.bkt_ws = torch.zeros(max(int(nb), 256), dtype=torch.uint8, device=dev)
             self.bkt = L.ShplBuckets(self.B, self.max_points, self.N, self.Hb * self.Wb, self.Hi * self.Wi,
                                      self.frame_off.data_ptr(), self.frame_nnz.data_ptr(), self.cell.data_ptr(),
                                      self.pix.data_ptr(), self.val.data_ptr(), self.bkt_ws.data_ptr(),

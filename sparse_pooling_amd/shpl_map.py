@@ -71,6 +71,8 @@ class ShplMap:
                 what.append("number of M values does not match number of indices")
             if bits & L.EBIT_CAPACITY:
                 what.append("a frame holds more points than max_points_per_frame")
+            if bits & L.EBIT_BARRIER:  # not an input error: the one-launch index build could not proceed
+                raise RuntimeError("shpl_build_index_buckets: a frame barrier timed out (chunks not resident)")
             raise InvalidArgumentError("; ".join(what))
 
     # ------------------------------------------------------------------ CSR
