@@ -22,6 +22,13 @@
 namespace shpl {
 
 // Number of set bits of `mask` in lanes below this lane (wave64).
+// Wave-wide integer sum and inclusive scan (the device library's DPP / swizzle forms: a chain of ds_bpermute
+// shuffles per value was most of the aggregate reads' time in k_index1). Integer sums: any order, same result.
+extern "C" __device__ int __ockl_wfred_add_i32(int);
+extern "C" __device__ int __ockl_wfscan_add_i32(int, bool);
+__device__ __forceinline__ int32_t wave_sum(int32_t v) { return __ockl_wfred_add_i32(v); }
+__device__ __forceinline__ int32_t wave_incl_scan(int32_t v) { return __ockl_wfscan_add_i32(v, true); }
+
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                      __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));

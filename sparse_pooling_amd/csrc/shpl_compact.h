@@ -143,12 +143,6 @@ __device__ uint64_t g_idx1_probe[IDX1_PROBE_BLOCKS * 8];
     do {                   \
     } while (0)
 #endif
-// Wave-wide integer sum and inclusive scan (the device library's DPP / swizzle forms: a chain of ds_bpermute
-// shuffles per value was most of the aggregate reads' time in k_index1). Integer sums: any order, same result.
-extern "C" __device__ int __ockl_wfred_add_i32(int);
-extern "C" __device__ int __ockl_wfscan_add_i32(int, bool);
-__device__ __forceinline__ int32_t wave_sum(int32_t v) { return __ockl_wfred_add_i32(v); }
-
 // A block barrier for LDS data only: no wait for the wave's global stores (__syncthreads() drains vmcnt, which
 // after the entries' stores held each barrier of the placement for their round trip to memory).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -256,7 +250,7 @@ __device__ __forceinline__ void bucket_place(const Stage &st, const Frames &fr, 
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int bK = threadIdx.x / BK_MAX_RANGES, bq = threadIdx.x % BK_MAX_RANGES;
     // 1. each range's start in the frame: exclusive scan of the totals, per key
-    const int32_t x = __ockl_wfscan_add_i32(b_tot, true);  // inclusive, over the wave's 64 (key, range) lanes
+    const int32_t x = wave_incl_scan(b_tot);  // over the wave's 64 (key, range) lanes
     if (lane == 63) s_scan[wid] = x;
     lds_barrier();
     int32_t start = x - b_tot;

@@ -813,13 +813,17 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
                                                  int32_t *ent_col, int32_t *key_range) {
     constexpr int NW = BLOCK / 64;
     __shared__ int32_t cnt[NW][RANGE_KEYS], s_tot[RANGE_KEYS], s_beg[RANGE_KEYS];
+    __shared__ uint64_t s_peer[NW][RANGE_KEYS];  // per wave and destination: its batch's lanes (zero between uses)
     __shared__ uint32_t l_w[LCAP > 0 ? LCAP : 1];
     __shared__ int32_t l_s[LCAP > 0 ? LCAP : 1];
     __shared__ float l_v[LCAP > 0 ? LCAP : 1];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const bool staged = n <= LCAP;
     const int32_t L = (n + NW - 1) / NW;  // words per wave slice
-    for (int i = threadIdx.x; i < NW * RANGE_KEYS; i += BLOCK) cnt[i / RANGE_KEYS][i % RANGE_KEYS] = 0;
+    for (int i = threadIdx.x; i < NW * RANGE_KEYS; i += BLOCK) {
+        cnt[i / RANGE_KEYS][i % RANGE_KEYS] = 0;
+        s_peer[i / RANGE_KEYS][i % RANGE_KEYS] = 0;
+    }
     __syncthreads();
     // 1. per-slice counts (and, staged, the words with their sources and values into LDS)
     for (int32_t i0 = threadIdx.x; i0 < n; i0 += 4 * BLOCK) {  // 4 words per thread in flight
@@ -858,13 +862,7 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
         int32_t v = 0;
 #pragma unroll
         for (int s = 0; s < NW; ++s) v += cnt[s][threadIdx.x];
-        int32_t x = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        s_tot[threadIdx.x] = x;  // inclusive prefix inside the wave
+        s_tot[threadIdx.x] = wave_incl_scan(v);  // inclusive prefix inside the wave
     }
     __syncthreads();
     if ((int)threadIdx.x < RANGE_KEYS) {
@@ -904,12 +902,15 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
             }
         }
         const int t = (int)(w >> 24);
-        uint64_t peers = __ballot(ok);
-#pragma unroll
-        for (int bit = 0; bit < 7; ++bit) {
-            const uint64_t bm = __ballot(ok && ((t >> bit) & 1));
-            peers &= ((t >> bit) & 1) ? bm : ~bm;
-        }
+        // the batch's lanes of destination t: each ORs its bit into the wave's word of t, reads it back, and the
+        // lanes zero it again (one wave's LDS operations run in order; 7 ballots over the destination bits cost
+        // more VALU)
+        uint64_t peers = 0;
+        if (ok) atomicOr(reinterpret_cast<unsigned long long *>(&s_peer[wid][t]), 1ull << lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (ok) peers = s_peer[wid][t];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (ok) s_peer[wid][t] = 0;
         const int32_t rank = (int32_t)lane_rank(peers);
         const int32_t base = ok ? cnt[wid][t] : 0;
         // the batch's last lane of each destination moves the slice's cursor (after every lane's read: one
