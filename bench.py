@@ -94,6 +94,9 @@ def parse():
     ap.add_argument("--split-pull", default="once", choices=["once", "rows"],
                     help="split layer: the pooled half by shpl_pull_once (sparse walk + the empty rows' zeros) or by "
                          "the row-keyed k_rows (A/B)")
+    ap.add_argument("--head-k", type=int, default=None,
+                    help="bucketed pipelines: run heads per destination in the CSRs (FusedPipeline.HEAD_K; 0 = none; "
+                         "A/B)")
     ap.add_argument("--pixel-cols", action="store_true",
                     help="bucketed config 3: the pixel-keyed CSR keeps ent_col (per-column partials in its pulls) "
                          "instead of the identity-column form")
@@ -443,6 +446,8 @@ def main():
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, dev)
     pipeline.FusedPipeline.PIXEL_COLS = args.pixel_cols
     pipeline.FusedPipeline.SPLIT_ONCE = args.split_pull == "once"
+    if args.head_k is not None:
+        pipeline.FusedPipeline.HEAD_K = args.head_k
     esz0 = 2 if dtype == torch.bfloat16 else 4
     split = (not dual and not args.rows and not args.no_overlap and
              (args.split == "on" or (args.split == "auto" and min(spec.c_bev, spec.c_img) * esz0 >= 1024)))

@@ -308,7 +308,14 @@ typedef struct {
     int64_t n_frames;
     int64_t flags;     /* SHPL_CSR_IDENTITY_COLS: a pixel-keyed CSR whose every entry is a column of its own
                           (built by shpl_build_csr_buckets), so ent_col may be NULL; 0 otherwise */
+    int32_t *heads;    /* optional [n_keys][head_k][2] run heads: (ent_src, ent_val bits) of each destination's
+                          first min(run, head_k) sorted entries, filled by shpl_build_csr_buckets beside
+                          key_range (the other builders take a CSR without them: SHPL_ERR_ARG otherwise). The
+                          row-keyed pulls read them in the round trip of key_range instead of reading the
+                          entries after it (bitwise the same). NULL: not built. */
+    int64_t head_k;    /* 1 .. SHPL_CSR_MAX_HEAD when heads is set */
 } shpl_csr;
+#define SHPL_CSR_MAX_HEAD 32
 #define SHPL_LIVE_MAX_FRAMES 1024
 #define SHPL_CSR_IDENTITY_COLS 1
 

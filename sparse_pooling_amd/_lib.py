@@ -24,6 +24,7 @@ OUT_POOL, OUT_CONCAT, OUT_ADD = 0, 1, 2
 ACT_NONE, ACT_RELU = 0, 1
 CSR_AUTO, CSR_FRAME, CSR_SEGMENT, CSR_RANGE = 0, 1, 2, 3
 CSR_IDENTITY_COLS = 1
+CSR_MAX_HEAD = 32
 
 _lib = None
 
@@ -41,16 +42,17 @@ class ShplCsr(ctypes.Structure):
                 ("ent_val", ctypes.c_void_p), ("ent_col", ctypes.c_void_p),
                 ("n_keys", ctypes.c_int64), ("nnz_cap", ctypes.c_int64), ("key_range", ctypes.c_void_p),
                 ("frame_off", ctypes.c_void_p), ("frame_nnz", ctypes.c_void_p), ("n_frames", ctypes.c_int64),
-                ("flags", ctypes.c_int64)]
+                ("flags", ctypes.c_int64), ("heads", ctypes.c_void_p), ("head_k", ctypes.c_int64)]
 
 
 class Csr:
     """Device buffers of one destination-sorted entry list (owned tensors + the ABI struct)."""
 
-    def __init__(self, n_keys, nnz_cap, device, with_col, key_range=False, identity_cols=False):
+    def __init__(self, n_keys, nnz_cap, device, with_col, key_range=False, identity_cols=False, head_k=0):
         """key_range: also keep the (first, end) entry of every destination
         (shpl_csr.key_range): shpl_pull then runs its one-launch row-keyed form.
-        identity_cols: a pixel-keyed CSR of shpl_build_csr_buckets without ent_col (SHPL_CSR_IDENTITY_COLS)."""
+        identity_cols: a pixel-keyed CSR of shpl_build_csr_buckets without ent_col (SHPL_CSR_IDENTITY_COLS).
+        head_k: run heads of that many entries per destination (shpl_csr.heads; shpl_build_csr_buckets)."""
         i32 = dict(dtype=torch.int32, device=device)
         cap = max(int(nnz_cap), 1)
         self.n_keys, self.nnz_cap = int(n_keys), int(nnz_cap)
@@ -64,6 +66,11 @@ class Csr:
                               self.ent_col.data_ptr() if with_col else None, self.n_keys, self.nnz_cap,
                               self.key_range.data_ptr() if key_range else None)
         self.struct.flags = CSR_IDENTITY_COLS if identity_cols else 0
+        self.heads = None
+        if head_k:
+            assert key_range and 1 <= head_k <= CSR_MAX_HEAD
+            self.heads = torch.empty((max(self.n_keys, 1), int(head_k), 2), **i32)
+            self.struct.heads, self.struct.head_k = self.heads.data_ptr(), int(head_k)
 
     def live_frames(self, frame_off, frame_nnz):
         """Hand the sparse pass the frame layout the CSR was built with (device i64 [F+1] / [F],

@@ -810,7 +810,8 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
                                                  int64_t k0, int nk, int direction, const int32_t *col,
                                                  const int32_t *cell, const int32_t *pix, const float *vals,
                                                  int32_t *ent_dst, int32_t *ent_src, float *ent_val,
-                                                 int32_t *ent_col, int32_t *key_range) {
+                                                 int32_t *ent_col, int32_t *key_range, int2 *heads = nullptr,
+                                                 int head_k = 0) {
     constexpr int NW = BLOCK / 64;
     __shared__ int32_t cnt[NW][RANGE_KEYS], s_tot[RANGE_KEYS], s_beg[RANGE_KEYS];
     __shared__ uint64_t s_peer[NW][RANGE_KEYS];  // per wave and destination: its batch's lanes (zero between uses)
@@ -922,6 +923,8 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
             ent_src[o] = src;
             ent_val[o] = val;
             if (ent_col) ent_col[o] = kk;
+            const int32_t hp = base + rank - s_beg[t];  // the entry's place in its destination's run
+            if (heads && hp < head_k) heads[(k0 + t) * head_k + hp] = int2{src, __float_as_int(val)};
         }
     }
 }
@@ -938,6 +941,8 @@ struct BsSide {
     float *ent_val;
     int32_t *ent_col, *key_range;
     int64_t blocks;    // n_frames * nr
+    int2 *heads;       // optional run heads (shpl_csr.heads)
+    int head_k;
 };
 
 struct BsIn {
@@ -991,7 +996,7 @@ __global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide 
     }
     const int64_t out0 = p0 + start;
     bucket_sort_emit<BS_BLOCK, BS_LCAP>(W, n, p0, out0, k0, nk, direction, nullptr, in.cell, in.pix, in.val, sd.ent_dst,
-                                        sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range);
+                                        sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range, sd.heads, sd.head_k);
     // the frame's unused capacity (its last range), the slots and key ranges after the last frame
     if (q != sd.nr - 1) return;
     for (int64_t h = p0 + valid + threadIdx.x; h < cap_end; h += BS_BLOCK) sd.ent_dst[h] = -1;
@@ -1076,6 +1081,7 @@ extern "C" int shpl_build_csr_path(int path, int direction, int order, int n_fra
                                    const shpl_csr *csr, void *d_ws, size_t ws_bytes, void *stream) {
     if (path < SHPL_CSR_AUTO || path > SHPL_CSR_RANGE) return SHPL_ERR_ARG;
     if (!csr || !d_frame_off || n_frames < 1) return SHPL_ERR_ARG;
+    if (csr->heads) return SHPL_ERR_ARG;  // run heads: shpl_build_csr_buckets only
     if (direction != SHPL_BY_CELL && direction != SHPL_BY_PIXEL) return SHPL_ERR_ARG;
     if (order < SHPL_ORDER_ENTRY || order > SHPL_ORDER_COL_ENTRY) return SHPL_ERR_ARG;
     const int64_t nnz_cap = csr->nnz_cap;
@@ -1232,8 +1238,9 @@ extern "C" int shpl_build_csr_buckets(const shpl_buckets *bk, const shpl_csr *by
             return SHPL_ERR_BAD_SHAPE;
         if (bk->nnz_cap > 0 && (!c->ent_dst || !c->ent_src || !c->ent_val)) return SHPL_ERR_ARG;
         if (k == 1 && !c->ent_col && !(c->flags & SHPL_CSR_IDENTITY_COLS)) return SHPL_ERR_ARG;
+        if (c->heads && (c->head_k < 1 || c->head_k > SHPL_CSR_MAX_HEAD || !c->key_range)) return SHPL_ERR_ARG;
         s[k] = BsSide{l.nr[k], l.kpf[k], c->n_keys, c->nnz_cap, c->ent_dst, c->ent_src, c->ent_val, c->ent_col,
-                      c->key_range, (int64_t)bk->n_frames * l.nr[k]};
+                      c->key_range, (int64_t)bk->n_frames * l.nr[k], (int2 *)c->heads, (int)c->head_k};
         if (l.nr[k] == 0) s[k].blocks = 0;
     }
     hipStream_t st = (hipStream_t)stream;

@@ -159,6 +159,10 @@ struct Ents {
     // [frame_off[f], frame_off[f+1]), the rest of the capacity is empty
     const int64_t *frame_off, *frame_nnz;
     int n_frames;
+    // optional run heads (shpl_csr.heads, row-keyed pulls): (source, value bits) of each destination's first
+    // head_k entries, loaded in the round trip of its key_range
+    const int2 *heads;
+    int head_k;
 };
 
 // The live-entry table of a frame layout in LDS (one per workgroup): s_off[f] = frame f's first slot
@@ -560,7 +564,8 @@ __device__ uint64_t g_probe[2 * PROBE_WAVES];
 template <typename T, int VEC, bool GROUP, int G, int MODE = -1>
 __device__ __forceinline__ void row_walk(const Feat &f, const Ents &e, int64_t row, bool live, int32_t first,
                                          int32_t end, bool p0, typename Chunk<T, VEC>::raw_t pv,
-                                         typename Chunk<T, VEC>::raw_t av) {
+                                         typename Chunk<T, VEC>::raw_t av, int2 head = int2{0, 0},
+                                         bool has_head = false) {
     typedef Chunk<T, VEC> C;
     const int lane = threadIdx.x & 63, lg = lane & (G - 1), gbase = lane & ~(G - 1);
     T *out = reinterpret_cast<T *>(f.out);
@@ -586,10 +591,12 @@ __device__ __forceinline__ void row_walk(const Feat &f, const Ents &e, int64_t r
         for (int j = 0; j < VEC; ++j) acc[j] = q[j] = 0.0f;
         int32_t kprev = -1;
         for (int32_t j0 = 0; j0 < wlen; j0 += G) {
-            // index words of entries first + j0 + lg of this lane's row
+            // index words of entries first + j0 + lg of this lane's row (the first ones from the run heads,
+            // already in registers, when the CSR carries them)
             const bool has = j0 + lg < len;
-            const int32_t my_src = has ? e.src[first + j0 + lg] : 0;
-            const float my_val = has ? e.val[first + j0 + lg] : 0.0f;
+            const bool from_head = has_head && j0 == 0;
+            const int32_t my_src = !has ? 0 : from_head ? head.x : e.src[first + j0 + lg];
+            const float my_val = !has ? 0.0f : from_head ? __int_as_float(head.y) : e.val[first + j0 + lg];
             const int32_t my_col = (GROUP && has) ? e.col[first + j0 + lg] : 0;
             const int32_t n = min(G, wlen - j0);
             for (int32_t u0 = 0; u0 < n; u0 += ROWS_WALK) {
@@ -668,9 +675,14 @@ __device__ __forceinline__ void rows_body(const Feat &f, const Ents &e, const in
         first = key_range[2 * row];
         end = key_range[2 * row + 1];
     }
+    // the run's first head_k entries from the run heads, in the same round trip (lanes past head_k, and
+    // entries past it, read the CSR arrays in row_walk)
+    const bool has_head = !GROUP && e.heads != nullptr && lg < e.head_k;
+    int2 head = int2{0, 0};
+    if (live && has_head) head = e.heads[row * e.head_k + lg];
     if (p0) pv = C::load_nt(pass + (row * f.pass_stride + (int64_t)lg * VEC));
     if (a0) av = C::load(pass + (row * f.pass_stride + (int64_t)lg * VEC));
-    row_walk<T, VEC, GROUP, G, MODE>(f, e, row, live, first, end, p0, pv, av);
+    row_walk<T, VEC, GROUP, G, MODE>(f, e, row, live, first, end, p0, pv, av, head, has_head);
 }
 
 template <typename T, int VEC, bool GROUP, int G>
@@ -744,6 +756,7 @@ int plan(int direction, int dtype, const shpl_csr *csr, const void *d_src, int64
         return SHPL_ERR_ARG;
     if (mode != SHPL_OUT_POOL && !d_pass) return SHPL_ERR_ARG;
     if (mode == SHPL_OUT_ADD && c_pass != c_pool) return SHPL_ERR_BAD_SHAPE;
+    if (csr->heads && (csr->head_k < 1 || csr->head_k > SHPL_CSR_MAX_HEAD || !csr->key_range)) return SHPL_ERR_ARG;
     const int64_t width = mode == SHPL_OUT_CONCAT ? c_pass + c_pool : c_pool;
     if (out_stride < width || (c_pool > 0 && src_stride < src_off + c_pool) ||
         (mode != SHPL_OUT_POOL && pass_stride < pass_off + c_pass))
@@ -903,6 +916,8 @@ int sparse(const Plan &pl, const shpl_csr *csr, int direction, hipStream_t s) {
 template <typename T, int VEC, bool GROUP>
 int rows_t(const Plan &pl, const shpl_csr *csr, hipStream_t s) {
     Ents e{csr->nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_col, csr->ent_val};
+    e.heads = (const int2 *)csr->heads;
+    e.head_k = (int)csr->head_k;
     // lanes per row: the pooled chunks of a row, at least 8 (index words come G at a time), at most a wave
     int G = 8;
     while (G < 64 && (uint32_t)G < pl.f.cpool) G <<= 1;
@@ -1071,6 +1086,8 @@ extern "C" int shpl_pull_pair(const shpl_csr *by_cell, const shpl_pull_desc *d_c
         while (G < 64 && (uint32_t)G < pl[k].f.cpool) G <<= 1;  // lanes per row: the widest pooled row
         s[k] = RowsSide{pl[k].f, Ents{c->nnz_cap, c->ent_dst, c->ent_src, c->ent_col, c->ent_val}, c->key_range,
                         pl[k].n_dst, 0};
+        s[k].e.heads = (const int2 *)c->heads;
+        s[k].e.head_k = (int)c->head_k;
     }
     if (dtype < 0) return SHPL_OK;
     if (dtype == SHPL_F32) return v16 ? pair_t<float, 4>(s, G, st) : pair_t<float, 1>(s, G, st);

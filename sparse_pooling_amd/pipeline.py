@@ -31,6 +31,9 @@ class FusedPipeline:
     # split: the pooled half by shpl_pull_once (k_sparse's walk + the empty rows' zeros, one launch); False: the
     # row-keyed k_rows (1.11 ms per 64 frames at config 6, a wave per 1 KB row: latency-bound)
     SPLIT_ONCE = True
+    # bucketed CSRs: run heads of this many entries per destination (shpl_csr.heads; 0 = none): the row-keyed
+    # pulls read a row's first entries in the round trip of its key_range
+    HEAD_K = 8
 
     def __init__(self, n_frames, max_points_per_frame, total_points, im_size, bv_size, stride,
                  c_bev, c_img, dtype=torch.float32, device="cuda", dual=False, rows=None, live=False,
@@ -84,14 +87,15 @@ class FusedPipeline:
         self.err = torch.zeros(1, **i32)
         self.index_ws = L.workspace(L.index_ws_bytes(self.B, self.max_points), dev)
         # rows pulls: with key_range
+        head_k = self.HEAD_K if self.buckets else 0
         self.csr = L.Csr(self.n_cells, self.N, dev, with_col=False,
-                         key_range=self.rows or self.split)  # BEV-cell CSR (img -> BEV)
+                         key_range=self.rows or self.split, head_k=head_k)  # BEV-cell CSR (img -> BEV)
         self.bv_fused = torch.empty((self.B, self.Hb, self.Wb, self.Cb + self.Ci), dtype=dtype, device=dev)
         if dual:
             # pixel CSR (BEV -> img); from the buckets without ent_col: every entry its own column (shpl.h)
             with_col = not self.buckets or self.PIXEL_COLS
             self.pcsr = L.Csr(self.n_pix, self.N, dev, with_col=with_col, key_range=self.rows,
-                              identity_cols=not with_col)
+                              identity_cols=not with_col, head_k=head_k)
             self.img_fused = torch.empty((self.B, self.Hi, self.Wi, self.Ci + self.Cb), dtype=dtype,
                                          device=dev)
         if live:

@@ -141,6 +141,16 @@ def test_argument_validation_is_host_side():
     pnocol = L.ShplCsr(256, 256, 256, None, 4 * 6750, 80000, 256)  # pixel side: neither ent_col nor the flag
     assert lib.shpl_pull_pair(None, None, ctypes.byref(pnocol), ctypes.byref(d32), N) == L.ERR_ARG
     assert lib.shpl_build_csr_buckets(ctypes.byref(bk), None, ctypes.byref(pnocol), N) == L.ERR_ARG
+    # run heads (shpl_csr.heads): head_k in [1, SHPL_CSR_MAX_HEAD] with key_range, built by the bucket CSR only
+    for k, with_range in ((0, True), (L.CSR_MAX_HEAD + 1, True), (8, False)):
+        hc = L.ShplCsr(256, 256, 256, None, 4 * 8800, 80000, 256 if with_range else None)
+        hc.heads, hc.head_k = 256, k
+        assert lib.shpl_build_csr_buckets(ctypes.byref(bk), ctypes.byref(hc), None, N) == L.ERR_ARG
+        assert lib.shpl_pull_pair(ctypes.byref(hc), ctypes.byref(d32), None, None, N) == L.ERR_ARG
+    hc = L.ShplCsr(256, 256, 256, None, 4 * 8800, 80000, 256)
+    hc.heads, hc.head_k = 256, 8
+    assert lib.shpl_build_csr(L.BY_CELL, L.ORDER_ENTRY, 4, P, N, 8800, P, N, P, P, ctypes.byref(hc), P, 1 << 24,
+                              N) == L.ERR_ARG  # the other builders do not fill run heads
     # velodyne loader: P2 without image size, misaligned scan
     assert lib.shpl_velo_to_cam(1, P, 10, P, P, P, N, math.nan, N, P, P, N, P, 1 << 20, N) == L.ERR_ARG
     assert lib.shpl_velo_to_cam(1, P, 10, ctypes.c_void_p(260), P, N, N, math.nan, N, P, P, N, P, 1 << 20,

@@ -700,10 +700,18 @@ def _ragged_pipeline_run(cfg, sizes, dtype, paths, channels=None, frames=None):
     codes = {None: L.CSR_AUTO, "frame": L.CSR_FRAME, "segment": L.CSR_SEGMENT, "range": L.CSR_RANGE}
     for path in paths:
         # a named CSR builder: the CSR pulls (no buckets); None: the pipeline's default
+        # "buckets_hK": the bucketed step with K run heads per destination in its CSRs (shpl_csr.heads)
         kw = {"buckets": dict(rows=True, buckets=True),
-              "csr_rows": dict(rows=True, buckets=False), None: {}}.get(path, dict(buckets=False))
-        pl = pipeline.FusedPipeline(B, maxp, N, base.im_size, base.bv_size, base.stride, Cb, Ci, dtype=tdt,
-                                    dual=True, **kw)
+              "csr_rows": dict(rows=True, buckets=False), None: {}}.get(
+                  path, dict(rows=True, buckets=True) if path and path.startswith("buckets_h") else dict(buckets=False))
+        head_k = pipeline.FusedPipeline.HEAD_K
+        if path and path.startswith("buckets_h"):
+            pipeline.FusedPipeline.HEAD_K = int(path[len("buckets_h"):])
+        try:
+            pl = pipeline.FusedPipeline(B, maxp, N, base.im_size, base.bv_size, base.stride, Cb, Ci, dtype=tdt,
+                                        dual=True, **kw)
+        finally:
+            pipeline.FusedPipeline.HEAD_K = head_k
         if path is not None:
             assert pl.buckets == path.startswith("buckets")
         pl.csr_path = codes.get(path, L.CSR_AUTO)
@@ -731,15 +739,17 @@ def test_bucket_pulls_ragged_batch(dtype, cb, ci):
     one point, no survivor, one survivor among 14 points (the dgemv projection order: no
     bucket, the entry read from the index arrays), chunk-straddling and full frames --
     bitwise against the oracle and against the range CSR + k_rows path, for every lane
-    group width (G = 8 .. 64) and the unvectorised form (3 / 5 and 4 / 6 f32 channels)."""
-    _ragged_pipeline_run(3, [0, 1, -40, 1025, 20000, 2], dtype, ["buckets", "csr_rows"],
+    group width (G = 8 .. 64) and the unvectorised form (3 / 5 and 4 / 6 f32 channels); with the default
+    run heads (shpl_csr.heads), none and one per destination."""
+    _ragged_pipeline_run(3, [0, 1, -40, 1025, 20000, 2], dtype, ["buckets", "csr_rows", "buckets_h0", "buckets_h1"],
                          channels=(cb, ci))
 
 
 def test_bucket_pulls_long_runs():
     """One frame whose 3000 points are one point repeated (one cell, one pixel: one bucket, one
     run of 3000 entries, sorted in 12 rounds) beside a frame with half its points on one cell:
-    bitwise against the oracle, f32 and bf16."""
+    bitwise against the oracle, f32 and bf16, with the default run heads, 32 (more than some lane groups
+    hold) and none."""
     base = synth.CONFIGS[3]
     rng = np.random.default_rng(9)
     one = synth.make_frame(synth.FrameSpec(1, base.im_size, base.bv_size, base.stride, 32, 32), seed=3)
@@ -752,7 +762,8 @@ def test_bucket_pulls_long_runs():
     frames = [heavy, synth.make_frame(synth.FrameSpec(3000, base.im_size, base.bv_size, base.stride, 32, 32),
                                       seed=5, n_outside=int(rng.integers(1, 50))), mixed]
     for dtype in ("f32", "bf16"):
-        _ragged_pipeline_run(3, None, dtype, ["buckets"], channels=(32, 32), frames=frames)
+        _ragged_pipeline_run(3, None, dtype, ["buckets", "buckets_h32", "buckets_h0"], channels=(32, 32),
+                             frames=frames)
 
 
 def test_pipeline_ragged_batch_every_csr_path():
