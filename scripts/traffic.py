@@ -15,7 +15,8 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-SHORT = (("k_conv_rows<4, 2, true", "k_conv_rows_pooled_bf16"), ("k_conv_rows<4, 4, false", "k_conv_rows_dense_bf16"),
+SHORT = (("k_conv_wide", "k_conv_wide"), ("k_pool_runs_wide", "k_pool_runs_wide"), ("k_pack_wide", "k_pack_wide"),
+         ("k_conv_rows<4, 2, true", "k_conv_rows_pooled_bf16"), ("k_conv_rows<4, 4, false", "k_conv_rows_dense_bf16"),
          ("k_pool_runs", "k_pool_runs"), ("k_occ_frame", "k_occ_frame"), ("k_pack_w", "k_pack_w"),
          ("k_conv3x3<float, true", "k_conv3x3_pooled_f32"), ("k_conv3x3<float, false", "k_conv3x3_dense_f32"),
          ("k_conv3x3<unsigned short, true", "k_conv3x3_pooled_bf16"),
@@ -60,13 +61,14 @@ def per_kernel(counter, pattern=None):
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
-def conv(key, dt):
-    """scripts/gpu_conv_prof.sh passes: pmc_conv_<dt>_1 FETCH_SIZE, _2 WRITE_SIZE,
-    _3 SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE (MFMA busy share, clock)."""
-    fetch = per_kernel("FETCH_SIZE", f"pmc_conv_{dt}_1")
-    write = per_kernel("WRITE_SIZE", f"pmc_conv_{dt}_2")
-    mfma = per_kernel("SQ_VALU_MFMA_BUSY_CYCLES", f"pmc_conv_{dt}_3")
-    grbm = per_kernel("GRBM_GUI_ACTIVE", f"pmc_conv_{dt}_3")
+def conv(key, dt, tag=None):
+    """scripts/gpu_conv_prof.sh passes: pmc_conv_<tag>_1 FETCH_SIZE, _2 WRITE_SIZE,
+    _3 SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE (MFMA busy share, clock); tag = dt, or c6_<dt> (CFG=6)."""
+    tag = tag or dt
+    fetch = per_kernel("FETCH_SIZE", f"pmc_conv_{tag}_1")
+    write = per_kernel("WRITE_SIZE", f"pmc_conv_{tag}_2")
+    mfma = per_kernel("SQ_VALU_MFMA_BUSY_CYCLES", f"pmc_conv_{tag}_3")
+    grbm = per_kernel("GRBM_GUI_ACTIVE", f"pmc_conv_{tag}_3")
     out = {}
     for k in sorted(set(fetch) | set(write)):
         f_b, w_b = 2 * fetch.get(k, 0.0) * 1024, write.get(k, 0.0) * 1024
@@ -77,12 +79,14 @@ def conv(key, dt):
                   "mfma_busy_share": mfma.get(k, 0.0) / (1024 * cyc) if cyc else None}
     # bf16: the fused call is k_pack_w + k_occ_frame + k_pool_runs + k_conv_rows (row-streaming kernel);
     # f32: k_pack_w + k_row_ptr + k_conv3x3 (tiled)
-    main_k = "k_conv_rows_pooled_bf16" if dt == "bf16" else f"k_conv3x3_pooled_{dt}"
-    call = [main_k] + (["k_pool_runs", "k_occ_frame", "k_pack_w"] if dt == "bf16" else [])
+    wide = tag.startswith("c6_") and dt == "bf16"
+    main_k = "k_conv_wide" if wide else "k_conv_rows_pooled_bf16" if dt == "bf16" else f"k_conv3x3_pooled_{dt}"
+    call = [main_k] + (["k_pool_runs_wide", "k_occ_frame", "k_pack_wide"] if wide else
+                       ["k_pool_runs", "k_occ_frame", "k_pack_w"] if dt == "bf16" else [])
     path = os.path.join(ROOT, "profiles", "traffic.json")
     tj = json.load(open(path)) if os.path.exists(path) else {}
     tj[key] = {"hbm_bytes_per_launch": sum(out[k]["fetch_bytes"] + out[k]["write_bytes"] for k in call if k in out),
-               **stamp(f"pmc_conv_{dt}_1.log", f"pmc_conv_{dt}_2.log"),
+               **stamp(f"pmc_conv_{tag}_1.log", f"pmc_conv_{tag}_2.log"),
                "main_kernel": main_k, "mfma_busy_share": out[main_k]["mfma_busy_share"], "kernels": out,
                "note": (f"hbm_bytes_per_launch: the fused conv call ({' + '.join(call)}); FETCH_SIZE x2 (gfx950 "
                         "wide-read correction), KiB -> bytes; WRITE_SIZE exact (16 B/lane stores); mfma_busy_share "
@@ -110,7 +114,7 @@ def main(key):
     print(json.dumps(tj[key], indent=1))
 
 
-LAYER = ("k_dense", "k_sparse", "k_sparse_long", "k_rows", "k_bpull")
+LAYER = ("k_dense", "k_sparse", "k_sparse_long", "k_rows", "k_bpull", "k_once")
 
 
 def step_traffic(key, tag, layer_kernels=LAYER, anchor="k_count"):
@@ -163,7 +167,9 @@ if __name__ == "__main__":
         every = len(sys.argv) > 4 and sys.argv[4] == "all"
         step_traffic(sys.argv[2], sys.argv[3], None if every else LAYER, sys.argv[5] if len(sys.argv) > 5 else "k_count")
         sys.exit(0)
-    if key.startswith("conv_"):
+    if key.startswith("conv_c6_"):  # conv_c6_<dt>_F64: the RetinaNet conv (gpu_conv_prof.sh CFG=6)
+        conv(key, key.split("_")[2], "c6_" + key.split("_")[2])
+    elif key.startswith("conv_"):
         conv(key, key.split("_")[1])
     else:
         main(key)
