@@ -91,6 +91,9 @@ def parse():
                     help="img->BEV layer: the pass-through copy beside the index chain and the pooled half written once "
                          "by a row-keyed pull after it, on a high-priority stream (FusedPipeline split); auto: on "
                          "for 1 KB halves (config 6)")
+    ap.add_argument("--split-chain", default="current", choices=["current", "stream"],
+                    help="split layer: the index chain on the (high-priority) stream the step runs on, only the copy "
+                         "forked (current), or on a stream of its own forked beside the copy (stream; A/B)")
     ap.add_argument("--split-pull", default="once", choices=["once", "rows"],
                     help="split layer: the pooled half by shpl_pull_once (sparse walk + the empty rows' zeros) or by "
                          "the row-keyed k_rows (A/B)")
@@ -455,6 +458,9 @@ def main():
                                 spec.c_img, dtype=dtype, dual=dual, device=dev, rows=True if args.rows else None,
                                 buckets=False if args.no_buckets else None, split=split)
     chain = torch.cuda.Stream(device=dev, priority=-1) if split else None
+    if split and args.split_chain == "current":
+        # every launch of this run on the high-priority stream: a caller whose layer runs on such a stream
+        torch.cuda.set_stream(chain)
     Hb, Wb = spec.bev_feat_hw
     Hi, Wi = spec.img_feat_hw
     feats = lambda shape, seed: sd.fill_features(torch.empty(shape, dtype=dtype, device=dev), fids, seed)  # noqa
@@ -486,6 +492,10 @@ def main():
             pl.layer_sparse(bev, img)
             if ev is not None:
                 ev[3].record()
+        elif split and args.split_chain == "current":
+            # the layer called on the high-priority stream the whole run is on (below): the chain runs there,
+            # only the copy forks to `side`
+            pl.step_split(pts, vox, off, P, bev, img, side, None, events=ev[:4] if ev else None)
         elif split:
             pl.step_split(pts, vox, off, P, bev, img, side, chain, events=ev[:4] if ev else None)
         else:

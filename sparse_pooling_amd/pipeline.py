@@ -283,10 +283,15 @@ class FusedPipeline:
     def step_split(self, points, voxels, point_offsets, P, bev, img, side, chain, events=None):
         """split: the pass-through copy on `side`, the index chain and then the pooled half on `chain` (a
         high-priority stream, so its latency-bound workgroups are dispatched ahead of the copy's); neither
-        waits for the other (disjoint columns of bv_fused). events: [copy start, copy end, chain start, end]."""
+        waits for the other (disjoint columns of bv_fused). events: [copy start, copy end, chain start, end].
+        chain None: the chain runs on the current stream itself (a caller running on a high-priority stream),
+        so that one step's chain follows the previous one's with no cross-stream hop; only the copy forks."""
         main = torch.cuda.current_stream(self.dev)
         side.wait_stream(main)
-        chain.wait_stream(main)
+        if chain is None:
+            chain = main
+        else:
+            chain.wait_stream(main)
         # the chain is issued (and, in a captured graph, its nodes created) first: its first launch is
         # dispatched before the copy's workgroups fill the chip
         with torch.cuda.stream(chain):
@@ -304,7 +309,8 @@ class FusedPipeline:
             if events:
                 events[1].record(side)
         main.wait_stream(side)
-        main.wait_stream(chain)
+        if chain is not main:
+            main.wait_stream(chain)
 
     def step_overlapped(self, points, voxels, point_offsets, P, bev, img, side, mval=None, events=None,
                         side2=None):

@@ -469,13 +469,15 @@ def test_pipeline_batch_matches_oracle(cfg, dual):
             _close_and_exact(iout[f:f + 1], ei)
 
 
-@pytest.mark.parametrize("cfg,dtype,graph,once", [(6, "f32", False, True), (6, "f32", True, True),
-                                                  (6, "bf16", False, True), (2, "f32", False, True),
-                                                  (6, "f32", False, False), (2, "bf16", True, False)])
-def test_split_pipeline_matches_oracle(cfg, dtype, graph, once, monkeypatch):
+@pytest.mark.parametrize("cfg,dtype,graph,once,own", [(6, "f32", False, True, True), (6, "f32", True, True, True),
+                                                      (6, "bf16", False, True, True), (2, "f32", False, True, True),
+                                                      (6, "f32", False, False, True), (2, "bf16", True, False, True),
+                                                      (6, "f32", False, True, False), (6, "bf16", True, True, False)])
+def test_split_pipeline_matches_oracle(cfg, dtype, graph, once, own, monkeypatch):
     """FusedPipeline(split=True): the pass-through copy beside the index chain, the frame CSR with key ranges
     (k_csr_frame + k_key_range) and the pooled half written once (shpl_pull_once, or the row-keyed k_rows) -- eager and captured
-    in a HIP graph (two replays) -- bitwise the oracle's bv_fused on 3 frames (one with no point)."""
+    in a HIP graph (two replays) -- bitwise the oracle's bv_fused on 3 frames (one with no point). own: the chain
+    on a stream of its own; else on the (high-priority) stream the step is called on (chain=None)."""
     from sparse_pooling_amd import pipeline
     monkeypatch.setattr(pipeline.FusedPipeline, "SPLIT_ONCE", once)
     spec = synth.CONFIGS[cfg]
@@ -497,17 +499,21 @@ def test_split_pipeline_matches_oracle(cfg, dtype, graph, once, monkeypatch):
     side = torch.cuda.Stream(device=DEV)
     chain = torch.cuda.Stream(device=DEV, priority=-1)
     pl.bv_fused.fill_(float("nan"))  # every element must be written
+    torch.cuda.synchronize()
     if graph:
         g = torch.cuda.CUDAGraph()
         gs = torch.cuda.Stream(device=DEV)
         gs.wait_stream(torch.cuda.current_stream())
         with torch.cuda.graph(g, stream=gs):
-            pl.step_split(pts, vox, off, P, tb, ti, side, chain)
+            pl.step_split(pts, vox, off, P, tb, ti, side, chain if own else None)
         pl.bv_fused.fill_(float("nan"))
         g.replay()
         g.replay()
-    else:
+    elif own:
         pl.step_split(pts, vox, off, P, tb, ti, side, chain)
+    else:
+        with torch.cuda.stream(chain):
+            pl.step_split(pts, vox, off, P, tb, ti, side, None)
     torch.cuda.synchronize()
     assert int(pl.err.item()) == 0
     out = pl.bv_fused.float().cpu().numpy()
