@@ -45,23 +45,25 @@ def test_bench_outputs_equal_oracle_tables(args, key, frames):
     assert out.get("index_errors", 0) == 0
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "f32"])
-def test_conv_table_is_a_tolerance_checked_output(dtype):
-    """The conv workload's tables (conv_<dtype>_frames64) come from a GPU run: TF's Conv2D fixes no summation
-    order, so no oracle checksum exists (bench.py labels them self-referential). What pins them: the bench's
-    conv of global frames 0 and 1 -- built here as run_conv builds it, 2 frames instead of 64 -- has the stored
-    checksums (the output does not depend on the batch), and a band of each frame is within the conv tests'
-    tolerance of the oracle's double-precision conv of the oracle's bv_fused (tests/test_gpu_conv.py bounds)."""
+@pytest.mark.parametrize("cfg,dtype", [(2, "bf16"), (2, "f32"), (6, "bf16"), (6, "f32")])
+def test_conv_table_is_a_tolerance_checked_output(cfg, dtype):
+    """The conv workload's tables (conv[_c6]_<dtype>_frames64) come from a GPU run: TF's Conv2D fixes no
+    summation order, so no oracle checksum exists (bench.py labels them self-referential). What pins them: the
+    bench's conv of global frames 0 and 1 -- built here as run_conv builds it, 2 frames instead of 64 -- has the
+    stored checksums (the output does not depend on the batch), and a band of each frame is within the conv
+    tests' tolerance of the oracle's double-precision conv of the oracle's bv_fused (tests/test_gpu_conv.py
+    bounds). cfg 6: RetinaNet's 512 -> 256 conv with a bias and ReLU (bf16: k_conv_wide)."""
     import numpy as np
     import torch
 
     from oracle import shpl_oracle as orc
     from sparse_pooling_amd import dist as sd, fusion_conv as fc, pipeline, synth
+    retina = cfg == 6
     with open(os.path.join(ROOT, "profiles", "frame_checksums.json")) as fh:
-        table = json.load(fh)[f"conv_{dtype}_frames64"]
+        table = json.load(fh)[f"conv{'_c6' if retina else ''}_{dtype}_frames64"]
     dev = torch.device("cuda", 0)
     dt = torch.bfloat16 if dtype == "bf16" else torch.float32
-    spec = synth.CONFIG2
+    spec = synth.CONFIGS[cfg]
     fids = [0, 1]
     frames = [synth.make_frame(spec, seed=s, n_outside=200) for s in fids]
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, dev)
@@ -72,8 +74,13 @@ def test_conv_table_is_a_tolerance_checked_output(dtype):
     cb, ci = spec.c_bev, spec.c_img
     bev = sd.fill_features(torch.empty((2, Hb, Wb, cb), dtype=dt, device=dev), fids, 1)
     img = sd.fill_features(torch.empty((2, Hi, Wi, ci), dtype=dt, device=dev), fids, 2)
-    conv = fc.FusionConv(cb + ci, ci, dtype=dt, device=dev, seed=0)
-    out = torch.empty((2, Hb, Wb, ci), dtype=dt, device=dev)
+    c_out = 256 if retina else ci
+    if retina:  # as bench.py run_conv builds it
+        conv = fc.FusionConv(cb + ci, c_out, batch_norm=False, bias=True, relu=True, dtype=dt, device=dev, seed=0)
+        conv.bias.copy_(torch.linspace(-0.5, 0.5, c_out, device=dev))
+    else:
+        conv = fc.FusionConv(cb + ci, ci, dtype=dt, device=dev, seed=0)
+    out = torch.empty((2, Hb, Wb, c_out), dtype=dt, device=dev)
     pl.build_index(pts, vox, off, P)
     pl.build_csr(("cell",))
     conv.fused_csr(bev, img, pl.csr, pl.frame_off, is_training=False, out=out)
@@ -81,8 +88,8 @@ def test_conv_table_is_a_tolerance_checked_output(dtype):
     cs = sd.frame_checksums(out).tolist()
     assert cs == table[:2], (cs, table[:2])
     w = conv.weights.float().cpu().numpy()
-    center, scale, shift = (v.cpu().numpy() for v in conv._inference_epilogue())
-    y0, y1 = 296, 344
+    center, scale, shift = (None if v is None else v.float().cpu().numpy() for v in conv._inference_epilogue())
+    y0, y1 = (80, 88) if retina else (296, 344)  # a band of rows (the 512-channel oracle conv is slow)
     for k, fid in enumerate(fids):
         fr = frames[k]
         g = orc.gen_sparse_pooling_input_avod(fr.points, fr.voxel_indices, fr.P, list(spec.im_size),
@@ -96,7 +103,7 @@ def test_conv_table_is_a_tolerance_checked_output(dtype):
         x = np.ascontiguousarray(eb[:, y0 - 1:y1 + 1])
         want = orc.conv3x3(x, w, center, scale, shift, True)
         _, ab = orc.conv3x3(np.abs(x), np.abs(w), raw=True)
-        bound = 1e-5 + 2.0 ** -19 * ab * np.abs(scale)
+        bound = 1e-5 + 2.0 ** -19 * ab * (np.abs(scale) if scale is not None else 1.0)
         if dtype == "bf16":
             bound = bound + np.abs(want) * 2.0 ** -8
         got = out[k:k + 1, y0 - 1:y1 + 1].float().cpu().numpy()
