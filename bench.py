@@ -375,7 +375,8 @@ def pinned_to(key):
         return None
     if key.startswith("layer_config") or key.startswith("frames_"):
         return "oracle"
-    return "gpu-run (self-referential; parity by tolerance tests, tests/test_gpu_conv.py)"
+    return ("gpu-run (self-referential; frames 0-1 rebuilt and checked against the oracle's double conv within "
+            "tolerance: tests/test_gpu_checksums_oracle.py::test_conv_table_is_a_tolerance_checked_output)")
 
 
 def lib_sha256():
