@@ -97,6 +97,10 @@ def parse():
     ap.add_argument("--split-pull", default="once", choices=["once", "rows"],
                     help="split layer: the pooled half by shpl_pull_once (sparse walk + the empty rows' zeros) or by "
                          "the row-keyed k_rows (A/B)")
+    ap.add_argument("--sparse-tail", type=int, default=None,
+                    help="img->BEV layers: the streaming pass in two launches, the sparse pass of the first frames "
+                         "beside the last B // N frames' stream (FusedPipeline.SPARSE_TAIL, default 0 = one streaming launch; "
+                         "A/B)")
     ap.add_argument("--head-k", type=int, default=None,
                     help="bucketed pipelines: run heads per destination in the CSRs (FusedPipeline.HEAD_K; 0 = none; "
                          "A/B)")
@@ -452,6 +456,8 @@ def main():
     pipeline.FusedPipeline.SPLIT_ONCE = args.split_pull == "once"
     if args.head_k is not None:
         pipeline.FusedPipeline.HEAD_K = args.head_k
+    if args.sparse_tail is not None:
+        pipeline.FusedPipeline.SPARSE_TAIL = args.sparse_tail
     esz0 = 2 if dtype == torch.bfloat16 else 4
     split = (not dual and not args.rows and not args.no_overlap and
              (args.split == "on" or (args.split == "auto" and min(spec.c_bev, spec.c_img) * esz0 >= 1024)))
@@ -572,6 +578,8 @@ def main():
     comm = sd.comm_report(dev)
     nbytes = step_bytes(cfg, spec, nnz, u_pix, u_cell, F, esz)
     interleaved = dual and not args.no_overlap and not pl.rows and pl.interleave
+    # img->BEV with the sparse tail: the head frames' sparse pass runs beside the tail's stream
+    interleaved = interleaved or (not args.no_overlap and not split and pl._sparse_tail() > 0)
     dense_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args_steps_ev
     sparse_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args_steps_ev
     bwd_ms = sum(e[4].elapsed_time(e[5]) for e in evs) / args_steps_ev if backward else 0.0
@@ -645,8 +653,11 @@ def main():
             "roofline": {
                 "bound": "hbm",
                 "kernel": ("SHPL layer pulls: k_dense (concat stream) + k_sparse (pooled gather); achieved over "
-                           + ("the layer's window (first k_dense start to last k_sparse end: the cell-keyed gathers "
-                              "run beside img_fused's stream)" if interleaved else "their summed durations")
+                           + (("the layer's window (first k_dense start to last k_sparse end: the cell-keyed "
+                               "gathers run beside img_fused's stream)") if interleaved and dual else
+                              ("the layer's window (first k_dense start to last k_sparse end: the head frames' "
+                               "k_sparse runs beside the last frames' k_dense)") if interleaved else
+                              "their summed durations")
                            + ("; split step (the pass-through copy beside the index chain, then the pooled half "
                               "written once by the row-keyed pull): every kernel of the step, timed as the replayed "
                               "step (HIP events around the graph replays)" if split else "")
