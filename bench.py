@@ -97,6 +97,9 @@ def parse():
     ap.add_argument("--split-pull", default="once", choices=["once", "rows"],
                     help="split layer: the pooled half by shpl_pull_once (sparse walk + the empty rows' zeros) or by "
                          "the row-keyed k_rows (A/B)")
+    ap.add_argument("--split-form", default="serial", choices=["serial", "overlap"],
+                    help="split layer: the pooled half after the pass-through copy, the step captured in a graph "
+                         "(serial), or beside the copy, eager with the chain at high priority (overlap; A/B)")
     ap.add_argument("--sparse-tail", type=int, default=None,
                     help="img->BEV layers: the streaming pass in two launches, the sparse pass of the first frames "
                          "beside the last B // N frames' stream (FusedPipeline.SPARSE_TAIL, default 0 = one streaming launch; "
@@ -454,6 +457,7 @@ def main():
     pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, dev)
     pipeline.FusedPipeline.PIXEL_COLS = args.pixel_cols
     pipeline.FusedPipeline.SPLIT_ONCE = args.split_pull == "once"
+    pipeline.FusedPipeline.SPLIT_SERIAL = args.split_form == "serial"
     if args.head_k is not None:
         pipeline.FusedPipeline.HEAD_K = args.head_k
     if args.sparse_tail is not None:
@@ -526,7 +530,7 @@ def main():
     # the timed loop replays it, so host launch gaps leave the step. Kernel
     # durations for the roofline come from the same step run eagerly with events.
     graph, graph_note = None, None
-    if split and not args.graph:
+    if split and not args.graph and args.split_form == "overlap":
         # a captured graph of the split step ran its two branches nearly in series (the chain's nodes start
         # after the copy has filled the chip: no stream priority inside a graph): 1.77 vs 1.40 ms eager at
         # config 6 (profiles/r05_c6b_ab.log); --graph forces the capture
@@ -658,9 +662,11 @@ def main():
                               ("the layer's window (first k_dense start to last k_sparse end: the head frames' "
                                "k_sparse runs beside the last frames' k_dense)") if interleaved else
                               "their summed durations")
-                           + ("; split step (the pass-through copy beside the index chain, then the pooled half "
-                              "written once by the row-keyed pull): every kernel of the step, timed as the replayed "
-                              "step (HIP events around the graph replays)" if split else "")
+                           + (("; split step (the pass-through copy k_dense beside the index chain, then the "
+                               "pooled half written once by shpl_pull_once's k_once): every kernel of the step, "
+                               + ("timed as the replayed step (HIP events around the graph replays)"
+                                  if graph is not None else "the eager step's window from the chain's start"))
+                              if split else "")
                            + ("; bucketed one-stream step: the forward bracket spans the whole forward "
                               "(index + buckets with the pass-through copies riding its launches, both CSRs, the "
                               "pooled pull pair), the backward bracket the gradient pull pair -- every kernel of "

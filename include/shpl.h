@@ -404,8 +404,9 @@ int shpl_pull_sparse(int direction, int dtype, const shpl_csr *csr, const void *
  * SHPL_OUT_POOL only (out rows' pooled columns; a concat's pass-through half is the caller's, e.g. a
  * shpl_pull_dense with c_pool = 0 beside the index build), csr->key_range required (shpl_build_csr_path(
  * SHPL_CSR_FRAME) fills it from the frame sort). Destinations whose run is empty get zeros; the others the
- * sums of shpl_pull (same order, bitwise). ONE launch: k_sparse's (entry, chunk) walk over every run beside
- * a wave per 16 rows storing the empty rows' zeros. Replaces: the pooled half of sparse_pool_utils.py:96-103
+ * sums of shpl_pull (same order, bitwise). ONE launch: the occupied rows by a wave per 64 sorted entries
+ * (cell-keyed rows of >= 32 chunks of 16 bytes; else a thread per (entry, chunk)) beside a wave per 16 rows
+ * storing the empty rows' zeros. Replaces: the pooled half of sparse_pool_utils.py:96-103
  * + :72 where k_dense's zeros would be rewritten (wide channels: RetinaNet's 256). */
 int shpl_pull_once(int direction, int dtype, const shpl_csr *csr, const void *d_src, int64_t src_stride,
                    int64_t src_off, int64_t c_pool, const void *d_pass, int64_t pass_stride, int64_t pass_off,

@@ -367,26 +367,150 @@ __global__ __launch_bounds__(SHPL_BLOCK) void k_sparse(const Feat f, const Ents 
 }
 
 // shpl_pull_once: the pooled part of every destination row written exactly once, in ONE launch and with no
-// streaming pass before it. Blocks [0, sblocks) run k_sparse's (entry, chunk) walk over every run (the run
-// heads write the occupied rows); the rest zero the rows whose key_range is empty: a wave per ONCE_ROWS rows,
-// one key_range load for all of them, then their zero chunks stored with nothing to wait for. Rows and
-// stores are disjoint between the two parts.
+// streaming pass before it. The sblocks run-walking blocks write the occupied rows: seg_window's wave per 64
+// sorted entries for wide cell-keyed rows (once_seg), else k_sparse's (entry, chunk) walk over every run; the
+// rest zero the rows whose key_range is empty: a wave per ONCE_ROWS rows, one key_range load for all of them,
+// then their zero chunks stored with nothing to wait for. Rows and stores are disjoint between the two parts.
 #ifndef SHPL_ONCE_ROWS
 #define SHPL_ONCE_ROWS 16
+#endif
+#ifndef SHPL_ONCE_XCD
+#define SHPL_ONCE_XCD 1
 #endif
 #ifndef SHPL_ONCE_ZERO_FIRST
 #define SHPL_ONCE_ZERO_FIRST 1  // the zeroing blocks first: 1.401-1.404 vs 1.408-1.410 ms at config 6 (profiles/r05_once_ab.log)
 #endif
 constexpr int ONCE_ROWS = SHPL_ONCE_ROWS;
+#ifndef SHPL_ONCE_SEG
+#define SHPL_ONCE_SEG 1
+#endif
+#ifndef SHPL_SEG_BATCH
+#define SHPL_SEG_BATCH 8
+#endif
+constexpr int SEG_BATCH = SHPL_SEG_BATCH;
+// the window walk for cell-keyed rows of at least half a wave of chunks (RetinaNet's 256 channels: 64 f32 /
+// 32 bf16 chunks); narrower rows would leave most lanes idle through the window's serial walk (measured as
+// shpl_pull_sparse's form at config 2's 32 channels: 205 vs 80 us)
+__host__ __device__ constexpr bool once_seg(bool group, uint32_t cpool) {
+    return SHPL_ONCE_SEG && !group && cpool >= 32;
+}
+
+template <typename T, int VEC>
+__device__ __forceinline__ void seg_load(const T *sc, int64_t stride, int32_t sr, bool ok,
+                                         typename Chunk<T, VEC>::raw_t &raw) {
+    if (ok) raw = Chunk<T, VEC>::load(sc + (int64_t)sr * stride);
+}
+
+// The occupied rows of shpl_pull_once by windows of 64 sorted entries, one wave per window (cell-keyed, no
+// column partials): the window's index words in one coalesced round trip (lane l holds entry s0 + l), the run
+// heads and boundaries as ballots, then the window's entries walked in order, wave-uniform, SEG_BATCH
+// gathered rows in flight at a time (lane = 16-byte chunk of the pooled part); each run's sum is stored where
+// the run ends. A run that starts in the window and runs past it is finished from the entries after it;
+// entries before the window's first head belong to the previous window's last run. Same sums as walk_run
+// (entries in CSR order, separate multiply and add), one wave per 64 entries instead of one per entry.
+template <typename T, int VEC>
+__device__ __forceinline__ void seg_window(const Feat &f, const Ents &e, int64_t s0) {
+    typedef Chunk<T, VEC> C;
+    const int lane = threadIdx.x & 63;
+    const int64_t i = s0 + lane;
+    const bool ok = i < e.n;
+    const int32_t d = ok ? e.dst[i] : -1;
+    const int32_t sr = ok ? e.src[i] : 0;
+    const int32_t wb = ok ? __float_as_int(e.val[i]) : 0;
+    const int32_t before = s0 > 0 ? e.dst[s0 - 1] : -1;
+    int32_t prev = __shfl_up(d, 1);
+    if (lane == 0) prev = before;
+    const uint64_t heads = __ballot(d >= 0 && d != prev);
+    if (!heads) return;
+    const uint64_t bnd = __ballot(d != prev);  // a run, or an empty stretch, starts here
+    const int first = __builtin_ctzll(heads);
+    for (uint32_t c = lane; c - lane < f.cpool; c += SHPL_WAVE) {
+        const bool act = c < f.cpool;
+        const T *sc = reinterpret_cast<const T *>(f.src) + f.src_off + (int64_t)c * VEC;
+        float acc[VEC];
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) acc[q] = 0.0f;
+        int32_t key = -1;
+        for (int j = first; j < SHPL_WAVE; j += SEG_BATCH) {
+            typename C::raw_t raw[SEG_BATCH];
+#pragma unroll
+            for (int u = 0; u < SEG_BATCH; ++u) {
+                const int jj = j + u < SHPL_WAVE ? j + u : SHPL_WAVE - 1;
+                const int32_t dd = __builtin_amdgcn_readlane(d, jj);
+                seg_load<T, VEC>(sc, f.src_stride, __builtin_amdgcn_readlane(sr, jj), act && j + u < SHPL_WAVE && dd >= 0,
+                                 raw[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < SEG_BATCH; ++u) {
+                const int jj = j + u;
+                if (jj < SHPL_WAVE) {
+                    const int32_t dd = __builtin_amdgcn_readlane(d, jj);
+                    if ((bnd >> jj) & 1) {
+                        if (key >= 0 && act) store_pooled<T, VEC>(f, key, c, acc);
+#pragma unroll
+                        for (int q = 0; q < VEC; ++q) acc[q] = 0.0f;
+                        key = dd;
+                    }
+                    if (dd >= 0) {
+                        float x[VEC];
+                        C::to_f32(raw[u], x);
+                        fma_free_accumulate<VEC>(acc, __int_as_float(__builtin_amdgcn_readlane(wb, jj)), x);
+                    }
+                }
+            }
+        }
+        if (key < 0) continue;
+        // the window's last run: on past the window while the destination stays
+        for (int64_t t = s0 + SHPL_WAVE;; t += SEG_BATCH) {
+            int32_t dd[SEG_BATCH], ss[SEG_BATCH];
+            float ww[SEG_BATCH];
+            bool in[SEG_BATCH];
+#pragma unroll
+            for (int u = 0; u < SEG_BATCH; ++u) {
+                const bool okk = t + u < e.n;
+                dd[u] = okk ? e.dst[t + u] : -1;
+                ss[u] = okk ? e.src[t + u] : 0;
+                ww[u] = okk ? e.val[t + u] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < SEG_BATCH; ++u) in[u] = dd[u] == key && (u == 0 || in[u - 1]);
+            typename C::raw_t raw[SEG_BATCH];
+#pragma unroll
+            for (int u = 0; u < SEG_BATCH; ++u) seg_load<T, VEC>(sc, f.src_stride, ss[u], act && in[u], raw[u]);
+#pragma unroll
+            for (int u = 0; u < SEG_BATCH; ++u) {
+                if (in[u]) {
+                    float x[VEC];
+                    C::to_f32(raw[u], x);
+                    fma_free_accumulate<VEC>(acc, ww[u], x);
+                }
+            }
+            if (!in[SEG_BATCH - 1]) break;
+        }
+        if (act) store_pooled<T, VEC>(f, key, c, acc);
+    }
+}
+
 template <typename T, int VEC, bool GROUP, bool POW2>
 __global__ __launch_bounds__(SHPL_BLOCK) void k_once(const Feat f, const Ents e, int cpool_shift,
                                                      const int32_t *key_range, int64_t n_rows, int64_t sblocks) {
     const int64_t zblocks = (int64_t)gridDim.x - sblocks;
     const int64_t zb = SHPL_ONCE_ZERO_FIRST ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - sblocks;
     if (zb < 0 || zb >= zblocks) {
-        sparse_body<T, VEC, GROUP, false, POW2, false>(f, e, cpool_shift,
-                                                       SHPL_ONCE_ZERO_FIRST ? zb - zblocks : (int64_t)blockIdx.x,
-                                                       sblocks);
+        int64_t sb = SHPL_ONCE_ZERO_FIRST ? zb - zblocks : (int64_t)blockIdx.x;
+#if SHPL_ONCE_XCD
+        // workgroups go to the 8 XCDs round-robin by id: sb % 8 picks the XCD, so each XCD walks a contiguous
+        // eighth of the entries in order and the image rows its neighbouring destinations share stay in its
+        // own L2 (the launcher makes sblocks a multiple of 8)
+        sb = (sb & 7) * (sblocks >> 3) + (sb >> 3);
+#endif
+        if (once_seg(GROUP, f.cpool)) {
+            const int64_t wpb = SHPL_BLOCK / SHPL_WAVE;
+            for (int64_t win = sb * wpb + (threadIdx.x >> 6); win * SHPL_WAVE < e.n; win += sblocks * wpb)
+                seg_window<T, VEC>(f, e, win * SHPL_WAVE);
+        } else {
+            sparse_body<T, VEC, GROUP, false, POW2, false>(f, e, cpool_shift, sb, sblocks);
+        }
         return;
     }
     typedef Chunk<T, VEC> C;
@@ -868,7 +992,10 @@ int sparse_tg(const Plan &pl, const Ents &e, int64_t nnz_cap, hipStream_t s) {
 template <typename T, int VEC, bool GROUP>
 int once_tg(const Plan &pl, const shpl_csr *csr, hipStream_t s) {
     Ents e{csr->nnz_cap, csr->ent_dst, csr->ent_src, csr->ent_col, csr->ent_val};
-    const int64_t sblocks = csr->nnz_cap > 0 ? grid_for(csr->nnz_cap * (int64_t)pl.f.cpool, SHPL_BLOCK, 1 << 20) : 0;
+    // the run-walking blocks: a thread per (entry, chunk), or (cell-keyed) a wave per 64 entries
+    const int64_t swork = once_seg(GROUP, pl.f.cpool) ? csr->nnz_cap : csr->nnz_cap * (int64_t)pl.f.cpool;
+    int64_t sblocks = csr->nnz_cap > 0 ? grid_for(swork, SHPL_BLOCK, 1 << 20) : 0;
+    if (SHPL_ONCE_XCD) sblocks = (sblocks + 7) & ~(int64_t)7;  // k_once's XCD-contiguous block order
     const int64_t zblocks = (pl.n_dst + ONCE_ROWS * (SHPL_BLOCK / SHPL_WAVE) - 1) / (ONCE_ROWS * (SHPL_BLOCK / SHPL_WAVE));
     if (sblocks + zblocks > 0x7fffffffLL) return SHPL_ERR_BAD_SHAPE;
     int shift = -1;

@@ -280,6 +280,12 @@ class FusedPipeline:
         L.check(fn(L.BY_CELL, L.dtype_code(self.bv_fused), self.csr.ref(), L.ptr(img), self.Ci, 0,
                    self.Ci, None, 0, 0, 0, L.OUT_POOL, out, self.Cb + self.Ci, L.stream_of(self.dev)), "shpl_pull")
 
+    # split: the pooled half after the copy instead of beside it -- each alone at its own rate rather than
+    # the two sharing HBM, and the step capturable in a graph (the chain only has to finish under the copy,
+    # no stream priority needed): 1.345 vs 1.36 (graph) / 1.385 ms (eager) overlapped at config 6
+    # (profiles/r05_c6segg_ab.log)
+    SPLIT_SERIAL = True
+
     def step_split(self, points, voxels, point_offsets, P, bev, img, side, chain, events=None):
         """split: the pass-through copy on `side`, the index chain and then the pooled half on `chain` (a
         high-priority stream, so its latency-bound workgroups are dispatched ahead of the copy's); neither
@@ -299,15 +305,22 @@ class FusedPipeline:
                 events[2].record(chain)
             self.build_index(points, voxels, point_offsets, P)
             self.build_csr(("cell",))
-            self._pooled_half(img)
-            if events:
-                events[3].record(chain)
+            if not self.SPLIT_SERIAL:
+                self._pooled_half(img)
+                if events:
+                    events[3].record(chain)
         with torch.cuda.stream(side):
             if events:
                 events[0].record(side)
             self._pass_copies(bev, img, ("cell",))
             if events:
                 events[1].record(side)
+        if self.SPLIT_SERIAL:
+            with torch.cuda.stream(chain):
+                chain.wait_stream(side)
+                self._pooled_half(img)
+                if events:
+                    events[3].record(chain)
         main.wait_stream(side)
         if chain is not main:
             main.wait_stream(chain)

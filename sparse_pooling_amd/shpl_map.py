@@ -175,10 +175,12 @@ def pull(smap, direction, order, src, src_stride, src_off, c_pool, out, out_stri
          pass_=None, pass_stride=0, pass_off=0, c_pass=0, mode=L.OUT_POOL, part=None):
     """shpl_pull through smap's CSR; part "dense" / "sparse": only shpl_pull_dense (the pass-through chunks and
     the pooled chunks' zeros, no index read) or shpl_pull_sparse (the pooled rows over them), which together
-    give shpl_pull's output bit for bit -- so the dense half can run early, on another stream."""
+    give shpl_pull's output bit for bit -- so the dense half can run early, on another stream. part "once":
+    shpl_pull_once (OUT_POOL over a CSR with key ranges: every row written once, the zeros included)."""
     c = smap.csr(direction, order)
     fn, name = {None: (L.lib().shpl_pull, "shpl_pull"), "dense": (L.lib().shpl_pull_dense, "shpl_pull_dense"),
-                "sparse": (L.lib().shpl_pull_sparse, "shpl_pull_sparse")}[part]
+                "sparse": (L.lib().shpl_pull_sparse, "shpl_pull_sparse"),
+                "once": (L.lib().shpl_pull_once, "shpl_pull_once")}[part]
     L.check(fn(direction, L.dtype_code(out), c.ref(), L.ptr(src), src_stride, src_off, c_pool, L.ptr(pass_),
                pass_stride, pass_off, c_pass, mode, L.ptr(out), out_stride, L.stream_of(out.device)), name)
     return out

@@ -425,6 +425,44 @@ def test_range_csr_one_long_run(n):
         np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
+@pytest.mark.parametrize("dtype,c", [("f32", 8), ("f32", 256), ("f32", 320), ("bf16", 256), ("bf16", 24)])
+def test_pull_once_runs_across_windows(dtype, c):
+    """shpl_pull_once's cell-keyed run walk (a wave per 64 sorted entries from 32 chunks of 16 bytes up; the
+    (entry, chunk) walk below): runs of 1-3 entries, runs that end on and cross the 64-entry window edges, runs
+    of 64, 70 and 150 entries (continued past their window, a window with no head at all), pooled widths of 2
+    to 80 chunks (a partial second chunk group at 320 f32 channels) -- every row written once, against the
+    oracle's sparse_pool_op (bitwise, or bf16 output rounding)."""
+    from sparse_pooling_amd import _lib as L
+    from sparse_pooling_amd import shpl_map as sm
+    rng = np.random.default_rng(11)
+    R, h, w = 700, 9, 11
+    lens = [1] * 63 + [2] + [150] + list(rng.integers(1, 4, 200)) + [64] + [1] * 5 + [70] + [3] * 30
+    cells = np.sort(rng.choice(R, len(lens), replace=False))
+    cell = np.repeat(cells, lens)
+    n = cell.size
+    mij = np.stack([cell, np.arange(n)], 1).astype(np.int64)
+    mval = rng.uniform(-1, 1, n).astype(np.float32)
+    idx = np.stack([np.zeros(n), rng.integers(0, h, n), rng.integers(0, w, n)], 1).astype(np.int64)
+    img = rng.standard_normal((1, h, w, c)).astype(np.float32)
+    dt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    if dtype == "bf16":
+        img = orc.from_bf16_bits(orc.to_bf16_bits(img))
+    ti = torch.from_numpy(img).to(DEV).to(dt)
+    sm.ShplMap.ROW_PULLS = True
+    try:
+        smap = sm.pack_map(torch.from_numpy(mij).to(DEV), torch.from_numpy(mval).to(DEV), np.array([R, n]),
+                           torch.from_numpy(idx).to(DEV), img.shape)
+        pool = torch.full((R, c), float("nan"), device=DEV, dtype=dt)
+        sm.pull(smap, L.BY_CELL, L.ORDER_ENTRY, ti, c, 0, c, pool, c, part="once")
+        torch.cuda.synchronize()
+    finally:
+        sm.ShplMap.ROW_PULLS = None
+    ref = orc.sparse_pool_op(mij, mval, [R, n], img, idx).reshape(R, c)
+    if dtype == "bf16":
+        ref = orc.from_bf16_bits(orc.to_bf16_bits(ref))
+    _close_and_exact(pool.float().cpu().numpy(), ref)
+
+
 def test_bf16_storage_fp32_accumulate():
     """Config 3 storage: bf16 in/out, f32 accumulation, rounded once (RNE)."""
     from sparse_pooling_amd import sparse_pool_utils as spu
@@ -535,6 +573,24 @@ def test_split_pipeline_matches_oracle(cfg, dtype, graph, once, own, monkeypatch
     on a stream of its own; else on the (high-priority) stream the step is called on (chain=None)."""
     from sparse_pooling_amd import pipeline
     monkeypatch.setattr(pipeline.FusedPipeline, "SPLIT_ONCE", once)
+    monkeypatch.setattr(pipeline.FusedPipeline, "SPLIT_SERIAL", False)
+    _split_run(cfg, dtype, graph, own)
+
+
+@pytest.mark.parametrize("cfg,dtype,graph,own", [(6, "f32", True, True), (6, "f32", False, False),
+                                                 (6, "bf16", True, False), (6, "bf16", False, True),
+                                                 (2, "f32", True, False)])
+def test_split_serial_matches_oracle(cfg, dtype, graph, own):
+    """The split layer's default form (SPLIT_SERIAL: the pooled half -- shpl_pull_once, its wave per 64
+    entries at 256 channels -- after the side stream's copy instead of beside it), eager and graph-replayed,
+    bitwise the oracle's bv_fused on 3 frames (one with no point)."""
+    from sparse_pooling_amd import pipeline
+    assert pipeline.FusedPipeline.SPLIT_SERIAL
+    _split_run(cfg, dtype, graph, own)
+
+
+def _split_run(cfg, dtype, graph, own):
+    from sparse_pooling_amd import pipeline
     spec = synth.CONFIGS[cfg]
     frames = [synth.make_frame(spec, seed=60 + f, n_outside=25) for f in range(2)]
     frames.insert(1, synth.make_frame(synth.FrameSpec(0, spec.im_size, spec.bv_size, spec.stride, spec.c_bev,
