@@ -241,6 +241,7 @@ class _FusionConvFn(torch.autograd.Function):
             batch_norm_train(raw, stats, B * H * W, eps=conv.eps, beta=beta, relu=conv.relu,
                              moving_mean=conv.moving_mean, moving_var=conv.moving_var, decay=conv.decay, out=y,
                              ws=bn_ws)
+            conv._scale_key = None  # the moving statistics were updated through their device pointers
             mean, scale = bn_ws[:conv.c_out], bn_ws[conv.c_out:]
         ctx.conv, ctx.smap, ctx.pooled, ctx.train_bn = conv, smap, pooled, train_bn
         ctx.shapes = (Ca, Cb)
@@ -376,9 +377,14 @@ class FusionConv:
     def _inference_epilogue(self):
         if not self.batch_norm:
             return None, None, self.bias
-        # FusedBatchNorm inference: (x - moving_mean) * rsqrt(moving_var + eps) + beta
-        scale = 1.0 / torch.sqrt(self.moving_var + self.eps)
-        return self.moving_mean, scale, self.beta
+        # FusedBatchNorm inference: (x - moving_mean) * rsqrt(moving_var + eps) + beta. The scale is kept until
+        # moving_var changes (its tensor version, bumped by every in-place update, e.g. a training step's), so
+        # an inference step launches no elementwise kernels for it (4 small launches, ~20 us per step)
+        key = (self.moving_var.data_ptr(), self.moving_var._version, self.eps)
+        if getattr(self, "_scale_key", None) != key:
+            self._scale = 1.0 / torch.sqrt(self.moving_var + self.eps)
+            self._scale_key = key
+        return self.moving_mean, self._scale, self.beta
 
     def _ws_for(self, key, nbytes):
         t = self._ws.get(key)
@@ -401,6 +407,7 @@ class FusionConv:
                            shift=shift, relu=self.relu, out=out, ws=ws)
         stats = torch.empty((2, self.c_out), dtype=torch.float64, device=a.device)
         y = conv3x3(a, self.weights, b=b, pool=pool, frame_off=frame_off, relu=False, stats=stats, out=out, ws=ws)
+        self._scale_key = None  # batch_norm_train updates the moving statistics through their device pointers
         return batch_norm_train(y, stats, B * H * W, eps=self.eps, beta=self.beta, relu=self.relu,
                                 moving_mean=self.moving_mean, moving_var=self.moving_var, decay=self.decay)
 

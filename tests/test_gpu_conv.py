@@ -322,6 +322,7 @@ def test_batch_norm_training_vs_oracle():
     mm0 = rng.standard_normal(Cout).astype(np.float32)
     mv0 = rng.uniform(0.5, 2, Cout).astype(np.float32)
     conv.beta, conv.moving_mean, conv.moving_var = _t(beta), _t(mm0), _t(mv0)
+    conv(_t(x), is_training=False)  # an inference step first: its cached BN scale must not outlive the update
     y = conv(_t(x), is_training=True)
     _, raw = orc.conv3x3(x, w, raw=True)
     ey, bm, bv, emm, emv = orc.batch_norm_train(raw, 1e-3, None, beta, True, mm0, mv0, 0.999)
