@@ -388,6 +388,13 @@ constexpr int ONCE_ROWS = SHPL_ONCE_ROWS;
 #define SHPL_SEG_BATCH 8
 #endif
 constexpr int SEG_BATCH = SHPL_SEG_BATCH;
+#ifndef SHPL_SEG_CONT
+#define SHPL_SEG_CONT 2
+#endif
+// entries per step past the window (a run crossing it: rare, short); 2 keeps k_once at 84 VGPRs without spills
+// under its 5-waves bound (8: 136 VGPRs, 3 waves per SIMD, 0.578 vs 0.513-0.520 ms at config 6;
+// profiles/r05_c6c2_ab.log)
+constexpr int SEG_CONT = SHPL_SEG_CONT;
 // the window walk for cell-keyed rows of at least half a wave of chunks (RetinaNet's 256 channels: 64 f32 /
 // 32 bf16 chunks); narrower rows would leave most lanes idle through the window's serial walk (measured as
 // shpl_pull_sparse's form at config 2's 32 channels: 205 vs 80 us)
@@ -461,38 +468,45 @@ __device__ __forceinline__ void seg_window(const Feat &f, const Ents &e, int64_t
         }
         if (key < 0) continue;
         // the window's last run: on past the window while the destination stays
-        for (int64_t t = s0 + SHPL_WAVE;; t += SEG_BATCH) {
-            int32_t dd[SEG_BATCH], ss[SEG_BATCH];
-            float ww[SEG_BATCH];
-            bool in[SEG_BATCH];
+        for (int64_t t = s0 + SHPL_WAVE;; t += SEG_CONT) {
+            int32_t dd[SEG_CONT], ss[SEG_CONT];
+            float ww[SEG_CONT];
+            bool in[SEG_CONT];
 #pragma unroll
-            for (int u = 0; u < SEG_BATCH; ++u) {
+            for (int u = 0; u < SEG_CONT; ++u) {
                 const bool okk = t + u < e.n;
                 dd[u] = okk ? e.dst[t + u] : -1;
                 ss[u] = okk ? e.src[t + u] : 0;
                 ww[u] = okk ? e.val[t + u] : 0.0f;
             }
 #pragma unroll
-            for (int u = 0; u < SEG_BATCH; ++u) in[u] = dd[u] == key && (u == 0 || in[u - 1]);
-            typename C::raw_t raw[SEG_BATCH];
+            for (int u = 0; u < SEG_CONT; ++u) in[u] = dd[u] == key && (u == 0 || in[u - 1]);
+            typename C::raw_t raw[SEG_CONT];
 #pragma unroll
-            for (int u = 0; u < SEG_BATCH; ++u) seg_load<T, VEC>(sc, f.src_stride, ss[u], act && in[u], raw[u]);
+            for (int u = 0; u < SEG_CONT; ++u) seg_load<T, VEC>(sc, f.src_stride, ss[u], act && in[u], raw[u]);
 #pragma unroll
-            for (int u = 0; u < SEG_BATCH; ++u) {
+            for (int u = 0; u < SEG_CONT; ++u) {
                 if (in[u]) {
                     float x[VEC];
                     C::to_f32(raw[u], x);
                     fma_free_accumulate<VEC>(acc, ww[u], x);
                 }
             }
-            if (!in[SEG_BATCH - 1]) break;
+            if (!in[SEG_CONT - 1]) break;
         }
         if (act) store_pooled<T, VEC>(f, key, c, acc);
     }
 }
 
+#ifndef SHPL_ONCE_WPE
+#define SHPL_ONCE_WPE 5  // k_once at 5 waves per SIMD: the zero rows' write-only stream and the window walks
+#endif
 template <typename T, int VEC, bool GROUP, bool POW2>
-__global__ __launch_bounds__(SHPL_BLOCK) void k_once(const Feat f, const Ents e, int cpool_shift,
+__global__ __launch_bounds__(SHPL_BLOCK)
+#if SHPL_ONCE_WPE
+__attribute__((amdgpu_waves_per_eu(SHPL_ONCE_WPE, SHPL_ONCE_WPE)))
+#endif
+void k_once(const Feat f, const Ents e, int cpool_shift,
                                                      const int32_t *key_range, int64_t n_rows, int64_t sblocks) {
     const int64_t zblocks = (int64_t)gridDim.x - sblocks;
     const int64_t zb = SHPL_ONCE_ZERO_FIRST ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - sblocks;
