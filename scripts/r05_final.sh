@@ -12,10 +12,12 @@ if [ -z "$SKIP_TABLES" ]; then  # SKIP_TABLES=1: the committed tables stand (the
   done
   cp profiles/frame_checksums.json gpurun_out/frame_checksums.json
 fi
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r05_gpu_tests.log 2>&1
-rc=$?; echo "tests rc=$rc"; tail -1 gpurun_out/r05_gpu_tests.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/r05_gpu_tests.log | head; exit $rc; }
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('__SMOKE_OK__')" > gpurun_out/r05_smoke.log 2>&1 || exit 1
-tail -1 gpurun_out/r05_smoke.log
+if [ -z "$BENCH_ONLY" ]; then  # BENCH_ONLY=1: the bench lines alone (e.g. again once traffic.json is re-stamped)
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r05_gpu_tests.log 2>&1
+  rc=$?; echo "tests rc=$rc"; tail -1 gpurun_out/r05_gpu_tests.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/r05_gpu_tests.log | head; exit $rc; }
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('__SMOKE_OK__')" > gpurun_out/r05_smoke.log 2>&1 || exit 1
+  tail -1 gpurun_out/r05_smoke.log
+fi
 run() {  # name, args...
   local n=$1; shift
   timeout -k 10 400 python bench.py "$@" > gpurun_out/r05_bench_$n.log 2>&1 || { tail -5 gpurun_out/r05_bench_$n.log; exit 1; }
