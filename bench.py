@@ -115,9 +115,10 @@ def parse():
                          "index build instead of as extra workgroups of the index launches")
     ap.add_argument("--graph-steps", type=int, default=None,
                     help="layer workloads: consecutive steps captured in one HIP graph (the timed loop replays it "
-                         "steps / graph-steps times; --steps must divide). Default: 4 at config 3 when --steps "
-                         "divides (0.107 -> 0.103 ms per step: the replay boundary's ~8 us once per 4 steps), "
-                         "else 1 (config 2: no change, profiles/r03_graph_steps_ab.log)")
+                         "steps / graph-steps times; --steps must divide). Default at config 3: 8 when --steps divides, "
+                         "else 4 when it divides (0.107 -> 0.103 ms per step with 4: the replay boundary's ~8 us "
+                         "once per 4 steps; 8: -1 %, profiles/r05_c3gs_ab.log), else 1; elsewhere 1 (config 2: "
+                         "no change, profiles/r03_graph_steps_ab.log)")
     ap.add_argument("--no-pool-report", action="store_true",
                     help="config 2: skip the separate pool_fwd measurement (PMC passes count the step's launches only)")
     ap.add_argument("--graph", action="store_true",
@@ -445,7 +446,9 @@ def main():
 
     cfg = args.config
     if args.graph_steps is None:
-        args.graph_steps = 4 if cfg == 3 and args.steps % 4 == 0 else 1
+        # config 3 (~70 us steps): several steps per replay, so the graph launch is amortised (8: 0.0694-0.0701 vs
+        # 4: 0.0704-0.0707 ms per step, profiles/r05_c3gs_ab.log)
+        args.graph_steps = (8 if args.steps % 8 == 0 else 4 if args.steps % 4 == 0 else 1) if cfg == 3 else 1
     spec = synth.CONFIGS[cfg]
     dual = cfg in (3, 5)
     backward = cfg == 3
