@@ -118,7 +118,7 @@ def parse():
                          "steps / graph-steps times; --steps must divide). Default at config 3: 8 when --steps divides, "
                          "else 4 when it divides (0.107 -> 0.103 ms per step with 4: the replay boundary's ~8 us "
                          "once per 4 steps; 8: -1 %, profiles/r05_c3gs_ab.log), else 1; elsewhere 1 (config 2: "
-                         "no change, profiles/r03_graph_steps_ab.log)")
+                         "no change, profiles/r03_graph_steps_ab.log; configs 2 and 6 with 4: within 0.2 %, r05_c6gs_ab.log)")
     ap.add_argument("--no-pool-report", action="store_true",
                     help="config 2: skip the separate pool_fwd measurement (PMC passes count the step's launches only)")
     ap.add_argument("--graph", action="store_true",
