@@ -100,10 +100,6 @@ def parse():
     ap.add_argument("--split-form", default="serial", choices=["serial", "overlap"],
                     help="split layer: the pooled half after the pass-through copy, the step captured in a graph "
                          "(serial), or beside the copy, eager with the chain at high priority (overlap; A/B)")
-    ap.add_argument("--sparse-tail", type=int, default=None,
-                    help="img->BEV layers: the streaming pass in two launches, the sparse pass of the first frames "
-                         "beside the last B // N frames' stream (FusedPipeline.SPARSE_TAIL, default 0 = one streaming launch; "
-                         "A/B)")
     ap.add_argument("--head-k", type=int, default=None,
                     help="bucketed pipelines: run heads per destination in the CSRs (FusedPipeline.HEAD_K; 0 = none; "
                          "A/B)")
@@ -463,8 +459,6 @@ def main():
     pipeline.FusedPipeline.SPLIT_SERIAL = args.split_form == "serial"
     if args.head_k is not None:
         pipeline.FusedPipeline.HEAD_K = args.head_k
-    if args.sparse_tail is not None:
-        pipeline.FusedPipeline.SPARSE_TAIL = args.sparse_tail
     esz0 = 2 if dtype == torch.bfloat16 else 4
     split = (not dual and not args.rows and not args.no_overlap and
              (args.split == "on" or (args.split == "auto" and min(spec.c_bev, spec.c_img) * esz0 >= 1024)))
@@ -585,8 +579,6 @@ def main():
     comm = sd.comm_report(dev)
     nbytes = step_bytes(cfg, spec, nnz, u_pix, u_cell, F, esz)
     interleaved = dual and not args.no_overlap and not pl.rows and pl.interleave
-    # img->BEV with the sparse tail: the head frames' sparse pass runs beside the tail's stream
-    interleaved = interleaved or (not args.no_overlap and not split and pl._sparse_tail() > 0)
     dense_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args_steps_ev
     sparse_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args_steps_ev
     bwd_ms = sum(e[4].elapsed_time(e[5]) for e in evs) / args_steps_ev if backward else 0.0
@@ -661,9 +653,7 @@ def main():
                 "bound": "hbm",
                 "kernel": ("SHPL layer pulls: k_dense (concat stream) + k_sparse (pooled gather); achieved over "
                            + (("the layer's window (first k_dense start to last k_sparse end: the cell-keyed "
-                               "gathers run beside img_fused's stream)") if interleaved and dual else
-                              ("the layer's window (first k_dense start to last k_sparse end: the head frames' "
-                               "k_sparse runs beside the last frames' k_dense)") if interleaved else
+                               "gathers run beside img_fused's stream)") if interleaved else
                               "their summed durations")
                            + (("; split step (the pass-through copy k_dense beside the index chain, then the "
                                "pooled half written once by shpl_pull_once's k_once): every kernel of the step, "

@@ -351,10 +351,6 @@ class FusedPipeline:
             return
         main = torch.cuda.current_stream(self.dev)
         side.wait_stream(main)            # inputs / previous step done
-        tail = self._sparse_tail()
-        if tail:
-            self._overlapped_tail(points, voxels, point_offsets, P, bev, img, side, mval, events, tail)
-            return
         split = self.dual and side2 is not None
         # dual layers: the cell-keyed sparse pass needs only bv_fused's stream, so it runs
         # beside img_fused's stream (the gathers overlap the second dense pass)
@@ -386,75 +382,6 @@ class FusedPipeline:
         if split:
             main.wait_stream(side2)
         main.wait_stream(side)
-        if events:
-            events[3].record(main)
-
-    # img->BEV layers of several frames (not row-keyed, not split): the streaming pass in two launches, the
-    # frames before the last SPARSE_TAIL share and the rest, so that the sparse pass of the first frames runs
-    # beside the streaming pass of the last ones and only the tail's sparse pass follows the stream (0: one
-    # streaming launch, the sparse pass after it)
-    SPARSE_TAIL = 0  # the tail holds B // SPARSE_TAIL frames (at least one); off: profiles/r05_c2tail_ab.log
-
-    def _sparse_tail(self):
-        if self.dual or self.rows or self.split or self.SPARSE_TAIL <= 0 or self.B < 2:
-            return 0
-        return min(max(1, self.B // self.SPARSE_TAIL), self.B - 1)
-
-    def _frames_csr(self, f0, f1):
-        """A copy of the cell CSR's struct for frames [f0, f1): its live-entry walk over those frames only
-        (frame_off / frame_nnz from f0, n_frames = f1 - f0); the rows stay global, so the sparse pass writes
-        the right rows of bv_fused."""
-        c = L.ShplCsr()
-        ctypes.pointer(c)[0] = self.csr.struct
-        c.frame_off = self.frame_off.data_ptr() + 8 * f0
-        c.frame_nnz = self.frame_nnz.data_ptr() + 8 * f0
-        c.n_frames = f1 - f0
-        return c
-
-    def _dense_frames(self, bev, img, f0, f1):
-        """The streaming pass (pass-through copy + pooled zeros) of frames [f0, f1)."""
-        cells = self.Hb * self.Wb
-        c = L.ShplCsr()
-        ctypes.pointer(c)[0] = self.csr.struct
-        c.n_keys = (f1 - f0) * cells
-        esz = self.bv_fused.element_size()
-        L.check(self._lib.shpl_pull_dense(L.BY_CELL, L.dtype_code(self.bv_fused), ctypes.byref(c),
-                                          ctypes.c_void_p(img.data_ptr()), self.Ci, 0, self.Ci,
-                                          ctypes.c_void_p(bev.data_ptr() + f0 * cells * self.Cb * esz), self.Cb, 0,
-                                          self.Cb, L.OUT_CONCAT,
-                                          ctypes.c_void_p(self.bv_fused.data_ptr() +
-                                                          f0 * cells * (self.Cb + self.Ci) * esz),
-                                          self.Cb + self.Ci, L.stream_of(self.dev)), "shpl_pull_dense")
-
-    def _sparse_frames(self, bev, img, f0, f1):
-        """The sparse pass (pooled rows over the zeros) of frames [f0, f1)."""
-        c = self._frames_csr(f0, f1)
-        self._tail_structs.append(c)
-        args = self._concat_args(self.csr, L.BY_CELL, img, self.Ci, bev, self.Cb, self.bv_fused)
-        L.check(self._lib.shpl_pull_sparse(*args[:2], ctypes.byref(c), *args[3:], L.stream_of(self.dev)),
-                "shpl_pull_sparse")
-
-    def _overlapped_tail(self, points, voxels, point_offsets, P, bev, img, side, mval, events, tail):
-        main = torch.cuda.current_stream(self.dev)
-        B = self.B
-        head_done = torch.cuda.Event()
-        self._tail_structs = []
-        with torch.cuda.stream(side):
-            if events:
-                events[0].record(side)
-            self._dense_frames(bev, img, 0, B - tail)
-            head_done.record(side)
-            self._dense_frames(bev, img, B - tail, B)
-            if events:
-                events[1].record(side)
-        self.build_index(points, voxels, point_offsets, P, mval)
-        self.build_csr(("cell",))
-        main.wait_event(head_done)        # the head frames' rows streamed: their pooled rows go over them
-        if events:
-            events[2].record(main)
-        self._sparse_frames(bev, img, 0, B - tail)
-        main.wait_stream(side)
-        self._sparse_frames(bev, img, B - tail, B)
         if events:
             events[3].record(main)
 

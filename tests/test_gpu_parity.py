@@ -507,61 +507,6 @@ def test_pipeline_batch_matches_oracle(cfg, dual):
             _close_and_exact(iout[f:f + 1], ei)
 
 
-@pytest.mark.parametrize("dtype,tail,graph", [("f32", 8, False), ("f32", 2, True), ("bf16", 2, False),
-                                              ("f32", 0, True)])
-def test_overlapped_sparse_tail_matches_oracle(dtype, tail, graph, monkeypatch):
-    """step_overlapped of an img->BEV layer with FusedPipeline.SPARSE_TAIL: the streaming pass in two launches
-    (the head frames, then the last B // SPARSE_TAIL), the head frames' sparse pass (a live-entry walk over
-    their frames only) beside the tail's stream, then the tail's -- eager and replayed from a captured graph,
-    on 4 frames with an empty one in the head and one in the tail: bitwise the oracle's bv_fused (0: one
-    streaming launch, the sparse pass after it)."""
-    from sparse_pooling_amd import pipeline
-    monkeypatch.setattr(pipeline.FusedPipeline, "SPARSE_TAIL", tail)
-    spec = synth.CONFIGS[2]
-    empty = lambda: synth.make_frame(synth.FrameSpec(0, spec.im_size, spec.bv_size, spec.stride, spec.c_bev,  # noqa
-                                                     spec.c_img), seed=1)
-    frames = [synth.make_frame(spec, seed=70, n_outside=25), empty(),
-              synth.make_frame(spec, seed=71, n_outside=25), empty()]
-    pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
-    dt = torch.bfloat16 if dtype == "bf16" else torch.float32
-    pl = pipeline.FusedPipeline(4, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev, spec.c_img,
-                                dtype=dt)
-    assert pl._sparse_tail() == (0 if tail == 0 else max(1, 4 // tail))
-    Hb, Wb = spec.bev_feat_hw
-    Hi, Wi = spec.img_feat_hw
-    bev = synth.make_features((4, Hb, Wb, spec.c_bev), 5)
-    img = synth.make_features((4, Hi, Wi, spec.c_img), 6)
-    if dt == torch.bfloat16:
-        bev, img = (orc.from_bf16_bits(orc.to_bf16_bits(a)) for a in (bev, img))
-    tb, ti = torch.from_numpy(bev).to(DEV).to(dt), torch.from_numpy(img).to(DEV).to(dt)
-    side = torch.cuda.Stream(device=DEV)
-    pl.bv_fused.fill_(float("nan"))
-    torch.cuda.synchronize()
-    if graph:
-        pl.step_overlapped(pts, vox, off, P, tb, ti, side)  # warm (the graph replays the same step)
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        gs = torch.cuda.Stream(device=DEV)
-        gs.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.graph(g, stream=gs):
-            pl.step_overlapped(pts, vox, off, P, tb, ti, side)
-        pl.bv_fused.fill_(float("nan"))
-        g.replay()
-        g.replay()
-    else:
-        pl.step_overlapped(pts, vox, off, P, tb, ti, side)
-    torch.cuda.synchronize()
-    assert int(pl.err.item()) == 0
-    out = pl.bv_fused.float().cpu().numpy()
-    for f, fr in enumerate(frames):
-        ref = _oracle_frame(fr, spec.stride)
-        eb, _ = orc.sparse_pool_layer(bev[f:f + 1], img[f:f + 1], ref["Mij_pool"], ref["M_val"], ref["M_size"],
-                                      ref["img_index_flip_pool"])
-        if dt == torch.bfloat16:
-            eb = orc.from_bf16_bits(orc.to_bf16_bits(eb))
-        _close_and_exact(out[f:f + 1], eb)
-
-
 @pytest.mark.parametrize("cfg,dtype,graph,once,own", [(6, "f32", False, True, True), (6, "f32", True, True, True),
                                                       (6, "bf16", False, True, True), (2, "f32", False, True, True),
                                                       (6, "f32", False, False, True), (2, "bf16", True, False, True),
