@@ -573,6 +573,9 @@ def main():
         tinfo = {}
         elapsed = sd.timed(lambda k: step(evs[k]), args.steps, device=dev, info=tinfo)
     args_steps_ev = n_ev
+    # every error bit the steps set, the timed ones included (FusedPipeline.check: one read, outside the timed
+    # region): SHPL_EBIT_BARRIER or an input error ends the run here instead of reporting invalid results
+    pl.check()
     outs = [pl.bv_fused] + ([pl.img_fused] if dual else []) + ([d_bev, d_img] if backward else [])
     checks = checksum_report(f"layer_config{cfg}", sd.combine_checksums([sd.frame_checksums(t) for t in outs]), fids,
                              dev, rank, args)

@@ -428,10 +428,13 @@ int shpl_pull_once(int direction, int dtype, const shpl_csr *csr, const void *d_
  * Limits (SHPL_ERR_BAD_SHAPE otherwise): at most 65536 cells and 65536 pixels
  * per frame, max_points_per_frame below 2^24.
  * Frames of at most 32 chunks of 1024 points run both passes in ONE launch
- * (k_index1: a frame barrier between them inside the launch); its barrier
- * words live at the start of d_bkt, which must be ZEROED once before its first
- * use -- every call leaves them zero. SHPL_EBIT_BARRIER in *d_err: a barrier
- * gave up (the call's results are invalid).
+ * (k_index1: a frame barrier between them inside the launch) when every chunk
+ * workgroup of the batch fits on the GPU at once (else the two-launch form);
+ * its barrier words live at the start of d_bkt, which must be ZEROED before
+ * its first use (shpl_bucket_workspace_reset, or a memset of the whole
+ * workspace) -- every call leaves them zero. SHPL_EBIT_BARRIER in *d_err: a
+ * barrier gave up, or found its words not zeroed; the call's results are
+ * invalid, and after a dirty start the words need shpl_bucket_workspace_reset.
  * Replaces what shpl_build_index + two shpl_build_csr calls feed the pulls
  * (kitti_dataset.py:374-379, then rpn_model.py:330-331's SparseTensor). */
 /* Optional riders of shpl_build_index_buckets: the concat's pass-through half
@@ -452,6 +455,9 @@ typedef struct {
 
 int shpl_bucket_workspace_bytes(int n_frames, int64_t max_points_per_frame, int64_t nnz_cap,
                                 int64_t cells_per_frame, int64_t pix_per_frame, size_t *bytes);
+/* Zero the frame barrier words of a bucket workspace sized for n_frames (stream-ordered): before its first
+ * shpl_build_index_buckets, and after a call that reported SHPL_EBIT_BARRIER. */
+int shpl_bucket_workspace_reset(int n_frames, void *d_bkt, size_t bkt_bytes, void *stream);
 int shpl_build_index_buckets(int n_frames, const int64_t *d_point_offsets, const int64_t *d_point_counts,
                              int64_t max_points_per_frame, const void *d_points, int points_dtype,
                              const void *d_voxels, int voxels_itype, int64_t vox_stride, const double *d_P,

@@ -151,6 +151,7 @@ def _declare(lib):
         "shpl_build_csr_path": (i32, [i32, i32, i32, i32, p, p, i64, p, p, p, p, ctypes.POINTER(ShplCsr), p,
                                       sz, p]),
         "shpl_bucket_workspace_bytes": (i32, [i32, i64, i64, i64, i64, psz]),
+        "shpl_bucket_workspace_reset": (i32, [i32, p, sz, p]),
         "shpl_build_index_buckets": (i32, [i32, p, p, i64, p, i32, p, i32, i64, p, d, d, d, d, d, d, p,
                                            p, p, p, p, p, p, p, sz, i64, p, sz, ctypes.POINTER(ShplPassCopy),
                                            ctypes.POINTER(ShplPassCopy), p]),
@@ -253,3 +254,17 @@ def bucket_ws_bytes(n_frames, max_points, nnz_cap, cells_per_frame, pix_per_fram
     check(lib().shpl_bucket_workspace_bytes(int(n_frames), int(max_points), int(nnz_cap), int(cells_per_frame),
                                             int(pix_per_frame), ctypes.byref(out)), "shpl_bucket_workspace_bytes")
     return out.value
+
+
+def bucket_workspace(n_frames, max_points, nnz_cap, cells_per_frame, pix_per_frame, device):
+    """A bucket workspace for shpl_build_index_buckets, ZEROED: its frame barrier words must start at zero
+    (include/shpl.h; every call leaves them so, and shpl_bucket_workspace_reset restores them after a
+    SHPL_EBIT_BARRIER)."""
+    nb = bucket_ws_bytes(n_frames, max_points, nnz_cap, cells_per_frame, pix_per_frame)
+    return torch.zeros(max(int(nb), 256), dtype=torch.uint8, device=device)
+
+
+def bucket_workspace_reset(n_frames, ws, device=None):
+    """shpl_bucket_workspace_reset on the current stream."""
+    check(lib().shpl_bucket_workspace_reset(int(n_frames), ptr(ws), ws.numel(), stream_of(device)),
+          "shpl_bucket_workspace_reset")

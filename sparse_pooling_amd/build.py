@@ -43,7 +43,27 @@ def build(verbose=False, out=OUT, defines=()):
                        check=True)
     if verbose:
         print("built", out)
+    if out == OUT and not defines:
+        build_fault(objs, verbose)
     return out
+
+
+# Test-only library: libshpl.so with shpl_index.hip built with SHPL_IDX1_FAULT=1 (chunk 0 of frame 0 skips its
+# frame-barrier arrival, so k_index1's give-up path runs; tests/test_gpu_parity.py loads it by path). Never the
+# product library: _lib.LIB_PATH is libshpl.so.
+FAULT_OUT = os.path.join(HERE, "libshpl_fault.so")
+
+
+def build_fault(objs, verbose=False):
+    obj_dir = os.path.join(OBJ, "fault")
+    os.makedirs(obj_dir, exist_ok=True)
+    fault = _compile(os.path.join(CSRC, "shpl_index.hip"), obj_dir, ["-DSHPL_IDX1_FAULT=1"])
+    objs = [fault if os.path.basename(o) == "shpl_index.o" else o for o in objs]
+    if not os.path.exists(FAULT_OUT) or os.path.getmtime(FAULT_OUT) < max(os.path.getmtime(o) for o in objs):
+        subprocess.run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", FAULT_OUT], check=True)
+    if verbose:
+        print("built", FAULT_OUT)
+    return FAULT_OUT
 
 
 if __name__ == "__main__":

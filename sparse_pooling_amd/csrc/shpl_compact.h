@@ -323,8 +323,9 @@ __device__ __forceinline__ void compact_phase(const Stage &st, const Frames &fr,
     __shared__ int32_t wsum[IDX_BATCH][IDX_BLOCK / 64];
     __shared__ int32_t pre[2][IDX_BLOCK / 64], all[2][IDX_BLOCK / 64], naux[IDX_BLOCK / 64];
     __shared__ int32_t s_off[BKT ? 2 * BK_MAX_RANGES : 1], s_scan[IDX_BLOCK / 64];
-    // per-wave range counts, then their prefixes over the waves (at most IDX_BLOCK: 16 bits, so that k_index1's
-    // two phases fit two 1024-thread workgroups per CU)
+    // per-wave range counts, then their prefixes over the waves (at most IDX_BLOCK: 16 bits). LDS of the
+    // bucketed form, with s_peer's 64 KiB: ~113 KiB per 1024-thread workgroup, one workgroup per CU (two would
+    // also need <= 64 VGPRs: amdgpu_waves_per_eu(8) measured 41 vs 17 us for k_index1)
     __shared__ int16_t s_w[BKT ? 2 : 1][IDX_BLOCK / 64][BKT ? BK_MAX_RANGES : 1];
     __shared__ int32_t s_tb[BKT ? 4 * BK_MAX_RANGES : 1];  // per (key, range): entries in the frame, in earlier chunks
     __shared__ uint64_t s_peer[BKT ? IDX_BLOCK / 64 : 1][BKT ? BK_MAX_RANGES : 1];  // per wave and range: lane bits
@@ -499,19 +500,32 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_compact(Stage st, Frames fr, Bkt 
 // bounded: SHPL_EBIT_BARRIER on give-up), and every load of the aggregates is an sc1 load (no acquire fence). The chunk's points stay
 // in registers between the passes (no second load). Each chunk then adds to the frame's departure word, and
 // the last to depart zeroes both words for the next call (the words start at zero: the caller's workspace is
-// zeroed once; every call leaves them zero, a timed-out one included). Residency: the barrier waits only for
-// the frame's own chunks, all dispatched before any rider of the launch; the host takes this form only for
-// frames of at most IDX1_MAX_CHUNKS chunks, so a frame's chunks never fill an XCD's workgroup slots.
+// zeroed once; every call leaves them zero, a timed-out one included).
+// Dirty words (a workspace never zeroed): the arrivals the chunks of a frame see are n_chunks consecutive
+// values from the word's start value, so unless it started at zero some chunk sees one outside [0, n_chunks)
+// -- that chunk raises SHPL_EBIT_BARRIER (so does one whose departure count is outside that range): the call
+// reports the bad state instead of handing out half-aggregated buckets (shpl_bucket_workspace_reset clears it).
+// Residency, independent of the order in which workgroups are dispatched: the host takes this form only when
+// the launch's chunk workgroups all fit on the GPU at once (the kernel's occupancy x the CUs) and frames have
+// at most IDX1_MAX_CHUNKS chunks. A chunk waits only for its own frame's chunks; riders never wait, so while
+// a chunk of the launch is undispatched at most (chunks - 1) slots are held by waiting chunks and one is free
+// for it. (A GPU shared with other processes can still starve a frame: then the give-up below.)
 constexpr int IDX1_MAX_CHUNKS = 32;
 constexpr uint64_t IDX1_SPIN_TICKS = 2000000;  // 20 ms of s_memrealtime (100 MHz): the barrier's give-up
+#ifndef SHPL_IDX1_FAULT
+#define SHPL_IDX1_FAULT 0  // test builds only (libshpl_fault.so): chunk 0 of frame 0 never arrives -> the give-up
+#endif
 
-__device__ __forceinline__ void frame_barrier(const Frames &fr, const Bkt &bk, int f) {
+__device__ __forceinline__ void frame_barrier(const Frames &fr, const Bkt &bk, int f, int j) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through aggregate stores done
     __syncthreads();
     if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(bk.bar + f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool skip = SHPL_IDX1_FAULT && f == 0 && j == 0;
+        const int32_t a = skip ? 0 : __hip_atomic_fetch_add(bk.bar + f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool dirty = a < 0 || a >= fr.n_chunks;  // the word did not start the call at zero
+        if (dirty && fr.err) atomicOr(fr.err, SHPL_EBIT_BARRIER);
         const uint64_t t0 = wall_clock64();
-        while (__hip_atomic_load(bk.bar + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < fr.n_chunks) {
+        while (!dirty && __hip_atomic_load(bk.bar + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < fr.n_chunks) {
             if (wall_clock64() - t0 > IDX1_SPIN_TICKS) {
                 if (fr.err) atomicOr(fr.err, SHPL_EBIT_BARRIER);
                 break;
@@ -552,7 +566,7 @@ void k_index1(Stage st, Frames fr, Bkt bk) {
     typename Stage::Payload pl[IDX_BATCH];
     count_phase<Stage, true>(sf, fr, bk, f, j, in, m, pl);
     SHPL_IDX1_STAMP(1);
-    frame_barrier(fr, bk, f);
+    frame_barrier(fr, bk, f, j);
     SHPL_IDX1_STAMP(2);
     compact_phase<Stage, true>(sf, fr, bk, f, j, in, true, m, pl);
     lds_barrier();  // every wave is past its reads of the frame's aggregates
@@ -560,11 +574,26 @@ void k_index1(Stage st, Frames fr, Bkt bk) {
     if (threadIdx.x == 0) {
         const int32_t d = __hip_atomic_fetch_add(bk.bar + fr.n_frames + f, 1, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
+        if ((d < 0 || d >= fr.n_chunks) && fr.err) atomicOr(fr.err, SHPL_EBIT_BARRIER);  // dirty departure word
         if (d == fr.n_chunks - 1) {  // the last to leave: every chunk of the frame is past its poll
             __hip_atomic_store(bk.bar + f, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(bk.bar + fr.n_frames + f, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+}
+
+// k_index1 workgroups the current device holds at once: the kernel's occupancy (its LDS and registers: one per
+// CU) x the CUs. 0 when the runtime cannot say (the two-launch form then runs).
+template <typename Stage>
+int64_t index1_resident() {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_index1<Stage>, IDX_BLOCK, 0) != hipSuccess) {
+        (void)hipGetLastError();  // not the caller's launch error
+        return 0;
+    }
+    return (int64_t)cus * per_cu;
 }
 
 int n_chunks_for(int64_t max_points) {
@@ -594,7 +623,8 @@ int run_compaction(const Stage &st, int n_frames, int64_t max_points, const int6
 #ifndef SHPL_IDX1_RIDERS
 #define SHPL_IDX1_RIDERS 240
 #endif
-            if (SHPL_INDEX1 && bk->bar && fr.n_chunks <= IDX1_MAX_CHUNKS) {
+            if (SHPL_INDEX1 && bk->bar && fr.n_chunks <= IDX1_MAX_CHUNKS &&
+                (int64_t)n_frames * fr.n_chunks <= index1_resident<Stage>()) {
                 // rider workgroups per copy and frame: SHPL_IDX1_RIDERS per copy over the batch, at most one per
                 // 64 KiB of a frame's copy (the two-launch form's cp_blocks bound)
                 int per = SHPL_IDX1_RIDERS / n_frames;

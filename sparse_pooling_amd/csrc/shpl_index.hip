@@ -356,6 +356,15 @@ extern "C" int shpl_bucket_workspace_bytes(int n_frames, int64_t max_points_per_
     return SHPL_OK;
 }
 
+extern "C" int shpl_bucket_workspace_reset(int n_frames, void *d_bkt, size_t bkt_bytes, void *stream) {
+    if (n_frames < 1 || !d_bkt) return SHPL_ERR_ARG;
+    const BkLayout l = bk_layout(n_frames, 1, 0, 0, 0);  // the barrier words' place depends on n_frames alone
+    const size_t bytes = 4 * 2 * (size_t)n_frames;
+    if (bkt_bytes < l.bar + bytes) return SHPL_ERR_WORKSPACE;
+    return hipMemsetAsync((char *)d_bkt + l.bar, 0, bytes, (hipStream_t)stream) == hipSuccess ? SHPL_OK
+                                                                                             : SHPL_ERR_HIP;
+}
+
 extern "C" int shpl_build_index_buckets(int n_frames, const int64_t *d_point_offsets, const int64_t *d_point_counts,
                                         int64_t max_points_per_frame, const void *d_points, int points_dtype,
                                         const void *d_voxels, int voxels_itype, int64_t vox_stride, const double *d_P,

@@ -224,17 +224,6 @@ def gather_floats(values, device=None):
     return [[float(x) for x in o.cpu().tolist()] for o in out]
 
 
-def gather_checksums(value, device=None):
-    """All ranks' scalar checksums, rank order."""
-    on = dist.is_available() and dist.is_initialized()
-    t = torch.tensor([float(value)], dtype=torch.float64, device=_coll_device(device))
-    if not on:
-        return [float(value)]
-    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
-    dist.all_gather(out, t)
-    return [float(x.item()) for x in out]
-
-
 def gather_frame_checksums(local, device=None):
     """All-gather the ranks' per-frame checksums (int64 [F_rank], every rank
     the same F_rank) into one list in rank order -- global frame order for

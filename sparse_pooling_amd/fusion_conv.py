@@ -228,6 +228,8 @@ class _FusionConvFn(torch.autograd.Function):
         raw, mean, scale = None, None, None
         if not train_bn:
             center, scale, shift = conv._inference_epilogue()
+            if scale is not None:  # saved for the backward: a copy, not the buffer a training step rewrites
+                scale = scale.clone()
             mean = center
             if not conv.batch_norm:
                 shift = bias
@@ -241,7 +243,7 @@ class _FusionConvFn(torch.autograd.Function):
             batch_norm_train(raw, stats, B * H * W, eps=conv.eps, beta=beta, relu=conv.relu,
                              moving_mean=conv.moving_mean, moving_var=conv.moving_var, decay=conv.decay, out=y,
                              ws=bn_ws)
-            conv._scale_key = None  # the moving statistics were updated through their device pointers
+            conv._refresh_scale()  # the moving statistics were updated through their device pointers
             mean, scale = bn_ws[:conv.c_out], bn_ws[conv.c_out:]
         ctx.conv, ctx.smap, ctx.pooled, ctx.train_bn = conv, smap, pooled, train_bn
         ctx.shapes = (Ca, Cb)
@@ -373,18 +375,27 @@ class FusionConv:
         self.moving_var = torch.ones(c_out, **f32) if batch_norm else None
         self.bias = torch.zeros(c_out, **f32) if (bias and not batch_norm) else None
         self._ws = {}
+        self._scale = torch.empty(c_out, **f32) if batch_norm else None
+        if batch_norm:
+            self._refresh_scale()
 
     def _inference_epilogue(self):
         if not self.batch_norm:
             return None, None, self.bias
-        # FusedBatchNorm inference: (x - moving_mean) * rsqrt(moving_var + eps) + beta. The scale is kept until
-        # moving_var changes (its tensor version, bumped by every in-place update, e.g. a training step's), so
-        # an inference step launches no elementwise kernels for it (4 small launches, ~20 us per step)
-        key = (self.moving_var.data_ptr(), self.moving_var._version, self.eps)
-        if getattr(self, "_scale_key", None) != key:
-            self._scale = 1.0 / torch.sqrt(self.moving_var + self.eps)
-            self._scale_key = key
+        # FusedBatchNorm inference: (x - moving_mean) * rsqrt(moving_var + eps) + beta. The scale lives in one
+        # tensor, rewritten ON THE DEVICE right after every batch_norm_train (which updates moving_var through
+        # its device pointer, bumping no tensor version), so a training step replayed from a captured graph
+        # refreshes it too, and an inference graph reads the current one; an eager in-place update of moving_var
+        # (its version) refreshes it here. An inference step launches nothing for it.
+        if self._scale_key != (self.moving_var.data_ptr(), self.moving_var._version, self.eps):
+            self._refresh_scale()
         return self.moving_mean, self._scale, self.beta
+
+    def _refresh_scale(self):
+        """self._scale = 1 / sqrt(moving_var + eps), in place (three launches, stream-ordered, capturable)."""
+        torch.add(self.moving_var, self.eps, out=self._scale)
+        self._scale.sqrt_().reciprocal_()
+        self._scale_key = (self.moving_var.data_ptr(), self.moving_var._version, self.eps)
 
     def _ws_for(self, key, nbytes):
         t = self._ws.get(key)
@@ -407,9 +418,10 @@ class FusionConv:
                            shift=shift, relu=self.relu, out=out, ws=ws)
         stats = torch.empty((2, self.c_out), dtype=torch.float64, device=a.device)
         y = conv3x3(a, self.weights, b=b, pool=pool, frame_off=frame_off, relu=False, stats=stats, out=out, ws=ws)
-        self._scale_key = None  # batch_norm_train updates the moving statistics through their device pointers
-        return batch_norm_train(y, stats, B * H * W, eps=self.eps, beta=self.beta, relu=self.relu,
-                                moving_mean=self.moving_mean, moving_var=self.moving_var, decay=self.decay)
+        y = batch_norm_train(y, stats, B * H * W, eps=self.eps, beta=self.beta, relu=self.relu,
+                             moving_mean=self.moving_mean, moving_var=self.moving_var, decay=self.decay)
+        self._refresh_scale()  # batch_norm_train updated the moving statistics through their device pointers
+        return y
 
     def _grad_wanted(self, *tensors):
         return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in

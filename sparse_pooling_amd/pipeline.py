@@ -19,7 +19,7 @@ import numpy as np
 import torch
 
 from . import _lib as L
-from .shpl_map import ShplMap
+from .shpl_map import ShplMap, raise_for_bits
 
 
 class FusedPipeline:
@@ -104,9 +104,9 @@ class FusedPipeline:
                     c.live_frames(self.frame_off, self.frame_nnz)
         self._lib = L.lib()
         if self.buckets:
-            nb = L.bucket_ws_bytes(self.B, self.max_points, self.N, self.Hb * self.Wb, self.Hi * self.Wi)
             # zeroed once: its frame barrier words start at zero (every call leaves them so)
-            self.bkt_ws = torch.zeros(max(int(nb), 256), dtype=torch.uint8, device=dev)
+            self.bkt_ws = L.bucket_workspace(self.B, self.max_points, self.N, self.Hb * self.Wb, self.Hi * self.Wi,
+                                             dev)
             self.bkt = L.ShplBuckets(self.B, self.max_points, self.N, self.Hb * self.Wb, self.Hi * self.Wi,
                                      self.frame_off.data_ptr(), self.frame_nnz.data_ptr(), self.cell.data_ptr(),
                                      self.pix.data_ptr(), self.val.data_ptr(), self.bkt_ws.data_ptr(),
@@ -416,6 +416,20 @@ class FusedPipeline:
             self._sparse(pix)
         if side2 is not None:
             main.wait_stream(side2)
+
+    def check(self):
+        """Raise if a step since the last check set a bit of the device error word (one device->host read:
+        call it outside timed or captured regions). The steps never read it themselves. SHPL_EBIT_BARRIER (the
+        one-launch index build gave up at a frame barrier, or found its words not zeroed) raises RuntimeError
+        after the word and the barrier words are reset, so the next step can run; an input bit raises
+        ShplMap.check's InvalidArgumentError."""
+        bits = int(self.err.item()) & 0xFFFFFFFF
+        if not bits:
+            return
+        self.err.zero_()
+        if bits & L.EBIT_BARRIER and self.buckets:
+            L.bucket_workspace_reset(self.B, self.bkt_ws, self.dev)
+        raise_for_bits(bits)
 
     def map(self):
         """The current M as a ShplMap (for tests)."""

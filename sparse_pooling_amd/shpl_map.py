@@ -29,6 +29,27 @@ def _i32(n, device):
 _SIDE = {}  # device -> the side stream of ShplMap.prefetch_csr
 
 
+def raise_for_bits(bits):
+    """The exception a device error word's bits (SHPL_EBIT_*) stand for, raised; nothing for 0."""
+    if not bits:
+        return
+    what = []
+    if bits & L.EBIT_ROW:
+        what.append("M row index outside [0, M_size[0])")
+    if bits & L.EBIT_COL:
+        what.append("M column index outside [0, M_size[1])")
+    if bits & L.EBIT_PIXEL:
+        what.append("source index (b, v, u) outside the feature map")
+    if bits & L.EBIT_VALUES:
+        what.append("number of M values does not match number of indices")
+    if bits & L.EBIT_CAPACITY:
+        what.append("a frame holds more points than max_points_per_frame")
+    if bits & L.EBIT_BARRIER:  # not an input error: the one-launch index build could not proceed
+        raise RuntimeError("shpl_build_index_buckets: a frame barrier gave up (chunks not resident) or "
+                           "found its words not zeroed; the step's results are invalid")
+    raise InvalidArgumentError("; ".join(what))
+
+
 class ShplMap:
     """M on the device. Entries are grouped by frame: frame f owns entry slots
     [frame_off[f], frame_off[f+1]) of which the first frame_nnz[f] are live
@@ -58,22 +79,7 @@ class ShplMap:
     def check(self):
         """Raise like TF-CPU's InvalidArgumentError if any index was invalid
         (one device->host read of the error word)."""
-        bits = self.error_bits()
-        if bits:
-            what = []
-            if bits & L.EBIT_ROW:
-                what.append("M row index outside [0, M_size[0])")
-            if bits & L.EBIT_COL:
-                what.append("M column index outside [0, M_size[1])")
-            if bits & L.EBIT_PIXEL:
-                what.append("source index (b, v, u) outside the feature map")
-            if bits & L.EBIT_VALUES:
-                what.append("number of M values does not match number of indices")
-            if bits & L.EBIT_CAPACITY:
-                what.append("a frame holds more points than max_points_per_frame")
-            if bits & L.EBIT_BARRIER:  # not an input error: the one-launch index build could not proceed
-                raise RuntimeError("shpl_build_index_buckets: a frame barrier timed out (chunks not resident)")
-            raise InvalidArgumentError("; ".join(what))
+        raise_for_bits(self.error_bits())
 
     # ------------------------------------------------------------------ CSR
     # Row-keyed pulls (shpl_csr.key_range: one launch per pull) for maps of fewer

@@ -336,6 +336,44 @@ def test_batch_norm_training_vs_oracle():
     _assert_within(yi, orc.conv3x3(x, w, emm, k, beta, True), _bound(x, w, k))
 
 
+def test_inference_scale_follows_graph_replayed_training():
+    """The inference epilogue's scale 1/sqrt(moving_var + eps) follows moving_var when the training steps run
+    from a captured HIP graph (no Python per step; batch_norm_train updates moving_var through its device
+    pointer): after three replays of a captured training step, an eager inference call AND an inference graph
+    captured before those replays both equal the conv with the scale recomputed from the current moving_var,
+    bitwise."""
+    from sparse_pooling_amd import fusion_conv as fc
+    B, H, W, Cin, Cout = 1, 12, 20, 16, 32
+    conv = fc.FusionConv(Cin, Cout, device=DEV, seed=5)
+    conv.beta = _t(np.random.default_rng(4).standard_normal(Cout).astype(np.float32))
+    x = _t(synth.make_features((B, H, W, Cin), 11) + 0.5)
+    y_inf = torch.empty((B, H, W, Cout), device=DEV)
+    conv(x, is_training=False, out=y_inf)  # the scale of the initial moving_var (all ones)
+    gs = torch.cuda.Stream()
+    gs.wait_stream(torch.cuda.current_stream())
+    g_inf = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g_inf, stream=gs):
+        conv(x, is_training=False, out=y_inf)
+    y_tr = torch.empty_like(y_inf)
+    conv(x, is_training=True, out=y_tr)  # warm-up: workspaces allocated before the capture
+    torch.cuda.synchronize()
+    g_tr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g_tr, stream=gs):
+        conv(x, is_training=True, out=y_tr)
+    mv_before = conv.moving_var.clone()
+    for _ in range(3):
+        g_tr.replay()
+    torch.cuda.synchronize()
+    assert not torch.equal(conv.moving_var, mv_before)  # the replays did move the statistics
+    want = fc.conv3x3(x, conv.weights, center=conv.moving_mean, scale=1.0 / torch.sqrt(conv.moving_var + conv.eps),
+                      shift=conv.beta, relu=True)
+    assert torch.equal(conv(x, is_training=False), want)
+    y_inf.fill_(float("nan"))
+    g_inf.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(y_inf, want)
+
+
 def test_bf16_conv_and_fused():
     """bf16 storage: bf16 MFMA products are exact, f32 accumulation, one
     rounding at the store (|err| <= one bf16 ulp of the f32 result + TOL).

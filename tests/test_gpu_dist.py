@@ -79,3 +79,22 @@ def test_weak_partition_is_the_global_batch_of_frames_times_ranks():
                   "--no-cpu-baseline"], {"SHPL_DIST_BACKEND": "gloo"})
     assert two["scaling"] == "weak" and two["config"]["global_batch"] == 4
     assert one["frame_checksums"]["digest"] == two["frame_checksums"]["digest"]
+
+
+def test_config4_eight_ranks_on_one_device_matches_stored_n1_table():
+    """Config 4 at its real rank count: `bench.py --gpus 8` (self-launched, 8 ranks, gloo control plane on one
+    device) strong-partitions the 64-frame batch, 8 frames per rank; every gathered frame equals the oracle-written
+    64-frame N=1 table by its global frame id, the 8 ranks are distinct, and the roofline lists all 8 ranks."""
+    eight = _bench(["--gpus", "8", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--partition", "strong"],
+                   {"SHPL_DIST_BACKEND": "gloo"}, timeout=420)
+    assert eight["n_gpus"] == 8 and eight["config"]["global_batch"] == 64
+    assert eight["config"]["frames_per_gpu_per_step"] == 8
+    c = eight["frame_checksums"]
+    assert c["frames"] == 64 and c["frame_ids"] == [0, 63] and c["compared_with"] == "layer_config2_frames64"
+    assert c["match_n1"] is True, c
+    assert eight["comm"]["world_size"] == 8
+    assert sorted(r["rank"] for r in eight["comm"]["ranks"]) == list(range(8))
+    per = eight["roofline"]["per_rank"]
+    assert len(per) == 8 and [r["rank"] for r in per] == list(range(8))
+    assert eight["roofline"]["kernel_ms"] == max(r["kernel_ms"] for r in per)
+    assert eight["index_errors"] == 0

@@ -696,6 +696,64 @@ def test_pipeline_backward_matches_oracle(cfg, dtype, mode, rows):
         same(d_bev[f:f + 1], e_bev)
 
 
+def test_index1_barrier_give_up_and_dirty_words():
+    """k_index1's frame barrier (the one-launch bucketed index build at config 3's shape) fails loudly,
+    never silently: (1) a bucket workspace whose barrier words were never zeroed (0xFF) -> FusedPipeline.check()
+    raises RuntimeError and resets them, and the next step is bitwise the oracle's; (2) the fault-injection
+    build (libshpl_fault.so: SHPL_IDX1_FAULT, chunk 0 of frame 0 never arrives) -> every chunk of frame 0 gives
+    up after 20 ms, check() raises RuntimeError, and the call still leaves the words zero."""
+    import ctypes
+
+    from sparse_pooling_amd import _lib as L
+    from sparse_pooling_amd import build as B_
+    from sparse_pooling_amd import pipeline
+    assert os.path.exists(B_.FAULT_OUT), "build the test library: python -m sparse_pooling_amd.build"
+    spec = synth.CONFIGS[3]
+    B = 4
+    frames = [synth.make_frame(spec, seed=90 + f, n_outside=10) for f in range(B)]
+    pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
+    pl = pipeline.FusedPipeline(B, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev, spec.c_img,
+                                dtype=torch.bfloat16, dual=True)
+    assert pl.buckets
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    tb = torch.randn((B, Hb, Wb, spec.c_bev), device=DEV).to(torch.bfloat16)
+    ti = torch.randn((B, Hi, Wi, spec.c_img), device=DEV).to(torch.bfloat16)
+
+    def clean_step_matches_oracle():
+        pl.step(pts, vox, off, P, tb, ti)
+        pl.check()  # no bit set
+        assert not pl.bkt_ws[:8 * B].view(torch.int32).any()
+        bev, img = tb[:1].float().cpu().numpy(), ti[:1].float().cpu().numpy()
+        ref = _oracle_frame(frames[0], spec.stride)
+        eb, ei = orc.sparse_pool_layer(bev, img, ref["Mij_pool"], ref["M_val"], ref["M_size"],
+                                       ref["img_index_flip_pool"], dual=True)
+        for got, want in ((pl.bv_fused[:1], eb), (pl.img_fused[:1], ei)):
+            np.testing.assert_array_equal(_np(got.view(torch.int16)).view(np.uint16),
+                                          orc.to_bf16_bits(want.astype(np.float32)))
+
+    # (1) dirty barrier words
+    pl.bkt_ws.fill_(0xFF)
+    pl.step(pts, vox, off, P, tb, ti)
+    with pytest.raises(RuntimeError, match="frame barrier"):
+        pl.check()
+    assert int(pl.err.item()) == 0 and not pl.bkt_ws[:8 * B].view(torch.int32).any()  # check() reset both
+    clean_step_matches_oracle()
+    # (2) the give-up, forced
+    fault = ctypes.CDLL(B_.FAULT_OUT)
+    L._declare(fault)
+    pl._lib = fault
+    try:
+        pl.step(pts, vox, off, P, tb, ti)
+        torch.cuda.synchronize()
+        assert not pl.bkt_ws[:8 * B].view(torch.int32).any()  # the timed-out call left them zero too
+        with pytest.raises(RuntimeError, match="frame barrier"):
+            pl.check()
+    finally:
+        pl._lib = L.lib()
+    clean_step_matches_oracle()
+
+
 # ---------------------------------------------------------------- BEV voxelizer
 
 def _ragged_frames(base, sizes, seed):
