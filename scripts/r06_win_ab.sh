@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 V=${V:-sparse_pooling_amd/variants/libshpl_win.so}
 N=sparse_pooling_amd/libshpl.so
 SHPL_LIB=$V timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
-  tests/test_gpu_parity.py -k "test_pipeline_backward_matches_oracle or test_bucket_pulls_ragged_batch or barrier" \
+  tests/test_gpu_parity.py -k "test_pipeline_backward_matches_oracle or test_bucket_pulls_ragged_batch or barrier or test_window_pulls" \
   tests/test_gpu_checksums_oracle.py > gpurun_out/r06_win_tests.log 2>&1
 rc=$?; tail -2 gpurun_out/r06_win_tests.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r06_win_tests.log | head -20; exit $rc; }
 bash scripts/ab_kernels.sh r06_win "--config 3 --steps 200" "k_index1|k_bsort2|k_rows2|k_win2" rows2=$N win=$V rows2b=$N winb=$V

@@ -325,7 +325,7 @@ __device__ __forceinline__ void compact_phase(const Stage &st, const Frames &fr,
     __shared__ int32_t s_off[BKT ? 2 * BK_MAX_RANGES : 1], s_scan[IDX_BLOCK / 64];
     // per-wave range counts, then their prefixes over the waves (at most IDX_BLOCK: 16 bits). LDS of the
     // bucketed form, with s_peer's 64 KiB: ~113 KiB per 1024-thread workgroup, one workgroup per CU (two would
-    // also need <= 64 VGPRs: amdgpu_waves_per_eu(8) measured 41 vs 17 us for k_index1)
+    // also need <= 64 VGPRs: amdgpu_waves_per_eu(8) measured 41 vs 17 us for k_index1, docs/HISTORY.md §4)
     __shared__ int16_t s_w[BKT ? 2 : 1][IDX_BLOCK / 64][BKT ? BK_MAX_RANGES : 1];
     __shared__ int32_t s_tb[BKT ? 4 * BK_MAX_RANGES : 1];  // per (key, range): entries in the frame, in earlier chunks
     __shared__ uint64_t s_peer[BKT ? IDX_BLOCK / 64 : 1][BKT ? BK_MAX_RANGES : 1];  // per wave and range: lane bits

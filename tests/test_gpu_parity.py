@@ -754,6 +754,17 @@ def test_index1_barrier_give_up_and_dirty_words():
     clean_step_matches_oracle()
 
 
+@pytest.mark.parametrize("dtype,cb,ci,sizes", [("bf16", 256, 256, [1500, 1500, 700]), ("f32", 128, 128, [1500, 900]),
+                                               ("bf16", 256, 256, [0, 3000, 1, 5]), ("bf16", 256, 128, [2500, 2500])])
+def test_window_pulls_short_stretches(dtype, cb, ci, sizes):
+    """The bucketed step's pull pairs at config 3's row width (32 chunks of 16 bytes: bf16 256 / f32 128
+    channels, the entry-window form k_win2 when the library has it) on batches so small that every workgroup
+    owns one or two 32-entry windows: pixel runs of up to ~50 entries cross several workgroups' stretches (the
+    run's owner fetches past its stretch; the others skip it), frames without entries, and (256 / 128) one side
+    of another row width (k_rows2 then) -- bitwise against the oracle, forward and gradients."""
+    _ragged_pipeline_run(3, sizes, dtype, ["buckets"], channels=(cb, ci))
+
+
 # ---------------------------------------------------------------- BEV voxelizer
 
 def _ragged_frames(base, sizes, seed):
