@@ -869,543 +869,6 @@ void k_rows2(const RowsSide s0, const RowsSide s1) {
 #endif
 }
 
-// ---------------------------------------------------------------- k_win2
-// Both row-keyed pulls of a pair as windows of WIN_E sorted entries (config 3's shape: rows of 32 chunks of 16
-// bytes, no per-column partials, both pulls SHPL_OUT_POOL or both SHPL_OUT_ADD) -- the gather decoupled from
-// the index walk. Each 256-thread workgroup owns a contiguous stretch of windows of one pull (the pixel-keyed
-// pull's workgroups first) and the same share of its destination rows:
-//   wave 0, the loader, issues LDS-DMAs only: window j's index words (destination, source, value) three
-//   windows ahead, and its 32 gathered source rows (16 KiB; DMA k: entries k and k + 16) two windows ahead into a
-//   ring of WIN_NS slots; a counted vmcnt and one block barrier per window (its queue holds no stores, so the
-//   count is exact and nothing waits on a store's round trip);
-//   waves 1-3, the consumers, first write the empty rows of their row share (zeros, or pass + 0 in ADD mode),
-//   then per window take its runs (boundaries by one ballot) six at a time, a run per 32 lanes (lane = chunk),
-//   and sum each run's rows from LDS in entry order with separate multiply and add -- k_rows' arithmetic,
-//   bitwise -- storing the row where the run ends. A run that crosses a window boundary carries its partial
-//   sums to the next window through LDS; one that crosses the stretch's end is finished by this workgroup
-//   from the next stretch's entries (the loader keeps fetching while that run lasts); one that started in the
-//   previous stretch is left to that workgroup. ADD mode: each consumer loads the pass rows of its next
-//   window's runs one window ahead.
-// Entries with destination -1 (capacity holes) and entries another workgroup sums gather a zero piece.
-#ifndef SHPL_PAIR_WIN
-#define SHPL_PAIR_WIN 0
-#endif
-#ifndef SHPL_WIN_XCD
-#define SHPL_WIN_XCD 1  // each XCD a contiguous run of workgroups: its L2 sees few frames' source rows
-#endif
-constexpr int WIN_E = 32;                       // entries per window
-constexpr int WIN_NC = 32;                      // 16-byte chunks per row (the only row width of this form)
-constexpr int WIN_SLOT = WIN_E * WIN_NC * 16;   // 16 KiB of gathered rows per window
-constexpr int WIN_NS = 4;                       // gather slots (window j in slot j % 4)
-constexpr int WIN_NI = 8;                       // index slots (window j in slot j & 7; j = -1 -> 7)
-constexpr int WIN_GD = WIN_E / 2;               // gather DMAs per window
-constexpr int WIN_ID = 3;                       // index DMAs per window
-constexpr int WIN_CW = SHPL_BLOCK / SHPL_WAVE - 1;  // consumer waves
-constexpr int WIN_SL = 2 * WIN_CW;              // consumer slots (32 lanes each)
-constexpr int WIN_PF = (WIN_E + WIN_SL - 1) / WIN_SL;  // runs per slot and window at most
-static_assert((WIN_NI & (WIN_NI - 1)) == 0, "index slots: a power of two");
-
-#define SHPL_NEG8 -1, -1, -1, -1, -1, -1, -1, -1
-__device__ int32_t g_win_neg1[64] = {SHPL_NEG8, SHPL_NEG8, SHPL_NEG8, SHPL_NEG8,
-                                     SHPL_NEG8, SHPL_NEG8, SHPL_NEG8, SHPL_NEG8};
-#undef SHPL_NEG8
-__device__ u32x4 g_win_zero;
-
-struct WinSide {
-    Feat f;
-    const int32_t *dst, *src;
-    const float *val;
-    const int32_t *key_range;
-    int64_t nnz, n_rows, nwin, wpb, blocks, rpb;  // entries, rows, windows, windows / rows per workgroup
-};
-
-// One LDS-DMA per lane (16 or 4 bytes), hidden from the compiler in inline asm (seeing an LDS write by DMA it
-// would drain every outstanding DMA before the next LDS read); M0 = the wave's destination, lane k's piece at
-// M0 + k * size. The kernel orders them itself (counted vmcnt + barriers).
-__device__ __forceinline__ void win_dma16(const void *src, void *dst) {
-    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"((uint32_t)(uintptr_t)dst)
-                 : "memory");
-}
-// A block barrier for LDS data only (an inline-asm s_barrier: __syncthreads() would drain vmcnt, the DMAs
-// in flight and the consumers' stores with it)
-__device__ __forceinline__ void win_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-__device__ __forceinline__ void win_dma4(const void *src, void *dst) {
-    asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "{m0}"((uint32_t)(uintptr_t)dst)
-                 : "memory");
-}
-
-template <typename T, int VEC, int MODE>
-__global__ __launch_bounds__(SHPL_BLOCK, 2) void k_win2(const WinSide s0, const WinSide s1) {
-    typedef Chunk<T, VEC> C;
-    static_assert(sizeof(T) * VEC == 16, "16-byte chunks");
-    __shared__ __attribute__((aligned(1024))) uint8_t s_rows[WIN_NS][WIN_SLOT];
-    __shared__ __attribute__((aligned(256))) int32_t s_dst[WIN_NI][64];
-    __shared__ __attribute__((aligned(256))) int32_t s_src[WIN_NI][64];
-    __shared__ __attribute__((aligned(256))) float s_val[WIN_NI][64];
-    __shared__ float s_carry[2][WIN_NC][VEC];
-    __shared__ int32_t s_seg[WIN_CW][2][WIN_E + 1];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t nblk = (int64_t)s0.blocks + s1.blocks;
-    const int64_t lb = SHPL_WIN_XCD ? xcd_block(blockIdx.x, nblk) : (int64_t)blockIdx.x;
-    const bool pix = lb < s1.blocks;  // the pixel-keyed pull's workgroups first (its long runs)
-    const WinSide &sd = pix ? s1 : s0;
-    const int64_t b = pix ? lb : lb - s1.blocks;
-    const int64_t w0 = b * sd.wpb, w1 = (w0 + sd.wpb < sd.nwin) ? w0 + sd.wpb : sd.nwin;
-    if (w0 >= w1) return;  // (uniform) no window: the host sizes the grid so that this never happens
-    const Feat &f = sd.f;
-    const T *srcb = reinterpret_cast<const T *>(f.src) + f.src_off;
-    const T *pass = reinterpret_cast<const T *>(f.pass) + f.pass_off;
-    T *out = reinterpret_cast<T *>(f.out);
-    auto go_on = [&](int64_t i, int32_t Kprev, int32_t K) {  // is window i + 1 this workgroup's? (all waves)
-        const int64_t n = i + 1;
-        if (n < w1) return true;
-        return n < sd.nwin && K >= 0 && K != Kprev && s_dst[i & (WIN_NI - 1)][WIN_E - 1] == K &&
-               s_dst[n & (WIN_NI - 1)][0] == K;
-    };
-
-    if (wave == 0) {
-        // ------------------------------------------------------------ loader
-        auto idx_dma = [&](int64_t j) {
-            const int64_t e = j * WIN_E + lane;
-            const bool ok = j >= 0 && j < sd.nwin && lane < WIN_E && e < sd.nnz;
-            const int s = (int)(j & (WIN_NI - 1));
-            win_dma4(ok ? (const void *)(sd.dst + e) : (const void *)(g_win_neg1 + lane), &s_dst[s][0]);
-            win_dma4(ok ? (const void *)(sd.src + e) : (const void *)(g_win_neg1 + lane), &s_src[s][0]);
-            win_dma4(ok ? (const void *)(sd.val + e) : (const void *)(g_win_neg1 + lane), &s_val[s][0]);
-        };
-        int32_t Kprev = -2, K = -2;  // read from LDS once landed (-2: not yet)
-        auto gather_dma = [&](int64_t j) {
-            const int s = (int)(j & (WIN_NI - 1));
-            bool cont = false;
-            if (j >= w1 && j < sd.nwin) {
-                if (K == -2) K = s_dst[(w1 - 1) & (WIN_NI - 1)][WIN_E - 1];
-                cont = K >= 0 && K != Kprev && s_dst[(j - 1) & (WIN_NI - 1)][WIN_E - 1] == K && s_dst[s][0] == K;
-            }
-            uint8_t *slot = s_rows[j & (WIN_NS - 1)];
-            const uint32_t c = lane & 31;
-            // every address first (the LDS reads in flight together), then the DMAs: an LDS read after an
-            // inline-asm DMA (its memory clobber) could not be hoisted, one LDS round trip per DMA
-            // DMA k carries entry k (lanes 0-31) and entry k + 16 (lanes 32-63): a lane's 16 entries are
-            // contiguous, read as four 16-byte words of each array
-            const int h = lane >> 5;
-            int32_t dv[WIN_GD], sv[WIN_GD];
-#pragma unroll
-            for (int q = 0; q < WIN_GD / 4; ++q) {
-                const int4 a = *reinterpret_cast<const int4 *>(&s_dst[s][16 * h + 4 * q]);
-                const int4 b2 = *reinterpret_cast<const int4 *>(&s_src[s][16 * h + 4 * q]);
-                dv[4 * q] = a.x, dv[4 * q + 1] = a.y, dv[4 * q + 2] = a.z, dv[4 * q + 3] = a.w;
-                sv[4 * q] = b2.x, sv[4 * q + 1] = b2.y, sv[4 * q + 2] = b2.z, sv[4 * q + 3] = b2.w;
-            }
-            const void *srcp[WIN_GD];
-#pragma unroll
-            for (int k = 0; k < WIN_GD; ++k) {
-                const int32_t d = dv[k], sr = sv[k];
-                bool live = j < sd.nwin && d >= 0;
-                live = live && d != Kprev;                   // the previous stretch's run (it may span windows)
-                if (j >= w1) live = live && cont && d == K;  // only the run this stretch finishes
-                srcp[k] = live ? (const void *)(srcb + (int64_t)sr * f.src_stride + (int64_t)c * VEC)
-                               : (const void *)&g_win_zero;
-            }
-#pragma unroll
-            for (int k = 0; k < WIN_GD; ++k) win_dma16(srcp[k], slot + k * 1024);
-        };
-        idx_dma(w0 - 1);
-        idx_dma(w0);
-        idx_dma(w0 + 1);
-        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // I(w0 - 1), I(w0) landed
-        Kprev = s_dst[(w0 - 1) & (WIN_NI - 1)][WIN_E - 1];
-        gather_dma(w0);
-        idx_dma(w0 + 2);
-        asm volatile("s_waitcnt vmcnt(19)" ::: "memory");  // I(w0 + 1) landed (G(w0), I(w0 + 2) may not)
-        gather_dma(w0 + 1);
-        int32_t Kc = -2;
-        for (int64_t i = w0;; ++i) {
-            idx_dma(i + 3);
-            asm volatile("s_waitcnt vmcnt(19)" ::: "memory");  // I(i + 2): younger G(i + 1), I(i + 3)
-            gather_dma(i + 2);
-            asm volatile("s_waitcnt vmcnt(38)" ::: "memory");  // G(i): younger I(i+2), G(i+1), I(i+3), G(i+2)
-            win_barrier();                                     // window i landed, visible to the consumers
-            if (i + 1 >= w1 && Kc == -2) Kc = s_dst[(w1 - 1) & (WIN_NI - 1)][WIN_E - 1];
-            if (!go_on(i, Kprev, Kc)) break;
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMAs issued past the last window
-        return;
-    }
-
-    // ---------------------------------------------------------------- consumers
-    const int cw = wave - 1, slot = 2 * cw + (lane >> 5);
-    const uint32_t c = lane & 31;
-    // 1. the empty rows of this workgroup's row share, 64 rows per step (a wave's key ranges in one load)
-    {
-        const int64_t r0 = b * sd.rpb, r1 = (r0 + sd.rpb < sd.n_rows) ? r0 + sd.rpb : sd.n_rows;
-        for (int64_t g = r0 + (int64_t)cw * 64; g < r1; g += (int64_t)WIN_CW * 64) {
-            bool empty = false;
-            if (g + lane < r1) {
-                const int2 kr = *reinterpret_cast<const int2 *>(sd.key_range + 2 * (g + lane));
-                empty = kr.x == kr.y;
-            }
-            const uint64_t em = __ballot(empty);
-            if (!em) continue;
-            if (MODE == SHPL_OUT_ADD) {
-                for (int q0 = 0; q0 < 32; q0 += 8) {  // 8 pass rows in flight (unconditional loads, row g for
-                    typename C::raw_t v[8];           // a non-empty one: no branch around a load)
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        const int r = 2 * (q0 + u) + (lane >> 5);
-                        const int64_t row = ((em >> r) & 1) ? g + r : g;
-                        v[u] = C::load(pass + (row * f.pass_stride + (int64_t)c * VEC));
-                    }
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        const int r = 2 * (q0 + u) + (lane >> 5);
-                        if (!((em >> r) & 1)) continue;
-                        float a[VEC];
-                        C::to_f32(v[u], a);
-#pragma unroll
-                        for (int j = 0; j < VEC; ++j) a[j] = __fadd_rn(a[j], 0.0f);  // pass + 0 (k_dense: -0 -> +0)
-                        C::store_nt(out + ((g + r) * f.out_stride + (int64_t)c * VEC), C::from_f32(a));
-                    }
-                }
-            } else {
-#pragma unroll 4
-                for (int q = 0; q < 32; ++q) {
-                    const int r = 2 * q + (lane >> 5);
-                    if ((em >> r) & 1) C::store_nt(out + ((g + r) * f.out_stride + (int64_t)c * VEC), C::zero());
-                }
-            }
-        }
-    }
-    // 2. the windows
-    // runs of window j (its boundaries against the last entry of window j - 1): start positions into
-    // s_seg[cw][j & 1] (this wave's own copy), returns the boundary mask (bit e: entry e starts a run)
-    auto plan = [&](int64_t j) -> uint32_t {
-        const int s = (int)(j & (WIN_NI - 1)), e = lane & 31;
-        const int32_t d = s_dst[s][e];
-        const int32_t pd = e ? s_dst[s][e - 1] : s_dst[(j - 1) & (WIN_NI - 1)][WIN_E - 1];
-        const uint32_t bm = (uint32_t)__ballot(lane < 32 && d != pd);
-        const uint32_t st = bm | 1u;
-        int32_t *sg = s_seg[cw][j & 1];
-        if (lane < 32 && ((st >> lane) & 1)) sg[__popc(st & ((1u << lane) - 1u))] = lane;
-        if (lane == 0) sg[__popc(st)] = WIN_E;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave's LDS operations: in order
-        return bm;
-    };
-    typename C::raw_t pv[MODE == SHPL_OUT_ADD ? WIN_PF : 1];
-    // ADD: the pass rows of this slot's runs of window j (unconditional loads: row 0 stands in for absent runs)
-    auto prefetch = [&](int64_t j, uint32_t bm) {
-        if constexpr (MODE == SHPL_OUT_ADD) {
-            const uint32_t st = bm | 1u;
-            const int ns = __popc(st);
-            const int32_t *sg = s_seg[cw][j & 1];
-            const int s = (int)(j & (WIN_NI - 1));
-#pragma unroll
-            for (int m = 0; m < WIN_PF; ++m) {
-                const int k = slot + m * WIN_SL;
-                int32_t key = k < ns ? s_dst[s][sg[k]] : -1;
-                if (key < 0) key = 0;
-                pv[m] = C::load(pass + ((int64_t)key * f.pass_stride + (int64_t)c * VEC));
-            }
-        }
-    };
-    uint32_t bm = 0;
-    int32_t Kprev = -2, K = -2;
-    for (int64_t i = w0;; ++i) {
-        win_barrier();  // window i landed
-        const int s = (int)(i & (WIN_NI - 1));
-        if (i == w0) {
-            Kprev = s_dst[(w0 - 1) & (WIN_NI - 1)][WIN_E - 1];
-            bm = plan(i);
-            prefetch(i, bm);
-        }
-        if (i + 1 >= w1 && K == -2) K = s_dst[(w1 - 1) & (WIN_NI - 1)][WIN_E - 1];
-        const bool more = go_on(i, Kprev, K);
-        const uint32_t st = bm | 1u;
-        const int ns = __popc(st);
-        const int32_t *sg = s_seg[cw][i & 1];
-        const int32_t ndst = s_dst[(i + 1) & (WIN_NI - 1)][0];
-        const uint8_t *rows = s_rows[i & (WIN_NS - 1)];
-#pragma unroll
-        for (int m = 0; m < WIN_PF; ++m) {
-            const int k = slot + m * WIN_SL;
-            if (k >= ns) break;
-            const int a = sg[k], e_end = sg[k + 1];
-            const int32_t key = s_dst[s][a];
-            const bool cont_in = k == 0 && !(bm & 1u);  // the run of the previous window goes on
-            if (key < 0) continue;
-            if (key == Kprev) continue;  // the previous stretch's run (it may span several windows)
-            if (i >= w1 && !cont_in) continue;  // the next stretch's runs
-            float acc[VEC];
-#pragma unroll
-            for (int j = 0; j < VEC; ++j) acc[j] = cont_in ? s_carry[i & 1][c][j] : 0.0f;
-            for (int e0 = a; e0 < e_end; e0 += 8) {  // 8 LDS row reads in flight, then the sums in order
-                typename C::raw_t r8[8];
-                float w8[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int e = e0 + u < WIN_E ? e0 + u : WIN_E - 1;
-                    // entry e's row: DMA e & 15, its first or second 512 bytes
-                    r8[u] = *reinterpret_cast<const typename C::raw_t *>(rows + (e & 15) * 1024 + (e >> 4) * 512 +
-                                                                          c * 16);
-                    w8[u] = s_val[s][e];
-                }
-                asm volatile("" ::: "memory");  // keep the 8 reads issued ahead of the sums (no sinking)
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    if (e0 + u >= e_end) break;
-                    float x[VEC];
-                    C::to_f32(r8[u], x);
-                    fma_free_accumulate<VEC>(acc, w8[u], x);
-                }
-            }
-            if (e_end == WIN_E && ndst == key && more) {  // goes on in the next window
-#pragma unroll
-                for (int j = 0; j < VEC; ++j) s_carry[(i + 1) & 1][c][j] = acc[j];
-                continue;
-            }
-            if (MODE == SHPL_OUT_ADD) {
-                float p[VEC];
-                C::to_f32(pv[m], p);
-#pragma unroll
-                for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(p[j], acc[j]);
-            }
-            C::store_nt(out + ((int64_t)key * f.out_stride + (int64_t)c * VEC), C::from_f32(acc));
-        }
-        if (!more) break;
-        bm = plan(i + 1);
-        prefetch(i + 1, bm);
-    }
-}
-
-// ---------------------------------------------------------------- k_seg2
-// Both row-keyed pulls of a pair as independent waves over windows of 64 sorted entries (config 3's shape:
-// rows of 32 chunks of 16 bytes, no per-column partials, both pulls SHPL_OUT_POOL or both SHPL_OUT_ADD). A
-// window wave loads its 64 entries' index words and the next 64's in one coalesced round trip (into its own LDS
-// scratch), finds every run boundary by two ballots, and walks as two halves: lanes 0-31 own the runs that
-// start in entries [0, 32), lanes 32-63 those that start in [32, 64), each following its last run past its
-// half (into the next 64 words; a run longer than that by global loads). A half takes SEG2_B entries per step,
-// their gathered rows (lane = 16-byte chunk) in flight together, and sums every run in entry order with
-// separate multiply and add -- k_rows' arithmetic, bitwise -- storing a row where its run ends. Entries before
-// a half's first run head belong to the run of the previous half / window. The empty rows are written by
-// zero waves, SEG2_ZR rows each (one key_range load per lane): zeros, or pass + 0 in ADD mode. One index round
-// trip per 64 entries instead of one per pair of rows (k_rows2), and no barrier anywhere.
-#ifndef SHPL_SEG2_XCD
-#define SHPL_SEG2_XCD 0  // window blocks XCD-contiguous (each XCD's L2 sees few frames' source rows)
-#endif
-constexpr int SEG2_W = 64;   // entries per window wave
-constexpr int SEG2_B = 8;    // entries per half and step (gathered rows in flight per lane)
-constexpr int SEG2_ZR = 64;  // rows per zero wave
-constexpr int SEG2_NC = 32;  // 16-byte chunks per row (the only row width of this form)
-
-struct Seg2Side {
-    Feat f;
-    const int32_t *dst, *src;
-    const float *val;
-    const int32_t *key_range;
-    int64_t nnz, n_rows, nwin, nzero;  // entries, rows, window waves, zero waves
-};
-
-template <typename T, int VEC, int MODE>
-__device__ __forceinline__ void seg2_zero(const Seg2Side &sd, int64_t z) {
-    typedef Chunk<T, VEC> C;
-    const int lane = threadIdx.x & 63;
-    const uint32_t c = lane & 31;
-    const Feat &f = sd.f;
-    const T *pass = reinterpret_cast<const T *>(f.pass) + f.pass_off;
-    T *out = reinterpret_cast<T *>(f.out);
-    const int64_t g = z * SEG2_ZR;
-    bool empty = false;
-    if (g + lane < sd.n_rows) {
-        const int2 kr = *reinterpret_cast<const int2 *>(sd.key_range + 2 * (g + lane));
-        empty = kr.x == kr.y;
-    }
-    const uint64_t em = __ballot(empty);
-    if (!em) return;
-    if (MODE == SHPL_OUT_ADD) {
-        for (int q0 = 0; q0 < SEG2_ZR / 2; q0 += 8) {
-            if (!((em >> (2 * q0)) & 0xFFFFull)) continue;  // (uniform) no empty row among these 16
-            typename C::raw_t v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {  // unconditional loads (row g for a non-empty one): no branch per load
-                const int r = 2 * (q0 + u) + (lane >> 5);
-                const int64_t row = ((em >> r) & 1) ? g + r : g;
-                v[u] = C::load(pass + (row * f.pass_stride + (int64_t)c * VEC));
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int r = 2 * (q0 + u) + (lane >> 5);
-                if (!((em >> r) & 1)) continue;
-                float a[VEC];
-                C::to_f32(v[u], a);
-#pragma unroll
-                for (int j = 0; j < VEC; ++j) a[j] = __fadd_rn(a[j], 0.0f);  // pass + 0 (k_dense: -0 -> +0)
-                C::store_nt(out + ((g + r) * f.out_stride + (int64_t)c * VEC), C::from_f32(a));
-            }
-        }
-    } else {
-#pragma unroll 8
-        for (int q = 0; q < SEG2_ZR / 2; ++q) {
-            const int r = 2 * q + (lane >> 5);
-            if ((em >> r) & 1) C::store_nt(out + ((g + r) * f.out_stride + (int64_t)c * VEC), C::zero());
-        }
-    }
-}
-
-template <typename T, int VEC, int MODE>
-__device__ __forceinline__ void seg2_window(const Seg2Side &sd, int64_t k, int32_t *sdst, int32_t *ssrc, float *sval) {
-    typedef Chunk<T, VEC> C;
-    const int lane = threadIdx.x & 63, h = lane >> 5;
-    const uint32_t c = lane & 31;
-    const Feat &f = sd.f;
-    const T *srcb = reinterpret_cast<const T *>(f.src) + f.src_off + (int64_t)c * VEC;
-    const T *pass = reinterpret_cast<const T *>(f.pass) + f.pass_off + (int64_t)c * VEC;
-    T *out = reinterpret_cast<T *>(f.out) + (int64_t)c * VEC;
-    const int64_t s0 = k * SEG2_W;
-    // the window's index words and the next window's: one round trip
-    int32_t d[2], sr[2];
-    float w[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int64_t e = s0 + q * SEG2_W + lane;
-        const bool ok = e < sd.nnz;
-        d[q] = ok ? sd.dst[e] : -1;
-        sr[q] = ok ? sd.src[e] : 0;
-        w[q] = ok ? sd.val[e] : 0.0f;
-    }
-    const int32_t before = s0 > 0 ? sd.dst[s0 - 1] : -1;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        sdst[q * SEG2_W + lane] = d[q];
-        ssrc[q * SEG2_W + lane] = sr[q] < 0 ? 0 : sr[q];
-        sval[q * SEG2_W + lane] = w[q];
-    }
-    int32_t p0 = __shfl_up(d[0], 1), p1 = __shfl_up(d[1], 1);
-    if (lane == 0) {
-        p0 = before;
-        p1 = __builtin_amdgcn_readlane(d[0], 63);
-    }
-    const uint64_t b0 = __ballot(d[0] != p0), b1 = __ballot(d[1] != p1);  // run (or hole stretch) starts
-    // this half's walk: from its first boundary in [32 h, 32 h + 32) to the first boundary at or after 32 h + 32
-    const uint32_t own = (uint32_t)(b0 >> (32 * h));
-    int start = -1, end = 2 * SEG2_W;
-    if (own) start = 32 * h + __builtin_ctz(own);
-    if (h == 0 && (b0 >> 32)) {
-        end = 32 + __builtin_ctzll(b0 >> 32);
-    } else if (b1) {
-        end = SEG2_W + __builtin_ctzll(b1);
-    }
-    const int len = start >= 0 ? end - start : 0;
-    const int wlen = max(len, __shfl_xor(len, 32, 64));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the scratch words (one wave's LDS operations: in order)
-    const uint64_t bnd[2] = {b0, b1};
-    int32_t key = -1;
-    float acc[VEC];
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) acc[j] = 0.0f;
-    typename C::raw_t pv = C::zero();
-    auto finish = [&]() {
-        if (key < 0) return;
-        if (MODE == SHPL_OUT_ADD) {
-            float a[VEC];
-            C::to_f32(pv, a);
-#pragma unroll
-            for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(a[j], acc[j]);
-        }
-        C::store_nt(out + (int64_t)key * f.out_stride, C::from_f32(acc));
-    };
-    for (int t0 = 0; t0 < wlen; t0 += SEG2_B) {
-        typename C::raw_t g[SEG2_B], pu[MODE == SHPL_OUT_ADD ? SEG2_B : 1];
-        int32_t dk[SEG2_B];
-        float wk[SEG2_B];
-        // the step's rows (and in ADD mode the pass rows of the runs starting in it): unconditional loads,
-        // row 0 standing in for entries past the walk or in a hole stretch
-#pragma unroll
-        for (int u = 0; u < SEG2_B; ++u) {
-            const int t = t0 + u;
-            const int p = min(max(start + t, 0), 2 * SEG2_W - 1);  // (a lane with no walk: start -1)
-            const bool act = t < len;
-            dk[u] = act ? sdst[p] : -1;
-            wk[u] = sval[p];
-            const int32_t row = dk[u] >= 0 ? ssrc[p] : 0;
-            g[u] = C::load(srcb + (int64_t)row * f.src_stride);
-            if (MODE == SHPL_OUT_ADD) {
-                const bool head = dk[u] >= 0 && ((bnd[p >> 6] >> (p & 63)) & 1);
-                pu[u] = C::load(pass + (int64_t)(head ? dk[u] : 0) * f.pass_stride);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < SEG2_B; ++u) {
-            const int t = t0 + u;
-            if (t >= len) break;
-            const int p = start + t;
-            if ((bnd[p >> 6] >> (p & 63)) & 1) {  // a run (or a hole stretch) starts here
-                finish();
-                key = dk[u];
-#pragma unroll
-                for (int j = 0; j < VEC; ++j) acc[j] = 0.0f;
-                if (MODE == SHPL_OUT_ADD) pv = pu[u];
-            }
-            if (key >= 0) {
-                float x[VEC];
-                C::to_f32(g[u], x);
-                fma_free_accumulate<VEC>(acc, wk[u], x);
-            }
-        }
-    }
-    // a run still going at the end of the next window's words: on by global loads while the destination stays
-    if (len > 0 && end == 2 * SEG2_W && key >= 0) {
-        for (int64_t e = s0 + 2 * SEG2_W;; e += 2) {
-            int32_t dd[2], ss[2];
-            float ww[2];
-            bool in[2];
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const bool okk = e + u < sd.nnz;
-                dd[u] = okk ? sd.dst[e + u] : -1;
-                ss[u] = okk ? sd.src[e + u] : 0;
-                ww[u] = okk ? sd.val[e + u] : 0.0f;
-            }
-#pragma unroll
-            for (int u = 0; u < 2; ++u) in[u] = dd[u] == key && (u == 0 || in[u - 1]);
-            typename C::raw_t raw[2];
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-                if (in[u]) raw[u] = C::load(srcb + (int64_t)ss[u] * f.src_stride);
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                if (in[u]) {
-                    float x[VEC];
-                    C::to_f32(raw[u], x);
-                    fma_free_accumulate<VEC>(acc, ww[u], x);
-                }
-            }
-            if (!in[1]) break;
-        }
-    }
-    if (len > 0) finish();
-}
-
-template <typename T, int VEC, int MODE>
-__global__ __launch_bounds__(SHPL_BLOCK) void k_seg2(const Seg2Side s0, const Seg2Side s1, int64_t wblocks) {
-    __shared__ int32_t s_dst[SHPL_BLOCK / SHPL_WAVE][2 * SEG2_W], s_src[SHPL_BLOCK / SHPL_WAVE][2 * SEG2_W];
-    __shared__ float s_val[SHPL_BLOCK / SHPL_WAVE][2 * SEG2_W];
-    const int wave = threadIdx.x >> 6;
-    int64_t b = blockIdx.x;
-    if (SHPL_SEG2_XCD && b < wblocks) b = xcd_block(b, wblocks);
-    const int64_t gw = b * (SHPL_BLOCK / SHPL_WAVE) + wave;
-    // the window waves (pixel-keyed pull first: its long runs), then the zero waves
-    if (gw < s1.nwin) {
-        seg2_window<T, VEC, MODE>(s1, gw, s_dst[wave], s_src[wave], s_val[wave]);
-    } else if (gw < s1.nwin + s0.nwin) {
-        seg2_window<T, VEC, MODE>(s0, gw - s1.nwin, s_dst[wave], s_src[wave], s_val[wave]);
-    } else {
-        const int64_t z = gw - s1.nwin - s0.nwin;
-        if (z < s1.nzero)
-            seg2_zero<T, VEC, MODE>(s1, z);
-        else if (z < s1.nzero + s0.nzero)
-            seg2_zero<T, VEC, MODE>(s0, z - s1.nzero);
-    }
-}
-
 bool aligned(const void *ptr, int64_t a) { return ((uintptr_t)ptr) % (uintptr_t)a == 0; }
 
 struct Plan {
@@ -1679,88 +1142,6 @@ extern "C" int shpl_pull_once(SHPL_PULL_ARGS) {
 namespace shpl {
 namespace {
 
-#ifndef SHPL_WIN_BLOCKS
-#define SHPL_WIN_BLOCKS 512  // k_win2 workgroups to aim for (two per CU: 72 KiB of LDS each)
-#endif
-// k_win2 for a pull pair it fits (rows of 32 chunks, no per-column partials, one mode: POOL or ADD); false:
-// the caller launches k_rows2.
-template <typename T, int VEC>
-bool pair_win(const RowsSide s[2], int mode, hipStream_t st, int *rc) {
-    if (!SHPL_PAIR_WIN || (mode != SHPL_OUT_POOL && mode != SHPL_OUT_ADD)) return false;
-    WinSide w[2] = {};
-    int64_t nwin = 0;
-    for (int k = 0; k < 2; ++k) {
-        if (s[k].n_rows == 0) continue;
-        if (s[k].f.cpool != (uint32_t)WIN_NC || s[k].e.col || !s[k].key_range || s[k].e.n <= 0) return false;
-        w[k].f = s[k].f;
-        w[k].dst = s[k].e.dst;
-        w[k].src = s[k].e.src;
-        w[k].val = s[k].e.val;
-        w[k].key_range = s[k].key_range;
-        w[k].nnz = s[k].e.n;
-        w[k].n_rows = s[k].n_rows;
-        w[k].nwin = (s[k].e.n + WIN_E - 1) / WIN_E;
-        nwin += w[k].nwin;
-    }
-    if (nwin == 0) return false;
-    int64_t wpb = (nwin + SHPL_WIN_BLOCKS - 1) / SHPL_WIN_BLOCKS;
-    if (wpb < 1) wpb = 1;
-    int64_t blocks = 0;
-    for (int k = 0; k < 2; ++k) {
-        if (w[k].nwin == 0) continue;
-        w[k].wpb = wpb;
-        w[k].blocks = (w[k].nwin + wpb - 1) / wpb;
-        w[k].rpb = (w[k].n_rows + w[k].blocks - 1) / w[k].blocks;
-        blocks += w[k].blocks;
-    }
-    if (blocks > 0x7fffffffLL) return false;
-    if (mode == SHPL_OUT_POOL)
-        hipLaunchKernelGGL((k_win2<T, VEC, SHPL_OUT_POOL>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, w[0],
-                           w[1]);
-    else
-        hipLaunchKernelGGL((k_win2<T, VEC, SHPL_OUT_ADD>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, w[0],
-                           w[1]);
-    *rc = hipGetLastError() == hipSuccess ? SHPL_OK : SHPL_ERR_HIP;
-    return true;
-}
-
-// k_seg2 for a pull pair it fits (the same conditions as k_win2); false: the caller launches another form.
-template <typename T, int VEC>
-bool pair_seg(const RowsSide s[2], int mode, hipStream_t st, int *rc) {
-    if (mode != SHPL_OUT_POOL && mode != SHPL_OUT_ADD) return false;
-    Seg2Side w[2] = {};
-    for (int k = 0; k < 2; ++k) {
-        if (s[k].n_rows == 0) continue;
-        if (s[k].f.cpool != (uint32_t)SEG2_NC || s[k].e.col || !s[k].key_range || s[k].e.n <= 0) return false;
-        w[k].f = s[k].f;
-        w[k].dst = s[k].e.dst;
-        w[k].src = s[k].e.src;
-        w[k].val = s[k].e.val;
-        w[k].key_range = s[k].key_range;
-        w[k].nnz = s[k].e.n;
-        w[k].n_rows = s[k].n_rows;
-        w[k].nwin = (s[k].e.n + SEG2_W - 1) / SEG2_W;
-        w[k].nzero = (s[k].n_rows + SEG2_ZR - 1) / SEG2_ZR;
-    }
-    const int64_t wpb = SHPL_BLOCK / SHPL_WAVE;
-    const int64_t wblocks = (w[0].nwin + w[1].nwin) / wpb;  // blocks of window waves only
-    const int64_t blocks = (w[0].nwin + w[1].nwin + w[0].nzero + w[1].nzero + wpb - 1) / wpb;
-    if (blocks == 0) return false;
-    if (blocks > 0x7fffffffLL) return false;
-    if (mode == SHPL_OUT_POOL)
-        hipLaunchKernelGGL((k_seg2<T, VEC, SHPL_OUT_POOL>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, w[0],
-                           w[1], wblocks);
-    else
-        hipLaunchKernelGGL((k_seg2<T, VEC, SHPL_OUT_ADD>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, w[0],
-                           w[1], wblocks);
-    *rc = hipGetLastError() == hipSuccess ? SHPL_OK : SHPL_ERR_HIP;
-    return true;
-}
-
-#ifndef SHPL_PAIR_SEG
-#define SHPL_PAIR_SEG 0
-#endif
-
 template <typename T, int VEC>
 int pair_t(RowsSide s[2], int G, hipStream_t st) {
     const int rpb = SHPL_BLOCK / G;
@@ -1775,11 +1156,6 @@ int pair_t(RowsSide s[2], int G, hipStream_t st) {
     int mode = -1;
     if (s[0].n_rows == 0 || s[1].n_rows == 0 || s[0].f.mode == s[1].f.mode)
         mode = s[0].n_rows ? s[0].f.mode : s[1].f.mode;
-    if constexpr (sizeof(T) * VEC == 16) {
-        int rc = SHPL_OK;
-        if (G == 32 && SHPL_PAIR_SEG && pair_seg<T, VEC>(s, mode, st, &rc)) return rc;
-        if (G == 32 && pair_win<T, VEC>(s, mode, st, &rc)) return rc;
-    }
 #define SHPL_ROWS2_M(GG, GR, M) \
     hipLaunchKernelGGL((k_rows2<T, VEC, GG, GR, M>), dim3((unsigned)blocks), dim3(SHPL_BLOCK), 0, st, s[0], s[1])
 #define SHPL_ROWS2_G(GG, GR)                                                  \
