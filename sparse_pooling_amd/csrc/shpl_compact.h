@@ -117,6 +117,36 @@ __device__ __forceinline__ void pass_copy(const PassCopy &c, int f, int b, int n
     }
 }
 
+// A caller's shpl_pass_copy (rows_per_frame rows per frame) as a PassCopy: SHPL_OK, or the status its shape
+// gets (SHPL_ERR_ARG / SHPL_ERR_BAD_SHAPE); *bytes += its read + write bytes per frame. NULL or 0 channels:
+// no copy (row_bytes 0).
+inline int make_pass_copy(const shpl_pass_copy *c, int64_t rows_per_frame, PassCopy *pc, int64_t *bytes) {
+    *pc = PassCopy{};
+    if (!c || c->channels == 0) return SHPL_OK;
+    if (c->dtype != SHPL_F32 && c->dtype != SHPL_BF16) return SHPL_ERR_ARG;
+    if (!c->src || !c->out || c->channels < 0) return SHPL_ERR_ARG;
+    const int64_t esz = c->dtype == SHPL_F32 ? 4 : 2;
+    const int64_t rb = c->channels * esz;
+    if (rb % 16 || (c->src_stride * esz) % 16 || (c->out_stride * esz) % 16 || ((uintptr_t)c->src & 15) ||
+        ((uintptr_t)c->out & 15) || c->src_stride < c->channels || c->out_stride < c->channels ||
+        (rb / 16) * rows_per_frame >= ((int64_t)1 << 31))  // a frame's pieces in 32 bits
+        return SHPL_ERR_BAD_SHAPE;
+    *pc = PassCopy{(const uint8_t *)c->src, (uint8_t *)c->out, c->src_stride * esz, c->out_stride * esz, rb,
+                   rows_per_frame};
+    *bytes += 2 * rb * rows_per_frame;
+    return SHPL_OK;
+}
+
+// Rider workgroups per frame for copies of `bytes` per frame: ~240 over the batch (the chip's CUs beside the
+// latency-bound workgroups), at most one per 64 KiB of a frame's copy.
+inline int rider_blocks(int n_frames, int64_t bytes) {
+    if (bytes <= 0) return 0;
+    int64_t per = 240 / n_frames;
+    const int64_t by_size = bytes / (64 * 1024);
+    if (per > by_size) per = by_size;
+    return (int)(per < 1 ? 1 : per);
+}
+
 __device__ __forceinline__ void frame_range(const Frames &fr, int f, int64_t &p0, int64_t &p1, int64_t &cap_end) {
     p0 = fr.pt_off[f];
     cap_end = fr.pt_off[f + 1];

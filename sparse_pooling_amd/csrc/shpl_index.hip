@@ -394,28 +394,10 @@ extern "C" int shpl_build_index_buckets(int n_frames, const int64_t *d_point_off
     const shpl_pass_copy *cps[2] = {cell_copy, pixel_copy};
     int64_t copy_bytes = 0;
     for (int k = 0; k < 2; ++k) {
-        const shpl_pass_copy *c = cps[k];
-        if (!c || c->channels == 0) continue;
-        if (c->dtype != SHPL_F32 && c->dtype != SHPL_BF16) return SHPL_ERR_ARG;
-        if (!c->src || !c->out || c->channels < 0) return SHPL_ERR_ARG;
-        const int64_t esz = c->dtype == SHPL_F32 ? 4 : 2;
-        const int64_t rb = c->channels * esz;
-        if (rb % 16 || (c->src_stride * esz) % 16 || (c->out_stride * esz) % 16 || ((uintptr_t)c->src & 15) ||
-            ((uintptr_t)c->out & 15) || c->src_stride < c->channels || c->out_stride < c->channels ||
-            (rb / 16) * (k ? g.n_pix : g.n_cells) >= ((int64_t)1 << 31))  // a frame's pieces in 32 bits
-            return SHPL_ERR_BAD_SHAPE;
-        bk.cp[k] = PassCopy{(const uint8_t *)c->src, (uint8_t *)c->out, c->src_stride * esz, c->out_stride * esz, rb,
-                            k ? g.n_pix : g.n_cells};
-        copy_bytes += 2 * rb * (k ? g.n_pix : g.n_cells);
+        rc = make_pass_copy(cps[k], k ? g.n_pix : g.n_cells, &bk.cp[k], &copy_bytes);
+        if (rc) return rc;
     }
-    if (copy_bytes > 0) {
-        // rider workgroups per frame: ~240 over the batch (the chip's CUs beside the index workgroups),
-        // at most one per 64 KiB of a frame's copy
-        int64_t per = 240 / n_frames;
-        const int64_t by_size = copy_bytes / (64 * 1024);
-        if (per > by_size) per = by_size;
-        bk.cp_blocks = (int)(per < 1 ? 1 : per);
-    }
+    bk.cp_blocks = rider_blocks(n_frames, copy_bytes);
     return build_index(n_frames, d_point_offsets, d_point_counts, max_points_per_frame, d_points, points_dtype,
                        d_voxels, voxels_itype, vox_stride, d_P, g, d_mval, d_cell, d_pix, d_val, nullptr, nullptr,
                        d_frame_nnz, d_frame_out_off, d_err, d_ws, ws_bytes, (hipStream_t)stream, &bk);
