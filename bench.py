@@ -100,9 +100,6 @@ def parse():
     ap.add_argument("--split-form", default="serial", choices=["serial", "overlap"],
                     help="split layer: the pooled half after the pass-through copy, the step captured in a graph "
                          "(serial), or beside the copy, eager with the chain at high priority (overlap; A/B)")
-    ap.add_argument("--copy-at", default=None, metavar="CELL,PIXEL",
-                    help="bucketed steps: the launch each forward pass-through copy rides, 'index' or 'csr' "
-                         "(pipeline.FusedPipeline.CELL_COPY_AT / PIXEL_COPY_AT)")
     ap.add_argument("--head-k", type=int, default=None,
                     help="bucketed pipelines: run heads per destination in the CSRs (FusedPipeline.HEAD_K; 0 = none; "
                          "A/B)")
@@ -462,8 +459,6 @@ def main():
     pipeline.FusedPipeline.SPLIT_SERIAL = args.split_form == "serial"
     if args.head_k is not None:
         pipeline.FusedPipeline.HEAD_K = args.head_k
-    if args.copy_at:
-        pipeline.FusedPipeline.CELL_COPY_AT, pipeline.FusedPipeline.PIXEL_COPY_AT = args.copy_at.split(",")
     esz0 = 2 if dtype == torch.bfloat16 else 4
     split = (not dual and not args.rows and not args.no_overlap and
              (args.split == "on" or (args.split == "auto" and min(spec.c_bev, spec.c_img) * esz0 >= 1024)))

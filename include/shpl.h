@@ -478,10 +478,6 @@ typedef struct {
     const float *val;                     /* [nnz_cap] */
     void *ws;                             /* the bucket workspace */
     size_t ws_bytes;
-    /* optional riders of shpl_build_csr_buckets' launch (NULL: none): pass-through copies as in
-     * shpl_build_index_buckets -- a copy rides one of the two calls, so each launch's length is set by its
-     * bytes rather than by the latency-bound sort or index work beside them */
-    const shpl_pass_copy *cell_copy, *pixel_copy;
 } shpl_buckets;
 
 /* One pull of shpl_pull_pair: the arguments of shpl_pull after its csr. */
@@ -502,9 +498,7 @@ typedef struct {
  * bucket by destination, stably (the bucket is in entry order), emits the
  * sorted entries and key_range (when set) and clears the unused capacity --
  * the same lists shpl_build_csr makes of the same index arrays. No counting or
- * bucketing pass: the index build did both. bk->cell_copy / pixel_copy: extra
- * workgroups of the launch copy those pass-through halves (shape rules and
- * SHPL_ERR_BAD_SHAPE as shpl_build_index_buckets' riders). */
+ * bucketing pass: the index build did both. */
 int shpl_build_csr_buckets(const shpl_buckets *bk, const shpl_csr *by_cell, const shpl_csr *by_pixel,
                            void *stream);
 

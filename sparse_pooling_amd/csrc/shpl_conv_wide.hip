@@ -191,12 +191,6 @@ __global__ __launch_bounds__(BLOCK, 2) void k_conv_wide(const WideArgs p) {
         a_off[ks] = (uint32_t)((wn * 64 + l16) * 128 + (((4 * ks + kg) ^ (lane & 7)) << 4));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-#ifndef SHPL_WIDE_PRIO
-#define SHPL_WIDE_PRIO 0
-#endif
-    // static priority for the second-dispatched half (waves 4-7: each SIMD's arbitration loser), once, no flips
-    // (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-    if (SHPL_WIDE_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
     for (int s = 0; s < steps; ++s) {
         const int q = s / 9, t = s - 9 * q, ky = t / 3, kx = t - 3 * ky;
         const uint8_t *hb = hbuf0 + (q & 1) * HALO_BYTES;

@@ -13,7 +13,7 @@
 // rank fix-up that restores TF's order inside each tile. Nothing is sized by
 // the number of destinations (no per-cell counters in HBM), and tiles hold
 // a few entries each, so the quadratic rank costs less than a sort pass.
-#include "shpl_compact.h"  // (PassCopy: the riders of k_bsort2)
+#include "shpl_common.h"
 
 namespace shpl {
 namespace {
@@ -958,22 +958,8 @@ struct BsIn {
 constexpr int BS_BLOCK = 1024;  // threads of a k_bsort2 workgroup (the horizon's 2 k-entry pixel buckets: 3 rounds)
 constexpr int BS_LCAP = 4096;   // bucket words staged in LDS with their source rows and values (48 KiB)
 
-// Riders of k_bsort2 (optional): pass-through copies, as k_index1's (shpl_compact.h pass_copy), in blocks past
-// the sort's; per frame `per` workgroups for each copy.
-struct BsRiders {
-    PassCopy cp[2];
-    int per;
-};
-
-__global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide s1, BsRiders rd) {
-    static_assert(BS_BLOCK == IDX_BLOCK, "pass_copy's thread count");
+__global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide s1) {
     __shared__ uint32_t one[1];
-    if ((int64_t)blockIdx.x >= s0.blocks + s1.blocks) {  // a rider (uniform): copy c's workgroup r of frame f
-        const int64_t rj = (int64_t)blockIdx.x - s0.blocks - s1.blocks;
-        const int f = (int)(rj / (2 * rd.per)), c = (int)((rj / rd.per) & 1), r = (int)(rj % rd.per);
-        if (rd.cp[c].row_bytes > 0) pass_copy(rd.cp[c], f, r, rd.per);
-        return;
-    }
     // the pixel-keyed buckets first (the horizon's heavy ones start early instead of forming the tail)
     const bool second = (int64_t)blockIdx.x < s1.blocks;
     const int64_t b = second ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - s1.blocks;
@@ -1258,30 +1244,21 @@ extern "C" int shpl_build_csr_buckets(const shpl_buckets *bk, const shpl_csr *by
         if (l.nr[k] == 0) s[k].blocks = 0;
     }
     hipStream_t st = (hipStream_t)stream;
-    BsRiders rd = {};
-    int64_t copy_bytes = 0;
-    const shpl_pass_copy *cps[2] = {bk->cell_copy, bk->pixel_copy};
-    for (int k = 0; k < 2; ++k) {
-        rc = make_pass_copy(cps[k], l.kpf[k], &rd.cp[k], &copy_bytes);
-        if (rc) return rc;
-    }
-    rd.per = rider_blocks(bk->n_frames, copy_bytes);
-    if (bk->nnz_cap == 0) {  // an empty map: empty runs everywhere (and the riders alone)
+    if (bk->nnz_cap == 0) {  // an empty map: empty runs everywhere
         for (int k = 0; k < 2; ++k) {
             if (cs[k] && cs[k]->key_range && cs[k]->n_keys > 0 &&
                 hipMemsetAsync(cs[k]->key_range, 0, sizeof(int32_t) * 2 * (size_t)cs[k]->n_keys, st) != hipSuccess)
                 return SHPL_ERR_HIP;
         }
-        s[0].blocks = s[1].blocks = 0;
-        if (rd.per == 0) return SHPL_OK;
+        return SHPL_OK;
     }
-    const int64_t blocks = s[0].blocks + s[1].blocks + (int64_t)bk->n_frames * 2 * rd.per;
+    const int64_t blocks = s[0].blocks + s[1].blocks;
     if (blocks == 0) return SHPL_OK;
     if (blocks > 0x7fffffffLL) return SHPL_ERR_BAD_SHAPE;
     char *w = (char *)bk->ws;
     const BsIn in{bk->frame_off, bk->frame_nnz, bk->cell, bk->pix, bk->val, (const int32_t *)(w + l.ext),
                   (const uint32_t *)(w + l.words), bk->n_frames, l.nrmax, bk->nnz_cap};
-    hipLaunchKernelGGL(k_bsort2, dim3((unsigned)blocks), dim3(BS_BLOCK), 0, st, in, s[0], s[1], rd);
+    hipLaunchKernelGGL(k_bsort2, dim3((unsigned)blocks), dim3(BS_BLOCK), 0, st, in, s[0], s[1]);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;
 }

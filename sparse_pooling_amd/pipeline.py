@@ -128,7 +128,7 @@ class FusedPipeline:
                 float(self.bv_size[1]), self.stride[0], self.stride[1], L.ptr(mval), L.ptr(self.cell),
                 L.ptr(self.pix), L.ptr(self.val), L.ptr(self.frame_nnz), L.ptr(self.frame_off),
                 L.ptr(self.err), L.ptr(self.index_ws), self.index_ws.numel(), self.N, L.ptr(self.bkt_ws),
-                self.bkt_ws.numel(), *self._index_riders(pass_copies), st), "shpl_build_index_buckets")
+                self.bkt_ws.numel(), *self._copy_riders(pass_copies), st), "shpl_build_index_buckets")
             return
         L.check(self._lib.shpl_build_index(
             self.B, L.ptr(point_offsets), L.ptr(point_counts), self.max_points, L.ptr(points),
@@ -198,32 +198,16 @@ class FusedPipeline:
                                          ctypes.byref(pix_desc) if pix_desc else None,
                                          L.stream_of(self.dev)), "shpl_pull_pair")
 
-    # bucketed steps: which launch each forward pass-through copy rides -- "index" (shpl_build_index_buckets)
-    # or "csr" (shpl_build_csr_buckets, shpl_buckets.cell_copy / pixel_copy)
-    CELL_COPY_AT, PIXEL_COPY_AT = "index", "index"
-
     def _copy_riders(self, pass_copies):
-        """The forward's pass-through copies as (cell, pixel) shpl_pass_copy structs (None without copies)."""
         if pass_copies is None:
-            self._riders = (None, None)
-            return self._riders
+            return None, None
         bev, img = pass_copies
         dt = L.dtype_code(self.bv_fused)
         cell = L.ShplPassCopy(dt, bev.data_ptr(), self.Cb, self.bv_fused.data_ptr(), self.Cb + self.Ci, self.Cb)
         pix = L.ShplPassCopy(dt, img.data_ptr(), self.Ci, self.img_fused.data_ptr(), self.Ci + self.Cb,
                              self.Ci) if self.dual else None
-        self._riders = (cell, pix)  # kept alive until the calls that take them return
-        return self._riders
-
-    def _index_riders(self, pass_copies):
-        """The rider arguments of shpl_build_index_buckets; the copies that ride the CSR launch instead go into
-        the shpl_buckets struct (cleared when there are none)."""
-        cell, pix = self._copy_riders(pass_copies)
-        at = (self.CELL_COPY_AT, self.PIXEL_COPY_AT)
-        for c, a, field in ((cell, at[0], "cell_copy"), (pix, at[1], "pixel_copy")):
-            setattr(self.bkt, field, ctypes.addressof(c) if (c is not None and a == "csr") else None)
-        ref = lambda c, a: ctypes.byref(c) if (c is not None and a == "index") else None  # noqa: E731
-        return ref(cell, at[0]), ref(pix, at[1])
+        self._riders = (cell, pix)  # kept alive until the call returns
+        return ctypes.byref(cell), (ctypes.byref(pix) if pix is not None else None)
 
     riders = True  # bucketed step_overlapped: pass-through halves ride the index launches (False: k_dense copies)
 

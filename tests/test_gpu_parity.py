@@ -754,50 +754,6 @@ def test_index1_barrier_give_up_and_dirty_words():
     clean_step_matches_oracle()
 
 
-@pytest.mark.parametrize("at", [("csr", "index"), ("index", "csr"), ("csr", "csr")])
-def test_pass_copies_ride_either_launch(at):
-    """The forward concats' pass-through halves ride the index launch or the CSR launch
-    (shpl_buckets.cell_copy / pixel_copy: extra k_bsort2 workgroups) -- bitwise the same step as both on the
-    index launch, and the oracle's layer (config 3's shape, bf16, 4 frames, graph-replayed like the bench)."""
-    from sparse_pooling_amd import pipeline
-    spec = synth.CONFIGS[3]
-    B = 4
-    frames = [synth.make_frame(spec, seed=120 + f, n_outside=10) for f in range(B)]
-    pts, vox, off, P, maxp, N = pipeline.stack_frames(frames, DEV)
-    Hb, Wb = spec.bev_feat_hw
-    Hi, Wi = spec.img_feat_hw
-    tb = torch.randn((B, Hb, Wb, spec.c_bev), device=DEV).to(torch.bfloat16)
-    ti = torch.randn((B, Hi, Wi, spec.c_img), device=DEV).to(torch.bfloat16)
-    outs = []
-    for where in (("index", "index"), at):
-        pl = pipeline.FusedPipeline(B, maxp, N, spec.im_size, spec.bv_size, spec.stride, spec.c_bev, spec.c_img,
-                                    dtype=torch.bfloat16, dual=True)
-        pl.CELL_COPY_AT, pl.PIXEL_COPY_AT = where
-        side, side2 = torch.cuda.Stream(), torch.cuda.Stream()
-        pl.step_overlapped(pts, vox, off, P, tb, ti, side, side2=side2)
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        gs = torch.cuda.Stream()
-        gs.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.graph(g, stream=gs):
-            pl.step_overlapped(pts, vox, off, P, tb, ti, side, side2=side2)
-        pl.bv_fused.fill_(float("nan"))
-        pl.img_fused.fill_(float("nan"))
-        g.replay()
-        torch.cuda.synchronize()
-        pl.check()
-        outs.append((pl.bv_fused.clone(), pl.img_fused.clone()))
-    assert torch.equal(outs[0][0].view(torch.int16), outs[1][0].view(torch.int16))
-    assert torch.equal(outs[0][1].view(torch.int16), outs[1][1].view(torch.int16))
-    bev, img = tb[:1].float().cpu().numpy(), ti[:1].float().cpu().numpy()
-    ref = _oracle_frame(frames[0], spec.stride)
-    eb, ei = orc.sparse_pool_layer(bev, img, ref["Mij_pool"], ref["M_val"], ref["M_size"], ref["img_index_flip_pool"],
-                                   dual=True)
-    for got, want in ((outs[1][0][:1], eb), (outs[1][1][:1], ei)):
-        np.testing.assert_array_equal(_np(got.view(torch.int16)).view(np.uint16),
-                                      orc.to_bf16_bits(want.astype(np.float32)))
-
-
 @pytest.mark.parametrize("dtype,cb,ci,sizes", [("bf16", 256, 256, [1500, 1500, 700]), ("f32", 128, 128, [1500, 900]),
                                                ("bf16", 256, 256, [0, 3000, 1, 5]), ("bf16", 256, 128, [2500, 2500])])
 def test_window_pulls_short_stretches(dtype, cb, ci, sizes):
