@@ -81,7 +81,6 @@ struct Bkt {
     int cp_at[2];     // the launch each copy rides: 0 = k_count, 1 = k_compact
     int cp_blocks;    // rider workgroups per frame in each launch (0: none)
     int32_t *bar;     // [2][F] k_index1's frame barrier words (arrivals, departures): zero between calls
-    int xcd;          // k_index1: each frame's chunks on one XCD (at most 8 frames; host-chosen)
 };
 
 #ifndef SHPL_CP_BATCH
@@ -570,20 +569,13 @@ __device__ __forceinline__ void frame_barrier(const Frames &fr, const Bkt &bk, i
 #ifndef SHPL_IDX1_WPE
 #define SHPL_IDX1_WPE 0  // waves per SIMD asked of the register allocator (8: two workgroups per CU); 0 = its own
 #endif
-#ifndef SHPL_IDX1_XCD
-#define SHPL_IDX1_XCD 0
-#endif
-// block ids k_index1 gives its chunk workgroups (xcd: 8 per chunk index, those of absent frames idle)
-__host__ __device__ inline int64_t index1_chunk_ids(int n_frames, int n_chunks, int xcd) {
-    return xcd ? (int64_t)8 * n_chunks : (int64_t)n_frames * n_chunks;
-}
 template <typename Stage>
 __global__ __launch_bounds__(IDX_BLOCK)
 #if SHPL_IDX1_WPE
 __attribute__((amdgpu_waves_per_eu(SHPL_IDX1_WPE, SHPL_IDX1_WPE)))
 #endif
 void k_index1(Stage st, Frames fr, Bkt bk) {
-    const int64_t b = blockIdx.x, n_ch = index1_chunk_ids(fr.n_frames, fr.n_chunks, bk.xcd);
+    const int64_t b = blockIdx.x, n_ch = (int64_t)fr.n_frames * fr.n_chunks;
     if (b >= n_ch) {  // a rider workgroup (uniform): copy c's workgroup r of frame f
         const int64_t rj = b - n_ch;
         const int per = bk.cp_blocks;
@@ -591,18 +583,7 @@ void k_index1(Stage st, Frames fr, Bkt bk) {
         if (bk.cp[c].row_bytes > 0) pass_copy(bk.cp[c], f, r, per);
         return;
     }
-    int f, j;
-    if (bk.xcd) {
-        // a frame's chunks on one XCD (blocks are dealt round-robin over the 8: b and b + 8 share one -- for
-        // speed only, nothing depends on it): chunk j of frame f at id 8 j + f (at most 8 frames: an XCD never
-        // holds more than one frame's <= 32 chunk workgroups); the ids of absent frames idle
-        f = (int)(b & 7);
-        j = (int)(b >> 3);
-        if (f >= fr.n_frames) return;  // (uniform)
-    } else {
-        f = (int)(b / fr.n_chunks);
-        j = (int)(b - (int64_t)f * fr.n_chunks);
-    }
+    const int f = (int)(b / fr.n_chunks), j = (int)(b - (int64_t)f * fr.n_chunks);
     SHPL_IDX1_STAMP(0);
     // the frame's projection matrix into LDS, its loads in flight beside the frame offsets' (count_phase's first
     // block barrier precedes every eval): read from global memory inside eval it was one more round trip
@@ -682,9 +663,7 @@ int run_compaction(const Stage &st, int n_frames, int64_t max_points, const int6
                 Bkt b1 = *bk;
                 b1.cp_blocks = per;
                 const bool any = bk->cp[0].row_bytes > 0 || bk->cp[1].row_bytes > 0;
-                b1.xcd = SHPL_IDX1_XCD && n_frames <= 8;
-                const int64_t blocks =
-                    index1_chunk_ids(n_frames, fr.n_chunks, b1.xcd) + (any ? (int64_t)n_frames * 2 * per : 0);
+                const int64_t blocks = (int64_t)n_frames * fr.n_chunks + (any ? (int64_t)n_frames * 2 * per : 0);
                 hipLaunchKernelGGL((k_index1<Stage>), dim3((unsigned)blocks), dim3(IDX_BLOCK), 0, stream, st, fr, b1);
                 SHPL_LAUNCH_CHECK();
                 return SHPL_OK;
