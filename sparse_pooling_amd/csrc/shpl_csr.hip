@@ -811,7 +811,8 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
                                                  const int32_t *cell, const int32_t *pix, const float *vals,
                                                  int32_t *ent_dst, int32_t *ent_src, float *ent_val,
                                                  int32_t *ent_col, int32_t *key_range, int2 *heads = nullptr,
-                                                 int head_k = 0) {
+                                                 int head_k = 0, const int32_t *wsrc = nullptr,
+                                                 const float *wval = nullptr) {
     constexpr int NW = BLOCK / 64;
     __shared__ int32_t cnt[NW][RANGE_KEYS], s_tot[RANGE_KEYS], s_beg[RANGE_KEYS];
     __shared__ uint64_t s_peer[NW][RANGE_KEYS];  // per wave and destination: its batch's lanes (zero between uses)
@@ -829,18 +830,27 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
     // 1. per-slice counts (and, staged, the words with their sources and values into LDS)
     for (int32_t i0 = threadIdx.x; i0 < n; i0 += 4 * BLOCK) {  // 4 words per thread in flight
         uint32_t w[4];
+        int32_t sr[4];
+        float vl[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) w[u] = i0 + u * BLOCK < n ? words[i0 + u * BLOCK] : 0u;
+        for (int u = 0; u < 4; ++u) {  // (with wsrc / wval: every load of the word's entry in one round trip)
+            const bool in = i0 + u * BLOCK < n;
+            w[u] = in ? words[i0 + u * BLOCK] : 0u;
+            if (wsrc && staged) {
+                sr[u] = in ? wsrc[i0 + u * BLOCK] : 0;
+                vl[u] = in ? wval[i0 + u * BLOCK] : 0.0f;
+            }
+        }
         if (staged) {
-            int32_t sr[4];
-            float vl[4];
+            if (!wsrc) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                if (i0 + u * BLOCK >= n) continue;
-                const int64_t e = e0 + (w[u] & 0xffffffu);
-                const int32_t kk = col ? col[e] : (int32_t)e;
-                vl[u] = vals[e];
-                sr[u] = direction == SHPL_BY_CELL ? pix[kk] : cell[e];
+                for (int u = 0; u < 4; ++u) {
+                    if (i0 + u * BLOCK >= n) continue;
+                    const int64_t e = e0 + (w[u] & 0xffffffu);
+                    const int32_t kk = col ? col[e] : (int32_t)e;
+                    vl[u] = vals[e];
+                    sr[u] = direction == SHPL_BY_CELL ? pix[kk] : cell[e];
+                }
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -894,6 +904,11 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
                 src = l_s[i];
                 val = l_v[i];
                 if (ent_col) kk = col ? col[e0 + (w & 0xffffffu)] : (int32_t)(e0 + (w & 0xffffffu));
+            } else if (wsrc) {
+                w = words[i];
+                src = wsrc[i];
+                val = wval[i];
+                kk = col ? col[e0 + (w & 0xffffffu)] : (int32_t)(e0 + (w & 0xffffffu));
             } else {
                 w = words[i];
                 const int64_t e = e0 + (w & 0xffffffu);
@@ -951,6 +966,8 @@ struct BsIn {
     const float *val;
     const int32_t *ext;
     const uint32_t *words;
+    const int32_t *wsrc;  // beside each word: the entry's source row and value (shpl_common.h BkLayout)
+    const float *wval;
     int n_frames, nrmax;
     int64_t nnz_cap;
 };
@@ -975,11 +992,15 @@ __global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide 
     const int direction = key ? SHPL_BY_PIXEL : SHPL_BY_CELL;
     int32_t start = 0, n = 0, valid = 0;
     const uint32_t *W = one;
+    const int32_t *WS = nullptr;  // the words' source rows and values (no bucket: the index arrays, read there)
+    const float *WV = nullptr;
     if (nnz >= 2) {
         const int32_t *x = in.ext + (((int64_t)key * in.n_frames + f) * in.nrmax + q) * 2;
         start = x[0];
         n = x[1];
         W = in.words + (int64_t)key * in.nnz_cap + p0 + start;
+        WS = in.wsrc + (int64_t)key * in.nnz_cap + p0 + start;
+        WV = in.wval + (int64_t)key * in.nnz_cap + p0 + start;
         if (q == sd.nr - 1) valid = start + n;  // the frame's entries with valid destinations
     } else if (nnz == 1) {
         // no bucket: the frame's one entry, in this range or not
@@ -996,7 +1017,7 @@ __global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide 
     }
     const int64_t out0 = p0 + start;
     bucket_sort_emit<BS_BLOCK, BS_LCAP>(W, n, p0, out0, k0, nk, direction, nullptr, in.cell, in.pix, in.val, sd.ent_dst,
-                                        sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range, sd.heads, sd.head_k);
+                                        sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range, sd.heads, sd.head_k, WS, WV);
     // the frame's unused capacity (its last range), the slots and key ranges after the last frame
     if (q != sd.nr - 1) return;
     for (int64_t h = p0 + valid + threadIdx.x; h < cap_end; h += BS_BLOCK) sd.ent_dst[h] = -1;
@@ -1257,7 +1278,8 @@ extern "C" int shpl_build_csr_buckets(const shpl_buckets *bk, const shpl_csr *by
     if (blocks > 0x7fffffffLL) return SHPL_ERR_BAD_SHAPE;
     char *w = (char *)bk->ws;
     const BsIn in{bk->frame_off, bk->frame_nnz, bk->cell, bk->pix, bk->val, (const int32_t *)(w + l.ext),
-                  (const uint32_t *)(w + l.words), bk->n_frames, l.nrmax, bk->nnz_cap};
+                  (const uint32_t *)(w + l.words), (const int32_t *)(w + l.wsrc), (const float *)(w + l.wval),
+                  bk->n_frames, l.nrmax, bk->nnz_cap};
     hipLaunchKernelGGL(k_bsort2, dim3((unsigned)blocks), dim3(BS_BLOCK), 0, st, in, s[0], s[1]);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;

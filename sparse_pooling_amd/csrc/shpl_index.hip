@@ -47,7 +47,24 @@ struct Geometry {
     double wq, hq, bhq, bwq;  // floor(size / stride)
     int64_t n_cells;          // int(bhq*bwq)
     int64_t n_pix;            // hq*wq
+    double inv_img, inv_bv;   // 1 / stride when the stride is a power of two (x / 2^k == x * 2^-k exactly), else 0
 };
+
+// 1 / s when s is a power of two (its reciprocal exact, so x * (1 / s) is bitwise x / s for every finite x that
+// stays normal -- the image and voxel indices here), else 0: the division then stays a division.
+#ifndef SHPL_POW2_DIV
+#define SHPL_POW2_DIV 1
+#endif
+inline double pow2_reciprocal(double s) {
+    if (!SHPL_POW2_DIV) return 0.0;
+    int e = 0;
+    return (s > 0.0 && frexp(s, &e) == 0.5 && e > -1000 && e < 1000) ? ldexp(1.0, 1 - e) : 0.0;
+}
+
+// x / s (IEEE), as a multiply when the reciprocal is exact (inv != 0)
+__device__ __forceinline__ double div_stride(double x, double s, double inv) {
+    return inv != 0.0 ? __dmul_rn(x, inv) : __ddiv_rn(x, s);
+}
 
 Geometry make_geometry(double im_w, double im_h, double bv_h, double bv_w, double s_img, double s_bv) {
     Geometry g = {};
@@ -61,6 +78,8 @@ Geometry make_geometry(double im_w, double im_h, double bv_h, double bv_w, doubl
     g.bwq = floor(bv_w / s_bv);
     g.n_cells = (int64_t)(g.bhq * g.bwq);
     g.n_pix = (int64_t)g.hq * (int64_t)g.wq;
+    g.inv_img = pow2_reciprocal(s_img);
+    g.inv_bv = pow2_reciprocal(s_bv);
     return g;
 }
 
@@ -75,14 +94,14 @@ struct Produced {
 __device__ __forceinline__ Produced produce(const Geometry &g, double ur, double vr, int64_t vx,
                                             int64_t vz) {
     Produced o = {};
-    double u = floor(__ddiv_rn(ur, g.s_img));
-    double v = floor(__ddiv_rn(vr, g.s_img));
+    double u = floor(div_stride(ur, g.s_img, g.inv_img));
+    double v = floor(div_stride(vr, g.s_img, g.inv_img));
     if (u >= g.wq) u = g.wq - 1.0;
     if (v >= g.hq) v = g.hq - 1.0;
     o.u = u;
     o.v = v;
-    const double bx = floor(__ddiv_rn((double)vx, g.s_bv));
-    const double bz = floor(__ddiv_rn((double)vz, g.s_bv));
+    const double bx = floor(div_stride((double)vx, g.s_bv, g.inv_bv));
+    const double bz = floor(div_stride((double)vz, g.s_bv, g.inv_bv));
     o.r = (int64_t)__dadd_rn(__dmul_rn(bz, g.bwq), bx);
     o.inside = o.r < g.n_cells;
     return o;
@@ -164,6 +183,13 @@ struct FusedStage {
         pix[pos] = -1;
         val[pos] = 0.0f;
     }
+    // the global source rows of a bucketed entry (frame-local cell kc, pixel kp): the pixel for its cell
+    // bucket's pull, the cell for its pixel bucket's (what emit() writes into pix / cell)
+    __device__ void bucket_rows(int f, int32_t kc, int32_t kp, int32_t &row_cell, int32_t &row_pix) const {
+        row_cell = (int32_t)(f * g.n_pix + kp);
+        row_pix = (int32_t)(f * g.n_cells + kc);
+    }
+    __device__ float bucket_val(int64_t i) const { return mval ? mval[i] : 1.0f; }
     // frame-local destinations of a kept entry (buckets): the cell and pixel emit() writes, unless -1
     __device__ bool bucket_keys(const Payload &pl, int32_t &kc, int32_t &kp) const {
         const int64_t r = pl.pr.r, vi = (int64_t)pl.pr.v, ui = (int64_t)pl.pr.u;
@@ -389,8 +415,8 @@ extern "C" int shpl_build_index_buckets(int n_frames, const int64_t *d_point_off
 #define SHPL_RIDERS 0
 #endif
     Bkt bk{{l.nr[0], l.nr[1]}, l.nrmax, nnz_cap, (int32_t *)(b + l.hist), (int32_t *)(b + l.ext),
-           (uint32_t *)(b + l.words), {}, {SHPL_RIDERS == 2 ? 1 : 0, SHPL_RIDERS == 1 ? 0 : 1}, 0,
-           (int32_t *)(b + l.bar)};
+           (uint32_t *)(b + l.words), (int32_t *)(b + l.wsrc), (float *)(b + l.wval), {},
+           {SHPL_RIDERS == 2 ? 1 : 0, SHPL_RIDERS == 1 ? 0 : 1}, 0, (int32_t *)(b + l.bar)};
     const shpl_pass_copy *cps[2] = {cell_copy, pixel_copy};
     int64_t copy_bytes = 0;
     for (int k = 0; k < 2; ++k) {
