@@ -274,7 +274,7 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr, Bkt bk
 // point's entry slot in the frame when `keep`.
 template <typename Stage>
 __device__ __forceinline__ void bucket_place(const Stage &st, const Frames &fr, const Bkt &bk, int f, int j,
-                                             int64_t p0, int64_t total, bool keep,
+                                             int64_t p0, int64_t cap, int64_t total, bool keep,
                                              const typename Stage::Payload &pl, int64_t i, int64_t pos,
                                              int32_t b_tot,
                                              int32_t b_bef, int32_t *s_off, int32_t *s_scan,
@@ -303,7 +303,7 @@ __device__ __forceinline__ void bucket_place(const Stage &st, const Frames &fr, 
     // order, so the reads follow every OR of the wave and the zeroing every read. (Measured: a multisplit of
     // ballots over the range bits spent ~2.4 us of VALU here at config 3.)
     int32_t kk[2] = {0, 0};
-    const bool ok = total >= 2 && keep && st.bucket_keys(pl, kk[0], kk[1]);
+    const bool ok = total >= 2 && keep && pos >= 0 && st.bucket_keys(pl, kk[0], kk[1]);
     int32_t rank[2];
 #pragma unroll
     for (int K = 0; K < 2; ++K) {
@@ -337,7 +337,12 @@ __device__ __forceinline__ void bucket_place(const Stage &st, const Frames &fr, 
 #pragma unroll
     for (int K = 0; K < 2; ++K) {
         const int r = kk[K] / BK_KEYS;
-        const int64_t slot = (int64_t)K * bk.nnz_cap + p0 + s_off[K * BK_MAX_RANGES + r] + s_w[K][wid][r] + rank[K];
+        const int64_t at = (int64_t)s_off[K * BK_MAX_RANGES + r] + s_w[K][wid][r] + rank[K];  // in the frame
+        if (at < 0 || at >= cap) {  // half-written aggregates (a failed barrier): no stray write
+            if (fr.err) atomicOr(fr.err, SHPL_EBIT_BARRIER);
+            continue;
+        }
+        const int64_t slot = (int64_t)K * bk.nnz_cap + p0 + at;
         bk.words[slot] = ((uint32_t)(kk[K] % BK_KEYS) << 24) | (uint32_t)pos;
         bk.wsrc[slot] = row[K];
         bk.wval[slot] = v;
@@ -485,8 +490,13 @@ __device__ __forceinline__ void compact_phase(const Stage &st, const Frames &fr,
             tot += c;
         }
         const int64_t i = base + (int64_t)u * IDX_BLOCK + threadIdx.x;
-        if (keep[u]) st.emit(f, i, p0 + kept + before + lane_rank(m[u]), p0, pl[u]);
-        if constexpr (BKT) b_pos = kept + before + lane_rank(m[u]);
+        const int64_t slot = kept + before + lane_rank(m[u]);  // (entries of the frame before this one)
+        // every write the frame's aggregates address stays inside the frame's capacity: aggregates a failed
+        // barrier left half-written (SHPL_EBIT_BARRIER is set then) can make a wrong map, never a stray write
+        const bool in_cap = slot >= 0 && slot < cap_end - p0;
+        if (keep[u] && !in_cap && fr.err) atomicOr(fr.err, SHPL_EBIT_BARRIER);
+        if (keep[u] && in_cap) st.emit(f, i, p0 + slot, p0, pl[u]);
+        if constexpr (BKT) b_pos = in_cap ? slot : -1;
         kept += tot;
     }
     // sentinels of the unused capacity [p0 + total, cap_end), each chunk its own stretch
@@ -495,7 +505,7 @@ __device__ __forceinline__ void compact_phase(const Stage &st, const Frames &fr,
     SHPL_IDX1_STAMP(4);
     if constexpr (BKT) {  // (s_tb written before k_compact's first barrier; entries past nr[K] never)
         const bool live = (int)(threadIdx.x % BK_MAX_RANGES) < bk.nr[threadIdx.x / BK_MAX_RANGES];
-        bucket_place(st, fr, bk, f, j, p0, total, keep[0], pl[0], base + threadIdx.x, b_pos,
+        bucket_place(st, fr, bk, f, j, p0, cap_end - p0, total, keep[0], pl[0], base + threadIdx.x, b_pos,
                      live ? s_tb[threadIdx.x] : 0,
                      live ? s_tb[2 * BK_MAX_RANGES + threadIdx.x] : 0, s_off, s_scan, s_w, s_peer);
     }

@@ -812,7 +812,15 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
                                                  int32_t *ent_dst, int32_t *ent_src, float *ent_val,
                                                  int32_t *ent_col, int32_t *key_range, int2 *heads = nullptr,
                                                  int head_k = 0, const int32_t *wsrc = nullptr,
-                                                 const float *wval = nullptr) {
+                                                 const float *wval = nullptr, int64_t off_cap = 1 << 24,
+                                                 int64_t src_rows = 0) {
+    // a word (and, with wsrc, its source row) outside what the frame can hold -- buckets an index build left
+    // half-written when its frame barrier failed (it reported SHPL_EBIT_BARRIER) -- is left out, counted nowhere:
+    // the map is then wrong, but no entry points outside the frame or the source map
+    auto valid = [&](uint32_t w, int32_t src) {
+        return (int)(w >> 24) < nk && (int64_t)(w & 0xffffffu) < off_cap &&
+               (src_rows == 0 || (src >= 0 && (int64_t)src < src_rows));
+    };
     constexpr int NW = BLOCK / 64;
     __shared__ int32_t cnt[NW][RANGE_KEYS], s_tot[RANGE_KEYS], s_beg[RANGE_KEYS];
     __shared__ uint64_t s_peer[NW][RANGE_KEYS];  // per wave and destination: its batch's lanes (zero between uses)
@@ -836,7 +844,8 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
         for (int u = 0; u < 4; ++u) {  // (with wsrc / wval: every load of the word's entry in one round trip)
             const bool in = i0 + u * BLOCK < n;
             w[u] = in ? words[i0 + u * BLOCK] : 0u;
-            if (wsrc && staged) {
+            sr[u] = 0;
+            if (wsrc) {
                 sr[u] = in ? wsrc[i0 + u * BLOCK] : 0;
                 vl[u] = in ? wval[i0 + u * BLOCK] : 0.0f;
             }
@@ -845,7 +854,7 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
             if (!wsrc) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    if (i0 + u * BLOCK >= n) continue;
+                    if (i0 + u * BLOCK >= n || !valid(w[u], 0)) continue;
                     const int64_t e = e0 + (w[u] & 0xffffffu);
                     const int32_t kk = col ? col[e] : (int32_t)e;
                     vl[u] = vals[e];
@@ -864,7 +873,7 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int32_t i = i0 + u * BLOCK;
-            if (i < n) atomicAdd(&cnt[i / L][w[u] >> 24], 1);
+            if (i < n && valid(w[u], wsrc ? sr[u] : 0)) atomicAdd(&cnt[i / L][w[u] >> 24], 1);
         }
     }
     __syncthreads();
@@ -894,7 +903,7 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
     const int32_t s0 = wid * L, s1 = min(n, s0 + L);
     for (int32_t b0 = s0; b0 < s1; b0 += 64) {
         const int32_t i = b0 + lane;
-        const bool ok = i < s1;
+        bool ok = i < s1;
         uint32_t w = 0u;
         int32_t kk = 0, src = 0;
         float val = 0.0f;
@@ -911,13 +920,16 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
                 kk = col ? col[e0 + (w & 0xffffffu)] : (int32_t)(e0 + (w & 0xffffffu));
             } else {
                 w = words[i];
-                const int64_t e = e0 + (w & 0xffffffu);
-                kk = col ? col[e] : (int32_t)e;
-                val = vals[e];
-                src = direction == SHPL_BY_CELL ? pix[kk] : cell[e];
+                if (valid(w, 0)) {
+                    const int64_t e = e0 + (w & 0xffffffu);
+                    kk = col ? col[e] : (int32_t)e;
+                    val = vals[e];
+                    src = direction == SHPL_BY_CELL ? pix[kk] : cell[e];
+                }
             }
         }
-        const int t = (int)(w >> 24);
+        ok = ok && valid(w, wsrc ? src : 0);
+        const int t = ok ? (int)(w >> 24) : 0;
         // the batch's lanes of destination t: each ORs its bit into the wave's word of t, reads it back, and the
         // lanes zero it again (one wave's LDS operations run in order; 7 ballots over the destination bits cost
         // more VALU)
@@ -958,6 +970,7 @@ struct BsSide {
     int64_t blocks;    // n_frames * nr
     int2 *heads;       // optional run heads (shpl_csr.heads)
     int head_k;
+    int64_t src_rows;  // rows of the map this side's entries gather from (the other key's, all frames)
 };
 
 struct BsIn {
@@ -998,6 +1011,9 @@ __global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide 
         const int32_t *x = in.ext + (((int64_t)key * in.n_frames + f) * in.nrmax + q) * 2;
         start = x[0];
         n = x[1];
+        // a bucket outside the frame's entries (an index build whose frame barrier failed: it reported
+        // SHPL_EBIT_BARRIER) reads as empty -- a wrong map, never a stray access
+        if (start < 0 || n < 0 || (int64_t)start + n > nnz) start = n = 0;
         W = in.words + (int64_t)key * in.nnz_cap + p0 + start;
         WS = in.wsrc + (int64_t)key * in.nnz_cap + p0 + start;
         WV = in.wval + (int64_t)key * in.nnz_cap + p0 + start;
@@ -1017,7 +1033,8 @@ __global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide 
     }
     const int64_t out0 = p0 + start;
     bucket_sort_emit<BS_BLOCK, BS_LCAP>(W, n, p0, out0, k0, nk, direction, nullptr, in.cell, in.pix, in.val, sd.ent_dst,
-                                        sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range, sd.heads, sd.head_k, WS, WV);
+                                        sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range, sd.heads, sd.head_k, WS, WV,
+                                        nnz, sd.src_rows);
     // the frame's unused capacity (its last range), the slots and key ranges after the last frame
     if (q != sd.nr - 1) return;
     for (int64_t h = p0 + valid + threadIdx.x; h < cap_end; h += BS_BLOCK) sd.ent_dst[h] = -1;
@@ -1261,7 +1278,8 @@ extern "C" int shpl_build_csr_buckets(const shpl_buckets *bk, const shpl_csr *by
         if (k == 1 && !c->ent_col && !(c->flags & SHPL_CSR_IDENTITY_COLS)) return SHPL_ERR_ARG;
         if (c->heads && (c->head_k < 1 || c->head_k > SHPL_CSR_MAX_HEAD || !c->key_range)) return SHPL_ERR_ARG;
         s[k] = BsSide{l.nr[k], l.kpf[k], c->n_keys, c->nnz_cap, c->ent_dst, c->ent_src, c->ent_val, c->ent_col,
-                      c->key_range, (int64_t)bk->n_frames * l.nr[k], (int2 *)c->heads, (int)c->head_k};
+                      c->key_range, (int64_t)bk->n_frames * l.nr[k], (int2 *)c->heads, (int)c->head_k,
+                      (int64_t)bk->n_frames * l.kpf[1 - k]};
         if (l.nr[k] == 0) s[k].blocks = 0;
     }
     hipStream_t st = (hipStream_t)stream;
