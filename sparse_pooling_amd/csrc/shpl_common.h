@@ -149,9 +149,6 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 //   hist  [2][F][n_chunks][nrmax] i32  entries per (index chunk, range)
 //   ext   [2][F][nrmax][2]        i32  bucket (start from the frame's first slot, entries)
 //   words [2][nnz_cap]            u32  the buckets, frame f's at [off[f], off[f] + nnz_f)
-//   wsrc  [2][nnz_cap]            i32  beside each word: the entry's source row for that key's pull (the pixel
-//                                        for a cell bucket, the cell for a pixel bucket) ...
-//   wval  [2][nnz_cap]            f32  ... and its value: the bucket sort reads them with the word, no gather
 constexpr int BK_KEYS = 128;        // destinations per range
 constexpr int BK_MAX_RANGES = 512;  // ranges per frame (65536 destinations)
 constexpr int BK_RBITS = 9;         // range bits matched by the placement's multisplit
@@ -159,7 +156,7 @@ constexpr int BK_RBITS = 9;         // range bits matched by the placement's mul
 struct BkLayout {
     int n_frames, n_chunks, nr[2], nrmax;
     int64_t nnz_cap, kpf[2];
-    size_t bar, hist, ext, words, wsrc, wval, bytes;  // byte offsets into the workspace, total
+    size_t bar, hist, ext, words, bytes;  // byte offsets into the workspace, total
 };
 
 inline BkLayout bk_layout(int n_frames, int n_chunks, int64_t nnz_cap, int64_t cells_per_frame,
@@ -182,10 +179,6 @@ inline BkLayout bk_layout(int n_frames, int n_chunks, int64_t nnz_cap, int64_t c
     l.ext = o;
     o = align_up(o + 4 * 2 * F * (size_t)l.nrmax * 2, 256);
     l.words = o;
-    o = align_up(o + 4 * 2 * cap, 256);
-    l.wsrc = o;
-    o = align_up(o + 4 * 2 * cap, 256);
-    l.wval = o;
     o = align_up(o + 4 * 2 * cap, 256);
     l.bytes = o;
     return l;

@@ -77,8 +77,6 @@ struct Bkt {
     int32_t *hist;    // [2][F][n_chunks][nrmax]
     int32_t *ext;     // [2][F][nrmax][2]
     uint32_t *words;  // [2][nnz_cap]
-    int32_t *wsrc;    // [2][nnz_cap] beside each word: the entry's source row for that key's pull
-    float *wval;      // [2][nnz_cap] beside each word: the entry's value
     PassCopy cp[2];
     int cp_at[2];     // the launch each copy rides: 0 = k_count, 1 = k_compact
     int cp_blocks;    // rider workgroups per frame in each launch (0: none)
@@ -275,8 +273,7 @@ __global__ __launch_bounds__(IDX_BLOCK) void k_count(Stage st, Frames fr, Bkt bk
 template <typename Stage>
 __device__ __forceinline__ void bucket_place(const Stage &st, const Frames &fr, const Bkt &bk, int f, int j,
                                              int64_t p0, int64_t cap, int64_t total, bool keep,
-                                             const typename Stage::Payload &pl, int64_t i, int64_t pos,
-                                             int32_t b_tot,
+                                             const typename Stage::Payload &pl, int64_t pos, int32_t b_tot,
                                              int32_t b_bef, int32_t *s_off, int32_t *s_scan,
                                              int16_t (*s_w)[IDX_BLOCK / 64][BK_MAX_RANGES],
                                              uint64_t (*s_peer)[BK_MAX_RANGES]) {
@@ -331,9 +328,6 @@ __device__ __forceinline__ void bucket_place(const Stage &st, const Frames &fr, 
     lds_barrier();
     SHPL_IDX1_STAMP(6);
     if (!ok) return;
-    int32_t row[2];
-    st.bucket_rows(f, kk[0], kk[1], row[0], row[1]);
-    const float v = st.bucket_val(i);
 #pragma unroll
     for (int K = 0; K < 2; ++K) {
         const int r = kk[K] / BK_KEYS;
@@ -344,8 +338,6 @@ __device__ __forceinline__ void bucket_place(const Stage &st, const Frames &fr, 
         }
         const int64_t slot = (int64_t)K * bk.nnz_cap + p0 + at;
         bk.words[slot] = ((uint32_t)(kk[K] % BK_KEYS) << 24) | (uint32_t)pos;
-        bk.wsrc[slot] = row[K];
-        bk.wval[slot] = v;
     }
 }
 
@@ -505,7 +497,7 @@ __device__ __forceinline__ void compact_phase(const Stage &st, const Frames &fr,
     SHPL_IDX1_STAMP(4);
     if constexpr (BKT) {  // (s_tb written before k_compact's first barrier; entries past nr[K] never)
         const bool live = (int)(threadIdx.x % BK_MAX_RANGES) < bk.nr[threadIdx.x / BK_MAX_RANGES];
-        bucket_place(st, fr, bk, f, j, p0, cap_end - p0, total, keep[0], pl[0], base + threadIdx.x, b_pos,
+        bucket_place(st, fr, bk, f, j, p0, cap_end - p0, total, keep[0], pl[0], b_pos,
                      live ? s_tb[threadIdx.x] : 0,
                      live ? s_tb[2 * BK_MAX_RANGES + threadIdx.x] : 0, s_off, s_scan, s_w, s_peer);
     }

@@ -811,12 +811,10 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
                                                  const int32_t *cell, const int32_t *pix, const float *vals,
                                                  int32_t *ent_dst, int32_t *ent_src, float *ent_val,
                                                  int32_t *ent_col, int32_t *key_range, int2 *heads = nullptr,
-                                                 int head_k = 0, const int32_t *wsrc = nullptr,
-                                                 const float *wval = nullptr, int64_t off_cap = 1 << 24,
-                                                 int64_t src_rows = 0) {
-    // a word (and, with wsrc, its source row) outside what the frame can hold -- buckets an index build left
-    // half-written when its frame barrier failed (it reported SHPL_EBIT_BARRIER) -- is left out, counted nowhere:
-    // the map is then wrong, but no entry points outside the frame or the source map
+                                                 int head_k = 0, int64_t off_cap = 1 << 24, int64_t src_rows = 0) {
+    // a word outside what the frame holds, or one whose source row is outside the source map -- buckets an index
+    // build left half-written when its frame barrier failed (it reported SHPL_EBIT_BARRIER) -- is left out,
+    // counted nowhere: the map is then wrong, but no entry points outside the frame or the source map
     auto valid = [&](uint32_t w, int32_t src) {
         return (int)(w >> 24) < nk && (int64_t)(w & 0xffffffu) < off_cap &&
                (src_rows == 0 || (src >= 0 && (int64_t)src < src_rows));
@@ -841,26 +839,20 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
         int32_t sr[4];
         float vl[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {  // (with wsrc / wval: every load of the word's entry in one round trip)
-            const bool in = i0 + u * BLOCK < n;
-            w[u] = in ? words[i0 + u * BLOCK] : 0u;
-            sr[u] = 0;
-            if (wsrc) {
-                sr[u] = in ? wsrc[i0 + u * BLOCK] : 0;
-                vl[u] = in ? wval[i0 + u * BLOCK] : 0.0f;
-            }
+        for (int u = 0; u < 4; ++u) {
+            w[u] = i0 + u * BLOCK < n ? words[i0 + u * BLOCK] : 0u;
+            sr[u] = -1;
+        }
+        // every word's source (staged or not: the counts check it as the placement will)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (i0 + u * BLOCK >= n || !valid(w[u], 0)) continue;
+            const int64_t e = e0 + (w[u] & 0xffffffu);
+            const int32_t kk = col ? col[e] : (int32_t)e;
+            if (staged) vl[u] = vals[e];
+            sr[u] = direction == SHPL_BY_CELL ? pix[kk] : cell[e];
         }
         if (staged) {
-            if (!wsrc) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    if (i0 + u * BLOCK >= n || !valid(w[u], 0)) continue;
-                    const int64_t e = e0 + (w[u] & 0xffffffu);
-                    const int32_t kk = col ? col[e] : (int32_t)e;
-                    vl[u] = vals[e];
-                    sr[u] = direction == SHPL_BY_CELL ? pix[kk] : cell[e];
-                }
-            }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int32_t i = i0 + u * BLOCK;
@@ -873,7 +865,7 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int32_t i = i0 + u * BLOCK;
-            if (i < n && valid(w[u], wsrc ? sr[u] : 0)) atomicAdd(&cnt[i / L][w[u] >> 24], 1);
+            if (i < n && valid(w[u], sr[u])) atomicAdd(&cnt[i / L][w[u] >> 24], 1);
         }
     }
     __syncthreads();
@@ -913,11 +905,6 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
                 src = l_s[i];
                 val = l_v[i];
                 if (ent_col) kk = col ? col[e0 + (w & 0xffffffu)] : (int32_t)(e0 + (w & 0xffffffu));
-            } else if (wsrc) {
-                w = words[i];
-                src = wsrc[i];
-                val = wval[i];
-                kk = col ? col[e0 + (w & 0xffffffu)] : (int32_t)(e0 + (w & 0xffffffu));
             } else {
                 w = words[i];
                 if (valid(w, 0)) {
@@ -928,7 +915,7 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
                 }
             }
         }
-        ok = ok && valid(w, wsrc ? src : 0);
+        ok = ok && valid(w, src);
         const int t = ok ? (int)(w >> 24) : 0;
         // the batch's lanes of destination t: each ORs its bit into the wave's word of t, reads it back, and the
         // lanes zero it again (one wave's LDS operations run in order; 7 ballots over the destination bits cost
@@ -979,8 +966,6 @@ struct BsIn {
     const float *val;
     const int32_t *ext;
     const uint32_t *words;
-    const int32_t *wsrc;  // beside each word: the entry's source row and value (shpl_common.h BkLayout)
-    const float *wval;
     int n_frames, nrmax;
     int64_t nnz_cap;
 };
@@ -1005,8 +990,6 @@ __global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide 
     const int direction = key ? SHPL_BY_PIXEL : SHPL_BY_CELL;
     int32_t start = 0, n = 0, valid = 0;
     const uint32_t *W = one;
-    const int32_t *WS = nullptr;  // the words' source rows and values (no bucket: the index arrays, read there)
-    const float *WV = nullptr;
     if (nnz >= 2) {
         const int32_t *x = in.ext + (((int64_t)key * in.n_frames + f) * in.nrmax + q) * 2;
         start = x[0];
@@ -1015,8 +998,6 @@ __global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide 
         // SHPL_EBIT_BARRIER) reads as empty -- a wrong map, never a stray access
         if (start < 0 || n < 0 || (int64_t)start + n > nnz) start = n = 0;
         W = in.words + (int64_t)key * in.nnz_cap + p0 + start;
-        WS = in.wsrc + (int64_t)key * in.nnz_cap + p0 + start;
-        WV = in.wval + (int64_t)key * in.nnz_cap + p0 + start;
         if (q == sd.nr - 1) valid = start + n;  // the frame's entries with valid destinations
     } else if (nnz == 1) {
         // no bucket: the frame's one entry, in this range or not
@@ -1033,8 +1014,8 @@ __global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide 
     }
     const int64_t out0 = p0 + start;
     bucket_sort_emit<BS_BLOCK, BS_LCAP>(W, n, p0, out0, k0, nk, direction, nullptr, in.cell, in.pix, in.val, sd.ent_dst,
-                                        sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range, sd.heads, sd.head_k, WS, WV,
-                                        nnz, sd.src_rows);
+                                        sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range, sd.heads, sd.head_k, nnz,
+                                        sd.src_rows);
     // the frame's unused capacity (its last range), the slots and key ranges after the last frame
     if (q != sd.nr - 1) return;
     for (int64_t h = p0 + valid + threadIdx.x; h < cap_end; h += BS_BLOCK) sd.ent_dst[h] = -1;
@@ -1296,8 +1277,7 @@ extern "C" int shpl_build_csr_buckets(const shpl_buckets *bk, const shpl_csr *by
     if (blocks > 0x7fffffffLL) return SHPL_ERR_BAD_SHAPE;
     char *w = (char *)bk->ws;
     const BsIn in{bk->frame_off, bk->frame_nnz, bk->cell, bk->pix, bk->val, (const int32_t *)(w + l.ext),
-                  (const uint32_t *)(w + l.words), (const int32_t *)(w + l.wsrc), (const float *)(w + l.wval),
-                  bk->n_frames, l.nrmax, bk->nnz_cap};
+                  (const uint32_t *)(w + l.words), bk->n_frames, l.nrmax, bk->nnz_cap};
     hipLaunchKernelGGL(k_bsort2, dim3((unsigned)blocks), dim3(BS_BLOCK), 0, st, in, s[0], s[1]);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;

@@ -183,13 +183,6 @@ struct FusedStage {
         pix[pos] = -1;
         val[pos] = 0.0f;
     }
-    // the global source rows of a bucketed entry (frame-local cell kc, pixel kp): the pixel for its cell
-    // bucket's pull, the cell for its pixel bucket's (what emit() writes into pix / cell)
-    __device__ void bucket_rows(int f, int32_t kc, int32_t kp, int32_t &row_cell, int32_t &row_pix) const {
-        row_cell = (int32_t)(f * g.n_pix + kp);
-        row_pix = (int32_t)(f * g.n_cells + kc);
-    }
-    __device__ float bucket_val(int64_t i) const { return mval ? mval[i] : 1.0f; }
     // frame-local destinations of a kept entry (buckets): the cell and pixel emit() writes, unless -1
     __device__ bool bucket_keys(const Payload &pl, int32_t &kc, int32_t &kp) const {
         const int64_t r = pl.pr.r, vi = (int64_t)pl.pr.v, ui = (int64_t)pl.pr.u;
@@ -415,8 +408,8 @@ extern "C" int shpl_build_index_buckets(int n_frames, const int64_t *d_point_off
 #define SHPL_RIDERS 0
 #endif
     Bkt bk{{l.nr[0], l.nr[1]}, l.nrmax, nnz_cap, (int32_t *)(b + l.hist), (int32_t *)(b + l.ext),
-           (uint32_t *)(b + l.words), (int32_t *)(b + l.wsrc), (float *)(b + l.wval), {},
-           {SHPL_RIDERS == 2 ? 1 : 0, SHPL_RIDERS == 1 ? 0 : 1}, 0, (int32_t *)(b + l.bar)};
+           (uint32_t *)(b + l.words), {}, {SHPL_RIDERS == 2 ? 1 : 0, SHPL_RIDERS == 1 ? 0 : 1}, 0,
+           (int32_t *)(b + l.bar)};
     const shpl_pass_copy *cps[2] = {cell_copy, pixel_copy};
     int64_t copy_bytes = 0;
     for (int k = 0; k < 2; ++k) {
