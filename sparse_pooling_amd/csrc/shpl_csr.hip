@@ -812,12 +812,12 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
                                                  int32_t *ent_dst, int32_t *ent_src, float *ent_val,
                                                  int32_t *ent_col, int32_t *key_range, int2 *heads = nullptr,
                                                  int head_k = 0, int64_t off_cap = 1 << 24, int64_t src_rows = 0) {
-    // a word outside what the frame holds, or one whose source row is outside the source map -- buckets an index
-    // build left half-written when its frame barrier failed (it reported SHPL_EBIT_BARRIER) -- is left out,
-    // counted nowhere: the map is then wrong, but no entry points outside the frame or the source map
-    auto valid = [&](uint32_t w, int32_t src) {
-        return (int)(w >> 24) < nk && (int64_t)(w & 0xffffffu) < off_cap &&
-               (src_rows == 0 || (src >= 0 && (int64_t)src < src_rows));
+    // a word outside what the frame holds -- buckets an index build left half-written when its frame barrier
+    // failed (it reported SHPL_EBIT_BARRIER) -- is left out, counted nowhere, and a source row outside the source
+    // map is emitted as row 0: the map is then wrong, but no entry points outside the frame or the source map
+    auto valid = [&](uint32_t w) { return (int)(w >> 24) < nk && (int64_t)(w & 0xffffffu) < off_cap; };
+    auto clamp_src = [&](int32_t src) {
+        return (src_rows == 0 || (src >= 0 && (int64_t)src < src_rows)) ? src : 0;
     };
     constexpr int NW = BLOCK / 64;
     __shared__ int32_t cnt[NW][RANGE_KEYS], s_tot[RANGE_KEYS], s_beg[RANGE_KEYS];
@@ -839,20 +839,16 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
         int32_t sr[4];
         float vl[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            w[u] = i0 + u * BLOCK < n ? words[i0 + u * BLOCK] : 0u;
-            sr[u] = -1;
-        }
-        // every word's source (staged or not: the counts check it as the placement will)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (i0 + u * BLOCK >= n || !valid(w[u], 0)) continue;
-            const int64_t e = e0 + (w[u] & 0xffffffu);
-            const int32_t kk = col ? col[e] : (int32_t)e;
-            if (staged) vl[u] = vals[e];
-            sr[u] = direction == SHPL_BY_CELL ? pix[kk] : cell[e];
-        }
+        for (int u = 0; u < 4; ++u) w[u] = i0 + u * BLOCK < n ? words[i0 + u * BLOCK] : 0u;
         if (staged) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (i0 + u * BLOCK >= n || !valid(w[u])) continue;
+                const int64_t e = e0 + (w[u] & 0xffffffu);
+                const int32_t kk = col ? col[e] : (int32_t)e;
+                vl[u] = vals[e];
+                sr[u] = direction == SHPL_BY_CELL ? pix[kk] : cell[e];
+            }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int32_t i = i0 + u * BLOCK;
@@ -865,7 +861,7 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int32_t i = i0 + u * BLOCK;
-            if (i < n && valid(w[u], sr[u])) atomicAdd(&cnt[i / L][w[u] >> 24], 1);
+            if (i < n && valid(w[u])) atomicAdd(&cnt[i / L][w[u] >> 24], 1);
         }
     }
     __syncthreads();
@@ -907,7 +903,7 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
                 if (ent_col) kk = col ? col[e0 + (w & 0xffffffu)] : (int32_t)(e0 + (w & 0xffffffu));
             } else {
                 w = words[i];
-                if (valid(w, 0)) {
+                if (valid(w)) {
                     const int64_t e = e0 + (w & 0xffffffu);
                     kk = col ? col[e] : (int32_t)e;
                     val = vals[e];
@@ -915,7 +911,8 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
                 }
             }
         }
-        ok = ok && valid(w, src);
+        ok = ok && valid(w);
+        src = clamp_src(src);
         const int t = ok ? (int)(w >> 24) : 0;
         // the batch's lanes of destination t: each ORs its bit into the wave's word of t, reads it back, and the
         // lanes zero it again (one wave's LDS operations run in order; 7 ballots over the destination bits cost
