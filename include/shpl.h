@@ -429,7 +429,8 @@ int shpl_pull_once(int direction, int dtype, const shpl_csr *csr, const void *d_
  * per frame, max_points_per_frame below 2^24.
  * Frames of at most 32 chunks of 1024 points run both passes in ONE launch
  * (k_index1: a frame barrier between them inside the launch) when every chunk
- * workgroup of the batch fits on the GPU at once (else the two-launch form);
+ * workgroup of the batch fits on the GPU at once and d_err is given (else the
+ * two-launch form);
  * its barrier words live at the start of d_bkt, which must be ZEROED before
  * its first use (shpl_bucket_workspace_reset, or a memset of the whole
  * workspace) -- every call leaves them zero. SHPL_EBIT_BARRIER in *d_err: a
@@ -478,6 +479,9 @@ typedef struct {
     const float *val;                     /* [nnz_cap] */
     void *ws;                             /* the bucket workspace */
     size_t ws_bytes;
+    const uint32_t *err;                  /* the index call's d_err: after a SHPL_EBIT_BARRIER (or with NULL) the
+                                           * bucket sort checks every bucket word, so a failed barrier's
+                                           * half-written buckets never address outside the frame */
 } shpl_buckets;
 
 /* One pull of shpl_pull_pair: the arguments of shpl_pull after its csr. */

@@ -96,7 +96,7 @@ class ShplBuckets(ctypes.Structure):
                 ("cells_per_frame", ctypes.c_int64), ("pix_per_frame", ctypes.c_int64),
                 ("frame_off", ctypes.c_void_p), ("frame_nnz", ctypes.c_void_p), ("cell", ctypes.c_void_p),
                 ("pix", ctypes.c_void_p), ("val", ctypes.c_void_p), ("ws", ctypes.c_void_p),
-                ("ws_bytes", ctypes.c_size_t)]
+                ("ws_bytes", ctypes.c_size_t), ("err", ctypes.c_void_p)]
 
 
 class ShplPullDesc(ctypes.Structure):

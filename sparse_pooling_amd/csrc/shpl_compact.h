@@ -664,7 +664,8 @@ int run_compaction(const Stage &st, int n_frames, int64_t max_points, const int6
 #ifndef SHPL_IDX1_RIDERS
 #define SHPL_IDX1_RIDERS 240
 #endif
-            if (SHPL_INDEX1 && bk->bar && fr.n_chunks <= IDX1_MAX_CHUNKS &&
+            // (an error word is needed to report a failed barrier: without one, the two launches)
+            if (SHPL_INDEX1 && bk->bar && err && fr.n_chunks <= IDX1_MAX_CHUNKS &&
                 (int64_t)n_frames * fr.n_chunks <= index1_resident<Stage>()) {
                 // rider workgroups per copy and frame: SHPL_IDX1_RIDERS per copy over the batch, at most one per
                 // 64 KiB of a frame's copy (the two-launch form's cp_blocks bound)

@@ -805,7 +805,7 @@ static_assert(BK_KEYS == RANGE_KEYS, "the index builder's buckets are the sort's
 // destination bits rank a word among its batch's equals, one lane per destination moves the slice's
 // cursor) -- three block barriers whatever the bucket's size. Buckets of at most LCAP words are read
 // into LDS first together with their entries' source rows and values (every load in flight at once).
-template <int BLOCK, int LCAP>
+template <int BLOCK, int LCAP, bool CHECKS = false>
 __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t n, int64_t e0, int64_t out0,
                                                  int64_t k0, int nk, int direction, const int32_t *col,
                                                  const int32_t *cell, const int32_t *pix, const float *vals,
@@ -815,9 +815,13 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
     // a word outside what the frame holds -- buckets an index build left half-written when its frame barrier
     // failed (it reported SHPL_EBIT_BARRIER) -- is left out, counted nowhere, and a source row outside the source
     // map is emitted as row 0: the map is then wrong, but no entry points outside the frame or the source map
-    auto valid = [&](uint32_t w) { return (int)(w >> 24) < nk && (int64_t)(w & 0xffffffu) < off_cap; };
+    // (CHECKS: the instantiation k_bsort2 runs after an index build that reported SHPL_EBIT_BARRIER; the checks
+    // cost the fast path ~2 us of its 10.6, so it does without them)
+    auto valid = [&](uint32_t w) {
+        return !CHECKS || ((int)(w >> 24) < nk && (int64_t)(w & 0xffffffu) < off_cap);
+    };
     auto clamp_src = [&](int32_t src) {
-        return (src_rows == 0 || (src >= 0 && (int64_t)src < src_rows)) ? src : 0;
+        return (!CHECKS || src_rows == 0 || (src >= 0 && (int64_t)src < src_rows)) ? src : 0;
     };
     constexpr int NW = BLOCK / 64;
     __shared__ int32_t cnt[NW][RANGE_KEYS], s_tot[RANGE_KEYS], s_beg[RANGE_KEYS];
@@ -963,6 +967,7 @@ struct BsIn {
     const float *val;
     const int32_t *ext;
     const uint32_t *words;
+    const uint32_t *err;  // the index build's error word (shpl_buckets.err; NULL: treated as failed)
     int n_frames, nrmax;
     int64_t nnz_cap;
 };
@@ -1010,9 +1015,15 @@ __global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide 
         __syncthreads();
     }
     const int64_t out0 = p0 + start;
-    bucket_sort_emit<BS_BLOCK, BS_LCAP>(W, n, p0, out0, k0, nk, direction, nullptr, in.cell, in.pix, in.val, sd.ent_dst,
-                                        sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range, sd.heads, sd.head_k, nnz,
-                                        sd.src_rows);
+    // the index build's barrier failed (or its caller gave no error word): every word and source checked
+    if (!in.err || (*in.err & SHPL_EBIT_BARRIER))
+        bucket_sort_emit<BS_BLOCK, BS_LCAP, true>(W, n, p0, out0, k0, nk, direction, nullptr, in.cell, in.pix, in.val,
+                                                  sd.ent_dst, sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range, sd.heads,
+                                                  sd.head_k, nnz, sd.src_rows);
+    else
+        bucket_sort_emit<BS_BLOCK, BS_LCAP, false>(W, n, p0, out0, k0, nk, direction, nullptr, in.cell, in.pix,
+                                                   in.val, sd.ent_dst, sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range,
+                                                   sd.heads, sd.head_k, nnz, sd.src_rows);
     // the frame's unused capacity (its last range), the slots and key ranges after the last frame
     if (q != sd.nr - 1) return;
     for (int64_t h = p0 + valid + threadIdx.x; h < cap_end; h += BS_BLOCK) sd.ent_dst[h] = -1;
@@ -1274,7 +1285,7 @@ extern "C" int shpl_build_csr_buckets(const shpl_buckets *bk, const shpl_csr *by
     if (blocks > 0x7fffffffLL) return SHPL_ERR_BAD_SHAPE;
     char *w = (char *)bk->ws;
     const BsIn in{bk->frame_off, bk->frame_nnz, bk->cell, bk->pix, bk->val, (const int32_t *)(w + l.ext),
-                  (const uint32_t *)(w + l.words), bk->n_frames, l.nrmax, bk->nnz_cap};
+                  (const uint32_t *)(w + l.words), bk->err, bk->n_frames, l.nrmax, bk->nnz_cap};
     hipLaunchKernelGGL(k_bsort2, dim3((unsigned)blocks), dim3(BS_BLOCK), 0, st, in, s[0], s[1]);
     SHPL_LAUNCH_CHECK();
     return SHPL_OK;

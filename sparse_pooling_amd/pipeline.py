@@ -110,7 +110,7 @@ class FusedPipeline:
             self.bkt = L.ShplBuckets(self.B, self.max_points, self.N, self.Hb * self.Wb, self.Hi * self.Wi,
                                      self.frame_off.data_ptr(), self.frame_nnz.data_ptr(), self.cell.data_ptr(),
                                      self.pix.data_ptr(), self.val.data_ptr(), self.bkt_ws.data_ptr(),
-                                     self.bkt_ws.numel())
+                                     self.bkt_ws.numel(), self.err.data_ptr())
 
     # ------------------------------------------------------------------ steps
     def build_index(self, points, voxels, point_offsets, P, mval=None, point_counts=None, pass_copies=None):
