@@ -479,9 +479,11 @@ typedef struct {
     const float *val;                     /* [nnz_cap] */
     void *ws;                             /* the bucket workspace */
     size_t ws_bytes;
-    const uint32_t *err;                  /* the index call's d_err: after a SHPL_EBIT_BARRIER (or with NULL) the
-                                           * bucket sort checks every bucket word, so a failed barrier's
-                                           * half-written buckets never address outside the frame */
+    const uint32_t *err;                  /* the index call's d_err (NULL if it had none): after a
+                                           * SHPL_EBIT_BARRIER the bucket sort reads every bucket as empty, so a
+                                           * failed barrier's half-written buckets never address anything; the bit
+                                           * stays until the caller clears the word (its maps stay empty until
+                                           * then: FusedPipeline.check() clears it and resets the barrier words) */
 } shpl_buckets;
 
 /* One pull of shpl_pull_pair: the arguments of shpl_pull after its csr. */

@@ -13,4 +13,4 @@ timeout -k 10 500 python -u -m pytest -x -q --timeout 300 --timeout-method threa
   tests/test_gpu_parity.py -k "index or golden or test_pipeline_backward_matches_oracle or ragged or kitti or mv3d or window or barrier" \
   tests/test_gpu_checksums_oracle.py > gpurun_out/r06_div_tests.log 2>&1
 rc=$?; tail -1 gpurun_out/r06_div_tests.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/r06_div_tests.log | head; exit $rc; }
-bash scripts/ab_kernels.sh r06_div4 "--config 3 --steps 200" "k_index1|k_bsort2" r5idx=$A now=$N r5idxb=$A nowb=$N
+bash scripts/ab_kernels.sh r06_div5 "--config 3 --steps 200" "k_index1|k_bsort2" r5idx=$A now=$N r5idxb=$A nowb=$N

@@ -805,24 +805,13 @@ static_assert(BK_KEYS == RANGE_KEYS, "the index builder's buckets are the sort's
 // destination bits rank a word among its batch's equals, one lane per destination moves the slice's
 // cursor) -- three block barriers whatever the bucket's size. Buckets of at most LCAP words are read
 // into LDS first together with their entries' source rows and values (every load in flight at once).
-template <int BLOCK, int LCAP, bool CHECKS = false>
+template <int BLOCK, int LCAP>
 __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t n, int64_t e0, int64_t out0,
                                                  int64_t k0, int nk, int direction, const int32_t *col,
                                                  const int32_t *cell, const int32_t *pix, const float *vals,
                                                  int32_t *ent_dst, int32_t *ent_src, float *ent_val,
                                                  int32_t *ent_col, int32_t *key_range, int2 *heads = nullptr,
-                                                 int head_k = 0, int64_t off_cap = 1 << 24, int64_t src_rows = 0) {
-    // a word outside what the frame holds -- buckets an index build left half-written when its frame barrier
-    // failed (it reported SHPL_EBIT_BARRIER) -- is left out, counted nowhere, and a source row outside the source
-    // map is emitted as row 0: the map is then wrong, but no entry points outside the frame or the source map
-    // (CHECKS: the instantiation k_bsort2 runs after an index build that reported SHPL_EBIT_BARRIER; the checks
-    // cost the fast path ~2 us of its 10.6, so it does without them)
-    auto valid = [&](uint32_t w) {
-        return !CHECKS || ((int)(w >> 24) < nk && (int64_t)(w & 0xffffffu) < off_cap);
-    };
-    auto clamp_src = [&](int32_t src) {
-        return (!CHECKS || src_rows == 0 || (src >= 0 && (int64_t)src < src_rows)) ? src : 0;
-    };
+                                                 int head_k = 0) {
     constexpr int NW = BLOCK / 64;
     __shared__ int32_t cnt[NW][RANGE_KEYS], s_tot[RANGE_KEYS], s_beg[RANGE_KEYS];
     __shared__ uint64_t s_peer[NW][RANGE_KEYS];  // per wave and destination: its batch's lanes (zero between uses)
@@ -840,14 +829,14 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
     // 1. per-slice counts (and, staged, the words with their sources and values into LDS)
     for (int32_t i0 = threadIdx.x; i0 < n; i0 += 4 * BLOCK) {  // 4 words per thread in flight
         uint32_t w[4];
-        int32_t sr[4];
-        float vl[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) w[u] = i0 + u * BLOCK < n ? words[i0 + u * BLOCK] : 0u;
         if (staged) {
+            int32_t sr[4];
+            float vl[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                if (i0 + u * BLOCK >= n || !valid(w[u])) continue;
+                if (i0 + u * BLOCK >= n) continue;
                 const int64_t e = e0 + (w[u] & 0xffffffu);
                 const int32_t kk = col ? col[e] : (int32_t)e;
                 vl[u] = vals[e];
@@ -865,7 +854,7 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int32_t i = i0 + u * BLOCK;
-            if (i < n && valid(w[u])) atomicAdd(&cnt[i / L][w[u] >> 24], 1);
+            if (i < n) atomicAdd(&cnt[i / L][w[u] >> 24], 1);
         }
     }
     __syncthreads();
@@ -895,7 +884,7 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
     const int32_t s0 = wid * L, s1 = min(n, s0 + L);
     for (int32_t b0 = s0; b0 < s1; b0 += 64) {
         const int32_t i = b0 + lane;
-        bool ok = i < s1;
+        const bool ok = i < s1;
         uint32_t w = 0u;
         int32_t kk = 0, src = 0;
         float val = 0.0f;
@@ -907,17 +896,13 @@ __device__ __forceinline__ void bucket_sort_emit(const uint32_t *words, int32_t 
                 if (ent_col) kk = col ? col[e0 + (w & 0xffffffu)] : (int32_t)(e0 + (w & 0xffffffu));
             } else {
                 w = words[i];
-                if (valid(w)) {
-                    const int64_t e = e0 + (w & 0xffffffu);
-                    kk = col ? col[e] : (int32_t)e;
-                    val = vals[e];
-                    src = direction == SHPL_BY_CELL ? pix[kk] : cell[e];
-                }
+                const int64_t e = e0 + (w & 0xffffffu);
+                kk = col ? col[e] : (int32_t)e;
+                val = vals[e];
+                src = direction == SHPL_BY_CELL ? pix[kk] : cell[e];
             }
         }
-        ok = ok && valid(w);
-        src = clamp_src(src);
-        const int t = ok ? (int)(w >> 24) : 0;
+        const int t = (int)(w >> 24);
         // the batch's lanes of destination t: each ORs its bit into the wave's word of t, reads it back, and the
         // lanes zero it again (one wave's LDS operations run in order; 7 ballots over the destination bits cost
         // more VALU)
@@ -958,7 +943,6 @@ struct BsSide {
     int64_t blocks;    // n_frames * nr
     int2 *heads;       // optional run heads (shpl_csr.heads)
     int head_k;
-    int64_t src_rows;  // rows of the map this side's entries gather from (the other key's, all frames)
 };
 
 struct BsIn {
@@ -967,7 +951,7 @@ struct BsIn {
     const float *val;
     const int32_t *ext;
     const uint32_t *words;
-    const uint32_t *err;  // the index build's error word (shpl_buckets.err; NULL: treated as failed)
+    const uint32_t *err;  // the index build's error word (shpl_buckets.err; NULL: no one-launch build, none failed)
     int n_frames, nrmax;
     int64_t nnz_cap;
 };
@@ -996,9 +980,11 @@ __global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide 
         const int32_t *x = in.ext + (((int64_t)key * in.n_frames + f) * in.nrmax + q) * 2;
         start = x[0];
         n = x[1];
-        // a bucket outside the frame's entries (an index build whose frame barrier failed: it reported
-        // SHPL_EBIT_BARRIER) reads as empty -- a wrong map, never a stray access
-        if (start < 0 || n < 0 || (int64_t)start + n > nnz) start = n = 0;
+        // after an index build whose frame barrier failed (it reported SHPL_EBIT_BARRIER; its buckets may be
+        // half-written) every bucket reads as empty, and so does one outside the frame's entries: a wrong map
+        // (the call is reported invalid), never a stray access; one scalar test, nothing per word
+        if ((in.err && (*in.err & SHPL_EBIT_BARRIER)) || start < 0 || n < 0 || (int64_t)start + n > nnz)
+            start = n = 0;
         W = in.words + (int64_t)key * in.nnz_cap + p0 + start;
         if (q == sd.nr - 1) valid = start + n;  // the frame's entries with valid destinations
     } else if (nnz == 1) {
@@ -1015,15 +1001,8 @@ __global__ __launch_bounds__(BS_BLOCK) void k_bsort2(BsIn in, BsSide s0, BsSide 
         __syncthreads();
     }
     const int64_t out0 = p0 + start;
-    // the index build's barrier failed (or its caller gave no error word): every word and source checked
-    if (!in.err || (*in.err & SHPL_EBIT_BARRIER))
-        bucket_sort_emit<BS_BLOCK, BS_LCAP, true>(W, n, p0, out0, k0, nk, direction, nullptr, in.cell, in.pix, in.val,
-                                                  sd.ent_dst, sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range, sd.heads,
-                                                  sd.head_k, nnz, sd.src_rows);
-    else
-        bucket_sort_emit<BS_BLOCK, BS_LCAP, false>(W, n, p0, out0, k0, nk, direction, nullptr, in.cell, in.pix,
-                                                   in.val, sd.ent_dst, sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range,
-                                                   sd.heads, sd.head_k, nnz, sd.src_rows);
+    bucket_sort_emit<BS_BLOCK, BS_LCAP>(W, n, p0, out0, k0, nk, direction, nullptr, in.cell, in.pix, in.val, sd.ent_dst,
+                                        sd.ent_src, sd.ent_val, sd.ent_col, sd.key_range, sd.heads, sd.head_k);
     // the frame's unused capacity (its last range), the slots and key ranges after the last frame
     if (q != sd.nr - 1) return;
     for (int64_t h = p0 + valid + threadIdx.x; h < cap_end; h += BS_BLOCK) sd.ent_dst[h] = -1;
@@ -1267,8 +1246,7 @@ extern "C" int shpl_build_csr_buckets(const shpl_buckets *bk, const shpl_csr *by
         if (k == 1 && !c->ent_col && !(c->flags & SHPL_CSR_IDENTITY_COLS)) return SHPL_ERR_ARG;
         if (c->heads && (c->head_k < 1 || c->head_k > SHPL_CSR_MAX_HEAD || !c->key_range)) return SHPL_ERR_ARG;
         s[k] = BsSide{l.nr[k], l.kpf[k], c->n_keys, c->nnz_cap, c->ent_dst, c->ent_src, c->ent_val, c->ent_col,
-                      c->key_range, (int64_t)bk->n_frames * l.nr[k], (int2 *)c->heads, (int)c->head_k,
-                      (int64_t)bk->n_frames * l.kpf[1 - k]};
+                      c->key_range, (int64_t)bk->n_frames * l.nr[k], (int2 *)c->heads, (int)c->head_k};
         if (l.nr[k] == 0) s[k].blocks = 0;
     }
     hipStream_t st = (hipStream_t)stream;
