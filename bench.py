@@ -134,6 +134,9 @@ def parse():
     ap.add_argument("--no-wgrad-reuse", action="store_true",
                     help="conv training (bf16): the weight gradient prepares its own pooled operand instead of "
                          "reading the forward's (shpl_conv3x3_wgrad_reuse; A/B)")
+    ap.add_argument("--no-dgrad-occ", action="store_true",
+                    help="conv training (bf16): the input gradient writes its pooled channels' map whole instead of "
+                         "at the occupied cells only (shpl_conv3x3_dgrad_reuse; A/B)")
     ap.add_argument("--wgrad-side", choices=["on", "off"], default=None,
                     help="conv training: the weight gradient on a side stream beside the input gradient "
                          "(FusionConv.WGRAD_SIDE; default: the class's)")
@@ -944,6 +947,7 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
     cb, ci = spec.c_bev, spec.c_img
     esz = 2 if dtype == torch.bfloat16 else 4
     conv.WGRAD_REUSE = not args.no_wgrad_reuse
+    conv.DGRAD_OCC = not args.no_dgrad_occ
     if args.wgrad_side is not None:
         conv.WGRAD_SIDE = args.wgrad_side == "on"
     if args.img_zero_side is not None:
@@ -995,13 +999,16 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
     px = F * Hb * Wb * esz
     if esz == 2:  # bf16: both convs gather the pooled rows (compact per-run buffer), bv_fused is never stored
         # per pixel, in channels: forward cb read (the pooled half is gathered: u_pix rows below) + ci written,
-        # BN apply 2 ci, BN backward 5 ci, input gradient ci read + (cb + ci) written, weight gradient cb + ci
-        # read (its pooled half again gathered); the image gradient's ci per image pixel written; the pooled
-        # rows' gathers (once per step with the weight gradient reading the forward's operand, else twice) and
-        # the image gradient's gathers of u_cell rows; the entries read by each of those passes
+        # BN apply 2 ci, BN backward 5 ci, input gradient ci read + (cb + ci) written (with DGRAD_OCC its pooled
+        # channels' ci only at the u_cell occupied cells), weight gradient cb + ci read (its pooled half again
+        # gathered); the image gradient's ci per image pixel written; the pooled rows' gathers (once per step
+        # with the weight gradient reading the forward's operand, else twice) and the image gradient's gathers
+        # of u_cell rows; the entries read by each of those passes
         n_pool = 1 if conv.WGRAD_REUSE else 2
-        hbm_bytes = (px * ((cb + ci) + 2 * ci + 5 * ci + (ci + (cb + ci)) + (cb + ci))
-                     + F * Hi * Wi * ci * esz + (n_pool * u_pix + u_cell) * ci * esz + (n_pool + 1) * 12 * nnz)
+        dgrad_occ = conv.WGRAD_REUSE and conv.DGRAD_OCC
+        hbm_bytes = (px * ((cb + ci) + 2 * ci + 5 * ci + (ci + cb + (0 if dgrad_occ else ci)) + (cb + ci))
+                     + F * Hi * Wi * ci * esz + (n_pool * u_pix + u_cell + (u_cell if dgrad_occ else 0)) * ci * esz
+                     + (n_pool + 1) * 12 * nnz)
     else:  # f32: the pooled map written once in the forward, read by the forward and the weight gradient
         hbm_bytes = (px * (ci + (cb + ci + ci) + 2 * ci + 2 * ci + 3 * ci + (ci + cb + ci) + (cb + ci + ci))
                      + F * Hi * Wi * ci * esz + (u_pix + u_cell) * ci * esz + 2 * 12 * nnz)
@@ -1026,7 +1033,8 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
                                     "the weight gradient, bv_fused never stored; f32: the pooled map built once in the "
                                     "forward, reused by the weight gradient), backward to bev, img, weights, beta"),
                        "global_batch": F * world, "frames_per_gpu_per_step": F, "hip_graph": False,
-                       "wgrad_reuse": conv.WGRAD_REUSE, "wgrad_side_stream": conv.WGRAD_SIDE,
+                       "wgrad_reuse": conv.WGRAD_REUSE, "dgrad_occ": esz == 2 and conv.WGRAD_REUSE and conv.DGRAD_OCC,
+                       "wgrad_side_stream": conv.WGRAD_SIDE,
                        "img_zero_side_stream": conv.IMG_ZERO_SIDE,
                        "bn_statistics": "per rank (no cross-rank sync)", "parallelism": f"frame-sharded x{world}"},
             "roofline": ({"bound": "hbm", "kernel": "the whole forward + backward step: algorithmic bytes of its passes "

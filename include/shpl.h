@@ -628,6 +628,23 @@ int shpl_conv3x3_dgrad(int dtype, int n_frames, int64_t h, int64_t w, const void
                        int64_t c_split, void *d_dx_b, int64_t dx_b_stride, void *d_ws, size_t ws_bytes,
                        void *stream);
 
+/* shpl_conv3x3_dgrad of the pooled bf16 fusion conv's two maps, d_dx_b (the pooled channels' gradient) written
+ * only at the cells the pool's CSR has entries for -- the rows a pixel-keyed pull of it back to the image reads
+ * (shpl_pull SHPL_BY_PIXEL); its other cells are left as they were. The occupancy comes from the forward
+ * shpl_conv3x3 call over the same map, frames and shape (A = c_split channels, B = c_dx - c_split pooled
+ * channels, c_gy outputs) that left it in d_fwd_ws (fwd_stats: whether that call took statistics), as
+ * shpl_conv3x3_wgrad_reuse reads it: valid only for a forward for which shpl_conv3x3_rows_form reported 1;
+ * what this call can check of that is SHPL_ERR_ARG when false. d_dx and the written cells of d_dx_b are
+ * shpl_conv3x3_dgrad's, bit for bit. When the input gradient itself does not run the row-streaming form (f32,
+ * misaligned maps) or has more than 32 gradient channels (c_gy), d_dx_b is written whole.
+ * Replaces: the image half of TF's conv2d backprop input in the rpn_model.py:338-354 fusion, which the
+ * gradient of tf.gather_nd / tf.segment_sum (sparse_pool_utils.py:96-117) reads only at occupied cells. */
+int shpl_conv3x3_dgrad_reuse(int dtype, int n_frames, int64_t h, int64_t w, const void *d_gy, int64_t gy_stride,
+                             int64_t c_gy, const void *d_weights, int64_t c_dx, void *d_dx, int64_t dx_stride,
+                             int64_t c_split, void *d_dx_b, int64_t dx_b_stride, void *d_ws, size_t ws_bytes,
+                             const shpl_csr *pool, const void *d_fwd_ws, size_t fwd_ws_bytes, int fwd_stats,
+                             void *stream);
+
 /* Weight gradient: dw[ky][kx][ci][co] = sum over pixels of x[p + (ky-1, kx-1)][ci]
  * * gy[p][co], x given exactly as shpl_conv3x3's input (A channels, then B
  * channels, dense or pooled from the CSR -- recomputed, never stored). f32

@@ -174,6 +174,8 @@ def _declare(lib):
         "shpl_batch_norm_backward_workspace_bytes": (i32, [i64, i64, psz]),
         "shpl_batch_norm_backward": (i32, [i32, i64, p, p, p, i64, i64, p, p, p, p, i32, i32, p, p, p, p, sz, p]),
         "shpl_conv3x3_dgrad": (i32, [i32, i32, i64, i64, p, i64, i64, p, i64, p, i64, i64, p, i64, p, sz, p]),
+        "shpl_conv3x3_dgrad_reuse": (i32, [i32, i32, i64, i64, p, i64, i64, p, i64, p, i64, i64, p, i64, p, sz,
+                                           ctypes.POINTER(ShplCsr), p, sz, i32, p]),
         "shpl_conv3x3_wgrad_workspace_bytes": (i32, [i32, i32, i64, i64, i64, i64, i64, i64, psz]),
         "shpl_conv3x3_wgrad": (i32, [i32, i32, i64, i64, p, i64, i64, i64, p, i64, i64, i64,
                                      ctypes.POINTER(ShplCsr), p, p, i64, i64, p, p, sz, p]),

@@ -108,6 +108,7 @@ struct ConvArgs {
     void *out2;
     int64_t out2_stride;
     int c_split;
+    const uint32_t *occ2;  // rows form: out2 written only at the cells set in these occupancy words (NULL: all)
     bool vec_out;  // out (and out2) rows and c_split 16-byte aligned: 16-byte stores
     double *part;  // STATS: [(co_block*32 + co)*2 + stat][n_tiles]
 };
@@ -1674,6 +1675,7 @@ int conv_rows_launch(const ConvPlan &pl, const ConvArgs &a, bool pooled, bool st
     r.out2 = reinterpret_cast<uint16_t *>(a.out2);
     r.out2_stride = a.out2_stride;
     r.c_split = a.c_split;
+    r.occ2 = a.occ2;
     r.n_cob = pl.n_cob;
     r.part = stats ? a.part : nullptr;  // n_items <= n_tiles: the tiled plan's partials hold the rows kernel's
     uint8_t *ws = reinterpret_cast<uint8_t *>(const_cast<void *>(a.wp)) + pl.wp_bytes + pl.rp_bytes + pl.part_bytes;
@@ -2050,10 +2052,11 @@ extern "C" int shpl_batch_norm_backward(int dtype, int64_t rows, const void *d_y
     return SHPL_OK;
 }
 
-extern "C" int shpl_conv3x3_dgrad(int dtype, int n_frames, int64_t h, int64_t w, const void *d_gy, int64_t gy_stride,
-                                  int64_t c_gy, const void *d_weights, int64_t c_dx, void *d_dx, int64_t dx_stride,
-                                  int64_t c_split, void *d_dx_b, int64_t dx_b_stride, void *d_ws, size_t ws_bytes,
-                                  void *stream) {
+namespace {
+// shpl_conv3x3_dgrad; occ2: the occupancy words (wpr per row) limiting d_dx_b's stores (shpl_conv3x3_dgrad_reuse)
+int dgrad_impl(int dtype, int n_frames, int64_t h, int64_t w, const void *d_gy, int64_t gy_stride, int64_t c_gy,
+               const void *d_weights, int64_t c_dx, void *d_dx, int64_t dx_stride, int64_t c_split, void *d_dx_b,
+               int64_t dx_b_stride, void *d_ws, size_t ws_bytes, const uint32_t *occ2, void *stream) {
     ConvPlan pl;
     int rc = conv_plan(dtype, n_frames, h, w, c_gy, 0, c_dx, false, false, &pl);
     if (rc) return rc;
@@ -2089,9 +2092,41 @@ extern "C" int shpl_conv3x3_dgrad(int dtype, int n_frames, int64_t h, int64_t w,
     a.c_split = (int)c_split;
     a.vec_out = (!d_dx || (aligned16(d_dx) && dx_stride % he == 0)) &&
                 (!d_dx_b || (aligned16(d_dx_b) && dx_b_stride % he == 0 && c_split % he == 0));
+    a.occ2 = d_dx_b ? occ2 : nullptr;
     hipStream_t s = (hipStream_t)stream;
     if (dtype == SHPL_F32) return conv_launch<float>(pl, a, false, false, d_weights, nullptr, nullptr, s, 1);
     return conv_launch<uint16_t>(pl, a, false, false, d_weights, nullptr, nullptr, s, 1);
+}
+}  // namespace
+
+extern "C" int shpl_conv3x3_dgrad(int dtype, int n_frames, int64_t h, int64_t w, const void *d_gy, int64_t gy_stride,
+                                  int64_t c_gy, const void *d_weights, int64_t c_dx, void *d_dx, int64_t dx_stride,
+                                  int64_t c_split, void *d_dx_b, int64_t dx_b_stride, void *d_ws, size_t ws_bytes,
+                                  void *stream) {
+    return dgrad_impl(dtype, n_frames, h, w, d_gy, gy_stride, c_gy, d_weights, c_dx, d_dx, dx_stride, c_split, d_dx_b,
+                      dx_b_stride, d_ws, ws_bytes, nullptr, stream);
+}
+
+extern "C" int shpl_conv3x3_dgrad_reuse(int dtype, int n_frames, int64_t h, int64_t w, const void *d_gy,
+                                        int64_t gy_stride, int64_t c_gy, const void *d_weights, int64_t c_dx,
+                                        void *d_dx, int64_t dx_stride, int64_t c_split, void *d_dx_b,
+                                        int64_t dx_b_stride, void *d_ws, size_t ws_bytes, const shpl_csr *pool,
+                                        const void *d_fwd_ws, size_t fwd_ws_bytes, int fwd_stats, void *stream) {
+    // the forward's occupancy words, where its plan put them: the forward is the conv of [A (c_split) || B pooled
+    // (c_dx - c_split)] to c_gy channels, the plan wgrad_impl's reuse checks too
+    if (!pool || !d_fwd_ws || !d_dx_b) return SHPL_ERR_ARG;
+    if (pool->n_keys != (int64_t)n_frames * h * w || c_split < 1 || c_split >= c_dx) return SHPL_ERR_BAD_SHAPE;
+    ConvPlan fp;
+    int rc = conv_plan(dtype, n_frames, h, w, c_split, c_dx - c_split, c_gy, true, fwd_stats != 0, &fp, 0,
+                       pool->nnz_cap);
+    if (rc) return rc;
+    if (!fp.rows || fwd_ws_bytes < fp.total || c_gy % NCO != 0 ||
+        (fwd_stats != 0 && !rows::supported_st(fp.qa + fp.qb, fp.qa, true)))
+        return SHPL_ERR_ARG;
+    const uint32_t *occ = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(d_fwd_ws) + fp.wp_bytes +
+                                                             fp.rp_bytes + fp.part_bytes);
+    return dgrad_impl(dtype, n_frames, h, w, d_gy, gy_stride, c_gy, d_weights, c_dx, d_dx, dx_stride, c_split, d_dx_b,
+                      dx_b_stride, d_ws, ws_bytes, occ, stream);
 }
 
 namespace {

@@ -27,6 +27,7 @@ struct RowArgs {
     uint16_t *out2;              // output blocks from channel c_split on go here (the input gradient's two maps)
     int64_t out2_stride;
     int c_split;                 // a multiple of 32 when out2 is set
+    const uint32_t *occ2;        // out2 written only at the cells set in these occupancy words (wpr per row; NULL: all)
     int n_cob;                   // output blocks (the fastest index of a workgroup's item)
     double *part;                // ST: per-item channel sums [(co * 2 + stat) * n_items + item]
 };

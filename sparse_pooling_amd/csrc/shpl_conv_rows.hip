@@ -384,6 +384,13 @@ __device__ __forceinline__ void stage(const RowArgs &r, int64_t pix0, bool yok, 
 // epilogue of output row j-2 of the band (always stored: rows and pixels
 // outside the map go to the junk line; its accumulator is cleared), then
 // stage input row j + RING into the slot just read.
+// The forms whose out2 stores may be limited to occupied cells (RowArgs::occ2): the input gradient's (dense A,
+// no ReLU, no statistics) of at most 32 gradient channels (the 4-chunk form has no register for the mask: it
+// spills; it writes out2 whole)
+template <int Q, bool CMP, bool RELU, bool ST>
+constexpr bool occ2_form() { return Q <= 2 && !CMP && !RELU && !ST && !SHPL_ROWS_EPI8; }
+static_assert(TW == 32, "occ2: one occupancy word per strip row");
+
 template <int Q, int QA, bool CMP, bool RELU, bool ST, int U>
 __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9], f32x16 (&acc)[3],
                                      const float (*s_par)[NCO], const uint8_t *rd, uint8_t *s_ring,
@@ -393,7 +400,7 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
                                      const uint32_t (&offa)[Layout<Q, QA>::NA],
                                      const int32_t (&offb)[Layout<Q, QA>::NB > 0 ? Layout<Q, QA>::NB : 1],
                                      const uint32_t *s_offs, const uint32_t (&rdq)[2], int lane,
-                                     f32x4 (&str)[2], uint64_t (&ph)[5]) {
+                                     f32x4 (&str)[2], uint64_t (&ph)[5], uint32_t m2row, bool m2) {
     typedef Layout<Q, QA, ST> L;
 #if SHPL_ROWS_PROBE == 3
     uint64_t t0, t1, t2, t3, t4;
@@ -546,6 +553,23 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
         }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (occ2_form<Q, CMP, RELU, ST>()) {
+            // buffer stores, whose masked lanes carry an offset past the row's range that the hardware drops:
+            // pixels outside the map, and with m2 the unoccupied cells of out2 (the input gradient's pooled
+            // channels: the pixel-keyed pull back to the image reads no other row) -- both stores always
+            // issued, on one path (the ring's vmcnt arithmetic; no branch on m2)
+            const uint32_t m = m2 ? (uint32_t)__builtin_amdgcn_readlane((int)m2row, b < 0 ? 0 : b) : 0xffffffffu;
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(orow, (short)0, (int)((31 * ostr + 32) * 2), 0x00020000);
+    #pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int pc = lane + 64 * k, px = pc >> 2, pi = pc & 3;
+                const u32x4 v = *reinterpret_cast<const u32x4 *>(s_o + px * REPI + pi * 16);
+                const bool ok = row_ok && x0 + px < r.w && ((m >> px) & 1u);
+                const int off = ok ? (int)((px * ostr + pi * 8) * 2) : (int)0x80000000u;
+                __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, SHPL_ROWS_NTSTORE ? 2 : 0);  // 2: nt
+            }
+        } else {
     #pragma unroll
         for (int k = 0; k < 2; ++k) {  // 32 pixels x 4 pieces of 8 channels
             const int pc = lane + 64 * k, px = pc >> 2, pi = pc & 3;
@@ -556,6 +580,7 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
 #else
             *reinterpret_cast<u32x4 *>(dst) = v;
 #endif
+        }
         }
 #endif
         if constexpr (streg<Q, QA, CMP, ST>()) {
@@ -734,6 +759,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rows_wpe_min
         b_rows = __ballot(occ_row != 0);  // input rows with an occupied cell in their window
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own LDS writes, in order
     }
+    // out2 by occupancy: lane b holds the occupancy word of the strip's cells in output row ya + b (TW = 32: one
+    // word), loaded before the weights' vmcnt(0) below retires it with them
+    uint32_t m2row = 0u;
+    const bool m2 = occ2_form<Q, CMP, RELU, ST>() && second && r.occ2 != nullptr;
+    if (m2 && lane < n_out) m2row = r.occ2[((int64_t)f * H + ya + lane) * r.wpr + (x0 >> 5)];
     uint32_t offa[L::NA];
     int32_t offb[L::NB > 0 ? L::NB : 1];
     lane_offsets<Q, QA, CMP>(r, x0, lane, offa, offb);
@@ -804,7 +834,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rows_wpe_min
 #define SHPL_ROWS_STEP(UU)                                                                                          \
     if (j + UU >= n_in) break;                                                                                      \
     step<Q, QA, CMP, RELU, ST, UU>(r, wr, acc, s_par, rd, s_ring, frame_row0, x0, ya, n_in, n_out, obase, ostr, s_st, \
-                                   j + UU, s_occ, s_first, b_rows, offa, offb, s_offs, rdq, lane, str, ph);
+                                   j + UU, s_occ, s_first, b_rows, offa, offb, s_offs, rdq, lane, str, ph, m2row, m2);
         SHPL_ROWS_STEP(0)
         SHPL_ROWS_STEP(1)
         SHPL_ROWS_STEP(2)

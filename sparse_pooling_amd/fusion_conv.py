@@ -144,10 +144,13 @@ def batch_norm_backward(gy, y=None, raw=None, mean=None, scale=None, gamma=None,
     return out, dbeta, dgamma
 
 
-def conv3x3_dgrad(gy, weights, c_dx, split=None):
+def conv3x3_dgrad(gy, weights, c_dx, split=None, pool=None, fwd_ws=None, fwd_stats=False):
     """Input gradient [B,H,W,c_dx] of the SAME 3x3 conv with HWIO ``weights``;
     with ``split`` = c, the pair (channels [0, c), channels [c, c_dx)) as two
-    dense maps written by the kernel's epilogue (no slicing copies)."""
+    dense maps written by the kernel's epilogue (no slicing copies). ``fwd_ws`` (with ``pool``, the pooled bf16
+    forward's CSR, and ``split``): the workspace of that forward conv3x3 (taken with statistics: fwd_stats),
+    whose occupancy words limit the second map to the occupied cells -- the only rows the pixel-keyed pull
+    back to the image reads; its other cells are left unwritten (shpl_conv3x3_dgrad_reuse)."""
     gy = gy.contiguous()
     B, H, W, Cg = (int(s) for s in gy.shape)
     weights = weights.to(gy.dtype).contiguous()
@@ -156,10 +159,14 @@ def conv3x3_dgrad(gy, weights, c_dx, split=None):
     dx = torch.empty((B, H, W, c0), dtype=gy.dtype, device=gy.device)
     dx_b = None if split is None else torch.empty((B, H, W, c_dx - c0), dtype=gy.dtype, device=gy.device)
     ws = L.workspace(conv_ws_bytes(L.dtype_code(gy), B, H, W, Cg, 0, c_dx, None, False), gy.device)
-    L.check(L.lib().shpl_conv3x3_dgrad(L.dtype_code(gy), B, H, W, L.ptr(gy), Cg, Cg, L.ptr(weights), c_dx,
-                                       L.ptr(dx), max(c0, 1), c0, L.ptr(dx_b), max(c_dx - c0, 1), L.ptr(ws),
-                                       ws.numel(), L.stream_of(gy.device)),
-            "shpl_conv3x3_dgrad")
+    args = (L.dtype_code(gy), B, H, W, L.ptr(gy), Cg, Cg, L.ptr(weights), c_dx, L.ptr(dx), max(c0, 1), c0,
+            L.ptr(dx_b), max(c_dx - c0, 1), L.ptr(ws), ws.numel())
+    if fwd_ws is not None:
+        L.check(L.lib().shpl_conv3x3_dgrad_reuse(*args, pool.ref(), L.ptr(fwd_ws), fwd_ws.numel(),
+                                                 int(bool(fwd_stats)), L.stream_of(gy.device)),
+                "shpl_conv3x3_dgrad_reuse")
+    else:
+        L.check(L.lib().shpl_conv3x3_dgrad(*args, L.stream_of(gy.device)), "shpl_conv3x3_dgrad")
     return dx if split is None else (dx, dx_b)
 
 
@@ -296,7 +303,10 @@ class _FusionConvFn(torch.autograd.Function):
             if b is None:
                 d_a = conv3x3_dgrad(g_raw, weights, Ca)
             else:  # the epilogue writes the two sources' gradients as separate dense maps
-                d_a, dx_b = conv3x3_dgrad(g_raw, weights, Ca + Cb, split=Ca)
+                occ = pooled and ctx.fwd_ws is not None and conv.DGRAD_OCC and ctx.needs_input_grad[1]
+                d_a, dx_b = conv3x3_dgrad(g_raw, weights, Ca + Cb, split=Ca,
+                                          pool=smap.csr(L.BY_CELL, L.ORDER_ENTRY) if occ else None,
+                                          fwd_ws=ctx.fwd_ws if occ else None, fwd_stats=ctx.train_bn)
                 if ctx.needs_input_grad[1]:
                     if pooled and zeros_done is not None:  # its zero rows are on the side stream already
                         cur.wait_event(zeros_done)
@@ -358,6 +368,9 @@ class FusionConv:
     # side measured slower: 7.34-7.35 vs 7.14-7.20 ms per bf16 training step, profiles/r05_wside_ab.log)
     IMG_ZERO_SIDE = True
     WGRAD_SIDE = False
+    # bf16 fused() backward: the input gradient's pooled channels stored at the occupied cells only, by the
+    # forward's occupancy words (shpl_conv3x3_dgrad_reuse; False: the whole map, shpl_conv3x3_dgrad)
+    DGRAD_OCC = True
 
     def __init__(self, c_in, c_out, batch_norm=True, bias=False, relu=True, eps=1e-3, decay=0.999,
                  dtype=torch.float32, device="cuda", seed=0):

@@ -426,3 +426,52 @@ def test_wgrad_reuse_rejects_a_tiled_forward_workspace():
                                           L.ptr(smap.frame_off), L.ptr(gy), 32, 32, L.ptr(dw), L.ptr(ws), ws.numel(),
                                           L.ptr(fws), fws.numel(), 1, L.stream_of(DEV))
     assert rc == L.ERR_ARG
+
+
+@pytest.mark.parametrize("stats,frames", [(True, 2), (False, 1)])
+def test_dgrad_reuse_writes_occupied_cells_only(stats, frames):
+    """shpl_conv3x3_dgrad_reuse: the input gradient's first map and, at every occupied cell of the pooled forward's
+    CSR, its second map are bitwise shpl_conv3x3_dgrad's; every other cell of the second map keeps what it held
+    (a NaN fill here). The forward (its workspace) with and without batch statistics; two frames: the occupancy
+    words of frame 1 are found at its own rows. Config 1's geometry."""
+    from sparse_pooling_amd import _lib as L, fusion_conv as fc, pipeline, shpl_map as sm
+    spec = synth.CONFIGS[1]
+    frs = [synth.make_frame(spec, seed=931 + f, n_outside=20 * f) for f in range(frames)]
+    pts, vox, off, P, maxp, N = pipeline.stack_frames(frs, DEV)
+    ib = sm.build_index_batch(pts, vox, off, P, spec.im_size, spec.bv_size, spec.stride, maxp)
+    smap = ib.map
+    Hb, Wb = spec.bev_feat_hw
+    Hi, Wi = spec.img_feat_hw
+    bev = _t(synth.make_features((frames, Hb, Wb, 32), 61)).to(torch.bfloat16)
+    img = _t(synth.make_features((frames, Hi, Wi, 32), 62)).to(torch.bfloat16)
+    pool = smap.csr(L.BY_CELL, L.ORDER_ENTRY)
+    w = _t(np.random.default_rng(63).uniform(-0.1, 0.1, (3, 3, 64, 32)).astype(np.float32)).to(torch.bfloat16)
+    assert fc.rows_form(bev, w, b=img, pool=pool, frame_off=smap.frame_off, relu=False, stats=stats)
+    fws = L.workspace(fc.conv_ws_bytes(L.BF16, frames, Hb, Wb, 32, 32, 32, pool.nnz_cap, stats), DEV)
+    st = torch.empty((2, 32), dtype=torch.float64, device=DEV) if stats else None
+    fc.conv3x3(bev, w, b=img, pool=pool, frame_off=smap.frame_off, relu=False, stats=st, ws=fws)
+    gy = _t(np.random.default_rng(64).standard_normal((frames, Hb, Wb, 32)).astype(np.float32)).to(torch.bfloat16)
+    da, db = fc.conv3x3_dgrad(gy, w, 64, split=32)
+    ws = L.workspace(fc.conv_ws_bytes(L.BF16, frames, Hb, Wb, 32, 0, 64, None, False), DEV)
+    ra = torch.empty_like(da)
+    rb = torch.full_like(db, float("nan"))
+    L.check(L.lib().shpl_conv3x3_dgrad_reuse(L.BF16, frames, Hb, Wb, L.ptr(gy), 32, 32, L.ptr(w), 64, L.ptr(ra), 32,
+                                             32, L.ptr(rb), 32, L.ptr(ws), ws.numel(), pool.ref(), L.ptr(fws),
+                                             fws.numel(), int(stats), L.stream_of(DEV)), "shpl_conv3x3_dgrad_reuse")
+    torch.cuda.synchronize()
+    assert torch.equal(ra, da)
+    dst, fo, fn = (_np(t) for t in (pool.ent_dst, smap.frame_off, ib.frame_nnz))
+    occ = np.zeros(frames * Hb * Wb, dtype=bool)
+    for f in range(frames):
+        d = dst[fo[f]:fo[f] + fn[f]]
+        occ[d[d >= 0]] = True
+    occ = torch.from_numpy(occ).to(DEV)
+    assert 0 < int(occ.sum()) < occ.numel()
+    flat_b, flat_r = db.reshape(-1, 32), rb.reshape(-1, 32)
+    assert torch.equal(flat_r[occ], flat_b[occ])
+    assert bool(torch.isnan(flat_r[~occ].float()).all())
+    # a workspace too small for the forward's plan is refused, not read
+    rc = L.lib().shpl_conv3x3_dgrad_reuse(L.BF16, frames, Hb, Wb, L.ptr(gy), 32, 32, L.ptr(w), 64, L.ptr(ra), 32, 32,
+                                          L.ptr(rb), 32, L.ptr(ws), ws.numel(), pool.ref(), L.ptr(fws), 256,
+                                          int(stats), L.stream_of(DEV))
+    assert rc == L.ERR_ARG
