@@ -400,7 +400,7 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
                                      const uint32_t (&offa)[Layout<Q, QA>::NA],
                                      const int32_t (&offb)[Layout<Q, QA>::NB > 0 ? Layout<Q, QA>::NB : 1],
                                      const uint32_t *s_offs, const uint32_t (&rdq)[2], int lane,
-                                     f32x4 (&str)[2], uint64_t (&ph)[5], uint32_t m2row, bool m2) {
+                                     f32x4 (&str)[2], uint64_t (&ph)[5], uint32_t m2row, bool m2, uint64_t m2live) {
     typedef Layout<Q, QA, ST> L;
 #if SHPL_ROWS_PROBE == 3
     uint64_t t0, t1, t2, t3, t4;
@@ -412,6 +412,11 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
     SHPL_STAMP(t1);
 #endif
     f32x16 &a0 = acc[(U + 1) % 3], &a1 = acc[U], &a2 = acc[(U + 2) % 3];
+    // m2: output rows j-2 .. j (the three accumulators' rows) all without an occupied cell -- none of them is
+    // stored, so their MFMAs are skipped (a uniform branch: no memory operation inside)
+    bool dead3 = false;
+    if constexpr (occ2_form<Q, CMP, RELU, ST>()) dead3 = m2 && (((m2live << 2) >> j) & 7ull) == 0;
+    if (!dead3) {
     if constexpr (m16<Q, ST>()) {
         // K-chunk c (32 channels: pieces 4c .. 4c+3, each lane its piece 4c + lane / 16 from A or B), then kx,
         // then the pixel half nb; both output halves h per operand read. A split between A and B and the
@@ -466,6 +471,7 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
                 a2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[q][6 + kx], xv, a2, 0, 0, 0);
             }
         }
+    }
     }
     }
 #if SHPL_ROWS_PROBE == 3
@@ -809,6 +815,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rows_wpe_min
     // rows and the stores) every row. The builtin clears its scoreboard (the prologue's DMAs land too)
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 #endif
+    const uint64_t m2live = m2 ? __ballot(m2row != 0u) : ~0ull;  // m2: the output rows with an occupied cell
     f32x16 acc[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k)
@@ -834,7 +841,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rows_wpe_min
 #define SHPL_ROWS_STEP(UU)                                                                                          \
     if (j + UU >= n_in) break;                                                                                      \
     step<Q, QA, CMP, RELU, ST, UU>(r, wr, acc, s_par, rd, s_ring, frame_row0, x0, ya, n_in, n_out, obase, ostr, s_st, \
-                                   j + UU, s_occ, s_first, b_rows, offa, offb, s_offs, rdq, lane, str, ph, m2row, m2);
+                                   j + UU, s_occ, s_first, b_rows, offa, offb, s_offs, rdq, lane, str, ph, m2row, m2, m2live);
         SHPL_ROWS_STEP(0)
         SHPL_ROWS_STEP(1)
         SHPL_ROWS_STEP(2)
