@@ -82,6 +82,9 @@ constexpr int REPI = NCO * 2 + 16;  // epilogue transpose pitch (bytes per pixel
 #define SHPL_ROWS_EPI8 0  // 1: 8-byte stores straight from the accumulators (4 per lane and row), no LDS transpose: correct
                           // with RSTORES = 4, measured 1.2-1.6x slower (profiles/r04_epi_ab.log)
 #endif
+#ifndef SHPL_ROWS_DEAD3
+#define SHPL_ROWS_DEAD3 1  // 0: the occupancy-limited input gradient computes every row (A/B)
+#endif
 #ifndef SHPL_ROWS_NTSTORE
 #define SHPL_ROWS_NTSTORE 1  // the epilogue's stores nontemporal (0: plain stores, A/B)
 #endif
@@ -415,7 +418,7 @@ __device__ __forceinline__ void step(const RowArgs &r, const bf16x8 (&wr)[Q][9],
     // m2: output rows j-2 .. j (the three accumulators' rows) all without an occupied cell -- none of them is
     // stored, so their MFMAs are skipped (a uniform branch: no memory operation inside)
     bool dead3 = false;
-    if constexpr (occ2_form<Q, CMP, RELU, ST>()) dead3 = m2 && (((m2live << 2) >> j) & 7ull) == 0;
+    if constexpr (occ2_form<Q, CMP, RELU, ST>()) dead3 = SHPL_ROWS_DEAD3 && m2 && (((m2live << 2) >> j) & 7ull) == 0;
     if (!dead3) {
     if constexpr (m16<Q, ST>()) {
         // K-chunk c (32 channels: pieces 4c .. 4c+3, each lane its piece 4c + lane / 16 from A or B), then kx,
