@@ -83,7 +83,7 @@ constexpr int REPI = NCO * 2 + 16;  // epilogue transpose pitch (bytes per pixel
                           // with RSTORES = 4, measured 1.2-1.6x slower (profiles/r04_epi_ab.log)
 #endif
 #ifndef SHPL_ROWS_DEAD3
-#define SHPL_ROWS_DEAD3 1  // 0: the occupancy-limited input gradient computes every row (A/B)
+#define SHPL_ROWS_DEAD3 0  // 1: masked input-gradient waves skip three dead rows' MFMAs (A/B: within noise, profiles/r06_ab/dead3_*)
 #endif
 #ifndef SHPL_ROWS_NTSTORE
 #define SHPL_ROWS_NTSTORE 1  // the epilogue's stores nontemporal (0: plain stores, A/B)
