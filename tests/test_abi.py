@@ -109,6 +109,19 @@ def test_argument_validation_is_host_side():
         assert rf.value == want, (dt, cb, stats)
     assert lib.shpl_conv3x3_rows_form(L.BF16, 1, 176, 200, P, 32, 0, 32, P, 32, 0, 32, ctypes.byref(ccell1), P, P,
                                       16, L.ACT_NONE, P, 16, 0, ctypes.byref(rf)) == L.OK and rf.value == 0
+    # the occupancy-limited input gradient: no pool / forward workspace / second map, keys that are not the map's,
+    # a split outside (0, c_dx), a forward workspace smaller than that forward's plan -- all before any launch
+    dg = (L.BF16, 1, 176, 200, P, 32, 32, P, 64, P, 32)
+    fws = 1 << 24
+    assert lib.shpl_conv3x3_dgrad_reuse(*dg, 32, P, 32, P, 1 << 20, None, P, fws, 0, N) == L.ERR_ARG
+    assert lib.shpl_conv3x3_dgrad_reuse(*dg, 32, P, 32, P, 1 << 20, ctypes.byref(ccell1), N, fws, 0, N) == L.ERR_ARG
+    assert lib.shpl_conv3x3_dgrad_reuse(*dg, 32, N, 32, P, 1 << 20, ctypes.byref(ccell1), P, fws, 0, N) == L.ERR_ARG
+    assert lib.shpl_conv3x3_dgrad_reuse(*dg[:2], 175, *dg[3:], 32, P, 32, P, 1 << 20, ctypes.byref(ccell1), P, fws, 0,
+                                        N) == L.ERR_BAD_SHAPE
+    for split in (0, 64):
+        assert lib.shpl_conv3x3_dgrad_reuse(*dg, split, P, 32, P, 1 << 20, ctypes.byref(ccell1), P, fws, 0,
+                                            N) == L.ERR_BAD_SHAPE
+    assert lib.shpl_conv3x3_dgrad_reuse(*dg, 32, P, 32, P, 1 << 20, ctypes.byref(ccell1), P, 16, 1, N) == L.ERR_ARG
     # buckets: shapes over the limits (65536 destinations per frame, 2^24 points per frame), workspace size,
     # missing bucket workspace; CSRs from buckets: null map, too few keys, small
     # workspace; pull pair: null CSR, the bad-shape checks of shpl_pull, no key_range
