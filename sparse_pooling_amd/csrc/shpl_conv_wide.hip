@@ -326,6 +326,97 @@ __global__ __launch_bounds__(256) void k_pool_runs_wide(const int32_t *ent_dst, 
     *reinterpret_cast<u32x4 *>(cmp + (frame_off[f] + rid) * (int64_t)c_b + g * 8) = *reinterpret_cast<u32x4 *>(v);
 }
 
+// K consecutive entries per thread, one 8-channel piece g of each: their index words in one round trip and
+// their K row pieces in flight together (the runs of a cell are mostly one entry long, so a thread per entry
+// spent a round trip per index word and per row with little else in flight); each run head sums its run in
+// entry order from 0 with separate multiply and add, as k_pool_runs_wide does -- bit for bit -- walking on past
+// the group when the run does.
+#ifndef SHPL_WIDE_RUNS_K
+#define SHPL_WIDE_RUNS_K 4  // 1: k_pool_runs_wide (a thread per entry and piece)
+#endif
+template <int K>
+__global__ __launch_bounds__(256) void k_pool_runs_wide_k(const int32_t *ent_dst, const int32_t *ent_src,
+                                                          const float *ent_val, int64_t nnz_cap, const uint16_t *img,
+                                                          int64_t img_stride, int64_t img_off, int c_b, int np, int H,
+                                                          int W, int wpr, const uint32_t *occ,
+                                                          const int32_t *occ_base, const int64_t *frame_off,
+                                                          uint16_t *cmp) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t grp = t / np;
+    const int g = (int)(t - grp * np);
+    const int64_t e0 = grp * K;
+    if (e0 >= nnz_cap) return;
+    int32_t d[K + 1], src[K];
+    float wv[K];
+    const int32_t prev0 = e0 > 0 ? ent_dst[e0 - 1] : -1;
+#pragma unroll
+    for (int k = 0; k <= K; ++k) d[k] = e0 + k < nnz_cap ? ent_dst[e0 + k] : -1;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const bool in = e0 + k < nnz_cap;
+        wv[k] = in ? ent_val[e0 + k] : 0.0f;
+        src[k] = in ? ent_src[e0 + k] : 0;
+    }
+    u32x4 raw[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        raw[k] = d[k] >= 0 ? *reinterpret_cast<const u32x4 *>(img + (int64_t)src[k] * img_stride + img_off + g * 8)
+                           : u32x4{0u, 0u, 0u, 0u};
+    const int64_t cells = (int64_t)H * W;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        if (d[k] < 0 || d[k] == (k ? d[k - 1] : prev0)) continue;  // not a run head
+        float sum[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sum[j] = 0.0f;
+        bool tail = true;  // the run reaches past the group
+#pragma unroll
+        for (int m = k; m < K; ++m) {
+            if (m > k && d[m] != d[k]) {
+                tail = false;
+                break;
+            }
+            uint16_t xv[8];
+            __builtin_memcpy(xv, &raw[m], 16);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sum[j] = __fadd_rn(sum[j], __fmul_rn(wv[m], bf16_to_f32(xv[j])));
+        }
+        if (tail && d[K] == d[k]) {  // entries e0 + K, ... of the same cell, one round trip each
+            int64_t i = e0 + K;
+            float w = ent_val[i];
+            int32_t sr = ent_src[i];
+            int32_t dn = i + 1 < nnz_cap ? ent_dst[i + 1] : -1;
+            for (;; ++i) {
+                const u32x4 r = *reinterpret_cast<const u32x4 *>(img + (int64_t)sr * img_stride + img_off + g * 8);
+                const bool more = dn == d[k];
+                float wn = 0.0f;
+                int32_t sn = 0, dnn = -1;
+                if (more) {
+                    wn = ent_val[i + 1];
+                    sn = ent_src[i + 1];
+                    dnn = i + 2 < nnz_cap ? ent_dst[i + 2] : -1;
+                }
+                uint16_t xv[8];
+                __builtin_memcpy(xv, &r, 16);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) sum[j] = __fadd_rn(sum[j], __fmul_rn(w, bf16_to_f32(xv[j])));
+                if (!more) break;
+                w = wn;
+                sr = sn;
+                dn = dnn;
+            }
+        }
+        const int f = (int)(d[k] / cells);
+        const int c = (int)(d[k] - f * cells), y = c / W, x = c - y * W;
+        const int64_t wi = ((int64_t)f * H + y) * wpr + (x >> 5);
+        const int32_t rid = occ_base[wi] + __popc(occ[wi] & ((1u << (x & 31)) - 1u));
+        uint16_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = f32_to_bf16(sum[j]);
+        *reinterpret_cast<u32x4 *>(cmp + (frame_off[f] + rid) * (int64_t)c_b + g * 8) = *reinterpret_cast<u32x4 *>(v);
+    }
+}
+
 }  // namespace
 
 int prep(int n_frames, int h, int w, int wpr, const int32_t *ent_dst, const int32_t *ent_src, const float *ent_val,
@@ -336,7 +427,13 @@ int prep(int n_frames, int h, int w, int wpr, const int32_t *ent_dst, const int3
                                img_off, 0, occ, occ_base, cmp, s);
     if (rc) return rc;
     const int np = c_b / 8;
-    if (nnz_cap > 0 && np > 0) {
+    if (nnz_cap > 0 && np > 0 && SHPL_WIDE_RUNS_K > 1) {
+        const int64_t threads = (nnz_cap + SHPL_WIDE_RUNS_K - 1) / SHPL_WIDE_RUNS_K * np;
+        hipLaunchKernelGGL(k_pool_runs_wide_k<SHPL_WIDE_RUNS_K>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                           s, ent_dst, ent_src, ent_val, nnz_cap, img, img_stride, img_off, c_b, np, h, w, wpr, occ,
+                           occ_base, frame_off, cmp);
+        SHPL_LAUNCH_CHECK();
+    } else if (nnz_cap > 0 && np > 0) {
         const int64_t threads = nnz_cap * np;
         hipLaunchKernelGGL(k_pool_runs_wide, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, ent_dst,
                            ent_src, ent_val, nnz_cap, img, img_stride, img_off, c_b, np, h, w, wpr, occ, occ_base,
