@@ -140,6 +140,9 @@ def parse():
     ap.add_argument("--wgrad-side", choices=["on", "off"], default=None,
                     help="conv training: the weight gradient on a side stream beside the input gradient "
                          "(FusionConv.WGRAD_SIDE; default: the class's)")
+    ap.add_argument("--img-beside", choices=["dgrad", "wgrad"], default=None,
+                    help="conv training: the image gradient's side-stream work beside the input gradient (its zero "
+                         "rows) or beside the weight gradient (zero rows and pull; FusionConv.IMG_BESIDE_WGRAD)")
     ap.add_argument("--img-zero-side", choices=["on", "off"], default=None,
                     help="conv training: the image gradient's zero rows on a side stream beside the input gradient "
                          "(FusionConv.IMG_ZERO_SIDE; default: the class's)")
@@ -948,6 +951,8 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
     esz = 2 if dtype == torch.bfloat16 else 4
     conv.WGRAD_REUSE = not args.no_wgrad_reuse
     conv.DGRAD_OCC = not args.no_dgrad_occ
+    if args.img_beside is not None:
+        conv.IMG_BESIDE_WGRAD = args.img_beside == "wgrad"
     if args.wgrad_side is not None:
         conv.WGRAD_SIDE = args.wgrad_side == "on"
     if args.img_zero_side is not None:
@@ -1035,7 +1040,7 @@ def run_conv_train(args, world, rank, dev, spec, fids, dtype, pl, pts, vox, off,
                        "global_batch": F * world, "frames_per_gpu_per_step": F, "hip_graph": False,
                        "wgrad_reuse": conv.WGRAD_REUSE, "dgrad_occ": esz == 2 and conv.WGRAD_REUSE and conv.DGRAD_OCC,
                        "wgrad_side_stream": conv.WGRAD_SIDE,
-                       "img_zero_side_stream": conv.IMG_ZERO_SIDE,
+                       "img_zero_side_stream": conv.IMG_ZERO_SIDE, "img_beside_wgrad": conv.IMG_BESIDE_WGRAD,
                        "bn_statistics": "per rank (no cross-rank sync)", "parallelism": f"frame-sharded x{world}"},
             "roofline": ({"bound": "hbm", "kernel": "the whole forward + backward step: algorithmic bytes of its passes "
                           "(pooled map, conv fwd, BN apply, BN backward x2, input and weight gradients, image "

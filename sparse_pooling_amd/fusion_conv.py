@@ -282,7 +282,11 @@ class _FusionConvFn(torch.autograd.Function):
         img_grad = need_x and pooled and b is not None and ctx.needs_input_grad[1]
         zero_side = img_grad and conv.IMG_ZERO_SIDE
         wgrad_side = need_x and ctx.needs_input_grad[2] and conv.WGRAD_SIDE
-        if g_raw.is_cuda and (zero_side or wgrad_side):
+        # IMG_BESIDE_WGRAD: the image gradient (zero rows, then the pull) on the side stream after the input
+        # gradient, beside the weight gradient, instead of its zero rows beside the input gradient
+        late_zero = (zero_side and conv.IMG_BESIDE_WGRAD and ctx.needs_input_grad[2] and not wgrad_side and
+                     g_raw.is_cuda)
+        if g_raw.is_cuda and ((zero_side and not late_zero) or wgrad_side):
             cur = torch.cuda.current_stream(g_raw.device)
             side = _side_stream(g_raw.device)
             side.wait_stream(cur)
@@ -308,7 +312,17 @@ class _FusionConvFn(torch.autograd.Function):
                                           pool=smap.csr(L.BY_CELL, L.ORDER_ENTRY) if occ else None,
                                           fwd_ws=ctx.fwd_ws if occ else None, fwd_stats=ctx.train_bn)
                 if ctx.needs_input_grad[1]:
-                    if pooled and zeros_done is not None:  # its zero rows are on the side stream already
+                    if late_zero:
+                        cur = torch.cuda.current_stream(g_raw.device)
+                        side = _side_stream(g_raw.device)
+                        side.wait_stream(cur)
+                        d_b = torch.empty(b.shape, dtype=a.dtype, device=a.device)
+                        with torch.cuda.stream(side):
+                            sm.pull(smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, d_b, Cb, 0, Cb, d_b, Cb, part="dense")
+                            sm.pull(smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, dx_b, Cb, 0, Cb, d_b, Cb, part="sparse")
+                        for t in (dx_b, d_b):
+                            t.record_stream(side)
+                    elif pooled and zeros_done is not None:  # its zero rows are on the side stream already
                         cur.wait_event(zeros_done)
                         sm.pull(smap, L.BY_PIXEL, L.ORDER_COL_ENTRY, dx_b, Cb, 0, Cb, d_b, Cb, part="sparse")
                     elif pooled:  # the pooled channels' gradient back to the image (a8's TF gradient)
@@ -319,8 +333,10 @@ class _FusionConvFn(torch.autograd.Function):
             if not ctx.needs_input_grad[0]:
                 d_a = None
         if side is not None:
+            if late_zero and dw is None and ctx.needs_input_grad[2]:  # on the main stream, beside the side's work
+                dw = _FusionConvFn._wgrad(ctx, a, b, weights, g_raw)
             cur.wait_stream(side)
-            if dw is not None:
+            if dw is not None and not late_zero:
                 dw.record_stream(cur)
         if dw is None and ctx.needs_input_grad[2]:
             dw = _FusionConvFn._wgrad(ctx, a, b, weights, g_raw)
@@ -371,6 +387,10 @@ class FusionConv:
     # bf16 fused() backward: the input gradient's pooled channels stored at the occupied cells only, by the
     # forward's occupancy words (shpl_conv3x3_dgrad_reuse; False: the whole map, shpl_conv3x3_dgrad)
     DGRAD_OCC = True
+    # the image gradient (zero rows, then the pull of the pooled channels' gradient) on the side stream after the
+    # input gradient, beside the weight gradient (False: only its zero rows, beside the input gradient): 6.93-7.00
+    # against 6.98-7.04 ms per bf16 training step, interleaved (profiles/r06_ab/beside_*)
+    IMG_BESIDE_WGRAD = True
 
     def __init__(self, c_in, c_out, batch_norm=True, bias=False, relu=True, eps=1e-3, decay=0.999,
                  dtype=torch.float32, device="cuda", seed=0):

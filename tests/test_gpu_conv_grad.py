@@ -357,9 +357,10 @@ def test_fused_bf16_wgrad_reuses_forward_operand(train, cb, ci, cout):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_side_stream_backward_matches_one_stream(dtype):
-    """FusionConv.IMG_ZERO_SIDE / WGRAD_SIDE: the image gradient's zero rows and / or the weight gradient on a
-    side stream beside the input gradient give bitwise the gradients of the one-stream backward, over three
-    steps (the side stream's allocations reused across steps)."""
+    """FusionConv.IMG_ZERO_SIDE / WGRAD_SIDE / IMG_BESIDE_WGRAD: the image gradient's zero rows and / or the
+    weight gradient on a side stream beside the input gradient, or the whole image gradient beside the weight
+    gradient, give bitwise the gradients of the one-stream backward, over three steps (the side stream's
+    allocations reused across steps)."""
     from sparse_pooling_amd import fusion_conv as fc, shpl_map as sm
     spec = synth.FrameSpec(2000, (1200, 360), (704, 800), (4, 4), 32, 32)
     fr = synth.make_frame(spec, seed=911, n_outside=10)
@@ -371,11 +372,12 @@ def test_side_stream_backward_matches_one_stream(dtype):
     bev = _t(synth.make_features((1, Hb, Wb, 32), 41)).to(dtype)
     img = _t(synth.make_features((1, Hi, Wi, 32), 42)).to(dtype)
     grads = []
-    for zero_side, wgrad_side in ((False, False), (True, False), (False, True), (True, True)):
+    for zero_side, wgrad_side, beside in ((False, False, False), (True, False, False), (False, True, False),
+                                          (True, True, False), (True, False, True)):
         smap = sm.pack_map(_t(ref["Mij_pool"]), _t(ref["M_val"].astype(np.float32)), ref["M_size"],
                            _t(ref["img_index_flip_pool"]), img.shape)
         conv = fc.FusionConv(64, 32, dtype=dtype, device=DEV, seed=5)
-        conv.IMG_ZERO_SIDE, conv.WGRAD_SIDE = zero_side, wgrad_side
+        conv.IMG_ZERO_SIDE, conv.WGRAD_SIDE, conv.IMG_BESIDE_WGRAD = zero_side, wgrad_side, beside
         conv.weights.requires_grad_(True)
         conv.beta.requires_grad_(True)
         tb, ti = bev.clone().requires_grad_(True), img.clone().requires_grad_(True)
